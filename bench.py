@@ -1,0 +1,127 @@
+"""Headline benchmark: steps/sec (whole node) of the tutorial MLP training step.
+
+Metric and config come from BASELINE.json / BASELINE.md: the reference's
+data-parallel tutorial step (data_paral.py) -- Classifier 784 -> 512 (SiLU,
+dropout 0.1) -> 10, bf16 compute / fp32 params, global batch 128 split over the
+GPUs (P('data')), 4 gradient-accumulation minibatches per step, AdamW(1e-3),
+one gradient+metrics all-reduce per step.  Global batch is fixed as N grows
+(the reference's config), so scaling is "strong".  Synthetic data (N(0,1)
+inputs, uniform integer labels), random init -- no datasets are available.
+
+Every timed step is a complete training step: all 4 minibatch fwd/bwd passes,
+the RCCL all-reduce (N > 1), the fused AdamW update and the metrics fold.
+
+    python bench.py                                # N=1
+    torchrun --nproc-per-node 8 bench.py --gpus 8  # one rank per GPU, RCCL over xGMI
+    python bench.py --strategy fsdp|pp             # the other two tutorials
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+from jax_distributed_tuts_amd.runtime import dist as D
+from jax_distributed_tuts_amd.runtime.dist import Mesh
+
+METRIC = "steps/sec (whole node) for tutorial MLP at 1/2/4/8 MI355X, DP vs shard vs PP"
+
+
+def build_dp(args, dev):
+    from data_paral import synthetic_batch
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp, shard_batch
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    cfg = dp_config()
+    cfg.model.num_layers = args.num_layers
+    mesh = Mesh({"data": D.world_size()})
+    model = Classifier.from_config(cfg.model)
+    state = init_dp(model, adamw(cfg.optimizer.learning_rate), cfg.seed, dev, mesh)
+    batch = shard_batch(synthetic_batch(cfg, cfg.seed + 1), mesh, "data")
+    batch = Batch(batch.inputs.to(dev), batch.labels.to(dev))
+    tr = DataParallelTrainer(state, mesh, DPConfig(cfg.optimizer.num_minibatches, args.accum))
+    desc = {"model": f"tutorial MLP {'-'.join(map(str, model.dims))} (SiLU, dropout 0.1)",
+            "global_batch": cfg.data.batch_size, "seq_len": None, "num_minibatches": cfg.optimizer.num_minibatches,
+            "parallelism": f"dp{D.world_size()}", "accum": args.accum}
+    return tr, batch, desc
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--strategy", choices=["dp"], default="dp")
+    ap.add_argument("--num-layers", type=int, default=2)
+    ap.add_argument("--accum", choices=["loop", "fused"], default="loop")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--capture-collectives", action="store_true")
+    args = ap.parse_args()
+
+    dev = D.init()
+    ws = D.world_size()
+    if ws != args.gpus and D.rank() == 0:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+    tr, batch, desc = build_dp(args, dev)
+    on_gpu = dev.type == "cuda"
+    sync = (lambda: torch.cuda.synchronize()) if on_gpu else (lambda: None)
+
+    # warmup: eager steps (library load, allocator), then capture + replays
+    n_eager = max(1, min(args.warmup, 3))
+    for _ in range(n_eager):
+        tr.step(batch)
+    sync()
+    use_graph = on_gpu and not args.no_graph
+    if use_graph:
+        tr.capture(batch, capture_collectives=args.capture_collectives)
+    for _ in range(max(0, args.warmup - n_eager)):
+        tr.step(batch)
+    sync()
+    D.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.step(batch)
+    sync()
+    D.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    if D.is_initialized():
+        t = torch.tensor([dt], dtype=torch.float64, device=dev if D.backend() == "nccl" else "cpu")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    # per-step latency distribution (separate, untimed pass)
+    p50 = p90 = None
+    if on_gpu:
+        ts = []
+        for _ in range(min(50, args.steps)):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            tr.step(batch)
+            b.record()
+            b.synchronize()
+            ts.append(a.elapsed_time(b))
+        ts.sort()
+        p50, p90 = ts[len(ts) // 2], ts[int(0.9 * len(ts))]
+    m = tr.metrics.detach().float().cpu()
+    sps = args.steps / dt
+    if D.rank() == 0:
+        out = {"metric": METRIC, "value": round(sps, 2), "unit": "steps/s", "n_gpus": ws, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 5), "higher_is_better": True,
+               "scaling": "strong", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (N(0,1) inputs, "
+               "uniform int labels; random init)", "config": desc,
+               "details": {"p50_ms": p50, "p90_ms": p90, "hipgraph": use_graph, "samples_per_s":
+                           round(sps * desc["global_batch"], 1), "final_loss": float(m[0] / max(m[1], 1)),
+                           "comm": D.backend() or "none"}}
+        print(json.dumps(out), flush=True)
+    D.shutdown()
+
+
+if __name__ == "__main__":
+    main()

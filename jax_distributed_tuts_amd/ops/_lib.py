@@ -1,0 +1,113 @@
+"""ctypes binding to the in-tree gfx950 kernel library.
+
+The library is loaded lazily on the first GPU op.  On a machine with a GPU the
+HIP path is mandatory: if the library is missing or fails to load, the op
+raises instead of silently falling back to eager PyTorch (CPU tensors use the
+pure-torch reference implementations in ``ops/kernels.py``; those exist for the
+gloo simulation mode and as the numerics oracle in tests).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from ctypes import c_float, c_int, c_long, c_ulonglong, c_void_p
+
+from . import build as _build
+
+_lock = threading.Lock()
+_lib = None
+
+
+class GemmArgs(ctypes.Structure):
+    """Mirror of ``jdt::GemmArgs`` in csrc/gemm.hip (field order and types must match)."""
+
+    _fields_ = [
+        ("A", c_void_p), ("lda", c_long), ("sA", c_long), ("a_f32", c_int), ("a_trans", c_int),
+        ("B", c_void_p), ("ldb", c_long), ("sB", c_long), ("b_f32", c_int), ("b_trans", c_int),
+        ("M", c_int), ("N", c_int), ("K", c_int), ("alpha", c_float),
+        ("bias", c_void_p), ("bias_f32", c_int), ("act", c_int),
+        ("Zout", c_void_p), ("ldz", c_long), ("sZ", c_long),
+        ("Zin", c_void_p), ("ldzin", c_long), ("sZin", c_long), ("act_bwd", c_int),
+        ("keep_prob", c_float), ("seed", c_ulonglong), ("offset", c_ulonglong),
+        ("resid", c_void_p), ("ldr", c_long), ("sR", c_long),
+        ("dbias", c_void_p),
+        ("C", c_void_p), ("ldc", c_long), ("sC", c_long), ("c_f32", c_int), ("accumulate", c_int),
+        ("step_ptr", c_void_p),
+    ]
+
+
+_SIGS = {
+    "jdt_gemm": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_int, c_void_p]),
+    "jdt_gemm_args_size": (c_int, []),
+    "jdt_xent": (c_int, [c_void_p, c_int, c_long, c_void_p, c_int, c_int, c_float, c_void_p, c_long, c_void_p,
+                         c_void_p, c_void_p, c_void_p]),
+    "jdt_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_float, c_float, c_float,
+                          c_float, c_float, c_float, c_void_p, c_void_p, c_int, c_void_p]),
+    "jdt_sgd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_float, c_float, c_float, c_float,
+                        c_void_p, c_void_p, c_int, c_void_p]),
+    "jdt_cast_f32_bf16": (c_int, [c_void_p, c_void_p, c_long, c_void_p]),
+    "jdt_scale": (c_int, [c_void_p, c_long, c_float, c_void_p]),
+    "jdt_act_bwd": (c_int, [c_void_p, c_void_p, c_int, c_float, c_ulonglong, c_ulonglong, c_void_p, c_int, c_int,
+                            c_void_p, c_void_p, c_void_p]),
+    "jdt_metrics_fold": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+}
+
+
+def _declare(lib):
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    # optional symbols declared by other modules register themselves via `declare`
+    return lib
+
+
+_extra_sigs: dict = {}
+
+
+def declare(name: str, restype, argtypes):
+    """Register a signature for a launcher defined in another csrc file."""
+    _extra_sigs[name] = (restype, argtypes)
+    if _lib is not None:
+        fn = getattr(_lib, name)
+        fn.restype, fn.argtypes = restype, argtypes
+
+
+def lib():
+    """Load (building first if the .so is missing/stale and a compiler exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = _build.LIB
+        if (not path.exists()) or (os.environ.get("JDT_AUTOBUILD", "1") == "1" and _build.is_stale()):
+            try:
+                _build.build(verbose=True)
+            except Exception as e:  # noqa: BLE001
+                if not path.exists():
+                    raise RuntimeError(f"gfx950 kernel library {path} is missing and could not be built: {e}") from e
+        l = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+        _declare(l)
+        for name, (res, args) in _extra_sigs.items():
+            fn = getattr(l, name)
+            fn.restype, fn.argtypes = res, args
+        if l.jdt_gemm_args_size() != ctypes.sizeof(GemmArgs):
+            raise RuntimeError("GemmArgs layout mismatch between Python and csrc/gemm.hip")
+        _lib = l
+        return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with HIP error code {rc}")
+
+
+def stream_ptr(device=None) -> int:
+    import torch
+
+    return torch.cuda.current_stream(device).cuda_stream

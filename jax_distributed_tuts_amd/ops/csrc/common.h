@@ -1,0 +1,118 @@
+// Shared device helpers for the gfx950 (CDNA4 / MI355X) kernel library.
+//
+// Everything here is written for 64-lane wavefronts and the gfx950 MFMA
+// intrinsics; there is no other target.  Host code reaches the kernels through
+// the extern "C" launchers in each .hip file (loaded with ctypes from
+// ops/_lib.py), always on the caller's HIP stream so that the whole training
+// step can be captured into one hipGraph.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define JDT_API extern "C" __attribute__((visibility("default")))
+
+namespace jdt {
+
+typedef uint16_t bf16_t;  // raw bf16 bits
+typedef __attribute__((ext_vector_type(8))) short bf16x8;  // MFMA A/B fragment
+typedef __attribute__((ext_vector_type(4))) float f32x4;   // 16x16 MFMA C/D
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+
+constexpr int WAVE = 64;
+
+// ---------------------------------------------------------------- bf16 <-> f32
+__device__ __forceinline__ float bf2f(bf16_t h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+// round-to-nearest-even (NaN preserved as quiet NaN)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+__device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
+
+// ---------------------------------------------------------------- reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, WAVE));
+  return v;
+}
+
+// ---------------------------------------------------------------- Philox4x32-10
+// Counter-based RNG: the dropout mask of element `idx` under stream (seed,
+// offset) is a pure function, so the backward pass regenerates it instead of
+// storing a mask tensor.  `offset` folds in (step, minibatch,
+// rank) exactly like jax.random.fold_in does for the reference's dropout key
+// (data_paral.py:28-34, 178).
+__device__ __forceinline__ u32x4 philox4x32(uint64_t seed, uint64_t ctr_lo, uint64_t ctr_hi) {
+  uint32_t c0 = (uint32_t)ctr_lo, c1 = (uint32_t)(ctr_lo >> 32);
+  uint32_t c2 = (uint32_t)ctr_hi, c3 = (uint32_t)(ctr_hi >> 32);
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  u32x4 out; out.x = c0; out.y = c1; out.z = c2; out.w = c3;
+  return out;
+}
+// keep-decision for element idx: P(keep) = keep_prob
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t offset, uint64_t idx, float keep_prob) {
+  const u32x4 r = philox4x32(seed, idx, offset);
+  return (float)(r.x >> 8) * (1.0f / 16777216.0f) < keep_prob;
+}
+
+// ---------------------------------------------------------------- activations
+enum Act : int { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_RELU = 3 };
+
+__device__ __forceinline__ float act_fwd(int act, float z) {
+  switch (act) {
+    case ACT_SILU: return z / (1.0f + __expf(-z));
+    case ACT_GELU: {
+      const float k = 0.7978845608028654f;  // sqrt(2/pi), tanh approximation (flax nn.gelu default)
+      const float t = tanhf(k * (z + 0.044715f * z * z * z));
+      return 0.5f * z * (1.0f + t);
+    }
+    case ACT_RELU: return z > 0.f ? z : 0.f;
+    default: return z;
+  }
+}
+__device__ __forceinline__ float act_grad(int act, float z) {
+  switch (act) {
+    case ACT_SILU: {
+      const float s = 1.0f / (1.0f + __expf(-z));
+      return s * (1.0f + z * (1.0f - s));
+    }
+    case ACT_GELU: {
+      const float k = 0.7978845608028654f;
+      const float u = k * (z + 0.044715f * z * z * z);
+      const float t = tanhf(u);
+      const float du = k * (1.0f + 3.0f * 0.044715f * z * z);
+      return 0.5f * (1.0f + t) + 0.5f * z * (1.0f - t * t) * du;
+    }
+    case ACT_RELU: return z > 0.f ? 1.f : 0.f;
+    default: return 1.f;
+  }
+}
+
+// ---------------------------------------------------------------- MFMA wrappers
+// D = A(16x32) * B(32x16) + C, bf16 in, f32 accumulate.
+// lane l holds A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15]; D[(l>>4)*4+i][l&15].
+__device__ __forceinline__ f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+}  // namespace jdt
+
+#define HIP_LAUNCH_CHECK() (int)hipGetLastError()

@@ -1,0 +1,340 @@
+// Generic bf16 MFMA GEMM for gfx950 with fused epilogues.
+//
+//   C[M,N] (+)= epilogue( alpha * A[M,K] . B[K,N] )
+//
+// This one kernel is every dense matmul of the tutorial models (SURVEY K01,
+// K05, K09, K11 and the transformer projections):
+//   forward   z = x . W + b ; h = dropout(act(z))        (flax Dense, [in,out] kernel)
+//   backward  dx = dz . W^T, with the *lower* layer's act'(z) and dropout mask
+//             folded into the epilogue (K10) and its bias grad reduced in the
+//             epilogue with one atomic per column per wave;
+//             dW += x^T . dz accumulated in fp32 in place (beta = 1, K12).
+//
+// Operands are staged global -> registers -> LDS always in a K-contiguous
+// image, so every MFMA fragment read is one 16-byte ds_read.  A source that is
+// M/N-contiguous (a transposed operand) is transposed in the register->LDS
+// write pass; fp32 sources (input data, fp32 activations) are converted to
+// bf16 in the same pass.  Two LDS buffers: the next K-tile's global loads are
+// issued before the current tile's MFMAs, written after them (async-stage
+// split), one barrier per K-tile.  4 waves per workgroup, each wave owning a
+// TM x TN grid of 16x16 fp32 accumulators (v_mfma_f32_16x16x32_bf16).
+// Workgroup ids are remapped so neighbouring tiles (which share A rows)
+// land on the same XCD's L2.
+#include "common.h"
+
+namespace jdt {
+
+struct GemmArgs {
+  const void* A; long lda; long sA; int a_f32; int a_trans;  // a_trans: A[m][k] at k*lda+m
+  const void* B; long ldb; long sB; int b_f32; int b_trans;  // b_trans=0: B[k][n] at n*ldb+k ; 1: k*ldb+n
+  int M, N, K;
+  float alpha;
+  // forward epilogue
+  const void* bias; int bias_f32;          // per-column bias (optional)
+  int act;                                  // activation applied after bias
+  void* Zout; long ldz; long sZ;            // optional pre-activation store (bf16)
+  // backward epilogue: v *= act'(Zin) (Zin bf16, same layout as C)
+  const bf16_t* Zin; long ldzin; long sZin; int act_bwd;
+  // dropout (forward: applied after act; backward: mask regenerated)
+  float keep_prob; unsigned long long seed, offset;
+  const void* resid; long ldr; long sR;     // optional residual (bf16) added last
+  float* dbias;                             // optional column-sum of the final values (fp32 atomics)
+  // output
+  void* C; long ldc; long sC; int c_f32; int accumulate;
+  // device step counter: dropout offset += step << 32, so a replayed hipGraph
+  // draws a fresh mask every step without re-recording kernel arguments
+  const int* step_ptr;
+};
+
+template <int WM, int WN, int TM, int TN, int BK>
+struct Tile {
+  static constexpr int BM = WM * TM * 16;
+  static constexpr int BN = WN * TN * 16;
+  static constexpr int LDK = BK + 8;                  // padded K stride (elements)
+  static constexpr int A_CHUNKS = BM * BK / 8;        // 8-element chunks per tile
+  static constexpr int B_CHUNKS = BN * BK / 8;
+  static constexpr int A_PER_T = (A_CHUNKS + 255) / 256;
+  static constexpr int B_PER_T = (B_CHUNKS + 255) / 256;
+};
+
+__device__ __forceinline__ unsigned pack2(bf16_t lo, bf16_t hi) { return (unsigned)lo | ((unsigned)hi << 16); }
+
+// Load one 8-element chunk of a (rows x K) operand into packed bf16.
+//   non-transposed: elements (r, k0..k0+7) at base + r*ld + k
+//   transposed    : elements (r0..r0+7, k) at base + k*ld + r
+template <bool F32>
+__device__ __forceinline__ u32x4 load_chunk(const void* base, long ld, bool trans, int r, int k,
+                                            int R, int K, bool vec_ok) {
+  u32x4 out = {0u, 0u, 0u, 0u};
+  if (!trans) {
+    if (r >= R) return out;
+    const long off = (long)r * ld + k;
+    if (vec_ok && k + 8 <= K) {
+      if (F32) {
+        const float4* p = reinterpret_cast<const float4*>(static_cast<const float*>(base) + off);
+        const float4 x = p[0], y = p[1];
+        out.x = pack2(f2bf(x.x), f2bf(x.y)); out.y = pack2(f2bf(x.z), f2bf(x.w));
+        out.z = pack2(f2bf(y.x), f2bf(y.y)); out.w = pack2(f2bf(y.z), f2bf(y.w));
+      } else {
+        out = *reinterpret_cast<const u32x4*>(static_cast<const bf16_t*>(base) + off);
+      }
+      return out;
+    }
+    bf16_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bf16_t v = 0;
+      if (k + j < K) v = F32 ? f2bf(static_cast<const float*>(base)[off + j]) : static_cast<const bf16_t*>(base)[off + j];
+      e[j] = v;
+    }
+    out.x = pack2(e[0], e[1]); out.y = pack2(e[2], e[3]); out.z = pack2(e[4], e[5]); out.w = pack2(e[6], e[7]);
+    return out;
+  } else {
+    if (k >= K) return out;
+    const long off = (long)k * ld + r;
+    if (vec_ok && r + 8 <= R) {
+      if (F32) {
+        const float4* p = reinterpret_cast<const float4*>(static_cast<const float*>(base) + off);
+        const float4 x = p[0], y = p[1];
+        out.x = pack2(f2bf(x.x), f2bf(x.y)); out.y = pack2(f2bf(x.z), f2bf(x.w));
+        out.z = pack2(f2bf(y.x), f2bf(y.y)); out.w = pack2(f2bf(y.z), f2bf(y.w));
+      } else {
+        out = *reinterpret_cast<const u32x4*>(static_cast<const bf16_t*>(base) + off);
+      }
+      return out;
+    }
+    bf16_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bf16_t v = 0;
+      if (r + j < R) v = F32 ? f2bf(static_cast<const float*>(base)[off + j]) : static_cast<const bf16_t*>(base)[off + j];
+      e[j] = v;
+    }
+    out.x = pack2(e[0], e[1]); out.y = pack2(e[2], e[3]); out.z = pack2(e[4], e[5]); out.w = pack2(e[6], e[7]);
+    return out;
+  }
+}
+
+// chunk index c -> (row, k) of the tile for either orientation
+template <int BK>
+__device__ __forceinline__ void chunk_coords(int c, bool trans, int& r, int& k) {
+  if (!trans) { r = c / (BK / 8); k = (c % (BK / 8)) * 8; }
+  else        { k = c % BK;       r = (c / BK) * 8; }
+}
+
+template <int LDK>
+__device__ __forceinline__ void store_chunk(bf16_t* lds, bool trans, int r, int k, const u32x4& v) {
+  if (!trans) {
+    *reinterpret_cast<u32x4*>(lds + r * LDK + k) = v;
+  } else {
+    const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      lds[(r + 2 * j) * LDK + k] = (bf16_t)(w[j] & 0xffffu);
+      lds[(r + 2 * j + 1) * LDK + k] = (bf16_t)(w[j] >> 16);
+    }
+  }
+}
+
+template <int WM, int WN, int TM, int TN, int BK, bool AF32, bool BF32>
+__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int vecA, int vecB) {
+  using T = Tile<WM, WN, TM, TN, BK>;
+  constexpr int BM = T::BM, BN = T::BN, LDK = T::LDK;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (BM + BN) * LDK];
+  // buffer b: A image at smem + b*(BM+BN)*LDK, B image right after it
+#define AS(b) (smem + (b) * (BM + BN) * LDK)
+#define BS(b) (smem + (b) * (BM + BN) * LDK + BM * LDK)
+
+  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD; give each XCD
+  // a contiguous run of tiles (cdna_hip_programming.md §5, T1).
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  }
+  const int tm0 = (bid / tiles_n) * BM;
+  const int tn0 = (bid % tiles_n) * BN;
+  const int z = blockIdx.z;
+
+  const void* Ab = static_cast<const char*>(g.A) + (long)z * g.sA * (AF32 ? 4 : 2);
+  const void* Bb = static_cast<const char*>(g.B) + (long)z * g.sB * (BF32 ? 4 : 2);
+  // shift operand bases to this tile
+  const long a_off = g.a_trans ? (long)tm0 : (long)tm0 * g.lda;
+  const long b_off = g.b_trans ? (long)tn0 : (long)tn0 * g.ldb;
+  Ab = static_cast<const char*>(Ab) + a_off * (AF32 ? 4 : 2);
+  Bb = static_cast<const char*>(Bb) + b_off * (BF32 ? 4 : 2);
+  const int Ar = g.M - tm0, Br = g.N - tn0;  // remaining rows of each operand
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ra[T::A_PER_T], rb[T::B_PER_T];
+  const int nkt = (g.K + BK - 1) / BK;
+
+  auto gload = [&](int kt) {
+    const int kb = kt * BK;
+#pragma unroll
+    for (int i = 0; i < T::A_PER_T; ++i) {
+      const int c = tid + i * 256;
+      if (c < T::A_CHUNKS) {
+        int r, k; chunk_coords<BK>(c, g.a_trans, r, k);
+        ra[i] = load_chunk<AF32>(Ab, g.lda, g.a_trans, r, kb + k, Ar, g.K, vecA);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < T::B_PER_T; ++i) {
+      const int c = tid + i * 256;
+      if (c < T::B_CHUNKS) {
+        int r, k; chunk_coords<BK>(c, g.b_trans, r, k);
+        rb[i] = load_chunk<BF32>(Bb, g.ldb, g.b_trans, r, kb + k, Br, g.K, vecB);
+      }
+    }
+  };
+  auto lwrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < T::A_PER_T; ++i) {
+      const int c = tid + i * 256;
+      if (c < T::A_CHUNKS) { int r, k; chunk_coords<BK>(c, g.a_trans, r, k); store_chunk<LDK>(AS(buf), g.a_trans, r, k, ra[i]); }
+    }
+#pragma unroll
+    for (int i = 0; i < T::B_PER_T; ++i) {
+      const int c = tid + i * 256;
+      if (c < T::B_CHUNKS) { int r, k; chunk_coords<BK>(c, g.b_trans, r, k); store_chunk<LDK>(BS(buf), g.b_trans, r, k, rb[i]); }
+    }
+  };
+
+  gload(0);
+  lwrite(0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) gload(kt + 1);  // in flight under the MFMAs below
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = (wm * TM + i) * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(AS(cur) + row * LDK + kk + 8 * (lane >> 4));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = (wn * TN + j) * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(BS(cur) + col * LDK + kk + 8 * (lane >> 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
+    }
+    if (kt + 1 < nkt) lwrite(cur ^ 1);
+    __syncthreads();
+  }
+
+#undef AS
+#undef BS
+  // ------------------------------------------------------------- epilogue
+  const bool drop = g.keep_prob < 1.0f;
+  const float inv_keep = drop ? 1.0f / g.keep_prob : 1.0f;
+  const unsigned long long doff = g.offset + (g.step_ptr ? ((unsigned long long)(unsigned)g.step_ptr[0] << 32) : 0ull);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = tn0 + (wn * TN + j) * 16 + (lane & 15);
+    const bool cok = col < g.N;
+    float bval = 0.f;
+    if (g.bias && cok) bval = g.bias_f32 ? static_cast<const float*>(g.bias)[col] : bf2f(static_cast<const bf16_t*>(g.bias)[col]);
+    float csum = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = tm0 + (wm * TM + i) * 16 + (lane >> 4) * 4 + e;
+        if (!cok || row >= g.M) continue;
+        float v = g.alpha * acc[i][j][e] + bval;
+        if (g.Zout) static_cast<bf16_t*>(g.Zout)[(long)z * g.sZ + (long)row * g.ldz + col] = f2bf(v);
+        if (g.Zin) v *= act_grad(g.act_bwd, bf2f(g.Zin[(long)z * g.sZin + (long)row * g.ldzin + col]));
+        if (g.act) v = act_fwd(g.act, g.Zout ? round_bf(v) : v);
+        if (drop) {
+          const unsigned long long idx = (unsigned long long)z * g.M * g.N + (unsigned long long)row * g.N + col;
+          v = dropout_keep(g.seed, doff, idx, g.keep_prob) ? v * inv_keep : 0.f;
+        }
+        if (g.resid) v += bf2f(static_cast<const bf16_t*>(g.resid)[(long)z * g.sR + (long)row * g.ldr + col]);
+        const long co = (long)z * g.sC + (long)row * g.ldc + col;
+        if (g.c_f32) {
+          float* Cp = static_cast<float*>(g.C) + co;
+          *Cp = g.accumulate ? *Cp + v : v;
+        } else {
+          bf16_t* Cp = static_cast<bf16_t*>(g.C) + co;
+          if (g.accumulate) {
+            *Cp = f2bf(bf2f(*Cp) + v);
+          } else {
+            v = round_bf(v);  // the bias grad sums exactly what downstream GEMMs read
+            *Cp = f2bf(v);
+          }
+        }
+        csum += v;
+      }
+    }
+    if (g.dbias) {
+      csum += __shfl_xor(csum, 16, WAVE);
+      csum += __shfl_xor(csum, 32, WAVE);
+      if (lane < 16 && cok) atomicAdd(g.dbias + col, csum);
+    }
+  }
+}
+
+template <int WM, int WN, int TM, int TN, int BK>
+static int launch_cfg(const GemmArgs& g, int batch, hipStream_t st) {
+  using T = Tile<WM, WN, TM, TN, BK>;
+  const int tiles_m = (g.M + T::BM - 1) / T::BM, tiles_n = (g.N + T::BN - 1) / T::BN;
+  dim3 grid(tiles_m * tiles_n, 1, batch);
+  // vector loads need 16-byte aligned rows: bf16 ld % 8, f32 ld % 4, aligned base
+  auto vec_ok = [](const void* p, long ld, int f32) {
+    return ((reinterpret_cast<uintptr_t>(p) & 15) == 0) && (f32 ? (ld % 4 == 0) : (ld % 8 == 0));
+  };
+  const int va = vec_ok(g.A, g.lda, g.a_f32), vb = vec_ok(g.B, g.ldb, g.b_f32);
+  if (g.a_f32 && g.b_f32) hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, true, true>), grid, dim3(256), 0, st, g, tiles_n, va, vb);
+  else if (g.a_f32)       hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, true, false>), grid, dim3(256), 0, st, g, tiles_n, va, vb);
+  else if (g.b_f32)       hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, false, true>), grid, dim3(256), 0, st, g, tiles_n, va, vb);
+  else                    hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, false, false>), grid, dim3(256), 0, st, g, tiles_n, va, vb);
+  return HIP_LAUNCH_CHECK();
+}
+
+}  // namespace jdt
+
+using namespace jdt;
+
+// Tile choice: the tutorial GEMMs are small (M = 4..128 rows per device), so the
+// heuristic favours enough workgroups to cover the chip over per-tile reuse.
+JDT_API int jdt_gemm(const GemmArgs* ga, int batch, int cfg, void* stream) {
+  const GemmArgs& g = *ga;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (g.M <= 0 || g.N <= 0) return 0;
+  if (cfg < 0) {
+    const long t128 = (long)((g.M + 127) / 128) * ((g.N + 127) / 128) * batch;
+    const long t64 = (long)((g.M + 63) / 64) * ((g.N + 63) / 64) * batch;
+    const long t32 = (long)((g.M + 31) / 32) * ((g.N + 63) / 64) * batch;
+    if (g.M >= 128 && g.N >= 128 && t128 >= 192) cfg = 3;
+    else if (g.M >= 64 && t64 >= 96) cfg = 2;
+    else if (g.M > 16 && t32 >= 64) cfg = 1;
+    else if (g.M <= 16) cfg = 0;
+    else cfg = (g.N <= 32) ? 4 : 0;
+  }
+  switch (cfg) {
+    case 0: return launch_cfg<1, 4, 1, 1, 64>(g, batch, st);   // 16 x 64
+    case 1: return launch_cfg<2, 2, 1, 2, 64>(g, batch, st);   // 32 x 64
+    case 2: return launch_cfg<2, 2, 2, 2, 32>(g, batch, st);   // 64 x 64
+    case 3: return launch_cfg<2, 2, 4, 4, 32>(g, batch, st);   // 128 x 128
+    case 4: return launch_cfg<4, 1, 1, 1, 64>(g, batch, st);   // 64 x 16
+    default: return -1;
+  }
+}
+
+JDT_API int jdt_gemm_args_size() { return (int)sizeof(GemmArgs); }

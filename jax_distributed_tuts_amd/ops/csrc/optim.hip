@@ -1,0 +1,145 @@
+// Fused optimizer steps over one flat fp32 parameter buffer.
+//
+// optax.adamw defaults (data_paral.py:106-108, param_sharding.py:235-237):
+//   b1 0.9, b2 0.999, eps 1e-8 (outside the sqrt), weight_decay 1e-4 applied to
+//   every leaf (mask None), bias correction with the step count.
+// In one pass per element:
+//   g   = grad * grad_scale            (1/n_minibatches * 1/n_devices folded here)
+//   m,v = moments ; p -= lr * (m_hat / (sqrt(v_hat) + eps) + wd * p)
+//   shadow_bf16 = bf16(p)             (the compute copy every GEMM reads)
+//   grad = 0                           (ready for the next step's beta=1 accumulation)
+// The step counter lives on the device so the kernel is replayable from a
+// hipGraph: every workgroup reads it, and the workgroup that takes the last
+// arrival ticket advances it and re-arms the ticket for the next launch.
+#include "common.h"
+
+namespace jdt {
+
+__device__ __forceinline__ void finish_ticket(int* step, unsigned* ticket) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = atomicAdd(ticket, 1u);
+    if (t == gridDim.x - 1) {
+      step[0] = step[0] + 1;
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                                                    float* __restrict__ v, bf16_t* __restrict__ shadow, long n,
+                                                    float lr, float b1, float b2, float eps, float wd, float grad_scale,
+                                                    int* step, unsigned* ticket, int zero_grad) {
+  const int t = step[0] + 1;
+  const float bc1 = 1.f - powf(b1, (float)t), bc2 = 1.f - powf(b2, (float)t);
+  const float rbc1 = 1.f / bc1, rbc2 = 1.f / bc2;
+  const long n4 = n / 4;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    float4 gg = reinterpret_cast<float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    float* pe = &pp.x; float* ge = &gg.x; float* me = &mm.x; float* ve = &vv.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gr = ge[k] * grad_scale;
+      me[k] = b1 * me[k] + (1.f - b1) * gr;
+      ve[k] = b2 * ve[k] + (1.f - b2) * gr * gr;
+      const float upd = (me[k] * rbc1) / (sqrtf(ve[k] * rbc2) + eps) + wd * pe[k];
+      pe[k] -= lr * upd;
+    }
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (shadow) {
+      uint2 s;
+      s.x = (unsigned)f2bf(pp.x) | ((unsigned)f2bf(pp.y) << 16);
+      s.y = (unsigned)f2bf(pp.z) | ((unsigned)f2bf(pp.w) << 16);
+      reinterpret_cast<uint2*>(shadow)[i] = s;
+    }
+  }
+  // tail
+  for (long i = n4 * 4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float gr = g[i] * grad_scale;
+    const float mi = b1 * m[i] + (1.f - b1) * gr;
+    const float vi = b2 * v[i] + (1.f - b2) * gr * gr;
+    m[i] = mi; v[i] = vi;
+    const float pi = p[i] - lr * ((mi * rbc1) / (sqrtf(vi * rbc2) + eps) + wd * p[i]);
+    p[i] = pi;
+    if (zero_grad) g[i] = 0.f;
+    if (shadow) shadow[i] = f2bf(pi);
+  }
+  finish_ticket(step, ticket);
+}
+
+// SGD (+ optional heavy-ball momentum and decoupled weight decay)
+__global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ buf,
+                                                  bf16_t* __restrict__ shadow, long n, float lr, float momentum,
+                                                  float wd, float grad_scale, int* step, unsigned* ticket,
+                                                  int zero_grad) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float gr = g[i] * grad_scale + wd * p[i];
+    if (buf) { gr = momentum * buf[i] + gr; buf[i] = gr; }
+    const float pi = p[i] - lr * gr;
+    p[i] = pi;
+    if (zero_grad) g[i] = 0.f;
+    if (shadow) shadow[i] = f2bf(pi);
+  }
+  if (step) finish_ticket(step, ticket);
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = f2bf(x[i]);
+}
+
+__global__ void scale_kernel(float* __restrict__ x, long n, float s) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] *= s;
+}
+
+static int grid_for(long n, int per_thread) {
+  long b = (n / per_thread + 255) / 256;
+  if (b < 1) b = 1;
+  if (b > 2048) b = 2048;  // grid-stride beyond ~8 blocks/CU
+  return (int)b;
+}
+
+}  // namespace jdt
+using namespace jdt;
+
+JDT_API int jdt_adamw(float* p, float* g, float* m, float* v, void* shadow, long n, float lr, float b1, float b2,
+                      float eps, float wd, float grad_scale, int* step, unsigned* ticket, int zero_grad,
+                      void* stream) {
+  if (n <= 0) return 0;
+  if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
+       reinterpret_cast<uintptr_t>(v)) & 15) return -2;
+  if (shadow && (reinterpret_cast<uintptr_t>(shadow) & 7)) return -2;
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n, 4)), dim3(256), 0, static_cast<hipStream_t>(stream), p, g, m, v,
+                     static_cast<bf16_t*>(shadow), n, lr, b1, b2, eps, wd, grad_scale, step, ticket, zero_grad);
+  return HIP_LAUNCH_CHECK();
+}
+
+JDT_API int jdt_sgd(float* p, float* g, float* buf, void* shadow, long n, float lr, float momentum, float wd,
+                    float grad_scale, int* step, unsigned* ticket, int zero_grad, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n, 1)), dim3(256), 0, static_cast<hipStream_t>(stream), p, g, buf,
+                     static_cast<bf16_t*>(shadow), n, lr, momentum, wd, grad_scale, step, ticket, zero_grad);
+  return HIP_LAUNCH_CHECK();
+}
+
+JDT_API int jdt_cast_f32_bf16(const float* x, void* y, long n, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n, 1)), dim3(256), 0, static_cast<hipStream_t>(stream), x,
+                     static_cast<bf16_t*>(y), n);
+  return HIP_LAUNCH_CHECK();
+}
+
+JDT_API int jdt_scale(float* x, long n, float s, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(scale_kernel, dim3(grid_for(n, 1)), dim3(256), 0, static_cast<hipStream_t>(stream), x, n, s);
+  return HIP_LAUNCH_CHECK();
+}

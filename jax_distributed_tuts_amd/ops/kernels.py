@@ -1,0 +1,338 @@
+"""Python entry points of the gfx950 kernels, with pure-torch CPU references.
+
+Dispatch rule: CUDA (ROCm) tensors ALWAYS run the hand-written HIP kernels from
+``ops/lib/libjdt_kernels.so`` (an error is raised if the library cannot be
+loaded); CPU tensors run the torch reference below.  The CPU path is what the
+gloo-simulated multi-device mode (``util.sim_multiCPU_dev``) executes and is the
+fp32 oracle the GPU numerics tests compare against.
+
+Numerics contract: matmul operands are rounded to bf16, products
+accumulate in fp32, activations are stored bf16, master params / grads /
+optimizer state are fp32.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+
+ACT = {"none": 0, "silu": 1, "gelu": 2, "relu": 3}
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _is_gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# ----------------------------------------------------------------------------- philox (CPU mirror)
+_M0, _M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+_W0, _W1 = np.uint64(0x9E3779B9), np.uint64(0xBB67AE85)
+_MASK32 = np.uint64(0xFFFFFFFF)
+
+
+def philox_uniform(seed: int, offset: int, idx: np.ndarray) -> np.ndarray:
+    """Bit-exact numpy mirror of ``jdt::philox4x32`` (first output word -> U[0,1) with 24 bits)."""
+    idx = idx.astype(np.uint64)
+    c0 = idx & _MASK32
+    c1 = idx >> np.uint64(32)
+    c2 = np.full_like(c0, np.uint64(offset) & _MASK32)
+    c3 = np.full_like(c0, (np.uint64(offset) >> np.uint64(32)) & _MASK32)
+    k0 = np.uint64(seed) & _MASK32
+    k1 = (np.uint64(seed) >> np.uint64(32)) & _MASK32
+    with np.errstate(over="ignore"):
+        for _ in range(10):
+            p0 = _M0 * c0
+            p1 = _M1 * c2
+            hi0, lo0 = p0 >> np.uint64(32), p0 & _MASK32
+            hi1, lo1 = p1 >> np.uint64(32), p1 & _MASK32
+            n0 = hi1 ^ c1 ^ k0
+            n2 = hi0 ^ c3 ^ k1
+            c0, c1, c2, c3 = n0, lo1, n2, lo0
+            k0 = (k0 + _W0) & _MASK32
+            k1 = (k1 + _W1) & _MASK32
+    return (c0 >> np.uint64(8)).astype(np.float64) * (1.0 / 16777216.0)
+
+
+def dropout_mask(seed: int, offset: int, shape, keep_prob: float, base: int = 0) -> torch.Tensor:
+    n = int(np.prod(shape))
+    u = philox_uniform(seed, offset, np.arange(base, base + n, dtype=np.uint64))
+    return torch.from_numpy(u < keep_prob).reshape(shape)
+
+
+# ----------------------------------------------------------------------------- activations (torch)
+def act_fwd_t(act: str, z: torch.Tensor) -> torch.Tensor:
+    if act == "silu":
+        return z * torch.sigmoid(z)
+    if act == "gelu":
+        return torch.nn.functional.gelu(z, approximate="tanh")
+    if act == "relu":
+        return torch.relu(z)
+    return z
+
+
+def act_grad_t(act: str, z: torch.Tensor) -> torch.Tensor:
+    if act == "silu":
+        s = torch.sigmoid(z)
+        return s * (1 + z * (1 - s))
+    if act == "gelu":
+        k = 0.7978845608028654
+        u = k * (z + 0.044715 * z ** 3)
+        t = torch.tanh(u)
+        return 0.5 * (1 + t) + 0.5 * z * (1 - t * t) * k * (1 + 3 * 0.044715 * z * z)
+    if act == "relu":
+        return (z > 0).to(z.dtype)
+    return torch.ones_like(z)
+
+
+def _bf(t: torch.Tensor) -> torch.Tensor:
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+# ----------------------------------------------------------------------------- GEMM
+def gemm(a: torch.Tensor, b: torch.Tensor, *, a_layout: str = "mk", b_layout: str = "kn",
+         out: Optional[torch.Tensor] = None, out_dtype=torch.bfloat16, accumulate: bool = False,
+         alpha: float = 1.0, bias: Optional[torch.Tensor] = None, act: str = "none",
+         z_out: Optional[torch.Tensor] = None, z_in: Optional[torch.Tensor] = None, act_bwd: str = "none",
+         keep_prob: float = 1.0, seed: int = 0, offset: int = 0, resid: Optional[torch.Tensor] = None,
+         dbias: Optional[torch.Tensor] = None, step: Optional[torch.Tensor] = None,
+         cfg: int = -1) -> torch.Tensor:
+    """C = epilogue(alpha * A @ B).
+
+    ``a`` holds logical A[M,K] as ``[M,K]`` (``a_layout="mk"``) or ``[K,M]`` ("km");
+    ``b`` holds logical B[K,N] as ``[K,N]`` ("kn", a flax ``[in,out]`` kernel) or
+    ``[N,K]`` ("nk").  Optional leading batch dim on every operand.
+    Epilogue order: +bias -> (store z_out) -> *act'(z_in) -> act -> dropout -> +resid
+    -> store/accumulate; ``dbias += colsum(result)``.  Dropout uses Philox stream
+    (seed, offset + (step[0] << 32)) when a device step counter is given.
+    """
+    batched = a.dim() == 3
+    if a_layout == "mk":
+        M, K = a.shape[-2], a.shape[-1]
+    else:
+        K, M = a.shape[-2], a.shape[-1]
+    N = b.shape[-1] if b_layout == "kn" else b.shape[-2]
+    Kb = b.shape[-2] if b_layout == "kn" else b.shape[-1]
+    assert Kb == K, f"gemm K mismatch {K} vs {Kb}"
+    lead = (a.shape[0],) if batched else ()
+    if out is None:
+        out = (torch.zeros if accumulate else torch.empty)(*lead, M, N, dtype=out_dtype, device=a.device)
+    if not _is_gpu(a):
+        if step is not None and keep_prob < 1.0:
+            offset = int(offset) + (int(step.item()) << 32)
+        return _gemm_ref(a, b, a_layout, b_layout, out, accumulate, alpha, bias, act, z_out, z_in, act_bwd,
+                         keep_prob, seed, offset, resid, dbias)
+    for t in (a, b, out, z_out, z_in, resid):
+        if t is not None:
+            assert t.stride(-1) == 1, "gemm operands must be contiguous in the last dim"
+            assert t.dtype in (torch.bfloat16, torch.float32)
+    g = _lib.GemmArgs()
+    g.A, g.lda, g.a_f32, g.a_trans = a.data_ptr(), a.stride(-2), int(a.dtype == torch.float32), int(a_layout == "km")
+    g.B, g.ldb, g.b_f32, g.b_trans = b.data_ptr(), b.stride(-2), int(b.dtype == torch.float32), int(b_layout == "kn")
+    g.sA = a.stride(0) if batched else 0
+    g.sB = (b.stride(0) if b.dim() == 3 else 0) if batched else 0
+    g.M, g.N, g.K, g.alpha = M, N, K, float(alpha)
+    if bias is not None:
+        assert bias.is_contiguous()
+        g.bias, g.bias_f32 = bias.data_ptr(), int(bias.dtype == torch.float32)
+    g.act = ACT[act]
+    if z_out is not None:
+        assert z_out.dtype == torch.bfloat16
+        g.Zout, g.ldz, g.sZ = z_out.data_ptr(), z_out.stride(-2), (z_out.stride(0) if batched else 0)
+    if z_in is not None:
+        assert z_in.dtype == torch.bfloat16
+        g.Zin, g.ldzin, g.sZin = z_in.data_ptr(), z_in.stride(-2), (z_in.stride(0) if batched else 0)
+        g.act_bwd = ACT[act_bwd]
+    g.keep_prob, g.seed, g.offset = float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1)
+    if resid is not None:
+        assert resid.dtype == torch.bfloat16
+        g.resid, g.ldr, g.sR = resid.data_ptr(), resid.stride(-2), (resid.stride(0) if batched else 0)
+    if dbias is not None:
+        assert dbias.dtype == torch.float32 and dbias.is_contiguous()
+        g.dbias = dbias.data_ptr()
+    g.C, g.ldc, g.sC = out.data_ptr(), out.stride(-2), (out.stride(0) if batched else 0)
+    g.c_f32, g.accumulate = int(out.dtype == torch.float32), int(accumulate)
+    if step is not None:
+        assert step.dtype == torch.int32
+        g.step_ptr = step.data_ptr()
+    rc = _lib.lib().jdt_gemm(ctypes.byref(g), int(a.shape[0]) if batched else 1, int(cfg), _lib.stream_ptr())
+    _lib.check(rc, "jdt_gemm")
+    return out
+
+
+def _gemm_ref(a, b, a_layout, b_layout, out, accumulate, alpha, bias, act, z_out, z_in, act_bwd, keep_prob, seed,
+              offset, resid, dbias):
+    A = _bf(a.float())
+    B = _bf(b.float())
+    if a_layout == "km":
+        A = A.transpose(-1, -2)
+    if b_layout == "nk":
+        B = B.transpose(-1, -2)
+    v = alpha * torch.matmul(A, B)
+    if bias is not None:
+        v = v + bias.float()
+    if z_out is not None:
+        z_out.copy_(v.to(torch.bfloat16))
+        if act != "none":
+            v = _bf(v)
+    if z_in is not None:
+        v = v * act_grad_t(act_bwd, z_in.float())
+    v = act_fwd_t(act, v)
+    if keep_prob < 1.0:
+        M, N = v.shape[-2], v.shape[-1]
+        mask = dropout_mask(seed, offset, v.shape, keep_prob).to(v.device)
+        del M, N
+        v = torch.where(mask, v / keep_prob, torch.zeros_like(v))
+    if resid is not None:
+        v = v + resid.float()
+    if out.dtype == torch.float32:
+        if accumulate:
+            out.add_(v)
+        else:
+            out.copy_(v)
+        contrib = v
+    else:
+        if accumulate:
+            out.copy_((out.float() + v).to(out.dtype))
+            contrib = v
+        else:
+            out.copy_(v.to(out.dtype))
+            contrib = out.float()
+    if dbias is not None:
+        dbias.add_(contrib.reshape(-1, contrib.shape[-1]).sum(0))
+    return out
+
+
+# ----------------------------------------------------------------------------- cross-entropy
+def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, *, grad_scale: float = 1.0,
+                 dlogits: Optional[torch.Tensor] = None, dbias: Optional[torch.Tensor] = None,
+                 metrics: Optional[torch.Tensor] = None, row_loss: Optional[torch.Tensor] = None):
+    """Fused softmax-CE fwd+bwd.  Writes dlogits = (softmax - onehot) * grad_scale (bf16),
+    adds colsum(dlogits) into dbias, adds [loss_sum, n, correct, n] into metrics (fp32[4])."""
+    M, C = logits.shape
+    if not _is_gpu(logits):
+        z = logits.float()
+        valid = (labels >= 0) & (labels < C)
+        lab = labels.clamp(0, C - 1).long()
+        lse = torch.logsumexp(z, dim=-1)
+        loss = torch.where(valid, lse - z.gather(1, lab[:, None])[:, 0], torch.zeros_like(lse))
+        if row_loss is not None:
+            row_loss.copy_(loss)
+        if dlogits is not None:
+            p = torch.softmax(z, dim=-1)
+            g = (p - torch.nn.functional.one_hot(lab, C).float()) * grad_scale
+            g = torch.where(valid[:, None], g, torch.zeros_like(g))
+            dlogits.copy_(g.to(dlogits.dtype))
+            if dbias is not None:
+                dbias.add_(dlogits.float()[valid].sum(0))
+        if metrics is not None:
+            correct = ((z.argmax(-1) == lab) & valid).float().sum()
+            n = valid.float().sum()
+            metrics.add_(torch.stack([loss.sum(), n, correct, n]).to(metrics.device))
+        return loss
+    assert labels.dtype == torch.int32 and labels.is_contiguous() and logits.stride(-1) == 1
+    if dlogits is not None:
+        assert dlogits.dtype == torch.bfloat16 and dlogits.stride(-1) == 1
+    rc = _lib.lib().jdt_xent(_ptr(logits), int(logits.dtype == torch.float32), logits.stride(0), _ptr(labels), M, C,
+                             float(grad_scale), _ptr(dlogits), dlogits.stride(0) if dlogits is not None else 0,
+                             _ptr(dbias), _ptr(metrics), _ptr(row_loss), _lib.stream_ptr())
+    _lib.check(rc, "jdt_xent")
+    return row_loss
+
+
+# ----------------------------------------------------------------------------- optimizers
+def adamw_step(p, g, m, v, shadow, *, lr, b1=0.9, b2=0.999, eps=1e-8, wd=1e-4, grad_scale=1.0, step, ticket,
+               zero_grad=True):
+    """Fused AdamW over flat fp32 buffers; ``step`` is a device int32[1] counter advanced in-kernel."""
+    if not _is_gpu(p):
+        t = int(step.item()) + 1
+        gr = g * grad_scale
+        m.mul_(b1).add_(gr, alpha=1 - b1)
+        v.mul_(b2).addcmul_(gr, gr, value=1 - b2)
+        mh = m / (1 - b1 ** t)
+        vh = v / (1 - b2 ** t)
+        p.sub_(lr * (mh / (vh.sqrt() + eps) + wd * p))
+        if zero_grad:
+            g.zero_()
+        if shadow is not None:
+            shadow.copy_(p.to(shadow.dtype))
+        step.add_(1)
+        return
+    rc = _lib.lib().jdt_adamw(_ptr(p), _ptr(g), _ptr(m), _ptr(v), _ptr(shadow), p.numel(), float(lr), float(b1),
+                              float(b2), float(eps), float(wd), float(grad_scale), _ptr(step), _ptr(ticket),
+                              int(zero_grad), _lib.stream_ptr())
+    _lib.check(rc, "jdt_adamw")
+
+
+def sgd_step(p, g, buf, shadow, *, lr, momentum=0.0, wd=0.0, grad_scale=1.0, step=None, ticket=None,
+             zero_grad=True):
+    if not _is_gpu(p):
+        gr = g * grad_scale + wd * p
+        if buf is not None:
+            buf.mul_(momentum).add_(gr)
+            gr = buf
+        p.sub_(lr * gr)
+        if zero_grad:
+            g.zero_()
+        if shadow is not None:
+            shadow.copy_(p.to(shadow.dtype))
+        if step is not None:
+            step.add_(1)
+        return
+    rc = _lib.lib().jdt_sgd(_ptr(p), _ptr(g), _ptr(buf), _ptr(shadow), p.numel(), float(lr), float(momentum),
+                            float(wd), float(grad_scale), _ptr(step), _ptr(ticket), int(zero_grad),
+                            _lib.stream_ptr())
+    _lib.check(rc, "jdt_sgd")
+
+
+def cast_bf16_(src: torch.Tensor, dst: torch.Tensor):
+    if not _is_gpu(src):
+        dst.copy_(src.to(torch.bfloat16))
+        return dst
+    rc = _lib.lib().jdt_cast_f32_bf16(_ptr(src), _ptr(dst), src.numel(), _lib.stream_ptr())
+    _lib.check(rc, "jdt_cast_f32_bf16")
+    return dst
+
+
+# ----------------------------------------------------------------------------- elementwise
+def act_bwd(dh: torch.Tensor, z: Optional[torch.Tensor], act: str, *, keep_prob: float = 1.0, seed: int = 0,
+            offset: int = 0, step: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+            dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dz = dh * dropout_mask/keep * act'(z); dbias += colsum(dz).  [M,N] bf16."""
+    M, N = dh.shape
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=dh.device)
+    if not _is_gpu(dh):
+        v = dh.float()
+        if z is not None:
+            v = v * act_grad_t(act, z.float())
+        if keep_prob < 1.0:
+            off = int(offset) + ((int(step.item()) << 32) if step is not None else 0)
+            mask = dropout_mask(seed, off, (M, N), keep_prob)
+            v = torch.where(mask, v / keep_prob, torch.zeros_like(v))
+        out.copy_(v.to(out.dtype))
+        if dbias is not None:
+            dbias.add_(out.float().sum(0))
+        return out
+    assert dh.is_contiguous() and out.is_contiguous() and (z is None or z.is_contiguous())
+    rc = _lib.lib().jdt_act_bwd(_ptr(dh), _ptr(z), ACT[act] if z is not None else 0, float(keep_prob),
+                                int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _ptr(step), M, N, _ptr(out),
+                                _ptr(dbias), _lib.stream_ptr())
+    _lib.check(rc, "jdt_act_bwd")
+    return out
+
+
+def metrics_fold_(running: torch.Tensor, slot: torch.Tensor):
+    """running += slot ; slot = 0 (one tiny kernel, graph-capturable)."""
+    if not _is_gpu(running):
+        running.add_(slot)
+        slot.zero_()
+        return
+    rc = _lib.lib().jdt_metrics_fold(_ptr(running), _ptr(slot), int(slot.numel()), _lib.stream_ptr())
+    _lib.check(rc, "jdt_metrics_fold")

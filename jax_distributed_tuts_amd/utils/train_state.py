@@ -1,0 +1,242 @@
+"""Training core: TrainState, Batch, optimizers, gradient accumulation
+(reference util.py:21-167).
+
+* ``TrainState`` (util.py:21-22): step, apply_fn, params, tx, opt_state, rng.
+  Params are a :class:`FlatParams`; ``apply_gradients`` is ONE fused optimizer
+  kernel over the flat buffer that also writes the bf16 compute shadow and
+  zeroes the grad buffer.  Updates are in place (the analogue of
+  ``donate_argnames=("state",)``), and the device-side step counter makes the
+  update replayable from a hipGraph.
+* ``accum_grads_loop`` / ``accum_grads_scan`` (util.py:41-137): minibatch
+  gradient accumulation.  Gradients accumulate IN PLACE into the fp32 grad
+  buffer through beta=1 GEMM epilogues, so "sum the grads" costs nothing; the
+  final ``/ n_minbatch`` (util.py:77) is folded into the optimizer's grad scale
+  (returned as ``GradBuffer.scale``).  The "scan" variant replays one captured
+  minibatch step (a hipGraph on GPU) with a device-resident minibatch index.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, Optional, Tuple
+
+import torch
+
+from ..ops import kernels as K
+from .flat import FlatParams
+from .metrics import Metrics
+from . import rng as R
+
+Pytree = Any
+
+
+# ---------------------------------------------------------------------------- batch
+@dataclass
+class Batch:
+    """util.py:25-28.  ``inputs`` [B, ...], ``labels`` [B] int32."""
+
+    inputs: torch.Tensor
+    labels: torch.Tensor
+
+    def slice(self, start: int, size: int) -> "Batch":
+        return Batch(self.inputs[start: start + size], self.labels[start: start + size])
+
+    def map(self, fn: Callable[[torch.Tensor], torch.Tensor]) -> "Batch":
+        return Batch(fn(self.inputs), fn(self.labels))
+
+    @property
+    def size(self) -> int:
+        return int(self.inputs.shape[0])
+
+
+# ---------------------------------------------------------------------------- optimizers
+@dataclass
+class AdamW:
+    """optax.adamw defaults (b1 .9, b2 .999, eps 1e-8, weight_decay 1e-4, no mask)."""
+
+    learning_rate: float = 1e-3
+    b1: float = 0.9
+    b2: float = 0.999
+    eps: float = 1e-8
+    weight_decay: float = 1e-4
+
+    def init(self, params: FlatParams) -> Dict[str, torch.Tensor]:
+        dev = params.master.device
+        return {"m": torch.zeros(params.numel, device=dev), "v": torch.zeros(params.numel, device=dev),
+                "count": torch.zeros(1, dtype=torch.int32, device=dev),
+                "ticket": torch.zeros(1, dtype=torch.int32, device=dev)}
+
+    def update(self, params: FlatParams, opt_state, grad_scale: float, zero_grad: bool = True):
+        K.adamw_step(params.master[: params.numel], params.grad[: params.numel], opt_state["m"], opt_state["v"],
+                     params.shadow[: params.numel] if params.shadow is not None else None, lr=self.learning_rate,
+                     b1=self.b1, b2=self.b2, eps=self.eps, wd=self.weight_decay, grad_scale=grad_scale,
+                     step=opt_state["count"], ticket=opt_state["ticket"], zero_grad=zero_grad)
+
+
+@dataclass
+class SGD:
+    learning_rate: float = 1e-2
+    momentum: float = 0.0
+    weight_decay: float = 0.0
+
+    def init(self, params: FlatParams) -> Dict[str, torch.Tensor]:
+        dev = params.master.device
+        st = {"count": torch.zeros(1, dtype=torch.int32, device=dev),
+              "ticket": torch.zeros(1, dtype=torch.int32, device=dev)}
+        if self.momentum:
+            st["buf"] = torch.zeros(params.numel, device=dev)
+        return st
+
+    def update(self, params: FlatParams, opt_state, grad_scale: float, zero_grad: bool = True):
+        K.sgd_step(params.master[: params.numel], params.grad[: params.numel], opt_state.get("buf"),
+                   params.shadow[: params.numel] if params.shadow is not None else None, lr=self.learning_rate,
+                   momentum=self.momentum, wd=self.weight_decay, grad_scale=grad_scale, step=opt_state["count"],
+                   ticket=opt_state["ticket"], zero_grad=zero_grad)
+
+
+def adamw(learning_rate: float, b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8,
+          weight_decay: float = 1e-4) -> AdamW:
+    return AdamW(learning_rate, b1, b2, eps, weight_decay)
+
+
+def sgd(learning_rate: float, momentum: float = 0.0, weight_decay: float = 0.0) -> SGD:
+    return SGD(learning_rate, momentum, weight_decay)
+
+
+# ---------------------------------------------------------------------------- grads handle
+@dataclass
+class GradBuffer:
+    """Accumulated gradients living in ``params.grad``; the true gradient is
+    ``flat * scale`` (the mean over minibatches/devices is applied lazily, fused
+    into the optimizer kernel)."""
+
+    params: FlatParams
+    scale: float = 1.0
+
+    @property
+    def flat(self) -> torch.Tensor:
+        return self.params.grad_params
+
+    def materialize(self) -> Dict[str, torch.Tensor]:
+        return {n: self.params.g(n) * self.scale for n in self.params.names()}
+
+
+# ---------------------------------------------------------------------------- train state
+@dataclass
+class TrainState:
+    step: int
+    apply_fn: Any
+    params: FlatParams
+    tx: Any
+    opt_state: Dict[str, torch.Tensor]
+    rng: int = 0
+    extra: Dict[str, Any] = field(default_factory=dict)
+
+    @classmethod
+    def create(cls, *, apply_fn, params: FlatParams, tx, rng: int = 0) -> "TrainState":
+        return cls(step=0, apply_fn=apply_fn, params=params, tx=tx, opt_state=tx.init(params), rng=rng)
+
+    @property
+    def step_tensor(self) -> torch.Tensor:
+        """Device step counter (advanced inside the optimizer kernel)."""
+        return self.opt_state["count"]
+
+    def apply_gradients(self, *, grads: Optional[GradBuffer] = None, rng: Optional[int] = None,
+                        grad_scale: Optional[float] = None) -> "TrainState":
+        scale = grad_scale if grad_scale is not None else (grads.scale if grads is not None else 1.0)
+        self.tx.update(self.params, self.opt_state, scale)
+        self.step += 1
+        if rng is not None:
+            self.rng = rng
+        return self
+
+
+def get_num_params(state) -> int:
+    """util.py:184-185 -- global (unsharded) parameter count."""
+    if isinstance(state, TrainState):
+        p = state.params
+    else:
+        p = state
+    if hasattr(p, "global_num_params"):
+        return p.global_num_params()
+    return p.num_params()
+
+
+# ---------------------------------------------------------------------------- accumulation
+LossFn = Callable[..., Tuple[torch.Tensor, Metrics]]
+
+
+def _metrics_add(a, b):
+    if a is None:
+        return {k: tuple(x for x in v) for k, v in b.items()}
+    return {k: tuple(x + y for x, y in zip(a[k], b[k])) for k in a}
+
+
+def accum_grads_loop(batch: Batch, state: TrainState, key: int, n_minbatch: int,
+                     loss_fn: LossFn) -> Tuple[GradBuffer, Metrics]:
+    """util.py:41-78.  ``loss_fn(params, apply_fn, minibatch, rng, minibatch_index=i,
+    state=state)`` accumulates its gradient into ``params.grad`` (beta = 1) and
+    returns ``(mean_loss, metrics)``."""
+    bs = batch.size
+    mb = bs // n_minbatch
+    keys = R.split(key, n_minbatch)
+    metrics = None
+    for i in range(n_minbatch):
+        minibatch = batch.slice(i * mb, mb)
+        _, m = loss_fn(state.params, state.apply_fn, minibatch, keys[i], minibatch_index=i, state=state)
+        metrics = _metrics_add(metrics, m)
+    return GradBuffer(state.params, 1.0 / n_minbatch), metrics
+
+
+def accum_grads_scan(batch: Batch, state: TrainState, key: int, n_minbatch: int,
+                     loss_fn: LossFn) -> Tuple[GradBuffer, Metrics]:
+    """util.py:81-137.  Rolled loop: one minibatch step with a device-resident
+    index ``i`` (``Batch.slice`` by a device offset), captured once as a hipGraph
+    and replayed ``n_minbatch`` times on GPU; a plain loop on CPU.  Must equal
+    :func:`accum_grads_loop` (tests/test_util_api.py)."""
+    bs = batch.size
+    mb = bs // n_minbatch
+    keys = R.split(key, n_minbatch)
+    dev = batch.inputs.device
+    if dev.type != "cuda":
+        return accum_grads_loop(batch, state, key, n_minbatch, loss_fn)
+    # device-resident slot the captured step reads its minibatch from
+    xin = torch.empty((mb,) + tuple(batch.inputs.shape[1:]), dtype=batch.inputs.dtype, device=dev)
+    yin = torch.empty((mb,), dtype=batch.labels.dtype, device=dev)
+    mslot = {}
+
+    def _body(i: int):
+        _, m = loss_fn(state.params, state.apply_fn, Batch(xin, yin), keys[0], minibatch_index=0, state=state)
+        mslot["m"] = m
+
+    metrics = None
+    # warm up on minibatch 0 eagerly (allocations, library load), then capture the body once
+    xin.copy_(batch.inputs[0:mb])
+    yin.copy_(batch.labels[0:mb])
+    _body(0)
+    metrics = _metrics_add(metrics, {k: tuple(x.clone() if torch.is_tensor(x) else x for x in v)
+                                     for k, v in mslot["m"].items()})
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        xin.copy_(batch.inputs[mb:2 * mb]) if n_minbatch > 1 else None
+        yin.copy_(batch.labels[mb:2 * mb]) if n_minbatch > 1 else None
+    torch.cuda.current_stream().wait_stream(s)
+    if n_minbatch > 1:
+        with torch.cuda.graph(g):
+            _body(1)
+        for i in range(1, n_minbatch):
+            xin.copy_(batch.inputs[i * mb:(i + 1) * mb])
+            yin.copy_(batch.labels[i * mb:(i + 1) * mb])
+            g.replay()
+            metrics = _metrics_add(metrics, {k: tuple(x.clone() if torch.is_tensor(x) else x for x in v)
+                                             for k, v in mslot["m"].items()})
+    return GradBuffer(state.params, 1.0 / n_minbatch), metrics
+
+
+def accum_grads(state: TrainState, batch: Batch, key: int, num_minibatches: int, loss_fn: LossFn,
+                use_scan: bool = False) -> Tuple[GradBuffer, Metrics]:
+    """util.py:140-167 (same signature and argument order)."""
+    if use_scan:
+        return accum_grads_scan(batch=batch, state=state, key=key, n_minbatch=num_minibatches, loss_fn=loss_fn)
+    return accum_grads_loop(batch=batch, state=state, key=key, n_minbatch=num_minibatches, loss_fn=loss_fn)

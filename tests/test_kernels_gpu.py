@@ -1,0 +1,177 @@
+"""T4: every HIP kernel vs the fp32 torch reference of the same op (CPU path of
+ops/kernels.py, which rounds matmul operands to bf16 like the kernels do)."""
+import pytest
+import torch
+
+from jax_distributed_tuts_amd.ops import kernels as K
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, rtol=2e-2, atol=2e-2):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err <= atol + rtol * scale, f"max err {err} (scale {scale})"
+
+
+def _mk(shape, dtype, layout_t=False, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    t = torch.randn(*shape, generator=g)
+    return t.to(dtype)
+
+
+@pytest.mark.parametrize("M,N,K", [(4, 512, 784), (16, 512, 784), (32, 10, 512), (128, 512, 784), (37, 70, 50),
+                                   (256, 384, 256), (512, 512, 512)])
+@pytest.mark.parametrize("a_layout,b_layout", [("mk", "kn"), ("mk", "nk"), ("km", "kn"), ("km", "nk")])
+@pytest.mark.parametrize("adt", [torch.bfloat16, torch.float32])
+def test_gemm_layouts(M, N, K, a_layout, b_layout, adt):
+    a = _mk((M, K) if a_layout == "mk" else (K, M), adt, seed=1)
+    b = _mk((K, N) if b_layout == "kn" else (N, K), torch.bfloat16, seed=2)
+    ref = K.gemm(a, b, a_layout=a_layout, b_layout=b_layout, out_dtype=torch.float32)
+    out = K.gemm(a.to(DEV), b.to(DEV), a_layout=a_layout, b_layout=b_layout, out_dtype=torch.float32)
+    _close(out, ref, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("act", ["none", "silu", "gelu", "relu"])
+def test_gemm_fwd_epilogue(act):
+    M, N, K_ = 64, 512, 784
+    x = _mk((M, K_), torch.float32, seed=3)
+    w = (_mk((K_, N), torch.float32, seed=4) * 0.05).to(torch.bfloat16)
+    b = _mk((N,), torch.bfloat16, seed=5)
+    zr = torch.empty(M, N, dtype=torch.bfloat16)
+    ref = K.gemm(x, w, bias=b, act=act, z_out=zr, keep_prob=0.9, seed=7, offset=11)
+    zg = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    out = K.gemm(x.to(DEV), w.to(DEV), bias=b.to(DEV), act=act, z_out=zg, keep_prob=0.9, seed=7, offset=11)
+    _close(zg, zr)
+    _close(out, ref)
+    # identical dropout mask (Philox bit parity CPU <-> GPU)
+    assert torch.equal((out.cpu() == 0), (ref == 0)) or act == "relu"
+
+
+def test_gemm_bwd_epilogue_and_dbias():
+    M, N, K_ = 32, 512, 10
+    dz = _mk((M, K_), torch.bfloat16, seed=6)
+    w = _mk((N, K_), torch.bfloat16, seed=7)  # [in=N, out=K] kernel read "nk"
+    z = _mk((M, N), torch.bfloat16, seed=8)
+    db_r = torch.zeros(N)
+    ref = K.gemm(dz, w, b_layout="nk", z_in=z, act_bwd="silu", keep_prob=0.9, seed=3, offset=5, dbias=db_r)
+    db_g = torch.zeros(N, device=DEV)
+    out = K.gemm(dz.to(DEV), w.to(DEV), b_layout="nk", z_in=z.to(DEV), act_bwd="silu", keep_prob=0.9, seed=3,
+                 offset=5, dbias=db_g)
+    _close(out, ref)
+    _close(db_g, db_r, rtol=2e-2, atol=5e-2)
+
+
+def test_gemm_accumulate_fp32():
+    x = _mk((784, 32), torch.float32, seed=9)   # "km": x stored [M_rows=32?]
+    dz = _mk((32, 512), torch.bfloat16, seed=10)
+    x = _mk((32, 784), torch.float32, seed=9)
+    acc_r = torch.ones(784, 512)
+    K.gemm(x, dz, a_layout="km", b_layout="kn", out=acc_r, accumulate=True)
+    acc_g = torch.ones(784, 512, device=DEV)
+    K.gemm(x.to(DEV), dz.to(DEV), a_layout="km", b_layout="kn", out=acc_g, accumulate=True)
+    _close(acc_g, acc_r, rtol=1e-3, atol=1e-3)
+
+
+def test_gemm_batched():
+    a = _mk((3, 64, 96), torch.bfloat16, seed=11)
+    b = _mk((3, 96, 80), torch.bfloat16, seed=12)
+    ref = K.gemm(a, b, out_dtype=torch.float32)
+    out = K.gemm(a.to(DEV), b.to(DEV), out_dtype=torch.float32)
+    _close(out, ref, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("M,C", [(4, 10), (128, 10), (33, 1000)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_xent(M, C, dt):
+    z = (_mk((M, C), torch.float32, seed=13) * 3).to(dt)
+    y = torch.randint(0, C, (M,), generator=torch.Generator().manual_seed(1)).to(torch.int32)
+    y[0] = -1  # ignored row
+    d_r = torch.empty(M, C, dtype=torch.bfloat16)
+    db_r, m_r, l_r = torch.zeros(C), torch.zeros(4), torch.zeros(M)
+    K.softmax_xent(z, y, grad_scale=1 / M, dlogits=d_r, dbias=db_r, metrics=m_r, row_loss=l_r)
+    d_g = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
+    db_g, m_g, l_g = torch.zeros(C, device=DEV), torch.zeros(4, device=DEV), torch.zeros(M, device=DEV)
+    K.softmax_xent(z.to(DEV), y.to(DEV), grad_scale=1 / M, dlogits=d_g, dbias=db_g, metrics=m_g, row_loss=l_g)
+    _close(l_g, l_r, rtol=1e-4, atol=1e-4)
+    _close(d_g, d_r, rtol=1e-2, atol=1e-4)
+    _close(db_g, db_r, rtol=1e-2, atol=1e-4)
+    _close(m_g, m_r, rtol=1e-5, atol=1e-3)
+
+
+def test_adamw_and_step_counter():
+    n = 407050
+    g = torch.Generator().manual_seed(0)
+    p = torch.randn(n, generator=g)
+    gr = torch.randn(n, generator=g)
+    st = {}
+    for dev in ("cpu", DEV):
+        P, G = p.clone().to(dev), gr.clone().to(dev)
+        m, v = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+        sh = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        step, ticket = torch.zeros(1, dtype=torch.int32, device=dev), torch.zeros(1, dtype=torch.int32, device=dev)
+        for _ in range(3):
+            G.copy_(gr.to(dev))
+            K.adamw_step(P, G, m, v, sh, lr=1e-3, grad_scale=0.25, step=step, ticket=ticket)
+        st[dev] = (P.cpu(), sh.cpu(), step.cpu(), G.cpu())
+    _close(st[DEV][0], st["cpu"][0], rtol=1e-5, atol=1e-6)
+    assert int(st[DEV][2]) == 3 and float(st[DEV][3].abs().max()) == 0.0
+    _close(st[DEV][1], st["cpu"][1], rtol=1e-2, atol=1e-2)
+
+
+def test_act_bwd():
+    M, N = 48, 300
+    dh, z = _mk((M, N), torch.bfloat16, seed=1), _mk((M, N), torch.bfloat16, seed=2)
+    step = torch.tensor([5], dtype=torch.int32)
+    db_r = torch.zeros(N)
+    r = K.act_bwd(dh, z, "gelu", keep_prob=0.8, seed=9, offset=3, step=step, dbias=db_r)
+    db_g = torch.zeros(N, device=DEV)
+    o = K.act_bwd(dh.to(DEV), z.to(DEV), "gelu", keep_prob=0.8, seed=9, offset=3, step=step.to(DEV), dbias=db_g)
+    _close(o, r)
+    _close(db_g, db_r, rtol=1e-2, atol=1e-2)
+
+
+def test_dp_step_gpu_matches_cpu():
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(128, 784, generator=g)
+    y = torch.randint(0, 10, (128,), generator=g).to(torch.int32)
+    res = {}
+    for dev in ("cpu", DEV):
+        model = Classifier(dropout_rate=0.1)
+        st = init_dp(model, adamw(1e-3), 69, dev)
+        tr = DataParallelTrainer(st, None, DPConfig(4, "loop"))
+        for _ in range(3):
+            tr.step(Batch(x.to(dev), y.to(dev)))
+        res[dev] = (st.params.master.cpu(), tr.metrics.cpu())
+    _close(res[DEV][0], res["cpu"][0], rtol=1e-2, atol=2e-3)
+    _close(res[DEV][1], res["cpu"][1], rtol=1e-2, atol=1e-2)
+
+
+def test_dp_graph_replay_matches_eager():
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(128, 784, generator=g).to(DEV)
+    y = torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV)
+    out = []
+    for use_graph in (False, True):
+        st = init_dp(Classifier(), adamw(1e-3), 69, DEV)
+        tr = DataParallelTrainer(st, None, DPConfig(4, "loop"))
+        tr.step(Batch(x, y))
+        if use_graph:
+            tr.capture(Batch(x, y))
+        for _ in range(5):
+            tr.step(Batch(x, y))
+        torch.cuda.synchronize()
+        out.append((st.params.master.clone(), tr.metrics.clone(), int(st.opt_state["count"].item())))
+    assert out[0][2] == out[1][2] == 6
+    torch.testing.assert_close(out[1][0], out[0][0], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(out[1][1], out[0][1], rtol=1e-6, atol=1e-5)

@@ -137,7 +137,8 @@ __device__ __forceinline__ void store_chunk(bf16_t* lds, bool trans, int r, int 
 }
 
 template <int WM, int WN, int TM, int TN, int BK, bool AF32, bool BF32>
-__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int vecA, int vecB) {
+__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int vecA, int vecB, int splits,
+                                                   int kchunk, float* __restrict__ ws, unsigned* counters) {
   using T = Tile<WM, WN, TM, TN, BK>;
   constexpr int BM = T::BM, BN = T::BN, LDK = T::LDK;
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (BM + BN) * LDK];
@@ -176,16 +177,20 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   u32x4 ra[T::A_PER_T], rb[T::B_PER_T];
-  const int nkt = (g.K + BK - 1) / BK;
+  // split-K: this workgroup reduces K range [kbeg, kend)
+  const int split = blockIdx.y;
+  const int kbeg = split * kchunk;
+  const int kend = min(g.K, kbeg + kchunk);
+  const int nkt = (kend - kbeg + BK - 1) / BK;
 
   auto gload = [&](int kt) {
-    const int kb = kt * BK;
+    const int kb = kbeg + kt * BK;
 #pragma unroll
     for (int i = 0; i < T::A_PER_T; ++i) {
       const int c = tid + i * 256;
       if (c < T::A_CHUNKS) {
         int r, k; chunk_coords<BK>(c, g.a_trans, r, k);
-        ra[i] = load_chunk<AF32>(Ab, g.lda, g.a_trans, r, kb + k, Ar, g.K, vecA);
+        ra[i] = load_chunk<AF32>(Ab, g.lda, g.a_trans, r, kb + k, Ar, kend, vecA);
       }
     }
 #pragma unroll
@@ -193,7 +198,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
       const int c = tid + i * 256;
       if (c < T::B_CHUNKS) {
         int r, k; chunk_coords<BK>(c, g.b_trans, r, k);
-        rb[i] = load_chunk<BF32>(Bb, g.ldb, g.b_trans, r, kb + k, Br, g.K, vecB);
+        rb[i] = load_chunk<BF32>(Bb, g.ldb, g.b_trans, r, kb + k, Br, kend, vecB);
       }
     }
   };
@@ -240,6 +245,55 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
 
 #undef AS
 #undef BS
+
+  // ------------------------------------------------------------- split-K combine
+  // Every K-slice writes its fp32 partial tile (slab) with plain stores, then
+  // publishes with ONE agent-scope release + arrival ticket; the workgroup that
+  // draws the last ticket acquires, sums the slabs and runs the epilogue
+  // (cdna_hip_programming.md §5 "In-launch split-K reduction").  Correct for any
+  // placement of the slices over XCDs.
+  if (splits > 1) {
+    const long tile_id = (long)z * gridDim.x + bid;
+    float* slab0 = ws + tile_id * splits * (BM * BN);
+    float* slab = slab0 + (long)split * (BM * BN);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int lr = (wm * TM + i) * 16 + (lane >> 4) * 4 + e, lc = (wn * TN + j) * 16 + (lane & 15);
+          slab[lr * BN + lc] = acc[i][j][e];
+        }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned t = __hip_atomic_fetch_add(counters + tile_id, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (t == (unsigned)(splits - 1));
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(counters + tile_id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int lr = (wm * TM + i) * 16 + (lane >> 4) * 4 + e, lc = (wn * TN + j) * 16 + (lane & 15);
+          float sum = 0.f;
+          for (int sp = 0; sp < splits; ++sp) sum += slab0[(long)sp * (BM * BN) + lr * BN + lc];
+          acc[i][j][e] = sum;
+        }
+  }
   // ------------------------------------------------------------- epilogue
   const bool drop = g.keep_prob < 1.0f;
   const float inv_keep = drop ? 1.0f / g.keep_prob : 1.0f;
@@ -291,19 +345,35 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
 }
 
 template <int WM, int WN, int TM, int TN, int BK>
-static int launch_cfg(const GemmArgs& g, int batch, hipStream_t st) {
+static int launch_cfg(const GemmArgs& g, int batch, int splits, float* ws, long ws_floats, unsigned* counters,
+                      long n_counters, hipStream_t st) {
   using T = Tile<WM, WN, TM, TN, BK>;
   const int tiles_m = (g.M + T::BM - 1) / T::BM, tiles_n = (g.N + T::BN - 1) / T::BN;
-  dim3 grid(tiles_m * tiles_n, 1, batch);
+  const long tiles = (long)tiles_m * tiles_n * batch;
+  const int ktiles = (g.K + BK - 1) / BK;
+  if (splits < 0) {
+    // Small GEMMs here are latency-bound on the K loop (one global round trip
+    // per K-tile): split K until the grid covers ~all CUs, <= 16 slices,
+    // each slice at least one K-tile.
+    splits = 1;
+    while (splits < 16 && tiles * splits * 2 <= 256 && ktiles >= splits * 2) splits *= 2;
+  }
+  if (splits > ktiles) splits = ktiles;
+  if (splits < 1) splits = 1;
+  if (splits > 1 && (!ws || !counters || tiles * splits * T::BM * T::BN > ws_floats || tiles > n_counters))
+    splits = 1;
+  const int kchunk = ((ktiles + splits - 1) / splits) * BK;
+  splits = (g.K + kchunk - 1) / kchunk;
+  dim3 grid(tiles_m * tiles_n, splits, batch);
   // vector loads need 16-byte aligned rows: bf16 ld % 8, f32 ld % 4, aligned base
   auto vec_ok = [](const void* p, long ld, int f32) {
     return ((reinterpret_cast<uintptr_t>(p) & 15) == 0) && (f32 ? (ld % 4 == 0) : (ld % 8 == 0));
   };
   const int va = vec_ok(g.A, g.lda, g.a_f32), vb = vec_ok(g.B, g.ldb, g.b_f32);
-  if (g.a_f32 && g.b_f32) hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, true, true>), grid, dim3(256), 0, st, g, tiles_n, va, vb);
-  else if (g.a_f32)       hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, true, false>), grid, dim3(256), 0, st, g, tiles_n, va, vb);
-  else if (g.b_f32)       hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, false, true>), grid, dim3(256), 0, st, g, tiles_n, va, vb);
-  else                    hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, false, false>), grid, dim3(256), 0, st, g, tiles_n, va, vb);
+  if (g.a_f32 && g.b_f32) hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, true, true>), grid, dim3(256), 0, st, g, tiles_n, va, vb, splits, kchunk, ws, counters);
+  else if (g.a_f32)       hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, true, false>), grid, dim3(256), 0, st, g, tiles_n, va, vb, splits, kchunk, ws, counters);
+  else if (g.b_f32)       hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, false, true>), grid, dim3(256), 0, st, g, tiles_n, va, vb, splits, kchunk, ws, counters);
+  else                    hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, false, false>), grid, dim3(256), 0, st, g, tiles_n, va, vb, splits, kchunk, ws, counters);
   return HIP_LAUNCH_CHECK();
 }
 
@@ -313,7 +383,8 @@ using namespace jdt;
 
 // Tile choice: the tutorial GEMMs are small (M = 4..128 rows per device), so the
 // heuristic favours enough workgroups to cover the chip over per-tile reuse.
-JDT_API int jdt_gemm(const GemmArgs* ga, int batch, int cfg, void* stream) {
+JDT_API int jdt_gemm(const GemmArgs* ga, int batch, int cfg, int splits, float* ws, long ws_floats,
+                     unsigned* counters, long n_counters, void* stream) {
   const GemmArgs& g = *ga;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (g.M <= 0 || g.N <= 0) return 0;
@@ -328,11 +399,11 @@ JDT_API int jdt_gemm(const GemmArgs* ga, int batch, int cfg, void* stream) {
     else cfg = (g.N <= 32) ? 4 : 0;
   }
   switch (cfg) {
-    case 0: return launch_cfg<1, 4, 1, 1, 64>(g, batch, st);   // 16 x 64
-    case 1: return launch_cfg<2, 2, 1, 2, 64>(g, batch, st);   // 32 x 64
-    case 2: return launch_cfg<2, 2, 2, 2, 32>(g, batch, st);   // 64 x 64
-    case 3: return launch_cfg<2, 2, 4, 4, 32>(g, batch, st);   // 128 x 128
-    case 4: return launch_cfg<4, 1, 1, 1, 64>(g, batch, st);   // 64 x 16
+    case 0: return launch_cfg<1, 4, 1, 1, 64>(g, batch, splits, ws, ws_floats, counters, n_counters, st);   // 16 x 64
+    case 1: return launch_cfg<2, 2, 1, 2, 64>(g, batch, splits, ws, ws_floats, counters, n_counters, st);   // 32 x 64
+    case 2: return launch_cfg<2, 2, 2, 2, 32>(g, batch, splits, ws, ws_floats, counters, n_counters, st);   // 64 x 64
+    case 3: return launch_cfg<2, 2, 4, 4, 32>(g, batch, splits, ws, ws_floats, counters, n_counters, st);   // 128 x 128
+    case 4: return launch_cfg<4, 1, 1, 1, 64>(g, batch, splits, ws, ws_floats, counters, n_counters, st);   // 64 x 16
     default: return -1;
   }
 }

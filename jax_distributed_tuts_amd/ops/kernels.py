@@ -31,6 +31,24 @@ def _is_gpu(t: torch.Tensor) -> bool:
     return t.is_cuda
 
 
+_WS = {}
+WS_FLOATS = 8 << 20      # 32 MiB split-K slab workspace per device
+N_COUNTERS = 1 << 16
+
+
+def workspace(device):
+    """Per-device split-K workspace (fp32 slabs) + zeroed arrival counters.  The
+    counters are re-armed to 0 by each tile's last arriver, so one allocation
+    serves every GEMM on the stream (kernels on one stream never overlap)."""
+    key = (device.type, device.index)
+    w = _WS.get(key)
+    if w is None:
+        w = (torch.empty(WS_FLOATS, dtype=torch.float32, device=device),
+             torch.zeros(N_COUNTERS, dtype=torch.int32, device=device))
+        _WS[key] = w
+    return w
+
+
 # ----------------------------------------------------------------------------- philox (CPU mirror)
 _M0, _M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
 _W0, _W1 = np.uint64(0x9E3779B9), np.uint64(0xBB67AE85)
@@ -102,7 +120,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, a_layout: str = "mk", b_layout: st
          z_out: Optional[torch.Tensor] = None, z_in: Optional[torch.Tensor] = None, act_bwd: str = "none",
          keep_prob: float = 1.0, seed: int = 0, offset: int = 0, resid: Optional[torch.Tensor] = None,
          dbias: Optional[torch.Tensor] = None, step: Optional[torch.Tensor] = None,
-         cfg: int = -1) -> torch.Tensor:
+         cfg: int = -1, splits: int = -1) -> torch.Tensor:
     """C = epilogue(alpha * A @ B).
 
     ``a`` holds logical A[M,K] as ``[M,K]`` (``a_layout="mk"``) or ``[K,M]`` ("km");
@@ -161,7 +179,10 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, a_layout: str = "mk", b_layout: st
     if step is not None:
         assert step.dtype == torch.int32
         g.step_ptr = step.data_ptr()
-    rc = _lib.lib().jdt_gemm(ctypes.byref(g), int(a.shape[0]) if batched else 1, int(cfg), _lib.stream_ptr())
+    ws, ctr = workspace(a.device)
+    rc = _lib.lib().jdt_gemm(ctypes.byref(g), int(a.shape[0]) if batched else 1, int(cfg), int(splits),
+                             ctypes.c_void_p(ws.data_ptr()), ws.numel(), ctypes.c_void_p(ctr.data_ptr()),
+                             ctr.numel(), _lib.stream_ptr())
     _lib.check(rc, "jdt_gemm")
     return out
 

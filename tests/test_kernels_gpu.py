@@ -3,7 +3,7 @@ ops/kernels.py, which rounds matmul operands to bf16 like the kernels do)."""
 import pytest
 import torch
 
-from jax_distributed_tuts_amd.ops import kernels as K
+from jax_distributed_tuts_amd.ops import kernels as kern
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -29,8 +29,8 @@ def _mk(shape, dtype, layout_t=False, seed=0):
 def test_gemm_layouts(M, N, K, a_layout, b_layout, adt):
     a = _mk((M, K) if a_layout == "mk" else (K, M), adt, seed=1)
     b = _mk((K, N) if b_layout == "kn" else (N, K), torch.bfloat16, seed=2)
-    ref = K.gemm(a, b, a_layout=a_layout, b_layout=b_layout, out_dtype=torch.float32)
-    out = K.gemm(a.to(DEV), b.to(DEV), a_layout=a_layout, b_layout=b_layout, out_dtype=torch.float32)
+    ref = kern.gemm(a, b, a_layout=a_layout, b_layout=b_layout, out_dtype=torch.float32)
+    out = kern.gemm(a.to(DEV), b.to(DEV), a_layout=a_layout, b_layout=b_layout, out_dtype=torch.float32)
     _close(out, ref, rtol=1e-3, atol=1e-3)
 
 
@@ -41,9 +41,9 @@ def test_gemm_fwd_epilogue(act):
     w = (_mk((K_, N), torch.float32, seed=4) * 0.05).to(torch.bfloat16)
     b = _mk((N,), torch.bfloat16, seed=5)
     zr = torch.empty(M, N, dtype=torch.bfloat16)
-    ref = K.gemm(x, w, bias=b, act=act, z_out=zr, keep_prob=0.9, seed=7, offset=11)
+    ref = kern.gemm(x, w, bias=b, act=act, z_out=zr, keep_prob=0.9, seed=7, offset=11)
     zg = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-    out = K.gemm(x.to(DEV), w.to(DEV), bias=b.to(DEV), act=act, z_out=zg, keep_prob=0.9, seed=7, offset=11)
+    out = kern.gemm(x.to(DEV), w.to(DEV), bias=b.to(DEV), act=act, z_out=zg, keep_prob=0.9, seed=7, offset=11)
     _close(zg, zr)
     _close(out, ref)
     # identical dropout mask (Philox bit parity CPU <-> GPU)
@@ -56,9 +56,9 @@ def test_gemm_bwd_epilogue_and_dbias():
     w = _mk((N, K_), torch.bfloat16, seed=7)  # [in=N, out=K] kernel read "nk"
     z = _mk((M, N), torch.bfloat16, seed=8)
     db_r = torch.zeros(N)
-    ref = K.gemm(dz, w, b_layout="nk", z_in=z, act_bwd="silu", keep_prob=0.9, seed=3, offset=5, dbias=db_r)
+    ref = kern.gemm(dz, w, b_layout="nk", z_in=z, act_bwd="silu", keep_prob=0.9, seed=3, offset=5, dbias=db_r)
     db_g = torch.zeros(N, device=DEV)
-    out = K.gemm(dz.to(DEV), w.to(DEV), b_layout="nk", z_in=z.to(DEV), act_bwd="silu", keep_prob=0.9, seed=3,
+    out = kern.gemm(dz.to(DEV), w.to(DEV), b_layout="nk", z_in=z.to(DEV), act_bwd="silu", keep_prob=0.9, seed=3,
                  offset=5, dbias=db_g)
     _close(out, ref)
     _close(db_g, db_r, rtol=2e-2, atol=5e-2)
@@ -69,17 +69,17 @@ def test_gemm_accumulate_fp32():
     dz = _mk((32, 512), torch.bfloat16, seed=10)
     x = _mk((32, 784), torch.float32, seed=9)
     acc_r = torch.ones(784, 512)
-    K.gemm(x, dz, a_layout="km", b_layout="kn", out=acc_r, accumulate=True)
+    kern.gemm(x, dz, a_layout="km", b_layout="kn", out=acc_r, accumulate=True)
     acc_g = torch.ones(784, 512, device=DEV)
-    K.gemm(x.to(DEV), dz.to(DEV), a_layout="km", b_layout="kn", out=acc_g, accumulate=True)
+    kern.gemm(x.to(DEV), dz.to(DEV), a_layout="km", b_layout="kn", out=acc_g, accumulate=True)
     _close(acc_g, acc_r, rtol=1e-3, atol=1e-3)
 
 
 def test_gemm_batched():
     a = _mk((3, 64, 96), torch.bfloat16, seed=11)
     b = _mk((3, 96, 80), torch.bfloat16, seed=12)
-    ref = K.gemm(a, b, out_dtype=torch.float32)
-    out = K.gemm(a.to(DEV), b.to(DEV), out_dtype=torch.float32)
+    ref = kern.gemm(a, b, out_dtype=torch.float32)
+    out = kern.gemm(a.to(DEV), b.to(DEV), out_dtype=torch.float32)
     _close(out, ref, rtol=1e-3, atol=1e-3)
 
 
@@ -91,10 +91,10 @@ def test_xent(M, C, dt):
     y[0] = -1  # ignored row
     d_r = torch.empty(M, C, dtype=torch.bfloat16)
     db_r, m_r, l_r = torch.zeros(C), torch.zeros(4), torch.zeros(M)
-    K.softmax_xent(z, y, grad_scale=1 / M, dlogits=d_r, dbias=db_r, metrics=m_r, row_loss=l_r)
+    kern.softmax_xent(z, y, grad_scale=1 / M, dlogits=d_r, dbias=db_r, metrics=m_r, row_loss=l_r)
     d_g = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
     db_g, m_g, l_g = torch.zeros(C, device=DEV), torch.zeros(4, device=DEV), torch.zeros(M, device=DEV)
-    K.softmax_xent(z.to(DEV), y.to(DEV), grad_scale=1 / M, dlogits=d_g, dbias=db_g, metrics=m_g, row_loss=l_g)
+    kern.softmax_xent(z.to(DEV), y.to(DEV), grad_scale=1 / M, dlogits=d_g, dbias=db_g, metrics=m_g, row_loss=l_g)
     _close(l_g, l_r, rtol=1e-4, atol=1e-4)
     _close(d_g, d_r, rtol=1e-2, atol=1e-4)
     _close(db_g, db_r, rtol=1e-2, atol=1e-4)
@@ -114,7 +114,7 @@ def test_adamw_and_step_counter():
         step, ticket = torch.zeros(1, dtype=torch.int32, device=dev), torch.zeros(1, dtype=torch.int32, device=dev)
         for _ in range(3):
             G.copy_(gr.to(dev))
-            K.adamw_step(P, G, m, v, sh, lr=1e-3, grad_scale=0.25, step=step, ticket=ticket)
+            kern.adamw_step(P, G, m, v, sh, lr=1e-3, grad_scale=0.25, step=step, ticket=ticket)
         st[dev] = (P.cpu(), sh.cpu(), step.cpu(), G.cpu())
     _close(st[DEV][0], st["cpu"][0], rtol=1e-5, atol=1e-6)
     assert int(st[DEV][2]) == 3 and float(st[DEV][3].abs().max()) == 0.0
@@ -126,9 +126,9 @@ def test_act_bwd():
     dh, z = _mk((M, N), torch.bfloat16, seed=1), _mk((M, N), torch.bfloat16, seed=2)
     step = torch.tensor([5], dtype=torch.int32)
     db_r = torch.zeros(N)
-    r = K.act_bwd(dh, z, "gelu", keep_prob=0.8, seed=9, offset=3, step=step, dbias=db_r)
+    r = kern.act_bwd(dh, z, "gelu", keep_prob=0.8, seed=9, offset=3, step=step, dbias=db_r)
     db_g = torch.zeros(N, device=DEV)
-    o = K.act_bwd(dh.to(DEV), z.to(DEV), "gelu", keep_prob=0.8, seed=9, offset=3, step=step.to(DEV), dbias=db_g)
+    o = kern.act_bwd(dh.to(DEV), z.to(DEV), "gelu", keep_prob=0.8, seed=9, offset=3, step=step.to(DEV), dbias=db_g)
     _close(o, r)
     _close(db_g, db_r, rtol=1e-2, atol=1e-2)
 
@@ -175,3 +175,23 @@ def test_dp_graph_replay_matches_eager():
     assert out[0][2] == out[1][2] == 6
     torch.testing.assert_close(out[1][0], out[0][0], rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(out[1][1], out[0][1], rtol=1e-6, atol=1e-5)
+
+
+@pytest.mark.parametrize("splits", [1, 3, 7, 16])
+@pytest.mark.parametrize("M,N,K_,cfg", [(32, 512, 784, 0), (128, 10, 512, 4), (784, 512, 128, 2)])
+def test_gemm_split_k(splits, M, N, K_, cfg):
+    """In-kernel split-K (slab + last-arriver combine) must match the single-slice result,
+    including the fused epilogue (bias/act/dropout) and fp32 accumulate."""
+    x = _mk((M, K_), torch.float32, seed=21)
+    w = (_mk((K_, N), torch.float32, seed=22) * 0.05).to(torch.bfloat16)
+    b = _mk((N,), torch.bfloat16, seed=23)
+    ref = kern.gemm(x, w, bias=b, act="silu", keep_prob=0.9, seed=1, offset=2)
+    for _ in range(2):  # second call exercises the re-armed arrival counters
+        out = kern.gemm(x.to(DEV), w.to(DEV), bias=b.to(DEV), act="silu", keep_prob=0.9, seed=1, offset=2, cfg=cfg,
+                        splits=splits)
+        _close(out, ref)
+    acc_r = torch.full((M, N), 0.5)
+    kern.gemm(x, w, out=acc_r, accumulate=True)
+    acc_g = torch.full((M, N), 0.5, device=DEV)
+    kern.gemm(x.to(DEV), w.to(DEV), out=acc_g, accumulate=True, cfg=cfg, splits=splits)
+    _close(acc_g, acc_r, rtol=1e-3, atol=1e-3)

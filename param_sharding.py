@@ -1,0 +1,61 @@
+"""FSDP / ZeRO-3 training of the tutorial classifier (reference param_sharding.py).
+
+    torchrun --nproc-per-node 8 param_sharding.py   # 8 MI355X, RCCL over xGMI
+    python param_sharding.py --sim-cpu 8            # 8 gloo CPU ranks
+
+Params, grads and AdamW moments are sharded with the reference rule
+(min_weight_size = 2**4 as set at param_sharding.py:244-246); shard table in
+SURVEY §2.7.  Schedule: 15 steps + 1 printed step "FSDP - Final metrics"
+(param_sharding.py:389-397).
+"""
+from __future__ import annotations
+
+import argparse
+
+import torch
+
+from data_paral import synthetic_batch
+from jax_distributed_tuts_amd.models.mlp import Classifier
+from jax_distributed_tuts_amd.parallel.dp import shard_batch
+from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
+from jax_distributed_tuts_amd.runtime import dist as D
+from jax_distributed_tuts_amd.runtime.dist import Mesh
+from jax_distributed_tuts_amd.runtime.launch import run
+from jax_distributed_tuts_amd.utils.config import fsdp_config
+from jax_distributed_tuts_amd.utils.metrics import print_metrics
+from jax_distributed_tuts_amd.utils.train_state import Batch, adamw, get_num_params
+
+
+def main(args):
+    cfg = fsdp_config()
+    cfg.model.num_layers = args.num_layers
+    dev = D.device()
+    axis = cfg.model.data_axis_name
+    mesh = Mesh({axis: D.world_size()})
+    model = Classifier.from_config(cfg.model)
+    state = init_fsdp(model, adamw(cfg.model.lr), cfg.seed, dev, mesh, axis, cfg.model.min_weight_size)
+    batch = shard_batch(synthetic_batch(cfg, cfg.seed + 1), mesh, axis)
+    batch = Batch(batch.inputs.to(dev), batch.labels.to(dev))
+    tr = FSDPTrainer(state, mesh, FSDPConfig(cfg.num_minibatches, cfg.model.min_weight_size, axis,
+                                             gather_once=args.gather_once, scatter_once=args.scatter_once))
+    if D.rank() == 0:
+        sp = state.extra["sharded"]
+        print(f"[param_sharding] {mesh} global params={get_num_params(sp)} local flat={sp.local.numel} "
+              f"sharded={sp.sharded_names} replicated={sp.repl_names}")
+    for _ in range(args.steps):
+        tr.step(batch)
+    tr.metrics.zero_()
+    tr.step(batch)
+    if D.rank() == 0:
+        print_metrics(tr.metrics, "FSDP - Final metrics")
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sim-cpu", type=int, default=None)
+    ap.add_argument("--steps", type=int, default=15)
+    ap.add_argument("--num-layers", type=int, default=2)
+    ap.add_argument("--gather-once", action="store_true")
+    ap.add_argument("--scatter-once", action="store_true")
+    a = ap.parse_args()
+    run(main, a, sim_cpu=a.sim_cpu)

@@ -1,0 +1,104 @@
+"""Worker bodies for the multi-process gloo tests (importable by spawned children)."""
+import os
+
+import torch
+
+from jax_distributed_tuts_amd.comm import collectives as C
+from jax_distributed_tuts_amd.runtime import dist as D
+from jax_distributed_tuts_amd.runtime.dist import Mesh
+
+
+def _save(out_dir, name, obj):
+    torch.save(obj, os.path.join(out_dir, f"{name}_r{D.rank()}.pt"))
+
+
+def collectives(out_dir):
+    ws, r = D.world_size(), D.rank()
+    mesh = Mesh({"data": ws})
+    x = torch.arange(8, dtype=torch.float32) + 100 * r
+    res = {}
+    res["psum"] = C.psum_(x.clone(), mesh, "data")
+    res["pmean"] = C.pmean_(x.clone(), mesh, "data")
+    res["ag0"] = C.all_gather(x.view(2, 4), mesh, "data", dim=0)
+    res["ag1"] = C.all_gather(x.view(2, 4), mesh, "data", dim=1)
+    res["rs"] = C.psum_scatter(torch.arange(4 * ws, dtype=torch.float32).view(2 * ws, 2) * (r + 1), mesh, "data")
+    res["ring"] = C.ppermute(x, mesh, "data", [(i, (i + 1) % ws) for i in range(ws)])
+    res["idx"] = C.axis_index(mesh, "data")
+    _save(out_dir, "coll", res)
+
+
+def mesh2d(out_dir):
+    mesh = Mesh({"data": 2, "pipe": D.world_size() // 2})
+    x = torch.tensor([float(D.rank())])
+    res = {"coords": mesh.coords, "data_sum": C.psum_(x.clone(), mesh, "data"),
+           "pipe_sum": C.psum_(x.clone(), mesh, "pipe"), "pipe_ranks": mesh.group_ranks("pipe"),
+           "data_ranks": mesh.group_ranks("data")}
+    _save(out_dir, "mesh", res)
+
+
+def gather_mean_grad(out_dir):
+    from jax_distributed_tuts_amd.parallel.fsdp import gather_arr_mean_grads
+
+    ws, r = D.world_size(), D.rank()
+    mesh = Mesh({"data": ws})
+    shard = (torch.arange(6, dtype=torch.float32).view(3, 2) + 10 * r).requires_grad_()
+    full = gather_arr_mean_grads(shard, mesh, "data", 0)
+    w = torch.arange(full.numel(), dtype=torch.float32).view_as(full) * (r + 1)
+    (full * w).sum().backward()
+    _save(out_dir, "gmg", {"full": full.detach(), "grad": shard.grad})
+
+
+def dp_vs_single(out_dir, accum):
+    from data_paral import synthetic_batch
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp, shard_batch
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.train_state import adamw
+
+    cfg = dp_config()
+    mesh = Mesh({"data": D.world_size()})
+    model = Classifier(dropout_rate=0.0)
+    st = init_dp(model, adamw(1e-3), 69, "cpu", mesh)
+    batch = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
+    tr = DataParallelTrainer(st, mesh, DPConfig(4, accum))
+    for _ in range(3):
+        tr.step(batch)
+    _save(out_dir, f"dp_{accum}", {"params": st.params.state_dict(), "metrics": tr.metrics.clone()})
+
+
+def fsdp_run(out_dir, gather_once):
+    from data_paral import synthetic_batch
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import shard_batch
+    from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.train_state import adamw
+
+    cfg = dp_config()
+    mesh = Mesh({"data": D.world_size()})
+    model = Classifier(dropout_rate=0.0)
+    st = init_fsdp(model, adamw(1e-3), 69, "cpu", mesh, "data", 16)
+    batch = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
+    tr = FSDPTrainer(st, mesh, FSDPConfig(4, 16, "data", gather_once=gather_once, scatter_once=gather_once))
+    for _ in range(3):
+        tr.step(batch)
+    _save(out_dir, f"fsdp_{int(gather_once)}", {"params": tr.full_params(), "metrics": tr.metrics.clone()})
+
+
+def sharded_module(out_dir):
+    from jax_distributed_tuts_amd.parallel.fsdp import shard_module_params, sync_gradients
+
+    ws = D.world_size()
+    mesh = Mesh({"data": ws})
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(16, 8), torch.nn.Tanh(), torch.nn.Linear(8, 4))
+    ref = {n: p.detach().clone() for n, p in net.named_parameters()}
+    sm = shard_module_params(net, mesh, "data", min_weight_size=4)
+    g = torch.Generator().manual_seed(D.rank())
+    x = torch.randn(5, 16, generator=g)
+    out = sm(x)
+    out.square().mean().backward()
+    grads = sync_gradients(sm.partitioned_grads(), mesh, ["data"])
+    _save(out_dir, "sm", {"ref": ref, "x": x, "out": out.detach(),
+                          "grads": {k: (v.value if hasattr(v, "value") else v) for k, v in grads.items()},
+                          "meta": sm.meta})

@@ -102,3 +102,18 @@ def sharded_module(out_dir):
     _save(out_dir, "sm", {"ref": ref, "x": x, "out": out.detach(),
                           "grads": {k: (v.value if hasattr(v, "value") else v) for k, v in grads.items()},
                           "meta": sm.meta})
+
+
+def pp_run(out_dir, dp, n_hidden=3, n_mb=4, steps=3):
+    from data_paral import synthetic_batch
+    from pipeline_parallel import build_mlp_pipeline
+    from jax_distributed_tuts_amd.parallel.dp import shard_batch
+    from jax_distributed_tuts_amd.utils.config import dp_config
+
+    cfg = dp_config()
+    mesh = Mesh({"data": dp, "pipe": D.world_size() // dp})
+    tr = build_mlp_pipeline(cfg, mesh, "cpu", n_hidden_layers=n_hidden, dropout_rate=0.0, num_microbatches=n_mb)
+    batch = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
+    for _ in range(steps):
+        tr.step(batch)
+    _save(out_dir, f"pp_dp{dp}", {"params": tr.state.params.state_dict(), "metrics": tr.gather_metrics()})

@@ -13,13 +13,13 @@ from . import dist_workers as W
 pytestmark = pytest.mark.slow
 
 
-def _adam_close(a, b, lr=1e-3, steps=3):
+def _adam_close(a, b, lr=1e-3, steps=3, frac=1e-3):
     """Adam normalises each coordinate, so an element whose gradient is ~0 can move
     by up to lr per step from rounding-order noise alone; require that only a tiny
     fraction of elements deviate, and none by more than the Adam step bound."""
     d = (a.float() - b.float()).abs()
     assert float(d.max()) <= 2 * lr * steps + 1e-6, float(d.max())
-    assert float((d > 5e-5).float().mean()) < 1e-3
+    assert float((d > 5e-5).float().mean()) < frac
 
 
 def _metrics_close(m, ref):
@@ -138,3 +138,42 @@ def test_shard_module_params_autograd(tmp_path):
             else:
                 exp = full_grads[n]
             torch.testing.assert_close(g, exp, rtol=1e-4, atol=1e-6)
+
+
+def _single_mlp_reference(n_hidden=3, steps=3, n_mb=4):
+    from data_paral import synthetic_batch
+    from pipeline_parallel import pp_mlp_dims
+    from jax_distributed_tuts_amd.models.mlp import MLP
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.flat import FlatParams
+    from jax_distributed_tuts_amd.utils.train_state import TrainState, adamw
+    from jax_distributed_tuts_amd.utils import rng as R
+
+    cfg = dp_config()
+    model = MLP(pp_mlp_dims(cfg, n_hidden), dropout_rate=0.0)
+    P = FlatParams(model.param_specs()).init_(cfg.seed)
+    st = TrainState.create(apply_fn=model, params=P, tx=adamw(1e-3), rng=R.PRNGKey(cfg.seed))
+    tr = DataParallelTrainer(st, None, DPConfig(n_mb, "loop"))
+    b = synthetic_batch(cfg, 70)
+    for _ in range(steps):
+        tr.step(b)
+    return P.state_dict(), tr.metrics
+
+
+@pytest.mark.parametrize("ws,dp", [(2, 1), (4, 1), (4, 2)])
+def test_pipeline_equals_single_device(tmp_path, ws, dp):
+    """GPipe over S stages (and hybrid DP x PP) == the un-split model on one device
+    (dropout off): per-stage params match the corresponding slice."""
+    spawn(functools.partial(W.pp_run, dp=dp), ws, str(tmp_path))
+    res = _load(tmp_path, f"pp_dp{dp}", ws)
+    ref_p, ref_m = _single_mlp_reference()
+    seen = set()
+    for o in res:
+        for k, v in o["params"].items():
+            # a stage boundary rounds dh to bf16 before act' (the fused single-device
+            # epilogue rounds once), so allow a few % of Adam-amplified coordinates
+            _adam_close(v, ref_p[k], frac=5e-2)
+            seen.add(k)
+        _metrics_close(o["metrics"], ref_m)
+    assert seen == set(ref_p)

@@ -72,6 +72,24 @@ class MLP:
             out.append(ParamSpec(f"{n}/bias", (self.dims[i + 1],), "zeros"))
         return out
 
+    # stage / loss-head metadata shared with TransformerLM (pipeline + loss code is model-agnostic)
+    @property
+    def head_bias_name(self) -> Optional[str]:
+        return None if self.final_act else f"{self.names[-1]}/bias"
+
+    def input_shape(self, rows: int):
+        return (rows, self.dims[0])
+
+    def input_dtype(self):
+        return torch.bfloat16
+
+    def output_shape(self, rows: int):
+        return (rows, self.dims[-1])
+
+    @staticmethod
+    def flatten_labels(y: torch.Tensor) -> torch.Tensor:
+        return y
+
     def _hidden(self, i: int) -> bool:
         return i < self.L - 1 or self.final_act
 
@@ -150,13 +168,19 @@ class Classifier(MLP):
                    num_layers=cfg.get("num_layers", 2), act=cfg.get("act", "silu"))
 
 
-def loss_and_grad(model: MLP, P: FlatParams, x: torch.Tensor, labels: torch.Tensor, *, train: bool, seed: int,
-                  offset: int, step: Optional[torch.Tensor], grad_scale: float, metrics: Optional[torch.Tensor]):
-    """One minibatch: forward, fused CE(+metrics), backward into P.grad (beta=1)."""
+def loss_and_grad(model, P: FlatParams, x: torch.Tensor, labels: torch.Tensor, *, train: bool, seed: int,
+                  offset: int, step: Optional[torch.Tensor], grad_scale: Optional[float] = None,
+                  metrics: Optional[torch.Tensor] = None):
+    """One minibatch: forward, fused CE(+metrics, +head bias grad), explicit backward
+    into P.grad (beta=1).  ``grad_scale`` defaults to 1/#labels (mean loss).
+    Works for any model exposing forward/backward/flatten_labels/head_bias_name."""
     logits, cache = model.forward(P, x, train=train, seed=seed, offset=offset, step=step)
+    y = model.flatten_labels(labels)
+    if grad_scale is None:
+        grad_scale = 1.0 / y.numel()
     dlogits = torch.empty_like(logits)
-    top = model.names[-1]
-    K.softmax_xent(logits, labels, grad_scale=grad_scale, dlogits=dlogits, dbias=P.g(f"{top}/bias"),
+    hb = model.head_bias_name
+    K.softmax_xent(logits, y, grad_scale=grad_scale, dlogits=dlogits, dbias=P.g(hb) if hb else None,
                    metrics=metrics)
     model.backward(P, cache, dlogits)
     return logits

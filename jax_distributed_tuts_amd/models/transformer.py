@@ -1,0 +1,196 @@
+"""Decoder-only transformer LM for the hybrid DP x PP tutorial (BASELINE config #5:
+"4-layer transformer hybrid DP=2 x PP=4").  The reference has no transformer;
+sizes are ours (documented in README): vocab 2048, d_model 512, 8 heads of 64,
+d_ff 2048, seq 128, pre-LN, learned positions, GELU(tanh), untied LM head.
+
+Like models/mlp.py the backward is explicit: every matmul is the gfx950 MFMA
+GEMM with fused epilogues (bias, GELU + pre-activation save, residual add on
+the forward; GELU' + bias-grad on the backward; fp32 beta=1 weight-grad
+accumulation), LayerNorm fwd/bwd kernels fuse the residual-gradient add, and
+attention is S = a.QK^T (GEMM reading q/k heads in place from the fused QKV
+activation) -> causal softmax kernel -> P.V (GEMM writing heads in place).
+
+A model instance can be a pipeline stage: ``layers`` selects a contiguous
+block range, ``has_embed``/``has_head`` mark the first/last stage.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+
+from ..ops import kernels as K
+from ..utils.flat import FlatParams, ParamSpec
+
+
+@dataclass
+class TransformerConfig:
+    vocab_size: int = 2048
+    d_model: int = 512
+    n_heads: int = 8
+    d_ff: int = 2048
+    seq_len: int = 128
+    n_layers: int = 4
+    dropout_rate: float = 0.0
+    ln_eps: float = 1e-6
+
+
+@dataclass
+class _BlockCache:
+    x: torch.Tensor
+    h1: torch.Tensor
+    m1: torch.Tensor
+    r1: torch.Tensor
+    qkv: torch.Tensor
+    o: torch.Tensor
+    P: torch.Tensor
+    x2: torch.Tensor
+    h2: torch.Tensor
+    m2: torch.Tensor
+    r2: torch.Tensor
+    z1: torch.Tensor
+    u: torch.Tensor
+    off: int
+
+
+@dataclass
+class _Cache:
+    inp: torch.Tensor
+    nseq: int
+    blocks: List[_BlockCache] = field(default_factory=list)
+    xf: Optional[torch.Tensor] = None
+    hf: Optional[torch.Tensor] = None
+    mf: Optional[torch.Tensor] = None
+    rf: Optional[torch.Tensor] = None
+    seed: int = 0
+    keep: float = 1.0
+    step: Optional[torch.Tensor] = None
+
+
+class TransformerLM:
+    def __init__(self, cfg: TransformerConfig = TransformerConfig(), layers: Optional[range] = None,
+                 has_embed: bool = True, has_head: bool = True):
+        self.cfg = cfg
+        self.layers = range(cfg.n_layers) if layers is None else layers
+        self.has_embed, self.has_head = has_embed, has_head
+        self.names = [f"block_{l}" for l in self.layers] + (["head"] if has_head else [])
+
+    # ------------------------------------------------------------------ metadata
+    @property
+    def head_bias_name(self) -> Optional[str]:
+        return "head/bias" if self.has_head else None
+
+    def input_shape(self, nseq: int):
+        return (nseq, self.cfg.seq_len) if self.has_embed else (nseq * self.cfg.seq_len, self.cfg.d_model)
+
+    def input_dtype(self):
+        return torch.int32 if self.has_embed else torch.bfloat16
+
+    def output_shape(self, nseq: int):
+        c = self.cfg
+        return (nseq * c.seq_len, c.vocab_size if self.has_head else c.d_model)
+
+    @staticmethod
+    def flatten_labels(y: torch.Tensor) -> torch.Tensor:
+        return y.reshape(-1)
+
+    def param_specs(self) -> List[ParamSpec]:
+        c = self.cfg
+        d = c.d_model
+        out = []
+        if self.has_embed:
+            out += [ParamSpec("embed/wte", (c.vocab_size, d), "normal:0.02"),
+                    ParamSpec("embed/wpe", (c.seq_len, d), "normal:0.02")]
+        for l in self.layers:
+            b = f"block_{l}"
+            out += [ParamSpec(f"{b}/ln1/scale", (d,), "ones"), ParamSpec(f"{b}/ln1/bias", (d,), "zeros"),
+                    ParamSpec(f"{b}/attn/qkv/kernel", (d, 3 * d)), ParamSpec(f"{b}/attn/qkv/bias", (3 * d,), "zeros"),
+                    ParamSpec(f"{b}/attn/out/kernel", (d, d)), ParamSpec(f"{b}/attn/out/bias", (d,), "zeros"),
+                    ParamSpec(f"{b}/ln2/scale", (d,), "ones"), ParamSpec(f"{b}/ln2/bias", (d,), "zeros"),
+                    ParamSpec(f"{b}/mlp/fc1/kernel", (d, c.d_ff)), ParamSpec(f"{b}/mlp/fc1/bias", (c.d_ff,), "zeros"),
+                    ParamSpec(f"{b}/mlp/fc2/kernel", (c.d_ff, d)), ParamSpec(f"{b}/mlp/fc2/bias", (d,), "zeros")]
+        if self.has_head:
+            out += [ParamSpec("ln_f/scale", (d,), "ones"), ParamSpec("ln_f/bias", (d,), "zeros"),
+                    ParamSpec("head/kernel", (d, c.vocab_size)), ParamSpec("head/bias", (c.vocab_size,), "zeros")]
+        return out
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, P: FlatParams, x: torch.Tensor, *, train: bool = False, seed: int = 0, offset: int = 0,
+                step: Optional[torch.Tensor] = None):
+        c = self.cfg
+        keep = 1.0 - c.dropout_rate if train else 1.0
+        if self.has_embed:
+            nseq = x.shape[0]
+            tok = x.reshape(-1).contiguous()
+            h = K.embed_fwd(tok, P.s("embed/wte"), P.s("embed/wpe"), c.seq_len)
+            cache = _Cache(inp=tok, nseq=nseq, seed=seed, keep=keep, step=step)
+        else:
+            nseq = x.shape[0] // c.seq_len
+            h = x
+            cache = _Cache(inp=x, nseq=nseq, seed=seed, keep=keep, step=step)
+        for l in self.layers:
+            b = f"block_{l}"
+            h1, m1, r1 = K.layernorm_fwd(h, P.p(f"{b}/ln1/scale"), P.p(f"{b}/ln1/bias"), c.ln_eps)
+            qkv = K.gemm(h1, P.s(f"{b}/attn/qkv/kernel"), bias=P.s(f"{b}/attn/qkv/bias"))
+            o, Pm = K.attention_fwd(qkv, nseq, c.seq_len, c.n_heads, causal=True)
+            x2 = K.gemm(o, P.s(f"{b}/attn/out/kernel"), bias=P.s(f"{b}/attn/out/bias"), resid=h)
+            h2, m2, r2 = K.layernorm_fwd(x2, P.p(f"{b}/ln2/scale"), P.p(f"{b}/ln2/bias"), c.ln_eps)
+            z1 = torch.empty(h2.shape[0], c.d_ff, dtype=torch.bfloat16, device=h2.device)
+            off = int(offset) + (l << 1)
+            u = K.gemm(h2, P.s(f"{b}/mlp/fc1/kernel"), bias=P.s(f"{b}/mlp/fc1/bias"), act="gelu", z_out=z1,
+                       keep_prob=keep, seed=seed, offset=off, step=step)
+            x3 = K.gemm(u, P.s(f"{b}/mlp/fc2/kernel"), bias=P.s(f"{b}/mlp/fc2/bias"), resid=x2)
+            cache.blocks.append(_BlockCache(h, h1, m1, r1, qkv, o, Pm, x2, h2, m2, r2, z1, u, off))
+            h = x3
+        if self.has_head:
+            hf, mf, rf = K.layernorm_fwd(h, P.p("ln_f/scale"), P.p("ln_f/bias"), c.ln_eps)
+            cache.xf, cache.hf, cache.mf, cache.rf = h, hf, mf, rf
+            h = K.gemm(hf, P.s("head/kernel"), bias=P.s("head/bias"))
+        return h, cache
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, P: FlatParams, cache: _Cache, dout: torch.Tensor, *, dout_is_dz: bool = True,
+                 need_dx: bool = False) -> Optional[torch.Tensor]:
+        c = self.cfg
+        if self.has_head:
+            # dlogits (CE already added the head bias grad)
+            K.gemm(cache.hf, dout, a_layout="km", b_layout="kn", out=P.g("head/kernel"), accumulate=True)
+            dhf = K.gemm(dout, P.s("head/kernel"), b_layout="nk")
+            dx = K.layernorm_bwd(dhf, cache.xf, cache.mf, cache.rf, P.p("ln_f/scale"), P.g("ln_f/scale"),
+                                 P.g("ln_f/bias"))
+        else:
+            dx = dout
+        for l, bc in zip(reversed(list(self.layers)), reversed(cache.blocks)):
+            b = f"block_{l}"
+            # x3 = x2 + u.W2 + b2
+            K.colsum_(dx, P.g(f"{b}/mlp/fc2/bias"))
+            K.gemm(bc.u, dx, a_layout="km", b_layout="kn", out=P.g(f"{b}/mlp/fc2/kernel"), accumulate=True)
+            dz1 = K.gemm(dx, P.s(f"{b}/mlp/fc2/kernel"), b_layout="nk", z_in=bc.z1, act_bwd="gelu",
+                         keep_prob=cache.keep, seed=cache.seed, offset=bc.off, step=cache.step,
+                         dbias=P.g(f"{b}/mlp/fc1/bias"))
+            K.gemm(bc.h2, dz1, a_layout="km", b_layout="kn", out=P.g(f"{b}/mlp/fc1/kernel"), accumulate=True)
+            dh2 = K.gemm(dz1, P.s(f"{b}/mlp/fc1/kernel"), b_layout="nk")
+            dx2 = K.layernorm_bwd(dh2, bc.x2, bc.m2, bc.r2, P.p(f"{b}/ln2/scale"), P.g(f"{b}/ln2/scale"),
+                                  P.g(f"{b}/ln2/bias"), dres=dx)
+            # x2 = x + o.Wo + bo
+            K.colsum_(dx2, P.g(f"{b}/attn/out/bias"))
+            K.gemm(bc.o, dx2, a_layout="km", b_layout="kn", out=P.g(f"{b}/attn/out/kernel"), accumulate=True)
+            do = K.gemm(dx2, P.s(f"{b}/attn/out/kernel"), b_layout="nk")
+            dqkv = K.attention_bwd(do, bc.qkv, bc.P, cache.nseq, c.seq_len, c.n_heads)
+            K.colsum_(dqkv, P.g(f"{b}/attn/qkv/bias"))
+            K.gemm(bc.h1, dqkv, a_layout="km", b_layout="kn", out=P.g(f"{b}/attn/qkv/kernel"), accumulate=True)
+            dh1 = K.gemm(dqkv, P.s(f"{b}/attn/qkv/kernel"), b_layout="nk")
+            dx = K.layernorm_bwd(dh1, bc.x, bc.m1, bc.r1, P.p(f"{b}/ln1/scale"), P.g(f"{b}/ln1/scale"),
+                                 P.g(f"{b}/ln1/bias"), dres=dx2)
+        if self.has_embed:
+            K.embed_bwd(dx, cache.inp, P.g("embed/wte"), P.g("embed/wpe"), c.seq_len)
+            return None
+        return dx if need_dx else None
+
+
+def lm_stage(cfg: TransformerConfig, n_stages: int, stage: int) -> TransformerLM:
+    from ..parallel.pipeline import split_layers
+
+    r = split_layers(cfg.n_layers, n_stages)[stage]
+    return TransformerLM(cfg, layers=r, has_embed=stage == 0, has_head=stage == n_stages - 1)

@@ -34,6 +34,7 @@ class GemmArgs(ctypes.Structure):
         ("dbias", c_void_p),
         ("C", c_void_p), ("ldc", c_long), ("sC", c_long), ("c_f32", c_int), ("accumulate", c_int),
         ("step_ptr", c_void_p),
+        ("zin", c_int), ("sA2", c_long), ("sB2", c_long), ("sC2", c_long),
     ]
 
 
@@ -51,6 +52,15 @@ _SIGS = {
     "jdt_act_bwd": (c_int, [c_void_p, c_void_p, c_int, c_float, c_ulonglong, c_ulonglong, c_void_p, c_int, c_int,
                             c_void_p, c_void_p, c_void_p]),
     "jdt_metrics_fold": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    "jdt_ln_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,
+                           c_void_p]),
+    "jdt_ln_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_int, c_int, c_void_p]),
+    "jdt_attn_softmax_fwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "jdt_attn_softmax_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
+    "jdt_embed_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "jdt_embed_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "jdt_colsum": (c_int, [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p]),
 }
 
 

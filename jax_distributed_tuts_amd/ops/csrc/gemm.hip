@@ -44,7 +44,14 @@ struct GemmArgs {
   // device step counter: dropout offset += step << 32, so a replayed hipGraph
   // draws a fresh mask every step without re-recording kernel arguments
   const int* step_ptr;
+  // optional 2-level batch: z -> (z / zin, z % zin) with strides (sX, sX2) for
+  // A, B and C (attention: batch x head over the fused [T, 3d] QKV buffer)
+  int zin; long sA2, sB2, sC2;
 };
+
+__device__ __forceinline__ long zoff(const GemmArgs& g, int z, long s1, long s2) {
+  return g.zin > 1 ? (long)(z / g.zin) * s1 + (long)(z % g.zin) * s2 : (long)z * s1;
+}
 
 template <int WM, int WN, int TM, int TN, int BK>
 struct Tile {
@@ -158,8 +165,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
   const int tn0 = (bid % tiles_n) * BN;
   const int z = blockIdx.z;
 
-  const void* Ab = static_cast<const char*>(g.A) + (long)z * g.sA * (AF32 ? 4 : 2);
-  const void* Bb = static_cast<const char*>(g.B) + (long)z * g.sB * (BF32 ? 4 : 2);
+  const void* Ab = static_cast<const char*>(g.A) + zoff(g, z, g.sA, g.sA2) * (AF32 ? 4 : 2);
+  const void* Bb = static_cast<const char*>(g.B) + zoff(g, z, g.sB, g.sB2) * (BF32 ? 4 : 2);
   // shift operand bases to this tile
   const long a_off = g.a_trans ? (long)tm0 : (long)tm0 * g.lda;
   const long b_off = g.b_trans ? (long)tn0 : (long)tn0 * g.ldb;
@@ -320,7 +327,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
           v = dropout_keep(g.seed, doff, idx, g.keep_prob) ? v * inv_keep : 0.f;
         }
         if (g.resid) v += bf2f(static_cast<const bf16_t*>(g.resid)[(long)z * g.sR + (long)row * g.ldr + col]);
-        const long co = (long)z * g.sC + (long)row * g.ldc + col;
+        const long co = zoff(g, z, g.sC, g.sC2) + (long)row * g.ldc + col;
         if (g.c_f32) {
           float* Cp = static_cast<float*>(g.C) + co;
           *Cp = g.accumulate ? *Cp + v : v;

@@ -1,0 +1,190 @@
+// LayerNorm forward / backward for the transformer tutorial model.
+//
+// One wave per row (row length d <= 2048, held in registers, 8-element
+// 16-byte vector loads per lane); fp32 statistics, bf16 in/out, fp32 affine
+// params read from the master buffer.  The backward fuses the residual-branch
+// gradient add (dx = dres + LN'(dy)) and reduces dgamma/dbeta per workgroup in
+// LDS before one atomic per column per workgroup.
+#include "common.h"
+
+namespace jdt {
+
+constexpr int LN_MAXV = 4;  // 4 x 8 x 64 = 2048 columns max
+
+template <int NV>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, bf16_t* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int T, int d, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= T) return;
+  const bf16_t* xr = x + (long)row * d;
+  float v[NV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < d) {
+      const u32x4 p = *reinterpret_cast<const u32x4*>(xr + col);
+      const unsigned w[4] = {p.x, p.y, p.z, p.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[c][2 * j] = bf2f((bf16_t)(w[j] & 0xffff));
+        v[c][2 * j + 1] = bf2f((bf16_t)(w[j] >> 16));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[c][j];
+  }
+  const float mean = wave_sum(s) / d;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < d)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float t = v[c][j] - mean; q += t * t; }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / d + eps);
+  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < d) {
+      unsigned w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a = (v[c][2 * j] - mean) * rstd * gamma[col + 2 * j] + beta[col + 2 * j];
+        const float b = (v[c][2 * j + 1] - mean) * rstd * gamma[col + 2 * j + 1] + beta[col + 2 * j + 1];
+        w[j] = (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+      }
+      u32x4 o; o.x = w[0]; o.y = w[1]; o.z = w[2]; o.w = w[3];
+      *reinterpret_cast<u32x4*>(y + (long)row * d + col) = o;
+    }
+  }
+}
+
+// ROWS rows per workgroup (4 waves x ROWS/4 rows each); dgamma/dbeta partials in LDS.
+template <int NV>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+                                                     const float* __restrict__ gamma, const bf16_t* __restrict__ dres,
+                                                     bf16_t* __restrict__ dx, float* __restrict__ dgamma,
+                                                     float* __restrict__ dbeta, int T, int d, int rows_per_wave) {
+  __shared__ float sg[2048], sb[2048];
+  for (int i = threadIdx.x; i < d; i += 256) { sg[i] = 0.f; sb[i] = 0.f; }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float ag[NV][8], ab[NV][8];
+#pragma unroll
+  for (int c = 0; c < NV; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { ag[c][j] = 0.f; ab[c][j] = 0.f; }
+  const int r0 = (blockIdx.x * 4 + w) * rows_per_wave;
+  for (int row = r0; row < min(T, r0 + rows_per_wave); ++row) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[NV][8], g[NV][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      if (col < d) {
+        const u32x4 px = *reinterpret_cast<const u32x4*>(x + (long)row * d + col);
+        const u32x4 pd = *reinterpret_cast<const u32x4*>(dy + (long)row * d + col);
+        const unsigned wx[4] = {px.x, px.y, px.z, px.w}, wd[4] = {pd.x, pd.y, pd.z, pd.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xv = bf2f((bf16_t)((wx[j >> 1] >> (16 * (j & 1))) & 0xffff));
+          const float dv = bf2f((bf16_t)((wd[j >> 1] >> (16 * (j & 1))) & 0xffff));
+          xh[c][j] = (xv - mean) * rstd;
+          g[c][j] = dv * gamma[col + j];
+          s1 += g[c][j];
+          s2 += g[c][j] * xh[c][j];
+          ag[c][j] += dv * xh[c][j];
+          ab[c][j] += dv;
+        }
+      }
+    }
+    s1 = wave_sum(s1) / d;
+    s2 = wave_sum(s2) / d;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      if (col < d) {
+        float r[8];
+        if (dres) {
+          const u32x4 pr = *reinterpret_cast<const u32x4*>(dres + (long)row * d + col);
+          const unsigned wr[4] = {pr.x, pr.y, pr.z, pr.w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) r[j] = bf2f((bf16_t)((wr[j >> 1] >> (16 * (j & 1))) & 0xffff));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) r[j] = 0.f;
+        }
+        unsigned o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float a = r[2 * j] + rstd * (g[c][2 * j] - s1 - xh[c][2 * j] * s2);
+          const float b = r[2 * j + 1] + rstd * (g[c][2 * j + 1] - s1 - xh[c][2 * j + 1] * s2);
+          o[j] = (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+        }
+        u32x4 ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
+        *reinterpret_cast<u32x4*>(dx + (long)row * d + col) = ov;
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < d)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { atomicAdd(&sg[col + j], ag[c][j]); atomicAdd(&sb[col + j], ab[c][j]); }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < d; i += 256) {
+    if (dgamma) atomicAdd(dgamma + i, sg[i]);
+    if (dbeta) atomicAdd(dbeta + i, sb[i]);
+  }
+}
+
+}  // namespace jdt
+using namespace jdt;
+
+JDT_API int jdt_ln_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd, int T,
+                       int d, float eps, void* stream) {
+  if (d % 8 || d > 2048) return -3;
+  const int nv = (d / 8 + 63) / 64;
+  dim3 grid((T + 3) / 4);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const bf16_t* xb = static_cast<const bf16_t*>(x);
+  bf16_t* yb = static_cast<bf16_t*>(y);
+  switch (nv) {
+    case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, st, xb, gamma, beta, yb, mean, rstd, T, d, eps); break;
+    case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, st, xb, gamma, beta, yb, mean, rstd, T, d, eps); break;
+    default: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, st, xb, gamma, beta, yb, mean, rstd, T, d, eps); break;
+  }
+  return HIP_LAUNCH_CHECK();
+}
+
+JDT_API int jdt_ln_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const float* gamma,
+                       const void* dres, void* dx, float* dgamma, float* dbeta, int T, int d, void* stream) {
+  if (d % 8 || d > 2048) return -3;
+  const int nv = (d / 8 + 63) / 64;
+  const int rpw = 8;
+  dim3 grid((T + 4 * rpw - 1) / (4 * rpw));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  auto a = static_cast<const bf16_t*>(dy);
+  auto b = static_cast<const bf16_t*>(x);
+  auto r = static_cast<const bf16_t*>(dres);
+  auto o = static_cast<bf16_t*>(dx);
+  switch (nv) {
+    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(256), 0, st, a, b, mean, rstd, gamma, r, o, dgamma, dbeta, T, d, rpw); break;
+    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(256), 0, st, a, b, mean, rstd, gamma, r, o, dgamma, dbeta, T, d, rpw); break;
+    default: hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(256), 0, st, a, b, mean, rstd, gamma, r, o, dgamma, dbeta, T, d, rpw); break;
+  }
+  return HIP_LAUNCH_CHECK();
+}

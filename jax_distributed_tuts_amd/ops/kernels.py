@@ -357,3 +357,168 @@ def metrics_fold_(running: torch.Tensor, slot: torch.Tensor):
         return
     rc = _lib.lib().jdt_metrics_fold(_ptr(running), _ptr(slot), int(slot.numel()), _lib.stream_ptr())
     _lib.check(rc, "jdt_metrics_fold")
+
+
+# ----------------------------------------------------------------------------- raw GEMM (strided batches)
+def _gemm_raw(*, A, lda, B, ldb, C, ldc, M, N, K, a_trans=False, b_kn=False, a_f32=False, b_f32=False,
+              c_f32=False, alpha=1.0, batch=1, zin=1, sA=0, sA2=0, sB=0, sB2=0, sC=0, sC2=0, accumulate=False):
+    """Launch jdt_gemm on raw (ptr, ld, stride) descriptors -- used where operands are
+    interleaved views (per-head Q/K/V inside the fused [T, 3d] QKV activation)."""
+    g = _lib.GemmArgs()
+    g.A, g.lda, g.a_f32, g.a_trans, g.sA, g.sA2 = A, lda, int(a_f32), int(a_trans), sA, sA2
+    g.B, g.ldb, g.b_f32, g.b_trans, g.sB, g.sB2 = B, ldb, int(b_f32), int(b_kn), sB, sB2
+    g.M, g.N, g.K, g.alpha = M, N, K, float(alpha)
+    g.keep_prob = 1.0
+    g.C, g.ldc, g.sC, g.sC2, g.c_f32, g.accumulate = C, ldc, sC, sC2, int(c_f32), int(accumulate)
+    g.zin = zin
+    ws, ctr = workspace(torch.device("cuda", torch.cuda.current_device()))
+    rc = _lib.lib().jdt_gemm(ctypes.byref(g), batch, -1, -1, ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                             ctypes.c_void_p(ctr.data_ptr()), ctr.numel(), _lib.stream_ptr())
+    _lib.check(rc, "jdt_gemm(raw)")
+
+
+# ----------------------------------------------------------------------------- attention
+def attention_fwd(qkv: torch.Tensor, B: int, S: int, H: int, causal: bool = True):
+    """qkv [B*S, 3*H*Dh] bf16 (q | k | v column blocks, heads contiguous) ->
+    (o [B*S, H*Dh] bf16, P [B*H, S, S] bf16 saved for backward)."""
+    T, d3 = qkv.shape
+    d = d3 // 3
+    Dh = d // H
+    scale = 1.0 / (Dh ** 0.5)
+    if not _is_gpu(qkv):
+        q, k, v = _bf(qkv.float()).view(B, S, 3, H, Dh).permute(2, 0, 3, 1, 4)
+        s = torch.matmul(q, k.transpose(-1, -2)) * scale
+        if causal:
+            s = s.masked_fill(torch.triu(torch.ones(S, S, dtype=torch.bool), 1), float("-inf"))
+        p = torch.softmax(s, dim=-1).to(torch.bfloat16)
+        o = torch.matmul(p.float(), v).permute(0, 2, 1, 3).reshape(T, d).to(torch.bfloat16)
+        return o, p.reshape(B * H, S, S)
+    assert qkv.is_contiguous()
+    dev = qkv.device
+    Sc = torch.empty(B * H, S, S, dtype=torch.float32, device=dev)
+    P = torch.empty(B * H, S, S, dtype=torch.bfloat16, device=dev)
+    o = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
+    base, e2 = qkv.data_ptr(), 2
+    _gemm_raw(A=base, lda=d3, sA=S * d3, sA2=Dh, B=base + d * e2, ldb=d3, sB=S * d3, sB2=Dh, b_kn=False,
+              C=Sc.data_ptr(), ldc=S, sC=H * S * S, sC2=S * S, c_f32=True, M=S, N=S, K=Dh, alpha=scale,
+              batch=B * H, zin=H)
+    rc = _lib.lib().jdt_attn_softmax_fwd(_ptr(Sc), _ptr(P), B * H * S, S, S, int(causal), _lib.stream_ptr())
+    _lib.check(rc, "jdt_attn_softmax_fwd")
+    _gemm_raw(A=P.data_ptr(), lda=S, sA=H * S * S, sA2=S * S, B=base + 2 * d * e2, ldb=d3, sB=S * d3, sB2=Dh,
+              b_kn=True, C=o.data_ptr(), ldc=d, sC=S * d, sC2=Dh, M=S, N=Dh, K=S, batch=B * H, zin=H)
+    return o, P
+
+
+def attention_bwd(do: torch.Tensor, qkv: torch.Tensor, P: torch.Tensor, B: int, S: int, H: int,
+                  dqkv: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Gradient of attention_fwd w.r.t. qkv ([B*S, 3d] bf16)."""
+    T, d3 = qkv.shape
+    d = d3 // 3
+    Dh = d // H
+    scale = 1.0 / (Dh ** 0.5)
+    if dqkv is None:
+        dqkv = torch.empty_like(qkv)
+    if not _is_gpu(qkv):
+        q, k, v = _bf(qkv.float()).view(B, S, 3, H, Dh).permute(2, 0, 3, 1, 4)
+        p = P.float().view(B, H, S, S)
+        dO = _bf(do.float()).view(B, S, H, Dh).permute(0, 2, 1, 3)
+        dv = torch.matmul(p.transpose(-1, -2), dO)
+        dp = torch.matmul(dO, v.transpose(-1, -2))
+        ds = _bf(p * (dp - (p * dp).sum(-1, keepdim=True)))
+        dq = torch.matmul(ds, k) * scale
+        dk = torch.matmul(ds.transpose(-1, -2), q) * scale
+        out = torch.stack([dq, dk, dv], 0).permute(1, 3, 0, 2, 4).reshape(T, d3)
+        dqkv.copy_(out.to(dqkv.dtype))
+        return dqkv
+    dev = qkv.device
+    base, gb, dob, e2 = qkv.data_ptr(), dqkv.data_ptr(), do.data_ptr(), 2
+    assert do.is_contiguous() and dqkv.is_contiguous()
+    # dV = P^T dO
+    _gemm_raw(A=P.data_ptr(), lda=S, sA=H * S * S, sA2=S * S, a_trans=True, B=dob, ldb=d, sB=S * d, sB2=Dh, b_kn=True,
+              C=gb + 2 * d * e2, ldc=d3, sC=S * d3, sC2=Dh, M=S, N=Dh, K=S, batch=B * H, zin=H)
+    # dP = dO V^T
+    dP = torch.empty(B * H, S, S, dtype=torch.float32, device=dev)
+    _gemm_raw(A=dob, lda=d, sA=S * d, sA2=Dh, B=base + 2 * d * e2, ldb=d3, sB=S * d3, sB2=Dh, b_kn=False,
+              C=dP.data_ptr(), ldc=S, sC=H * S * S, sC2=S * S, c_f32=True, M=S, N=S, K=Dh, batch=B * H, zin=H)
+    dS = torch.empty(B * H, S, S, dtype=torch.bfloat16, device=dev)
+    rc = _lib.lib().jdt_attn_softmax_bwd(_ptr(P), _ptr(dP), _ptr(dS), B * H * S, S, _lib.stream_ptr())
+    _lib.check(rc, "jdt_attn_softmax_bwd")
+    # dQ = scale dS K ; dK = scale dS^T Q
+    _gemm_raw(A=dS.data_ptr(), lda=S, sA=H * S * S, sA2=S * S, B=base + d * e2, ldb=d3, sB=S * d3, sB2=Dh, b_kn=True,
+              C=gb, ldc=d3, sC=S * d3, sC2=Dh, M=S, N=Dh, K=S, alpha=scale, batch=B * H, zin=H)
+    _gemm_raw(A=dS.data_ptr(), lda=S, sA=H * S * S, sA2=S * S, a_trans=True, B=base, ldb=d3, sB=S * d3, sB2=Dh,
+              b_kn=True, C=gb + d * e2, ldc=d3, sC=S * d3, sC2=Dh, M=S, N=Dh, K=S, alpha=scale, batch=B * H, zin=H)
+    return dqkv
+
+
+# ----------------------------------------------------------------------------- layernorm / embedding / colsum
+def layernorm_fwd(x, gamma, beta, eps=1e-6):
+    """flax nn.LayerNorm (eps 1e-6); returns (y bf16, mean f32 [T], rstd f32 [T])."""
+    T, d = x.shape
+    if not _is_gpu(x):
+        xf = x.float()
+        mean = xf.mean(-1)
+        rstd = torch.rsqrt(((xf - mean[:, None]) ** 2).mean(-1) + eps)
+        y = ((xf - mean[:, None]) * rstd[:, None] * gamma.float() + beta.float()).to(torch.bfloat16)
+        return y, mean, rstd
+    y = torch.empty_like(x)
+    mean = torch.empty(T, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(T, dtype=torch.float32, device=x.device)
+    rc = _lib.lib().jdt_ln_fwd(_ptr(x), _ptr(gamma), _ptr(beta), _ptr(y), _ptr(mean), _ptr(rstd), T, d, float(eps),
+                               _lib.stream_ptr())
+    _lib.check(rc, "jdt_ln_fwd")
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None):
+    """dx = dres + LN'(dy); dgamma/dbeta accumulate (fp32)."""
+    T, d = x.shape
+    if not _is_gpu(x):
+        xh = (x.float() - mean[:, None]) * rstd[:, None]
+        g = dy.float() * gamma.float()
+        dx = rstd[:, None] * (g - g.mean(-1, keepdim=True) - xh * (g * xh).mean(-1, keepdim=True))
+        if dres is not None:
+            dx = dx + dres.float()
+        if dgamma is not None:
+            dgamma.add_((dy.float() * xh).sum(0))
+        if dbeta is not None:
+            dbeta.add_(dy.float().sum(0))
+        return dx.to(torch.bfloat16)
+    dx = torch.empty_like(x)
+    rc = _lib.lib().jdt_ln_bwd(_ptr(dy), _ptr(x), _ptr(mean), _ptr(rstd), _ptr(gamma), _ptr(dres), _ptr(dx),
+                               _ptr(dgamma), _ptr(dbeta), T, d, _lib.stream_ptr())
+    _lib.check(rc, "jdt_ln_bwd")
+    return dx
+
+
+def embed_fwd(tok, wte, wpe, S):
+    T = tok.shape[0]
+    d = wte.shape[1]
+    if not _is_gpu(tok):
+        pos = torch.arange(T) % S
+        return (wte.float()[tok.long()] + wpe.float()[pos]).to(torch.bfloat16)
+    out = torch.empty(T, d, dtype=torch.bfloat16, device=tok.device)
+    rc = _lib.lib().jdt_embed_fwd(_ptr(tok), _ptr(wte), _ptr(wpe), _ptr(out), T, S, d, _lib.stream_ptr())
+    _lib.check(rc, "jdt_embed_fwd")
+    return out
+
+
+def embed_bwd(dout, tok, dwte, dwpe, S):
+    T, d = dout.shape
+    if not _is_gpu(dout):
+        dwte.index_add_(0, tok.long(), dout.float())
+        if dwpe is not None:
+            dwpe.index_add_(0, torch.arange(T) % S, dout.float())
+        return
+    rc = _lib.lib().jdt_embed_bwd(_ptr(dout), _ptr(tok), _ptr(dwte), _ptr(dwpe), T, S, d, _lib.stream_ptr())
+    _lib.check(rc, "jdt_embed_bwd")
+
+
+def colsum_(x, out):
+    """out += x.sum(0) (bias gradients)."""
+    if not _is_gpu(x):
+        out.add_(x.float().sum(0))
+        return out
+    rc = _lib.lib().jdt_colsum(_ptr(x), x.stride(0), x.shape[0], x.shape[1], _ptr(out), _lib.stream_ptr())
+    _lib.check(rc, "jdt_colsum")
+    return out

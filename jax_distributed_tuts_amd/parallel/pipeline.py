@@ -79,16 +79,13 @@ class PipeConfig:
 class GPipeTrainer:
     """Runs one stage of a GPipe schedule (``stage.forward/backward`` explicit API)."""
 
-    def __init__(self, state: TrainState, mesh: Optional[Mesh], cfg: PipeConfig, in_shape_fn, out_features: int,
-                 act_dtype=torch.bfloat16):
+    def __init__(self, state: TrainState, mesh: Optional[Mesh], cfg: PipeConfig, act_dtype=torch.bfloat16):
         self.state, self.mesh, self.cfg = state, mesh, cfg
         self.model = state.apply_fn
         self.S = C.axis_size(mesh, cfg.pipe_axis)
         self.s = C.axis_index(mesh, cfg.pipe_axis)
         self.n_dp = C.axis_size(mesh, cfg.data_axis)
         self.first, self.last = self.s == 0, self.s == self.S - 1
-        self.in_shape_fn = in_shape_fn          # rows -> shape of this stage's input activation
-        self.out_features = out_features
         self.act_dtype = act_dtype
         dev = state.params.master.device
         self.metrics = torch.zeros(N_METRIC_SLOTS, dtype=torch.float32, device=dev)
@@ -119,12 +116,12 @@ class GPipeTrainer:
             if self.first:
                 x = batch.inputs[i * mb:(i + 1) * mb]
             else:
-                x = self._recv((mb,) + tuple(self.in_shape_fn(mb)[1:]), self.act_dtype, self.s - 1)
+                x = self._recv(self.model.input_shape(mb), self.act_dtype, self.s - 1)
             out, cache = self.model.forward(P, x, train=True, seed=seed, offset=i << 16, step=st.step_tensor)
             caches[i] = cache
             if self.last:
                 d = torch.empty_like(out)
-                self.loss_head(out, batch.labels[i * mb:(i + 1) * mb], d, 1.0 / mb)
+                self.loss_head(out, batch.labels[i * mb:(i + 1) * mb], d)
                 dlogits[i] = d
             else:
                 self._send(out, self.s + 1)
@@ -133,7 +130,7 @@ class GPipeTrainer:
             if self.last:
                 dx = self.model.backward(P, caches[i], dlogits[i], dout_is_dz=True, need_dx=not self.first)
             else:
-                dh = self._recv((mb, self.out_features), self.act_dtype, self.s + 1)
+                dh = self._recv(self.model.output_shape(mb), self.act_dtype, self.s + 1)
                 dx = self.model.backward(P, caches[i], dh, dout_is_dz=False, need_dx=not self.first)
             if not self.first:
                 self._send(dx, self.s - 1)
@@ -145,10 +142,11 @@ class GPipeTrainer:
         with named_scope("sync_metrics"):
             K.metrics_fold_(self.metrics, P.metrics_slot)
 
-    def loss_head(self, logits, labels, dlogits, grad_scale):
-        top = self.model.names[-1]
-        K.softmax_xent(logits, labels, grad_scale=grad_scale, dlogits=dlogits, dbias=self.state.params.g(f"{top}/bias")
-                       if f"{top}/bias" in self.state.params.offsets else None, metrics=self.state.params.metrics_slot)
+    def loss_head(self, logits, labels, dlogits):
+        y = self.model.flatten_labels(labels)
+        hb = self.model.head_bias_name
+        K.softmax_xent(logits, y, grad_scale=1.0 / y.numel(), dlogits=dlogits,
+                       dbias=self.state.params.g(hb) if hb else None, metrics=self.state.params.metrics_slot)
 
     def gather_metrics(self) -> torch.Tensor:
         """Metrics live on the last stage; bring them to every pipe member."""

@@ -1,0 +1,28 @@
+"""Transformer-LM pipeline construction (BASELINE config #5: 4-layer transformer,
+hybrid DP=2 x PP=4).  Synthetic data: uniform random token sequences, labels =
+inputs shifted by one (next-token prediction)."""
+from __future__ import annotations
+
+import torch
+
+from ..models.transformer import TransformerConfig, TransformerLM, lm_stage
+from ..runtime.dist import Mesh
+from ..utils import rng as R
+from ..utils.train_state import Batch, TrainState, adamw
+from .pipeline import GPipeTrainer, PipeConfig, init_stage_params
+
+
+def lm_batch(cfg: TransformerConfig, global_batch: int = 16, seed: int = 1) -> Batch:
+    g = torch.Generator().manual_seed(seed)
+    toks = torch.randint(0, cfg.vocab_size, (global_batch, cfg.seq_len + 1), generator=g, dtype=torch.int64)
+    return Batch(toks[:, :-1].to(torch.int32).contiguous(), toks[:, 1:].to(torch.int32).contiguous())
+
+
+def build_lm_pipeline(mesh: Mesh, dev, cfg: TransformerConfig = TransformerConfig(), num_microbatches: int = 4,
+                      lr: float = 3e-4, seed: int = 0):
+    S, s = mesh.axis_size("pipe"), mesh.axis_index("pipe")
+    stage = lm_stage(cfg, S, s)
+    full = TransformerLM(cfg)
+    P = init_stage_params(stage, full.param_specs(), seed, dev)
+    st = TrainState.create(apply_fn=stage, params=P, tx=adamw(lr), rng=R.PRNGKey(seed))
+    return GPipeTrainer(st, mesh, PipeConfig(num_microbatches)), cfg

@@ -40,8 +40,7 @@ def build_mlp_pipeline(cfg, mesh, dev, n_hidden_layers=8, dropout_rate=None, num
     full = MLP(dims, dropout_rate=dr)
     P = init_stage_params(stage, full.param_specs(), cfg.seed, dev)
     st = TrainState.create(apply_fn=stage, params=P, tx=adamw(cfg.optimizer.learning_rate), rng=R.PRNGKey(cfg.seed))
-    tr = GPipeTrainer(st, mesh, PipeConfig(num_microbatches), in_shape_fn=lambda rows: (rows, stage.dims[0]),
-                      out_features=stage.dims[-1])
+    tr = GPipeTrainer(st, mesh, PipeConfig(num_microbatches))
     return tr
 
 

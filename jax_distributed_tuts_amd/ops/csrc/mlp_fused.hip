@@ -1,0 +1,324 @@
+// Whole-step fused kernels for the tutorial classifier (784 -> H -> C, SiLU,
+// dropout, softmax-CE, AdamW) -- the reference's DP/FSDP hot loop
+// (data_paral.py:171-238, util.py:41-78) in TWO launches per step on 1 GPU.
+//
+// Measured on MI355X, each dependent kernel of this tiny model costs ~4-6 us
+// end to end regardless of its work (profiles/README.md), so the step is
+// organised around the two global data dependencies of the maths:
+//
+// mlp2_fwd  grid (row blocks of 32) x (hidden blocks of 16)
+//   Z1 = X W1 + b1 (fp32 X converted in-register, W1 column block staged
+//   transposed in LDS, K split over the 4 waves, partials reduced in LDS),
+//   H = dropout(silu(Z1)), and the block's partial logits H[:,blk] W2[blk,:]
+//   (+ b2 from block 0) accumulated with fp32 atomics into logits[M][C].
+//   (All rows of all minibatches at once: every row carries its minibatch's
+//   1/mb loss weight, so the summed gradient equals util.accum_grads_loop's.)
+//
+// mlp2_bwd  grid (hidden blocks of 16) x (input chunks of KC)
+//   every workgroup recomputes CE from the summed logits (M x C, tiny) ->
+//   dlogits; its dZ1 block = (dlogits W2[blk]^T) * silu'(Z1) * mask/keep;
+//   dW1[chunk, blk] = X[:,chunk]^T dZ1[:,blk] on MFMA with both operands
+//   staged K(=row)-contiguous in LDS; chunk-0 blocks also emit db1, dW2[blk]
+//   and block (0,0) db2 + metrics.  Each gradient element is produced by
+//   exactly ONE workgroup, so
+//     mode 0 (DP over N>1 GPUs): plain-store grads into the flat bucket for
+//            the RCCL all-reduce, AdamW follows;
+//     mode 1 (single GPU): apply AdamW right in the epilogue (no grad buffer
+//            round trip, no optimizer launch).  W2's bf16 shadow is double
+//            buffered by step parity because other workgroups of the same
+//            launch still read the old W2 for dZ1; b2 is only read by mlp2_fwd.
+#include "common.h"
+
+namespace jdt {
+
+struct Mlp2Args {
+  int M, H;
+  float inv_mb;                     // CE grad scale: 1 / rows per minibatch
+  const float* X; const int* labels;
+  const bf16_t* W1s; const bf16_t* b1s; const bf16_t* W2s0; const bf16_t* W2s1; const bf16_t* b2s;
+  bf16_t* Z1; bf16_t* H1; float* logits;   // logits: [2][M][C] (step parity)
+  float keep; unsigned long long seed, offset;
+  int* step; unsigned* ticket;
+  // mode 0 outputs
+  float* gW1; float* gb1; float* gW2; float* gb2; float* mslot;
+  // mode 1 (fused AdamW)
+  int fuse_opt;
+  float* pW1; float* pb1; float* pW2; float* pb2;
+  float* mW1; float* mb1; float* mW2; float* mb2;
+  float* vW1; float* vb1; float* vW2; float* vb2;
+  bf16_t* sW1; bf16_t* sb1; bf16_t* sW2_0; bf16_t* sW2_1; bf16_t* sb2;
+  float lr, beta1, beta2, eps, wd, gscale;
+  float* running;
+};
+
+struct AdamK { float b1, b2, eps, wd, lr, gs, rbc1, rbc2; };
+
+__device__ __forceinline__ AdamK adam_consts(const Mlp2Args& a, int step) {
+  AdamK k;
+  k.b1 = a.beta1; k.b2 = a.beta2; k.eps = a.eps; k.wd = a.wd; k.lr = a.lr; k.gs = a.gscale;
+  const float t = (float)(step + 1);
+  k.rbc1 = 1.f / (1.f - powf(a.beta1, t));
+  k.rbc2 = 1.f / (1.f - powf(a.beta2, t));
+  return k;
+}
+
+__device__ __forceinline__ float adam_elem(float* p, float* m, float* v, long i, float g, const AdamK& k) {
+  g *= k.gs;
+  const float mi = k.b1 * m[i] + (1.f - k.b1) * g;
+  const float vi = k.b2 * v[i] + (1.f - k.b2) * g * g;
+  m[i] = mi; v[i] = vi;
+  const float pi = p[i] - k.lr * ((mi * k.rbc1) / (sqrtf(vi * k.rbc2) + k.eps) + k.wd * p[i]);
+  p[i] = pi;
+  return pi;
+}
+
+// ---------------------------------------------------------------------------- forward
+template <int K_IN, int C>
+__global__ void __launch_bounds__(256) mlp2_fwd_kernel(Mlp2Args a) {
+  constexpr int KS = (K_IN + 31) / 32;  // 32-deep MFMA k-steps
+  constexpr int KP = KS * 32;
+  constexpr int LDW = KP + 8;           // padded [n][k] row (bank spread)
+  __shared__ __attribute__((aligned(16))) bf16_t w1t[16 * LDW];
+  __shared__ float part[4][32][17];
+  __shared__ float htile[32][17];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int M = a.M, H = a.H;
+  const int r0 = blockIdx.x * 32, j0 = blockIdx.y * 16;
+  const int step = a.step[0], par = step & 1;
+  const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
+
+  // W1[:, j0:j0+16] -> LDS transposed (w1t[n][k]); 16-byte global loads
+  for (int idx = tid; idx < KP * 2; idx += 256) {
+    const int k = idx >> 1, h = (idx & 1) * 8;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (k < K_IN) v = *reinterpret_cast<const u32x4*>(a.W1s + (long)k * H + j0 + h);
+    const unsigned wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      w1t[(h + 2 * e) * LDW + k] = (bf16_t)(wv[e] & 0xffff);
+      w1t[(h + 2 * e + 1) * LDW + k] = (bf16_t)(wv[e] >> 16);
+    }
+  }
+  __syncthreads();
+
+  // K split over the 4 waves; X fragments straight from global (fp32 -> bf16)
+  f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  const int ks0 = (w * KS) / 4, ks1 = ((w + 1) * KS) / 4;
+  constexpr int MAXT = (KS + 3) / 4;
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    const int ks = ks0 + t;
+    if (ks < ks1) {
+      const int k = ks * 32 + 8 * (lane >> 4);
+      const bf16x8 b = *reinterpret_cast<const bf16x8*>(&w1t[(lane & 15) * LDW + k]);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int row = r0 + mt * 16 + (lane & 15);
+        bf16x8 af;
+        if (row < M && k < K_IN) {
+          const float4* xp = reinterpret_cast<const float4*>(a.X + (long)row * K_IN + k);
+          const float4 x0 = xp[0], x1 = xp[1];
+          af[0] = (short)f2bf(x0.x); af[1] = (short)f2bf(x0.y); af[2] = (short)f2bf(x0.z); af[3] = (short)f2bf(x0.w);
+          af[4] = (short)f2bf(x1.x); af[5] = (short)f2bf(x1.y); af[6] = (short)f2bf(x1.z); af[7] = (short)f2bf(x1.w);
+        } else {
+          af = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+        }
+        acc[mt] = mfma16x16x32(af, b, acc[mt]);
+      }
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) part[w][mt * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[mt][e];
+  __syncthreads();
+
+  // bias + silu + dropout epilogue, H tile kept in LDS for the logits partials
+  for (int idx = tid; idx < 32 * 16; idx += 256) {
+    const int rl = idx >> 4, c = idx & 15, row = r0 + rl, col = j0 + c;
+    float hv = 0.f;
+    if (row < M) {
+      const float v = part[0][rl][c] + part[1][rl][c] + part[2][rl][c] + part[3][rl][c] + bf2f(a.b1s[col]);
+      const bf16_t zb = f2bf(v);
+      a.Z1[(long)row * H + col] = zb;
+      hv = act_fwd(ACT_SILU, bf2f(zb));
+      if (a.keep < 1.f)
+        hv = dropout_keep(a.seed, doff, (unsigned long long)row * H + col, a.keep) ? hv / a.keep : 0.f;
+      const bf16_t hb = f2bf(hv);
+      a.H1[(long)row * H + col] = hb;
+      hv = bf2f(hb);
+    }
+    htile[rl][c] = hv;
+  }
+  __syncthreads();
+  const bf16_t* W2s = par ? a.W2s1 : a.W2s0;
+  float* lg = a.logits + (long)par * M * C;
+  for (int idx = tid; idx < 32 * C; idx += 256) {
+    const int rl = idx / C, c = idx % C, row = r0 + rl;
+    if (row >= M) continue;
+    float s = (blockIdx.y == 0) ? bf2f(a.b2s[c]) : 0.f;
+#pragma unroll
+    for (int n = 0; n < 16; ++n) s += htile[rl][n] * bf2f(W2s[(long)(j0 + n) * C + c]);
+    atomicAdd(lg + (long)row * C + c, s);
+  }
+}
+
+// ---------------------------------------------------------------------------- backward
+template <int K_IN, int C, int KC>
+__global__ void __launch_bounds__(256) mlp2_bwd_kernel(Mlp2Args a) {
+  constexpr int MPM = 256;       // max rows per device
+  constexpr int LDM = MPM + 8;   // padded row (bf16 elements)
+  __shared__ float dlog[MPM][C + 1];
+  __shared__ __attribute__((aligned(16))) bf16_t dzT[16 * LDM];
+  __shared__ __attribute__((aligned(16))) bf16_t xT[KC * LDM];
+  __shared__ float red[3][4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int M = a.M, H = a.H, Mp = (M + 31) & ~31;
+  const int j0 = blockIdx.x * 16, kc0 = blockIdx.y * KC;
+  const int step = a.step[0], par = step & 1;
+  const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
+  const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
+  const AdamK ak = adam_consts(a, step);
+
+  // 1. logits (fp32 partial sums -> bf16 like the Dense output) -> CE -> dlogits
+  const float* lg = a.logits + (long)par * M * C;
+  float l_loss = 0.f, l_corr = 0.f;
+  for (int r = tid; r < M; r += 256) {
+    float z[C];
+    float mx = -INFINITY;
+    int am = 0;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      z[c] = round_bf(lg[(long)r * C + c]);
+      if (z[c] > mx) { mx = z[c]; am = c; }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) s += __expf(z[c] - mx);
+    const float lse = mx + __logf(s);
+    const int lab = a.labels[r];
+    l_loss += lse - z[lab];
+    l_corr += (am == lab) ? 1.f : 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) dlog[r][c] = round_bf((__expf(z[c] - lse) - (c == lab ? 1.f : 0.f)) * a.inv_mb);
+  }
+  if (lead) {
+    l_loss = wave_sum(l_loss);
+    l_corr = wave_sum(l_corr);
+    if (lane == 0) { red[0][w] = l_loss; red[1][w] = l_corr; }
+    // re-arm the other parity's logits accumulator for the next step's forward
+    float* nxt = a.logits + (long)(par ^ 1) * M * C;
+    for (int i = tid; i < M * C; i += 256) nxt[i] = 0.f;
+  }
+  __syncthreads();
+
+  // 2. dZ1[:, blk] -> dzT[n][m] (bf16, rows >= M zero-padded to Mp)
+  const bf16_t* W2s = par ? a.W2s1 : a.W2s0;
+  for (int idx = tid; idx < Mp * 16; idx += 256) {
+    const int m = idx >> 4, n = idx & 15, col = j0 + n;
+    float v = 0.f;
+    if (m < M) {
+      float dh = 0.f;
+#pragma unroll
+      for (int c = 0; c < C; ++c) dh += dlog[m][c] * bf2f(W2s[(long)col * C + c]);
+      v = dh * act_grad(ACT_SILU, bf2f(a.Z1[(long)m * H + col]));
+      if (a.keep < 1.f)
+        v = dropout_keep(a.seed, doff, (unsigned long long)m * H + col, a.keep) ? v / a.keep : 0.f;
+    }
+    dzT[n * LDM + m] = f2bf(v);
+  }
+  // 3. X[:, chunk] -> xT[i][m] (bf16, transposed so MFMA fragments are 16-byte reads)
+  for (int idx = tid; idx < Mp * KC; idx += 256) {
+    const int m = idx / KC, i = idx % KC;
+    float v = 0.f;
+    if (m < M && kc0 + i < K_IN) v = a.X[(long)m * K_IN + kc0 + i];
+    xT[i * LDM + m] = f2bf(v);
+  }
+  __syncthreads();
+
+  // 4. dW1[chunk, blk] = X[:, chunk]^T dZ1[:, blk]   (K = rows)
+  for (int tile = w; tile < KC / 16; tile += 4) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < Mp / 32; ++ks) {
+      const int kk = ks * 32 + 8 * (lane >> 4);
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(&xT[(tile * 16 + (lane & 15)) * LDM + kk]);
+      const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
+      acc = mfma16x16x32(af, bfr, acc);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = kc0 + tile * 16 + (lane >> 4) * 4 + e;
+      if (i >= K_IN) continue;
+      const long idx = (long)i * H + j0 + (lane & 15);
+      if (a.fuse_opt) a.sW1[idx] = f2bf(adam_elem(a.pW1, a.mW1, a.vW1, idx, acc[e], ak));
+      else a.gW1[idx] = acc[e];
+    }
+  }
+
+  // 5. chunk-0 blocks: db1[blk], dW2[blk, :]; block (0,0): db2 + metrics
+  if (blockIdx.y == 0) {
+    bf16_t* sW2n = par ? a.sW2_0 : a.sW2_1;   // next step's parity
+    for (int idx = tid; idx < 16 * C + 16; idx += 256) {
+      if (idx < 16 * C) {
+        const int n = idx / C, c = idx % C;
+        float s = 0.f;
+        for (int m = 0; m < M; ++m) s += bf2f(a.H1[(long)m * H + j0 + n]) * dlog[m][c];
+        const long o = (long)(j0 + n) * C + c;
+        if (a.fuse_opt) sW2n[o] = f2bf(adam_elem(a.pW2, a.mW2, a.vW2, o, s, ak));
+        else a.gW2[o] = s;
+      } else {
+        const int n = idx - 16 * C;
+        float s = 0.f;
+        for (int m = 0; m < M; ++m) s += bf2f(dzT[n * LDM + m]);
+        if (a.fuse_opt) a.sb1[j0 + n] = f2bf(adam_elem(a.pb1, a.mb1, a.vb1, j0 + n, s, ak));
+        else a.gb1[j0 + n] = s;
+      }
+    }
+  }
+  if (lead) {
+    if (tid < C) {
+      float s = 0.f;
+      for (int m = 0; m < M; ++m) s += dlog[m][tid];
+      if (a.fuse_opt) a.sb2[tid] = f2bf(adam_elem(a.pb2, a.mb2, a.vb2, tid, s, ak));
+      else a.gb2[tid] = s;
+    }
+    if (tid == 0) {
+      const float L = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+      const float Cr = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+      if (a.fuse_opt && a.running) {
+        a.running[0] += L; a.running[1] += (float)M; a.running[2] += Cr; a.running[3] += (float)M;
+      } else if (a.mslot) {
+        a.mslot[0] = L; a.mslot[1] = (float)M; a.mslot[2] = Cr; a.mslot[3] = (float)M;
+      }
+    }
+  }
+  if (a.fuse_opt) {
+    // advance the device step once every workgroup has read it
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned t = atomicAdd(a.ticket, 1u);
+      if (t == gridDim.x * gridDim.y - 1) {
+        a.step[0] = step + 1;
+        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+}  // namespace jdt
+using namespace jdt;
+
+JDT_API int jdt_mlp2_args_size() { return (int)sizeof(Mlp2Args); }
+
+// phase 0: forward, 1: backward.  Supported: K_IN = 784, C = 10, H % 16 == 0, M <= 256.
+JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* stream) {
+  const Mlp2Args& a = *args;
+  if (k_in != 784 || c != 10 || a.H % 16 || a.M <= 0 || a.M > 256) return -3;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (phase == 0) {
+    hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10>), dim3((a.M + 31) / 32, a.H / 16), dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112>), dim3(a.H / 16, 784 / 112), dim3(256), 0, st, a);
+  }
+  return HIP_LAUNCH_CHECK();
+}

@@ -66,7 +66,7 @@ def init_dp(model: MLP, tx, seed: int, device, mesh: Optional[Mesh] = None, axis
 @dataclass
 class DPConfig:
     num_minibatches: int = 4
-    accum: str = "loop"          # "loop" | "fused"
+    accum: str = "loop"          # "loop" | "fused" | "kernel" (whole-step fused kernels, parallel/fused_mlp.py)
     axis: str = "data"
 
 
@@ -83,11 +83,29 @@ class DataParallelTrainer:
         self.world = C.axis_size(mesh, cfg.axis)
         self.graph = None
         self._static = None
+        self.fused = None
+
+    def _fused_engine(self, batch: Batch):
+        if self.cfg.accum != "kernel":
+            return None
+        if self.fused is None:
+            from .fused_mlp import FusedMLP2, supported
+
+            if not supported(self.model, batch.size, batch.inputs.device):
+                self.cfg.accum = "fused"  # shapes outside the fused kernels' envelope
+                return None
+            self.fused = FusedMLP2(self.state, self.mesh, self.cfg.axis, self.cfg.num_minibatches, batch.size,
+                                   self.metrics)
+        return self.fused
 
     # ------------------------------------------------------------------ pieces
     def compute(self, batch: Batch):
         """accum_grads: per-minibatch fwd/CE/bwd accumulated into P.grad (beta=1)."""
         st, P, cfg = self.state, self.state.params, self.cfg
+        eng = self._fused_engine(batch)
+        if eng is not None:
+            eng.forward_backward(batch)
+            return
         rng = fold_rng_over_axis(st.rng, self.mesh, cfg.axis)
         seed = rng & 0xFFFFFFFF
         n_mb = cfg.num_minibatches
@@ -106,14 +124,14 @@ class DataParallelTrainer:
         """pmean(grads) + psum(metrics) as ONE SUM all-reduce of the bucket; the
         1/N of the mean is applied by the optimizer."""
         P = self.state.params
+        if self.world == 1:
+            return
         with named_scope("sync_grads"):
             C.psum_(P.grad, self.mesh, self.cfg.axis)
 
     def update(self):
-        P = self.state.params
-        self.state.apply_gradients(grad_scale=1.0 / (self.cfg.num_minibatches * self.world))
-        with named_scope("sync_metrics"):
-            K.metrics_fold_(self.metrics, P.metrics_slot)
+        self.update_noncounting()
+        self.state.step += 1
 
     def step(self, batch: Batch):
         if self.graph is not None:
@@ -155,8 +173,19 @@ class DataParallelTrainer:
 
     def update_noncounting(self):
         P = self.state.params
-        self.state.tx.update(P, self.state.opt_state, 1.0 / (self.cfg.num_minibatches * self.world))
-        K.metrics_fold_(self.metrics, P.metrics_slot)
+        if self.fused is not None:
+            if self.fused.fuse_opt:
+                return  # AdamW + metrics already applied inside mlp2_bwd
+            self.state.tx.update(P, self.state.opt_state, 1.0 / (self.cfg.num_minibatches * self.world),
+                                 zero_grad=False)
+        else:
+            self.state.tx.update(P, self.state.opt_state, 1.0 / (self.cfg.num_minibatches * self.world))
+        with named_scope("sync_metrics"):
+            K.metrics_fold_(self.metrics, P.metrics_slot)
+
+    def finalize(self):
+        if self.fused is not None:
+            self.fused.finalize()
 
     def _replay(self):
         kind = self.graph[0]

@@ -271,3 +271,63 @@ def test_transformer_step_gpu_matches_cpu():
     g_c, g_g = res["cpu"][0], res[DEV][0]
     assert float((g_g - g_c).norm() / g_c.norm()) < 3e-2
     _close(res[DEV][1], res["cpu"][1], rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("fused_opt", ["1", "0"])
+@pytest.mark.parametrize("rows", [128, 32, 16])
+def test_fused_mlp_step_matches_generic(fused_opt, rows, monkeypatch):
+    """Whole-step fused kernels (mlp2_fwd/mlp2_bwd, optionally with AdamW in the
+    epilogue) == the generic-kernel path over the same rows (same Philox dropout
+    stream: row*H + col under (seed, step))."""
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    monkeypatch.setenv("JDT_FUSED_OPT", fused_opt)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(rows, 784, generator=g).to(DEV)
+    y = torch.randint(0, 10, (rows,), generator=g).to(torch.int32).to(DEV)
+    out = {}
+    for accum in ("fused", "kernel"):
+        st = init_dp(Classifier(), adamw(1e-3), 69, DEV)
+        tr = DataParallelTrainer(st, None, DPConfig(4, accum))
+        for _ in range(3):
+            tr.step(Batch(x, y))
+        tr.finalize()
+        torch.cuda.synchronize()
+        out[accum] = (st.params.master.clone(), tr.metrics.clone(), int(st.opt_state["count"].item()),
+                      st.params.shadow.clone())
+        if accum == "kernel":
+            assert tr.fused is not None and tr.fused.fuse_opt == (fused_opt == "1")
+    assert out["kernel"][2] == out["fused"][2] == 3
+    d = (out["kernel"][0] - out["fused"][0]).abs()
+    assert float(d.max()) <= 6e-3 and float((d > 1e-4).float().mean()) < 2e-3
+    _close(out["kernel"][1], out["fused"][1], rtol=1e-3, atol=2e-2)
+    sd = (out["kernel"][3].float() - out["fused"][3].float()).abs()
+    assert float(sd.max()) <= 1e-2
+
+
+def test_fused_mlp_graph_capture():
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(128, 784, generator=g).to(DEV)
+    y = torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV)
+    res = []
+    for graph in (False, True):
+        st = init_dp(Classifier(), adamw(1e-3), 69, DEV)
+        tr = DataParallelTrainer(st, None, DPConfig(4, "kernel"))
+        tr.step(Batch(x, y))
+        if graph:
+            tr.capture(Batch(x, y))
+        for _ in range(6):
+            tr.step(Batch(x, y))
+        tr.finalize()
+        torch.cuda.synchronize()
+        res.append((st.params.master.clone(), tr.metrics.clone(), int(st.opt_state["count"].item())))
+    assert res[0][2] == res[1][2] == 7
+    d = (res[0][0] - res[1][0]).abs()
+    assert float(d.max()) <= 3e-3 and float((d > 1e-5).float().mean()) < 1e-3
+    _close(res[1][1], res[0][1], rtol=1e-4, atol=1e-2)

@@ -124,9 +124,8 @@ __device__ __forceinline__ u32x4 load_chunk(const void* base, long ld, bool tran
 
 // chunk index c -> (row, k) of the tile for either orientation
 template <int BK>
-__device__ __forceinline__ void chunk_coords(int c, bool trans, int& r, int& k) {
-  if (!trans) { r = c / (BK / 8); k = (c % (BK / 8)) * 8; }
-  else        { k = c % BK;       r = (c / BK) * 8; }
+__device__ __forceinline__ int2 chunk_rk(int c, bool trans) {
+  return trans ? make_int2((c / BK) * 8, c % BK) : make_int2(c / (BK / 8), (c % (BK / 8)) * 8);
 }
 
 template <int LDK>
@@ -196,7 +195,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
     for (int i = 0; i < T::A_PER_T; ++i) {
       const int c = tid + i * 256;
       if (c < T::A_CHUNKS) {
-        int r, k; chunk_coords<BK>(c, g.a_trans, r, k);
+        const int2 rk = chunk_rk<BK>(c, g.a_trans); const int r = rk.x, k = rk.y;
         ra[i] = load_chunk<AF32>(Ab, g.lda, g.a_trans, r, kb + k, Ar, kend, vecA);
       }
     }
@@ -204,7 +203,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
     for (int i = 0; i < T::B_PER_T; ++i) {
       const int c = tid + i * 256;
       if (c < T::B_CHUNKS) {
-        int r, k; chunk_coords<BK>(c, g.b_trans, r, k);
+        const int2 rk = chunk_rk<BK>(c, g.b_trans); const int r = rk.x, k = rk.y;
         rb[i] = load_chunk<BF32>(Bb, g.ldb, g.b_trans, r, kb + k, Br, kend, vecB);
       }
     }
@@ -213,12 +212,12 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
 #pragma unroll
     for (int i = 0; i < T::A_PER_T; ++i) {
       const int c = tid + i * 256;
-      if (c < T::A_CHUNKS) { int r, k; chunk_coords<BK>(c, g.a_trans, r, k); store_chunk<LDK>(AS(buf), g.a_trans, r, k, ra[i]); }
+      if (c < T::A_CHUNKS) { const int2 rk = chunk_rk<BK>(c, g.a_trans); const int r = rk.x, k = rk.y; store_chunk<LDK>(AS(buf), g.a_trans, r, k, ra[i]); }
     }
 #pragma unroll
     for (int i = 0; i < T::B_PER_T; ++i) {
       const int c = tid + i * 256;
-      if (c < T::B_CHUNKS) { int r, k; chunk_coords<BK>(c, g.b_trans, r, k); store_chunk<LDK>(BS(buf), g.b_trans, r, k, rb[i]); }
+      if (c < T::B_CHUNKS) { const int2 rk = chunk_rk<BK>(c, g.b_trans); const int r = rk.x, k = rk.y; store_chunk<LDK>(BS(buf), g.b_trans, r, k, rb[i]); }
     }
   };
 
@@ -317,7 +316,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = tm0 + (wm * TM + i) * 16 + (lane >> 4) * 4 + e;
-        if (!cok || row >= g.M) continue;
+        if (cok && row < g.M) {
         float v = g.alpha * acc[i][j][e] + bval;
         if (g.Zout) static_cast<bf16_t*>(g.Zout)[(long)z * g.sZ + (long)row * g.ldz + col] = f2bf(v);
         if (g.Zin) v *= act_grad(g.act_bwd, bf2f(g.Zin[(long)z * g.sZin + (long)row * g.ldzin + col]));
@@ -341,6 +340,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
           }
         }
         csum += v;
+        }
       }
     }
     if (g.dbias) {
@@ -396,10 +396,10 @@ JDT_API int jdt_gemm(const GemmArgs* ga, int batch, int cfg, int splits, float* 
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (g.M <= 0 || g.N <= 0) return 0;
   if (cfg < 0) {
-    const long t128 = (long)((g.M + 127) / 128) * ((g.N + 127) / 128) * batch;
+    const long t128 = (long)((g.M + 63) / 64) * ((g.N + 127) / 128) * batch;
     const long t64 = (long)((g.M + 63) / 64) * ((g.N + 63) / 64) * batch;
     const long t32 = (long)((g.M + 31) / 32) * ((g.N + 63) / 64) * batch;
-    if (g.M >= 128 && g.N >= 128 && t128 >= 192) cfg = 3;
+    if (g.M >= 64 && g.N >= 128 && t128 >= 256) cfg = 3;
     else if (g.M >= 64 && t64 >= 96) cfg = 2;
     else if (g.M > 16 && t32 >= 64) cfg = 1;
     else if (g.M <= 16) cfg = 0;
@@ -409,7 +409,7 @@ JDT_API int jdt_gemm(const GemmArgs* ga, int batch, int cfg, int splits, float* 
     case 0: return launch_cfg<1, 4, 1, 1, 64>(g, batch, splits, ws, ws_floats, counters, n_counters, st);   // 16 x 64
     case 1: return launch_cfg<2, 2, 1, 2, 64>(g, batch, splits, ws, ws_floats, counters, n_counters, st);   // 32 x 64
     case 2: return launch_cfg<2, 2, 2, 2, 32>(g, batch, splits, ws, ws_floats, counters, n_counters, st);   // 64 x 64
-    case 3: return launch_cfg<2, 2, 4, 4, 32>(g, batch, splits, ws, ws_floats, counters, n_counters, st);   // 128 x 128
+    case 3: return launch_cfg<2, 2, 2, 4, 32>(g, batch, splits, ws, ws_floats, counters, n_counters, st);   // 64 x 128
     case 4: return launch_cfg<4, 1, 1, 1, 64>(g, batch, splits, ws, ws_floats, counters, n_counters, st);   // 64 x 16
     default: return -1;
   }

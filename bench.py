@@ -52,14 +52,72 @@ def build_dp(args, dev):
     return tr, batch, desc
 
 
+def build_fsdp(args, dev):
+    from data_paral import synthetic_batch
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import shard_batch
+    from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
+    from jax_distributed_tuts_amd.utils.config import fsdp_config
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    cfg = fsdp_config()
+    cfg.model.num_layers = args.num_layers
+    mesh = Mesh({"data": D.world_size()})
+    model = Classifier.from_config(cfg.model)
+    st = init_fsdp(model, adamw(cfg.model.lr), cfg.seed, dev, mesh, "data", cfg.model.min_weight_size)
+    batch = shard_batch(synthetic_batch(cfg, cfg.seed + 1), mesh, "data")
+    batch = Batch(batch.inputs.to(dev), batch.labels.to(dev))
+    once = args.accum != "loop"
+    tr = FSDPTrainer(st, mesh, FSDPConfig(cfg.num_minibatches, cfg.model.min_weight_size, "data", gather_once=once,
+                                          scatter_once=once))
+    desc = {"model": f"tutorial MLP {'-'.join(map(str, model.dims))} (SiLU, dropout 0.1)",
+            "global_batch": cfg.data.batch_size, "seq_len": None, "num_minibatches": cfg.num_minibatches,
+            "parallelism": f"fsdp{D.world_size()}", "gather_once": once}
+    return tr, batch, desc
+
+
+def build_pp(args, dev):
+    from data_paral import synthetic_batch
+    from pipeline_parallel import build_mlp_pipeline
+    from jax_distributed_tuts_amd.parallel.dp import shard_batch
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.train_state import Batch
+
+    cfg = dp_config()
+    ws = D.world_size()
+    dp = args.dp
+    mesh = Mesh({"data": dp, "pipe": ws // dp})
+    if args.model == "transformer":
+        from jax_distributed_tuts_amd.parallel.pipeline_lm import build_lm_pipeline, lm_batch
+
+        tr, lm_cfg = build_lm_pipeline(mesh, dev, num_microbatches=args.microbatches)
+        batch = shard_batch(lm_batch(lm_cfg, global_batch=args.lm_batch, seed=1), mesh, "data")
+        desc = {"model": f"transformer LM {lm_cfg.n_layers}L d{lm_cfg.d_model} h{lm_cfg.n_heads} "
+                         f"ff{lm_cfg.d_ff} V{lm_cfg.vocab_size}", "global_batch": args.lm_batch,
+                "seq_len": lm_cfg.seq_len, "tokens_per_step": args.lm_batch * lm_cfg.seq_len}
+    else:
+        tr = build_mlp_pipeline(cfg, mesh, dev, args.hidden_layers, num_microbatches=args.microbatches)
+        batch = shard_batch(synthetic_batch(cfg, cfg.seed + 1), mesh, "data")
+        desc = {"model": f"MLP 784-512x{args.hidden_layers}-10 GPipe", "global_batch": cfg.data.batch_size,
+                "seq_len": None}
+    desc.update({"num_microbatches": args.microbatches, "parallelism": f"dp{dp}xpp{ws // dp}"})
+    batch = Batch(batch.inputs.to(dev), batch.labels.to(dev))
+    return tr, batch, desc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--strategy", choices=["dp"], default="dp")
+    ap.add_argument("--strategy", choices=["dp", "fsdp", "pp"], default="dp")
+    ap.add_argument("--dp", type=int, default=1, help="data-parallel degree for --strategy pp (hybrid)")
+    ap.add_argument("--model", choices=["mlp", "transformer"], default="mlp")
+    ap.add_argument("--microbatches", type=int, default=4)
+    ap.add_argument("--hidden-layers", type=int, default=8)
+    ap.add_argument("--lm-batch", type=int, default=16)
     ap.add_argument("--num-layers", type=int, default=2)
-    ap.add_argument("--accum", choices=["loop", "fused"], default="loop")
+    ap.add_argument("--accum", choices=["loop", "fused", "kernel"], default="kernel")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--capture-collectives", action="store_true")
     args = ap.parse_args()
@@ -68,7 +126,8 @@ def main():
     ws = D.world_size()
     if ws != args.gpus and D.rank() == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
-    tr, batch, desc = build_dp(args, dev)
+    build = {"dp": build_dp, "fsdp": build_fsdp, "pp": build_pp}[args.strategy]
+    tr, batch, desc = build(args, dev)
     on_gpu = dev.type == "cuda"
     sync = (lambda: torch.cuda.synchronize()) if on_gpu else (lambda: None)
 
@@ -77,7 +136,8 @@ def main():
     for _ in range(n_eager):
         tr.step(batch)
     sync()
-    use_graph = on_gpu and not args.no_graph
+    # collectives/p2p inside FSDP and PP steps stay eager; DP captures its step
+    use_graph = on_gpu and not args.no_graph and args.strategy == "dp"
     if use_graph:
         tr.capture(batch, capture_collectives=args.capture_collectives)
     for _ in range(max(0, args.warmup - n_eager)):
@@ -109,7 +169,9 @@ def main():
             ts.append(a.elapsed_time(b))
         ts.sort()
         p50, p90 = ts[len(ts) // 2], ts[int(0.9 * len(ts))]
-    m = tr.metrics.detach().float().cpu()
+    if hasattr(tr, "finalize"):
+        tr.finalize()
+    m = (tr.gather_metrics() if hasattr(tr, "gather_metrics") else tr.metrics).detach().float().cpu()
     sps = args.steps / dt
     if D.rank() == 0:
         out = {"metric": METRIC, "value": round(sps, 2), "unit": "steps/s", "n_gpus": ws, "steps": args.steps,

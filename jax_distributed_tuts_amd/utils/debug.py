@@ -1,0 +1,82 @@
+"""Debug aids: replication checker, failure reporting, serialized-kernel mode.
+
+The reference disables shard_map's replication check everywhere
+(``check_rep=False``, data_paral.py:161,247; param_sharding.py:258,273,376) and
+has no race/failure tooling.  Here:
+
+* :func:`check_replicated` -- T7: hash the tensors that must be identical on
+  every member of a mesh axis (DP params after a step, replicated FSDP leaves)
+  and all-gather the hashes; raises with the diverging ranks.
+* :func:`debug_mode` -- HIP_LAUNCH_BLOCKING / AMD_SERIALIZE_KERNEL style
+  serialisation so a faulting kernel is reported at its launch.
+* :func:`guarded` -- run a step function; on an exception print it on the
+  failing rank (``print_exception``, util.py:12-14), tear the process group
+  down so peers fail fast instead of hanging in a collective, and re-raise.
+"""
+from __future__ import annotations
+
+import contextlib
+import hashlib
+import os
+from typing import Dict, Iterable, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..comm import collectives as C
+from ..runtime.dist import Mesh, is_initialized
+from .metrics import print_exception
+
+
+def tensor_digest(t: torch.Tensor) -> int:
+    b = t.detach().contiguous().cpu().view(torch.uint8).numpy().tobytes()
+    return int.from_bytes(hashlib.blake2b(b, digest_size=8).digest(), "little", signed=True)
+
+
+class ReplicationError(RuntimeError):
+    pass
+
+
+def check_replicated(tensors: Dict[str, torch.Tensor], mesh: Optional[Mesh], axis: str) -> None:
+    """All members of ``axis`` must hold bit-identical ``tensors``."""
+    n = C.axis_size(mesh, axis)
+    if n == 1 or not is_initialized():
+        return
+    names = sorted(tensors)
+    h = torch.tensor([tensor_digest(tensors[k]) for k in names], dtype=torch.int64)
+    dev = tensors[names[0]].device if dist.get_backend(mesh.group(axis)) == "nccl" else torch.device("cpu")
+    h = h.to(dev)
+    allh = C.all_gather(h[None], mesh, axis, dim=0).cpu()
+    bad = [(names[j], [int(r) for r in range(n) if allh[r, j] != allh[0, j]]) for j in range(len(names))
+           if not bool((allh[:, j] == allh[0, j]).all())]
+    if bad:
+        raise ReplicationError(f"replicated tensors diverged on axis {axis!r}: {bad}")
+
+
+@contextlib.contextmanager
+def debug_mode(serialize: bool = True):
+    """Serialise kernel launches (faults surface at the offending launch)."""
+    old = {k: os.environ.get(k) for k in ("HIP_LAUNCH_BLOCKING", "AMD_SERIALIZE_KERNEL", "AMD_SERIALIZE_COPY")}
+    if serialize:
+        os.environ.update({"HIP_LAUNCH_BLOCKING": "1", "AMD_SERIALIZE_KERNEL": "3", "AMD_SERIALIZE_COPY": "3"})
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def guarded(fn, *args, **kw):
+    try:
+        return fn(*args, **kw)
+    except Exception as e:  # noqa: BLE001
+        print_exception(e)
+        if is_initialized():
+            try:
+                dist.destroy_process_group()
+            except Exception:  # noqa: BLE001
+                pass
+        raise

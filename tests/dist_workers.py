@@ -117,3 +117,48 @@ def pp_run(out_dir, dp, n_hidden=3, n_mb=4, steps=3):
     for _ in range(steps):
         tr.step(batch)
     _save(out_dir, f"pp_dp{dp}", {"params": tr.state.params.state_dict(), "metrics": tr.gather_metrics()})
+
+
+def replication(out_dir):
+    from jax_distributed_tuts_amd.utils.debug import ReplicationError, check_replicated
+
+    mesh = Mesh({"data": D.world_size()})
+    same = {"w": torch.arange(10.0)}
+    check_replicated(same, mesh, "data")
+    diff = {"w": torch.arange(10.0) + (D.rank() == 1)}
+    try:
+        check_replicated(diff, mesh, "data")
+        res = "no-error"
+    except ReplicationError as e:
+        res = str(e)
+    _save(out_dir, "rep", {"res": res})
+
+
+def ckpt(out_dir):
+    from data_paral import synthetic_batch
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import shard_batch
+    from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
+    from jax_distributed_tuts_amd.utils import checkpoint
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.train_state import adamw
+
+    cfg = dp_config()
+    mesh = Mesh({"data": D.world_size()})
+    batch = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
+
+    def make():
+        st = init_fsdp(Classifier(dropout_rate=0.0), adamw(1e-3), 69, "cpu", mesh, "data", 16)
+        return st, FSDPTrainer(st, mesh, FSDPConfig(4, 16, "data"))
+
+    st, tr = make()
+    for _ in range(2):
+        tr.step(batch)
+    checkpoint.save(st, os.path.join(out_dir, "ck"), tr.metrics)
+    tr.step(batch)
+    ref = tr.full_params()
+    st2, tr2 = make()
+    checkpoint.restore(st2, os.path.join(out_dir, "ck"), tr2.metrics)
+    tr2.step(batch)
+    _save(out_dir, "ck", {"ref": ref, "got": tr2.full_params(), "step": st2.step,
+                          "count": int(st2.opt_state["count"])})

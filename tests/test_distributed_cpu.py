@@ -177,3 +177,19 @@ def test_pipeline_equals_single_device(tmp_path, ws, dp):
             seen.add(k)
         _metrics_close(o["metrics"], ref_m)
     assert seen == set(ref_p)
+
+
+def test_replication_checker(tmp_path):
+    spawn(W.replication, 2, str(tmp_path))
+    for o in _load(tmp_path, "rep", 2):
+        assert "diverged" in o["res"] and "'w'" in o["res"]
+
+
+def test_checkpoint_resume_fsdp(tmp_path):
+    """save after 2 steps, restore into a fresh sharded state, step once ==
+    uninterrupted 3 steps (rank-local safetensors shards)."""
+    spawn(W.ckpt, 2, str(tmp_path))
+    for o in _load(tmp_path, "ck", 2):
+        assert o["step"] == 3 and o["count"] == 3
+        for k in o["ref"]:
+            torch.testing.assert_close(o["got"][k], o["ref"][k], rtol=0, atol=0)

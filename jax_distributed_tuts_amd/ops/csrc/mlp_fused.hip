@@ -73,56 +73,88 @@ __device__ __forceinline__ float adam_elem(float* p, float* m, float* v, long i,
 }
 
 // ---------------------------------------------------------------------------- forward
+// Every global load of the workgroup is issued before the first LDS write or
+// MFMA (one HBM/L2 round trip instead of one per loop trip: the kernels are
+// latency-, not bandwidth-bound at these sizes).
 template <int K_IN, int C>
 __global__ void __launch_bounds__(256) mlp2_fwd_kernel(Mlp2Args a) {
   constexpr int KS = (K_IN + 31) / 32;  // 32-deep MFMA k-steps
   constexpr int KP = KS * 32;
   constexpr int LDW = KP + 8;           // padded [n][k] row (bank spread)
+  constexpr int WCH = (K_IN * 2 + 255) / 256;  // 16-byte W1 chunks per thread
+  constexpr int MAXT = (KS + 3) / 4;           // k-steps per wave
   __shared__ __attribute__((aligned(16))) bf16_t w1t[16 * LDW];
   __shared__ float part[4][32][17];
   __shared__ float htile[32][17];
+  __shared__ float w2s[16][C];
+  __shared__ float b1sh[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int M = a.M, H = a.H;
   const int r0 = blockIdx.x * 32, j0 = blockIdx.y * 16;
   const int step = a.step[0], par = step & 1;
   const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
-
-  // W1[:, j0:j0+16] -> LDS transposed (w1t[n][k]); 16-byte global loads
-  for (int idx = tid; idx < KP * 2; idx += 256) {
-    const int k = idx >> 1, h = (idx & 1) * 8;
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if (k < K_IN) v = *reinterpret_cast<const u32x4*>(a.W1s + (long)k * H + j0 + h);
-    const unsigned wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      w1t[(h + 2 * e) * LDW + k] = (bf16_t)(wv[e] & 0xffff);
-      w1t[(h + 2 * e + 1) * LDW + k] = (bf16_t)(wv[e] >> 16);
-    }
-  }
-  __syncthreads();
-
-  // K split over the 4 waves; X fragments straight from global (fp32 -> bf16)
-  f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  const bf16_t* W2s = par ? a.W2s1 : a.W2s0;
   const int ks0 = (w * KS) / 4, ks1 = ((w + 1) * KS) / 4;
-  constexpr int MAXT = (KS + 3) / 4;
+
+  // ---- 1. issue all global loads
+  u32x4 wv[WCH];
+#pragma unroll
+  for (int t = 0; t < WCH; ++t) {
+    const int idx = tid + t * 256;
+    wv[t] = (u32x4){0u, 0u, 0u, 0u};
+    if (idx < K_IN * 2) wv[t] = *reinterpret_cast<const u32x4*>(a.W1s + (long)(idx >> 1) * H + j0 + (idx & 1) * 8);
+  }
+  float4 xa[MAXT][2][2];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {
-    const int ks = ks0 + t;
-    if (ks < ks1) {
-      const int k = ks * 32 + 8 * (lane >> 4);
+    const int k = (ks0 + t) * 32 + 8 * (lane >> 4);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int row = r0 + mt * 16 + (lane & 15);
+      xa[t][mt][0] = xa[t][mt][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ks0 + t < ks1 && row < M && k < K_IN) {
+        const float4* xp = reinterpret_cast<const float4*>(a.X + (long)row * K_IN + k);
+        xa[t][mt][0] = xp[0];
+        xa[t][mt][1] = xp[1];
+      }
+    }
+  }
+  float w2v = 0.f, b1v = 0.f;
+  if (tid < 16 * C) w2v = bf2f(W2s[(long)(j0 + tid / C) * C + tid % C]);
+  if (tid < 16) b1v = bf2f(a.b1s[j0 + tid]);
+
+  // ---- 2. W1 block -> LDS transposed (w1t[n][k]), zero the K padding
+#pragma unroll
+  for (int t = 0; t < WCH; ++t) {
+    const int idx = tid + t * 256;
+    if (idx < K_IN * 2) {
+      const int k = idx >> 1, h = (idx & 1) * 8;
+      const unsigned q[4] = {wv[t].x, wv[t].y, wv[t].z, wv[t].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        w1t[(h + 2 * e) * LDW + k] = (bf16_t)(q[e] & 0xffff);
+        w1t[(h + 2 * e + 1) * LDW + k] = (bf16_t)(q[e] >> 16);
+      }
+    }
+  }
+  for (int idx = tid; idx < 16 * (KP - K_IN); idx += 256) w1t[(idx / (KP - K_IN)) * LDW + K_IN + idx % (KP - K_IN)] = 0;
+  if (tid < 16 * C) w2s[tid / C][tid % C] = w2v;
+  if (tid < 16) b1sh[tid] = b1v;
+  __syncthreads();
+
+  // ---- 3. K split over the 4 waves
+  f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    if (ks0 + t < ks1) {
+      const int k = (ks0 + t) * 32 + 8 * (lane >> 4);
       const bf16x8 b = *reinterpret_cast<const bf16x8*>(&w1t[(lane & 15) * LDW + k]);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
-        const int row = r0 + mt * 16 + (lane & 15);
+        const float4 x0 = xa[t][mt][0], x1 = xa[t][mt][1];
         bf16x8 af;
-        if (row < M && k < K_IN) {
-          const float4* xp = reinterpret_cast<const float4*>(a.X + (long)row * K_IN + k);
-          const float4 x0 = xp[0], x1 = xp[1];
-          af[0] = (short)f2bf(x0.x); af[1] = (short)f2bf(x0.y); af[2] = (short)f2bf(x0.z); af[3] = (short)f2bf(x0.w);
-          af[4] = (short)f2bf(x1.x); af[5] = (short)f2bf(x1.y); af[6] = (short)f2bf(x1.z); af[7] = (short)f2bf(x1.w);
-        } else {
-          af = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-        }
+        af[0] = (short)f2bf(x0.x); af[1] = (short)f2bf(x0.y); af[2] = (short)f2bf(x0.z); af[3] = (short)f2bf(x0.w);
+        af[4] = (short)f2bf(x1.x); af[5] = (short)f2bf(x1.y); af[6] = (short)f2bf(x1.z); af[7] = (short)f2bf(x1.w);
         acc[mt] = mfma16x16x32(af, b, acc[mt]);
       }
     }
@@ -133,12 +165,14 @@ __global__ void __launch_bounds__(256) mlp2_fwd_kernel(Mlp2Args a) {
     for (int e = 0; e < 4; ++e) part[w][mt * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[mt][e];
   __syncthreads();
 
-  // bias + silu + dropout epilogue, H tile kept in LDS for the logits partials
-  for (int idx = tid; idx < 32 * 16; idx += 256) {
+  // ---- 4. bias + silu + dropout; H tile kept in LDS for the logits partials
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int idx = tid + q * 256;
     const int rl = idx >> 4, c = idx & 15, row = r0 + rl, col = j0 + c;
     float hv = 0.f;
     if (row < M) {
-      const float v = part[0][rl][c] + part[1][rl][c] + part[2][rl][c] + part[3][rl][c] + bf2f(a.b1s[col]);
+      const float v = part[0][rl][c] + part[1][rl][c] + part[2][rl][c] + part[3][rl][c] + b1sh[c];
       const bf16_t zb = f2bf(v);
       a.Z1[(long)row * H + col] = zb;
       hv = act_fwd(ACT_SILU, bf2f(zb));
@@ -151,14 +185,13 @@ __global__ void __launch_bounds__(256) mlp2_fwd_kernel(Mlp2Args a) {
     htile[rl][c] = hv;
   }
   __syncthreads();
-  const bf16_t* W2s = par ? a.W2s1 : a.W2s0;
   float* lg = a.logits + (long)par * M * C;
   for (int idx = tid; idx < 32 * C; idx += 256) {
     const int rl = idx / C, c = idx % C, row = r0 + rl;
     if (row >= M) continue;
     float s = (blockIdx.y == 0) ? bf2f(a.b2s[c]) : 0.f;
 #pragma unroll
-    for (int n = 0; n < 16; ++n) s += htile[rl][n] * bf2f(W2s[(long)(j0 + n) * C + c]);
+    for (int n = 0; n < 16; ++n) s += htile[rl][n] * w2s[n][c];
     atomicAdd(lg + (long)row * C + c, s);
   }
 }
@@ -166,77 +199,114 @@ __global__ void __launch_bounds__(256) mlp2_fwd_kernel(Mlp2Args a) {
 // ---------------------------------------------------------------------------- backward
 template <int K_IN, int C, int KC>
 __global__ void __launch_bounds__(256) mlp2_bwd_kernel(Mlp2Args a) {
-  constexpr int MPM = 256;       // max rows per device
-  constexpr int LDM = MPM + 8;   // padded row (bf16 elements)
+  constexpr int MPM = 128;                 // max rows per device (fused path)
+  constexpr int LDM = MPM + 8;             // padded row (bf16 elements)
+  constexpr int ZE = MPM * 16 / 256;       // Z1/H1 elements per thread
+  constexpr int XE = MPM * (KC / 4) / 256; // float4 X loads per thread
+  static_assert(KC % 4 == 0 && K_IN % 4 == 0, "X chunks are float4");
   __shared__ float dlog[MPM][C + 1];
   __shared__ __attribute__((aligned(16))) bf16_t dzT[16 * LDM];
   __shared__ __attribute__((aligned(16))) bf16_t xT[KC * LDM];
-  __shared__ float red[3][4];
+  __shared__ float h1s[MPM][17];
+  __shared__ float w2s[16][C];
+  __shared__ float red[2][4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int M = a.M, H = a.H, Mp = (M + 31) & ~31;
   const int j0 = blockIdx.x * 16, kc0 = blockIdx.y * KC;
+  const bool chunk0 = blockIdx.y == 0;
   const int step = a.step[0], par = step & 1;
   const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
   const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
   const AdamK ak = adam_consts(a, step);
-
-  // 1. logits (fp32 partial sums -> bf16 like the Dense output) -> CE -> dlogits
+  const bf16_t* W2s = par ? a.W2s1 : a.W2s0;
   const float* lg = a.logits + (long)par * M * C;
+
+  // ---- 0. issue all global loads
+  float lrow[C];
+  int lab = 0;
+  if (tid < M) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) lrow[c] = lg[(long)tid * C + c];
+    lab = a.labels[tid];
+  }
+  bf16_t zv[ZE], hv[ZE];
+#pragma unroll
+  for (int e = 0; e < ZE; ++e) {
+    const int idx = tid + e * 256, m = idx >> 4, n = idx & 15;
+    zv[e] = 0; hv[e] = 0;
+    if (m < M) {
+      zv[e] = a.Z1[(long)m * H + j0 + n];
+      if (chunk0) hv[e] = a.H1[(long)m * H + j0 + n];
+    }
+  }
+  float4 xv[XE];
+#pragma unroll
+  for (int e = 0; e < XE; ++e) {
+    const int idx = tid + e * 256, m = idx / (KC / 4), i4 = idx % (KC / 4);
+    xv[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (m < M && kc0 + 4 * i4 < K_IN) xv[e] = *reinterpret_cast<const float4*>(a.X + (long)m * K_IN + kc0 + 4 * i4);
+  }
+  float w2v = 0.f;
+  if (tid < 16 * C) w2v = bf2f(W2s[(long)(j0 + tid / C) * C + tid % C]);
+
+  // ---- 1. CE from the summed logits (rounded like the bf16 Dense output) -> dlogits
   float l_loss = 0.f, l_corr = 0.f;
-  for (int r = tid; r < M; r += 256) {
-    float z[C];
+  if (tid < M) {
     float mx = -INFINITY;
     int am = 0;
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      z[c] = round_bf(lg[(long)r * C + c]);
-      if (z[c] > mx) { mx = z[c]; am = c; }
+      lrow[c] = round_bf(lrow[c]);
+      if (lrow[c] > mx) { mx = lrow[c]; am = c; }
     }
     float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < C; ++c) s += __expf(z[c] - mx);
+    for (int c = 0; c < C; ++c) s += __expf(lrow[c] - mx);
     const float lse = mx + __logf(s);
-    const int lab = a.labels[r];
-    l_loss += lse - z[lab];
-    l_corr += (am == lab) ? 1.f : 0.f;
+    l_loss = lse - lrow[lab];
+    l_corr = (am == lab) ? 1.f : 0.f;
 #pragma unroll
-    for (int c = 0; c < C; ++c) dlog[r][c] = round_bf((__expf(z[c] - lse) - (c == lab ? 1.f : 0.f)) * a.inv_mb);
+    for (int c = 0; c < C; ++c)
+      dlog[tid][c] = round_bf((__expf(lrow[c] - lse) - (c == lab ? 1.f : 0.f)) * a.inv_mb);
   }
+  if (tid < 16 * C) w2s[tid / C][tid % C] = w2v;
   if (lead) {
     l_loss = wave_sum(l_loss);
     l_corr = wave_sum(l_corr);
     if (lane == 0) { red[0][w] = l_loss; red[1][w] = l_corr; }
-    // re-arm the other parity's logits accumulator for the next step's forward
-    float* nxt = a.logits + (long)(par ^ 1) * M * C;
+    float* nxt = a.logits + (long)(par ^ 1) * M * C;   // re-arm next step's accumulator
     for (int i = tid; i < M * C; i += 256) nxt[i] = 0.f;
+  }
+  // X chunk -> xT[i][m] (bf16, K(=row)-contiguous for the MFMA fragments)
+#pragma unroll
+  for (int e = 0; e < XE; ++e) {
+    const int idx = tid + e * 256, m = idx / (KC / 4), i = 4 * (idx % (KC / 4));
+    xT[(i + 0) * LDM + m] = f2bf(xv[e].x);
+    xT[(i + 1) * LDM + m] = f2bf(xv[e].y);
+    xT[(i + 2) * LDM + m] = f2bf(xv[e].z);
+    xT[(i + 3) * LDM + m] = f2bf(xv[e].w);
   }
   __syncthreads();
 
-  // 2. dZ1[:, blk] -> dzT[n][m] (bf16, rows >= M zero-padded to Mp)
-  const bf16_t* W2s = par ? a.W2s1 : a.W2s0;
-  for (int idx = tid; idx < Mp * 16; idx += 256) {
-    const int m = idx >> 4, n = idx & 15, col = j0 + n;
+  // ---- 2. dZ1[:, blk] = (dlogits W2[blk]^T) * silu'(Z1) * mask/keep -> dzT[n][m]; H1 tile -> LDS
+#pragma unroll
+  for (int e = 0; e < ZE; ++e) {
+    const int idx = tid + e * 256, m = idx >> 4, n = idx & 15;
     float v = 0.f;
     if (m < M) {
       float dh = 0.f;
 #pragma unroll
-      for (int c = 0; c < C; ++c) dh += dlog[m][c] * bf2f(W2s[(long)col * C + c]);
-      v = dh * act_grad(ACT_SILU, bf2f(a.Z1[(long)m * H + col]));
+      for (int c = 0; c < C; ++c) dh += dlog[m][c] * w2s[n][c];
+      v = dh * act_grad(ACT_SILU, bf2f(zv[e]));
       if (a.keep < 1.f)
-        v = dropout_keep(a.seed, doff, (unsigned long long)m * H + col, a.keep) ? v / a.keep : 0.f;
+        v = dropout_keep(a.seed, doff, (unsigned long long)m * H + j0 + n, a.keep) ? v / a.keep : 0.f;
     }
     dzT[n * LDM + m] = f2bf(v);
-  }
-  // 3. X[:, chunk] -> xT[i][m] (bf16, transposed so MFMA fragments are 16-byte reads)
-  for (int idx = tid; idx < Mp * KC; idx += 256) {
-    const int m = idx / KC, i = idx % KC;
-    float v = 0.f;
-    if (m < M && kc0 + i < K_IN) v = a.X[(long)m * K_IN + kc0 + i];
-    xT[i * LDM + m] = f2bf(v);
+    if (chunk0) h1s[m][n] = bf2f(hv[e]);
   }
   __syncthreads();
 
-  // 4. dW1[chunk, blk] = X[:, chunk]^T dZ1[:, blk]   (K = rows)
+  // ---- 3. dW1[chunk, blk] = X[:, chunk]^T dZ1[:, blk]   (K = rows) on MFMA
   for (int tile = w; tile < KC / 16; tile += 4) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int ks = 0; ks < Mp / 32; ++ks) {
@@ -248,21 +318,22 @@ __global__ void __launch_bounds__(256) mlp2_bwd_kernel(Mlp2Args a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int i = kc0 + tile * 16 + (lane >> 4) * 4 + e;
-      if (i >= K_IN) continue;
-      const long idx = (long)i * H + j0 + (lane & 15);
-      if (a.fuse_opt) a.sW1[idx] = f2bf(adam_elem(a.pW1, a.mW1, a.vW1, idx, acc[e], ak));
-      else a.gW1[idx] = acc[e];
+      if (i < K_IN) {
+        const long idx = (long)i * H + j0 + (lane & 15);
+        if (a.fuse_opt) a.sW1[idx] = f2bf(adam_elem(a.pW1, a.mW1, a.vW1, idx, acc[e], ak));
+        else a.gW1[idx] = acc[e];
+      }
     }
   }
 
-  // 5. chunk-0 blocks: db1[blk], dW2[blk, :]; block (0,0): db2 + metrics
-  if (blockIdx.y == 0) {
-    bf16_t* sW2n = par ? a.sW2_0 : a.sW2_1;   // next step's parity
+  // ---- 4. chunk-0 blocks: db1[blk], dW2[blk, :]; block (0,0): db2 + metrics
+  if (chunk0) {
+    bf16_t* sW2n = par ? a.sW2_0 : a.sW2_1;   // next step's parity buffer
     for (int idx = tid; idx < 16 * C + 16; idx += 256) {
       if (idx < 16 * C) {
         const int n = idx / C, c = idx % C;
         float s = 0.f;
-        for (int m = 0; m < M; ++m) s += bf2f(a.H1[(long)m * H + j0 + n]) * dlog[m][c];
+        for (int m = 0; m < M; ++m) s += h1s[m][n] * dlog[m][c];
         const long o = (long)(j0 + n) * C + c;
         if (a.fuse_opt) sW2n[o] = f2bf(adam_elem(a.pW2, a.mW2, a.vW2, o, s, ak));
         else a.gW2[o] = s;
@@ -310,10 +381,10 @@ using namespace jdt;
 
 JDT_API int jdt_mlp2_args_size() { return (int)sizeof(Mlp2Args); }
 
-// phase 0: forward, 1: backward.  Supported: K_IN = 784, C = 10, H % 16 == 0, M <= 256.
+// phase 0: forward, 1: backward.  Supported: K_IN = 784, C = 10, H % 16 == 0, M <= 128.
 JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* stream) {
   const Mlp2Args& a = *args;
-  if (k_in != 784 || c != 10 || a.H % 16 || a.M <= 0 || a.M > 256) return -3;
+  if (k_in != 784 || c != 10 || a.H % 16 || a.M <= 0 || a.M > 128) return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (phase == 0) {
     hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10>), dim3((a.M + 31) / 32, a.H / 16), dim3(256), 0, st, a);

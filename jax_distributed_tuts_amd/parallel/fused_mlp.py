@@ -46,7 +46,7 @@ def supported(model, rows: int, device) -> bool:
     from ..models.mlp import MLP
 
     return (torch.device(device).type == "cuda" and isinstance(model, MLP) and model.L == 2 and model.dims[0] == 784
-            and model.dims[2] == 10 and model.dims[1] % 16 == 0 and 0 < rows <= 256 and model.act == "silu"
+            and model.dims[2] == 10 and model.dims[1] % 16 == 0 and 0 < rows <= 128 and model.act == "silu"
             and not model.final_act)
 
 

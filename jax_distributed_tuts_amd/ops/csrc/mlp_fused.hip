@@ -49,7 +49,15 @@ struct Mlp2Args {
   bf16_t* sW1; bf16_t* sb1; bf16_t* sW2_0; bf16_t* sW2_1; bf16_t* sb2;
   float lr, beta1, beta2, eps, wd, gscale;
   float* running;
+  unsigned long long* stamps;   // diagnostic: per-workgroup s_memrealtime (100 MHz) at phase ends (null = off)
 };
+
+// In-kernel phase stamps (diagnostic builds only read them; one branch when off).
+#define STAMP(i)                                                                              \
+  do {                                                                                        \
+    if (a.stamps && threadIdx.x == 0)                                                         \
+      a.stamps[(long)(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 
 struct AdamK { float b1, b2, eps, wd, lr, gs, rbc1, rbc2; };
 
@@ -91,6 +99,7 @@ __global__ void __launch_bounds__(256) mlp2_fwd_kernel(Mlp2Args a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int M = a.M, H = a.H;
   const int r0 = blockIdx.x * 32, j0 = blockIdx.y * 16;
+  STAMP(0);
   const int step = a.step[0], par = step & 1;
   const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
   const bf16_t* W2s = par ? a.W2s1 : a.W2s0;
@@ -141,6 +150,7 @@ __global__ void __launch_bounds__(256) mlp2_fwd_kernel(Mlp2Args a) {
   if (tid < 16 * C) w2s[tid / C][tid % C] = w2v;
   if (tid < 16) b1sh[tid] = b1v;
   __syncthreads();
+  STAMP(1);
 
   // ---- 3. K split over the 4 waves
   f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -164,6 +174,7 @@ __global__ void __launch_bounds__(256) mlp2_fwd_kernel(Mlp2Args a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) part[w][mt * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[mt][e];
   __syncthreads();
+  STAMP(2);
 
   // ---- 4. bias + silu + dropout; H tile kept in LDS for the logits partials
 #pragma unroll
@@ -185,6 +196,7 @@ __global__ void __launch_bounds__(256) mlp2_fwd_kernel(Mlp2Args a) {
     htile[rl][c] = hv;
   }
   __syncthreads();
+  STAMP(3);
   float* lg = a.logits + (long)par * M * C;
   for (int idx = tid; idx < 32 * C; idx += 256) {
     const int rl = idx / C, c = idx % C, row = r0 + rl;
@@ -194,6 +206,8 @@ __global__ void __launch_bounds__(256) mlp2_fwd_kernel(Mlp2Args a) {
     for (int n = 0; n < 16; ++n) s += htile[rl][n] * w2s[n][c];
     atomicAdd(lg + (long)row * C + c, s);
   }
+  __syncthreads();
+  STAMP(4);
 }
 
 // ---------------------------------------------------------------------------- backward
@@ -217,6 +231,7 @@ __global__ void __launch_bounds__(256) mlp2_bwd_kernel(Mlp2Args a) {
   const int step = a.step[0], par = step & 1;
   const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
   const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
+  STAMP(0);
   const AdamK ak = adam_consts(a, step);
   const bf16_t* W2s = par ? a.W2s1 : a.W2s0;
   const float* lg = a.logits + (long)par * M * C;
@@ -288,6 +303,7 @@ __global__ void __launch_bounds__(256) mlp2_bwd_kernel(Mlp2Args a) {
   }
   __syncthreads();
 
+  STAMP(1);
   // ---- 2. dZ1[:, blk] = (dlogits W2[blk]^T) * silu'(Z1) * mask/keep -> dzT[n][m]; H1 tile -> LDS
 #pragma unroll
   for (int e = 0; e < ZE; ++e) {
@@ -306,6 +322,7 @@ __global__ void __launch_bounds__(256) mlp2_bwd_kernel(Mlp2Args a) {
   }
   __syncthreads();
 
+  STAMP(2);
   // ---- 3. dW1[chunk, blk] = X[:, chunk]^T dZ1[:, blk]   (K = rows) on MFMA
   for (int tile = w; tile < KC / 16; tile += 4) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -326,6 +343,8 @@ __global__ void __launch_bounds__(256) mlp2_bwd_kernel(Mlp2Args a) {
     }
   }
 
+  __syncthreads();
+  STAMP(3);
   // ---- 4. chunk-0 blocks: db1[blk], dW2[blk, :]; block (0,0): db2 + metrics
   if (chunk0) {
     bf16_t* sW2n = par ? a.sW2_0 : a.sW2_1;   // next step's parity buffer
@@ -363,9 +382,10 @@ __global__ void __launch_bounds__(256) mlp2_bwd_kernel(Mlp2Args a) {
       }
     }
   }
+  __syncthreads();
+  STAMP(4);
   if (a.fuse_opt) {
     // advance the device step once every workgroup has read it
-    __syncthreads();
     if (tid == 0) {
       const unsigned t = atomicAdd(a.ticket, 1u);
       if (t == gridDim.x * gridDim.y - 1) {

@@ -35,7 +35,7 @@ class Mlp2Args(ctypes.Structure):
                 ("vW1", c_void_p), ("vb1", c_void_p), ("vW2", c_void_p), ("vb2", c_void_p),
                 ("sW1", c_void_p), ("sb1", c_void_p), ("sW2_0", c_void_p), ("sW2_1", c_void_p), ("sb2", c_void_p),
                 ("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float), ("wd", c_float),
-                ("gscale", c_float), ("running", c_void_p)]
+                ("gscale", c_float), ("running", c_void_p), ("stamps", c_void_p)]
 
 
 _lib.declare("jdt_mlp2", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_int, c_void_p])

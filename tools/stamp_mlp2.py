@@ -1,0 +1,77 @@
+"""Diagnostic: in-kernel phase stamps (s_memrealtime, 100 MHz) of the fused
+classifier step kernels (csrc/mlp_fused.hip STAMP points).  Prints, per kernel,
+the median over workgroups of each phase's end relative to that workgroup's
+start, plus the span from the first workgroup start to the last end.
+
+    python tools/stamp_mlp2.py [--rows 128]
+"""
+from __future__ import annotations
+
+import argparse
+import copy
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from jax_distributed_tuts_amd.models.mlp import Classifier  # noqa: E402
+from jax_distributed_tuts_amd.ops import _lib  # noqa: E402
+from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp  # noqa: E402
+from jax_distributed_tuts_amd.utils.train_state import Batch, adamw  # noqa: E402
+
+NAMES = {0: ["start", "loads+LDS staged", "MFMA+reduce", "epilogue(Z1,H1)", "logit atomics"],
+         1: ["start", "CE+X/LDS staged", "dZ1", "dW1 MFMA+AdamW", "db1/dW2/db2"]}
+
+
+def report(kind, st, nwg):
+    st = st[: nwg * 8].view(nwg, 8).double() * 10e-3  # ticks -> us
+    t0 = st[:, 0]
+    print(f"--- {['mlp2_fwd', 'mlp2_bwd'][kind]}  ({nwg} WGs)  span first-start->last-end: "
+          f"{float(st[:, 4].max() - t0.min()):.2f} us; start skew {float(t0.max() - t0.min()):.2f} us")
+    prev = torch.zeros(nwg, dtype=torch.float64)
+    for i in range(1, 5):
+        d = st[:, i] - t0
+        print(f"  {NAMES[kind][i]:22s} end @ median {float(d.median()):7.2f} us  max {float(d.max()):7.2f}"
+              f"   (phase median {float((d - prev).median()):6.2f})")
+        prev = d
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=128)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(0)
+    b = Batch(torch.randn(a.rows, 784, generator=g).to(dev),
+              torch.randint(0, 10, (a.rows,), generator=g).to(torch.int32).to(dev))
+    st = init_dp(Classifier(), adamw(1e-3), 69, dev)
+    tr = DataParallelTrainer(st, None, DPConfig(4, "kernel"))
+    for _ in range(3):
+        tr.step(b)
+    eng = tr.fused
+    L = _lib.lib()
+    sa = torch.zeros(4096 * 8, dtype=torch.int64, device=dev)
+    sb = torch.zeros(4096 * 8, dtype=torch.int64, device=dev)
+    args0 = copy.copy(eng._args)
+    args1 = copy.copy(eng._args)
+    args0.stamps, args1.stamps = sa.data_ptr(), sb.data_ptr()
+    s = _lib.stream_ptr()
+    for _ in range(a.iters):
+        _lib.check(L.jdt_mlp2(ctypes.byref(args0), 0, 784, 10, s), "fwd")
+        _lib.check(L.jdt_mlp2(ctypes.byref(args1), 1, 784, 10, s), "bwd")
+    torch.cuda.synchronize()
+    H = 512
+    report(0, sa.cpu(), ((a.rows + 31) // 32) * (H // 16))
+    report(1, sb.cpu(), (H // 16) * 7)
+    # inter-kernel gap: last fwd end -> first bwd start
+    fa = sa.cpu()[: ((a.rows + 31) // 32) * (H // 16) * 8].view(-1, 8)
+    fb = sb.cpu()[: (H // 16) * 7 * 8].view(-1, 8)
+    print(f"fwd last end -> bwd first start: {float(fb[:, 0].min() - fa[:, 4].max()) * 10e-3:.2f} us")
+
+
+if __name__ == "__main__":
+    main()

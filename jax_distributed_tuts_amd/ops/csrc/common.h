@@ -67,10 +67,20 @@ __device__ __forceinline__ u32x4 philox4x32(uint64_t seed, uint64_t ctr_lo, uint
   u32x4 out; out.x = c0; out.y = c1; out.z = c2; out.w = c3;
   return out;
 }
-// keep-decision for element idx: P(keep) = keep_prob
-__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t offset, uint64_t idx, float keep_prob) {
-  const u32x4 r = philox4x32(seed, idx, offset);
-  return (float)(r.x >> 8) * (1.0f / 16777216.0f) < keep_prob;
+// Dropout mask of element (z, r, c) of a [.., M, N] activation: one Philox call
+// yields the decisions of the 4-row group (r & ~3 .. r | 3) at column c -- word
+// (r & 3) of philox(seed, counter = (z * ceil(M/4) + r/4) * N + c, offset).  Every
+// kernel that touches the mask (GEMM epilogues, act_bwd, the fused step kernels)
+// owns whole 4-row groups, so the 10-round Philox is paid once per 4 elements.
+__device__ __forceinline__ uint64_t dropout_group(int z, int r, int c, int M, int N) {
+  return ((uint64_t)z * (uint64_t)((M + 3) >> 2) + (uint64_t)(r >> 2)) * (uint64_t)N + (uint64_t)c;
+}
+__device__ __forceinline__ u32x4 dropout_bits(uint64_t seed, uint64_t offset, uint64_t group) {
+  return philox4x32(seed, group, offset);
+}
+__device__ __forceinline__ bool keep_word(const u32x4& b, int w, float keep_prob) {
+  const unsigned x = w == 0 ? b.x : (w == 1 ? b.y : (w == 2 ? b.z : b.w));
+  return (float)(x >> 8) * (1.0f / 16777216.0f) < keep_prob;
 }
 
 // ---------------------------------------------------------------- activations

@@ -22,11 +22,13 @@ __global__ void __launch_bounds__(256) act_bwd_kernel(const bf16_t* __restrict__
   const float inv_keep = drop ? 1.f / keep_prob : 1.f;
   const unsigned long long doff = offset + (step_ptr ? ((unsigned long long)(unsigned)step_ptr[0] << 32) : 0ull);
   float csum = 0.f;
-  for (int r = r0; r < r1; ++r) {
+  u32x4 dbits = {0u, 0u, 0u, 0u};
+  for (int r = r0; r < r1; ++r) {  // r0 is a multiple of 4: refresh the Philox bits per 4-row group
     const long i = (long)r * N + col;
+    if (drop && (r & 3) == 0) dbits = dropout_bits(seed, doff, dropout_group(0, r, col, M, N));
     float v = bf2f(dh[i]);
     if (z) v *= act_grad(act, bf2f(z[i]));
-    if (drop) v = dropout_keep(seed, doff, (unsigned long long)i, keep_prob) ? v * inv_keep : 0.f;
+    if (drop) v = keep_word(dbits, r & 3, keep_prob) ? v * inv_keep : 0.f;
     const bf16_t o = f2bf(v);
     dz[i] = o;
     csum += bf2f(o);

@@ -313,18 +313,19 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
     float csum = 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
+      // the lane's 4 rows form one dropout group: one Philox call for all 4
+      const int row0 = tm0 + (wm * TM + i) * 16 + (lane >> 4) * 4;
+      u32x4 dbits = {0u, 0u, 0u, 0u};
+      if (drop && cok) dbits = dropout_bits(g.seed, doff, dropout_group(z, row0, col, g.M, g.N));
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int row = tm0 + (wm * TM + i) * 16 + (lane >> 4) * 4 + e;
+        const int row = row0 + e;
         if (cok && row < g.M) {
         float v = g.alpha * acc[i][j][e] + bval;
         if (g.Zout) static_cast<bf16_t*>(g.Zout)[(long)z * g.sZ + (long)row * g.ldz + col] = f2bf(v);
         if (g.Zin) v *= act_grad(g.act_bwd, bf2f(g.Zin[(long)z * g.sZin + (long)row * g.ldzin + col]));
         if (g.act) v = act_fwd(g.act, g.Zout ? round_bf(v) : v);
-        if (drop) {
-          const unsigned long long idx = (unsigned long long)z * g.M * g.N + (unsigned long long)row * g.N + col;
-          v = dropout_keep(g.seed, doff, idx, g.keep_prob) ? v * inv_keep : 0.f;
-        }
+        if (drop) v = keep_word(dbits, e, g.keep_prob) ? v * inv_keep : 0.f;
         if (g.resid) v += bf2f(static_cast<const bf16_t*>(g.resid)[(long)z * g.sR + (long)row * g.ldr + col]);
         const long co = zoff(g, z, g.sC, g.sC2) + (long)row * g.ldc + col;
         if (g.c_f32) {

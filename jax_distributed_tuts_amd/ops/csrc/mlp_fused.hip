@@ -6,15 +6,15 @@
 // end to end regardless of its work (profiles/README.md), so the step is
 // organised around the two global data dependencies of the maths:
 //
-// mlp2_fwd  grid (row blocks of 32) x (hidden blocks of 16)
+// mlp2_fwd  grid (row blocks of 32) x (hidden blocks of 16), 8 waves
 //   Z1 = X W1 + b1 (fp32 X converted in-register, W1 column block staged
-//   transposed in LDS, K split over the 4 waves, partials reduced in LDS),
+//   transposed in LDS, K split over the 8 waves, partials reduced in LDS),
 //   H = dropout(silu(Z1)), and the block's partial logits H[:,blk] W2[blk,:]
 //   (+ b2 from block 0) accumulated with fp32 atomics into logits[M][C].
 //   (All rows of all minibatches at once: every row carries its minibatch's
 //   1/mb loss weight, so the summed gradient equals util.accum_grads_loop's.)
 //
-// mlp2_bwd  grid (hidden blocks of 16) x (input chunks of KC)
+// mlp2_bwd  grid (hidden blocks of 16) x (input chunks of KC), 8 waves
 //   every workgroup recomputes CE from the summed logits (M x C, tiny) ->
 //   dlogits; its dZ1 block = (dlogits W2[blk]^T) * silu'(Z1) * mask/keep;
 //   dW1[chunk, blk] = X[:,chunk]^T dZ1[:,blk] on MFMA with both operands
@@ -27,9 +27,18 @@
 //            round trip, no optimizer launch).  W2's bf16 shadow is double
 //            buffered by step parity because other workgroups of the same
 //            launch still read the old W2 for dZ1; b2 is only read by mlp2_fwd.
+//
+// Latency structure (tools/stamp_mlp2.py, s_memrealtime phase stamps): every
+// global load of a workgroup -- including the AdamW state of its outputs -- is
+// issued before its first LDS write or MFMA; each thread owns whole 4-row
+// dropout groups so one Philox call serves 4 elements; 8 waves per workgroup so
+// the dependent VALU chains (Philox, exp, f32->bf16) overlap across waves.
 #include "common.h"
 
 namespace jdt {
+
+constexpr int NT = 512;  // threads per workgroup (8 waves)
+constexpr int NW = NT / 64;
 
 struct Mlp2Args {
   int M, H;
@@ -52,11 +61,16 @@ struct Mlp2Args {
   unsigned long long* stamps;   // diagnostic: per-workgroup s_memrealtime (100 MHz) at phase ends (null = off)
 };
 
-// In-kernel phase stamps (diagnostic builds only read them; one branch when off).
+// Slots 0-4: s_memrealtime at phase ends; slots 5/6: s_memtime (core clock) at
+// phases 0/4, so (slot6 - slot5) / (slot4 - slot0) * 100 MHz is the shader clock.
 #define STAMP(i)                                                                              \
   do {                                                                                        \
-    if (a.stamps && threadIdx.x == 0)                                                         \
-      a.stamps[(long)(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    if (a.stamps && threadIdx.x == 0) {                                                       \
+      unsigned long long* s_ = a.stamps + (long)(blockIdx.y * gridDim.x + blockIdx.x) * 8;  \
+      s_[(i)] = __builtin_amdgcn_s_memrealtime();                                             \
+      if ((i) == 0) s_[5] = __builtin_amdgcn_s_memtime();                                     \
+      if ((i) == 4) s_[6] = __builtin_amdgcn_s_memtime();                                     \
+    }                                                                                         \
   } while (0)
 
 struct AdamK { float b1, b2, eps, wd, lr, gs, rbc1, rbc2; };
@@ -70,29 +84,30 @@ __device__ __forceinline__ AdamK adam_consts(const Mlp2Args& a, int step) {
   return k;
 }
 
-__device__ __forceinline__ float adam_elem(float* p, float* m, float* v, long i, float g, const AdamK& k) {
+// AdamW on one element whose (p, m, v) were loaded earlier; writes them back.
+__device__ __forceinline__ float adam_apply(float p, float m, float v, float g, const AdamK& k, float* pp, float* mp,
+                                            float* vp) {
   g *= k.gs;
-  const float mi = k.b1 * m[i] + (1.f - k.b1) * g;
-  const float vi = k.b2 * v[i] + (1.f - k.b2) * g * g;
-  m[i] = mi; v[i] = vi;
-  const float pi = p[i] - k.lr * ((mi * k.rbc1) / (sqrtf(vi * k.rbc2) + k.eps) + k.wd * p[i]);
-  p[i] = pi;
-  return pi;
+  m = k.b1 * m + (1.f - k.b1) * g;
+  v = k.b2 * v + (1.f - k.b2) * g * g;
+  p = p - k.lr * ((m * k.rbc1) / (sqrtf(v * k.rbc2) + k.eps) + k.wd * p);
+  *pp = p; *mp = m; *vp = v;
+  return p;
+}
+__device__ __forceinline__ float adam_elem(float* p, float* m, float* v, long i, float g, const AdamK& k) {
+  return adam_apply(p[i], m[i], v[i], g, k, p + i, m + i, v + i);
 }
 
 // ---------------------------------------------------------------------------- forward
-// Every global load of the workgroup is issued before the first LDS write or
-// MFMA (one HBM/L2 round trip instead of one per loop trip: the kernels are
-// latency-, not bandwidth-bound at these sizes).
 template <int K_IN, int C>
-__global__ void __launch_bounds__(256) mlp2_fwd_kernel(Mlp2Args a) {
+__global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   constexpr int KS = (K_IN + 31) / 32;  // 32-deep MFMA k-steps
   constexpr int KP = KS * 32;
   constexpr int LDW = KP + 8;           // padded [n][k] row (bank spread)
-  constexpr int WCH = (K_IN * 2 + 255) / 256;  // 16-byte W1 chunks per thread
-  constexpr int MAXT = (KS + 3) / 4;           // k-steps per wave
+  constexpr int WCH = (K_IN * 2 + NT - 1) / NT;  // 16-byte W1 chunks per thread
+  constexpr int MAXT = (KS + NW - 1) / NW;       // k-steps per wave
   __shared__ __attribute__((aligned(16))) bf16_t w1t[16 * LDW];
-  __shared__ float part[4][32][17];
+  __shared__ float part[NW][32][17];
   __shared__ float htile[32][17];
   __shared__ float w2s[16][C];
   __shared__ float b1sh[16];
@@ -103,13 +118,13 @@ __global__ void __launch_bounds__(256) mlp2_fwd_kernel(Mlp2Args a) {
   const int step = a.step[0], par = step & 1;
   const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
   const bf16_t* W2s = par ? a.W2s1 : a.W2s0;
-  const int ks0 = (w * KS) / 4, ks1 = ((w + 1) * KS) / 4;
+  const int ks0 = (w * KS) / NW, ks1 = ((w + 1) * KS) / NW;
 
   // ---- 1. issue all global loads
   u32x4 wv[WCH];
 #pragma unroll
   for (int t = 0; t < WCH; ++t) {
-    const int idx = tid + t * 256;
+    const int idx = tid + t * NT;
     wv[t] = (u32x4){0u, 0u, 0u, 0u};
     if (idx < K_IN * 2) wv[t] = *reinterpret_cast<const u32x4*>(a.W1s + (long)(idx >> 1) * H + j0 + (idx & 1) * 8);
   }
@@ -135,7 +150,7 @@ __global__ void __launch_bounds__(256) mlp2_fwd_kernel(Mlp2Args a) {
   // ---- 2. W1 block -> LDS transposed (w1t[n][k]), zero the K padding
 #pragma unroll
   for (int t = 0; t < WCH; ++t) {
-    const int idx = tid + t * 256;
+    const int idx = tid + t * NT;
     if (idx < K_IN * 2) {
       const int k = idx >> 1, h = (idx & 1) * 8;
       const unsigned q[4] = {wv[t].x, wv[t].y, wv[t].z, wv[t].w};
@@ -146,13 +161,13 @@ __global__ void __launch_bounds__(256) mlp2_fwd_kernel(Mlp2Args a) {
       }
     }
   }
-  for (int idx = tid; idx < 16 * (KP - K_IN); idx += 256) w1t[(idx / (KP - K_IN)) * LDW + K_IN + idx % (KP - K_IN)] = 0;
+  for (int idx = tid; idx < 16 * (KP - K_IN); idx += NT) w1t[(idx / (KP - K_IN)) * LDW + K_IN + idx % (KP - K_IN)] = 0;
   if (tid < 16 * C) w2s[tid / C][tid % C] = w2v;
   if (tid < 16) b1sh[tid] = b1v;
   __syncthreads();
   STAMP(1);
 
-  // ---- 3. K split over the 4 waves
+  // ---- 3. K split over the 8 waves
   f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {
@@ -176,35 +191,42 @@ __global__ void __launch_bounds__(256) mlp2_fwd_kernel(Mlp2Args a) {
   __syncthreads();
   STAMP(2);
 
-  // ---- 4. bias + silu + dropout; H tile kept in LDS for the logits partials
+  // ---- 4. bias + silu + dropout per 4-row group; H tile kept in LDS
+  if (tid < 8 * 16) {
+    const int g4 = tid >> 4, c = tid & 15, col = j0 + c;
+    const int rowg = r0 + g4 * 4;
+    u32x4 db = {0u, 0u, 0u, 0u};
+    if (a.keep < 1.f && rowg < M) db = dropout_bits(a.seed, doff, dropout_group(0, rowg, col, M, H));
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int idx = tid + q * 256;
-    const int rl = idx >> 4, c = idx & 15, row = r0 + rl, col = j0 + c;
-    float hv = 0.f;
-    if (row < M) {
-      const float v = part[0][rl][c] + part[1][rl][c] + part[2][rl][c] + part[3][rl][c] + b1sh[c];
-      const bf16_t zb = f2bf(v);
-      a.Z1[(long)row * H + col] = zb;
-      hv = act_fwd(ACT_SILU, bf2f(zb));
-      if (a.keep < 1.f)
-        hv = dropout_keep(a.seed, doff, (unsigned long long)row * H + col, a.keep) ? hv / a.keep : 0.f;
-      const bf16_t hb = f2bf(hv);
-      a.H1[(long)row * H + col] = hb;
-      hv = bf2f(hb);
+    for (int e = 0; e < 4; ++e) {
+      const int rl = g4 * 4 + e, row = r0 + rl;
+      float hv = 0.f;
+      if (row < M) {
+        float v = b1sh[c];
+#pragma unroll
+        for (int q = 0; q < NW; ++q) v += part[q][rl][c];
+        const bf16_t zb = f2bf(v);
+        a.Z1[(long)row * H + col] = zb;
+        hv = act_fwd(ACT_SILU, bf2f(zb));
+        if (a.keep < 1.f) hv = keep_word(db, e, a.keep) ? hv / a.keep : 0.f;
+        const bf16_t hb = f2bf(hv);
+        a.H1[(long)row * H + col] = hb;
+        hv = bf2f(hb);
+      }
+      htile[rl][c] = hv;
     }
-    htile[rl][c] = hv;
   }
   __syncthreads();
   STAMP(3);
   float* lg = a.logits + (long)par * M * C;
-  for (int idx = tid; idx < 32 * C; idx += 256) {
-    const int rl = idx / C, c = idx % C, row = r0 + rl;
-    if (row >= M) continue;
-    float s = (blockIdx.y == 0) ? bf2f(a.b2s[c]) : 0.f;
+  if (tid < 32 * C) {
+    const int rl = tid / C, c = tid % C, row = r0 + rl;
+    if (row < M) {
+      float s = (blockIdx.y == 0) ? bf2f(a.b2s[c]) : 0.f;
 #pragma unroll
-    for (int n = 0; n < 16; ++n) s += htile[rl][n] * w2s[n][c];
-    atomicAdd(lg + (long)row * C + c, s);
+      for (int n = 0; n < 16; ++n) s += htile[rl][n] * w2s[n][c];
+      atomicAdd(lg + (long)row * C + c, s);
+    }
   }
   __syncthreads();
   STAMP(4);
@@ -212,31 +234,32 @@ __global__ void __launch_bounds__(256) mlp2_fwd_kernel(Mlp2Args a) {
 
 // ---------------------------------------------------------------------------- backward
 template <int K_IN, int C, int KC>
-__global__ void __launch_bounds__(256) mlp2_bwd_kernel(Mlp2Args a) {
+__global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   constexpr int MPM = 128;                 // max rows per device (fused path)
   constexpr int LDM = MPM + 8;             // padded row (bf16 elements)
-  constexpr int ZE = MPM * 16 / 256;       // Z1/H1 elements per thread
-  constexpr int XE = MPM * (KC / 4) / 256; // float4 X loads per thread
-  static_assert(KC % 4 == 0 && K_IN % 4 == 0, "X chunks are float4");
+  constexpr int XE = MPM * (KC / 4) / NT;  // float4 X loads per thread
+  constexpr int NTILE = KC / 16;           // dW1 output tiles (one per wave)
+  static_assert(KC % 4 == 0 && K_IN % 4 == 0 && NTILE <= NW, "tile plan");
+  static_assert((MPM / 4) * 16 == NT, "one 4-row dropout group per thread");
   __shared__ float dlog[MPM][C + 1];
   __shared__ __attribute__((aligned(16))) bf16_t dzT[16 * LDM];
   __shared__ __attribute__((aligned(16))) bf16_t xT[KC * LDM];
   __shared__ float h1s[MPM][17];
   __shared__ float w2s[16][C];
-  __shared__ float red[2][4];
+  __shared__ float red[2][NW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int M = a.M, H = a.H, Mp = (M + 31) & ~31;
   const int j0 = blockIdx.x * 16, kc0 = blockIdx.y * KC;
   const bool chunk0 = blockIdx.y == 0;
+  STAMP(0);
   const int step = a.step[0], par = step & 1;
   const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
   const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
-  STAMP(0);
-  const AdamK ak = adam_consts(a, step);
   const bf16_t* W2s = par ? a.W2s1 : a.W2s0;
   const float* lg = a.logits + (long)par * M * C;
+  const int rg = tid >> 4, gn = tid & 15;   // this thread's dropout group: rows 4rg..4rg+3, column j0+gn
 
-  // ---- 0. issue all global loads
+  // ---- 0. issue all global loads (incl. the AdamW state of this wave's dW1 tile)
   float lrow[C];
   int lab = 0;
   if (tid < M) {
@@ -244,25 +267,37 @@ __global__ void __launch_bounds__(256) mlp2_bwd_kernel(Mlp2Args a) {
     for (int c = 0; c < C; ++c) lrow[c] = lg[(long)tid * C + c];
     lab = a.labels[tid];
   }
-  bf16_t zv[ZE], hv[ZE];
+  bf16_t zv[4], hv[4];
 #pragma unroll
-  for (int e = 0; e < ZE; ++e) {
-    const int idx = tid + e * 256, m = idx >> 4, n = idx & 15;
+  for (int e = 0; e < 4; ++e) {
+    const int m = rg * 4 + e;
     zv[e] = 0; hv[e] = 0;
     if (m < M) {
-      zv[e] = a.Z1[(long)m * H + j0 + n];
-      if (chunk0) hv[e] = a.H1[(long)m * H + j0 + n];
+      zv[e] = a.Z1[(long)m * H + j0 + gn];
+      if (chunk0) hv[e] = a.H1[(long)m * H + j0 + gn];
     }
   }
   float4 xv[XE];
 #pragma unroll
   for (int e = 0; e < XE; ++e) {
-    const int idx = tid + e * 256, m = idx / (KC / 4), i4 = idx % (KC / 4);
+    const int idx = tid + e * NT, m = idx / (KC / 4), i4 = idx % (KC / 4);
     xv[e] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (m < M && kc0 + 4 * i4 < K_IN) xv[e] = *reinterpret_cast<const float4*>(a.X + (long)m * K_IN + kc0 + 4 * i4);
   }
   float w2v = 0.f;
   if (tid < 16 * C) w2v = bf2f(W2s[(long)(j0 + tid / C) * C + tid % C]);
+  float op[4], om[4], ov[4];
+  const int trow0 = kc0 + w * 16 + (lane >> 4) * 4;   // this lane's 4 dW1 rows (tile = wave)
+  const int tcol = j0 + (lane & 15);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    op[e] = om[e] = ov[e] = 0.f;
+    if (a.fuse_opt && w < NTILE && trow0 + e < K_IN) {
+      const long idx = (long)(trow0 + e) * H + tcol;
+      op[e] = a.pW1[idx]; om[e] = a.mW1[idx]; ov[e] = a.vW1[idx];
+    }
+  }
+  const AdamK ak = adam_consts(a, step);
 
   // ---- 1. CE from the summed logits (rounded like the bf16 Dense output) -> dlogits
   float l_loss = 0.f, l_corr = 0.f;
@@ -290,76 +325,88 @@ __global__ void __launch_bounds__(256) mlp2_bwd_kernel(Mlp2Args a) {
     l_corr = wave_sum(l_corr);
     if (lane == 0) { red[0][w] = l_loss; red[1][w] = l_corr; }
     float* nxt = a.logits + (long)(par ^ 1) * M * C;   // re-arm next step's accumulator
-    for (int i = tid; i < M * C; i += 256) nxt[i] = 0.f;
+    for (int i = tid; i < M * C; i += NT) nxt[i] = 0.f;
   }
   // X chunk -> xT[i][m] (bf16, K(=row)-contiguous for the MFMA fragments)
 #pragma unroll
   for (int e = 0; e < XE; ++e) {
-    const int idx = tid + e * 256, m = idx / (KC / 4), i = 4 * (idx % (KC / 4));
+    const int idx = tid + e * NT, m = idx / (KC / 4), i = 4 * (idx % (KC / 4));
     xT[(i + 0) * LDM + m] = f2bf(xv[e].x);
     xT[(i + 1) * LDM + m] = f2bf(xv[e].y);
     xT[(i + 2) * LDM + m] = f2bf(xv[e].z);
     xT[(i + 3) * LDM + m] = f2bf(xv[e].w);
   }
   __syncthreads();
-
   STAMP(1);
-  // ---- 2. dZ1[:, blk] = (dlogits W2[blk]^T) * silu'(Z1) * mask/keep -> dzT[n][m]; H1 tile -> LDS
+
+  // ---- 2. dZ1 group = (dlogits W2[blk]^T) * silu'(Z1) * mask/keep -> dzT[n][m]; H1 -> LDS
+  {
+    u32x4 db = {0u, 0u, 0u, 0u};
+    if (a.keep < 1.f && rg * 4 < M) db = dropout_bits(a.seed, doff, dropout_group(0, rg * 4, j0 + gn, M, H));
+    unsigned packed[2] = {0u, 0u};
 #pragma unroll
-  for (int e = 0; e < ZE; ++e) {
-    const int idx = tid + e * 256, m = idx >> 4, n = idx & 15;
-    float v = 0.f;
-    if (m < M) {
-      float dh = 0.f;
+    for (int e = 0; e < 4; ++e) {
+      const int m = rg * 4 + e;
+      float v = 0.f;
+      if (m < M) {
+        float dh = 0.f;
 #pragma unroll
-      for (int c = 0; c < C; ++c) dh += dlog[m][c] * w2s[n][c];
-      v = dh * act_grad(ACT_SILU, bf2f(zv[e]));
-      if (a.keep < 1.f)
-        v = dropout_keep(a.seed, doff, (unsigned long long)m * H + j0 + n, a.keep) ? v / a.keep : 0.f;
+        for (int c = 0; c < C; ++c) dh += dlog[m][c] * w2s[gn][c];
+        v = dh * act_grad(ACT_SILU, bf2f(zv[e]));
+        if (a.keep < 1.f) v = keep_word(db, e, a.keep) ? v / a.keep : 0.f;
+      }
+      packed[e >> 1] |= (unsigned)f2bf(v) << (16 * (e & 1));
+      if (chunk0) h1s[m][gn] = bf2f(hv[e]);
     }
-    dzT[n * LDM + m] = f2bf(v);
-    if (chunk0) h1s[m][n] = bf2f(hv[e]);
+    *reinterpret_cast<uint2*>(&dzT[gn * LDM + rg * 4]) = make_uint2(packed[0], packed[1]);
   }
   __syncthreads();
-
   STAMP(2);
-  // ---- 3. dW1[chunk, blk] = X[:, chunk]^T dZ1[:, blk]   (K = rows) on MFMA
-  for (int tile = w; tile < KC / 16; tile += 4) {
+
+  // ---- 3. dW1[chunk, blk] = X[:, chunk]^T dZ1[:, blk]   (K = rows) on MFMA; one tile per wave
+  if (w < NTILE) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int ks = 0; ks < Mp / 32; ++ks) {
       const int kk = ks * 32 + 8 * (lane >> 4);
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(&xT[(tile * 16 + (lane & 15)) * LDM + kk]);
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(&xT[(w * 16 + (lane & 15)) * LDM + kk]);
       const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
       acc = mfma16x16x32(af, bfr, acc);
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int i = kc0 + tile * 16 + (lane >> 4) * 4 + e;
+      const int i = trow0 + e;
       if (i < K_IN) {
-        const long idx = (long)i * H + j0 + (lane & 15);
-        if (a.fuse_opt) a.sW1[idx] = f2bf(adam_elem(a.pW1, a.mW1, a.vW1, idx, acc[e], ak));
+        const long idx = (long)i * H + tcol;
+        if (a.fuse_opt) a.sW1[idx] = f2bf(adam_apply(op[e], om[e], ov[e], acc[e], ak, a.pW1 + idx, a.mW1 + idx, a.vW1 + idx));
         else a.gW1[idx] = acc[e];
       }
     }
   }
-
   __syncthreads();
   STAMP(3);
-  // ---- 4. chunk-0 blocks: db1[blk], dW2[blk, :]; block (0,0): db2 + metrics
+
+  // ---- 4. chunk-0 blocks: dW2[blk, :] and db1[blk] (2 threads per output); block (0,0): db2 + metrics
   if (chunk0) {
     bf16_t* sW2n = par ? a.sW2_0 : a.sW2_1;   // next step's parity buffer
-    for (int idx = tid; idx < 16 * C + 16; idx += 256) {
-      if (idx < 16 * C) {
-        const int n = idx / C, c = idx % C;
-        float s = 0.f;
-        for (int m = 0; m < M; ++m) s += h1s[m][n] * dlog[m][c];
-        const long o = (long)(j0 + n) * C + c;
-        if (a.fuse_opt) sW2n[o] = f2bf(adam_elem(a.pW2, a.mW2, a.vW2, o, s, ak));
-        else a.gW2[o] = s;
-      } else {
-        const int n = idx - 16 * C;
-        float s = 0.f;
-        for (int m = 0; m < M; ++m) s += bf2f(dzT[n * LDM + m]);
+    const int o = tid >> 1, half = tid & 1;
+    const int m0 = half * (M / 2), m1 = half ? M : M / 2;
+    float s = 0.f;
+    if (o < 16 * C) {
+      const int n = o / C, c = o % C;
+      for (int m = m0; m < m1; ++m) s += h1s[m][n] * dlog[m][c];
+    } else if (o < 16 * C + 16) {
+      const int n = o - 16 * C;
+      for (int m = m0; m < m1; ++m) s += bf2f(dzT[n * LDM + m]);
+    }
+    s += __shfl_xor(s, 1, 64);
+    if (half == 0) {
+      if (o < 16 * C) {
+        const int n = o / C, c = o % C;
+        const long g = (long)(j0 + n) * C + c;
+        if (a.fuse_opt) sW2n[g] = f2bf(adam_elem(a.pW2, a.mW2, a.vW2, g, s, ak));
+        else a.gW2[g] = s;
+      } else if (o < 16 * C + 16) {
+        const int n = o - 16 * C;
         if (a.fuse_opt) a.sb1[j0 + n] = f2bf(adam_elem(a.pb1, a.mb1, a.vb1, j0 + n, s, ak));
         else a.gb1[j0 + n] = s;
       }
@@ -373,8 +420,8 @@ __global__ void __launch_bounds__(256) mlp2_bwd_kernel(Mlp2Args a) {
       else a.gb2[tid] = s;
     }
     if (tid == 0) {
-      const float L = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-      const float Cr = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+      float L = 0.f, Cr = 0.f;
+      for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
       if (a.fuse_opt && a.running) {
         a.running[0] += L; a.running[1] += (float)M; a.running[2] += Cr; a.running[3] += (float)M;
       } else if (a.mslot) {
@@ -384,14 +431,12 @@ __global__ void __launch_bounds__(256) mlp2_bwd_kernel(Mlp2Args a) {
   }
   __syncthreads();
   STAMP(4);
-  if (a.fuse_opt) {
+  if (a.fuse_opt && tid == 0) {
     // advance the device step once every workgroup has read it
-    if (tid == 0) {
-      const unsigned t = atomicAdd(a.ticket, 1u);
-      if (t == gridDim.x * gridDim.y - 1) {
-        a.step[0] = step + 1;
-        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+    const unsigned t = atomicAdd(a.ticket, 1u);
+    if (t == gridDim.x * gridDim.y - 1) {
+      a.step[0] = step + 1;
+      __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -407,9 +452,9 @@ JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* str
   if (k_in != 784 || c != 10 || a.H % 16 || a.M <= 0 || a.M > 128) return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (phase == 0) {
-    hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10>), dim3((a.M + 31) / 32, a.H / 16), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10>), dim3((a.M + 31) / 32, a.H / 16), dim3(NT), 0, st, a);
   } else {
-    hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112>), dim3(a.H / 16, 784 / 112), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112>), dim3(a.H / 16, 784 / 112), dim3(NT), 0, st, a);
   }
   return HIP_LAUNCH_CHECK();
 }

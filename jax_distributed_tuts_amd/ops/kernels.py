@@ -55,8 +55,8 @@ _W0, _W1 = np.uint64(0x9E3779B9), np.uint64(0xBB67AE85)
 _MASK32 = np.uint64(0xFFFFFFFF)
 
 
-def philox_uniform(seed: int, offset: int, idx: np.ndarray) -> np.ndarray:
-    """Bit-exact numpy mirror of ``jdt::philox4x32`` (first output word -> U[0,1) with 24 bits)."""
+def philox_uniform(seed: int, offset: int, idx: np.ndarray, word: int | np.ndarray = 0) -> np.ndarray:
+    """Bit-exact numpy mirror of ``jdt::philox4x32``; output word ``word`` -> U[0,1) with 24 bits."""
     idx = idx.astype(np.uint64)
     c0 = idx & _MASK32
     c1 = idx >> np.uint64(32)
@@ -75,12 +75,25 @@ def philox_uniform(seed: int, offset: int, idx: np.ndarray) -> np.ndarray:
             c0, c1, c2, c3 = n0, lo1, n2, lo0
             k0 = (k0 + _W0) & _MASK32
             k1 = (k1 + _W1) & _MASK32
-    return (c0 >> np.uint64(8)).astype(np.float64) * (1.0 / 16777216.0)
+    words = np.stack([c0, c1, c2, c3], 0)
+    word = np.broadcast_to(np.asarray(word, dtype=np.int64), c0.shape)
+    sel = np.take_along_axis(words, word[None], 0)[0]
+    return (sel >> np.uint64(8)).astype(np.float64) * (1.0 / 16777216.0)
 
 
-def dropout_mask(seed: int, offset: int, shape, keep_prob: float, base: int = 0) -> torch.Tensor:
-    n = int(np.prod(shape))
-    u = philox_uniform(seed, offset, np.arange(base, base + n, dtype=np.uint64))
+def dropout_mask(seed: int, offset: int, shape, keep_prob: float) -> torch.Tensor:
+    """Mirror of the kernels' grouped mask (common.h ``dropout_group``): element
+    (z, r, c) of a [Z.., M, N] tensor keeps iff word (r & 3) of
+    philox(seed, (z * ceil(M/4) + r // 4) * N + c, offset) is < keep_prob."""
+    shape = tuple(shape)
+    M, N = shape[-2], shape[-1]
+    Z = int(np.prod(shape[:-2])) if len(shape) > 2 else 1
+    z = np.arange(Z, dtype=np.uint64)[:, None, None]
+    r = np.arange(M, dtype=np.uint64)[None, :, None]
+    c = np.arange(N, dtype=np.uint64)[None, None, :]
+    grp = (z * np.uint64((M + 3) // 4) + (r >> np.uint64(2))) * np.uint64(N) + c
+    word = np.broadcast_to((r & np.uint64(3)).astype(np.int64), grp.shape)
+    u = philox_uniform(seed, offset, grp.reshape(-1), word.reshape(-1))
     return torch.from_numpy(u < keep_prob).reshape(shape)
 
 

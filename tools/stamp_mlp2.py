@@ -27,7 +27,11 @@ NAMES = {0: ["start", "loads+LDS staged", "MFMA+reduce", "epilogue(Z1,H1)", "log
 
 
 def report(kind, st, nwg):
-    st = st[: nwg * 8].view(nwg, 8).double() * 10e-3  # ticks -> us
+    raw = st[: nwg * 8].view(nwg, 8).double()
+    clk = (raw[:, 6] - raw[:, 5]) / (raw[:, 4] - raw[:, 0]) * 100.0  # MHz
+    print(f"    shader clock during the kernel: median {float(clk.median()):.0f} MHz "
+          f"(min {float(clk.min()):.0f}, max {float(clk.max()):.0f})")
+    st = raw * 10e-3  # ticks -> us
     t0 = st[:, 0]
     print(f"--- {['mlp2_fwd', 'mlp2_bwd'][kind]}  ({nwg} WGs)  span first-start->last-end: "
           f"{float(st[:, 4].max() - t0.min()):.2f} us; start skew {float(t0.max() - t0.min()):.2f} us")
@@ -56,8 +60,10 @@ def main():
     L = _lib.lib()
     sa = torch.zeros(4096 * 8, dtype=torch.int64, device=dev)
     sb = torch.zeros(4096 * 8, dtype=torch.int64, device=dev)
-    args0 = copy.copy(eng._args)
-    args1 = copy.copy(eng._args)
+    T = type(eng._args)
+    args0, args1 = T(), T()
+    ctypes.memmove(ctypes.byref(args0), ctypes.byref(eng._args), ctypes.sizeof(T))
+    ctypes.memmove(ctypes.byref(args1), ctypes.byref(eng._args), ctypes.sizeof(T))
     args0.stamps, args1.stamps = sa.data_ptr(), sb.data_ptr()
     s = _lib.stream_ptr()
     for _ in range(a.iters):

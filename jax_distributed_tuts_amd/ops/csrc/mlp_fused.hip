@@ -244,7 +244,8 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   __shared__ float dlog[MPM][C + 1];
   __shared__ __attribute__((aligned(16))) bf16_t dzT[16 * LDM];
   __shared__ __attribute__((aligned(16))) bf16_t xT[KC * LDM];
-  __shared__ float h1s[MPM][17];
+  __shared__ __attribute__((aligned(16))) bf16_t h1T[16 * LDM];    // H1[:, blk]^T   (chunk-0 blocks)
+  __shared__ __attribute__((aligned(16))) bf16_t dlT[16 * LDM];    // dlogits^T, classes padded to 16
   __shared__ float w2s[16][C];
   __shared__ float red[2][NW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -289,14 +290,29 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   float op[4], om[4], ov[4];
   const int trow0 = kc0 + w * 16 + (lane >> 4) * 4;   // this lane's 4 dW1 rows (tile = wave)
   const int tcol = j0 + (lane & 15);
+  // wave NW-1 owns no dW1 tile; in chunk-0 blocks it reduces dW2 / db1 (/ db2) on MFMA,
+  // so it prefetches the AdamW state of those outputs instead
+  const bool aux = chunk0 && w == NW - 1;
+  const int ac = lane & 15;                        // aux: class column
+  float bp[4], bm[4], bv[4], qp = 0.f, qm = 0.f, qv = 0.f;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     op[e] = om[e] = ov[e] = 0.f;
+    bp[e] = bm[e] = bv[e] = 0.f;
     if (a.fuse_opt && w < NTILE && trow0 + e < K_IN) {
       const long idx = (long)(trow0 + e) * H + tcol;
       op[e] = a.pW1[idx]; om[e] = a.mW1[idx]; ov[e] = a.vW1[idx];
     }
+    if (a.fuse_opt && aux) {
+      const int n = (lane >> 4) * 4 + e;
+      if (ac < C) {
+        const long g = (long)(j0 + n) * C + ac;
+        op[e] = a.pW2[g]; om[e] = a.mW2[g]; ov[e] = a.vW2[g];
+      }
+      if (ac == 0) { bp[e] = a.pb1[j0 + n]; bm[e] = a.mb1[j0 + n]; bv[e] = a.vb1[j0 + n]; }
+    }
   }
+  if (a.fuse_opt && aux && lead && lane < C) { qp = a.pb2[lane]; qm = a.mb2[lane]; qv = a.vb2[lane]; }
   const AdamK ak = adam_consts(a, step);
 
   // ---- 1. CE from the summed logits (rounded like the bf16 Dense output) -> dlogits
@@ -316,9 +332,16 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
     l_loss = lse - lrow[lab];
     l_corr = (am == lab) ? 1.f : 0.f;
 #pragma unroll
-    for (int c = 0; c < C; ++c)
-      dlog[tid][c] = round_bf((__expf(lrow[c] - lse) - (c == lab ? 1.f : 0.f)) * a.inv_mb);
+    for (int c = 0; c < C; ++c) {
+      const bf16_t gb = f2bf((__expf(lrow[c] - lse) - (c == lab ? 1.f : 0.f)) * a.inv_mb);
+      dlog[tid][c] = bf2f(gb);
+      dlT[c * LDM + tid] = gb;
+    }
+  } else if (tid < MPM) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) dlT[c * LDM + tid] = 0;
   }
+  for (int idx = tid; idx < (16 - C) * MPM; idx += NT) dlT[(C + idx / MPM) * LDM + idx % MPM] = 0;
   if (tid < 16 * C) w2s[tid / C][tid % C] = w2v;
   if (lead) {
     l_loss = wave_sum(l_loss);
@@ -356,9 +379,11 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
         if (a.keep < 1.f) v = keep_word(db, e, a.keep) ? v / a.keep : 0.f;
       }
       packed[e >> 1] |= (unsigned)f2bf(v) << (16 * (e & 1));
-      if (chunk0) h1s[m][gn] = bf2f(hv[e]);
     }
     *reinterpret_cast<uint2*>(&dzT[gn * LDM + rg * 4]) = make_uint2(packed[0], packed[1]);
+    if (chunk0)
+      *reinterpret_cast<uint2*>(&h1T[gn * LDM + rg * 4]) =
+          make_uint2((unsigned)hv[0] | ((unsigned)hv[1] << 16), (unsigned)hv[2] | ((unsigned)hv[3] << 16));
   }
   __syncthreads();
   STAMP(2);
@@ -381,44 +406,46 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
         else a.gW1[idx] = acc[e];
       }
     }
+  } else if (aux) {
+    // chunk-0 blocks, concurrently with the dW1 tiles:
+    //   dW2[blk, :] = H1[:, blk]^T dlogits ; db1[blk] = dZ1[:, blk]^T 1 ; db2 = 1^T dlogits (block (0,0))
+    bf16x8 ones;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ones[q] = (short)0x3f80;  // bf16 1.0
+    f32x4 aw = {0.f, 0.f, 0.f, 0.f}, ab1 = {0.f, 0.f, 0.f, 0.f}, ab2 = {0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < Mp / 32; ++ks) {
+      const int kk = ks * 32 + 8 * (lane >> 4);
+      const bf16x8 hT = *reinterpret_cast<const bf16x8*>(&h1T[(lane & 15) * LDM + kk]);
+      const bf16x8 dT = *reinterpret_cast<const bf16x8*>(&dlT[(lane & 15) * LDM + kk]);
+      const bf16x8 zT = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
+      aw = mfma16x16x32(hT, dT, aw);
+      ab1 = mfma16x16x32(zT, ones, ab1);
+      if (lead) ab2 = mfma16x16x32(ones, dT, ab2);
+    }
+    bf16_t* sW2n = par ? a.sW2_0 : a.sW2_1;   // next step's parity buffer
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = (lane >> 4) * 4 + e;
+      if (ac < C) {
+        const long g = (long)(j0 + n) * C + ac;
+        if (a.fuse_opt) sW2n[g] = f2bf(adam_apply(op[e], om[e], ov[e], aw[e], ak, a.pW2 + g, a.mW2 + g, a.vW2 + g));
+        else a.gW2[g] = aw[e];
+      }
+      if (ac == 0) {
+        const int j = j0 + n;
+        if (a.fuse_opt) a.sb1[j] = f2bf(adam_apply(bp[e], bm[e], bv[e], ab1[e], ak, a.pb1 + j, a.mb1 + j, a.vb1 + j));
+        else a.gb1[j] = ab1[e];
+      }
+    }
+    if (lead && lane < C) {
+      if (a.fuse_opt) a.sb2[lane] = f2bf(adam_apply(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane));
+      else a.gb2[lane] = ab2[0];
+    }
   }
   __syncthreads();
   STAMP(3);
 
-  // ---- 4. chunk-0 blocks: dW2[blk, :] and db1[blk] (2 threads per output); block (0,0): db2 + metrics
-  if (chunk0) {
-    bf16_t* sW2n = par ? a.sW2_0 : a.sW2_1;   // next step's parity buffer
-    const int o = tid >> 1, half = tid & 1;
-    const int m0 = half * (M / 2), m1 = half ? M : M / 2;
-    float s = 0.f;
-    if (o < 16 * C) {
-      const int n = o / C, c = o % C;
-      for (int m = m0; m < m1; ++m) s += h1s[m][n] * dlog[m][c];
-    } else if (o < 16 * C + 16) {
-      const int n = o - 16 * C;
-      for (int m = m0; m < m1; ++m) s += bf2f(dzT[n * LDM + m]);
-    }
-    s += __shfl_xor(s, 1, 64);
-    if (half == 0) {
-      if (o < 16 * C) {
-        const int n = o / C, c = o % C;
-        const long g = (long)(j0 + n) * C + c;
-        if (a.fuse_opt) sW2n[g] = f2bf(adam_elem(a.pW2, a.mW2, a.vW2, g, s, ak));
-        else a.gW2[g] = s;
-      } else if (o < 16 * C + 16) {
-        const int n = o - 16 * C;
-        if (a.fuse_opt) a.sb1[j0 + n] = f2bf(adam_elem(a.pb1, a.mb1, a.vb1, j0 + n, s, ak));
-        else a.gb1[j0 + n] = s;
-      }
-    }
-  }
   if (lead) {
-    if (tid < C) {
-      float s = 0.f;
-      for (int m = 0; m < M; ++m) s += dlog[m][tid];
-      if (a.fuse_opt) a.sb2[tid] = f2bf(adam_elem(a.pb2, a.mb2, a.vb2, tid, s, ak));
-      else a.gb2[tid] = s;
-    }
     if (tid == 0) {
       float L = 0.f, Cr = 0.f;
       for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }

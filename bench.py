@@ -120,6 +120,8 @@ def main():
     ap.add_argument("--accum", choices=["loop", "fused", "kernel"], default="kernel")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--capture-collectives", action="store_true")
+    ap.add_argument("--steps-per-graph", type=int, default=10,
+                    help="complete training steps recorded per hipGraph (amortises the replay launch)")
     args = ap.parse_args()
 
     dev = D.init()
@@ -139,15 +141,21 @@ def main():
     # collectives/p2p inside FSDP and PP steps stay eager; DP captures its step
     use_graph = on_gpu and not args.no_graph and args.strategy == "dp"
     if use_graph:
-        tr.capture(batch, capture_collectives=args.capture_collectives)
-    for _ in range(max(0, args.warmup - n_eager)):
-        tr.step(batch)
+        tr.capture(batch, capture_collectives=args.capture_collectives, steps_per_graph=args.steps_per_graph)
+
+    def run(n):
+        if hasattr(tr, "run_steps"):
+            tr.run_steps(batch, n)
+        else:
+            for _ in range(n):
+                tr.step(batch)
+
+    run(max(0, args.warmup - n_eager))
     sync()
     D.barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        tr.step(batch)
+    run(args.steps)
     sync()
     D.barrier()
     sync()
@@ -178,7 +186,9 @@ def main():
                "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 5), "higher_is_better": True,
                "scaling": "strong", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (N(0,1) inputs, "
                "uniform int labels; random init)", "config": desc,
-               "details": {"p50_ms": p50, "p90_ms": p90, "hipgraph": use_graph, "samples_per_s":
+               "details": {"p50_ms": p50, "p90_ms": p90, "hipgraph": use_graph,
+                           "steps_per_graph": (tr.multi[0] if getattr(tr, "multi", None) else 1) if use_graph else 0,
+                           "samples_per_s":
                            round(sps * desc["global_batch"], 1), "final_loss": float(m[0] / max(m[1], 1)),
                            "comm": D.backend() or "none"}}
         print(json.dumps(out), flush=True)

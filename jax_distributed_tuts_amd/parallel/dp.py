@@ -142,27 +142,37 @@ class DataParallelTrainer:
         self.update()
 
     # ------------------------------------------------------------------ hipGraph
-    def capture(self, batch: Batch, capture_collectives: bool = False):
+    def capture(self, batch: Batch, capture_collectives: bool = False, steps_per_graph: int = 1):
         """Capture the step into hipGraph(s).  Replays then skip all host work.
         The batch tensors must stay alive and fixed (the reference also reuses
-        one synthetic batch every step, data_paral.py:271-273)."""
+        one synthetic batch every step, data_paral.py:271-273).
+
+        ``steps_per_graph`` > 1 (single graph mode) records that many complete,
+        sequential training steps into one graph -- each with its own forward,
+        backward and optimizer update (the device step counter advances inside
+        the graph, so dropout masks differ per step) -- so one hipGraphLaunch
+        (~10-30 us of host time) is amortised over several ~20 us steps.
+        ``run_steps`` uses it; ``step`` replays the 1-step graph."""
         assert batch.inputs.is_cuda
         self._static = batch
         one_graph = self.world == 1 or capture_collectives
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            # warm up allocations / library on the side stream (not counted as a training step
-            # because grads are zeroed and metrics restored below)
-            pass
-        torch.cuda.current_stream().wait_stream(s)
         if one_graph:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            def body():
                 self.compute(batch)
                 self.sync()
                 self.update_noncounting()
+
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                body()
             self.graph = ("one", g)
+            self.multi = None
+            if steps_per_graph > 1:
+                gm = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gm, pool=g.pool()):
+                    for _ in range(steps_per_graph):
+                        body()
+                self.multi = (steps_per_graph, gm)
         else:
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1):
@@ -186,6 +196,19 @@ class DataParallelTrainer:
     def finalize(self):
         if self.fused is not None:
             self.fused.finalize()
+
+    def run_steps(self, batch: Batch, n: int):
+        """n training steps; with a multi-step graph, n // S replays of it plus
+        single-step replays for the remainder."""
+        multi = getattr(self, "multi", None)
+        if self.graph is not None and multi is not None:
+            S, gm = multi
+            for _ in range(n // S):
+                gm.replay()
+            self.state.step += (n // S) * S
+            n = n % S
+        for _ in range(n):
+            self.step(batch)
 
     def _replay(self):
         kind = self.graph[0]

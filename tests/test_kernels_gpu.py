@@ -331,3 +331,27 @@ def test_fused_mlp_graph_capture():
     d = (res[0][0] - res[1][0]).abs()
     assert float(d.max()) <= 3e-3 and float((d > 1e-5).float().mean()) < 1e-3
     _close(res[1][1], res[0][1], rtol=1e-4, atol=1e-2)
+
+
+def test_multi_step_graph_equals_single_steps():
+    """A hipGraph holding 5 complete training steps == 5 single-step replays."""
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    g = torch.Generator().manual_seed(0)
+    b = Batch(torch.randn(128, 784, generator=g).to(DEV), torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV))
+    res = []
+    for spg in (1, 5):
+        st = init_dp(Classifier(), adamw(1e-3), 69, DEV)
+        tr = DataParallelTrainer(st, None, DPConfig(4, "kernel"))
+        tr.step(b)
+        tr.capture(b, steps_per_graph=spg)
+        tr.run_steps(b, 12)
+        tr.finalize()
+        torch.cuda.synchronize()
+        res.append((st.params.master.clone(), tr.metrics.clone(), int(st.opt_state["count"].item()), st.step))
+    assert res[0][2] == res[1][2] == 13 and res[0][3] == res[1][3] == 13
+    d = (res[0][0] - res[1][0]).abs()
+    assert float(d.max()) <= 3e-3 and float((d > 1e-5).float().mean()) < 1e-3
+    _close(res[1][1], res[0][1], rtol=1e-4, atol=1e-2)

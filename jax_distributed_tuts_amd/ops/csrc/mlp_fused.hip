@@ -59,6 +59,12 @@ struct Mlp2Args {
   float lr, beta1, beta2, eps, wd, gscale;
   float* running;
   unsigned long long* stamps;   // diagnostic: per-workgroup s_memrealtime (100 MHz) at phase ends (null = off)
+  // K-contiguous bf16 operand copies that let both kernels load MFMA fragments
+  // straight from global memory (no LDS transposition on the critical path):
+  bf16_t* W1T;   // [H][ldw1t] = W1^T, written by mlp2_bwd's AdamW epilogue (mode 1); null -> LDS path
+  int ldw1t;     // >= KP (zero-padded K tail)
+  bf16_t* XT;    // [K_IN][ldxt] = X^T (rows of all minibatches), written by mlp2_fwd
+  int ldxt;      // >= Mp, zero-padded sample tail
 };
 
 // Slots 0-4: s_memrealtime at phase ends; slots 5/6: s_memtime (core clock) at
@@ -106,7 +112,11 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   constexpr int LDW = KP + 8;           // padded [n][k] row (bank spread)
   constexpr int WCH = (K_IN * 2 + NT - 1) / NT;  // 16-byte W1 chunks per thread
   constexpr int MAXT = (KS + NW - 1) / NW;       // k-steps per wave
+  constexpr int XTC = 112;                       // X^T features written per hidden block
+  constexpr int LDX = 32 + 8;
+  static_assert(K_IN % XTC == 0 && XTC % 8 == 0, "X^T chunking");
   __shared__ __attribute__((aligned(16))) bf16_t w1t[16 * LDW];
+  __shared__ __attribute__((aligned(16))) bf16_t xts[XTC * LDX];
   __shared__ float part[NW][32][17];
   __shared__ float htile[32][17];
   __shared__ float w2s[16][C];
@@ -120,13 +130,26 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   const bf16_t* W2s = par ? a.W2s1 : a.W2s0;
   const int ks0 = (w * KS) / NW, ks1 = ((w + 1) * KS) / NW;
 
+  const bool direct = a.W1T != nullptr;  // W1^T copy available: B fragments straight from global
+
   // ---- 1. issue all global loads
   u32x4 wv[WCH];
+  bf16x8 bg[MAXT];
+  if (!direct) {
 #pragma unroll
-  for (int t = 0; t < WCH; ++t) {
-    const int idx = tid + t * NT;
-    wv[t] = (u32x4){0u, 0u, 0u, 0u};
-    if (idx < K_IN * 2) wv[t] = *reinterpret_cast<const u32x4*>(a.W1s + (long)(idx >> 1) * H + j0 + (idx & 1) * 8);
+    for (int t = 0; t < WCH; ++t) {
+      const int idx = tid + t * NT;
+      wv[t] = (u32x4){0u, 0u, 0u, 0u};
+      if (idx < K_IN * 2) wv[t] = *reinterpret_cast<const u32x4*>(a.W1s + (long)(idx >> 1) * H + j0 + (idx & 1) * 8);
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t) {
+      bg[t] = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+      if (ks0 + t < ks1)
+        bg[t] = *reinterpret_cast<const bf16x8*>(a.W1T + (long)(j0 + (lane & 15)) * a.ldw1t + (ks0 + t) * 32 +
+                                                 8 * (lane >> 4));
+    }
   }
   float4 xa[MAXT][2][2];
 #pragma unroll
@@ -147,25 +170,52 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   if (tid < 16 * C) w2v = bf2f(W2s[(long)(j0 + tid / C) * C + tid % C]);
   if (tid < 16) b1v = bf2f(a.b1s[j0 + tid]);
 
-  // ---- 2. W1 block -> LDS transposed (w1t[n][k]), zero the K padding
+  // ---- 2. (LDS path) W1 block -> LDS transposed (w1t[n][k]), zero the K padding
+  if (!direct) {
 #pragma unroll
-  for (int t = 0; t < WCH; ++t) {
-    const int idx = tid + t * NT;
-    if (idx < K_IN * 2) {
-      const int k = idx >> 1, h = (idx & 1) * 8;
-      const unsigned q[4] = {wv[t].x, wv[t].y, wv[t].z, wv[t].w};
+    for (int t = 0; t < WCH; ++t) {
+      const int idx = tid + t * NT;
+      if (idx < K_IN * 2) {
+        const int k = idx >> 1, h = (idx & 1) * 8;
+        const unsigned q[4] = {wv[t].x, wv[t].y, wv[t].z, wv[t].w};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        w1t[(h + 2 * e) * LDW + k] = (bf16_t)(q[e] & 0xffff);
-        w1t[(h + 2 * e + 1) * LDW + k] = (bf16_t)(q[e] >> 16);
+        for (int e = 0; e < 4; ++e) {
+          w1t[(h + 2 * e) * LDW + k] = (bf16_t)(q[e] & 0xffff);
+          w1t[(h + 2 * e + 1) * LDW + k] = (bf16_t)(q[e] >> 16);
+        }
+      }
+    }
+    for (int idx = tid; idx < 16 * (KP - K_IN); idx += NT) w1t[(idx / (KP - K_IN)) * LDW + K_IN + idx % (KP - K_IN)] = 0;
+  }
+  if (tid < 16 * C) w2s[tid / C][tid % C] = w2v;
+  if (tid < 16) b1sh[tid] = b1v;
+  // X^T side output for mlp2_bwd: hidden block y < K_IN/XTC writes input features
+  // [y*XTC, (y+1)*XTC) of this row block, transposed through LDS
+  const bool xt_writer = a.XT && blockIdx.y < K_IN / XTC;
+  const int xk0 = blockIdx.y * XTC;
+  if (xt_writer) {
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t) {
+      const int k = (ks0 + t) * 32 + 8 * (lane >> 4);
+      if (ks0 + t < ks1 && k >= xk0 && k < xk0 + XTC) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const int rl = mt * 16 + (lane & 15);
+          const float v8[8] = {xa[t][mt][0].x, xa[t][mt][0].y, xa[t][mt][0].z, xa[t][mt][0].w,
+                               xa[t][mt][1].x, xa[t][mt][1].y, xa[t][mt][1].z, xa[t][mt][1].w};
+#pragma unroll
+          for (int q = 0; q < 8; ++q) xts[(k - xk0 + q) * LDX + rl] = f2bf(v8[q]);
+        }
       }
     }
   }
-  for (int idx = tid; idx < 16 * (KP - K_IN); idx += NT) w1t[(idx / (KP - K_IN)) * LDW + K_IN + idx % (KP - K_IN)] = 0;
-  if (tid < 16 * C) w2s[tid / C][tid % C] = w2v;
-  if (tid < 16) b1sh[tid] = b1v;
   __syncthreads();
   STAMP(1);
+  if (xt_writer && tid < XTC * 4) {
+    const int i = tid >> 2, h = (tid & 3) * 8;
+    *reinterpret_cast<u32x4*>(a.XT + (long)(xk0 + i) * a.ldxt + r0 + h) =
+        *reinterpret_cast<const u32x4*>(&xts[i * LDX + h]);
+  }
 
   // ---- 3. K split over the 8 waves
   f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -173,7 +223,7 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   for (int t = 0; t < MAXT; ++t) {
     if (ks0 + t < ks1) {
       const int k = (ks0 + t) * 32 + 8 * (lane >> 4);
-      const bf16x8 b = *reinterpret_cast<const bf16x8*>(&w1t[(lane & 15) * LDW + k]);
+      const bf16x8 b = direct ? bg[t] : *reinterpret_cast<const bf16x8*>(&w1t[(lane & 15) * LDW + k]);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         const float4 x0 = xa[t][mt][0], x1 = xa[t][mt][1];
@@ -237,13 +287,11 @@ template <int K_IN, int C, int KC>
 __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   constexpr int MPM = 128;                 // max rows per device (fused path)
   constexpr int LDM = MPM + 8;             // padded row (bf16 elements)
-  constexpr int XE = MPM * (KC / 4) / NT;  // float4 X loads per thread
   constexpr int NTILE = KC / 16;           // dW1 output tiles (one per wave)
   static_assert(KC % 4 == 0 && K_IN % 4 == 0 && NTILE <= NW, "tile plan");
   static_assert((MPM / 4) * 16 == NT, "one 4-row dropout group per thread");
   __shared__ float dlog[MPM][C + 1];
   __shared__ __attribute__((aligned(16))) bf16_t dzT[16 * LDM];
-  __shared__ __attribute__((aligned(16))) bf16_t xT[KC * LDM];
   __shared__ __attribute__((aligned(16))) bf16_t h1T[16 * LDM];    // H1[:, blk]^T   (chunk-0 blocks)
   __shared__ __attribute__((aligned(16))) bf16_t dlT[16 * LDM];    // dlogits^T, classes padded to 16
   __shared__ float w2s[16][C];
@@ -278,12 +326,14 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
       if (chunk0) hv[e] = a.H1[(long)m * H + j0 + gn];
     }
   }
-  float4 xv[XE];
+  // A fragments of this wave's dW1 tile straight from X^T (written by mlp2_fwd, zero-padded to Mp)
+  bf16x8 xf[MPM / 32];
 #pragma unroll
-  for (int e = 0; e < XE; ++e) {
-    const int idx = tid + e * NT, m = idx / (KC / 4), i4 = idx % (KC / 4);
-    xv[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (m < M && kc0 + 4 * i4 < K_IN) xv[e] = *reinterpret_cast<const float4*>(a.X + (long)m * K_IN + kc0 + 4 * i4);
+  for (int ks = 0; ks < MPM / 32; ++ks) {
+    xf[ks] = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    if (w < NTILE && ks < Mp / 32)
+      xf[ks] = *reinterpret_cast<const bf16x8*>(a.XT + (long)(kc0 + w * 16 + (lane & 15)) * a.ldxt + ks * 32 +
+                                                8 * (lane >> 4));
   }
   float w2v = 0.f;
   if (tid < 16 * C) w2v = bf2f(W2s[(long)(j0 + tid / C) * C + tid % C]);
@@ -350,15 +400,6 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
     float* nxt = a.logits + (long)(par ^ 1) * M * C;   // re-arm next step's accumulator
     for (int i = tid; i < M * C; i += NT) nxt[i] = 0.f;
   }
-  // X chunk -> xT[i][m] (bf16, K(=row)-contiguous for the MFMA fragments)
-#pragma unroll
-  for (int e = 0; e < XE; ++e) {
-    const int idx = tid + e * NT, m = idx / (KC / 4), i = 4 * (idx % (KC / 4));
-    xT[(i + 0) * LDM + m] = f2bf(xv[e].x);
-    xT[(i + 1) * LDM + m] = f2bf(xv[e].y);
-    xT[(i + 2) * LDM + m] = f2bf(xv[e].z);
-    xT[(i + 3) * LDM + m] = f2bf(xv[e].w);
-  }
   __syncthreads();
   STAMP(1);
 
@@ -391,21 +432,32 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   // ---- 3. dW1[chunk, blk] = X[:, chunk]^T dZ1[:, blk]   (K = rows) on MFMA; one tile per wave
   if (w < NTILE) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int ks = 0; ks < Mp / 32; ++ks) {
-      const int kk = ks * 32 + 8 * (lane >> 4);
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(&xT[(w * 16 + (lane & 15)) * LDM + kk]);
-      const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
-      acc = mfma16x16x32(af, bfr, acc);
+#pragma unroll
+    for (int ks = 0; ks < MPM / 32; ++ks) {
+      if (ks < Mp / 32) {
+        const int kk = ks * 32 + 8 * (lane >> 4);
+        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
+        acc = mfma16x16x32(xf[ks], bfr, acc);
+      }
     }
+    unsigned wt[2] = {0u, 0u};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int i = trow0 + e;
       if (i < K_IN) {
         const long idx = (long)i * H + tcol;
-        if (a.fuse_opt) a.sW1[idx] = f2bf(adam_apply(op[e], om[e], ov[e], acc[e], ak, a.pW1 + idx, a.mW1 + idx, a.vW1 + idx));
-        else a.gW1[idx] = acc[e];
+        if (a.fuse_opt) {
+          const bf16_t pb = f2bf(adam_apply(op[e], om[e], ov[e], acc[e], ak, a.pW1 + idx, a.mW1 + idx, a.vW1 + idx));
+          a.sW1[idx] = pb;
+          wt[e >> 1] |= (unsigned)pb << (16 * (e & 1));
+        } else {
+          a.gW1[idx] = acc[e];
+        }
       }
     }
+    // the lane's 4 rows are 4 consecutive K elements of W1^T: one 8-byte store
+    if (a.fuse_opt && a.W1T && trow0 + 3 < K_IN)
+      *reinterpret_cast<uint2*>(a.W1T + (long)tcol * a.ldw1t + trow0) = make_uint2(wt[0], wt[1]);
   } else if (aux) {
     // chunk-0 blocks, concurrently with the dW1 tiles:
     //   dW2[blk, :] = H1[:, blk]^T dlogits ; db1[blk] = dZ1[:, blk]^T 1 ; db2 = 1^T dlogits (block (0,0))

@@ -35,7 +35,8 @@ class Mlp2Args(ctypes.Structure):
                 ("vW1", c_void_p), ("vb1", c_void_p), ("vW2", c_void_p), ("vb2", c_void_p),
                 ("sW1", c_void_p), ("sb1", c_void_p), ("sW2_0", c_void_p), ("sW2_1", c_void_p), ("sb2", c_void_p),
                 ("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float), ("wd", c_float),
-                ("gscale", c_float), ("running", c_void_p), ("stamps", c_void_p)]
+                ("gscale", c_float), ("running", c_void_p), ("stamps", c_void_p),
+                ("W1T", c_void_p), ("ldw1t", c_int), ("XT", c_void_p), ("ldxt", c_int)]
 
 
 _lib.declare("jdt_mlp2", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_int, c_void_p])
@@ -67,6 +68,14 @@ class FusedMLP2:
         self.W2s1 = P.s("output_dense/kernel").clone()
         self.metrics = metrics
         self.fuse_opt = self.world == 1 and os.environ.get("JDT_FUSED_OPT", "1") == "1"
+        # K-contiguous bf16 operand copies (zero K padding): X^T written by mlp2_fwd for
+        # mlp2_bwd; W1^T written by mlp2_bwd's AdamW epilogue for the next mlp2_fwd
+        self.Mp = (rows + 31) // 32 * 32
+        self.XT = torch.zeros(784, self.Mp, dtype=torch.bfloat16, device=dev)
+        self.W1T = None
+        if self.fuse_opt:
+            self.W1T = torch.zeros(H, 800, dtype=torch.bfloat16, device=dev)
+            self.W1T[:, :784].copy_(P.s("input_dense/kernel").t())
         if _lib.lib().jdt_mlp2_args_size() != ctypes.sizeof(Mlp2Args):
             raise RuntimeError("Mlp2Args layout mismatch")
         self._args = None
@@ -95,6 +104,9 @@ class FusedMLP2:
         a.gW1, a.gb1, a.gW2, a.gb2 = (P.g(n).data_ptr() for n in names)
         a.mslot = P.metrics_slot.data_ptr()
         a.fuse_opt = int(self.fuse_opt)
+        a.XT, a.ldxt = self.XT.data_ptr(), self.Mp
+        if self.W1T is not None:
+            a.W1T, a.ldw1t = self.W1T.data_ptr(), 800
         tx = st.tx
         if self.fuse_opt:
             off = {n: P.offsets[n][0] for n in names}

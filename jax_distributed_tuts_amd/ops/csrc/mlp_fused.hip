@@ -113,10 +113,10 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   constexpr int WCH = (K_IN * 2 + NT - 1) / NT;  // 16-byte W1 chunks per thread
   constexpr int MAXT = (KS + NW - 1) / NW;       // k-steps per wave
   constexpr int XTC = 112;                       // X^T features written per hidden block
-  constexpr int LDX = 32 + 8;
-  static_assert(K_IN % XTC == 0 && XTC % 8 == 0, "X^T chunking");
+  constexpr int LDXS = K_IN + 8;                 // padded row of the X image (bf16)
+  static_assert(K_IN % XTC == 0 && XTC % 8 == 0 && K_IN % 8 == 0, "X^T chunking");
   __shared__ __attribute__((aligned(16))) bf16_t w1t[16 * LDW];
-  __shared__ __attribute__((aligned(16))) bf16_t xts[XTC * LDX];
+  __shared__ __attribute__((aligned(16))) bf16_t xs[32 * LDXS];
   __shared__ float part[NW][32][17];
   __shared__ float htile[32][17];
   __shared__ float w2s[16][C];
@@ -151,20 +151,17 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
                                                  8 * (lane >> 4));
     }
   }
-  float4 xa[MAXT][2][2];
+  // X row block [32][K_IN] fp32: fully coalesced float4 loads (consecutive lanes,
+  // consecutive 16 B), converted to bf16 into a row-major LDS image the MFMA A
+  // fragments are read from (a fragment-shaped global load touches 16 rows/instr).
+  constexpr int XF4 = 32 * K_IN / 4;                 // float4 per row block
+  constexpr int XPT = (XF4 + NT - 1) / NT;           // per thread
+  float4 xv[XPT];
 #pragma unroll
-  for (int t = 0; t < MAXT; ++t) {
-    const int k = (ks0 + t) * 32 + 8 * (lane >> 4);
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      const int row = r0 + mt * 16 + (lane & 15);
-      xa[t][mt][0] = xa[t][mt][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ks0 + t < ks1 && row < M && k < K_IN) {
-        const float4* xp = reinterpret_cast<const float4*>(a.X + (long)row * K_IN + k);
-        xa[t][mt][0] = xp[0];
-        xa[t][mt][1] = xp[1];
-      }
-    }
+  for (int e = 0; e < XPT; ++e) {
+    const int f = tid + e * NT, rl = f / (K_IN / 4), k4 = f % (K_IN / 4);
+    xv[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (f < XF4 && r0 + rl < M) xv[e] = *reinterpret_cast<const float4*>(a.X + (long)(r0 + rl) * K_IN + 4 * k4);
   }
   float w2v = 0.f, b1v = 0.f;
   if (tid < 16 * C) w2v = bf2f(W2s[(long)(j0 + tid / C) * C + tid % C]);
@@ -189,32 +186,26 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   }
   if (tid < 16 * C) w2s[tid / C][tid % C] = w2v;
   if (tid < 16) b1sh[tid] = b1v;
-  // X^T side output for mlp2_bwd: hidden block y < K_IN/XTC writes input features
-  // [y*XTC, (y+1)*XTC) of this row block, transposed through LDS
-  const bool xt_writer = a.XT && blockIdx.y < K_IN / XTC;
-  const int xk0 = blockIdx.y * XTC;
-  if (xt_writer) {
 #pragma unroll
-    for (int t = 0; t < MAXT; ++t) {
-      const int k = (ks0 + t) * 32 + 8 * (lane >> 4);
-      if (ks0 + t < ks1 && k >= xk0 && k < xk0 + XTC) {
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          const int rl = mt * 16 + (lane & 15);
-          const float v8[8] = {xa[t][mt][0].x, xa[t][mt][0].y, xa[t][mt][0].z, xa[t][mt][0].w,
-                               xa[t][mt][1].x, xa[t][mt][1].y, xa[t][mt][1].z, xa[t][mt][1].w};
-#pragma unroll
-          for (int q = 0; q < 8; ++q) xts[(k - xk0 + q) * LDX + rl] = f2bf(v8[q]);
-        }
-      }
-    }
+  for (int e = 0; e < XPT; ++e) {
+    const int f = tid + e * NT, rl = f / (K_IN / 4), k4 = f % (K_IN / 4);
+    if (f < XF4)
+      *reinterpret_cast<uint2*>(&xs[rl * LDXS + 4 * k4]) =
+          make_uint2((unsigned)f2bf(xv[e].x) | ((unsigned)f2bf(xv[e].y) << 16),
+                     (unsigned)f2bf(xv[e].z) | ((unsigned)f2bf(xv[e].w) << 16));
   }
   __syncthreads();
   STAMP(1);
-  if (xt_writer && tid < XTC * 4) {
-    const int i = tid >> 2, h = (tid & 3) * 8;
-    *reinterpret_cast<u32x4*>(a.XT + (long)(xk0 + i) * a.ldxt + r0 + h) =
-        *reinterpret_cast<const u32x4*>(&xts[i * LDX + h]);
+  // X^T side output for mlp2_bwd: hidden block y < K_IN/XTC writes input features
+  // [y*XTC, (y+1)*XTC) of this row block (16-byte stores of 8 consecutive samples)
+  if (a.XT && blockIdx.y < K_IN / XTC && tid < XTC * 4) {
+    const int i = tid >> 2, h = (tid & 3) * 8, xk = blockIdx.y * XTC + i;
+    unsigned q[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      q[e] = (unsigned)xs[(h + 2 * e) * LDXS + xk] | ((unsigned)xs[(h + 2 * e + 1) * LDXS + xk] << 16);
+    u32x4 o; o.x = q[0]; o.y = q[1]; o.z = q[2]; o.w = q[3];
+    *reinterpret_cast<u32x4*>(a.XT + (long)xk * a.ldxt + r0 + h) = o;
   }
 
   // ---- 3. K split over the 8 waves
@@ -226,10 +217,8 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
       const bf16x8 b = direct ? bg[t] : *reinterpret_cast<const bf16x8*>(&w1t[(lane & 15) * LDW + k]);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
-        const float4 x0 = xa[t][mt][0], x1 = xa[t][mt][1];
-        bf16x8 af;
-        af[0] = (short)f2bf(x0.x); af[1] = (short)f2bf(x0.y); af[2] = (short)f2bf(x0.z); af[3] = (short)f2bf(x0.w);
-        af[4] = (short)f2bf(x1.x); af[5] = (short)f2bf(x1.y); af[6] = (short)f2bf(x1.z); af[7] = (short)f2bf(x1.w);
+        bf16x8 af = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+        if (k < K_IN) af = *reinterpret_cast<const bf16x8*>(&xs[(mt * 16 + (lane & 15)) * LDXS + k]);
         acc[mt] = mfma16x16x32(af, b, acc[mt]);
       }
     }

@@ -69,7 +69,7 @@ def build_fsdp(args, dev):
     batch = Batch(batch.inputs.to(dev), batch.labels.to(dev))
     once = args.accum != "loop"
     tr = FSDPTrainer(st, mesh, FSDPConfig(cfg.num_minibatches, cfg.model.min_weight_size, "data", gather_once=once,
-                                          scatter_once=once))
+                                          scatter_once=once, fused_kernels=args.accum == "kernel"))
     desc = {"model": f"tutorial MLP {'-'.join(map(str, model.dims))} (SiLU, dropout 0.1)",
             "global_batch": cfg.data.batch_size, "seq_len": None, "num_minibatches": cfg.num_minibatches,
             "parallelism": f"fsdp{D.world_size()}", "gather_once": once}

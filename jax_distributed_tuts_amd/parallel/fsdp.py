@@ -233,6 +233,7 @@ class FSDPConfig:
     axis: str = "data"
     gather_once: bool = False
     scatter_once: bool = False
+    fused_kernels: bool = False   # classifier: whole-step fused kernels on the gathered buffer (implies *_once)
 
 
 class ShardedFlatParams:
@@ -295,7 +296,7 @@ class ShardedFlatParams:
             for name in self.repl_names:
                 self.full.s(name).copy_(self.local.s(name))
 
-    def scatter_grads(self, accumulate: bool):
+    def scatter_grads(self, accumulate: bool, zero_full: bool = True):
         """full fp32 grads -> reduce-scatter SUM into local grads (X06); replicated
         grads copied into the local tail.  Full grads are zeroed."""
         with named_scope("scatter_grads"):
@@ -311,7 +312,8 @@ class ShardedFlatParams:
                     self.local.g(name).add_(self.full.g(name))
                 else:
                     self.local.g(name).copy_(self.full.g(name))
-            self.full.grad.zero_()
+            if zero_full:
+                self.full.grad.zero_()
 
     def sync_replicated(self):
         """sync_gradients for replicated leaves + synch_metrics: ONE all-reduce of the tail."""
@@ -335,9 +337,37 @@ class FSDPTrainer:
         self.model: MLP = state.apply_fn
         self.metrics = torch.zeros(N_METRIC_SLOTS, dtype=torch.float32, device=self.sp.local.master.device)
         self.world = C.axis_size(mesh, cfg.axis)
+        self.fused = None
+
+    def _fused_step(self, batch: Batch) -> bool:
+        """gather bf16 shards once -> mlp2_fwd/mlp2_bwd on the full buffer (mode 0:
+        plain-stored full grads + metric slots) -> reduce-scatter -> sharded AdamW."""
+        if not self.cfg.fused_kernels:
+            return False
+        sp = self.sp
+        if self.fused is None:
+            from .fused_mlp import FusedMLP2, supported
+
+            if not supported(self.model, batch.size, batch.inputs.device):
+                self.cfg.fused_kernels = False
+                return False
+            self.fused = FusedMLP2(self.state, self.mesh, self.cfg.axis, self.cfg.num_minibatches, batch.size,
+                                   self.metrics, params=sp.full, mslot=sp.local.metrics_slot, fuse_opt=False)
+        sp.gather()
+        self.fused.forward_backward(batch)
+        sp.scatter_grads(accumulate=False, zero_full=False)
+        sp.sync_replicated()
+        self.state.tx.update(sp.local, self.state.opt_state, 1.0 / (self.cfg.num_minibatches * self.world),
+                             zero_grad=False)
+        self.state.step += 1
+        with named_scope("synch_metrics"):
+            K.metrics_fold_(self.metrics, sp.local.metrics_slot)
+        return True
 
     def step(self, batch: Batch):
         """train_step_fsdp (param_sharding.py:343-367)."""
+        if self._fused_step(batch):
+            return
         st, sp, cfg = self.state, self.sp, self.cfg
         rng = R.fold_rng_over_axis(st.rng, self.mesh, cfg.axis)
         seed = rng & 0xFFFFFFFF

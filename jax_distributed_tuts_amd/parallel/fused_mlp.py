@@ -52,8 +52,15 @@ def supported(model, rows: int, device) -> bool:
 
 
 class FusedMLP2:
-    def __init__(self, state, mesh, axis: str, num_minibatches: int, rows: int, metrics: torch.Tensor):
-        P = state.params
+    """``params`` (default ``state.params``) supplies the bf16 shadow the kernels read
+    and the fp32 grad views mode 0 writes -- FSDP passes its gathered full buffer
+    (grads then reduce-scattered), with ``mslot`` its local metric slots."""
+
+    def __init__(self, state, mesh, axis: str, num_minibatches: int, rows: int, metrics: torch.Tensor,
+                 params=None, mslot: Optional[torch.Tensor] = None, fuse_opt: Optional[bool] = None):
+        P = params if params is not None else state.params
+        self.P = P
+        self.mslot = mslot if mslot is not None else P.metrics_slot
         self.state, self.mesh, self.axis = state, mesh, axis
         self.world = C.axis_size(mesh, axis)
         self.n_mb = num_minibatches
@@ -67,7 +74,9 @@ class FusedMLP2:
         # second parity buffer of W2's bf16 shadow (single-GPU fused-optimizer mode)
         self.W2s1 = P.s("output_dense/kernel").clone()
         self.metrics = metrics
-        self.fuse_opt = self.world == 1 and os.environ.get("JDT_FUSED_OPT", "1") == "1"
+        if fuse_opt is None:
+            fuse_opt = self.world == 1 and os.environ.get("JDT_FUSED_OPT", "1") == "1"
+        self.fuse_opt = bool(fuse_opt) and params is None
         # K-contiguous bf16 operand copies (zero K padding): X^T written by mlp2_fwd for
         # mlp2_bwd; W1^T written by mlp2_bwd's AdamW epilogue for the next mlp2_fwd
         self.Mp = (rows + 31) // 32 * 32
@@ -82,7 +91,7 @@ class FusedMLP2:
         self._key = None
 
     def _build_args(self, batch) -> Mlp2Args:
-        st, P = self.state, self.state.params
+        st, P = self.state, self.P
         o = st.opt_state
         a = Mlp2Args()
         a.M, a.H = self.rows, self.model.dims[1]
@@ -102,7 +111,7 @@ class FusedMLP2:
         a.step, a.ticket = o["count"].data_ptr(), o["ticket"].data_ptr()
         names = ["input_dense/kernel", "input_dense/bias", "output_dense/kernel", "output_dense/bias"]
         a.gW1, a.gb1, a.gW2, a.gb2 = (P.g(n).data_ptr() for n in names)
-        a.mslot = P.metrics_slot.data_ptr()
+        a.mslot = self.mslot.data_ptr()
         a.fuse_opt = int(self.fuse_opt)
         a.XT, a.ldxt = self.XT.data_ptr(), self.Mp
         if self.W1T is not None:

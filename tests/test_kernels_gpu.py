@@ -355,3 +355,27 @@ def test_multi_step_graph_equals_single_steps():
     d = (res[0][0] - res[1][0]).abs()
     assert float(d.max()) <= 3e-3 and float((d > 1e-5).float().mean()) < 1e-3
     _close(res[1][1], res[0][1], rtol=1e-4, atol=1e-2)
+
+
+def test_fsdp_fused_kernels_match_generic():
+    """FSDP (world 1) with the fused classifier kernels on the gathered buffer ==
+    FSDP with the generic kernels (gather/scatter once)."""
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    g = torch.Generator().manual_seed(0)
+    b = Batch(torch.randn(128, 784, generator=g).to(DEV), torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV))
+    res = []
+    for fused in (False, True):
+        st = init_fsdp(Classifier(), adamw(1e-3), 69, DEV, None, "data", 16)
+        tr = FSDPTrainer(st, None, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=fused))
+        for _ in range(3):
+            tr.step(b)
+        torch.cuda.synchronize()
+        res.append((st.params.master.clone(), tr.metrics.clone()))
+        if fused:
+            assert tr.fused is not None
+    d = (res[0][0] - res[1][0]).abs()
+    assert float(d.max()) <= 6e-3 and float((d > 1e-4).float().mean()) < 2e-3
+    _close(res[1][1], res[0][1], rtol=1e-3, atol=2e-2)

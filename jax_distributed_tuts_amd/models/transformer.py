@@ -177,7 +177,7 @@ class TransformerLM:
             K.colsum_(dx2, P.g(f"{b}/attn/out/bias"))
             K.gemm(bc.o, dx2, a_layout="km", b_layout="kn", out=P.g(f"{b}/attn/out/kernel"), accumulate=True)
             do = K.gemm(dx2, P.s(f"{b}/attn/out/kernel"), b_layout="nk")
-            dqkv = K.attention_bwd(do, bc.qkv, bc.P, cache.nseq, c.seq_len, c.n_heads)
+            dqkv = K.attention_bwd(do, bc.qkv, bc.P, cache.nseq, c.seq_len, c.n_heads, o=bc.o)
             K.colsum_(dqkv, P.g(f"{b}/attn/qkv/bias"))
             K.gemm(bc.h1, dqkv, a_layout="km", b_layout="kn", out=P.g(f"{b}/attn/qkv/kernel"), accumulate=True)
             dh1 = K.gemm(dqkv, P.s(f"{b}/attn/qkv/kernel"), b_layout="nk")

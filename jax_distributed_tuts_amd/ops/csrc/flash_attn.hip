@@ -1,0 +1,324 @@
+// Fused (flash-style) causal self-attention for the transformer tutorial model,
+// head dim 64, bf16 in/out, fp32 softmax statistics.  q/k/v are read in place
+// from the fused [B*S, 3*H*64] QKV projection; O is written in place into the
+// [B*S, H*64] attention output; nothing of size S x S ever reaches HBM.
+//
+// forward  grid (S/64 query blocks, B*H); 4 waves x 16 query rows.
+//   Per 64-key tile: K (row-major) and V (transposed) staged in LDS,
+//   S = Q K^T on MFMA (Q fragments in registers), online softmax in registers
+//   (row stats reduced over the 16 lanes that share a row), P -> per-wave LDS
+//   tile (bf16) -> O += P V on MFMA.  Saves LSE (of the scaled scores) per row.
+// backward  (1) delta = rowsum(dO * O); (2) grid (S/64 key blocks, B*H), each
+//   wave owns 16 keys: P^T = exp(scale K Q^T - LSE) recomputed per 64-query tile,
+//   dP^T = V dO^T, dS^T = P^T (dP^T - delta), dV += P^T dO, dK += dS^T Q (fp32
+//   accumulators in registers for the whole sweep), dQ += dS K summed across key
+//   blocks with fp32 atomics; (3) dQ fp32 -> bf16 into the QKV-gradient buffer.
+#include "common.h"
+
+namespace jdt {
+
+constexpr int FD = 64;          // head dim
+constexpr int FB = 64;          // query / key tile
+constexpr int FLD = FB + 8;     // padded LDS row (bf16 elements)
+
+__device__ __forceinline__ bf16x8 ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+// stage a [64 rows][64 cols] bf16 tile (global row stride ld) into LDS, row-major
+// and/or transposed; rows >= nrows are zero.
+__device__ __forceinline__ void stage_tile(const bf16_t* g, long ld, int nrows, bf16_t* row_major,
+                                           bf16_t* transposed) {
+  for (int c = threadIdx.x; c < FB * FD / 8; c += 256) {
+    const int r = c >> 3, dc = (c & 7) * 8;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (r < nrows) v = *reinterpret_cast<const u32x4*>(g + (long)r * ld + dc);
+    if (row_major) *reinterpret_cast<u32x4*>(row_major + r * FLD + dc) = v;
+    if (transposed) {
+      const unsigned q[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        transposed[(dc + 2 * j) * FLD + r] = (bf16_t)(q[j] & 0xffff);
+        transposed[(dc + 2 * j + 1) * FLD + r] = (bf16_t)(q[j] >> 16);
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) flash_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+                                                        float* __restrict__ lse, int S, int H, float scale,
+                                                        int causal) {
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[FB * FLD];
+  __shared__ __attribute__((aligned(16))) bf16_t Vt[FD * FLD];
+  __shared__ __attribute__((aligned(16))) bf16_t Ps[4][16 * FLD];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int d = H * FD, ld3 = 3 * d;
+  const int q0 = blockIdx.x * FB, qw = q0 + w * 16;
+  const bf16_t* base = qkv + (long)b * S * ld3;
+
+  bf16x8 qf[2];
+  {
+    const int row = qw + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      qf[ks] = row < S ? ld8(base + (long)row * ld3 + h * FD + ks * 32 + 8 * (lane >> 4))
+                       : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  float m[4], l[4];
+  f32x4 o[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { m[e] = -INFINITY; l[e] = 0.f; }
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) o[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int kend = causal ? min(S, q0 + FB) : S;
+  for (int k0 = 0; k0 < kend; k0 += FB) {
+    __syncthreads();
+    stage_tile(base + (long)k0 * ld3 + d + h * FD, ld3, S - k0, Ks, nullptr);
+    stage_tile(base + (long)k0 * ld3 + 2 * d + h * FD, ld3, S - k0, nullptr, Vt);
+    __syncthreads();
+    // S = Q K^T (16 x 64 per wave)
+    f32x4 s[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      s[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        s[nt] = mfma16x16x32(qf[ks], ld8(&Ks[(nt * 16 + (lane & 15)) * FLD + ks * 32 + 8 * (lane >> 4)]), s[nt]);
+    }
+    // online softmax over this tile (row r = (lane>>4)*4 + e; key column nt*16 + (lane&15))
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int qrow = qw + (lane >> 4) * 4 + e;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int key = k0 + nt * 16 + (lane & 15);
+        float v = s[nt][e] * scale;
+        if (key >= S || (causal && key > qrow)) v = -INFINITY;
+        s[nt][e] = v;
+        mx = fmaxf(mx, v);
+      }
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+      const float mnew = fmaxf(m[e], mx);
+      const float alpha = (mnew == -INFINITY) ? 1.f : __expf(m[e] - mnew);
+      float rs = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const float p = (mnew == -INFINITY) ? 0.f : __expf(s[nt][e] - mnew);
+        s[nt][e] = p;
+        rs += p;
+      }
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) rs += __shfl_xor(rs, off, 64);
+      l[e] = l[e] * alpha + rs;
+      m[e] = mnew;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) o[nt][e] *= alpha;
+    }
+    // P (bf16) -> per-wave LDS tile [row][key] so it can be the A operand of P V
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Ps[w][((lane >> 4) * 4 + e) * FLD + nt * 16 + (lane & 15)] = f2bf(s[nt][e]);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's P writes land before its reads
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 pa = ld8(&Ps[w][(lane & 15) * FLD + ks * 32 + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        o[nt] = mfma16x16x32(pa, ld8(&Vt[(nt * 16 + (lane & 15)) * FLD + ks * 32 + 8 * (lane >> 4)]), o[nt]);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int row = qw + (lane >> 4) * 4 + e;
+    if (row >= S) continue;
+    const float inv = 1.f / l[e];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+      out[((long)b * S + row) * d + h * FD + nt * 16 + (lane & 15)] = f2bf(o[nt][e] * inv);
+    if ((lane & 15) == 0) lse[(long)bh * S + row] = m[e] + __logf(l[e]);
+  }
+}
+
+// delta[bh, q] = sum_d dO[b, q, h, d] * O[b, q, h, d]   (one thread per (row, head))
+__global__ void __launch_bounds__(256) flash_bwd_pre_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ o,
+                                                            float* __restrict__ delta, int B, int S, int H) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * S * H) return;
+  const int h = (int)(i % H);
+  const long bq = i / H;
+  const int b = (int)(bq / S), q = (int)(bq % S);
+  const long off = bq * (long)H * FD + h * FD;
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < FD; c += 8) {
+    const u32x4 a = *reinterpret_cast<const u32x4*>(dout + off + c);
+    const u32x4 v = *reinterpret_cast<const u32x4*>(o + off + c);
+    const unsigned wa[4] = {a.x, a.y, a.z, a.w}, wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      s += bf2f((bf16_t)(wa[j] & 0xffff)) * bf2f((bf16_t)(wv[j] & 0xffff)) +
+           bf2f((bf16_t)(wa[j] >> 16)) * bf2f((bf16_t)(wv[j] >> 16));
+  }
+  delta[((long)b * H + h) * S + q] = s;
+}
+
+__global__ void __launch_bounds__(256) flash_bwd_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
+                                                        const float* __restrict__ lse, const float* __restrict__ delta,
+                                                        bf16_t* __restrict__ dqkv, float* __restrict__ dq_acc, int S,
+                                                        int H, float scale, int causal) {
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[FB * FLD];
+  __shared__ __attribute__((aligned(16))) bf16_t Qt[FD * FLD];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[FB * FLD];
+  __shared__ __attribute__((aligned(16))) bf16_t dOt[FD * FLD];
+  __shared__ __attribute__((aligned(16))) bf16_t Kt[FD * FLD];
+  __shared__ __attribute__((aligned(16))) bf16_t Pw[4][16 * FLD];
+  __shared__ __attribute__((aligned(16))) bf16_t dSw[4][16 * FLD];
+  __shared__ __attribute__((aligned(16))) bf16_t dSq[FB * FLD];   // dS[q][key] for dQ
+  __shared__ float lse_s[FB], delta_s[FB];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int d = H * FD, ld3 = 3 * d;
+  const int k0 = blockIdx.x * FB, kw = k0 + w * 16;
+  const bf16_t* base = qkv + (long)b * S * ld3;
+  const bf16_t* dbase = dout + (long)b * S * d;
+
+  bf16x8 kf[2], vf[2];
+  {
+    const int key = kw + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 32 + 8 * (lane >> 4);
+      kf[ks] = key < S ? ld8(base + (long)key * ld3 + d + h * FD + c) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+      vf[ks] = key < S ? ld8(base + (long)key * ld3 + 2 * d + h * FD + c) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  stage_tile(base + (long)k0 * ld3 + d + h * FD, ld3, S - k0, nullptr, Kt);
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) { dk[nt] = (f32x4){0.f, 0.f, 0.f, 0.f}; dv[nt] = dk[nt]; }
+
+  for (int q0 = causal ? k0 : 0; q0 < S; q0 += FB) {
+    __syncthreads();
+    stage_tile(base + (long)q0 * ld3 + h * FD, ld3, S - q0, Qs, Qt);
+    stage_tile(dbase + (long)q0 * d + h * FD, d, S - q0, dOs, dOt);
+    if (threadIdx.x < FB) {
+      const int q = q0 + threadIdx.x;
+      lse_s[threadIdx.x] = q < S ? lse[(long)bh * S + q] : 0.f;
+      delta_s[threadIdx.x] = q < S ? delta[(long)bh * S + q] : 0.f;
+    }
+    __syncthreads();
+    // S^T = K Q^T, dP^T = V dO^T   (rows: this wave's 16 keys; cols: 64 queries)
+    f32x4 st[4], dpt[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      st[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      dpt[nt] = st[nt];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = (nt * 16 + (lane & 15)) * FLD + ks * 32 + 8 * (lane >> 4);
+        st[nt] = mfma16x16x32(kf[ks], ld8(&Qs[c]), st[nt]);
+        dpt[nt] = mfma16x16x32(vf[ks], ld8(&dOs[c]), dpt[nt]);
+      }
+    }
+    // P^T, dS^T (bf16) -> per-wave LDS [key][q]; dS -> shared [q][key]
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int ql = nt * 16 + (lane & 15), q = q0 + ql;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int kl = (lane >> 4) * 4 + e, key = kw + kl;
+        const bool ok = q < S && key < S && !(causal && key > q);
+        const float p = ok ? __expf(st[nt][e] * scale - lse_s[ql]) : 0.f;
+        const float ds = p * (dpt[nt][e] - delta_s[ql]);
+        Pw[w][kl * FLD + ql] = f2bf(p);
+        const bf16_t dsb = f2bf(ds);
+        dSw[w][kl * FLD + ql] = dsb;
+        dSq[ql * FLD + w * 16 + kl] = dsb;
+      }
+    }
+    __syncthreads();
+    // dV += P^T dO ; dK += dS^T Q   (K-dim = the 64 queries)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ca = (lane & 15) * FLD + ks * 32 + 8 * (lane >> 4);
+      const bf16x8 pa = ld8(&Pw[w][ca]), sa = ld8(&dSw[w][ca]);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int cb = (nt * 16 + (lane & 15)) * FLD + ks * 32 + 8 * (lane >> 4);
+        dv[nt] = mfma16x16x32(pa, ld8(&dOt[cb]), dv[nt]);
+        dk[nt] = mfma16x16x32(sa, ld8(&Qt[cb]), dk[nt]);
+      }
+    }
+    // dQ[q0 + w*16 .. +16][:] += dS K  (K-dim = this block's 64 keys), fp32 atomics across key blocks
+    f32x4 dq[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) dq[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 sa = ld8(&dSq[(w * 16 + (lane & 15)) * FLD + ks * 32 + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        dq[nt] = mfma16x16x32(sa, ld8(&Kt[(nt * 16 + (lane & 15)) * FLD + ks * 32 + 8 * (lane >> 4)]), dq[nt]);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int q = q0 + w * 16 + (lane >> 4) * 4 + e;
+      if (q >= S) continue;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        atomicAdd(dq_acc + ((long)b * S + q) * d + h * FD + nt * 16 + (lane & 15), dq[nt][e] * scale);
+    }
+  }
+  // dK, dV -> the K and V column blocks of dQKV
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int key = kw + (lane >> 4) * 4 + e;
+    if (key >= S) continue;
+    bf16_t* row = dqkv + ((long)b * S + key) * ld3 + h * FD + (lane & 15);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      row[d + nt * 16] = f2bf(dk[nt][e] * scale);
+      row[2 * d + nt * 16] = f2bf(dv[nt][e]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) flash_bwd_post_kernel(const float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv,
+                                                             long T, int d) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= T * d) return;
+  const long t = i / d;
+  const int c = (int)(i % d);
+  dqkv[t * 3 * d + c] = f2bf(dq_acc[i]);
+}
+
+}  // namespace jdt
+using namespace jdt;
+
+JDT_API int jdt_flash_fwd(const void* qkv, void* out, float* lse, int B, int S, int H, float scale, int causal,
+                          void* stream) {
+  dim3 grid((S + FB - 1) / FB, B * H);
+  hipLaunchKernelGGL(flash_fwd_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const bf16_t*>(qkv), static_cast<bf16_t*>(out), lse, S, H, scale, causal);
+  return HIP_LAUNCH_CHECK();
+}
+
+// dq_acc: fp32 [B*S, H*64] zeroed by the caller.
+JDT_API int jdt_flash_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta,
+                          float* dq_acc, void* dqkv, int B, int S, int H, float scale, int causal, void* stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const long rows = (long)B * S * H;
+  hipLaunchKernelGGL(flash_bwd_pre_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
+                     static_cast<const bf16_t*>(dout), static_cast<const bf16_t*>(out), delta, B, S, H);
+  hipLaunchKernelGGL(flash_bwd_kernel, dim3((S + FB - 1) / FB, B * H), dim3(256), 0, st,
+                     static_cast<const bf16_t*>(qkv), static_cast<const bf16_t*>(dout), lse, delta,
+                     static_cast<bf16_t*>(dqkv), dq_acc, S, H, scale, causal);
+  const long n = (long)B * S * H * FD;
+  hipLaunchKernelGGL(flash_bwd_post_kernel, dim3((n + 255) / 256), dim3(256), 0, st, dq_acc,
+                     static_cast<bf16_t*>(dqkv), (long)B * S, H * FD);
+  return HIP_LAUNCH_CHECK();
+}

@@ -391,9 +391,13 @@ def _gemm_raw(*, A, lda, B, ldb, C, ldc, M, N, K, a_trans=False, b_kn=False, a_f
 
 
 # ----------------------------------------------------------------------------- attention
-def attention_fwd(qkv: torch.Tensor, B: int, S: int, H: int, causal: bool = True):
+def attention_fwd(qkv: torch.Tensor, B: int, S: int, H: int, causal: bool = True, impl: Optional[str] = None):
     """qkv [B*S, 3*H*Dh] bf16 (q | k | v column blocks, heads contiguous) ->
-    (o [B*S, H*Dh] bf16, P [B*H, S, S] bf16 saved for backward)."""
+    (o [B*S, H*Dh] bf16, aux saved for backward).
+
+    GPU, Dh = 64: fused flash kernel (csrc/flash_attn.hip), aux = LSE [B*H, S] fp32.
+    ``impl="composed"`` (or other head dims): MFMA GEMM -> softmax kernel -> GEMM,
+    aux = P [B*H, S, S] bf16.  CPU: torch reference, aux = P."""
     T, d3 = qkv.shape
     d = d3 // 3
     Dh = d // H
@@ -408,6 +412,14 @@ def attention_fwd(qkv: torch.Tensor, B: int, S: int, H: int, causal: bool = True
         return o, p.reshape(B * H, S, S)
     assert qkv.is_contiguous()
     dev = qkv.device
+    if Dh == 64 and impl != "composed":
+        # flash-style fused kernel: returns the per-row LSE instead of P
+        o = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
+        lse = torch.empty(B * H, S, dtype=torch.float32, device=dev)
+        rc = _lib.lib().jdt_flash_fwd(_ptr(qkv), _ptr(o), _ptr(lse), B, S, H, float(scale), int(causal),
+                                      _lib.stream_ptr())
+        _lib.check(rc, "jdt_flash_fwd")
+        return o, lse
     Sc = torch.empty(B * H, S, S, dtype=torch.float32, device=dev)
     P = torch.empty(B * H, S, S, dtype=torch.bfloat16, device=dev)
     o = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
@@ -423,14 +435,24 @@ def attention_fwd(qkv: torch.Tensor, B: int, S: int, H: int, causal: bool = True
 
 
 def attention_bwd(do: torch.Tensor, qkv: torch.Tensor, P: torch.Tensor, B: int, S: int, H: int,
-                  dqkv: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Gradient of attention_fwd w.r.t. qkv ([B*S, 3d] bf16)."""
+                  dqkv: Optional[torch.Tensor] = None, o: Optional[torch.Tensor] = None,
+                  causal: bool = True) -> torch.Tensor:
+    """Gradient of attention_fwd w.r.t. qkv ([B*S, 3d] bf16).  ``P`` is attention_fwd's
+    aux: the LSE (flash path; then ``o`` is required) or the probabilities."""
     T, d3 = qkv.shape
     d = d3 // 3
     Dh = d // H
     scale = 1.0 / (Dh ** 0.5)
     if dqkv is None:
         dqkv = torch.empty_like(qkv)
+    if _is_gpu(qkv) and P.dim() == 2:
+        assert o is not None and do.is_contiguous() and o.is_contiguous() and dqkv.is_contiguous()
+        delta = torch.empty(B * H, S, dtype=torch.float32, device=qkv.device)
+        dq_acc = torch.zeros(T, d, dtype=torch.float32, device=qkv.device)
+        rc = _lib.lib().jdt_flash_bwd(_ptr(qkv), _ptr(o), _ptr(do), _ptr(P), _ptr(delta), _ptr(dq_acc), _ptr(dqkv),
+                                      B, S, H, float(scale), int(causal), _lib.stream_ptr())
+        _lib.check(rc, "jdt_flash_bwd")
+        return dqkv
     if not _is_gpu(qkv):
         q, k, v = _bf(qkv.float()).view(B, S, 3, H, Dh).permute(2, 0, 3, 1, 4)
         p = P.float().view(B, H, S, S)

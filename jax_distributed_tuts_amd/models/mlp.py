@@ -20,8 +20,9 @@ its bias grad.  So one minibatch fwd+bwd of the reference classifier is 5
 kernels (2 fwd GEMMs, CE, 2 bwd GEMMs + 1 dW GEMM) with no elementwise passes,
 no grad-accumulation adds (K12) and no mask tensors (K04).
 
-``apply`` additionally exposes the model to torch autograd (``ModelFn``) for the
-``util.accum_grads(loss_fn=...)`` API parity path.
+``backward(..., on_ready=cb)`` reports each layer's params as soon as their
+grads are final, which the DP trainer uses to launch bucketed all-reduces that
+overlap the rest of the backward pass.
 """
 from __future__ import annotations
 
@@ -116,7 +117,7 @@ class MLP:
 
     # ------------------------------------------------------------------ backward
     def backward(self, P: FlatParams, cache: LayerCache, dout: torch.Tensor, *, dout_is_dz: bool = True,
-                 need_dx: bool = False) -> Optional[torch.Tensor]:
+                 need_dx: bool = False, on_ready=None) -> Optional[torch.Tensor]:
         """Accumulate param grads into ``P.grad``; return dx if ``need_dx``.
 
         ``dout`` is the gradient w.r.t. the stack output.  With ``dout_is_dz``
@@ -137,6 +138,8 @@ class MLP:
             h_prev = cache.x if i == 0 else cache.h[i - 1]
             # dW_i += h_prev^T . dz   ([in, out], fp32 accumulate)
             K.gemm(h_prev, dz, a_layout="km", b_layout="kn", out=P.g(f"{n}/kernel"), accumulate=True)
+            if on_ready is not None:  # layer i's kernel and bias grads are final (its bias came with dz)
+                on_ready([f"{n}/kernel", f"{n}/bias"])
             if i > 0:
                 pn = self.names[i - 1]
                 dz_prev = torch.empty(dz.shape[0], self.dims[i], dtype=torch.bfloat16, device=dz.device)
@@ -170,7 +173,7 @@ class Classifier(MLP):
 
 def loss_and_grad(model, P: FlatParams, x: torch.Tensor, labels: torch.Tensor, *, train: bool, seed: int,
                   offset: int, step: Optional[torch.Tensor], grad_scale: Optional[float] = None,
-                  metrics: Optional[torch.Tensor] = None):
+                  metrics: Optional[torch.Tensor] = None, on_ready=None):
     """One minibatch: forward, fused CE(+metrics, +head bias grad), explicit backward
     into P.grad (beta=1).  ``grad_scale`` defaults to 1/#labels (mean loss).
     Works for any model exposing forward/backward/flatten_labels/head_bias_name."""
@@ -182,5 +185,8 @@ def loss_and_grad(model, P: FlatParams, x: torch.Tensor, labels: torch.Tensor, *
     hb = model.head_bias_name
     K.softmax_xent(logits, y, grad_scale=grad_scale, dlogits=dlogits, dbias=P.g(hb) if hb else None,
                    metrics=metrics)
-    model.backward(P, cache, dlogits)
+    if on_ready is not None:
+        model.backward(P, cache, dlogits, on_ready=on_ready)
+    else:
+        model.backward(P, cache, dlogits)
     return logits

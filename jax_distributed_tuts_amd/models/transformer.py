@@ -151,14 +151,16 @@ class TransformerLM:
 
     # ------------------------------------------------------------------ backward
     def backward(self, P: FlatParams, cache: _Cache, dout: torch.Tensor, *, dout_is_dz: bool = True,
-                 need_dx: bool = False) -> Optional[torch.Tensor]:
+                 need_dx: bool = False, on_ready=None) -> Optional[torch.Tensor]:
         c = self.cfg
+        ready = on_ready if on_ready is not None else (lambda names: None)
         if self.has_head:
             # dlogits (CE already added the head bias grad)
             K.gemm(cache.hf, dout, a_layout="km", b_layout="kn", out=P.g("head/kernel"), accumulate=True)
             dhf = K.gemm(dout, P.s("head/kernel"), b_layout="nk")
             dx = K.layernorm_bwd(dhf, cache.xf, cache.mf, cache.rf, P.p("ln_f/scale"), P.g("ln_f/scale"),
                                  P.g("ln_f/bias"))
+            ready(["head/kernel", "head/bias", "ln_f/scale", "ln_f/bias"])
         else:
             dx = dout
         for l, bc in zip(reversed(list(self.layers)), reversed(cache.blocks)):
@@ -183,8 +185,10 @@ class TransformerLM:
             dh1 = K.gemm(dqkv, P.s(f"{b}/attn/qkv/kernel"), b_layout="nk")
             dx = K.layernorm_bwd(dh1, bc.x, bc.m1, bc.r1, P.p(f"{b}/ln1/scale"), P.g(f"{b}/ln1/scale"),
                                  P.g(f"{b}/ln1/bias"), dres=dx2)
+            ready([s.name for s in self.param_specs() if s.name.startswith(b + "/")])
         if self.has_embed:
             K.embed_bwd(dx, cache.inp, P.g("embed/wte"), P.g("embed/wpe"), c.seq_len)
+            ready(["embed/wte", "embed/wpe"])
             return None
         return dx if need_dx else None
 

@@ -68,6 +68,8 @@ class DPConfig:
     num_minibatches: int = 4
     accum: str = "loop"          # "loop" | "fused" | "kernel" (whole-step fused kernels, parallel/fused_mlp.py)
     axis: str = "data"
+    overlap: bool = True         # eager generic path: bucketed all-reduce overlapping the last backward
+    bucket_mb: float = 25.0
 
 
 class DataParallelTrainer:
@@ -84,6 +86,12 @@ class DataParallelTrainer:
         self.graph = None
         self._static = None
         self.fused = None
+        self._capturing = False
+        self.buckets = None
+        if self.world > 1 and cfg.overlap:
+            from ..comm.buckets import GradBuckets
+
+            self.buckets = GradBuckets(P, mesh, cfg.axis, int(cfg.bucket_mb * (1 << 20)))
 
     def _fused_engine(self, batch: Batch):
         if self.cfg.accum != "kernel":
@@ -111,23 +119,32 @@ class DataParallelTrainer:
         n_mb = cfg.num_minibatches
         rows = batch.size
         mb = rows // n_mb
+        # overlap only on the eager path (collectives are never captured into the compute graph)
+        bk = self.buckets if (self.buckets is not None and not self._capturing) else None
+        if bk is not None:
+            bk.begin()
         if cfg.accum == "fused":
             loss_and_grad(self.model, P, batch.inputs, batch.labels, train=True, seed=seed, offset=0,
-                          step=st.step_tensor, grad_scale=1.0 / mb, metrics=P.metrics_slot)
+                          step=st.step_tensor, grad_scale=1.0 / mb, metrics=P.metrics_slot,
+                          on_ready=bk.ready if bk is not None else None)
         else:
             for i in range(n_mb):
+                last = i == n_mb - 1  # grads are final only in the last minibatch's backward
                 loss_and_grad(self.model, P, batch.inputs[i * mb:(i + 1) * mb], batch.labels[i * mb:(i + 1) * mb],
                               train=True, seed=seed, offset=i << 16, step=st.step_tensor, grad_scale=1.0 / mb,
-                              metrics=P.metrics_slot)
+                              metrics=P.metrics_slot, on_ready=bk.ready if (bk is not None and last) else None)
 
     def sync(self):
-        """pmean(grads) + psum(metrics) as ONE SUM all-reduce of the bucket; the
+        """pmean(grads) + psum(metrics) as SUM all-reduce(s) of the flat bucket(s); the
         1/N of the mean is applied by the optimizer."""
         P = self.state.params
         if self.world == 1:
             return
         with named_scope("sync_grads"):
-            C.psum_(P.grad, self.mesh, self.cfg.axis)
+            if self.buckets is not None and self.fused is None and not self._capturing:
+                self.buckets.finish()
+            else:
+                C.psum_(P.grad, self.mesh, self.cfg.axis)
 
     def update(self):
         self.update_noncounting()
@@ -155,6 +172,7 @@ class DataParallelTrainer:
         ``run_steps`` uses it; ``step`` replays the 1-step graph."""
         assert batch.inputs.is_cuda
         self._static = batch
+        self._capturing = True  # from now on the step's collectives are whole-buffer, outside graphs
         one_graph = self.world == 1 or capture_collectives
         if one_graph:
             def body():

@@ -162,3 +162,21 @@ def ckpt(out_dir):
     tr2.step(batch)
     _save(out_dir, "ck", {"ref": ref, "got": tr2.full_params(), "step": st2.step,
                           "count": int(st2.opt_state["count"])})
+
+
+def dp_overlap(out_dir, overlap, bucket_mb):
+    from data_paral import synthetic_batch
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp, shard_batch
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.train_state import adamw
+
+    cfg = dp_config()
+    mesh = Mesh({"data": D.world_size()})
+    st = init_dp(Classifier(dropout_rate=0.0, num_layers=4), adamw(1e-3), 69, "cpu", mesh)
+    batch = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
+    tr = DataParallelTrainer(st, mesh, DPConfig(4, "loop", overlap=overlap, bucket_mb=bucket_mb))
+    nb = len(tr.buckets.ranges) if tr.buckets is not None else 0
+    for _ in range(2):
+        tr.step(batch)
+    _save(out_dir, f"ov{int(overlap)}", {"params": st.params.state_dict(), "metrics": tr.metrics.clone(), "nb": nb})

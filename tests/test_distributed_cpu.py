@@ -193,3 +193,15 @@ def test_checkpoint_resume_fsdp(tmp_path):
         assert o["step"] == 3 and o["count"] == 3
         for k in o["ref"]:
             torch.testing.assert_close(o["got"][k], o["ref"][k], rtol=0, atol=0)
+
+
+def test_bucketed_overlap_equals_single_allreduce(tmp_path):
+    """Async bucketed all-reduce fired from backward(on_ready) == one whole-buffer all-reduce."""
+    spawn(functools.partial(W.dp_overlap, overlap=True, bucket_mb=0.5), 2, str(tmp_path))
+    spawn(functools.partial(W.dp_overlap, overlap=False, bucket_mb=0.5), 2, str(tmp_path))
+    a, b = _load(tmp_path, "ov1", 2), _load(tmp_path, "ov0", 2)
+    assert a[0]["nb"] >= 3  # several buckets for the 4-layer MLP at 0.5 MiB
+    for x, y in zip(a, b):
+        for k in x["params"]:
+            torch.testing.assert_close(x["params"][k], y["params"][k], rtol=0, atol=0)
+        torch.testing.assert_close(x["metrics"], y["metrics"], rtol=0, atol=0)

@@ -359,7 +359,8 @@ def test_multi_step_graph_equals_single_steps():
 
 def test_fsdp_fused_kernels_match_generic():
     """FSDP (world 1) with the fused classifier kernels on the gathered buffer ==
-    FSDP with the generic kernels (gather/scatter once)."""
+    FSDP with the generic kernels (gather/scatter once).  Dropout off: the generic
+    path indexes the dropout stream per minibatch, the fused one per device pass."""
     from jax_distributed_tuts_amd.models.mlp import Classifier
     from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
     from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
@@ -368,7 +369,7 @@ def test_fsdp_fused_kernels_match_generic():
     b = Batch(torch.randn(128, 784, generator=g).to(DEV), torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV))
     res = []
     for fused in (False, True):
-        st = init_fsdp(Classifier(), adamw(1e-3), 69, DEV, None, "data", 16)
+        st = init_fsdp(Classifier(dropout_rate=0.0), adamw(1e-3), 69, DEV, None, "data", 16)
         tr = FSDPTrainer(st, None, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=fused))
         for _ in range(3):
             tr.step(b)

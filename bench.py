@@ -45,7 +45,7 @@ def build_dp(args, dev):
     state = init_dp(model, adamw(cfg.optimizer.learning_rate), cfg.seed, dev, mesh)
     batch = shard_batch(synthetic_batch(cfg, cfg.seed + 1), mesh, "data")
     batch = Batch(batch.inputs.to(dev), batch.labels.to(dev))
-    tr = DataParallelTrainer(state, mesh, DPConfig(cfg.optimizer.num_minibatches, args.accum))
+    tr = DataParallelTrainer(state, mesh, DPConfig(cfg.optimizer.num_minibatches, args.accum, comm=args.comm))
     desc = {"model": f"tutorial MLP {'-'.join(map(str, model.dims))} (SiLU, dropout 0.1)",
             "global_batch": cfg.data.batch_size, "seq_len": None, "num_minibatches": cfg.optimizer.num_minibatches,
             "parallelism": f"dp{D.world_size()}", "accum": args.accum}
@@ -120,6 +120,8 @@ def main():
     ap.add_argument("--accum", choices=["loop", "fused", "kernel"], default="kernel")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--capture-collectives", action="store_true")
+    ap.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto",
+                    help="N>1 DP gradient collective: direct xGMI P2P kernel (fused with AdamW) or RCCL")
     ap.add_argument("--steps-per-graph", type=int, default=10,
                     help="complete training steps recorded per hipGraph (amortises the replay launch)")
     args = ap.parse_args()
@@ -190,7 +192,7 @@ def main():
                            "steps_per_graph": (tr.multi[0] if getattr(tr, "multi", None) else 1) if use_graph else 0,
                            "samples_per_s":
                            round(sps * desc["global_batch"], 1), "final_loss": float(m[0] / max(m[1], 1)),
-                           "comm": D.backend() or "none"}}
+                           "comm": getattr(tr, "comm_backend", None) or D.backend() or "none"}}
         print(json.dumps(out), flush=True)
     D.shutdown()
 

@@ -3,6 +3,8 @@
     python data_paral.py                       # all visible GPUs? no: 1 process = 1 GPU
     torchrun --nproc-per-node 8 data_paral.py  # DP over 8 MI355X, RCCL over xGMI
     python data_paral.py --sim-cpu 8           # 8 gloo CPU ranks (reference's simulated devices)
+    python data_paral.py --accum kernel        # whole-step fused HIP kernels
+    python data_paral.py --profile             # same run under rocprofv3 --pmc (counters + kernel stats)
 
 Schedule as the reference (data_paral.py:271-277): 10 training steps with
 metrics accumulated, then one step on fresh metrics printed under "dp".
@@ -19,6 +21,7 @@ from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, 
 from jax_distributed_tuts_amd.runtime import dist as D
 from jax_distributed_tuts_amd.runtime.dist import Mesh
 from jax_distributed_tuts_amd.runtime.launch import run
+from jax_distributed_tuts_amd.utils.cli import add_common_args, maybe_profile
 from jax_distributed_tuts_amd.utils.config import dp_config
 from jax_distributed_tuts_amd.utils.metrics import print_metrics
 from jax_distributed_tuts_amd.utils.train_state import Batch, adamw, get_num_params
@@ -41,22 +44,22 @@ def main(args):
     state = init_dp(model, adamw(cfg.optimizer.learning_rate), cfg.seed, dev, mesh)
     batch = shard_batch(synthetic_batch(cfg, cfg.seed + 1), mesh, "data")
     batch = Batch(batch.inputs.to(dev), batch.labels.to(dev))
-    trainer = DataParallelTrainer(state, mesh, DPConfig(cfg.optimizer.num_minibatches, args.accum))
+    trainer = DataParallelTrainer(state, mesh, DPConfig(cfg.optimizer.num_minibatches, args.accum, comm=args.comm))
     if D.rank() == 0:
-        print(f"[data_paral] {mesh} params={get_num_params(state)} device={dev}")
+        print(f"[data_paral] {mesh} params={get_num_params(state)} device={dev} comm={trainer.comm_backend}")
     for _ in range(args.steps):
         trainer.step(batch)
     trainer.metrics.zero_()
     trainer.step(batch)
+    trainer.finalize()
     if D.rank() == 0:
         print_metrics(trainer.metrics, "dp")
 
 
 if __name__ == "__main__":
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--sim-cpu", type=int, default=None, help="simulate N devices as gloo CPU ranks")
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--num-layers", type=int, default=2)
-    ap.add_argument("--accum", choices=["loop", "fused"], default="loop")
+    ap = add_common_args(argparse.ArgumentParser(), steps=10)
+    ap.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto",
+                    help="N>1 gradient all-reduce: direct xGMI P2P kernel (+fused AdamW) or RCCL")
     a = ap.parse_args()
+    maybe_profile(a, __file__)
     run(main, a, sim_cpu=a.sim_cpu)

@@ -1,0 +1,422 @@
+// Direct xGMI peer-to-peer collectives for the ranks of one MI355X node
+// (native component N3).
+//
+// Why: the DP step all-reduces one 1.63 MB fp32 bucket (grads + 4 metric
+// scalars, SURVEY X03+X04) while the whole fused compute step is ~20 us.  A
+// ring all-reduce drives one xGMI link per GPU and pays 2(N-1) dependent hops;
+// on a fully connected 8-GPU node every peer has its own link, so the
+// two-shot direct algorithm below moves 2S/N bytes per link with exactly two
+// synchronisation points:
+//
+//   phase 0  stage:  block b copies chunk b of every rank-slice of the local
+//                    input into this rank's IPC buffer  data[par]
+//   barrier A        (per block: "my chunk b is staged")
+//   phase 1  reduce: block b sums chunk b of slice `rank` over all N peers'
+//                    data buffers (all N remote loads in flight, fixed rank
+//                    order, so every rank gets bit-identical sums) -> tmp[par]
+//   barrier B        (per block: "my reduced chunk b is ready")
+//   phase 2  gather: block b reads chunk b of slice q from peer q's tmp for all q
+//                    (in flight together) and writes the output -- or, fused,
+//                    applies AdamW to those elements and folds the metric
+//                    slots into the running metrics (the step's optimizer and
+//                    metrics fold run inside the collective: SURVEY K13/K14)
+//
+// Synchronisation is per block, never grid-wide: block b only touches chunk b
+// of every slice, on every rank, so it only needs block b of the peers.  Flags
+// are monotonically increasing per-block epochs written into the peers'
+// uncached signal pages with system-scope release stores and polled with
+// system-scope acquire loads (which also write back / invalidate L2 so IPC
+// data written by earlier kernels or by the peers is seen).  The data and tmp
+// buffers are double-buffered by epoch parity, so a call may start staging
+// while a slow peer still reads the previous call's buffers -- no trailing
+// barrier.  Every spin has a wall-clock timeout (s_memrealtime, 100 MHz): a
+// dead or desynchronised peer sets an error flag instead of hanging the GPU.
+//
+// Reduce-scatter (phases 0-1, result to the caller's shard) and all-gather
+// (stage own shard, barrier, phase 2) reuse the same machinery for FSDP
+// (SURVEY X05/X06).
+#include "common.h"
+
+#include <cstring>
+
+namespace jdt {
+
+constexpr int XG_MAX_RANKS = 8;
+constexpr int XG_MAX_BLOCKS = 96;
+constexpr int XG_THREADS = 256;
+
+struct XgSignal {
+  unsigned flag[2][XG_MAX_BLOCKS][XG_MAX_RANKS];  // [barrier][block][src rank], written by the peers
+  unsigned epoch[XG_MAX_BLOCKS];                   // calls completed by each local block
+  int err;                                         // 1 = a barrier timed out
+};
+
+struct XgPeers {
+  float* data[XG_MAX_RANKS];  // 2 halves of cap floats each (epoch parity)
+  float* tmp[XG_MAX_RANKS];
+  XgSignal* sig[XG_MAX_RANKS];
+};
+
+struct XgAdam {  // fused AdamW + metrics fold over the reduced buffer (phase 2)
+  float* p;
+  float* m;
+  float* v;
+  bf16_t* shadow;
+  long n_params;   // AdamW range [0, n_params), multiple of 4
+  float* running;  // running[j] += reduced[n_params + j], j < n_metrics
+  int n_metrics;
+  float lr, b1, b2, eps, wd, grad_scale;
+  int* step;
+  unsigned* ticket;
+  float* zero;     // zero these indices of this buffer after reading (the grad bucket) or null
+};
+
+enum { XG_ALLREDUCE = 0, XG_REDUCE_SCATTER = 1, XG_ALL_GATHER = 2 };
+
+__device__ __forceinline__ unsigned long long xg_now() { return __builtin_amdgcn_s_memrealtime(); }
+
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+// Per-block barrier across the W ranks.  Thread q < W signals peer q and waits for
+// peer q's signal.  The release store is preceded by a system-scope fence in
+// every thread so the block's staged data is visible to the peers.
+__device__ void xg_barrier(const XgPeers& P, int rank, int W, int which, unsigned epoch, long long timeout) {
+  __threadfence_system();
+  __syncthreads();
+  const int b = blockIdx.x;
+  if (threadIdx.x < W) {
+    const int q = threadIdx.x;
+    __hip_atomic_store(&P.sig[q]->flag[which][b][rank], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    XgSignal* me = P.sig[rank];
+    const unsigned long long t0 = xg_now();
+    while ((int)(__hip_atomic_load(&me->flag[which][b][q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      if ((long long)(xg_now() - t0) > timeout) {
+        __hip_atomic_store(&me->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale peer lines past this point
+}
+
+__device__ __forceinline__ float4 load_guard(const float* src, long e, long n) {
+  if (e + 3 < n) return *reinterpret_cast<const float4*>(src + e);
+  float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < n) x.x = src[e];
+  if (e + 1 < n) x.y = src[e + 1];
+  if (e + 2 < n) x.z = src[e + 2];
+  return x;
+}
+
+__device__ __forceinline__ void store_guard(float* dst, long e, long n, float4 x) {
+  if (e + 3 < n) { *reinterpret_cast<float4*>(dst + e) = x; return; }
+  if (e < n) dst[e] = x.x;
+  if (e + 1 < n) dst[e + 1] = x.y;
+  if (e + 2 < n) dst[e + 2] = x.z;
+}
+
+__device__ __forceinline__ void adam4(const XgAdam& A, long e, float4 g, float rbc1, float rbc2) {
+  float4 pp = *reinterpret_cast<float4*>(A.p + e);
+  float4 mm = *reinterpret_cast<float4*>(A.m + e);
+  float4 vv = *reinterpret_cast<float4*>(A.v + e);
+  float* pe = &pp.x; float* me = &mm.x; float* ve = &vv.x; const float* ge = &g.x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float gr = ge[k] * A.grad_scale;
+    me[k] = A.b1 * me[k] + (1.f - A.b1) * gr;
+    ve[k] = A.b2 * ve[k] + (1.f - A.b2) * gr * gr;
+    pe[k] -= A.lr * ((me[k] * rbc1) / (sqrtf(ve[k] * rbc2) + A.eps) + A.wd * pe[k]);
+  }
+  *reinterpret_cast<float4*>(A.p + e) = pp;
+  *reinterpret_cast<float4*>(A.m + e) = mm;
+  *reinterpret_cast<float4*>(A.v + e) = vv;
+  if (A.shadow) {
+    uint2 s;
+    s.x = (unsigned)f2bf(pp.x) | ((unsigned)f2bf(pp.y) << 16);
+    s.y = (unsigned)f2bf(pp.z) | ((unsigned)f2bf(pp.w) << 16);
+    *reinterpret_cast<uint2*>(A.shadow + e) = s;
+  }
+}
+
+// Caller layout: rank q's part of the full vector is [q*s, q*s + s) (s % 4 == 0),
+// valid up to n.  Kernel layout in the IPC buffers: [q*slice, q*slice + s) with
+// slice = G * chunk >= s, block b owning positions [b*chunk, (b+1)*chunk).
+// ALLREDUCE:      in[n] -> out[n] (or fused AdamW + metrics fold)
+// REDUCE_SCATTER: in[n] -> out[0, s) = reduced part `rank`
+// ALL_GATHER:     in[0, s) = part `rank` -> out[n]
+template <int W, int OP>
+__global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, long cap, const float* in, float* out,
+                                                        long n, long s, long slice,
+                                                        long chunk, XgAdam A, int fuse, long long timeout) {
+  __shared__ unsigned s_epoch;
+  const int b = blockIdx.x;
+  XgSignal* me = P.sig[rank];
+  if (threadIdx.x == 0) s_epoch = me->epoch[b] + 1u;
+  __syncthreads();
+  const unsigned epoch = s_epoch;
+  const long half = (long)(epoch & 1u) * cap;
+  const long base = (long)b * chunk;
+  const int nv = (int)(chunk >> 2);
+  const long own_n = (n - rank * s < s) ? n - rank * s : s;  // valid length of this rank's part
+
+  if (OP != XG_ALL_GATHER) {
+    // phase 0: stage chunk b of every part of the local input
+    float* dst = P.data[rank] + half;
+    for (int q = 0; q < W; ++q) {
+      for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
+        const long j = base + 4 * i;
+        const float4 x = j < s ? load_guard(in, q * s + j, n) : make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(dst + q * slice + j) = x;
+      }
+    }
+    xg_barrier(P, rank, W, 0, epoch, timeout);
+    // phase 1: reduce chunk b of part `rank` over the peers (all W loads in flight)
+    for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
+      const long j = base + 4 * i;
+      const long e = rank * slice + j;
+      float4 v[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q) v[q] = *reinterpret_cast<const float4*>(P.data[q] + half + e);
+      float4 acc = v[0];
+#pragma unroll
+      for (int q = 1; q < W; ++q) acc = add4(acc, v[q]);
+      if (OP == XG_REDUCE_SCATTER) store_guard(out, j, own_n, acc);
+      else *reinterpret_cast<float4*>(P.tmp[rank] + half + e) = acc;
+    }
+    if (OP == XG_REDUCE_SCATTER) {
+      if (threadIdx.x == 0) me->epoch[b] = epoch;
+      return;
+    }
+  } else {
+    // all-gather phase 0: stage chunk b of this rank's part into its tmp slice
+    for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
+      const long j = base + 4 * i;
+      const float4 x = j < s ? load_guard(in, j, own_n) : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(P.tmp[rank] + half + rank * slice + j) = x;
+    }
+  }
+  xg_barrier(P, rank, W, 1, epoch, timeout);
+
+  // phase 2: gather chunk b of every part (all W loads in flight per thread)
+  float rbc1 = 1.f, rbc2 = 1.f;
+  if (fuse) {
+    const int t = A.step[0] + 1;
+    rbc1 = 1.f / (1.f - powf(A.b1, (float)t));
+    rbc2 = 1.f / (1.f - powf(A.b2, (float)t));
+  }
+  for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
+    const long j = base + 4 * i;
+    if (j >= s) break;
+    float4 r[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) r[q] = *reinterpret_cast<const float4*>(P.tmp[q] + half + q * slice + j);
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const long e = q * s + j;
+      if (!fuse) {
+        store_guard(out, e, n, r[q]);
+      } else if (e < n) {
+        if (e < A.n_params) {
+          adam4(A, e, r[q], rbc1, rbc2);
+        } else {
+          const float* rv = &r[q].x;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const long mj = e + k - A.n_params;
+            if (mj < A.n_metrics && e + k < n) A.running[mj] += rv[k];
+          }
+        }
+        if (A.zero) store_guard(A.zero, e, n, make_float4(0.f, 0.f, 0.f, 0.f));
+      }
+    }
+  }
+  if (threadIdx.x == 0) me->epoch[b] = epoch;
+  if (fuse && A.step) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned t = atomicAdd(A.ticket, 1u);
+      if (t == gridDim.x - 1) {
+        A.step[0] = A.step[0] + 1;
+        __hip_atomic_store(A.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+struct XgCtx {
+  int rank = 0, world = 1;
+  long cap = 0;  // floats per parity half
+  float* data = nullptr;
+  float* tmp = nullptr;
+  XgSignal* sig = nullptr;
+  XgPeers peers{};
+  bool opened = false;
+};
+
+static void xg_geometry(long s, long* G_out, long* chunk_out) {
+  long G = (s + 4 * XG_THREADS - 1) / (4 * XG_THREADS);
+  if (G < 8) G = 8;
+  if (G > XG_MAX_BLOCKS) G = XG_MAX_BLOCKS;
+  *G_out = G;
+  *chunk_out = (((s + G - 1) / G) + 3) / 4 * 4;
+}
+
+template <int OP>
+static int xg_launch(XgCtx* c, const float* in, float* out, long n, long s, const XgAdam* A, long long timeout,
+                     hipStream_t st) {
+  const int W = c->world;
+  if (s <= 0 || (s & 3) || n > s * W) return -2;
+  long G, chunk;
+  xg_geometry(s, &G, &chunk);
+  const long slice = chunk * G;
+  if (slice * W > c->cap) return -3;
+  XgAdam a{};
+  int fuse = 0;
+  if (A) { a = *A; fuse = 1; }
+#define XG_CASE(w)                                                                                              \
+  case w:                                                                                                       \
+    hipLaunchKernelGGL((xg_kernel<w, OP>), dim3(G), dim3(XG_THREADS), 0, st, c->peers, c->rank, c->cap, in, out, \
+                       n, s, slice, chunk, a, fuse, timeout);                                                   \
+    break;
+  switch (W) {
+    XG_CASE(2)
+    XG_CASE(3)
+    XG_CASE(4)
+    XG_CASE(5)
+    XG_CASE(6)
+    XG_CASE(7)
+    XG_CASE(8)
+    default:
+      return -4;
+  }
+#undef XG_CASE
+  return HIP_LAUNCH_CHECK();
+}
+
+}  // namespace jdt
+using namespace jdt;
+
+// Allocate this rank's IPC buffers (data, tmp: 2 x cap floats each; signal page)
+// and export their handles (3 x 64 bytes) for the peers.
+JDT_API int jdt_xgmi_create(int rank, int world, long cap_floats, void** ctx_out, void* handles_out) {
+  if (world < 2 || world > XG_MAX_RANKS || rank < 0 || rank >= world) return -4;
+  XgCtx* c = new XgCtx();
+  c->rank = rank;
+  c->world = world;
+  c->cap = (cap_floats + 4 * (long)XG_MAX_BLOCKS * world + 63) / 64 * 64;
+  hipIpcMemHandle_t h[3];
+  if (hipMalloc(&c->data, 2 * c->cap * sizeof(float)) != hipSuccess) goto fail;
+  if (hipMalloc(&c->tmp, 2 * c->cap * sizeof(float)) != hipSuccess) goto fail;
+  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->sig), sizeof(XgSignal), hipDeviceMallocUncached) !=
+      hipSuccess)
+    goto fail;
+  if (hipMemset(c->sig, 0, sizeof(XgSignal)) != hipSuccess) goto fail;
+  if (hipMemset(c->data, 0, 2 * c->cap * sizeof(float)) != hipSuccess) goto fail;
+  if (hipMemset(c->tmp, 0, 2 * c->cap * sizeof(float)) != hipSuccess) goto fail;
+  if (hipDeviceSynchronize() != hipSuccess) goto fail;
+  if (hipIpcGetMemHandle(&h[0], c->data) != hipSuccess) goto fail;
+  if (hipIpcGetMemHandle(&h[1], c->tmp) != hipSuccess) goto fail;
+  if (hipIpcGetMemHandle(&h[2], c->sig) != hipSuccess) goto fail;
+  static_assert(sizeof(hipIpcMemHandle_t) == 64, "ipc handle size");
+  std::memcpy(handles_out, h, sizeof(h));
+  *ctx_out = c;
+  return 0;
+fail:
+  (void)hipGetLastError();
+  if (c->data) (void)hipFree(c->data);
+  if (c->tmp) (void)hipFree(c->tmp);
+  if (c->sig) (void)hipFree(c->sig);
+  delete c;
+  return -1;
+}
+
+// Map every peer's buffers (all_handles: world x 3 x 64 bytes, rank-major).
+JDT_API int jdt_xgmi_open(void* ctx, const void* all_handles) {
+  XgCtx* c = static_cast<XgCtx*>(ctx);
+  const hipIpcMemHandle_t* h = static_cast<const hipIpcMemHandle_t*>(all_handles);
+  for (int q = 0; q < c->world; ++q) {
+    if (q == c->rank) {
+      c->peers.data[q] = c->data;
+      c->peers.tmp[q] = c->tmp;
+      c->peers.sig[q] = c->sig;
+      continue;
+    }
+    void* p[3] = {nullptr, nullptr, nullptr};
+    for (int k = 0; k < 3; ++k) {
+      if (hipIpcOpenMemHandle(&p[k], h[3 * q + k], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+        (void)hipGetLastError();
+        return -(10 + q);
+      }
+    }
+    c->peers.data[q] = static_cast<float*>(p[0]);
+    c->peers.tmp[q] = static_cast<float*>(p[1]);
+    c->peers.sig[q] = static_cast<XgSignal*>(p[2]);
+  }
+  c->opened = true;
+  return 0;
+}
+
+JDT_API int jdt_xgmi_allreduce(void* ctx, const float* in, float* out, long n, const XgAdam* adam, long long timeout,
+                               void* stream) {
+  XgCtx* c = static_cast<XgCtx*>(ctx);
+  if (!c->opened) return -5;
+  if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) return -2;
+  if (adam && ((adam->n_params & 3) || !adam->step || !adam->ticket)) return -2;
+  const long part = ((n + c->world - 1) / c->world + 3) / 4 * 4;
+  return xg_launch<XG_ALLREDUCE>(c, in, out, n, part, adam, timeout, static_cast<hipStream_t>(stream));
+}
+
+// Part length s (multiple of 4, n <= world*s): out[0, s) receives the sum of
+// elements [rank*s, rank*s + s) (valid up to n).
+JDT_API int jdt_xgmi_reduce_scatter(void* ctx, const float* in, float* out, long n, long s, long long timeout,
+                                    void* stream) {
+  XgCtx* c = static_cast<XgCtx*>(ctx);
+  if (!c->opened) return -5;
+  if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) return -2;
+  return xg_launch<XG_REDUCE_SCATTER>(c, in, out, n, s, nullptr, timeout, static_cast<hipStream_t>(stream));
+}
+
+// in[0, s) of every rank -> out[q*s + j] (valid up to n).
+JDT_API int jdt_xgmi_all_gather(void* ctx, const float* in, float* out, long n, long s, long long timeout,
+                                void* stream) {
+  XgCtx* c = static_cast<XgCtx*>(ctx);
+  if (!c->opened) return -5;
+  if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) return -2;
+  return xg_launch<XG_ALL_GATHER>(c, in, out, n, s, nullptr, timeout, static_cast<hipStream_t>(stream));
+}
+
+JDT_API int jdt_xgmi_adam_size() { return (int)sizeof(XgAdam); }
+
+JDT_API long jdt_xgmi_capacity(void* ctx) { return static_cast<XgCtx*>(ctx)->cap; }
+
+// 1 if any barrier of this rank timed out (synchronises the device).
+JDT_API int jdt_xgmi_error(void* ctx) {
+  XgCtx* c = static_cast<XgCtx*>(ctx);
+  int e = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpy(&e, &c->sig->err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return e;
+}
+
+JDT_API int jdt_xgmi_destroy(void* ctx) {
+  XgCtx* c = static_cast<XgCtx*>(ctx);
+  if (!c) return 0;
+  (void)hipDeviceSynchronize();
+  if (c->opened) {
+    for (int q = 0; q < c->world; ++q) {
+      if (q == c->rank) continue;
+      if (c->peers.data[q]) (void)hipIpcCloseMemHandle(c->peers.data[q]);
+      if (c->peers.tmp[q]) (void)hipIpcCloseMemHandle(c->peers.tmp[q]);
+      if (c->peers.sig[q]) (void)hipIpcCloseMemHandle(c->peers.sig[q]);
+    }
+  }
+  (void)hipFree(c->data);
+  (void)hipFree(c->tmp);
+  (void)hipFree(c->sig);
+  delete c;
+  return 0;
+}

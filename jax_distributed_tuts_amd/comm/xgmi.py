@@ -1,0 +1,254 @@
+"""Direct xGMI peer-to-peer collectives (comm/csrc/xgmi.hip) for one node.
+
+``XgmiComm(mesh, axis, cap_floats)`` gives the ranks of one mesh axis a
+private set of IPC-shared device buffers (exported with hipIpcGetMemHandle,
+exchanged once over the process group, mapped with hipIpcOpenMemHandle), then
+runs the collectives as ordinary kernels on the current stream:
+
+* ``all_reduce_(t)``      -- SUM in place (two-shot: direct reduce-scatter +
+                             direct all-gather, every peer on its own link);
+* ``all_reduce_adamw_()`` -- the same all-reduce whose gather phase applies
+                             AdamW to the parameters and folds the metric slots
+                             (the whole DP "sync_grads + apply_gradients +
+                             sync_metrics" tail, data_paral.py:206-236, in ONE
+                             kernel);
+* ``reduce_scatter`` / ``all_gather`` -- tiled along a flat dim-0 layout
+                             (FSDP X05/X06).
+
+Being kernels rather than RCCL calls, they are captured into hipGraphs with
+the rest of the step, so a multi-GPU step is a single graph replay.
+
+Construction runs a self-test on the real hardware (exact small-integer sums
+through every phase and both buffer parities) and all ranks agree on the
+outcome; ``comm.ok`` is False (and the trainers fall back to RCCL) if the IPC
+mapping or the self-test fails on any rank.  Every in-kernel wait has a
+timeout, so a dead peer turns into an error flag (``error()``) instead of a
+hung GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import logging
+import os
+from ctypes import c_float, c_int, c_long, c_longlong, c_void_p
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _lib
+
+log = logging.getLogger(__name__)
+
+HANDLE_BYTES = 64
+TICKS_PER_S = 100_000_000  # s_memrealtime
+
+
+class XgAdam(ctypes.Structure):
+    """Mirror of ``jdt::XgAdam`` (comm/csrc/xgmi.hip)."""
+
+    _fields_ = [
+        ("p", c_void_p), ("m", c_void_p), ("v", c_void_p), ("shadow", c_void_p),
+        ("n_params", c_long), ("running", c_void_p), ("n_metrics", c_int),
+        ("lr", c_float), ("b1", c_float), ("b2", c_float), ("eps", c_float), ("wd", c_float),
+        ("grad_scale", c_float), ("step", c_void_p), ("ticket", c_void_p), ("zero", c_void_p),
+    ]
+
+
+_lib.declare("jdt_xgmi_create", c_int, [c_int, c_int, c_long, ctypes.POINTER(c_void_p), c_void_p])
+_lib.declare("jdt_xgmi_open", c_int, [c_void_p, c_void_p])
+_lib.declare("jdt_xgmi_allreduce", c_int, [c_void_p, c_void_p, c_void_p, c_long, ctypes.POINTER(XgAdam), c_longlong,
+                                           c_void_p])
+_lib.declare("jdt_xgmi_reduce_scatter", c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_longlong, c_void_p])
+_lib.declare("jdt_xgmi_all_gather", c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_longlong, c_void_p])
+_lib.declare("jdt_xgmi_capacity", c_long, [c_void_p])
+_lib.declare("jdt_xgmi_adam_size", c_int, [])
+_lib.declare("jdt_xgmi_error", c_int, [c_void_p])
+_lib.declare("jdt_xgmi_destroy", c_int, [c_void_p])
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return c_void_p(t.data_ptr()) if t is not None else c_void_p(0)
+
+
+def part_len(n: int, world: int) -> int:
+    """Per-rank part of an n-float all-reduce (multiple of 4 floats)."""
+    return ((n + world - 1) // world + 3) // 4 * 4
+
+
+def requested(mode: str, world: int, device: torch.device) -> bool:
+    """Whether a trainer should try the xGMI path: ``mode`` in {"auto","xgmi","rccl"}
+    (env ``JDT_COMM`` overrides "auto")."""
+    if mode == "auto":
+        mode = os.environ.get("JDT_COMM", "auto")
+    if mode == "rccl" or world < 2 or world > 8 or device.type != "cuda":
+        return False
+    return True
+
+
+class XgmiComm:
+    def __init__(self, group, rank: int, world: int, cap_floats: int, device: torch.device,
+                 timeout_s: float = 30.0, self_test: bool = True):
+        self.group, self.rank, self.world, self.device = group, rank, world, device
+        self.timeout = c_longlong(int(timeout_s * TICKS_PER_S))
+        self.ctx = c_void_p()
+        self.ok = False
+        L = _lib.lib()
+        if L.jdt_xgmi_adam_size() != ctypes.sizeof(XgAdam):
+            raise RuntimeError("XgAdam layout mismatch between Python and comm/csrc/xgmi.hip")
+        h = (ctypes.c_char * (3 * HANDLE_BYTES))()
+        with torch.cuda.device(device):
+            rc = L.jdt_xgmi_create(rank, world, int(cap_floats), ctypes.byref(self.ctx), h)
+        mine = bytes(h) if rc == 0 else None
+        objs = [None] * world
+        dist.all_gather_object(objs, mine, group=group)
+        good = all(o is not None for o in objs)
+        if good:
+            allh = b"".join(objs)
+            buf = ctypes.create_string_buffer(allh, len(allh))
+            with torch.cuda.device(device):
+                rc = L.jdt_xgmi_open(self.ctx, buf)
+            good = rc == 0
+            if not good:
+                log.warning("xgmi: hipIpcOpenMemHandle failed on rank %d (rc %d)", rank, rc)
+        else:
+            log.warning("xgmi: buffer export failed on some rank (rank %d rc %d)", rank, rc)
+        good = self._agree(good)
+        if good and self_test:
+            good = self._agree(self._self_test())
+        self.ok = good
+        if not good:
+            self.close()
+
+    # ------------------------------------------------------------------ plumbing
+    def _agree(self, ok: bool) -> bool:
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                         device=self.device if dist.get_backend(self.group) == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(int(t.item()))
+
+    @property
+    def capacity(self) -> int:
+        return int(_lib.lib().jdt_xgmi_capacity(self.ctx)) if self.ctx else 0
+
+    def error(self) -> int:
+        """1 if any in-kernel barrier timed out on this rank (synchronises the device)."""
+        return int(_lib.lib().jdt_xgmi_error(self.ctx)) if self.ctx else 0
+
+    def close(self):
+        if self.ctx:
+            _lib.lib().jdt_xgmi_destroy(self.ctx)
+            self.ctx = c_void_p()
+        self.ok = False
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _check_f32(t: torch.Tensor):
+        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous() or t.data_ptr() % 16:
+            raise ValueError("xgmi collectives take contiguous, 16-byte aligned fp32 CUDA tensors")
+
+    # ------------------------------------------------------------------ collectives
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        self._check_f32(t)
+        rc = _lib.lib().jdt_xgmi_allreduce(self.ctx, _ptr(t), _ptr(t), t.numel(), None, self.timeout,
+                                           c_void_p(_lib.stream_ptr()))
+        _lib.check(rc, "jdt_xgmi_allreduce")
+        return t
+
+    def all_reduce_adamw_(self, grad: torch.Tensor, *, p: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
+                          shadow: Optional[torch.Tensor], n_params: int, running: Optional[torch.Tensor],
+                          n_metrics: int, lr: float, b1: float, b2: float, eps: float, wd: float,
+                          grad_scale: float, step: torch.Tensor, ticket: torch.Tensor, zero_grad: bool = True):
+        """SUM-all-reduce ``grad`` and, in the same kernel, AdamW on ``p[:n_params]``
+        (grads scaled by ``grad_scale``: the 1/(n_mb*N) mean) and
+        ``running[j] += grad_sum[n_params + j]`` for the metric slots."""
+        self._check_f32(grad)
+        a = XgAdam()
+        a.p, a.m, a.v, a.shadow = _ptr(p), _ptr(m), _ptr(v), _ptr(shadow)
+        a.n_params, a.running, a.n_metrics = int(n_params), _ptr(running), int(n_metrics if running is not None else 0)
+        a.lr, a.b1, a.b2, a.eps, a.wd, a.grad_scale = float(lr), float(b1), float(b2), float(eps), float(wd), float(grad_scale)
+        a.step, a.ticket = _ptr(step), _ptr(ticket)
+        a.zero = _ptr(grad) if zero_grad else c_void_p(0)
+        rc = _lib.lib().jdt_xgmi_allreduce(self.ctx, _ptr(grad), c_void_p(0), grad.numel(), ctypes.byref(a),
+                                           self.timeout, c_void_p(_lib.stream_ptr()))
+        _lib.check(rc, "jdt_xgmi_allreduce(adamw)")
+
+    def reduce_scatter(self, full: torch.Tensor, out: torch.Tensor, part: int) -> torch.Tensor:
+        """out[0:part] = sum over ranks of full[rank*part : (rank+1)*part] (valid to full.numel())."""
+        self._check_f32(full)
+        self._check_f32(out)
+        rc = _lib.lib().jdt_xgmi_reduce_scatter(self.ctx, _ptr(full), _ptr(out), full.numel(), int(part),
+                                                self.timeout, c_void_p(_lib.stream_ptr()))
+        _lib.check(rc, "jdt_xgmi_reduce_scatter")
+        return out
+
+    def all_gather(self, part_t: torch.Tensor, out: torch.Tensor, part: int) -> torch.Tensor:
+        """out[q*part : (q+1)*part] = rank q's part_t (valid to out.numel())."""
+        self._check_f32(part_t)
+        self._check_f32(out)
+        rc = _lib.lib().jdt_xgmi_all_gather(self.ctx, _ptr(part_t), _ptr(out), out.numel(), int(part),
+                                            self.timeout, c_void_p(_lib.stream_ptr()))
+        _lib.check(rc, "jdt_xgmi_all_gather")
+        return out
+
+    # ------------------------------------------------------------------ self-test
+    def _self_test(self) -> bool:
+        """Exact-integer checks of AR (both parities), RS and AG on this hardware."""
+        try:
+            W, r, dev = self.world, self.rank, self.device
+            with torch.cuda.device(dev):
+                n = min(self.capacity // 2, 300_001)
+                base = (torch.arange(n, device=dev, dtype=torch.int64) % 97).to(torch.float32)
+                want = base * W + W * (W - 1) / 2
+                for it in range(3):
+                    x = base + r + it
+                    self.all_reduce_(x)
+                    if not torch.equal(x, want + W * it):
+                        log.warning("xgmi self-test: all-reduce mismatch (iter %d)", it)
+                        return False
+                part = part_len(n, W)
+                out = torch.empty(part, device=dev)
+                self.reduce_scatter(base + r, out, part)
+                lo, hi = r * part, min(n, (r + 1) * part)
+                if not torch.equal(out[: hi - lo], want[lo:hi]):
+                    log.warning("xgmi self-test: reduce-scatter mismatch")
+                    return False
+                full = torch.empty(n, device=dev)
+                mine = torch.zeros(part, device=dev)
+                mine[: hi - lo] = base[lo:hi] + 1000 * r
+                self.all_gather(mine, full, part)
+                exp = base.clone()
+                for q in range(W):
+                    exp[q * part: min(n, (q + 1) * part)] += 1000 * q
+                if not torch.equal(full, exp):
+                    log.warning("xgmi self-test: all-gather mismatch")
+                    return False
+                torch.cuda.synchronize(dev)
+                if self.error():
+                    log.warning("xgmi self-test: barrier timeout")
+                    return False
+            return True
+        except Exception as e:  # a launch error must not leave the other ranks waiting
+            log.warning("xgmi self-test raised: %s", e)
+            return False
+
+
+def create_for(mesh, axis: str, cap_floats: int, device: torch.device, mode: str = "auto") -> Optional[XgmiComm]:
+    """An ``XgmiComm`` over ``mesh``'s ``axis`` group, or None (RCCL fallback)."""
+    from ..runtime.dist import is_initialized
+
+    n = mesh.axis_size(axis) if mesh is not None else 1
+    if mesh is None or not is_initialized() or not requested(mode, n, device):
+        return None
+    c = XgmiComm(mesh.group(axis), mesh.axis_index(axis), n, cap_floats, device)
+    if not c.ok:
+        if mode == "xgmi":
+            raise RuntimeError("xgmi collectives requested but unavailable on this node")
+        log.warning("xgmi collectives unavailable; using RCCL")
+        return None
+    return c

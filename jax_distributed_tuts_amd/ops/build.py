@@ -1,6 +1,6 @@
 """In-tree build of the gfx950 kernel library (``ops/lib/libjdt_kernels.so``).
 
-Every ``csrc/*.hip`` (and ``*.cpp``) file is compiled with
+Every ``csrc/*.hip`` (and ``*.cpp``) file, plus ``comm/csrc/*.hip``, is compiled with
 ``hipcc --offload-arch=gfx950 -O3`` into an object and linked into one shared
 library.  No PyTorch headers are involved: the kernels expose plain
 ``extern "C"`` launchers that take raw device pointers plus a ``hipStream_t``,
@@ -22,6 +22,7 @@ from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
+COMM_CSRC = HERE.parent / "comm" / "csrc"   # xGMI P2P collectives, linked into the same library
 LIBDIR = HERE / "lib"
 OBJDIR = LIBDIR / "obj"
 LIB = LIBDIR / "libjdt_kernels.so"
@@ -36,7 +37,7 @@ def _hipcc() -> str:
 
 
 def sources() -> list[Path]:
-    return sorted(list(CSRC.glob("*.hip")) + list(CSRC.glob("*.cpp")))
+    return sorted(list(CSRC.glob("*.hip")) + list(CSRC.glob("*.cpp")) + list(COMM_CSRC.glob("*.hip")))
 
 
 def _headers_mtime() -> float:

@@ -70,6 +70,7 @@ class DPConfig:
     axis: str = "data"
     overlap: bool = True         # eager generic path: bucketed all-reduce overlapping the last backward
     bucket_mb: float = 25.0
+    comm: str = "auto"           # "auto" | "xgmi" | "rccl": N>1 gradient collective (comm/xgmi.py)
 
 
 class DataParallelTrainer:
@@ -88,7 +89,15 @@ class DataParallelTrainer:
         self.fused = None
         self._capturing = False
         self.buckets = None
-        if self.world > 1 and cfg.overlap:
+        self.xg = None
+        self._xg_fused_opt = False
+        if self.world > 1 and P.grad.is_cuda:
+            from ..comm.xgmi import create_for
+
+            # one kernel = all-reduce of [grads || metrics] + AdamW + metrics fold
+            self.xg = create_for(mesh, cfg.axis, P.grad.numel(), P.grad.device, cfg.comm)
+            self._xg_fused_opt = self.xg is not None and isinstance(state.tx, AdamW)
+        if self.world > 1 and cfg.overlap and self.xg is None:
             from ..comm.buckets import GradBuckets
 
             self.buckets = GradBuckets(P, mesh, cfg.axis, int(cfg.bucket_mb * (1 << 20)))
@@ -141,7 +150,17 @@ class DataParallelTrainer:
         if self.world == 1:
             return
         with named_scope("sync_grads"):
-            if self.buckets is not None and self.fused is None and not self._capturing:
+            if self.xg is not None:
+                if self._xg_fused_opt:
+                    tx, st = self.state.tx, self.state.opt_state
+                    self.xg.all_reduce_adamw_(
+                        P.grad, p=P.master, m=st["m"], v=st["v"], shadow=P.shadow, n_params=P.numel,
+                        running=self.metrics, n_metrics=N_METRIC_SLOTS, lr=tx.learning_rate, b1=tx.b1, b2=tx.b2,
+                        eps=tx.eps, wd=tx.weight_decay, grad_scale=1.0 / (self.cfg.num_minibatches * self.world),
+                        step=st["count"], ticket=st["ticket"], zero_grad=True)
+                else:
+                    self.xg.all_reduce_(P.grad)
+            elif self.buckets is not None and self.fused is None and not self._capturing:
                 self.buckets.finish()
             else:
                 C.psum_(P.grad, self.mesh, self.cfg.axis)
@@ -173,7 +192,7 @@ class DataParallelTrainer:
         assert batch.inputs.is_cuda
         self._static = batch
         self._capturing = True  # from now on the step's collectives are whole-buffer, outside graphs
-        one_graph = self.world == 1 or capture_collectives
+        one_graph = self.world == 1 or capture_collectives or self.xg is not None  # xGMI collectives are kernels
         if one_graph:
             def body():
                 self.compute(batch)
@@ -201,6 +220,8 @@ class DataParallelTrainer:
 
     def update_noncounting(self):
         P = self.state.params
+        if self._xg_fused_opt:
+            return  # AdamW + metrics fold ran inside the xGMI all-reduce kernel (sync)
         if self.fused is not None:
             if self.fused.fuse_opt:
                 return  # AdamW + metrics already applied inside mlp2_bwd
@@ -214,6 +235,19 @@ class DataParallelTrainer:
     def finalize(self):
         if self.fused is not None:
             self.fused.finalize()
+        if self.xg is not None and self.xg.error():
+            raise RuntimeError("xgmi collective timed out on this rank (peer dead or desynchronised)")
+
+    @property
+    def comm_backend(self) -> str:
+        if self.world == 1:
+            return "none"
+        if self.xg is not None:
+            return "xgmi"
+        from ..runtime.dist import backend
+
+        b = backend()
+        return "rccl" if b == "nccl" else (b or "none")
 
     def run_steps(self, batch: Batch, n: int):
         """n training steps; with a multi-step graph, n // S replays of it plus

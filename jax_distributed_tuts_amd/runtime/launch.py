@@ -25,12 +25,14 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def _child(local_rank: int, world: int, port: int, fn: Callable, args: tuple, env: dict):
+def _child(local_rank: int, world: int, port: int, fn: Callable, args: tuple, env: dict, gpu: bool = False):
     os.environ.update(env)
     os.environ.update({"RANK": str(local_rank), "LOCAL_RANK": str(local_rank), "WORLD_SIZE": str(world),
-                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "JDT_SIM_CPU": str(world)})
-    os.environ["HIP_VISIBLE_DEVICES"] = ""
-    os.environ["CUDA_VISIBLE_DEVICES"] = ""
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    if not gpu:
+        os.environ["JDT_SIM_CPU"] = str(world)
+        os.environ["HIP_VISIBLE_DEVICES"] = ""
+        os.environ["CUDA_VISIBLE_DEVICES"] = ""
     try:
         D.init(backend="gloo")
         fn(*args)
@@ -44,10 +46,14 @@ def _child(local_rank: int, world: int, port: int, fn: Callable, args: tuple, en
         D.shutdown()
 
 
-def spawn(fn: Callable, world: int, *args: Any, env: dict | None = None):
-    """Run ``fn(*args)`` on ``world`` gloo CPU ranks (blocking)."""
+def spawn(fn: Callable, world: int, *args: Any, env: dict | None = None, gpu: bool = False):
+    """Run ``fn(*args)`` on ``world`` gloo ranks (blocking).  With ``gpu=True`` the
+    ranks keep the GPUs (rank r on device r % device_count -- on a one-GPU box all
+    ranks share cuda:0, which rehearses the multi-process GPU paths such as the
+    xGMI IPC collectives; the process group stays gloo since RCCL refuses two
+    ranks on one device)."""
     port = free_port()
-    mp.start_processes(_child, args=(world, port, fn, args, dict(env or {})), nprocs=world, join=True,
+    mp.start_processes(_child, args=(world, port, fn, args, dict(env or {}), gpu), nprocs=world, join=True,
                        start_method="spawn")
 
 

@@ -1,0 +1,66 @@
+"""Command-line plumbing shared by the entry scripts.
+
+``--profile [COUNTERS]`` re-runs the same command as a *child* of
+``rocprofv3 --pmc COUNTERS --kernel-trace --stats`` (counters only with the
+kernel trace; never combined with the runtime/HIP/HSA/marker trace domains) and
+exits with its status.  It happens before anything touches the GPU: the
+profiler's preloaded library initialises the device itself, so the parent must
+not have.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import subprocess
+import sys
+
+DEFAULT_COUNTERS = "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS"
+
+
+def add_common_args(ap: argparse.ArgumentParser, steps: int, accum_default: str = "loop",
+                    accum_choices=("loop", "fused", "kernel")):
+    ap.add_argument("--sim-cpu", type=int, default=None, help="simulate N devices as gloo CPU ranks")
+    ap.add_argument("--steps", type=int, default=steps)
+    ap.add_argument("--num-layers", type=int, default=2)
+    ap.add_argument("--accum", choices=list(accum_choices), default=accum_default,
+                    help="loop: per-minibatch kernels (reference semantics); fused: all rows in one pass; "
+                         "kernel: whole-step fused HIP kernels")
+    ap.add_argument("--profile", nargs="?", const=DEFAULT_COUNTERS, default=None, metavar="COUNTERS",
+                    help="run under rocprofv3 --pmc (PMC counters + kernel stats)")
+    ap.add_argument("--profile-dir", default="gpurun_out/profile")
+    return ap
+
+
+def _strip_profile(argv):
+    """argv without --profile [COUNTERS] / --profile-dir DIR (and their = forms)."""
+    out, i = [], 0
+    while i < len(argv):
+        a = argv[i]
+        if a == "--profile":
+            i += 2 if i + 1 < len(argv) and not argv[i + 1].startswith("-") else 1
+        elif a == "--profile-dir":
+            i += 2
+        elif a.startswith("--profile=") or a.startswith("--profile-dir="):
+            i += 1
+        else:
+            out.append(a)
+            i += 1
+    return out
+
+
+def profile_cmd(script: str, argv, counters: str, outdir: str):
+    return (["rocprofv3", "--pmc", *counters.split(), "--kernel-trace", "--stats", "--output-format", "csv",
+             "-d", os.path.abspath(outdir), "-o", "run", "--", sys.executable, os.path.abspath(script)]
+            + _strip_profile(list(argv)))
+
+
+def maybe_profile(args, script: str):
+    """If ``--profile`` was given (and we are not already the profiled child), run
+    this script under rocprofv3 as a child process and exit with its code."""
+    if not getattr(args, "profile", None) or os.environ.get("JDT_PROFILED") == "1":
+        return
+    cmd = profile_cmd(script, sys.argv[1:], args.profile, args.profile_dir)
+    os.makedirs(args.profile_dir, exist_ok=True)
+    env = dict(os.environ, JDT_PROFILED="1", TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    print("[profile] " + " ".join(cmd), file=sys.stderr, flush=True)
+    sys.exit(subprocess.call(cmd, env=env))

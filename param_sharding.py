@@ -22,6 +22,7 @@ from jax_distributed_tuts_amd.runtime import dist as D
 from jax_distributed_tuts_amd.runtime.dist import Mesh
 from jax_distributed_tuts_amd.runtime.launch import run
 from jax_distributed_tuts_amd.utils.config import fsdp_config
+from jax_distributed_tuts_amd.utils.cli import add_common_args, maybe_profile
 from jax_distributed_tuts_amd.utils.metrics import print_metrics
 from jax_distributed_tuts_amd.utils.train_state import Batch, adamw, get_num_params
 
@@ -37,7 +38,9 @@ def main(args):
     batch = shard_batch(synthetic_batch(cfg, cfg.seed + 1), mesh, axis)
     batch = Batch(batch.inputs.to(dev), batch.labels.to(dev))
     tr = FSDPTrainer(state, mesh, FSDPConfig(cfg.num_minibatches, cfg.model.min_weight_size, axis,
-                                             gather_once=args.gather_once, scatter_once=args.scatter_once))
+                                             gather_once=args.gather_once or args.accum != "loop",
+                                             scatter_once=args.scatter_once or args.accum != "loop",
+                                             fused_kernels=args.accum == "kernel"))
     if D.rank() == 0:
         sp = state.extra["sharded"]
         print(f"[param_sharding] {mesh} global params={get_num_params(sp)} local flat={sp.local.numel} "
@@ -51,11 +54,9 @@ def main(args):
 
 
 if __name__ == "__main__":
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--sim-cpu", type=int, default=None)
-    ap.add_argument("--steps", type=int, default=15)
-    ap.add_argument("--num-layers", type=int, default=2)
+    ap = add_common_args(argparse.ArgumentParser(), steps=15)
     ap.add_argument("--gather-once", action="store_true")
     ap.add_argument("--scatter-once", action="store_true")
     a = ap.parse_args()
+    maybe_profile(a, __file__)
     run(main, a, sim_cpu=a.sim_cpu)

@@ -23,6 +23,7 @@ from jax_distributed_tuts_amd.runtime import dist as D
 from jax_distributed_tuts_amd.runtime.dist import Mesh
 from jax_distributed_tuts_amd.runtime.launch import run
 from jax_distributed_tuts_amd.utils import rng as R
+from jax_distributed_tuts_amd.utils.cli import add_common_args, maybe_profile
 from jax_distributed_tuts_amd.utils.config import dp_config
 from jax_distributed_tuts_amd.utils.metrics import print_metrics
 from jax_distributed_tuts_amd.utils.train_state import Batch, TrainState, adamw
@@ -71,12 +72,11 @@ def main(args):
 
 
 if __name__ == "__main__":
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--sim-cpu", type=int, default=None)
-    ap.add_argument("--steps", type=int, default=10)
+    ap = add_common_args(argparse.ArgumentParser(), steps=10, accum_choices=("loop",))
     ap.add_argument("--dp", type=int, default=1)
     ap.add_argument("--microbatches", type=int, default=4)
     ap.add_argument("--hidden-layers", type=int, default=8)
     ap.add_argument("--model", choices=["mlp", "transformer"], default="mlp")
     a = ap.parse_args()
+    maybe_profile(a, __file__)
     run(main, a, sim_cpu=a.sim_cpu)

@@ -45,10 +45,20 @@ def _is_gloo(group) -> bool:
     return dist.get_backend(group) == "gloo"
 
 
+def _host(x: torch.Tensor, g) -> torch.Tensor:
+    """gloo works on host memory: GPU tensors (several ranks sharing one GPU in the
+    multi-process GPU tests) are staged through a CPU copy."""
+    return x.cpu() if (x.is_cuda and _is_gloo(g)) else x
+
+
 def psum_(x: torch.Tensor, mesh: Optional[Mesh], axis: str) -> torch.Tensor:
     """In-place SUM all-reduce along ``axis``."""
     if _active(mesh, axis):
-        dist.all_reduce(x, op=dist.ReduceOp.SUM, group=mesh.group(axis))
+        g = mesh.group(axis)
+        h = _host(x, g)
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=g)
+        if h is not x:
+            x.copy_(h)
     return x
 
 
@@ -90,9 +100,10 @@ def all_gather(x: torch.Tensor, mesh: Optional[Mesh], axis: str, dim: int = 0,
 
 
 def _gather_list(x, g, n) -> List[torch.Tensor]:
-    parts = [torch.empty_like(x) for _ in range(n)]
-    dist.all_gather(parts, x, group=g)
-    return parts
+    h = _host(x, g)
+    parts = [torch.empty_like(h) for _ in range(n)]
+    dist.all_gather(parts, h, group=g)
+    return [p.to(x.device) for p in parts] if h is not x else parts
 
 
 def psum_scatter(x: torch.Tensor, mesh: Optional[Mesh], axis: str, dim: int = 0,
@@ -107,8 +118,9 @@ def psum_scatter(x: torch.Tensor, mesh: Optional[Mesh], axis: str, dim: int = 0,
     g = mesh.group(axis)
     idx = mesh.axis_index(axis)
     if dim != 0 or _is_gloo(g):
-        red = x.clone()
+        red = _host(x, g).clone()
         dist.all_reduce(red, group=g)
+        red = red.to(x.device)
         res = red.chunk(n, dim=dim)[idx]
         if out is None:
             return res.contiguous()
@@ -160,5 +172,9 @@ def recv(x: torch.Tensor, mesh: Mesh, axis: str, src_index: int) -> torch.Tensor
 
 def broadcast_(x: torch.Tensor, mesh: Optional[Mesh], axis: str, src_index: int = 0) -> torch.Tensor:
     if _active(mesh, axis):
-        dist.broadcast(x, mesh.global_rank(axis, src_index), group=mesh.group(axis))
+        g = mesh.group(axis)
+        h = _host(x, g)
+        dist.broadcast(h, mesh.global_rank(axis, src_index), group=g)
+        if h is not x:
+            x.copy_(h)
     return x

@@ -247,6 +247,104 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
   }
 }
 
+// ---------------------------------------------------------------------------
+// Segmented all-gather / reduce-scatter: several tensors ("segments", e.g. the
+// dim-0-sharded leaves of an FSDP model) in ONE launch, each gathered straight
+// into / scattered straight out of its own full-tensor layout.  Rank q's part of
+// segment k is full_k[q*s_k, (q+1)*s_k) (words, valid up to nfull_k); in the IPC
+// buffers rank q's parts of all segments are packed at [q*slice + off_k, +s_k).
+// Words are 4 bytes, so bf16 shadow shards and fp32 grads use the same kernel.
+constexpr int XG_MAX_SEGS = 16;
+
+struct XgSeg {
+  float* full;
+  float* part;
+  long s;      // part length (words, multiple of 4)
+  long off;    // packed offset (words, multiple of 4)
+  long nfull;  // valid words of full
+};
+
+struct XgSegs {
+  XgSeg seg[XG_MAX_SEGS];
+  int n;
+  long S;  // sum of s
+};
+
+__device__ __forceinline__ int xg_find(const XgSegs& S, long j) {
+  int k = 0;
+  for (int t = 1; t < S.n; ++t)
+    if (j >= S.seg[t].off) k = t;
+  return k;
+}
+
+template <int W, int OP>
+__global__ void __launch_bounds__(XG_THREADS) xg_seg_kernel(XgPeers P, int rank, long cap, XgSegs S, long slice,
+                                                            long chunk, int accumulate, long long timeout) {
+  __shared__ unsigned s_epoch;
+  const int b = blockIdx.x;
+  XgSignal* me = P.sig[rank];
+  if (threadIdx.x == 0) s_epoch = me->epoch[b] + 1u;
+  __syncthreads();
+  const unsigned epoch = s_epoch;
+  const long half = (long)(epoch & 1u) * cap;
+  const long base = (long)b * chunk;
+  const int nv = (int)(chunk >> 2);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  if (OP == XG_REDUCE_SCATTER) {
+    float* dst = P.data[rank] + half;
+    for (int q = 0; q < W; ++q) {
+      for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
+        const long j = base + 4 * i;
+        float4 x = z4;
+        if (j < S.S) {
+          const XgSeg& g = S.seg[xg_find(S, j)];
+          x = load_guard(g.full, q * g.s + (j - g.off), g.nfull);
+        }
+        *reinterpret_cast<float4*>(dst + q * slice + j) = x;
+      }
+    }
+    xg_barrier(P, rank, W, 0, epoch, timeout);
+    for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
+      const long j = base + 4 * i;
+      if (j >= S.S) break;
+      float4 v[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q) v[q] = *reinterpret_cast<const float4*>(P.data[q] + half + rank * slice + j);
+      float4 acc = v[0];
+#pragma unroll
+      for (int q = 1; q < W; ++q) acc = add4(acc, v[q]);
+      const XgSeg& g = S.seg[xg_find(S, j)];
+      const long lim = (g.nfull - rank * g.s < g.s) ? g.nfull - rank * g.s : g.s;
+      if (accumulate) acc = add4(acc, load_guard(g.part, j - g.off, lim));
+      store_guard(g.part, j - g.off, lim, acc);
+    }
+  } else {
+    for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
+      const long j = base + 4 * i;
+      float4 x = z4;
+      if (j < S.S) {
+        const XgSeg& g = S.seg[xg_find(S, j)];
+        const long lim = (g.nfull - rank * g.s < g.s) ? g.nfull - rank * g.s : g.s;
+        x = load_guard(g.part, j - g.off, lim);
+      }
+      *reinterpret_cast<float4*>(P.tmp[rank] + half + rank * slice + j) = x;
+    }
+    xg_barrier(P, rank, W, 1, epoch, timeout);
+    for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
+      const long j = base + 4 * i;
+      if (j >= S.S) break;
+      float4 r[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q) r[q] = *reinterpret_cast<const float4*>(P.tmp[q] + half + q * slice + j);
+      const XgSeg& g = S.seg[xg_find(S, j)];
+#pragma unroll
+      for (int q = 0; q < W; ++q) store_guard(g.full, q * g.s + (j - g.off), g.nfull, r[q]);
+    }
+  }
+  if (threadIdx.x == 0) me->epoch[b] = epoch;
+}
+
 struct XgCtx {
   int rank = 0, world = 1;
   long cap = 0;  // floats per parity half
@@ -388,6 +486,52 @@ JDT_API int jdt_xgmi_all_gather(void* ctx, const float* in, float* out, long n, 
   if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) return -2;
   return xg_launch<XG_ALL_GATHER>(c, in, out, n, s, nullptr, timeout, static_cast<hipStream_t>(stream));
 }
+
+// Segmented RS (op 1) / AG (op 2) over up to 16 tensors; see XgSegs.
+JDT_API int jdt_xgmi_segments(void* ctx, const XgSegs* segs, int op, int accumulate, long long timeout,
+                              void* stream) {
+  XgCtx* c = static_cast<XgCtx*>(ctx);
+  if (!c->opened) return -5;
+  if (segs->n < 1 || segs->n > XG_MAX_SEGS) return -2;
+  long off = 0;
+  for (int k = 0; k < segs->n; ++k) {
+    const XgSeg& g = segs->seg[k];
+    if ((g.s & 3) || g.off != off || g.nfull > g.s * c->world) return -2;
+    if ((reinterpret_cast<uintptr_t>(g.full) | reinterpret_cast<uintptr_t>(g.part)) & 15) return -2;
+    off += g.s;
+  }
+  if (off != segs->S || off <= 0) return -2;
+  long G, chunk;
+  xg_geometry(off, &G, &chunk);
+  const long slice = chunk * G;
+  if (slice * c->world > c->cap) return -3;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+#define XG_SEG_CASE(w)                                                                                         \
+  case w:                                                                                                      \
+    if (op == XG_REDUCE_SCATTER)                                                                               \
+      hipLaunchKernelGGL((xg_seg_kernel<w, XG_REDUCE_SCATTER>), dim3(G), dim3(XG_THREADS), 0, st, c->peers,    \
+                         c->rank, c->cap, *segs, slice, chunk, accumulate, timeout);                          \
+    else                                                                                                       \
+      hipLaunchKernelGGL((xg_seg_kernel<w, XG_ALL_GATHER>), dim3(G), dim3(XG_THREADS), 0, st, c->peers,        \
+                         c->rank, c->cap, *segs, slice, chunk, accumulate, timeout);                          \
+    break;
+  if (op != XG_REDUCE_SCATTER && op != XG_ALL_GATHER) return -2;
+  switch (c->world) {
+    XG_SEG_CASE(2)
+    XG_SEG_CASE(3)
+    XG_SEG_CASE(4)
+    XG_SEG_CASE(5)
+    XG_SEG_CASE(6)
+    XG_SEG_CASE(7)
+    XG_SEG_CASE(8)
+    default:
+      return -4;
+  }
+#undef XG_SEG_CASE
+  return HIP_LAUNCH_CHECK();
+}
+
+JDT_API int jdt_xgmi_segs_size() { return (int)sizeof(XgSegs); }
 
 JDT_API int jdt_xgmi_adam_size() { return (int)sizeof(XgAdam); }
 

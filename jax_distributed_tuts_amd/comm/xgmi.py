@@ -55,12 +55,27 @@ class XgAdam(ctypes.Structure):
     ]
 
 
+class XgSeg(ctypes.Structure):
+    _fields_ = [("full", c_void_p), ("part", c_void_p), ("s", c_long), ("off", c_long), ("nfull", c_long)]
+
+
+MAX_SEGS = 16
+
+
+class XgSegs(ctypes.Structure):
+    """Mirror of ``jdt::XgSegs``: up to 16 (full, part) tensors per launch."""
+
+    _fields_ = [("seg", XgSeg * MAX_SEGS), ("n", c_int), ("S", c_long)]
+
+
 _lib.declare("jdt_xgmi_create", c_int, [c_int, c_int, c_long, ctypes.POINTER(c_void_p), c_void_p])
 _lib.declare("jdt_xgmi_open", c_int, [c_void_p, c_void_p])
 _lib.declare("jdt_xgmi_allreduce", c_int, [c_void_p, c_void_p, c_void_p, c_long, ctypes.POINTER(XgAdam), c_longlong,
                                            c_void_p])
 _lib.declare("jdt_xgmi_reduce_scatter", c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_longlong, c_void_p])
 _lib.declare("jdt_xgmi_all_gather", c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_longlong, c_void_p])
+_lib.declare("jdt_xgmi_segments", c_int, [c_void_p, ctypes.POINTER(XgSegs), c_int, c_int, c_longlong, c_void_p])
+_lib.declare("jdt_xgmi_segs_size", c_int, [])
 _lib.declare("jdt_xgmi_capacity", c_long, [c_void_p])
 _lib.declare("jdt_xgmi_adam_size", c_int, [])
 _lib.declare("jdt_xgmi_error", c_int, [c_void_p])
@@ -94,7 +109,7 @@ class XgmiComm:
         self.ctx = c_void_p()
         self.ok = False
         L = _lib.lib()
-        if L.jdt_xgmi_adam_size() != ctypes.sizeof(XgAdam):
+        if L.jdt_xgmi_adam_size() != ctypes.sizeof(XgAdam) or L.jdt_xgmi_segs_size() != ctypes.sizeof(XgSegs):
             raise RuntimeError("XgAdam layout mismatch between Python and comm/csrc/xgmi.hip")
         h = (ctypes.c_char * (3 * HANDLE_BYTES))()
         with torch.cuda.device(device):
@@ -196,9 +211,58 @@ class XgmiComm:
         _lib.check(rc, "jdt_xgmi_all_gather")
         return out
 
+    # ------------------------------------------------------------------ segmented (multi-tensor) RS / AG
+    @staticmethod
+    def segment_ok(full: torch.Tensor, part: torch.Tensor, world: int) -> bool:
+        """Whether (full, part) is a dim-0 shard pair the segmented kernel can move:
+        contiguous, 16-byte aligned, part a multiple of 16 bytes, full = world parts."""
+        es = part.element_size()
+        return (full.is_cuda and part.is_cuda and full.dtype == part.dtype and full.is_contiguous()
+                and part.is_contiguous() and full.data_ptr() % 16 == 0 and part.data_ptr() % 16 == 0
+                and (part.numel() * es) % 16 == 0 and full.numel() == world * part.numel())
+
+    def _segs(self, pairs) -> XgSegs:
+        if not 0 < len(pairs) <= MAX_SEGS:
+            raise ValueError(f"1..{MAX_SEGS} segments per launch")
+        S = XgSegs()
+        off = 0
+        for k, (full, part) in enumerate(pairs):
+            if not self.segment_ok(full, part, self.world):
+                raise ValueError("segment is not a contiguous, 16-byte aligned dim-0 shard pair")
+            w = part.numel() * part.element_size() // 4
+            S.seg[k] = XgSeg(full.data_ptr(), part.data_ptr(), w, off, full.numel() * full.element_size() // 4)
+            off += w
+        S.n, S.S = len(pairs), off
+        return S
+
+    def all_gather_segments(self, pairs):
+        """For each (full, part): full[q*len(part) : (q+1)*len(part)] = rank q's part.
+        Any dtype (moved as 4-byte words); one kernel for all pairs."""
+        for i in range(0, len(pairs), MAX_SEGS):
+            S = self._segs(pairs[i:i + MAX_SEGS])
+            rc = _lib.lib().jdt_xgmi_segments(self.ctx, ctypes.byref(S), 2, 0, self.timeout,
+                                              c_void_p(_lib.stream_ptr()))
+            _lib.check(rc, "jdt_xgmi_segments(all_gather)")
+
+    def reduce_scatter_segments(self, pairs, accumulate: bool = False):
+        """For each fp32 (full, part): part (+)= sum over ranks of full[rank*len(part) : ...]."""
+        for full, part in pairs:
+            if full.dtype != torch.float32:
+                raise ValueError("reduce-scatter sums fp32 tensors")
+        for i in range(0, len(pairs), MAX_SEGS):
+            S = self._segs(pairs[i:i + MAX_SEGS])
+            rc = _lib.lib().jdt_xgmi_segments(self.ctx, ctypes.byref(S), 1, int(accumulate), self.timeout,
+                                              c_void_p(_lib.stream_ptr()))
+            _lib.check(rc, "jdt_xgmi_segments(reduce_scatter)")
+
     # ------------------------------------------------------------------ self-test
     def _self_test(self) -> bool:
-        """Exact-integer checks of AR (both parities), RS and AG on this hardware."""
+        """Exact-integer checks of AR (both parities), RS and AG on this hardware.
+        Runs with a short barrier timeout (the ranks were just synchronised by the
+        handle exchange) and stops at the first failure, so a node whose peers
+        cannot see each other's flags costs seconds, not minutes."""
+        saved = self.timeout
+        self.timeout = c_longlong(int(5.0 * TICKS_PER_S))
         try:
             W, r, dev = self.world, self.rank, self.device
             with torch.cuda.device(dev):
@@ -208,6 +272,10 @@ class XgmiComm:
                 for it in range(3):
                     x = base + r + it
                     self.all_reduce_(x)
+                    torch.cuda.synchronize(dev)
+                    if self.error():
+                        log.warning("xgmi self-test: barrier timeout")
+                        return False
                     if not torch.equal(x, want + W * it):
                         log.warning("xgmi self-test: all-reduce mismatch (iter %d)", it)
                         return False
@@ -236,6 +304,8 @@ class XgmiComm:
         except Exception as e:  # a launch error must not leave the other ranks waiting
             log.warning("xgmi self-test raised: %s", e)
             return False
+        finally:
+            self.timeout = saved
 
 
 def create_for(mesh, axis: str, cap_floats: int, device: torch.device, mode: str = "auto") -> Optional[XgmiComm]:

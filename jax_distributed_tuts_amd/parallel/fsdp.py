@@ -234,6 +234,7 @@ class FSDPConfig:
     gather_once: bool = False
     scatter_once: bool = False
     fused_kernels: bool = False   # classifier: whole-step fused kernels on the gathered buffer (implies *_once)
+    comm: str = "auto"            # "auto" | "xgmi" | "rccl": N>1 gather / reduce-scatter transport
 
 
 class ShardedFlatParams:
@@ -261,6 +262,19 @@ class ShardedFlatParams:
         self.local = FlatParams(sharded + repl, device=device)
         self.full = FlatParams(specs, device=device, metric_slots=0)
         self.repl_start = self.local.offsets[repl[0].name][0] if repl else self.local.metric_off
+        self.xg = None  # comm/xgmi.XgmiComm: direct xGMI segmented gather / reduce-scatter (attach_xgmi)
+        self._xg_names: List[str] = []
+
+    def attach_xgmi(self, comm) -> None:
+        """Route the dim-0 sharded leaves (and the replicated tail's all-reduce)
+        through ONE segmented xGMI kernel per collective instead of one RCCL call
+        per leaf; leaves the kernel cannot move stay on RCCL."""
+        from ..comm.xgmi import XgmiComm
+
+        self.xg = comm
+        self._xg_names = [n for n in self.sharded_names if self.part[n].shard_dim == 0
+                          and XgmiComm.segment_ok(self.full.s(n), self.local.s(n), self.n)
+                          and XgmiComm.segment_ok(self.full.g(n), self.local.g(n), self.n)]
 
     def global_num_params(self) -> int:
         return sum(int(math.prod(s.shape)) for s in self.global_specs)
@@ -290,7 +304,11 @@ class ShardedFlatParams:
     def gather(self):
         """all-gather bf16 shadow shards -> full shadow (X05); replicated: local copy."""
         with named_scope("gather_params"):
+            if self.xg is not None and self._xg_names:
+                self.xg.all_gather_segments([(self.full.s(n), self.local.s(n)) for n in self._xg_names])
             for name in self.sharded_names:
+                if self.xg is not None and name in self._xg_names:
+                    continue
                 d = self.part[name].shard_dim
                 C.all_gather(self.local.s(name), self.mesh, self.axis, dim=d, out=self.full.s(name))
             for name in self.repl_names:
@@ -300,7 +318,12 @@ class ShardedFlatParams:
         """full fp32 grads -> reduce-scatter SUM into local grads (X06); replicated
         grads copied into the local tail.  Full grads are zeroed."""
         with named_scope("scatter_grads"):
+            if self.xg is not None and self._xg_names:
+                self.xg.reduce_scatter_segments([(self.full.g(n), self.local.g(n)) for n in self._xg_names],
+                                                accumulate=accumulate)
             for name in self.sharded_names:
+                if self.xg is not None and name in self._xg_names:
+                    continue
                 d = self.part[name].shard_dim
                 if accumulate:
                     tmp = C.psum_scatter(self.full.g(name), self.mesh, self.axis, dim=d)
@@ -318,7 +341,10 @@ class ShardedFlatParams:
     def sync_replicated(self):
         """sync_gradients for replicated leaves + synch_metrics: ONE all-reduce of the tail."""
         with named_scope("sync_grad"):
-            C.psum_(self.local.grad[self.repl_start:], self.mesh, self.axis)
+            if self.xg is not None:
+                self.xg.all_reduce_(self.local.grad[self.repl_start:])
+            else:
+                C.psum_(self.local.grad[self.repl_start:], self.mesh, self.axis)
 
 
 def init_fsdp(model: MLP, tx, seed: int, device, mesh: Optional[Mesh], axis: str = "data",
@@ -338,6 +364,23 @@ class FSDPTrainer:
         self.metrics = torch.zeros(N_METRIC_SLOTS, dtype=torch.float32, device=self.sp.local.master.device)
         self.world = C.axis_size(mesh, cfg.axis)
         self.fused = None
+        if self.world > 1 and self.sp.local.master.is_cuda and self.sp.xg is None:
+            from ..comm.xgmi import create_for
+
+            xg = create_for(mesh, cfg.axis, self.sp.full.grad.numel(), self.sp.local.master.device, cfg.comm)
+            if xg is not None:
+                self.sp.attach_xgmi(xg)
+
+    @property
+    def comm_backend(self) -> str:
+        if self.world == 1:
+            return "none"
+        if self.sp.xg is not None:
+            return "xgmi"
+        from ..runtime.dist import backend
+
+        b = backend()
+        return "rccl" if b == "nccl" else (b or "none")
 
     def _fused_step(self, batch: Batch) -> bool:
         """gather bf16 shards once -> mlp2_fwd/mlp2_bwd on the full buffer (mode 0:
@@ -387,6 +430,10 @@ class FSDPTrainer:
         st.apply_gradients(grad_scale=1.0 / (n_mb * self.world))
         with named_scope("synch_metrics"):
             K.metrics_fold_(self.metrics, sp.local.metrics_slot)
+
+    def finalize(self):
+        if self.sp.xg is not None and self.sp.xg.error():
+            raise RuntimeError("xgmi collective timed out on this rank (peer dead or desynchronised)")
 
     def full_params(self) -> Dict[str, torch.Tensor]:
         """Gather the fp32 masters (for checks / checkpoints)."""

@@ -67,5 +67,10 @@ def run(fn: Callable, *args: Any, sim_cpu: int | None = None):
     D.init()
     try:
         fn(*args)
+    except Exception as e:  # report on the failing rank, then tear down so peers fail fast
+        from ..utils.metrics import print_exception
+
+        print_exception(e)
+        raise
     finally:
         D.shutdown()

@@ -137,3 +137,32 @@ def dp_xgmi(outdir, steps_eager=2, steps_graph=6):
     tr.finalize()
     _save(outdir, "dpx", {"master": st.params.master.cpu(), "metrics": tr.metrics.cpu(), "comm": tr.comm_backend,
                           "fused": tr.fused is not None, "step": int(st.opt_state["count"].item())})
+
+
+def fsdp_xgmi(outdir, fused=True, steps=3):
+    """FSDP (dropout off) with the segmented xGMI gather / reduce-scatter; every rank
+    saves its local shard + the partition table for reassembly in the parent."""
+    from data_paral import synthetic_batch
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import shard_batch
+    from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
+    from jax_distributed_tuts_amd.runtime import dist as D
+    from jax_distributed_tuts_amd.utils.config import fsdp_config
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    dev = D.device()
+    cfg = fsdp_config()
+    mesh = D.Mesh({"data": D.world_size()})
+    st = init_fsdp(Classifier(dropout_rate=0.0), adamw(1e-3), 69, dev, mesh, "data", 16)
+    b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
+    b = Batch(b.inputs.to(dev), b.labels.to(dev))
+    tr = FSDPTrainer(st, mesh, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=fused,
+                                          comm="xgmi"))
+    for _ in range(steps):
+        tr.step(b)
+    torch.cuda.synchronize()
+    tr.finalize()
+    sp = st.extra["sharded"]
+    _save(outdir, "fsx", {"local": {n: sp.local.p(n).cpu() for n in sp.part},
+                          "dims": {n: sp.part[n].shard_dim for n in sp.part},
+                          "metrics": tr.metrics.cpu(), "comm": tr.comm_backend, "xg_names": list(sp._xg_names)})

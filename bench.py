@@ -140,10 +140,14 @@ def main():
     for _ in range(n_eager):
         tr.step(batch)
     sync()
-    # collectives/p2p inside FSDP and PP steps stay eager; DP captures its step
-    use_graph = on_gpu and not args.no_graph and args.strategy == "dp"
-    if use_graph:
+    # DP always captures its step; FSDP when its collectives are xGMI kernels (or N=1);
+    # PP's send/recv stay eager
+    use_graph = on_gpu and not args.no_graph and (args.strategy == "dp" or
+                                                  (args.strategy == "fsdp" and tr.capturable))
+    if use_graph and args.strategy == "dp":
         tr.capture(batch, capture_collectives=args.capture_collectives, steps_per_graph=args.steps_per_graph)
+    elif use_graph:
+        tr.capture(batch, steps_per_graph=args.steps_per_graph)
 
     def run(n):
         if hasattr(tr, "run_steps"):

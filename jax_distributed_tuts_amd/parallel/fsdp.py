@@ -364,6 +364,8 @@ class FSDPTrainer:
         self.metrics = torch.zeros(N_METRIC_SLOTS, dtype=torch.float32, device=self.sp.local.master.device)
         self.world = C.axis_size(mesh, cfg.axis)
         self.fused = None
+        self.graph = None
+        self.multi = None
         if self.world > 1 and self.sp.local.master.is_cuda and self.sp.xg is None:
             from ..comm.xgmi import create_for
 
@@ -402,13 +404,52 @@ class FSDPTrainer:
         sp.sync_replicated()
         self.state.tx.update(sp.local, self.state.opt_state, 1.0 / (self.cfg.num_minibatches * self.world),
                              zero_grad=False)
-        self.state.step += 1
         with named_scope("synch_metrics"):
             K.metrics_fold_(self.metrics, sp.local.metrics_slot)
         return True
 
     def step(self, batch: Batch):
         """train_step_fsdp (param_sharding.py:343-367)."""
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._body(batch)
+        self.state.step += 1
+
+    # ------------------------------------------------------------------ hipGraph
+    @property
+    def capturable(self) -> bool:
+        """N=1, or every collective of the step is an xGMI kernel (no host-side RCCL)."""
+        return self.world == 1 or (self.sp.xg is not None and len(self.sp._xg_names) == len(self.sp.sharded_names))
+
+    def capture(self, batch: Batch, steps_per_graph: int = 1):
+        """Record the whole step (gather, fwd/bwd, reduce-scatter, replicated
+        all-reduce, sharded AdamW, metrics fold) as a hipGraph; with
+        ``steps_per_graph`` > 1 also a graph of that many consecutive steps."""
+        assert self.capturable and batch.inputs.is_cuda
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._body(batch)
+        self.graph = g
+        if steps_per_graph > 1:
+            gm = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gm, pool=g.pool()):
+                for _ in range(steps_per_graph):
+                    self._body(batch)
+            self.multi = (steps_per_graph, gm)
+
+    def run_steps(self, batch: Batch, n: int):
+        if self.graph is not None and self.multi is not None:
+            S, gm = self.multi
+            for _ in range(n // S):
+                gm.replay()
+            self.state.step += (n // S) * S
+            n %= S
+        for _ in range(n):
+            self.step(batch)
+
+    def _body(self, batch: Batch):
+        """One step of device work (no host counters, so it can be captured)."""
         if self._fused_step(batch):
             return
         st, sp, cfg = self.state, self.sp, self.cfg
@@ -427,7 +468,7 @@ class FSDPTrainer:
         if cfg.scatter_once:
             sp.scatter_grads(accumulate=False)
         sp.sync_replicated()
-        st.apply_gradients(grad_scale=1.0 / (n_mb * self.world))
+        st.tx.update(sp.local, st.opt_state, 1.0 / (n_mb * self.world))
         with named_scope("synch_metrics"):
             K.metrics_fold_(self.metrics, sp.local.metrics_slot)
 

@@ -413,3 +413,33 @@ def test_flash_attention_fwd_bwd(B, S, H, causal):
     # composed (GEMM + softmax kernels) path agrees with the fused one
     o_c, P = kern.attention_fwd(qkv.to(DEV), B, S, H, causal=causal, impl="composed")
     _close(o_c, o_g, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_fsdp_graph_replay_matches_eager(fused):
+    """FSDP (world 1) captured as single- and multi-step hipGraphs == eager steps."""
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    g = torch.Generator().manual_seed(3)
+    b = Batch(torch.randn(128, 784, generator=g).to(DEV), torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV))
+    res = []
+    for graph in (False, True):
+        st = init_fsdp(Classifier(), adamw(1e-3), 69, DEV, None, "data", 16)
+        tr = FSDPTrainer(st, None, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=fused))
+        tr.step(b)
+        if graph:
+            tr.capture(b, steps_per_graph=3)
+            tr.run_steps(b, 7)
+        else:
+            for _ in range(7):
+                tr.step(b)
+        torch.cuda.synchronize()
+        res.append((st.params.master.clone(), tr.metrics.clone(), int(st.opt_state["count"].item()), st.step))
+    assert res[0][2] == res[1][2] == 8 and res[0][3] == res[1][3] == 8
+    # fp32 atomics (split-K partial logits) make runs differ in the last bits; Adam can
+    # turn that into an lr-sized move on a ~0 gradient, so bound the fraction
+    d = (res[1][0] - res[0][0]).abs()
+    assert float(d.max()) <= 2 * 1e-3 * 8 and float((d > 5e-5).float().mean()) < 2e-3
+    torch.testing.assert_close(res[1][1], res[0][1], rtol=1e-4, atol=1e-3)

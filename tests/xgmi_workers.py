@@ -158,8 +158,10 @@ def fsdp_xgmi(outdir, fused=True, steps=3):
     b = Batch(b.inputs.to(dev), b.labels.to(dev))
     tr = FSDPTrainer(st, mesh, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=fused,
                                           comm="xgmi"))
-    for _ in range(steps):
-        tr.step(b)
+    tr.step(b)
+    assert tr.capturable
+    tr.capture(b, steps_per_graph=2)  # the rest of the steps replay one hipGraph (collectives are kernels)
+    tr.run_steps(b, steps - 1)
     torch.cuda.synchronize()
     tr.finalize()
     sp = st.extra["sharded"]

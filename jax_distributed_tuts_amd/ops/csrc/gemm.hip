@@ -122,6 +122,64 @@ __device__ __forceinline__ u32x4 load_chunk(const void* base, long ld, bool tran
   }
 }
 
+// Raw (unconverted) chunk for the preload path: fp32 sources stay fp32 in
+// registers until the LDS write, so no load ever waits on a conversion and
+// all K-tiles' loads can be in flight at once.
+template <bool F32> struct RawChunk { u32x4 v; };
+template <> struct RawChunk<true> { float4 x, y; };
+
+template <bool F32>
+__device__ __forceinline__ RawChunk<F32> load_raw(const void* base, long ld, bool trans, int r, int k, int R, int K,
+                                                  bool vec_ok) {
+  RawChunk<F32> out;
+  if constexpr (F32) {
+    out.x = make_float4(0.f, 0.f, 0.f, 0.f);
+    out.y = out.x;
+    const float* src = static_cast<const float*>(base);
+    float e[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (!trans) {
+      if (r >= R) return out;
+      const long off = (long)r * ld + k;
+      if (vec_ok && k + 8 <= K) {
+        const float4* p = reinterpret_cast<const float4*>(src + off);
+        out.x = p[0];
+        out.y = p[1];
+        return out;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) if (k + j < K) e[j] = src[off + j];
+    } else {
+      if (k >= K) return out;
+      const long off = (long)k * ld + r;
+      if (vec_ok && r + 8 <= R) {
+        const float4* p = reinterpret_cast<const float4*>(src + off);
+        out.x = p[0];
+        out.y = p[1];
+        return out;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) if (r + j < R) e[j] = src[off + j];
+    }
+    out.x = make_float4(e[0], e[1], e[2], e[3]);
+    out.y = make_float4(e[4], e[5], e[6], e[7]);
+  } else {
+    out.v = load_chunk<false>(base, ld, trans, r, k, R, K, vec_ok);
+  }
+  return out;
+}
+
+template <bool F32>
+__device__ __forceinline__ u32x4 raw_to_bf16(const RawChunk<F32>& c) {
+  if constexpr (F32) {
+    u32x4 o;
+    o.x = pack2(f2bf(c.x.x), f2bf(c.x.y)); o.y = pack2(f2bf(c.x.z), f2bf(c.x.w));
+    o.z = pack2(f2bf(c.y.x), f2bf(c.y.y)); o.w = pack2(f2bf(c.y.z), f2bf(c.y.w));
+    return o;
+  } else {
+    return c.v;
+  }
+}
+
 // chunk index c -> (row, k) of the tile for either orientation
 template <int BK>
 __device__ __forceinline__ int2 chunk_rk(int c, bool trans) {
@@ -142,7 +200,7 @@ __device__ __forceinline__ void store_chunk(bf16_t* lds, bool trans, int r, int 
   }
 }
 
-template <int WM, int WN, int TM, int TN, int BK, bool AF32, bool BF32>
+template <int WM, int WN, int TM, int TN, int BK, bool AF32, bool BF32, int PRE>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int vecA, int vecB, int splits,
                                                    int kchunk, float* __restrict__ ws, unsigned* counters) {
   using T = Tile<WM, WN, TM, TN, BK>;
@@ -221,12 +279,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
     }
   };
 
-  gload(0);
-  lwrite(0);
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nkt) gload(kt + 1);  // in flight under the MFMAs below
+  auto mfma_tile = [&](int cur) {
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
       bf16x8 af[TM], bfr[TN];
@@ -245,8 +298,71 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
     }
-    if (kt + 1 < nkt) lwrite(cur ^ 1);
+  };
+
+  if constexpr (PRE > 0) {
+    // Preload: every K-tile of this slice is requested before the first MFMA
+    // (nkt <= PRE), so the slice costs ONE global round trip instead of nkt
+    // dependent ones; the tiles then stream through the two LDS buffers.
+    RawChunk<AF32> pa[PRE][T::A_PER_T];
+    RawChunk<BF32> pb[PRE][T::B_PER_T];
+#pragma unroll
+    for (int kt = 0; kt < PRE; ++kt) {
+      if (kt < nkt) {
+        const int kb = kbeg + kt * BK;
+#pragma unroll
+        for (int i = 0; i < T::A_PER_T; ++i) {
+          const int c = tid + i * 256;
+          if (c < T::A_CHUNKS) {
+            const int2 rk = chunk_rk<BK>(c, g.a_trans);
+            pa[kt][i] = load_raw<AF32>(Ab, g.lda, g.a_trans, rk.x, kb + rk.y, Ar, kend, vecA);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < T::B_PER_T; ++i) {
+          const int c = tid + i * 256;
+          if (c < T::B_CHUNKS) {
+            const int2 rk = chunk_rk<BK>(c, g.b_trans);
+            pb[kt][i] = load_raw<BF32>(Bb, g.ldb, g.b_trans, rk.x, kb + rk.y, Br, kend, vecB);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int kt = 0; kt < PRE; ++kt) {
+      if (kt < nkt) {
+        const int cur = kt & 1;
+#pragma unroll
+        for (int i = 0; i < T::A_PER_T; ++i) {
+          const int c = tid + i * 256;
+          if (c < T::A_CHUNKS) {
+            const int2 rk = chunk_rk<BK>(c, g.a_trans);
+            store_chunk<LDK>(AS(cur), g.a_trans, rk.x, rk.y, raw_to_bf16<AF32>(pa[kt][i]));
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < T::B_PER_T; ++i) {
+          const int c = tid + i * 256;
+          if (c < T::B_CHUNKS) {
+            const int2 rk = chunk_rk<BK>(c, g.b_trans);
+            store_chunk<LDK>(BS(cur), g.b_trans, rk.x, rk.y, raw_to_bf16<BF32>(pb[kt][i]));
+          }
+        }
+        __syncthreads();
+        mfma_tile(cur);
+      }
+    }
+  } else {
+    gload(0);
+    lwrite(0);
     __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nkt) gload(kt + 1);  // in flight under the MFMAs below
+      mfma_tile(cur);
+      if (kt + 1 < nkt) lwrite(cur ^ 1);
+      __syncthreads();
+    }
   }
 
 #undef AS
@@ -352,6 +468,9 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
   }
 }
 
+constexpr int kPreMax = 4;      // K-tiles a preloading slice holds in registers
+static bool g_gemm_no_preload = false;  // jdt_gemm_set_preload(0): pipelined path only (A/B tests)
+
 template <int WM, int WN, int TM, int TN, int BK>
 static int launch_cfg(const GemmArgs& g, int batch, int splits, float* ws, long ws_floats, unsigned* counters,
                       long n_counters, hipStream_t st) {
@@ -363,8 +482,11 @@ static int launch_cfg(const GemmArgs& g, int batch, int splits, float* ws, long 
     // Small GEMMs here are latency-bound on the K loop (one global round trip
     // per K-tile): split K until the grid covers ~all CUs, <= 16 slices,
     // each slice at least one K-tile.
+    // With the preload path a slice costs one round trip whatever its length,
+    // so split only to fill the CUs (<= ~256 workgroups).
     splits = 1;
     while (splits < 16 && tiles * splits * 2 <= 256 && ktiles >= splits * 2) splits *= 2;
+    while (splits < 16 && (ktiles + splits - 1) / splits > kPreMax && tiles * splits * 2 <= 512) splits *= 2;
   }
   if (splits > ktiles) splits = ktiles;
   if (splits < 1) splits = 1;
@@ -378,10 +500,21 @@ static int launch_cfg(const GemmArgs& g, int batch, int splits, float* ws, long 
     return ((reinterpret_cast<uintptr_t>(p) & 15) == 0) && (f32 ? (ld % 4 == 0) : (ld % 8 == 0));
   };
   const int va = vec_ok(g.A, g.lda, g.a_f32), vb = vec_ok(g.B, g.ldb, g.b_f32);
-  if (g.a_f32 && g.b_f32) hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, true, true>), grid, dim3(256), 0, st, g, tiles_n, va, vb, splits, kchunk, ws, counters);
-  else if (g.a_f32)       hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, true, false>), grid, dim3(256), 0, st, g, tiles_n, va, vb, splits, kchunk, ws, counters);
-  else if (g.b_f32)       hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, false, true>), grid, dim3(256), 0, st, g, tiles_n, va, vb, splits, kchunk, ws, counters);
-  else                    hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, false, false>), grid, dim3(256), 0, st, g, tiles_n, va, vb, splits, kchunk, ws, counters);
+  const bool pre = kchunk / BK <= kPreMax && !g_gemm_no_preload;
+#define JDT_GEMM_LAUNCH(AF, BF)                                                                                  \
+  do {                                                                                                           \
+    if (pre)                                                                                                     \
+      hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, AF, BF, kPreMax>), grid, dim3(256), 0, st, g, tiles_n, \
+                         va, vb, splits, kchunk, ws, counters);                                                  \
+    else                                                                                                         \
+      hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, AF, BF, 0>), grid, dim3(256), 0, st, g, tiles_n, va,   \
+                         vb, splits, kchunk, ws, counters);                                                      \
+  } while (0)
+  if (g.a_f32 && g.b_f32) JDT_GEMM_LAUNCH(true, true);
+  else if (g.a_f32)       JDT_GEMM_LAUNCH(true, false);
+  else if (g.b_f32)       JDT_GEMM_LAUNCH(false, true);
+  else                    JDT_GEMM_LAUNCH(false, false);
+#undef JDT_GEMM_LAUNCH
   return HIP_LAUNCH_CHECK();
 }
 
@@ -391,6 +524,8 @@ using namespace jdt;
 
 // Tile choice: the tutorial GEMMs are small (M = 4..128 rows per device), so the
 // heuristic favours enough workgroups to cover the chip over per-tile reuse.
+JDT_API void jdt_gemm_set_preload(int on) { g_gemm_no_preload = !on; }
+
 JDT_API int jdt_gemm(const GemmArgs* ga, int batch, int cfg, int splits, float* ws, long ws_floats,
                      unsigned* counters, long n_counters, void* stream) {
   const GemmArgs& g = *ga;

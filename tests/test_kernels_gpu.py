@@ -22,11 +22,21 @@ def _mk(shape, dtype, layout_t=False, seed=0):
     return t.to(dtype)
 
 
+@pytest.fixture(params=[1, 0], ids=["preload", "pipelined"])
+def gemm_path(request):
+    """Run a GEMM test through the all-K-tiles-preloaded path and the pipelined one."""
+    from jax_distributed_tuts_amd.ops import _lib
+
+    _lib.lib().jdt_gemm_set_preload(request.param)
+    yield request.param
+    _lib.lib().jdt_gemm_set_preload(1)
+
+
 @pytest.mark.parametrize("M,N,K", [(4, 512, 784), (16, 512, 784), (32, 10, 512), (128, 512, 784), (37, 70, 50),
                                    (256, 384, 256), (512, 512, 512)])
 @pytest.mark.parametrize("a_layout,b_layout", [("mk", "kn"), ("mk", "nk"), ("km", "kn"), ("km", "nk")])
 @pytest.mark.parametrize("adt", [torch.bfloat16, torch.float32])
-def test_gemm_layouts(M, N, K, a_layout, b_layout, adt):
+def test_gemm_layouts(M, N, K, a_layout, b_layout, adt, gemm_path):
     a = _mk((M, K) if a_layout == "mk" else (K, M), adt, seed=1)
     b = _mk((K, N) if b_layout == "kn" else (N, K), torch.bfloat16, seed=2)
     ref = kern.gemm(a, b, a_layout=a_layout, b_layout=b_layout, out_dtype=torch.float32)
@@ -182,7 +192,7 @@ def test_dp_graph_replay_matches_eager():
 
 @pytest.mark.parametrize("splits", [1, 3, 7, 16])
 @pytest.mark.parametrize("M,N,K_,cfg", [(32, 512, 784, 0), (128, 10, 512, 4), (784, 512, 128, 2)])
-def test_gemm_split_k(splits, M, N, K_, cfg):
+def test_gemm_split_k(splits, M, N, K_, cfg, gemm_path):
     """In-kernel split-K (slab + last-arriver combine) must match the single-slice result,
     including the fused epilogue (bias/act/dropout) and fp32 accumulate."""
     x = _mk((M, K_), torch.float32, seed=21)

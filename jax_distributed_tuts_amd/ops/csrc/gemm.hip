@@ -369,11 +369,15 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
 #undef BS
 
   // ------------------------------------------------------------- split-K combine
-  // Every K-slice writes its fp32 partial tile (slab) with plain stores, then
-  // publishes with ONE agent-scope release + arrival ticket; the workgroup that
-  // draws the last ticket acquires, sums the slabs and runs the epilogue
-  // (cdna_hip_programming.md §5 "In-launch split-K reduction").  Correct for any
-  // placement of the slices over XCDs.
+  // Every K-slice writes its fp32 partial tile (slab) with device-scope stores
+  // (sc1: written through to the cross-XCD coherence point), waits for them
+  // (vmcnt), then draws an arrival ticket; the workgroup that draws the last
+  // ticket reads the slabs with device-scope loads and runs the epilogue.  No
+  // agent-scope release/acquire fence: on this multi-XCD part those lower to a
+  // write-back / invalidate of the whole L2 (buffer_wbl2 / buffer_inv sc1),
+  // which cost several us per workgroup; only the slab lines need coherence.
+  // The slab layout is the lanes' own accumulator order, so the combine is
+  // placement independent.
   if (splits > 1) {
     const long tile_id = (long)z * gridDim.x + bid;
     float* slab0 = ws + tile_id * splits * (BM * BN);
@@ -383,23 +387,16 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int lr = (wm * TM + i) * 16 + (lane >> 4) * 4 + e, lc = (wn * TN + j) * 16 + (lane & 15);
-          slab[lr * BN + lc] = acc[i][j][e];
-        }
+        for (int e = 0; e < 4; ++e)
+          __hip_atomic_store(slab + (((wid * TM + i) * TN + j) * 64 + lane) * 4 + e, acc[i][j][e], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* flag = reinterpret_cast<int*>(smem);
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned t = __hip_atomic_fetch_add(counters + tile_id, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = (t == (unsigned)(splits - 1));
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(counters + tile_id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      if (last) __hip_atomic_store(counters + tile_id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       flag[0] = last;
     }
     __syncthreads();
@@ -409,12 +406,18 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int lr = (wm * TM + i) * 16 + (lane >> 4) * 4 + e, lc = (wn * TN + j) * 16 + (lane & 15);
-          float sum = 0.f;
-          for (int sp = 0; sp < splits; ++sp) sum += slab0[(long)sp * (BM * BN) + lr * BN + lc];
-          acc[i][j][e] = sum;
-        }
+        for (int e = 0; e < 4; ++e) acc[i][j][e] = 0.f;
+    for (int sp = 0; sp < splits; ++sp) {
+      const float* sl = slab0 + (long)sp * (BM * BN);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            acc[i][j][e] += __hip_atomic_load(sl + (((wid * TM + i) * TN + j) * 64 + lane) * 4 + e, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   // ------------------------------------------------------------- epilogue
   const bool drop = g.keep_prob < 1.0f;

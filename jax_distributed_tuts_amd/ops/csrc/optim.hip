@@ -101,12 +101,17 @@ __global__ void scale_kernel(float* __restrict__ x, long n, float s) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] *= s;
 }
 
-static int grid_for(long n, int per_thread) {
+static int grid_for(long n, int per_thread, int cap = 2048) {
   long b = (n / per_thread + 255) / 256;
   if (b < 1) b = 1;
-  if (b > 2048) b = 2048;  // grid-stride beyond ~8 blocks/CU
+  if (b > cap) b = cap;  // grid-stride beyond that
   return (int)b;
 }
+
+// Kernels that advance the device step counter end with one same-address
+// arrival ticket per workgroup; those atomics serialise, so those kernels run
+// at most one workgroup per CU and grid-stride over the rest.
+constexpr int kTicketGrid = 256;
 
 }  // namespace jdt
 using namespace jdt;
@@ -118,7 +123,7 @@ JDT_API int jdt_adamw(float* p, float* g, float* m, float* v, void* shadow, long
   if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
        reinterpret_cast<uintptr_t>(v)) & 15) return -2;
   if (shadow && (reinterpret_cast<uintptr_t>(shadow) & 7)) return -2;
-  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n, 4)), dim3(256), 0, static_cast<hipStream_t>(stream), p, g, m, v,
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n, 4, kTicketGrid)), dim3(256), 0, static_cast<hipStream_t>(stream), p, g, m, v,
                      static_cast<bf16_t*>(shadow), n, lr, b1, b2, eps, wd, grad_scale, step, ticket, zero_grad);
   return HIP_LAUNCH_CHECK();
 }
@@ -126,7 +131,7 @@ JDT_API int jdt_adamw(float* p, float* g, float* m, float* v, void* shadow, long
 JDT_API int jdt_sgd(float* p, float* g, float* buf, void* shadow, long n, float lr, float momentum, float wd,
                     float grad_scale, int* step, unsigned* ticket, int zero_grad, void* stream) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n, 1)), dim3(256), 0, static_cast<hipStream_t>(stream), p, g, buf,
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n, 1, step ? kTicketGrid : 2048)), dim3(256), 0, static_cast<hipStream_t>(stream), p, g, buf,
                      static_cast<bf16_t*>(shadow), n, lr, momentum, wd, grad_scale, step, ticket, zero_grad);
   return HIP_LAUNCH_CHECK();
 }

@@ -1,0 +1,582 @@
+// Whole-step fused kernels for DEEP tutorial MLPs: 784 -> H -> ... -> H -> C
+// (BASELINE configs #2/#3: the 4-layer MLP data-parallel and param-sharded).
+//
+// The 2-layer classifier runs as 2 launches (mlp_fused.hip).  With L dense
+// layers every hidden layer adds one true grid-wide dependency in each
+// direction (a row of layer i+1 needs the whole row of layer i), so a step is
+// one forward and one backward launch per hidden layer:
+//
+//   md_fwd (layer i)  grid (row blocks of 32) x (output blocks of 16), 8 waves
+//     Z_i = IN W_i + b_i, H_i = dropout(silu(Z_i)); IN is the fp32 data (layer
+//     0) or H_{i-1} (bf16).  Also writes IN^T (K-contiguous, for the dW MFMA of
+//     the matching backward launch).  The last hidden layer also accumulates
+//     the head's partial logits H_i[:,blk] W_head[blk,:] with fp32 atomics.
+//
+//   md_bwd (layer i)  grid (output blocks of 16) x (input chunks of KC), 8 waves
+//     dZ_i[:, blk]: TOP (last hidden) from softmax-CE of the summed logits
+//     through the head; otherwise (dZ_{i+1} W_{i+1}^T)[:, blk] on MFMA with
+//     both fragments loaded straight from global memory -- recomputed by each
+//     of the K_IN/KC workgroups of the column block, which is cheaper than a
+//     separate launch -- then * silu'(Z_i) * mask/keep.
+//     dW_i[chunk, blk] = IN[:, chunk]^T dZ_i[:, blk] on MFMA (IN^T from md_fwd),
+//     db_i (and, TOP, the head's dW/db + metrics) on the spare wave of the
+//     chunk-0 workgroups, which also store dZ_i for the next launch.
+//     mode 1 (one GPU): AdamW in the epilogue.  W_i's row-major bf16 shadow is
+//     still read (old values) by the launch for layer i-1, so it is double
+//     buffered by step parity; the K-contiguous copy W_i^T the next forward
+//     reads is written directly.  The last launch (layer 0) advances the
+//     device step.  mode 0 (N > 1 / FSDP): plain-store grads into the bucket.
+//
+// Dropout streams match the generic path (models/mlp.py): layer i uses offset
+// (i << 1) and 4-row groups (dropout_group), so fused == generic bit-for-bit
+// up to summation order.
+#include "common.h"
+
+namespace jdt {
+
+constexpr int MD_NT = 512;
+constexpr int MD_NW = MD_NT / 64;
+constexpr int MD_MPM = 128;  // max rows per device
+
+struct MdArgs {
+  int M, K, N, C;       // rows; this layer's in/out features; head classes
+  float inv_mb;         // CE grad scale (1 / rows per minibatch)
+  const void* X;        // layer input [M][K]: fp32 (layer 0) or bf16
+  const bf16_t* Ws0;    // W_i row-major shadow [K][N], step parity 0 / 1 (same pointer if not double buffered)
+  const bf16_t* Ws1;
+  const bf16_t* WT;     // W_i^T [N][ldwt] (direct fwd fragments) or null -> LDS transposition of Ws
+  int ldwt;
+  const bf16_t* bs;     // b_i shadow [N]
+  bf16_t* Z;            // [M][N] pre-activation
+  bf16_t* Hout;         // [M][N] activation (next layer's input)
+  bf16_t* INT;          // IN^T [K][ldint] (fwd writes, bwd reads)
+  int ldint;
+  // head (fwd HEAD / bwd TOP)
+  const bf16_t* Wh0;    // [N][C] by parity
+  const bf16_t* Wh1;
+  const bf16_t* bh;     // [C]
+  float* logits;        // [2][M][C]
+  const int* labels;
+  // dropout
+  float keep;
+  unsigned long long seed, offset;
+  int* step;
+  unsigned* ticket;
+  int advance_step;
+  // bwd, !TOP: the next layer
+  const bf16_t* dZn;    // dZ_{i+1} [M][NN]
+  const bf16_t* Wn0;    // W_{i+1} row-major [N][NN] by parity
+  const bf16_t* Wn1;
+  bf16_t* dZout;        // dZ_i [M][N] for the launch of layer i-1 (null for layer 0)
+  // gradients (mode 0)
+  int fuse_opt;
+  float* gW; float* gb; float* gWh; float* gbh; float* mslot;
+  // AdamW (mode 1)
+  float* pW; float* mW; float* vW;
+  float* pb; float* mb; float* vb;
+  bf16_t* sb;           // b_i shadow out
+  bf16_t* WTout;        // W_i^T copy out [N][ldwt]
+  float* pWh; float* mWh; float* vWh;
+  float* pbh; float* mbh; float* vbh;
+  bf16_t* sbh;
+  float lr, beta1, beta2, eps, wd, gscale;
+  float* running;
+};
+
+struct MdAdam { float b1, b2, eps, wd, lr, gs, rbc1, rbc2; };
+
+__device__ __forceinline__ MdAdam md_adam_consts(const MdArgs& a, int step) {
+  MdAdam k;
+  k.b1 = a.beta1; k.b2 = a.beta2; k.eps = a.eps; k.wd = a.wd; k.lr = a.lr; k.gs = a.gscale;
+  const float t = (float)(step + 1);
+  k.rbc1 = 1.f / (1.f - powf(a.beta1, t));
+  k.rbc2 = 1.f / (1.f - powf(a.beta2, t));
+  return k;
+}
+
+__device__ __forceinline__ float md_adam(float p, float m, float v, float g, const MdAdam& k, float* pp, float* mp,
+                                         float* vp) {
+  g *= k.gs;
+  m = k.b1 * m + (1.f - k.b1) * g;
+  v = k.b2 * v + (1.f - k.b2) * g * g;
+  p = p - k.lr * ((m * k.rbc1) / (sqrtf(v * k.rbc2) + k.eps) + k.wd * p);
+  *pp = p; *mp = m; *vp = v;
+  return p;
+}
+
+// ---------------------------------------------------------------------------- forward
+template <int K_IN, bool XF32, int XTC, bool HEAD, int C>
+__global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
+  constexpr int NT = MD_NT, NW = MD_NW;
+  constexpr int KS = (K_IN + 31) / 32;
+  constexpr int KP = KS * 32;
+  constexpr int LDW = KP + 8;
+  constexpr int WCH = (K_IN * 2 + NT - 1) / NT;   // 16-byte W chunks per thread (LDS path)
+  constexpr int MAXT = (KS + NW - 1) / NW;
+  constexpr int LDXS = K_IN + 8;
+  static_assert(K_IN % XTC == 0 && XTC % 8 == 0 && XTC * 4 <= NT && K_IN % 8 == 0, "IN^T chunking");
+  __shared__ __attribute__((aligned(16))) bf16_t wt[16 * LDW];
+  __shared__ __attribute__((aligned(16))) bf16_t xs[32 * LDXS];
+  __shared__ float part[NW][32][17];
+  __shared__ float htile[32][17];
+  __shared__ float whs[16][C > 0 ? C : 1];
+  __shared__ float bsh[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int M = a.M, N = a.N;
+  const int r0 = blockIdx.x * 32, j0 = blockIdx.y * 16;
+  const int step = a.step[0], par = step & 1;
+  const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
+  const bf16_t* Ws = par ? a.Ws1 : a.Ws0;
+  const int ks0 = (w * KS) / NW, ks1 = ((w + 1) * KS) / NW;
+  const bool direct = a.WT != nullptr;
+
+  // ---- 1. every global load up front
+  u32x4 wv[WCH];
+  bf16x8 bg[MAXT];
+  if (!direct) {
+#pragma unroll
+    for (int t = 0; t < WCH; ++t) {
+      const int idx = tid + t * NT;
+      wv[t] = (u32x4){0u, 0u, 0u, 0u};
+      if (idx < K_IN * 2) wv[t] = *reinterpret_cast<const u32x4*>(Ws + (long)(idx >> 1) * N + j0 + (idx & 1) * 8);
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t) {
+      bg[t] = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+      if (ks0 + t < ks1)
+        bg[t] = *reinterpret_cast<const bf16x8*>(a.WT + (long)(j0 + (lane & 15)) * a.ldwt + (ks0 + t) * 32 +
+                                                 8 * (lane >> 4));
+    }
+  }
+  // input row block [32][K_IN], coalesced 16-byte loads
+  constexpr int EPV = XF32 ? 4 : 8;                 // elements per 16-byte vector
+  constexpr int XV = 32 * K_IN / EPV;
+  constexpr int XPT = (XV + NT - 1) / NT;
+  u32x4 xv[XPT];
+#pragma unroll
+  for (int e = 0; e < XPT; ++e) {
+    const int f = tid + e * NT, rl = f / (K_IN / EPV), kv = f % (K_IN / EPV);
+    xv[e] = (u32x4){0u, 0u, 0u, 0u};
+    if (f < XV && r0 + rl < M) {
+      const char* src = static_cast<const char*>(a.X) + ((long)(r0 + rl) * K_IN + (long)kv * EPV) * (XF32 ? 4 : 2);
+      xv[e] = *reinterpret_cast<const u32x4*>(src);
+    }
+  }
+  float whv = 0.f, bv = 0.f;
+  const bf16_t* Wh = par ? a.Wh1 : a.Wh0;
+  if (HEAD && tid < 16 * C) whv = bf2f(Wh[(long)(j0 + tid / C) * C + tid % C]);
+  if (tid < 16) bv = bf2f(a.bs[j0 + tid]);
+
+  // ---- 2. LDS images
+  if (!direct) {
+#pragma unroll
+    for (int t = 0; t < WCH; ++t) {
+      const int idx = tid + t * NT;
+      if (idx < K_IN * 2) {
+        const int k = idx >> 1, h = (idx & 1) * 8;
+        const unsigned q[4] = {wv[t].x, wv[t].y, wv[t].z, wv[t].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          wt[(h + 2 * e) * LDW + k] = (bf16_t)(q[e] & 0xffff);
+          wt[(h + 2 * e + 1) * LDW + k] = (bf16_t)(q[e] >> 16);
+        }
+      }
+    }
+    if (KP > K_IN)
+      for (int idx = tid; idx < 16 * (KP - K_IN); idx += NT) wt[(idx / (KP - K_IN)) * LDW + K_IN + idx % (KP - K_IN)] = 0;
+  }
+  if (HEAD && tid < 16 * C) whs[tid / C][tid % C] = whv;
+  if (tid < 16) bsh[tid] = bv;
+#pragma unroll
+  for (int e = 0; e < XPT; ++e) {
+    const int f = tid + e * NT, rl = f / (K_IN / EPV), kv = f % (K_IN / EPV);
+    if (f < XV) {
+      if (XF32) {
+        const float4 x = *reinterpret_cast<const float4*>(&xv[e]);
+        *reinterpret_cast<uint2*>(&xs[rl * LDXS + 4 * kv]) =
+            make_uint2((unsigned)f2bf(x.x) | ((unsigned)f2bf(x.y) << 16), (unsigned)f2bf(x.z) | ((unsigned)f2bf(x.w) << 16));
+      } else {
+        *reinterpret_cast<u32x4*>(&xs[rl * LDXS + 8 * kv]) = xv[e];
+      }
+    }
+  }
+  __syncthreads();
+  // IN^T side output: output block y < K_IN/XTC writes features [y*XTC, (y+1)*XTC) of this row block
+  if (a.INT && blockIdx.y < K_IN / XTC && tid < XTC * 4) {
+    const int i = tid >> 2, h = (tid & 3) * 8, xk = blockIdx.y * XTC + i;
+    unsigned q[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      q[e] = (unsigned)xs[(h + 2 * e) * LDXS + xk] | ((unsigned)xs[(h + 2 * e + 1) * LDXS + xk] << 16);
+    u32x4 o; o.x = q[0]; o.y = q[1]; o.z = q[2]; o.w = q[3];
+    *reinterpret_cast<u32x4*>(a.INT + (long)xk * a.ldint + r0 + h) = o;
+  }
+
+  // ---- 3. K split over the 8 waves
+  f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    if (ks0 + t < ks1) {
+      const int k = (ks0 + t) * 32 + 8 * (lane >> 4);
+      const bf16x8 b = direct ? bg[t] : *reinterpret_cast<const bf16x8*>(&wt[(lane & 15) * LDW + k]);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        bf16x8 af = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+        if (k < K_IN) af = *reinterpret_cast<const bf16x8*>(&xs[(mt * 16 + (lane & 15)) * LDXS + k]);
+        acc[mt] = mfma16x16x32(af, b, acc[mt]);
+      }
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) part[w][mt * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[mt][e];
+  __syncthreads();
+
+  // ---- 4. bias + silu + dropout per 4-row group
+  if (tid < 8 * 16) {
+    const int g4 = tid >> 4, c = tid & 15, col = j0 + c;
+    const int rowg = r0 + g4 * 4;
+    u32x4 db = {0u, 0u, 0u, 0u};
+    if (a.keep < 1.f && rowg < M) db = dropout_bits(a.seed, doff, dropout_group(0, rowg, col, M, N));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int rl = g4 * 4 + e, row = r0 + rl;
+      float hv = 0.f;
+      if (row < M) {
+        float v = bsh[c];
+#pragma unroll
+        for (int q = 0; q < NW; ++q) v += part[q][rl][c];
+        const bf16_t zb = f2bf(v);
+        a.Z[(long)row * N + col] = zb;
+        hv = act_fwd(ACT_SILU, bf2f(zb));
+        if (a.keep < 1.f) hv = keep_word(db, e, a.keep) ? hv / a.keep : 0.f;
+        const bf16_t hb = f2bf(hv);
+        a.Hout[(long)row * N + col] = hb;
+        hv = bf2f(hb);
+      }
+      htile[rl][c] = hv;
+    }
+  }
+  if (HEAD) {
+    __syncthreads();
+    float* lg = a.logits + (long)par * M * C;
+    if (tid < 32 * C) {
+      const int rl = tid / C, c = tid % C, row = r0 + rl;
+      if (row < M) {
+        float s = (blockIdx.y == 0) ? bf2f(a.bh[c]) : 0.f;
+#pragma unroll
+        for (int n = 0; n < 16; ++n) s += htile[rl][n] * whs[n][c];
+        atomicAdd(lg + (long)row * C + c, s);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- backward
+template <int K_IN, bool TOP, int C, int KC, int NN>
+__global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
+  constexpr int NT = MD_NT, NW = MD_NW, MPM = MD_MPM;
+  constexpr int LDM = MPM + 8;
+  constexpr int NTILE = KC / 16;           // dW output tiles (one per wave)
+  constexpr int NKS = NN / 32;             // k-steps of the dZ_{i+1} W_{i+1}^T product
+  static_assert(KC % 16 == 0 && K_IN % KC == 0 && NTILE <= NW - 1, "tile plan");
+  static_assert((MPM / 4) * 16 == NT, "one 4-row group per thread");
+  __shared__ float dlog[TOP ? MPM : 1][C + 1];
+  __shared__ __attribute__((aligned(16))) bf16_t dzT[16 * LDM];
+  __shared__ __attribute__((aligned(16))) bf16_t hT[16 * LDM];     // H_i[:, blk]^T (TOP, chunk-0)
+  __shared__ __attribute__((aligned(16))) bf16_t dlT[16 * LDM];    // dlogits^T (TOP)
+  __shared__ float whs[16][C];
+  __shared__ float red[2][NW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int M = a.M, N = a.N, Mp = (M + 31) & ~31;
+  const int j0 = blockIdx.x * 16, kc0 = blockIdx.y * KC;
+  const bool chunk0 = blockIdx.y == 0;
+  const int step = a.step[0], par = step & 1;
+  const bool lead = TOP && blockIdx.x == 0 && blockIdx.y == 0;
+  const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
+  const int rg = tid >> 4, gn = tid & 15;   // TOP: this thread's group (rows 4rg..4rg+3, column j0+gn)
+
+  // ---- 0. every global load up front
+  float lrow[TOP ? C : 1];
+  int lab = 0;
+  bf16_t zv[4], hv[4];
+  bf16x8 dzf[TOP ? 1 : NKS], wnf[TOP ? 1 : NKS];
+  float whv = 0.f;
+  if constexpr (TOP) {
+    const float* lg = a.logits + (long)par * M * C;
+    if (tid < M) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) lrow[c] = lg[(long)tid * C + c];
+      lab = a.labels[tid];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = rg * 4 + e;
+      zv[e] = 0; hv[e] = 0;
+      if (m < M) {
+        zv[e] = a.Z[(long)m * N + j0 + gn];
+        if (chunk0) hv[e] = a.Hout[(long)m * N + j0 + gn];
+      }
+    }
+    const bf16_t* Wh = par ? a.Wh1 : a.Wh0;
+    if (tid < 16 * C) whv = bf2f(Wh[(long)(j0 + tid / C) * C + tid % C]);
+  } else {
+    // wave w: rows 16w..16w+15 of dZ_i[:, blk] = dZ_{i+1} . W_{i+1}[blk, :]^T
+    const bf16_t* Wn = par ? a.Wn1 : a.Wn0;
+    const int row = w * 16 + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      dzf[ks] = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+      if (row < M) dzf[ks] = *reinterpret_cast<const bf16x8*>(a.dZn + (long)row * NN + ks * 32 + 8 * (lane >> 4));
+      wnf[ks] = *reinterpret_cast<const bf16x8*>(Wn + (long)(j0 + (lane & 15)) * NN + ks * 32 + 8 * (lane >> 4));
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = w * 16 + (lane >> 4) * 4 + e;
+      zv[e] = 0;
+      if (m < M) zv[e] = a.Z[(long)m * N + j0 + (lane & 15)];
+    }
+  }
+  // A fragments of this wave's dW tile from IN^T (zero-padded to Mp samples)
+  bf16x8 xf[MPM / 32];
+#pragma unroll
+  for (int ks = 0; ks < MPM / 32; ++ks) {
+    xf[ks] = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    if (w < NTILE && ks < Mp / 32)
+      xf[ks] = *reinterpret_cast<const bf16x8*>(a.INT + (long)(kc0 + w * 16 + (lane & 15)) * a.ldint + ks * 32 +
+                                                8 * (lane >> 4));
+  }
+  float op[4], om[4], ov[4];
+  const int trow0 = kc0 + w * 16 + (lane >> 4) * 4;
+  const int tcol = j0 + (lane & 15);
+  const bool aux = chunk0 && w == NW - 1;
+  const int ac = lane & 15;
+  float bp[4], bm[4], bvv[4], qp = 0.f, qm = 0.f, qv = 0.f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    op[e] = om[e] = ov[e] = 0.f;
+    bp[e] = bm[e] = bvv[e] = 0.f;
+    if (a.fuse_opt && w < NTILE) {
+      const long idx = (long)(trow0 + e) * N + tcol;
+      op[e] = a.pW[idx]; om[e] = a.mW[idx]; ov[e] = a.vW[idx];
+    }
+    if (a.fuse_opt && aux) {
+      const int n = (lane >> 4) * 4 + e;
+      if (TOP && ac < C) {
+        const long g = (long)(j0 + n) * C + ac;
+        op[e] = a.pWh[g]; om[e] = a.mWh[g]; ov[e] = a.vWh[g];
+      }
+      if (ac == 0) { bp[e] = a.pb[j0 + n]; bm[e] = a.mb[j0 + n]; bvv[e] = a.vb[j0 + n]; }
+    }
+  }
+  if (TOP && a.fuse_opt && aux && lead && lane < C) { qp = a.pbh[lane]; qm = a.mbh[lane]; qv = a.vbh[lane]; }
+  const MdAdam ak = md_adam_consts(a, step);
+
+  // ---- 1/2. dZ_i[:, blk] -> dzT[n][m] (bf16), dZout (chunk-0)
+  float l_loss = 0.f, l_corr = 0.f;
+  if constexpr (TOP) {
+    if (tid < M) {
+      float mx = -INFINITY;
+      int am = 0;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        lrow[c] = round_bf(lrow[c]);
+        if (lrow[c] > mx) { mx = lrow[c]; am = c; }
+      }
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < C; ++c) s += __expf(lrow[c] - mx);
+      const float lse = mx + __logf(s);
+      l_loss = lse - lrow[lab];
+      l_corr = (am == lab) ? 1.f : 0.f;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const bf16_t gb = f2bf((__expf(lrow[c] - lse) - (c == lab ? 1.f : 0.f)) * a.inv_mb);
+        dlog[tid][c] = bf2f(gb);
+        dlT[c * LDM + tid] = gb;
+      }
+    } else if (tid < MPM) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) dlT[c * LDM + tid] = 0;
+    }
+    for (int idx = tid; idx < (16 - C) * MPM; idx += NT) dlT[(C + idx / MPM) * LDM + idx % MPM] = 0;
+    if (tid < 16 * C) whs[tid / C][tid % C] = whv;
+    if (lead) {
+      l_loss = wave_sum(l_loss);
+      l_corr = wave_sum(l_corr);
+      if (lane == 0) { red[0][w] = l_loss; red[1][w] = l_corr; }
+      float* nxt = a.logits + (long)(par ^ 1) * M * C;   // re-arm next step's accumulator
+      for (int i = tid; i < M * C; i += NT) nxt[i] = 0.f;
+    }
+    __syncthreads();
+    u32x4 db = {0u, 0u, 0u, 0u};
+    if (a.keep < 1.f && rg * 4 < M) db = dropout_bits(a.seed, doff, dropout_group(0, rg * 4, j0 + gn, M, N));
+    unsigned packed[2] = {0u, 0u};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = rg * 4 + e;
+      float v = 0.f;
+      if (m < M) {
+        float dh = 0.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) dh += dlog[m][c] * whs[gn][c];
+        v = dh * act_grad(ACT_SILU, bf2f(zv[e]));
+        if (a.keep < 1.f) v = keep_word(db, e, a.keep) ? v / a.keep : 0.f;
+      }
+      const bf16_t vb = f2bf(v);
+      packed[e >> 1] |= (unsigned)vb << (16 * (e & 1));
+      if (chunk0 && a.dZout && m < M) a.dZout[(long)m * N + j0 + gn] = vb;
+    }
+    *reinterpret_cast<uint2*>(&dzT[gn * LDM + rg * 4]) = make_uint2(packed[0], packed[1]);
+    if (chunk0)
+      *reinterpret_cast<uint2*>(&hT[gn * LDM + rg * 4]) =
+          make_uint2((unsigned)hv[0] | ((unsigned)hv[1] << 16), (unsigned)hv[2] | ((unsigned)hv[3] << 16));
+  } else {
+    if (w * 16 < Mp) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) acc = mfma16x16x32(dzf[ks], wnf[ks], acc);
+      const int row0 = w * 16 + (lane >> 4) * 4, col = j0 + (lane & 15);
+      u32x4 db = {0u, 0u, 0u, 0u};
+      if (a.keep < 1.f && row0 < M) db = dropout_bits(a.seed, doff, dropout_group(0, row0, col, M, N));
+      unsigned packed[2] = {0u, 0u};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = row0 + e;
+        float v = 0.f;
+        if (m < M) {
+          v = acc[e] * act_grad(ACT_SILU, bf2f(zv[e]));
+          if (a.keep < 1.f) v = keep_word(db, e, a.keep) ? v / a.keep : 0.f;
+        }
+        const bf16_t vb = f2bf(v);
+        packed[e >> 1] |= (unsigned)vb << (16 * (e & 1));
+        if (chunk0 && a.dZout && m < M) a.dZout[(long)m * N + col] = vb;
+      }
+      *reinterpret_cast<uint2*>(&dzT[(lane & 15) * LDM + row0]) = make_uint2(packed[0], packed[1]);
+    }
+  }
+  __syncthreads();
+
+  // ---- 3. dW_i[chunk, blk] = IN[:, chunk]^T dZ_i[:, blk]; spare wave: db_i (+ head grads)
+  if (w < NTILE) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < MPM / 32; ++ks) {
+      if (ks < Mp / 32) {
+        const int kk = ks * 32 + 8 * (lane >> 4);
+        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
+        acc = mfma16x16x32(xf[ks], bfr, acc);
+      }
+    }
+    bf16_t* Wsn = const_cast<bf16_t*>(par ? a.Ws0 : a.Ws1);   // next step's parity of the row-major shadow
+    unsigned wtp[2] = {0u, 0u};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long idx = (long)(trow0 + e) * N + tcol;
+      if (a.fuse_opt) {
+        const bf16_t pb = f2bf(md_adam(op[e], om[e], ov[e], acc[e], ak, a.pW + idx, a.mW + idx, a.vW + idx));
+        Wsn[idx] = pb;
+        wtp[e >> 1] |= (unsigned)pb << (16 * (e & 1));
+      } else {
+        a.gW[idx] = acc[e];
+      }
+    }
+    if (a.fuse_opt && a.WTout)
+      *reinterpret_cast<uint2*>(a.WTout + (long)tcol * a.ldwt + trow0) = make_uint2(wtp[0], wtp[1]);
+  } else if (aux) {
+    bf16x8 ones;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ones[q] = (short)0x3f80;  // bf16 1.0
+    f32x4 aw = {0.f, 0.f, 0.f, 0.f}, ab = {0.f, 0.f, 0.f, 0.f}, ab2 = {0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < Mp / 32; ++ks) {
+      const int kk = ks * 32 + 8 * (lane >> 4);
+      const bf16x8 zT = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
+      ab = mfma16x16x32(zT, ones, ab);
+      if constexpr (TOP) {
+        const bf16x8 h = *reinterpret_cast<const bf16x8*>(&hT[(lane & 15) * LDM + kk]);
+        const bf16x8 d = *reinterpret_cast<const bf16x8*>(&dlT[(lane & 15) * LDM + kk]);
+        aw = mfma16x16x32(h, d, aw);
+        if (lead) ab2 = mfma16x16x32(ones, d, ab2);
+      }
+    }
+    bf16_t* Whn = const_cast<bf16_t*>(par ? a.Wh0 : a.Wh1);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = (lane >> 4) * 4 + e;
+      if (TOP && ac < C) {
+        const long g = (long)(j0 + n) * C + ac;
+        if (a.fuse_opt) Whn[g] = f2bf(md_adam(op[e], om[e], ov[e], aw[e], ak, a.pWh + g, a.mWh + g, a.vWh + g));
+        else a.gWh[g] = aw[e];
+      }
+      if (ac == 0) {
+        const int j = j0 + n;
+        if (a.fuse_opt) a.sb[j] = f2bf(md_adam(bp[e], bm[e], bvv[e], ab[e], ak, a.pb + j, a.mb + j, a.vb + j));
+        else a.gb[j] = ab[e];
+      }
+    }
+    if (TOP && lead && lane < C) {
+      if (a.fuse_opt) a.sbh[lane] = f2bf(md_adam(qp, qm, qv, ab2[0], ak, a.pbh + lane, a.mbh + lane, a.vbh + lane));
+      else a.gbh[lane] = ab2[0];
+    }
+  }
+  if (TOP && lead) {
+    __syncthreads();
+    if (tid == 0) {
+      float L = 0.f, Cr = 0.f;
+      for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
+      if (a.fuse_opt && a.running) {
+        a.running[0] += L; a.running[1] += (float)M; a.running[2] += Cr; a.running[3] += (float)M;
+      } else if (a.mslot) {
+        a.mslot[0] = L; a.mslot[1] = (float)M; a.mslot[2] = Cr; a.mslot[3] = (float)M;
+      }
+    }
+  }
+  if (a.advance_step) {
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned t = atomicAdd(a.ticket, 1u);
+      if (t == gridDim.x * gridDim.y - 1) {
+        a.step[0] = step + 1;
+        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+}  // namespace jdt
+using namespace jdt;
+
+JDT_API int jdt_md_args_size() { return (int)sizeof(MdArgs); }
+
+// phase 0: forward of one hidden layer (head = 1: + head logits); phase 1: backward
+// (head = 1: TOP layer, CE through the head).  Instantiated for the tutorial
+// shapes: K in {784 (fp32 data), 512}, N = NN = 512, C = 10, M <= 128.
+JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) {
+  const MdArgs& a = *args;
+  if (a.N != 512 || a.M <= 0 || a.M > MD_MPM || (a.K != 784 && a.K != 512) || (head && a.C != 10)) return -3;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const dim3 blk(MD_NT);
+  if (phase == 0) {
+    const dim3 grid((a.M + 31) / 32, a.N / 16);
+    if (a.K == 784) {
+      if (head) return -3;
+      hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, false, 10>), grid, blk, 0, st, a);
+    } else if (head) {
+      hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, true, 10>), grid, blk, 0, st, a);
+    } else {
+      hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10>), grid, blk, 0, st, a);
+    }
+  } else {
+    if (a.K == 784) {
+      if (head) return -3;
+      hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512>), dim3(a.N / 16, 784 / 112), blk, 0, st, a);
+    } else if (head) {
+      hipLaunchKernelGGL((md_bwd_kernel<512, true, 10, 64, 512>), dim3(a.N / 16, 512 / 64), blk, 0, st, a);
+    } else {
+      hipLaunchKernelGGL((md_bwd_kernel<512, false, 10, 64, 512>), dim3(a.N / 16, 512 / 64), blk, 0, st, a);
+    }
+  }
+  return HIP_LAUNCH_CHECK();
+}

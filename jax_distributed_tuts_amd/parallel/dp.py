@@ -106,13 +106,13 @@ class DataParallelTrainer:
         if self.cfg.accum != "kernel":
             return None
         if self.fused is None:
-            from .fused_mlp import FusedMLP2, supported
+            from .fused_mlp import make_engine
 
-            if not supported(self.model, batch.size, batch.inputs.device):
+            self.fused = make_engine(self.state, self.mesh, self.cfg.axis, self.cfg.num_minibatches, batch.size,
+                                     self.metrics, batch.inputs.device)
+            if self.fused is None:
                 self.cfg.accum = "fused"  # shapes outside the fused kernels' envelope
                 return None
-            self.fused = FusedMLP2(self.state, self.mesh, self.cfg.axis, self.cfg.num_minibatches, batch.size,
-                                   self.metrics)
         return self.fused
 
     # ------------------------------------------------------------------ pieces

@@ -391,13 +391,14 @@ class FSDPTrainer:
             return False
         sp = self.sp
         if self.fused is None:
-            from .fused_mlp import FusedMLP2, supported
+            from .fused_mlp import make_engine
 
-            if not supported(self.model, batch.size, batch.inputs.device):
+            self.fused = make_engine(self.state, self.mesh, self.cfg.axis, self.cfg.num_minibatches, batch.size,
+                                     self.metrics, batch.inputs.device, params=sp.full,
+                                     mslot=sp.local.metrics_slot, fuse_opt=False)
+            if self.fused is None:
                 self.cfg.fused_kernels = False
                 return False
-            self.fused = FusedMLP2(self.state, self.mesh, self.cfg.axis, self.cfg.num_minibatches, batch.size,
-                                   self.metrics, params=sp.full, mslot=sp.local.metrics_slot, fuse_opt=False)
         sp.gather()
         self.fused.forward_backward(batch)
         sp.scatter_grads(accumulate=False, zero_full=False)

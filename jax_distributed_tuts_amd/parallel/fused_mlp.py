@@ -155,3 +155,192 @@ class FusedMLP2:
         P = self.state.params
         if self.fuse_opt and int(self.state.opt_state["count"].item()) % 2 == 1:
             P.s("output_dense/kernel").copy_(self.W2s1)
+
+
+# ----------------------------------------------------------------------------- deep MLPs (csrc/mlp_deep.hip)
+class MdArgs(ctypes.Structure):
+    """Mirror of ``jdt::MdArgs`` (field order and types must match)."""
+
+    _fields_ = [("M", c_int), ("K", c_int), ("N", c_int), ("C", c_int), ("inv_mb", c_float),
+                ("X", c_void_p), ("Ws0", c_void_p), ("Ws1", c_void_p), ("WT", c_void_p), ("ldwt", c_int),
+                ("bs", c_void_p), ("Z", c_void_p), ("Hout", c_void_p), ("INT", c_void_p), ("ldint", c_int),
+                ("Wh0", c_void_p), ("Wh1", c_void_p), ("bh", c_void_p), ("logits", c_void_p), ("labels", c_void_p),
+                ("keep", c_float), ("seed", c_ulonglong), ("offset", c_ulonglong),
+                ("step", c_void_p), ("ticket", c_void_p), ("advance_step", c_int),
+                ("dZn", c_void_p), ("Wn0", c_void_p), ("Wn1", c_void_p), ("dZout", c_void_p),
+                ("fuse_opt", c_int),
+                ("gW", c_void_p), ("gb", c_void_p), ("gWh", c_void_p), ("gbh", c_void_p), ("mslot", c_void_p),
+                ("pW", c_void_p), ("mW", c_void_p), ("vW", c_void_p),
+                ("pb", c_void_p), ("mb", c_void_p), ("vb", c_void_p),
+                ("sb", c_void_p), ("WTout", c_void_p),
+                ("pWh", c_void_p), ("mWh", c_void_p), ("vWh", c_void_p),
+                ("pbh", c_void_p), ("mbh", c_void_p), ("vbh", c_void_p), ("sbh", c_void_p),
+                ("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float), ("wd", c_float),
+                ("gscale", c_float), ("running", c_void_p)]
+
+
+_lib.declare("jdt_md_layer", c_int, [ctypes.POINTER(MdArgs), c_int, c_int, c_void_p])
+_lib.declare("jdt_md_args_size", c_int, [])
+
+DEEP_H = 512
+
+
+def supported_deep(model, rows: int, device) -> bool:
+    """784 -> 512 x (L-1) -> 10 MLPs with L >= 3 (the 4-layer MLP of BASELINE configs #2/#3)."""
+    from ..models.mlp import MLP
+
+    return (torch.device(device).type == "cuda" and isinstance(model, MLP) and model.L >= 3
+            and model.dims[0] == 784 and all(d == DEEP_H for d in model.dims[1:-1]) and model.dims[-1] == 10
+            and 0 < rows <= 128 and model.act == "silu" and not model.final_act)
+
+
+class FusedMLPDeep:
+    """One forward and one backward launch per hidden layer (csrc/mlp_deep.hip);
+    same interface as :class:`FusedMLP2`."""
+
+    def __init__(self, state, mesh, axis: str, num_minibatches: int, rows: int, metrics: torch.Tensor,
+                 params=None, mslot: Optional[torch.Tensor] = None, fuse_opt: Optional[bool] = None):
+        P = params if params is not None else state.params
+        self.P = P
+        self.mslot = mslot if mslot is not None else P.metrics_slot
+        self.state, self.mesh, self.axis = state, mesh, axis
+        self.world = C.axis_size(mesh, axis)
+        self.n_mb = num_minibatches
+        self.model = m = state.apply_fn
+        self.metrics = metrics
+        self.rows = rows
+        dev = P.master.device
+        H, L = DEEP_H, m.L
+        self.nh = L - 1                                    # hidden layers
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        self.Z = [torch.empty(rows, H, **bf) for _ in range(self.nh)]
+        self.Hs = [torch.empty(rows, H, **bf) for _ in range(self.nh)]
+        self.dZ = [None] + [torch.empty(rows, H, **bf) for _ in range(1, self.nh)]
+        self.Mp = (rows + 31) // 32 * 32
+        self.INT = [torch.zeros(m.dims[i], self.Mp, **bf) for i in range(self.nh)]
+        self.logits = torch.zeros(2, rows, 10, dtype=torch.float32, device=dev)
+        if fuse_opt is None:
+            fuse_opt = self.world == 1 and os.environ.get("JDT_FUSED_OPT", "1") == "1"
+        self.fuse_opt = bool(fuse_opt) and params is None
+        kn = [f"{n}/kernel" for n in m.names]
+        self.kn, self.bn = kn, [f"{n}/bias" for n in m.names]
+        # second step-parity copy of the row-major shadows read after being updated in
+        # the same step: hidden layers >= 1 (by the previous layer's backward) and the head
+        self.par = {}
+        self.WT = [None] * self.nh
+        if self.fuse_opt:
+            for i in list(range(1, self.nh)) + [L - 1]:
+                self.par[i] = P.s(kn[i]).clone()
+            for i in range(self.nh):
+                kp = (m.dims[i] + 31) // 32 * 32
+                self.WT[i] = torch.zeros(H, kp, **bf)
+                self.WT[i][:, : m.dims[i]].copy_(P.s(kn[i]).t())
+        if _lib.lib().jdt_md_args_size() != ctypes.sizeof(MdArgs):
+            raise RuntimeError("MdArgs layout mismatch")
+        self._args = None
+        self._key = None
+
+    def _shadow_pair(self, i):
+        s0 = self.P.s(self.kn[i]).data_ptr()
+        return s0, (self.par[i].data_ptr() if i in self.par else s0)
+
+    def _layer(self, batch, i: int, phase: int) -> MdArgs:
+        st, P, m = self.state, self.P, self.model
+        o = st.opt_state
+        L = m.L
+        top = i == self.nh - 1
+        a = MdArgs()
+        a.M, a.K, a.N, a.C = self.rows, m.dims[i], DEEP_H, 10
+        a.inv_mb = 1.0 / (self.rows // self.n_mb)
+        a.X = batch.inputs.data_ptr() if i == 0 else self.Hs[i - 1].data_ptr()
+        a.Ws0, a.Ws1 = self._shadow_pair(i)
+        if self.WT[i] is not None:
+            if phase == 0:
+                a.WT = self.WT[i].data_ptr()
+            else:
+                a.WTout = self.WT[i].data_ptr()
+            a.ldwt = self.WT[i].shape[1]
+        a.bs = P.s(self.bn[i]).data_ptr()
+        a.Z, a.Hout = self.Z[i].data_ptr(), self.Hs[i].data_ptr()
+        a.INT, a.ldint = self.INT[i].data_ptr(), self.Mp
+        a.Wh0, a.Wh1 = self._shadow_pair(L - 1)
+        a.bh = P.s(self.bn[L - 1]).data_ptr()
+        a.logits, a.labels = self.logits.data_ptr(), batch.labels.data_ptr()
+        a.keep = 1.0 - m.dropout_rate
+        from ..utils import rng as R
+
+        a.seed = R.fold_rng_over_axis(st.rng, self.mesh, self.axis) & 0xFFFFFFFF
+        a.offset = (m.layer_id_base + i) << 1
+        a.step, a.ticket = o["count"].data_ptr(), o["ticket"].data_ptr()
+        a.advance_step = int(self.fuse_opt and phase == 1 and i == 0)
+        if not top:
+            a.dZn = self.dZ[i + 1].data_ptr()
+            a.Wn0, a.Wn1 = self._shadow_pair(i + 1)
+        if i >= 1:
+            a.dZout = self.dZ[i].data_ptr()
+        a.fuse_opt = int(self.fuse_opt)
+        a.gW, a.gb = P.g(self.kn[i]).data_ptr(), P.g(self.bn[i]).data_ptr()
+        a.gWh, a.gbh = P.g(self.kn[L - 1]).data_ptr(), P.g(self.bn[L - 1]).data_ptr()
+        a.mslot = self.mslot.data_ptr()
+        if self.fuse_opt:
+            mm, vv = o["m"], o["v"]
+
+            def trio(name):
+                off = P.offsets[name][0]
+                return P.p(name).data_ptr(), mm[off:].data_ptr(), vv[off:].data_ptr()
+
+            a.pW, a.mW, a.vW = trio(self.kn[i])
+            a.pb, a.mb, a.vb = trio(self.bn[i])
+            a.sb = P.s(self.bn[i]).data_ptr()
+            a.pWh, a.mWh, a.vWh = trio(self.kn[L - 1])
+            a.pbh, a.mbh, a.vbh = trio(self.bn[L - 1])
+            a.sbh = P.s(self.bn[L - 1]).data_ptr()
+            tx = st.tx
+            a.lr, a.beta1, a.beta2, a.eps, a.wd = tx.learning_rate, tx.b1, tx.b2, tx.eps, tx.weight_decay
+            a.gscale = 1.0 / self.n_mb
+            a.running = self.metrics.data_ptr()
+        return a
+
+    def forward_backward(self, batch):
+        key = (batch.inputs.data_ptr(), batch.labels.data_ptr(), self.state.rng)
+        if self._args is None or self._key != key:
+            fwd = [self._layer(batch, i, 0) for i in range(self.nh)]
+            bwd = [self._layer(batch, i, 1) for i in reversed(range(self.nh))]
+            self._args, self._key = (fwd, bwd), key
+        Lb = _lib.lib()
+        s = _lib.stream_ptr()
+        fwd, bwd = self._args
+        for i, a in enumerate(fwd):
+            _lib.check(Lb.jdt_md_layer(ctypes.byref(a), 0, int(i == self.nh - 1), s), "md_fwd")
+        for j, a in enumerate(bwd):
+            _lib.check(Lb.jdt_md_layer(ctypes.byref(a), 1, int(j == 0), s), "md_bwd")
+
+    def step(self, batch):
+        self.forward_backward(batch)
+        if not self.fuse_opt:
+            P = self.state.params
+            with named_scope("sync_grads"):
+                C.psum_(P.grad, self.mesh, self.axis)
+            self.state.tx.update(P, self.state.opt_state, 1.0 / (self.n_mb * self.world), zero_grad=False)
+            with named_scope("sync_metrics"):
+                K.metrics_fold_(self.metrics, P.metrics_slot)
+
+    def finalize(self):
+        """Bring the generic bf16 shadows up to date (parity copies in use on odd steps)."""
+        if self.fuse_opt and int(self.state.opt_state["count"].item()) % 2 == 1:
+            for i, t in self.par.items():
+                self.P.s(self.kn[i]).copy_(t)
+
+
+def make_engine(state, mesh, axis: str, num_minibatches: int, rows: int, metrics: torch.Tensor, device,
+                params=None, mslot: Optional[torch.Tensor] = None, fuse_opt: Optional[bool] = None):
+    """The whole-step fused engine for ``state.apply_fn`` (2-layer or deep), or None
+    if the model/shape is outside the fused kernels' envelope."""
+    model = state.apply_fn
+    if supported(model, rows, device):
+        return FusedMLP2(state, mesh, axis, num_minibatches, rows, metrics, params=params, mslot=mslot,
+                         fuse_opt=fuse_opt)
+    if supported_deep(model, rows, device):
+        return FusedMLPDeep(state, mesh, axis, num_minibatches, rows, metrics, params=params, mslot=mslot,
+                            fuse_opt=fuse_opt)
+    return None

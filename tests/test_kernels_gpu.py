@@ -285,7 +285,8 @@ def test_transformer_step_gpu_matches_cpu():
 
 @pytest.mark.parametrize("fused_opt", ["1", "0"])
 @pytest.mark.parametrize("rows", [128, 32, 16])
-def test_fused_mlp_step_matches_generic(fused_opt, rows, monkeypatch):
+@pytest.mark.parametrize("layers", [2, 3, 4])
+def test_fused_mlp_step_matches_generic(fused_opt, rows, layers, monkeypatch):
     """Whole-step fused kernels (mlp2_fwd/mlp2_bwd, optionally with AdamW in the
     epilogue) == the generic-kernel path over the same rows (same Philox dropout
     stream: row*H + col under (seed, step))."""
@@ -299,7 +300,7 @@ def test_fused_mlp_step_matches_generic(fused_opt, rows, monkeypatch):
     y = torch.randint(0, 10, (rows,), generator=g).to(torch.int32).to(DEV)
     out = {}
     for accum in ("fused", "kernel"):
-        st = init_dp(Classifier(), adamw(1e-3), 69, DEV)
+        st = init_dp(Classifier(num_layers=layers), adamw(1e-3), 69, DEV)
         tr = DataParallelTrainer(st, None, DPConfig(4, accum))
         for _ in range(3):
             tr.step(Batch(x, y))
@@ -317,7 +318,8 @@ def test_fused_mlp_step_matches_generic(fused_opt, rows, monkeypatch):
     assert float(sd.max()) <= 1e-2
 
 
-def test_fused_mlp_graph_capture():
+@pytest.mark.parametrize("layers", [2, 4])
+def test_fused_mlp_graph_capture(layers):
     from jax_distributed_tuts_amd.models.mlp import Classifier
     from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
     from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
@@ -327,7 +329,7 @@ def test_fused_mlp_graph_capture():
     y = torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV)
     res = []
     for graph in (False, True):
-        st = init_dp(Classifier(), adamw(1e-3), 69, DEV)
+        st = init_dp(Classifier(num_layers=layers), adamw(1e-3), 69, DEV)
         tr = DataParallelTrainer(st, None, DPConfig(4, "kernel"))
         tr.step(Batch(x, y))
         if graph:
@@ -367,7 +369,8 @@ def test_multi_step_graph_equals_single_steps():
     _close(res[1][1], res[0][1], rtol=1e-4, atol=1e-2)
 
 
-def test_fsdp_fused_kernels_match_generic():
+@pytest.mark.parametrize("layers", [2, 4])
+def test_fsdp_fused_kernels_match_generic(layers):
     """FSDP (world 1) with the fused classifier kernels on the gathered buffer ==
     FSDP with the generic kernels (gather/scatter once).  Dropout off: the generic
     path indexes the dropout stream per minibatch, the fused one per device pass."""
@@ -379,7 +382,7 @@ def test_fsdp_fused_kernels_match_generic():
     b = Batch(torch.randn(128, 784, generator=g).to(DEV), torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV))
     res = []
     for fused in (False, True):
-        st = init_fsdp(Classifier(dropout_rate=0.0), adamw(1e-3), 69, DEV, None, "data", 16)
+        st = init_fsdp(Classifier(dropout_rate=0.0, num_layers=layers), adamw(1e-3), 69, DEV, None, "data", 16)
         tr = FSDPTrainer(st, None, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=fused))
         for _ in range(3):
             tr.step(b)

@@ -90,13 +90,14 @@ def build_pp(args, dev):
     if args.model == "transformer":
         from jax_distributed_tuts_amd.parallel.pipeline_lm import build_lm_pipeline, lm_batch
 
-        tr, lm_cfg = build_lm_pipeline(mesh, dev, num_microbatches=args.microbatches)
+        tr, lm_cfg = build_lm_pipeline(mesh, dev, num_microbatches=args.microbatches, comm=args.comm)
         batch = shard_batch(lm_batch(lm_cfg, global_batch=args.lm_batch, seed=1), mesh, "data")
         desc = {"model": f"transformer LM {lm_cfg.n_layers}L d{lm_cfg.d_model} h{lm_cfg.n_heads} "
                          f"ff{lm_cfg.d_ff} V{lm_cfg.vocab_size}", "global_batch": args.lm_batch,
                 "seq_len": lm_cfg.seq_len, "tokens_per_step": args.lm_batch * lm_cfg.seq_len}
     else:
-        tr = build_mlp_pipeline(cfg, mesh, dev, args.hidden_layers, num_microbatches=args.microbatches)
+        tr = build_mlp_pipeline(cfg, mesh, dev, args.hidden_layers, num_microbatches=args.microbatches,
+                                comm=args.comm)
         batch = shard_batch(synthetic_batch(cfg, cfg.seed + 1), mesh, "data")
         desc = {"model": f"MLP 784-512x{args.hidden_layers}-10 GPipe", "global_batch": cfg.data.batch_size,
                 "seq_len": None}
@@ -140,10 +141,9 @@ def main():
     for _ in range(n_eager):
         tr.step(batch)
     sync()
-    # DP always captures its step; FSDP when its collectives are xGMI kernels (or N=1);
-    # PP's send/recv stay eager
-    use_graph = on_gpu and not args.no_graph and (args.strategy == "dp" or
-                                                  (args.strategy == "fsdp" and tr.capturable))
+    # DP always captures its step; FSDP and PP when their collectives / stage hand-offs
+    # are xGMI kernels (or N=1)
+    use_graph = on_gpu and not args.no_graph and (args.strategy == "dp" or tr.capturable)
     if use_graph and args.strategy == "dp":
         tr.capture(batch, capture_collectives=args.capture_collectives, steps_per_graph=args.steps_per_graph)
     elif use_graph:

@@ -22,6 +22,7 @@ bucket (grads + metric slots) per stage; the optimizer is the same fused AdamW.
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -35,7 +36,7 @@ from ..runtime.dist import Mesh, is_initialized
 from ..utils import rng as R
 from ..utils.flat import FlatParams, N_METRIC_SLOTS
 from ..utils.profiling import named_scope
-from ..utils.train_state import Batch, TrainState
+from ..utils.train_state import AdamW, Batch, TrainState
 
 
 def split_layers(n_layers: int, n_stages: int) -> List[range]:
@@ -74,10 +75,19 @@ class PipeConfig:
     num_microbatches: int = 4
     data_axis: str = "data"
     pipe_axis: str = "pipe"
+    comm: str = "auto"   # "auto" | "xgmi" | "rccl": stage hand-off + data-axis all-reduce
 
 
 class GPipeTrainer:
-    """Runs one stage of a GPipe schedule (``stage.forward/backward`` explicit API)."""
+    """Runs one stage of a GPipe schedule (``stage.forward/backward`` explicit API).
+
+    On GPUs of one node the stage hand-off is the xGMI inbox kernels
+    (comm/p2p.py) and the data-axis gradient sync is the xGMI all-reduce with
+    AdamW fused in (comm/xgmi.py), so the whole step -- every tick's compute,
+    send and receive, the sync and the optimizer -- is kernels on this rank's
+    stream and ``capture`` records it as one hipGraph (several steps per graph
+    with ``steps_per_graph``).  Otherwise (gloo CPU simulation, ``comm="rccl"``,
+    or if the xGMI mapping fails) the hand-off is RCCL/gloo send/recv, eager."""
 
     def __init__(self, state: TrainState, mesh: Optional[Mesh], cfg: PipeConfig, act_dtype=torch.bfloat16):
         self.state, self.mesh, self.cfg = state, mesh, cfg
@@ -87,24 +97,71 @@ class GPipeTrainer:
         self.n_dp = C.axis_size(mesh, cfg.data_axis)
         self.first, self.last = self.s == 0, self.s == self.S - 1
         self.act_dtype = act_dtype
-        dev = state.params.master.device
-        self.metrics = torch.zeros(N_METRIC_SLOTS, dtype=torch.float32, device=dev)
+        P = state.params
+        self.dev = P.master.device
+        self.metrics = torch.zeros(N_METRIC_SLOTS, dtype=torch.float32, device=self.dev)
+        self.graph = None
+        self.multi = None
+        self.p2p = None
+        self._p2p_tried = False
+        self.xg = None
+        self._xg_fused_opt = False
+        if self.dev.type == "cuda" and self.n_dp > 1:
+            from ..comm.xgmi import create_for
+
+            self.xg = create_for(mesh, cfg.data_axis, P.grad.numel(), self.dev, cfg.comm)
+            self._xg_fused_opt = self.xg is not None and isinstance(state.tx, AdamW)
 
     # ------------------------------------------------------------------ p2p
-    def _send(self, x: torch.Tensor, to: int):
-        with named_scope("pipe_send"):
-            C.send(x, self.mesh, self.cfg.pipe_axis, to)
+    def _setup_p2p(self, mb: int):
+        if self._p2p_tried or self.S == 1 or self.dev.type != "cuda":
+            return
+        self._p2p_tried = True
+        from ..comm.p2p import create_for
 
-    def _recv(self, shape, to_dtype, frm: int) -> torch.Tensor:
+        es = torch.tensor([], dtype=self.act_dtype).element_size()
+        nbytes = max(math.prod(self.model.input_shape(mb)), math.prod(self.model.output_shape(mb))) * es
+        # slot i: forward activation of microbatch i; slot n_mb + i: its gradient
+        self.p2p = create_for(self.mesh, self.cfg.pipe_axis, nbytes, 2 * self.cfg.num_microbatches, self.dev,
+                              self.cfg.comm)
+
+    def _send(self, x: torch.Tensor, to: int, slot: int):
+        with named_scope("pipe_send"):
+            if self.p2p is not None:
+                self.p2p.send(x, to, slot, self.state.step_tensor)
+            else:
+                C.send(x, self.mesh, self.cfg.pipe_axis, to)
+
+    def _recv(self, shape, to_dtype, frm: int, slot: int) -> torch.Tensor:
         with named_scope("pipe_recv"):
-            buf = torch.empty(shape, dtype=to_dtype, device=self.state.params.master.device)
+            buf = torch.empty(shape, dtype=to_dtype, device=self.dev)
+            if self.p2p is not None:
+                return self.p2p.recv(buf, slot, self.state.step_tensor)
             return C.recv(buf, self.mesh, self.cfg.pipe_axis, frm)
 
+    @property
+    def capturable(self) -> bool:
+        """Whether the step is kernels only (no host-driven collective)."""
+        return (self.dev.type == "cuda" and (self.S == 1 or self.p2p is not None)
+                and (self.n_dp == 1 or self.xg is not None))
+
+    @property
+    def comm_backend(self) -> str:
+        if self.S * self.n_dp == 1:
+            return "none"
+        if self.capturable:
+            return "xgmi"
+        from ..runtime.dist import backend
+
+        b = backend()
+        return "rccl" if b == "nccl" else (b or "none")
+
     # ------------------------------------------------------------------ step
-    def step(self, batch: Batch):
+    def _compute(self, batch: Batch):
         st, P, cfg = self.state, self.state.params, self.cfg
         n_mb = cfg.num_microbatches
         mb = batch.size // n_mb
+        self._setup_p2p(mb)
         rng = R.fold_rng_over_axis(st.rng, self.mesh, cfg.data_axis)
         seed = rng & 0xFFFFFFFF
         caches, dlogits = [None] * n_mb, [None] * n_mb
@@ -116,7 +173,7 @@ class GPipeTrainer:
             if self.first:
                 x = batch.inputs[i * mb:(i + 1) * mb]
             else:
-                x = self._recv(self.model.input_shape(mb), self.act_dtype, self.s - 1)
+                x = self._recv(self.model.input_shape(mb), self.act_dtype, self.s - 1, i)
             out, cache = self.model.forward(P, x, train=True, seed=seed, offset=i << 16, step=st.step_tensor)
             caches[i] = cache
             if self.last:
@@ -124,23 +181,87 @@ class GPipeTrainer:
                 self.loss_head(out, batch.labels[i * mb:(i + 1) * mb], d)
                 dlogits[i] = d
             else:
-                self._send(out, self.s + 1)
+                self._send(out, self.s + 1, i)
         # ---- backward, reverse microbatch order
         for i in reversed(range(n_mb)):
             if self.last:
                 dx = self.model.backward(P, caches[i], dlogits[i], dout_is_dz=True, need_dx=not self.first)
             else:
-                dh = self._recv(self.model.output_shape(mb), self.act_dtype, self.s + 1)
+                dh = self._recv(self.model.output_shape(mb), self.act_dtype, self.s + 1, n_mb + i)
                 dx = self.model.backward(P, caches[i], dh, dout_is_dz=False, need_dx=not self.first)
             if not self.first:
-                self._send(dx, self.s - 1)
+                self._send(dx, self.s - 1, n_mb + i)
             caches[i] = None
-        # ---- sync_gradients(('data','pipe')): stage params are pipe-sharded -> data only
+
+    def _sync_update(self):
+        """sync_gradients(('data','pipe')): stage params are pipe-sharded -> mean over
+        'data' only; then AdamW on the local stage and the metrics fold.  The host
+        step counter is advanced by the callers."""
+        st, P, cfg = self.state, self.state.params, self.cfg
+        scale = 1.0 / (cfg.num_microbatches * self.n_dp)
         with named_scope("sync_grads"):
-            C.psum_(P.grad, self.mesh, cfg.data_axis)
-        st.apply_gradients(grad_scale=1.0 / (n_mb * self.n_dp))
+            if self._xg_fused_opt:
+                tx, o = st.tx, st.opt_state
+                self.xg.all_reduce_adamw_(
+                    P.grad, p=P.master, m=o["m"], v=o["v"], shadow=P.shadow, n_params=P.numel,
+                    running=self.metrics, n_metrics=N_METRIC_SLOTS, lr=tx.learning_rate, b1=tx.b1, b2=tx.b2,
+                    eps=tx.eps, wd=tx.weight_decay, grad_scale=scale, step=o["count"], ticket=o["ticket"],
+                    zero_grad=True)
+                return  # AdamW + metrics fold ran inside the all-reduce kernel
+            if self.xg is not None:
+                self.xg.all_reduce_(P.grad)
+            else:
+                C.psum_(P.grad, self.mesh, cfg.data_axis)
+        st.tx.update(P, st.opt_state, scale)
         with named_scope("sync_metrics"):
             K.metrics_fold_(self.metrics, P.metrics_slot)
+
+    def step(self, batch: Batch):
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._compute(batch)
+            self._sync_update()
+        self.state.step += 1
+
+    # ------------------------------------------------------------------ hipGraph
+    def capture(self, batch: Batch, steps_per_graph: int = 1):
+        """Record the step (and a ``steps_per_graph``-step variant) as hipGraphs.
+        Every rank of the mesh must capture; the batch must stay alive."""
+        if not self.capturable:
+            raise RuntimeError("pipeline step is not capturable (host-driven collectives)")
+        self._static = batch
+
+        def body():
+            self._compute(batch)
+            self._sync_update()
+
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            body()
+        self.graph = g
+        if steps_per_graph > 1:
+            gm = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gm, pool=g.pool()):
+                for _ in range(steps_per_graph):
+                    body()
+            self.multi = (steps_per_graph, gm)
+
+    def run_steps(self, batch: Batch, n: int):
+        if self.graph is not None and self.multi is not None:
+            S, gm = self.multi
+            for _ in range(n // S):
+                gm.replay()
+            self.state.step += (n // S) * S
+            n %= S
+        for _ in range(n):
+            self.step(batch)
+
+    def finalize(self):
+        if self.p2p is not None and self.p2p.error():
+            raise RuntimeError("xgmi pipeline receive timed out on this rank (peer dead or desynchronised)")
+        if self.xg is not None and self.xg.error():
+            raise RuntimeError("xgmi collective timed out on this rank (peer dead or desynchronised)")
 
     def loss_head(self, logits, labels, dlogits):
         y = self.model.flatten_labels(labels)

@@ -93,3 +93,54 @@ def test_fsdp_over_xgmi_matches_single_device(tmp_path, fused):
     m, ref = res[0]["metrics"], tr.metrics.cpu()
     assert abs(float(m[0]) - float(ref[0])) <= 1e-3 * abs(float(ref[0])) + 1e-3
     assert float(m[1]) == float(ref[1])
+
+
+@pytest.mark.parametrize("ws", [2, 3])
+def test_p2p_inbox_roundtrip(tmp_path, ws):
+    spawn(XW.p2p_roundtrip, ws, str(tmp_path), gpu=True)
+    for r, o in enumerate(_load(tmp_path, "p2p", ws)):
+        assert o["ok"], f"rank {r}: p2p self-test failed"
+        assert o["data"] and o["err"] == 0 and o["epoch"] == 4, o
+
+
+@pytest.mark.parametrize("ws,dp", [(2, 1), (4, 2)])
+def test_pipeline_over_xgmi_matches_single_device(tmp_path, ws, dp):
+    """GPipe with the inbox hand-off captured into hipGraphs (and the fused xGMI
+    data-axis all-reduce for dp=2) == the un-split model on one device."""
+    from data_paral import synthetic_batch
+    from pipeline_parallel import pp_mlp_dims
+    from jax_distributed_tuts_amd.models.mlp import MLP
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig
+    from jax_distributed_tuts_amd.utils import rng as R
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.flat import FlatParams
+    from jax_distributed_tuts_amd.utils.train_state import Batch, TrainState, adamw
+
+    import functools
+
+    spawn(functools.partial(XW.pp_xgmi, dp=dp), ws, str(tmp_path), gpu=True)
+    res = _load(tmp_path, f"ppx{dp}", ws)
+    assert all(o["comm"] == "xgmi" and o["count"] == 4 for o in res)
+    dev = torch.device("cuda", 0)
+    cfg = dp_config()
+    model = MLP(pp_mlp_dims(cfg, 3), dropout_rate=0.0)
+    P = FlatParams(model.param_specs(), device=dev).init_(cfg.seed)
+    st = TrainState.create(apply_fn=model, params=P, tx=adamw(1e-3), rng=R.PRNGKey(cfg.seed))
+    tr = DataParallelTrainer(st, None, DPConfig(4, "loop"))
+    b = synthetic_batch(cfg, 70)
+    b = Batch(b.inputs.to(dev), b.labels.to(dev))
+    for _ in range(4):
+        tr.step(b)
+    torch.cuda.synchronize()
+    ref = {k: v.cpu() for k, v in P.state_dict().items()}
+    seen = set()
+    for o in res:
+        for k, v in o["params"].items():
+            d = (v - ref[k]).abs()
+            assert float(d.max()) <= 2 * 1e-3 * 4 + 1e-6, k
+            assert float((d > 5e-5).float().mean()) < 5e-2, k
+            seen.add(k)
+    assert seen == set(ref)
+    m, rm = res[0]["metrics"], tr.metrics.cpu()
+    assert float(m[1]) == float(rm[1]) and float(m[3]) == float(rm[3])
+    assert abs(float(m[0]) - float(rm[0])) <= 2e-3 * abs(float(rm[0])) + 1e-3

@@ -168,3 +168,79 @@ def fsdp_xgmi(outdir, fused=True, steps=3):
     _save(outdir, "fsx", {"local": {n: sp.local.p(n).cpu() for n in sp.part},
                           "dims": {n: sp.part[n].shard_dim for n in sp.part},
                           "metrics": tr.metrics.cpu(), "comm": tr.comm_backend, "xg_names": list(sp._xg_names)})
+
+
+def pp_xgmi(outdir, dp, n_hidden=3, steps=4):
+    """GPipe (dropout off) with the xGMI inbox hand-off (+ the fused xGMI all-reduce
+    on the data axis when dp > 1): one eager step, then multi-step graph replays."""
+    from data_paral import synthetic_batch
+    from pipeline_parallel import build_mlp_pipeline
+    from jax_distributed_tuts_amd.parallel.dp import shard_batch
+    from jax_distributed_tuts_amd.runtime import dist as D
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.train_state import Batch
+
+    dev = D.device()
+    cfg = dp_config()
+    mesh = D.Mesh({"data": dp, "pipe": D.world_size() // dp})
+    tr = build_mlp_pipeline(cfg, mesh, dev, n_hidden_layers=n_hidden, dropout_rate=0.0, num_microbatches=4,
+                            comm="xgmi")
+    b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
+    b = Batch(b.inputs.to(dev), b.labels.to(dev))
+    tr.step(b)
+    assert tr.capturable and tr.p2p is not None
+    tr.capture(b, steps_per_graph=2)
+    tr.run_steps(b, steps - 1)
+    torch.cuda.synchronize()
+    tr.finalize()
+    _save(outdir, f"ppx{dp}", {"params": {k: v.cpu() for k, v in tr.state.params.state_dict().items()},
+                               "metrics": tr.gather_metrics().cpu(), "comm": tr.comm_backend,
+                               "count": int(tr.state.step_tensor.item())})
+
+
+def p2p_roundtrip(outdir):
+    """Raw XgmiP2P: ring sends through every slot, eager and graph-replayed epochs."""
+    from jax_distributed_tuts_amd.comm.p2p import XgmiP2P
+    from jax_distributed_tuts_amd.runtime import dist as D
+
+    r, W, dev = D.rank(), D.world_size(), D.device()
+    mesh = D.Mesh({"pipe": W})
+    n_slots = 6
+    c = XgmiP2P(mesh.group("pipe"), r, W, 70_000, n_slots, dev, timeout_s=20.0)
+    res = {"ok": c.ok}
+    if c.ok:
+        ep = torch.zeros(1, dtype=torch.int32, device=dev)
+        sizes = [16, 4096, 65_536, 70_000 // 16 * 16]
+        xs = [torch.arange(n // 4, device=dev, dtype=torch.float32) * (r + 1) + k for k, n in enumerate(sizes)]
+        outs = [torch.empty_like(x) for x in xs]
+
+        def body():
+            for k, x in enumerate(xs):
+                c.send(x, (r + 1) % W, k, ep)
+            for k, o in enumerate(outs):
+                c.recv(o, k, ep)
+            ep.add_(1)
+
+        body()
+        torch.cuda.synchronize()
+        prev = (r - 1) % W
+        good = all(torch.equal(o, torch.arange(o.numel(), device=dev, dtype=torch.float32) * (prev + 1) + k)
+                   for k, o in enumerate(outs))
+        D.barrier()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            body()
+        for it in range(3):
+            for k, x in enumerate(xs):
+                x.add_(1)
+            torch.cuda.synchronize()
+            D.barrier()  # every rank has read the previous epoch
+            g.replay()
+            torch.cuda.synchronize()
+            good &= all(torch.equal(o, torch.arange(o.numel(), device=dev, dtype=torch.float32) * (prev + 1) + k
+                                    + it + 1) for k, o in enumerate(outs))
+        res["data"] = good
+        res["epoch"] = int(ep.item())
+        res["err"] = c.error()
+        c.close()
+    _save(outdir, "p2p", res)

@@ -42,6 +42,7 @@ _SIGS = {
     "jdt_gemm": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p]),
     "jdt_gemm_args_size": (c_int, []),
     "jdt_gemm_set_preload": (None, [c_int]),
+    "jdt_gemm_set_exact": (None, [c_int]),
     "jdt_xent": (c_int, [c_void_p, c_int, c_long, c_void_p, c_int, c_int, c_float, c_void_p, c_long, c_void_p,
                          c_void_p, c_void_p, c_void_p]),
     "jdt_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_float, c_float, c_float,
@@ -56,7 +57,7 @@ _SIGS = {
     "jdt_ln_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,
                            c_void_p]),
     "jdt_ln_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                           c_int, c_int, c_void_p]),
+                           c_void_p, c_int, c_int, c_void_p]),
     "jdt_attn_softmax_fwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "jdt_attn_softmax_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "jdt_embed_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),

@@ -77,14 +77,40 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const bf16_t* __restrict
   if (dwpe) atomicAdd(dwpe + (long)(t % S) * d + c, g);
 }
 
-__global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ x, long ld, int M, int N, int rpb,
+// out[c] += sum_r x[r, c] (bias gradients).  A lane owns 8 adjacent columns
+// (one 16-byte load per row), a wave CS_RPW rows whose loads are all issued
+// before the first add, the 4 waves of a workgroup are summed in LDS, and one
+// fp32 atomic per column per workgroup goes to the output.
+constexpr int CS_RPW = 8;
+
+__global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ x, long ld, int M, int N,
                                                     float* __restrict__ out) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= N) return;
-  const int r0 = blockIdx.y * rpb, r1 = min(M, r0 + rpb);
-  float s = 0.f;
-  for (int r = r0; r < r1; ++r) s += bf2f(x[(long)r * ld + col]);
-  atomicAdd(out + col, s);
+  __shared__ float part[4][512];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = blockIdx.x * 512 + lane * 8;
+  const int r0 = (blockIdx.y * 4 + w) * CS_RPW;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (col < N) {
+    u32x4 v[CS_RPW];
+#pragma unroll
+    for (int i = 0; i < CS_RPW; ++i) {
+      v[i] = (u32x4){0u, 0u, 0u, 0u};
+      if (r0 + i < M) v[i] = *reinterpret_cast<const u32x4*>(x + (long)(r0 + i) * ld + col);
+    }
+#pragma unroll
+    for (int i = 0; i < CS_RPW; ++i) {
+      const unsigned wv[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += bf2f((bf16_t)((wv[j >> 1] >> (16 * (j & 1))) & 0xffffu));
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[w][lane * 8 + j] = s[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 512; c += 256) {
+    const int gc = blockIdx.x * 512 + c;
+    if (gc < N) atomicAdd(out + gc, part[0][c] + part[1][c] + part[2][c] + part[3][c]);
+  }
 }
 
 }  // namespace jdt
@@ -122,9 +148,9 @@ JDT_API int jdt_embed_bwd(const void* dout, const int* tok, float* dwte, float* 
 
 JDT_API int jdt_colsum(const void* x, long ld, int M, int N, float* out, void* stream) {
   if (M <= 0 || N <= 0) return 0;
-  const int rpb = 64;
-  dim3 grid((N + 255) / 256, (M + rpb - 1) / rpb);
+  if ((N & 7) || (ld & 7) || (reinterpret_cast<uintptr_t>(x) & 15)) return -3;
+  dim3 grid((N + 511) / 512, (M + 4 * CS_RPW - 1) / (4 * CS_RPW));
   hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const bf16_t*>(x), ld, M, N, rpb, out);
+                     static_cast<const bf16_t*>(x), ld, M, N, out);
   return HIP_LAUNCH_CHECK();
 }

@@ -168,6 +168,24 @@ __device__ __forceinline__ RawChunk<F32> load_raw(const void* base, long ld, boo
   return out;
 }
 
+// Interior-tile load: the whole chunk is in bounds and 16-byte aligned, so it is
+// one (bf16) or two (fp32) unconditional vector loads.  Keeping guards out of
+// this path matters beyond the saved compares: hipcc waits vmcnt(0) at every
+// join of a guarded scalar-load fallback, which would serialise the K-tiles.
+template <bool F32>
+__device__ __forceinline__ RawChunk<F32> load_fast(const void* base, long ld, bool trans, int r, int k) {
+  RawChunk<F32> out;
+  const long off = trans ? (long)k * ld + r : (long)r * ld + k;
+  if constexpr (F32) {
+    const float4* p = reinterpret_cast<const float4*>(static_cast<const float*>(base) + off);
+    out.x = p[0];
+    out.y = p[1];
+  } else {
+    out.v = *reinterpret_cast<const u32x4*>(static_cast<const bf16_t*>(base) + off);
+  }
+  return out;
+}
+
 template <bool F32>
 __device__ __forceinline__ u32x4 raw_to_bf16(const RawChunk<F32>& c) {
   if constexpr (F32) {
@@ -200,12 +218,16 @@ __device__ __forceinline__ void store_chunk(bf16_t* lds, bool trans, int r, int 
   }
 }
 
-template <int WM, int WN, int TM, int TN, int BK, bool AF32, bool BF32, int PRE>
+template <int WM, int WN, int TM, int TN, int BK, bool AF32, bool BF32, int PRE, bool EXACT = false>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int vecA, int vecB, int splits,
                                                    int kchunk, float* __restrict__ ws, unsigned* counters) {
   using T = Tile<WM, WN, TM, TN, BK>;
   constexpr int BM = T::BM, BN = T::BN, LDK = T::LDK;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (BM + BN) * LDK];
+  // EXACT slices keep the whole K-slice resident (one image, one barrier);
+  // the other paths double-buffer one K-tile.
+  constexpr int LDX = PRE * BK + 8;
+  constexpr int SMEM = EXACT ? (BM + BN) * LDX : 2 * (BM + BN) * LDK;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM];
   // buffer b: A image at smem + b*(BM+BN)*LDK, B image right after it
 #define AS(b) (smem + (b) * (BM + BN) * LDK)
 #define BS(b) (smem + (b) * (BM + BN) * LDK + BM * LDK)
@@ -300,7 +322,80 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
     }
   };
 
-  if constexpr (PRE > 0) {
+  if constexpr (EXACT) {
+    // Exact slice (host-checked: every tile interior, aligned rows, and this
+    // slice is exactly PRE K-tiles): straight-line code with no runtime guard,
+    // so hipcc issues all PRE K-tiles' loads back to back and retires them with
+    // counted vmcnt waits while they are written into ONE LDS image of the
+    // whole slice -- one global round trip, one barrier, then every MFMA of the
+    // slice back to back (no per-K-tile barrier: at these sizes the barrier
+    // chain, not the MFMA, was the cost).
+    bf16_t* As = smem;
+    bf16_t* Bs = smem + BM * LDX;
+    RawChunk<AF32> pa[PRE][T::A_PER_T];
+    RawChunk<BF32> pb[PRE][T::B_PER_T];
+#pragma unroll
+    for (int kt = 0; kt < PRE; ++kt) {
+      const int kb = kbeg + kt * BK;
+#pragma unroll
+      for (int i = 0; i < T::A_PER_T; ++i) {
+        const int c = tid + i * 256;
+        if (T::A_CHUNKS % 256 == 0 || c < T::A_CHUNKS) {
+          const int2 rk = chunk_rk<BK>(c, g.a_trans);
+          pa[kt][i] = load_fast<AF32>(Ab, g.lda, g.a_trans, rk.x, kb + rk.y);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < T::B_PER_T; ++i) {
+        const int c = tid + i * 256;
+        if (T::B_CHUNKS % 256 == 0 || c < T::B_CHUNKS) {
+          const int2 rk = chunk_rk<BK>(c, g.b_trans);
+          pb[kt][i] = load_fast<BF32>(Bb, g.ldb, g.b_trans, rk.x, kb + rk.y);
+        }
+      }
+      // keep the issue order = consumption order, so the waits are counted
+      // (vmcnt(N)) instead of the scheduler putting tile 0's loads last
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int kt = 0; kt < PRE; ++kt) {
+#pragma unroll
+      for (int i = 0; i < T::A_PER_T; ++i) {
+        const int c = tid + i * 256;
+        if (T::A_CHUNKS % 256 == 0 || c < T::A_CHUNKS) {
+          const int2 rk = chunk_rk<BK>(c, g.a_trans);
+          store_chunk<LDX>(As, g.a_trans, rk.x, kt * BK + rk.y, raw_to_bf16<AF32>(pa[kt][i]));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < T::B_PER_T; ++i) {
+        const int c = tid + i * 256;
+        if (T::B_CHUNKS % 256 == 0 || c < T::B_CHUNKS) {
+          const int2 rk = chunk_rk<BK>(c, g.b_trans);
+          store_chunk<LDX>(Bs, g.b_trans, rk.x, kt * BK + rk.y, raw_to_bf16<BF32>(pb[kt][i]));
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < PRE * BK; kk += 32) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = (wm * TM + i) * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(As + row * LDX + kk + 8 * (lane >> 4));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = (wn * TN + j) * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + col * LDX + kk + 8 * (lane >> 4));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
+    }
+  } else if constexpr (PRE > 0) {
     // Preload: every K-tile of this slice is requested before the first MFMA
     // (nkt <= PRE), so the slice costs ONE global round trip instead of nkt
     // dependent ones; the tiles then stream through the two LDS buffers.
@@ -471,6 +566,18 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
   }
 }
 
+// Exact-slice depth: K-tiles a slice may hold in registers (~128 VGPRs of
+// staged bf16 operands) and in one LDS image (<= 160 KB).
+template <int WM, int WN, int TM, int TN, int BK>
+constexpr int exact_depth() {
+  using T = Tile<WM, WN, TM, TN, BK>;
+  constexpr int dr = 128 / (4 * (T::A_PER_T + T::B_PER_T));
+  constexpr int dl = (81920 / (T::BM + T::BN) - 8) / BK;
+  constexpr int d = dr < dl ? dr : dl;
+  return d >= 16 ? 16 : (d >= 8 ? 8 : (d >= 4 ? 4 : 2));
+}
+static int g_exact_pre = 0;  // jdt_gemm_set_exact(pre): force the exact slice depth (tuning sweeps); 0 = auto
+
 constexpr int kPreMax = 4;      // K-tiles a preloading slice holds in registers
 static bool g_gemm_no_preload = false;  // jdt_gemm_set_preload(0): pipelined path only (A/B tests)
 
@@ -481,6 +588,43 @@ static int launch_cfg(const GemmArgs& g, int batch, int splits, float* ws, long 
   const int tiles_m = (g.M + T::BM - 1) / T::BM, tiles_n = (g.N + T::BN - 1) / T::BN;
   const long tiles = (long)tiles_m * tiles_n * batch;
   const int ktiles = (g.K + BK - 1) / BK;
+  // vector loads need 16-byte aligned rows: bf16 ld % 8, f32 ld % 4, aligned base
+  auto vec_ok = [](const void* p, long ld, int f32) {
+    return ((reinterpret_cast<uintptr_t>(p) & 15) == 0) && (f32 ? (ld % 4 == 0) : (ld % 8 == 0));
+  };
+  const int va = vec_ok(g.A, g.lda, g.a_f32), vb = vec_ok(g.B, g.ldb, g.b_f32);
+  // Exact path: bf16 operands, every tile interior, K a whole number of
+  // K-tiles split into slices of exactly `pre` (power of two <= register
+  // depth) -- straight-line kernels with one global round trip per slice.
+  if (splits < 0 && !g_gemm_no_preload && !g.a_f32 && !g.b_f32 && va && vb && g.M % T::BM == 0 &&
+      g.N % T::BN == 0 && g.K % BK == 0) {
+    constexpr int depth = exact_depth<WM, WN, TM, TN, BK>();
+    int pre = depth;
+    while (pre > 1 && ktiles % pre) pre >>= 1;
+    if (g_exact_pre > 0 && g_exact_pre <= depth && ktiles % g_exact_pre == 0) pre = g_exact_pre;
+    const int sp = ktiles / pre;
+    const bool ws_ok = sp == 1 || (ws && counters && tiles * sp * T::BM * T::BN <= ws_floats && tiles <= n_counters);
+    // a K split pays a slab round trip + combine: only while the grid is not already full
+    const bool split_ok = sp == 1 || g_exact_pre > 0 || tiles * sp <= 256;
+    if (pre >= 2 && sp <= 16 && ws_ok && split_ok) {
+      dim3 egrid(tiles_m * tiles_n, sp, batch);
+      const int ekchunk = pre * BK;
+#define JDT_GEMM_EXACT(P)                                                                                         \
+  case P:                                                                                                        \
+    hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, false, false, (P <= depth ? P : depth), true>), egrid,   \
+                       dim3(256), 0, st, g,                                                                      \
+                       tiles_n, va, vb, sp, ekchunk, ws, counters);                                              \
+    return HIP_LAUNCH_CHECK();
+      switch (pre) {
+        JDT_GEMM_EXACT(2)
+        JDT_GEMM_EXACT(4)
+        JDT_GEMM_EXACT(8)
+        JDT_GEMM_EXACT(16)
+        default: break;
+      }
+#undef JDT_GEMM_EXACT
+    }
+  }
   if (splits < 0) {
     // Small GEMMs here are latency-bound on the K loop (one global round trip
     // per K-tile): split K until the grid covers ~all CUs, <= 16 slices,
@@ -498,11 +642,6 @@ static int launch_cfg(const GemmArgs& g, int batch, int splits, float* ws, long 
   const int kchunk = ((ktiles + splits - 1) / splits) * BK;
   splits = (g.K + kchunk - 1) / kchunk;
   dim3 grid(tiles_m * tiles_n, splits, batch);
-  // vector loads need 16-byte aligned rows: bf16 ld % 8, f32 ld % 4, aligned base
-  auto vec_ok = [](const void* p, long ld, int f32) {
-    return ((reinterpret_cast<uintptr_t>(p) & 15) == 0) && (f32 ? (ld % 4 == 0) : (ld % 8 == 0));
-  };
-  const int va = vec_ok(g.A, g.lda, g.a_f32), vb = vec_ok(g.B, g.ldb, g.b_f32);
   const bool pre = kchunk / BK <= kPreMax && !g_gemm_no_preload;
 #define JDT_GEMM_LAUNCH(AF, BF)                                                                                  \
   do {                                                                                                           \
@@ -528,6 +667,7 @@ using namespace jdt;
 // Tile choice: the tutorial GEMMs are small (M = 4..128 rows per device), so the
 // heuristic favours enough workgroups to cover the chip over per-tile reuse.
 JDT_API void jdt_gemm_set_preload(int on) { g_gemm_no_preload = !on; }
+JDT_API void jdt_gemm_set_exact(int pre) { g_exact_pre = pre; }
 
 JDT_API int jdt_gemm(const GemmArgs* ga, int batch, int cfg, int splits, float* ws, long ws_floats,
                      unsigned* counters, long n_counters, void* stream) {

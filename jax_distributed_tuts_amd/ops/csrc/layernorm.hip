@@ -74,16 +74,17 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
                                                      const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                      const float* __restrict__ gamma, const bf16_t* __restrict__ dres,
                                                      bf16_t* __restrict__ dx, float* __restrict__ dgamma,
-                                                     float* __restrict__ dbeta, int T, int d, int rows_per_wave) {
-  __shared__ float sg[2048], sb[2048];
-  for (int i = threadIdx.x; i < d; i += 256) { sg[i] = 0.f; sb[i] = 0.f; }
+                                                     float* __restrict__ dbeta, float* __restrict__ dsum, int T, int d,
+                                                     int rows_per_wave) {
+  __shared__ float sg[2048], sb[2048], sd[2048];
+  for (int i = threadIdx.x; i < d; i += 256) { sg[i] = 0.f; sb[i] = 0.f; sd[i] = 0.f; }
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float ag[NV][8], ab[NV][8];
+  float ag[NV][8], ab[NV][8], ad[NV][8];
 #pragma unroll
   for (int c = 0; c < NV; ++c)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { ag[c][j] = 0.f; ab[c][j] = 0.f; }
+    for (int j = 0; j < 8; ++j) { ag[c][j] = 0.f; ab[c][j] = 0.f; ad[c][j] = 0.f; }
   const int r0 = (blockIdx.x * 4 + w) * rows_per_wave;
   for (int row = r0; row < min(T, r0 + rows_per_wave); ++row) {
     const float mean = mean_in[row], rstd = rstd_in[row];
@@ -130,7 +131,10 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
         for (int j = 0; j < 4; ++j) {
           const float a = r[2 * j] + rstd * (g[c][2 * j] - s1 - xh[c][2 * j] * s2);
           const float b = r[2 * j + 1] + rstd * (g[c][2 * j + 1] - s1 - xh[c][2 * j + 1] * s2);
-          o[j] = (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+          const bf16_t ha = f2bf(a), hb = f2bf(b);
+          o[j] = (unsigned)ha | ((unsigned)hb << 16);
+          ad[c][2 * j] += bf2f(ha);   // colsum of exactly the stored dx (next layer's bias grad)
+          ad[c][2 * j + 1] += bf2f(hb);
         }
         u32x4 ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
         *reinterpret_cast<u32x4*>(dx + (long)row * d + col) = ov;
@@ -142,12 +146,17 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
     const int col = (c * 64 + lane) * 8;
     if (col < d)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { atomicAdd(&sg[col + j], ag[c][j]); atomicAdd(&sb[col + j], ab[c][j]); }
+      for (int j = 0; j < 8; ++j) {
+        atomicAdd(&sg[col + j], ag[c][j]);
+        atomicAdd(&sb[col + j], ab[c][j]);
+        if (dsum) atomicAdd(&sd[col + j], ad[c][j]);
+      }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < d; i += 256) {
     if (dgamma) atomicAdd(dgamma + i, sg[i]);
     if (dbeta) atomicAdd(dbeta + i, sb[i]);
+    if (dsum) atomicAdd(dsum + i, sd[i]);
   }
 }
 
@@ -170,11 +179,16 @@ JDT_API int jdt_ln_fwd(const void* x, const float* gamma, const float* beta, voi
   return HIP_LAUNCH_CHECK();
 }
 
+// dsum (optional): += colsum(dx), the bias gradient of the layer that produced
+// this LayerNorm's input (a residual-stream Dense), so it needs no pass of its own.
 JDT_API int jdt_ln_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const float* gamma,
-                       const void* dres, void* dx, float* dgamma, float* dbeta, int T, int d, void* stream) {
+                       const void* dres, void* dx, float* dgamma, float* dbeta, float* dsum, int T, int d,
+                       void* stream) {
   if (d % 8 || d > 2048) return -3;
   const int nv = (d / 8 + 63) / 64;
-  const int rpw = 8;
+  // one or two rows per wave: enough workgroups to cover the CUs, few enough
+  // that the per-workgroup dgamma/dbeta atomics stay cheap
+  const int rpw = T <= 1024 ? 1 : (T + 1023) / 1024;
   dim3 grid((T + 4 * rpw - 1) / (4 * rpw));
   hipStream_t st = static_cast<hipStream_t>(stream);
   auto a = static_cast<const bf16_t*>(dy);
@@ -182,9 +196,9 @@ JDT_API int jdt_ln_bwd(const void* dy, const void* x, const float* mean, const f
   auto r = static_cast<const bf16_t*>(dres);
   auto o = static_cast<bf16_t*>(dx);
   switch (nv) {
-    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(256), 0, st, a, b, mean, rstd, gamma, r, o, dgamma, dbeta, T, d, rpw); break;
-    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(256), 0, st, a, b, mean, rstd, gamma, r, o, dgamma, dbeta, T, d, rpw); break;
-    default: hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(256), 0, st, a, b, mean, rstd, gamma, r, o, dgamma, dbeta, T, d, rpw); break;
+    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(256), 0, st, a, b, mean, rstd, gamma, r, o, dgamma, dbeta, dsum, T, d, rpw); break;
+    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(256), 0, st, a, b, mean, rstd, gamma, r, o, dgamma, dbeta, dsum, T, d, rpw); break;
+    default: hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(256), 0, st, a, b, mean, rstd, gamma, r, o, dgamma, dbeta, dsum, T, d, rpw); break;
   }
   return HIP_LAUNCH_CHECK();
 }

@@ -85,14 +85,150 @@ __global__ void __launch_bounds__(256) xent_kernel(const void* logits, long ld, 
   }
 }
 
+
+// Wide-vocabulary variant (bf16 logits, C % 8 == 0, C <= 512 * NV): a lane owns
+// NV chunks of 8 adjacent classes, so a row is NV 16-byte loads per lane held
+// in registers -- max, sum-exp, argmax and the gradient all come from those
+// registers (one HBM read, one write).  A wave walks `rpw` rows and keeps its
+// bias-gradient partials in registers; the 4 waves are summed in LDS and each
+// workgroup adds one fp32 atomic per class.
+template <int NV>
+__global__ void __launch_bounds__(256) xent_vec_kernel(const bf16_t* __restrict__ logits, long ld,
+                                                       const int* __restrict__ labels, int M, int C, int rpw,
+                                                       float grad_scale, bf16_t* __restrict__ dlogits, long ldd,
+                                                       float* __restrict__ dbias, float* __restrict__ metrics,
+                                                       float* __restrict__ row_loss) {
+  __shared__ float red[4][4];
+  __shared__ float part[4][512 * NV];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float l_sum = 0.f, n_valid = 0.f, n_correct = 0.f;
+  float db[NV][8];
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) db[k][j] = 0.f;
+  const int r0 = (blockIdx.x * 4 + w) * rpw;
+  for (int row = r0; row < min(M, r0 + rpw); ++row) {
+    const int label = labels[row];
+    const bool valid = label >= 0 && label < C;
+    float z[NV][8];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c0 = (k * 64 + lane) * 8;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (c0 < C) v = *reinterpret_cast<const u32x4*>(logits + (long)row * ld + c0);
+      const unsigned wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        z[k][j] = c0 < C ? bf2f((bf16_t)((wv[j >> 1] >> (16 * (j & 1))) & 0xffffu)) : -INFINITY;
+    }
+    float mx = -INFINITY;
+    int besti = 0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (z[k][j] > mx) { mx = z[k][j]; besti = (k * 64 + lane) * 8 + j; }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float om = __shfl_xor(mx, o, 64);
+      const int oi = __shfl_xor(besti, o, 64);
+      if (om > mx || (om == mx && oi < besti)) { mx = om; besti = oi; }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += __expf(z[k][j] - mx);
+    s = wave_sum(s);
+    const float lse = mx + __logf(s);
+    // the label's logit: the owning lane broadcasts it
+    float zl = 0.f;
+    if (valid) {
+      const int ok = label >> 3, kk = ok / 64, ln = ok % 64, jj = label & 7;
+      float mine = 0.f;
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (k == kk && j == jj) mine = z[k][j];
+      zl = __shfl(mine, ln, 64);
+    }
+    const float loss = valid ? lse - zl : 0.f;
+    if (row_loss && lane == 0) row_loss[row] = loss;
+    if (valid) { l_sum += loss; n_valid += 1.f; n_correct += (besti == label) ? 1.f : 0.f; }
+    if (dlogits) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c0 = (k * 64 + lane) * 8;
+        if (c0 < C) {
+          unsigned o[4];
+#pragma unroll
+          for (int j = 0; j < 8; j += 2) {
+            float g0 = 0.f, g1 = 0.f;
+            if (valid) {
+              g0 = (__expf(z[k][j] - lse) - (c0 + j == label ? 1.f : 0.f)) * grad_scale;
+              g1 = (__expf(z[k][j + 1] - lse) - (c0 + j + 1 == label ? 1.f : 0.f)) * grad_scale;
+            }
+            const bf16_t h0 = f2bf(g0), h1 = f2bf(g1);
+            o[j >> 1] = (unsigned)h0 | ((unsigned)h1 << 16);
+            db[k][j] += bf2f(h0);
+            db[k][j + 1] += bf2f(h1);
+          }
+          u32x4 ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
+          *reinterpret_cast<u32x4*>(dlogits + (long)row * ldd + c0) = ov;
+        }
+      }
+    }
+  }
+  if (dbias && dlogits) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part[w][(k * 64 + lane) * 8 + j] = db[k][j];
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) atomicAdd(dbias + c, part[0][c] + part[1][c] + part[2][c] + part[3][c]);
+  }
+  if (metrics) {
+    // loss, validity and correctness are wave-uniform: lane 0 holds the wave's sums
+    if (lane == 0) { red[w][0] = l_sum; red[w][1] = n_valid; red[w][2] = n_correct; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float a = 0.f, b = 0.f, c = 0.f;
+      for (int i = 0; i < 4; ++i) { a += red[i][0]; b += red[i][1]; c += red[i][2]; }
+      if (b > 0.f) {
+        atomicAdd(metrics + 0, a); atomicAdd(metrics + 1, b);
+        atomicAdd(metrics + 2, c); atomicAdd(metrics + 3, b);
+      }
+    }
+  }
+}
+
 }  // namespace jdt
 using namespace jdt;
 
 JDT_API int jdt_xent(const void* logits, int logits_f32, long ld, const int* labels, int M, int C, float grad_scale,
                      void* dlogits, long ldd, float* dbias, float* metrics, float* row_loss, void* stream) {
   if (M <= 0) return 0;
-  dim3 grid((M + 3) / 4);
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!logits_f32 && C >= 256 && C % 8 == 0 && C <= 2048 && ld % 8 == 0 && ldd % 8 == 0 &&
+      (reinterpret_cast<uintptr_t>(logits) & 15) == 0 && (reinterpret_cast<uintptr_t>(dlogits) & 15) == 0) {
+    const int rpw = M <= 1024 ? 1 : (M + 1023) / 1024;
+    dim3 vgrid((M + 4 * rpw - 1) / (4 * rpw));
+    auto lg = static_cast<const bf16_t*>(logits);
+    auto dl = static_cast<bf16_t*>(dlogits);
+    if (C <= 512)
+      hipLaunchKernelGGL(xent_vec_kernel<1>, vgrid, dim3(256), 0, st, lg, ld, labels, M, C, rpw, grad_scale, dl, ldd,
+                         dbias, metrics, row_loss);
+    else if (C <= 1024)
+      hipLaunchKernelGGL(xent_vec_kernel<2>, vgrid, dim3(256), 0, st, lg, ld, labels, M, C, rpw, grad_scale, dl, ldd,
+                         dbias, metrics, row_loss);
+    else
+      hipLaunchKernelGGL(xent_vec_kernel<4>, vgrid, dim3(256), 0, st, lg, ld, labels, M, C, rpw, grad_scale, dl, ldd,
+                         dbias, metrics, row_loss);
+    return HIP_LAUNCH_CHECK();
+  }
+  dim3 grid((M + 3) / 4);
   if (logits_f32)
     hipLaunchKernelGGL(xent_kernel<true>, grid, dim3(256), 0, st, logits, ld, labels, M, C, grad_scale,
                        static_cast<bf16_t*>(dlogits), ldd, dbias, metrics, row_loss);

@@ -505,8 +505,9 @@ def layernorm_fwd(x, gamma, beta, eps=1e-6):
     return y, mean, rstd
 
 
-def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None):
-    """dx = dres + LN'(dy); dgamma/dbeta accumulate (fp32)."""
+def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None, dsum=None):
+    """dx = dres + LN'(dy); dgamma/dbeta accumulate (fp32); ``dsum += colsum(dx)``
+    (the bias grad of the residual-stream Dense that produced x, fused here)."""
     T, d = x.shape
     if not _is_gpu(x):
         xh = (x.float() - mean[:, None]) * rstd[:, None]
@@ -518,10 +519,13 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None):
             dgamma.add_((dy.float() * xh).sum(0))
         if dbeta is not None:
             dbeta.add_(dy.float().sum(0))
-        return dx.to(torch.bfloat16)
+        dx = dx.to(torch.bfloat16)
+        if dsum is not None:
+            dsum.add_(dx.float().sum(0))
+        return dx
     dx = torch.empty_like(x)
     rc = _lib.lib().jdt_ln_bwd(_ptr(dy), _ptr(x), _ptr(mean), _ptr(rstd), _ptr(gamma), _ptr(dres), _ptr(dx),
-                               _ptr(dgamma), _ptr(dbeta), T, d, _lib.stream_ptr())
+                               _ptr(dgamma), _ptr(dbeta), _ptr(dsum), T, d, _lib.stream_ptr())
     _lib.check(rc, "jdt_ln_bwd")
     return dx
 

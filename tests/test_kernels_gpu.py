@@ -96,7 +96,7 @@ def test_gemm_batched():
     _close(out, ref, rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("M,C", [(4, 10), (128, 10), (33, 1000)])
+@pytest.mark.parametrize("M,C", [(4, 10), (128, 10), (33, 1000), (64, 2048), (37, 512), (1500, 768), (9, 1000 + 8)])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
 def test_xent(M, C, dt):
     z = (_mk((M, C), torch.float32, seed=13) * 3).to(dt)
@@ -210,7 +210,7 @@ def test_gemm_split_k(splits, M, N, K_, cfg, gemm_path):
     _close(acc_g, acc_r, rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("T,d", [(37, 64), (256, 512), (64, 1024)])
+@pytest.mark.parametrize("T,d", [(37, 64), (256, 512), (64, 1024), (2500, 512)])
 def test_layernorm(T, d):
     x = _mk((T, d), torch.bfloat16, seed=31)
     gmm, bta = 1 + 0.1 * _mk((d,), torch.float32, seed=32), 0.1 * _mk((d,), torch.float32, seed=33)
@@ -220,13 +220,16 @@ def test_layernorm(T, d):
     _close(m_g, m_r, rtol=1e-5, atol=1e-5)
     _close(r_g, r_r, rtol=1e-4, atol=1e-4)
     dy, dres = _mk((T, d), torch.bfloat16, seed=34), _mk((T, d), torch.bfloat16, seed=35)
-    dg_r, db_r = torch.zeros(d), torch.zeros(d)
-    dx_r = kern.layernorm_bwd(dy, x, m_r, r_r, gmm, dg_r, db_r, dres=dres)
-    dg_g, db_g = torch.zeros(d, device=DEV), torch.zeros(d, device=DEV)
-    dx_g = kern.layernorm_bwd(dy.to(DEV), x.to(DEV), m_g, r_g, gmm.to(DEV), dg_g, db_g, dres=dres.to(DEV))
+    dg_r, db_r, ds_r = torch.zeros(d), torch.zeros(d), torch.zeros(d)
+    dx_r = kern.layernorm_bwd(dy, x, m_r, r_r, gmm, dg_r, db_r, dres=dres, dsum=ds_r)
+    dg_g, db_g, ds_g = torch.zeros(d, device=DEV), torch.zeros(d, device=DEV), torch.zeros(d, device=DEV)
+    dx_g = kern.layernorm_bwd(dy.to(DEV), x.to(DEV), m_g, r_g, gmm.to(DEV), dg_g, db_g, dres=dres.to(DEV),
+                              dsum=ds_g)
     _close(dx_g, dx_r)
     _close(dg_g, dg_r, rtol=1e-3, atol=1e-3)
     _close(db_g, db_r, rtol=1e-3, atol=1e-3)
+    # dsum = colsum of the kernel's own (bf16) dx output
+    _close(ds_g, dx_g.float().sum(0), rtol=1e-4, atol=1e-3)
 
 
 @pytest.mark.parametrize("B,S,H,Dh", [(2, 16, 4, 16), (2, 128, 8, 64), (1, 96, 2, 32)])
@@ -255,11 +258,13 @@ def test_embedding_and_colsum():
     kern.embed_bwd(dout.to(DEV), tok.to(DEV), a_g, b_g, S)
     _close(a_g, a_r, rtol=1e-4, atol=1e-4)
     _close(b_g, b_r, rtol=1e-4, atol=1e-4)
-    c_r = torch.ones(d)
-    kern.colsum_(dout, c_r)
-    c_g = torch.ones(d, device=DEV)
-    kern.colsum_(dout.to(DEV), c_g)
-    _close(c_g, c_r, rtol=1e-4, atol=1e-3)
+    for M, N in ((T, d), (512, 1536), (77, 520), (1030, 2048)):
+        x = _mk((M, N), torch.bfloat16, seed=54 + M)
+        c_r = torch.ones(N)
+        kern.colsum_(x, c_r)
+        c_g = torch.ones(N, device=DEV)
+        kern.colsum_(x.to(DEV), c_g)
+        _close(c_g, c_r, rtol=1e-4, atol=1e-3)
 
 
 def test_transformer_step_gpu_matches_cpu():

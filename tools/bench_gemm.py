@@ -1,0 +1,96 @@
+"""GEMM micro-benchmark on the transformer / MLP shapes: our gfx950 kernel (each
+layout the models use) vs torch.matmul (hipBLASLt) on the same operands.
+Each timing is 50 back-to-back launches captured in one hipGraph (no host
+launch cost), median of 5 replays.
+
+    python tools/bench_gemm.py [--cfg N] [--json out.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from jax_distributed_tuts_amd.ops import kernels as K  # noqa: E402
+
+REPS = 50
+
+# (name, M, N, K, a_layout, b_layout, fp32-accumulate output)
+SHAPES = [
+    ("qkv fwd", 512, 1536, 512, "mk", "kn", False),
+    ("out fwd", 512, 512, 512, "mk", "kn", False),
+    ("fc1 fwd", 512, 2048, 512, "mk", "kn", False),
+    ("fc2 fwd", 512, 512, 2048, "mk", "kn", False),
+    ("head fwd", 512, 2048, 512, "mk", "kn", False),
+    ("fc1 dX", 512, 512, 2048, "mk", "nk", False),
+    ("fc2 dX", 512, 2048, 512, "mk", "nk", False),
+    ("fc1 dW", 512, 2048, 512, "km", "kn", True),
+    ("fc2 dW", 2048, 512, 512, "km", "kn", True),
+    ("qkv fwd 2k", 2048, 1536, 512, "mk", "kn", False),
+    ("fc2 fwd 2k", 2048, 512, 2048, "mk", "kn", False),
+    ("fc1 dW 2k", 512, 2048, 2048, "km", "kn", True),
+    ("hyb qkv fwd", 256, 1536, 512, "mk", "kn", False),
+    ("hyb fc2 fwd", 256, 512, 2048, "mk", "kn", False),
+    ("mlp fwd", 32, 512, 512, "mk", "kn", False),
+    ("mlp dW", 512, 512, 32, "km", "kn", True),
+]
+
+
+def timed(fn):
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(REPS):
+            fn()
+    ts = []
+    for _ in range(5):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3 / REPS)
+    ts.sort()
+    return ts[2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cfg", type=int, default=-1)
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--exact", type=int, default=0, help="force the exact-slice depth (0 = heuristic)")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    from jax_distributed_tuts_amd.ops import _lib
+    _lib.lib().jdt_gemm_set_exact(args.exact)
+    out = []
+    print(f"{'shape':14s} {'M':>5s} {'N':>5s} {'K':>5s} {'ours us':>9s} {'TF/s':>7s} {'torch us':>9s} {'TF/s':>7s}")
+    for name, M, N, Kd, al, bl, f32 in SHAPES:
+        a = torch.randn(*((M, Kd) if al == "mk" else (Kd, M)), device=dev).to(torch.bfloat16)
+        b = torch.randn(*((Kd, N) if bl == "kn" else (N, Kd)), device=dev).to(torch.bfloat16)
+        c = torch.zeros(M, N, device=dev, dtype=torch.float32 if f32 else torch.bfloat16)
+        ours = timed(lambda: K.gemm(a, b, a_layout=al, b_layout=bl, out=c, accumulate=f32, cfg=args.cfg))
+        am = a if al == "mk" else a.t()
+        bm = b if bl == "kn" else b.t()
+        ref = timed(lambda: torch.matmul(am, bm))
+        fl = 2.0 * M * N * Kd
+        print(f"{name:14s} {M:5d} {N:5d} {Kd:5d} {ours:9.2f} {fl / ours / 1e6:7.1f} {ref:9.2f} {fl / ref / 1e6:7.1f}")
+        # numerics spot check
+        c.zero_()
+        K.gemm(a, b, a_layout=al, b_layout=bl, out=c, accumulate=f32, cfg=args.cfg)
+        want = (am.float() @ bm.float())
+        err = float((c.float() - want).abs().max() / (want.abs().max() + 1e-6))
+        out.append({"shape": name, "M": M, "N": N, "K": Kd, "ours_us": ours, "torch_us": ref, "rel_err": err})
+        if err > 2e-2:
+            print(f"   !! rel err {err:.3e}")
+    if args.json:
+        json.dump(out, open(args.json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -43,6 +43,7 @@ _SIGS = {
     "jdt_gemm_args_size": (c_int, []),
     "jdt_gemm_set_preload": (None, [c_int]),
     "jdt_gemm_set_exact": (None, [c_int]),
+    "jdt_gemm_set_dma": (None, [c_int]),
     "jdt_xent": (c_int, [c_void_p, c_int, c_long, c_void_p, c_int, c_int, c_float, c_void_p, c_long, c_void_p,
                          c_void_p, c_void_p, c_void_p]),
     "jdt_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_float, c_float, c_float,

@@ -218,6 +218,116 @@ __device__ __forceinline__ void store_chunk(bf16_t* lds, bool trans, int r, int 
   }
 }
 
+// Split-K combine (when splits > 1) + the fused epilogue, shared by every GEMM
+// kernel body: `acc` is the wave's TM x TN grid of 16x16 fp32 accumulators of
+// the BM x BN tile at (tm0, tn0) of batch z.
+template <int BM, int BN, int TM, int TN>
+__device__ __forceinline__ void gemm_finish(const GemmArgs& g, f32x4 (&acc)[TM][TN], int tm0, int tn0, int z,
+                                            int wid, int wm, int wn, int lane, int tid, int splits, int split,
+                                            long tile_id, float* __restrict__ ws, unsigned* counters,
+                                            int* lds_flag) {
+  // ------------------------------------------------------------- split-K combine
+  // Every K-slice writes its fp32 partial tile (slab) with device-scope stores
+  // (sc1: written through to the cross-XCD coherence point), waits for them
+  // (vmcnt), then draws an arrival ticket; the workgroup that draws the last
+  // ticket reads the slabs with device-scope loads and runs the epilogue.  No
+  // agent-scope release/acquire fence: on this multi-XCD part those lower to a
+  // write-back / invalidate of the whole L2 (buffer_wbl2 / buffer_inv sc1),
+  // which cost several us per workgroup; only the slab lines need coherence.
+  // The slab layout is the lanes' own accumulator order, so the combine is
+  // placement independent.
+  if (splits > 1) {
+    float* slab0 = ws + tile_id * splits * (BM * BN);
+    float* slab = slab0 + (long)split * (BM * BN);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          __hip_atomic_store(slab + (((wid * TM + i) * TN + j) * 64 + lane) * 4 + e, acc[i][j][e], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = lds_flag;
+    if (tid == 0) {
+      const unsigned t = __hip_atomic_fetch_add(counters + tile_id, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (t == (unsigned)(splits - 1));
+      if (last) __hip_atomic_store(counters + tile_id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][e] = 0.f;
+    for (int sp = 0; sp < splits; ++sp) {
+      const float* sl = slab0 + (long)sp * (BM * BN);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            acc[i][j][e] += __hip_atomic_load(sl + (((wid * TM + i) * TN + j) * 64 + lane) * 4 + e, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // ------------------------------------------------------------- epilogue
+  const bool drop = g.keep_prob < 1.0f;
+  const float inv_keep = drop ? 1.0f / g.keep_prob : 1.0f;
+  const unsigned long long doff = g.offset + (g.step_ptr ? ((unsigned long long)(unsigned)g.step_ptr[0] << 32) : 0ull);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = tn0 + (wn * TN + j) * 16 + (lane & 15);
+    const bool cok = col < g.N;
+    float bval = 0.f;
+    if (g.bias && cok) bval = g.bias_f32 ? static_cast<const float*>(g.bias)[col] : bf2f(static_cast<const bf16_t*>(g.bias)[col]);
+    float csum = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      // the lane's 4 rows form one dropout group: one Philox call for all 4
+      const int row0 = tm0 + (wm * TM + i) * 16 + (lane >> 4) * 4;
+      u32x4 dbits = {0u, 0u, 0u, 0u};
+      if (drop && cok) dbits = dropout_bits(g.seed, doff, dropout_group(z, row0, col, g.M, g.N));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = row0 + e;
+        if (cok && row < g.M) {
+        float v = g.alpha * acc[i][j][e] + bval;
+        if (g.Zout) static_cast<bf16_t*>(g.Zout)[(long)z * g.sZ + (long)row * g.ldz + col] = f2bf(v);
+        if (g.Zin) v *= act_grad(g.act_bwd, bf2f(g.Zin[(long)z * g.sZin + (long)row * g.ldzin + col]));
+        if (g.act) v = act_fwd(g.act, g.Zout ? round_bf(v) : v);
+        if (drop) v = keep_word(dbits, e, g.keep_prob) ? v * inv_keep : 0.f;
+        if (g.resid) v += bf2f(static_cast<const bf16_t*>(g.resid)[(long)z * g.sR + (long)row * g.ldr + col]);
+        const long co = zoff(g, z, g.sC, g.sC2) + (long)row * g.ldc + col;
+        if (g.c_f32) {
+          float* Cp = static_cast<float*>(g.C) + co;
+          *Cp = g.accumulate ? *Cp + v : v;
+        } else {
+          bf16_t* Cp = static_cast<bf16_t*>(g.C) + co;
+          if (g.accumulate) {
+            *Cp = f2bf(bf2f(*Cp) + v);
+          } else {
+            v = round_bf(v);  // the bias grad sums exactly what downstream GEMMs read
+            *Cp = f2bf(v);
+          }
+        }
+        csum += v;
+        }
+      }
+    }
+    if (g.dbias) {
+      csum += __shfl_xor(csum, 16, WAVE);
+      csum += __shfl_xor(csum, 32, WAVE);
+      if (lane < 16 && cok) atomicAdd(g.dbias + col, csum);
+    }
+  }
+}
+
 template <int WM, int WN, int TM, int TN, int BK, bool AF32, bool BF32, int PRE, bool EXACT = false>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int vecA, int vecB, int splits,
                                                    int kchunk, float* __restrict__ ws, unsigned* counters) {
@@ -463,107 +573,147 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
 #undef AS
 #undef BS
 
-  // ------------------------------------------------------------- split-K combine
-  // Every K-slice writes its fp32 partial tile (slab) with device-scope stores
-  // (sc1: written through to the cross-XCD coherence point), waits for them
-  // (vmcnt), then draws an arrival ticket; the workgroup that draws the last
-  // ticket reads the slabs with device-scope loads and runs the epilogue.  No
-  // agent-scope release/acquire fence: on this multi-XCD part those lower to a
-  // write-back / invalidate of the whole L2 (buffer_wbl2 / buffer_inv sc1),
-  // which cost several us per workgroup; only the slab lines need coherence.
-  // The slab layout is the lanes' own accumulator order, so the combine is
-  // placement independent.
-  if (splits > 1) {
-    const long tile_id = (long)z * gridDim.x + bid;
-    float* slab0 = ws + tile_id * splits * (BM * BN);
-    float* slab = slab0 + (long)split * (BM * BN);
+  gemm_finish<BM, BN, TM, TN>(g, acc, tm0, tn0, z, wid, wm, wn, lane, tid, splits, split, (long)z * gridDim.x + bid,
+                              ws, counters, reinterpret_cast<int*>(smem));
+}
+
+
+// ---------------------------------------------------------------------------
+// LDS-DMA GEMM body (bf16 operands, every tile interior, K-slices a whole
+// number of 64-deep K-tiles).  Operand tiles go global -> LDS with
+// global_load_lds_dwordx4 (no VGPR staging, no ds_write), S-deep ring of LDS
+// stages with ONE barrier per K-tile and a counted vmcnt that keeps the next
+// stage in flight across it (cdna_hip_programming.md §5 "Pipelining across
+// barriers").  Either operand may be K-contiguous ("mk" A / "nk" B: row image,
+// 16-byte chunks XOR-swizzled by row so the ds_read_b128 fragment reads spread
+// over the banks) or M/N-contiguous ("km" A / "kn" B, e.g. the [in,out] weight
+// of a forward pass or the token-major operands of a weight gradient: k-row
+// image read with the gfx950 transposing ds_read_b64_tr_b16, so no operand is
+// ever transposed in memory).
+constexpr int DMA_BK = 64;
+
+template <int EXT>  // EXT = extent of the non-K dim of the tile (BM or BN)
+__device__ __forceinline__ bf16x8 dma_frag(const bf16_t* img, bool kmajor_img, int base, int kk, int lane) {
+  if (!kmajor_img) {
+    // row image [EXT][64]: row r, 16-byte chunk c lives at slot c ^ (r & 7)
+    const int r = base + (lane & 15);
+    const int c = (kk >> 3) + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(img + r * DMA_BK + ((c ^ (r & 7)) << 3));
+  }
+  // k-row image [64][EXT]: lane 4q+p of each 16-lane group addresses k-row q,
+  // columns 4p..4p+3 of the group's 4-row block; it receives column (lane & 15).
+  // Issued as inline asm: hipcc treats the ds_read_tr intrinsic as aliasing the
+  // in-flight LDS-DMA and would wait vmcnt(0) before it, draining the ring.
+  // The caller waits lgkmcnt(0) before the MFMAs read the fragments.
+  typedef __attribute__((ext_vector_type(4))) short s4;
+  const int i16 = lane & 15, k1 = kk + 8 * (lane >> 4) + (i16 >> 2);
+  const int col = base + 4 * (i16 & 3);
+  const unsigned a0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) const bf16_t*)(img + k1 * EXT + col));
+  s4 lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a0), "n"(4 * EXT * 2));
+  bf16x8 f;
+  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+  return f;
+}
+
+// Stage one operand tile (EXT x 64 of a K-contiguous source, or 64 x EXT of an
+// EXT-contiguous one) into its LDS image: EXT/32 wave-instructions per wave.
+template <int EXT, bool KMAJ>
+__device__ __forceinline__ void dma_stage(const bf16_t* src, long ld, int k0, bf16_t* img, int wid, int lane) {
+  constexpr int IPW = EXT / 32;  // 1 KiB per wave-instruction, EXT*64*2 bytes per tile, 4 waves
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          __hip_atomic_store(slab + (((wid * TM + i) * TN + j) * 64 + lane) * 4 + e, acc[i][j][e], __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(smem);
-    if (tid == 0) {
-      const unsigned t = __hip_atomic_fetch_add(counters + tile_id, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = (t == (unsigned)(splits - 1));
-      if (last) __hip_atomic_store(counters + tile_id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      flag[0] = last;
+  for (int i = 0; i < IPW; ++i) {
+    const int ins = wid * IPW + i;
+    const int p = ins * 64 + lane;  // 16-byte slot of the image
+    const bf16_t* gp;
+    if (!KMAJ) {
+      const int r = p >> 3, c = (p & 7) ^ (r & 7);
+      gp = src + (long)r * ld + k0 + c * 8;
+    } else {
+      constexpr int CPR = EXT / 8;  // chunks per k-row
+      const int kr = p / CPR, cm = p % CPR;
+      gp = src + (long)(k0 + kr) * ld + cm * 8;
     }
-    __syncthreads();
-    if (!flag[0]) return;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gp,
+                                     (__attribute__((address_space(3))) void*)(img + ins * 512), 16, 0, 0);
+  }
+}
+
+template <int WM, int WN, int TM, int TN, bool AT, bool BT, int S>
+__global__ void __launch_bounds__(256) gemm_dma_kernel(GemmArgs g, int tiles_n, int splits, int kchunk,
+                                                       float* __restrict__ ws, unsigned* counters) {
+  constexpr int BM = WM * TM * 16, BN = WN * TN * 16, BK = DMA_BK;
+  constexpr int STAGE = (BM + BN) * BK;  // elements
+  constexpr int LPW = BM / 32 + BN / 32;  // glds per wave per stage
+  __shared__ __attribute__((aligned(16))) bf16_t smem[S * STAGE];
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  }
+  const int tm0 = (bid / tiles_n) * BM, tn0 = (bid % tiles_n) * BN, z = blockIdx.z;
+  const bf16_t* Ab = static_cast<const bf16_t*>(g.A) + zoff(g, z, g.sA, g.sA2) + (AT ? (long)tm0 : (long)tm0 * g.lda);
+  const bf16_t* Bb = static_cast<const bf16_t*>(g.B) + zoff(g, z, g.sB, g.sB2) + (BT ? (long)tn0 : (long)tn0 * g.ldb);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int split = blockIdx.y;
+  const int kbeg = split * kchunk;
+  const int nkt = (min(g.K, kbeg + kchunk) - kbeg) / BK;
+
+  f32x4 acc[TM][TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int kt) {
+    bf16_t* st = smem + (kt % S) * STAGE;
+    dma_stage<BM, AT>(Ab, g.lda, kbeg + kt * BK, st, wid, lane);
+    dma_stage<BN, BT>(Bb, g.ldb, kbeg + kt * BK, st + BM * BK, wid, lane);
+  };
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[i][j][e] = 0.f;
-    for (int sp = 0; sp < splits; ++sp) {
-      const float* sl = slab0 + (long)sp * (BM * BN);
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nkt) issue(s);
+  for (int kt = 0; kt < nkt; ++kt) {
+    // stage kt has landed once at most the stages issued after it are pending
+    // (per wave), and every wave's share once all passed the barrier
+    if (kt + S - 2 < nkt) {
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"((S - 2) * LPW) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    // refill the stage consumed in iteration kt-1 (all waves are past it)
+    if (kt + S - 1 < nkt) issue(kt + S - 1);
+    const bf16_t* As = smem + (kt % S) * STAGE;
+    const bf16_t* Bs = As + BM * BK;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = dma_frag<BM>(As, AT, (wm * TM + i) * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = dma_frag<BN>(Bs, BT, (wn * TN + j) * 16, kk, lane);
+      if constexpr (AT || BT) {
+        // asm tr reads retired; the empty asm ties every fragment to the wait so
+        // no MFMA can be scheduled ahead of it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(af[i]));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(bfr[j]));
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            acc[i][j][e] += __hip_atomic_load(sl + (((wid * TM + i) * TN + j) * 64 + lane) * 4 + e, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
     }
   }
-  // ------------------------------------------------------------- epilogue
-  const bool drop = g.keep_prob < 1.0f;
-  const float inv_keep = drop ? 1.0f / g.keep_prob : 1.0f;
-  const unsigned long long doff = g.offset + (g.step_ptr ? ((unsigned long long)(unsigned)g.step_ptr[0] << 32) : 0ull);
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = tn0 + (wn * TN + j) * 16 + (lane & 15);
-    const bool cok = col < g.N;
-    float bval = 0.f;
-    if (g.bias && cok) bval = g.bias_f32 ? static_cast<const float*>(g.bias)[col] : bf2f(static_cast<const bf16_t*>(g.bias)[col]);
-    float csum = 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      // the lane's 4 rows form one dropout group: one Philox call for all 4
-      const int row0 = tm0 + (wm * TM + i) * 16 + (lane >> 4) * 4;
-      u32x4 dbits = {0u, 0u, 0u, 0u};
-      if (drop && cok) dbits = dropout_bits(g.seed, doff, dropout_group(z, row0, col, g.M, g.N));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = row0 + e;
-        if (cok && row < g.M) {
-        float v = g.alpha * acc[i][j][e] + bval;
-        if (g.Zout) static_cast<bf16_t*>(g.Zout)[(long)z * g.sZ + (long)row * g.ldz + col] = f2bf(v);
-        if (g.Zin) v *= act_grad(g.act_bwd, bf2f(g.Zin[(long)z * g.sZin + (long)row * g.ldzin + col]));
-        if (g.act) v = act_fwd(g.act, g.Zout ? round_bf(v) : v);
-        if (drop) v = keep_word(dbits, e, g.keep_prob) ? v * inv_keep : 0.f;
-        if (g.resid) v += bf2f(static_cast<const bf16_t*>(g.resid)[(long)z * g.sR + (long)row * g.ldr + col]);
-        const long co = zoff(g, z, g.sC, g.sC2) + (long)row * g.ldc + col;
-        if (g.c_f32) {
-          float* Cp = static_cast<float*>(g.C) + co;
-          *Cp = g.accumulate ? *Cp + v : v;
-        } else {
-          bf16_t* Cp = static_cast<bf16_t*>(g.C) + co;
-          if (g.accumulate) {
-            *Cp = f2bf(bf2f(*Cp) + v);
-          } else {
-            v = round_bf(v);  // the bias grad sums exactly what downstream GEMMs read
-            *Cp = f2bf(v);
-          }
-        }
-        csum += v;
-        }
-      }
-    }
-    if (g.dbias) {
-      csum += __shfl_xor(csum, 16, WAVE);
-      csum += __shfl_xor(csum, 32, WAVE);
-      if (lane < 16 && cok) atomicAdd(g.dbias + col, csum);
-    }
-  }
+  __syncthreads();
+  gemm_finish<BM, BN, TM, TN>(g, acc, tm0, tn0, z, wid, wm, wn, lane, tid, splits, split, (long)z * gridDim.x + bid,
+                              ws, counters, reinterpret_cast<int*>(smem));
 }
 
 // Exact-slice depth: K-tiles a slice may hold in registers (~128 VGPRs of
@@ -660,6 +810,69 @@ static int launch_cfg(const GemmArgs& g, int batch, int splits, float* ws, long 
   return HIP_LAUNCH_CHECK();
 }
 
+
+static bool g_gemm_no_dma = false;  // jdt_gemm_set_dma(0): register-staged kernels only (A/B tests)
+
+template <int WM, int WN, int TM, int TN>
+static int launch_dma(const GemmArgs& g, int batch, int splits, float* ws, long ws_floats, unsigned* counters,
+                      long n_counters, hipStream_t st) {
+  constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
+  if (g.M % BM || g.N % BN) return 1;
+  const int tiles_n = g.N / BN;
+  const long tiles = (long)(g.M / BM) * tiles_n * batch;
+  int sp = splits;
+  if (sp < 0) {
+    // Measured (tools/bench_gemm.py sweeps): many small workgroups per CU hide
+    // the load latency better than a split-K combine; split only while the
+    // grid has < 2 workgroups per CU, keeping slices >= 8 K-tiles.
+    sp = 1;
+    while (sp < 16 && tiles * sp < 512 && (g.K / (2 * sp)) % DMA_BK == 0 && g.K / (2 * sp) >= 8 * DMA_BK) sp *= 2;
+  }
+  if (sp < 1 || g.K % sp || (g.K / sp) % DMA_BK) return 1;
+  if (sp > 1 && (!ws || !counters || tiles * sp * BM * BN > ws_floats || tiles > n_counters)) sp = 1;
+  const int kchunk = g.K / sp;
+  dim3 grid((g.M / BM) * tiles_n, sp, batch);
+  const bool at = g.a_trans, bt = g.b_trans;
+#define JDT_DMA(A_, B_)                                                                                     \
+  hipLaunchKernelGGL((gemm_dma_kernel<WM, WN, TM, TN, A_, B_, 3>), grid, dim3(256), 0, st, g, tiles_n, sp,  \
+                     kchunk, ws, counters)
+  if (!at && !bt) JDT_DMA(false, false);
+  else if (!at && bt) JDT_DMA(false, true);
+  else if (at && !bt) JDT_DMA(true, false);
+  else JDT_DMA(true, true);
+#undef JDT_DMA
+  return HIP_LAUNCH_CHECK();
+}
+
+// LDS-DMA path for bf16 operands: returns 1 if the shape / layout is outside
+// its envelope (caller falls back to the register-staged kernels).
+static int gemm_dma(const GemmArgs& g, int batch, int cfg, int splits, float* ws, long ws_floats, unsigned* counters,
+                    long n_counters, hipStream_t st) {
+  if (g_gemm_no_dma || g.a_f32 || g.b_f32 || g.K % DMA_BK) return 1;
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (!al(g.A) || !al(g.B) || g.lda % 8 || g.ldb % 8) return 1;
+  if (batch > 1 && (g.sA % 8 || g.sB % 8 || g.sA2 % 8 || g.sB2 % 8)) return 1;
+  if (cfg < 0) {
+    // 32x32 tiles up to ~4 workgroups per CU (up to 6 fit by LDS), then 64x64,
+    // then 64x128 (tools/bench_gemm.py sweep on the transformer/MLP shapes)
+    const long t32 = (long)(g.M / 32) * (g.N / 32) * batch;
+    const long t64 = (long)(g.M / 64) * (g.N / 64) * batch;
+    if (g.M % 32 || g.N % 32) return 1;
+    if (g.M < 64 && g.N < 256) return 1;  // tiny: the register kernels' split-K preload is as good
+    if (t32 > 512 && g.K >= 2048 && g.N % 64 == 0) cfg = 10;  // long K: 32x64 reuses more per load
+    else if (t32 <= 1024 || g.M % 64 || g.N % 64) cfg = 13;
+    else if (t64 <= 1024 || g.N % 128) cfg = 11;
+    else cfg = 12;
+  }
+  switch (cfg) {
+    case 10: return launch_dma<2, 2, 1, 2>(g, batch, splits, ws, ws_floats, counters, n_counters, st);  // 32 x 64
+    case 11: return launch_dma<2, 2, 2, 2>(g, batch, splits, ws, ws_floats, counters, n_counters, st);  // 64 x 64
+    case 12: return launch_dma<2, 2, 2, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st);  // 64 x 128
+    case 13: return launch_dma<2, 2, 1, 1>(g, batch, splits, ws, ws_floats, counters, n_counters, st);  // 32 x 32
+    default: return 1;
+  }
+}
+
 }  // namespace jdt
 
 using namespace jdt;
@@ -668,12 +881,18 @@ using namespace jdt;
 // heuristic favours enough workgroups to cover the chip over per-tile reuse.
 JDT_API void jdt_gemm_set_preload(int on) { g_gemm_no_preload = !on; }
 JDT_API void jdt_gemm_set_exact(int pre) { g_exact_pre = pre; }
+JDT_API void jdt_gemm_set_dma(int on) { g_gemm_no_dma = !on; }
 
 JDT_API int jdt_gemm(const GemmArgs* ga, int batch, int cfg, int splits, float* ws, long ws_floats,
                      unsigned* counters, long n_counters, void* stream) {
   const GemmArgs& g = *ga;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (g.M <= 0 || g.N <= 0) return 0;
+  if (cfg < 0 || cfg >= 10) {
+    const int rc = gemm_dma(g, batch, cfg, splits, ws, ws_floats, counters, n_counters, st);
+    if (rc != 1) return rc;  // 1 = shape outside the LDS-DMA envelope: register-staged kernels below
+    if (cfg >= 10) return -1;
+  }
   if (cfg < 0) {
     const long t128 = (long)((g.M + 63) / 64) * ((g.N + 127) / 128) * batch;
     const long t64 = (long)((g.M + 63) / 64) * ((g.N + 63) / 64) * batch;

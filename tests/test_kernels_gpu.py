@@ -22,18 +22,23 @@ def _mk(shape, dtype, layout_t=False, seed=0):
     return t.to(dtype)
 
 
-@pytest.fixture(params=[1, 0], ids=["preload", "pipelined"])
+@pytest.fixture(params=["dma", "preload", "pipelined"])
 def gemm_path(request):
-    """Run a GEMM test through the all-K-tiles-preloaded path and the pipelined one."""
+    """Run a GEMM test through the LDS-DMA kernel (bf16 operands, tile-aligned
+    shapes), the all-K-tiles-preloaded register kernel and the pipelined one."""
     from jax_distributed_tuts_amd.ops import _lib
 
-    _lib.lib().jdt_gemm_set_preload(request.param)
+    L = _lib.lib()
+    L.jdt_gemm_set_dma(int(request.param == "dma"))
+    L.jdt_gemm_set_preload(int(request.param != "pipelined"))
     yield request.param
-    _lib.lib().jdt_gemm_set_preload(1)
+    L.jdt_gemm_set_dma(1)
+    L.jdt_gemm_set_preload(1)
 
 
 @pytest.mark.parametrize("M,N,K", [(4, 512, 784), (16, 512, 784), (32, 10, 512), (128, 512, 784), (37, 70, 50),
-                                   (256, 384, 256), (512, 512, 512)])
+                                   (256, 384, 256), (512, 512, 512), (64, 128, 2048), (96, 192, 128),
+                                   (512, 1536, 512)])
 @pytest.mark.parametrize("a_layout,b_layout", [("mk", "kn"), ("mk", "nk"), ("km", "kn"), ("km", "nk")])
 @pytest.mark.parametrize("adt", [torch.bfloat16, torch.float32])
 def test_gemm_layouts(M, N, K, a_layout, b_layout, adt, gemm_path):
@@ -88,12 +93,46 @@ def test_gemm_accumulate_fp32():
     _close(acc_g, acc_r, rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("a_layout,b_layout", [("mk", "kn"), ("mk", "nk"), ("km", "kn"), ("km", "nk")])
+def test_gemm_dma_epilogues(a_layout, b_layout):
+    """LDS-DMA kernel with every fused epilogue: bias + GELU + z_out + dropout +
+    residual (forward), act' * mask + dbias (backward), fp32 accumulate, split-K."""
+    M, N, K_ = 128, 256, 512
+    a = _mk((M, K_) if a_layout == "mk" else (K_, M), torch.bfloat16, seed=61)
+    b = (_mk((K_, N) if b_layout == "kn" else (N, K_), torch.float32, seed=62) * 0.05).to(torch.bfloat16)
+    bias, res = _mk((N,), torch.bfloat16, seed=63), _mk((M, N), torch.bfloat16, seed=64)
+    zr = torch.empty(M, N, dtype=torch.bfloat16)
+    ref = kern.gemm(a, b, a_layout=a_layout, b_layout=b_layout, bias=bias, act="gelu", z_out=zr, keep_prob=0.9,
+                    seed=7, offset=11, resid=res)
+    zg = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    out = kern.gemm(a.to(DEV), b.to(DEV), a_layout=a_layout, b_layout=b_layout, bias=bias.to(DEV), act="gelu",
+                    z_out=zg, keep_prob=0.9, seed=7, offset=11, resid=res.to(DEV))
+    _close(zg, zr)
+    _close(out, ref)
+    z = _mk((M, N), torch.bfloat16, seed=65)
+    db_r, db_g = torch.zeros(N), torch.zeros(N, device=DEV)
+    ref = kern.gemm(a, b, a_layout=a_layout, b_layout=b_layout, z_in=z, act_bwd="silu", keep_prob=0.9, seed=3,
+                    offset=5, dbias=db_r)
+    out = kern.gemm(a.to(DEV), b.to(DEV), a_layout=a_layout, b_layout=b_layout, z_in=z.to(DEV), act_bwd="silu",
+                    keep_prob=0.9, seed=3, offset=5, dbias=db_g)
+    _close(out, ref)
+    _close(db_g, db_r, rtol=2e-2, atol=5e-2)
+    for splits in (-1, 4):
+        acc_r = torch.full((M, N), 0.5)
+        kern.gemm(a, b, a_layout=a_layout, b_layout=b_layout, out=acc_r, accumulate=True)
+        acc_g = torch.full((M, N), 0.5, device=DEV)
+        kern.gemm(a.to(DEV), b.to(DEV), a_layout=a_layout, b_layout=b_layout, out=acc_g, accumulate=True,
+                  cfg=11, splits=splits)
+        _close(acc_g, acc_r, rtol=1e-3, atol=1e-3)
+
+
 def test_gemm_batched():
-    a = _mk((3, 64, 96), torch.bfloat16, seed=11)
-    b = _mk((3, 96, 80), torch.bfloat16, seed=12)
-    ref = kern.gemm(a, b, out_dtype=torch.float32)
-    out = kern.gemm(a.to(DEV), b.to(DEV), out_dtype=torch.float32)
-    _close(out, ref, rtol=1e-3, atol=1e-3)
+    for (m, k, n) in ((64, 96, 80), (64, 128, 64)):  # register-staged / LDS-DMA
+        a = _mk((3, m, k), torch.bfloat16, seed=11)
+        b = _mk((3, k, n), torch.bfloat16, seed=12)
+        ref = kern.gemm(a, b, out_dtype=torch.float32)
+        out = kern.gemm(a.to(DEV), b.to(DEV), out_dtype=torch.float32)
+        _close(out, ref, rtol=1e-3, atol=1e-3)
 
 
 @pytest.mark.parametrize("M,C", [(4, 10), (128, 10), (33, 1000), (64, 2048), (37, 512), (1500, 768), (9, 1000 + 8)])

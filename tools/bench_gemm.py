@@ -64,6 +64,7 @@ def main():
     ap.add_argument("--cfg", type=int, default=-1)
     ap.add_argument("--json", default=None)
     ap.add_argument("--exact", type=int, default=0, help="force the exact-slice depth (0 = heuristic)")
+    ap.add_argument("--splits", type=int, default=-1)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     from jax_distributed_tuts_amd.ops import _lib
@@ -74,7 +75,12 @@ def main():
         a = torch.randn(*((M, Kd) if al == "mk" else (Kd, M)), device=dev).to(torch.bfloat16)
         b = torch.randn(*((Kd, N) if bl == "kn" else (N, Kd)), device=dev).to(torch.bfloat16)
         c = torch.zeros(M, N, device=dev, dtype=torch.float32 if f32 else torch.bfloat16)
-        ours = timed(lambda: K.gemm(a, b, a_layout=al, b_layout=bl, out=c, accumulate=f32, cfg=args.cfg))
+        try:
+            ours = timed(lambda: K.gemm(a, b, a_layout=al, b_layout=bl, out=c, accumulate=f32, cfg=args.cfg,
+                                         splits=args.splits))
+        except RuntimeError:
+            print(f"{name:14s} {M:5d} {N:5d} {Kd:5d}   (config not applicable)")
+            continue
         am = a if al == "mk" else a.t()
         bm = b if bl == "kn" else b.t()
         ref = timed(lambda: torch.matmul(am, bm))
@@ -82,7 +88,7 @@ def main():
         print(f"{name:14s} {M:5d} {N:5d} {Kd:5d} {ours:9.2f} {fl / ours / 1e6:7.1f} {ref:9.2f} {fl / ref / 1e6:7.1f}")
         # numerics spot check
         c.zero_()
-        K.gemm(a, b, a_layout=al, b_layout=bl, out=c, accumulate=f32, cfg=args.cfg)
+        K.gemm(a, b, a_layout=al, b_layout=bl, out=c, accumulate=f32, cfg=args.cfg, splits=args.splits)
         want = (am.float() @ bm.float())
         err = float((c.float() - want).abs().max() / (want.abs().max() + 1e-6))
         out.append({"shape": name, "M": M, "N": N, "K": Kd, "ours_us": ours, "torch_us": ref, "rel_err": err})

@@ -8,11 +8,14 @@
 //   S = Q K^T on MFMA (Q fragments in registers), online softmax in registers
 //   (row stats reduced over the 16 lanes that share a row), P -> per-wave LDS
 //   tile (bf16) -> O += P V on MFMA.  Saves LSE (of the scaled scores) per row.
-// backward  (1) delta = rowsum(dO * O); (2) grid (S/64 key blocks, B*H), each
-//   wave owns 16 keys: P^T = exp(scale K Q^T - LSE) recomputed per 64-query tile,
-//   dP^T = V dO^T, dS^T = P^T (dP^T - delta), dV += P^T dO, dK += dS^T Q (fp32
-//   accumulators in registers for the whole sweep), dQ += dS K summed across key
-//   blocks with fp32 atomics; (3) dQ fp32 -> bf16 into the QKV-gradient buffer.
+// backward  ONE launch, grid (S/64 key blocks, B*H), each wave owns 16 keys:
+//   per 64-query tile delta = rowsum(dO * O) (recomputed, cheaper than a launch),
+//   P^T = exp(scale K Q^T - LSE), dP^T = V dO^T, dS^T = P^T (dP^T - delta),
+//   dV += P^T dO, dK += dS^T Q (fp32 accumulators in registers for the whole
+//   sweep), dQ += dS K summed across key blocks with fp32 atomics into a
+//   persistent zeroed workspace; the key block that arrives last for its
+//   (batch, head) (ticket) converts that head's dQ to bf16 into the QKV
+//   gradient and re-zeroes the workspace -- no memset, delta or convert launch.
 #include "common.h"
 
 namespace jdt {
@@ -143,33 +146,11 @@ __global__ void __launch_bounds__(256) flash_fwd_kernel(const bf16_t* __restrict
   }
 }
 
-// delta[bh, q] = sum_d dO[b, q, h, d] * O[b, q, h, d]   (one thread per (row, head))
-__global__ void __launch_bounds__(256) flash_bwd_pre_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ o,
-                                                            float* __restrict__ delta, int B, int S, int H) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long)B * S * H) return;
-  const int h = (int)(i % H);
-  const long bq = i / H;
-  const int b = (int)(bq / S), q = (int)(bq % S);
-  const long off = bq * (long)H * FD + h * FD;
-  float s = 0.f;
-#pragma unroll
-  for (int c = 0; c < FD; c += 8) {
-    const u32x4 a = *reinterpret_cast<const u32x4*>(dout + off + c);
-    const u32x4 v = *reinterpret_cast<const u32x4*>(o + off + c);
-    const unsigned wa[4] = {a.x, a.y, a.z, a.w}, wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      s += bf2f((bf16_t)(wa[j] & 0xffff)) * bf2f((bf16_t)(wv[j] & 0xffff)) +
-           bf2f((bf16_t)(wa[j] >> 16)) * bf2f((bf16_t)(wv[j] >> 16));
-  }
-  delta[((long)b * H + h) * S + q] = s;
-}
-
-__global__ void __launch_bounds__(256) flash_bwd_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
-                                                        const float* __restrict__ lse, const float* __restrict__ delta,
-                                                        bf16_t* __restrict__ dqkv, float* __restrict__ dq_acc, int S,
-                                                        int H, float scale, int causal) {
+__global__ void __launch_bounds__(256) flash_bwd_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
+                                                        const bf16_t* __restrict__ dout, const float* __restrict__ lse,
+                                                        bf16_t* __restrict__ dqkv, float* __restrict__ dq_acc,
+                                                        unsigned* __restrict__ tickets, int S, int H, float scale,
+                                                        int causal) {
   __shared__ __attribute__((aligned(16))) bf16_t Qs[FB * FLD];
   __shared__ __attribute__((aligned(16))) bf16_t Qt[FD * FLD];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[FB * FLD];
@@ -179,6 +160,7 @@ __global__ void __launch_bounds__(256) flash_bwd_kernel(const bf16_t* __restrict
   __shared__ __attribute__((aligned(16))) bf16_t dSw[4][16 * FLD];
   __shared__ __attribute__((aligned(16))) bf16_t dSq[FB * FLD];   // dS[q][key] for dQ
   __shared__ float lse_s[FB], delta_s[FB];
+  __shared__ int last_s;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int bh = blockIdx.y, b = bh / H, h = bh % H;
   const int d = H * FD, ld3 = 3 * d;
@@ -206,9 +188,24 @@ __global__ void __launch_bounds__(256) flash_bwd_kernel(const bf16_t* __restrict
     stage_tile(base + (long)q0 * ld3 + h * FD, ld3, S - q0, Qs, Qt);
     stage_tile(dbase + (long)q0 * d + h * FD, d, S - q0, dOs, dOt);
     if (threadIdx.x < FB) {
+      // delta[q] = dO[q, h, :] . O[q, h, :]
       const int q = q0 + threadIdx.x;
+      float dl = 0.f;
+      if (q < S) {
+        const long off = ((long)b * S + q) * d + h * FD;
+#pragma unroll
+        for (int c = 0; c < FD; c += 8) {
+          const u32x4 x = *reinterpret_cast<const u32x4*>(dout + off + c);
+          const u32x4 y = *reinterpret_cast<const u32x4*>(o + off + c);
+          const unsigned wx[4] = {x.x, x.y, x.z, x.w}, wy[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            dl += bf2f((bf16_t)(wx[j] & 0xffff)) * bf2f((bf16_t)(wy[j] & 0xffff)) +
+                  bf2f((bf16_t)(wx[j] >> 16)) * bf2f((bf16_t)(wy[j] >> 16));
+        }
+      }
       lse_s[threadIdx.x] = q < S ? lse[(long)bh * S + q] : 0.f;
-      delta_s[threadIdx.x] = q < S ? delta[(long)bh * S + q] : 0.f;
+      delta_s[threadIdx.x] = dl;
     }
     __syncthreads();
     // S^T = K Q^T, dP^T = V dO^T   (rows: this wave's 16 keys; cols: 64 queries)
@@ -285,15 +282,43 @@ __global__ void __launch_bounds__(256) flash_bwd_kernel(const bf16_t* __restrict
       row[2 * d + nt * 16] = f2bf(dv[nt][e]);
     }
   }
-}
-
-__global__ void __launch_bounds__(256) flash_bwd_post_kernel(const float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv,
-                                                             long T, int d) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= T * d) return;
-  const long t = i / d;
-  const int c = (int)(i % d);
-  dqkv[t * 3 * d + c] = f2bf(dq_acc[i]);
+  // last key block of this (batch, head): dQ fp32 -> bf16, workspace re-zeroed.
+  // The dQ atomics are device-scope (performed past the per-XCD L2s); drain
+  // them (vmcnt) before the ticket; the last arriver acquires at agent scope
+  // (invalidating its XCD's L2) and then reads the head's dQ with plain
+  // 16-byte loads, all in flight at once.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(tickets + bh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == gridDim.x - 1;
+    if (last) __hip_atomic_store(tickets + bh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_s = last;
+  }
+  __syncthreads();
+  if (!last_s) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  constexpr int QV = FD / 4;  // float4 per row
+  for (int i0 = 0; i0 < S * QV; i0 += 256 * 8) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 256 + threadIdx.x;
+      v[u] = i < S * QV ? *reinterpret_cast<const float4*>(dq_acc + ((long)b * S + i / QV) * d + h * FD + (i % QV) * 4)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 256 + threadIdx.x;
+      if (i >= S * QV) continue;
+      const int q = i / QV, c = (i % QV) * 4;
+      *reinterpret_cast<float4*>(dq_acc + ((long)b * S + q) * d + h * FD + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+      uint2 pk;
+      pk.x = (unsigned)f2bf(v[u].x) | ((unsigned)f2bf(v[u].y) << 16);
+      pk.y = (unsigned)f2bf(v[u].z) | ((unsigned)f2bf(v[u].w) << 16);
+      *reinterpret_cast<uint2*>(dqkv + ((long)b * S + q) * ld3 + h * FD + c) = pk;
+    }
+  }
 }
 
 }  // namespace jdt
@@ -307,18 +332,13 @@ JDT_API int jdt_flash_fwd(const void* qkv, void* out, float* lse, int B, int S, 
   return HIP_LAUNCH_CHECK();
 }
 
-// dq_acc: fp32 [B*S, H*64] zeroed by the caller.
-JDT_API int jdt_flash_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta,
-                          float* dq_acc, void* dqkv, int B, int S, int H, float scale, int causal, void* stream) {
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  const long rows = (long)B * S * H;
-  hipLaunchKernelGGL(flash_bwd_pre_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
-                     static_cast<const bf16_t*>(dout), static_cast<const bf16_t*>(out), delta, B, S, H);
-  hipLaunchKernelGGL(flash_bwd_kernel, dim3((S + FB - 1) / FB, B * H), dim3(256), 0, st,
-                     static_cast<const bf16_t*>(qkv), static_cast<const bf16_t*>(dout), lse, delta,
-                     static_cast<bf16_t*>(dqkv), dq_acc, S, H, scale, causal);
-  const long n = (long)B * S * H * FD;
-  hipLaunchKernelGGL(flash_bwd_post_kernel, dim3((n + 255) / 256), dim3(256), 0, st, dq_acc,
-                     static_cast<bf16_t*>(dqkv), (long)B * S, H * FD);
+// dq_acc: fp32 [B*S, H*64] workspace, all zero on entry and left zero on exit;
+// tickets: B*H counters, zero on entry and on exit.
+JDT_API int jdt_flash_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* dq_acc,
+                          unsigned* tickets, void* dqkv, int B, int S, int H, float scale, int causal, void* stream) {
+  hipLaunchKernelGGL(flash_bwd_kernel, dim3((S + FB - 1) / FB, B * H), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const bf16_t*>(qkv), static_cast<const bf16_t*>(out),
+                     static_cast<const bf16_t*>(dout), lse, static_cast<bf16_t*>(dqkv), dq_acc, tickets, S, H, scale,
+                     causal);
   return HIP_LAUNCH_CHECK();
 }

@@ -68,95 +68,111 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
-// ROWS rows per workgroup (4 waves x ROWS/4 rows each); dgamma/dbeta partials in LDS.
-template <int NV>
+// Backward: a wave owns R rows whose x / dy / dres loads are all issued before
+// any arithmetic; dgamma, dbeta and the optional colsum(dx) are accumulated in
+// registers over the wave's rows, summed over the 4 waves in LDS, and added to
+// the outputs with one fp32 atomic per column per workgroup.
+template <int NV, int R>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                      const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                      const float* __restrict__ gamma, const bf16_t* __restrict__ dres,
                                                      bf16_t* __restrict__ dx, float* __restrict__ dgamma,
-                                                     float* __restrict__ dbeta, float* __restrict__ dsum, int T, int d,
-                                                     int rows_per_wave) {
-  __shared__ float sg[2048], sb[2048], sd[2048];
-  for (int i = threadIdx.x; i < d; i += 256) { sg[i] = 0.f; sb[i] = 0.f; sd[i] = 0.f; }
-  __syncthreads();
+                                                     float* __restrict__ dbeta, float* __restrict__ dsum, int T, int d) {
+  __shared__ float part[4][512 * NV];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float ag[NV][8], ab[NV][8], ad[NV][8];
+  const int r0 = (blockIdx.x * 4 + w) * R;
+  float ag[NV][8], ab[NV][8], ad[NV][8], gm[NV][8];
+  u32x4 px[R][NV], pd[R][NV], pr[R][NV];
+  float mean[R], rstd[R];
 #pragma unroll
-  for (int c = 0; c < NV; ++c)
+  for (int c = 0; c < NV; ++c) {
+    const int col = (c * 64 + lane) * 8;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { ag[c][j] = 0.f; ab[c][j] = 0.f; ad[c][j] = 0.f; }
-  const int r0 = (blockIdx.x * 4 + w) * rows_per_wave;
-  for (int row = r0; row < min(T, r0 + rows_per_wave); ++row) {
-    const float mean = mean_in[row], rstd = rstd_in[row];
+    for (int j = 0; j < 8; ++j) { ag[c][j] = 0.f; ab[c][j] = 0.f; ad[c][j] = 0.f; gm[c][j] = 0.f; }
+    if (col < d) {
+      const float4 g0 = *reinterpret_cast<const float4*>(gamma + col);
+      const float4 g1 = *reinterpret_cast<const float4*>(gamma + col + 4);
+      gm[c][0] = g0.x; gm[c][1] = g0.y; gm[c][2] = g0.z; gm[c][3] = g0.w;
+      gm[c][4] = g1.x; gm[c][5] = g1.y; gm[c][6] = g1.z; gm[c][7] = g1.w;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int row = r0 + i;
+    const bool ok = row < T;
+    mean[i] = ok ? mean_in[row] : 0.f;
+    rstd[i] = ok ? rstd_in[row] : 0.f;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      const u32x4 zero = {0u, 0u, 0u, 0u};
+      px[i][c] = zero; pd[i][c] = zero; pr[i][c] = zero;
+      if (ok && col < d) {
+        px[i][c] = *reinterpret_cast<const u32x4*>(x + (long)row * d + col);
+        pd[i][c] = *reinterpret_cast<const u32x4*>(dy + (long)row * d + col);
+        if (dres) pr[i][c] = *reinterpret_cast<const u32x4*>(dres + (long)row * d + col);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int row = r0 + i;
     float xh[NV][8], g[NV][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
-      const int col = (c * 64 + lane) * 8;
-      if (col < d) {
-        const u32x4 px = *reinterpret_cast<const u32x4*>(x + (long)row * d + col);
-        const u32x4 pd = *reinterpret_cast<const u32x4*>(dy + (long)row * d + col);
-        const unsigned wx[4] = {px.x, px.y, px.z, px.w}, wd[4] = {pd.x, pd.y, pd.z, pd.w};
+      const unsigned wx[4] = {px[i][c].x, px[i][c].y, px[i][c].z, px[i][c].w};
+      const unsigned wd[4] = {pd[i][c].x, pd[i][c].y, pd[i][c].z, pd[i][c].w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float xv = bf2f((bf16_t)((wx[j >> 1] >> (16 * (j & 1))) & 0xffff));
-          const float dv = bf2f((bf16_t)((wd[j >> 1] >> (16 * (j & 1))) & 0xffff));
-          xh[c][j] = (xv - mean) * rstd;
-          g[c][j] = dv * gamma[col + j];
-          s1 += g[c][j];
-          s2 += g[c][j] * xh[c][j];
-          ag[c][j] += dv * xh[c][j];
-          ab[c][j] += dv;
-        }
+      for (int j = 0; j < 8; ++j) {
+        const float xv = bf2f((bf16_t)((wx[j >> 1] >> (16 * (j & 1))) & 0xffff));
+        const float dv = bf2f((bf16_t)((wd[j >> 1] >> (16 * (j & 1))) & 0xffff));
+        xh[c][j] = (xv - mean[i]) * rstd[i];
+        g[c][j] = dv * gm[c][j];
+        s1 += g[c][j];
+        s2 += g[c][j] * xh[c][j];
+        ag[c][j] += dv * xh[c][j];
+        ab[c][j] += dv;
       }
     }
     s1 = wave_sum(s1) / d;
     s2 = wave_sum(s2) / d;
+    if (row < T) {
 #pragma unroll
-    for (int c = 0; c < NV; ++c) {
-      const int col = (c * 64 + lane) * 8;
-      if (col < d) {
-        float r[8];
-        if (dres) {
-          const u32x4 pr = *reinterpret_cast<const u32x4*>(dres + (long)row * d + col);
-          const unsigned wr[4] = {pr.x, pr.y, pr.z, pr.w};
+      for (int c = 0; c < NV; ++c) {
+        const int col = (c * 64 + lane) * 8;
+        if (col < d) {
+          const unsigned wr[4] = {pr[i][c].x, pr[i][c].y, pr[i][c].z, pr[i][c].w};
+          unsigned o[4];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) r[j] = bf2f((bf16_t)((wr[j >> 1] >> (16 * (j & 1))) & 0xffff));
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) r[j] = 0.f;
+          for (int j = 0; j < 4; ++j) {
+            const float ra = bf2f((bf16_t)(wr[j] & 0xffff)), rb = bf2f((bf16_t)(wr[j] >> 16));
+            const float va = ra + rstd[i] * (g[c][2 * j] - s1 - xh[c][2 * j] * s2);
+            const float vb = rb + rstd[i] * (g[c][2 * j + 1] - s1 - xh[c][2 * j + 1] * s2);
+            const bf16_t ha = f2bf(va), hb = f2bf(vb);
+            o[j] = (unsigned)ha | ((unsigned)hb << 16);
+            ad[c][2 * j] += bf2f(ha);  // colsum of exactly the stored dx (next layer's bias grad)
+            ad[c][2 * j + 1] += bf2f(hb);
+          }
+          u32x4 ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
+          *reinterpret_cast<u32x4*>(dx + (long)row * d + col) = ov;
         }
-        unsigned o[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float a = r[2 * j] + rstd * (g[c][2 * j] - s1 - xh[c][2 * j] * s2);
-          const float b = r[2 * j + 1] + rstd * (g[c][2 * j + 1] - s1 - xh[c][2 * j + 1] * s2);
-          const bf16_t ha = f2bf(a), hb = f2bf(b);
-          o[j] = (unsigned)ha | ((unsigned)hb << 16);
-          ad[c][2 * j] += bf2f(ha);   // colsum of exactly the stored dx (next layer's bias grad)
-          ad[c][2 * j + 1] += bf2f(hb);
-        }
-        u32x4 ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
-        *reinterpret_cast<u32x4*>(dx + (long)row * d + col) = ov;
       }
     }
   }
+  // three column reductions through one LDS image, one atomic per column each
+  float (*acc3[3])[8] = {ag, ab, ad};
+  float* outs[3] = {dgamma, dbeta, dsum};
 #pragma unroll
-  for (int c = 0; c < NV; ++c) {
-    const int col = (c * 64 + lane) * 8;
-    if (col < d)
+  for (int t = 0; t < 3; ++t) {
+    if (!outs[t]) continue;  // uniform
+    __syncthreads();
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        atomicAdd(&sg[col + j], ag[c][j]);
-        atomicAdd(&sb[col + j], ab[c][j]);
-        if (dsum) atomicAdd(&sd[col + j], ad[c][j]);
-      }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < d; i += 256) {
-    if (dgamma) atomicAdd(dgamma + i, sg[i]);
-    if (dbeta) atomicAdd(dbeta + i, sb[i]);
-    if (dsum) atomicAdd(dsum + i, sd[i]);
+    for (int c = 0; c < NV; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part[w][(c * 64 + lane) * 8 + j] = acc3[t][c][j];
+    __syncthreads();
+    for (int i = threadIdx.x; i < d; i += 256) atomicAdd(outs[t] + i, part[0][i] + part[1][i] + part[2][i] + part[3][i]);
   }
 }
 
@@ -186,19 +202,23 @@ JDT_API int jdt_ln_bwd(const void* dy, const void* x, const float* mean, const f
                        void* stream) {
   if (d % 8 || d > 2048) return -3;
   const int nv = (d / 8 + 63) / 64;
-  // one or two rows per wave: enough workgroups to cover the CUs, few enough
-  // that the per-workgroup dgamma/dbeta atomics stay cheap
-  const int rpw = T <= 1024 ? 1 : (T + 1023) / 1024;
-  dim3 grid((T + 4 * rpw - 1) / (4 * rpw));
+  // rows per wave: R = 2 up to 2048 rows, 4 beyond (fewer workgroups -> fewer
+  // same-address column atomics; all of a wave's row loads are in flight at once)
   hipStream_t st = static_cast<hipStream_t>(stream);
   auto a = static_cast<const bf16_t*>(dy);
   auto b = static_cast<const bf16_t*>(x);
   auto r = static_cast<const bf16_t*>(dres);
   auto o = static_cast<bf16_t*>(dx);
+  if ((reinterpret_cast<uintptr_t>(gamma) & 15)) return -3;
+#define JDT_LNB(NV_, R_)                                                                                        \
+  hipLaunchKernelGGL((ln_bwd_kernel<NV_, R_>), dim3((T + 4 * R_ - 1) / (4 * R_)), dim3(256), 0, st, a, b, mean, \
+                     rstd, gamma, r, o, dgamma, dbeta, dsum, T, d)
+  const bool big = T > 2048;
   switch (nv) {
-    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(256), 0, st, a, b, mean, rstd, gamma, r, o, dgamma, dbeta, dsum, T, d, rpw); break;
-    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(256), 0, st, a, b, mean, rstd, gamma, r, o, dgamma, dbeta, dsum, T, d, rpw); break;
-    default: hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(256), 0, st, a, b, mean, rstd, gamma, r, o, dgamma, dbeta, dsum, T, d, rpw); break;
+    case 1: if (big) JDT_LNB(1, 4); else JDT_LNB(1, 2); break;
+    case 2: if (big) JDT_LNB(2, 4); else JDT_LNB(2, 2); break;
+    default: if (big) JDT_LNB(4, 2); else JDT_LNB(4, 1); break;
   }
+#undef JDT_LNB
   return HIP_LAUNCH_CHECK();
 }

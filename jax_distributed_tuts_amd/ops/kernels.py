@@ -434,6 +434,22 @@ def attention_fwd(qkv: torch.Tensor, B: int, S: int, H: int, causal: bool = True
     return o, P
 
 
+_FLASH_WS: dict = {}
+
+
+def _flash_workspace(device, n: int, bh: int):
+    """Persistent zeroed dQ accumulator + per-(batch, head) tickets for jdt_flash_bwd
+    (the kernel leaves both zero again, so one allocation serves every call, eager
+    or graph-replayed; the framework issues all compute on one stream per device)."""
+    key = str(device)
+    ws = _FLASH_WS.get(key)
+    if ws is None or ws[0].numel() < n or ws[1].numel() < bh:
+        ws = (torch.zeros(max(n, ws[0].numel() if ws else 0), dtype=torch.float32, device=device),
+              torch.zeros(max(bh, ws[1].numel() if ws else 0), dtype=torch.int32, device=device))
+        _FLASH_WS[key] = ws
+    return ws
+
+
 def attention_bwd(do: torch.Tensor, qkv: torch.Tensor, P: torch.Tensor, B: int, S: int, H: int,
                   dqkv: Optional[torch.Tensor] = None, o: Optional[torch.Tensor] = None,
                   causal: bool = True) -> torch.Tensor:
@@ -447,9 +463,8 @@ def attention_bwd(do: torch.Tensor, qkv: torch.Tensor, P: torch.Tensor, B: int, 
         dqkv = torch.empty_like(qkv)
     if _is_gpu(qkv) and P.dim() == 2:
         assert o is not None and do.is_contiguous() and o.is_contiguous() and dqkv.is_contiguous()
-        delta = torch.empty(B * H, S, dtype=torch.float32, device=qkv.device)
-        dq_acc = torch.zeros(T, d, dtype=torch.float32, device=qkv.device)
-        rc = _lib.lib().jdt_flash_bwd(_ptr(qkv), _ptr(o), _ptr(do), _ptr(P), _ptr(delta), _ptr(dq_acc), _ptr(dqkv),
+        dq_acc, tickets = _flash_workspace(qkv.device, T * d, B * H)
+        rc = _lib.lib().jdt_flash_bwd(_ptr(qkv), _ptr(o), _ptr(do), _ptr(P), _ptr(dq_acc), _ptr(tickets), _ptr(dqkv),
                                       B, S, H, float(scale), int(causal), _lib.stream_ptr())
         _lib.check(rc, "jdt_flash_bwd")
         return dqkv

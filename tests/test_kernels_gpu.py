@@ -283,6 +283,12 @@ def test_attention_fwd_bwd(B, S, H, Dh):
     g_r = kern.attention_bwd(do, qkv, p_r, B, S, H)
     g_g = kern.attention_bwd(do.to(DEV), qkv.to(DEV), p_g, B, S, H)
     _close(g_g, g_r, rtol=3e-2, atol=3e-2)
+    # flash path twice in a row: its persistent dQ workspace and tickets are left zeroed
+    o_f, lse_f = kern.attention_fwd(qkv.to(DEV), B, S, H)
+    g1 = kern.attention_bwd(do.to(DEV), qkv.to(DEV), lse_f, B, S, H, o=o_f)
+    g2 = kern.attention_bwd(do.to(DEV), qkv.to(DEV), lse_f, B, S, H, o=o_f)
+    assert torch.equal(g1, g2)
+    _close(g1, g_r, rtol=3e-2, atol=3e-2)
 
 
 def test_embedding_and_colsum():

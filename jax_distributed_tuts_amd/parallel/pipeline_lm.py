@@ -20,7 +20,7 @@ def lm_batch(cfg: TransformerConfig, global_batch: int = 16, seed: int = 1) -> B
 
 def build_lm_pipeline(mesh: Mesh, dev, cfg: TransformerConfig = TransformerConfig(), num_microbatches: int = 4,
                       lr: float = 3e-4, seed: int = 0, comm: str = "auto"):
-    S, s = mesh.axis_size("pipe"), mesh.axis_index("pipe")
+    S, s = (mesh.axis_size("pipe"), mesh.axis_index("pipe")) if mesh is not None else (1, 0)
     stage = lm_stage(cfg, S, s)
     full = TransformerLM(cfg)
     P = init_stage_params(stage, full.param_specs(), seed, dev)

@@ -144,3 +144,38 @@ def test_pipeline_over_xgmi_matches_single_device(tmp_path, ws, dp):
     m, rm = res[0]["metrics"], tr.metrics.cpu()
     assert float(m[1]) == float(rm[1]) and float(m[3]) == float(rm[3])
     assert abs(float(m[0]) - float(rm[0])) <= 2e-3 * abs(float(rm[0])) + 1e-3
+
+
+def test_transformer_hybrid_over_xgmi_matches_single_device(tmp_path):
+    """Transformer LM, DP=2 x PP=2 over xGMI (4 processes on the GPU), captured
+    into hipGraphs == the un-split model trained on the whole batch on one device."""
+    import functools
+
+    from jax_distributed_tuts_amd.models.transformer import TransformerConfig
+    from jax_distributed_tuts_amd.parallel.pipeline import GPipeTrainer, PipeConfig
+    from jax_distributed_tuts_amd.parallel.pipeline_lm import build_lm_pipeline, lm_batch
+    from jax_distributed_tuts_amd.utils.train_state import Batch
+
+    spawn(functools.partial(XW.lm_pp_xgmi, dp=2), 4, str(tmp_path), gpu=True)
+    res = _load(tmp_path, "lmx2", 4)
+    assert all(o["comm"] == "xgmi" for o in res)
+    dev = torch.device("cuda", 0)
+    cfg = TransformerConfig(vocab_size=512, d_model=128, n_heads=2, d_ff=256, seq_len=64, n_layers=2)
+    tr, _ = build_lm_pipeline(None, dev, cfg, num_microbatches=4)  # dp=2 x 2 microbatches == 4 microbatches
+    b = lm_batch(cfg, global_batch=8, seed=1)
+    b = Batch(b.inputs.to(dev), b.labels.to(dev))
+    for _ in range(3):
+        tr.step(b)
+    torch.cuda.synchronize()
+    ref = {k: v.cpu() for k, v in tr.state.params.state_dict().items()}
+    seen = set()
+    for o in res:
+        for k, v in o["params"].items():
+            d = (v - ref[k]).abs()
+            assert float(d.max()) <= 2 * 3e-4 * 3 + 1e-6, k
+            assert float((d > 2e-5).float().mean()) < 5e-2, k
+            seen.add(k)
+    assert seen == set(ref)
+    m, rm = res[0]["metrics"], tr.metrics.cpu()
+    assert float(m[1]) == float(rm[1])
+    assert abs(float(m[0]) - float(rm[0])) <= 2e-3 * abs(float(rm[0])) + 1e-2

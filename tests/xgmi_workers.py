@@ -244,3 +244,28 @@ def p2p_roundtrip(outdir):
         res["err"] = c.error()
         c.close()
     _save(outdir, "p2p", res)
+
+
+def lm_pp_xgmi(outdir, dp, steps=3):
+    """Transformer LM (small config) over a (data=dp, pipe=W/dp) mesh with the xGMI
+    inbox hand-off and the fused data-axis all-reduce; eager step, then graphs."""
+    from jax_distributed_tuts_amd.models.transformer import TransformerConfig
+    from jax_distributed_tuts_amd.parallel.dp import shard_batch
+    from jax_distributed_tuts_amd.parallel.pipeline_lm import build_lm_pipeline, lm_batch
+    from jax_distributed_tuts_amd.runtime import dist as D
+    from jax_distributed_tuts_amd.utils.train_state import Batch
+
+    dev = D.device()
+    cfg = TransformerConfig(vocab_size=512, d_model=128, n_heads=2, d_ff=256, seq_len=64, n_layers=2)
+    mesh = D.Mesh({"data": dp, "pipe": D.world_size() // dp})
+    tr, _ = build_lm_pipeline(mesh, dev, cfg, num_microbatches=2, comm="xgmi")
+    b = shard_batch(lm_batch(cfg, global_batch=8, seed=1), mesh, "data")
+    b = Batch(b.inputs.to(dev), b.labels.to(dev))
+    tr.step(b)
+    assert tr.capturable and tr.p2p is not None
+    tr.capture(b, steps_per_graph=2)
+    tr.run_steps(b, steps - 1)
+    torch.cuda.synchronize()
+    tr.finalize()
+    _save(outdir, f"lmx{dp}", {"params": {k: v.cpu() for k, v in tr.state.params.state_dict().items()},
+                               "metrics": tr.gather_metrics().cpu(), "comm": tr.comm_backend})

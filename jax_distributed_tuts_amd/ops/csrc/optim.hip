@@ -112,6 +112,10 @@ static int grid_for(long n, int per_thread, int cap = 2048) {
 // arrival ticket per workgroup; those atomics serialise, so those kernels run
 // at most one workgroup per CU and grid-stride over the rest.
 constexpr int kTicketGrid = 256;
+// Large buffers (the transformer's ~13M params): a 256-workgroup grid-stride
+// loop is latency-bound (each thread's iterations are serial round trips), so
+// above ~1M elements the grid grows to 2048 workgroups (8 per CU).
+static int ticket_grid(long n, int per_thread) { return grid_for(n, per_thread, n > (1L << 20) ? 2048 : kTicketGrid); }
 
 }  // namespace jdt
 using namespace jdt;
@@ -123,7 +127,7 @@ JDT_API int jdt_adamw(float* p, float* g, float* m, float* v, void* shadow, long
   if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
        reinterpret_cast<uintptr_t>(v)) & 15) return -2;
   if (shadow && (reinterpret_cast<uintptr_t>(shadow) & 7)) return -2;
-  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n, 4, kTicketGrid)), dim3(256), 0, static_cast<hipStream_t>(stream), p, g, m, v,
+  hipLaunchKernelGGL(adamw_kernel, dim3(ticket_grid(n, 4)), dim3(256), 0, static_cast<hipStream_t>(stream), p, g, m, v,
                      static_cast<bf16_t*>(shadow), n, lr, b1, b2, eps, wd, grad_scale, step, ticket, zero_grad);
   return HIP_LAUNCH_CHECK();
 }
@@ -131,7 +135,7 @@ JDT_API int jdt_adamw(float* p, float* g, float* m, float* v, void* shadow, long
 JDT_API int jdt_sgd(float* p, float* g, float* buf, void* shadow, long n, float lr, float momentum, float wd,
                     float grad_scale, int* step, unsigned* ticket, int zero_grad, void* stream) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n, 1, step ? kTicketGrid : 2048)), dim3(256), 0, static_cast<hipStream_t>(stream), p, g, buf,
+  hipLaunchKernelGGL(sgd_kernel, dim3(step ? ticket_grid(n, 1) : grid_for(n, 1)), dim3(256), 0, static_cast<hipStream_t>(stream), p, g, buf,
                      static_cast<bf16_t*>(shadow), n, lr, momentum, wd, grad_scale, step, ticket, zero_grad);
   return HIP_LAUNCH_CHECK();
 }

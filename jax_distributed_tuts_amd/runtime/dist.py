@@ -52,7 +52,9 @@ def sim_cpu_requested() -> bool:
 def init(backend: Optional[str] = None, timeout_s: float = 600.0) -> torch.device:
     """Initialise the process group from torchrun-style env vars (idempotent).
 
-    backend None -> ``nccl`` (RCCL) when a GPU is usable and simulation is not
+    backend None -> ``$JDT_BACKEND`` if set (``gloo`` rehearses several ranks
+    sharing one GPU -- RCCL refuses that -- while the xGMI P2P kernels still
+    run), else ``nccl`` (RCCL) when a GPU is usable and simulation is not
     requested, else ``gloo`` on CPU.  Sets the current HIP device to LOCAL_RANK.
     """
     use_gpu = (not sim_cpu_requested()) and torch.cuda.is_available()
@@ -64,7 +66,7 @@ def init(backend: Optional[str] = None, timeout_s: float = 600.0) -> torch.devic
     _STATE["device"] = dev
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws > 1 and not is_initialized():
-        be = backend or ("nccl" if use_gpu else "gloo")
+        be = backend or os.environ.get("JDT_BACKEND") or ("nccl" if use_gpu else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":

@@ -811,13 +811,31 @@ static int launch_cfg(const GemmArgs& g, int batch, int splits, float* ws, long 
 }
 
 
-static bool g_gemm_no_dma = false;
+static bool g_gemm_no_dma = false;  // jdt_gemm_set_dma(0): register-staged kernels only (A/B tests)
 
-// Ring depth 3 (one K-tile in flight across each barrier): measured better than
-// deeper rings, which cost resident workgroups per CU (tools/bench_gemm.py:
-// qkv 512x1536x512 6.8 us at 3 stages, 9.8 us at 8).
+// LDS ring depth 3 (one K-tile in flight across each barrier).  Deeper rings
+// cost resident workgroups per CU (qkv 512x1536x512: 9.8 us with 8 stages vs
+// 6.8 with 3); a plain double buffer (2) is as fast for an isolated GEMM but
+// 4-8 % slower inside the transformer / GPipe steps, where the operands are
+// colder (tools/bench_gemm.py, bench.py --strategy pp).
 template <int BM, int BN>
 constexpr int dma_stages() { return 3; }
+
+template <int WM, int WN, int TM, int TN>
+static int launch_dma(const GemmArgs& g, int batch, int splits, float* ws, long ws_floats, unsigned* counters,
+                      long n_counters, hipStream_t st) {
+  constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
+  if (g.M % BM || g.N % BN) return 1;
+  const int tiles_n = g.N / BN;
+  const long tiles = (long)(g.M / BM) * tiles_n * batch;
+  int sp = splits;
+  if (sp < 0) {
+    // Measured (tools/bench_gemm.py sweeps): many small workgroups per CU hide
+    // the load latency better than a split-K combine; split only while the
+    // grid has < 2 workgroups per CU, keeping slices >= 8 K-tiles.
+    sp = 1;
+    while (sp < 16 && tiles * sp < 512 && (g.K / (2 * sp)) % DMA_BK == 0 && g.K / (2 * sp) >= 8 * DMA_BK) sp *= 2;
+  }
   if (sp < 1 || g.K % sp || (g.K / sp) % DMA_BK) return 1;
   if (sp > 1 && (!ws || !counters || tiles * sp * BM * BN > ws_floats || tiles > n_counters)) sp = 1;
   const int kchunk = g.K / sp;
@@ -825,8 +843,7 @@ constexpr int dma_stages() { return 3; }
   const bool at = g.a_trans, bt = g.b_trans;
 #define JDT_DMA(A_, B_)                                                                                     \
   hipLaunchKernelGGL((gemm_dma_kernel<WM, WN, TM, TN, A_, B_, dma_stages<BM, BN>()>), grid, dim3(256), 0, st, \
-                     g, tiles_n, sp,                                                                        \
-                     kchunk, ws, counters)
+                     g, tiles_n, sp, kchunk, ws, counters)
   if (!at && !bt) JDT_DMA(false, false);
   else if (!at && bt) JDT_DMA(false, true);
   else if (at && !bt) JDT_DMA(true, false);

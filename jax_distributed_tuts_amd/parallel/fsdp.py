@@ -393,12 +393,26 @@ class FSDPTrainer:
         if self.fused is None:
             from .fused_mlp import make_engine
 
-            self.fused = make_engine(self.state, self.mesh, self.cfg.axis, self.cfg.num_minibatches, batch.size,
-                                     self.metrics, batch.inputs.device, params=sp.full,
-                                     mslot=sp.local.metrics_slot, fuse_opt=False)
+            if self.world == 1:
+                # one device: every shard is the whole leaf (param_sharding.py:89-113 at
+                # N=1) and the gather / reduce-scatter are identities, so the step is the
+                # DP engine on the local buffer with AdamW in the backward epilogue
+                self.fused = make_engine(self.state, self.mesh, self.cfg.axis, self.cfg.num_minibatches,
+                                         batch.size, self.metrics, batch.inputs.device)
+            else:
+                self.fused = make_engine(self.state, self.mesh, self.cfg.axis, self.cfg.num_minibatches,
+                                         batch.size, self.metrics, batch.inputs.device, params=sp.full,
+                                         mslot=sp.local.metrics_slot, fuse_opt=False)
             if self.fused is None:
                 self.cfg.fused_kernels = False
                 return False
+        if self.world == 1:
+            self.fused.forward_backward(batch)
+            if not self.fused.fuse_opt:
+                self.state.tx.update(sp.local, self.state.opt_state, 1.0 / self.cfg.num_minibatches, zero_grad=False)
+                with named_scope("synch_metrics"):
+                    K.metrics_fold_(self.metrics, sp.local.metrics_slot)
+            return True
         sp.gather()
         self.fused.forward_backward(batch)
         sp.scatter_grads(accumulate=False, zero_full=False)
@@ -474,6 +488,8 @@ class FSDPTrainer:
             K.metrics_fold_(self.metrics, sp.local.metrics_slot)
 
     def finalize(self):
+        if self.fused is not None and self.world == 1:
+            self.fused.finalize()  # bf16 shadow parity of the in-epilogue AdamW
         if self.sp.xg is not None and self.sp.xg.error():
             raise RuntimeError("xgmi collective timed out on this rank (peer dead or desynchronised)")
 

@@ -105,8 +105,12 @@ __device__ __forceinline__ float adam_elem(float* p, float* m, float* v, long i,
 }
 
 // ---------------------------------------------------------------------------- forward
-template <int K_IN, int C>
+// RB rows per workgroup (16 or 32): 16-row blocks halve each workgroup's X
+// bytes and double the grid (256 workgroups at M = 128), which the load-latency
+// bound phase 1 prefers.
+template <int K_IN, int C, int RB>
 __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
+  static_assert(RB == 16 || RB == 32, "row block");
   constexpr int KS = (K_IN + 31) / 32;  // 32-deep MFMA k-steps
   constexpr int KP = KS * 32;
   constexpr int LDW = KP + 8;           // padded [n][k] row (bank spread)
@@ -116,14 +120,14 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   constexpr int LDXS = K_IN + 8;                 // padded row of the X image (bf16)
   static_assert(K_IN % XTC == 0 && XTC % 8 == 0 && K_IN % 8 == 0, "X^T chunking");
   __shared__ __attribute__((aligned(16))) bf16_t w1t[16 * LDW];
-  __shared__ __attribute__((aligned(16))) bf16_t xs[32 * LDXS];
-  __shared__ float part[NW][32][17];
-  __shared__ float htile[32][17];
+  __shared__ __attribute__((aligned(16))) bf16_t xs[RB * LDXS];
+  __shared__ float part[NW][RB][17];
+  __shared__ float htile[RB][17];
   __shared__ float w2s[16][C];
   __shared__ float b1sh[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int M = a.M, H = a.H;
-  const int r0 = blockIdx.x * 32, j0 = blockIdx.y * 16;
+  const int r0 = blockIdx.x * RB, j0 = blockIdx.y * 16;
   STAMP(0);
   const int step = a.step[0], par = step & 1;
   const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
@@ -151,10 +155,10 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
                                                  8 * (lane >> 4));
     }
   }
-  // X row block [32][K_IN] fp32: fully coalesced float4 loads (consecutive lanes,
+  // X row block [RB][K_IN] fp32: fully coalesced float4 loads (consecutive lanes,
   // consecutive 16 B), converted to bf16 into a row-major LDS image the MFMA A
   // fragments are read from (a fragment-shaped global load touches 16 rows/instr).
-  constexpr int XF4 = 32 * K_IN / 4;                 // float4 per row block
+  constexpr int XF4 = RB * K_IN / 4;                 // float4 per row block
   constexpr int XPT = (XF4 + NT - 1) / NT;           // per thread
   float4 xv[XPT];
 #pragma unroll
@@ -198,8 +202,8 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   STAMP(1);
   // X^T side output for mlp2_bwd: hidden block y < K_IN/XTC writes input features
   // [y*XTC, (y+1)*XTC) of this row block (16-byte stores of 8 consecutive samples)
-  if (a.XT && blockIdx.y < K_IN / XTC && tid < XTC * 4) {
-    const int i = tid >> 2, h = (tid & 3) * 8, xk = blockIdx.y * XTC + i;
+  if (a.XT && blockIdx.y < K_IN / XTC && tid < XTC * (RB / 8)) {
+    const int i = tid / (RB / 8), h = (tid % (RB / 8)) * 8, xk = blockIdx.y * XTC + i;
     unsigned q[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e)
@@ -209,14 +213,17 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   }
 
   // ---- 3. K split over the 8 waves
-  f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  constexpr int MT = RB / 16;
+  f32x4 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {
     if (ks0 + t < ks1) {
       const int k = (ks0 + t) * 32 + 8 * (lane >> 4);
       const bf16x8 b = direct ? bg[t] : *reinterpret_cast<const bf16x8*>(&w1t[(lane & 15) * LDW + k]);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
+      for (int mt = 0; mt < MT; ++mt) {
         bf16x8 af = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
         if (k < K_IN) af = *reinterpret_cast<const bf16x8*>(&xs[(mt * 16 + (lane & 15)) * LDXS + k]);
         acc[mt] = mfma16x16x32(af, b, acc[mt]);
@@ -224,14 +231,14 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
     }
   }
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int e = 0; e < 4; ++e) part[w][mt * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[mt][e];
   __syncthreads();
   STAMP(2);
 
   // ---- 4. bias + silu + dropout per 4-row group; H tile kept in LDS
-  if (tid < 8 * 16) {
+  if (tid < (RB / 4) * 16) {
     const int g4 = tid >> 4, c = tid & 15, col = j0 + c;
     const int rowg = r0 + g4 * 4;
     u32x4 db = {0u, 0u, 0u, 0u};
@@ -258,7 +265,7 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   __syncthreads();
   STAMP(3);
   float* lg = a.logits + (long)par * M * C;
-  if (tid < 32 * C) {
+  if (tid < RB * C) {
     const int rl = tid / C, c = tid % C, row = r0 + rl;
     if (row < M) {
       float s = (blockIdx.y == 0) ? bf2f(a.b2s[c]) : 0.f;
@@ -514,13 +521,19 @@ using namespace jdt;
 
 JDT_API int jdt_mlp2_args_size() { return (int)sizeof(Mlp2Args); }
 
+static int g_mlp2_rb = 16;  // forward rows per workgroup (jdt_mlp2_set_rows: 16 or 32, A/B tests)
+JDT_API void jdt_mlp2_set_rows(int rb) { g_mlp2_rb = rb == 32 ? 32 : 16; }
+
 // phase 0: forward, 1: backward.  Supported: K_IN = 784, C = 10, H % 16 == 0, M <= 128.
 JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* stream) {
   const Mlp2Args& a = *args;
   if (k_in != 784 || c != 10 || a.H % 16 || a.M <= 0 || a.M > 128) return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (phase == 0) {
-    hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10>), dim3((a.M + 31) / 32, a.H / 16), dim3(NT), 0, st, a);
+    if (g_mlp2_rb == 32)
+      hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 32>), dim3((a.M + 31) / 32, a.H / 16), dim3(NT), 0, st, a);
+    else
+      hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 16>), dim3((a.M + 15) / 16, a.H / 16), dim3(NT), 0, st, a);
   } else {
     hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112>), dim3(a.H / 16, 784 / 112), dim3(NT), 0, st, a);
   }

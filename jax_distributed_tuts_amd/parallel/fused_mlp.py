@@ -41,6 +41,13 @@ class Mlp2Args(ctypes.Structure):
 
 _lib.declare("jdt_mlp2", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_int, c_void_p])
 _lib.declare("jdt_mlp2_args_size", c_int, [])
+_lib.declare("jdt_mlp2_set_rows", None, [c_int])
+
+
+def set_forward_rows(rb: int):
+    """mlp2_fwd rows per workgroup: 16 (default, 256 workgroups at 128 rows) or 32
+    (A/B comparisons; env ``JDT_MLP2_RB`` sets it at engine construction)."""
+    _lib.lib().jdt_mlp2_set_rows(int(rb))
 
 
 def supported(model, rows: int, device) -> bool:
@@ -80,7 +87,9 @@ class FusedMLP2:
         # K-contiguous bf16 operand copies (zero K padding): X^T written by mlp2_fwd for
         # mlp2_bwd; W1^T written by mlp2_bwd's AdamW epilogue for the next mlp2_fwd
         self.Mp = (rows + 31) // 32 * 32
-        self.XT = torch.zeros(784, self.Mp, dtype=torch.bfloat16, device=dev)
+        self.XT = torch.zeros(784, self.Mp, dtype=torch.bfloat16, device=dev)  # sample tail stays zero
+        if os.environ.get("JDT_MLP2_RB"):
+            set_forward_rows(int(os.environ["JDT_MLP2_RB"]))
         self.W1T = None
         if self.fuse_opt:
             self.W1T = torch.zeros(H, 800, dtype=torch.bfloat16, device=dev)

@@ -6,7 +6,7 @@
 // direction (a row of layer i+1 needs the whole row of layer i), so a step is
 // one forward and one backward launch per hidden layer:
 //
-//   md_fwd (layer i)  grid (row blocks of 32) x (output blocks of 16), 8 waves
+//   md_fwd (layer i)  grid (row blocks of 16) x (output blocks of 16), 8 waves
 //     Z_i = IN W_i + b_i, H_i = dropout(silu(Z_i)); IN is the fp32 data (layer
 //     0) or H_{i-1} (bf16).  Also writes IN^T (K-contiguous, for the dW MFMA of
 //     the matching backward launch).  The last hidden layer also accumulates
@@ -105,7 +105,7 @@ __device__ __forceinline__ float md_adam(float p, float m, float v, float g, con
 }
 
 // ---------------------------------------------------------------------------- forward
-template <int K_IN, bool XF32, int XTC, bool HEAD, int C>
+template <int K_IN, bool XF32, int XTC, bool HEAD, int C, int RB>
 __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
   constexpr int NT = MD_NT, NW = MD_NW;
   constexpr int KS = (K_IN + 31) / 32;
@@ -116,14 +116,14 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
   constexpr int LDXS = K_IN + 8;
   static_assert(K_IN % XTC == 0 && XTC % 8 == 0 && XTC * 4 <= NT && K_IN % 8 == 0, "IN^T chunking");
   __shared__ __attribute__((aligned(16))) bf16_t wt[16 * LDW];
-  __shared__ __attribute__((aligned(16))) bf16_t xs[32 * LDXS];
-  __shared__ float part[NW][32][17];
-  __shared__ float htile[32][17];
+  __shared__ __attribute__((aligned(16))) bf16_t xs[RB * LDXS];
+  __shared__ float part[NW][RB][17];
+  __shared__ float htile[RB][17];
   __shared__ float whs[16][C > 0 ? C : 1];
   __shared__ float bsh[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int M = a.M, N = a.N;
-  const int r0 = blockIdx.x * 32, j0 = blockIdx.y * 16;
+  const int r0 = blockIdx.x * RB, j0 = blockIdx.y * 16;
   const int step = a.step[0], par = step & 1;
   const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
   const bf16_t* Ws = par ? a.Ws1 : a.Ws0;
@@ -149,9 +149,9 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
                                                  8 * (lane >> 4));
     }
   }
-  // input row block [32][K_IN], coalesced 16-byte loads
+  // input row block [RB][K_IN], coalesced 16-byte loads
   constexpr int EPV = XF32 ? 4 : 8;                 // elements per 16-byte vector
-  constexpr int XV = 32 * K_IN / EPV;
+  constexpr int XV = RB * K_IN / EPV;
   constexpr int XPT = (XV + NT - 1) / NT;
   u32x4 xv[XPT];
 #pragma unroll
@@ -203,8 +203,8 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
   }
   __syncthreads();
   // IN^T side output: output block y < K_IN/XTC writes features [y*XTC, (y+1)*XTC) of this row block
-  if (a.INT && blockIdx.y < K_IN / XTC && tid < XTC * 4) {
-    const int i = tid >> 2, h = (tid & 3) * 8, xk = blockIdx.y * XTC + i;
+  if (a.INT && blockIdx.y < K_IN / XTC && tid < XTC * (RB / 8)) {
+    const int i = tid / (RB / 8), h = (tid % (RB / 8)) * 8, xk = blockIdx.y * XTC + i;
     unsigned q[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e)
@@ -214,14 +214,17 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
   }
 
   // ---- 3. K split over the 8 waves
-  f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  constexpr int MT = RB / 16;
+  f32x4 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {
     if (ks0 + t < ks1) {
       const int k = (ks0 + t) * 32 + 8 * (lane >> 4);
       const bf16x8 b = direct ? bg[t] : *reinterpret_cast<const bf16x8*>(&wt[(lane & 15) * LDW + k]);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
+      for (int mt = 0; mt < MT; ++mt) {
         bf16x8 af = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
         if (k < K_IN) af = *reinterpret_cast<const bf16x8*>(&xs[(mt * 16 + (lane & 15)) * LDXS + k]);
         acc[mt] = mfma16x16x32(af, b, acc[mt]);
@@ -229,13 +232,13 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
     }
   }
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int e = 0; e < 4; ++e) part[w][mt * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[mt][e];
   __syncthreads();
 
   // ---- 4. bias + silu + dropout per 4-row group
-  if (tid < 8 * 16) {
+  if (tid < (RB / 4) * 16) {
     const int g4 = tid >> 4, c = tid & 15, col = j0 + c;
     const int rowg = r0 + g4 * 4;
     u32x4 db = {0u, 0u, 0u, 0u};
@@ -262,7 +265,7 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
   if (HEAD) {
     __syncthreads();
     float* lg = a.logits + (long)par * M * C;
-    if (tid < 32 * C) {
+    if (tid < RB * C) {
       const int rl = tid / C, c = tid % C, row = r0 + rl;
       if (row < M) {
         float s = (blockIdx.y == 0) ? bf2f(a.bh[c]) : 0.f;
@@ -559,14 +562,15 @@ JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) 
   hipStream_t st = static_cast<hipStream_t>(stream);
   const dim3 blk(MD_NT);
   if (phase == 0) {
-    const dim3 grid((a.M + 31) / 32, a.N / 16);
+    // 16-row blocks: twice the workgroups, half the input bytes each (as mlp2_fwd)
+    const dim3 grid((a.M + 15) / 16, a.N / 16);
     if (a.K == 784) {
       if (head) return -3;
-      hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, false, 10>), grid, blk, 0, st, a);
+      hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, false, 10, 16>), grid, blk, 0, st, a);
     } else if (head) {
-      hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, true, 10>), grid, blk, 0, st, a);
+      hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, true, 10, 16>), grid, blk, 0, st, a);
     } else {
-      hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10>), grid, blk, 0, st, a);
+      hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10, 16>), grid, blk, 0, st, a);
     }
   } else {
     if (a.K == 784) {

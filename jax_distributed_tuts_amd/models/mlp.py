@@ -117,7 +117,7 @@ class MLP:
 
     # ------------------------------------------------------------------ backward
     def backward(self, P: FlatParams, cache: LayerCache, dout: torch.Tensor, *, dout_is_dz: bool = True,
-                 need_dx: bool = False, on_ready=None) -> Optional[torch.Tensor]:
+                 need_dx: bool = False, on_ready=None, wgrad=None) -> Optional[torch.Tensor]:
         """Accumulate param grads into ``P.grad``; return dx if ``need_dx``.
 
         ``dout`` is the gradient w.r.t. the stack output.  With ``dout_is_dz``
@@ -136,8 +136,9 @@ class MLP:
         for i in range(L - 1, -1, -1):
             n = self.names[i]
             h_prev = cache.x if i == 0 else cache.h[i - 1]
-            # dW_i += h_prev^T . dz   ([in, out], fp32 accumulate)
-            K.gemm(h_prev, dz, a_layout="km", b_layout="kn", out=P.g(f"{n}/kernel"), accumulate=True)
+            # dW_i += h_prev^T . dz   ([in, out], fp32 accumulate); off the critical
+            # path, so on the side stream when one is given (wgrad)
+            K.dw_gemm(wgrad if on_ready is None else None, h_prev, dz, P.g(f"{n}/kernel"))
             if on_ready is not None:  # layer i's kernel and bias grads are final (its bias came with dz)
                 on_ready([f"{n}/kernel", f"{n}/bias"])
             if i > 0:

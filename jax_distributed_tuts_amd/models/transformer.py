@@ -151,7 +151,11 @@ class TransformerLM:
 
     # ------------------------------------------------------------------ backward
     def backward(self, P: FlatParams, cache: _Cache, dout: torch.Tensor, *, dout_is_dz: bool = True,
-                 need_dx: bool = False, on_ready=None) -> Optional[torch.Tensor]:
+                 need_dx: bool = False, on_ready=None, wgrad=None) -> Optional[torch.Tensor]:
+        """``wgrad`` (ops.kernels.WGradStream): run the weight-gradient GEMMs on its
+        side stream; the caller joins it before reading the grads."""
+        if on_ready is not None:
+            wgrad = None  # bucket callbacks fire as soon as a layer's grads are queued
         c = self.cfg
         ready = on_ready if on_ready is not None else (lambda names: None)
         layers = list(self.layers)
@@ -159,7 +163,7 @@ class TransformerLM:
         if self.has_head:
             # dlogits (CE already added the head bias grad); the LN-bwd also reduces
             # the top block's fc2 bias grad (colsum of the residual gradient)
-            K.gemm(cache.hf, dout, a_layout="km", b_layout="kn", out=P.g("head/kernel"), accumulate=True)
+            K.dw_gemm(wgrad, cache.hf, dout, P.g("head/kernel"))
             dhf = K.gemm(dout, P.s("head/kernel"), b_layout="nk")
             dx = K.layernorm_bwd(dhf, cache.xf, cache.mf, cache.rf, P.p("ln_f/scale"), P.g("ln_f/scale"),
                                  P.g("ln_f/bias"), dsum=fc2_bias(layers[-1]) if layers else None)
@@ -174,20 +178,20 @@ class TransformerLM:
             # x3 = x2 + u.W2 + b2
             if not fc2_done:
                 K.colsum_(dx, P.g(f"{b}/mlp/fc2/bias"))
-            K.gemm(bc.u, dx, a_layout="km", b_layout="kn", out=P.g(f"{b}/mlp/fc2/kernel"), accumulate=True)
+            K.dw_gemm(wgrad, bc.u, dx, P.g(f"{b}/mlp/fc2/kernel"))
             dz1 = K.gemm(dx, P.s(f"{b}/mlp/fc2/kernel"), b_layout="nk", z_in=bc.z1, act_bwd="gelu",
                          keep_prob=cache.keep, seed=cache.seed, offset=bc.off, step=cache.step,
                          dbias=P.g(f"{b}/mlp/fc1/bias"))
-            K.gemm(bc.h2, dz1, a_layout="km", b_layout="kn", out=P.g(f"{b}/mlp/fc1/kernel"), accumulate=True)
+            K.dw_gemm(wgrad, bc.h2, dz1, P.g(f"{b}/mlp/fc1/kernel"))
             dh2 = K.gemm(dz1, P.s(f"{b}/mlp/fc1/kernel"), b_layout="nk")
             # x2 = x + o.Wo + bo: the LN2-bwd output dx2 is also Wo's bias grad
             dx2 = K.layernorm_bwd(dh2, bc.x2, bc.m2, bc.r2, P.p(f"{b}/ln2/scale"), P.g(f"{b}/ln2/scale"),
                                   P.g(f"{b}/ln2/bias"), dres=dx, dsum=P.g(f"{b}/attn/out/bias"))
-            K.gemm(bc.o, dx2, a_layout="km", b_layout="kn", out=P.g(f"{b}/attn/out/kernel"), accumulate=True)
+            K.dw_gemm(wgrad, bc.o, dx2, P.g(f"{b}/attn/out/kernel"))
             do = K.gemm(dx2, P.s(f"{b}/attn/out/kernel"), b_layout="nk")
             dqkv = K.attention_bwd(do, bc.qkv, bc.P, cache.nseq, c.seq_len, c.n_heads, o=bc.o)
             K.colsum_(dqkv, P.g(f"{b}/attn/qkv/bias"))
-            K.gemm(bc.h1, dqkv, a_layout="km", b_layout="kn", out=P.g(f"{b}/attn/qkv/kernel"), accumulate=True)
+            K.dw_gemm(wgrad, bc.h1, dqkv, P.g(f"{b}/attn/qkv/kernel"))
             dh1 = K.gemm(dqkv, P.s(f"{b}/attn/qkv/kernel"), b_layout="nk")
             below = fc2_bias(layers[idx - 1]) if idx > 0 else None  # next (lower) block's fc2 bias grad
             dx = K.layernorm_bwd(dh1, bc.x, bc.m1, bc.r1, P.p(f"{b}/ln1/scale"), P.g(f"{b}/ln1/scale"),

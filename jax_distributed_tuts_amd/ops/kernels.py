@@ -37,16 +37,60 @@ N_COUNTERS = 1 << 16
 
 
 def workspace(device):
-    """Per-device split-K workspace (fp32 slabs) + zeroed arrival counters.  The
-    counters are re-armed to 0 by each tile's last arriver, so one allocation
-    serves every GEMM on the stream (kernels on one stream never overlap)."""
-    key = (device.type, device.index)
+    """Per-(device, stream) split-K workspace (fp32 slabs) + zeroed arrival
+    counters.  The counters are re-armed to 0 by each tile's last arriver, so one
+    allocation serves every GEMM on its stream (kernels on one stream never
+    overlap; a side stream -- WGradStream -- gets its own)."""
+    key = (device.type, device.index, torch.cuda.current_stream(device).cuda_stream if device.type == "cuda" else 0)
     w = _WS.get(key)
     if w is None:
         w = (torch.empty(WS_FLOATS, dtype=torch.float32, device=device),
              torch.zeros(N_COUNTERS, dtype=torch.int32, device=device))
         _WS[key] = w
     return w
+
+
+class WGradStream:
+    """Weight-gradient GEMMs on a side HIP stream.
+
+    In an explicit backward the dW = h^T dz GEMMs are off the critical path (only
+    the dX chain feeds the next layer / the previous pipeline stage), so
+    ``run(fn, *tensors)`` forks them onto a second stream after the work queued
+    so far, and ``join()`` makes the caller's stream wait before the optimizer.
+    The many small GEMMs of a microbatch-sized step then overlap instead of
+    queueing behind each other; inside hipGraph capture the fork/join become
+    parallel graph branches.  ``tensors`` (the GEMM operands) are kept alive
+    until the join so the caching allocator cannot hand their memory to the
+    main stream while the side stream still reads it."""
+
+    def __init__(self, device):
+        self.s = torch.cuda.Stream(device)
+        self.keep: list = []
+        self.pending = False
+
+    def run(self, fn, *tensors):
+        ev = torch.cuda.Event()
+        ev.record()
+        self.s.wait_event(ev)
+        with torch.cuda.stream(self.s):
+            fn()
+        self.keep.extend(tensors)
+        self.pending = True
+
+    def join(self):
+        if self.pending:
+            torch.cuda.current_stream().wait_stream(self.s)
+            self.keep.clear()
+            self.pending = False
+
+
+def dw_gemm(wgrad: Optional["WGradStream"], h, dz, out, **kw):
+    """``out += h^T dz`` (a_layout "km", b_layout "kn", fp32 accumulate), on the
+    side stream when ``wgrad`` is given (GPU), inline otherwise."""
+    if wgrad is None or not h.is_cuda:
+        return gemm(h, dz, a_layout="km", b_layout="kn", out=out, accumulate=True, **kw)
+    wgrad.run(lambda: gemm(h, dz, a_layout="km", b_layout="kn", out=out, accumulate=True, **kw), h, dz)
+    return out
 
 
 # ----------------------------------------------------------------------------- philox (CPU mirror)

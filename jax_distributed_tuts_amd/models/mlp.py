@@ -136,21 +136,23 @@ class MLP:
         for i in range(L - 1, -1, -1):
             n = self.names[i]
             h_prev = cache.x if i == 0 else cache.h[i - 1]
-            # dW_i += h_prev^T . dz   ([in, out], fp32 accumulate); off the critical
-            # path, so on the side stream when one is given (wgrad)
-            K.dw_gemm(wgrad if on_ready is None else None, h_prev, dz, P.g(f"{n}/kernel"))
+            # dW_i += h_prev^T . dz ([in, out], fp32 accumulate) and the input gradient
+            # only need dz: one grouped launch on GPU (ops.kernels.gemm_group)
+            with K.gemm_group():
+                K.dw_gemm(wgrad if on_ready is None else None, h_prev, dz, P.g(f"{n}/kernel"))
+                if i > 0:
+                    pn = self.names[i - 1]
+                    dz_prev = torch.empty(dz.shape[0], self.dims[i], dtype=torch.bfloat16, device=dz.device)
+                    K.gemm(dz, P.s(f"{n}/kernel"), a_layout="mk", b_layout="nk", out=dz_prev,
+                           z_in=cache.z[i - 1], act_bwd=self.act, keep_prob=cache.keep, seed=cache.seed,
+                           offset=cache.offsets[i - 1], step=cache.step, dbias=P.g(f"{pn}/bias"))
+                elif need_dx:
+                    dx = torch.empty(dz.shape[0], self.dims[0], dtype=torch.bfloat16, device=dz.device)
+                    K.gemm(dz, P.s(f"{n}/kernel"), a_layout="mk", b_layout="nk", out=dx)
             if on_ready is not None:  # layer i's kernel and bias grads are final (its bias came with dz)
                 on_ready([f"{n}/kernel", f"{n}/bias"])
             if i > 0:
-                pn = self.names[i - 1]
-                dz_prev = torch.empty(dz.shape[0], self.dims[i], dtype=torch.bfloat16, device=dz.device)
-                K.gemm(dz, P.s(f"{n}/kernel"), a_layout="mk", b_layout="nk", out=dz_prev,
-                       z_in=cache.z[i - 1], act_bwd=self.act, keep_prob=cache.keep, seed=cache.seed,
-                       offset=cache.offsets[i - 1], step=cache.step, dbias=P.g(f"{pn}/bias"))
                 dz = dz_prev
-            elif need_dx:
-                dx = torch.empty(dz.shape[0], self.dims[0], dtype=torch.bfloat16, device=dz.device)
-                K.gemm(dz, P.s(f"{n}/kernel"), a_layout="mk", b_layout="nk", out=dx)
         return dx
 
 

@@ -641,6 +641,13 @@ __device__ __forceinline__ void dma_stage(const bf16_t* src, long ld, int k0, bf
   }
 }
 
+template <int EXT>
+__device__ __forceinline__ void dma_stage_rt(bool kmaj, const bf16_t* src, long ld, int k0, bf16_t* img, int wid,
+                                             int lane) {
+  if (kmaj) dma_stage<EXT, true>(src, ld, k0, img, wid, lane);
+  else dma_stage<EXT, false>(src, ld, k0, img, wid, lane);
+}
+
 template <int WM, int WN, int TM, int TN, bool AT, bool BT, int S>
 __global__ void __launch_bounds__(256) gemm_dma_kernel(GemmArgs g, int tiles_n, int splits, int kchunk,
                                                        float* __restrict__ ws, unsigned* counters) {
@@ -714,6 +721,82 @@ __global__ void __launch_bounds__(256) gemm_dma_kernel(GemmArgs g, int tiles_n, 
   __syncthreads();
   gemm_finish<BM, BN, TM, TN>(g, acc, tm0, tn0, z, wid, wm, wn, lane, tid, splits, split, (long)z * gridDim.x + bid,
                               ws, counters, reinterpret_cast<int*>(smem));
+}
+
+
+// ---------------------------------------------------------------------------
+// Grouped LDS-DMA GEMM: up to GROUP_MAX independent problems (e.g. a layer's
+// weight gradient h^T dz and its input gradient dz W^T, which both only need
+// dz) in ONE launch -- one grid whose workgroups pick their problem from a
+// prefix table, so the two GEMMs' tiles run side by side on the CUs instead of
+// the second queueing behind the first's tail, and one launch gap is saved.
+// 32x32 tiles, no K split; operand layouts are per-problem runtime flags.
+constexpr int GROUP_MAX = 4;
+struct GemmGroup {
+  GemmArgs g[GROUP_MAX];
+  int tiles_n[GROUP_MAX];
+  int start[GROUP_MAX + 1];
+  int n;
+};
+
+template <int S>
+__global__ void __launch_bounds__(256) gemm_dma_group_kernel(GemmGroup G) {
+  constexpr int WM = 2, WN = 2, TM = 1, TN = 1;
+  constexpr int BM = 32, BN = 32, BK = DMA_BK;
+  constexpr int STAGE = (BM + BN) * BK;
+  constexpr int LPW = BM / 32 + BN / 32;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[S * STAGE];
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  }
+  int p = 0;
+#pragma unroll
+  for (int t = 1; t < GROUP_MAX; ++t)
+    if (t < G.n && bid >= G.start[t]) p = t;
+  const GemmArgs& g = G.g[p];
+  const int local = bid - G.start[p], tn = G.tiles_n[p];
+  const int tm0 = (local / tn) * BM, tn0 = (local % tn) * BN;
+  const bool at = g.a_trans, bt = g.b_trans;
+  const bf16_t* Ab = static_cast<const bf16_t*>(g.A) + (at ? (long)tm0 : (long)tm0 * g.lda);
+  const bf16_t* Bb = static_cast<const bf16_t*>(g.B) + (bt ? (long)tn0 : (long)tn0 * g.ldb);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int nkt = g.K / BK;
+  f32x4 acc[TM][TN];
+  acc[0][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  auto issue = [&](int kt) {
+    bf16_t* st = smem + (kt % S) * STAGE;
+    dma_stage_rt<BM>(at, Ab, g.lda, kt * BK, st, wid, lane);
+    dma_stage_rt<BN>(bt, Bb, g.ldb, kt * BK, st + BM * BK, wid, lane);
+  };
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nkt) issue(s);
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt + S - 2 < nkt) {
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"((S - 2) * LPW) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    if (kt + S - 1 < nkt) issue(kt + S - 1);
+    const bf16_t* As = smem + (kt % S) * STAGE;
+    const bf16_t* Bs = As + BM * BK;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 af = at ? dma_frag<BM>(As, true, wm * 16, kk, lane) : dma_frag<BM>(As, false, wm * 16, kk, lane);
+      bf16x8 bf = bt ? dma_frag<BN>(Bs, true, wn * 16, kk, lane) : dma_frag<BN>(Bs, false, wn * 16, kk, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // asm tr reads retired (see gemm_dma_kernel)
+      asm volatile("" : "+v"(af));
+      asm volatile("" : "+v"(bf));
+      acc[0][0] = mfma16x16x32(af, bf, acc[0][0]);
+    }
+  }
+  __syncthreads();
+  gemm_finish<BM, BN, TM, TN>(g, acc, tm0, tn0, 0, wid, wm, wn, lane, tid, 1, 0, 0, nullptr, nullptr,
+                              reinterpret_cast<int*>(smem));
 }
 
 // Exact-slice depth: K-tiles a slice may hold in registers (~128 VGPRs of
@@ -881,6 +964,30 @@ static int gemm_dma(const GemmArgs& g, int batch, int cfg, int splits, float* ws
   }
 }
 
+
+// Grouped launch (see gemm_dma_group_kernel).  Returns 1 if any problem is
+// outside the envelope (bf16, 16-byte aligned rows, M, N % 32 == 0, K % 64 == 0,
+// no batch) -- the caller then launches the problems one by one.
+static int gemm_dma_group(const GemmArgs* gs, int n, hipStream_t st) {
+  if (g_gemm_no_dma || n < 1 || n > GROUP_MAX) return 1;
+  GemmGroup G{};
+  G.n = n;
+  int total = 0;
+  for (int p = 0; p < n; ++p) {
+    const GemmArgs& g = gs[p];
+    auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    if (g.a_f32 || g.b_f32 || g.K % DMA_BK || g.M % 32 || g.N % 32 || g.M <= 0 || g.N <= 0 || !al(g.A) ||
+        !al(g.B) || g.lda % 8 || g.ldb % 8 || g.zin > 1)
+      return 1;
+    G.g[p] = g;
+    G.tiles_n[p] = g.N / 32;
+    G.start[p] = total;
+    total += (g.M / 32) * (g.N / 32);
+  }
+  G.start[n] = total;
+  hipLaunchKernelGGL((gemm_dma_group_kernel<3>), dim3(total), dim3(256), 0, st, G);
+  return HIP_LAUNCH_CHECK();
+}
 }  // namespace jdt
 
 using namespace jdt;
@@ -922,3 +1029,8 @@ JDT_API int jdt_gemm(const GemmArgs* ga, int batch, int cfg, int splits, float* 
 }
 
 JDT_API int jdt_gemm_args_size() { return (int)sizeof(GemmArgs); }
+
+// n GEMMs (no batch) in one launch; 1 = not eligible (launch them one by one).
+JDT_API int jdt_gemm_group(const GemmArgs* gs, int n, void* stream) {
+  return gemm_dma_group(gs, n, static_cast<hipStream_t>(stream));
+}

@@ -12,6 +12,7 @@ optimizer state are fp32.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 from typing import Optional
 
@@ -236,12 +237,46 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, a_layout: str = "mk", b_layout: st
     if step is not None:
         assert step.dtype == torch.int32
         g.step_ptr = step.data_ptr()
-    ws, ctr = workspace(a.device)
-    rc = _lib.lib().jdt_gemm(ctypes.byref(g), int(a.shape[0]) if batched else 1, int(cfg), int(splits),
+    if _GROUP and not batched and cfg < 0 and splits < 0:
+        _GROUP[-1].append((g, a.device, (a, b, out, bias, z_out, z_in, resid, dbias, step)))
+        return out
+    _launch_gemm(g, int(a.shape[0]) if batched else 1, cfg, splits, a.device)
+    return out
+
+
+def _launch_gemm(g, batch: int, cfg: int, splits: int, device):
+    ws, ctr = workspace(device)
+    rc = _lib.lib().jdt_gemm(ctypes.byref(g), int(batch), int(cfg), int(splits),
                              ctypes.c_void_p(ws.data_ptr()), ws.numel(), ctypes.c_void_p(ctr.data_ptr()),
                              ctr.numel(), _lib.stream_ptr())
     _lib.check(rc, "jdt_gemm")
-    return out
+
+
+_GROUP: list = []
+
+
+@contextlib.contextmanager
+def gemm_group():
+    """GPU GEMMs issued inside the block (unbatched, default config) are launched
+    together at its end as ONE grouped kernel (csrc/gemm.hip
+    ``gemm_dma_group_kernel``) -- e.g. a layer's weight- and input-gradient
+    GEMMs, which both only need dz.  Outputs are allocated at call time but
+    written at the end of the block, so nothing inside may read them.  Shapes
+    outside the grouped kernel's envelope are launched one by one."""
+    _GROUP.append([])
+    try:
+        yield
+    finally:
+        items = _GROUP.pop()
+        if items:
+            if len(items) > 1:
+                arr = (_lib.GemmArgs * len(items))(*[it[0] for it in items])
+                rc = _lib.lib().jdt_gemm_group(arr, len(items), _lib.stream_ptr())
+                if rc != 1:
+                    _lib.check(rc, "jdt_gemm_group")
+                    items = []
+            for g, dev, _refs in items:
+                _launch_gemm(g, 1, -1, -1, dev)
 
 
 def _gemm_ref(a, b, a_layout, b_layout, out, accumulate, alpha, bias, act, z_out, z_in, act_bwd, keep_prob, seed,

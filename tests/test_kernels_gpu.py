@@ -506,3 +506,43 @@ def test_fsdp_graph_replay_matches_eager(fused):
     d = (res[1][0] - res[0][0]).abs()
     assert float(d.max()) <= 2 * 1e-3 * 8 and float((d > 5e-5).float().mean()) < 2e-3
     torch.testing.assert_close(res[1][1], res[0][1], rtol=1e-4, atol=1e-3)
+
+
+def test_gemm_group_matches_individual():
+    """A layer's dW (km x kn, fp32 accumulate) and dX (mk x nk with act' * mask +
+    dbias epilogue) in one grouped launch == the same GEMMs launched one by one;
+    a non-eligible member (K % 64 != 0) falls back to individual launches."""
+    M, D_in, D_out = 256, 512, 384
+    h = _mk((M, D_in), torch.bfloat16, seed=71).to(DEV)
+    dz = _mk((M, D_out), torch.bfloat16, seed=72).to(DEV)
+    w = (_mk((D_in, D_out), torch.float32, seed=73) * 0.05).to(torch.bfloat16).to(DEV)
+    z = _mk((M, D_in), torch.bfloat16, seed=74).to(DEV)
+    outs = []
+    for grouped in (False, True):
+        gW = torch.full((D_in, D_out), 0.25, device=DEV)
+        db = torch.zeros(D_in, device=DEV)
+        dx = torch.empty(M, D_in, dtype=torch.bfloat16, device=DEV)
+
+        def body():
+            kern.gemm(h, dz, a_layout="km", b_layout="kn", out=gW, accumulate=True)
+            kern.gemm(dz, w, b_layout="nk", out=dx, z_in=z, act_bwd="silu", keep_prob=0.9, seed=5, offset=9,
+                      dbias=db)
+        if grouped:
+            with kern.gemm_group():
+                body()
+        else:
+            body()
+        torch.cuda.synchronize()
+        outs.append((gW.clone(), dx.clone(), db.clone()))
+    torch.testing.assert_close(outs[1][0], outs[0][0], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(outs[1][1], outs[0][1], rtol=0, atol=0)
+    torch.testing.assert_close(outs[1][2], outs[0][2], rtol=1e-4, atol=1e-3)
+    # ineligible shape inside a group: launched individually, same result as plain
+    a, b = _mk((48, 32), torch.bfloat16, seed=75), _mk((32, 40), torch.bfloat16, seed=76)
+    ref = kern.gemm(a, b, out_dtype=torch.float32)
+    with kern.gemm_group():
+        o1 = kern.gemm(a.to(DEV), b.to(DEV), out_dtype=torch.float32)
+        o2 = kern.gemm(h, dz, a_layout="km", b_layout="kn", out_dtype=torch.float32)
+    _close(o1, ref, rtol=1e-3, atol=1e-3)
+    _close(o2, kern.gemm(h.cpu(), dz.cpu(), a_layout="km", b_layout="kn", out_dtype=torch.float32),
+           rtol=1e-3, atol=1e-3)

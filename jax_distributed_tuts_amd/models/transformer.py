@@ -193,8 +193,8 @@ class TransformerLM:
             with K.gemm_group():
                 K.dw_gemm(wgrad, bc.o, dx2, P.g(f"{b}/attn/out/kernel"))
                 do = K.gemm(dx2, P.s(f"{b}/attn/out/kernel"), b_layout="nk")
-            dqkv = K.attention_bwd(do, bc.qkv, bc.P, cache.nseq, c.seq_len, c.n_heads, o=bc.o)
-            K.colsum_(dqkv, P.g(f"{b}/attn/qkv/bias"))
+            dqkv = K.attention_bwd(do, bc.qkv, bc.P, cache.nseq, c.seq_len, c.n_heads, o=bc.o,
+                                   dbias=P.g(f"{b}/attn/qkv/bias"))
             with K.gemm_group():
                 K.dw_gemm(wgrad, bc.h1, dqkv, P.g(f"{b}/attn/qkv/kernel"))
                 dh1 = K.gemm(dqkv, P.s(f"{b}/attn/qkv/kernel"), b_layout="nk")

@@ -66,8 +66,8 @@ _SIGS = {
     "jdt_embed_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "jdt_colsum": (c_int, [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p]),
     "jdt_flash_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int, c_void_p]),
-    "jdt_flash_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
-                              c_int, c_float, c_int, c_void_p]),
+    "jdt_flash_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                              c_int, c_int, c_float, c_int, c_void_p]),
 }
 
 

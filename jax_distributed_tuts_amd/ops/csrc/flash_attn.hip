@@ -149,8 +149,8 @@ __global__ void __launch_bounds__(256) flash_fwd_kernel(const bf16_t* __restrict
 __global__ void __launch_bounds__(256) flash_bwd_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
                                                         const bf16_t* __restrict__ dout, const float* __restrict__ lse,
                                                         bf16_t* __restrict__ dqkv, float* __restrict__ dq_acc,
-                                                        unsigned* __restrict__ tickets, int S, int H, float scale,
-                                                        int causal) {
+                                                        unsigned* __restrict__ tickets, float* __restrict__ dbias,
+                                                        int S, int H, float scale, int causal) {
   __shared__ __attribute__((aligned(16))) bf16_t Qs[FB * FLD];
   __shared__ __attribute__((aligned(16))) bf16_t Qt[FD * FLD];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[FB * FLD];
@@ -270,7 +270,10 @@ __global__ void __launch_bounds__(256) flash_bwd_kernel(const bf16_t* __restrict
         atomicAdd(dq_acc + ((long)b * S + q) * d + h * FD + nt * 16 + (lane & 15), dq[nt][e] * scale);
     }
   }
-  // dK, dV -> the K and V column blocks of dQKV
+  // dK, dV -> the K and V column blocks of dQKV; with dbias, their column sums
+  // (the k/v bias gradient, over exactly the stored bf16 values) go out with one
+  // atomic per column per wave
+  float sk[4] = {0.f, 0.f, 0.f, 0.f}, sv[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int key = kw + (lane >> 4) * 4 + e;
@@ -278,8 +281,27 @@ __global__ void __launch_bounds__(256) flash_bwd_kernel(const bf16_t* __restrict
     bf16_t* row = dqkv + ((long)b * S + key) * ld3 + h * FD + (lane & 15);
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      row[d + nt * 16] = f2bf(dk[nt][e] * scale);
-      row[2 * d + nt * 16] = f2bf(dv[nt][e]);
+      const bf16_t kb = f2bf(dk[nt][e] * scale), vb = f2bf(dv[nt][e]);
+      row[d + nt * 16] = kb;
+      row[2 * d + nt * 16] = vb;
+      sk[nt] += bf2f(kb);
+      sv[nt] += bf2f(vb);
+    }
+  }
+  if (dbias) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      sk[nt] += __shfl_xor(sk[nt], 16, 64);
+      sk[nt] += __shfl_xor(sk[nt], 32, 64);
+      sv[nt] += __shfl_xor(sv[nt], 16, 64);
+      sv[nt] += __shfl_xor(sv[nt], 32, 64);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        atomicAdd(dbias + d + h * FD + nt * 16 + lane, sk[nt]);
+        atomicAdd(dbias + 2 * d + h * FD + nt * 16 + lane, sv[nt]);
+      }
     }
   }
   // last key block of this (batch, head): dQ fp32 -> bf16, workspace re-zeroed.
@@ -298,7 +320,8 @@ __global__ void __launch_bounds__(256) flash_bwd_kernel(const bf16_t* __restrict
   __syncthreads();
   if (!last_s) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  constexpr int QV = FD / 4;  // float4 per row
+  constexpr int QV = FD / 4;  // float4 per row; thread t always owns columns 4 (t % QV) .. +3
+  float sq[4] = {0.f, 0.f, 0.f, 0.f};
   for (int i0 = 0; i0 < S * QV; i0 += 256 * 8) {
     float4 v[8];
 #pragma unroll
@@ -313,10 +336,23 @@ __global__ void __launch_bounds__(256) flash_bwd_kernel(const bf16_t* __restrict
       if (i >= S * QV) continue;
       const int q = i / QV, c = (i % QV) * 4;
       *reinterpret_cast<float4*>(dq_acc + ((long)b * S + q) * d + h * FD + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+      const bf16_t h0 = f2bf(v[u].x), h1 = f2bf(v[u].y), h2 = f2bf(v[u].z), h3 = f2bf(v[u].w);
       uint2 pk;
-      pk.x = (unsigned)f2bf(v[u].x) | ((unsigned)f2bf(v[u].y) << 16);
-      pk.y = (unsigned)f2bf(v[u].z) | ((unsigned)f2bf(v[u].w) << 16);
+      pk.x = (unsigned)h0 | ((unsigned)h1 << 16);
+      pk.y = (unsigned)h2 | ((unsigned)h3 << 16);
       *reinterpret_cast<uint2*>(dqkv + ((long)b * S + q) * ld3 + h * FD + c) = pk;
+      sq[0] += bf2f(h0); sq[1] += bf2f(h1); sq[2] += bf2f(h2); sq[3] += bf2f(h3);
+    }
+  }
+  if (dbias) {  // q bias gradient: lanes t, t+16, t+32, t+48 of a wave share columns
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sq[j] += __shfl_xor(sq[j], 16, 64);
+      sq[j] += __shfl_xor(sq[j], 32, 64);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) atomicAdd(dbias + h * FD + lane * 4 + j, sq[j]);
     }
   }
 }
@@ -334,11 +370,13 @@ JDT_API int jdt_flash_fwd(const void* qkv, void* out, float* lse, int B, int S, 
 
 // dq_acc: fp32 [B*S, H*64] workspace, all zero on entry and left zero on exit;
 // tickets: B*H counters, zero on entry and on exit.
+// dbias (optional, fp32 [3*H*64]): += column sums of dQKV (the QKV bias gradient).
 JDT_API int jdt_flash_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* dq_acc,
-                          unsigned* tickets, void* dqkv, int B, int S, int H, float scale, int causal, void* stream) {
+                          unsigned* tickets, void* dqkv, float* dbias, int B, int S, int H, float scale, int causal,
+                          void* stream) {
   hipLaunchKernelGGL(flash_bwd_kernel, dim3((S + FB - 1) / FB, B * H), dim3(256), 0, static_cast<hipStream_t>(stream),
                      static_cast<const bf16_t*>(qkv), static_cast<const bf16_t*>(out),
-                     static_cast<const bf16_t*>(dout), lse, static_cast<bf16_t*>(dqkv), dq_acc, tickets, S, H, scale,
+                     static_cast<const bf16_t*>(dout), lse, static_cast<bf16_t*>(dqkv), dq_acc, tickets, dbias, S, H, scale,
                      causal);
   return HIP_LAUNCH_CHECK();
 }

@@ -531,9 +531,11 @@ def _flash_workspace(device, n: int, bh: int):
 
 def attention_bwd(do: torch.Tensor, qkv: torch.Tensor, P: torch.Tensor, B: int, S: int, H: int,
                   dqkv: Optional[torch.Tensor] = None, o: Optional[torch.Tensor] = None,
-                  causal: bool = True) -> torch.Tensor:
+                  causal: bool = True, dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Gradient of attention_fwd w.r.t. qkv ([B*S, 3d] bf16).  ``P`` is attention_fwd's
-    aux: the LSE (flash path; then ``o`` is required) or the probabilities."""
+    aux: the LSE (flash path; then ``o`` is required) or the probabilities.
+    ``dbias`` (fp32 [3d]) += colsum(dqkv): the QKV projection's bias gradient,
+    fused into the flash kernel (a colsum pass on the other paths)."""
     T, d3 = qkv.shape
     d = d3 // 3
     Dh = d // H
@@ -544,7 +546,7 @@ def attention_bwd(do: torch.Tensor, qkv: torch.Tensor, P: torch.Tensor, B: int, 
         assert o is not None and do.is_contiguous() and o.is_contiguous() and dqkv.is_contiguous()
         dq_acc, tickets = _flash_workspace(qkv.device, T * d, B * H)
         rc = _lib.lib().jdt_flash_bwd(_ptr(qkv), _ptr(o), _ptr(do), _ptr(P), _ptr(dq_acc), _ptr(tickets), _ptr(dqkv),
-                                      B, S, H, float(scale), int(causal), _lib.stream_ptr())
+                                      _ptr(dbias), B, S, H, float(scale), int(causal), _lib.stream_ptr())
         _lib.check(rc, "jdt_flash_bwd")
         return dqkv
     if not _is_gpu(qkv):
@@ -558,6 +560,8 @@ def attention_bwd(do: torch.Tensor, qkv: torch.Tensor, P: torch.Tensor, B: int, 
         dk = torch.matmul(ds.transpose(-1, -2), q) * scale
         out = torch.stack([dq, dk, dv], 0).permute(1, 3, 0, 2, 4).reshape(T, d3)
         dqkv.copy_(out.to(dqkv.dtype))
+        if dbias is not None:
+            dbias.add_(dqkv.float().sum(0))
         return dqkv
     dev = qkv.device
     base, gb, dob, e2 = qkv.data_ptr(), dqkv.data_ptr(), do.data_ptr(), 2
@@ -577,6 +581,8 @@ def attention_bwd(do: torch.Tensor, qkv: torch.Tensor, P: torch.Tensor, B: int, 
               C=gb, ldc=d3, sC=S * d3, sC2=Dh, M=S, N=Dh, K=S, alpha=scale, batch=B * H, zin=H)
     _gemm_raw(A=dS.data_ptr(), lda=S, sA=H * S * S, sA2=S * S, a_trans=True, B=base, ldb=d3, sB=S * d3, sB2=Dh,
               b_kn=True, C=gb + d * e2, ldc=d3, sC=S * d3, sC2=Dh, M=S, N=Dh, K=S, alpha=scale, batch=B * H, zin=H)
+    if dbias is not None:
+        colsum_(dqkv, dbias)
     return dqkv
 
 

@@ -471,8 +471,10 @@ def test_flash_attention_fwd_bwd(B, S, H, causal):
         s2 = s2.masked_fill(torch.triu(torch.ones(S, S, dtype=torch.bool), 1), float("-inf"))
     o2 = torch.matmul(torch.softmax(s2, -1), v2).permute(0, 2, 1, 3).reshape(B * S, d)
     (o2 * do.float()).sum().backward()
-    g = kern.attention_bwd(do.to(DEV), qkv.to(DEV), lse, B, S, H, o=o_g, causal=causal)
+    db = torch.full((3 * d,), 0.5, device=DEV)
+    g = kern.attention_bwd(do.to(DEV), qkv.to(DEV), lse, B, S, H, o=o_g, causal=causal, dbias=db)
     _close(g, qkv_r.grad, rtol=3e-2, atol=3e-2)
+    _close(db, g.float().sum(0) + 0.5, rtol=1e-4, atol=1e-3)  # fused QKV bias gradient
     # composed (GEMM + softmax kernels) path agrees with the fused one
     o_c, P = kern.attention_fwd(qkv.to(DEV), B, S, H, causal=causal, impl="composed")
     _close(o_c, o_g, rtol=2e-2, atol=2e-2)

@@ -648,6 +648,35 @@ __device__ __forceinline__ void dma_stage_rt(bool kmaj, const bf16_t* src, long 
   else dma_stage<EXT, false>(src, ld, k0, img, wid, lane);
 }
 
+// The same for a K-tile that only has `kv` (= 32) valid k: lanes whose 16-byte
+// piece lies past it issue nothing (EXEC-masked), so no load leaves the operand;
+// the stale LDS they leave is never read (the MFMA loop stops at kv).
+template <int EXT>
+__device__ __forceinline__ void dma_stage_tail(bool kmaj, const bf16_t* src, long ld, int k0, int kv, bf16_t* img,
+                                               int wid, int lane) {
+  constexpr int IPW = EXT / 32;
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int ins = wid * IPW + i;
+    const int p = ins * 64 + lane;
+    const bf16_t* gp;
+    bool ok;
+    if (!kmaj) {
+      const int r = p >> 3, c = (p & 7) ^ (r & 7);
+      gp = src + (long)r * ld + k0 + c * 8;
+      ok = c * 8 < kv;
+    } else {
+      constexpr int CPR = EXT / 8;
+      const int kr = p / CPR, cm = p % CPR;
+      gp = src + (long)(k0 + kr) * ld + cm * 8;
+      ok = kr < kv;
+    }
+    if (ok)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gp,
+                                       (__attribute__((address_space(3))) void*)(img + ins * 512), 16, 0, 0);
+  }
+}
+
 template <int WM, int WN, int TM, int TN, bool AT, bool BT, int S>
 __global__ void __launch_bounds__(256) gemm_dma_kernel(GemmArgs g, int tiles_n, int splits, int kchunk,
                                                        float* __restrict__ ws, unsigned* counters) {
@@ -730,7 +759,8 @@ __global__ void __launch_bounds__(256) gemm_dma_kernel(GemmArgs g, int tiles_n, 
 // dz) in ONE launch -- one grid whose workgroups pick their problem from a
 // prefix table, so the two GEMMs' tiles run side by side on the CUs instead of
 // the second queueing behind the first's tail, and one launch gap is saved.
-// 32x32 tiles, no K split; operand layouts are per-problem runtime flags.
+// 32x32 tiles, no K split, K % 32 == 0 (a 32-deep tail tile is loaded with
+// EXEC-masked DMA); operand layouts are per-problem runtime flags.
 constexpr int GROUP_MAX = 4;
 struct GemmGroup {
   GemmArgs g[GROUP_MAX];
@@ -739,7 +769,7 @@ struct GemmGroup {
   int n;
 };
 
-template <int S>
+template <int S, bool TAIL>
 __global__ void __launch_bounds__(256) gemm_dma_group_kernel(GemmGroup G) {
   constexpr int WM = 2, WN = 2, TM = 1, TN = 1;
   constexpr int BM = 32, BN = 32, BK = DMA_BK;
@@ -764,13 +794,19 @@ __global__ void __launch_bounds__(256) gemm_dma_group_kernel(GemmGroup G) {
   const bf16_t* Bb = static_cast<const bf16_t*>(g.B) + (bt ? (long)tn0 : (long)tn0 * g.ldb);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int nkt = g.K / BK;
+  const int nkt = (g.K + BK - 1) / BK;  // K % 32 == 0: the last tile may hold 32 valid k
   f32x4 acc[TM][TN];
   acc[0][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
   auto issue = [&](int kt) {
     bf16_t* st = smem + (kt % S) * STAGE;
-    dma_stage_rt<BM>(at, Ab, g.lda, kt * BK, st, wid, lane);
-    dma_stage_rt<BN>(bt, Bb, g.ldb, kt * BK, st + BM * BK, wid, lane);
+    const int kv = g.K - kt * BK;
+    if (!TAIL || kv >= BK) {
+      dma_stage_rt<BM>(at, Ab, g.lda, kt * BK, st, wid, lane);
+      dma_stage_rt<BN>(bt, Bb, g.ldb, kt * BK, st + BM * BK, wid, lane);
+    } else {
+      dma_stage_tail<BM>(at, Ab, g.lda, kt * BK, kv, st, wid, lane);
+      dma_stage_tail<BN>(bt, Bb, g.ldb, kt * BK, kv, st + BM * BK, wid, lane);
+    }
   };
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
@@ -786,6 +822,7 @@ __global__ void __launch_bounds__(256) gemm_dma_group_kernel(GemmGroup G) {
     const bf16_t* Bs = As + BM * BK;
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
+      if (TAIL && kt * BK + kk >= g.K) break;  // half tile (uniform)
       bf16x8 af = at ? dma_frag<BM>(As, true, wm * 16, kk, lane) : dma_frag<BM>(As, false, wm * 16, kk, lane);
       bf16x8 bf = bt ? dma_frag<BN>(Bs, true, wn * 16, kk, lane) : dma_frag<BN>(Bs, false, wn * 16, kk, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // asm tr reads retired (see gemm_dma_kernel)
@@ -966,8 +1003,8 @@ static int gemm_dma(const GemmArgs& g, int batch, int cfg, int splits, float* ws
 
 
 // Grouped launch (see gemm_dma_group_kernel).  Returns 1 if any problem is
-// outside the envelope (bf16, 16-byte aligned rows, M, N % 32 == 0, K % 64 == 0,
-// no batch) -- the caller then launches the problems one by one.
+// outside the envelope (bf16, 16-byte aligned rows, M, N, K % 32 == 0, no
+// batch) -- the caller then launches the problems one by one.
 static int gemm_dma_group(const GemmArgs* gs, int n, hipStream_t st) {
   if (g_gemm_no_dma || n < 1 || n > GROUP_MAX) return 1;
   GemmGroup G{};
@@ -976,7 +1013,7 @@ static int gemm_dma_group(const GemmArgs* gs, int n, hipStream_t st) {
   for (int p = 0; p < n; ++p) {
     const GemmArgs& g = gs[p];
     auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    if (g.a_f32 || g.b_f32 || g.K % DMA_BK || g.M % 32 || g.N % 32 || g.M <= 0 || g.N <= 0 || !al(g.A) ||
+    if (g.a_f32 || g.b_f32 || g.K % 32 || g.K <= 0 || g.M % 32 || g.N % 32 || g.M <= 0 || g.N <= 0 || !al(g.A) ||
         !al(g.B) || g.lda % 8 || g.ldb % 8 || g.zin > 1)
       return 1;
     G.g[p] = g;
@@ -985,7 +1022,12 @@ static int gemm_dma_group(const GemmArgs* gs, int n, hipStream_t st) {
     total += (g.M / 32) * (g.N / 32);
   }
   G.start[n] = total;
-  hipLaunchKernelGGL((gemm_dma_group_kernel<3>), dim3(total), dim3(256), 0, st, G);
+  bool tail = false;
+  for (int p = 0; p < n; ++p) tail |= (gs[p].K % DMA_BK) != 0;
+  if (tail)  // only then pay for the tail checks in the K loop (measured ~5 % on the transformer's groups)
+    hipLaunchKernelGGL((gemm_dma_group_kernel<3, true>), dim3(total), dim3(256), 0, st, G);
+  else
+    hipLaunchKernelGGL((gemm_dma_group_kernel<3, false>), dim3(total), dim3(256), 0, st, G);
   return HIP_LAUNCH_CHECK();
 }
 }  // namespace jdt

@@ -510,11 +510,13 @@ def test_fsdp_graph_replay_matches_eager(fused):
     torch.testing.assert_close(res[1][1], res[0][1], rtol=1e-4, atol=1e-3)
 
 
-def test_gemm_group_matches_individual():
-    """A layer's dW (km x kn, fp32 accumulate) and dX (mk x nk with act' * mask +
-    dbias epilogue) in one grouped launch == the same GEMMs launched one by one;
-    a non-eligible member (K % 64 != 0) falls back to individual launches."""
-    M, D_in, D_out = 256, 512, 384
+@pytest.mark.parametrize("M", [256, 32, 96])
+def test_gemm_group_matches_individual(M):
+    """A layer's dW (km x kn, fp32 accumulate; K = M rows, a 32-deep tail tile when
+    M % 64 == 32) and dX (mk x nk with act' * mask + dbias epilogue) in one
+    grouped launch == the same GEMMs launched one by one; a non-eligible member
+    falls back to individual launches."""
+    D_in, D_out = 512, 384
     h = _mk((M, D_in), torch.bfloat16, seed=71).to(DEV)
     dz = _mk((M, D_out), torch.bfloat16, seed=72).to(DEV)
     w = (_mk((D_in, D_out), torch.float32, seed=73) * 0.05).to(torch.bfloat16).to(DEV)
@@ -537,10 +539,12 @@ def test_gemm_group_matches_individual():
         torch.cuda.synchronize()
         outs.append((gW.clone(), dx.clone(), db.clone()))
     torch.testing.assert_close(outs[1][0], outs[0][0], rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(outs[1][1], outs[0][1], rtol=0, atol=0)
+    # dX: same MFMA order when both launches use the DMA path; the register path
+    # (ungrouped, small M) may round differently in the last bf16 bit
+    torch.testing.assert_close(outs[1][1].float(), outs[0][1].float(), rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(outs[1][2], outs[0][2], rtol=1e-4, atol=1e-3)
     # ineligible shape inside a group: launched individually, same result as plain
-    a, b = _mk((48, 32), torch.bfloat16, seed=75), _mk((32, 40), torch.bfloat16, seed=76)
+    a, b = _mk((48, 24), torch.bfloat16, seed=75), _mk((24, 40), torch.bfloat16, seed=76)
     ref = kern.gemm(a, b, out_dtype=torch.float32)
     with kern.gemm_group():
         o1 = kern.gemm(a.to(DEV), b.to(DEV), out_dtype=torch.float32)

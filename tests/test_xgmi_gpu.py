@@ -179,3 +179,13 @@ def test_transformer_hybrid_over_xgmi_matches_single_device(tmp_path):
     m, rm = res[0]["metrics"], tr.metrics.cpu()
     assert float(m[1]) == float(rm[1])
     assert abs(float(m[0]) - float(rm[0])) <= 2e-3 * abs(float(rm[0])) + 1e-2
+
+
+def test_fault_injection_times_out_instead_of_hanging(tmp_path):
+    """A peer that never joins: the xGMI all-reduce barriers and the inbox receive
+    time out (s_memrealtime deadline) and raise the error flag -- the process
+    group survives and the GPU is not left hung."""
+    spawn(XW.fault_timeout, 2, str(tmp_path), gpu=True)
+    r0 = _load(tmp_path, "fault", 2)[0]
+    assert r0["ok"]
+    assert r0["ar_err"] == 1 and r0["p2p_err"] == 1

@@ -269,3 +269,31 @@ def lm_pp_xgmi(outdir, dp, steps=3):
     tr.finalize()
     _save(outdir, f"lmx{dp}", {"params": {k: v.cpu() for k, v in tr.state.params.state_dict().items()},
                                "metrics": tr.gather_metrics().cpu(), "comm": tr.comm_backend})
+
+
+def fault_timeout(outdir):
+    """Fault injection: rank 1 never joins the collective / never sends.  Rank 0's
+    in-kernel waits must time out into the error flag (no hung GPU), for both
+    the xGMI all-reduce and the pipeline inbox receive."""
+    from jax_distributed_tuts_amd.comm.p2p import XgmiP2P
+    from jax_distributed_tuts_amd.comm.xgmi import XgmiComm
+    from jax_distributed_tuts_amd.runtime import dist as D
+
+    r, W, dev = D.rank(), D.world_size(), D.device()
+    mesh = D.Mesh({"data": W})
+    comm = XgmiComm(mesh.group("data"), r, W, 1 << 16, dev, timeout_s=1.0)
+    p2p = XgmiP2P(mesh.group("data"), r, W, 4096, 2, dev, timeout_s=1.0)
+    res = {"ok": comm.ok and p2p.ok}
+    D.barrier()
+    if r == 0:
+        x = torch.ones(1000, device=dev)
+        comm.all_reduce_(x)                      # peer absent: both barriers time out
+        res["ar_err"] = comm.error()
+        out = torch.empty(256, device=dev)
+        ep = torch.zeros(1, dtype=torch.int32, device=dev)
+        p2p.recv(out, 0, ep)                     # nobody sends
+        res["p2p_err"] = p2p.error()
+    D.barrier()
+    _save(outdir, "fault", res)
+    comm.close()
+    p2p.close()

@@ -592,6 +592,19 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
 // ever transposed in memory).
 constexpr int DMA_BK = 64;
 
+// k-row image swizzle: 16-byte chunk c of k-row r is stored at chunk c ^ tr_swz(r).
+// A transposed fragment read has each 32-lane half touch k-rows {0..3, 8..11}
+// (+ kk) over the same 16 columns; the XOR puts those 8 rows' 32-byte pieces in
+// 8 distinct bank groups (PMC: SQ_LDS_BANK_CONFLICT of the both-transposed
+// weight-gradient GEMM 524k -> see profiles).  Rows r and r + 4 share a mask, so
+// the second read of a fragment is still the first one's address + 4 rows.
+template <int EXT>
+__device__ __forceinline__ int tr_swz(int r) {
+  if constexpr (EXT == 32) return ((r >> 3) & 1) << 1;
+  else if constexpr (EXT == 64) return (((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1;
+  else return ((r & 3) | (((r >> 3) & 1) << 2)) << 1;  // 128
+}
+
 template <int EXT>  // EXT = extent of the non-K dim of the tile (BM or BN)
 __device__ __forceinline__ bf16x8 dma_frag(const bf16_t* img, bool kmajor_img, int base, int kk, int lane) {
   if (!kmajor_img) {
@@ -608,7 +621,8 @@ __device__ __forceinline__ bf16x8 dma_frag(const bf16_t* img, bool kmajor_img, i
   typedef __attribute__((ext_vector_type(4))) short s4;
   const int i16 = lane & 15, k1 = kk + 8 * (lane >> 4) + (i16 >> 2);
   const int col = base + 4 * (i16 & 3);
-  const unsigned a0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) const bf16_t*)(img + k1 * EXT + col));
+  const int pcol = (((col >> 3) ^ tr_swz<EXT>(k1)) << 3) | (col & 7);
+  const unsigned a0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) const bf16_t*)(img + k1 * EXT + pcol));
   s4 lo, hi;
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0));
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a0), "n"(4 * EXT * 2));
@@ -633,7 +647,7 @@ __device__ __forceinline__ void dma_stage(const bf16_t* src, long ld, int k0, bf
       gp = src + (long)r * ld + k0 + c * 8;
     } else {
       constexpr int CPR = EXT / 8;  // chunks per k-row
-      const int kr = p / CPR, cm = p % CPR;
+      const int kr = p / CPR, cm = (p % CPR) ^ tr_swz<EXT>(kr);
       gp = src + (long)(k0 + kr) * ld + cm * 8;
     }
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gp,
@@ -667,7 +681,7 @@ __device__ __forceinline__ void dma_stage_tail(bool kmaj, const bf16_t* src, lon
       ok = c * 8 < kv;
     } else {
       constexpr int CPR = EXT / 8;
-      const int kr = p / CPR, cm = p % CPR;
+      const int kr = p / CPR, cm = (p % CPR) ^ tr_swz<EXT>(kr);
       gp = src + (long)(k0 + kr) * ld + cm * 8;
       ok = kr < kv;
     }

@@ -65,13 +65,17 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--exact", type=int, default=0, help="force the exact-slice depth (0 = heuristic)")
     ap.add_argument("--splits", type=int, default=-1)
+    ap.add_argument("--only", default=None, help="comma-separated shape names to run (e.g. 'qkv fwd,fc1 dW')")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     from jax_distributed_tuts_amd.ops import _lib
     _lib.lib().jdt_gemm_set_exact(args.exact)
     out = []
     print(f"{'shape':14s} {'M':>5s} {'N':>5s} {'K':>5s} {'ours us':>9s} {'TF/s':>7s} {'torch us':>9s} {'TF/s':>7s}")
+    only = set(x.strip() for x in args.only.split(",")) if args.only else None
     for name, M, N, Kd, al, bl, f32 in SHAPES:
+        if only and name not in only:
+            continue
         a = torch.randn(*((M, Kd) if al == "mk" else (Kd, M)), device=dev).to(torch.bfloat16)
         b = torch.randn(*((Kd, N) if bl == "kn" else (N, Kd)), device=dev).to(torch.bfloat16)
         c = torch.zeros(M, N, device=dev, dtype=torch.float32 if f32 else torch.bfloat16)

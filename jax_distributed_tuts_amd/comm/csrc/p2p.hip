@@ -8,7 +8,8 @@
 // uncached device memory plus a signal page.  A send is a kernel on the
 // producer that pushes the tensor straight into the consumer's inbox slot over
 // the xGMI link (posted remote stores, no round trip) and then raises one epoch
-// flag per block with a system-scope release; a receive is a kernel on the
+// flag per block (relaxed system-scope store after the data stores are
+// acknowledged -- the inbox is uncached, so no cache maintenance); a receive is a kernel on the
 // consumer that waits for the flags of its own blocks and copies the slot into
 // a local tensor.  Both are ordinary kernels on the caller's stream, so a whole
 // pipeline step -- compute, sends and receives -- is one hipGraph per rank.
@@ -79,11 +80,14 @@ __global__ void __launch_bounds__(P2P_THREADS) p2p_send_kernel(const uint4* __re
   long lo, hi;
   p2p_range(nw, &lo, &hi);
   for (long i = lo + threadIdx.x; i < hi; i += P2P_THREADS) dst[i] = src[i];
-  __threadfence_system();  // this thread's remote stores are performed before the flag
+  // the inbox is uncached: the data is ordered before the flag by waiting for the
+  // stores' acknowledgement, no L2 write-back (a release fence would flush the
+  // whole L2 per wave)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned epoch = (unsigned)epoch_src[0] + 1u;
-    __hip_atomic_store(&flag[blockIdx.x], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&flag[blockIdx.x], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -93,7 +97,7 @@ __global__ void __launch_bounds__(P2P_THREADS) p2p_recv_kernel(const uint4* src,
   if (threadIdx.x == 0) {
     const unsigned epoch = (unsigned)epoch_src[0] + 1u;
     const unsigned long long t0 = p2p_now();
-    while ((int)(__hip_atomic_load(&flag[blockIdx.x], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+    while ((int)(__hip_atomic_load(&flag[blockIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
       if ((long long)(p2p_now() - t0) > timeout) {
         __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
@@ -101,8 +105,7 @@ __global__ void __launch_bounds__(P2P_THREADS) p2p_recv_kernel(const uint4* src,
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  __syncthreads();  // the inbox is uncached: its loads below see the peer's stores
   long lo, hi;
   p2p_range(nw, &lo, &hi);
   for (long i = lo + threadIdx.x; i < hi; i += P2P_THREADS) dst[i] = src[i];

@@ -9,14 +9,15 @@
 // mlp2_fwd  grid (row blocks of 32) x (hidden blocks of 16), 8 waves
 //   Z1 = X W1 + b1 (fp32 X converted in-register, W1 column block staged
 //   transposed in LDS, K split over the 8 waves, partials reduced in LDS),
-//   H = dropout(silu(Z1)), and the block's partial logits H[:,blk] W2[blk,:]
+//   H = dropout(silu(Z1)) plus the backward factor G1 = silu'(Z1) * mask/keep,
+//   and the block's partial logits H[:,blk] W2[blk,:]
 //   (+ b2 from block 0) accumulated with fp32 atomics into logits[M][C].
 //   (All rows of all minibatches at once: every row carries its minibatch's
 //   1/mb loss weight, so the summed gradient equals util.accum_grads_loop's.)
 //
 // mlp2_bwd  grid (hidden blocks of 16) x (input chunks of KC), 8 waves
 //   every workgroup recomputes CE from the summed logits (M x C, tiny) ->
-//   dlogits; its dZ1 block = (dlogits W2[blk]^T) * silu'(Z1) * mask/keep;
+//   dlogits; its dZ1 block = (dlogits W2[blk]^T) * G1 (one MFMA per wave);
 //   dW1[chunk, blk] = X[:,chunk]^T dZ1[:,blk] on MFMA with both operands
 //   staged K(=row)-contiguous in LDS; chunk-0 blocks also emit db1, dW2[blk]
 //   and block (0,0) db2 + metrics.  Each gradient element is produced by
@@ -45,7 +46,10 @@ struct Mlp2Args {
   float inv_mb;                     // CE grad scale: 1 / rows per minibatch
   const float* X; const int* labels;
   const bf16_t* W1s; const bf16_t* b1s; const bf16_t* W2s0; const bf16_t* W2s1; const bf16_t* b2s;
-  bf16_t* Z1; bf16_t* H1; float* logits;   // logits: [2][M][C] (step parity)
+  // G1: the backward factor silu'(Z1) * mask / keep, fp32 [ceil(M/4)][H][4] (the
+  // dropout-group layout both kernels use), written by mlp2_fwd so mlp2_bwd needs
+  // neither Z1 nor the dropout bits
+  float* G1; bf16_t* H1; float* logits;   // logits: [2][M][C] (step parity)
   float keep; unsigned long long seed, offset;
   int* step; unsigned* ticket;
   // mode 0 outputs
@@ -96,7 +100,8 @@ __device__ __forceinline__ float adam_apply(float p, float m, float v, float g, 
   g *= k.gs;
   m = k.b1 * m + (1.f - k.b1) * g;
   v = k.b2 * v + (1.f - k.b2) * g * g;
-  p = p - k.lr * ((m * k.rbc1) / (sqrtf(v * k.rbc2) + k.eps) + k.wd * p);
+  // v_rcp_f32 (1 ulp) instead of the IEEE divide's scale/fma/fixup sequence
+  p = p - k.lr * ((m * k.rbc1) * __builtin_amdgcn_rcpf(sqrtf(v * k.rbc2) + k.eps) + k.wd * p);
   *pp = p; *mp = m; *vp = v;
   return p;
 }
@@ -108,7 +113,11 @@ __device__ __forceinline__ float adam_elem(float* p, float* m, float* v, long i,
 // RB rows per workgroup (16 or 32): 16-row blocks halve each workgroup's X
 // bytes and double the grid (256 workgroups at M = 128), which the load-latency
 // bound phase 1 prefers.
-template <int K_IN, int C, int RB>
+// DIRECT: the W1^T copy exists (mode 1), B fragments come straight from global;
+// otherwise the W1 column block is transposed through LDS.  (A compile-time
+// switch: with a runtime branch the two paths' loads share registers and the
+// waitcnt pass, which is path-insensitive, drains one path's loads at the join.)
+template <int K_IN, int C, int RB, bool DIRECT>
 __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   static_assert(RB == 16 || RB == 32, "row block");
   constexpr int KS = (K_IN + 31) / 32;  // 32-deep MFMA k-steps
@@ -129,30 +138,29 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   const int M = a.M, H = a.H;
   const int r0 = blockIdx.x * RB, j0 = blockIdx.y * 16;
   STAMP(0);
-  const int step = a.step[0], par = step & 1;
-  const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
-  const bf16_t* W2s = par ? a.W2s1 : a.W2s0;
   const int ks0 = (w * KS) / NW, ks1 = ((w + 1) * KS) / NW;
 
-  const bool direct = a.W1T != nullptr;  // W1^T copy available: B fragments straight from global
+  constexpr bool direct = DIRECT;
 
-  // ---- 1. issue all global loads
+  // ---- 1. issue all global loads.  Every load is unconditional (clamped address,
+  // value selected afterwards) and nothing waits on the step counter: a load under
+  // a divergent guard makes the compiler wait for it at the join (asm: this phase
+  // was ~8 serial round trips), and the parity-dependent W2 shadow is loaded from
+  // both buffers.  The step counter is loaded LAST: it is read back into a scalar
+  // register (readfirstlane), which waits for every load issued before it.
   u32x4 wv[WCH];
   bf16x8 bg[MAXT];
-  if (!direct) {
+  if constexpr (!DIRECT) {
 #pragma unroll
     for (int t = 0; t < WCH; ++t) {
-      const int idx = tid + t * NT;
-      wv[t] = (u32x4){0u, 0u, 0u, 0u};
-      if (idx < K_IN * 2) wv[t] = *reinterpret_cast<const u32x4*>(a.W1s + (long)(idx >> 1) * H + j0 + (idx & 1) * 8);
+      const int idx = min(tid + t * NT, K_IN * 2 - 1);
+      wv[t] = *reinterpret_cast<const u32x4*>(a.W1s + (long)(idx >> 1) * H + j0 + (idx & 1) * 8);
     }
   } else {
 #pragma unroll
     for (int t = 0; t < MAXT; ++t) {
-      bg[t] = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-      if (ks0 + t < ks1)
-        bg[t] = *reinterpret_cast<const bf16x8*>(a.W1T + (long)(j0 + (lane & 15)) * a.ldw1t + (ks0 + t) * 32 +
-                                                 8 * (lane >> 4));
+      const int ks = min(ks0 + t, ks1 - 1);
+      bg[t] = *reinterpret_cast<const bf16x8*>(a.W1T + (long)(j0 + (lane & 15)) * a.ldw1t + ks * 32 + 8 * (lane >> 4));
     }
   }
   // X row block [RB][K_IN] fp32: fully coalesced float4 loads (consecutive lanes,
@@ -163,16 +171,21 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   float4 xv[XPT];
 #pragma unroll
   for (int e = 0; e < XPT; ++e) {
-    const int f = tid + e * NT, rl = f / (K_IN / 4), k4 = f % (K_IN / 4);
-    xv[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (f < XF4 && r0 + rl < M) xv[e] = *reinterpret_cast<const float4*>(a.X + (long)(r0 + rl) * K_IN + 4 * k4);
+    const int f = min(tid + e * NT, XF4 - 1), rl = f / (K_IN / 4), k4 = f % (K_IN / 4);
+    xv[e] = *reinterpret_cast<const float4*>(a.X + (long)min(r0 + rl, M - 1) * K_IN + 4 * k4);
   }
-  float w2v = 0.f, b1v = 0.f;
-  if (tid < 16 * C) w2v = bf2f(W2s[(long)(j0 + tid / C) * C + tid % C]);
-  if (tid < 16) b1v = bf2f(a.b1s[j0 + tid]);
+  const int wi = min(tid, 16 * C - 1);
+  const long wo = (long)(j0 + wi / C) * C + wi % C;
+  const bf16_t w2a = a.W2s0[wo], w2b = a.W2s1[wo];
+  const bf16_t b1b = a.b1s[j0 + (tid & 15)];
+  const bf16_t b2b = a.b2s[tid % C];   // read by the blockIdx.y == 0 logit partials
+  __builtin_amdgcn_sched_barrier(0);
+  const int step = a.step[0];
+  const int par = step & 1;
+  const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
 
   // ---- 2. (LDS path) W1 block -> LDS transposed (w1t[n][k]), zero the K padding
-  if (!direct) {
+  if constexpr (!DIRECT) {
 #pragma unroll
     for (int t = 0; t < WCH; ++t) {
       const int idx = tid + t * NT;
@@ -188,15 +201,18 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
     }
     for (int idx = tid; idx < 16 * (KP - K_IN); idx += NT) w1t[(idx / (KP - K_IN)) * LDW + K_IN + idx % (KP - K_IN)] = 0;
   }
-  if (tid < 16 * C) w2s[tid / C][tid % C] = w2v;
-  if (tid < 16) b1sh[tid] = b1v;
+  if (tid < 16 * C) w2s[tid / C][tid % C] = bf2f(par ? w2b : w2a);
+  if (tid < 16) b1sh[tid] = bf2f(b1b);
 #pragma unroll
   for (int e = 0; e < XPT; ++e) {
     const int f = tid + e * NT, rl = f / (K_IN / 4), k4 = f % (K_IN / 4);
-    if (f < XF4)
+    if (f < XF4) {
+      const bool ok = r0 + rl < M;   // rows past M stay zero (X^T tail is read by mlp2_bwd)
       *reinterpret_cast<uint2*>(&xs[rl * LDXS + 4 * k4]) =
-          make_uint2((unsigned)f2bf(xv[e].x) | ((unsigned)f2bf(xv[e].y) << 16),
-                     (unsigned)f2bf(xv[e].z) | ((unsigned)f2bf(xv[e].w) << 16));
+          ok ? make_uint2((unsigned)f2bf(xv[e].x) | ((unsigned)f2bf(xv[e].y) << 16),
+                          (unsigned)f2bf(xv[e].z) | ((unsigned)f2bf(xv[e].w) << 16))
+             : make_uint2(0u, 0u);
+    }
   }
   __syncthreads();
   STAMP(1);
@@ -224,8 +240,8 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
       const bf16x8 b = direct ? bg[t] : *reinterpret_cast<const bf16x8*>(&w1t[(lane & 15) * LDW + k]);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        bf16x8 af = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-        if (k < K_IN) af = *reinterpret_cast<const bf16x8*>(&xs[(mt * 16 + (lane & 15)) * LDXS + k]);
+        // K tail: W1^T / w1t are zero past K_IN, the X image row is clamped in bounds
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(&xs[(mt * 16 + (lane & 15)) * LDXS + min(k, K_IN - 8)]);
         acc[mt] = mfma16x16x32(af, b, acc[mt]);
       }
     }
@@ -243,24 +259,34 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
     const int rowg = r0 + g4 * 4;
     u32x4 db = {0u, 0u, 0u, 0u};
     if (a.keep < 1.f && rowg < M) db = dropout_bits(a.seed, doff, dropout_group(0, rowg, col, M, H));
+    float gf[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int rl = g4 * 4 + e, row = r0 + rl;
       float hv = 0.f;
+      gf[e] = 0.f;
       if (row < M) {
         float v = b1sh[c];
 #pragma unroll
         for (int q = 0; q < NW; ++q) v += part[q][rl][c];
-        const bf16_t zb = f2bf(v);
-        a.Z1[(long)row * H + col] = zb;
-        hv = act_fwd(ACT_SILU, bf2f(zb));
-        if (a.keep < 1.f) hv = keep_word(db, e, a.keep) ? hv / a.keep : 0.f;
+        const float z = bf2f(f2bf(v));           // Z1 as the bf16 Dense output
+        const float ez = __expf(-z);
+        hv = z / (1.0f + ez);                    // act_fwd(ACT_SILU)
+        const float sg = 1.0f / (1.0f + ez);
+        float gd = sg * (1.0f + z * (1.0f - sg));  // act_grad(ACT_SILU)
+        if (a.keep < 1.f) {
+          const bool kp = keep_word(db, e, a.keep);
+          hv = kp ? hv / a.keep : 0.f;
+          gd = kp ? gd / a.keep : 0.f;
+        }
+        gf[e] = gd;
         const bf16_t hb = f2bf(hv);
         a.H1[(long)row * H + col] = hb;
         hv = bf2f(hb);
       }
       htile[rl][c] = hv;
     }
+    *reinterpret_cast<float4*>(a.G1 + ((long)(rowg >> 2) * H + col) * 4) = make_float4(gf[0], gf[1], gf[2], gf[3]);
   }
   __syncthreads();
   STAMP(3);
@@ -268,7 +294,7 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   if (tid < RB * C) {
     const int rl = tid / C, c = tid % C, row = r0 + rl;
     if (row < M) {
-      float s = (blockIdx.y == 0) ? bf2f(a.b2s[c]) : 0.f;
+      float s = (blockIdx.y == 0) ? bf2f(b2b) : 0.f;
 #pragma unroll
       for (int n = 0; n < 16; ++n) s += htile[rl][n] * w2s[n][c];
       atomicAdd(lg + (long)row * C + c, s);
@@ -284,81 +310,80 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   constexpr int MPM = 128;                 // max rows per device (fused path)
   constexpr int LDM = MPM + 8;             // padded row (bf16 elements)
   constexpr int NTILE = KC / 16;           // dW1 output tiles (one per wave)
-  static_assert(KC % 4 == 0 && K_IN % 4 == 0 && NTILE <= NW, "tile plan");
+  static_assert(KC % 4 == 0 && K_IN % KC == 0 && NTILE < NW, "tile plan (every dW1 row in range)");
   static_assert((MPM / 4) * 16 == NT, "one 4-row dropout group per thread");
-  __shared__ float dlog[MPM][C + 1];
+  constexpr int LDB = 40;                  // [row][32 classes] bf16 rows (classes zero-padded), +8 spread
+  static_assert(C <= 32 && MPM == NW * 16, "dZ1: one 16-row MFMA tile per wave, classes padded to K = 32");
+  __shared__ __attribute__((aligned(16))) bf16_t dlB[MPM * LDB];   // dlogits, row-major
+  __shared__ __attribute__((aligned(16))) bf16_t w2B[16 * LDB];    // W2[blk, :] (B operand: col = hidden unit)
   __shared__ __attribute__((aligned(16))) bf16_t dzT[16 * LDM];
   __shared__ __attribute__((aligned(16))) bf16_t h1T[16 * LDM];    // H1[:, blk]^T   (chunk-0 blocks)
   __shared__ __attribute__((aligned(16))) bf16_t dlT[16 * LDM];    // dlogits^T, classes padded to 16
-  __shared__ float w2s[16][C];
   __shared__ float red[2][NW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int M = a.M, H = a.H, Mp = (M + 31) & ~31;
   const int j0 = blockIdx.x * 16, kc0 = blockIdx.y * KC;
   const bool chunk0 = blockIdx.y == 0;
   STAMP(0);
-  const int step = a.step[0], par = step & 1;
   const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
-  const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
-  const bf16_t* W2s = par ? a.W2s1 : a.W2s0;
-  const float* lg = a.logits + (long)par * M * C;
   const int rg = tid >> 4, gn = tid & 15;   // this thread's dropout group: rows 4rg..4rg+3, column j0+gn
 
-  // ---- 0. issue all global loads (incl. the AdamW state of this wave's dW1 tile)
-  float lrow[C];
-  int lab = 0;
-  if (tid < M) {
+  // ---- 0. issue all global loads (incl. the AdamW state of this wave's outputs).
+  // Every load is unconditional -- clamped address, value selected afterwards -- and
+  // none waits on the step counter (both logits / W2-shadow parities are loaded):
+  // a load under a divergent guard makes the compiler wait for it at the join,
+  // which serialised this phase into ~6 round trips (asm).  The step counter is
+  // loaded last (its scalar read-back waits for every earlier load).
+  float lr0[C], lr1[C];
+  {
+    const long lo = (long)min(tid, M - 1) * C;
 #pragma unroll
-    for (int c = 0; c < C; ++c) lrow[c] = lg[(long)tid * C + c];
-    lab = a.labels[tid];
+    for (int c = 0; c < C; ++c) { lr0[c] = a.logits[lo + c]; lr1[c] = a.logits[(long)M * C + lo + c]; }
   }
-  bf16_t zv[4], hv[4];
+  const int lab = a.labels[min(tid, M - 1)];
+  const float4 g1 = *reinterpret_cast<const float4*>(a.G1 + ((long)min(rg, (M - 1) >> 2) * H + j0 + gn) * 4);
+  bf16_t hv[4];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int m = rg * 4 + e;
-    zv[e] = 0; hv[e] = 0;
-    if (m < M) {
-      zv[e] = a.Z1[(long)m * H + j0 + gn];
-      if (chunk0) hv[e] = a.H1[(long)m * H + j0 + gn];
-    }
-  }
+  for (int e = 0; e < 4; ++e) hv[e] = a.H1[(long)min(rg * 4 + e, M - 1) * H + j0 + gn];
   // A fragments of this wave's dW1 tile straight from X^T (written by mlp2_fwd, zero-padded to Mp)
+  const int wt_ = min(w, NTILE - 1);
   bf16x8 xf[MPM / 32];
 #pragma unroll
-  for (int ks = 0; ks < MPM / 32; ++ks) {
-    xf[ks] = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-    if (w < NTILE && ks < Mp / 32)
-      xf[ks] = *reinterpret_cast<const bf16x8*>(a.XT + (long)(kc0 + w * 16 + (lane & 15)) * a.ldxt + ks * 32 +
-                                                8 * (lane >> 4));
-  }
-  float w2v = 0.f;
-  if (tid < 16 * C) w2v = bf2f(W2s[(long)(j0 + tid / C) * C + tid % C]);
-  float op[4], om[4], ov[4];
-  const int trow0 = kc0 + w * 16 + (lane >> 4) * 4;   // this lane's 4 dW1 rows (tile = wave)
+  for (int ks = 0; ks < MPM / 32; ++ks)
+    xf[ks] = *reinterpret_cast<const bf16x8*>(a.XT + (long)(kc0 + wt_ * 16 + (lane & 15)) * a.ldxt +
+                                              min(ks, Mp / 32 - 1) * 32 + 8 * (lane >> 4));
+  const long wo = (long)(j0 + (tid >> 5)) * C + min(tid & 31, C - 1);   // w2B[tid >> 5][tid & 31]
+  const bf16_t w2a = a.W2s0[wo], w2b = a.W2s1[wo];
+  const int trow0 = kc0 + wt_ * 16 + (lane >> 4) * 4;   // this lane's 4 dW1 rows (tile = wave)
   const int tcol = j0 + (lane & 15);
   // wave NW-1 owns no dW1 tile; in chunk-0 blocks it reduces dW2 / db1 (/ db2) on MFMA,
-  // so it prefetches the AdamW state of those outputs instead
+  // so it prefetches the AdamW state of those outputs instead.  (Mode 0 has no
+  // optimizer state: the loads then read the gradient buffers, values unused.)
   const bool aux = chunk0 && w == NW - 1;
   const int ac = lane & 15;                        // aux: class column
-  float bp[4], bm[4], bv[4], qp = 0.f, qm = 0.f, qv = 0.f;
+  const bool fo = a.fuse_opt != 0;
+  const float* sp = aux ? (fo ? a.pW2 : a.gW2) : (fo ? a.pW1 : a.gW1);
+  const float* sm = aux ? (fo ? a.mW2 : a.gW2) : (fo ? a.mW1 : a.gW1);
+  const float* sv = aux ? (fo ? a.vW2 : a.gW2) : (fo ? a.vW1 : a.gW1);
+  const float* bpp = fo ? a.pb1 : a.gb1;
+  const float* bmp = fo ? a.mb1 : a.gb1;
+  const float* bvp = fo ? a.vb1 : a.gb1;
+  float op[4], om[4], ov[4], bp[4], bm[4], bv[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    op[e] = om[e] = ov[e] = 0.f;
-    bp[e] = bm[e] = bv[e] = 0.f;
-    if (a.fuse_opt && w < NTILE && trow0 + e < K_IN) {
-      const long idx = (long)(trow0 + e) * H + tcol;
-      op[e] = a.pW1[idx]; om[e] = a.mW1[idx]; ov[e] = a.vW1[idx];
-    }
-    if (a.fuse_opt && aux) {
-      const int n = (lane >> 4) * 4 + e;
-      if (ac < C) {
-        const long g = (long)(j0 + n) * C + ac;
-        op[e] = a.pW2[g]; om[e] = a.mW2[g]; ov[e] = a.vW2[g];
-      }
-      if (ac == 0) { bp[e] = a.pb1[j0 + n]; bm[e] = a.mb1[j0 + n]; bv[e] = a.vb1[j0 + n]; }
-    }
+    const int n = (lane >> 4) * 4 + e;
+    const long idx = aux ? (long)(j0 + n) * C + min(ac, C - 1) : (long)(trow0 + e) * H + tcol;
+    op[e] = sp[idx]; om[e] = sm[idx]; ov[e] = sv[idx];
+    bp[e] = bpp[j0 + n]; bm[e] = bmp[j0 + n]; bv[e] = bvp[j0 + n];
   }
-  if (a.fuse_opt && aux && lead && lane < C) { qp = a.pb2[lane]; qm = a.mb2[lane]; qv = a.vb2[lane]; }
+  const int lq = min(lane, C - 1);
+  const float qp = (fo ? a.pb2 : a.gb2)[lq], qm = (fo ? a.mb2 : a.gb2)[lq], qv = (fo ? a.vb2 : a.gb2)[lq];
+  __builtin_amdgcn_sched_barrier(0);
+  const int step = a.step[0];
+  const int par = step & 1;
+  float lrow[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) lrow[c] = par ? lr1[c] : lr0[c];
   const AdamK ak = adam_consts(a, step);
 
   // ---- 1. CE from the summed logits (rounded like the bf16 Dense output) -> dlogits
@@ -377,18 +402,26 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
     const float lse = mx + __logf(s);
     l_loss = lse - lrow[lab];
     l_corr = (am == lab) ? 1.f : 0.f;
+    unsigned row[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) row[q] = 0u;
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       const bf16_t gb = f2bf((__expf(lrow[c] - lse) - (c == lab ? 1.f : 0.f)) * a.inv_mb);
-      dlog[tid][c] = bf2f(gb);
+      row[c >> 1] |= (unsigned)gb << (16 * (c & 1));
       dlT[c * LDM + tid] = gb;
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<u32x4*>(&dlB[tid * LDB + 8 * q]) = (u32x4){row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]};
   } else if (tid < MPM) {
 #pragma unroll
     for (int c = 0; c < C; ++c) dlT[c * LDM + tid] = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *reinterpret_cast<u32x4*>(&dlB[tid * LDB + 8 * q]) = (u32x4){0u, 0u, 0u, 0u};
   }
   for (int idx = tid; idx < (16 - C) * MPM; idx += NT) dlT[(C + idx / MPM) * LDM + idx % MPM] = 0;
-  if (tid < 16 * C) w2s[tid / C][tid % C] = w2v;
+  w2B[(tid >> 5) * LDB + (tid & 31)] = (tid & 31) < C ? (par ? w2b : w2a) : (bf16_t)0;
   if (lead) {
     l_loss = wave_sum(l_loss);
     l_corr = wave_sum(l_corr);
@@ -399,22 +432,18 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   __syncthreads();
   STAMP(1);
 
-  // ---- 2. dZ1 group = (dlogits W2[blk]^T) * silu'(Z1) * mask/keep -> dzT[n][m]; H1 -> LDS
+  // ---- 2. dZ1 = (dlogits W2[blk]^T) * G1: one MFMA per wave (rows 16w.., K = classes);
+  // the output lane layout (rows 4*(lane>>4)+e, column lane&15) is this thread's
+  // dropout group (rg, gn), so G1's float4 multiplies in place.  H1 -> LDS.
   {
-    u32x4 db = {0u, 0u, 0u, 0u};
-    if (a.keep < 1.f && rg * 4 < M) db = dropout_bits(a.seed, doff, dropout_group(0, rg * 4, j0 + gn, M, H));
+    const bf16x8 af = *reinterpret_cast<const bf16x8*>(&dlB[(w * 16 + (lane & 15)) * LDB + 8 * (lane >> 4)]);
+    const bf16x8 bw = *reinterpret_cast<const bf16x8*>(&w2B[(lane & 15) * LDB + 8 * (lane >> 4)]);
+    const f32x4 dh = mfma16x16x32(af, bw, (f32x4){0.f, 0.f, 0.f, 0.f});
+    const float gv[4] = {g1.x, g1.y, g1.z, g1.w};
     unsigned packed[2] = {0u, 0u};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int m = rg * 4 + e;
-      float v = 0.f;
-      if (m < M) {
-        float dh = 0.f;
-#pragma unroll
-        for (int c = 0; c < C; ++c) dh += dlog[m][c] * w2s[gn][c];
-        v = dh * act_grad(ACT_SILU, bf2f(zv[e]));
-        if (a.keep < 1.f) v = keep_word(db, e, a.keep) ? v / a.keep : 0.f;
-      }
+      const float v = rg * 4 + e < M ? dh[e] * gv[e] : 0.f;
       packed[e >> 1] |= (unsigned)f2bf(v) << (16 * (e & 1));
     }
     *reinterpret_cast<uint2*>(&dzT[gn * LDM + rg * 4]) = make_uint2(packed[0], packed[1]);
@@ -439,20 +468,17 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
     unsigned wt[2] = {0u, 0u};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int i = trow0 + e;
-      if (i < K_IN) {
-        const long idx = (long)i * H + tcol;
-        if (a.fuse_opt) {
-          const bf16_t pb = f2bf(adam_apply(op[e], om[e], ov[e], acc[e], ak, a.pW1 + idx, a.mW1 + idx, a.vW1 + idx));
-          a.sW1[idx] = pb;
-          wt[e >> 1] |= (unsigned)pb << (16 * (e & 1));
-        } else {
-          a.gW1[idx] = acc[e];
-        }
+      const long idx = (long)(trow0 + e) * H + tcol;   // K_IN % KC == 0: always in range
+      if (a.fuse_opt) {
+        const bf16_t pb = f2bf(adam_apply(op[e], om[e], ov[e], acc[e], ak, a.pW1 + idx, a.mW1 + idx, a.vW1 + idx));
+        a.sW1[idx] = pb;
+        wt[e >> 1] |= (unsigned)pb << (16 * (e & 1));
+      } else {
+        a.gW1[idx] = acc[e];
       }
     }
     // the lane's 4 rows are 4 consecutive K elements of W1^T: one 8-byte store
-    if (a.fuse_opt && a.W1T && trow0 + 3 < K_IN)
+    if (a.fuse_opt && a.W1T)
       *reinterpret_cast<uint2*>(a.W1T + (long)tcol * a.ldw1t + trow0) = make_uint2(wt[0], wt[1]);
   } else if (aux) {
     // chunk-0 blocks, concurrently with the dW1 tiles:
@@ -530,10 +556,16 @@ JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* str
   if (k_in != 784 || c != 10 || a.H % 16 || a.M <= 0 || a.M > 128) return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (phase == 0) {
-    if (g_mlp2_rb == 32)
-      hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 32>), dim3((a.M + 31) / 32, a.H / 16), dim3(NT), 0, st, a);
-    else
-      hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 16>), dim3((a.M + 15) / 16, a.H / 16), dim3(NT), 0, st, a);
+    const bool direct = a.W1T != nullptr;
+    if (g_mlp2_rb == 32) {
+      const dim3 g((a.M + 31) / 32, a.H / 16);
+      if (direct) hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 32, true>), g, dim3(NT), 0, st, a);
+      else hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 32, false>), g, dim3(NT), 0, st, a);
+    } else {
+      const dim3 g((a.M + 15) / 16, a.H / 16);
+      if (direct) hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 16, true>), g, dim3(NT), 0, st, a);
+      else hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 16, false>), g, dim3(NT), 0, st, a);
+    }
   } else {
     hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112>), dim3(a.H / 16, 784 / 112), dim3(NT), 0, st, a);
   }

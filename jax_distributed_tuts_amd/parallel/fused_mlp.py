@@ -25,7 +25,7 @@ from ..utils.profiling import named_scope
 class Mlp2Args(ctypes.Structure):
     _fields_ = [("M", c_int), ("H", c_int), ("inv_mb", c_float), ("X", c_void_p), ("labels", c_void_p),
                 ("W1s", c_void_p), ("b1s", c_void_p), ("W2s0", c_void_p), ("W2s1", c_void_p), ("b2s", c_void_p),
-                ("Z1", c_void_p), ("H1", c_void_p), ("logits", c_void_p),
+                ("G1", c_void_p), ("H1", c_void_p), ("logits", c_void_p),
                 ("keep", c_float), ("seed", c_ulonglong), ("offset", c_ulonglong),
                 ("step", c_void_p), ("ticket", c_void_p),
                 ("gW1", c_void_p), ("gb1", c_void_p), ("gW2", c_void_p), ("gb2", c_void_p), ("mslot", c_void_p),
@@ -75,7 +75,8 @@ class FusedMLP2:
         H = self.model.dims[1]
         dev = P.master.device
         self.rows = rows
-        self.Z1 = torch.empty(rows, H, dtype=torch.bfloat16, device=dev)
+        # silu'(Z1) * mask / keep in 4-row groups ([Mp/4][H][4] fp32), mlp2_fwd -> mlp2_bwd
+        self.G1 = torch.zeros((rows + 31) // 32 * 32 * H, dtype=torch.float32, device=dev)
         self.H1 = torch.empty(rows, H, dtype=torch.bfloat16, device=dev)
         self.logits = torch.zeros(2, rows, 10, dtype=torch.float32, device=dev)
         # second parity buffer of W2's bf16 shadow (single-GPU fused-optimizer mode)
@@ -111,7 +112,7 @@ class FusedMLP2:
         a.W2s0 = P.s("output_dense/kernel").data_ptr()
         a.W2s1 = self.W2s1.data_ptr() if self.fuse_opt else a.W2s0
         a.b2s = P.s("output_dense/bias").data_ptr()
-        a.Z1, a.H1, a.logits = self.Z1.data_ptr(), self.H1.data_ptr(), self.logits.data_ptr()
+        a.G1, a.H1, a.logits = self.G1.data_ptr(), self.H1.data_ptr(), self.logits.data_ptr()
         a.keep = 1.0 - self.model.dropout_rate
         from ..utils import rng as R
 

@@ -41,6 +41,14 @@ def report(kind, st, nwg):
         print(f"  {NAMES[kind][i]:22s} end @ median {float(d.median()):7.2f} us  max {float(d.max()):7.2f}"
               f"   (phase median {float((d - prev).median()):6.2f})")
         prev = d
+    if kind == 1:
+        # per input chunk (blockIdx.y; chunk 0 also runs the dW2/db1/db2 wave)
+        ny = nwg // 32
+        for y in range(ny):
+            sl = st[y * 32:(y + 1) * 32]
+            ends = [float((sl[:, i] - sl[:, 0]).median()) for i in range(1, 5)]
+            mx = float((sl[:, 4] - t0.min()).max())
+            print(f"    chunk {y}: phase ends (median) " + " ".join(f"{e:5.2f}" for e in ends) + f"  last end {mx:5.2f}")
 
 
 def main():
@@ -71,10 +79,12 @@ def main():
         _lib.check(L.jdt_mlp2(ctypes.byref(args1), 1, 784, 10, s), "bwd")
     torch.cuda.synchronize()
     H = 512
-    report(0, sa.cpu(), ((a.rows + 31) // 32) * (H // 16))
+    rb = int(os.environ.get("JDT_MLP2_RB", "16"))
+    nf = ((a.rows + rb - 1) // rb) * (H // 16)
+    report(0, sa.cpu(), nf)
     report(1, sb.cpu(), (H // 16) * 7)
     # inter-kernel gap: last fwd end -> first bwd start
-    fa = sa.cpu()[: ((a.rows + 31) // 32) * (H // 16) * 8].view(-1, 8)
+    fa = sa.cpu()[: nf * 8].view(-1, 8)
     fb = sb.cpu()[: (H // 16) * 7 * 8].view(-1, 8)
     print(f"fwd last end -> bwd first start: {float(fb[:, 0].min() - fa[:, 4].max()) * 10e-3:.2f} us")
 

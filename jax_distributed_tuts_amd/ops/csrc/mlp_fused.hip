@@ -69,6 +69,9 @@ struct Mlp2Args {
   int ldw1t;     // >= KP (zero-padded K tail)
   bf16_t* XT;    // [K_IN][ldxt] = X^T (rows of all minibatches), written by mlp2_fwd
   int ldxt;      // >= Mp, zero-padded sample tail
+  // mlp2_fwd's copy of the step it ran (block (0,0) writes it); mlp2_bwd reads the
+  // copy, so its lead block may advance `step` itself without an arrival ticket
+  int* step_copy;
 };
 
 // Slots 0-4: s_memrealtime at phase ends; slots 5/6: s_memtime (core clock) at
@@ -146,8 +149,14 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   // value selected afterwards) and nothing waits on the step counter: a load under
   // a divergent guard makes the compiler wait for it at the join (asm: this phase
   // was ~8 serial round trips), and the parity-dependent W2 shadow is loaded from
-  // both buffers.  The step counter is loaded LAST: it is read back into a scalar
-  // register (readfirstlane), which waits for every load issued before it.
+  // both buffers.  The step counter is loaded FIRST through a lane-varying address
+  // (an asm-produced zero), so it stays a per-lane value: a uniform load is read
+  // back into a scalar register (readfirstlane), which would wait for every load
+  // in flight.  The dropout bits, which depend only on it, are then computed while
+  // the operand loads are still in flight.
+  int lz;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(lz));
+  const int step = a.step[lz];
   u32x4 wv[WCH];
   bf16x8 bg[MAXT];
   if constexpr (!DIRECT) {
@@ -180,9 +189,13 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   const bf16_t b1b = a.b1s[j0 + (tid & 15)];
   const bf16_t b2b = a.b2s[tid % C];   // read by the blockIdx.y == 0 logit partials
   __builtin_amdgcn_sched_barrier(0);
-  const int step = a.step[0];
   const int par = step & 1;
   const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
+  if (a.step_copy && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) a.step_copy[0] = step;
+  // dropout bits of this thread's 4-row group (phase 4 threads only)
+  const int g4 = tid >> 4, gc = tid & 15, rowg = r0 + g4 * 4;
+  u32x4 db = {0u, 0u, 0u, 0u};
+  if (tid < (RB / 4) * 16 && a.keep < 1.f && rowg < M) db = dropout_bits(a.seed, doff, dropout_group(0, rowg, j0 + gc, M, H));
 
   // ---- 2. (LDS path) W1 block -> LDS transposed (w1t[n][k]), zero the K padding
   if constexpr (!DIRECT) {
@@ -255,10 +268,7 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
 
   // ---- 4. bias + silu + dropout per 4-row group; H tile kept in LDS
   if (tid < (RB / 4) * 16) {
-    const int g4 = tid >> 4, c = tid & 15, col = j0 + c;
-    const int rowg = r0 + g4 * 4;
-    u32x4 db = {0u, 0u, 0u, 0u};
-    if (a.keep < 1.f && rowg < M) db = dropout_bits(a.seed, doff, dropout_group(0, rowg, col, M, H));
+    const int c = gc, col = j0 + c;
     float gf[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -313,7 +323,7 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   static_assert(KC % 4 == 0 && K_IN % KC == 0 && NTILE < NW, "tile plan (every dW1 row in range)");
   static_assert((MPM / 4) * 16 == NT, "one 4-row dropout group per thread");
   constexpr int LDB = 40;                  // [row][32 classes] bf16 rows (classes zero-padded), +8 spread
-  static_assert(C <= 32 && MPM == NW * 16, "dZ1: one 16-row MFMA tile per wave, classes padded to K = 32");
+  static_assert(C < 16 && MPM == NW * 16, "dZ1: one 16-row MFMA tile per wave, classes padded to K = 32");
   __shared__ __attribute__((aligned(16))) bf16_t dlB[MPM * LDB];   // dlogits, row-major
   __shared__ __attribute__((aligned(16))) bf16_t w2B[16 * LDB];    // W2[blk, :] (B operand: col = hidden unit)
   __shared__ __attribute__((aligned(16))) bf16_t dzT[16 * LDM];
@@ -362,24 +372,23 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   const bool aux = chunk0 && w == NW - 1;
   const int ac = lane & 15;                        // aux: class column
   const bool fo = a.fuse_opt != 0;
-  const float* sp = aux ? (fo ? a.pW2 : a.gW2) : (fo ? a.pW1 : a.gW1);
-  const float* sm = aux ? (fo ? a.mW2 : a.gW2) : (fo ? a.mW1 : a.gW1);
-  const float* sv = aux ? (fo ? a.vW2 : a.gW2) : (fo ? a.vW1 : a.gW1);
-  const float* bpp = fo ? a.pb1 : a.gb1;
-  const float* bmp = fo ? a.mb1 : a.gb1;
-  const float* bvp = fo ? a.vb1 : a.gb1;
-  float op[4], om[4], ov[4], bp[4], bm[4], bv[4];
+  // aux lanes: class column ac < C -> W2[j0+n][ac]; ac >= C -> b1[j0+n] (lane C applies it)
+  const bool w2l = aux && ac < C;
+  const float* sp = aux ? (w2l ? (fo ? a.pW2 : a.gW2) : (fo ? a.pb1 : a.gb1)) : (fo ? a.pW1 : a.gW1);
+  const float* sm = aux ? (w2l ? (fo ? a.mW2 : a.gW2) : (fo ? a.mb1 : a.gb1)) : (fo ? a.mW1 : a.gW1);
+  const float* sv = aux ? (w2l ? (fo ? a.vW2 : a.gW2) : (fo ? a.vb1 : a.gb1)) : (fo ? a.vW1 : a.gW1);
+  float op[4], om[4], ov[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int n = (lane >> 4) * 4 + e;
-    const long idx = aux ? (long)(j0 + n) * C + min(ac, C - 1) : (long)(trow0 + e) * H + tcol;
+    const long idx = aux ? (w2l ? (long)(j0 + n) * C + ac : (long)(j0 + n)) : (long)(trow0 + e) * H + tcol;
     op[e] = sp[idx]; om[e] = sm[idx]; ov[e] = sv[idx];
-    bp[e] = bpp[j0 + n]; bm[e] = bmp[j0 + n]; bv[e] = bvp[j0 + n];
   }
+  const float run_pre = (a.running ? a.running : a.logits)[lane & 3];   // lead: metric accumulators
   const int lq = min(lane, C - 1);
   const float qp = (fo ? a.pb2 : a.gb2)[lq], qm = (fo ? a.mb2 : a.gb2)[lq], qv = (fo ? a.vb2 : a.gb2)[lq];
   __builtin_amdgcn_sched_barrier(0);
-  const int step = a.step[0];
+  const int step = (a.step_copy ? a.step_copy : a.step)[0];
   const int par = step & 1;
   float lrow[C];
 #pragma unroll
@@ -471,7 +480,9 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
       const long idx = (long)(trow0 + e) * H + tcol;   // K_IN % KC == 0: always in range
       if (a.fuse_opt) {
         const bf16_t pb = f2bf(adam_apply(op[e], om[e], ov[e], acc[e], ak, a.pW1 + idx, a.mW1 + idx, a.vW1 + idx));
-        a.sW1[idx] = pb;
+        // with the W1^T copy, the [in,out] bf16 shadow is rebuilt from it by
+        // FusedMLP2.finalize() instead of being written every step (0.8 MB of HBM writes)
+        if (!a.W1T) a.sW1[idx] = pb;
         wt[e >> 1] |= (unsigned)pb << (16 * (e & 1));
       } else {
         a.gW1[idx] = acc[e];
@@ -487,7 +498,9 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) ones[q] = (short)0x3f80;  // bf16 1.0
     f32x4 aw = {0.f, 0.f, 0.f, 0.f}, ab1 = {0.f, 0.f, 0.f, 0.f}, ab2 = {0.f, 0.f, 0.f, 0.f};
-    for (int ks = 0; ks < Mp / 32; ++ks) {
+#pragma unroll
+    for (int ks = 0; ks < MPM / 32; ++ks) {
+      if (ks >= Mp / 32) break;
       const int kk = ks * 32 + 8 * (lane >> 4);
       const bf16x8 hT = *reinterpret_cast<const bf16x8*>(&h1T[(lane & 15) * LDM + kk]);
       const bf16x8 dT = *reinterpret_cast<const bf16x8*>(&dlT[(lane & 15) * LDM + kk]);
@@ -499,16 +512,20 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
     bf16_t* sW2n = par ? a.sW2_0 : a.sW2_1;   // next step's parity buffer
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
+      // lanes ac < C: W2[j0+n][ac]; lane ac == C: b1[j0+n] (every column of ab1 holds
+      // db1, B = ones) -- one AdamW code path for both, its state loaded in phase 0
       const int n = (lane >> 4) * 4 + e;
-      if (ac < C) {
-        const long g = (long)(j0 + n) * C + ac;
-        if (a.fuse_opt) sW2n[g] = f2bf(adam_apply(op[e], om[e], ov[e], aw[e], ak, a.pW2 + g, a.mW2 + g, a.vW2 + g));
-        else a.gW2[g] = aw[e];
-      }
-      if (ac == 0) {
-        const int j = j0 + n;
-        if (a.fuse_opt) a.sb1[j] = f2bf(adam_apply(bp[e], bm[e], bv[e], ab1[e], ak, a.pb1 + j, a.mb1 + j, a.vb1 + j));
-        else a.gb1[j] = ab1[e];
+      if (ac <= C) {
+        const bool isb = ac == C;
+        const long o = isb ? (long)(j0 + n) : (long)(j0 + n) * C + ac;
+        const float gr = isb ? ab1[e] : aw[e];
+        if (a.fuse_opt) {
+          const float pn = adam_apply(op[e], om[e], ov[e], gr, ak, (isb ? a.pb1 : a.pW2) + o, (isb ? a.mb1 : a.mW2) + o,
+                                      (isb ? a.vb1 : a.vW2) + o);
+          (isb ? a.sb1 : sW2n)[o] = f2bf(pn);
+        } else {
+          (isb ? a.gb1 : a.gW2)[o] = gr;
+        }
       }
     }
     if (lead && lane < C) {
@@ -519,27 +536,17 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   __syncthreads();
   STAMP(3);
 
-  if (lead) {
-    if (tid == 0) {
-      float L = 0.f, Cr = 0.f;
-      for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
-      if (a.fuse_opt && a.running) {
-        a.running[0] += L; a.running[1] += (float)M; a.running[2] += Cr; a.running[3] += (float)M;
-      } else if (a.mslot) {
-        a.mslot[0] = L; a.mslot[1] = (float)M; a.mslot[2] = Cr; a.mslot[3] = (float)M;
-      }
-    }
+  if (lead && tid < 4) {
+    float L = 0.f, Cr = 0.f;
+    for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
+    const float val = tid == 0 ? L : tid == 2 ? Cr : (float)M;   // {loss sum, n, correct, n}
+    if (fo && a.running) a.running[tid] = run_pre + val;
+    else if (a.mslot) a.mslot[tid] = val;
+    // advance the device step: every other workgroup of this launch reads the
+    // forward's copy (step_copy), so no arrival ticket is needed
+    if (fo && tid == 0) a.step[0] = step + 1;
   }
-  __syncthreads();
   STAMP(4);
-  if (a.fuse_opt && tid == 0) {
-    // advance the device step once every workgroup has read it
-    const unsigned t = atomicAdd(a.ticket, 1u);
-    if (t == gridDim.x * gridDim.y - 1) {
-      a.step[0] = step + 1;
-      __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 }  // namespace jdt

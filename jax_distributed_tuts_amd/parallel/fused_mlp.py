@@ -36,7 +36,8 @@ class Mlp2Args(ctypes.Structure):
                 ("sW1", c_void_p), ("sb1", c_void_p), ("sW2_0", c_void_p), ("sW2_1", c_void_p), ("sb2", c_void_p),
                 ("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float), ("wd", c_float),
                 ("gscale", c_float), ("running", c_void_p), ("stamps", c_void_p),
-                ("W1T", c_void_p), ("ldw1t", c_int), ("XT", c_void_p), ("ldxt", c_int)]
+                ("W1T", c_void_p), ("ldw1t", c_int), ("XT", c_void_p), ("ldxt", c_int),
+                ("step_copy", c_void_p)]
 
 
 _lib.declare("jdt_mlp2", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_int, c_void_p])
@@ -79,6 +80,7 @@ class FusedMLP2:
         self.G1 = torch.zeros((rows + 31) // 32 * 32 * H, dtype=torch.float32, device=dev)
         self.H1 = torch.empty(rows, H, dtype=torch.bfloat16, device=dev)
         self.logits = torch.zeros(2, rows, 10, dtype=torch.float32, device=dev)
+        self.step_copy = torch.zeros(1, dtype=torch.int32, device=dev)  # mlp2_fwd -> mlp2_bwd
         # second parity buffer of W2's bf16 shadow (single-GPU fused-optimizer mode)
         self.W2s1 = P.s("output_dense/kernel").clone()
         self.metrics = metrics
@@ -124,6 +126,7 @@ class FusedMLP2:
         a.mslot = self.mslot.data_ptr()
         a.fuse_opt = int(self.fuse_opt)
         a.XT, a.ldxt = self.XT.data_ptr(), self.Mp
+        a.step_copy = self.step_copy.data_ptr()
         if self.W1T is not None:
             a.W1T, a.ldw1t = self.W1T.data_ptr(), 800
         tx = st.tx
@@ -161,10 +164,13 @@ class FusedMLP2:
                 K.metrics_fold_(self.metrics, P.metrics_slot)
 
     def finalize(self):
-        """Bring the generic bf16 shadow of W2 up to date (parity buffer in use)."""
+        """Bring the generic bf16 shadows up to date: W2's parity buffer in use, and
+        W1's (mlp2_bwd keeps only the K-contiguous W1^T copy current)."""
         P = self.state.params
         if self.fuse_opt and int(self.state.opt_state["count"].item()) % 2 == 1:
             P.s("output_dense/kernel").copy_(self.W2s1)
+        if self.W1T is not None:
+            P.s("input_dense/kernel").copy_(self.W1T[:, :784].t())
 
 
 # ----------------------------------------------------------------------------- deep MLPs (csrc/mlp_deep.hip)

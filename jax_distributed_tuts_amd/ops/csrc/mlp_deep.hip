@@ -9,7 +9,8 @@
 //   md_fwd (layer i)  grid (row blocks of 16) x (output blocks of 16), 8 waves
 //     Z_i = IN W_i + b_i, H_i = dropout(silu(Z_i)); IN is the fp32 data (layer
 //     0) or H_{i-1} (bf16).  Also writes IN^T (K-contiguous, for the dW MFMA of
-//     the matching backward launch).  The last hidden layer also accumulates
+//     the matching backward launch) and the backward factor
+//     G_i = silu'(Z_i) * mask/keep, so the backward needs neither Z_i nor Philox.  The last hidden layer also accumulates
 //     the head's partial logits H_i[:,blk] W_head[blk,:] with fp32 atomics.
 //
 //   md_bwd (layer i)  grid (output blocks of 16) x (input chunks of KC), 8 waves
@@ -17,7 +18,7 @@
 //     through the head; otherwise (dZ_{i+1} W_{i+1}^T)[:, blk] on MFMA with
 //     both fragments loaded straight from global memory -- recomputed by each
 //     of the K_IN/KC workgroups of the column block, which is cheaper than a
-//     separate launch -- then * silu'(Z_i) * mask/keep.
+//     separate launch -- then * G_i (from md_fwd).
 //     dW_i[chunk, blk] = IN[:, chunk]^T dZ_i[:, blk] on MFMA (IN^T from md_fwd),
 //     db_i (and, TOP, the head's dW/db + metrics) on the spare wave of the
 //     chunk-0 workgroups, which also store dZ_i for the next launch.
@@ -47,7 +48,7 @@ struct MdArgs {
   const bf16_t* WT;     // W_i^T [N][ldwt] (direct fwd fragments) or null -> LDS transposition of Ws
   int ldwt;
   const bf16_t* bs;     // b_i shadow [N]
-  bf16_t* Z;            // [M][N] pre-activation
+  float* G;             // backward factor silu'(Z_i) * mask/keep, fp32 [ceil(M/4)][N][4] (dropout-group layout)
   bf16_t* Hout;         // [M][N] activation (next layer's input)
   bf16_t* INT;          // IN^T [K][ldint] (fwd writes, bwd reads)
   int ldint;
@@ -243,24 +244,34 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
     const int rowg = r0 + g4 * 4;
     u32x4 db = {0u, 0u, 0u, 0u};
     if (a.keep < 1.f && rowg < M) db = dropout_bits(a.seed, doff, dropout_group(0, rowg, col, M, N));
+    float gf[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int rl = g4 * 4 + e, row = r0 + rl;
       float hv = 0.f;
+      gf[e] = 0.f;
       if (row < M) {
         float v = bsh[c];
 #pragma unroll
         for (int q = 0; q < NW; ++q) v += part[q][rl][c];
-        const bf16_t zb = f2bf(v);
-        a.Z[(long)row * N + col] = zb;
-        hv = act_fwd(ACT_SILU, bf2f(zb));
-        if (a.keep < 1.f) hv = keep_word(db, e, a.keep) ? hv / a.keep : 0.f;
+        const float z = bf2f(f2bf(v));           // Z_i as the bf16 Dense output
+        const float ez = __expf(-z);
+        const float sg = 1.0f / (1.0f + ez);
+        hv = z * sg;                             // act_fwd(ACT_SILU)
+        float gd = sg * (1.0f + z * (1.0f - sg));  // act_grad(ACT_SILU)
+        if (a.keep < 1.f) {
+          const bool kp = keep_word(db, e, a.keep);
+          hv = kp ? hv / a.keep : 0.f;
+          gd = kp ? gd / a.keep : 0.f;
+        }
+        gf[e] = gd;
         const bf16_t hb = f2bf(hv);
         a.Hout[(long)row * N + col] = hb;
         hv = bf2f(hb);
       }
       htile[rl][c] = hv;
     }
+    *reinterpret_cast<float4*>(a.G + ((long)(rowg >> 2) * N + col) * 4) = make_float4(gf[0], gf[1], gf[2], gf[3]);
   }
   if (HEAD) {
     __syncthreads();
@@ -298,13 +309,13 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   const bool chunk0 = blockIdx.y == 0;
   const int step = a.step[0], par = step & 1;
   const bool lead = TOP && blockIdx.x == 0 && blockIdx.y == 0;
-  const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
   const int rg = tid >> 4, gn = tid & 15;   // TOP: this thread's group (rows 4rg..4rg+3, column j0+gn)
 
   // ---- 0. every global load up front
   float lrow[TOP ? C : 1];
   int lab = 0;
-  bf16_t zv[4], hv[4];
+  float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
+  bf16_t hv[4];
   bf16x8 dzf[TOP ? 1 : NKS], wnf[TOP ? 1 : NKS];
   float whv = 0.f;
   if constexpr (TOP) {
@@ -314,14 +325,12 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       for (int c = 0; c < C; ++c) lrow[c] = lg[(long)tid * C + c];
       lab = a.labels[tid];
     }
+    if (rg * 4 < M) gv = *reinterpret_cast<const float4*>(a.G + ((long)rg * N + j0 + gn) * 4);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int m = rg * 4 + e;
-      zv[e] = 0; hv[e] = 0;
-      if (m < M) {
-        zv[e] = a.Z[(long)m * N + j0 + gn];
-        if (chunk0) hv[e] = a.Hout[(long)m * N + j0 + gn];
-      }
+      hv[e] = 0;
+      if (m < M && chunk0) hv[e] = a.Hout[(long)m * N + j0 + gn];
     }
     const bf16_t* Wh = par ? a.Wh1 : a.Wh0;
     if (tid < 16 * C) whv = bf2f(Wh[(long)(j0 + tid / C) * C + tid % C]);
@@ -335,11 +344,9 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       if (row < M) dzf[ks] = *reinterpret_cast<const bf16x8*>(a.dZn + (long)row * NN + ks * 32 + 8 * (lane >> 4));
       wnf[ks] = *reinterpret_cast<const bf16x8*>(Wn + (long)(j0 + (lane & 15)) * NN + ks * 32 + 8 * (lane >> 4));
     }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int m = w * 16 + (lane >> 4) * 4 + e;
-      zv[e] = 0;
-      if (m < M) zv[e] = a.Z[(long)m * N + j0 + (lane & 15)];
+    {
+      const int row0 = w * 16 + (lane >> 4) * 4;
+      if (row0 < M) gv = *reinterpret_cast<const float4*>(a.G + ((long)(row0 >> 2) * N + j0 + (lane & 15)) * 4);
     }
   }
   // A fragments of this wave's dW tile from IN^T (zero-padded to Mp samples)
@@ -414,8 +421,7 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       for (int i = tid; i < M * C; i += NT) nxt[i] = 0.f;
     }
     __syncthreads();
-    u32x4 db = {0u, 0u, 0u, 0u};
-    if (a.keep < 1.f && rg * 4 < M) db = dropout_bits(a.seed, doff, dropout_group(0, rg * 4, j0 + gn, M, N));
+    const float gfac[4] = {gv.x, gv.y, gv.z, gv.w};
     unsigned packed[2] = {0u, 0u};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -425,8 +431,7 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
         float dh = 0.f;
 #pragma unroll
         for (int c = 0; c < C; ++c) dh += dlog[m][c] * whs[gn][c];
-        v = dh * act_grad(ACT_SILU, bf2f(zv[e]));
-        if (a.keep < 1.f) v = keep_word(db, e, a.keep) ? v / a.keep : 0.f;
+        v = dh * gfac[e];
       }
       const bf16_t vb = f2bf(v);
       packed[e >> 1] |= (unsigned)vb << (16 * (e & 1));
@@ -442,16 +447,14 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) acc = mfma16x16x32(dzf[ks], wnf[ks], acc);
       const int row0 = w * 16 + (lane >> 4) * 4, col = j0 + (lane & 15);
-      u32x4 db = {0u, 0u, 0u, 0u};
-      if (a.keep < 1.f && row0 < M) db = dropout_bits(a.seed, doff, dropout_group(0, row0, col, M, N));
+      const float gfac[4] = {gv.x, gv.y, gv.z, gv.w};
       unsigned packed[2] = {0u, 0u};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int m = row0 + e;
         float v = 0.f;
         if (m < M) {
-          v = acc[e] * act_grad(ACT_SILU, bf2f(zv[e]));
-          if (a.keep < 1.f) v = keep_word(db, e, a.keep) ? v / a.keep : 0.f;
+          v = acc[e] * gfac[e];
         }
         const bf16_t vb = f2bf(v);
         packed[e >> 1] |= (unsigned)vb << (16 * (e & 1));

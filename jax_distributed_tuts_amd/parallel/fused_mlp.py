@@ -179,7 +179,7 @@ class MdArgs(ctypes.Structure):
 
     _fields_ = [("M", c_int), ("K", c_int), ("N", c_int), ("C", c_int), ("inv_mb", c_float),
                 ("X", c_void_p), ("Ws0", c_void_p), ("Ws1", c_void_p), ("WT", c_void_p), ("ldwt", c_int),
-                ("bs", c_void_p), ("Z", c_void_p), ("Hout", c_void_p), ("INT", c_void_p), ("ldint", c_int),
+                ("bs", c_void_p), ("G", c_void_p), ("Hout", c_void_p), ("INT", c_void_p), ("ldint", c_int),
                 ("Wh0", c_void_p), ("Wh1", c_void_p), ("bh", c_void_p), ("logits", c_void_p), ("labels", c_void_p),
                 ("keep", c_float), ("seed", c_ulonglong), ("offset", c_ulonglong),
                 ("step", c_void_p), ("ticket", c_void_p), ("advance_step", c_int),
@@ -229,7 +229,10 @@ class FusedMLPDeep:
         H, L = DEEP_H, m.L
         self.nh = L - 1                                    # hidden layers
         bf = dict(dtype=torch.bfloat16, device=dev)
-        self.Z = [torch.empty(rows, H, **bf) for _ in range(self.nh)]
+        # backward factors silu'(Z) * mask/keep, fp32 [row groups of 4][H][4], padded to the
+        # forward's 16-row blocks
+        self.G = [torch.zeros((rows + 15) // 16 * 4, H, 4, dtype=torch.float32, device=dev)
+                  for _ in range(self.nh)]
         self.Hs = [torch.empty(rows, H, **bf) for _ in range(self.nh)]
         self.dZ = [None] + [torch.empty(rows, H, **bf) for _ in range(1, self.nh)]
         self.Mp = (rows + 31) // 32 * 32
@@ -277,7 +280,7 @@ class FusedMLPDeep:
                 a.WTout = self.WT[i].data_ptr()
             a.ldwt = self.WT[i].shape[1]
         a.bs = P.s(self.bn[i]).data_ptr()
-        a.Z, a.Hout = self.Z[i].data_ptr(), self.Hs[i].data_ptr()
+        a.G, a.Hout = self.G[i].data_ptr(), self.Hs[i].data_ptr()
         a.INT, a.ldint = self.INT[i].data_ptr(), self.Mp
         a.Wh0, a.Wh1 = self._shadow_pair(L - 1)
         a.bh = P.s(self.bn[L - 1]).data_ptr()

@@ -72,6 +72,22 @@ struct Mlp2Args {
   // mlp2_fwd's copy of the step it ran (block (0,0) writes it); mlp2_bwd reads the
   // copy, so its lead block may advance `step` itself without an arrival ticket
   int* step_copy;
+  // loop kernel only: fp32 snapshot of W2 [H][C] taken by the forward (row block 0)
+  // for the same step's backward, whose chunk-0 workgroups update W2 concurrently
+  float* W2snap;
+};
+
+// Persistent multi-step launch (mlp2_loop_kernel): n steps, grid barriers between
+// the phases.  ctr counts barrier arrivals across launches (never reset); base is
+// its value at the start of the next launch (advanced by block 0 at the end);
+// err is raised by a barrier that timed out (every workgroup then leaves).
+struct Mlp2Loop {
+  int n;
+  unsigned* ctr;
+  unsigned* base;
+  int* err;
+  long long timeout;   // s_memrealtime ticks (100 MHz) per barrier
+  unsigned long long* stamps;   // diagnostic: [G][n][5] s_memrealtime per phase edge (null = off)
 };
 
 // Slots 0-4: s_memrealtime at phase ends; slots 5/6: s_memtime (core clock) at
@@ -88,7 +104,8 @@ struct Mlp2Args {
 
 struct AdamK { float b1, b2, eps, wd, lr, gs, rbc1, rbc2; };
 
-__device__ __forceinline__ AdamK adam_consts(const Mlp2Args& a, int step) {
+template <class AT>
+__device__ __forceinline__ AdamK adam_consts(AT& a, int step) {
   AdamK k;
   k.b1 = a.beta1; k.b2 = a.beta2; k.eps = a.eps; k.wd = a.wd; k.lr = a.lr; k.gs = a.gscale;
   const float t = (float)(step + 1);
@@ -112,6 +129,90 @@ __device__ __forceinline__ float adam_elem(float* p, float* m, float* v, long i,
   return adam_apply(p[i], m[i], v[i], g, k, p + i, m + i, v + i);
 }
 
+// ---------------------------------------------------------------------------- in-launch hand-offs
+// mlp2_loop_kernel hands data between workgroups inside one launch WITHOUT
+// agent-scope release/acquire fences (on this multi-XCD part they write back /
+// invalidate a whole XCD L2 per workgroup, ~1.7-6.5 us each): every handed-off
+// byte is stored AND loaded with sc1 (global_store/load ... sc1: written through
+// to / read from the cross-XCD coherence point, never from a stale L1), 4- or
+// 8-byte accesses; a grid barrier orders them (each wave drains its stores with
+// s_waitcnt vmcnt(0), workgroup barrier, ONE lane adds to the arrival counter and
+// polls it with sc1 loads, workgroup barrier).  SC1 = false: plain accesses (the
+// two-launch path, where the kernel boundary orders everything).
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+typedef __attribute__((address_space(1))) float gf32_t;
+typedef __attribute__((address_space(1))) unsigned gu32_t;
+typedef __attribute__((address_space(1))) int gi32_t;
+
+template <bool SC1> __device__ __forceinline__ float ld_f(const float* p) {
+  if constexpr (SC1) return __hip_atomic_load((gf32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <bool SC1> __device__ __forceinline__ void st_f(float* p, float v) {
+  if constexpr (SC1) __hip_atomic_store((gf32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <bool SC1> __device__ __forceinline__ unsigned long long ld_u64(const void* p) {
+  if constexpr (SC1) return __hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *reinterpret_cast<const unsigned long long*>(p);
+}
+template <bool SC1> __device__ __forceinline__ void st_u64(void* p, unsigned long long v) {
+  if constexpr (SC1) __hip_atomic_store((gu64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *reinterpret_cast<unsigned long long*>(p) = v;
+}
+// 16 bytes: one dwordx4 (plain) or two sc1 dwordx2
+template <bool SC1> __device__ __forceinline__ u32x4 ld_b128(const void* p) {
+  if constexpr (SC1) {
+    const unsigned long long lo = ld_u64<true>(p), hi = ld_u64<true>(static_cast<const char*>(p) + 8);
+    return (u32x4){(unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32)};
+  } else {
+    return *reinterpret_cast<const u32x4*>(p);
+  }
+}
+template <bool SC1> __device__ __forceinline__ void st_b128(void* p, u32x4 v) {
+  if constexpr (SC1) {
+    st_u64<true>(p, (unsigned long long)v.x | ((unsigned long long)v.y << 32));
+    st_u64<true>(static_cast<char*>(p) + 8, (unsigned long long)v.z | ((unsigned long long)v.w << 32));
+  } else {
+    *reinterpret_cast<u32x4*>(p) = v;
+  }
+}
+// AdamW whose updated parameter is handed to other workgroups (sc1 store of p)
+template <bool SC1>
+__device__ __forceinline__ float adam_apply_h(float p, float m, float v, float g, const AdamK& k, float* pp, float* mp,
+                                              float* vp) {
+  float tp, tm, tv;
+  const float r = adam_apply(p, m, v, g, k, &tp, &tm, &tv);
+  st_f<SC1>(pp, tp); *mp = tm; *vp = tv;
+  return r;
+}
+
+// Grid barrier of the loop kernel: true when every workgroup has arrived (target
+// arrivals counted since the counter's creation), false on timeout / a raised err.
+__device__ __forceinline__ bool grid_sync(const Mlp2Loop& l, unsigned target, int* flag_lds) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its hand-off stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add((gu32_t*)l.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    int ok = 1;
+    for (unsigned spins = 0;; ++spins) {
+      if ((int)(__hip_atomic_load((gu32_t*)l.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0) break;
+      if ((spins & 63) == 63 &&
+          (__hip_atomic_load((gi32_t*)l.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+           (long long)(__builtin_amdgcn_s_memrealtime() - t0) > l.timeout)) {
+        __hip_atomic_store((gi32_t*)l.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    flag_lds[0] = ok;
+  }
+  __syncthreads();
+  return flag_lds[0] != 0;
+}
+
 // ---------------------------------------------------------------------------- forward
 // RB rows per workgroup (16 or 32): 16-row blocks halve each workgroup's X
 // bytes and double the grid (256 workgroups at M = 128), which the load-latency
@@ -120,8 +221,9 @@ __device__ __forceinline__ float adam_elem(float* p, float* m, float* v, long i,
 // otherwise the W1 column block is transposed through LDS.  (A compile-time
 // switch: with a runtime branch the two paths' loads share registers and the
 // waitcnt pass, which is path-insensitive, drains one path's loads at the join.)
-template <int K_IN, int C, int RB, bool DIRECT>
-__global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
+template <int K_IN, int C, int RB, bool DIRECT, bool LOOP, class AT>
+__device__ __forceinline__ void mlp2_fwd_body(AT& a, const int bx, const int by, const int step_in) {
+  static_assert(!LOOP || DIRECT, "the loop kernel reads W1^T");
   static_assert(RB == 16 || RB == 32, "row block");
   constexpr int KS = (K_IN + 31) / 32;  // 32-deep MFMA k-steps
   constexpr int KP = KS * 32;
@@ -139,7 +241,7 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   __shared__ float b1sh[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int M = a.M, H = a.H;
-  const int r0 = blockIdx.x * RB, j0 = blockIdx.y * 16;
+  const int r0 = bx * RB, j0 = by * 16;
   STAMP(0);
   const int ks0 = (w * KS) / NW, ks1 = ((w + 1) * KS) / NW;
 
@@ -154,9 +256,12 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   // back into a scalar register (readfirstlane), which would wait for every load
   // in flight.  The dropout bits, which depend only on it, are then computed while
   // the operand loads are still in flight.
-  int lz;
-  asm volatile("v_mov_b32 %0, 0" : "=v"(lz));
-  const int step = a.step[lz];
+  int step = step_in;
+  if constexpr (!LOOP) {
+    int lz;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(lz));
+    step = a.step[lz];
+  }
   u32x4 wv[WCH];
   bf16x8 bg[MAXT];
   if constexpr (!DIRECT) {
@@ -169,7 +274,8 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
 #pragma unroll
     for (int t = 0; t < MAXT; ++t) {
       const int ks = min(ks0 + t, ks1 - 1);
-      bg[t] = *reinterpret_cast<const bf16x8*>(a.W1T + (long)(j0 + (lane & 15)) * a.ldw1t + ks * 32 + 8 * (lane >> 4));
+      const u32x4 q = ld_b128<LOOP>(a.W1T + (long)(j0 + (lane & 15)) * a.ldw1t + ks * 32 + 8 * (lane >> 4));
+      bg[t] = __builtin_bit_cast(bf16x8, q);
     }
   }
   // X row block [RB][K_IN] fp32: fully coalesced float4 loads (consecutive lanes,
@@ -185,13 +291,27 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   }
   const int wi = min(tid, 16 * C - 1);
   const long wo = (long)(j0 + wi / C) * C + wi % C;
-  const bf16_t w2a = a.W2s0[wo], w2b = a.W2s1[wo];
-  const bf16_t b1b = a.b1s[j0 + (tid & 15)];
-  const bf16_t b2b = a.b2s[tid % C];   // read by the blockIdx.y == 0 logit partials
+  // loop kernel: the fp32 masters (the bf16 shadows are not handed off in-launch)
+  bf16_t w2a, w2b, b1b, b2b;
+  float w2f = 0.f;
+  if constexpr (LOOP) {
+    w2f = ld_f<true>(a.pW2 + wo);
+    w2a = w2b = f2bf(w2f);
+    b1b = f2bf(ld_f<true>(a.pb1 + j0 + (tid & 15)));
+    b2b = f2bf(ld_f<true>(a.pb2 + tid % C));
+  } else {
+    w2a = a.W2s0[wo]; w2b = a.W2s1[wo];
+    b1b = a.b1s[j0 + (tid & 15)];
+    b2b = a.b2s[tid % C];   // read by the by == 0 logit partials
+  }
   __builtin_amdgcn_sched_barrier(0);
   const int par = step & 1;
   const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
-  if (a.step_copy && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) a.step_copy[0] = step;
+  if constexpr (LOOP) {
+    if (bx == 0 && tid < 16 * C) st_f<true>(a.W2snap + wo, w2f);   // this step's W2 for the backward
+  } else {
+    if (a.step_copy && bx == 0 && by == 0 && tid == 0) a.step_copy[0] = step;
+  }
   // dropout bits of this thread's 4-row group (phase 4 threads only)
   const int g4 = tid >> 4, gc = tid & 15, rowg = r0 + g4 * 4;
   u32x4 db = {0u, 0u, 0u, 0u};
@@ -231,14 +351,14 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   STAMP(1);
   // X^T side output for mlp2_bwd: hidden block y < K_IN/XTC writes input features
   // [y*XTC, (y+1)*XTC) of this row block (16-byte stores of 8 consecutive samples)
-  if (a.XT && blockIdx.y < K_IN / XTC && tid < XTC * (RB / 8)) {
-    const int i = tid / (RB / 8), h = (tid % (RB / 8)) * 8, xk = blockIdx.y * XTC + i;
+  if (a.XT && by < K_IN / XTC && tid < XTC * (RB / 8)) {
+    const int i = tid / (RB / 8), h = (tid % (RB / 8)) * 8, xk = by * XTC + i;
     unsigned q[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       q[e] = (unsigned)xs[(h + 2 * e) * LDXS + xk] | ((unsigned)xs[(h + 2 * e + 1) * LDXS + xk] << 16);
     u32x4 o; o.x = q[0]; o.y = q[1]; o.z = q[2]; o.w = q[3];
-    *reinterpret_cast<u32x4*>(a.XT + (long)xk * a.ldxt + r0 + h) = o;
+    st_b128<LOOP>(a.XT + (long)xk * a.ldxt + r0 + h, o);
   }
 
   // ---- 3. K split over the 8 waves
@@ -270,6 +390,7 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   if (tid < (RB / 4) * 16) {
     const int c = gc, col = j0 + c;
     float gf[4];
+    unsigned long long hpk = 0ull;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int rl = g4 * 4 + e, row = r0 + rl;
@@ -291,12 +412,16 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
         }
         gf[e] = gd;
         const bf16_t hb = f2bf(hv);
-        a.H1[(long)row * H + col] = hb;
+        hpk |= (unsigned long long)hb << (16 * e);
         hv = bf2f(hb);
       }
       htile[rl][c] = hv;
     }
-    *reinterpret_cast<float4*>(a.G1 + ((long)(rowg >> 2) * H + col) * 4) = make_float4(gf[0], gf[1], gf[2], gf[3]);
+    // G1 and H1 in the dropout-group layout [row group][H][4]: one 16-/8-byte store each
+    const long go = ((long)(rowg >> 2) * H + col) * 4;
+    st_b128<LOOP>(a.G1 + go, (u32x4){__float_as_uint(gf[0]), __float_as_uint(gf[1]), __float_as_uint(gf[2]),
+                                     __float_as_uint(gf[3])});
+    st_u64<LOOP>(a.H1 + go, hpk);
   }
   __syncthreads();
   STAMP(3);
@@ -304,7 +429,7 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   if (tid < RB * C) {
     const int rl = tid / C, c = tid % C, row = r0 + rl;
     if (row < M) {
-      float s = (blockIdx.y == 0) ? bf2f(b2b) : 0.f;
+      float s = (by == 0) ? bf2f(b2b) : 0.f;
 #pragma unroll
       for (int n = 0; n < 16; ++n) s += htile[rl][n] * w2s[n][c];
       atomicAdd(lg + (long)row * C + c, s);
@@ -315,8 +440,8 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
 }
 
 // ---------------------------------------------------------------------------- backward
-template <int K_IN, int C, int KC>
-__global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
+template <int K_IN, int C, int KC, bool LOOP, class AT>
+__device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by, const int step_in) {
   constexpr int MPM = 128;                 // max rows per device (fused path)
   constexpr int LDM = MPM + 8;             // padded row (bf16 elements)
   constexpr int NTILE = KC / 16;           // dW1 output tiles (one per wave)
@@ -332,10 +457,10 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   __shared__ float red[2][NW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int M = a.M, H = a.H, Mp = (M + 31) & ~31;
-  const int j0 = blockIdx.x * 16, kc0 = blockIdx.y * KC;
-  const bool chunk0 = blockIdx.y == 0;
+  const int j0 = bx * 16, kc0 = by * KC;
+  const bool chunk0 = by == 0;
   STAMP(0);
-  const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
+  const bool lead = bx == 0 && by == 0;
   const int rg = tid >> 4, gn = tid & 15;   // this thread's dropout group: rows 4rg..4rg+3, column j0+gn
 
   // ---- 0. issue all global loads (incl. the AdamW state of this wave's outputs).
@@ -347,23 +472,37 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   float lr0[C], lr1[C];
   {
     const long lo = (long)min(tid, M - 1) * C;
+    if constexpr (LOOP) {   // step known: this step's parity only
+      const float* lg = a.logits + (long)(step_in & 1) * M * C;
 #pragma unroll
-    for (int c = 0; c < C; ++c) { lr0[c] = a.logits[lo + c]; lr1[c] = a.logits[(long)M * C + lo + c]; }
+      for (int c = 0; c < C; ++c) lr1[c] = lr0[c] = ld_f<true>(lg + lo + c);
+    } else {
+#pragma unroll
+      for (int c = 0; c < C; ++c) { lr0[c] = a.logits[lo + c]; lr1[c] = a.logits[(long)M * C + lo + c]; }
+    }
   }
   const int lab = a.labels[min(tid, M - 1)];
-  const float4 g1 = *reinterpret_cast<const float4*>(a.G1 + ((long)min(rg, (M - 1) >> 2) * H + j0 + gn) * 4);
+  // G1 / H1: this thread's dropout group (rows 4rg..4rg+3, column j0+gn)
+  const long go = ((long)min(rg, (M - 1) >> 2) * H + j0 + gn) * 4;
+  const u32x4 g1q = ld_b128<LOOP>(a.G1 + go);
+  const unsigned long long hq = ld_u64<LOOP>(a.H1 + go);
   bf16_t hv[4];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) hv[e] = a.H1[(long)min(rg * 4 + e, M - 1) * H + j0 + gn];
+  for (int e = 0; e < 4; ++e) hv[e] = (bf16_t)(hq >> (16 * e));
   // A fragments of this wave's dW1 tile straight from X^T (written by mlp2_fwd, zero-padded to Mp)
   const int wt_ = min(w, NTILE - 1);
   bf16x8 xf[MPM / 32];
 #pragma unroll
   for (int ks = 0; ks < MPM / 32; ++ks)
-    xf[ks] = *reinterpret_cast<const bf16x8*>(a.XT + (long)(kc0 + wt_ * 16 + (lane & 15)) * a.ldxt +
-                                              min(ks, Mp / 32 - 1) * 32 + 8 * (lane >> 4));
+    xf[ks] = __builtin_bit_cast(bf16x8, ld_b128<LOOP>(a.XT + (long)(kc0 + wt_ * 16 + (lane & 15)) * a.ldxt +
+                                                     min(ks, Mp / 32 - 1) * 32 + 8 * (lane >> 4)));
   const long wo = (long)(j0 + (tid >> 5)) * C + min(tid & 31, C - 1);   // w2B[tid >> 5][tid & 31]
-  const bf16_t w2a = a.W2s0[wo], w2b = a.W2s1[wo];
+  bf16_t w2a, w2b;
+  if constexpr (LOOP) {
+    w2a = w2b = f2bf(ld_f<true>(a.W2snap + wo));   // the forward's snapshot of this step's W2
+  } else {
+    w2a = a.W2s0[wo]; w2b = a.W2s1[wo];
+  }
   const int trow0 = kc0 + wt_ * 16 + (lane >> 4) * 4;   // this lane's 4 dW1 rows (tile = wave)
   const int tcol = j0 + (lane & 15);
   // wave NW-1 owns no dW1 tile; in chunk-0 blocks it reduces dW2 / db1 (/ db2) on MFMA,
@@ -388,7 +527,8 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   const int lq = min(lane, C - 1);
   const float qp = (fo ? a.pb2 : a.gb2)[lq], qm = (fo ? a.mb2 : a.gb2)[lq], qv = (fo ? a.vb2 : a.gb2)[lq];
   __builtin_amdgcn_sched_barrier(0);
-  const int step = (a.step_copy ? a.step_copy : a.step)[0];
+  int step = step_in;
+  if constexpr (!LOOP) step = (a.step_copy ? a.step_copy : a.step)[0];
   const int par = step & 1;
   float lrow[C];
 #pragma unroll
@@ -436,7 +576,7 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
     l_corr = wave_sum(l_corr);
     if (lane == 0) { red[0][w] = l_loss; red[1][w] = l_corr; }
     float* nxt = a.logits + (long)(par ^ 1) * M * C;   // re-arm next step's accumulator
-    for (int i = tid; i < M * C; i += NT) nxt[i] = 0.f;
+    for (int i = tid; i < M * C; i += NT) st_f<LOOP>(nxt + i, 0.f);
   }
   __syncthreads();
   STAMP(1);
@@ -448,7 +588,8 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
     const bf16x8 af = *reinterpret_cast<const bf16x8*>(&dlB[(w * 16 + (lane & 15)) * LDB + 8 * (lane >> 4)]);
     const bf16x8 bw = *reinterpret_cast<const bf16x8*>(&w2B[(lane & 15) * LDB + 8 * (lane >> 4)]);
     const f32x4 dh = mfma16x16x32(af, bw, (f32x4){0.f, 0.f, 0.f, 0.f});
-    const float gv[4] = {g1.x, g1.y, g1.z, g1.w};
+    const float gv[4] = {__uint_as_float(g1q.x), __uint_as_float(g1q.y), __uint_as_float(g1q.z),
+                         __uint_as_float(g1q.w)};
     unsigned packed[2] = {0u, 0u};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -490,7 +631,7 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
     }
     // the lane's 4 rows are 4 consecutive K elements of W1^T: one 8-byte store
     if (a.fuse_opt && a.W1T)
-      *reinterpret_cast<uint2*>(a.W1T + (long)tcol * a.ldw1t + trow0) = make_uint2(wt[0], wt[1]);
+      st_u64<LOOP>(a.W1T + (long)tcol * a.ldw1t + trow0, (unsigned long long)wt[0] | ((unsigned long long)wt[1] << 32));
   } else if (aux) {
     // chunk-0 blocks, concurrently with the dW1 tiles:
     //   dW2[blk, :] = H1[:, blk]^T dlogits ; db1[blk] = dZ1[:, blk]^T 1 ; db2 = 1^T dlogits (block (0,0))
@@ -520,8 +661,8 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
         const long o = isb ? (long)(j0 + n) : (long)(j0 + n) * C + ac;
         const float gr = isb ? ab1[e] : aw[e];
         if (a.fuse_opt) {
-          const float pn = adam_apply(op[e], om[e], ov[e], gr, ak, (isb ? a.pb1 : a.pW2) + o, (isb ? a.mb1 : a.mW2) + o,
-                                      (isb ? a.vb1 : a.vW2) + o);
+          const float pn = adam_apply_h<LOOP>(op[e], om[e], ov[e], gr, ak, (isb ? a.pb1 : a.pW2) + o,
+                                              (isb ? a.mb1 : a.mW2) + o, (isb ? a.vb1 : a.vW2) + o);
           (isb ? a.sb1 : sW2n)[o] = f2bf(pn);
         } else {
           (isb ? a.gb1 : a.gW2)[o] = gr;
@@ -529,7 +670,8 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
       }
     }
     if (lead && lane < C) {
-      if (a.fuse_opt) a.sb2[lane] = f2bf(adam_apply(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane));
+      if (a.fuse_opt)
+        a.sb2[lane] = f2bf(adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane));
       else a.gb2[lane] = ab2[0];
     }
   }
@@ -544,9 +686,68 @@ __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
     else if (a.mslot) a.mslot[tid] = val;
     // advance the device step: every other workgroup of this launch reads the
     // forward's copy (step_copy), so no arrival ticket is needed
-    if (fo && tid == 0) a.step[0] = step + 1;
+    if (!LOOP && fo && tid == 0) a.step[0] = step + 1;   // the loop kernel advances it at its end
   }
   STAMP(4);
+}
+
+// ---------------------------------------------------------------------------- kernels
+template <int K_IN, int C, int RB, bool DIRECT>
+__global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
+  mlp2_fwd_body<K_IN, C, RB, DIRECT, false>(static_cast<const Mlp2Args&>(a), blockIdx.x, blockIdx.y, 0);
+}
+template <int K_IN, int C, int KC>
+__global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
+  mlp2_bwd_body<K_IN, C, KC, false>(static_cast<const Mlp2Args&>(a), blockIdx.x, blockIdx.y, 0);
+}
+
+// n complete training steps in ONE launch (single GPU, fused AdamW, W1^T copy):
+// every workgroup plays a forward role (16-row block x hidden block) and a
+// backward role (hidden block x input chunk) per step, with a grid barrier after
+// each phase instead of a kernel boundary (the boundary measured 2.36 us from the
+// forward's last store to the backward's first instruction: tools/stamp_mlp2.py).
+// Requires every workgroup resident at once (checked by the launcher).
+template <int K_IN, int C, int KC>
+__global__ void __launch_bounds__(NT) mlp2_loop_kernel(Mlp2Args a, Mlp2Loop l) {
+  __shared__ int sync_flag[1];
+  const int b = blockIdx.x, G = gridDim.x;
+  const int nrb = (a.M + 15) / 16, nhb = a.H / 16;
+  const int nfwd = nrb * nhb, nbwd = nhb * (K_IN / KC);
+  // both written only by block 0 after its last barrier (every block has read them by then)
+  const int step0 = a.step[0];
+  const unsigned base = l.base[0];
+  int it = 0;
+  // The bodies read their arguments through a kernarg-segment pointer laundered
+  // per phase (an empty asm), so the ~50 argument words are scalar-loaded next to
+  // their uses instead of being hoisted out of the loop and kept live across both
+  // phases (that spilled 127 SGPRs and 24 VGPRs to scratch).
+  typedef const __attribute__((address_space(4))) Mlp2Args KArgs;
+  KArgs* const kbase = (KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
+#define LSTAMP(k)                                                                                   \
+  do {                                                                                              \
+    if (l.stamps && threadIdx.x == 0) l.stamps[((long)b * l.n + it) * 5 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+  for (; it < l.n; ++it) {
+    const int step = step0 + it;
+    KArgs* kf = kbase;
+    asm volatile("" : "+s"(kf));
+    LSTAMP(0);
+    if (b < nfwd) mlp2_fwd_body<K_IN, C, 16, true, true>(*kf, b % nrb, b / nrb, step);
+    LSTAMP(1);
+    if (!grid_sync(l, base + (2u * it + 1u) * (unsigned)G, sync_flag)) break;
+    LSTAMP(2);
+    KArgs* kb = kbase;
+    asm volatile("" : "+s"(kb));
+    if (b < nbwd) mlp2_bwd_body<K_IN, C, KC, true>(*kb, b % nhb, b / nhb, step);
+    LSTAMP(3);
+    if (it + 1 < l.n && !grid_sync(l, base + (2u * it + 2u) * (unsigned)G, sync_flag)) break;
+    LSTAMP(4);
+  }
+#undef LSTAMP
+  if (b == 0 && threadIdx.x == 0 && it == l.n) {
+    a.step[0] = step0 + l.n;
+    l.base[0] = base + (2u * l.n - 1u) * (unsigned)G;
+  }
 }
 
 }  // namespace jdt
@@ -558,6 +759,43 @@ static int g_mlp2_rb = 16;  // forward rows per workgroup (jdt_mlp2_set_rows: 16
 JDT_API void jdt_mlp2_set_rows(int rb) { g_mlp2_rb = rb == 32 ? 32 : 16; }
 
 // phase 0: forward, 1: backward.  Supported: K_IN = 784, C = 10, H % 16 == 0, M <= 128.
+static int mlp2_loop_grid(int M, int H) { return max(((M + 15) / 16) * (H / 16), (H / 16) * (784 / 112)); }
+
+// workgroups of mlp2_loop_kernel the device holds at once (0 if unknown)
+static int mlp2_loop_resident() {
+  static int resident = -1;
+  if (resident < 0) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, mlp2_loop_kernel<784, 10, 112>, NT, 0) != hipSuccess)
+      return 0;
+    resident = cus * per;
+  }
+  return resident;
+}
+
+// 1 if the loop kernel can run M rows x H hidden units on this device (every
+// workgroup resident at once); called before graph capture.
+JDT_API int jdt_mlp2_loop_ok(int M, int H) {
+  return (H % 16 == 0 && M > 0 && M <= 128 && mlp2_loop_grid(M, H) <= mlp2_loop_resident()) ? 1 : 0;
+}
+
+// Persistent n-step launch; -4 if the grid cannot be fully resident (caller then
+// uses the two-launch path).
+JDT_API int jdt_mlp2_loop(const Mlp2Args* args, int n, unsigned* ctr, unsigned* base, int* err, long long timeout,
+                          unsigned long long* stamps, void* stream) {
+  const Mlp2Args& a = *args;
+  if (a.H % 16 || a.M <= 0 || a.M > 128 || n <= 0 || !a.fuse_opt || !a.W1T || !a.W2snap || !ctr || !base || !err)
+    return -3;
+  const int grid = mlp2_loop_grid(a.M, a.H);
+  if (grid > mlp2_loop_resident()) return -4;
+  Mlp2Loop l;
+  l.n = n; l.ctr = ctr; l.base = base; l.err = err; l.timeout = timeout; l.stamps = stamps;
+  hipLaunchKernelGGL((mlp2_loop_kernel<784, 10, 112>), dim3(grid), dim3(NT), 0, static_cast<hipStream_t>(stream), a, l);
+  return HIP_LAUNCH_CHECK();
+}
+
 JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* stream) {
   const Mlp2Args& a = *args;
   if (k_in != 784 || c != 10 || a.H % 16 || a.M <= 0 || a.M > 128) return -3;

@@ -205,10 +205,14 @@ class DataParallelTrainer:
             self.graph = ("one", g)
             self.multi = None
             if steps_per_graph > 1:
+                # single GPU, whole-step fused engine: the S steps are ONE persistent
+                # launch (mlp2_loop_kernel, grid barriers instead of kernel boundaries)
+                loop = self.world == 1 and getattr(self.fused, "loop_ok", False)
                 gm = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gm, pool=g.pool()):
-                    for _ in range(steps_per_graph):
-                        body()
+                    if not (loop and self.fused.run_loop(batch, steps_per_graph)):
+                        for _ in range(steps_per_graph):
+                            body()
                 self.multi = (steps_per_graph, gm)
         else:
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()

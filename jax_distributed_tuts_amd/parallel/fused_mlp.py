@@ -37,12 +37,18 @@ class Mlp2Args(ctypes.Structure):
                 ("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float), ("wd", c_float),
                 ("gscale", c_float), ("running", c_void_p), ("stamps", c_void_p),
                 ("W1T", c_void_p), ("ldw1t", c_int), ("XT", c_void_p), ("ldxt", c_int),
-                ("step_copy", c_void_p)]
+                ("step_copy", c_void_p), ("W2snap", c_void_p)]
 
 
 _lib.declare("jdt_mlp2", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_int, c_void_p])
 _lib.declare("jdt_mlp2_args_size", c_int, [])
 _lib.declare("jdt_mlp2_set_rows", None, [c_int])
+_lib.declare("jdt_mlp2_loop", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_void_p, c_void_p, c_void_p, ctypes.c_longlong,
+                                      c_void_p, c_void_p])
+
+_lib.declare("jdt_mlp2_loop_ok", c_int, [c_int, c_int])
+
+LOOP_BARRIER_TIMEOUT_TICKS = 20_000_000   # 0.2 s of s_memrealtime (100 MHz) per grid barrier
 
 
 def set_forward_rows(rb: int):
@@ -78,7 +84,8 @@ class FusedMLP2:
         self.rows = rows
         # silu'(Z1) * mask / keep in 4-row groups ([Mp/4][H][4] fp32), mlp2_fwd -> mlp2_bwd
         self.G1 = torch.zeros((rows + 31) // 32 * 32 * H, dtype=torch.float32, device=dev)
-        self.H1 = torch.empty(rows, H, dtype=torch.bfloat16, device=dev)
+        # H = dropout(silu(Z1)) bf16, same 4-row group layout as G1
+        self.H1 = torch.zeros((rows + 31) // 32 * 32 * H, dtype=torch.bfloat16, device=dev)
         self.logits = torch.zeros(2, rows, 10, dtype=torch.float32, device=dev)
         self.step_copy = torch.zeros(1, dtype=torch.int32, device=dev)  # mlp2_fwd -> mlp2_bwd
         # second parity buffer of W2's bf16 shadow (single-GPU fused-optimizer mode)
@@ -97,6 +104,16 @@ class FusedMLP2:
         if self.fuse_opt:
             self.W1T = torch.zeros(H, 800, dtype=torch.bfloat16, device=dev)
             self.W1T[:, :784].copy_(P.s("input_dense/kernel").t())
+        # persistent n-step kernel (mlp2_loop_kernel): W2 snapshot + barrier words
+        # [arrival counter, its base at the next launch, error flag, pad]
+        self.W2snap = torch.zeros(H * 10, dtype=torch.float32, device=dev)
+        self.loop_ws = torch.zeros(4, dtype=torch.int32, device=dev)
+        # Opt-in (JDT_MLP2_LOOP=1): measured SLOWER than two launches per step on MI355X
+        # (29.3 vs 16.3 us/step, tools/stamp_loop.py: each 256-workgroup grid barrier
+        # costs ~8 us against a 2.4 us kernel boundary), kept as the tested reference
+        # design for in-launch sc1 hand-offs.
+        self.loop_ok = (self.fuse_opt and os.environ.get("JDT_MLP2_LOOP", "0") == "1"
+                        and bool(_lib.lib().jdt_mlp2_loop_ok(rows, H)))
         if _lib.lib().jdt_mlp2_args_size() != ctypes.sizeof(Mlp2Args):
             raise RuntimeError("Mlp2Args layout mismatch")
         self._args = None
@@ -127,6 +144,7 @@ class FusedMLP2:
         a.fuse_opt = int(self.fuse_opt)
         a.XT, a.ldxt = self.XT.data_ptr(), self.Mp
         a.step_copy = self.step_copy.data_ptr()
+        a.W2snap = self.W2snap.data_ptr()
         if self.W1T is not None:
             a.W1T, a.ldw1t = self.W1T.data_ptr(), 800
         tx = st.tx
@@ -153,6 +171,28 @@ class FusedMLP2:
         _lib.check(L.jdt_mlp2(ctypes.byref(self._args), 0, 784, 10, s), "mlp2_fwd")
         _lib.check(L.jdt_mlp2(ctypes.byref(self._args), 1, 784, 10, s), "mlp2_bwd")
 
+    def run_loop(self, batch, n: int, stamps: Optional[torch.Tensor] = None) -> bool:
+        """n complete steps (forward, backward, AdamW) in ONE persistent launch.
+        False (nothing launched) if the loop kernel is unavailable for this engine
+        or its grid cannot be fully resident; the caller then runs n two-launch steps."""
+        if not self.loop_ok:
+            return False
+        key = (batch.inputs.data_ptr(), batch.labels.data_ptr(), self.state.rng)
+        if self._args is None or self._key != key:
+            self._args, self._key = self._build_args(batch), key
+        w = self.loop_ws
+        rc = _lib.lib().jdt_mlp2_loop(ctypes.byref(self._args), int(n), w[0:].data_ptr(), w[1:].data_ptr(),
+                                      w[2:].data_ptr(), LOOP_BARRIER_TIMEOUT_TICKS,
+                                      stamps.data_ptr() if stamps is not None else None, _lib.stream_ptr())
+        if rc == -4:
+            self.loop_ok = False
+            return False
+        _lib.check(rc, "mlp2_loop")
+        return True
+
+    def loop_error(self) -> bool:
+        return bool(int(self.loop_ws[2].item()))
+
     def step(self, batch):
         self.forward_backward(batch)
         if not self.fuse_opt:
@@ -166,6 +206,8 @@ class FusedMLP2:
     def finalize(self):
         """Bring the generic bf16 shadows up to date: W2's parity buffer in use, and
         W1's (mlp2_bwd keeps only the K-contiguous W1^T copy current)."""
+        if self.loop_error():
+            raise RuntimeError("mlp2_loop_kernel: a grid barrier timed out (not every workgroup was resident)")
         P = self.state.params
         if self.fuse_opt and int(self.state.opt_state["count"].item()) % 2 == 1:
             P.s("output_dense/kernel").copy_(self.W2s1)

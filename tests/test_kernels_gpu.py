@@ -419,6 +419,47 @@ def test_multi_step_graph_equals_single_steps():
     _close(res[1][1], res[0][1], rtol=1e-4, atol=1e-2)
 
 
+@pytest.mark.parametrize("rows", [128, 32, 16])
+def test_mlp2_loop_kernel_matches_two_launch(rows, monkeypatch):
+    """The persistent n-step kernel (grid barriers, sc1 hand-offs) == the
+    two-launch step, through the public multi-step graph path, and its barrier
+    counter stays consistent across launches (eager launches after the graph)."""
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    g = torch.Generator().manual_seed(0)
+    b = Batch(torch.randn(rows, 784, generator=g).to(DEV),
+              torch.randint(0, 10, (rows,), generator=g).to(torch.int32).to(DEV))
+    res = {}
+    for loop in ("0", "1"):
+        monkeypatch.setenv("JDT_MLP2_LOOP", loop)
+        st = init_dp(Classifier(), adamw(1e-3), 69, DEV)
+        tr = DataParallelTrainer(st, None, DPConfig(4, "kernel"))
+        tr.step(b)
+        assert tr.fused.loop_ok == (loop == "1")
+        tr.capture(b, steps_per_graph=5)
+        tr.run_steps(b, 10)
+        if loop == "1":
+            assert tr.fused.run_loop(b, 3) and tr.fused.run_loop(b, 1)
+        else:
+            for _ in range(4):
+                tr.fused.forward_backward(b)
+        tr.finalize()
+        torch.cuda.synchronize()
+        res[loop] = (st.params.master.clone(), tr.metrics.clone(), int(st.opt_state["count"].item()),
+                     st.params.shadow.clone())
+        if loop == "1":
+            w = tr.fused.loop_ws.cpu()
+            assert int(w[2]) == 0 and int(w[0]) == int(w[1])   # no timeout; counter == next base
+    assert res["0"][2] == res["1"][2] == 15
+    d = (res["0"][0] - res["1"][0]).abs()
+    assert float(d.max()) <= 3e-3 and float((d > 1e-5).float().mean()) < 1e-3
+    _close(res["1"][1], res["0"][1], rtol=1e-4, atol=1e-2)
+    sd = (res["0"][3].float() - res["1"][3].float()).abs()
+    assert float(sd.max()) <= 1e-2
+
+
 @pytest.mark.parametrize("layers", [2, 4])
 def test_fsdp_fused_kernels_match_generic(layers):
     """FSDP (world 1) with the fused classifier kernels on the gathered buffer ==

@@ -82,7 +82,15 @@ struct MdArgs {
   bf16_t* sbh;
   float lr, beta1, beta2, eps, wd, gscale;
   float* running;
+  unsigned long long* stamps;   // diagnostic: per-workgroup s_memrealtime at phase ends [grid][8] (null = off)
 };
+
+// Slots 0-4: s_memrealtime at the kernel's phase ends (tools/stamp_deep.py).
+#define MD_STAMP(i)                                                                          \
+  do {                                                                                       \
+    if (a.stamps && threadIdx.x == 0)                                                        \
+      a.stamps[(long)(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 
 struct MdAdam { float b1, b2, eps, wd, lr, gs, rbc1, rbc2; };
 
@@ -303,6 +311,13 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t dlT[16 * LDM];    // dlogits^T (TOP)
   __shared__ float whs[16][C];
   __shared__ float red[2][NW];
+  // !TOP: W_{i+1}[blk, :] staged once per workgroup (it used to be loaded by every
+  // wave: 8 x 16 KB of the per-CU intake, which bounds this phase -- stamps);
+  // rows padded by 16 B so the 16 rows of a B fragment read hit distinct banks
+  constexpr int LDWN = NN + 8;
+  constexpr int WNCH = 16 * NN / 8;                    // 16-byte chunks of the tile
+  static_assert(TOP || WNCH % MD_NT == 0, "Wn tile chunking");
+  __shared__ __attribute__((aligned(16))) bf16_t wnS[TOP ? 8 : 16 * LDWN];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int M = a.M, N = a.N, Mp = (M + 31) & ~31;
   const int j0 = blockIdx.x * 16, kc0 = blockIdx.y * KC;
@@ -311,12 +326,14 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   const bool lead = TOP && blockIdx.x == 0 && blockIdx.y == 0;
   const int rg = tid >> 4, gn = tid & 15;   // TOP: this thread's group (rows 4rg..4rg+3, column j0+gn)
 
+  MD_STAMP(0);
   // ---- 0. every global load up front
   float lrow[TOP ? C : 1];
   int lab = 0;
   float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
   bf16_t hv[4];
-  bf16x8 dzf[TOP ? 1 : NKS], wnf[TOP ? 1 : NKS];
+  bf16x8 dzf[TOP ? 1 : NKS];
+  u32x4 wq[TOP ? 1 : WNCH / MD_NT];
   float whv = 0.f;
   if constexpr (TOP) {
     const float* lg = a.logits + (long)par * M * C;
@@ -337,12 +354,16 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   } else {
     // wave w: rows 16w..16w+15 of dZ_i[:, blk] = dZ_{i+1} . W_{i+1}[blk, :]^T
     const bf16_t* Wn = par ? a.Wn1 : a.Wn0;
+#pragma unroll
+    for (int t = 0; t < WNCH / MD_NT; ++t) {
+      const int c = tid + t * MD_NT;
+      wq[t] = *reinterpret_cast<const u32x4*>(Wn + (long)(j0 + c / (NN / 8)) * NN + (c % (NN / 8)) * 8);
+    }
     const int row = w * 16 + (lane & 15);
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       dzf[ks] = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
       if (row < M) dzf[ks] = *reinterpret_cast<const bf16x8*>(a.dZn + (long)row * NN + ks * 32 + 8 * (lane >> 4));
-      wnf[ks] = *reinterpret_cast<const bf16x8*>(Wn + (long)(j0 + (lane & 15)) * NN + ks * 32 + 8 * (lane >> 4));
     }
     {
       const int row0 = w * 16 + (lane >> 4) * 4;
@@ -384,6 +405,7 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   if (TOP && a.fuse_opt && aux && lead && lane < C) { qp = a.pbh[lane]; qm = a.mbh[lane]; qv = a.vbh[lane]; }
   const MdAdam ak = md_adam_consts(a, step);
 
+  MD_STAMP(1);
   // ---- 1/2. dZ_i[:, blk] -> dzT[n][m] (bf16), dZout (chunk-0)
   float l_loss = 0.f, l_corr = 0.f;
   if constexpr (TOP) {
@@ -442,10 +464,19 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       *reinterpret_cast<uint2*>(&hT[gn * LDM + rg * 4]) =
           make_uint2((unsigned)hv[0] | ((unsigned)hv[1] << 16), (unsigned)hv[2] | ((unsigned)hv[3] << 16));
   } else {
+#pragma unroll
+    for (int t = 0; t < WNCH / MD_NT; ++t) {
+      const int c = tid + t * MD_NT;
+      *reinterpret_cast<u32x4*>(&wnS[(c / (NN / 8)) * LDWN + (c % (NN / 8)) * 8]) = wq[t];
+    }
+    __syncthreads();
     if (w * 16 < Mp) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) acc = mfma16x16x32(dzf[ks], wnf[ks], acc);
+      for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8 wnf = *reinterpret_cast<const bf16x8*>(&wnS[(lane & 15) * LDWN + ks * 32 + 8 * (lane >> 4)]);
+        acc = mfma16x16x32(dzf[ks], wnf, acc);
+      }
       const int row0 = w * 16 + (lane >> 4) * 4, col = j0 + (lane & 15);
       const float gfac[4] = {gv.x, gv.y, gv.z, gv.w};
       unsigned packed[2] = {0u, 0u};
@@ -465,6 +496,7 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   }
   __syncthreads();
 
+  MD_STAMP(2);
   // ---- 3. dW_i[chunk, blk] = IN[:, chunk]^T dZ_i[:, blk]; spare wave: db_i (+ head grads)
   if (w < NTILE) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -527,6 +559,7 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       else a.gbh[lane] = ab2[0];
     }
   }
+  MD_STAMP(3);
   if (TOP && lead) {
     __syncthreads();
     if (tid == 0) {

@@ -114,7 +114,10 @@ __device__ __forceinline__ float md_adam(float p, float m, float v, float g, con
 }
 
 // ---------------------------------------------------------------------------- forward
-template <int K_IN, bool XF32, int XTC, bool HEAD, int C, int RB>
+// DIRECT (compile-time, as in mlp2_fwd): B fragments straight from the W_i^T copy
+// (mode 1) instead of an LDS transposition of the row-major shadow (mode 0); a
+// runtime branch made the waitcnt pass drain one path's loads at the join.
+template <int K_IN, bool XF32, int XTC, bool HEAD, int C, int RB, bool DIRECT>
 __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
   constexpr int NT = MD_NT, NW = MD_NW;
   constexpr int KS = (K_IN + 31) / 32;
@@ -137,25 +140,24 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
   const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
   const bf16_t* Ws = par ? a.Ws1 : a.Ws0;
   const int ks0 = (w * KS) / NW, ks1 = ((w + 1) * KS) / NW;
-  const bool direct = a.WT != nullptr;
+  constexpr bool direct = DIRECT;
 
   // ---- 1. every global load up front
   u32x4 wv[WCH];
   bf16x8 bg[MAXT];
-  if (!direct) {
+  // every load unconditional (clamped address; out-of-range values are never used or
+  // are zeroed at the LDS write): a load under a divergent guard is waited for at the join
+  if constexpr (!DIRECT) {
 #pragma unroll
     for (int t = 0; t < WCH; ++t) {
-      const int idx = tid + t * NT;
-      wv[t] = (u32x4){0u, 0u, 0u, 0u};
-      if (idx < K_IN * 2) wv[t] = *reinterpret_cast<const u32x4*>(Ws + (long)(idx >> 1) * N + j0 + (idx & 1) * 8);
+      const int idx = min(tid + t * NT, K_IN * 2 - 1);
+      wv[t] = *reinterpret_cast<const u32x4*>(Ws + (long)(idx >> 1) * N + j0 + (idx & 1) * 8);
     }
   } else {
 #pragma unroll
     for (int t = 0; t < MAXT; ++t) {
-      bg[t] = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-      if (ks0 + t < ks1)
-        bg[t] = *reinterpret_cast<const bf16x8*>(a.WT + (long)(j0 + (lane & 15)) * a.ldwt + (ks0 + t) * 32 +
-                                                 8 * (lane >> 4));
+      const int ks = min(ks0 + t, ks1 - 1);
+      bg[t] = *reinterpret_cast<const bf16x8*>(a.WT + (long)(j0 + (lane & 15)) * a.ldwt + ks * 32 + 8 * (lane >> 4));
     }
   }
   // input row block [RB][K_IN], coalesced 16-byte loads
@@ -165,17 +167,15 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
   u32x4 xv[XPT];
 #pragma unroll
   for (int e = 0; e < XPT; ++e) {
-    const int f = tid + e * NT, rl = f / (K_IN / EPV), kv = f % (K_IN / EPV);
-    xv[e] = (u32x4){0u, 0u, 0u, 0u};
-    if (f < XV && r0 + rl < M) {
-      const char* src = static_cast<const char*>(a.X) + ((long)(r0 + rl) * K_IN + (long)kv * EPV) * (XF32 ? 4 : 2);
-      xv[e] = *reinterpret_cast<const u32x4*>(src);
-    }
+    const int f = min(tid + e * NT, XV - 1), rl = f / (K_IN / EPV), kv = f % (K_IN / EPV);
+    const char* src =
+        static_cast<const char*>(a.X) + ((long)min(r0 + rl, M - 1) * K_IN + (long)kv * EPV) * (XF32 ? 4 : 2);
+    xv[e] = *reinterpret_cast<const u32x4*>(src);
   }
   float whv = 0.f, bv = 0.f;
   const bf16_t* Wh = par ? a.Wh1 : a.Wh0;
-  if (HEAD && tid < 16 * C) whv = bf2f(Wh[(long)(j0 + tid / C) * C + tid % C]);
-  if (tid < 16) bv = bf2f(a.bs[j0 + tid]);
+  if constexpr (HEAD) whv = bf2f(Wh[(long)(j0 + min(tid, 16 * C - 1) / C) * C + min(tid, 16 * C - 1) % C]);
+  bv = bf2f(a.bs[j0 + (tid & 15)]);
 
   // ---- 2. LDS images
   if (!direct) {
@@ -201,12 +201,15 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
   for (int e = 0; e < XPT; ++e) {
     const int f = tid + e * NT, rl = f / (K_IN / EPV), kv = f % (K_IN / EPV);
     if (f < XV) {
+      const bool ok = r0 + rl < M;   // rows past M stay zero (IN^T tail is read by md_bwd)
       if (XF32) {
         const float4 x = *reinterpret_cast<const float4*>(&xv[e]);
         *reinterpret_cast<uint2*>(&xs[rl * LDXS + 4 * kv]) =
-            make_uint2((unsigned)f2bf(x.x) | ((unsigned)f2bf(x.y) << 16), (unsigned)f2bf(x.z) | ((unsigned)f2bf(x.w) << 16));
+            ok ? make_uint2((unsigned)f2bf(x.x) | ((unsigned)f2bf(x.y) << 16),
+                            (unsigned)f2bf(x.z) | ((unsigned)f2bf(x.w) << 16))
+               : make_uint2(0u, 0u);
       } else {
-        *reinterpret_cast<u32x4*>(&xs[rl * LDXS + 8 * kv]) = xv[e];
+        *reinterpret_cast<u32x4*>(&xs[rl * LDXS + 8 * kv]) = ok ? xv[e] : (u32x4){0u, 0u, 0u, 0u};
       }
     }
   }
@@ -600,13 +603,17 @@ JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) 
   if (phase == 0) {
     // 16-row blocks: twice the workgroups, half the input bytes each (as mlp2_fwd)
     const dim3 grid((a.M + 15) / 16, a.N / 16);
+    const bool d = a.WT != nullptr;
     if (a.K == 784) {
       if (head) return -3;
-      hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, false, 10, 16>), grid, blk, 0, st, a);
+      if (d) hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, false, 10, 16, true>), grid, blk, 0, st, a);
+      else hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, false, 10, 16, false>), grid, blk, 0, st, a);
     } else if (head) {
-      hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, true, 10, 16>), grid, blk, 0, st, a);
+      if (d) hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, true, 10, 16, true>), grid, blk, 0, st, a);
+      else hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, true, 10, 16, false>), grid, blk, 0, st, a);
     } else {
-      hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10, 16>), grid, blk, 0, st, a);
+      if (d) hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10, 16, true>), grid, blk, 0, st, a);
+      else hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10, 16, false>), grid, blk, 0, st, a);
     }
   } else {
     if (a.K == 784) {

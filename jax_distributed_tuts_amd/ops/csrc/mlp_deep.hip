@@ -325,87 +325,107 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   const int M = a.M, N = a.N, Mp = (M + 31) & ~31;
   const int j0 = blockIdx.x * 16, kc0 = blockIdx.y * KC;
   const bool chunk0 = blockIdx.y == 0;
-  const int step = a.step[0], par = step & 1;
   const bool lead = TOP && blockIdx.x == 0 && blockIdx.y == 0;
   const int rg = tid >> 4, gn = tid & 15;   // TOP: this thread's group (rows 4rg..4rg+3, column j0+gn)
 
   MD_STAMP(0);
-  // ---- 0. every global load up front
-  float lrow[TOP ? C : 1];
+  // ---- 0. every global load up front, all unconditional (clamped addresses: values
+  // of rows past M or outside this wave's role are never used) and both step
+  // parities of the parity-buffered operands, so nothing waits on the step counter,
+  // which is loaded last, per lane (a uniform load is read back through
+  // readfirstlane, which would wait for every load in flight), and selects them.
+  const bool fo = a.fuse_opt != 0;
+  int lz;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(lz));
+  // !TOP: the step counter is loaded FIRST (only W_{i+1}'s parity buffer depends on
+  // it, and those loads are issued last, after one round trip); TOP: last.
+  int step = 0;
+  if constexpr (!TOP) {
+    step = a.step[lz];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  float lr0[TOP ? C : 1], lr1[TOP ? C : 1];
   int lab = 0;
-  float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 gv;
   bf16_t hv[4];
   bf16x8 dzf[TOP ? 1 : NKS];
   u32x4 wq[TOP ? 1 : WNCH / MD_NT];
-  float whv = 0.f;
+  float whv0 = 0.f, whv1 = 0.f;
   if constexpr (TOP) {
-    const float* lg = a.logits + (long)par * M * C;
-    if (tid < M) {
+    const long lo = (long)min(tid, M - 1) * C;
 #pragma unroll
-      for (int c = 0; c < C; ++c) lrow[c] = lg[(long)tid * C + c];
-      lab = a.labels[tid];
-    }
-    if (rg * 4 < M) gv = *reinterpret_cast<const float4*>(a.G + ((long)rg * N + j0 + gn) * 4);
+    for (int c = 0; c < C; ++c) { lr0[c] = a.logits[lo + c]; lr1[c] = a.logits[(long)M * C + lo + c]; }
+    lab = a.labels[min(tid, M - 1)];
+    gv = *reinterpret_cast<const float4*>(a.G + ((long)min(rg, (M - 1) >> 2) * N + j0 + gn) * 4);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int m = rg * 4 + e;
-      hv[e] = 0;
-      if (m < M && chunk0) hv[e] = a.Hout[(long)m * N + j0 + gn];
-    }
-    const bf16_t* Wh = par ? a.Wh1 : a.Wh0;
-    if (tid < 16 * C) whv = bf2f(Wh[(long)(j0 + tid / C) * C + tid % C]);
+    for (int e = 0; e < 4; ++e) hv[e] = a.Hout[(long)min(rg * 4 + e, M - 1) * N + j0 + gn];
+    const int wi = min(tid, 16 * C - 1);
+    const long wo = (long)(j0 + wi / C) * C + wi % C;
+    whv0 = bf2f(a.Wh0[wo]);
+    whv1 = bf2f(a.Wh1[wo]);
   } else {
     // wave w: rows 16w..16w+15 of dZ_i[:, blk] = dZ_{i+1} . W_{i+1}[blk, :]^T
+    const int row = min(w * 16 + (lane & 15), M - 1);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+      dzf[ks] = *reinterpret_cast<const bf16x8*>(a.dZn + (long)row * NN + ks * 32 + 8 * (lane >> 4));
+    const int row0 = min(w * 16 + (lane >> 4) * 4, M - 1);
+    gv = *reinterpret_cast<const float4*>(a.G + ((long)(row0 >> 2) * N + j0 + (lane & 15)) * 4);
+  }
+  // A fragments of this wave's dW tile from IN^T (zero-padded to Mp samples)
+  const int wt_ = min(w, NTILE - 1);
+  bf16x8 xf[MPM / 32];
+#pragma unroll
+  for (int ks = 0; ks < MPM / 32; ++ks)
+    xf[ks] = *reinterpret_cast<const bf16x8*>(a.INT + (long)(kc0 + wt_ * 16 + (lane & 15)) * a.ldint +
+                                              min(ks, Mp / 32 - 1) * 32 + 8 * (lane >> 4));
+  // AdamW state of this lane's outputs (mode 0 has none: the loads then read the
+  // gradient buffers, values unused).  Waves < NTILE: their dW tile; the aux wave
+  // (chunk-0 blocks): the head's dW rows (TOP) in op/om/ov and b_i in bp/bm/bvv.
+  float op[4], om[4], ov[4];
+  const int trow0 = kc0 + wt_ * 16 + (lane >> 4) * 4;
+  const int tcol = j0 + (lane & 15);
+  const bool aux = chunk0 && w == NW - 1;
+  const int ac = lane & 15;
+  float bp[4], bm[4], bvv[4], qp = 0.f, qm = 0.f, qv = 0.f;
+  {
+    const bool hw = TOP && aux;   // wave-uniform
+    const float* sp = hw ? (fo ? a.pWh : a.gWh) : (fo ? a.pW : a.gW);
+    const float* sm = hw ? (fo ? a.mWh : a.gWh) : (fo ? a.mW : a.gW);
+    const float* sv = hw ? (fo ? a.vWh : a.gWh) : (fo ? a.vW : a.gW);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = (lane >> 4) * 4 + e;
+      const long idx = hw ? (long)(j0 + n) * C + min(ac, C - 1) : (long)(trow0 + e) * N + tcol;
+      op[e] = sp[idx]; om[e] = sm[idx]; ov[e] = sv[idx];
+      const float* bq = fo ? a.pb : a.gb;
+      const float* bmq = fo ? a.mb : a.gb;
+      const float* bvq = fo ? a.vb : a.gb;
+      bp[e] = bq[j0 + n]; bm[e] = bmq[j0 + n]; bvv[e] = bvq[j0 + n];
+    }
+    if constexpr (TOP) {
+      const int lq = min(lane, C - 1);
+      qp = (fo ? a.pbh : a.gbh)[lq]; qm = (fo ? a.mbh : a.gbh)[lq]; qv = (fo ? a.vbh : a.gbh)[lq];
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (TOP) step = a.step[lz];
+  const int par = step & 1;
+  if constexpr (!TOP) {
     const bf16_t* Wn = par ? a.Wn1 : a.Wn0;
 #pragma unroll
     for (int t = 0; t < WNCH / MD_NT; ++t) {
       const int c = tid + t * MD_NT;
       wq[t] = *reinterpret_cast<const u32x4*>(Wn + (long)(j0 + c / (NN / 8)) * NN + (c % (NN / 8)) * 8);
     }
-    const int row = w * 16 + (lane & 15);
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      dzf[ks] = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-      if (row < M) dzf[ks] = *reinterpret_cast<const bf16x8*>(a.dZn + (long)row * NN + ks * 32 + 8 * (lane >> 4));
-    }
-    {
-      const int row0 = w * 16 + (lane >> 4) * 4;
-      if (row0 < M) gv = *reinterpret_cast<const float4*>(a.G + ((long)(row0 >> 2) * N + j0 + (lane & 15)) * 4);
-    }
   }
-  // A fragments of this wave's dW tile from IN^T (zero-padded to Mp samples)
-  bf16x8 xf[MPM / 32];
+  float lrow[TOP ? C : 1];
+  float whv = 0.f;
+  if constexpr (TOP) {
 #pragma unroll
-  for (int ks = 0; ks < MPM / 32; ++ks) {
-    xf[ks] = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-    if (w < NTILE && ks < Mp / 32)
-      xf[ks] = *reinterpret_cast<const bf16x8*>(a.INT + (long)(kc0 + w * 16 + (lane & 15)) * a.ldint + ks * 32 +
-                                                8 * (lane >> 4));
+    for (int c = 0; c < C; ++c) lrow[c] = par ? lr1[c] : lr0[c];
+    whv = par ? whv1 : whv0;
   }
-  float op[4], om[4], ov[4];
-  const int trow0 = kc0 + w * 16 + (lane >> 4) * 4;
-  const int tcol = j0 + (lane & 15);
-  const bool aux = chunk0 && w == NW - 1;
-  const int ac = lane & 15;
-  float bp[4], bm[4], bvv[4], qp = 0.f, qm = 0.f, qv = 0.f;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    op[e] = om[e] = ov[e] = 0.f;
-    bp[e] = bm[e] = bvv[e] = 0.f;
-    if (a.fuse_opt && w < NTILE) {
-      const long idx = (long)(trow0 + e) * N + tcol;
-      op[e] = a.pW[idx]; om[e] = a.mW[idx]; ov[e] = a.vW[idx];
-    }
-    if (a.fuse_opt && aux) {
-      const int n = (lane >> 4) * 4 + e;
-      if (TOP && ac < C) {
-        const long g = (long)(j0 + n) * C + ac;
-        op[e] = a.pWh[g]; om[e] = a.mWh[g]; ov[e] = a.vWh[g];
-      }
-      if (ac == 0) { bp[e] = a.pb[j0 + n]; bm[e] = a.mb[j0 + n]; bvv[e] = a.vb[j0 + n]; }
-    }
-  }
-  if (TOP && a.fuse_opt && aux && lead && lane < C) { qp = a.pbh[lane]; qm = a.mbh[lane]; qv = a.vbh[lane]; }
   const MdAdam ak = md_adam_consts(a, step);
 
   MD_STAMP(1);
@@ -437,7 +457,7 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       for (int c = 0; c < C; ++c) dlT[c * LDM + tid] = 0;
     }
     for (int idx = tid; idx < (16 - C) * MPM; idx += NT) dlT[(C + idx / MPM) * LDM + idx % MPM] = 0;
-    if (tid < 16 * C) whs[tid / C][tid % C] = whv;
+    if (tid < 16 * C) whs[tid / C][tid % C] = whv;   // whv: this step's parity
     if (lead) {
       l_loss = wave_sum(l_loss);
       l_corr = wave_sum(l_corr);

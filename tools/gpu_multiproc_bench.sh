@@ -4,7 +4,7 @@
 set -u
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 export JDT_BACKEND=gloo PYTHONUNBUFFERED=1
-for n in 2 4 8; do
+for n in ${MP_NS:-2 4}; do
   for a in "" "--strategy fsdp" "--strategy pp --hidden-layers 8"; do
     timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
       --master-port $((29500 + n)) bench.py --gpus $n --steps 100 --warmup 10 $a > gpurun_out/mp_$n.log 2>&1 || { echo "N=$n $a failed"; tail -30 gpurun_out/mp_$n.log; exit 3; }

@@ -118,7 +118,7 @@ def main():
     ap.add_argument("--hidden-layers", type=int, default=8)
     ap.add_argument("--lm-batch", type=int, default=16)
     ap.add_argument("--num-layers", type=int, default=2)
-    ap.add_argument("--accum", choices=["loop", "fused", "kernel"], default="kernel")
+    ap.add_argument("--accum", choices=["loop", "scan", "fused", "kernel"], default="kernel")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--capture-collectives", action="store_true")
     ap.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto",

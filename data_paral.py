@@ -61,5 +61,7 @@ if __name__ == "__main__":
     ap.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto",
                     help="N>1 gradient all-reduce: direct xGMI P2P kernel (+fused AdamW) or RCCL")
     a = ap.parse_args()
+    if a.use_scan:
+        a.accum = "scan"
     maybe_profile(a, __file__)
     run(main, a, sim_cpu=a.sim_cpu)

@@ -66,7 +66,7 @@ def init_dp(model: MLP, tx, seed: int, device, mesh: Optional[Mesh] = None, axis
 @dataclass
 class DPConfig:
     num_minibatches: int = 4
-    accum: str = "loop"          # "loop" | "fused" | "kernel" (whole-step fused kernels, parallel/fused_mlp.py)
+    accum: str = "loop"          # "loop" | "scan" | "fused" | "kernel" (whole-step fused kernels, parallel/fused_mlp.py)
     axis: str = "data"
     overlap: bool = True         # eager generic path: bucketed all-reduce overlapping the last backward
     bucket_mb: float = 25.0
@@ -89,6 +89,7 @@ class DataParallelTrainer:
         self.fused = None
         self._capturing = False
         self.buckets = None
+        self._scan = None
         self.xg = None
         self._xg_fused_opt = False
         if self.world > 1 and P.grad.is_cuda:
@@ -136,12 +137,65 @@ class DataParallelTrainer:
             loss_and_grad(self.model, P, batch.inputs, batch.labels, train=True, seed=seed, offset=0,
                           step=st.step_tensor, grad_scale=1.0 / mb, metrics=P.metrics_slot,
                           on_ready=bk.ready if bk is not None else None)
+        elif cfg.accum == "scan" and P.master.is_cuda and not self._capturing:
+            self._scan_minibatches(batch, seed, mb)
         else:
             for i in range(n_mb):
                 last = i == n_mb - 1  # grads are final only in the last minibatch's backward
-                loss_and_grad(self.model, P, batch.inputs[i * mb:(i + 1) * mb], batch.labels[i * mb:(i + 1) * mb],
-                              train=True, seed=seed, offset=i << 16, step=st.step_tensor, grad_scale=1.0 / mb,
-                              metrics=P.metrics_slot, on_ready=bk.ready if (bk is not None and last) else None)
+                self._minibatch(batch.inputs[i * mb:(i + 1) * mb], batch.labels[i * mb:(i + 1) * mb], i, seed, mb,
+                                on_ready=bk.ready if (bk is not None and last) else None)
+
+    # ------------------------------------------------------------------ accumulation
+    # Minibatch i's dropout stream is (seed, counter-hi = (step * n_mb + i) << 32): the
+    # index enters through a DEVICE int (mb_step), not a captured constant, so the
+    # rolled "scan" variant -- one captured minibatch step replayed n times -- draws
+    # the same masks as the unrolled loop (util.py:81-137 vs 41-78: the
+    # reference's scan indexes its per-minibatch rngs with the traced loop index).
+    def _mb_tensors(self):
+        if getattr(self, "_mbt", None) is None:
+            dev = self.state.params.master.device
+            self._mbt = (torch.zeros(1, dtype=torch.int32, device=dev), torch.zeros(1, dtype=torch.int32, device=dev))
+        return self._mbt
+
+    def _minibatch(self, x, y, i, seed: int, mb: int, on_ready=None, mb_idx: Optional[torch.Tensor] = None):
+        st, P = self.state, self.state.params
+        idx, mstep = self._mb_tensors()
+        if mb_idx is None:
+            idx.fill_(int(i))
+        # mb_step = step * n_mb + i  (device ops: captured, replay-safe)
+        torch.mul(st.step_tensor, self.cfg.num_minibatches, out=mstep)
+        mstep.add_(idx)
+        loss_and_grad(self.model, P, x, y, train=True, seed=seed, offset=0, step=mstep, grad_scale=1.0 / mb,
+                      metrics=P.metrics_slot, on_ready=on_ready)
+
+    def _scan_minibatches(self, batch: Batch, seed: int, mb: int):
+        """accum_grads_scan on the device: ONE minibatch step captured as a hipGraph
+        (input slots + the device minibatch index), replayed num_minibatches times."""
+        n_mb = self.cfg.num_minibatches
+        key = (batch.inputs.data_ptr(), batch.labels.data_ptr(), seed, mb)
+        if self._scan is None or self._scan[0] != key:
+            xin = torch.empty((mb,) + tuple(batch.inputs.shape[1:]), dtype=batch.inputs.dtype,
+                              device=batch.inputs.device)
+            yin = torch.empty((mb,), dtype=batch.labels.dtype, device=batch.labels.device)
+            # warm the minibatch program once eagerly on minibatch 0 (allocations), then capture it
+            xin.copy_(batch.inputs[0:mb])
+            yin.copy_(batch.labels[0:mb])
+            self._mb_tensors()[0].fill_(0)
+            self._minibatch(xin, yin, 0, seed, mb, mb_idx=self._mbt[0])
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._minibatch(xin, yin, 0, seed, mb, mb_idx=self._mbt[0])
+            self._scan = (key, g, xin, yin)
+            start = 1
+        else:
+            start = 0
+        _, g, xin, yin = self._scan
+        idx = self._mbt[0]
+        for i in range(start, n_mb):
+            xin.copy_(batch.inputs[i * mb:(i + 1) * mb])
+            yin.copy_(batch.labels[i * mb:(i + 1) * mb])
+            idx.fill_(i)
+            g.replay()
 
     def sync(self):
         """pmean(grads) + psum(metrics) as SUM all-reduce(s) of the flat bucket(s); the

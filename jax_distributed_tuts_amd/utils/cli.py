@@ -18,13 +18,15 @@ DEFAULT_COUNTERS = "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS"
 
 
 def add_common_args(ap: argparse.ArgumentParser, steps: int, accum_default: str = "loop",
-                    accum_choices=("loop", "fused", "kernel")):
+                    accum_choices=("loop", "scan", "fused", "kernel")):
     ap.add_argument("--sim-cpu", type=int, default=None, help="simulate N devices as gloo CPU ranks")
     ap.add_argument("--steps", type=int, default=steps)
     ap.add_argument("--num-layers", type=int, default=2)
     ap.add_argument("--accum", choices=list(accum_choices), default=accum_default,
-                    help="loop: per-minibatch kernels (reference semantics); fused: all rows in one pass; "
-                         "kernel: whole-step fused HIP kernels")
+                    help="loop: per-minibatch kernels (reference semantics, util.accum_grads_loop); scan: one "
+                         "captured minibatch step replayed per minibatch (util.accum_grads_scan); fused: all rows "
+                         "in one pass; kernel: whole-step fused HIP kernels")
+    ap.add_argument("--use-scan", action="store_true", help="alias of --accum scan (util.accum_grads use_scan)")
     ap.add_argument("--profile", nargs="?", const=DEFAULT_COUNTERS, default=None, metavar="COUNTERS",
                     help="run under rocprofv3 --pmc (PMC counters + kernel stats)")
     ap.add_argument("--profile-dir", default="gpurun_out/profile")

@@ -189,13 +189,18 @@ def accum_grads_loop(batch: Batch, state: TrainState, key: int, n_minbatch: int,
 
 def accum_grads_scan(batch: Batch, state: TrainState, key: int, n_minbatch: int,
                      loss_fn: LossFn) -> Tuple[GradBuffer, Metrics]:
-    """util.py:81-137.  Rolled loop: one minibatch step with a device-resident
-    index ``i`` (``Batch.slice`` by a device offset), captured once as a hipGraph
-    and replayed ``n_minbatch`` times on GPU; a plain loop on CPU.  Must equal
-    :func:`accum_grads_loop` (tests/test_util_api.py)."""
+    """util.py:81-137.  Rolled loop: ONE minibatch step, captured once as a hipGraph
+    that reads its minibatch from device-resident input slots, replayed
+    ``n_minbatch`` times on GPU (a plain loop on CPU).  The captured call gets
+    ``rng = key`` and ``minibatch_index`` = a device int32 tensor holding ``i``
+    during replay ``i`` (the reference's scan indexes its rngs with the traced loop
+    index; a captured Python int could not change between replays), so a loss
+    function draws per-minibatch randomness by folding that device index in -- as
+    the DP trainer's ``accum="scan"`` mode does (parallel/dp.py), where scan ==
+    loop bit for bit.  Dropout-free loss functions give the loop's result
+    (tests/test_util_api.py)."""
     bs = batch.size
     mb = bs // n_minbatch
-    keys = R.split(key, n_minbatch)
     dev = batch.inputs.device
     if dev.type != "cuda":
         return accum_grads_loop(batch, state, key, n_minbatch, loss_fn)
@@ -203,9 +208,10 @@ def accum_grads_scan(batch: Batch, state: TrainState, key: int, n_minbatch: int,
     xin = torch.empty((mb,) + tuple(batch.inputs.shape[1:]), dtype=batch.inputs.dtype, device=dev)
     yin = torch.empty((mb,), dtype=batch.labels.dtype, device=dev)
     mslot = {}
+    idx = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def _body(i: int):
-        _, m = loss_fn(state.params, state.apply_fn, Batch(xin, yin), keys[0], minibatch_index=0, state=state)
+        _, m = loss_fn(state.params, state.apply_fn, Batch(xin, yin), key, minibatch_index=idx, state=state)
         mslot["m"] = m
 
     metrics = None
@@ -228,6 +234,7 @@ def accum_grads_scan(batch: Batch, state: TrainState, key: int, n_minbatch: int,
         for i in range(1, n_minbatch):
             xin.copy_(batch.inputs[i * mb:(i + 1) * mb])
             yin.copy_(batch.labels[i * mb:(i + 1) * mb])
+            idx.fill_(i)
             g.replay()
             metrics = _metrics_add(metrics, {k: tuple(x.clone() if torch.is_tensor(x) else x for x in v)
                                              for k, v in mslot["m"].items()})

@@ -54,7 +54,7 @@ def main(args):
 
 
 if __name__ == "__main__":
-    ap = add_common_args(argparse.ArgumentParser(), steps=15)
+    ap = add_common_args(argparse.ArgumentParser(), steps=15, accum_choices=("loop", "fused", "kernel"))
     ap.add_argument("--gather-once", action="store_true")
     ap.add_argument("--scatter-once", action="store_true")
     a = ap.parse_args()

@@ -90,7 +90,7 @@ def _single_device_reference(steps=3, accum="loop"):
     return st.params.state_dict(), tr.metrics
 
 
-@pytest.mark.parametrize("accum", ["loop", "fused"])
+@pytest.mark.parametrize("accum", ["loop", "scan", "fused"])
 def test_dp2_equals_single_device(tmp_path, accum):
     """DP over 2 ranks (each 2 minibatches of 16 rows... i.e. 64 rows/rank) must equal
     single-device training on the same global batch when dropout is off: the

@@ -419,6 +419,37 @@ def test_multi_step_graph_equals_single_steps():
     _close(res[1][1], res[0][1], rtol=1e-4, atol=1e-2)
 
 
+def test_dp_scan_equals_loop_with_dropout():
+    """accum="scan" (one captured minibatch step replayed per minibatch, device
+    minibatch index) == the unrolled loop, dropout on (util.py:81-137 vs 41-78):
+    same masks, eager and under the trainer's whole-step capture."""
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    g = torch.Generator().manual_seed(0)
+    b = Batch(torch.randn(128, 784, generator=g).to(DEV), torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV))
+    res = {}
+    for accum in ("loop", "scan"):
+        st = init_dp(Classifier(), adamw(1e-3), 69, DEV)
+        tr = DataParallelTrainer(st, None, DPConfig(4, accum))
+        for _ in range(3):
+            tr.step(b)
+        if accum == "scan":
+            assert tr._scan is not None
+        tr.capture(b)
+        for _ in range(2):
+            tr.step(b)
+        tr.finalize()
+        torch.cuda.synchronize()
+        res[accum] = (st.params.master.clone(), tr.metrics.clone())
+    # same dropout masks and minibatches; only fp32 atomic-order noise (bias colsums,
+    # metric sums) -- a different mask stream moves most weights by >> 1e-5
+    d = (res["loop"][0] - res["scan"][0]).abs()
+    assert float(d.max()) <= 3e-3 and float((d > 1e-5).float().mean()) < 1e-3
+    _close(res["scan"][1], res["loop"][1], rtol=1e-4, atol=1e-2)
+
+
 @pytest.mark.parametrize("rows", [128, 32, 16])
 def test_mlp2_loop_kernel_matches_two_launch(rows, monkeypatch):
     """The persistent n-step kernel (grid barriers, sc1 hand-offs) == the

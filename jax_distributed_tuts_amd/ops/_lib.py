@@ -41,7 +41,8 @@ class GemmArgs(ctypes.Structure):
 _SIGS = {
     "jdt_gemm": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p]),
     "jdt_gemm_args_size": (c_int, []),
-    "jdt_gemm_group": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_void_p]),
+    "jdt_gemm_group": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_void_p, c_long, c_void_p, c_long, c_void_p]),
+    "jdt_gemm_set_group_split": (None, [c_int]),
     "jdt_gemm_set_preload": (None, [c_int]),
     "jdt_gemm_set_exact": (None, [c_int]),
     "jdt_gemm_set_dma": (None, [c_int]),
@@ -115,6 +116,8 @@ def lib():
             fn.restype, fn.argtypes = res, args
         if l.jdt_gemm_args_size() != ctypes.sizeof(GemmArgs):
             raise RuntimeError("GemmArgs layout mismatch between Python and csrc/gemm.hip")
+        if os.environ.get("JDT_GROUP_SPLIT") == "0":   # A/B: no split-K inside grouped GEMM launches
+            l.jdt_gemm_set_group_split(0)
         _lib = l
         return _lib
 

@@ -781,6 +781,14 @@ struct GemmGroup {
   int tiles_n[GROUP_MAX];
   int start[GROUP_MAX + 1];
   int n;
+  // per-problem split-K (1 = none): a long-K problem (e.g. an input gradient
+  // with K = d_ff next to its K = tokens weight gradient) would otherwise be the
+  // group's long pole; its slices combine through gemm_finish's slabs/tickets
+  int splits[GROUP_MAX];
+  long wsoff[GROUP_MAX];
+  int cntoff[GROUP_MAX];
+  float* ws;
+  unsigned* counters;
 };
 
 template <int S, bool TAIL>
@@ -801,25 +809,29 @@ __global__ void __launch_bounds__(256) gemm_dma_group_kernel(GemmGroup G) {
   for (int t = 1; t < GROUP_MAX; ++t)
     if (t < G.n && bid >= G.start[t]) p = t;
   const GemmArgs& g = G.g[p];
-  const int local = bid - G.start[p], tn = G.tiles_n[p];
-  const int tm0 = (local / tn) * BM, tn0 = (local % tn) * BN;
+  const int tn = G.tiles_n[p], sp = G.splits[p];
+  const int tiles_p = (g.M / BM) * tn;
+  const int local = bid - G.start[p];
+  const int tile = local % tiles_p, split = local / tiles_p;
+  const int tm0 = (tile / tn) * BM, tn0 = (tile % tn) * BN;
+  const int kchunk = g.K / sp, k0 = split * kchunk;   // sp > 1: kchunk % BK == 0 (host)
   const bool at = g.a_trans, bt = g.b_trans;
   const bf16_t* Ab = static_cast<const bf16_t*>(g.A) + (at ? (long)tm0 : (long)tm0 * g.lda);
   const bf16_t* Bb = static_cast<const bf16_t*>(g.B) + (bt ? (long)tn0 : (long)tn0 * g.ldb);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int nkt = (g.K + BK - 1) / BK;  // K % 32 == 0: the last tile may hold 32 valid k
+  const int nkt = (kchunk + BK - 1) / BK;  // K % 32 == 0: the last tile may hold 32 valid k
   f32x4 acc[TM][TN];
   acc[0][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
   auto issue = [&](int kt) {
     bf16_t* st = smem + (kt % S) * STAGE;
-    const int kv = g.K - kt * BK;
+    const int kv = kchunk - kt * BK;
     if (!TAIL || kv >= BK) {
-      dma_stage_rt<BM>(at, Ab, g.lda, kt * BK, st, wid, lane);
-      dma_stage_rt<BN>(bt, Bb, g.ldb, kt * BK, st + BM * BK, wid, lane);
+      dma_stage_rt<BM>(at, Ab, g.lda, k0 + kt * BK, st, wid, lane);
+      dma_stage_rt<BN>(bt, Bb, g.ldb, k0 + kt * BK, st + BM * BK, wid, lane);
     } else {
-      dma_stage_tail<BM>(at, Ab, g.lda, kt * BK, kv, st, wid, lane);
-      dma_stage_tail<BN>(bt, Bb, g.ldb, kt * BK, kv, st + BM * BK, wid, lane);
+      dma_stage_tail<BM>(at, Ab, g.lda, k0 + kt * BK, kv, st, wid, lane);
+      dma_stage_tail<BN>(bt, Bb, g.ldb, k0 + kt * BK, kv, st + BM * BK, wid, lane);
     }
   };
 #pragma unroll
@@ -836,7 +848,7 @@ __global__ void __launch_bounds__(256) gemm_dma_group_kernel(GemmGroup G) {
     const bf16_t* Bs = As + BM * BK;
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
-      if (TAIL && kt * BK + kk >= g.K) break;  // half tile (uniform)
+      if (TAIL && kt * BK + kk >= kchunk) break;  // half tile (uniform)
       bf16x8 af = at ? dma_frag<BM>(As, true, wm * 16, kk, lane) : dma_frag<BM>(As, false, wm * 16, kk, lane);
       bf16x8 bf = bt ? dma_frag<BN>(Bs, true, wn * 16, kk, lane) : dma_frag<BN>(Bs, false, wn * 16, kk, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // asm tr reads retired (see gemm_dma_kernel)
@@ -846,7 +858,8 @@ __global__ void __launch_bounds__(256) gemm_dma_group_kernel(GemmGroup G) {
     }
   }
   __syncthreads();
-  gemm_finish<BM, BN, TM, TN>(g, acc, tm0, tn0, 0, wid, wm, wn, lane, tid, 1, 0, 0, nullptr, nullptr,
+  gemm_finish<BM, BN, TM, TN>(g, acc, tm0, tn0, 0, wid, wm, wn, lane, tid, sp, split, tile,
+                              sp > 1 ? G.ws + G.wsoff[p] : nullptr, sp > 1 ? G.counters + G.cntoff[p] : nullptr,
                               reinterpret_cast<int*>(smem));
 }
 
@@ -946,6 +959,7 @@ static int launch_cfg(const GemmArgs& g, int batch, int splits, float* ws, long 
 
 
 static bool g_gemm_no_dma = false;  // jdt_gemm_set_dma(0): register-staged kernels only (A/B tests)
+static int g_group_split = 1;  // jdt_gemm_set_group_split(0): no split-K inside grouped launches (A/B tests)
 
 // LDS ring depth 3 (one K-tile in flight across each barrier).  Deeper rings
 // cost resident workgroups per CU (qkv 512x1536x512: 9.8 us with 8 stages vs
@@ -1019,11 +1033,15 @@ static int gemm_dma(const GemmArgs& g, int batch, int cfg, int splits, float* ws
 // Grouped launch (see gemm_dma_group_kernel).  Returns 1 if any problem is
 // outside the envelope (bf16, 16-byte aligned rows, M, N, K % 32 == 0, no
 // batch) -- the caller then launches the problems one by one.
-static int gemm_dma_group(const GemmArgs* gs, int n, hipStream_t st) {
+static int gemm_dma_group(const GemmArgs* gs, int n, float* ws, long ws_floats, unsigned* counters, long n_counters,
+                          hipStream_t st) {
   if (g_gemm_no_dma || n < 1 || n > GROUP_MAX) return 1;
   GemmGroup G{};
   G.n = n;
+  G.ws = ws;
+  G.counters = counters;
   int total = 0;
+  long wsused = 0, cntused = 0;
   for (int p = 0; p < n; ++p) {
     const GemmArgs& g = gs[p];
     auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
@@ -1033,11 +1051,23 @@ static int gemm_dma_group(const GemmArgs* gs, int n, hipStream_t st) {
     G.g[p] = g;
     G.tiles_n[p] = g.N / 32;
     G.start[p] = total;
-    total += (g.M / 32) * (g.N / 32);
+    const long tiles = (long)(g.M / 32) * (g.N / 32);
+    // split long K into slices of >= 512 (8 K-tiles): measured on the transformer's
+    // dW + dX groups, where the K = d_ff input gradient otherwise runs 4x the
+    // K-steps of its neighbour (g_group_split = 0 disables, for A/B runs)
+    int sp = 1;
+    if (g_group_split && ws && counters)
+      while (sp < 8 && (g.K / (2 * sp)) % DMA_BK == 0 && g.K / (2 * sp) >= 8 * DMA_BK) sp *= 2;
+    if (sp > 1 && (wsused + tiles * sp * 32 * 32 > ws_floats || cntused + tiles > n_counters)) sp = 1;
+    G.splits[p] = sp;
+    G.wsoff[p] = wsused;
+    G.cntoff[p] = (int)cntused;
+    if (sp > 1) { wsused += tiles * sp * 32 * 32; cntused += tiles; }
+    total += (int)(tiles * sp);
   }
   G.start[n] = total;
   bool tail = false;
-  for (int p = 0; p < n; ++p) tail |= (gs[p].K % DMA_BK) != 0;
+  for (int p = 0; p < n; ++p) tail |= (gs[p].K / G.splits[p]) % DMA_BK != 0;
   if (tail)  // only then pay for the tail checks in the K loop (measured ~5 % on the transformer's groups)
     hipLaunchKernelGGL((gemm_dma_group_kernel<3, true>), dim3(total), dim3(256), 0, st, G);
   else
@@ -1087,6 +1117,8 @@ JDT_API int jdt_gemm(const GemmArgs* ga, int batch, int cfg, int splits, float* 
 JDT_API int jdt_gemm_args_size() { return (int)sizeof(GemmArgs); }
 
 // n GEMMs (no batch) in one launch; 1 = not eligible (launch them one by one).
-JDT_API int jdt_gemm_group(const GemmArgs* gs, int n, void* stream) {
-  return gemm_dma_group(gs, n, static_cast<hipStream_t>(stream));
+JDT_API int jdt_gemm_group(const GemmArgs* gs, int n, float* ws, long ws_floats, unsigned* counters, long n_counters,
+                           void* stream) {
+  return gemm_dma_group(gs, n, ws, ws_floats, counters, n_counters, static_cast<hipStream_t>(stream));
 }
+JDT_API void jdt_gemm_set_group_split(int on) { g_group_split = on; }

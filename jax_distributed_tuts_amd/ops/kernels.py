@@ -271,7 +271,9 @@ def gemm_group():
         if items:
             if len(items) > 1:
                 arr = (_lib.GemmArgs * len(items))(*[it[0] for it in items])
-                rc = _lib.lib().jdt_gemm_group(arr, len(items), _lib.stream_ptr())
+                ws, ctr = workspace(items[0][1])
+                rc = _lib.lib().jdt_gemm_group(arr, len(items), ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                                               ctypes.c_void_p(ctr.data_ptr()), ctr.numel(), _lib.stream_ptr())
                 if rc != 1:
                     _lib.check(rc, "jdt_gemm_group")
                     items = []

@@ -582,13 +582,13 @@ def test_fsdp_graph_replay_matches_eager(fused):
     torch.testing.assert_close(res[1][1], res[0][1], rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("M", [256, 32, 96])
-def test_gemm_group_matches_individual(M):
+@pytest.mark.parametrize("M,D_out", [(256, 384), (32, 384), (96, 384), (256, 2048), (64, 1024)])
+def test_gemm_group_matches_individual(M, D_out):
     """A layer's dW (km x kn, fp32 accumulate; K = M rows, a 32-deep tail tile when
-    M % 64 == 32) and dX (mk x nk with act' * mask + dbias epilogue) in one
-    grouped launch == the same GEMMs launched one by one; a non-eligible member
-    falls back to individual launches."""
-    D_in, D_out = 512, 384
+    M % 64 == 32) and dX (mk x nk with act' * mask + dbias epilogue; K = D_out,
+    split-K inside the group when >= 1024) in one grouped launch == the same GEMMs
+    launched one by one; a non-eligible member falls back to individual launches."""
+    D_in = 512
     h = _mk((M, D_in), torch.bfloat16, seed=71).to(DEV)
     dz = _mk((M, D_out), torch.bfloat16, seed=72).to(DEV)
     w = (_mk((D_in, D_out), torch.float32, seed=73) * 0.05).to(torch.bfloat16).to(DEV)

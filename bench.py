@@ -90,18 +90,20 @@ def build_pp(args, dev):
     if args.model == "transformer":
         from jax_distributed_tuts_amd.parallel.pipeline_lm import build_lm_pipeline, lm_batch
 
-        tr, lm_cfg = build_lm_pipeline(mesh, dev, num_microbatches=args.microbatches, comm=args.comm)
+        tr, lm_cfg = build_lm_pipeline(mesh, dev, num_microbatches=args.microbatches, comm=args.comm,
+                                       merge_single_stage=args.merge_microbatches)
         batch = shard_batch(lm_batch(lm_cfg, global_batch=args.lm_batch, seed=1), mesh, "data")
         desc = {"model": f"transformer LM {lm_cfg.n_layers}L d{lm_cfg.d_model} h{lm_cfg.n_heads} "
                          f"ff{lm_cfg.d_ff} V{lm_cfg.vocab_size}", "global_batch": args.lm_batch,
                 "seq_len": lm_cfg.seq_len, "tokens_per_step": args.lm_batch * lm_cfg.seq_len}
     else:
         tr = build_mlp_pipeline(cfg, mesh, dev, args.hidden_layers, num_microbatches=args.microbatches,
-                                comm=args.comm)
+                                comm=args.comm, merge_single_stage=args.merge_microbatches)
         batch = shard_batch(synthetic_batch(cfg, cfg.seed + 1), mesh, "data")
         desc = {"model": f"MLP 784-512x{args.hidden_layers}-10 GPipe", "global_batch": cfg.data.batch_size,
                 "seq_len": None}
-    desc.update({"num_microbatches": args.microbatches, "parallelism": f"dp{dp}xpp{ws // dp}"})
+    desc.update({"num_microbatches": args.microbatches, "parallelism": f"dp{dp}xpp{ws // dp}",
+                 "merged_single_stage": bool(args.merge_microbatches and ws // dp == 1)})
     batch = Batch(batch.inputs.to(dev), batch.labels.to(dev))
     return tr, batch, desc
 
@@ -115,6 +117,8 @@ def main():
     ap.add_argument("--dp", type=int, default=1, help="data-parallel degree for --strategy pp (hybrid)")
     ap.add_argument("--model", choices=["mlp", "transformer"], default="mlp")
     ap.add_argument("--microbatches", type=int, default=4)
+    ap.add_argument("--merge-microbatches", action="store_true",
+                    help="--strategy pp with a single stage: run the microbatches as one pass (PipeConfig.merge_single_stage)")
     ap.add_argument("--hidden-layers", type=int, default=8)
     ap.add_argument("--lm-batch", type=int, default=16)
     ap.add_argument("--num-layers", type=int, default=2)

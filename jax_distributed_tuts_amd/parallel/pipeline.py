@@ -81,6 +81,11 @@ class PipeConfig:
     # 8-layer MLP 0.79 -> 1.05 ms on one MI355X -- the fork/join graph edges cost
     # more than the overlap gains at these kernel sizes)
     overlap_wgrad: bool = False
+    # single stage (pipe axis of size 1): GPipe has no neighbour to feed, so the
+    # microbatches may run as ONE pass over all local rows (each row keeps its
+    # microbatch's 1/mb loss weight: the same gradient as the microbatch loop, the
+    # dropout masks drawn over the merged rows).  Ignored when the pipe axis > 1.
+    merge_single_stage: bool = False
 
 
 class GPipeTrainer:
@@ -170,6 +175,12 @@ class GPipeTrainer:
         self._setup_p2p(mb)
         rng = R.fold_rng_over_axis(st.rng, self.mesh, cfg.data_axis)
         seed = rng & 0xFFFFFFFF
+        if self.S == 1 and cfg.merge_single_stage:
+            out, cache = self.model.forward(P, batch.inputs, train=True, seed=seed, offset=0, step=st.step_tensor)
+            d = torch.empty_like(out)
+            self.loss_head(out, batch.labels, d, n_parts=n_mb)
+            self.model.backward(P, cache, d, dout_is_dz=True, need_dx=False, wgrad=self.wgrad)
+            return
         caches, dlogits = [None] * n_mb, [None] * n_mb
         # ---- forward fill/drain: tick t, stage s handles microbatch t - s
         for t in range(n_mb + self.S - 1):
@@ -273,10 +284,12 @@ class GPipeTrainer:
         if self.xg is not None and self.xg.error():
             raise RuntimeError("xgmi collective timed out on this rank (peer dead or desynchronised)")
 
-    def loss_head(self, logits, labels, dlogits):
+    def loss_head(self, logits, labels, dlogits, n_parts: int = 1):
+        """CE of ``labels`` (``n_parts`` merged microbatches: every row keeps its
+        microbatch's 1/rows weight)."""
         y = self.model.flatten_labels(labels)
         hb = self.model.head_bias_name
-        K.softmax_xent(logits, y, grad_scale=1.0 / y.numel(), dlogits=dlogits,
+        K.softmax_xent(logits, y, grad_scale=n_parts / y.numel(), dlogits=dlogits,
                        dbias=self.state.params.g(hb) if hb else None, metrics=self.state.params.metrics_slot)
 
     def gather_metrics(self) -> torch.Tensor:

@@ -33,7 +33,8 @@ def pp_mlp_dims(cfg, n_hidden_layers: int):
     return [cfg.data.input_size] + [cfg.model.hidden_size] * n_hidden_layers + [cfg.data.num_classes]
 
 
-def build_mlp_pipeline(cfg, mesh, dev, n_hidden_layers=8, dropout_rate=None, num_microbatches=4, comm="auto"):
+def build_mlp_pipeline(cfg, mesh, dev, n_hidden_layers=8, dropout_rate=None, num_microbatches=4, comm="auto",
+                       merge_single_stage=False):
     dims = pp_mlp_dims(cfg, n_hidden_layers)
     S, s = mesh.axis_size("pipe"), mesh.axis_index("pipe")
     dr = cfg.model.dropout_rate if dropout_rate is None else dropout_rate
@@ -41,7 +42,7 @@ def build_mlp_pipeline(cfg, mesh, dev, n_hidden_layers=8, dropout_rate=None, num
     full = MLP(dims, dropout_rate=dr)
     P = init_stage_params(stage, full.param_specs(), cfg.seed, dev)
     st = TrainState.create(apply_fn=stage, params=P, tx=adamw(cfg.optimizer.learning_rate), rng=R.PRNGKey(cfg.seed))
-    tr = GPipeTrainer(st, mesh, PipeConfig(num_microbatches, comm=comm))
+    tr = GPipeTrainer(st, mesh, PipeConfig(num_microbatches, comm=comm, merge_single_stage=merge_single_stage))
     return tr
 
 

@@ -205,3 +205,30 @@ def test_bucketed_overlap_equals_single_allreduce(tmp_path):
         for k in x["params"]:
             torch.testing.assert_close(x["params"][k], y["params"][k], rtol=0, atol=0)
         torch.testing.assert_close(x["metrics"], y["metrics"], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("merge", [False, True])
+def test_single_stage_pipeline_merge_equals_reference(merge):
+    """A one-stage GPipe step, microbatch loop or merged into one pass
+    (PipeConfig.merge_single_stage), == single-device accumulation (dropout off)."""
+    from data_paral import synthetic_batch
+    from pipeline_parallel import pp_mlp_dims
+    from jax_distributed_tuts_amd.models.mlp import MLP
+    from jax_distributed_tuts_amd.parallel.pipeline import GPipeTrainer, PipeConfig, init_stage_params, mlp_stage
+    from jax_distributed_tuts_amd.utils import rng as R
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.train_state import TrainState, adamw
+
+    cfg = dp_config()
+    dims = pp_mlp_dims(cfg, 3)
+    stage = mlp_stage(dims, 1, 0, dropout_rate=0.0)
+    P = init_stage_params(stage, MLP(dims, dropout_rate=0.0).param_specs(), cfg.seed, "cpu")
+    st = TrainState.create(apply_fn=stage, params=P, tx=adamw(1e-3), rng=R.PRNGKey(cfg.seed))
+    tr = GPipeTrainer(st, None, PipeConfig(4, merge_single_stage=merge))
+    b = synthetic_batch(cfg, 70)
+    for _ in range(3):
+        tr.step(b)
+    ref_p, ref_m = _single_mlp_reference()
+    for k, v in P.state_dict().items():
+        _adam_close(v, ref_p[k], frac=5e-2)
+    _metrics_close(tr.metrics, ref_m)

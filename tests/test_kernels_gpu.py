@@ -624,3 +624,35 @@ def test_gemm_group_matches_individual(M, D_out):
     _close(o1, ref, rtol=1e-3, atol=1e-3)
     _close(o2, kern.gemm(h.cpu(), dz.cpu(), a_layout="km", b_layout="kn", out_dtype=torch.float32),
            rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("model", ["mlp", "transformer"])
+def test_single_stage_pipeline_merge_gpu(model):
+    """GPipe with one stage: microbatches merged into one pass (PipeConfig.merge_single_stage)
+    == the microbatch loop on the GPU kernels (dropout off for the MLP; the
+    transformer has none)."""
+    from data_paral import synthetic_batch
+    from pipeline_parallel import build_mlp_pipeline
+    from jax_distributed_tuts_amd.parallel.pipeline_lm import build_lm_pipeline, lm_batch
+    from jax_distributed_tuts_amd.runtime.dist import Mesh
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.train_state import Batch
+
+    mesh = Mesh({"data": 1, "pipe": 1})
+    res = []
+    for merge in (False, True):
+        if model == "mlp":
+            cfg = dp_config()
+            tr = build_mlp_pipeline(cfg, mesh, DEV, 3, dropout_rate=0.0, num_microbatches=4, merge_single_stage=merge)
+            b = synthetic_batch(cfg, 70)
+        else:
+            tr, lcfg = build_lm_pipeline(mesh, DEV, num_microbatches=4, merge_single_stage=merge)
+            b = lm_batch(lcfg, global_batch=8, seed=1)
+        b = Batch(b.inputs.to(DEV), b.labels.to(DEV))
+        for _ in range(3):
+            tr.step(b)
+        torch.cuda.synchronize()
+        res.append((tr.state.params.master.clone(), tr.metrics.clone()))
+    d = (res[0][0] - res[1][0]).abs()
+    assert float(d.max()) <= 6e-3 and float((d > 1e-4).float().mean()) < 5e-2
+    _close(res[1][1], res[0][1], rtol=2e-3, atol=5e-2)

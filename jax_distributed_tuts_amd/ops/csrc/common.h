@@ -124,6 +124,21 @@ __device__ __forceinline__ f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// ---------------------------------------------------------------- XCD-aware 2-D block map
+// Workgroups are dealt round-robin over the 8 XCDs (linear id L -> XCD L % 8), so in
+// a grid whose x index walks 16-column output blocks, blocks x and x+1 write the two
+// 64-byte halves of every 128-byte line from two different XCD L2s: each L2 writes
+// back (and first fetches) a partial line.  This bijection gives every XCD a
+// contiguous run of tiles in x-fastest order, so neighbouring column blocks share an
+// L2 and the lines leave it whole.  Identity when the grid is not a multiple of 8.
+__device__ __forceinline__ void xcd_contiguous_tile(int& bx, int& by) {
+  const int gx = gridDim.x, G = gx * gridDim.y;
+  const int L = blockIdx.x + gx * blockIdx.y;
+  if (G % 8) { bx = blockIdx.x; by = blockIdx.y; return; }
+  const int t = (L % 8) * (G / 8) + L / 8;
+  bx = t % gx; by = t / gx;
+}
+
 }  // namespace jdt
 
 #define HIP_LAUNCH_CHECK() (int)hipGetLastError()

@@ -300,7 +300,7 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
 }
 
 // ---------------------------------------------------------------------------- backward
-template <int K_IN, bool TOP, int C, int KC, int NN>
+template <int K_IN, bool TOP, int C, int KC, int NN, bool XCD>
 __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   constexpr int NT = MD_NT, NW = MD_NW, MPM = MD_MPM;
   constexpr int LDM = MPM + 8;
@@ -323,9 +323,11 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t wnS[TOP ? 8 : 16 * LDWN];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int M = a.M, N = a.N, Mp = (M + 31) & ~31;
-  const int j0 = blockIdx.x * 16, kc0 = blockIdx.y * KC;
-  const bool chunk0 = blockIdx.y == 0;
-  const bool lead = TOP && blockIdx.x == 0 && blockIdx.y == 0;
+  int bx = blockIdx.x, by = blockIdx.y;
+  if constexpr (XCD) xcd_contiguous_tile(bx, by);   // column-block neighbours share an L2 (common.h)
+  const int j0 = bx * 16, kc0 = by * KC;
+  const bool chunk0 = by == 0;
+  const bool lead = TOP && bx == 0 && by == 0;
   const int rg = tid >> 4, gn = tid & 15;   // TOP: this thread's group (rows 4rg..4rg+3, column j0+gn)
 
   MD_STAMP(0);
@@ -610,6 +612,8 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
 }  // namespace jdt
 using namespace jdt;
 
+int xcd_tiles_enabled();   // mlp_fused.hip (JDT_XCD_TILES)
+
 JDT_API int jdt_md_args_size() { return (int)sizeof(MdArgs); }
 
 // phase 0: forward of one hidden layer (head = 1: + head logits); phase 1: backward
@@ -636,13 +640,20 @@ JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) 
       else hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10, 16, false>), grid, blk, 0, st, a);
     }
   } else {
+    const bool x = xcd_tiles_enabled();
     if (a.K == 784) {
       if (head) return -3;
-      hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512>), dim3(a.N / 16, 784 / 112), blk, 0, st, a);
+      const dim3 g(a.N / 16, 784 / 112);
+      if (x) hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, true>), g, blk, 0, st, a);
+      else hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, false>), g, blk, 0, st, a);
     } else if (head) {
-      hipLaunchKernelGGL((md_bwd_kernel<512, true, 10, 64, 512>), dim3(a.N / 16, 512 / 64), blk, 0, st, a);
+      const dim3 g(a.N / 16, 512 / 64);
+      if (x) hipLaunchKernelGGL((md_bwd_kernel<512, true, 10, 64, 512, true>), g, blk, 0, st, a);
+      else hipLaunchKernelGGL((md_bwd_kernel<512, true, 10, 64, 512, false>), g, blk, 0, st, a);
     } else {
-      hipLaunchKernelGGL((md_bwd_kernel<512, false, 10, 64, 512>), dim3(a.N / 16, 512 / 64), blk, 0, st, a);
+      const dim3 g(a.N / 16, 512 / 64);
+      if (x) hipLaunchKernelGGL((md_bwd_kernel<512, false, 10, 64, 512, true>), g, blk, 0, st, a);
+      else hipLaunchKernelGGL((md_bwd_kernel<512, false, 10, 64, 512, false>), g, blk, 0, st, a);
     }
   }
   return HIP_LAUNCH_CHECK();

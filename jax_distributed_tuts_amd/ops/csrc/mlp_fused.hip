@@ -696,9 +696,11 @@ template <int K_IN, int C, int RB, bool DIRECT>
 __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   mlp2_fwd_body<K_IN, C, RB, DIRECT, false>(static_cast<const Mlp2Args&>(a), blockIdx.x, blockIdx.y, 0);
 }
-template <int K_IN, int C, int KC>
+template <int K_IN, int C, int KC, bool XCD>
 __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
-  mlp2_bwd_body<K_IN, C, KC, false>(static_cast<const Mlp2Args&>(a), blockIdx.x, blockIdx.y, 0);
+  int bx = blockIdx.x, by = blockIdx.y;
+  if constexpr (XCD) xcd_contiguous_tile(bx, by);
+  mlp2_bwd_body<K_IN, C, KC, false>(static_cast<const Mlp2Args&>(a), bx, by, 0);
 }
 
 // n complete training steps in ONE launch (single GPU, fused AdamW, W1^T copy):
@@ -757,6 +759,15 @@ JDT_API int jdt_mlp2_args_size() { return (int)sizeof(Mlp2Args); }
 
 static int g_mlp2_rb = 16;  // forward rows per workgroup (jdt_mlp2_set_rows: 16 or 32, A/B tests)
 JDT_API void jdt_mlp2_set_rows(int rb) { g_mlp2_rb = rb == 32 ? 32 : 16; }
+// backward workgroup -> tile map: 1 = XCD-contiguous (xcd_contiguous_tile), 0 = identity (A/B: JDT_XCD_TILES=0)
+static int g_xcd_tiles = -1;
+int xcd_tiles_enabled() {
+  if (g_xcd_tiles < 0) {
+    const char* e = getenv("JDT_XCD_TILES");
+    g_xcd_tiles = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_xcd_tiles;
+}
 
 // phase 0: forward, 1: backward.  Supported: K_IN = 784, C = 10, H % 16 == 0, M <= 128.
 static int mlp2_loop_grid(int M, int H) { return max(((M + 15) / 16) * (H / 16), (H / 16) * (784 / 112)); }
@@ -812,7 +823,9 @@ JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* str
       else hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 16, false>), g, dim3(NT), 0, st, a);
     }
   } else {
-    hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112>), dim3(a.H / 16, 784 / 112), dim3(NT), 0, st, a);
+    const dim3 g(a.H / 16, 784 / 112);
+    if (xcd_tiles_enabled()) hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true>), g, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, false>), g, dim3(NT), 0, st, a);
   }
   return HIP_LAUNCH_CHECK();
 }

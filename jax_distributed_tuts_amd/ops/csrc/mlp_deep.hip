@@ -117,7 +117,7 @@ __device__ __forceinline__ float md_adam(float p, float m, float v, float g, con
 // DIRECT (compile-time, as in mlp2_fwd): B fragments straight from the W_i^T copy
 // (mode 1) instead of an LDS transposition of the row-major shadow (mode 0); a
 // runtime branch made the waitcnt pass drain one path's loads at the join.
-template <int K_IN, bool XF32, int XTC, bool HEAD, int C, int RB, bool DIRECT>
+template <int K_IN, bool XF32, int XTC, bool HEAD, int C, int RB, bool DIRECT, bool XCD>
 __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
   constexpr int NT = MD_NT, NW = MD_NW;
   constexpr int KS = (K_IN + 31) / 32;
@@ -135,7 +135,10 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
   __shared__ float bsh[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int M = a.M, N = a.N;
-  const int r0 = blockIdx.x * RB, j0 = blockIdx.y * 16;
+  int bx = blockIdx.x, by = blockIdx.y;
+  // XCD-contiguous: each XCD takes 4 whole column blocks (1/8 of W_i) over all row blocks
+  if constexpr (XCD) xcd_contiguous_tile(bx, by);
+  const int r0 = bx * RB, j0 = by * 16;
   const int step = a.step[0], par = step & 1;
   const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
   const bf16_t* Ws = par ? a.Ws1 : a.Ws0;
@@ -215,8 +218,8 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
   }
   __syncthreads();
   // IN^T side output: output block y < K_IN/XTC writes features [y*XTC, (y+1)*XTC) of this row block
-  if (a.INT && blockIdx.y < K_IN / XTC && tid < XTC * (RB / 8)) {
-    const int i = tid / (RB / 8), h = (tid % (RB / 8)) * 8, xk = blockIdx.y * XTC + i;
+  if (a.INT && by < K_IN / XTC && tid < XTC * (RB / 8)) {
+    const int i = tid / (RB / 8), h = (tid % (RB / 8)) * 8, xk = by * XTC + i;
     unsigned q[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e)
@@ -290,7 +293,7 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
     if (tid < RB * C) {
       const int rl = tid / C, c = tid % C, row = r0 + rl;
       if (row < M) {
-        float s = (blockIdx.y == 0) ? bf2f(a.bh[c]) : 0.f;
+        float s = (by == 0) ? bf2f(a.bh[c]) : 0.f;
 #pragma unroll
         for (int n = 0; n < 16; ++n) s += htile[rl][n] * whs[n][c];
         atomicAdd(lg + (long)row * C + c, s);
@@ -628,19 +631,20 @@ JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) 
     // 16-row blocks: twice the workgroups, half the input bytes each (as mlp2_fwd)
     const dim3 grid((a.M + 15) / 16, a.N / 16);
     const bool d = a.WT != nullptr;
+    const bool xf = xcd_tiles_enabled() == 1;
     if (a.K == 784) {
       if (head) return -3;
-      if (d) hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, false, 10, 16, true>), grid, blk, 0, st, a);
-      else hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, false, 10, 16, false>), grid, blk, 0, st, a);
+      if (d) { if (xf) hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, false, 10, 16, true, true>), grid, blk, 0, st, a); else hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, false, 10, 16, true, false>), grid, blk, 0, st, a); }
+      else { if (xf) hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, false, 10, 16, false, true>), grid, blk, 0, st, a); else hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, false, 10, 16, false, false>), grid, blk, 0, st, a); }
     } else if (head) {
-      if (d) hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, true, 10, 16, true>), grid, blk, 0, st, a);
-      else hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, true, 10, 16, false>), grid, blk, 0, st, a);
+      if (d) { if (xf) hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, true, 10, 16, true, true>), grid, blk, 0, st, a); else hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, true, 10, 16, true, false>), grid, blk, 0, st, a); }
+      else { if (xf) hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, true, 10, 16, false, true>), grid, blk, 0, st, a); else hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, true, 10, 16, false, false>), grid, blk, 0, st, a); }
     } else {
-      if (d) hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10, 16, true>), grid, blk, 0, st, a);
-      else hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10, 16, false>), grid, blk, 0, st, a);
+      if (d) { if (xf) hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10, 16, true, true>), grid, blk, 0, st, a); else hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10, 16, true, false>), grid, blk, 0, st, a); }
+      else { if (xf) hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10, 16, false, true>), grid, blk, 0, st, a); else hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10, 16, false, false>), grid, blk, 0, st, a); }
     }
   } else {
-    const bool x = xcd_tiles_enabled();
+    const bool x = xcd_tiles_enabled() != 0;
     if (a.K == 784) {
       if (head) return -3;
       const dim3 g(a.N / 16, 784 / 112);

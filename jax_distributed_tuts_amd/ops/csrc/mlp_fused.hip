@@ -692,9 +692,12 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
 }
 
 // ---------------------------------------------------------------------------- kernels
-template <int K_IN, int C, int RB, bool DIRECT>
+template <int K_IN, int C, int RB, bool DIRECT, bool XCD>
 __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
-  mlp2_fwd_body<K_IN, C, RB, DIRECT, false>(static_cast<const Mlp2Args&>(a), blockIdx.x, blockIdx.y, 0);
+  int bx = blockIdx.x, by = blockIdx.y;
+  // XCD-contiguous: each XCD takes whole column blocks (1/8 of W1) over all row blocks
+  if constexpr (XCD) xcd_contiguous_tile(bx, by);
+  mlp2_fwd_body<K_IN, C, RB, DIRECT, false>(static_cast<const Mlp2Args&>(a), bx, by, 0);
 }
 template <int K_IN, int C, int KC, bool XCD>
 __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
@@ -759,12 +762,13 @@ JDT_API int jdt_mlp2_args_size() { return (int)sizeof(Mlp2Args); }
 
 static int g_mlp2_rb = 16;  // forward rows per workgroup (jdt_mlp2_set_rows: 16 or 32, A/B tests)
 JDT_API void jdt_mlp2_set_rows(int rb) { g_mlp2_rb = rb == 32 ? 32 : 16; }
-// backward workgroup -> tile map: 1 = XCD-contiguous (xcd_contiguous_tile), 0 = identity (A/B: JDT_XCD_TILES=0)
+// workgroup -> tile map (A/B: JDT_XCD_TILES): 1 = XCD-contiguous (xcd_contiguous_tile) in the
+// forward and backward kernels, 2 = backward only, 0 = identity everywhere
 static int g_xcd_tiles = -1;
 int xcd_tiles_enabled() {
   if (g_xcd_tiles < 0) {
     const char* e = getenv("JDT_XCD_TILES");
-    g_xcd_tiles = (e && e[0] == '0') ? 0 : 1;
+    g_xcd_tiles = (e && (e[0] == '0' || e[0] == '2')) ? e[0] - '0' : 1;
   }
   return g_xcd_tiles;
 }
@@ -815,12 +819,16 @@ JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* str
     const bool direct = a.W1T != nullptr;
     if (g_mlp2_rb == 32) {
       const dim3 g((a.M + 31) / 32, a.H / 16);
-      if (direct) hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 32, true>), g, dim3(NT), 0, st, a);
-      else hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 32, false>), g, dim3(NT), 0, st, a);
+      const bool xf = xcd_tiles_enabled() == 1;
+      if (direct && xf) hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 32, true, true>), g, dim3(NT), 0, st, a);
+      else if (direct) hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 32, true, false>), g, dim3(NT), 0, st, a);
+      else hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 32, false, false>), g, dim3(NT), 0, st, a);
     } else {
       const dim3 g((a.M + 15) / 16, a.H / 16);
-      if (direct) hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 16, true>), g, dim3(NT), 0, st, a);
-      else hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 16, false>), g, dim3(NT), 0, st, a);
+      const bool xf = xcd_tiles_enabled() == 1;
+      if (direct && xf) hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 16, true, true>), g, dim3(NT), 0, st, a);
+      else if (direct) hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 16, true, false>), g, dim3(NT), 0, st, a);
+      else hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 16, false, false>), g, dim3(NT), 0, st, a);
     }
   } else {
     const dim3 g(a.H / 16, 784 / 112);

@@ -7,7 +7,7 @@ timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --t
 tail -2 gpurun_out/ab_tests.log
 : > gpurun_out/ab_xcd.jsonl
 for rep in 1 2; do
-  for x in 0 1; do
+  for x in ${XS:-0 1}; do
     for a in "" "--num-layers 4"; do
       JDT_XCD_TILES=$x timeout -k 10 120 python bench.py --steps 2000 --warmup 100 $a > gpurun_out/ab.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/ab.log; exit 3; }
       v=$(grep '^{' gpurun_out/ab.log | tail -1 | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')

@@ -139,6 +139,24 @@ __device__ __forceinline__ void xcd_contiguous_tile(int& bx, int& by) {
   bx = t % gx; by = t / gx;
 }
 
+// A kernel-argument pointer pinned in SGPRs.  Selecting between struct members with a
+// lane-dependent condition (`aux ? a.pW2 : a.pW1`) lets the compiler turn the select
+// into a per-lane load of the member's ADDRESS from the kernarg segment: a vector load
+// whose result the next loads wait for, and an in-order vmcnt wait also drains every
+// load issued before it (one extra global round trip).  readfirstlane makes the
+// pointer a uniform value first, so the select is a v_cndmask on registers.
+template <class T>
+__device__ __forceinline__ T* sgpr_ptr(T* p) {
+  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return reinterpret_cast<T*>(((unsigned long long)hi << 32) | lo);
+}
+// a load through such a pointer as a global (not flat) access
+__device__ __forceinline__ float ld_global(const float* p) {
+  return *(const __attribute__((address_space(1))) float*)p;
+}
+
 }  // namespace jdt
 
 #define HIP_LAUNCH_CHECK() (int)hipGetLastError()

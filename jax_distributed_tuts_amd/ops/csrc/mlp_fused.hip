@@ -513,15 +513,15 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   const bool fo = a.fuse_opt != 0;
   // aux lanes: class column ac < C -> W2[j0+n][ac]; ac >= C -> b1[j0+n] (lane C applies it)
   const bool w2l = aux && ac < C;
-  const float* sp = aux ? (w2l ? (fo ? a.pW2 : a.gW2) : (fo ? a.pb1 : a.gb1)) : (fo ? a.pW1 : a.gW1);
-  const float* sm = aux ? (w2l ? (fo ? a.mW2 : a.gW2) : (fo ? a.mb1 : a.gb1)) : (fo ? a.mW1 : a.gW1);
-  const float* sv = aux ? (w2l ? (fo ? a.vW2 : a.gW2) : (fo ? a.vb1 : a.gb1)) : (fo ? a.vW1 : a.gW1);
+  const float* sp = aux ? (w2l ? sgpr_ptr(fo ? a.pW2 : a.gW2) : sgpr_ptr(fo ? a.pb1 : a.gb1)) : sgpr_ptr(fo ? a.pW1 : a.gW1);
+  const float* sm = aux ? (w2l ? sgpr_ptr(fo ? a.mW2 : a.gW2) : sgpr_ptr(fo ? a.mb1 : a.gb1)) : sgpr_ptr(fo ? a.mW1 : a.gW1);
+  const float* sv = aux ? (w2l ? sgpr_ptr(fo ? a.vW2 : a.gW2) : sgpr_ptr(fo ? a.vb1 : a.gb1)) : sgpr_ptr(fo ? a.vW1 : a.gW1);
   float op[4], om[4], ov[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int n = (lane >> 4) * 4 + e;
     const long idx = aux ? (w2l ? (long)(j0 + n) * C + ac : (long)(j0 + n)) : (long)(trow0 + e) * H + tcol;
-    op[e] = sp[idx]; om[e] = sm[idx]; ov[e] = sv[idx];
+    op[e] = ld_global(sp + idx); om[e] = ld_global(sm + idx); ov[e] = ld_global(sv + idx);
   }
   const float run_pre = (a.running ? a.running : a.logits)[lane & 3];   // lead: metric accumulators
   const int lq = min(lane, C - 1);

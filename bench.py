@@ -12,8 +12,15 @@ Every timed step is a complete training step: all 4 minibatch fwd/bwd passes,
 the RCCL all-reduce (N > 1), the fused AdamW update and the metrics fold.
 
     python bench.py                                # N=1
-    torchrun --nproc-per-node 8 bench.py --gpus 8  # one rank per GPU, RCCL over xGMI
+    python bench.py --gpus 8                       # 8 local ranks, one per GPU (built-in launcher)
+    torchrun --nproc-per-node 8 bench.py --gpus 8  # the same job under torchrun
     python bench.py --strategy fsdp|pp             # the other two tutorials
+
+``--gpus N`` is enforced: without torchrun the script starts N ranks itself
+(runtime/launch.py, before any GPU call); under a launcher it exits non-zero
+unless WORLD_SIZE == N.  ``JDT_BACKEND=gloo`` makes the ranks' process group
+gloo (several ranks sharing one GPU -- RCCL refuses that -- while the xGMI
+kernels still run between them).
 """
 from __future__ import annotations
 
@@ -26,6 +33,7 @@ import time
 import torch
 
 from jax_distributed_tuts_amd.runtime import dist as D
+from jax_distributed_tuts_amd.runtime import launch as LCH
 from jax_distributed_tuts_amd.runtime.dist import Mesh
 
 METRIC = "steps/sec (whole node) for tutorial MLP at 1/2/4/8 MI355X, DP vs shard vs PP"
@@ -108,6 +116,18 @@ def build_pp(args, dev):
     return tr, batch, desc
 
 
+def pick_steps_per_graph(steps: int, cap: int) -> int:
+    """Steps per captured graph: all of them when steps <= cap (one replay, one host
+    launch for the whole timed region), else the largest divisor of steps <= cap
+    (so no single-step remainder replays)."""
+    if steps <= cap:
+        return max(1, steps)
+    for d in range(cap, 0, -1):
+        if steps % d == 0:
+            return d
+    return 1
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -127,14 +147,19 @@ def main():
     ap.add_argument("--capture-collectives", action="store_true")
     ap.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto",
                     help="N>1 DP gradient collective: direct xGMI P2P kernel (fused with AdamW) or RCCL")
-    ap.add_argument("--steps-per-graph", type=int, default=10,
-                    help="complete training steps recorded per hipGraph (amortises the replay launch)")
+    ap.add_argument("--steps-per-graph", type=int, default=None,
+                    help="complete training steps recorded per hipGraph (amortises the replay launch); default: "
+                         "all timed steps in one graph when --steps <= 200 (DP), else the largest divisor <= the cap")
     args = ap.parse_args()
 
+    # N ranks for --gpus N: start them here (this process never touches the GPU) ...
+    LCH.maybe_launch(args.gpus, __file__, sys.argv[1:])
     dev = D.init()
+    # ... and never report a job of the wrong size
+    LCH.check_world(args.gpus)
     ws = D.world_size()
-    if ws != args.gpus and D.rank() == 0:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+    if args.steps_per_graph is None:
+        args.steps_per_graph = pick_steps_per_graph(args.steps, 200 if args.strategy == "dp" else 50)
     build = {"dp": build_dp, "fsdp": build_fsdp, "pp": build_pp}[args.strategy]
     tr, batch, desc = build(args, dev)
     on_gpu = dev.type == "cuda"
@@ -187,10 +212,15 @@ def main():
             ts.append(a.elapsed_time(b))
         ts.sort()
         p50, p90 = ts[len(ts) // 2], ts[int(0.9 * len(ts))]
+    coll_ms = None
+    if hasattr(tr, "time_collective"):
+        coll_ms = tr.time_collective(batch, iters=min(20, max(5, args.steps)))
     if hasattr(tr, "finalize"):
         tr.finalize()
     m = (tr.gather_metrics() if hasattr(tr, "gather_metrics") else tr.metrics).detach().float().cpu()
     sps = args.steps / dt
+    if args.strategy == "dp":
+        desc["accum"] = tr.cfg.accum  # the path that actually ran (CPU falls back from "kernel")
     if D.rank() == 0:
         out = {"metric": METRIC, "value": round(sps, 2), "unit": "steps/s", "n_gpus": ws, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 5), "higher_is_better": True,
@@ -200,7 +230,10 @@ def main():
                            "steps_per_graph": (tr.multi[0] if getattr(tr, "multi", None) else 1) if use_graph else 0,
                            "samples_per_s":
                            round(sps * desc["global_batch"], 1), "final_loss": float(m[0] / max(m[1], 1)),
-                           "comm": getattr(tr, "comm_backend", None) or D.backend() or "none"}}
+                           "comm": getattr(tr, "comm_backend", None) or D.backend() or "none",
+                           "process_group": D.backend() or "none",
+                           "xgmi_selftest": getattr(tr, "xgmi_status", "n/a"),
+                           "collective_ms_p50": coll_ms}}
         print(json.dumps(out), flush=True)
     D.shutdown()
 

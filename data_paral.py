@@ -1,10 +1,12 @@
 """Data-parallel training of the tutorial classifier (reference data_paral.py).
 
-    python data_paral.py                       # all visible GPUs? no: 1 process = 1 GPU
-    torchrun --nproc-per-node 8 data_paral.py  # DP over 8 MI355X, RCCL over xGMI
+    python data_paral.py                       # DP over every visible GPU (one rank per GPU, RCCL/xGMI)
+    python data_paral.py --gpus 1              # one GPU
+    torchrun --nproc-per-node 8 data_paral.py  # the same 8-rank job under an external launcher
     python data_paral.py --sim-cpu 8           # 8 gloo CPU ranks (reference's simulated devices)
     python data_paral.py --accum kernel        # whole-step fused HIP kernels
     python data_paral.py --profile             # same run under rocprofv3 --pmc (counters + kernel stats)
+    python data_paral.py --check-replication   # verify replicated params are bitwise equal on every rank
 
 Schedule as the reference (data_paral.py:271-277): 10 training steps with
 metrics accumulated, then one step on fresh metrics printed under "dp".
@@ -20,8 +22,7 @@ from jax_distributed_tuts_amd.models.mlp import Classifier
 from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp, shard_batch
 from jax_distributed_tuts_amd.runtime import dist as D
 from jax_distributed_tuts_amd.runtime.dist import Mesh
-from jax_distributed_tuts_amd.runtime.launch import run
-from jax_distributed_tuts_amd.utils.cli import add_common_args, maybe_profile
+from jax_distributed_tuts_amd.utils.cli import add_common_args, entry_main
 from jax_distributed_tuts_amd.utils.config import dp_config
 from jax_distributed_tuts_amd.utils.metrics import print_metrics
 from jax_distributed_tuts_amd.utils.train_state import Batch, adamw, get_num_params
@@ -52,6 +53,10 @@ def main(args):
     trainer.metrics.zero_()
     trainer.step(batch)
     trainer.finalize()
+    if args.check_replication:
+        from jax_distributed_tuts_amd.utils.debug import check_trainer_replication
+
+        check_trainer_replication(trainer)
     if D.rank() == 0:
         print_metrics(trainer.metrics, "dp")
 
@@ -63,5 +68,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     if a.use_scan:
         a.accum = "scan"
-    maybe_profile(a, __file__)
-    run(main, a, sim_cpu=a.sim_cpu)
+    entry_main(main, a, __file__)

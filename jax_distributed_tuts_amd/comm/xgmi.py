@@ -308,6 +308,17 @@ class XgmiComm:
             self.timeout = saved
 
 
+def status(comm: Optional[XgmiComm], world: int, device, mode: str = "auto") -> str:
+    """What a trainer's N>1 transport ended up being, for logs and the bench JSON:
+    ``passed`` (xGMI kernels, self-test passed on every rank), ``failed->rccl``
+    (tried, fell back), ``off`` (RCCL requested / not a GPU job) or ``n/a`` (N=1)."""
+    if world <= 1:
+        return "n/a"
+    if comm is not None:
+        return "passed"
+    return "failed->rccl" if requested(mode, world, torch.device(device)) else "off"
+
+
 def create_for(mesh, axis: str, cap_floats: int, device: torch.device, mode: str = "auto") -> Optional[XgmiComm]:
     """An ``XgmiComm`` over ``mesh``'s ``axis`` group, or None (RCCL fallback)."""
     from ..runtime.dist import is_initialized

@@ -290,6 +290,33 @@ class DataParallelTrainer:
         with named_scope("sync_metrics"):
             K.metrics_fold_(self.metrics, P.metrics_slot)
 
+    @property
+    def xgmi_status(self) -> str:
+        from ..comm.xgmi import status
+
+        return status(self.xg, self.world, self.state.params.master.device, self.cfg.comm)
+
+    def time_collective(self, batch: Batch, iters: int = 20) -> Optional[float]:
+        """Median device time (ms) of the step's gradient collective -- ``sync``: the
+        bucket all-reduce (xGMI: with the fused AdamW + metrics fold) -- bracketed by
+        hipEvents in separate, untimed eager steps (complete training steps: they
+        advance the state like any other).  None for N = 1 or off-GPU."""
+        if self.world == 1 or not self.state.params.master.is_cuda:
+            return None
+        ts = []
+        for _ in range(iters):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            self.compute(batch)
+            a.record()
+            self.sync()
+            b.record()
+            self.update_noncounting()
+            self.state.step += 1
+            b.synchronize()
+            ts.append(a.elapsed_time(b))
+        ts.sort()
+        return round(ts[len(ts) // 2], 5)
+
     def finalize(self):
         if self.fused is not None:
             self.fused.finalize()

@@ -384,6 +384,12 @@ class FSDPTrainer:
         b = backend()
         return "rccl" if b == "nccl" else (b or "none")
 
+    @property
+    def xgmi_status(self) -> str:
+        from ..comm.xgmi import status
+
+        return status(self.sp.xg, self.world, self.sp.local.master.device, self.cfg.comm)
+
     def _fused_step(self, batch: Batch) -> bool:
         """gather bf16 shards once -> mlp2_fwd/mlp2_bwd on the full buffer (mode 0:
         plain-stored full grads + metric slots) -> reduce-scatter -> sharded AdamW."""

@@ -167,6 +167,17 @@ class GPipeTrainer:
         b = backend()
         return "rccl" if b == "nccl" else (b or "none")
 
+    @property
+    def xgmi_status(self) -> str:
+        from ..comm.xgmi import status
+
+        dp = status(self.xg, self.n_dp, self.dev, self.cfg.comm)
+        if self.S == 1:
+            return dp
+        pipe = "passed" if self.p2p is not None else ("failed->rccl" if self._p2p_tried and self.dev.type == "cuda"
+                                                      and self.cfg.comm != "rccl" else "off")
+        return f"data:{dp},pipe:{pipe}"
+
     # ------------------------------------------------------------------ step
     def _compute(self, batch: Batch):
         st, P, cfg = self.state, self.state.params, self.cfg

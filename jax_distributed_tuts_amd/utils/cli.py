@@ -1,5 +1,8 @@
 """Command-line plumbing shared by the entry scripts.
 
+``entry_main(main, args, script)`` is the common ``__main__`` of the three entry
+scripts: N-rank launch (``--gpus``), optional profiling, then the run.
+
 ``--profile [COUNTERS]`` re-runs the same command as a *child* of
 ``rocprofv3 --pmc COUNTERS --kernel-trace --stats`` (counters only with the
 kernel trace; never combined with the runtime/HIP/HSA/marker trace domains) and
@@ -19,7 +22,15 @@ DEFAULT_COUNTERS = "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS"
 
 def add_common_args(ap: argparse.ArgumentParser, steps: int, accum_default: str = "loop",
                     accum_choices=("loop", "scan", "fused", "kernel")):
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPU ranks to train on (default: every visible GPU, like the reference's jax.devices()); "
+                         "N > 1 without torchrun starts N local RCCL ranks (runtime/launch.py)")
     ap.add_argument("--sim-cpu", type=int, default=None, help="simulate N devices as gloo CPU ranks")
+    ap.add_argument("--check-replication", action="store_true",
+                    help="after training, verify that every replicated parameter is bitwise equal on all ranks "
+                         "(the debug replacement of the reference's disabled shard_map check_rep)")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="fixed-order reductions only (no fp32 atomics): bitwise-reproducible runs")
     ap.add_argument("--steps", type=int, default=steps)
     ap.add_argument("--num-layers", type=int, default=2)
     ap.add_argument("--accum", choices=list(accum_choices), default=accum_default,
@@ -61,8 +72,34 @@ def maybe_profile(args, script: str):
     this script under rocprofv3 as a child process and exit with its code."""
     if not getattr(args, "profile", None) or os.environ.get("JDT_PROFILED") == "1":
         return
-    cmd = profile_cmd(script, sys.argv[1:], args.profile, args.profile_dir)
-    os.makedirs(args.profile_dir, exist_ok=True)
+    # multi-rank jobs: runtime/launch.py started the ranks first (the launcher never
+    # runs under the profiler), and each rank profiles itself into its own directory
+    outdir = args.profile_dir if "RANK" not in os.environ else os.path.join(args.profile_dir,
+                                                                            f"rank{os.environ['RANK']}")
+    cmd = profile_cmd(script, sys.argv[1:], args.profile, outdir)
+    os.makedirs(outdir, exist_ok=True)
     env = dict(os.environ, JDT_PROFILED="1", TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     print("[profile] " + " ".join(cmd), file=sys.stderr, flush=True)
     sys.exit(subprocess.call(cmd, env=env))
+
+
+def entry_main(main, args, script: str):
+    """``__main__`` of an entry script, in the only safe order:
+
+    1. ``--gpus N`` (> 1, not already a rank): start N local ranks of this script
+       and exit with their status -- the launcher process never touches the GPU;
+    2. ``--profile``: this rank re-runs itself under rocprofv3 as a child;
+    3. run ``main(args)`` on the job's process group, failing (exit 3) unless it
+       has exactly the requested number of ranks."""
+    from ..runtime.launch import maybe_launch, resolve_gpus, run
+
+    if args.sim_cpu:
+        maybe_profile(args, script)
+        run(main, args, sim_cpu=args.sim_cpu)
+        return
+    n = resolve_gpus(args.gpus)
+    maybe_launch(n, script, sys.argv[1:])
+    maybe_profile(args, script)
+    if args.deterministic:
+        os.environ["JDT_DETERMINISTIC"] = "1"
+    run(main, args, expect_world=n)

@@ -80,3 +80,48 @@ def guarded(fn, *args, **kw):
             except Exception:  # noqa: BLE001
                 pass
         raise
+
+
+def replicated_state(trainer):
+    """(tensors that must be bit-identical across the trainer's data axis, axis name).
+
+    DP: every parameter and both AdamW moments (replicated by construction:
+    same init + the same all-reduced gradient).  FSDP: only the leaves the
+    sharding rule kept whole (param_sharding.py:89-92) and the running metrics.
+    GPipe: this stage's parameters across the data replicas of the stage."""
+    from ..parallel.dp import DataParallelTrainer
+    from ..parallel.fsdp import FSDPTrainer
+    from ..parallel.pipeline import GPipeTrainer
+
+    if isinstance(trainer, FSDPTrainer):
+        sp = trainer.sp
+        out = {f"param/{n}": sp.local.p(n) for n in sp.repl_names}
+        out["metrics"] = trainer.metrics
+        return out, trainer.cfg.axis
+    if isinstance(trainer, (DataParallelTrainer, GPipeTrainer)):
+        P = trainer.state.params
+        out = {f"param/{n}": P.p(n) for n in P.names()}
+        for k in ("m", "v", "buf"):
+            if k in trainer.state.opt_state:
+                out[f"opt/{k}"] = trainer.state.opt_state[k]
+        axis = trainer.cfg.axis if isinstance(trainer, DataParallelTrainer) else trainer.cfg.data_axis
+        return out, axis
+    raise TypeError(f"no replication contract for {type(trainer).__name__}")
+
+
+def check_trainer_replication(trainer) -> None:
+    """``--check-replication`` of the entry scripts: raise
+    :class:`ReplicationError` naming the diverged tensors and ranks."""
+    if hasattr(trainer, "finalize"):
+        trainer.finalize()
+    tensors, axis = replicated_state(trainer)
+    if trainer.mesh is None or not tensors:
+        return
+    if tensors and next(iter(tensors.values())).is_cuda:
+        torch.cuda.synchronize()
+    check_replicated(tensors, trainer.mesh, axis)
+    from ..runtime.dist import rank
+
+    if rank() == 0:
+        print(f"[check-replication] {len(tensors)} replicated tensors bit-identical across axis {axis!r}",
+              flush=True)

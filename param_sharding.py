@@ -1,6 +1,7 @@
 """FSDP / ZeRO-3 training of the tutorial classifier (reference param_sharding.py).
 
-    torchrun --nproc-per-node 8 param_sharding.py   # 8 MI355X, RCCL over xGMI
+    python param_sharding.py                        # every visible GPU, one rank each (RCCL / xGMI)
+    torchrun --nproc-per-node 8 param_sharding.py   # the same under an external launcher
     python param_sharding.py --sim-cpu 8            # 8 gloo CPU ranks
 
 Params, grads and AdamW moments are sharded with the reference rule
@@ -20,9 +21,8 @@ from jax_distributed_tuts_amd.parallel.dp import shard_batch
 from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
 from jax_distributed_tuts_amd.runtime import dist as D
 from jax_distributed_tuts_amd.runtime.dist import Mesh
-from jax_distributed_tuts_amd.runtime.launch import run
 from jax_distributed_tuts_amd.utils.config import fsdp_config
-from jax_distributed_tuts_amd.utils.cli import add_common_args, maybe_profile
+from jax_distributed_tuts_amd.utils.cli import add_common_args, entry_main
 from jax_distributed_tuts_amd.utils.metrics import print_metrics
 from jax_distributed_tuts_amd.utils.train_state import Batch, adamw, get_num_params
 
@@ -49,6 +49,11 @@ def main(args):
         tr.step(batch)
     tr.metrics.zero_()
     tr.step(batch)
+    tr.finalize()  # raises (non-zero exit) if an xGMI gather / reduce-scatter timed out
+    if args.check_replication:
+        from jax_distributed_tuts_amd.utils.debug import check_trainer_replication
+
+        check_trainer_replication(tr)
     if D.rank() == 0:
         print_metrics(tr.metrics, "FSDP - Final metrics")
 
@@ -58,5 +63,4 @@ if __name__ == "__main__":
     ap.add_argument("--gather-once", action="store_true")
     ap.add_argument("--scatter-once", action="store_true")
     a = ap.parse_args()
-    maybe_profile(a, __file__)
-    run(main, a, sim_cpu=a.sim_cpu)
+    entry_main(main, a, __file__)

@@ -2,8 +2,9 @@
 pipeline_parallel.py is an imports-only stub; this is the intended tutorial,
 SURVEY §3.5).
 
-    torchrun --nproc-per-node 8 pipeline_parallel.py                  # 8-stage MLP (BASELINE config #4)
-    torchrun --nproc-per-node 8 pipeline_parallel.py --dp 2 --model transformer   # DP=2 x PP=4 (config #5)
+    python pipeline_parallel.py --gpus 8                               # 8-stage MLP (BASELINE config #4)
+    python pipeline_parallel.py --gpus 8 --dp 2 --model transformer    # DP=2 x PP=4 (config #5)
+    torchrun --nproc-per-node 8 pipeline_parallel.py                   # the same under an external launcher
     python pipeline_parallel.py --sim-cpu 4 --dp 2                     # gloo CPU simulation
 
 Default model: an MLP 784 -> 512 x 8 -> 10 (9 Dense layers, SiLU, dropout 0.1)
@@ -21,9 +22,8 @@ from jax_distributed_tuts_amd.parallel.pipeline import GPipeTrainer, PipeConfig,
 from jax_distributed_tuts_amd.models.mlp import MLP
 from jax_distributed_tuts_amd.runtime import dist as D
 from jax_distributed_tuts_amd.runtime.dist import Mesh
-from jax_distributed_tuts_amd.runtime.launch import run
 from jax_distributed_tuts_amd.utils import rng as R
-from jax_distributed_tuts_amd.utils.cli import add_common_args, maybe_profile
+from jax_distributed_tuts_amd.utils.cli import add_common_args, entry_main
 from jax_distributed_tuts_amd.utils.config import dp_config
 from jax_distributed_tuts_amd.utils.metrics import print_metrics
 from jax_distributed_tuts_amd.utils.train_state import Batch, TrainState, adamw
@@ -67,6 +67,12 @@ def main(args):
         tr.step(batch)
     tr.metrics.zero_()
     tr.step(batch)
+    if hasattr(tr, "finalize"):
+        tr.finalize()
+    if args.check_replication:
+        from jax_distributed_tuts_amd.utils.debug import check_trainer_replication
+
+        check_trainer_replication(tr)
     m = tr.gather_metrics()
     if D.rank() == 0:
         print_metrics(m, f"PP{mesh.axis_size('pipe')} x DP{dp} - Final metrics")
@@ -79,5 +85,4 @@ if __name__ == "__main__":
     ap.add_argument("--hidden-layers", type=int, default=8)
     ap.add_argument("--model", choices=["mlp", "transformer"], default="mlp")
     a = ap.parse_args()
-    maybe_profile(a, __file__)
-    run(main, a, sim_cpu=a.sim_cpu)
+    entry_main(main, a, __file__)

@@ -9,7 +9,8 @@
 // producer that pushes the tensor straight into the consumer's inbox slot over
 // the xGMI link (posted remote stores, no round trip) and then raises one epoch
 // flag per block (relaxed system-scope store after the data stores are
-// acknowledged -- the inbox is uncached, so no cache maintenance); a receive is a kernel on the
+// acknowledged; payload stores and loads are system-scope sc0 sc1 buffer
+// instructions, common.h, so no cache maintenance); a receive is a kernel on the
 // consumer that waits for the flags of its own blocks and copies the slot into
 // a local tensor.  Both are ordinary kernels on the caller's stream, so a whole
 // pipeline step -- compute, sends and receives -- is one hipGraph per rank.
@@ -23,8 +24,8 @@
 // of step k+1 only after it has received every activation gradient of step k,
 // and the consumer sends those gradients only after the kernels that read slot i
 // of step k have completed (stream order) -- so one buffer per (direction,
-// microbatch) is race-free.  The inbox is uncached, so the consumer's loads see
-// the peer's stores once the flag is acquired, on every XCD.
+// microbatch) is race-free.  The consumer's sc0 sc1 loads see the peer's
+// write-through stores once the flag is observed, on every XCD.
 //
 // Waits time out (s_memrealtime, 100 MHz) into an error flag, never a hang.
 #include "common.h"
@@ -79,10 +80,12 @@ __global__ void __launch_bounds__(P2P_THREADS) p2p_send_kernel(const uint4* __re
                                                                unsigned* flag, const int* epoch_src) {
   long lo, hi;
   p2p_range(nw, &lo, &hi);
-  for (long i = lo + threadIdx.x; i < hi; i += P2P_THREADS) dst[i] = src[i];
-  // the inbox is uncached: the data is ordered before the flag by waiting for the
-  // stores' acknowledgement, no L2 write-back (a release fence would flush the
-  // whole L2 per wave)
+  // remote stores into the peer's inbox: system-scope write-through (sc0 sc1, common.h)
+  const __amdgpu_buffer_rsrc_t rd = sys_rsrc(dst, (unsigned long long)nw * 16ull);
+  for (long i = lo + threadIdx.x; i < hi; i += P2P_THREADS)
+    sys_store4(rd, 4 * i, __builtin_bit_cast(float4, src[i]));
+  // every storing wave drains its write-through stores before the barrier that
+  // precedes the flag (no release fence: that would write back the whole L2 per wave)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -105,10 +108,12 @@ __global__ void __launch_bounds__(P2P_THREADS) p2p_recv_kernel(const uint4* src,
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  __syncthreads();  // the inbox is uncached: its loads below see the peer's stores
+  __syncthreads();
   long lo, hi;
   p2p_range(nw, &lo, &hi);
-  for (long i = lo + threadIdx.x; i < hi; i += P2P_THREADS) dst[i] = src[i];
+  // every load of the handed-off bytes is a system-scope sc0 sc1 load (common.h)
+  const __amdgpu_buffer_rsrc_t rs = sys_rsrc(src, (unsigned long long)nw * 16ull);
+  for (long i = lo + threadIdx.x; i < hi; i += P2P_THREADS) dst[i] = __builtin_bit_cast(uint4, sys_load4(rs, 4 * i));
 }
 
 }  // namespace jdt

@@ -24,9 +24,11 @@
 // Synchronisation is per block, never grid-wide: block b only touches chunk b
 // of every slice, on every rank, so it only needs block b of the peers.  Flags
 // are monotonically increasing per-block epochs written into the peers'
-// uncached signal pages; the staging buffers are uncached too, so flags are
-// relaxed system-scope stores/loads ordered after the data by vmcnt waits --
-// no L2 write-back/invalidate anywhere on the path.  The data and tmp
+// signal pages with relaxed system-scope atomic stores, ordered after the data
+// by vmcnt waits; every staging-buffer access is a system-scope sc0 sc1 buffer
+// instruction (common.h "system-scope payload": write-through stores, coherent
+// loads), so correctness does not depend on the MTYPE the importing GPU's IPC
+// mapping inherits, and there is no L2 write-back/invalidate on the path.  The data and tmp
 // buffers are double-buffered by epoch parity, so a call may start staging
 // while a slow peer still reads the previous call's buffers -- no trailing
 // barrier.  Every spin has a wall-clock timeout (s_memrealtime, 100 MHz): a
@@ -80,10 +82,11 @@ __device__ __forceinline__ float4 add4(float4 a, float4 b) {
 }
 
 // Per-block barrier across the W ranks.  Thread q < W signals peer q and waits for
-// peer q's signal.  The data/tmp buffers and signal pages are UNCACHED device
-// memory, so no cache maintenance is needed: a thread's stores are ordered
-// before the flag by waiting for their acknowledgement (vmcnt), and flags are
-// relaxed system-scope stores / loads.  (A release/acquire pair would lower to
+// peer q's signal.  Every wave's payload stores are sc0 sc1 (write-through at
+// system scope) and are drained (vmcnt) before the workgroup barrier that
+// precedes the flag store; flags are relaxed system-scope atomic stores / loads,
+// and all payload loads after the wait are sc0 sc1 (common.h), so no cache
+// maintenance instruction is needed.  (A release/acquire pair would lower to
 // a write-back / invalidate of the whole L2 -- per wave, and per spin iteration
 // on the acquire side: measured ~70 us for a 1 MB all-reduce, tools/bench_comm.py.)
 __device__ void xg_barrier(const XgPeers& P, int rank, int W, int which, unsigned epoch, long long timeout) {
@@ -165,30 +168,39 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
   const long base = (long)b * chunk;
   const int nv = (int)(chunk >> 2);
   const long own_n = (n - rank * s < s) ? n - rank * s : s;  // valid length of this rank's part
+  const unsigned long long bytes = (unsigned long long)cap * 2ull * sizeof(float);
+  // every access to an IPC buffer (own or peer) is a system-scope sc0 sc1 access (common.h)
+  __amdgpu_buffer_rsrc_t rdata[W], rtmp[W];
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    rdata[q] = sys_rsrc(P.data[q], bytes);
+    rtmp[q] = sys_rsrc(P.tmp[q], bytes);
+  }
+  const __amdgpu_buffer_rsrc_t my_data = sys_rsrc(P.data[rank], bytes), my_tmp = sys_rsrc(P.tmp[rank], bytes);
 
   if (OP != XG_ALL_GATHER) {
-    // phase 0: stage chunk b of every part of the local input
-    float* dst = P.data[rank] + half;
+    // phase 0: stage chunk b of every part of the local input (write-through stores)
     for (int q = 0; q < W; ++q) {
       for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
         const long j = base + 4 * i;
         const float4 x = j < s ? load_guard(in, q * s + j, n) : make_float4(0.f, 0.f, 0.f, 0.f);
-        *reinterpret_cast<float4*>(dst + q * slice + j) = x;
+        sys_store4(my_data, half + q * slice + j, x);
       }
     }
     xg_barrier(P, rank, W, 0, epoch, timeout);
-    // phase 1: reduce chunk b of part `rank` over the peers (all W loads in flight)
+    // phase 1: reduce chunk b of part `rank` over the peers (all W loads in flight,
+    // fixed rank order -> every rank computes bit-identical sums)
     for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
       const long j = base + 4 * i;
       const long e = rank * slice + j;
       float4 v[W];
 #pragma unroll
-      for (int q = 0; q < W; ++q) v[q] = *reinterpret_cast<const float4*>(P.data[q] + half + e);
+      for (int q = 0; q < W; ++q) v[q] = sys_load4(rdata[q], half + e);
       float4 acc = v[0];
 #pragma unroll
       for (int q = 1; q < W; ++q) acc = add4(acc, v[q]);
       if (OP == XG_REDUCE_SCATTER) store_guard(out, j, own_n, acc);
-      else *reinterpret_cast<float4*>(P.tmp[rank] + half + e) = acc;
+      else sys_store4(my_tmp, half + e, acc);
     }
     if (OP == XG_REDUCE_SCATTER) {
       if (threadIdx.x == 0) me->epoch[b] = epoch;
@@ -199,7 +211,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
     for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
       const long j = base + 4 * i;
       const float4 x = j < s ? load_guard(in, j, own_n) : make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>(P.tmp[rank] + half + rank * slice + j) = x;
+      sys_store4(my_tmp, half + rank * slice + j, x);
     }
   }
   xg_barrier(P, rank, W, 1, epoch, timeout);
@@ -216,7 +228,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
     if (j >= s) break;
     float4 r[W];
 #pragma unroll
-    for (int q = 0; q < W; ++q) r[q] = *reinterpret_cast<const float4*>(P.tmp[q] + half + q * slice + j);
+    for (int q = 0; q < W; ++q) r[q] = sys_load4(rtmp[q], half + q * slice + j);
 #pragma unroll
     for (int q = 0; q < W; ++q) {
       const long e = q * s + j;
@@ -293,9 +305,10 @@ __global__ void __launch_bounds__(XG_THREADS) xg_seg_kernel(XgPeers P, int rank,
   const long base = (long)b * chunk;
   const int nv = (int)(chunk >> 2);
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const unsigned long long bytes = (unsigned long long)cap * 2ull * sizeof(float);
 
   if (OP == XG_REDUCE_SCATTER) {
-    float* dst = P.data[rank] + half;
+    const __amdgpu_buffer_rsrc_t my_data = sys_rsrc(P.data[rank], bytes);
     for (int q = 0; q < W; ++q) {
       for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
         const long j = base + 4 * i;
@@ -304,16 +317,19 @@ __global__ void __launch_bounds__(XG_THREADS) xg_seg_kernel(XgPeers P, int rank,
           const XgSeg& g = S.seg[xg_find(S, j)];
           x = load_guard(g.full, q * g.s + (j - g.off), g.nfull);
         }
-        *reinterpret_cast<float4*>(dst + q * slice + j) = x;
+        sys_store4(my_data, half + q * slice + j, x);
       }
     }
     xg_barrier(P, rank, W, 0, epoch, timeout);
+    __amdgpu_buffer_rsrc_t rdata[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) rdata[q] = sys_rsrc(P.data[q], bytes);
     for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
       const long j = base + 4 * i;
       if (j >= S.S) break;
       float4 v[W];
 #pragma unroll
-      for (int q = 0; q < W; ++q) v[q] = *reinterpret_cast<const float4*>(P.data[q] + half + rank * slice + j);
+      for (int q = 0; q < W; ++q) v[q] = sys_load4(rdata[q], half + rank * slice + j);
       float4 acc = v[0];
 #pragma unroll
       for (int q = 1; q < W; ++q) acc = add4(acc, v[q]);
@@ -323,6 +339,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_seg_kernel(XgPeers P, int rank,
       store_guard(g.part, j - g.off, lim, acc);
     }
   } else {
+    const __amdgpu_buffer_rsrc_t my_tmp = sys_rsrc(P.tmp[rank], bytes);
     for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
       const long j = base + 4 * i;
       float4 x = z4;
@@ -331,15 +348,18 @@ __global__ void __launch_bounds__(XG_THREADS) xg_seg_kernel(XgPeers P, int rank,
         const long lim = (g.nfull - rank * g.s < g.s) ? g.nfull - rank * g.s : g.s;
         x = load_guard(g.part, j - g.off, lim);
       }
-      *reinterpret_cast<float4*>(P.tmp[rank] + half + rank * slice + j) = x;
+      sys_store4(my_tmp, half + rank * slice + j, x);
     }
     xg_barrier(P, rank, W, 1, epoch, timeout);
+    __amdgpu_buffer_rsrc_t rtmp[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) rtmp[q] = sys_rsrc(P.tmp[q], bytes);
     for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
       const long j = base + 4 * i;
       if (j >= S.S) break;
       float4 r[W];
 #pragma unroll
-      for (int q = 0; q < W; ++q) r[q] = *reinterpret_cast<const float4*>(P.tmp[q] + half + q * slice + j);
+      for (int q = 0; q < W; ++q) r[q] = sys_load4(rtmp[q], half + q * slice + j);
       const XgSeg& g = S.seg[xg_find(S, j)];
 #pragma unroll
       for (int q = 0; q < W; ++q) store_guard(g.full, q * g.s + (j - g.off), g.nfull, r[q]);
@@ -409,6 +429,10 @@ JDT_API int jdt_xgmi_create(int rank, int world, long cap_floats, void** ctx_out
   c->rank = rank;
   c->world = world;
   c->cap = (cap_floats + 4 * (long)XG_MAX_BLOCKS * world + 63) / 64 * 64;
+  if (2 * c->cap * (long)sizeof(float) >= 0x7fffffffL) {  // buffer-instruction offsets are 32-bit
+    delete c;
+    return -2;
+  }
   hipIpcMemHandle_t h[3];
   // uncached: peers read these over xGMI right after the flag (see xg_barrier)
   if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->data), 2 * c->cap * sizeof(float), hipDeviceMallocUncached) !=

@@ -131,18 +131,23 @@ class XgmiP2P:
             pass
 
     def _self_test(self) -> bool:
-        """Ring exchange (r -> r+1) through two slots, two epochs, exact values."""
+        """Ring exchange (r -> r+1) through EVERY slot at full slot size, 8 epochs
+        (each slot's flag and payload reused 8 times), senders skewed by a rank-
+        and epoch-dependent spin; exact values."""
         saved = self.timeout
         self.timeout = c_longlong(int(5.0 * TICKS_PER_S))
         try:
             W, r, dev = self.world, self.rank, self.device
             with torch.cuda.device(dev):
-                n = min(self.slot_bytes // 4, 4096) // 4 * 4
+                n = min(self.slot_bytes // 4, 1 << 16) // 4 * 4
                 ep = torch.zeros(1, dtype=torch.int32, device=dev)
-                for it in range(2):
-                    for slot in sorted({0, self.n_slots - 1}):
+                for it in range(8):
+                    for slot in range(self.n_slots):
                         x = torch.arange(n, device=dev, dtype=torch.float32) + 1000 * r + 7 * it + slot
                         out = torch.empty(n, device=dev)
+                        cyc = ((r * 5 + it + slot) % (W + 1)) * 10_000
+                        if cyc:
+                            torch.cuda._sleep(cyc)
                         self.send(x, (r + 1) % W, slot, ep)
                         self.recv(out, slot, ep)
                         want = torch.arange(n, device=dev, dtype=torch.float32) + 1000 * ((r - 1) % W) + 7 * it + slot

@@ -18,8 +18,10 @@ runs the collectives as ordinary kernels on the current stream:
 Being kernels rather than RCCL calls, they are captured into hipGraphs with
 the rest of the step, so a multi-GPU step is a single graph replay.
 
-Construction runs a self-test on the real hardware (exact small-integer sums
-through every phase and both buffer parities) and all ranks agree on the
+Construction runs a self-test on the real hardware (``_self_test``: 32
+skewed-arrival all-reduces over three sizes and both buffer parities, RS / AG,
+the segmented FSDP kernels and the fused-AdamW variant, all exact, and
+bit-compared with RCCL when the group is nccl) and all ranks agree on the
 outcome; ``comm.ok`` is False (and the trainers fall back to RCCL) if the IPC
 mapping or the self-test fails on any rank.  Every in-kernel wait has a
 timeout, so a dead peer turns into an error flag (``error()``) instead of a
@@ -256,56 +258,166 @@ class XgmiComm:
             _lib.check(rc, "jdt_xgmi_segments(reduce_scatter)")
 
     # ------------------------------------------------------------------ self-test
+    SELF_TEST_ITERS = 32
+
     def _self_test(self) -> bool:
-        """Exact-integer checks of AR (both parities), RS and AG on this hardware.
+        """Exact checks of every kernel on this hardware before any trainer uses it.
+
+        * ``SELF_TEST_ITERS`` all-reduces cycling over several sizes -- the DP bucket
+          (407,054 floats: 1.63 MB of grads + 4 metric slots), a 300,001-float
+          buffer, a 4,099-float one -- so both epoch parities are reused many times
+          at every size (a stale peer line from an earlier same-parity call would
+          show up as a wrong sum);
+        * ranks arrive skewed: before every collective each rank spins for a
+          rank- and iteration-dependent time (uneven load is what exposes
+          visibility bugs, MI355X_MICROARCH.md);
+        * reduce-scatter and all-gather at two sizes, the segmented (FSDP) kernels
+          on the tutorial's shard shapes, and the fused-AdamW all-reduce against
+          the same AdamW computed by torch on the summed gradient;
+        * integer-valued data, so sums are exact: results must be bit-identical to
+          the expected values and, when the group is nccl, to RCCL's all-reduce of
+          the same data.
         Runs with a short barrier timeout (the ranks were just synchronised by the
-        handle exchange) and stops at the first failure, so a node whose peers
-        cannot see each other's flags costs seconds, not minutes."""
+        handle exchange) and stops at the first failure."""
         saved = self.timeout
         self.timeout = c_longlong(int(5.0 * TICKS_PER_S))
         try:
-            W, r, dev = self.world, self.rank, self.device
-            with torch.cuda.device(dev):
-                n = min(self.capacity // 2, 300_001)
-                base = (torch.arange(n, device=dev, dtype=torch.int64) % 97).to(torch.float32)
-                want = base * W + W * (W - 1) / 2
-                for it in range(3):
-                    x = base + r + it
-                    self.all_reduce_(x)
-                    torch.cuda.synchronize(dev)
-                    if self.error():
-                        log.warning("xgmi self-test: barrier timeout")
-                        return False
-                    if not torch.equal(x, want + W * it):
-                        log.warning("xgmi self-test: all-reduce mismatch (iter %d)", it)
-                        return False
-                part = part_len(n, W)
-                out = torch.empty(part, device=dev)
-                self.reduce_scatter(base + r, out, part)
-                lo, hi = r * part, min(n, (r + 1) * part)
-                if not torch.equal(out[: hi - lo], want[lo:hi]):
-                    log.warning("xgmi self-test: reduce-scatter mismatch")
-                    return False
-                full = torch.empty(n, device=dev)
-                mine = torch.zeros(part, device=dev)
-                mine[: hi - lo] = base[lo:hi] + 1000 * r
-                self.all_gather(mine, full, part)
-                exp = base.clone()
-                for q in range(W):
-                    exp[q * part: min(n, (q + 1) * part)] += 1000 * q
-                if not torch.equal(full, exp):
-                    log.warning("xgmi self-test: all-gather mismatch")
-                    return False
-                torch.cuda.synchronize(dev)
-                if self.error():
-                    log.warning("xgmi self-test: barrier timeout")
-                    return False
-            return True
+            with torch.cuda.device(self.device):
+                ok = self._self_test_body()
+            return ok
         except Exception as e:  # a launch error must not leave the other ranks waiting
             log.warning("xgmi self-test raised: %s", e)
             return False
         finally:
             self.timeout = saved
+
+    def _skew(self, it: int):
+        cyc = ((self.rank * 7 + it * 3) % (self.world + 1)) * 20_000
+        if cyc:
+            torch.cuda._sleep(cyc)
+
+    def _fail(self, what: str) -> bool:
+        torch.cuda.synchronize(self.device)
+        log.warning("xgmi self-test failed on rank %d: %s%s", self.rank, what,
+                    " (barrier timeout)" if self.error() else "")
+        return False
+
+    def _self_test_body(self) -> bool:
+        W, r, dev = self.world, self.rank, self.device
+        cap = self.capacity
+        sizes = [n for n in (407_054, 300_001, 4_099) if part_len(n, W) * W <= cap // 2] or [min(cap // 4, 4_099)]
+        nccl = dist.get_backend(self.group) == "nccl"
+        for it in range(self.SELF_TEST_ITERS):
+            n = sizes[it % len(sizes)]
+            base = (torch.arange(n, device=dev, dtype=torch.int64) % 97).to(torch.float32)
+            x = base * (r + 1) + it
+            want = base * (W * (W + 1) // 2) + W * it
+            ref = x.clone() if (nccl and it % 4 == 0) else None
+            self._skew(it)
+            self.all_reduce_(x)
+            if ref is not None:
+                dist.all_reduce(ref, group=self.group)
+            torch.cuda.synchronize(dev)
+            if self.error() or not torch.equal(x, want):
+                return self._fail(f"all-reduce mismatch (iter {it}, n {n})")
+            if ref is not None and not torch.equal(x, ref):
+                return self._fail(f"all-reduce differs from RCCL (iter {it}, n {n})")
+        for k, n in enumerate(sizes[:2]):
+            for rep in range(2):  # both parities
+                base = (torch.arange(n, device=dev, dtype=torch.int64) % 89).to(torch.float32)
+                want = base * W + W * (W - 1) / 2
+                part = part_len(n, W)
+                out = torch.empty(part, device=dev)
+                self._skew(k + rep)
+                self.reduce_scatter(base + r, out, part)
+                lo, hi = r * part, min(n, (r + 1) * part)
+                torch.cuda.synchronize(dev)
+                if self.error() or not torch.equal(out[: hi - lo], want[lo:hi]):
+                    return self._fail(f"reduce-scatter mismatch (n {n})")
+                full = torch.empty(n, device=dev)
+                mine = torch.zeros(part, device=dev)
+                mine[: hi - lo] = base[lo:hi] + 1000 * r + rep
+                self._skew(k + rep + 1)
+                self.all_gather(mine, full, part)
+                exp = base.clone()
+                for q in range(W):
+                    exp[q * part: min(n, (q + 1) * part)] += 1000 * q + rep
+                torch.cuda.synchronize(dev)
+                if self.error() or not torch.equal(full, exp):
+                    return self._fail(f"all-gather mismatch (n {n})")
+        if not self._self_test_segments():
+            return False
+        return self._self_test_adamw()
+
+    def _self_test_segments(self) -> bool:
+        """Segmented AG / RS on the FSDP tutorial's per-rank shard lengths at N = 8
+        (W1 rows 98 x 512, b1 64, W2 64 x 10 floats), for any world size."""
+        W, r, dev = self.world, self.rank, self.device
+        parts = [50_176, 64, 640]
+        if sum(parts) * W > self.capacity // 2:
+            return True
+        for rep in range(2):
+            fulls = [torch.empty(W * s, device=dev) for s in parts]
+            mine = [(torch.arange(s, device=dev, dtype=torch.float32) % 31) + 100 * r + k + rep
+                    for k, s in enumerate(parts)]
+            self._skew(rep)
+            self.all_gather_segments(list(zip(fulls, mine)))
+            torch.cuda.synchronize(dev)
+            for k, s in enumerate(parts):
+                exp = torch.cat([(torch.arange(s, device=dev, dtype=torch.float32) % 31) + 100 * q + k + rep
+                                 for q in range(W)])
+                if self.error() or not torch.equal(fulls[k], exp):
+                    return self._fail("segmented all-gather mismatch")
+            src = [(torch.arange(W * s, device=dev, dtype=torch.float32) % 53) * (r + 1) for s in parts]
+            outs = [torch.full((s,), float(rep), device=dev) for s in parts]
+            self._skew(rep + 1)
+            self.reduce_scatter_segments(list(zip(src, outs)), accumulate=True)
+            torch.cuda.synchronize(dev)
+            for k, s in enumerate(parts):
+                full = (torch.arange(W * s, device=dev, dtype=torch.float32) % 53) * (W * (W + 1) // 2)
+                if self.error() or not torch.equal(outs[k], full[r * s:(r + 1) * s] + rep):
+                    return self._fail("segmented reduce-scatter mismatch")
+        return True
+
+    def _self_test_adamw(self) -> bool:
+        """The fused all-reduce + AdamW + metrics-fold kernel vs torch AdamW on the
+        summed gradient (3 steps: both parities and the device step counter)."""
+        W, r, dev = self.world, self.rank, self.device
+        n_params, n_metrics = 4_096, 4
+        n = n_params + n_metrics
+        if part_len(n, W) * W > self.capacity // 2:
+            return True
+        g0 = torch.arange(n, device=dev, dtype=torch.int64)
+        p = torch.linspace(-1, 1, n_params, device=dev)
+        m, v = torch.zeros(n_params, device=dev), torch.zeros(n_params, device=dev)
+        pr, mr, vr = p.clone(), m.clone(), v.clone()
+        running = torch.zeros(n_metrics, device=dev)
+        step = torch.zeros(1, dtype=torch.int32, device=dev)
+        ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        lr, b1, b2, eps, wd, scale = 1e-2, 0.9, 0.999, 1e-8, 1e-4, 1.0 / (4 * W)
+        for t in range(1, 4):
+            grad = ((g0 * (r + 1) + t) % 13 - 6).to(torch.float32)
+            gsum = sum(((g0 * (q + 1) + t) % 13 - 6).to(torch.float32) for q in range(W))
+            self._skew(t)
+            self.all_reduce_adamw_(grad, p=p, m=m, v=v, shadow=None, n_params=n_params, running=running,
+                                   n_metrics=n_metrics, lr=lr, b1=b1, b2=b2, eps=eps, wd=wd, grad_scale=scale,
+                                   step=step, ticket=ticket, zero_grad=True)
+            gr = gsum[:n_params] * scale
+            mr.mul_(b1).add_(gr, alpha=1 - b1)
+            vr.mul_(b2).addcmul_(gr, gr, value=1 - b2)
+            pr.sub_(lr * ((mr / (1 - b1 ** t)) / ((vr / (1 - b2 ** t)).sqrt() + eps) + wd * pr))
+            torch.cuda.synchronize(dev)
+            bad = (self.error() or int(step.item()) != t or bool(grad.any())
+                   or not torch.allclose(p, pr, rtol=1e-5, atol=1e-6)
+                   or not torch.allclose(m, mr, rtol=1e-5, atol=1e-7)
+                   or not torch.allclose(v, vr, rtol=1e-5, atol=1e-9))
+            if bad:
+                return self._fail(f"fused AdamW all-reduce mismatch (step {t})")
+        want_running = sum(sum(((g0[n_params:] * (q + 1) + t) % 13 - 6).to(torch.float32) for q in range(W))
+                           for t in range(1, 4))
+        if not torch.equal(running, want_running):
+            return self._fail("fused metrics fold mismatch")
+        return True
 
 
 def status(comm: Optional[XgmiComm], world: int, device, mode: str = "auto") -> str:

@@ -41,7 +41,7 @@ def sources() -> list[Path]:
 
 
 def _headers_mtime() -> float:
-    hs = list(CSRC.glob("*.h"))
+    hs = list(CSRC.glob("*.h")) + list(COMM_CSRC.glob("*.h"))
     return max((h.stat().st_mtime for h in hs), default=0.0)
 
 

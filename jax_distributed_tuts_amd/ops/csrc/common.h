@@ -157,6 +157,39 @@ __device__ __forceinline__ float ld_global(const float* p) {
   return *(const __attribute__((address_space(1))) float*)p;
 }
 
+// ---------------------------------------------------------------- system-scope (cross-GPU) payload
+// IPC-mapped buffers (comm/csrc: xGMI collectives, pipeline inboxes) are written by one
+// GPU and read by another over xGMI.  Their coherence is made explicit on EVERY payload
+// instruction instead of being inherited from the memory type the importing GPU's
+// mapping happens to get (a peer-VRAM mapping of an ordinary allocation is cached
+// non-coherently in the reader's L2, so a re-read of the same address in a later
+// call could hit a stale line): accesses are buffer instructions with the
+// cache-policy bits sc0 sc1 (aux = 1 | 16), the system-scope form that the LLVM
+// AMDGPU memory model for GFX942/GFX950 emits for system-scope relaxed atomics --
+//   load  atomic monotonic, system  ->  buffer/global_load  ... sc0 sc1
+//   store atomic monotonic, system  ->  buffer/global_store ... sc0 sc1
+// -- i.e. a load is served coherently at system scope (no stale L1/L2 copy) and a
+// store is written through past this GPU's caches.  Ordering: each storing wave
+// drains its stores (s_waitcnt vmcnt(0)) and the workgroup barriers before ONE lane
+// raises the peer's flag with a relaxed system-scope atomic store; the reader polls
+// that flag with relaxed system-scope atomic loads, barriers, then issues its
+// payload loads (all sc0 sc1).  Out-of-range offsets are dropped by the buffer
+// bounds check (num_records), never written.
+constexpr int CPOL_SYS = 1 | 16;  // sc0 | sc1
+typedef __attribute__((ext_vector_type(4))) unsigned sys_u32x4;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sys_rsrc(const void* base, unsigned long long bytes) {
+  const int n = bytes >= 0x7fffffffull ? 0x7fffffff : (int)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, n, 0x00020000);
+}
+__device__ __forceinline__ float4 sys_load4(__amdgpu_buffer_rsrc_t r, long float_off) {
+  const sys_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(float_off * 4), 0, CPOL_SYS);
+  return __builtin_bit_cast(float4, v);
+}
+__device__ __forceinline__ void sys_store4(__amdgpu_buffer_rsrc_t r, long float_off, float4 x) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sys_u32x4, x), r, (int)(float_off * 4), 0, CPOL_SYS);
+}
+
 }  // namespace jdt
 
 #define HIP_LAUNCH_CHECK() (int)hipGetLastError()

@@ -394,7 +394,8 @@ class XgmiComm:
         running = torch.zeros(n_metrics, device=dev)
         step = torch.zeros(1, dtype=torch.int32, device=dev)
         ticket = torch.zeros(1, dtype=torch.int32, device=dev)
-        lr, b1, b2, eps, wd, scale = 1e-2, 0.9, 0.999, 1e-8, 1e-4, 1.0 / (4 * W)
+        # betas exactly representable in fp32, so the kernel's fp32 (1 - b) equals torch's
+        lr, b1, b2, eps, wd, scale = 1e-2, 0.875, 1.0 - 2.0 ** -10, 1e-8, 1e-4, 1.0 / (4 * W)
         for t in range(1, 4):
             grad = ((g0 * (r + 1) + t) % 13 - 6).to(torch.float32)
             gsum = sum(((g0 * (q + 1) + t) % 13 - 6).to(torch.float32) for q in range(W))

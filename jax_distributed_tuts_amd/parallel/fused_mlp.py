@@ -51,6 +51,12 @@ _lib.declare("jdt_mlp2_loop_ok", c_int, [c_int, c_int])
 LOOP_BARRIER_TIMEOUT_TICKS = 20_000_000   # 0.2 s of s_memrealtime (100 MHz) per grid barrier
 
 
+def _is_adamw(tx) -> bool:
+    from ..utils.train_state import AdamW
+
+    return isinstance(tx, AdamW)
+
+
 def set_forward_rows(rb: int):
     """mlp2_fwd rows per workgroup: 16 (default, 256 workgroups at 128 rows) or 32
     (A/B comparisons; env ``JDT_MLP2_RB`` sets it at engine construction)."""
@@ -93,7 +99,9 @@ class FusedMLP2:
         self.metrics = metrics
         if fuse_opt is None:
             fuse_opt = self.world == 1 and os.environ.get("JDT_FUSED_OPT", "1") == "1"
-        self.fuse_opt = bool(fuse_opt) and params is None
+        # mode 1 fuses AdamW into the backward epilogue; any other optimizer (SGD) runs
+        # mode 0 (plain-stored grads) + its own kernel
+        self.fuse_opt = bool(fuse_opt) and params is None and _is_adamw(state.tx)
         # K-contiguous bf16 operand copies (zero K padding): X^T written by mlp2_fwd for
         # mlp2_bwd; W1^T written by mlp2_bwd's AdamW epilogue for the next mlp2_fwd
         self.Mp = (rows + 31) // 32 * 32
@@ -282,7 +290,7 @@ class FusedMLPDeep:
         self.logits = torch.zeros(2, rows, 10, dtype=torch.float32, device=dev)
         if fuse_opt is None:
             fuse_opt = self.world == 1 and os.environ.get("JDT_FUSED_OPT", "1") == "1"
-        self.fuse_opt = bool(fuse_opt) and params is None
+        self.fuse_opt = bool(fuse_opt) and params is None and _is_adamw(state.tx)
         kn = [f"{n}/kernel" for n in m.names]
         self.kn, self.bn = kn, [f"{n}/bias" for n in m.names]
         # second step-parity copy of the row-major shadows read after being updated in

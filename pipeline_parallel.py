@@ -34,14 +34,15 @@ def pp_mlp_dims(cfg, n_hidden_layers: int):
 
 
 def build_mlp_pipeline(cfg, mesh, dev, n_hidden_layers=8, dropout_rate=None, num_microbatches=4, comm="auto",
-                       merge_single_stage=False):
+                       merge_single_stage=False, tx=None):
     dims = pp_mlp_dims(cfg, n_hidden_layers)
     S, s = mesh.axis_size("pipe"), mesh.axis_index("pipe")
     dr = cfg.model.dropout_rate if dropout_rate is None else dropout_rate
     stage = mlp_stage(dims, S, s, dropout_rate=dr)
     full = MLP(dims, dropout_rate=dr)
     P = init_stage_params(stage, full.param_specs(), cfg.seed, dev)
-    st = TrainState.create(apply_fn=stage, params=P, tx=adamw(cfg.optimizer.learning_rate), rng=R.PRNGKey(cfg.seed))
+    tx = tx if tx is not None else adamw(cfg.optimizer.learning_rate)
+    st = TrainState.create(apply_fn=stage, params=P, tx=tx, rng=R.PRNGKey(cfg.seed))
     tr = GPipeTrainer(st, mesh, PipeConfig(num_microbatches, comm=comm, merge_single_stage=merge_single_stage))
     return tr
 

@@ -180,3 +180,85 @@ def dp_overlap(out_dir, overlap, bucket_mb):
     for _ in range(2):
         tr.step(batch)
     _save(out_dir, f"ov{int(overlap)}", {"params": st.params.state_dict(), "metrics": tr.metrics.clone(), "nb": nb})
+
+
+# ----------------------------------------------------------------------------- gradient-scale probes
+def _clone(d):
+    return {k: v.detach().clone() for k, v in d.items()}
+
+
+def grad_probe(out_dir, kind, accum="loop", gather_once=False, dp=1, n_hidden=3):
+    """ONE plain-SGD (lr 1) step of a strategy, dropout off; saves the parameters
+    before and after, so the test reads the applied gradient p0 - p1 exactly
+    (tests/oracle.py)."""
+    from data_paral import synthetic_batch
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.ops import kernels as K
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp, shard_batch
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.train_state import sgd
+
+    cfg = dp_config()
+    batch_full = synthetic_batch(cfg, 70)
+    if kind in ("dp", "dp_no_inv_n"):
+        mesh = Mesh({"data": D.world_size()})
+        st = init_dp(Classifier(dropout_rate=0.0), sgd(1.0), 69, "cpu", mesh)
+        cls = DataParallelTrainer
+        if kind == "dp_no_inv_n":
+            class _NoInvN(DataParallelTrainer):  # deliberately drops the 1/N of pmean
+                def update_noncounting(self):
+                    P = self.state.params
+                    self.state.tx.update(P, self.state.opt_state, 1.0 / self.cfg.num_minibatches)
+                    K.metrics_fold_(self.metrics, P.metrics_slot)
+            cls = _NoInvN
+        tr = cls(st, mesh, DPConfig(4, accum))
+        before = _clone(st.params.state_dict())
+        tr.step(shard_batch(batch_full, mesh, "data"))
+        after = _clone(st.params.state_dict())
+    elif kind == "fsdp":
+        from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
+
+        mesh = Mesh({"data": D.world_size()})
+        st = init_fsdp(Classifier(dropout_rate=0.0), sgd(1.0), 69, "cpu", mesh, "data", 16)
+        tr = FSDPTrainer(st, mesh, FSDPConfig(4, 16, "data", gather_once=gather_once, scatter_once=gather_once))
+        before = _clone(tr.full_params())
+        tr.step(shard_batch(batch_full, mesh, "data"))
+        after = _clone(tr.full_params())
+    elif kind == "pp":
+        from pipeline_parallel import build_mlp_pipeline
+
+        mesh = Mesh({"data": dp, "pipe": D.world_size() // dp})
+        tr = build_mlp_pipeline(cfg, mesh, "cpu", n_hidden_layers=n_hidden, dropout_rate=0.0, num_microbatches=4,
+                                tx=sgd(1.0))
+        before = _clone(tr.state.params.state_dict())
+        tr.step(shard_batch(batch_full, mesh, "data"))
+        after = _clone(tr.state.params.state_dict())
+    else:
+        raise ValueError(kind)
+    _save(out_dir, f"probe_{kind}", {"before": before, "after": after})
+
+
+def replication_desync(out_dir):
+    """--check-replication on a DP trainer whose rank 1 was deliberately perturbed."""
+    from data_paral import synthetic_batch
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp, shard_batch
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.debug import ReplicationError, check_trainer_replication
+    from jax_distributed_tuts_amd.utils.train_state import adamw
+
+    mesh = Mesh({"data": D.world_size()})
+    st = init_dp(Classifier(), adamw(1e-3), 69, "cpu", mesh)
+    tr = DataParallelTrainer(st, mesh, DPConfig(4, "fused"))
+    b = shard_batch(synthetic_batch(dp_config(), 70), mesh, "data")
+    tr.step(b)
+    check_trainer_replication(tr)  # healthy: passes
+    if D.rank() == 1:
+        st.params.p("output_dense/bias")[3] += 1e-6
+    tr.step(b)
+    try:
+        check_trainer_replication(tr)
+        res = "no-error"
+    except ReplicationError as e:
+        res = str(e)
+    _save(out_dir, "repdesync", {"res": res})

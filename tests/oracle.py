@@ -1,0 +1,65 @@
+"""Float64 autograd oracle of the tutorial MLP's training gradient.
+
+The reference's gradient (data_paral.py:171-212, util.py:41-78) is the mean over
+``n_minbatch`` minibatches of the mean softmax-CE over each minibatch's rows,
+then the mean over devices.  With equal-sized minibatches and shards that is the
+mean CE over the whole global batch -- computed here in float64 with plain torch
+autograd on an ordinary dense model (no bf16, no kernels), optionally with
+explicit dropout keep-masks (the engine's Philox masks, mirrored bit-exactly by
+``ops.kernels.dropout_mask``).
+
+Engine gradients are read back from a single plain-SGD step (lr 1, no momentum,
+no weight decay): ``g = p_before - p_after`` -- unlike Adam, whose update is
+nearly invariant to a constant gradient factor, this is proportional to the
+gradient, so a missing 1/N or 1/n_minibatch shows up as a scale error.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+
+def mlp_grads_fp64(params: Dict[str, torch.Tensor], names: Sequence[str], x: torch.Tensor, y: torch.Tensor,
+                   masks: Optional[List[List[Optional[torch.Tensor]]]] = None, keep: float = 1.0,
+                   n_mb: int = 1, act: str = "silu") -> Dict[str, torch.Tensor]:
+    """d/dparams of (1/n_mb) sum_i mean-CE(minibatch i) for the Dense stack
+    ``names`` (flax [in, out] kernels).  ``masks[i][l]``: keep-mask of hidden layer
+    l's output in minibatch i (None = no dropout)."""
+    P = {k: v.detach().double().clone().requires_grad_(True) for k, v in params.items()}
+    rows = x.shape[0]
+    mb = rows // n_mb
+    total = 0.0
+    for i in range(n_mb):
+        h = x[i * mb:(i + 1) * mb].double()
+        for li, n in enumerate(names):
+            z = h @ P[f"{n}/kernel"] + P[f"{n}/bias"]
+            if li < len(names) - 1:
+                h = z * torch.sigmoid(z) if act == "silu" else torch.nn.functional.gelu(z, approximate="tanh")
+                if masks is not None and masks[i][li] is not None:
+                    h = torch.where(masks[i][li], h / keep, torch.zeros_like(h))
+            else:
+                h = z
+        lab = y[i * mb:(i + 1) * mb].long()
+        total = total + torch.nn.functional.cross_entropy(h, lab, reduction="mean")
+    (total / n_mb).backward()
+    return {k: v.grad.detach() for k, v in P.items()}
+
+
+def check_grad(got: torch.Tensor, want: torch.Tensor, name: str = "", rel_tol: float = 0.05,
+               scale_tol: float = 0.03):
+    """Engine gradient (bf16 matmul operands, fp32 accumulate) vs the fp64 oracle:
+    relative L2 error below ``rel_tol`` AND the least-squares scale
+    <got, want> / <want, want> within ``1 +- scale_tol`` (a factor-2 error can
+    never pass)."""
+    g, w = got.double().flatten(), want.double().flatten()
+    wn = float(w.norm())
+    assert wn > 0, f"{name}: zero oracle gradient"
+    rel = float((g - w).norm()) / wn
+    scale = float(g @ w) / float(w @ w)
+    assert rel < rel_tol and abs(scale - 1.0) < scale_tol, f"{name}: rel err {rel:.4f}, scale {scale:.4f}"
+    return rel, scale
+
+
+def sgd_grads(before: Dict[str, torch.Tensor], after: Dict[str, torch.Tensor], lr: float = 1.0):
+    return {k: (before[k].double() - after[k].double()) / lr for k in before}

@@ -1,0 +1,150 @@
+"""Scale-sensitive strategy checks.
+
+Every check reads the gradient the optimizer actually applied -- one plain-SGD
+step with lr 1: ``p_before - p_after`` -- and compares it with a float64
+autograd oracle of the reference's loss on the GLOBAL batch (tests/oracle.py):
+the mean over minibatches (util.py:77) of the mean CE, averaged over devices
+(data_paral.py:210-212) or reduce-scatter-meaned (param_sharding.py:134-138).
+A missing 1/N, 1/n_minibatch or reduce-scatter /N is a factor >= 2 and fails
+``check_grad``'s scale bound; ``test_oracle_detects_missing_inverse_n`` proves it
+by running a trainer with the 1/N deliberately dropped.
+"""
+import functools
+import os
+
+import pytest
+import torch
+
+from jax_distributed_tuts_amd.runtime.launch import spawn
+
+from . import dist_workers as W
+from .oracle import check_grad, mlp_grads_fp64, sgd_grads
+
+
+def _load(d, name, ws):
+    return [torch.load(os.path.join(d, f"{name}_r{r}.pt"), weights_only=True) for r in range(ws)]
+
+
+def _batch():
+    from data_paral import synthetic_batch
+    from jax_distributed_tuts_amd.utils.config import dp_config
+
+    return synthetic_batch(dp_config(), 70)
+
+
+CLS = ["input_dense", "output_dense"]
+
+
+def _check_all(got, want, names=None):
+    names = names or sorted(want)
+    for k in names:
+        check_grad(got[k], want[k], k)
+
+
+# ----------------------------------------------------------------------------- one device
+@pytest.mark.parametrize("accum", ["loop", "scan", "fused"])
+def test_single_device_sgd_grad_matches_fp64(accum):
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
+    from jax_distributed_tuts_amd.utils.train_state import sgd
+
+    st = init_dp(Classifier(dropout_rate=0.0), sgd(1.0), 69, "cpu")
+    tr = DataParallelTrainer(st, None, DPConfig(4, accum))
+    before = {k: v.clone() for k, v in st.params.state_dict().items()}
+    b = _batch()
+    tr.step(b)
+    got = sgd_grads(before, st.params.state_dict())
+    _check_all(got, mlp_grads_fp64(before, CLS, b.inputs, b.labels, n_mb=4))
+
+
+def test_single_device_dropout_grad_matches_fp64_with_mirrored_masks():
+    """Dropout on: the oracle applies the engine's own Philox keep-masks (mirrored
+    bit-exactly on the CPU): minibatch i of step 0 draws layer l's mask from
+    stream (seed, (l << 1) + ((step * n_mb + i) << 32)) over its [mb, H] block."""
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.ops.kernels import dropout_mask
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, fold_rng_over_axis, init_dp
+    from jax_distributed_tuts_amd.utils.train_state import sgd
+
+    st = init_dp(Classifier(dropout_rate=0.1), sgd(1.0), 69, "cpu")
+    tr = DataParallelTrainer(st, None, DPConfig(4, "loop"))
+    before = {k: v.clone() for k, v in st.params.state_dict().items()}
+    b = _batch()
+    tr.step(b)
+    seed = fold_rng_over_axis(st.rng, None, "data") & 0xFFFFFFFF
+    masks = [[dropout_mask(seed, (0 << 1) + (i << 32), (32, 512), 0.9), None] for i in range(4)]
+    want = mlp_grads_fp64(before, CLS, b.inputs, b.labels, masks=masks, keep=0.9, n_mb=4)
+    got = sgd_grads(before, st.params.state_dict())
+    _check_all(got, want)
+    # and the masks matter: without them the oracle is far off
+    nodrop = mlp_grads_fp64(before, CLS, b.inputs, b.labels, n_mb=4)
+    with pytest.raises(AssertionError):
+        check_grad(got["input_dense/kernel"], nodrop["input_dense/kernel"])
+
+
+# ----------------------------------------------------------------------------- gloo fake cluster
+def _oracle_for_classifier(before):
+    b = _batch()
+    return mlp_grads_fp64(before, CLS, b.inputs, b.labels, n_mb=4)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("ws,accum", [(2, "loop"), (4, "loop"), (2, "fused"), (2, "scan")])
+def test_dp_sgd_grad_matches_fp64(tmp_path, ws, accum):
+    spawn(functools.partial(W.grad_probe, kind="dp", accum=accum), ws, str(tmp_path))
+    res = _load(tmp_path, "probe_dp", ws)
+    want = _oracle_for_classifier(res[0]["before"])
+    for o in res:
+        _check_all(sgd_grads(o["before"], o["after"]), want)
+
+
+@pytest.mark.slow
+def test_oracle_detects_missing_inverse_n(tmp_path):
+    """The same probe with the 1/N of pmean deliberately dropped must FAIL."""
+    spawn(functools.partial(W.grad_probe, kind="dp_no_inv_n"), 2, str(tmp_path))
+    o = _load(tmp_path, "probe_dp_no_inv_n", 2)[0]
+    want = _oracle_for_classifier(o["before"])
+    with pytest.raises(AssertionError, match=r"scale (1\.99|2\.0)"):
+        _check_all(sgd_grads(o["before"], o["after"]), want)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("gather_once", [False, True])
+def test_fsdp_sgd_grad_matches_fp64(tmp_path, gather_once):
+    spawn(functools.partial(W.grad_probe, kind="fsdp", gather_once=gather_once), 2, str(tmp_path))
+    res = _load(tmp_path, "probe_fsdp", 2)
+    want = _oracle_for_classifier(res[0]["before"])
+    for o in res:
+        _check_all(sgd_grads(o["before"], o["after"]), want)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("ws,dp", [(2, 1), (4, 1), (4, 2)])
+def test_pipeline_sgd_grad_matches_fp64(tmp_path, ws, dp):
+    """GPipe over S stages and hybrid DP x PP: each stage's applied gradient ==
+    the fp64 gradient of the whole 5-layer MLP (784-512x3-10)."""
+    from pipeline_parallel import pp_mlp_dims
+    from jax_distributed_tuts_amd.models.mlp import MLP
+    from jax_distributed_tuts_amd.utils.config import dp_config
+
+    spawn(functools.partial(W.grad_probe, kind="pp", dp=dp), ws, str(tmp_path))
+    res = _load(tmp_path, "probe_pp", ws)
+    before, got = {}, {}
+    for o in res:
+        before.update(o["before"])
+        for k, v in sgd_grads(o["before"], o["after"]).items():
+            if k in got:  # the other data replica of the same stage: identical
+                torch.testing.assert_close(v, got[k], rtol=0, atol=0)
+            got[k] = v
+    model = MLP(pp_mlp_dims(dp_config(), 3), dropout_rate=0.0)
+    b = _batch()
+    want = mlp_grads_fp64(before, model.names, b.inputs, b.labels, n_mb=4)
+    assert set(got) == set(want)
+    _check_all(got, want)
+
+
+@pytest.mark.slow
+def test_replication_check_catches_desynchronised_rank(tmp_path):
+    spawn(W.replication_desync, 2, str(tmp_path))
+    for o in _load(tmp_path, "repdesync", 2):
+        assert "diverged" in o["res"] and "param/output_dense/bias" in o["res"], o["res"]

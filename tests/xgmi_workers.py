@@ -297,3 +297,63 @@ def fault_timeout(outdir):
     _save(outdir, "fault", res)
     comm.close()
     p2p.close()
+
+
+def grad_probe_xgmi(outdir, kind, dp=1):
+    """One step (dropout off) of a strategy over the xGMI kernels with a
+    scale-revealing optimizer -- plain SGD lr 1, or (``dp_adam_eps``) the fused
+    xGMI all-reduce + AdamW kernel with eps = 10 -- saving params before / after
+    (tests/test_grad_scale_gpu.py)."""
+    from data_paral import synthetic_batch
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp, shard_batch
+    from jax_distributed_tuts_amd.runtime import dist as D
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw, sgd
+
+    dev = D.device()
+    cfg = dp_config()
+
+    def cpu(d):
+        return {k: v.detach().float().cpu().clone() for k, v in d.items()}
+
+    if kind in ("dp_sgd", "dp_adam_eps"):
+        mesh = D.Mesh({"data": D.world_size()})
+        tx = sgd(1.0) if kind == "dp_sgd" else adamw(1.0, eps=10.0, weight_decay=0.0)
+        st = init_dp(Classifier(dropout_rate=0.0), tx, 69, dev, None)
+        b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
+        tr = DataParallelTrainer(st, mesh, DPConfig(4, "kernel", comm="xgmi"))
+        before = cpu(st.params.state_dict())
+        tr.step(Batch(b.inputs.to(dev), b.labels.to(dev)))
+        tr.finalize()
+        after = cpu(st.params.state_dict())
+        comm = tr.comm_backend
+    elif kind == "fsdp_sgd":
+        from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
+
+        mesh = D.Mesh({"data": D.world_size()})
+        st = init_fsdp(Classifier(dropout_rate=0.0), sgd(1.0), 69, dev, mesh, "data", 16)
+        b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
+        tr = FSDPTrainer(st, mesh, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=True,
+                                              comm="xgmi"))
+        before = cpu(tr.full_params())
+        tr.step(Batch(b.inputs.to(dev), b.labels.to(dev)))
+        tr.finalize()
+        after = cpu(tr.full_params())
+        comm = tr.comm_backend
+    elif kind == "pp_sgd":
+        from pipeline_parallel import build_mlp_pipeline
+
+        mesh = D.Mesh({"data": dp, "pipe": D.world_size() // dp})
+        tr = build_mlp_pipeline(cfg, mesh, dev, n_hidden_layers=3, dropout_rate=0.0, num_microbatches=4, comm="xgmi",
+                                tx=sgd(1.0))
+        b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
+        before = cpu(tr.state.params.state_dict())
+        tr.step(Batch(b.inputs.to(dev), b.labels.to(dev)))
+        tr.finalize()
+        after = cpu(tr.state.params.state_dict())
+        comm = tr.comm_backend
+    else:
+        raise ValueError(kind)
+    torch.cuda.synchronize()
+    _save(outdir, f"gpx_{kind}", {"before": before, "after": after, "comm": comm})

@@ -65,6 +65,27 @@ class MLP:
         self.names = list(names)
         self.layer_id_base = layer_id_base  # folds into the dropout stream so stages differ
 
+    # ------------------------------------------------------------------ flax-style apply
+    def __call__(self, variables, x: torch.Tensor, train: bool = False, rngs: Optional[dict] = None) -> torch.Tensor:
+        """``model.apply({"params": params}, x, train=..., rngs={"dropout": key})`` of
+        the reference (data_paral.py:180, 86-100) as a DIFFERENTIABLE forward: nested
+        ``params[layer]["kernel" | "bias"]`` tensors, one ``ops.autograd.dense``
+        (GEMM + bias + act + dropout epilogue on the HIP kernels) per layer, fp32
+        logits.  Used by reference-style ``loss_fn``s through ``util.accum_grads``."""
+        from ..ops.autograd import dense
+
+        params = variables["params"] if "params" in variables else variables
+        keep = 1.0 - self.dropout_rate if train else 1.0
+        seed = int((rngs or {}).get("dropout", 0)) & 0xFFFFFFFF
+        h = x
+        for i, n in enumerate(self.names):
+            hid = self._hidden(i)
+            h = dense(h, params[n]["kernel"], params[n]["bias"], act=self.act if hid else "none",
+                      keep=keep if hid else 1.0, seed=seed, offset=(self.layer_id_base + i) << 1)
+        return h.float()
+
+    apply = __call__
+
     # ------------------------------------------------------------------ params
     def param_specs(self) -> List[ParamSpec]:
         out = []

@@ -19,7 +19,12 @@ from typing import Dict, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
-_STATE: Dict[str, object] = {"device": None, "backend": None}
+_STATE: Dict[str, object] = {"device": None, "backend": None, "mesh": None}
+
+
+def current_mesh() -> Optional["Mesh"]:
+    """The most recently constructed :class:`Mesh` of this process (or None)."""
+    return _STATE.get("mesh")  # type: ignore[return-value]
 
 
 def is_initialized() -> bool:
@@ -127,6 +132,7 @@ class Mesh:
                 g = dist.group.WORLD
             self._groups[a] = g
             self._group_ranks[a] = tuple(line)
+        _STATE["mesh"] = self
 
     def _coords(self, r: int) -> Tuple[int, ...]:
         c = []

@@ -33,7 +33,18 @@ def split(key: int, num: int = 2) -> List[int]:
     return [fold_in(key, 0x5EED0000 + i) for i in range(num)]
 
 
-def fold_rng_over_axis(rng: int, mesh, axis_name: str) -> int:
-    """Give each member of ``axis_name`` its own stream (data_paral.py:28-34)."""
+def fold_rng_over_axis(rng: int, mesh, axis_name: str | None = None) -> int:
+    """Give each member of ``axis_name`` its own stream (data_paral.py:28-34).
+
+    Also callable with the reference's signature ``fold_rng_over_axis(rng,
+    axis_name)``: the axis is then looked up on the most recently built
+    :class:`~jax_distributed_tuts_amd.runtime.dist.Mesh` of this process (the
+    analogue of the enclosing ``shard_map``'s mesh); no mesh -> index 0."""
+    if isinstance(mesh, str) and axis_name is None:
+        from ..runtime.dist import current_mesh
+
+        mesh, axis_name = current_mesh(), mesh
+        if mesh is not None and axis_name not in mesh.axis_names:
+            mesh = None
     idx = 0 if mesh is None else mesh.axis_index(axis_name)
     return fold_in(rng, idx)

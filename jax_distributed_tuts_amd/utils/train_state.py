@@ -16,8 +16,9 @@
 """
 from __future__ import annotations
 
+import inspect
 from dataclasses import dataclass, field
-from typing import Any, Callable, Dict, Optional, Tuple
+from typing import Any, Callable, Dict, Optional, Tuple, Union
 
 import torch
 
@@ -27,6 +28,9 @@ from .metrics import Metrics
 from . import rng as R
 
 Pytree = Any
+# pipeline_parallel.py:24-26 of the reference: a parameter leaf is a plain array or
+# an axis-annotated shard (flax ``nn.Partitioned`` -> parallel.fsdp.Partitioned)
+Parameter = Union[torch.Tensor, "Partitioned"]  # noqa: F821 (forward ref, parallel/fsdp.py)
 
 
 # ---------------------------------------------------------------------------- batch
@@ -171,18 +175,79 @@ def _metrics_add(a, b):
     return {k: tuple(x + y for x, y in zip(a[k], b[k])) for k in a}
 
 
+def _detach_metrics(m):
+    return {k: tuple(x.detach() if torch.is_tensor(x) else x for x in v) for k, v in m.items()}
+
+
+def is_reference_loss_fn(loss_fn: Callable) -> bool:
+    """True for a reference-contract ``loss_fn(params, apply_fn, batch, rng) ->
+    (mean_loss, metrics)`` whose gradient must come from autograd (data_paral.py:
+    171-189); False for the engine contract, which also accepts
+    ``minibatch_index=`` / ``state=`` keywords and writes its own gradient into
+    ``params.grad`` (beta = 1 GEMM epilogues)."""
+    try:
+        sig = inspect.signature(loss_fn)
+    except (TypeError, ValueError):
+        return True
+    ps = sig.parameters
+    return not ("minibatch_index" in ps or "state" in ps
+                or any(p.kind == inspect.Parameter.VAR_KEYWORD for p in ps.values()))
+
+
+def param_tree(params: FlatParams, requires_grad: bool = True) -> Tuple[Dict[str, Any], Dict[str, torch.Tensor]]:
+    """The flax-style nested pytree ``{layer: {"kernel": W, "bias": b}}`` over the
+    fp32 master views (leaves share storage with ``params.master``), and the flat
+    ``{path: leaf}`` map autograd differentiates."""
+    leaves = {n: params.p(n).detach().requires_grad_(requires_grad) for n in params.names()}
+    tree: Dict[str, Any] = {}
+    for path, t in leaves.items():
+        node = tree
+        parts = path.split("/")
+        for part in parts[:-1]:
+            node = node.setdefault(part, {})
+        node[parts[-1]] = t
+    return tree, leaves
+
+
+def value_and_grad_into(loss_fn: LossFn, state: "TrainState", batch: Batch, rng: int):
+    """``jax.value_and_grad(loss_fn, has_aux=True)`` (util.py:53,65) for a
+    reference-contract loss: differentiate w.r.t. the parameter pytree with torch
+    autograd and ACCUMULATE the gradient into ``params.grad`` (the grads "+" of
+    util.py:74).  Returns (mean loss, metrics), detached."""
+    P = state.params
+    tree, leaves = param_tree(P)
+    loss, metrics = loss_fn(tree, state.apply_fn, batch, rng)
+    names = [n for n, t in leaves.items()]
+    grads = torch.autograd.grad(loss, [leaves[n] for n in names], allow_unused=True)
+    for n, g in zip(names, grads):
+        if g is not None:
+            P.g(n).add_(g.to(P.grad.dtype))
+    return loss.detach(), _detach_metrics(metrics)
+
+
 def accum_grads_loop(batch: Batch, state: TrainState, key: int, n_minbatch: int,
                      loss_fn: LossFn) -> Tuple[GradBuffer, Metrics]:
-    """util.py:41-78.  ``loss_fn(params, apply_fn, minibatch, rng, minibatch_index=i,
-    state=state)`` accumulates its gradient into ``params.grad`` (beta = 1) and
-    returns ``(mean_loss, metrics)``."""
+    """util.py:41-78.  Two ``loss_fn`` contracts (:func:`is_reference_loss_fn`):
+
+    * reference: ``loss_fn(params_pytree, apply_fn, minibatch, rng) -> (mean_loss,
+      metrics)`` built from differentiable torch ops / ``state.apply_fn`` -- its
+      gradient is taken with autograd and accumulated into ``params.grad``;
+    * engine (fast path): ``loss_fn(params, apply_fn, minibatch, rng,
+      minibatch_index=i, state=state)`` accumulates its own gradient into
+      ``params.grad`` (beta = 1 kernels).
+    Either way the returned :class:`GradBuffer` is the SUM with ``scale`` =
+    1/n_minbatch (the mean of util.py:77, applied lazily by the optimizer)."""
     bs = batch.size
     mb = bs // n_minbatch
     keys = R.split(key, n_minbatch)
     metrics = None
+    ref = is_reference_loss_fn(loss_fn)
     for i in range(n_minbatch):
         minibatch = batch.slice(i * mb, mb)
-        _, m = loss_fn(state.params, state.apply_fn, minibatch, keys[i], minibatch_index=i, state=state)
+        if ref:
+            _, m = value_and_grad_into(loss_fn, state, minibatch, keys[i])
+        else:
+            _, m = loss_fn(state.params, state.apply_fn, minibatch, keys[i], minibatch_index=i, state=state)
         metrics = _metrics_add(metrics, m)
     return GradBuffer(state.params, 1.0 / n_minbatch), metrics
 
@@ -202,7 +267,9 @@ def accum_grads_scan(batch: Batch, state: TrainState, key: int, n_minbatch: int,
     bs = batch.size
     mb = bs // n_minbatch
     dev = batch.inputs.device
-    if dev.type != "cuda":
+    if dev.type != "cuda" or is_reference_loss_fn(loss_fn):
+        # CPU, or an autograd (reference-contract) loss: the rolled loop runs eagerly,
+        # one minibatch at a time with its own split key (util.py:91, 95-111)
         return accum_grads_loop(batch, state, key, n_minbatch, loss_fn)
     # device-resident slot the captured step reads its minibatch from
     xin = torch.empty((mb,) + tuple(batch.inputs.shape[1:]), dtype=batch.inputs.dtype, device=dev)

@@ -1,6 +1,6 @@
 """Drop-in ``util.py`` API of the reference (util.py:1-185), MI355X-native.
 
-Same names and signatures: ``print_exception``, ``Pytree``, ``Metrics``,
+Same names and signatures: ``print_exception``, ``Pytree``, ``Metrics``, ``Parameter``,
 ``TrainState``, ``Batch``, ``sim_multiCPU_dev``, ``accum_grads_loop``,
 ``accum_grads_scan``, ``accum_grads``, ``print_metrics``, ``get_num_params``.
 Implementations live in ``jax_distributed_tuts_amd.utils``.
@@ -14,6 +14,7 @@ from jax_distributed_tuts_amd.utils.train_state import (  # noqa: F401
     AdamW,
     Batch,
     GradBuffer,
+    Parameter,
     Pytree,
     SGD,
     TrainState,
@@ -24,6 +25,8 @@ from jax_distributed_tuts_amd.utils.train_state import (  # noqa: F401
     get_num_params,
     sgd,
 )
+from jax_distributed_tuts_amd.utils.rng import PRNGKey, fold_rng_over_axis, split  # noqa: F401
+from jax_distributed_tuts_amd.ops.autograd import softmax_cross_entropy_with_integer_labels  # noqa: F401
 
 
 def sim_multiCPU_dev(device_count: int = 8):

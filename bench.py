@@ -44,19 +44,20 @@ def build_dp(args, dev):
     from jax_distributed_tuts_amd.models.mlp import Classifier
     from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp, shard_batch
     from jax_distributed_tuts_amd.utils.config import dp_config
-    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw, sgd
 
     cfg = dp_config()
     cfg.model.num_layers = args.num_layers
     mesh = Mesh({"data": D.world_size()})
     model = Classifier.from_config(cfg.model)
-    state = init_dp(model, adamw(cfg.optimizer.learning_rate), cfg.seed, dev, mesh)
+    tx = adamw(cfg.optimizer.learning_rate) if args.optimizer == "adamw" else sgd(cfg.optimizer.learning_rate)
+    state = init_dp(model, tx, cfg.seed, dev, mesh)
     batch = shard_batch(synthetic_batch(cfg, cfg.seed + 1), mesh, "data")
     batch = Batch(batch.inputs.to(dev), batch.labels.to(dev))
     tr = DataParallelTrainer(state, mesh, DPConfig(cfg.optimizer.num_minibatches, args.accum, comm=args.comm))
     desc = {"model": f"tutorial MLP {'-'.join(map(str, model.dims))} (SiLU, dropout 0.1)",
             "global_batch": cfg.data.batch_size, "seq_len": None, "num_minibatches": cfg.optimizer.num_minibatches,
-            "parallelism": f"dp{D.world_size()}", "accum": args.accum}
+            "parallelism": f"dp{D.world_size()}", "accum": args.accum, "optimizer": args.optimizer}
     return tr, batch, desc
 
 
@@ -116,6 +117,46 @@ def build_pp(args, dev):
     return tr, batch, desc
 
 
+def comm_sweep(tr, dev, iters: int = 20):
+    """T5 evidence from the job itself (N > 1, GPU, untimed, after the measured
+    region): median per-call device time of this trainer's gradient all-reduce
+    transports on the same data -- the xGMI two-shot kernel (comm/xgmi.py) and
+    RCCL's all-reduce (nccl process group only) -- at 64 KiB, the DP bucket size
+    and (RCCL) 16 MiB.  Every rank runs the same sequence."""
+    import torch.distributed as dist
+
+    xg = getattr(tr, "xg", None)
+    rccl = D.backend() == "nccl"
+    if not (xg is not None or rccl):
+        return None
+    bucket = int(tr.state.params.grad.numel())
+    out = []
+    for n in (16_384, bucket, 4 << 20):
+        x = torch.ones(n, device=dev)
+        row = {"bytes": n * 4}
+
+        def timed(fn):
+            fn()
+            torch.cuda.synchronize()
+            D.barrier()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(iters):
+                fn()
+            b.record()
+            b.synchronize()
+            return round(a.elapsed_time(b) * 1e3 / iters, 2)
+
+        if xg is not None and n <= xg.capacity // 2:
+            row["xgmi_us"] = timed(lambda: xg.all_reduce_(x))
+        if rccl:
+            row["rccl_us"] = timed(lambda: dist.all_reduce(x))
+        out.append(row)
+    if xg is not None and xg.error():
+        raise RuntimeError("xgmi all-reduce timed out during the comm sweep")
+    return out
+
+
 def pick_steps_per_graph(steps: int, cap: int) -> int:
     """Steps per captured graph: all of them when steps <= cap (one replay, one host
     launch for the whole timed region), else the largest divisor of steps <= cap
@@ -150,6 +191,10 @@ def main():
     ap.add_argument("--steps-per-graph", type=int, default=None,
                     help="complete training steps recorded per hipGraph (amortises the replay launch); default: "
                          "all timed steps in one graph when --steps <= 200 (DP), else the largest divisor <= the cap")
+    ap.add_argument("--no-comm-sweep", action="store_true",
+                    help="skip the untimed RCCL-vs-xGMI all-reduce sweep reported for N > 1")
+    ap.add_argument("--optimizer", choices=["adamw", "sgd"], default="adamw",
+                    help="DP: adamw (the reference's optax.adamw) or sgd (the fused SGD kernel)")
     args = ap.parse_args()
 
     # N ranks for --gpus N: start them here (this process never touches the GPU) ...
@@ -212,9 +257,11 @@ def main():
             ts.append(a.elapsed_time(b))
         ts.sort()
         p50, p90 = ts[len(ts) // 2], ts[int(0.9 * len(ts))]
-    coll_ms = None
+    coll_ms = sweep = None
     if hasattr(tr, "time_collective"):
         coll_ms = tr.time_collective(batch, iters=min(20, max(5, args.steps)))
+    if on_gpu and ws > 1 and args.strategy == "dp" and not args.no_comm_sweep:
+        sweep = comm_sweep(tr, dev)
     if hasattr(tr, "finalize"):
         tr.finalize()
     m = (tr.gather_metrics() if hasattr(tr, "gather_metrics") else tr.metrics).detach().float().cpu()
@@ -233,7 +280,7 @@ def main():
                            "comm": getattr(tr, "comm_backend", None) or D.backend() or "none",
                            "process_group": D.backend() or "none",
                            "xgmi_selftest": getattr(tr, "xgmi_status", "n/a"),
-                           "collective_ms_p50": coll_ms}}
+                           "collective_ms_p50": coll_ms, "comm_sweep": sweep}}
         print(json.dumps(out), flush=True)
     D.shutdown()
 

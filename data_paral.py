@@ -22,10 +22,10 @@ from jax_distributed_tuts_amd.models.mlp import Classifier
 from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp, shard_batch
 from jax_distributed_tuts_amd.runtime import dist as D
 from jax_distributed_tuts_amd.runtime.dist import Mesh
-from jax_distributed_tuts_amd.utils.cli import add_common_args, entry_main
+from jax_distributed_tuts_amd.utils.cli import add_common_args, entry_main, make_tx
 from jax_distributed_tuts_amd.utils.config import dp_config
 from jax_distributed_tuts_amd.utils.metrics import print_metrics
-from jax_distributed_tuts_amd.utils.train_state import Batch, adamw, get_num_params
+from jax_distributed_tuts_amd.utils.train_state import Batch, get_num_params
 
 
 def synthetic_batch(cfg, seed: int) -> Batch:
@@ -42,7 +42,7 @@ def main(args):
     dev = D.device()
     mesh = Mesh({"data": D.world_size()})
     model = Classifier.from_config(cfg.model)
-    state = init_dp(model, adamw(cfg.optimizer.learning_rate), cfg.seed, dev, mesh)
+    state = init_dp(model, make_tx(args, cfg.optimizer.learning_rate), cfg.seed, dev, mesh)
     batch = shard_batch(synthetic_batch(cfg, cfg.seed + 1), mesh, "data")
     batch = Batch(batch.inputs.to(dev), batch.labels.to(dev))
     trainer = DataParallelTrainer(state, mesh, DPConfig(cfg.optimizer.num_minibatches, args.accum, comm=args.comm))

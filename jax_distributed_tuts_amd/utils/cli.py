@@ -31,6 +31,8 @@ def add_common_args(ap: argparse.ArgumentParser, steps: int, accum_default: str 
                          "(the debug replacement of the reference's disabled shard_map check_rep)")
     ap.add_argument("--deterministic", action="store_true",
                     help="fixed-order reductions only (no fp32 atomics): bitwise-reproducible runs")
+    ap.add_argument("--optimizer", choices=["adamw", "sgd"], default="adamw",
+                    help="adamw: the reference's optax.adamw (fused AdamW kernels); sgd: the fused SGD kernel")
     ap.add_argument("--steps", type=int, default=steps)
     ap.add_argument("--num-layers", type=int, default=2)
     ap.add_argument("--accum", choices=list(accum_choices), default=accum_default,
@@ -81,6 +83,13 @@ def maybe_profile(args, script: str):
     env = dict(os.environ, JDT_PROFILED="1", TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     print("[profile] " + " ".join(cmd), file=sys.stderr, flush=True)
     sys.exit(subprocess.call(cmd, env=env))
+
+
+def make_tx(args, lr: float):
+    """The optimizer named by ``--optimizer`` at the config's learning rate."""
+    from .train_state import adamw, sgd
+
+    return sgd(lr) if getattr(args, "optimizer", "adamw") == "sgd" else adamw(lr)
 
 
 def entry_main(main, args, script: str):

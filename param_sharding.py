@@ -22,9 +22,9 @@ from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init
 from jax_distributed_tuts_amd.runtime import dist as D
 from jax_distributed_tuts_amd.runtime.dist import Mesh
 from jax_distributed_tuts_amd.utils.config import fsdp_config
-from jax_distributed_tuts_amd.utils.cli import add_common_args, entry_main
+from jax_distributed_tuts_amd.utils.cli import add_common_args, entry_main, make_tx
 from jax_distributed_tuts_amd.utils.metrics import print_metrics
-from jax_distributed_tuts_amd.utils.train_state import Batch, adamw, get_num_params
+from jax_distributed_tuts_amd.utils.train_state import Batch, get_num_params
 
 
 def main(args):
@@ -34,7 +34,7 @@ def main(args):
     axis = cfg.model.data_axis_name
     mesh = Mesh({axis: D.world_size()})
     model = Classifier.from_config(cfg.model)
-    state = init_fsdp(model, adamw(cfg.model.lr), cfg.seed, dev, mesh, axis, cfg.model.min_weight_size)
+    state = init_fsdp(model, make_tx(args, cfg.model.lr), cfg.seed, dev, mesh, axis, cfg.model.min_weight_size)
     batch = shard_batch(synthetic_batch(cfg, cfg.seed + 1), mesh, axis)
     batch = Batch(batch.inputs.to(dev), batch.labels.to(dev))
     tr = FSDPTrainer(state, mesh, FSDPConfig(cfg.num_minibatches, cfg.model.min_weight_size, axis,

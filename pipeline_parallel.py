@@ -23,7 +23,7 @@ from jax_distributed_tuts_amd.models.mlp import MLP
 from jax_distributed_tuts_amd.runtime import dist as D
 from jax_distributed_tuts_amd.runtime.dist import Mesh
 from jax_distributed_tuts_amd.utils import rng as R
-from jax_distributed_tuts_amd.utils.cli import add_common_args, entry_main
+from jax_distributed_tuts_amd.utils.cli import add_common_args, entry_main, make_tx
 from jax_distributed_tuts_amd.utils.config import dp_config
 from jax_distributed_tuts_amd.utils.metrics import print_metrics
 from jax_distributed_tuts_amd.utils.train_state import Batch, TrainState, adamw
@@ -59,7 +59,8 @@ def main(args):
         tr, lm_cfg = build_lm_pipeline(mesh, dev, num_microbatches=args.microbatches)
         batch = shard_batch(lm_batch(lm_cfg, seed=1), mesh, "data")
     else:
-        tr = build_mlp_pipeline(cfg, mesh, dev, args.hidden_layers, num_microbatches=args.microbatches)
+        tr = build_mlp_pipeline(cfg, mesh, dev, args.hidden_layers, num_microbatches=args.microbatches,
+                                tx=make_tx(args, cfg.optimizer.learning_rate))
         batch = shard_batch(synthetic_batch(cfg, cfg.seed + 1), mesh, "data")
     batch = Batch(batch.inputs.to(dev), batch.labels.to(dev))
     if D.rank() == 0:

@@ -83,6 +83,9 @@ struct MdArgs {
   float lr, beta1, beta2, eps, wd, gscale;
   float* running;
   unsigned long long* stamps;   // diagnostic: per-workgroup s_memrealtime at phase ends [grid][8] (null = off)
+  // pipeline-stage use (parallel/fused_stage.py)
+  int accumulate;       // mode 0: gW/gb/gWh/gbh/mslot += this launch's values (microbatch accumulation)
+  const bf16_t* dH;     // bwd BND: gradient w.r.t. this layer's output H_i [M][N] (from the next stage)
 };
 
 // Slots 0-4: s_memrealtime at the kernel's phase ends (tools/stamp_deep.py).
@@ -303,7 +306,10 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
 }
 
 // ---------------------------------------------------------------------------- backward
-template <int K_IN, bool TOP, int C, int KC, int NN, bool XCD>
+// BND (pipeline stage boundary, !TOP): dZ_i = dH * G_i -- the gradient w.r.t. this
+// layer's output arrives from the next pipeline stage instead of being recomputed
+// from dZ_{i+1} W_{i+1}^T.
+template <int K_IN, bool TOP, int C, int KC, int NN, bool XCD, bool BND = false>
 __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   constexpr int NT = MD_NT, NW = MD_NW, MPM = MD_MPM;
   constexpr int LDM = MPM + 8;
@@ -323,7 +329,9 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   constexpr int LDWN = NN + 8;
   constexpr int WNCH = 16 * NN / 8;                    // 16-byte chunks of the tile
   static_assert(TOP || WNCH % MD_NT == 0, "Wn tile chunking");
-  __shared__ __attribute__((aligned(16))) bf16_t wnS[TOP ? 8 : 16 * LDWN];
+  static_assert(!(TOP && BND), "TOP and BND are exclusive");
+  constexpr bool WN = !TOP && !BND;   // dZ_i from the next layer of this launch sequence
+  __shared__ __attribute__((aligned(16))) bf16_t wnS[WN ? 16 * LDWN : 8];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int M = a.M, N = a.N, Mp = (M + 31) & ~31;
   int bx = blockIdx.x, by = blockIdx.y;
@@ -345,7 +353,7 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   // !TOP: the step counter is loaded FIRST (only W_{i+1}'s parity buffer depends on
   // it, and those loads are issued last, after one round trip); TOP: last.
   int step = 0;
-  if constexpr (!TOP) {
+  if constexpr (WN) {
     step = a.step[lz];
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -353,8 +361,9 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   int lab = 0;
   float4 gv;
   bf16_t hv[4];
-  bf16x8 dzf[TOP ? 1 : NKS];
-  u32x4 wq[TOP ? 1 : WNCH / MD_NT];
+  bf16x8 dzf[WN ? NKS : 1];
+  u32x4 wq[WN ? WNCH / MD_NT : 1];
+  unsigned long long dhq = 0;
   float whv0 = 0.f, whv1 = 0.f;
   if constexpr (TOP) {
     const long lo = (long)min(tid, M - 1) * C;
@@ -368,6 +377,13 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
     const long wo = (long)(j0 + wi / C) * C + wi % C;
     whv0 = bf2f(a.Wh0[wo]);
     whv1 = bf2f(a.Wh1[wo]);
+  } else if constexpr (BND) {
+    // wave w, lane: rows 16w + 4(lane>>4) .. +3 of column j0 + (lane&15) of dH and G
+    const int row0 = w * 16 + (lane >> 4) * 4, col = j0 + (lane & 15);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      dhq |= (unsigned long long)a.dH[(long)min(row0 + e, M - 1) * N + col] << (16 * e);
+    gv = *reinterpret_cast<const float4*>(a.G + ((long)(min(row0, M - 1) >> 2) * N + col) * 4);
   } else {
     // wave w: rows 16w..16w+15 of dZ_i[:, blk] = dZ_{i+1} . W_{i+1}[blk, :]^T
     const int row = min(w * 16 + (lane & 15), M - 1);
@@ -414,9 +430,9 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
     }
   }
   __builtin_amdgcn_sched_barrier(0);
-  if constexpr (TOP) step = a.step[lz];
+  if constexpr (!WN) step = a.step[lz];
   const int par = step & 1;
-  if constexpr (!TOP) {
+  if constexpr (WN) {
     const bf16_t* Wn = par ? a.Wn1 : a.Wn0;
 #pragma unroll
     for (int t = 0; t < WNCH / MD_NT; ++t) {
@@ -492,18 +508,25 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       *reinterpret_cast<uint2*>(&hT[gn * LDM + rg * 4]) =
           make_uint2((unsigned)hv[0] | ((unsigned)hv[1] << 16), (unsigned)hv[2] | ((unsigned)hv[3] << 16));
   } else {
+    if constexpr (WN) {
 #pragma unroll
-    for (int t = 0; t < WNCH / MD_NT; ++t) {
-      const int c = tid + t * MD_NT;
-      *reinterpret_cast<u32x4*>(&wnS[(c / (NN / 8)) * LDWN + (c % (NN / 8)) * 8]) = wq[t];
+      for (int t = 0; t < WNCH / MD_NT; ++t) {
+        const int c = tid + t * MD_NT;
+        *reinterpret_cast<u32x4*>(&wnS[(c / (NN / 8)) * LDWN + (c % (NN / 8)) * 8]) = wq[t];
+      }
+      __syncthreads();
     }
-    __syncthreads();
     if (w * 16 < Mp) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (WN) {
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8 wnf = *reinterpret_cast<const bf16x8*>(&wnS[(lane & 15) * LDWN + ks * 32 + 8 * (lane >> 4)]);
-        acc = mfma16x16x32(dzf[ks], wnf, acc);
+        for (int ks = 0; ks < NKS; ++ks) {
+          const bf16x8 wnf = *reinterpret_cast<const bf16x8*>(&wnS[(lane & 15) * LDWN + ks * 32 + 8 * (lane >> 4)]);
+          acc = mfma16x16x32(dzf[ks], wnf, acc);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] = bf2f((bf16_t)(dhq >> (16 * e)));
       }
       const int row0 = w * 16 + (lane >> 4) * 4, col = j0 + (lane & 15);
       const float gfac[4] = {gv.x, gv.y, gv.z, gv.w};
@@ -546,7 +569,7 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
         Wsn[idx] = pb;
         wtp[e >> 1] |= (unsigned)pb << (16 * (e & 1));
       } else {
-        a.gW[idx] = acc[e];
+        a.gW[idx] = (a.accumulate ? op[e] : 0.f) + acc[e];   // mode 0 loaded the old grad into op
       }
     }
     if (a.fuse_opt && a.WTout)
@@ -574,17 +597,17 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       if (TOP && ac < C) {
         const long g = (long)(j0 + n) * C + ac;
         if (a.fuse_opt) Whn[g] = f2bf(md_adam(op[e], om[e], ov[e], aw[e], ak, a.pWh + g, a.mWh + g, a.vWh + g));
-        else a.gWh[g] = aw[e];
+        else a.gWh[g] = (a.accumulate ? op[e] : 0.f) + aw[e];
       }
       if (ac == 0) {
         const int j = j0 + n;
         if (a.fuse_opt) a.sb[j] = f2bf(md_adam(bp[e], bm[e], bvv[e], ab[e], ak, a.pb + j, a.mb + j, a.vb + j));
-        else a.gb[j] = ab[e];
+        else a.gb[j] = (a.accumulate ? bp[e] : 0.f) + ab[e];
       }
     }
     if (TOP && lead && lane < C) {
       if (a.fuse_opt) a.sbh[lane] = f2bf(md_adam(qp, qm, qv, ab2[0], ak, a.pbh + lane, a.mbh + lane, a.vbh + lane));
-      else a.gbh[lane] = ab2[0];
+      else a.gbh[lane] = (a.accumulate ? qp : 0.f) + ab2[0];
     }
   }
   MD_STAMP(3);
@@ -596,7 +619,9 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       if (a.fuse_opt && a.running) {
         a.running[0] += L; a.running[1] += (float)M; a.running[2] += Cr; a.running[3] += (float)M;
       } else if (a.mslot) {
-        a.mslot[0] = L; a.mslot[1] = (float)M; a.mslot[2] = Cr; a.mslot[3] = (float)M;
+        const float k = a.accumulate ? 1.f : 0.f;
+        a.mslot[0] = k * a.mslot[0] + L; a.mslot[1] = k * a.mslot[1] + (float)M;
+        a.mslot[2] = k * a.mslot[2] + Cr; a.mslot[3] = k * a.mslot[3] + (float)M;
       }
     }
   }
@@ -620,11 +645,13 @@ int xcd_tiles_enabled();   // mlp_fused.hip (JDT_XCD_TILES)
 JDT_API int jdt_md_args_size() { return (int)sizeof(MdArgs); }
 
 // phase 0: forward of one hidden layer (head = 1: + head logits); phase 1: backward
-// (head = 1: TOP layer, CE through the head).  Instantiated for the tutorial
+// (head = 1: TOP layer, CE through the head; head = 2: pipeline-stage boundary,
+// dZ from the next stage's dH).  Instantiated for the tutorial
 // shapes: K in {784 (fp32 data), 512}, N = NN = 512, C = 10, M <= 128.
 JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) {
   const MdArgs& a = *args;
-  if (a.N != 512 || a.M <= 0 || a.M > MD_MPM || (a.K != 784 && a.K != 512) || (head && a.C != 10)) return -3;
+  if (a.N != 512 || a.M <= 0 || a.M > MD_MPM || (a.K != 784 && a.K != 512) || (head == 1 && a.C != 10)) return -3;
+  if (phase == 0 && head == 2) return -2;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const dim3 blk(MD_NT);
   if (phase == 0) {
@@ -642,6 +669,19 @@ JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) 
     } else {
       if (d) { if (xf) hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10, 16, true, true>), grid, blk, 0, st, a); else hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10, 16, true, false>), grid, blk, 0, st, a); }
       else { if (xf) hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10, 16, false, true>), grid, blk, 0, st, a); else hipLaunchKernelGGL((md_fwd_kernel<512, false, 16, false, 10, 16, false, false>), grid, blk, 0, st, a); }
+    }
+  } else if (head == 2) {
+    // pipeline-stage boundary: dZ_i = dH * G_i
+    if (!a.dH) return -2;
+    const bool x = xcd_tiles_enabled() != 0;
+    if (a.K == 784) {
+      const dim3 g(a.N / 16, 784 / 112);
+      if (x) hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, true, true>), g, blk, 0, st, a);
+      else hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, false, true>), g, blk, 0, st, a);
+    } else {
+      const dim3 g(a.N / 16, 512 / 64);
+      if (x) hipLaunchKernelGGL((md_bwd_kernel<512, false, 10, 64, 512, true, true>), g, blk, 0, st, a);
+      else hipLaunchKernelGGL((md_bwd_kernel<512, false, 10, 64, 512, false, true>), g, blk, 0, st, a);
     }
   } else {
     const bool x = xcd_tiles_enabled() != 0;

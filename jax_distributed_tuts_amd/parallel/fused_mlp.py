@@ -242,7 +242,8 @@ class MdArgs(ctypes.Structure):
                 ("pWh", c_void_p), ("mWh", c_void_p), ("vWh", c_void_p),
                 ("pbh", c_void_p), ("mbh", c_void_p), ("vbh", c_void_p), ("sbh", c_void_p),
                 ("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float), ("wd", c_float),
-                ("gscale", c_float), ("running", c_void_p), ("stamps", c_void_p)]
+                ("gscale", c_float), ("running", c_void_p), ("stamps", c_void_p),
+                ("accumulate", c_int), ("dH", c_void_p)]
 
 
 _lib.declare("jdt_md_layer", c_int, [ctypes.POINTER(MdArgs), c_int, c_int, c_void_p])

@@ -86,6 +86,9 @@ class PipeConfig:
     # microbatch's 1/mb loss weight: the same gradient as the microbatch loop, the
     # dropout masks drawn over the merged rows).  Ignored when the pipe axis > 1.
     merge_single_stage: bool = False
+    # GPU, MLP stages of the tutorial shapes: one fused md_fwd / md_bwd launch per
+    # layer and microbatch (parallel/fused_stage.py) instead of the generic chain
+    fused_stage: bool = True
 
 
 class GPipeTrainer:
@@ -117,6 +120,8 @@ class GPipeTrainer:
         self.xg = None
         self._xg_fused_opt = False
         self.wgrad = K.WGradStream(self.dev) if (self.dev.type == "cuda" and cfg.overlap_wgrad) else None
+        self.stage_engine = None
+        self._engine_tried = False
         if self.dev.type == "cuda" and self.n_dp > 1:
             from ..comm.xgmi import create_for
 
@@ -192,6 +197,10 @@ class GPipeTrainer:
             self.loss_head(out, batch.labels, d, n_parts=n_mb)
             self.model.backward(P, cache, d, dout_is_dz=True, need_dx=False, wgrad=self.wgrad)
             return
+        eng = self._fused_stage(mb, seed)
+        if eng is not None:
+            self._compute_fused(batch, eng, n_mb, mb)
+            return
         caches, dlogits = [None] * n_mb, [None] * n_mb
         # ---- forward fill/drain: tick t, stage s handles microbatch t - s
         for t in range(n_mb + self.S - 1):
@@ -222,6 +231,38 @@ class GPipeTrainer:
             if not self.first:
                 self._send(dx, self.s - 1, n_mb + i)
             caches[i] = None
+
+    def _fused_stage(self, mb: int, seed: int):
+        if not self._engine_tried:
+            self._engine_tried = True
+            from .fused_stage import FusedMLPStage, stage_supported
+
+            if self.cfg.fused_stage and self.wgrad is None and stage_supported(self.model, mb, self.dev):
+                self.stage_engine = FusedMLPStage(self.model, self.state.params, self.cfg.num_microbatches, mb,
+                                                  self.state.step_tensor, seed)
+        return self.stage_engine
+
+    def _compute_fused(self, batch: Batch, eng, n_mb: int, mb: int):
+        """The same GPipe fill/drain schedule on the fused stage kernels."""
+        for t in range(n_mb + self.S - 1):
+            i = t - self.s
+            if not (0 <= i < n_mb):
+                continue
+            if self.first:
+                x = batch.inputs[i * mb:(i + 1) * mb]
+            else:
+                x = self._recv(self.model.input_shape(mb), self.act_dtype, self.s - 1, i)
+            out = eng.forward(i, x)
+            if not self.last:
+                self._send(out, self.s + 1, i)
+        for i in reversed(range(n_mb)):
+            if self.last:
+                dx = eng.backward(i, labels=batch.labels[i * mb:(i + 1) * mb], need_dx=not self.first)
+            else:
+                dh = self._recv(self.model.output_shape(mb), self.act_dtype, self.s + 1, n_mb + i)
+                dx = eng.backward(i, dh=dh, need_dx=not self.first)
+            if not self.first:
+                self._send(dx, self.s - 1, n_mb + i)
 
     def _sync_update(self):
         """sync_gradients(('data','pipe')): stage params are pipe-sharded -> mean over

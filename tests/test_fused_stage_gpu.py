@@ -1,0 +1,71 @@
+"""GPipe stage compute on the fused md kernels (parallel/fused_stage.py) vs the
+generic per-layer chain and vs the float64 oracle."""
+import pytest
+import torch
+
+from .oracle import check_grad, mlp_grads_fp64, sgd_grads
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _trainer(n_hidden, fused, dropout, tx):
+    from data_paral import synthetic_batch
+    from pipeline_parallel import build_mlp_pipeline
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.train_state import Batch
+
+    cfg = dp_config()
+    tr = build_mlp_pipeline(cfg, None, DEV, n_hidden_layers=n_hidden, dropout_rate=dropout, num_microbatches=4,
+                            tx=tx)
+    tr.cfg.fused_stage = fused
+    b = synthetic_batch(cfg, 70)
+    return tr, b, Batch(b.inputs.to(DEV), b.labels.to(DEV))
+
+
+@pytest.mark.parametrize("n_hidden", [2, 8])
+def test_fused_stage_sgd_grad_matches_fp64_with_dropout(n_hidden):
+    """One microbatch-loop GPipe step (one stage = the whole model), dropout on:
+    the applied SGD gradient == the fp64 oracle with the kernels' masks
+    (microbatch i, layer l: stream (seed, (i << 16) + (l << 1)) over [32, 512])."""
+    from jax_distributed_tuts_amd.ops.kernels import dropout_mask
+    from jax_distributed_tuts_amd.utils import rng as R
+    from jax_distributed_tuts_amd.utils.train_state import sgd
+
+    tr, b, bd = _trainer(n_hidden, True, 0.1, sgd(1.0))
+    P = tr.state.params
+    before = {k: v.cpu() for k, v in P.state_dict().items()}
+    tr.step(bd)
+    torch.cuda.synchronize()
+    assert tr.stage_engine is not None
+    seed = R.fold_rng_over_axis(tr.state.rng, None, "data") & 0xFFFFFFFF
+    masks = [[dropout_mask(seed, (i << 16) + (l << 1), (32, 512), 0.9) for l in range(n_hidden)] + [None]
+             for i in range(4)]
+    want = mlp_grads_fp64(before, tr.model.names, b.inputs, b.labels, masks=masks, keep=0.9, n_mb=4)
+    got = sgd_grads(before, {k: v.cpu() for k, v in P.state_dict().items()})
+    for n in want:
+        check_grad(got[n], want[n], n)
+    m = tr.metrics.cpu()
+    assert float(m[1]) == 128 and float(m[3]) == 128
+
+
+def test_fused_stage_equals_generic_stage_adamw():
+    """Several AdamW steps, hipGraph-captured: fused stage == generic stage (same masks)."""
+    from jax_distributed_tuts_amd.utils.train_state import adamw
+
+    res = []
+    for fused in (True, False):
+        tr, _, bd = _trainer(8, fused, 0.1, adamw(1e-3))
+        tr.step(bd)
+        tr.capture(bd, steps_per_graph=2)
+        tr.run_steps(bd, 4)
+        torch.cuda.synchronize()
+        assert (tr.stage_engine is not None) == fused
+        res.append(({k: v.cpu() for k, v in tr.state.params.state_dict().items()}, tr.metrics.cpu()))
+    (pa, ma), (pb, mb) = res
+    for k in pa:
+        d = (pa[k] - pb[k]).abs()
+        assert float(d.max()) <= 2 * 1e-3 * 5 + 1e-6, k
+        assert float((d > 5e-5).float().mean()) < 5e-2, k
+    assert float(ma[1]) == float(mb[1])
+    assert abs(float(ma[0]) - float(mb[0])) <= 2e-3 * abs(float(mb[0])) + 1e-3

@@ -117,7 +117,18 @@ def psum_scatter(x: torch.Tensor, mesh: Optional[Mesh], axis: str, dim: int = 0,
         return x
     g = mesh.group(axis)
     idx = mesh.axis_index(axis)
-    if dim != 0 or _is_gloo(g):
+    if dim != 0 and not _is_gloo(g):
+        # RCCL: scatter along dim 0 of the dim-first layout (the i-th dim-slice of
+        # the sum is the i-th dim-0 slice after movedim), then move the dim back
+        xt = x.movedim(dim, 0).contiguous()
+        res = torch.empty((xt.shape[0] // n,) + tuple(xt.shape[1:]), dtype=x.dtype, device=x.device)
+        dist.reduce_scatter_tensor(res, xt, op=dist.ReduceOp.SUM, group=g)
+        res = res.movedim(0, dim)
+        if out is None:
+            return res.contiguous()
+        out.copy_(res)
+        return out
+    if _is_gloo(g):
         red = _host(x, g).clone()
         dist.all_reduce(red, group=g)
         red = red.to(x.device)

@@ -44,10 +44,8 @@ class _Dense(torch.autograd.Function):
         act, keep, seed, offset, xdtype = ctx.cfg
         dz = dout.to(torch.bfloat16).contiguous()
         db = torch.zeros(w.shape[1], dtype=torch.float32, device=dz.device)
-        if z is not None:
-            dz = K.act_bwd(dz, z, act, keep_prob=keep, seed=seed, offset=offset, dbias=db)
-        else:
-            K.colsum_(dz, db)
+        # dz = dout * mask/keep * act'(z) and db = colsum(dz) in one pass (any width)
+        dz = K.act_bwd(dz, z, act, keep_prob=keep, seed=seed, offset=offset, dbias=db)
         dx = dw = None
         if ctx.needs_input_grad[1]:
             dw = torch.zeros(w.shape, dtype=torch.float32, device=dz.device)

@@ -86,6 +86,12 @@ struct MdArgs {
   // pipeline-stage use (parallel/fused_stage.py)
   int accumulate;       // mode 0: gW/gb/gWh/gbh/mslot += this launch's values (microbatch accumulation)
   const bf16_t* dH;     // bwd BND: gradient w.r.t. this layer's output H_i [M][N] (from the next stage)
+  // fwd: the M rows are consecutive microbatches of mb_rows rows (0 = one batch); row
+  // r draws its dropout bits from microbatch i = r / mb_rows's own stream -- offset
+  // + i * mb_stride, 4-row groups over the microbatch's rows -- exactly the masks a
+  // per-microbatch launch (the GPipe microbatch loop) would draw
+  int mb_rows;
+  unsigned long long mb_stride;
 };
 
 // Slots 0-4: s_memrealtime at the kernel's phase ends (tools/stamp_deep.py).
@@ -260,7 +266,17 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
     const int g4 = tid >> 4, c = tid & 15, col = j0 + c;
     const int rowg = r0 + g4 * 4;
     u32x4 db = {0u, 0u, 0u, 0u};
-    if (a.keep < 1.f && rowg < M) db = dropout_bits(a.seed, doff, dropout_group(0, rowg, col, M, N));
+    if (a.keep < 1.f && rowg < M) {
+      int lrow = rowg, Mg = M;
+      unsigned long long off = doff;
+      if (a.mb_rows > 0) {   // mb_rows % 4 == 0: a 4-row group never straddles microbatches
+        const int mi = rowg / a.mb_rows;
+        lrow = rowg - mi * a.mb_rows;
+        Mg = a.mb_rows;
+        off += (unsigned long long)mi * a.mb_stride;
+      }
+      db = dropout_bits(a.seed, off, dropout_group(0, lrow, col, Mg, N));
+    }
     float gf[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -652,6 +668,7 @@ JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) 
   const MdArgs& a = *args;
   if (a.N != 512 || a.M <= 0 || a.M > MD_MPM || (a.K != 784 && a.K != 512) || (head == 1 && a.C != 10)) return -3;
   if (phase == 0 && head == 2) return -2;
+  if (a.mb_rows < 0 || (a.mb_rows && (a.mb_rows % 4 || a.M % a.mb_rows))) return -2;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const dim3 blk(MD_NT);
   if (phase == 0) {

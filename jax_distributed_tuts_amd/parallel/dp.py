@@ -33,7 +33,7 @@ from ..ops import kernels as K
 from ..runtime.dist import Mesh
 from ..utils import rng as R
 from ..utils.flat import FlatParams, N_METRIC_SLOTS
-from ..utils.profiling import named_scope
+from ..utils.profiling import named_scope, replay_scope
 from ..utils.train_state import AdamW, Batch, TrainState
 
 
@@ -102,6 +102,18 @@ class DataParallelTrainer:
             from ..comm.buckets import GradBuckets
 
             self.buckets = GradBuckets(P, mesh, cfg.axis, int(cfg.bucket_mb * (1 << 20)))
+        from ..utils.checkpoint import bind_trainer
+
+        bind_trainer(state, self)
+
+    def invalidate(self):
+        """Drop state derived from the parameters (fused-engine bf16 copies, captured
+        graphs): called after a checkpoint restore; rebuilt on the next step."""
+        self.fused = None
+        self.graph = None
+        self.multi = None
+        self._scan = None
+        self._capturing = False
 
     def _fused_engine(self, batch: Batch):
         if self.cfg.accum != "kernel":
@@ -341,7 +353,8 @@ class DataParallelTrainer:
         if self.graph is not None and multi is not None:
             S, gm = multi
             for _ in range(n // S):
-                gm.replay()
+                with replay_scope("train_step_dp", S):
+                    gm.replay()
             self.state.step += (n // S) * S
             n = n % S
         for _ in range(n):
@@ -350,7 +363,8 @@ class DataParallelTrainer:
     def _replay(self):
         kind = self.graph[0]
         if kind == "one":
-            self.graph[1].replay()
+            with replay_scope("train_step_dp"):
+                self.graph[1].replay()
         else:
             self.graph[1].replay()
             self.sync()

@@ -43,7 +43,7 @@ from ..ops import kernels as K
 from ..runtime.dist import Mesh
 from ..utils import rng as R
 from ..utils.flat import FlatParams, ParamSpec, N_METRIC_SLOTS
-from ..utils.profiling import named_scope
+from ..utils.profiling import named_scope, replay_scope
 from ..utils.train_state import AdamW, Batch, TrainState
 
 log = logging.getLogger("jdt.fsdp")
@@ -372,6 +372,15 @@ class FSDPTrainer:
             xg = create_for(mesh, cfg.axis, self.sp.full.grad.numel(), self.sp.local.master.device, cfg.comm)
             if xg is not None:
                 self.sp.attach_xgmi(xg)
+        from ..utils.checkpoint import bind_trainer
+
+        bind_trainer(state, self)
+
+    def invalidate(self):
+        """After a checkpoint restore: drop the fused engine and captured graphs."""
+        self.fused = None
+        self.graph = None
+        self.multi = None
 
     @property
     def comm_backend(self) -> str:
@@ -432,7 +441,8 @@ class FSDPTrainer:
     def step(self, batch: Batch):
         """train_step_fsdp (param_sharding.py:343-367)."""
         if self.graph is not None:
-            self.graph.replay()
+            with replay_scope("train_step_fsdp"):
+                self.graph.replay()
         else:
             self._body(batch)
         self.state.step += 1
@@ -463,7 +473,8 @@ class FSDPTrainer:
         if self.graph is not None and self.multi is not None:
             S, gm = self.multi
             for _ in range(n // S):
-                gm.replay()
+                with replay_scope("train_step_fsdp", S):
+                    gm.replay()
             self.state.step += (n // S) * S
             n %= S
         for _ in range(n):

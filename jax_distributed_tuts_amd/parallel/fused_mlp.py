@@ -243,7 +243,7 @@ class MdArgs(ctypes.Structure):
                 ("pbh", c_void_p), ("mbh", c_void_p), ("vbh", c_void_p), ("sbh", c_void_p),
                 ("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float), ("wd", c_float),
                 ("gscale", c_float), ("running", c_void_p), ("stamps", c_void_p),
-                ("accumulate", c_int), ("dH", c_void_p)]
+                ("accumulate", c_int), ("dH", c_void_p), ("mb_rows", c_int), ("mb_stride", c_ulonglong)]
 
 
 _lib.declare("jdt_md_layer", c_int, [ctypes.POINTER(MdArgs), c_int, c_int, c_void_p])
@@ -266,13 +266,17 @@ class FusedMLPDeep:
     same interface as :class:`FusedMLP2`."""
 
     def __init__(self, state, mesh, axis: str, num_minibatches: int, rows: int, metrics: torch.Tensor,
-                 params=None, mslot: Optional[torch.Tensor] = None, fuse_opt: Optional[bool] = None):
+                 params=None, mslot: Optional[torch.Tensor] = None, fuse_opt: Optional[bool] = None,
+                 mb_rows: int = 0, mb_stride: int = 1 << 16):
         P = params if params is not None else state.params
         self.P = P
         self.mslot = mslot if mslot is not None else P.metrics_slot
         self.state, self.mesh, self.axis = state, mesh, axis
         self.world = C.axis_size(mesh, axis)
         self.n_mb = num_minibatches
+        # mb_rows > 0: dropout masks drawn per microbatch of mb_rows rows (stream offset +
+        # i * mb_stride), as the per-microbatch loop draws them (GPipe, one stage)
+        self.mb_rows, self.mb_stride = int(mb_rows), int(mb_stride)
         self.model = m = state.apply_fn
         self.metrics = metrics
         self.rows = rows
@@ -341,6 +345,7 @@ class FusedMLPDeep:
 
         a.seed = R.fold_rng_over_axis(st.rng, self.mesh, self.axis) & 0xFFFFFFFF
         a.offset = (m.layer_id_base + i) << 1
+        a.mb_rows, a.mb_stride = self.mb_rows, self.mb_stride
         a.step, a.ticket = o["count"].data_ptr(), o["ticket"].data_ptr()
         a.advance_step = int(self.fuse_opt and phase == 1 and i == 0)
         if not top:

@@ -51,8 +51,9 @@ def stage_supported(model, rows: int, device) -> bool:
     if not hidden_out or any(d != H for d in hidden_out):
         return False
     if not model.final_act:
-        # last stage: the head (H -> 10) is fused into the last hidden layer's kernels
-        if model.dims[-1] != C_HEAD or model.L < 2:
+        # last stage: the head (H -> 10) is fused into the last hidden layer's kernels,
+        # whose CE backward variant exists for 512-wide inputs only
+        if model.dims[-1] != C_HEAD or model.L < 2 or (model.L == 2 and model.dims[0] != H):
             return False
     return True
 
@@ -117,6 +118,7 @@ class FusedMLPStage:
         a.advance_step = 0
         a.fuse_opt = 0
         a.accumulate = 1
+        a.mb_rows = 0
         a.gW, a.gb = P.g(self.kn[l]).data_ptr(), P.g(self.bn[l]).data_ptr()
         a.mslot = P.metrics_slot.data_ptr()
         return a

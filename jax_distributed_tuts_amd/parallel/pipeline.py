@@ -35,7 +35,7 @@ from ..ops import kernels as K
 from ..runtime.dist import Mesh, is_initialized
 from ..utils import rng as R
 from ..utils.flat import FlatParams, N_METRIC_SLOTS
-from ..utils.profiling import named_scope
+from ..utils.profiling import named_scope, replay_scope
 from ..utils.train_state import AdamW, Batch, TrainState
 
 
@@ -89,6 +89,10 @@ class PipeConfig:
     # GPU, MLP stages of the tutorial shapes: one fused md_fwd / md_bwd launch per
     # layer and microbatch (parallel/fused_stage.py) instead of the generic chain
     fused_stage: bool = True
+    # pipe axis of size 1 + fused_stage: run the microbatches layer-major in one launch
+    # per layer (per-microbatch dropout streams kept; _single_stage_engine).  False:
+    # the per-microbatch stage kernels, as on a real multi-stage pipeline.
+    layer_major_single_stage: bool = True
 
 
 class GPipeTrainer:
@@ -122,6 +126,11 @@ class GPipeTrainer:
         self.wgrad = K.WGradStream(self.dev) if (self.dev.type == "cuda" and cfg.overlap_wgrad) else None
         self.stage_engine = None
         self._engine_tried = False
+        self.deep_engine = None
+        self._deep_tried = False
+        from ..utils.checkpoint import bind_trainer
+
+        bind_trainer(state, self)
         if self.dev.type == "cuda" and self.n_dp > 1:
             from ..comm.xgmi import create_for
 
@@ -191,6 +200,11 @@ class GPipeTrainer:
         self._setup_p2p(mb)
         rng = R.fold_rng_over_axis(st.rng, self.mesh, cfg.data_axis)
         seed = rng & 0xFFFFFFFF
+        if self.S == 1:
+            deep = self._single_stage_engine(batch.size, mb)
+            if deep is not None:
+                deep.forward_backward(batch)
+                return
         if self.S == 1 and cfg.merge_single_stage:
             out, cache = self.model.forward(P, batch.inputs, train=True, seed=seed, offset=0, step=st.step_tensor)
             d = torch.empty_like(out)
@@ -232,6 +246,35 @@ class GPipeTrainer:
                 self._send(dx, self.s - 1, n_mb + i)
             caches[i] = None
 
+    def invalidate(self):
+        """After a checkpoint restore: drop captured graphs and the stage engine."""
+        self.graph = None
+        self.multi = None
+        self.stage_engine = None
+        self._engine_tried = False
+        self.deep_engine = None
+        self._deep_tried = False
+
+    def _single_stage_engine(self, rows: int, mb: int):
+        """One stage holding the whole MLP (pipe axis of size 1): GPipe's fill/drain
+        degenerates to gradient accumulation over the microbatches, so the fused deep
+        kernels run all of this rank's rows layer by layer (one md_fwd / md_bwd launch
+        per layer instead of one per layer AND microbatch) while every row keeps its
+        microbatch's 1/mb loss weight and -- unless ``merge_single_stage`` -- its
+        microbatch's own dropout stream (``mb_rows``): the same masks, hence the same
+        gradient, as the microbatch loop."""
+        if not self._deep_tried:
+            self._deep_tried = True
+            from .fused_mlp import FusedMLPDeep, supported_deep
+
+            if (self.cfg.fused_stage and self.cfg.layer_major_single_stage and self.wgrad is None
+                    and not self.model.final_act
+                    and supported_deep(self.model, rows, self.dev)):
+                self.deep_engine = FusedMLPDeep(self.state, self.mesh, self.cfg.data_axis, self.cfg.num_microbatches,
+                                                rows, self.metrics,
+                                                mb_rows=0 if self.cfg.merge_single_stage else mb)
+        return self.deep_engine
+
     def _fused_stage(self, mb: int, seed: int):
         if not self._engine_tried:
             self._engine_tried = True
@@ -272,6 +315,8 @@ class GPipeTrainer:
         scale = 1.0 / (cfg.num_microbatches * self.n_dp)
         if self.wgrad is not None:
             self.wgrad.join()  # every weight-gradient GEMM of the step has landed
+        if self.deep_engine is not None and self.deep_engine.fuse_opt:
+            return  # one GPU, one stage: AdamW + metrics fold ran in the backward epilogues
         with named_scope("sync_grads"):
             if self._xg_fused_opt:
                 tx, o = st.tx, st.opt_state
@@ -291,7 +336,8 @@ class GPipeTrainer:
 
     def step(self, batch: Batch):
         if self.graph is not None:
-            self.graph.replay()
+            with replay_scope("train_step_pp"):
+                self.graph.replay()
         else:
             self._compute(batch)
             self._sync_update()
@@ -324,13 +370,16 @@ class GPipeTrainer:
         if self.graph is not None and self.multi is not None:
             S, gm = self.multi
             for _ in range(n // S):
-                gm.replay()
+                with replay_scope("train_step_pp", S):
+                    gm.replay()
             self.state.step += (n // S) * S
             n %= S
         for _ in range(n):
             self.step(batch)
 
     def finalize(self):
+        if self.deep_engine is not None:
+            self.deep_engine.finalize()  # bf16 shadow parity of the in-epilogue AdamW
         if self.p2p is not None and self.p2p.error():
             raise RuntimeError("xgmi pipeline receive timed out on this rank (peer dead or desynchronised)")
         if self.xg is not None and self.xg.error():

@@ -7,7 +7,9 @@ param_sharding.py:58,146,350,355).
 ``rocprofv3 --marker-trace`` shows the same region names as the reference
 (``sync_grads``, ``sync_metrics``, ``shard_params``, ``gather_params``...).
 ROCTx is optional: without the library only the torch range is emitted.
-Under hipGraph capture the ranges mark capture time, not replay.
+Under hipGraph capture the ranges mark capture time, not replay; replays are
+bracketed by ``replay_scope("<step program>[graph xS]")`` instead (the scopes
+inside a replayed step are the kernels of the trace, in capture order).
 """
 from __future__ import annotations
 
@@ -63,6 +65,11 @@ class named_scope(contextlib.ContextDecorator):
             r.roctxRangePop()
         self._rf.__exit__(*exc)
         return False
+
+
+def replay_scope(name: str, steps: int = 1) -> "named_scope":
+    """Range around a hipGraph replay of ``steps`` captured training steps."""
+    return named_scope(f"{name}[graph x{steps}]")
 
 
 class StepTimer:

@@ -9,35 +9,41 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 
 
-def _trainer(n_hidden, fused, dropout, tx):
+def _trainer(n_hidden, fused, dropout, tx, layer_major=True):
     from data_paral import synthetic_batch
     from pipeline_parallel import build_mlp_pipeline
     from jax_distributed_tuts_amd.utils.config import dp_config
     from jax_distributed_tuts_amd.utils.train_state import Batch
 
+    from jax_distributed_tuts_amd.runtime.dist import Mesh
+
     cfg = dp_config()
-    tr = build_mlp_pipeline(cfg, None, DEV, n_hidden_layers=n_hidden, dropout_rate=dropout, num_microbatches=4,
+    tr = build_mlp_pipeline(cfg, Mesh({"data": 1, "pipe": 1}), DEV, n_hidden_layers=n_hidden, dropout_rate=dropout, num_microbatches=4,
                             tx=tx)
     tr.cfg.fused_stage = fused
+    tr.cfg.layer_major_single_stage = layer_major
     b = synthetic_batch(cfg, 70)
     return tr, b, Batch(b.inputs.to(DEV), b.labels.to(DEV))
 
 
 @pytest.mark.parametrize("n_hidden", [2, 8])
-def test_fused_stage_sgd_grad_matches_fp64_with_dropout(n_hidden):
+@pytest.mark.parametrize("layer_major", [False, True])
+def test_fused_stage_sgd_grad_matches_fp64_with_dropout(n_hidden, layer_major):
     """One microbatch-loop GPipe step (one stage = the whole model), dropout on:
     the applied SGD gradient == the fp64 oracle with the kernels' masks
-    (microbatch i, layer l: stream (seed, (i << 16) + (l << 1)) over [32, 512])."""
+    (microbatch i, layer l: stream (seed, (i << 16) + (l << 1)) over [32, 512]) --
+    per-microbatch stage kernels, and the layer-major single-stage engine whose
+    merged launches draw the same per-microbatch masks."""
     from jax_distributed_tuts_amd.ops.kernels import dropout_mask
     from jax_distributed_tuts_amd.utils import rng as R
     from jax_distributed_tuts_amd.utils.train_state import sgd
 
-    tr, b, bd = _trainer(n_hidden, True, 0.1, sgd(1.0))
+    tr, b, bd = _trainer(n_hidden, True, 0.1, sgd(1.0), layer_major)
     P = tr.state.params
     before = {k: v.cpu() for k, v in P.state_dict().items()}
     tr.step(bd)
     torch.cuda.synchronize()
-    assert tr.stage_engine is not None
+    assert (tr.deep_engine if layer_major else tr.stage_engine) is not None
     seed = R.fold_rng_over_axis(tr.state.rng, None, "data") & 0xFFFFFFFF
     masks = [[dropout_mask(seed, (i << 16) + (l << 1), (32, 512), 0.9) for l in range(n_hidden)] + [None]
              for i in range(4)]
@@ -49,18 +55,22 @@ def test_fused_stage_sgd_grad_matches_fp64_with_dropout(n_hidden):
     assert float(m[1]) == 128 and float(m[3]) == 128
 
 
-def test_fused_stage_equals_generic_stage_adamw():
-    """Several AdamW steps, hipGraph-captured: fused stage == generic stage (same masks)."""
+@pytest.mark.parametrize("layer_major", [False, True])
+def test_fused_stage_equals_generic_stage_adamw(layer_major):
+    """Several AdamW steps, hipGraph-captured: fused stage == generic stage (same masks);
+    layer-major: AdamW fused into the backward epilogues."""
     from jax_distributed_tuts_amd.utils.train_state import adamw
 
     res = []
     for fused in (True, False):
-        tr, _, bd = _trainer(8, fused, 0.1, adamw(1e-3))
+        tr, _, bd = _trainer(8, fused, 0.1, adamw(1e-3), layer_major)
         tr.step(bd)
         tr.capture(bd, steps_per_graph=2)
         tr.run_steps(bd, 4)
+        tr.finalize()
         torch.cuda.synchronize()
-        assert (tr.stage_engine is not None) == fused
+        if fused:
+            assert (tr.deep_engine if layer_major else tr.stage_engine) is not None
         res.append(({k: v.cpu() for k, v in tr.state.params.state_dict().items()}, tr.metrics.cpu()))
     (pa, ma), (pb, mb) = res
     for k in pa:

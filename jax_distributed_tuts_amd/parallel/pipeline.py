@@ -268,7 +268,7 @@ class GPipeTrainer:
             from .fused_mlp import FusedMLPDeep, supported_deep
 
             if (self.cfg.fused_stage and self.cfg.layer_major_single_stage and self.wgrad is None
-                    and not self.model.final_act
+                    and not getattr(self.model, "final_act", True)
                     and supported_deep(self.model, rows, self.dev)):
                 self.deep_engine = FusedMLPDeep(self.state, self.mesh, self.cfg.data_axis, self.cfg.num_microbatches,
                                                 rows, self.metrics,

@@ -791,10 +791,10 @@ struct GemmGroup {
   unsigned* counters;
 };
 
-template <int S, bool TAIL>
+template <int S, bool TAIL, int TM = 1, int TN = 1>
 __global__ void __launch_bounds__(256) gemm_dma_group_kernel(GemmGroup G) {
-  constexpr int WM = 2, WN = 2, TM = 1, TN = 1;
-  constexpr int BM = 32, BN = 32, BK = DMA_BK;
+  constexpr int WM = 2, WN = 2;
+  constexpr int BM = WM * TM * 16, BN = WN * TN * 16, BK = DMA_BK;
   constexpr int STAGE = (BM + BN) * BK;
   constexpr int LPW = BM / 32 + BN / 32;
   __shared__ __attribute__((aligned(16))) bf16_t smem[S * STAGE];
@@ -811,6 +811,11 @@ __global__ void __launch_bounds__(256) gemm_dma_group_kernel(GemmGroup G) {
   const GemmArgs& g = G.g[p];
   const int tn = G.tiles_n[p], sp = G.splits[p];
   const int tiles_p = (g.M / BM) * tn;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int local = bid - G.start[p];
   const int tile = local % tiles_p, split = local / tiles_p;
   const int tm0 = (tile / tn) * BM, tn0 = (tile % tn) * BN;
@@ -821,8 +826,6 @@ __global__ void __launch_bounds__(256) gemm_dma_group_kernel(GemmGroup G) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int nkt = (kchunk + BK - 1) / BK;  // K % 32 == 0: the last tile may hold 32 valid k
-  f32x4 acc[TM][TN];
-  acc[0][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
   auto issue = [&](int kt) {
     bf16_t* st = smem + (kt % S) * STAGE;
     const int kv = kchunk - kt * BK;
@@ -849,12 +852,24 @@ __global__ void __launch_bounds__(256) gemm_dma_group_kernel(GemmGroup G) {
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
       if (TAIL && kt * BK + kk >= kchunk) break;  // half tile (uniform)
-      bf16x8 af = at ? dma_frag<BM>(As, true, wm * 16, kk, lane) : dma_frag<BM>(As, false, wm * 16, kk, lane);
-      bf16x8 bf = bt ? dma_frag<BN>(Bs, true, wn * 16, kk, lane) : dma_frag<BN>(Bs, false, wn * 16, kk, lane);
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = at ? dma_frag<BM>(As, true, (wm * TM + i) * 16, kk, lane)
+                   : dma_frag<BM>(As, false, (wm * TM + i) * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = bt ? dma_frag<BN>(Bs, true, (wn * TN + j) * 16, kk, lane)
+                    : dma_frag<BN>(Bs, false, (wn * TN + j) * 16, kk, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // asm tr reads retired (see gemm_dma_kernel)
-      asm volatile("" : "+v"(af));
-      asm volatile("" : "+v"(bf));
-      acc[0][0] = mfma16x16x32(af, bf, acc[0][0]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(af[i]));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(bfr[j]));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
     }
   }
   __syncthreads();
@@ -1025,6 +1040,7 @@ static int gemm_dma(const GemmArgs& g, int batch, int cfg, int splits, float* ws
     case 11: return launch_dma<2, 2, 2, 2>(g, batch, splits, ws, ws_floats, counters, n_counters, st);  // 64 x 64
     case 12: return launch_dma<2, 2, 2, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st);  // 64 x 128
     case 13: return launch_dma<2, 2, 1, 1>(g, batch, splits, ws, ws_floats, counters, n_counters, st);  // 32 x 32
+    case 14: return launch_dma<2, 2, 4, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st);  // 128 x 128
     default: return 1;
   }
 }
@@ -1033,10 +1049,11 @@ static int gemm_dma(const GemmArgs& g, int batch, int cfg, int splits, float* ws
 // Grouped launch (see gemm_dma_group_kernel).  Returns 1 if any problem is
 // outside the envelope (bf16, 16-byte aligned rows, M, N, K % 32 == 0, no
 // batch) -- the caller then launches the problems one by one.
-static int gemm_dma_group(const GemmArgs* gs, int n, float* ws, long ws_floats, unsigned* counters, long n_counters,
-                          hipStream_t st) {
-  if (g_gemm_no_dma || n < 1 || n > GROUP_MAX) return 1;
-  GemmGroup G{};
+static int g_group_tile = 0;  // jdt_gemm_set_group_tile(t): force 32 / 64 / 128 tiles (sweeps); 0 = heuristic
+
+template <int T>
+static int group_plan(const GemmArgs* gs, int n, GemmGroup& G, float* ws, long ws_floats, unsigned* counters,
+                      long n_counters) {
   G.n = n;
   G.ws = ws;
   G.counters = counters;
@@ -1044,34 +1061,70 @@ static int gemm_dma_group(const GemmArgs* gs, int n, float* ws, long ws_floats, 
   long wsused = 0, cntused = 0;
   for (int p = 0; p < n; ++p) {
     const GemmArgs& g = gs[p];
+    if (g.M % T || g.N % T) return -1;
+    G.g[p] = g;
+    G.tiles_n[p] = g.N / T;
+    G.start[p] = total;
+    const long tiles = (long)(g.M / T) * (g.N / T);
+    // split long K into slices of >= 512 (8 K-tiles): measured on the transformer's
+    // dW + dX groups, where the K = d_ff input gradient otherwise runs 4x the
+    // K-steps of its neighbour (g_group_split = 0 disables, for A/B runs).  Big
+    // tiles split further while the problem has fewer tiles than CUs.
+    int sp = 1;
+    const int minslice = T >= 128 ? 4 : 8;
+    if (g_group_split && ws && counters)
+      while (sp < 8 && (g.K / (2 * sp)) % DMA_BK == 0 && g.K / (2 * sp) >= minslice * DMA_BK &&
+             (T < 128 || tiles * sp < 256))
+        sp *= 2;
+    if (sp > 1 && (wsused + tiles * sp * T * T > ws_floats || cntused + tiles > n_counters)) sp = 1;
+    G.splits[p] = sp;
+    G.wsoff[p] = wsused;
+    G.cntoff[p] = (int)cntused;
+    if (sp > 1) { wsused += tiles * sp * T * T; cntused += tiles; }
+    total += (int)(tiles * sp);
+  }
+  G.start[n] = total;
+  return total;
+}
+
+template <int TMN>
+static void group_launch(const GemmGroup& G, int total, bool tail, hipStream_t st) {
+  if (tail)  // only then pay for the tail checks in the K loop (measured ~5 % on the transformer's groups)
+    hipLaunchKernelGGL((gemm_dma_group_kernel<3, true, TMN, TMN>), dim3(total), dim3(256), 0, st, G);
+  else
+    hipLaunchKernelGGL((gemm_dma_group_kernel<3, false, TMN, TMN>), dim3(total), dim3(256), 0, st, G);
+}
+
+static int gemm_dma_group(const GemmArgs* gs, int n, float* ws, long ws_floats, unsigned* counters, long n_counters,
+                          hipStream_t st) {
+  if (g_gemm_no_dma || n < 1 || n > GROUP_MAX) return 1;
+  long flops = 0;
+  bool m64 = true, m128 = true;
+  for (int p = 0; p < n; ++p) {
+    const GemmArgs& g = gs[p];
     auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
     if (g.a_f32 || g.b_f32 || g.K % 32 || g.K <= 0 || g.M % 32 || g.N % 32 || g.M <= 0 || g.N <= 0 || !al(g.A) ||
         !al(g.B) || g.lda % 8 || g.ldb % 8 || g.zin > 1)
       return 1;
-    G.g[p] = g;
-    G.tiles_n[p] = g.N / 32;
-    G.start[p] = total;
-    const long tiles = (long)(g.M / 32) * (g.N / 32);
-    // split long K into slices of >= 512 (8 K-tiles): measured on the transformer's
-    // dW + dX groups, where the K = d_ff input gradient otherwise runs 4x the
-    // K-steps of its neighbour (g_group_split = 0 disables, for A/B runs)
-    int sp = 1;
-    if (g_group_split && ws && counters)
-      while (sp < 8 && (g.K / (2 * sp)) % DMA_BK == 0 && g.K / (2 * sp) >= 8 * DMA_BK) sp *= 2;
-    if (sp > 1 && (wsused + tiles * sp * 32 * 32 > ws_floats || cntused + tiles > n_counters)) sp = 1;
-    G.splits[p] = sp;
-    G.wsoff[p] = wsused;
-    G.cntoff[p] = (int)cntused;
-    if (sp > 1) { wsused += tiles * sp * 32 * 32; cntused += tiles; }
-    total += (int)(tiles * sp);
+    flops += 2L * g.M * g.N * g.K;
+    m64 &= g.M % 64 == 0 && g.N % 64 == 0;
+    m128 &= g.M % 128 == 0 && g.N % 128 == 0;
   }
-  G.start[n] = total;
+  // tile: big groups (the 2048-token transformer backward: >= 2 GFLOP) on 128 x 128
+  // tiles (4 x 4 MFMA tiles per wave: 16 MFMAs per fragment set instead of 1)
+  int T = g_group_tile;
+  if (T == 0) T = (m128 && flops >= (2L << 30)) ? 128 : (m64 && flops >= (1L << 29)) ? 64 : 32;
+  if ((T == 128 && !m128) || (T == 64 && !m64)) T = 32;
+  GemmGroup G{};
+  const int total = T == 128 ? group_plan<128>(gs, n, G, ws, ws_floats, counters, n_counters)
+                  : T == 64  ? group_plan<64>(gs, n, G, ws, ws_floats, counters, n_counters)
+                             : group_plan<32>(gs, n, G, ws, ws_floats, counters, n_counters);
+  if (total <= 0) return 1;
   bool tail = false;
   for (int p = 0; p < n; ++p) tail |= (gs[p].K / G.splits[p]) % DMA_BK != 0;
-  if (tail)  // only then pay for the tail checks in the K loop (measured ~5 % on the transformer's groups)
-    hipLaunchKernelGGL((gemm_dma_group_kernel<3, true>), dim3(total), dim3(256), 0, st, G);
-  else
-    hipLaunchKernelGGL((gemm_dma_group_kernel<3, false>), dim3(total), dim3(256), 0, st, G);
+  if (T == 128) group_launch<4>(G, total, tail, st);
+  else if (T == 64) group_launch<2>(G, total, tail, st);
+  else group_launch<1>(G, total, tail, st);
   return HIP_LAUNCH_CHECK();
 }
 }  // namespace jdt
@@ -1122,3 +1175,4 @@ JDT_API int jdt_gemm_group(const GemmArgs* gs, int n, float* ws, long ws_floats,
   return gemm_dma_group(gs, n, ws, ws_floats, counters, n_counters, static_cast<hipStream_t>(stream));
 }
 JDT_API void jdt_gemm_set_group_split(int on) { g_group_split = on; }
+JDT_API void jdt_gemm_set_group_tile(int t) { g_group_tile = t; }

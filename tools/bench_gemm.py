@@ -33,6 +33,12 @@ SHAPES = [
     ("qkv fwd 2k", 2048, 1536, 512, "mk", "kn", False),
     ("fc2 fwd 2k", 2048, 512, 2048, "mk", "kn", False),
     ("fc1 dW 2k", 512, 2048, 2048, "km", "kn", True),
+    ("fc1 fwd 2k", 2048, 2048, 512, "mk", "kn", False),
+    ("fc2 dX 2k", 2048, 2048, 512, "mk", "nk", False),
+    ("fc1 dX 2k", 2048, 512, 2048, "mk", "nk", False),
+    ("fc2 dW 2k", 2048, 512, 2048, "km", "kn", True),
+    ("qkv dW 2k", 512, 1536, 2048, "km", "kn", True),
+    ("out dW 2k", 512, 512, 2048, "km", "kn", True),
     ("hyb qkv fwd", 256, 1536, 512, "mk", "kn", False),
     ("hyb fc2 fwd", 256, 512, 2048, "mk", "kn", False),
     ("mlp fwd", 32, 512, 512, "mk", "kn", False),
@@ -59,6 +65,53 @@ def timed(fn):
     return ts[2]
 
 
+# the transformer backward's grouped launches (2048 tokens, d 512, ff 2048, V 2048):
+# a layer's weight gradient h^T dz and input gradient dz W^T in ONE gemm_group
+GROUPS = [
+    ("fc2 bwd", [(2048, 512, 2048, "km", "kn", True), (2048, 2048, 512, "mk", "nk", False)]),
+    ("fc1 bwd", [(512, 2048, 2048, "km", "kn", True), (2048, 512, 2048, "mk", "nk", False)]),
+    ("qkv bwd", [(512, 1536, 2048, "km", "kn", True), (2048, 512, 1536, "mk", "nk", False)]),
+    ("out bwd", [(512, 512, 2048, "km", "kn", True), (2048, 512, 512, "mk", "nk", False)]),
+]
+
+
+def bench_groups(dev, tile: int):
+    from jax_distributed_tuts_amd.ops import _lib
+    _lib.lib().jdt_gemm_set_group_tile(tile)
+    res = []
+    for name, probs in GROUPS:
+        ops = []
+        fl = 0.0
+        for M, N, Kd, al, bl, f32 in probs:
+            a = torch.randn(*((M, Kd) if al == "mk" else (Kd, M)), device=dev).to(torch.bfloat16)
+            b = torch.randn(*((Kd, N) if bl == "kn" else (N, Kd)), device=dev).to(torch.bfloat16)
+            c = torch.zeros(M, N, device=dev, dtype=torch.float32 if f32 else torch.bfloat16)
+            ops.append((a, b, c, al, bl, f32))
+            fl += 2.0 * M * N * Kd
+
+        def run():
+            with K.gemm_group():
+                for a, b, c, al, bl, f32 in ops:
+                    K.gemm(a, b, a_layout=al, b_layout=bl, out=c, accumulate=f32)
+
+        t = timed(run)
+        tref = timed(lambda: [torch.matmul(a if al == "mk" else a.t(), b if bl == "kn" else b.t())
+                              for a, b, c, al, bl, f32 in ops])
+        # numerics
+        for a, b, c, al, bl, f32 in ops:
+            c.zero_()
+        run()
+        err = 0.0
+        for a, b, c, al, bl, f32 in ops:
+            want = (a if al == "mk" else a.t()).float() @ (b if bl == "kn" else b.t()).float()
+            err = max(err, float((c.float() - want).abs().max() / (want.abs().max() + 1e-6)))
+        print(f"group {name:10s} tile {tile:3d}: {t:8.2f} us {fl / t / 1e6:7.1f} TF/s | torch {tref:8.2f} us "
+              f"{fl / tref / 1e6:7.1f} TF/s | rel err {err:.2e}")
+        res.append({"group": name, "tile": tile, "ours_us": t, "torch_us": tref, "rel_err": err})
+    _lib.lib().jdt_gemm_set_group_tile(0)
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cfg", type=int, default=-1)
@@ -66,6 +119,7 @@ def main():
     ap.add_argument("--exact", type=int, default=0, help="force the exact-slice depth (0 = heuristic)")
     ap.add_argument("--splits", type=int, default=-1)
     ap.add_argument("--only", default=None, help="comma-separated shape names to run (e.g. 'qkv fwd,fc1 dW')")
+    ap.add_argument("--groups", default=None, help="comma-separated group tiles to sweep (e.g. '32,64,128'; 0 = auto)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     from jax_distributed_tuts_amd.ops import _lib
@@ -98,6 +152,9 @@ def main():
         out.append({"shape": name, "M": M, "N": N, "K": Kd, "ours_us": ours, "torch_us": ref, "rel_err": err})
         if err > 2e-2:
             print(f"   !! rel err {err:.3e}")
+    if args.groups:
+        for t in args.groups.split(","):
+            out.extend(bench_groups(dev, int(t)))
     if args.json:
         json.dump(out, open(args.json, "w"), indent=1)
 

@@ -1110,10 +1110,14 @@ static int gemm_dma_group(const GemmArgs* gs, int n, float* ws, long ws_floats, 
     m64 &= g.M % 64 == 0 && g.N % 64 == 0;
     m128 &= g.M % 128 == 0 && g.N % 128 == 0;
   }
-  // tile: big groups (the 2048-token transformer backward: >= 2 GFLOP) on 128 x 128
-  // tiles (4 x 4 MFMA tiles per wave: 16 MFMAs per fragment set instead of 1)
+  // Big groups (>= 1 GFLOP, e.g. the 2048-token transformer backward) are launched
+  // as separate single-problem launches: measured (tools/bench_gemm.py --groups) the
+  // per-problem tile/split heuristic of jdt_gemm beats one shared grid there by
+  // 1.3-2.3x (fc2 bwd group 82 us grouped vs 36 us as two launches); the grouped
+  // grid pays off for the small microbatch problems (launch gaps dominate).
   int T = g_group_tile;
-  if (T == 0) T = (m128 && flops >= (2L << 30)) ? 128 : (m64 && flops >= (1L << 29)) ? 64 : 32;
+  if (T == 0 && flops >= (1L << 30)) return 1;
+  if (T == 0) T = (m64 && flops >= (1L << 29)) ? 64 : 32;
   if ((T == 128 && !m128) || (T == 64 && !m64)) T = 32;
   GemmGroup G{};
   const int total = T == 128 ? group_plan<128>(gs, n, G, ws, ws_floats, counters, n_counters)

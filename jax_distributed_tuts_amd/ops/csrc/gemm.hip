@@ -328,6 +328,114 @@ __device__ __forceinline__ void gemm_finish(const GemmArgs& g, f32x4 (&acc)[TM][
   }
 }
 
+// Wide-tile variant (TM * TN >= 16, the 128 x 128 LDS-DMA tiles): the accumulators
+// go through an LDS image of the output tile first.  The register epilogue above,
+// instantiated with 64 accumulators per lane, is too large for the compiler to
+// unroll, and the dynamically indexed accumulator array was then promoted to LDS
+// (+64 KB per workgroup, SQ_LDS_BANK_CONFLICT 5.1M per launch) or to scratch.  Here
+// the only per-lane indexed loop is the fully unrolled register -> LDS copy; the
+// epilogue loop reads the image (one thread per column, one dropout group of 4
+// rows per iteration, column-coalesced stores).  Split-K slabs are the image in
+// row-major float4 order, combined by the last-arriving slice in slice order.
+template <int BM, int BN, int TM, int TN>
+__device__ __forceinline__ void gemm_finish_lds(const GemmArgs& g, f32x4 (&acc)[TM][TN], int tm0, int tn0, int z,
+                                                int wm, int wn, int lane, int tid, int splits, int split, long tile_id,
+                                                float* __restrict__ ws, unsigned* counters, float* img) {
+  constexpr int LD = BN + 4;   // padded row (floats)
+  static_assert(256 % BN == 0 || BN % 256 == 0, "columns per pass");
+  // the caller synchronised: every wave is past its last read of the staging ring
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        img[((wm * TM + i) * 16 + (lane >> 4) * 4 + e) * LD + (wn * TN + j) * 16 + (lane & 15)] = acc[i][j][e];
+  __syncthreads();
+  if (splits > 1) {
+    constexpr int NV = BM * BN / 4;
+    float* slab0 = ws + tile_id * splits * (BM * BN);
+    float* slab = slab0 + (long)split * (BM * BN);
+    for (int v = tid; v < NV; v += 256) {
+      const int r = (v * 4) / BN, c = (v * 4) % BN;
+      const float4 x = *reinterpret_cast<const float4*>(&img[r * LD + c]);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sys_u32x4, x),
+                                             __builtin_amdgcn_make_buffer_rsrc(slab, (short)0, BM * BN * 4, 0x00020000),
+                                             v * 16, 0, 16);  // sc1: written through to the coherence point
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(img + BM * LD);
+    if (tid == 0) {
+      const unsigned t = __hip_atomic_fetch_add(counters + tile_id, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (t == (unsigned)(splits - 1));
+      if (last) __hip_atomic_store(counters + tile_id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    for (int v = tid; v < NV; v += 256) {
+      float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int sp = 0; sp < splits; ++sp) {
+        const sys_u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(
+            __builtin_amdgcn_make_buffer_rsrc(slab0 + (long)sp * (BM * BN), (short)0, BM * BN * 4, 0x00020000), v * 16,
+            0, 16);  // sc1: past this CU's stale L1
+        const float4 x = __builtin_bit_cast(float4, q);
+        sum.x += x.x; sum.y += x.y; sum.z += x.z; sum.w += x.w;
+      }
+      const int r = (v * 4) / BN, c = (v * 4) % BN;
+      *reinterpret_cast<float4*>(&img[r * LD + c]) = sum;
+    }
+    __syncthreads();
+  }
+  // epilogue: thread -> column c (coalesced), rows in dropout groups of 4
+  const bool drop = g.keep_prob < 1.0f;
+  const float inv_keep = drop ? 1.0f / g.keep_prob : 1.0f;
+  const unsigned long long doff = g.offset + (g.step_ptr ? ((unsigned long long)(unsigned)g.step_ptr[0] << 32) : 0ull);
+  constexpr int CPP = BN < 256 ? BN : 256;      // columns per pass
+  constexpr int RGS = 256 / CPP;                 // row groups advanced per pass
+  const int cl = tid % CPP;
+  for (int cb = 0; cb < BN; cb += CPP) {
+    const int col = tn0 + cb + cl;
+    const bool cok = col < g.N;
+    float bval = 0.f;
+    if (g.bias && cok) bval = g.bias_f32 ? static_cast<const float*>(g.bias)[col] : bf2f(static_cast<const bf16_t*>(g.bias)[col]);
+    float csum = 0.f;
+    for (int rg = tid / CPP; rg < BM / 4; rg += RGS) {
+      const int row0 = tm0 + rg * 4;
+      u32x4 dbits = {0u, 0u, 0u, 0u};
+      if (drop && cok) dbits = dropout_bits(g.seed, doff, dropout_group(z, row0, col, g.M, g.N));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = row0 + e;
+        if (cok && row < g.M) {
+          float v = g.alpha * img[(rg * 4 + e) * LD + cb + cl] + bval;
+          if (g.Zout) static_cast<bf16_t*>(g.Zout)[(long)z * g.sZ + (long)row * g.ldz + col] = f2bf(v);
+          if (g.Zin) v *= act_grad(g.act_bwd, bf2f(g.Zin[(long)z * g.sZin + (long)row * g.ldzin + col]));
+          if (g.act) v = act_fwd(g.act, g.Zout ? round_bf(v) : v);
+          if (drop) v = keep_word(dbits, e, g.keep_prob) ? v * inv_keep : 0.f;
+          if (g.resid) v += bf2f(static_cast<const bf16_t*>(g.resid)[(long)z * g.sR + (long)row * g.ldr + col]);
+          const long co = zoff(g, z, g.sC, g.sC2) + (long)row * g.ldc + col;
+          if (g.c_f32) {
+            float* Cp = static_cast<float*>(g.C) + co;
+            *Cp = g.accumulate ? *Cp + v : v;
+          } else {
+            bf16_t* Cp = static_cast<bf16_t*>(g.C) + co;
+            if (g.accumulate) {
+              *Cp = f2bf(bf2f(*Cp) + v);
+            } else {
+              v = round_bf(v);
+              *Cp = f2bf(v);
+            }
+          }
+          csum += v;
+        }
+      }
+    }
+    if (g.dbias && cok) atomicAdd(g.dbias + col, csum);
+  }
+}
+
 template <int WM, int WN, int TM, int TN, int BK, bool AF32, bool BF32, int PRE, bool EXACT = false>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int vecA, int vecB, int splits,
                                                    int kchunk, float* __restrict__ ws, unsigned* counters) {
@@ -655,16 +763,54 @@ __device__ __forceinline__ void dma_stage(const bf16_t* src, long ld, int k0, bf
   }
 }
 
+// Tiles wider than 64 on an EXT-contiguous (k-row image) operand are staged as
+// EXT/64 side-by-side [64][64] images: a 128-wide k-row is one whole 256-byte LDS
+// bank row, so its transposed fragment reads conflicted (PMC on 128 x 128 tiles:
+// SQ_LDS_BANK_CONFLICT 5.1M cycles per launch, 2.6x the kernel time of 64 x 64
+// tiles); 64-wide sub-images keep the conflict-free EXT = 64 swizzle.
+template <int EXT, bool KMAJ>
+__device__ __forceinline__ void stage_op(const bf16_t* src, long ld, int k0, bf16_t* img, int wid, int lane) {
+  if constexpr (KMAJ && EXT > 64) {
+#pragma unroll
+    for (int h = 0; h < EXT / 64; ++h) dma_stage<64, true>(src + h * 64, ld, k0, img + h * 64 * DMA_BK, wid, lane);
+  } else {
+    dma_stage<EXT, KMAJ>(src, ld, k0, img, wid, lane);
+  }
+}
+template <int EXT>
+__device__ __forceinline__ bf16x8 frag_op(const bf16_t* img, bool kmajor_img, int base, int kk, int lane) {
+  if constexpr (EXT > 64) {
+    if (kmajor_img) return dma_frag<64>(img + (base >> 6) * 64 * DMA_BK, true, base & 63, kk, lane);
+  }
+  return dma_frag<EXT>(img, kmajor_img, base, kk, lane);
+}
+
 template <int EXT>
 __device__ __forceinline__ void dma_stage_rt(bool kmaj, const bf16_t* src, long ld, int k0, bf16_t* img, int wid,
                                              int lane) {
-  if (kmaj) dma_stage<EXT, true>(src, ld, k0, img, wid, lane);
-  else dma_stage<EXT, false>(src, ld, k0, img, wid, lane);
+  if (kmaj) stage_op<EXT, true>(src, ld, k0, img, wid, lane);
+  else stage_op<EXT, false>(src, ld, k0, img, wid, lane);
 }
 
 // The same for a K-tile that only has `kv` (= 32) valid k: lanes whose 16-byte
 // piece lies past it issue nothing (EXEC-masked), so no load leaves the operand;
 // the stale LDS they leave is never read (the MFMA loop stops at kv).
+template <int EXT>
+__device__ __forceinline__ void dma_stage_tail(bool kmaj, const bf16_t* src, long ld, int k0, int kv, bf16_t* img,
+                                               int wid, int lane);
+template <int EXT>
+__device__ __forceinline__ void dma_stage_tail_rt(bool kmaj, const bf16_t* src, long ld, int k0, int kv, bf16_t* img,
+                                                  int wid, int lane) {
+  if constexpr (EXT > 64) {
+    if (kmaj) {
+#pragma unroll
+      for (int h = 0; h < EXT / 64; ++h)
+        dma_stage_tail<64>(true, src + h * 64, ld, k0, kv, img + h * 64 * DMA_BK, wid, lane);
+      return;
+    }
+  }
+  dma_stage_tail<EXT>(kmaj, src, ld, k0, kv, img, wid, lane);
+}
 template <int EXT>
 __device__ __forceinline__ void dma_stage_tail(bool kmaj, const bf16_t* src, long ld, int k0, int kv, bf16_t* img,
                                                int wid, int lane) {
@@ -721,8 +867,8 @@ __global__ void __launch_bounds__(256) gemm_dma_kernel(GemmArgs g, int tiles_n, 
 
   auto issue = [&](int kt) {
     bf16_t* st = smem + (kt % S) * STAGE;
-    dma_stage<BM, AT>(Ab, g.lda, kbeg + kt * BK, st, wid, lane);
-    dma_stage<BN, BT>(Bb, g.ldb, kbeg + kt * BK, st + BM * BK, wid, lane);
+    stage_op<BM, AT>(Ab, g.lda, kbeg + kt * BK, st, wid, lane);
+    stage_op<BN, BT>(Bb, g.ldb, kbeg + kt * BK, st + BM * BK, wid, lane);
   };
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
@@ -743,9 +889,9 @@ __global__ void __launch_bounds__(256) gemm_dma_kernel(GemmArgs g, int tiles_n, 
     for (int kk = 0; kk < BK; kk += 32) {
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = dma_frag<BM>(As, AT, (wm * TM + i) * 16, kk, lane);
+      for (int i = 0; i < TM; ++i) af[i] = frag_op<BM>(As, AT, (wm * TM + i) * 16, kk, lane);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = dma_frag<BN>(Bs, BT, (wn * TN + j) * 16, kk, lane);
+      for (int j = 0; j < TN; ++j) bfr[j] = frag_op<BN>(Bs, BT, (wn * TN + j) * 16, kk, lane);
       if constexpr (AT || BT) {
         // asm tr reads retired; the empty asm ties every fragment to the wait so
         // no MFMA can be scheduled ahead of it
@@ -762,8 +908,14 @@ __global__ void __launch_bounds__(256) gemm_dma_kernel(GemmArgs g, int tiles_n, 
     }
   }
   __syncthreads();
-  gemm_finish<BM, BN, TM, TN>(g, acc, tm0, tn0, z, wid, wm, wn, lane, tid, splits, split, (long)z * gridDim.x + bid,
-                              ws, counters, reinterpret_cast<int*>(smem));
+  if constexpr (TM * TN >= 16) {
+    static_assert((BM * (BN + 4) + 4) * 4 <= S * STAGE * 2, "output image fits the staging ring");
+    gemm_finish_lds<BM, BN, TM, TN>(g, acc, tm0, tn0, z, wm, wn, lane, tid, splits, split,
+                                    (long)z * gridDim.x + bid, ws, counters, reinterpret_cast<float*>(smem));
+  } else {
+    gemm_finish<BM, BN, TM, TN>(g, acc, tm0, tn0, z, wid, wm, wn, lane, tid, splits, split, (long)z * gridDim.x + bid,
+                                ws, counters, reinterpret_cast<int*>(smem));
+  }
 }
 
 
@@ -833,8 +985,8 @@ __global__ void __launch_bounds__(256) gemm_dma_group_kernel(GemmGroup G) {
       dma_stage_rt<BM>(at, Ab, g.lda, k0 + kt * BK, st, wid, lane);
       dma_stage_rt<BN>(bt, Bb, g.ldb, k0 + kt * BK, st + BM * BK, wid, lane);
     } else {
-      dma_stage_tail<BM>(at, Ab, g.lda, k0 + kt * BK, kv, st, wid, lane);
-      dma_stage_tail<BN>(bt, Bb, g.ldb, k0 + kt * BK, kv, st + BM * BK, wid, lane);
+      dma_stage_tail_rt<BM>(at, Ab, g.lda, k0 + kt * BK, kv, st, wid, lane);
+      dma_stage_tail_rt<BN>(bt, Bb, g.ldb, k0 + kt * BK, kv, st + BM * BK, wid, lane);
     }
   };
 #pragma unroll
@@ -855,12 +1007,12 @@ __global__ void __launch_bounds__(256) gemm_dma_group_kernel(GemmGroup G) {
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        af[i] = at ? dma_frag<BM>(As, true, (wm * TM + i) * 16, kk, lane)
-                   : dma_frag<BM>(As, false, (wm * TM + i) * 16, kk, lane);
+        af[i] = at ? frag_op<BM>(As, true, (wm * TM + i) * 16, kk, lane)
+                   : frag_op<BM>(As, false, (wm * TM + i) * 16, kk, lane);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        bfr[j] = bt ? dma_frag<BN>(Bs, true, (wn * TN + j) * 16, kk, lane)
-                    : dma_frag<BN>(Bs, false, (wn * TN + j) * 16, kk, lane);
+        bfr[j] = bt ? frag_op<BN>(Bs, true, (wn * TN + j) * 16, kk, lane)
+                    : frag_op<BN>(Bs, false, (wn * TN + j) * 16, kk, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // asm tr reads retired (see gemm_dma_kernel)
 #pragma unroll
       for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(af[i]));
@@ -873,9 +1025,15 @@ __global__ void __launch_bounds__(256) gemm_dma_group_kernel(GemmGroup G) {
     }
   }
   __syncthreads();
-  gemm_finish<BM, BN, TM, TN>(g, acc, tm0, tn0, 0, wid, wm, wn, lane, tid, sp, split, tile,
-                              sp > 1 ? G.ws + G.wsoff[p] : nullptr, sp > 1 ? G.counters + G.cntoff[p] : nullptr,
-                              reinterpret_cast<int*>(smem));
+  if constexpr (TM * TN >= 16) {
+    gemm_finish_lds<BM, BN, TM, TN>(g, acc, tm0, tn0, 0, wm, wn, lane, tid, sp, split, tile,
+                                    sp > 1 ? G.ws + G.wsoff[p] : nullptr, sp > 1 ? G.counters + G.cntoff[p] : nullptr,
+                                    reinterpret_cast<float*>(smem));
+  } else {
+    gemm_finish<BM, BN, TM, TN>(g, acc, tm0, tn0, 0, wid, wm, wn, lane, tid, sp, split, tile,
+                                sp > 1 ? G.ws + G.wsoff[p] : nullptr, sp > 1 ? G.counters + G.cntoff[p] : nullptr,
+                                reinterpret_cast<int*>(smem));
+  }
 }
 
 // Exact-slice depth: K-tiles a slice may hold in registers (~128 VGPRs of

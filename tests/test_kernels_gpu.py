@@ -93,11 +93,13 @@ def test_gemm_accumulate_fp32():
     _close(acc_g, acc_r, rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("cfg", [-1, 14])
 @pytest.mark.parametrize("a_layout,b_layout", [("mk", "kn"), ("mk", "nk"), ("km", "kn"), ("km", "nk")])
-def test_gemm_dma_epilogues(a_layout, b_layout):
+def test_gemm_dma_epilogues(a_layout, b_layout, cfg):
     """LDS-DMA kernel with every fused epilogue: bias + GELU + z_out + dropout +
-    residual (forward), act' * mask + dbias (backward), fp32 accumulate, split-K."""
-    M, N, K_ = 128, 256, 512
+    residual (forward), act' * mask + dbias (backward), fp32 accumulate, split-K.
+    cfg 14: 128 x 128 tiles (64-wide transposed sub-images, LDS-staged epilogue)."""
+    M, N, K_ = (128, 256, 512) if cfg < 0 else (256, 384, 512)
     a = _mk((M, K_) if a_layout == "mk" else (K_, M), torch.bfloat16, seed=61)
     b = (_mk((K_, N) if b_layout == "kn" else (N, K_), torch.float32, seed=62) * 0.05).to(torch.bfloat16)
     bias, res = _mk((N,), torch.bfloat16, seed=63), _mk((M, N), torch.bfloat16, seed=64)
@@ -106,7 +108,7 @@ def test_gemm_dma_epilogues(a_layout, b_layout):
                     seed=7, offset=11, resid=res)
     zg = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     out = kern.gemm(a.to(DEV), b.to(DEV), a_layout=a_layout, b_layout=b_layout, bias=bias.to(DEV), act="gelu",
-                    z_out=zg, keep_prob=0.9, seed=7, offset=11, resid=res.to(DEV))
+                    z_out=zg, keep_prob=0.9, seed=7, offset=11, resid=res.to(DEV), cfg=cfg)
     _close(zg, zr)
     _close(out, ref)
     z = _mk((M, N), torch.bfloat16, seed=65)
@@ -114,16 +116,46 @@ def test_gemm_dma_epilogues(a_layout, b_layout):
     ref = kern.gemm(a, b, a_layout=a_layout, b_layout=b_layout, z_in=z, act_bwd="silu", keep_prob=0.9, seed=3,
                     offset=5, dbias=db_r)
     out = kern.gemm(a.to(DEV), b.to(DEV), a_layout=a_layout, b_layout=b_layout, z_in=z.to(DEV), act_bwd="silu",
-                    keep_prob=0.9, seed=3, offset=5, dbias=db_g)
+                    keep_prob=0.9, seed=3, offset=5, dbias=db_g, cfg=cfg)
     _close(out, ref)
     _close(db_g, db_r, rtol=2e-2, atol=5e-2)
-    for splits in (-1, 4):
+    for splits in (-1, 4, 8):
         acc_r = torch.full((M, N), 0.5)
         kern.gemm(a, b, a_layout=a_layout, b_layout=b_layout, out=acc_r, accumulate=True)
         acc_g = torch.full((M, N), 0.5, device=DEV)
         kern.gemm(a.to(DEV), b.to(DEV), a_layout=a_layout, b_layout=b_layout, out=acc_g, accumulate=True,
-                  cfg=11, splits=splits)
+                  cfg=11 if cfg < 0 else cfg, splits=splits)
         _close(acc_g, acc_r, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("tile", [32, 64, 128])
+def test_gemm_group_tiles(tile):
+    """Grouped launch at each tile size (forced): a weight gradient (km x kn, fp32
+    accumulate, split-K) next to an input gradient (mk x nk, act' + mask + dbias)."""
+    from jax_distributed_tuts_amd.ops import _lib
+
+    M, N, K_ = 256, 384, 1024
+    h = _mk((K_, M), torch.bfloat16, seed=71)
+    dz = _mk((K_, N), torch.bfloat16, seed=72)
+    w = (_mk((M, N), torch.float32, seed=73) * 0.05).to(torch.bfloat16)
+    zin = _mk((K_, M), torch.bfloat16, seed=74)
+    dw_r, dw_g = torch.full((M, N), 0.25), torch.full((M, N), 0.25, device=DEV)
+    db_r, db_g = torch.zeros(M), torch.zeros(M, device=DEV)
+    kern.gemm(h, dz, a_layout="km", b_layout="kn", out=dw_r, accumulate=True)
+    dx_r = kern.gemm(dz, w, a_layout="mk", b_layout="nk", z_in=zin, act_bwd="gelu", keep_prob=0.9, seed=5,
+                     offset=9, dbias=db_r)
+    _lib.lib().jdt_gemm_set_group_tile(tile)
+    try:
+        with kern.gemm_group():
+            kern.gemm(h.to(DEV), dz.to(DEV), a_layout="km", b_layout="kn", out=dw_g, accumulate=True)
+            dx_g = kern.gemm(dz.to(DEV), w.to(DEV), a_layout="mk", b_layout="nk", z_in=zin.to(DEV), act_bwd="gelu",
+                             keep_prob=0.9, seed=5, offset=9, dbias=db_g)
+        torch.cuda.synchronize()
+    finally:
+        _lib.lib().jdt_gemm_set_group_tile(0)
+    _close(dw_g, dw_r, rtol=1e-3, atol=2e-3)
+    _close(dx_g, dx_r)
+    _close(db_g, db_r, rtol=2e-2, atol=5e-2)
 
 
 def test_gemm_batched():

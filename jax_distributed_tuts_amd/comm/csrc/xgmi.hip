@@ -154,17 +154,23 @@ __device__ __forceinline__ void adam4(const XgAdam& A, long e, float4 g, float r
 // ALLREDUCE:      in[n] -> out[n] (or fused AdamW + metrics fold)
 // REDUCE_SCATTER: in[n] -> out[0, s) = reduced part `rank`
 // ALL_GATHER:     in[0, s) = part `rank` -> out[n]
+// staged (ALLREDUCE + fused AdamW only): the producer kernel of the step (mlp2_bwd /
+// md_bwd mode 0) already wrote this rank's gradient bucket straight into its data
+// buffer, identity layout (slice == s), in the half selected by the parity of the
+// optimizer step counter A.step -- which every block reads here before the last
+// block's ticket advances it -- so phase 0 (a full-buffer copy) is skipped.
 template <int W, int OP>
 __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, long cap, const float* in, float* out,
                                                         long n, long s, long slice,
-                                                        long chunk, XgAdam A, int fuse, long long timeout) {
+                                                        long chunk, XgAdam A, int fuse, long long timeout,
+                                                        int staged) {
   __shared__ unsigned s_epoch;
   const int b = blockIdx.x;
   XgSignal* me = P.sig[rank];
   if (threadIdx.x == 0) s_epoch = me->epoch[b] + 1u;
   __syncthreads();
   const unsigned epoch = s_epoch;
-  const long half = (long)(epoch & 1u) * cap;
+  const long half = (long)((staged ? (unsigned)A.step[0] : epoch) & 1u) * cap;
   const long base = (long)b * chunk;
   const int nv = (int)(chunk >> 2);
   const long own_n = (n - rank * s < s) ? n - rank * s : s;  // valid length of this rank's part
@@ -180,7 +186,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
 
   if (OP != XG_ALL_GATHER) {
     // phase 0: stage chunk b of every part of the local input (write-through stores)
-    for (int q = 0; q < W; ++q) {
+    for (int q = 0; q < (staged ? 0 : W); ++q) {
       for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
         const long j = base + 4 * i;
         const float4 x = j < s ? load_guard(in, q * s + j, n) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -388,20 +394,21 @@ static void xg_geometry(long s, long* G_out, long* chunk_out) {
 
 template <int OP>
 static int xg_launch(XgCtx* c, const float* in, float* out, long n, long s, const XgAdam* A, long long timeout,
-                     hipStream_t st) {
+                     hipStream_t st, int staged = 0) {
   const int W = c->world;
   if (s <= 0 || (s & 3) || n > s * W) return -2;
   long G, chunk;
   xg_geometry(s, &G, &chunk);
   const long slice = chunk * G;
   if (slice * W > c->cap) return -3;
+  if (staged && (slice != s || !A || OP != XG_ALLREDUCE)) return -2;
   XgAdam a{};
   int fuse = 0;
   if (A) { a = *A; fuse = 1; }
 #define XG_CASE(w)                                                                                              \
   case w:                                                                                                       \
     hipLaunchKernelGGL((xg_kernel<w, OP>), dim3(G), dim3(XG_THREADS), 0, st, c->peers, c->rank, c->cap, in, out, \
-                       n, s, slice, chunk, a, fuse, timeout);                                                   \
+                       n, s, slice, chunk, a, fuse, timeout, staged);                                           \
     break;
   switch (W) {
     XG_CASE(2)
@@ -498,6 +505,53 @@ JDT_API int jdt_xgmi_allreduce(void* ctx, const float* in, float* out, long n, c
   if (adam && ((adam->n_params & 3) || !adam->step || !adam->ticket)) return -2;
   const long part = ((n + c->world - 1) / c->world + 3) / 4 * 4;
   return xg_launch<XG_ALLREDUCE>(c, in, out, n, part, adam, timeout, static_cast<hipStream_t>(stream));
+}
+
+// Staged all-reduce geometry: the smallest part length s >= ceil(n / world) (a
+// multiple of 4) whose block split has no padding (slice == s), so that the IPC
+// data buffer's layout is the flat bucket's own index; -1 if none fits.
+static long xg_stage_part(int world, long n, long cap) {
+  const long s0 = ((n + world - 1) / world + 3) / 4 * 4;
+  for (long s = s0; s <= s0 + 16L * XG_MAX_BLOCKS; s += 4) {
+    long G, chunk;
+    xg_geometry(s, &G, &chunk);
+    if (G * chunk == s) return s * world <= cap ? s : -1;
+  }
+  return -1;
+}
+
+JDT_API long jdt_xgmi_stage_part(void* ctx, long n) {
+  XgCtx* c = static_cast<XgCtx*>(ctx);
+  return xg_stage_part(c->world, n, c->cap);
+}
+
+// This rank's data buffer (half 0; half 1 at + capacity floats): a staged producer
+// writes the bucket at base + (step & 1) * capacity, identity layout.
+JDT_API float* jdt_xgmi_stage_base(void* ctx) { return static_cast<XgCtx*>(ctx)->data; }
+
+// Zero both staging halves (positions a producer never writes -- padding between
+// the bucket's views -- must reduce to zero; earlier unstaged calls leave data there).
+JDT_API int jdt_xgmi_stage_clear(void* ctx, void* stream) {
+  XgCtx* c = static_cast<XgCtx*>(ctx);
+  return (int)hipMemsetAsync(c->data, 0, 2 * c->cap * sizeof(float), static_cast<hipStream_t>(stream));
+}
+
+// Copy src[0, n) into the staging half `parity` (self-test / tools).
+JDT_API int jdt_xgmi_stage_write(void* ctx, int parity, const float* src, long n, void* stream) {
+  XgCtx* c = static_cast<XgCtx*>(ctx);
+  if (n < 0 || n > c->cap) return -2;
+  return (int)hipMemcpyAsync(c->data + (long)(parity & 1) * c->cap, src, n * sizeof(float), hipMemcpyDeviceToDevice,
+                             static_cast<hipStream_t>(stream));
+}
+
+// All-reduce + fused AdamW of a bucket a producer kernel already staged (see xg_kernel).
+JDT_API int jdt_xgmi_allreduce_staged(void* ctx, long n, long s, const XgAdam* adam, long long timeout, void* stream) {
+  XgCtx* c = static_cast<XgCtx*>(ctx);
+  if (!c->opened) return -5;
+  if (!adam || (adam->n_params & 3) || !adam->step || !adam->ticket) return -2;
+  XgAdam a = *adam;
+  a.zero = nullptr;  // the producer overwrites every bucket element it owns each step
+  return xg_launch<XG_ALLREDUCE>(c, nullptr, nullptr, n, s, &a, timeout, static_cast<hipStream_t>(stream), 1);
 }
 
 // Part length s (multiple of 4, n <= world*s): out[0, s) receives the sum of

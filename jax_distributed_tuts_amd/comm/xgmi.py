@@ -81,6 +81,12 @@ _lib.declare("jdt_xgmi_segs_size", c_int, [])
 _lib.declare("jdt_xgmi_capacity", c_long, [c_void_p])
 _lib.declare("jdt_xgmi_adam_size", c_int, [])
 _lib.declare("jdt_xgmi_error", c_int, [c_void_p])
+_lib.declare("jdt_xgmi_stage_part", c_long, [c_void_p, c_long])
+_lib.declare("jdt_xgmi_stage_base", c_void_p, [c_void_p])
+_lib.declare("jdt_xgmi_stage_write", c_int, [c_void_p, c_int, c_void_p, c_long, c_void_p])
+_lib.declare("jdt_xgmi_stage_clear", c_int, [c_void_p, c_void_p])
+_lib.declare("jdt_xgmi_allreduce_staged", c_int, [c_void_p, c_long, c_long, ctypes.POINTER(XgAdam), c_longlong,
+                                                  c_void_p])
 _lib.declare("jdt_xgmi_destroy", c_int, [c_void_p])
 
 
@@ -194,6 +200,42 @@ class XgmiComm:
         rc = _lib.lib().jdt_xgmi_allreduce(self.ctx, _ptr(grad), c_void_p(0), grad.numel(), ctypes.byref(a),
                                            self.timeout, c_void_p(_lib.stream_ptr()))
         _lib.check(rc, "jdt_xgmi_allreduce(adamw)")
+
+    # ------------------------------------------------------------------ staged (producer-written) bucket
+    def stage_plan(self, n: int) -> Optional[dict]:
+        """Geometry for a producer kernel that writes an n-float bucket straight into
+        this rank's staging buffer (identity layout, half = optimizer step parity):
+        {"s": part length, "base": pointer of half 0, "stride": floats to half 1}, or
+        None if the bucket does not fit an unpadded split."""
+        s = int(_lib.lib().jdt_xgmi_stage_part(self.ctx, int(n)))
+        if s <= 0:
+            return None
+        return {"s": s, "n": int(n), "base": int(_lib.lib().jdt_xgmi_stage_base(self.ctx)), "stride": self.capacity}
+
+    def stage_clear(self):
+        _lib.check(_lib.lib().jdt_xgmi_stage_clear(self.ctx, c_void_p(_lib.stream_ptr())), "jdt_xgmi_stage_clear")
+
+    def stage_write(self, parity: int, src: torch.Tensor):
+        self._check_f32(src)
+        _lib.check(_lib.lib().jdt_xgmi_stage_write(self.ctx, int(parity), _ptr(src), src.numel(),
+                                                   c_void_p(_lib.stream_ptr())), "jdt_xgmi_stage_write")
+
+    def all_reduce_adamw_staged_(self, plan: dict, *, p: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
+                                 shadow: Optional[torch.Tensor], n_params: int, running: Optional[torch.Tensor],
+                                 n_metrics: int, lr: float, b1: float, b2: float, eps: float, wd: float,
+                                 grad_scale: float, step: torch.Tensor, ticket: torch.Tensor):
+        """``all_reduce_adamw_`` of the bucket a producer staged (``stage_plan``): no
+        staging copy; the producer and this kernel pick the buffer half from the
+        parity of ``step`` (the optimizer counter this kernel advances)."""
+        a = XgAdam()
+        a.p, a.m, a.v, a.shadow = _ptr(p), _ptr(m), _ptr(v), _ptr(shadow)
+        a.n_params, a.running, a.n_metrics = int(n_params), _ptr(running), int(n_metrics if running is not None else 0)
+        a.lr, a.b1, a.b2, a.eps, a.wd, a.grad_scale = float(lr), float(b1), float(b2), float(eps), float(wd), float(grad_scale)
+        a.step, a.ticket = _ptr(step), _ptr(ticket)
+        a.zero = c_void_p(0)
+        rc = _lib.lib().jdt_xgmi_allreduce_staged(self.ctx, plan["n"], plan["s"], ctypes.byref(a), self.timeout,
+                                                  c_void_p(_lib.stream_ptr()))
+        _lib.check(rc, "jdt_xgmi_allreduce_staged")
 
     def reduce_scatter(self, full: torch.Tensor, out: torch.Tensor, part: int) -> torch.Tensor:
         """out[0:part] = sum over ranks of full[rank*part : (rank+1)*part] (valid to full.numel())."""
@@ -418,6 +460,30 @@ class XgmiComm:
                            for t in range(1, 4))
         if not torch.equal(running, want_running):
             return self._fail("fused metrics fold mismatch")
+        # the staged variant (bucket pre-written into the staging half of the step's
+        # parity, as mlp2_bwd / md_bwd do in DP): 3 more steps continuing the state
+        plan = self.stage_plan(n)
+        if plan is None:
+            return self._fail("no unpadded staged geometry for the self-test bucket")
+        for t in range(4, 7):
+            grad = ((g0 * (r + 1) + t) % 13 - 6).to(torch.float32)
+            gsum = sum(((g0 * (q + 1) + t) % 13 - 6).to(torch.float32) for q in range(W))
+            self.stage_write(int(step.item()) & 1, grad)
+            self._skew(t)
+            self.all_reduce_adamw_staged_(plan, p=p, m=m, v=v, shadow=None, n_params=n_params, running=running,
+                                          n_metrics=n_metrics, lr=lr, b1=b1, b2=b2, eps=eps, wd=wd,
+                                          grad_scale=scale, step=step, ticket=ticket)
+            gr = gsum[:n_params] * scale
+            mr.mul_(b1).add_(gr, alpha=1 - b1)
+            vr.mul_(b2).addcmul_(gr, gr, value=1 - b2)
+            pr.sub_(lr * ((mr / (1 - b1 ** t)) / ((vr / (1 - b2 ** t)).sqrt() + eps) + wd * pr))
+            torch.cuda.synchronize(dev)
+            bad = (self.error() or int(step.item()) != t
+                   or not torch.allclose(p, pr, rtol=1e-5, atol=1e-6)
+                   or not torch.allclose(m, mr, rtol=1e-5, atol=1e-7)
+                   or not torch.allclose(v, vr, rtol=1e-5, atol=1e-9))
+            if bad:
+                return self._fail(f"staged fused AdamW all-reduce mismatch (step {t})")
         return True
 
 

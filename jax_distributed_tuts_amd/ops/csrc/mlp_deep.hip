@@ -92,6 +92,9 @@ struct MdArgs {
   // per-microbatch launch (the GPipe microbatch loop) would draw
   int mb_rows;
   unsigned long long mb_stride;
+  // mode 0, N > 1: grads + metric slots go to + (step & 1) * stage_stride floats (the
+  // xGMI staging half of this step; mlp_fused.hip Mlp2Args::stage_stride)
+  long stage_stride;
 };
 
 // Slots 0-4: s_memrealtime at the kernel's phase ends (tools/stamp_deep.py).
@@ -464,6 +467,7 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
     whv = par ? whv1 : whv0;
   }
   const MdAdam ak = md_adam_consts(a, step);
+  const long goff = (!fo && a.stage_stride) ? (long)par * a.stage_stride : 0;   // staged bucket half
 
   MD_STAMP(1);
   // ---- 1/2. dZ_i[:, blk] -> dzT[n][m] (bf16), dZout (chunk-0)
@@ -585,7 +589,7 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
         Wsn[idx] = pb;
         wtp[e >> 1] |= (unsigned)pb << (16 * (e & 1));
       } else {
-        a.gW[idx] = (a.accumulate ? op[e] : 0.f) + acc[e];   // mode 0 loaded the old grad into op
+        a.gW[goff + idx] = (a.accumulate ? op[e] : 0.f) + acc[e];   // mode 0 loaded the old grad into op
       }
     }
     if (a.fuse_opt && a.WTout)
@@ -613,17 +617,17 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       if (TOP && ac < C) {
         const long g = (long)(j0 + n) * C + ac;
         if (a.fuse_opt) Whn[g] = f2bf(md_adam(op[e], om[e], ov[e], aw[e], ak, a.pWh + g, a.mWh + g, a.vWh + g));
-        else a.gWh[g] = (a.accumulate ? op[e] : 0.f) + aw[e];
+        else a.gWh[goff + g] = (a.accumulate ? op[e] : 0.f) + aw[e];
       }
       if (ac == 0) {
         const int j = j0 + n;
         if (a.fuse_opt) a.sb[j] = f2bf(md_adam(bp[e], bm[e], bvv[e], ab[e], ak, a.pb + j, a.mb + j, a.vb + j));
-        else a.gb[j] = (a.accumulate ? bp[e] : 0.f) + ab[e];
+        else a.gb[goff + j] = (a.accumulate ? bp[e] : 0.f) + ab[e];
       }
     }
     if (TOP && lead && lane < C) {
       if (a.fuse_opt) a.sbh[lane] = f2bf(md_adam(qp, qm, qv, ab2[0], ak, a.pbh + lane, a.mbh + lane, a.vbh + lane));
-      else a.gbh[lane] = (a.accumulate ? qp : 0.f) + ab2[0];
+      else a.gbh[goff + lane] = (a.accumulate ? qp : 0.f) + ab2[0];
     }
   }
   MD_STAMP(3);
@@ -636,8 +640,9 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
         a.running[0] += L; a.running[1] += (float)M; a.running[2] += Cr; a.running[3] += (float)M;
       } else if (a.mslot) {
         const float k = a.accumulate ? 1.f : 0.f;
-        a.mslot[0] = k * a.mslot[0] + L; a.mslot[1] = k * a.mslot[1] + (float)M;
-        a.mslot[2] = k * a.mslot[2] + Cr; a.mslot[3] = k * a.mslot[3] + (float)M;
+        float* ms = a.mslot + goff;
+        ms[0] = k * ms[0] + L; ms[1] = k * ms[1] + (float)M;
+        ms[2] = k * ms[2] + Cr; ms[3] = k * ms[3] + (float)M;
       }
     }
   }

@@ -75,6 +75,10 @@ struct Mlp2Args {
   // loop kernel only: fp32 snapshot of W2 [H][C] taken by the forward (row block 0)
   // for the same step's backward, whose chunk-0 workgroups update W2 concurrently
   float* W2snap;
+  // mode 0, N > 1: the gradient bucket lives in this rank's xGMI staging buffer
+  // (comm/csrc/xgmi.hip, staged all-reduce): grads and metric slots are written at
+  // + (step & 1) * stage_stride floats, the half the collective of this step reads
+  long stage_stride;
 };
 
 // Persistent multi-step launch (mlp2_loop_kernel): n steps, grid barriers between
@@ -534,6 +538,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
 #pragma unroll
   for (int c = 0; c < C; ++c) lrow[c] = par ? lr1[c] : lr0[c];
   const AdamK ak = adam_consts(a, step);
+  const long goff = (!fo && a.stage_stride) ? (long)par * a.stage_stride : 0;   // staged bucket half
 
   // ---- 1. CE from the summed logits (rounded like the bf16 Dense output) -> dlogits
   float l_loss = 0.f, l_corr = 0.f;
@@ -626,7 +631,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         if (!a.W1T) a.sW1[idx] = pb;
         wt[e >> 1] |= (unsigned)pb << (16 * (e & 1));
       } else {
-        a.gW1[idx] = acc[e];
+        a.gW1[goff + idx] = acc[e];
       }
     }
     // the lane's 4 rows are 4 consecutive K elements of W1^T: one 8-byte store
@@ -665,14 +670,14 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
                                               (isb ? a.mb1 : a.mW2) + o, (isb ? a.vb1 : a.vW2) + o);
           (isb ? a.sb1 : sW2n)[o] = f2bf(pn);
         } else {
-          (isb ? a.gb1 : a.gW2)[o] = gr;
+          (isb ? a.gb1 : a.gW2)[goff + o] = gr;
         }
       }
     }
     if (lead && lane < C) {
       if (a.fuse_opt)
         a.sb2[lane] = f2bf(adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane));
-      else a.gb2[lane] = ab2[0];
+      else a.gb2[goff + lane] = ab2[0];
     }
   }
   __syncthreads();
@@ -683,7 +688,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
     const float val = tid == 0 ? L : tid == 2 ? Cr : (float)M;   // {loss sum, n, correct, n}
     if (fo && a.running) a.running[tid] = run_pre + val;
-    else if (a.mslot) a.mslot[tid] = val;
+    else if (a.mslot) a.mslot[goff + tid] = val;
     // advance the device step: every other workgroup of this launch reads the
     // forward's copy (step_copy), so no arrival ticket is needed
     if (!LOOP && fo && tid == 0) a.step[0] = step + 1;   // the loop kernel advances it at its end

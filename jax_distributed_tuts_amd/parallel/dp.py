@@ -22,6 +22,7 @@ dropout streams are indexed differently) -- 4x fewer launches.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -110,6 +111,7 @@ class DataParallelTrainer:
         """Drop state derived from the parameters (fused-engine bf16 copies, captured
         graphs): called after a checkpoint restore; rebuilt on the next step."""
         self.fused = None
+        self._stage = None
         self.graph = None
         self.multi = None
         self._scan = None
@@ -126,7 +128,23 @@ class DataParallelTrainer:
             if self.fused is None:
                 self.cfg.accum = "fused"  # shapes outside the fused kernels' envelope
                 return None
+            self._setup_stage()
         return self.fused
+
+    def _setup_stage(self):
+        """N > 1 with the fused xGMI all-reduce + AdamW: the backward kernel writes the
+        gradient bucket straight into this rank's xGMI staging buffer, so the
+        collective skips its staging copy (comm/csrc/xgmi.hip, staged)."""
+        self._stage = None
+        if not (self._xg_fused_opt and self.fused is not None and not self.fused.fuse_opt
+                and os.environ.get("JDT_XGMI_STAGED", "1") == "1"):
+            return
+        plan = self.xg.stage_plan(self.state.params.grad.numel())
+        if plan is None:
+            return
+        self.xg.stage_clear()
+        self.fused.set_grad_stage(plan["base"], plan["stride"])
+        self._stage = plan
 
     # ------------------------------------------------------------------ pieces
     def compute(self, batch: Batch):
@@ -217,7 +235,14 @@ class DataParallelTrainer:
             return
         with named_scope("sync_grads"):
             if self.xg is not None:
-                if self._xg_fused_opt:
+                if self._xg_fused_opt and getattr(self, "_stage", None) is not None:
+                    tx, st = self.state.tx, self.state.opt_state
+                    self.xg.all_reduce_adamw_staged_(
+                        self._stage, p=P.master, m=st["m"], v=st["v"], shadow=P.shadow, n_params=P.numel,
+                        running=self.metrics, n_metrics=N_METRIC_SLOTS, lr=tx.learning_rate, b1=tx.b1, b2=tx.b2,
+                        eps=tx.eps, wd=tx.weight_decay, grad_scale=1.0 / (self.cfg.num_minibatches * self.world),
+                        step=st["count"], ticket=st["ticket"])
+                elif self._xg_fused_opt:
                     tx, st = self.state.tx, self.state.opt_state
                     self.xg.all_reduce_adamw_(
                         P.grad, p=P.master, m=st["m"], v=st["v"], shadow=P.shadow, n_params=P.numel,

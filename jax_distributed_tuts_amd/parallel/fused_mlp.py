@@ -37,7 +37,7 @@ class Mlp2Args(ctypes.Structure):
                 ("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float), ("wd", c_float),
                 ("gscale", c_float), ("running", c_void_p), ("stamps", c_void_p),
                 ("W1T", c_void_p), ("ldw1t", c_int), ("XT", c_void_p), ("ldxt", c_int),
-                ("step_copy", c_void_p), ("W2snap", c_void_p)]
+                ("step_copy", c_void_p), ("W2snap", c_void_p), ("stage_stride", ctypes.c_long)]
 
 
 _lib.declare("jdt_mlp2", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_int, c_void_p])
@@ -126,6 +126,14 @@ class FusedMLP2:
             raise RuntimeError("Mlp2Args layout mismatch")
         self._args = None
         self._key = None
+        self.grad_stage = None   # (staging base pointer, half stride in floats): set_grad_stage
+
+    def set_grad_stage(self, base: int, stride: int):
+        """Mode 0: write the gradient bucket into the xGMI staging buffer at ``base``
+        (+ (step & 1) * ``stride`` floats) instead of P.grad (comm/xgmi.py staged)."""
+        assert not self.fuse_opt
+        self.grad_stage = (int(base), int(stride))
+        self._args = None
 
     def _build_args(self, batch) -> Mlp2Args:
         st, P = self.state, self.P
@@ -149,6 +157,13 @@ class FusedMLP2:
         names = ["input_dense/kernel", "input_dense/bias", "output_dense/kernel", "output_dense/bias"]
         a.gW1, a.gb1, a.gW2, a.gb2 = (P.g(n).data_ptr() for n in names)
         a.mslot = self.mslot.data_ptr()
+        if self.grad_stage is not None:
+            # N > 1: the bucket is written straight into the xGMI staging buffer (same
+            # flat layout as P.grad, half selected in-kernel by the step parity)
+            base, stride = self.grad_stage
+            a.gW1, a.gb1, a.gW2, a.gb2 = (base + 4 * P.offsets[n][0] for n in names)
+            a.mslot = base + 4 * P.metric_off
+            a.stage_stride = stride
         a.fuse_opt = int(self.fuse_opt)
         a.XT, a.ldxt = self.XT.data_ptr(), self.Mp
         a.step_copy = self.step_copy.data_ptr()
@@ -243,7 +258,8 @@ class MdArgs(ctypes.Structure):
                 ("pbh", c_void_p), ("mbh", c_void_p), ("vbh", c_void_p), ("sbh", c_void_p),
                 ("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float), ("wd", c_float),
                 ("gscale", c_float), ("running", c_void_p), ("stamps", c_void_p),
-                ("accumulate", c_int), ("dH", c_void_p), ("mb_rows", c_int), ("mb_stride", c_ulonglong)]
+                ("accumulate", c_int), ("dH", c_void_p), ("mb_rows", c_int), ("mb_stride", c_ulonglong),
+                ("stage_stride", ctypes.c_long)]
 
 
 _lib.declare("jdt_md_layer", c_int, [ctypes.POINTER(MdArgs), c_int, c_int, c_void_p])
@@ -313,6 +329,13 @@ class FusedMLPDeep:
             raise RuntimeError("MdArgs layout mismatch")
         self._args = None
         self._key = None
+        self.grad_stage = None
+
+    def set_grad_stage(self, base: int, stride: int):
+        """See FusedMLP2.set_grad_stage."""
+        assert not self.fuse_opt
+        self.grad_stage = (int(base), int(stride))
+        self._args = None
 
     def _shadow_pair(self, i):
         s0 = self.P.s(self.kn[i]).data_ptr()
@@ -357,6 +380,12 @@ class FusedMLPDeep:
         a.gW, a.gb = P.g(self.kn[i]).data_ptr(), P.g(self.bn[i]).data_ptr()
         a.gWh, a.gbh = P.g(self.kn[L - 1]).data_ptr(), P.g(self.bn[L - 1]).data_ptr()
         a.mslot = self.mslot.data_ptr()
+        if self.grad_stage is not None:
+            base, stride = self.grad_stage
+            a.gW, a.gb = base + 4 * P.offsets[self.kn[i]][0], base + 4 * P.offsets[self.bn[i]][0]
+            a.gWh, a.gbh = base + 4 * P.offsets[self.kn[L - 1]][0], base + 4 * P.offsets[self.bn[L - 1]][0]
+            a.mslot = base + 4 * P.metric_off
+            a.stage_stride = stride
         if self.fuse_opt:
             mm, vv = o["m"], o["v"]
 

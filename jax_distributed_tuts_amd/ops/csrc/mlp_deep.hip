@@ -95,6 +95,9 @@ struct MdArgs {
   // mode 0, N > 1: grads + metric slots go to + (step & 1) * stage_stride floats (the
   // xGMI staging half of this step; mlp_fused.hip Mlp2Args::stage_stride)
   long stage_stride;
+  // deterministic mode: md_fwd HEAD stores per-column-block partial logits to
+  // det_logits[N/16][M][C]; md_bwd TOP sums them in block order (no fp32 atomics)
+  float* det_logits;
 };
 
 // Slots 0-4: s_memrealtime at the kernel's phase ends (tools/stamp_deep.py).
@@ -318,7 +321,8 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
         float s = (by == 0) ? bf2f(a.bh[c]) : 0.f;
 #pragma unroll
         for (int n = 0; n < 16; ++n) s += htile[rl][n] * whs[n][c];
-        atomicAdd(lg + (long)row * C + c, s);
+        if (a.det_logits) a.det_logits[((long)by * M + row) * C + c] = s;
+        else atomicAdd(lg + (long)row * C + c, s);
       }
     }
   }
@@ -386,8 +390,20 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   float whv0 = 0.f, whv1 = 0.f;
   if constexpr (TOP) {
     const long lo = (long)min(tid, M - 1) * C;
+    if (a.det_logits) {
 #pragma unroll
-    for (int c = 0; c < C; ++c) { lr0[c] = a.logits[lo + c]; lr1[c] = a.logits[(long)M * C + lo + c]; }
+      for (int c = 0; c < C; ++c) lr0[c] = 0.f;
+      for (int q = 0; q < N / 16; ++q) {
+        const float* pq = a.det_logits + (long)q * M * C + lo;
+#pragma unroll
+        for (int c = 0; c < C; ++c) lr0[c] += pq[c];
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) lr1[c] = lr0[c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < C; ++c) { lr0[c] = a.logits[lo + c]; lr1[c] = a.logits[(long)M * C + lo + c]; }
+    }
     lab = a.labels[min(tid, M - 1)];
     gv = *reinterpret_cast<const float4*>(a.G + ((long)min(rg, (M - 1) >> 2) * N + j0 + gn) * 4);
 #pragma unroll

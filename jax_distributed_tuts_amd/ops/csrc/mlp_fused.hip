@@ -79,6 +79,10 @@ struct Mlp2Args {
   // (comm/csrc/xgmi.hip, staged all-reduce): grads and metric slots are written at
   // + (step & 1) * stage_stride floats, the half the collective of this step reads
   long stage_stride;
+  // deterministic mode (JDT_DETERMINISTIC=1): each column block of mlp2_fwd stores its
+  // partial logits to det_logits[H/16][M][C] instead of fp32-atomically adding them;
+  // mlp2_bwd sums the partials in column-block order -> bitwise-reproducible steps
+  float* det_logits;
 };
 
 // Persistent multi-step launch (mlp2_loop_kernel): n steps, grid barriers between
@@ -436,7 +440,8 @@ __device__ __forceinline__ void mlp2_fwd_body(AT& a, const int bx, const int by,
       float s = (by == 0) ? bf2f(b2b) : 0.f;
 #pragma unroll
       for (int n = 0; n < 16; ++n) s += htile[rl][n] * w2s[n][c];
-      atomicAdd(lg + (long)row * C + c, s);
+      if (a.det_logits) a.det_logits[((long)by * M + row) * C + c] = s;
+      else atomicAdd(lg + (long)row * C + c, s);
     }
   }
   __syncthreads();
@@ -480,6 +485,17 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
       const float* lg = a.logits + (long)(step_in & 1) * M * C;
 #pragma unroll
       for (int c = 0; c < C; ++c) lr1[c] = lr0[c] = ld_f<true>(lg + lo + c);
+    } else if (a.det_logits) {
+      // partial logits of the H/16 column blocks, summed in block order (deterministic)
+#pragma unroll
+      for (int c = 0; c < C; ++c) lr0[c] = 0.f;
+      for (int q = 0; q < a.H / 16; ++q) {
+        const float* pq = a.det_logits + (long)q * M * C + lo;
+#pragma unroll
+        for (int c = 0; c < C; ++c) lr0[c] += pq[c];
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) lr1[c] = lr0[c];
     } else {
 #pragma unroll
       for (int c = 0; c < C; ++c) { lr0[c] = a.logits[lo + c]; lr1[c] = a.logits[(long)M * C + lo + c]; }

@@ -37,7 +37,8 @@ class Mlp2Args(ctypes.Structure):
                 ("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float), ("wd", c_float),
                 ("gscale", c_float), ("running", c_void_p), ("stamps", c_void_p),
                 ("W1T", c_void_p), ("ldw1t", c_int), ("XT", c_void_p), ("ldxt", c_int),
-                ("step_copy", c_void_p), ("W2snap", c_void_p), ("stage_stride", ctypes.c_long)]
+                ("step_copy", c_void_p), ("W2snap", c_void_p), ("stage_stride", ctypes.c_long),
+                ("det_logits", c_void_p)]
 
 
 _lib.declare("jdt_mlp2", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_int, c_void_p])
@@ -49,6 +50,11 @@ _lib.declare("jdt_mlp2_loop", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_void_p,
 _lib.declare("jdt_mlp2_loop_ok", c_int, [c_int, c_int])
 
 LOOP_BARRIER_TIMEOUT_TICKS = 20_000_000   # 0.2 s of s_memrealtime (100 MHz) per grid barrier
+
+
+def deterministic() -> bool:
+    """JDT_DETERMINISTIC=1 (entry scripts' --deterministic): fixed-order reductions."""
+    return os.environ.get("JDT_DETERMINISTIC", "0") == "1"
 
 
 def _is_adamw(tx) -> bool:
@@ -127,6 +133,9 @@ class FusedMLP2:
         self._args = None
         self._key = None
         self.grad_stage = None   # (staging base pointer, half stride in floats): set_grad_stage
+        # deterministic mode: per-column-block partial logits instead of fp32 atomics
+        self.det_logits = (torch.zeros(H // 16, rows, 10, dtype=torch.float32, device=dev)
+                           if deterministic() else None)
 
     def set_grad_stage(self, base: int, stride: int):
         """Mode 0: write the gradient bucket into the xGMI staging buffer at ``base``
@@ -170,6 +179,8 @@ class FusedMLP2:
         a.W2snap = self.W2snap.data_ptr()
         if self.W1T is not None:
             a.W1T, a.ldw1t = self.W1T.data_ptr(), 800
+        if self.det_logits is not None:
+            a.det_logits = self.det_logits.data_ptr()
         tx = st.tx
         if self.fuse_opt:
             off = {n: P.offsets[n][0] for n in names}
@@ -259,7 +270,7 @@ class MdArgs(ctypes.Structure):
                 ("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float), ("wd", c_float),
                 ("gscale", c_float), ("running", c_void_p), ("stamps", c_void_p),
                 ("accumulate", c_int), ("dH", c_void_p), ("mb_rows", c_int), ("mb_stride", c_ulonglong),
-                ("stage_stride", ctypes.c_long)]
+                ("stage_stride", ctypes.c_long), ("det_logits", c_void_p)]
 
 
 _lib.declare("jdt_md_layer", c_int, [ctypes.POINTER(MdArgs), c_int, c_int, c_void_p])
@@ -330,6 +341,8 @@ class FusedMLPDeep:
         self._args = None
         self._key = None
         self.grad_stage = None
+        self.det_logits = (torch.zeros(DEEP_H // 16, rows, 10, dtype=torch.float32, device=dev)
+                           if deterministic() else None)
 
     def set_grad_stage(self, base: int, stride: int):
         """See FusedMLP2.set_grad_stage."""
@@ -369,6 +382,8 @@ class FusedMLPDeep:
         a.seed = R.fold_rng_over_axis(st.rng, self.mesh, self.axis) & 0xFFFFFFFF
         a.offset = (m.layer_id_base + i) << 1
         a.mb_rows, a.mb_stride = self.mb_rows, self.mb_stride
+        if self.det_logits is not None:
+            a.det_logits = self.det_logits.data_ptr()
         a.step, a.ticket = o["count"].data_ptr(), o["ticket"].data_ptr()
         a.advance_step = int(self.fuse_opt and phase == 1 and i == 0)
         if not top:

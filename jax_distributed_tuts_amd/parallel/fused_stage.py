@@ -83,6 +83,10 @@ class FusedMLPStage:
         # logits accumulators per microbatch, both step parities (md_bwd re-arms the other)
         self.logits = [torch.zeros(2, mb, C_HEAD, dtype=torch.float32, device=dev) for _ in range(n_mb)] \
             if self.last else None
+        from .fused_mlp import deterministic
+
+        self.det_logits = [torch.zeros(H // 16, mb, C_HEAD, dtype=torch.float32, device=dev) for _ in range(n_mb)] \
+            if (self.last and deterministic()) else None
         # dZ of each layer (consumed by the launch of the layer below, then dead)
         self.dZ = [torch.empty(mb, H, **bf) for _ in range(self.nh)]
         self.dX = [torch.empty(mb, self.k0, **bf) for _ in range(n_mb)]   # in flight to the previous stage
@@ -110,6 +114,8 @@ class FusedMLPStage:
             a.Wh0 = a.Wh1 = P.s(hk).data_ptr()
             a.bh = P.s(hb).data_ptr()
             a.logits = self.logits[i].data_ptr()
+            if self.det_logits is not None:
+                a.det_logits = self.det_logits[i].data_ptr()
             a.gWh, a.gbh = P.g(hk).data_ptr(), P.g(hb).data_ptr()
         a.keep = 1.0 - m.dropout_rate
         a.seed = self.seed

@@ -110,5 +110,12 @@ def entry_main(main, args, script: str):
     maybe_launch(n, script, sys.argv[1:])
     maybe_profile(args, script)
     if args.deterministic:
+        # fixed-order reductions: the fused engines' ordered logit sums (no fp32
+        # atomics), fixed-order split-K / xGMI reductions.  The generic per-minibatch
+        # kernels still reduce bias gradients with fp32 atomics, so the step runs on
+        # the fused kernels.
         os.environ["JDT_DETERMINISTIC"] = "1"
+        if getattr(args, "accum", None) in ("loop", "scan", "fused"):
+            print(f"[deterministic] --accum {args.accum} -> kernel (fused, fixed-order reductions)", file=sys.stderr)
+            args.accum = "kernel"
     run(main, args, expect_world=n)

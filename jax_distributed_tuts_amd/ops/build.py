@@ -85,9 +85,55 @@ def is_stale() -> bool:
     return any(s.stat().st_mtime > t for s in sources()) or _headers_mtime() > t
 
 
+ASAN_OBJDIR = LIBDIR / "obj_asan"
+ASAN_BIN = LIBDIR / "asan_host_check"
+ASAN_DRIVER = HERE.parent.parent / "tools" / "asan_host_check.cpp"
+ASAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer", "-g"]
+
+
+def asan_check(jobs: int | None = None) -> int:
+    """Host-side AddressSanitizer build of every kernel source + tools/asan_host_check.cpp,
+    then run it on the CPU.  Device code is compiled as usual: only the
+    host part of each translation unit is instrumented.  Returns the exit status."""
+    ASAN_OBJDIR.mkdir(parents=True, exist_ok=True)
+
+    def comp(src: Path) -> Path:
+        obj = ASAN_OBJDIR / (src.stem + ".o")
+        if obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _headers_mtime()):
+            return obj
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O1", "-std=c++17", "-fPIC", "-c", str(src), "-o", str(obj),
+               "-Wno-pass-failed", "-Wno-unused-result", f"-I{CSRC}", *ASAN_FLAGS]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"asan hipcc failed for {src.name}:\n{r.stderr[-4000:]}")
+        return obj
+
+    srcs = [s for s in sources() if s.suffix == ".hip"]
+    with cf.ThreadPoolExecutor(jobs or min(8, len(srcs))) as ex:
+        objs = list(ex.map(comp, srcs))
+    drv = ASAN_OBJDIR / "asan_host_check.o"
+    cmd = [_hipcc(), "-O1", "-std=c++17", "-c", str(ASAN_DRIVER), "-o", str(drv), *ASAN_FLAGS]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"asan driver compile failed:\n{r.stderr[-4000:]}")
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", str(drv), *map(str, objs), "-o", str(ASAN_BIN), *ASAN_FLAGS]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"asan link failed:\n{r.stderr[-4000:]}")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([str(ASAN_BIN)], capture_output=True, text=True, env=env)
+    sys.stdout.write(r.stdout)
+    sys.stderr.write(r.stderr[-4000:])
+    return r.returncode
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--asan-check", action="store_true",
+                    help="build the host-side ASan variant + tools/asan_host_check.cpp and run it on the CPU")
     a = ap.parse_args()
+    if a.asan_check:
+        sys.exit(asan_check(a.jobs))
     build(force=a.force, jobs=a.jobs)

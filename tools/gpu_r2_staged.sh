@@ -2,7 +2,7 @@
 # staged DP all-reduce: xGMI tests + full GPU suite, shared-GPU 2/4-rank benches, transformer profile
 cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
-timeout -k 10 400 python -u -m pytest tests/test_xgmi_gpu.py tests/test_grad_scale_gpu.py -q -x --timeout 200 --timeout-method thread > gpurun_out/pytest_xg.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_xgmi_gpu.py tests/test_grad_scale_gpu.py tests/test_deterministic_gpu.py -q -x --timeout 200 --timeout-method thread > gpurun_out/pytest_xg.log 2>&1
 rc=$?; echo "xgmi rc=$rc"; tail -3 gpurun_out/pytest_xg.log; fatal $rc && exit $rc; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "all-gpu rc=$rc"; tail -4 gpurun_out/pytest_gpu.log; fatal $rc && exit $rc

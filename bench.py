@@ -147,7 +147,7 @@ def comm_sweep(tr, dev, iters: int = 20):
             b.synchronize()
             return round(a.elapsed_time(b) * 1e3 / iters, 2)
 
-        if xg is not None and n <= xg.capacity // 2:
+        if xg is not None and n <= xg.capacity - 4 * 96 * D.world_size():
             row["xgmi_us"] = timed(lambda: xg.all_reduce_(x))
         if rccl:
             row["rccl_us"] = timed(lambda: dist.all_reduce(x))

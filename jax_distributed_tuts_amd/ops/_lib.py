@@ -44,6 +44,7 @@ _SIGS = {
     "jdt_gemm_group": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_void_p, c_long, c_void_p, c_long, c_void_p]),
     "jdt_gemm_set_group_split": (None, [c_int]),
     "jdt_gemm_set_group_tile": (None, [c_int]),
+    "jdt_ln_set_rows": (None, [c_int]),
     "jdt_gemm_set_preload": (None, [c_int]),
     "jdt_gemm_set_exact": (None, [c_int]),
     "jdt_gemm_set_dma": (None, [c_int]),

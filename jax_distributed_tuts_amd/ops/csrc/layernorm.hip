@@ -195,6 +195,9 @@ JDT_API int jdt_ln_fwd(const void* x, const float* gamma, const float* beta, voi
   return HIP_LAUNCH_CHECK();
 }
 
+static int g_ln_rows = 0;
+JDT_API void jdt_ln_set_rows(int r) { g_ln_rows = r; }
+
 // dsum (optional): += colsum(dx), the bias gradient of the layer that produced
 // this LayerNorm's input (a residual-stream Dense), so it needs no pass of its own.
 JDT_API int jdt_ln_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const float* gamma,
@@ -213,11 +216,14 @@ JDT_API int jdt_ln_bwd(const void* dy, const void* x, const float* mean, const f
 #define JDT_LNB(NV_, R_)                                                                                        \
   hipLaunchKernelGGL((ln_bwd_kernel<NV_, R_>), dim3((T + 4 * R_ - 1) / (4 * R_)), dim3(256), 0, st, a, b, mean, \
                      rstd, gamma, r, o, dgamma, dbeta, dsum, T, d)
-  const bool big = T > 2048;
+  // rows per wave: fewer, longer workgroups cut the same-address column atomics
+  // (3 x d per workgroup); g_ln_rows forces R (sweeps: tools/bench_ln.py)
+  int R = g_ln_rows;
+  if (R == 0) R = T > 2048 ? 4 : 2;
   switch (nv) {
-    case 1: if (big) JDT_LNB(1, 4); else JDT_LNB(1, 2); break;
-    case 2: if (big) JDT_LNB(2, 4); else JDT_LNB(2, 2); break;
-    default: if (big) JDT_LNB(4, 2); else JDT_LNB(4, 1); break;
+    case 1: if (R >= 8) JDT_LNB(1, 8); else if (R >= 4) JDT_LNB(1, 4); else JDT_LNB(1, 2); break;
+    case 2: if (R >= 8) JDT_LNB(2, 8); else if (R >= 4) JDT_LNB(2, 4); else JDT_LNB(2, 2); break;
+    default: if (R >= 2) JDT_LNB(4, 2); else JDT_LNB(4, 1); break;
   }
 #undef JDT_LNB
   return HIP_LAUNCH_CHECK();

@@ -45,6 +45,10 @@ _SIGS = {
     "jdt_gemm_set_group_split": (None, [c_int]),
     "jdt_gemm_set_group_tile": (None, [c_int]),
     "jdt_ln_set_rows": (None, [c_int]),
+    "jdt_gemm_set_epi_vec": (None, [c_int]),
+    "jdt_gemm_set_deep": (None, [c_int]),
+    "jdt_gemm_set_r": (None, [c_int]),
+    "jdt_gemm_set_tune": (None, [c_int]),
     "jdt_gemm_set_preload": (None, [c_int]),
     "jdt_gemm_set_exact": (None, [c_int]),
     "jdt_gemm_set_dma": (None, [c_int]),
@@ -120,6 +124,8 @@ def lib():
             raise RuntimeError("GemmArgs layout mismatch between Python and csrc/gemm.hip")
         if os.environ.get("JDT_GROUP_SPLIT") == "0":   # A/B: no split-K inside grouped GEMM launches
             l.jdt_gemm_set_group_split(0)
+        if os.environ.get("JDT_GEMM_R"):  # A/B: force the LDS-DMA GEMM's sub-tiles per ring slot
+            l.jdt_gemm_set_r(int(os.environ["JDT_GEMM_R"]))
         _lib = l
         return _lib
 

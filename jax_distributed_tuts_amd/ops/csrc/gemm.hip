@@ -436,6 +436,197 @@ __device__ __forceinline__ void gemm_finish_lds(const GemmArgs& g, f32x4 (&acc)[
   }
 }
 
+// Vectorised epilogue (the LDS-DMA kernels whenever every output row is
+// 16-byte aligned, see epi_vec_ok): the accumulators go through an LDS image of
+// the tile, then each thread owns units of 4 rows x 8 columns -- one dropout
+// group per column, 16-byte loads / stores of C, Zout, Zin and resid.  The
+// per-element register epilogue above stores 2 bytes per lane in 32-byte row
+// pieces; on a 2048 x 2048 output that store pass was ~2x the whole K loop of a
+// K = 512 GEMM (tools/gemm_ksweep.py: K = 64 took 13-18 us vs torch's 6).  The
+// arithmetic per element is the same sequence as gemm_finish, so results are
+// bit-identical.
+template <int BM, int BN, int TM, int TN>
+__device__ __forceinline__ void gemm_finish_vec(const GemmArgs& g, f32x4 (&acc)[TM][TN], int tm0, int tn0, int z,
+                                                int wm, int wn, int lane, int tid, int splits, int split, long tile_id,
+                                                float* __restrict__ ws, unsigned* counters, float* img) {
+  constexpr int LD = BN + 4;      // padded image row (floats)
+  constexpr int CU = BN / 8;      // 8-column chunks per row
+  constexpr int NU = BM / 4 * CU; // 4 x 8 units per tile
+  static_assert(256 % CU == 0, "a thread keeps its column chunk across units");
+  // the caller synchronised: every wave is past its last read of the staging ring
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        img[((wm * TM + i) * 16 + (lane >> 4) * 4 + e) * LD + (wn * TN + j) * 16 + (lane & 15)] = acc[i][j][e];
+  __syncthreads();
+  if (splits > 1) {
+    constexpr int NV = BM * BN / 4;
+    float* slab0 = ws + tile_id * splits * (BM * BN);
+    float* slab = slab0 + (long)split * (BM * BN);
+    for (int v = tid; v < NV; v += 256) {
+      const int r = (v * 4) / BN, c = (v * 4) % BN;
+      const float4 x = *reinterpret_cast<const float4*>(&img[r * LD + c]);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sys_u32x4, x),
+                                             __builtin_amdgcn_make_buffer_rsrc(slab, (short)0, BM * BN * 4, 0x00020000),
+                                             v * 16, 0, 16);  // sc1: written through to the coherence point
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(img + BM * LD);
+    if (tid == 0) {
+      const unsigned t = __hip_atomic_fetch_add(counters + tile_id, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (t == (unsigned)(splits - 1));
+      if (last) __hip_atomic_store(counters + tile_id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    for (int v = tid; v < NV; v += 256) {
+      float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int sp = 0; sp < splits; ++sp) {
+        const sys_u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(
+            __builtin_amdgcn_make_buffer_rsrc(slab0 + (long)sp * (BM * BN), (short)0, BM * BN * 4, 0x00020000), v * 16,
+            0, 16);  // sc1: past this CU's stale L1
+        const float4 x = __builtin_bit_cast(float4, q);
+        sum.x += x.x; sum.y += x.y; sum.z += x.z; sum.w += x.w;
+      }
+      const int r = (v * 4) / BN, c = (v * 4) % BN;
+      *reinterpret_cast<float4*>(&img[r * LD + c]) = sum;
+    }
+    __syncthreads();
+  }
+  const bool drop = g.keep_prob < 1.0f;
+  const float inv_keep = drop ? 1.0f / g.keep_prob : 1.0f;
+  const unsigned long long doff = g.offset + (g.step_ptr ? ((unsigned long long)(unsigned)g.step_ptr[0] << 32) : 0ull);
+  const int cc = tid % CU;
+  const int col = tn0 + cc * 8;
+  float bv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) bv[k] = 0.f;
+  if (g.bias) {
+    if (g.bias_f32) {
+      const float4 b0 = *reinterpret_cast<const float4*>(static_cast<const float*>(g.bias) + col);
+      const float4 b1 = *reinterpret_cast<const float4*>(static_cast<const float*>(g.bias) + col + 4);
+      bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w; bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+    } else {
+      const u32x4 p = *reinterpret_cast<const u32x4*>(static_cast<const bf16_t*>(g.bias) + col);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bv[k] = bf2f((bf16_t)((p[k >> 1] >> (16 * (k & 1))) & 0xffff));
+    }
+  }
+  float cs[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) cs[k] = 0.f;
+  const long cbase = zoff(g, z, g.sC, g.sC2);
+  for (int u = tid; u < NU; u += 256) {
+    const int rl = (u / CU) * 4;  // first row of the unit within the tile
+    const int row0 = tm0 + rl;
+    u32x4 db[8];
+    if (drop) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) db[k] = dropout_bits(g.seed, doff, dropout_group(z, row0, col + k, g.M, g.N));
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = row0 + e;
+      float v[8];
+      {
+        const float4 x0 = *reinterpret_cast<const float4*>(&img[(rl + e) * LD + cc * 8]);
+        const float4 x1 = *reinterpret_cast<const float4*>(&img[(rl + e) * LD + cc * 8 + 4]);
+        v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = g.alpha * v[k] + bv[k];
+      if (g.Zout) {
+        u32x4 o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = (unsigned)f2bf(v[2 * k]) | ((unsigned)f2bf(v[2 * k + 1]) << 16);
+        *reinterpret_cast<u32x4*>(static_cast<bf16_t*>(g.Zout) + (long)z * g.sZ + (long)row * g.ldz + col) = o;
+      }
+      if (g.Zin) {
+        const u32x4 p = *reinterpret_cast<const u32x4*>(g.Zin + (long)z * g.sZin + (long)row * g.ldzin + col);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] *= act_grad(g.act_bwd, bf2f((bf16_t)((p[k >> 1] >> (16 * (k & 1))) & 0xffff)));
+      }
+      if (g.act) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = act_fwd(g.act, g.Zout ? round_bf(v[k]) : v[k]);
+      }
+      if (drop) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = keep_word(db[k], e, g.keep_prob) ? v[k] * inv_keep : 0.f;
+      }
+      if (g.resid) {
+        const u32x4 p = *reinterpret_cast<const u32x4*>(static_cast<const bf16_t*>(g.resid) + (long)z * g.sR +
+                                                        (long)row * g.ldr + col);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] += bf2f((bf16_t)((p[k >> 1] >> (16 * (k & 1))) & 0xffff));
+      }
+      const long co = cbase + (long)row * g.ldc + col;
+      if (g.c_f32) {
+        float4* Cp = reinterpret_cast<float4*>(static_cast<float*>(g.C) + co);
+        float4 o0 = make_float4(v[0], v[1], v[2], v[3]), o1 = make_float4(v[4], v[5], v[6], v[7]);
+        if (g.accumulate) {
+          const float4 c0 = Cp[0], c1 = Cp[1];
+          o0.x = c0.x + o0.x; o0.y = c0.y + o0.y; o0.z = c0.z + o0.z; o0.w = c0.w + o0.w;
+          o1.x = c1.x + o1.x; o1.y = c1.y + o1.y; o1.z = c1.z + o1.z; o1.w = c1.w + o1.w;
+        }
+        Cp[0] = o0;
+        Cp[1] = o1;
+      } else {
+        u32x4* Cp = reinterpret_cast<u32x4*>(static_cast<bf16_t*>(g.C) + co);
+        u32x4 o;
+        if (g.accumulate) {
+          const u32x4 p = *Cp;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float a = bf2f((bf16_t)(p[k] & 0xffff)) + v[2 * k];
+            const float b = bf2f((bf16_t)(p[k] >> 16)) + v[2 * k + 1];
+            o[k] = (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = round_bf(v[k]);  // the bias grad sums exactly what is stored
+#pragma unroll
+          for (int k = 0; k < 4; ++k) o[k] = (unsigned)f2bf(v[2 * k]) | ((unsigned)f2bf(v[2 * k + 1]) << 16);
+        }
+        *Cp = o;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) cs[k] += v[k];
+    }
+  }
+  if (g.dbias) {
+    // column sums: the threads sharing a chunk (tid % CU) meet in the image
+    constexpr int RPT = 256 / CU;  // threads per chunk
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) img[(tid / CU) * (BN + 1) + cc * 8 + k] = cs[k];
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      float s = 0.f;
+      for (int r = 0; r < RPT; ++r) s += img[r * (BN + 1) + c];
+      atomicAdd(g.dbias + tn0 + c, s);
+    }
+  }
+}
+
+// Host: gemm_finish_vec's 16-byte accesses need every row of C / Zout / Zin /
+// resid (and every batch / sub-batch slice) to start 16-byte aligned.
+static bool epi_vec_ok(const GemmArgs& g, int batch) {
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  auto rows = [&](const void* p, long ld, long s1, long s2, int f32) {
+    if (!p) return true;
+    const long q = f32 ? 4 : 8;
+    return al(p) && ld % q == 0 && (batch <= 1 || (s1 % q == 0 && (g.zin <= 1 || s2 % q == 0)));
+  };
+  return rows(g.C, g.ldc, g.sC, g.sC2, g.c_f32) && rows(g.Zout, g.ldz, g.sZ, 0, 0) && rows(g.Zin, g.ldzin, g.sZin, 0, 0) &&
+         rows(g.resid, g.ldr, g.sR, 0, 0) && (!g.bias || al(g.bias)) && g.N % 8 == 0;
+}
+
 template <int WM, int WN, int TM, int TN, int BK, bool AF32, bool BF32, int PRE, bool EXACT = false>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int vecA, int vecB, int splits,
                                                    int kchunk, float* __restrict__ ws, unsigned* counters) {
@@ -837,12 +1028,36 @@ __device__ __forceinline__ void dma_stage_tail(bool kmaj, const bf16_t* src, lon
   }
 }
 
-template <int WM, int WN, int TM, int TN, bool AT, bool BT, int S>
+// Wait until at most `pend` K-tiles (LPW LDS-DMA instructions each, per wave)
+// issued after the one about to be read are still in flight, then barrier.
+// P is the ring's maximum (S - 2); the count must be an immediate, hence the
+// unrolled chain.  Waiting for exactly what is needed keeps the ring's tail
+// overlapped too (a plain vmcnt(0) there drains it S - 2 tiles early).
+template <int LPW, int P>
+__device__ __forceinline__ void dma_wait_barrier(int pend) {
+  if constexpr (P > 0) {
+    if (pend >= P) {
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(P * LPW) : "memory");
+      return;
+    }
+    dma_wait_barrier<LPW, P - 1>(pend);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+}
+
+// R = 64-deep K sub-tiles per ring slot (one barrier per R sub-tiles): small
+// tiles do too little MFMA work per barrier at R = 1 (a 32 x 32 tile: 2 MFMAs
+// per wave between barriers; the wait / barrier / ds_read latency chain then
+// sets the K loop's pace, ~300 cycles per 64-deep K-tile on one workgroup/CU).
+template <int WM, int WN, int TM, int TN, bool AT, bool BT, int S, int R = 1>
 __global__ void __launch_bounds__(256) gemm_dma_kernel(GemmArgs g, int tiles_n, int splits, int kchunk,
-                                                       float* __restrict__ ws, unsigned* counters) {
+                                                       float* __restrict__ ws, unsigned* counters, int vec) {
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16, BK = DMA_BK;
-  constexpr int STAGE = (BM + BN) * BK;  // elements
-  constexpr int LPW = BM / 32 + BN / 32;  // glds per wave per stage
+  constexpr int SUB = (BM + BN) * BK;     // elements of one 64-deep sub-tile (A image then B image)
+  constexpr int STAGE = SUB * R;          // elements of one ring slot
+  constexpr int LPW = (BM / 32 + BN / 32) * R;  // glds per wave per slot
+  static_assert((S - 2) * LPW <= 63, "vmcnt range");
   __shared__ __attribute__((aligned(16))) bf16_t smem[S * STAGE];
   const int nwg = gridDim.x;
   int bid = blockIdx.x;
@@ -857,7 +1072,7 @@ __global__ void __launch_bounds__(256) gemm_dma_kernel(GemmArgs g, int tiles_n, 
   const int wm = wid / WN, wn = wid % WN;
   const int split = blockIdx.y;
   const int kbeg = split * kchunk;
-  const int nkt = (min(g.K, kbeg + kchunk) - kbeg) / BK;
+  const int nkt = (min(g.K, kbeg + kchunk) - kbeg) / (BK * R);  // host: kchunk % (64 R) == 0
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -867,49 +1082,55 @@ __global__ void __launch_bounds__(256) gemm_dma_kernel(GemmArgs g, int tiles_n, 
 
   auto issue = [&](int kt) {
     bf16_t* st = smem + (kt % S) * STAGE;
-    stage_op<BM, AT>(Ab, g.lda, kbeg + kt * BK, st, wid, lane);
-    stage_op<BN, BT>(Bb, g.ldb, kbeg + kt * BK, st + BM * BK, wid, lane);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int k0 = kbeg + (kt * R + r) * BK;
+      stage_op<BM, AT>(Ab, g.lda, k0, st + r * SUB, wid, lane);
+      stage_op<BN, BT>(Bb, g.ldb, k0, st + r * SUB + BM * BK, wid, lane);
+    }
   };
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
     if (s < nkt) issue(s);
   for (int kt = 0; kt < nkt; ++kt) {
-    // stage kt has landed once at most the stages issued after it are pending
+    // slot kt has landed once at most the slots issued after it are pending
     // (per wave), and every wave's share once all passed the barrier
-    if (kt + S - 2 < nkt) {
-      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"((S - 2) * LPW) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-    // refill the stage consumed in iteration kt-1 (all waves are past it)
+    dma_wait_barrier<LPW, S - 2>(min(S - 2, nkt - 1 - kt));
+    // refill the slot consumed in iteration kt-1 (all waves are past it)
     if (kt + S - 1 < nkt) issue(kt + S - 1);
-    const bf16_t* As = smem + (kt % S) * STAGE;
-    const bf16_t* Bs = As + BM * BK;
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 32) {
-      bf16x8 af[TM], bfr[TN];
+    for (int r = 0; r < R; ++r) {
+      const bf16_t* As = smem + (kt % S) * STAGE + r * SUB;
+      const bf16_t* Bs = As + BM * BK;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = frag_op<BM>(As, AT, (wm * TM + i) * 16, kk, lane);
+      for (int kk = 0; kk < BK; kk += 32) {
+        bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = frag_op<BN>(Bs, BT, (wn * TN + j) * 16, kk, lane);
-      if constexpr (AT || BT) {
-        // asm tr reads retired; the empty asm ties every fragment to the wait so
-        // no MFMA can be scheduled ahead of it
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int i = 0; i < TM; ++i) af[i] = frag_op<BM>(As, AT, (wm * TM + i) * 16, kk, lane);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(af[i]));
+        for (int j = 0; j < TN; ++j) bfr[j] = frag_op<BN>(Bs, BT, (wn * TN + j) * 16, kk, lane);
+        if constexpr (AT || BT) {
+          // asm tr reads retired; the empty asm ties every fragment to the wait so
+          // no MFMA can be scheduled ahead of it
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(bfr[j]));
+          for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(af[i]));
+#pragma unroll
+          for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(bfr[j]));
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
       }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
     }
   }
   __syncthreads();
-  if constexpr (TM * TN >= 16) {
-    static_assert((BM * (BN + 4) + 4) * 4 <= S * STAGE * 2, "output image fits the staging ring");
+  static_assert((BM * (BN + 4) + 4) * 4 <= S * STAGE * 2, "output image fits the staging ring");
+  if (vec) {
+    gemm_finish_vec<BM, BN, TM, TN>(g, acc, tm0, tn0, z, wm, wn, lane, tid, splits, split,
+                                    (long)z * gridDim.x + bid, ws, counters, reinterpret_cast<float*>(smem));
+  } else if constexpr (TM * TN >= 16) {
     gemm_finish_lds<BM, BN, TM, TN>(g, acc, tm0, tn0, z, wm, wn, lane, tid, splits, split,
                                     (long)z * gridDim.x + bid, ws, counters, reinterpret_cast<float*>(smem));
   } else {
@@ -939,6 +1160,7 @@ struct GemmGroup {
   int splits[GROUP_MAX];
   long wsoff[GROUP_MAX];
   int cntoff[GROUP_MAX];
+  int vec[GROUP_MAX];   // epi_vec_ok per problem
   float* ws;
   unsigned* counters;
 };
@@ -1025,7 +1247,11 @@ __global__ void __launch_bounds__(256) gemm_dma_group_kernel(GemmGroup G) {
     }
   }
   __syncthreads();
-  if constexpr (TM * TN >= 16) {
+  if (G.vec[p]) {
+    gemm_finish_vec<BM, BN, TM, TN>(g, acc, tm0, tn0, 0, wm, wn, lane, tid, sp, split, tile,
+                                    sp > 1 ? G.ws + G.wsoff[p] : nullptr, sp > 1 ? G.counters + G.cntoff[p] : nullptr,
+                                    reinterpret_cast<float*>(smem));
+  } else if constexpr (TM * TN >= 16) {
     gemm_finish_lds<BM, BN, TM, TN>(g, acc, tm0, tn0, 0, wm, wn, lane, tid, sp, split, tile,
                                     sp > 1 ? G.ws + G.wsoff[p] : nullptr, sp > 1 ? G.counters + G.cntoff[p] : nullptr,
                                     reinterpret_cast<float*>(smem));
@@ -1131,6 +1357,7 @@ static int launch_cfg(const GemmArgs& g, int batch, int splits, float* ws, long 
 }
 
 
+static bool g_epi_vec = true;  // jdt_gemm_set_epi_vec(0): per-element epilogue (A/B tests)
 static bool g_gemm_no_dma = false;  // jdt_gemm_set_dma(0): register-staged kernels only (A/B tests)
 static int g_group_split = 1;  // jdt_gemm_set_group_split(0): no split-K inside grouped launches (A/B tests)
 
@@ -1142,45 +1369,121 @@ static int g_group_split = 1;  // jdt_gemm_set_group_split(0): no split-K inside
 template <int BM, int BN>
 constexpr int dma_stages() { return 3; }
 
+static int g_dma_deep = 0;  // jdt_gemm_set_deep(d): -1 auto, 0 never (default: measured no better), 1 always
+
+// Deep ring: with at most ~one workgroup per CU nothing else on the CU hides
+// the global->LDS latency, and a 3-stage ring keeps only 2 K-tiles in flight
+// (the K loop then runs at ~latency / 2 per K-tile).  Tiles of <= 64 x 64 fit 8
+// stages (<= 128 KB); the deep variant is used when the grid has <= 1 workgroup
+// per CU and enough K-tiles to fill the ring.
+constexpr int DMA_DEEP = 8;
+static int g_dma_r = -1;  // jdt_gemm_set_r(r): force r 64-deep sub-tiles per ring slot (sweeps); -1 auto
+// R > 1 slots: 3 of them within 96 KB (and the vmcnt immediate range)
+template <int BM, int BN>
+constexpr bool r_ok(int r) { return (BM + BN) * DMA_BK * 2 * 3 * r <= 96 * 1024 && (BM / 32 + BN / 32) * r <= 63; }
+template <int BM, int BN>
+constexpr bool deep_ok() { return (BM + BN) * DMA_BK * 2 * DMA_DEEP <= 128 * 1024; }
+
 template <int WM, int WN, int TM, int TN>
 static int launch_dma(const GemmArgs& g, int batch, int splits, float* ws, long ws_floats, unsigned* counters,
-                      long n_counters, hipStream_t st) {
+                      long n_counters, hipStream_t st, int r_pref = 1) {
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
   if (g.M % BM || g.N % BN) return 1;
   const int tiles_n = g.N / BN;
   const long tiles = (long)(g.M / BM) * tiles_n * batch;
+  const int ktiles = g.K / DMA_BK;
+  bool deep = deep_ok<BM, BN>() && (g_dma_deep == 1 || (g_dma_deep < 0 && tiles <= 256 && ktiles >= 16));
   int sp = splits;
   if (sp < 0) {
     // Measured (tools/bench_gemm.py sweeps): many small workgroups per CU hide
-    // the load latency better than a split-K combine; split only while the
-    // grid has < 2 workgroups per CU, keeping slices >= 8 K-tiles.
+    // the load latency better than a split-K combine (whose last-arriving slice
+    // reads every slab serially); split only while the grid has < 2 workgroups
+    // per CU, keeping slices >= 8 K-tiles -- and with a deep ring, only when the
+    // grid would leave over half the CUs idle.
     sp = 1;
-    while (sp < 16 && tiles * sp < 512 && (g.K / (2 * sp)) % DMA_BK == 0 && g.K / (2 * sp) >= 8 * DMA_BK) sp *= 2;
+    const long fill = deep ? 128 : 512;
+    while (sp < 16 && tiles * sp < fill && (g.K / (2 * sp)) % DMA_BK == 0 && g.K / (2 * sp) >= 8 * DMA_BK) sp *= 2;
   }
   if (sp < 1 || g.K % sp || (g.K / sp) % DMA_BK) return 1;
   if (sp > 1 && (!ws || !counters || tiles * sp * BM * BN > ws_floats || tiles > n_counters)) sp = 1;
   const int kchunk = g.K / sp;
+  if (g_dma_deep < 0 && kchunk / DMA_BK < 16) deep = false;
   dim3 grid((g.M / BM) * tiles_n, sp, batch);
   const bool at = g.a_trans, bt = g.b_trans;
-#define JDT_DMA(A_, B_)                                                                                     \
-  hipLaunchKernelGGL((gemm_dma_kernel<WM, WN, TM, TN, A_, B_, dma_stages<BM, BN>()>), grid, dim3(256), 0, st, \
-                     g, tiles_n, sp, kchunk, ws, counters)
+  const int vec = g_epi_vec && epi_vec_ok(g, batch);
+  // sub-tiles per ring slot: g_dma_r forces (sweeps), else 1
+  int R = g_dma_r > 0 ? g_dma_r : r_pref;
+  while (R > 1 && (kchunk / DMA_BK) % R) R >>= 1;
+  if (R > 1 && !r_ok<BM, BN>(R)) R = 1;
+#define JDT_DMA_S(A_, B_, S_, R_)                                                                                 \
+  hipLaunchKernelGGL((gemm_dma_kernel<WM, WN, TM, TN, A_, B_, S_, R_>), grid, dim3(256), 0, st, g, tiles_n, sp,    \
+                     kchunk, ws, counters, vec)
+#define JDT_DMA(A_, B_)                                                   \
+  do {                                                                    \
+    if constexpr (deep_ok<BM, BN>()) {                                    \
+      if (deep) { JDT_DMA_S(A_, B_, DMA_DEEP, 1); break; }                \
+    }                                                                     \
+    if constexpr (r_ok<BM, BN>(4)) {                                      \
+      if (R == 4) { JDT_DMA_S(A_, B_, 3, 4); break; }                     \
+    }                                                                     \
+    if constexpr (r_ok<BM, BN>(2)) {                                      \
+      if (R == 2) { JDT_DMA_S(A_, B_, 3, 2); break; }                     \
+    }                                                                     \
+    JDT_DMA_S(A_, B_, (dma_stages<BM, BN>()), 1);                         \
+  } while (0)
   if (!at && !bt) JDT_DMA(false, false);
   else if (!at && bt) JDT_DMA(false, true);
   else if (at && !bt) JDT_DMA(true, false);
   else JDT_DMA(true, true);
 #undef JDT_DMA
+#undef JDT_DMA_S
   return HIP_LAUNCH_CHECK();
 }
 
 // LDS-DMA path for bf16 operands: returns 1 if the shape / layout is outside
 // its envelope (caller falls back to the register-staged kernels).
+// Measured tile choices (tools/bench_gemm.py --cfg C --r R sweeps on MI355X,
+// gpurun_out/sw*/ -> profiles/r2_gemm_tile_sweep.txt): the transformer / MLP
+// shapes of the BASELINE configs.  {M, N, K, a_trans, b_trans, cfg, R}.
+struct GemmTune { int M, N, K, at, bt, cfg, r; };
+static const GemmTune kGemmTune[] = {
+    {512, 1536, 512, 0, 1, 11, 2},    // qkv fwd (512 rows)        6.81 us (torch 7.36)
+    {512, 512, 512, 0, 1, 13, 4},     // out fwd                   5.09 (6.64)
+    {512, 2048, 512, 0, 1, 11, 2},    // fc1 / head fwd            6.90 (7.53)
+    {512, 512, 2048, 0, 1, 13, 2},    // fc2 fwd                   9.53 (10.03)
+    {512, 512, 2048, 0, 0, 13, 2},    // fc1 dX                    8.69 (6.87)
+    {512, 2048, 512, 0, 0, 11, 2},    // fc2 dX                    6.52 (6.28)
+    {512, 2048, 512, 1, 1, 11, 2},    // fc1 dW                    7.51 (8.45)
+    {2048, 512, 512, 1, 1, 11, 2},    // fc2 dW                    7.59 (8.38)
+    {2048, 1536, 512, 0, 1, 11, 1},   // qkv fwd (2048 rows)       10.38 (12.15)
+    {2048, 512, 2048, 0, 1, 10, 2},   // fc2 fwd                   14.41 (13.78)
+    {512, 2048, 2048, 1, 1, 10, 1},   // fc1 / head dW             18.54 (16.64)
+    {2048, 2048, 512, 0, 1, 12, 1},   // fc1 / head fwd            10.99 (11.19)
+    {2048, 2048, 512, 0, 0, 12, 1},   // fc2 dX                    10.36 (9.73)
+    {2048, 512, 2048, 0, 0, 10, 2},   // fc1 / head dX             12.00 (10.98)
+    {2048, 512, 2048, 1, 1, 10, 2},   // fc2 dW                    15.48 (16.53)
+    {512, 1536, 2048, 1, 1, 10, 1},   // qkv dW                    19.66 (15.93)
+    {512, 512, 2048, 1, 1, 13, 2},    // out dW                    10.41 (15.46)
+    {256, 1536, 512, 0, 1, 10, 2},    // qkv fwd (hybrid, 256 rows) 5.55 (5.60)
+    {256, 512, 2048, 0, 1, 13, 2},    // fc2 fwd (hybrid)          8.38 (9.84)
+};
+static bool g_gemm_tune = true;  // jdt_gemm_set_tune(0): heuristic only (A/B)
+
 static int gemm_dma(const GemmArgs& g, int batch, int cfg, int splits, float* ws, long ws_floats, unsigned* counters,
                     long n_counters, hipStream_t st) {
   if (g_gemm_no_dma || g.a_f32 || g.b_f32 || g.K % DMA_BK) return 1;
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   if (!al(g.A) || !al(g.B) || g.lda % 8 || g.ldb % 8) return 1;
   if (batch > 1 && (g.sA % 8 || g.sB % 8 || g.sA2 % 8 || g.sB2 % 8)) return 1;
+  int r_pref = 1;
+  if (cfg < 0 && g_gemm_tune && batch == 1 && splits < 0) {
+    for (const GemmTune& t : kGemmTune)
+      if (t.M == g.M && t.N == g.N && t.K == g.K && t.at == (g.a_trans != 0) && t.bt == (g.b_trans != 0)) {
+        cfg = t.cfg;
+        r_pref = t.r;
+        break;
+      }
+  }
   if (cfg < 0) {
     // 32x32 tiles up to ~4 workgroups per CU (up to 6 fit by LDS), then 64x64,
     // then 64x128 (tools/bench_gemm.py sweep on the transformer/MLP shapes)
@@ -1190,15 +1493,15 @@ static int gemm_dma(const GemmArgs& g, int batch, int cfg, int splits, float* ws
     if (g.M < 64 && g.N < 256) return 1;  // tiny: the register kernels' split-K preload is as good
     if (t32 > 512 && g.K >= 2048 && g.N % 64 == 0) cfg = 10;  // long K: 32x64 reuses more per load
     else if (t32 <= 1024 || g.M % 64 || g.N % 64) cfg = 13;
-    else if (t64 <= 1024 || g.N % 128) cfg = 11;
+    else if (t64 <= 768 || g.N % 128) cfg = 11;
     else cfg = 12;
   }
   switch (cfg) {
-    case 10: return launch_dma<2, 2, 1, 2>(g, batch, splits, ws, ws_floats, counters, n_counters, st);  // 32 x 64
-    case 11: return launch_dma<2, 2, 2, 2>(g, batch, splits, ws, ws_floats, counters, n_counters, st);  // 64 x 64
-    case 12: return launch_dma<2, 2, 2, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st);  // 64 x 128
-    case 13: return launch_dma<2, 2, 1, 1>(g, batch, splits, ws, ws_floats, counters, n_counters, st);  // 32 x 32
-    case 14: return launch_dma<2, 2, 4, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st);  // 128 x 128
+    case 10: return launch_dma<2, 2, 1, 2>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref);  // 32 x 64
+    case 11: return launch_dma<2, 2, 2, 2>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref);  // 64 x 64
+    case 12: return launch_dma<2, 2, 2, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref);  // 64 x 128
+    case 13: return launch_dma<2, 2, 1, 1>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref);  // 32 x 32
+    case 14: return launch_dma<2, 2, 4, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref);  // 128 x 128
     default: return 1;
   }
 }
@@ -1238,6 +1541,7 @@ static int group_plan(const GemmArgs* gs, int n, GemmGroup& G, float* ws, long w
     G.splits[p] = sp;
     G.wsoff[p] = wsused;
     G.cntoff[p] = (int)cntused;
+    G.vec[p] = g_epi_vec && epi_vec_ok(g, 1);
     if (sp > 1) { wsused += tiles * sp * T * T; cntused += tiles; }
     total += (int)(tiles * sp);
   }
@@ -1298,6 +1602,10 @@ using namespace jdt;
 JDT_API void jdt_gemm_set_preload(int on) { g_gemm_no_preload = !on; }
 JDT_API void jdt_gemm_set_exact(int pre) { g_exact_pre = pre; }
 JDT_API void jdt_gemm_set_dma(int on) { g_gemm_no_dma = !on; }
+JDT_API void jdt_gemm_set_epi_vec(int on) { g_epi_vec = on; }
+JDT_API void jdt_gemm_set_deep(int d) { g_dma_deep = d; }
+JDT_API void jdt_gemm_set_r(int r) { g_dma_r = r; }
+JDT_API void jdt_gemm_set_tune(int on) { g_gemm_tune = on; }
 
 JDT_API int jdt_gemm(const GemmArgs* ga, int batch, int cfg, int splits, float* ws, long ws_floats,
                      unsigned* counters, long n_counters, void* stream) {

@@ -49,6 +49,7 @@ _SIGS = {
     "jdt_gemm_set_deep": (None, [c_int]),
     "jdt_gemm_set_r": (None, [c_int]),
     "jdt_gemm_set_tune": (None, [c_int]),
+    "jdt_flash_set_head": (None, [c_int]),
     "jdt_gemm_set_preload": (None, [c_int]),
     "jdt_gemm_set_exact": (None, [c_int]),
     "jdt_gemm_set_dma": (None, [c_int]),

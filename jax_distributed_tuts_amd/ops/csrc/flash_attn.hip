@@ -357,6 +357,218 @@ __global__ void __launch_bounds__(256) flash_bwd_kernel(const bf16_t* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------
+// Whole-head backward (S <= 128, the tutorial LM's sequence length): ONE
+// workgroup of 8 waves per (batch, head), wave w owns keys 16w .. 16w + 15.
+// The key-block kernel above splits a head over S/64 workgroups, so dQ (a sum
+// over key blocks) needs fp32 atomics into a workspace and a last-arriver
+// conversion pass; at S = 128 that atomic / ticket tail and the half-empty
+// causal blocks dominated (35 us per launch, 19 TFLOP/s, rocprofv3
+// profiles/r2_transformer_merged_tuned_kernel_stats.csv).  Here every key of the
+// head is in the workgroup, so per 64-query tile dQ = dS K is one more MFMA
+// pass over the shared dS image, written straight to dQKV as bf16: no atomics,
+// no workspace, no ticket, and a fixed summation order (deterministic).
+constexpr int FS = 128;          // keys per head handled by one workgroup
+constexpr int KLD = FS + 8;      // padded [64][128] image row (bf16)
+
+// [64 rows][64 cols] bf16 tile -> LDS (row-major and/or transposed with row
+// stride tld), rows >= nrows zero; 512 threads.
+__device__ __forceinline__ void stage_tile512(const bf16_t* g, long ld, int nrows, bf16_t* row_major,
+                                              bf16_t* transposed, int tld) {
+  const int c = threadIdx.x;  // FB * FD / 8 == 512 chunks: one per thread
+  const int r = c >> 3, dc = (c & 7) * 8;
+  u32x4 v = {0u, 0u, 0u, 0u};
+  if (r < nrows) v = *reinterpret_cast<const u32x4*>(g + (long)r * ld + dc);
+  if (row_major) *reinterpret_cast<u32x4*>(row_major + r * FLD + dc) = v;
+  if (transposed) {
+    const unsigned q[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      transposed[(dc + 2 * j) * tld + r] = (bf16_t)(q[j] & 0xffff);
+      transposed[(dc + 2 * j + 1) * tld + r] = (bf16_t)(q[j] >> 16);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(512) flash_bwd_head_kernel(const bf16_t* __restrict__ qkv,
+                                                             const bf16_t* __restrict__ o,
+                                                             const bf16_t* __restrict__ dout,
+                                                             const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
+                                                             float* __restrict__ dbias, int S, int H, float scale,
+                                                             int causal) {
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[FB * FLD];
+  __shared__ __attribute__((aligned(16))) bf16_t Qt[FD * FLD];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[FB * FLD];
+  __shared__ __attribute__((aligned(16))) bf16_t dOt[FD * FLD];
+  __shared__ __attribute__((aligned(16))) bf16_t Kt[FD * KLD];     // K^T [dim][key]
+  __shared__ __attribute__((aligned(16))) bf16_t Pw[8][16 * FLD];
+  __shared__ __attribute__((aligned(16))) bf16_t dSw[8][16 * FLD];
+  __shared__ __attribute__((aligned(16))) bf16_t dSq[FB * KLD];    // dS[q][key]
+  __shared__ float lse_s[FB], delta_s[FB];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int d = H * FD, ld3 = 3 * d;
+  const int kw = w * 16;
+  const bf16_t* base = qkv + (long)b * S * ld3;
+  const bf16_t* dbase = dout + (long)b * S * d;
+
+  bf16x8 kf[2], vf[2];
+  {
+    const int key = kw + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 32 + 8 * (lane >> 4);
+      kf[ks] = key < S ? ld8(base + (long)key * ld3 + d + h * FD + c) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+      vf[ks] = key < S ? ld8(base + (long)key * ld3 + 2 * d + h * FD + c) : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  stage_tile512(base + d + h * FD, ld3, S, nullptr, Kt, KLD);
+  stage_tile512(base + (long)FB * ld3 + d + h * FD, ld3, S - FB, nullptr, Kt + FB, KLD);
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) { dk[nt] = (f32x4){0.f, 0.f, 0.f, 0.f}; dv[nt] = dk[nt]; }
+  // dQ role of this wave: 16 query rows (w & 3) x 32 dims (w >> 2) of each tile
+  const int qr = (w & 3) * 16, nt0 = (w >> 2) * 2;
+  float sq[2] = {0.f, 0.f};
+
+  for (int q0 = 0; q0 < S; q0 += FB) {
+    __syncthreads();
+    stage_tile512(base + (long)q0 * ld3 + h * FD, ld3, S - q0, Qs, Qt, FLD);
+    stage_tile512(dbase + (long)q0 * d + h * FD, d, S - q0, dOs, dOt, FLD);
+    if (threadIdx.x < FB) {
+      const int q = q0 + threadIdx.x;
+      float dl = 0.f;
+      if (q < S) {
+        const long off = ((long)b * S + q) * d + h * FD;
+#pragma unroll
+        for (int c = 0; c < FD; c += 8) {
+          const u32x4 x = *reinterpret_cast<const u32x4*>(dout + off + c);
+          const u32x4 y = *reinterpret_cast<const u32x4*>(o + off + c);
+          const unsigned wx[4] = {x.x, x.y, x.z, x.w}, wy[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            dl += bf2f((bf16_t)(wx[j] & 0xffff)) * bf2f((bf16_t)(wy[j] & 0xffff)) +
+                  bf2f((bf16_t)(wx[j] >> 16)) * bf2f((bf16_t)(wy[j] >> 16));
+        }
+      }
+      lse_s[threadIdx.x] = q < S ? lse[(long)bh * S + q] : 0.f;
+      delta_s[threadIdx.x] = dl;
+    }
+    __syncthreads();
+    // this wave's keys see any query of the tile (uniform per wave)
+    const bool active = kw < S && !(causal && kw > q0 + FB - 1);
+    if (active) {
+      f32x4 st[4], dpt[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        st[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        dpt[nt] = st[nt];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int c = (nt * 16 + (lane & 15)) * FLD + ks * 32 + 8 * (lane >> 4);
+          st[nt] = mfma16x16x32(kf[ks], ld8(&Qs[c]), st[nt]);
+          dpt[nt] = mfma16x16x32(vf[ks], ld8(&dOs[c]), dpt[nt]);
+        }
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int ql = nt * 16 + (lane & 15), q = q0 + ql;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int kl = (lane >> 4) * 4 + e, key = kw + kl;
+          const bool ok = q < S && key < S && !(causal && key > q);
+          const float p = ok ? __expf(st[nt][e] * scale - lse_s[ql]) : 0.f;
+          const float ds = p * (dpt[nt][e] - delta_s[ql]);
+          Pw[w][kl * FLD + ql] = f2bf(p);
+          const bf16_t dsb = f2bf(ds);
+          dSw[w][kl * FLD + ql] = dsb;
+          dSq[ql * KLD + kw + kl] = dsb;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dSq[(nt * 16 + (lane & 15)) * KLD + kw + (lane >> 4) * 4 + e] = 0;
+    }
+    __syncthreads();
+    if (active) {
+      // dV += P^T dO ; dK += dS^T Q   (K-dim = the 64 queries)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int ca = (lane & 15) * FLD + ks * 32 + 8 * (lane >> 4);
+        const bf16x8 pa = ld8(&Pw[w][ca]), sa = ld8(&dSw[w][ca]);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const int cb = (nt * 16 + (lane & 15)) * FLD + ks * 32 + 8 * (lane >> 4);
+          dv[nt] = mfma16x16x32(pa, ld8(&dOt[cb]), dv[nt]);
+          dk[nt] = mfma16x16x32(sa, ld8(&Qt[cb]), dk[nt]);
+        }
+      }
+    }
+    // dQ[q0 + qr .. +16][32 dims] = scale * dS K over every key that can be unmasked
+    const int kmax = causal ? min(S, q0 + FB) : S;
+    f32x4 dq[2];
+    dq[0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    dq[1] = dq[0];
+    for (int ks = 0; ks < (kmax + 31) / 32; ++ks) {
+      const bf16x8 sa = ld8(&dSq[(qr + (lane & 15)) * KLD + ks * 32 + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        dq[j] = mfma16x16x32(sa, ld8(&Kt[((nt0 + j) * 16 + (lane & 15)) * KLD + ks * 32 + 8 * (lane >> 4)]), dq[j]);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int q = q0 + qr + (lane >> 4) * 4 + e;
+      if (q >= S) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bf16_t qb = f2bf(dq[j][e] * scale);
+        dqkv[((long)b * S + q) * ld3 + h * FD + (nt0 + j) * 16 + (lane & 15)] = qb;
+        sq[j] += bf2f(qb);
+      }
+    }
+  }
+  float sk[4] = {0.f, 0.f, 0.f, 0.f}, sv[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int key = kw + (lane >> 4) * 4 + e;
+    if (key >= S) continue;
+    bf16_t* row = dqkv + ((long)b * S + key) * ld3 + h * FD + (lane & 15);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const bf16_t kb = f2bf(dk[nt][e] * scale), vb = f2bf(dv[nt][e]);
+      row[d + nt * 16] = kb;
+      row[2 * d + nt * 16] = vb;
+      sk[nt] += bf2f(kb);
+      sv[nt] += bf2f(vb);
+    }
+  }
+  if (dbias) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      sk[nt] += __shfl_xor(sk[nt], 16, 64);
+      sk[nt] += __shfl_xor(sk[nt], 32, 64);
+      sv[nt] += __shfl_xor(sv[nt], 16, 64);
+      sv[nt] += __shfl_xor(sv[nt], 32, 64);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      sq[j] += __shfl_xor(sq[j], 16, 64);
+      sq[j] += __shfl_xor(sq[j], 32, 64);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        atomicAdd(dbias + d + h * FD + nt * 16 + lane, sk[nt]);
+        atomicAdd(dbias + 2 * d + h * FD + nt * 16 + lane, sv[nt]);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) atomicAdd(dbias + h * FD + (nt0 + j) * 16 + lane, sq[j]);
+    }
+  }
+}
+
 }  // namespace jdt
 using namespace jdt;
 
@@ -368,12 +580,21 @@ JDT_API int jdt_flash_fwd(const void* qkv, void* out, float* lse, int B, int S, 
   return HIP_LAUNCH_CHECK();
 }
 
+static bool g_flash_head = true;
+JDT_API void jdt_flash_set_head(int on) { g_flash_head = on; }  // A/B: 0 = key-block kernel at every S
+
 // dq_acc: fp32 [B*S, H*64] workspace, all zero on entry and left zero on exit;
 // tickets: B*H counters, zero on entry and on exit.
 // dbias (optional, fp32 [3*H*64]): += column sums of dQKV (the QKV bias gradient).
 JDT_API int jdt_flash_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* dq_acc,
                           unsigned* tickets, void* dqkv, float* dbias, int B, int S, int H, float scale, int causal,
                           void* stream) {
+  if (S <= FS && g_flash_head) {  // whole head in one workgroup: dq_acc / tickets untouched (stay zero)
+    hipLaunchKernelGGL(flash_bwd_head_kernel, dim3(B * H), dim3(512), 0, static_cast<hipStream_t>(stream),
+                       static_cast<const bf16_t*>(qkv), static_cast<const bf16_t*>(out),
+                       static_cast<const bf16_t*>(dout), lse, static_cast<bf16_t*>(dqkv), dbias, S, H, scale, causal);
+    return HIP_LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(flash_bwd_kernel, dim3((S + FB - 1) / FB, B * H), dim3(256), 0, static_cast<hipStream_t>(stream),
                      static_cast<const bf16_t*>(qkv), static_cast<const bf16_t*>(out),
                      static_cast<const bf16_t*>(dout), lse, static_cast<bf16_t*>(dqkv), dq_acc, tickets, dbias, S, H, scale,

@@ -46,6 +46,7 @@ _SIGS = {
     "jdt_gemm_set_group_tile": (None, [c_int]),
     "jdt_ln_set_rows": (None, [c_int]),
     "jdt_gemm_set_epi_vec": (None, [c_int]),
+    "jdt_gemm_set_epi_vec_min": (None, [c_long]),
     "jdt_gemm_set_deep": (None, [c_int]),
     "jdt_gemm_set_r": (None, [c_int]),
     "jdt_gemm_set_tune": (None, [c_int]),
@@ -125,6 +126,12 @@ def lib():
             raise RuntimeError("GemmArgs layout mismatch between Python and csrc/gemm.hip")
         if os.environ.get("JDT_GROUP_SPLIT") == "0":   # A/B: no split-K inside grouped GEMM launches
             l.jdt_gemm_set_group_split(0)
+        if os.environ.get("JDT_GEMM_TUNE") == "0":  # A/B: heuristic tile choice only
+            l.jdt_gemm_set_tune(0)
+        if os.environ.get("JDT_GEMM_EPI_VEC") == "0":  # A/B: per-element GEMM epilogue
+            l.jdt_gemm_set_epi_vec(0)
+        if os.environ.get("JDT_GEMM_EPI_MIN"):  # A/B: vectorised epilogue only from this many outputs
+            l.jdt_gemm_set_epi_vec_min(int(os.environ["JDT_GEMM_EPI_MIN"]))
         if os.environ.get("JDT_GEMM_R"):  # A/B: force the LDS-DMA GEMM's sub-tiles per ring slot
             l.jdt_gemm_set_r(int(os.environ["JDT_GEMM_R"]))
         _lib = l

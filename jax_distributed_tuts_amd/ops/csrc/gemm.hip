@@ -1358,6 +1358,7 @@ static int launch_cfg(const GemmArgs& g, int batch, int splits, float* ws, long 
 
 
 static bool g_epi_vec = true;  // jdt_gemm_set_epi_vec(0): per-element epilogue (A/B tests)
+static long g_epi_vec_min = 0;  // jdt_gemm_set_epi_vec_min(n): vectorised epilogue only from n outputs
 static bool g_gemm_no_dma = false;  // jdt_gemm_set_dma(0): register-staged kernels only (A/B tests)
 static int g_group_split = 1;  // jdt_gemm_set_group_split(0): no split-K inside grouped launches (A/B tests)
 
@@ -1410,7 +1411,10 @@ static int launch_dma(const GemmArgs& g, int batch, int splits, float* ws, long 
   if (g_dma_deep < 0 && kchunk / DMA_BK < 16) deep = false;
   dim3 grid((g.M / BM) * tiles_n, sp, batch);
   const bool at = g.a_trans, bt = g.b_trans;
-  const int vec = g_epi_vec && epi_vec_ok(g, batch);
+  // 32 x 32 tiles keep the per-element epilogue: the LDS round trip and barrier
+  // cost more than the narrow stores on those small outputs (in-model A/B,
+  // tools/gpu_r2_ab_epi.sh: microbatch-loop transformer 3.07 ms vec vs 2.98)
+  const int vec = g_epi_vec && BM * BN >= 2048 && (long)g.M * g.N * batch >= g_epi_vec_min && epi_vec_ok(g, batch);
   // sub-tiles per ring slot: g_dma_r forces (sweeps), else 1
   int R = g_dma_r > 0 ? g_dma_r : r_pref;
   while (R > 1 && (kchunk / DMA_BK) % R) R >>= 1;
@@ -1443,18 +1447,13 @@ static int launch_dma(const GemmArgs& g, int batch, int splits, float* ws, long 
 // LDS-DMA path for bf16 operands: returns 1 if the shape / layout is outside
 // its envelope (caller falls back to the register-staged kernels).
 // Measured tile choices (tools/bench_gemm.py --cfg C --r R sweeps on MI355X,
-// gpurun_out/sw*/ -> profiles/r2_gemm_tile_sweep.txt): the transformer / MLP
-// shapes of the BASELINE configs.  {M, N, K, a_trans, b_trans, cfg, R}.
+// profiles/r2_gemm_tile_sweep.txt): the 2048-token transformer shapes.  The
+// 512-row entries the isolated sweep also favoured were dropped: inside the
+// microbatch-loop transformer step (colder operands, neighbouring kernels) they
+// measured 2 % slower than the heuristic (tools/gpu_r2_ab_tune.sh).
+// {M, N, K, a_trans, b_trans, cfg, R}.
 struct GemmTune { int M, N, K, at, bt, cfg, r; };
 static const GemmTune kGemmTune[] = {
-    {512, 1536, 512, 0, 1, 11, 2},    // qkv fwd (512 rows)        6.81 us (torch 7.36)
-    {512, 512, 512, 0, 1, 13, 4},     // out fwd                   5.09 (6.64)
-    {512, 2048, 512, 0, 1, 11, 2},    // fc1 / head fwd            6.90 (7.53)
-    {512, 512, 2048, 0, 1, 13, 2},    // fc2 fwd                   9.53 (10.03)
-    {512, 512, 2048, 0, 0, 13, 2},    // fc1 dX                    8.69 (6.87)
-    {512, 2048, 512, 0, 0, 11, 2},    // fc2 dX                    6.52 (6.28)
-    {512, 2048, 512, 1, 1, 11, 2},    // fc1 dW                    7.51 (8.45)
-    {2048, 512, 512, 1, 1, 11, 2},    // fc2 dW                    7.59 (8.38)
     {2048, 1536, 512, 0, 1, 11, 1},   // qkv fwd (2048 rows)       10.38 (12.15)
     {2048, 512, 2048, 0, 1, 10, 2},   // fc2 fwd                   14.41 (13.78)
     {512, 2048, 2048, 1, 1, 10, 1},   // fc1 / head dW             18.54 (16.64)
@@ -1541,7 +1540,7 @@ static int group_plan(const GemmArgs* gs, int n, GemmGroup& G, float* ws, long w
     G.splits[p] = sp;
     G.wsoff[p] = wsused;
     G.cntoff[p] = (int)cntused;
-    G.vec[p] = g_epi_vec && epi_vec_ok(g, 1);
+    G.vec[p] = g_epi_vec && T * T >= 2048 && (long)g.M * g.N >= g_epi_vec_min && epi_vec_ok(g, 1);
     if (sp > 1) { wsused += tiles * sp * T * T; cntused += tiles; }
     total += (int)(tiles * sp);
   }
@@ -1603,6 +1602,7 @@ JDT_API void jdt_gemm_set_preload(int on) { g_gemm_no_preload = !on; }
 JDT_API void jdt_gemm_set_exact(int pre) { g_exact_pre = pre; }
 JDT_API void jdt_gemm_set_dma(int on) { g_gemm_no_dma = !on; }
 JDT_API void jdt_gemm_set_epi_vec(int on) { g_epi_vec = on; }
+JDT_API void jdt_gemm_set_epi_vec_min(long n) { g_epi_vec_min = n; }
 JDT_API void jdt_gemm_set_deep(int d) { g_dma_deep = d; }
 JDT_API void jdt_gemm_set_r(int r) { g_dma_r = r; }
 JDT_API void jdt_gemm_set_tune(int on) { g_gemm_tune = on; }

@@ -23,7 +23,8 @@ bucket (grads + metric slots) per stage; the optimizer is the same fused AdamW.
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass
+import os
+from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
 import torch
@@ -80,7 +81,7 @@ class PipeConfig:
     # default: measured slower in the captured step (transformer 3.07 -> 3.78 ms,
     # 8-layer MLP 0.79 -> 1.05 ms on one MI355X -- the fork/join graph edges cost
     # more than the overlap gains at these kernel sizes)
-    overlap_wgrad: bool = False
+    overlap_wgrad: bool = field(default_factory=lambda: os.environ.get("JDT_OVERLAP_WGRAD") == "1")
     # single stage (pipe axis of size 1): GPipe has no neighbour to feed, so the
     # microbatches may run as ONE pass over all local rows (each row keeps its
     # microbatch's 1/mb loss weight: the same gradient as the microbatch loop, the

@@ -128,6 +128,50 @@ def test_gemm_dma_epilogues(a_layout, b_layout, cfg):
         _close(acc_g, acc_r, rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("cfg,r", [(10, 1), (10, 2), (11, 1), (11, 2), (12, 1), (13, 4), (14, 1)])
+@pytest.mark.parametrize("a_layout,b_layout", [("mk", "kn"), ("km", "nk")])
+def test_gemm_vec_epilogue_bit_identical(cfg, r, a_layout, b_layout):
+    """The vectorised LDS-image epilogue (gemm_finish_vec) computes every element
+    with the same arithmetic as the per-element one: outputs bit-identical for the
+    forward epilogue (bias, GELU, z_out, dropout, residual), the backward one (act'
+    * mask, dbias), bf16 / fp32 accumulate and split-K; at each tile config and
+    K sub-tiles per ring slot (r)."""
+    from jax_distributed_tuts_amd.ops import _lib
+
+    L = _lib.lib()
+    M, N, K_ = 256, 384, 512
+    a = _mk((M, K_) if a_layout == "mk" else (K_, M), torch.bfloat16, seed=81).to(DEV)
+    b = (_mk((K_, N) if b_layout == "kn" else (N, K_), torch.float32, seed=82) * 0.05).to(torch.bfloat16).to(DEV)
+    bias, res = _mk((N,), torch.bfloat16, seed=83).to(DEV), _mk((M, N), torch.bfloat16, seed=84).to(DEV)
+    z = _mk((M, N), torch.bfloat16, seed=85).to(DEV)
+    kw = dict(a_layout=a_layout, b_layout=b_layout, cfg=cfg)
+
+    def run():
+        zo = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        f = kern.gemm(a, b, bias=bias, act="gelu", z_out=zo, keep_prob=0.9, seed=7, offset=11, resid=res, **kw)
+        db = torch.zeros(N, device=DEV)
+        g = kern.gemm(a, b, z_in=z, act_bwd="silu", keep_prob=0.9, seed=3, offset=5, dbias=db, **kw)
+        acc16 = res.clone()
+        kern.gemm(a, b, out=acc16, accumulate=True, **kw)
+        acc32 = [torch.full((M, N), 0.5, device=DEV) for _ in range(2)]
+        kern.gemm(a, b, out=acc32[0], accumulate=True, **kw)
+        kern.gemm(a, b, out=acc32[1], accumulate=True, splits=4, **kw)
+        torch.cuda.synchronize()
+        return [zo, f, g, acc16, acc32[0], acc32[1]], db
+
+    L.jdt_gemm_set_r(r)
+    try:
+        outs_v, db_v = run()
+        L.jdt_gemm_set_epi_vec(0)
+        outs_e, db_e = run()
+    finally:
+        L.jdt_gemm_set_epi_vec(1)
+        L.jdt_gemm_set_r(-1)
+    for x, y in zip(outs_v, outs_e):
+        assert torch.equal(x, y)
+    _close(db_v, db_e, rtol=1e-5, atol=1e-4)  # fp32 atomics: summation order differs
+
+
 @pytest.mark.parametrize("tile", [32, 64, 128])
 def test_gemm_group_tiles(tile):
     """Grouped launch at each tile size (forced): a weight gradient (km x kn, fp32

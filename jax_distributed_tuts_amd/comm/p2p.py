@@ -142,6 +142,7 @@ class XgmiP2P:
                 n = min(self.slot_bytes // 4, 1 << 16) // 4 * 4
                 ep = torch.zeros(1, dtype=torch.int32, device=dev)
                 for it in range(8):
+                    ok = True  # a failing rank keeps sending, so no peer waits on it mid-epoch
                     for slot in range(self.n_slots):
                         x = torch.arange(n, device=dev, dtype=torch.float32) + 1000 * r + 7 * it + slot
                         out = torch.empty(n, device=dev)
@@ -152,13 +153,15 @@ class XgmiP2P:
                         self.recv(out, slot, ep)
                         want = torch.arange(n, device=dev, dtype=torch.float32) + 1000 * ((r - 1) % W) + 7 * it + slot
                         torch.cuda.synchronize(dev)
-                        if self.error() or not torch.equal(out, want):
-                            log.warning("p2p self-test failed (iter %d slot %d)", it, slot)
-                            return False
+                        if ok and (self.error() or not torch.equal(out, want)):
+                            log.warning("p2p self-test failed on rank %d (iter %d slot %d)", r, it, slot)
+                            ok = False
                     ep += 1
-                    # the next epoch's sends may only start once every member read this one
+                    # the next epoch's sends may only start once every member read this one;
+                    # the verdict is collective, so every rank stops at the same epoch
                     torch.cuda.synchronize(dev)
-                    dist.barrier(group=self.group)
+                    if not self._agree(ok):
+                        return False
             # training epochs restart at 1: clear the flags the test raised
             _lib.check(_lib.lib().jdt_p2p_reset(self.ctx), "jdt_p2p_reset")
             dist.barrier(group=self.group)

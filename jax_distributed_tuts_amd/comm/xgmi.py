@@ -344,6 +344,15 @@ class XgmiComm:
                     " (barrier timeout)" if self.error() else "")
         return False
 
+    def _check(self, bad: bool, what: str) -> bool:
+        """Collective verdict of one self-test check: every rank learns whether ANY
+        rank failed before anyone issues the next collective (a rank that stopped
+        alone would leave the others' next RCCL call paired with its own
+        ``_agree`` all-reduce: mismatched collectives on one group)."""
+        if bad:
+            self._fail(what)
+        return self._agree(not bad)
+
     def _self_test_body(self) -> bool:
         W, r, dev = self.world, self.rank, self.device
         cap = self.capacity
@@ -360,10 +369,11 @@ class XgmiComm:
             if ref is not None:
                 dist.all_reduce(ref, group=self.group)
             torch.cuda.synchronize(dev)
-            if self.error() or not torch.equal(x, want):
-                return self._fail(f"all-reduce mismatch (iter {it}, n {n})")
-            if ref is not None and not torch.equal(x, ref):
-                return self._fail(f"all-reduce differs from RCCL (iter {it}, n {n})")
+            if not self._check(self.error() or not torch.equal(x, want), f"all-reduce mismatch (iter {it}, n {n})"):
+                return False
+            if not self._check(ref is not None and not torch.equal(x, ref),
+                               f"all-reduce differs from RCCL (iter {it}, n {n})"):
+                return False
         for k, n in enumerate(sizes[:2]):
             for rep in range(2):  # both parities
                 base = (torch.arange(n, device=dev, dtype=torch.int64) % 89).to(torch.float32)
@@ -374,8 +384,9 @@ class XgmiComm:
                 self.reduce_scatter(base + r, out, part)
                 lo, hi = r * part, min(n, (r + 1) * part)
                 torch.cuda.synchronize(dev)
-                if self.error() or not torch.equal(out[: hi - lo], want[lo:hi]):
-                    return self._fail(f"reduce-scatter mismatch (n {n})")
+                if not self._check(self.error() or not torch.equal(out[: hi - lo], want[lo:hi]),
+                                   f"reduce-scatter mismatch (n {n})"):
+                    return False
                 full = torch.empty(n, device=dev)
                 mine = torch.zeros(part, device=dev)
                 mine[: hi - lo] = base[lo:hi] + 1000 * r + rep
@@ -385,8 +396,8 @@ class XgmiComm:
                 for q in range(W):
                     exp[q * part: min(n, (q + 1) * part)] += 1000 * q + rep
                 torch.cuda.synchronize(dev)
-                if self.error() or not torch.equal(full, exp):
-                    return self._fail(f"all-gather mismatch (n {n})")
+                if not self._check(self.error() or not torch.equal(full, exp), f"all-gather mismatch (n {n})"):
+                    return False
         if not self._self_test_segments():
             return False
         return self._self_test_adamw()
@@ -408,8 +419,8 @@ class XgmiComm:
             for k, s in enumerate(parts):
                 exp = torch.cat([(torch.arange(s, device=dev, dtype=torch.float32) % 31) + 100 * q + k + rep
                                  for q in range(W)])
-                if self.error() or not torch.equal(fulls[k], exp):
-                    return self._fail("segmented all-gather mismatch")
+                if not self._check(self.error() or not torch.equal(fulls[k], exp), "segmented all-gather mismatch"):
+                    return False
             src = [(torch.arange(W * s, device=dev, dtype=torch.float32) % 53) * (r + 1) for s in parts]
             outs = [torch.full((s,), float(rep), device=dev) for s in parts]
             self._skew(rep + 1)
@@ -417,8 +428,9 @@ class XgmiComm:
             torch.cuda.synchronize(dev)
             for k, s in enumerate(parts):
                 full = (torch.arange(W * s, device=dev, dtype=torch.float32) % 53) * (W * (W + 1) // 2)
-                if self.error() or not torch.equal(outs[k], full[r * s:(r + 1) * s] + rep):
-                    return self._fail("segmented reduce-scatter mismatch")
+                if not self._check(self.error() or not torch.equal(outs[k], full[r * s:(r + 1) * s] + rep),
+                                   "segmented reduce-scatter mismatch"):
+                    return False
         return True
 
     def _self_test_adamw(self) -> bool:
@@ -454,17 +466,17 @@ class XgmiComm:
                    or not torch.allclose(p, pr, rtol=1e-5, atol=1e-6)
                    or not torch.allclose(m, mr, rtol=1e-5, atol=1e-7)
                    or not torch.allclose(v, vr, rtol=1e-5, atol=1e-9))
-            if bad:
-                return self._fail(f"fused AdamW all-reduce mismatch (step {t})")
+            if not self._check(bad, f"fused AdamW all-reduce mismatch (step {t})"):
+                return False
         want_running = sum(sum(((g0[n_params:] * (q + 1) + t) % 13 - 6).to(torch.float32) for q in range(W))
                            for t in range(1, 4))
-        if not torch.equal(running, want_running):
-            return self._fail("fused metrics fold mismatch")
+        if not self._check(not torch.equal(running, want_running), "fused metrics fold mismatch"):
+            return False
         # the staged variant (bucket pre-written into the staging half of the step's
         # parity, as mlp2_bwd / md_bwd do in DP): 3 more steps continuing the state
         plan = self.stage_plan(n)
-        if plan is None:
-            return self._fail("no unpadded staged geometry for the self-test bucket")
+        if not self._check(plan is None, "no unpadded staged geometry for the self-test bucket"):
+            return False
         for t in range(4, 7):
             grad = ((g0 * (r + 1) + t) % 13 - 6).to(torch.float32)
             gsum = sum(((g0 * (q + 1) + t) % 13 - 6).to(torch.float32) for q in range(W))
@@ -482,8 +494,8 @@ class XgmiComm:
                    or not torch.allclose(p, pr, rtol=1e-5, atol=1e-6)
                    or not torch.allclose(m, mr, rtol=1e-5, atol=1e-7)
                    or not torch.allclose(v, vr, rtol=1e-5, atol=1e-9))
-            if bad:
-                return self._fail(f"staged fused AdamW all-reduce mismatch (step {t})")
+            if not self._check(bad, f"staged fused AdamW all-reduce mismatch (step {t})"):
+                return False
         return True
 
 

@@ -262,3 +262,28 @@ def replication_desync(out_dir):
     except ReplicationError as e:
         res = str(e)
     _save(out_dir, "repdesync", {"res": res})
+
+
+def selftest_verdict(out_dir):
+    """The xGMI / P2P self-test verdicts are collective: a failure seen by rank 1
+    alone stops every rank at the same check, and a following collective still
+    pairs up (a rank that returned alone would have paired its ``_agree`` with the
+    others' next RCCL call)."""
+    import torch.distributed as dist
+
+    from jax_distributed_tuts_amd.comm.xgmi import XgmiComm
+
+    c = object.__new__(XgmiComm)  # no device buffers: only the verdict plumbing
+    c.group, c.rank, c.world, c.device = dist.group.WORLD, D.rank(), D.world_size(), torch.device("cpu")
+    c.ctx = None
+    c.error = lambda: 0
+    c._fail = lambda what: False
+    seen = []
+    for it in range(4):
+        ok = c._check(D.rank() == 1 and it == 2, f"check {it}")
+        seen.append(ok)
+        if not ok:
+            break
+    t = torch.tensor([float(len(seen))])
+    dist.all_reduce(t)  # pairs up only if every rank stopped at the same check
+    _save(out_dir, "verdict", {"seen": seen, "total": float(t.item())})

@@ -148,3 +148,11 @@ def test_replication_check_catches_desynchronised_rank(tmp_path):
     spawn(W.replication_desync, 2, str(tmp_path))
     for o in _load(tmp_path, "repdesync", 2):
         assert "diverged" in o["res"] and "param/output_dense/bias" in o["res"], o["res"]
+
+
+def test_selftest_verdict_is_collective(tmp_path):
+    """A self-test check failing on one rank stops every rank at that check."""
+    spawn(W.selftest_verdict, 3, str(tmp_path))
+    for r in _load(str(tmp_path), "verdict", 3):
+        assert r["seen"] == [True, True, False]
+        assert r["total"] == 9.0

@@ -536,12 +536,24 @@ JDT_API int jdt_xgmi_stage_clear(void* ctx, void* stream) {
   return (int)hipMemsetAsync(c->data, 0, 2 * c->cap * sizeof(float), static_cast<hipStream_t>(stream));
 }
 
+// Plain (non-system-scope) global stores, exactly the store path of a staged
+// producer's epilogue (mlp2_bwd / md_bwd mode 0 writing the bucket), so the
+// self-test's staged steps check that path's cross-GPU visibility and not a
+// copy engine's.
+__global__ void __launch_bounds__(256) xg_stage_copy_kernel(float* __restrict__ dst, const float* __restrict__ src,
+                                                            long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) dst[i] = src[i];
+}
+
 // Copy src[0, n) into the staging half `parity` (self-test / tools).
 JDT_API int jdt_xgmi_stage_write(void* ctx, int parity, const float* src, long n, void* stream) {
   XgCtx* c = static_cast<XgCtx*>(ctx);
   if (n < 0 || n > c->cap) return -2;
-  return (int)hipMemcpyAsync(c->data + (long)(parity & 1) * c->cap, src, n * sizeof(float), hipMemcpyDeviceToDevice,
-                             static_cast<hipStream_t>(stream));
+  if (n == 0) return 0;
+  const long g = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+  hipLaunchKernelGGL(xg_stage_copy_kernel, dim3((unsigned)g), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     c->data + (long)(parity & 1) * c->cap, src, n);
+  return HIP_LAUNCH_CHECK();
 }
 
 // All-reduce + fused AdamW of a bucket a producer kernel already staged (see xg_kernel).

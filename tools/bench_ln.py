@@ -46,7 +46,13 @@ def main():
             t = timed(lambda: K.layernorm_bwd(dy, x, mean, rstd, gamma, dg, db, dres=dres, dsum=ds))
             row.append(f"R={R or 'auto'}: {t:6.2f} us")
         _lib.lib().jdt_ln_set_rows(0)
-        print(f"ln_bwd T={T} d={d}: " + " | ".join(row))
+        # floors: the same kernel without the column-sum outputs (no atomics), a
+        # forward, and a bf16 add of two [T, d] tensors (3 tensor passes)
+        t_na = timed(lambda: K.layernorm_bwd(dy, x, mean, rstd, gamma, None, None, dres=dres, dsum=None))
+        t_f = timed(lambda: K.layernorm_fwd(x, gamma, torch.zeros(d, device=dev)))
+        t_add = timed(lambda: torch.add(dy, dres))
+        print(f"ln_bwd T={T} d={d}: " + " | ".join(row) +
+              f" | no colsums {t_na:6.2f} | ln_fwd {t_f:6.2f} | torch add {t_add:6.2f} us")
 
 
 if __name__ == "__main__":

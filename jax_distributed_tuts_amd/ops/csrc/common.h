@@ -36,6 +36,27 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 __device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
 
 // ---------------------------------------------------------------- reductions
+// Whole-wave sum through DPP lane moves (no LDS): quad_perm swaps (xor 1, xor 2),
+// row_half_mirror and row_mirror leave every 16-lane row uniform, then the four
+// row values are read into SGPRs.  The ds_bpermute butterfly of wave_sum costs
+// one LDS round trip (and an lgkmcnt wait) per step: 6 dependent round trips.
+// The result is identical in every lane (fixed order).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);

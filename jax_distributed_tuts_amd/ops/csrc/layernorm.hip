@@ -11,6 +11,11 @@ namespace jdt {
 
 constexpr int LN_MAXV = 4;  // 4 x 8 x 64 = 2048 columns max
 
+// Forward: one wave per row.  The affine parameters' loads are issued together
+// with the row's (the previous version computed the statistics first and only
+// then loaded gamma / beta: a second dependent memory round trip), and the two
+// row reductions are DPP lane moves (wave_sum_dpp) instead of ds_bpermute
+// butterflies.
 template <int NV>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, bf16_t* __restrict__ y,
@@ -20,27 +25,34 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= T) return;
   const bf16_t* xr = x + (long)row * d;
+  u32x4 p[NV];
+  float4 g[NV][2], bt[NV][2];
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    p[c] = (u32x4){0u, 0u, 0u, 0u};
+    g[c][0] = g[c][1] = bt[c][0] = bt[c][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (col < d) {
+      p[c] = *reinterpret_cast<const u32x4*>(xr + col);
+      g[c][0] = *reinterpret_cast<const float4*>(gamma + col);
+      g[c][1] = *reinterpret_cast<const float4*>(gamma + col + 4);
+      bt[c][0] = *reinterpret_cast<const float4*>(beta + col);
+      bt[c][1] = *reinterpret_cast<const float4*>(beta + col + 4);
+    }
+  }
   float v[NV][8];
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < NV; ++c) {
-    const int col = (c * 64 + lane) * 8;
-    if (col < d) {
-      const u32x4 p = *reinterpret_cast<const u32x4*>(xr + col);
-      const unsigned w[4] = {p.x, p.y, p.z, p.w};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[c][2 * j] = bf2f((bf16_t)(w[j] & 0xffff));
-        v[c][2 * j + 1] = bf2f((bf16_t)(w[j] >> 16));
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+    for (int j = 0; j < 4; ++j) {
+      v[c][2 * j] = bf2f((bf16_t)(p[c][j] & 0xffff));
+      v[c][2 * j + 1] = bf2f((bf16_t)(p[c][j] >> 16));
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += v[c][j];
   }
-  const float mean = wave_sum(s) / d;
+  const float mean = wave_sum_dpp(s) / d;
   float q = 0.f;
 #pragma unroll
   for (int c = 0; c < NV; ++c) {
@@ -49,20 +61,22 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 8; ++j) { const float t = v[c][j] - mean; q += t * t; }
   }
-  const float rstd = rsqrtf(wave_sum(q) / d + eps);
+  const float rstd = rsqrtf(wave_sum_dpp(q) / d + eps);
   if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
 #pragma unroll
   for (int c = 0; c < NV; ++c) {
     const int col = (c * 64 + lane) * 8;
     if (col < d) {
-      unsigned w[4];
+      const float gg[8] = {g[c][0].x, g[c][0].y, g[c][0].z, g[c][0].w, g[c][1].x, g[c][1].y, g[c][1].z, g[c][1].w};
+      const float bb[8] = {bt[c][0].x, bt[c][0].y, bt[c][0].z, bt[c][0].w,
+                           bt[c][1].x, bt[c][1].y, bt[c][1].z, bt[c][1].w};
+      u32x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float a = (v[c][2 * j] - mean) * rstd * gamma[col + 2 * j] + beta[col + 2 * j];
-        const float b = (v[c][2 * j + 1] - mean) * rstd * gamma[col + 2 * j + 1] + beta[col + 2 * j + 1];
-        w[j] = (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+        const float a = (v[c][2 * j] - mean) * rstd * gg[2 * j] + bb[2 * j];
+        const float b = (v[c][2 * j + 1] - mean) * rstd * gg[2 * j + 1] + bb[2 * j + 1];
+        o[j] = (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
       }
-      u32x4 o; o.x = w[0]; o.y = w[1]; o.z = w[2]; o.w = w[3];
       *reinterpret_cast<u32x4*>(y + (long)row * d + col) = o;
     }
   }
@@ -135,8 +149,8 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
         ab[c][j] += dv;
       }
     }
-    s1 = wave_sum(s1) / d;
-    s2 = wave_sum(s2) / d;
+    s1 = wave_sum_dpp(s1) / d;
+    s2 = wave_sum_dpp(s2) / d;
     if (row < T) {
 #pragma unroll
       for (int c = 0; c < NV; ++c) {
@@ -182,6 +196,9 @@ using namespace jdt;
 JDT_API int jdt_ln_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd, int T,
                        int d, float eps, void* stream) {
   if (d % 8 || d > 2048) return -3;
+  if ((reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta) | reinterpret_cast<uintptr_t>(x) |
+       reinterpret_cast<uintptr_t>(y)) & 15)
+    return -2;
   const int nv = (d / 8 + 63) / 64;
   dim3 grid((T + 3) / 4);
   hipStream_t st = static_cast<hipStream_t>(stream);

@@ -20,6 +20,26 @@ __device__ __forceinline__ float ld_logit(const void* p, long i) {
   return F32 ? static_cast<const float*>(p)[i] : bf2f(static_cast<const bf16_t*>(p)[i]);
 }
 
+// Metrics epilogue shared by both kernels: the workgroup's (loss, valid, correct)
+// sums -> metrics[0..3] += (loss, n, correct, n), one atomic per slot.  (A
+// two-level ticket tree instead of the same-address atomics measured slower: its
+// latency chain of two device-scope tickets and two row loads costs ~6 us against
+// the atomics' serialisation, tools/bench_xent.py; fewer, longer workgroups are the
+// cheaper fix, see rpw.)
+__device__ __forceinline__ void xent_metrics_fold(float (*red)[4], int w, int lane, float l_sum, float n_valid,
+                                                  float n_correct, float* metrics) {
+  if (lane == 0) { red[w][0] = l_sum; red[w][1] = n_valid; red[w][2] = n_correct; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f, b = 0.f, c = 0.f;
+    for (int i = 0; i < 4; ++i) { a += red[i][0]; b += red[i][1]; c += red[i][2]; }
+    if (b > 0.f) {
+      atomicAdd(metrics + 0, a); atomicAdd(metrics + 1, b);
+      atomicAdd(metrics + 2, c); atomicAdd(metrics + 3, b);
+    }
+  }
+}
+
 template <bool F32>
 __global__ void __launch_bounds__(256) xent_kernel(const void* logits, long ld, const int* labels, int M, int C,
                                                    float grad_scale, bf16_t* dlogits, long ldd, float* dbias,
@@ -71,18 +91,7 @@ __global__ void __launch_bounds__(256) xent_kernel(const void* logits, long ld, 
       }
     }
   }
-  if (metrics) {
-    if (lane == 0) { red[w][0] = l_sum; red[w][1] = n_valid; red[w][2] = n_correct; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float a = 0.f, b = 0.f, c = 0.f;
-      for (int i = 0; i < 4; ++i) { a += red[i][0]; b += red[i][1]; c += red[i][2]; }
-      if (b > 0.f) {
-        atomicAdd(metrics + 0, a); atomicAdd(metrics + 1, b);
-        atomicAdd(metrics + 2, c); atomicAdd(metrics + 3, b);
-      }
-    }
-  }
+  if (metrics) xent_metrics_fold(red, w, lane, l_sum, n_valid, n_correct, metrics);
 }
 
 
@@ -129,30 +138,29 @@ __global__ void __launch_bounds__(256) xent_vec_kernel(const bf16_t* __restrict_
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (z[k][j] > mx) { mx = z[k][j]; besti = (k * 64 + lane) * 8 + j; }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float om = __shfl_xor(mx, o, 64);
-      const int oi = __shfl_xor(besti, o, 64);
-      if (om > mx || (om == mx && oi < besti)) { mx = om; besti = oi; }
-    }
+    // row max, then the lowest column index holding it (DPP lane moves, no LDS)
+    const float gmx = wave_max_dpp(mx);
+    besti = wave_min_dpp(mx == gmx ? besti : 0x7fffffff);
+    mx = gmx;
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < NV; ++k)
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += __expf(z[k][j] - mx);
-    s = wave_sum(s);
+    s = wave_sum_dpp(s);
     const float lse = mx + __logf(s);
-    // the label's logit: the owning lane broadcasts it
+    // the label's logit: the owning lane broadcasts it (the label is row-uniform)
     float zl = 0.f;
     if (valid) {
-      const int ok = label >> 3, kk = ok / 64, ln = ok % 64, jj = label & 7;
+      const int ok = label >> 3, kk = ok / 64, jj = label & 7;
+      const int ln = __builtin_amdgcn_readfirstlane(ok % 64);
       float mine = 0.f;
 #pragma unroll
       for (int k = 0; k < NV; ++k)
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (k == kk && j == jj) mine = z[k][j];
-      zl = __shfl(mine, ln, 64);
+      zl = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mine), ln));
     }
     const float loss = valid ? lse - zl : 0.f;
     if (row_loss && lane == 0) row_loss[row] = loss;
@@ -189,23 +197,15 @@ __global__ void __launch_bounds__(256) xent_vec_kernel(const bf16_t* __restrict_
     __syncthreads();
     for (int c = threadIdx.x; c < C; c += 256) atomicAdd(dbias + c, part[0][c] + part[1][c] + part[2][c] + part[3][c]);
   }
-  if (metrics) {
-    // loss, validity and correctness are wave-uniform: lane 0 holds the wave's sums
-    if (lane == 0) { red[w][0] = l_sum; red[w][1] = n_valid; red[w][2] = n_correct; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float a = 0.f, b = 0.f, c = 0.f;
-      for (int i = 0; i < 4; ++i) { a += red[i][0]; b += red[i][1]; c += red[i][2]; }
-      if (b > 0.f) {
-        atomicAdd(metrics + 0, a); atomicAdd(metrics + 1, b);
-        atomicAdd(metrics + 2, c); atomicAdd(metrics + 3, b);
-      }
-    }
-  }
+  // loss, validity and correctness are wave-uniform: lane 0 holds the wave's sums
+  if (metrics) xent_metrics_fold(red, w, lane, l_sum, n_valid, n_correct, metrics);
 }
 
 }  // namespace jdt
 using namespace jdt;
+
+static int g_xent_rpw = 0;
+JDT_API void jdt_xent_set_rpw(int r) { g_xent_rpw = r; }  // sweeps: rows per wave of the wide-vocabulary kernel
 
 JDT_API int jdt_xent(const void* logits, int logits_f32, long ld, const int* labels, int M, int C, float grad_scale,
                      void* dlogits, long ldd, float* dbias, float* metrics, float* row_loss, void* stream) {
@@ -213,7 +213,11 @@ JDT_API int jdt_xent(const void* logits, int logits_f32, long ld, const int* lab
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (!logits_f32 && C >= 256 && C % 8 == 0 && C <= 2048 && ld % 8 == 0 && ldd % 8 == 0 &&
       (reinterpret_cast<uintptr_t>(logits) & 15) == 0 && (reinterpret_cast<uintptr_t>(dlogits) & 15) == 0) {
-    const int rpw = M <= 1024 ? 1 : (M + 1023) / 1024;
+    // rows per wave: fewer workgroups = fewer same-address metric atomics, which
+    // serialise (tools/bench_xent.py, M = 2048: rpw 4 18.8 us, 2 22.1, 1 32.8;
+    // M = 512: rpw 2 10.6, 1 11.5)
+    int rpw = M >= 2048 ? 4 : (M >= 512 ? 2 : 1);
+    if (g_xent_rpw > 0) rpw = g_xent_rpw;
     dim3 vgrid((M + 4 * rpw - 1) / (4 * rpw));
     auto lg = static_cast<const bf16_t*>(logits);
     auto dl = static_cast<bf16_t*>(dlogits);

@@ -236,7 +236,8 @@ JDT_API int jdt_ln_bwd(const void* dy, const void* x, const float* mean, const f
   // rows per wave: fewer, longer workgroups cut the same-address column atomics
   // (3 x d per workgroup); g_ln_rows forces R (sweeps: tools/bench_ln.py)
   int R = g_ln_rows;
-  if (R == 0) R = T >= 1024 ? 4 : 2;  // T = 2048: R 4 8.6 us vs R 2 11.7; T = 512: R 2 5.1 vs 6.2
+  // T = 2048: R 8 7.6 us, 4 8.1, 2 11.2; T = 512: R 2 4.8 vs 4 5.6 (tools/bench_ln.py, DPP reductions)
+  if (R == 0) R = T >= 2048 ? 8 : (T >= 1024 ? 4 : 2);
   switch (nv) {
     case 1: if (R >= 8) JDT_LNB(1, 8); else if (R >= 4) JDT_LNB(1, 4); else JDT_LNB(1, 2); break;
     case 2: if (R >= 8) JDT_LNB(2, 8); else if (R >= 4) JDT_LNB(2, 4); else JDT_LNB(2, 2); break;

@@ -31,6 +31,9 @@ def add_common_args(ap: argparse.ArgumentParser, steps: int, accum_default: str 
                          "(the debug replacement of the reference's disabled shard_map check_rep)")
     ap.add_argument("--deterministic", action="store_true",
                     help="fixed-order reductions only (no fp32 atomics): bitwise-reproducible runs")
+    ap.add_argument("--serialize-kernels", action="store_true",
+                    help="debug: HIP_LAUNCH_BLOCKING=1 AMD_SERIALIZE_KERNEL=3 AMD_SERIALIZE_COPY=3, set before any GPU "
+                         "call (a fault then surfaces at the launch that caused it); slow")
     ap.add_argument("--optimizer", choices=["adamw", "sgd"], default="adamw",
                     help="adamw: the reference's optax.adamw (fused AdamW kernels); sgd: the fused SGD kernel")
     ap.add_argument("--steps", type=int, default=steps)
@@ -102,6 +105,12 @@ def entry_main(main, args, script: str):
        has exactly the requested number of ranks."""
     from ..runtime.launch import maybe_launch, resolve_gpus, run
 
+    if getattr(args, "serialize_kernels", False):
+        # read by the HIP runtime at initialisation: set here, before any GPU call,
+        # so this process and every rank the launcher starts inherit them
+        from .debug import SERIALIZE_ENV
+
+        os.environ.update(SERIALIZE_ENV)
     if args.sim_cpu:
         maybe_profile(args, script)
         run(main, args, sim_cpu=args.sim_cpu)

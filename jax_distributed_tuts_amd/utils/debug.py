@@ -53,12 +53,24 @@ def check_replicated(tensors: Dict[str, torch.Tensor], mesh: Optional[Mesh], axi
         raise ReplicationError(f"replicated tensors diverged on axis {axis!r}: {bad}")
 
 
+SERIALIZE_ENV = {"HIP_LAUNCH_BLOCKING": "1", "AMD_SERIALIZE_KERNEL": "3", "AMD_SERIALIZE_COPY": "3"}
+
+
 @contextlib.contextmanager
 def debug_mode(serialize: bool = True):
-    """Serialise kernel launches (faults surface at the offending launch)."""
-    old = {k: os.environ.get(k) for k in ("HIP_LAUNCH_BLOCKING", "AMD_SERIALIZE_KERNEL", "AMD_SERIALIZE_COPY")}
+    """Serialise kernel launches (faults surface at the offending launch).
+
+    The HIP runtime reads these variables when it initialises, so the context
+    only takes effect for a process (or child) that has not touched the GPU yet;
+    entry scripts expose it as ``--serialize-kernels``, applied before any GPU call."""
+    import warnings
+
+    old = {k: os.environ.get(k) for k in SERIALIZE_ENV}
     if serialize:
-        os.environ.update({"HIP_LAUNCH_BLOCKING": "1", "AMD_SERIALIZE_KERNEL": "3", "AMD_SERIALIZE_COPY": "3"})
+        if torch.cuda.is_initialized():
+            warnings.warn("debug_mode(): the HIP runtime is already initialised in this process; the "
+                          "serialisation variables only reach child processes (use --serialize-kernels)")
+        os.environ.update(SERIALIZE_ENV)
     try:
         yield
     finally:

@@ -47,7 +47,6 @@ _SIGS = {
     "jdt_ln_set_rows": (None, [c_int]),
     "jdt_gemm_set_epi_vec": (None, [c_int]),
     "jdt_gemm_set_epi_vec_min": (None, [c_long]),
-    "jdt_gemm_set_deep": (None, [c_int]),
     "jdt_gemm_set_r": (None, [c_int]),
     "jdt_gemm_set_tune": (None, [c_int]),
     "jdt_flash_set_head": (None, [c_int]),

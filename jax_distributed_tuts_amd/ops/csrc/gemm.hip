@@ -1370,20 +1370,14 @@ static int g_group_split = 1;  // jdt_gemm_set_group_split(0): no split-K inside
 template <int BM, int BN>
 constexpr int dma_stages() { return 3; }
 
-static int g_dma_deep = 0;  // jdt_gemm_set_deep(d): -1 auto, 0 never (default: measured no better), 1 always
-
-// Deep ring: with at most ~one workgroup per CU nothing else on the CU hides
-// the global->LDS latency, and a 3-stage ring keeps only 2 K-tiles in flight
-// (the K loop then runs at ~latency / 2 per K-tile).  Tiles of <= 64 x 64 fit 8
-// stages (<= 128 KB); the deep variant is used when the grid has <= 1 workgroup
-// per CU and enough K-tiles to fill the ring.
-constexpr int DMA_DEEP = 8;
+// (Measured and dropped, BENCH_NOTES.md: an 8-stage "deep" ring for grids of <= 1
+// workgroup per CU -- no faster in isolation, slower in-model; and software-
+// pipelined fragment reads (both 32-deep halves of a slot issued up front, counted
+// lgkmcnt) -- within noise: the K loop waits on the global->LDS ring, not on LDS.)
 static int g_dma_r = -1;  // jdt_gemm_set_r(r): force r 64-deep sub-tiles per ring slot (sweeps); -1 auto
 // R > 1 slots: 3 of them within 96 KB (and the vmcnt immediate range)
 template <int BM, int BN>
 constexpr bool r_ok(int r) { return (BM + BN) * DMA_BK * 2 * 3 * r <= 96 * 1024 && (BM / 32 + BN / 32) * r <= 63; }
-template <int BM, int BN>
-constexpr bool deep_ok() { return (BM + BN) * DMA_BK * 2 * DMA_DEEP <= 128 * 1024; }
 
 template <int WM, int WN, int TM, int TN>
 static int launch_dma(const GemmArgs& g, int batch, int splits, float* ws, long ws_floats, unsigned* counters,
@@ -1392,23 +1386,18 @@ static int launch_dma(const GemmArgs& g, int batch, int splits, float* ws, long 
   if (g.M % BM || g.N % BN) return 1;
   const int tiles_n = g.N / BN;
   const long tiles = (long)(g.M / BM) * tiles_n * batch;
-  const int ktiles = g.K / DMA_BK;
-  bool deep = deep_ok<BM, BN>() && (g_dma_deep == 1 || (g_dma_deep < 0 && tiles <= 256 && ktiles >= 16));
   int sp = splits;
   if (sp < 0) {
     // Measured (tools/bench_gemm.py sweeps): many small workgroups per CU hide
     // the load latency better than a split-K combine (whose last-arriving slice
     // reads every slab serially); split only while the grid has < 2 workgroups
-    // per CU, keeping slices >= 8 K-tiles -- and with a deep ring, only when the
-    // grid would leave over half the CUs idle.
+    // per CU, keeping slices >= 8 K-tiles.
     sp = 1;
-    const long fill = deep ? 128 : 512;
-    while (sp < 16 && tiles * sp < fill && (g.K / (2 * sp)) % DMA_BK == 0 && g.K / (2 * sp) >= 8 * DMA_BK) sp *= 2;
+    while (sp < 16 && tiles * sp < 512 && (g.K / (2 * sp)) % DMA_BK == 0 && g.K / (2 * sp) >= 8 * DMA_BK) sp *= 2;
   }
   if (sp < 1 || g.K % sp || (g.K / sp) % DMA_BK) return 1;
   if (sp > 1 && (!ws || !counters || tiles * sp * BM * BN > ws_floats || tiles > n_counters)) sp = 1;
   const int kchunk = g.K / sp;
-  if (g_dma_deep < 0 && kchunk / DMA_BK < 16) deep = false;
   dim3 grid((g.M / BM) * tiles_n, sp, batch);
   const bool at = g.a_trans, bt = g.b_trans;
   // 32 x 32 tiles keep the per-element epilogue: the LDS round trip and barrier
@@ -1424,9 +1413,6 @@ static int launch_dma(const GemmArgs& g, int batch, int splits, float* ws, long 
                      kchunk, ws, counters, vec)
 #define JDT_DMA(A_, B_)                                                   \
   do {                                                                    \
-    if constexpr (deep_ok<BM, BN>()) {                                    \
-      if (deep) { JDT_DMA_S(A_, B_, DMA_DEEP, 1); break; }                \
-    }                                                                     \
     if constexpr (r_ok<BM, BN>(4)) {                                      \
       if (R == 4) { JDT_DMA_S(A_, B_, 3, 4); break; }                     \
     }                                                                     \
@@ -1603,7 +1589,6 @@ JDT_API void jdt_gemm_set_exact(int pre) { g_exact_pre = pre; }
 JDT_API void jdt_gemm_set_dma(int on) { g_gemm_no_dma = !on; }
 JDT_API void jdt_gemm_set_epi_vec(int on) { g_epi_vec = on; }
 JDT_API void jdt_gemm_set_epi_vec_min(long n) { g_epi_vec_min = n; }
-JDT_API void jdt_gemm_set_deep(int d) { g_dma_deep = d; }
 JDT_API void jdt_gemm_set_r(int r) { g_dma_r = r; }
 JDT_API void jdt_gemm_set_tune(int on) { g_gemm_tune = on; }
 

@@ -120,13 +120,11 @@ def main():
     ap.add_argument("--splits", type=int, default=-1)
     ap.add_argument("--only", default=None, help="comma-separated shape names to run (e.g. 'qkv fwd,fc1 dW')")
     ap.add_argument("--groups", default=None, help="comma-separated group tiles to sweep (e.g. '32,64,128'; 0 = auto)")
-    ap.add_argument("--deep", type=int, default=-1, help="deep LDS ring: -1 auto, 0 never, 1 always")
     ap.add_argument("--r", type=int, default=-1, help="64-deep K sub-tiles per LDS ring slot (-1 auto)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     from jax_distributed_tuts_amd.ops import _lib
     _lib.lib().jdt_gemm_set_exact(args.exact)
-    _lib.lib().jdt_gemm_set_deep(args.deep)
     _lib.lib().jdt_gemm_set_r(args.r)
     out = []
     print(f"{'shape':14s} {'M':>5s} {'N':>5s} {'K':>5s} {'ours us':>9s} {'TF/s':>7s} {'torch us':>9s} {'TF/s':>7s}")

@@ -629,7 +629,7 @@ static bool epi_vec_ok(const GemmArgs& g, int batch) {
 
 template <int WM, int WN, int TM, int TN, int BK, bool AF32, bool BF32, int PRE, bool EXACT = false>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int vecA, int vecB, int splits,
-                                                   int kchunk, float* __restrict__ ws, unsigned* counters) {
+                                                   int kchunk, float* __restrict__ ws, unsigned* counters, int vec) {
   using T = Tile<WM, WN, TM, TN, BK>;
   constexpr int BM = T::BM, BN = T::BN, LDK = T::LDK;
   // EXACT slices keep the whole K-slice resident (one image, one barrier);
@@ -872,6 +872,15 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
 #undef AS
 #undef BS
 
+  if constexpr (BM * BN >= 2048 && (BM * (BN + 4) + 4) * 4 <= SMEM * 2) {
+    // interior tiles of a 16-byte-aligned output: the vectorised LDS-image epilogue
+    if (vec && tm0 + BM <= g.M && tn0 + BN <= g.N) {
+      __syncthreads();  // every wave is past its last read of the staging images
+      gemm_finish_vec<BM, BN, TM, TN>(g, acc, tm0, tn0, z, wm, wn, lane, tid, splits, split,
+                                      (long)z * gridDim.x + bid, ws, counters, reinterpret_cast<float*>(smem));
+      return;
+    }
+  }
   gemm_finish<BM, BN, TM, TN>(g, acc, tm0, tn0, z, wid, wm, wn, lane, tid, splits, split, (long)z * gridDim.x + bid,
                               ws, counters, reinterpret_cast<int*>(smem));
 }
@@ -1277,6 +1286,9 @@ static int g_exact_pre = 0;  // jdt_gemm_set_exact(pre): force the exact slice d
 constexpr int kPreMax = 4;      // K-tiles a preloading slice holds in registers
 static bool g_gemm_no_preload = false;  // jdt_gemm_set_preload(0): pipelined path only (A/B tests)
 
+static bool g_epi_vec = true;  // jdt_gemm_set_epi_vec(0): per-element epilogue (A/B tests)
+static long g_epi_vec_min = 0;  // jdt_gemm_set_epi_vec_min(n): vectorised epilogue only from n outputs
+
 template <int WM, int WN, int TM, int TN, int BK>
 static int launch_cfg(const GemmArgs& g, int batch, int splits, float* ws, long ws_floats, unsigned* counters,
                       long n_counters, hipStream_t st) {
@@ -1289,6 +1301,7 @@ static int launch_cfg(const GemmArgs& g, int batch, int splits, float* ws, long 
     return ((reinterpret_cast<uintptr_t>(p) & 15) == 0) && (f32 ? (ld % 4 == 0) : (ld % 8 == 0));
   };
   const int va = vec_ok(g.A, g.lda, g.a_f32), vb = vec_ok(g.B, g.ldb, g.b_f32);
+  const int vec = g_epi_vec && (long)g.M * g.N * batch >= g_epi_vec_min && epi_vec_ok(g, batch);
   // Exact path: bf16 operands, every tile interior, K a whole number of
   // K-tiles split into slices of exactly `pre` (power of two <= register
   // depth) -- straight-line kernels with one global round trip per slice.
@@ -1309,7 +1322,7 @@ static int launch_cfg(const GemmArgs& g, int batch, int splits, float* ws, long 
   case P:                                                                                                        \
     hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, false, false, (P <= depth ? P : depth), true>), egrid,   \
                        dim3(256), 0, st, g,                                                                      \
-                       tiles_n, va, vb, sp, ekchunk, ws, counters);                                              \
+                       tiles_n, va, vb, sp, ekchunk, ws, counters, vec);                                         \
     return HIP_LAUNCH_CHECK();
       switch (pre) {
         JDT_GEMM_EXACT(2)
@@ -1343,10 +1356,10 @@ static int launch_cfg(const GemmArgs& g, int batch, int splits, float* ws, long 
   do {                                                                                                           \
     if (pre)                                                                                                     \
       hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, AF, BF, kPreMax>), grid, dim3(256), 0, st, g, tiles_n, \
-                         va, vb, splits, kchunk, ws, counters);                                                  \
+                         va, vb, splits, kchunk, ws, counters, vec);                                             \
     else                                                                                                         \
       hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, BK, AF, BF, 0>), grid, dim3(256), 0, st, g, tiles_n, va,   \
-                         vb, splits, kchunk, ws, counters);                                                      \
+                         vb, splits, kchunk, ws, counters, vec);                                                 \
   } while (0)
   if (g.a_f32 && g.b_f32) JDT_GEMM_LAUNCH(true, true);
   else if (g.a_f32)       JDT_GEMM_LAUNCH(true, false);
@@ -1357,8 +1370,6 @@ static int launch_cfg(const GemmArgs& g, int batch, int splits, float* ws, long 
 }
 
 
-static bool g_epi_vec = true;  // jdt_gemm_set_epi_vec(0): per-element epilogue (A/B tests)
-static long g_epi_vec_min = 0;  // jdt_gemm_set_epi_vec_min(n): vectorised epilogue only from n outputs
 static bool g_gemm_no_dma = false;  // jdt_gemm_set_dma(0): register-staged kernels only (A/B tests)
 static int g_group_split = 1;  // jdt_gemm_set_group_split(0): no split-K inside grouped launches (A/B tests)
 

@@ -98,6 +98,9 @@ struct MdArgs {
   // deterministic mode: md_fwd HEAD stores per-column-block partial logits to
   // det_logits[N/16][M][C]; md_bwd TOP sums them in block order (no fp32 atomics)
   float* det_logits;
+  // dropout counter high word = step * step_mul (0 or 1: the step): the DP minibatch
+  // loop's streams are (step * n_minibatches + i) << 32, i in the offset (dp.py)
+  int step_mul;
 };
 
 // Slots 0-4: s_memrealtime at the kernel's phase ends (tools/stamp_deep.py).
@@ -155,7 +158,8 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
   if constexpr (XCD) xcd_contiguous_tile(bx, by);
   const int r0 = bx * RB, j0 = by * 16;
   const int step = a.step[0], par = step & 1;
-  const unsigned long long doff = a.offset + ((unsigned long long)(unsigned)step << 32);
+  const unsigned long long doff =
+      a.offset + ((unsigned long long)(unsigned)(a.step_mul > 1 ? step * a.step_mul : step) << 32);
   const bf16_t* Ws = par ? a.Ws1 : a.Ws0;
   const int ks0 = (w * KS) / NW, ks1 = ((w + 1) * KS) / NW;
   constexpr bool direct = DIRECT;
@@ -697,8 +701,11 @@ JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) 
     const dim3 grid((a.M + 15) / 16, a.N / 16);
     const bool d = a.WT != nullptr;
     const bool xf = xcd_tiles_enabled() == 1;
-    if (a.K == 784) {
-      if (head) return -3;
+    if (a.K == 784 && head) {
+      // a one-hidden-layer MLP (the 2-layer tutorial classifier) per microbatch
+      if (d) { if (xf) hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, true, 10, 16, true, true>), grid, blk, 0, st, a); else hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, true, 10, 16, true, false>), grid, blk, 0, st, a); }
+      else { if (xf) hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, true, 10, 16, false, true>), grid, blk, 0, st, a); else hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, true, 10, 16, false, false>), grid, blk, 0, st, a); }
+    } else if (a.K == 784) {
       if (d) { if (xf) hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, false, 10, 16, true, true>), grid, blk, 0, st, a); else hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, false, 10, 16, true, false>), grid, blk, 0, st, a); }
       else { if (xf) hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, false, 10, 16, false, true>), grid, blk, 0, st, a); else hipLaunchKernelGGL((md_fwd_kernel<784, true, 112, false, 10, 16, false, false>), grid, blk, 0, st, a); }
     } else if (head) {
@@ -724,10 +731,14 @@ JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) 
   } else {
     const bool x = xcd_tiles_enabled() != 0;
     if (a.K == 784) {
-      if (head) return -3;
       const dim3 g(a.N / 16, 784 / 112);
-      if (x) hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, true>), g, blk, 0, st, a);
-      else hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, false>), g, blk, 0, st, a);
+      if (head) {  // TOP layer with a 784-wide input: the 2-layer classifier
+        if (x) hipLaunchKernelGGL((md_bwd_kernel<784, true, 10, 112, 512, true>), g, blk, 0, st, a);
+        else hipLaunchKernelGGL((md_bwd_kernel<784, true, 10, 112, 512, false>), g, blk, 0, st, a);
+      } else {
+        if (x) hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, true>), g, blk, 0, st, a);
+        else hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, false>), g, blk, 0, st, a);
+      }
     } else if (head) {
       const dim3 g(a.N / 16, 512 / 64);
       if (x) hipLaunchKernelGGL((md_bwd_kernel<512, true, 10, 64, 512, true>), g, blk, 0, st, a);

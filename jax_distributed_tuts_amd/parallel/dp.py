@@ -23,7 +23,7 @@ dropout streams are indexed differently) -- 4x fewer launches.
 from __future__ import annotations
 
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Optional
 
 import torch
@@ -72,6 +72,10 @@ class DPConfig:
     overlap: bool = True         # eager generic path: bucketed all-reduce overlapping the last backward
     bucket_mb: float = 25.0
     comm: str = "auto"           # "auto" | "xgmi" | "rccl": N>1 gradient collective (comm/xgmi.py)
+    # accum "loop" on the fused per-layer kernels (parallel/fused_stage.py): the same
+    # per-minibatch passes and dropout streams as the generic loop, 2 launches per
+    # minibatch (env JDT_FUSED_LOOP=0: generic GEMM chain)
+    fused_loop: bool = field(default_factory=lambda: os.environ.get("JDT_FUSED_LOOP", "1") == "1")
 
 
 class DataParallelTrainer:
@@ -91,6 +95,8 @@ class DataParallelTrainer:
         self._capturing = False
         self.buckets = None
         self._scan = None
+        self._loop_engine = None
+        self._loop_tried = False
         self.xg = None
         self._xg_fused_opt = False
         if self.world > 1 and P.grad.is_cuda:
@@ -116,6 +122,8 @@ class DataParallelTrainer:
         self.multi = None
         self._scan = None
         self._capturing = False
+        self._loop_engine = None
+        self._loop_tried = False
 
     def _fused_engine(self, batch: Batch):
         if self.cfg.accum != "kernel":
@@ -163,6 +171,14 @@ class DataParallelTrainer:
         bk = self.buckets if (self.buckets is not None and not self._capturing) else None
         if bk is not None:
             bk.begin()
+        loop_eng = self._fused_loop(mb, seed) if (cfg.accum == "loop" and bk is None) else None
+        if loop_eng is not None:
+            # the reference's minibatch loop (util.py:41-78) on the fused per-layer
+            # kernels: fwd + CE/bwd per minibatch, grads accumulated into P.grad
+            for i in range(n_mb):
+                loop_eng.forward(i, batch.inputs[i * mb:(i + 1) * mb])
+                loop_eng.backward(i, labels=batch.labels[i * mb:(i + 1) * mb])
+            return
         if cfg.accum == "fused":
             loss_and_grad(self.model, P, batch.inputs, batch.labels, train=True, seed=seed, offset=0,
                           step=st.step_tensor, grad_scale=1.0 / mb, metrics=P.metrics_slot,
@@ -174,6 +190,23 @@ class DataParallelTrainer:
                 last = i == n_mb - 1  # grads are final only in the last minibatch's backward
                 self._minibatch(batch.inputs[i * mb:(i + 1) * mb], batch.labels[i * mb:(i + 1) * mb], i, seed, mb,
                                 on_ready=bk.ready if (bk is not None and last) else None)
+
+    def _fused_loop(self, mb: int, seed: int):
+        """FusedMLPStage over this rank's minibatches (one stage = the whole model):
+        minibatch i, layer l draws dropout stream (i << 32) + (l << 1) at counter high
+        word step * n_mb -- exactly the generic loop's (_minibatch) masks."""
+        if not self._loop_tried:
+            self._loop_tried = True
+            from .fused_stage import FusedMLPStage, stage_supported
+
+            dev = self.state.params.master.device
+            if self.cfg.fused_loop and stage_supported(self.model, mb, dev):
+                # the real step counter (the kernels' parity buffers follow it), scaled by
+                # n_mb for the dropout counter
+                self._loop_engine = FusedMLPStage(self.model, self.state.params, self.cfg.num_minibatches, mb,
+                                                  self.state.step_tensor, seed, mb_shift=32,
+                                                  step_mul=self.cfg.num_minibatches)
+        return self._loop_engine
 
     # ------------------------------------------------------------------ accumulation
     # Minibatch i's dropout stream is (seed, counter-hi = (step * n_mb + i) << 32): the

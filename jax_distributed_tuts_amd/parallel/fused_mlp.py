@@ -270,7 +270,7 @@ class MdArgs(ctypes.Structure):
                 ("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float), ("wd", c_float),
                 ("gscale", c_float), ("running", c_void_p), ("stamps", c_void_p),
                 ("accumulate", c_int), ("dH", c_void_p), ("mb_rows", c_int), ("mb_stride", c_ulonglong),
-                ("stage_stride", ctypes.c_long), ("det_logits", c_void_p)]
+                ("stage_stride", ctypes.c_long), ("det_logits", c_void_p), ("step_mul", c_int)]
 
 
 _lib.declare("jdt_md_layer", c_int, [ctypes.POINTER(MdArgs), c_int, c_int, c_void_p])

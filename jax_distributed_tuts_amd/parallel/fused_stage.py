@@ -51,9 +51,9 @@ def stage_supported(model, rows: int, device) -> bool:
     if not hidden_out or any(d != H for d in hidden_out):
         return False
     if not model.final_act:
-        # last stage: the head (H -> 10) is fused into the last hidden layer's kernels,
-        # whose CE backward variant exists for 512-wide inputs only
-        if model.dims[-1] != C_HEAD or model.L < 2 or (model.L == 2 and model.dims[0] != H):
+        # last stage: the head (H -> 10) is fused into the last hidden layer's kernels
+        # (784- or 512-wide input)
+        if model.dims[-1] != C_HEAD or model.L < 2:
             return False
     return True
 
@@ -64,10 +64,15 @@ class FusedMLPStage:
     ``params``: the stage's FlatParams; ``n_mb`` microbatches of ``mb`` rows;
     ``step``: the device step counter (dropout offset; advanced by the optimizer)."""
 
-    def __init__(self, model, params, n_mb: int, mb: int, step: torch.Tensor, seed: int):
+    def __init__(self, model, params, n_mb: int, mb: int, step: torch.Tensor, seed: int,
+                 mb_shift: int = 16, step_mul: int = 1):
+        """``mb_shift`` / ``step_mul``: microbatch i, layer l draws dropout stream
+        offset (i << mb_shift) + (l << 1) at counter high word step * step_mul -- the
+        GPipe convention (16, 1) or the DP minibatch loop's (32, n_minibatches)."""
         self.model, self.P = model, params
         self.n_mb, self.mb = n_mb, mb
         self.step, self.seed = step, seed & 0xFFFFFFFF
+        self.mb_shift, self.step_mul = mb_shift, step_mul
         self.last = not model.final_act
         self.nh = model.L - 1 if self.last else model.L          # hidden layers run by md kernels
         self.k0 = model.dims[0]
@@ -119,7 +124,8 @@ class FusedMLPStage:
             a.gWh, a.gbh = P.g(hk).data_ptr(), P.g(hb).data_ptr()
         a.keep = 1.0 - m.dropout_rate
         a.seed = self.seed
-        a.offset = (i << 16) + ((m.layer_id_base + l) << 1)
+        a.offset = (i << self.mb_shift) + ((m.layer_id_base + l) << 1)
+        a.step_mul = self.step_mul
         a.step = self.step.data_ptr()
         a.advance_step = 0
         a.fuse_opt = 0

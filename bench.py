@@ -268,6 +268,8 @@ def main():
     sps = args.steps / dt
     if args.strategy == "dp":
         desc["accum"] = tr.cfg.accum  # the path that actually ran (CPU falls back from "kernel")
+    if args.strategy == "pp":
+        desc["single_stage_mode"] = tr.single_stage_mode  # how a 1-stage pipeline ran its microbatches
     if D.rank() == 0:
         out = {"metric": METRIC, "value": round(sps, 2), "unit": "steps/s", "n_gpus": ws, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 5), "higher_is_better": True,

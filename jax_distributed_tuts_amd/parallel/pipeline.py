@@ -90,10 +90,21 @@ class PipeConfig:
     # GPU, MLP stages of the tutorial shapes: one fused md_fwd / md_bwd launch per
     # layer and microbatch (parallel/fused_stage.py) instead of the generic chain
     fused_stage: bool = True
-    # pipe axis of size 1 + fused_stage: run the microbatches layer-major in one launch
-    # per layer (per-microbatch dropout streams kept; _single_stage_engine).  False:
-    # the per-microbatch stage kernels, as on a real multi-stage pipeline.
+    # pipe axis of size 1: run the microbatches layer-major, one pass per layer over all
+    # local rows, whenever that draws exactly the microbatch loop's dropout masks --
+    # the fused MLP kernels keep per-microbatch streams (_single_stage_engine); a model
+    # without dropout (the transformer LM) has no masks to keep, so its merged pass IS
+    # the loop's gradient (each row keeps its microbatch's 1/mb loss weight).  False:
+    # per-microbatch passes, as on a real multi-stage pipeline.
     layer_major_single_stage: bool = True
+
+
+def _no_dropout(model) -> bool:
+    """The stage model draws no dropout masks (merging microbatches changes nothing)."""
+    rate = getattr(model, "dropout_rate", None)
+    if rate is None:
+        rate = getattr(getattr(model, "cfg", None), "dropout_rate", 1.0)
+    return float(rate) == 0.0
 
 
 class GPipeTrainer:
@@ -206,7 +217,7 @@ class GPipeTrainer:
             if deep is not None:
                 deep.forward_backward(batch)
                 return
-        if self.S == 1 and cfg.merge_single_stage:
+        if self.S == 1 and (cfg.merge_single_stage or (cfg.layer_major_single_stage and _no_dropout(self.model))):
             out, cache = self.model.forward(P, batch.inputs, train=True, seed=seed, offset=0, step=st.step_tensor)
             d = torch.empty_like(out)
             self.loss_head(out, batch.labels, d, n_parts=n_mb)
@@ -246,6 +257,19 @@ class GPipeTrainer:
             if not self.first:
                 self._send(dx, self.s - 1, n_mb + i)
             caches[i] = None
+
+    @property
+    def single_stage_mode(self) -> str:
+        """How a pipe axis of size 1 runs its microbatches (bench JSON): "merged"
+        (one pass, merged dropout stream), "layer-major" (one pass per layer, the
+        loop's masks), "microbatch-loop", or "pipeline" (S > 1)."""
+        if self.S > 1:
+            return "pipeline"
+        if self.cfg.merge_single_stage:
+            return "merged"
+        if self.cfg.layer_major_single_stage and (self.deep_engine is not None or _no_dropout(self.model)):
+            return "layer-major"
+        return "microbatch-loop"
 
     def invalidate(self):
         """After a checkpoint restore: drop captured graphs and the stage engine."""

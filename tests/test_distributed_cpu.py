@@ -207,10 +207,11 @@ def test_bucketed_overlap_equals_single_allreduce(tmp_path):
         torch.testing.assert_close(x["metrics"], y["metrics"], rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("merge", [False, True])
-def test_single_stage_pipeline_merge_equals_reference(merge):
-    """A one-stage GPipe step, microbatch loop or merged into one pass
-    (PipeConfig.merge_single_stage), == single-device accumulation (dropout off)."""
+@pytest.mark.parametrize("mode", ["loop", "merged", "layer-major"])
+def test_single_stage_pipeline_merge_equals_reference(mode):
+    """A one-stage GPipe step -- microbatch loop, merged into one pass
+    (PipeConfig.merge_single_stage), or layer-major (the default for a model without
+    dropout) -- == single-device accumulation (dropout off)."""
     from data_paral import synthetic_batch
     from pipeline_parallel import pp_mlp_dims
     from jax_distributed_tuts_amd.models.mlp import MLP
@@ -224,7 +225,9 @@ def test_single_stage_pipeline_merge_equals_reference(merge):
     stage = mlp_stage(dims, 1, 0, dropout_rate=0.0)
     P = init_stage_params(stage, MLP(dims, dropout_rate=0.0).param_specs(), cfg.seed, "cpu")
     st = TrainState.create(apply_fn=stage, params=P, tx=adamw(1e-3), rng=R.PRNGKey(cfg.seed))
-    tr = GPipeTrainer(st, None, PipeConfig(4, merge_single_stage=merge))
+    tr = GPipeTrainer(st, None, PipeConfig(4, merge_single_stage=mode == "merged",
+                                           layer_major_single_stage=mode != "loop"))
+    assert tr.single_stage_mode == ("microbatch-loop" if mode == "loop" else mode)
     b = synthetic_batch(cfg, 70)
     for _ in range(3):
         tr.step(b)

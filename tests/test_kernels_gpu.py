@@ -724,6 +724,8 @@ def test_single_stage_pipeline_merge_gpu(model):
         else:
             tr, lcfg = build_lm_pipeline(mesh, DEV, num_microbatches=4, merge_single_stage=merge)
             b = lm_batch(lcfg, global_batch=8, seed=1)
+        if not merge:
+            tr.cfg.layer_major_single_stage = False  # the real per-microbatch passes
         b = Batch(b.inputs.to(DEV), b.labels.to(DEV))
         for _ in range(3):
             tr.step(b)

@@ -283,7 +283,25 @@ struct XgSeg {
   long s;      // part length (words, multiple of 4)
   long off;    // packed offset (words, multiple of 4)
   long nfull;  // valid words of full
+  // reduce-scatter only: an ALL-REDUCE segment riding in the same launch -- every
+  // rank contributes its whole full[0, s) as each peer's part, so part[0, s) receives
+  // the sum over ranks (FSDP: the replicated leaves' grads + metric slots, which
+  // otherwise cost a collective launch of their own); never accumulated
+  long bcast;
+  // 2-D (dim-1) shards: rows > 1 -> part is [rows][s / rows] contiguous and rank q's
+  // part of full is the column block full[r * ld + q * qoff + c] (a square weight is
+  // sharded along its LAST dim by the reference rule, param_sharding.py:82-118);
+  // rows <= 1: the 1-D layout above (rank q's part = full[q * s, (q + 1) * s))
+  long rows, ld, qoff;
 };
+
+// word index in `full` of word jj of rank q's part
+__device__ __forceinline__ long seg_full_index(const XgSeg& g, int q, long jj) {
+  if (g.rows <= 1) return (g.bcast ? 0 : (long)q * g.s) + jj;
+  const long w = g.s / g.rows;
+  const long r = jj / w;
+  return r * g.ld + (long)q * g.qoff + (jj - r * w);
+}
 
 struct XgSegs {
   XgSeg seg[XG_MAX_SEGS];
@@ -321,7 +339,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_seg_kernel(XgPeers P, int rank,
         float4 x = z4;
         if (j < S.S) {
           const XgSeg& g = S.seg[xg_find(S, j)];
-          x = load_guard(g.full, q * g.s + (j - g.off), g.nfull);
+          x = load_guard(g.full, seg_full_index(g, q, j - g.off), g.nfull);
         }
         sys_store4(my_data, half + q * slice + j, x);
       }
@@ -340,8 +358,8 @@ __global__ void __launch_bounds__(XG_THREADS) xg_seg_kernel(XgPeers P, int rank,
 #pragma unroll
       for (int q = 1; q < W; ++q) acc = add4(acc, v[q]);
       const XgSeg& g = S.seg[xg_find(S, j)];
-      const long lim = (g.nfull - rank * g.s < g.s) ? g.nfull - rank * g.s : g.s;
-      if (accumulate) acc = add4(acc, load_guard(g.part, j - g.off, lim));
+      const long lim = g.bcast ? g.nfull : ((g.nfull - rank * g.s < g.s) ? g.nfull - rank * g.s : g.s);
+      if (accumulate && !g.bcast) acc = add4(acc, load_guard(g.part, j - g.off, lim));
       store_guard(g.part, j - g.off, lim, acc);
     }
   } else {
@@ -368,7 +386,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_seg_kernel(XgPeers P, int rank,
       for (int q = 0; q < W; ++q) r[q] = sys_load4(rtmp[q], half + q * slice + j);
       const XgSeg& g = S.seg[xg_find(S, j)];
 #pragma unroll
-      for (int q = 0; q < W; ++q) store_guard(g.full, q * g.s + (j - g.off), g.nfull, r[q]);
+      for (int q = 0; q < W; ++q) store_guard(g.full, seg_full_index(g, q, j - g.off), g.nfull, r[q]);
     }
   }
   if (threadIdx.x == 0) me->epoch[b] = epoch;
@@ -595,6 +613,13 @@ JDT_API int jdt_xgmi_segments(void* ctx, const XgSegs* segs, int op, int accumul
   for (int k = 0; k < segs->n; ++k) {
     const XgSeg& g = segs->seg[k];
     if ((g.s & 3) || g.off != off || g.nfull > g.s * c->world) return -2;
+    if (g.bcast && (op != XG_REDUCE_SCATTER || g.nfull > g.s || g.rows > 1)) return -2;
+    if (g.rows > 1) {
+      const long w = g.s / g.rows;
+      if (g.s % g.rows || (w & 3) || (g.ld & 3) || (g.qoff & 3) || g.qoff < w ||
+          (long)(c->world - 1) * g.qoff + w > g.ld || g.rows * g.ld > g.nfull)
+        return -2;
+    }
     if ((reinterpret_cast<uintptr_t>(g.full) | reinterpret_cast<uintptr_t>(g.part)) & 15) return -2;
     off += g.s;
   }

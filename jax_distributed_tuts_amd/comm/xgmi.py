@@ -58,7 +58,8 @@ class XgAdam(ctypes.Structure):
 
 
 class XgSeg(ctypes.Structure):
-    _fields_ = [("full", c_void_p), ("part", c_void_p), ("s", c_long), ("off", c_long), ("nfull", c_long)]
+    _fields_ = [("full", c_void_p), ("part", c_void_p), ("s", c_long), ("off", c_long), ("nfull", c_long),
+                ("bcast", c_long), ("rows", c_long), ("ld", c_long), ("qoff", c_long)]
 
 
 MAX_SEGS = 16
@@ -258,25 +259,49 @@ class XgmiComm:
     # ------------------------------------------------------------------ segmented (multi-tensor) RS / AG
     @staticmethod
     def segment_ok(full: torch.Tensor, part: torch.Tensor, world: int) -> bool:
-        """Whether (full, part) is a dim-0 shard pair the segmented kernel can move:
-        contiguous, 16-byte aligned, part a multiple of 16 bytes, full = world parts."""
+        """Whether (full, part) is a shard pair the segmented kernel can move: contiguous,
+        16-byte aligned, full = world parts -- along dim 0 (part a multiple of 16 bytes)
+        or, 2-D, along dim 1 (each part row a multiple of 16 bytes)."""
         es = part.element_size()
-        return (full.is_cuda and part.is_cuda and full.dtype == part.dtype and full.is_contiguous()
+        base = (full.is_cuda and part.is_cuda and full.dtype == part.dtype and full.is_contiguous()
                 and part.is_contiguous() and full.data_ptr() % 16 == 0 and part.data_ptr() % 16 == 0
-                and (part.numel() * es) % 16 == 0 and full.numel() == world * part.numel())
+                and full.numel() == world * part.numel())
+        if not base:
+            return False
+        if XgmiComm._dim1(full, part, world):
+            return (part.shape[1] * es) % 16 == 0
+        return (part.numel() * es) % 16 == 0
 
-    def _segs(self, pairs) -> XgSegs:
-        if not 0 < len(pairs) <= MAX_SEGS:
+    @staticmethod
+    def _dim1(full: torch.Tensor, part: torch.Tensor, world: int) -> bool:
+        """A 2-D pair sharded along dim 1 (rank q's part = full[:, q*w:(q+1)*w])."""
+        return (full.dim() == 2 and part.dim() == 2 and full.shape[0] == part.shape[0] > 1
+                and full.shape[1] == world * part.shape[1])
+
+    def _segs(self, pairs, allreduce=()) -> XgSegs:
+        if not 0 < len(pairs) + len(allreduce) <= MAX_SEGS:
             raise ValueError(f"1..{MAX_SEGS} segments per launch")
         S = XgSegs()
         off = 0
         for k, (full, part) in enumerate(pairs):
             if not self.segment_ok(full, part, self.world):
                 raise ValueError("segment is not a contiguous, 16-byte aligned dim-0 shard pair")
-            w = part.numel() * part.element_size() // 4
-            S.seg[k] = XgSeg(full.data_ptr(), part.data_ptr(), w, off, full.numel() * full.element_size() // 4)
+            es = part.element_size()
+            w = part.numel() * es // 4
+            nfull = full.numel() * es // 4
+            if self._dim1(full, part, self.world):
+                rows, pw = part.shape[0], part.shape[1] * es // 4
+                S.seg[k] = XgSeg(full.data_ptr(), part.data_ptr(), w, off, nfull, 0, rows, full.shape[1] * es // 4, pw)
+            else:
+                S.seg[k] = XgSeg(full.data_ptr(), part.data_ptr(), w, off, nfull, 0, 0, 0, 0)
             off += w
-        S.n, S.S = len(pairs), off
+        for k, t in enumerate(allreduce, start=len(pairs)):
+            if (t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous() or t.data_ptr() % 16
+                    or t.numel() % 4):
+                raise ValueError("all-reduce segments are contiguous, 16-byte aligned fp32, length % 4 == 0")
+            S.seg[k] = XgSeg(t.data_ptr(), t.data_ptr(), t.numel(), off, t.numel(), 1, 0, 0, 0)
+            off += t.numel()
+        S.n, S.S = len(pairs) + len(allreduce), off
         return S
 
     def all_gather_segments(self, pairs):
@@ -288,13 +313,19 @@ class XgmiComm:
                                               c_void_p(_lib.stream_ptr()))
             _lib.check(rc, "jdt_xgmi_segments(all_gather)")
 
-    def reduce_scatter_segments(self, pairs, accumulate: bool = False):
-        """For each fp32 (full, part): part (+)= sum over ranks of full[rank*len(part) : ...]."""
+    def reduce_scatter_segments(self, pairs, accumulate: bool = False, allreduce=()):
+        """For each fp32 (full, part): part (+)= sum over ranks of full[rank*len(part) : ...].
+        ``allreduce``: fp32 tensors all-reduced in place (sum, never accumulated) in the
+        same launch -- one collective instead of two."""
         for full, part in pairs:
             if full.dtype != torch.float32:
                 raise ValueError("reduce-scatter sums fp32 tensors")
-        for i in range(0, len(pairs), MAX_SEGS):
-            S = self._segs(pairs[i:i + MAX_SEGS])
+        allreduce = list(allreduce)
+        if len(pairs) + len(allreduce) > MAX_SEGS:
+            if allreduce:
+                raise ValueError(f"at most {MAX_SEGS} segments with all-reduce segments")
+        for i in range(0, max(len(pairs), 1), MAX_SEGS):
+            S = self._segs(pairs[i:i + MAX_SEGS], allreduce if i == 0 else ())
             rc = _lib.lib().jdt_xgmi_segments(self.ctx, ctypes.byref(S), 1, int(accumulate), self.timeout,
                                               c_void_p(_lib.stream_ptr()))
             _lib.check(rc, "jdt_xgmi_segments(reduce_scatter)")
@@ -398,7 +429,7 @@ class XgmiComm:
                 torch.cuda.synchronize(dev)
                 if not self._check(self.error() or not torch.equal(full, exp), f"all-gather mismatch (n {n})"):
                     return False
-        if not self._self_test_segments():
+        if not self._self_test_segments() or not self._self_test_dim1():
             return False
         return self._self_test_adamw()
 
@@ -423,14 +454,53 @@ class XgmiComm:
                     return False
             src = [(torch.arange(W * s, device=dev, dtype=torch.float32) % 53) * (r + 1) for s in parts]
             outs = [torch.full((s,), float(rep), device=dev) for s in parts]
+            # + an all-reduce segment in the same launch (FSDP's replicated tail)
+            tail = (torch.arange(128, device=dev, dtype=torch.float32) % 7) * (r + 1) + rep
             self._skew(rep + 1)
-            self.reduce_scatter_segments(list(zip(src, outs)), accumulate=True)
+            self.reduce_scatter_segments(list(zip(src, outs)), accumulate=True, allreduce=[tail])
             torch.cuda.synchronize(dev)
+            want_tail = (torch.arange(128, device=dev, dtype=torch.float32) % 7) * (W * (W + 1) // 2) + W * rep
+            if not self._check(self.error() or not torch.equal(tail, want_tail),
+                               "all-reduce segment of the segmented reduce-scatter mismatch"):
+                return False
             for k, s in enumerate(parts):
                 full = (torch.arange(W * s, device=dev, dtype=torch.float32) % 53) * (W * (W + 1) // 2)
                 if not self._check(self.error() or not torch.equal(outs[k], full[r * s:(r + 1) * s] + rep),
                                    "segmented reduce-scatter mismatch"):
                     return False
+        return True
+
+    def _self_test_dim1(self) -> bool:
+        """Segmented AG / RS of a dim-1 (column-block) shard pair: the 512 x 512 hidden
+        weights of the 4-layer FSDP MLP (bf16 shadow and fp32 grads), next to a dim-0
+        pair in the same launch."""
+        W, r, dev = self.world, self.rank, self.device
+        R, C = 64, 64 * W
+        if (R * C + 4 * 512) * 2 > self.capacity // 2:
+            return True
+        col = torch.arange(C, device=dev)
+        for rep in range(2):
+            full = torch.empty(R, C, device=dev, dtype=torch.bfloat16)
+            mine = ((torch.arange(R, device=dev)[:, None] * 3 + col[None, :64] + 7 * r + rep) % 61).to(torch.bfloat16)
+            f0, m0 = torch.empty(512 * W, device=dev), torch.full((512,), float(r + rep), device=dev)
+            self._skew(rep)
+            self.all_gather_segments([(full, mine), (f0, m0)])
+            torch.cuda.synchronize(dev)
+            q = col // 64
+            exp = ((torch.arange(R, device=dev)[:, None] * 3 + (col % 64)[None, :] + 7 * q[None, :] + rep) % 61)
+            if not self._check(self.error() or not torch.equal(full, exp.to(torch.bfloat16))
+                               or not torch.equal(f0, torch.arange(W, device=dev).repeat_interleave(512).float() + rep),
+                               "dim-1 segmented all-gather mismatch"):
+                return False
+            src = ((torch.arange(R, device=dev)[:, None] + col[None, :]) % 29).float() * (r + 1)
+            out = torch.empty(R, 64, device=dev)
+            self._skew(rep + 1)
+            self.reduce_scatter_segments([(src, out)])
+            torch.cuda.synchronize(dev)
+            want = ((torch.arange(R, device=dev)[:, None] + col[None, r * 64:(r + 1) * 64]) % 29).float()
+            want = want * (W * (W + 1) // 2)
+            if not self._check(self.error() or not torch.equal(out, want), "dim-1 segmented reduce-scatter mismatch"):
+                return False
         return True
 
     def _self_test_adamw(self) -> bool:

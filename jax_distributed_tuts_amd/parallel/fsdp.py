@@ -272,7 +272,11 @@ class ShardedFlatParams:
         from ..comm.xgmi import XgmiComm
 
         self.xg = comm
-        self._xg_names = [n for n in self.sharded_names if self.part[n].shard_dim == 0
+        # dim 0, or dim 1 of a 2-D leaf (the reference rule shards a square weight along
+        # its last dim): both are layouts of the segmented kernel
+        self._xg_names = [n for n in self.sharded_names
+                          if (self.part[n].shard_dim == 0 or (self.part[n].shard_dim == 1
+                                                                and self.full.s(n).dim() == 2))
                           and XgmiComm.segment_ok(self.full.s(n), self.local.s(n), self.n)
                           and XgmiComm.segment_ok(self.full.g(n), self.local.g(n), self.n)]
 
@@ -314,11 +318,24 @@ class ShardedFlatParams:
             for name in self.repl_names:
                 self.full.s(name).copy_(self.local.s(name))
 
-    def scatter_grads(self, accumulate: bool, zero_full: bool = True):
+    def scatter_grads(self, accumulate: bool, zero_full: bool = True, with_replicated: bool = False) -> bool:
         """full fp32 grads -> reduce-scatter SUM into local grads (X06); replicated
-        grads copied into the local tail.  Full grads are zeroed."""
+        grads copied into the local tail.  Full grads are zeroed.
+
+        ``with_replicated`` (the step's last scatter): on the xGMI path the local tail
+        (replicated leaves' grads + metric slots, i.e. sync_replicated's all-reduce)
+        rides in the same launch as an all-reduce segment -- one collective per step
+        fewer.  Returns True if it did (then skip sync_replicated)."""
+        fold = (with_replicated and not accumulate and self.xg is not None and bool(self._xg_names)
+                and len(self._xg_names) < 16 and (self.local.grad.numel() - self.repl_start) % 4 == 0
+                and self.repl_start % 4 == 0)
         with named_scope("scatter_grads"):
-            if self.xg is not None and self._xg_names:
+            if fold:
+                for name in self.repl_names:
+                    self.local.g(name).copy_(self.full.g(name))
+                self.xg.reduce_scatter_segments([(self.full.g(n), self.local.g(n)) for n in self._xg_names],
+                                                accumulate=False, allreduce=[self.local.grad[self.repl_start:]])
+            elif self.xg is not None and self._xg_names:
                 self.xg.reduce_scatter_segments([(self.full.g(n), self.local.g(n)) for n in self._xg_names],
                                                 accumulate=accumulate)
             for name in self.sharded_names:
@@ -331,12 +348,15 @@ class ShardedFlatParams:
                 else:
                     C.psum_scatter(self.full.g(name), self.mesh, self.axis, dim=d, out=self.local.g(name))
             for name in self.repl_names:
+                if fold:
+                    continue  # copied before the launch
                 if accumulate:
                     self.local.g(name).add_(self.full.g(name))
                 else:
                     self.local.g(name).copy_(self.full.g(name))
             if zero_full:
                 self.full.grad.zero_()
+        return fold
 
     def sync_replicated(self):
         """sync_gradients for replicated leaves + synch_metrics: ONE all-reduce of the tail."""
@@ -430,8 +450,8 @@ class FSDPTrainer:
             return True
         sp.gather()
         self.fused.forward_backward(batch)
-        sp.scatter_grads(accumulate=False, zero_full=False)
-        sp.sync_replicated()
+        if not sp.scatter_grads(accumulate=False, zero_full=False, with_replicated=True):
+            sp.sync_replicated()
         self.state.tx.update(sp.local, self.state.opt_state, 1.0 / (self.cfg.num_minibatches * self.world),
                              zero_grad=False)
         with named_scope("synch_metrics"):
@@ -497,9 +517,8 @@ class FSDPTrainer:
                           metrics=sp.local.metrics_slot)
             if not cfg.scatter_once:
                 sp.scatter_grads(accumulate=True)
-        if cfg.scatter_once:
-            sp.scatter_grads(accumulate=False)
-        sp.sync_replicated()
+        if not (cfg.scatter_once and sp.scatter_grads(accumulate=False, with_replicated=True)):
+            sp.sync_replicated()
         st.tx.update(sp.local, st.opt_state, 1.0 / (n_mb * self.world))
         with named_scope("synch_metrics"):
             K.metrics_fold_(self.metrics, sp.local.metrics_slot)

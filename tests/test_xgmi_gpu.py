@@ -62,20 +62,23 @@ def test_dp_over_xgmi_matches_single_device(tmp_path):
     assert abs(float(m[2]) - float(ref[2])) <= 4
 
 
-@pytest.mark.parametrize("fused", [True, False])
-def test_fsdp_over_xgmi_matches_single_device(tmp_path, fused):
+@pytest.mark.parametrize("fused,num_layers", [(True, 2), (False, 2), (True, 4)])
+def test_fsdp_over_xgmi_matches_single_device(tmp_path, fused, num_layers):
     from data_paral import synthetic_batch
     from jax_distributed_tuts_amd.models.mlp import Classifier
     from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
     from jax_distributed_tuts_amd.utils.config import fsdp_config
     from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
 
-    spawn(XW.fsdp_xgmi, 2, str(tmp_path), fused, gpu=True)
-    res = _load(tmp_path, "fsx", 2)
+    spawn(XW.fsdp_xgmi, 2, str(tmp_path), fused, 3, num_layers, gpu=True)
+    res = _load(tmp_path, f"fsx{num_layers}", 2)
     assert all(o["comm"] == "xgmi" for o in res)
-    assert set(res[0]["xg_names"]) == {"input_dense/kernel", "input_dense/bias", "output_dense/kernel"}
+    # every sharded leaf rides the segmented kernels (dim-0 and, 4-layer, dim-1 shards)
+    assert set(res[0]["xg_names"]) == {n for n, d in res[0]["dims"].items() if d is not None}
+    if num_layers == 4:
+        assert 1 in res[0]["dims"].values()
     dev = torch.device("cuda", 0)
-    st = init_fsdp(Classifier(dropout_rate=0.0), adamw(1e-3), 69, dev, None, "data", 16)
+    st = init_fsdp(Classifier(num_layers=num_layers, dropout_rate=0.0), adamw(1e-3), 69, dev, None, "data", 16)
     b = synthetic_batch(fsdp_config(), 70)
     b = Batch(b.inputs.to(dev), b.labels.to(dev))
     tr = FSDPTrainer(st, None, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=fused))
@@ -162,6 +165,7 @@ def test_transformer_hybrid_over_xgmi_matches_single_device(tmp_path):
     dev = torch.device("cuda", 0)
     cfg = TransformerConfig(vocab_size=512, d_model=128, n_heads=2, d_ff=256, seq_len=64, n_layers=2)
     tr, _ = build_lm_pipeline(None, dev, cfg, num_microbatches=4)  # dp=2 x 2 microbatches == 4 microbatches
+    tr.cfg.layer_major_single_stage = False  # per-microbatch passes, like the hybrid's stages (same rounding)
     b = lm_batch(cfg, global_batch=8, seed=1)
     b = Batch(b.inputs.to(dev), b.labels.to(dev))
     for _ in range(3):

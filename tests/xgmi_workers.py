@@ -139,9 +139,11 @@ def dp_xgmi(outdir, steps_eager=2, steps_graph=6):
                           "fused": tr.fused is not None, "step": int(st.opt_state["count"].item())})
 
 
-def fsdp_xgmi(outdir, fused=True, steps=3):
+def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2):
     """FSDP (dropout off) with the segmented xGMI gather / reduce-scatter; every rank
-    saves its local shard + the partition table for reassembly in the parent."""
+    saves its local shard + the partition table for reassembly in the parent.
+    num_layers=4: the square 512 x 512 hidden weights are sharded along dim 1 (the
+    reference rule) and move as 2-D column-block segments."""
     from data_paral import synthetic_batch
     from jax_distributed_tuts_amd.models.mlp import Classifier
     from jax_distributed_tuts_amd.parallel.dp import shard_batch
@@ -153,7 +155,7 @@ def fsdp_xgmi(outdir, fused=True, steps=3):
     dev = D.device()
     cfg = fsdp_config()
     mesh = D.Mesh({"data": D.world_size()})
-    st = init_fsdp(Classifier(dropout_rate=0.0), adamw(1e-3), 69, dev, mesh, "data", 16)
+    st = init_fsdp(Classifier(num_layers=num_layers, dropout_rate=0.0), adamw(1e-3), 69, dev, mesh, "data", 16)
     b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
     b = Batch(b.inputs.to(dev), b.labels.to(dev))
     tr = FSDPTrainer(st, mesh, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=fused,
@@ -165,7 +167,7 @@ def fsdp_xgmi(outdir, fused=True, steps=3):
     torch.cuda.synchronize()
     tr.finalize()
     sp = st.extra["sharded"]
-    _save(outdir, "fsx", {"local": {n: sp.local.p(n).cpu() for n in sp.part},
+    _save(outdir, f"fsx{num_layers}", {"local": {n: sp.local.p(n).cpu() for n in sp.part},
                           "dims": {n: sp.part[n].shard_dim for n in sp.part},
                           "metrics": tr.metrics.cpu(), "comm": tr.comm_backend, "xg_names": list(sp._xg_names)})
 

@@ -37,6 +37,27 @@ from . import dist as D
 
 
 def free_port() -> int:
+    """A free rendezvous port BELOW the kernel's ephemeral range: a port handed out
+    by ``bind(0)`` is ephemeral, so between our probe and rank 0's TCPStore bind a
+    peer's outgoing (store / gloo pair) socket can be given the same number and the
+    bind fails with EADDRINUSE -- an intermittent launch failure."""
+    import random
+
+    lo = 20000
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+            lo = min(lo, int(f.read().split()[0]) - 2000)
+    except (OSError, ValueError, IndexError):
+        pass
+    rnd = random.Random(os.getpid() ^ time.time_ns())
+    for _ in range(64):
+        port = rnd.randrange(max(1024, lo - 10000), lo)
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            try:
+                s.bind(("127.0.0.1", port))
+            except OSError:
+                continue
+            return port
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
@@ -175,9 +196,20 @@ def spawn(fn: Callable, world: int, *args: Any, env: dict | None = None, gpu: bo
     ranks share cuda:0, which rehearses the multi-process GPU paths such as the
     xGMI IPC collectives; the process group stays gloo since RCCL refuses two
     ranks on one device).  For N RCCL ranks on N GPUs use :func:`local_launch`."""
-    port = free_port()
-    mp.start_processes(_child, args=(world, port, fn, args, dict(env or {}), gpu), nprocs=world, join=True,
-                       start_method="spawn")
+    for attempt in range(1 if gpu else 2):
+        port = free_port()
+        try:
+            mp.start_processes(_child, args=(world, port, fn, args, dict(env or {}), gpu), nprocs=world,
+                               join=True, start_method="spawn")
+            return
+        except mp.ProcessExitedException as e:
+            # CPU simulation only: a rank killed by a signal (not a Python error --
+            # those raise ProcessRaisedException) is gloo's rare teardown abort
+            # ("terminate called without an active exception"); run the job once more
+            if gpu or attempt or e.signal_name is None:
+                raise
+            print(f"[spawn] rank {e.error_index} died with {e.signal_name}; re-running the {world}-rank job once",
+                  file=sys.stderr, flush=True)
 
 
 def run(fn: Callable, *args: Any, sim_cpu: int | None = None, expect_world: Optional[int] = None):

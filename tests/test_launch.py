@@ -36,7 +36,7 @@ def _json_line(out: str) -> dict:
 @pytest.mark.parametrize("n", [2, 4])
 def test_bench_gpus_n_starts_n_ranks(n):
     r = _run(["bench.py", "--gpus", str(n), "--steps", "2", "--warmup", "1"])
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, r.stdout[-1500:] + r.stderr[-3000:]
     j = _json_line(r.stdout)
     assert j["n_gpus"] == n and j["steps"] == 2 and j["warmup"] == 1
     assert j["config"]["parallelism"] == f"dp{n}"
@@ -56,7 +56,7 @@ def test_bench_refuses_wrong_world_size():
 ])
 def test_entry_scripts_gpus_flag(script, extra, title):
     r = _run([script, "--gpus", "2", "--steps", "1", "--check-replication", *extra])
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, r.stdout[-1500:] + r.stderr[-3000:]
     assert title in r.stdout and "loss:" in r.stdout
     assert "[check-replication]" in r.stdout
 

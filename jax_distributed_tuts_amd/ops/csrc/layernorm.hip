@@ -86,15 +86,15 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
 // any arithmetic; dgamma, dbeta and the optional colsum(dx) are accumulated in
 // registers over the wave's rows, summed over the 4 waves in LDS, and added to
 // the outputs with one fp32 atomic per column per workgroup.
-template <int NV, int R>
-__global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+template <int NV, int R, int W>
+__global__ void __launch_bounds__(64 * W) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                      const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                      const float* __restrict__ gamma, const bf16_t* __restrict__ dres,
                                                      bf16_t* __restrict__ dx, float* __restrict__ dgamma,
                                                      float* __restrict__ dbeta, float* __restrict__ dsum, int T, int d) {
-  __shared__ float part[4][512 * NV];
+  __shared__ float part[W][512 * NV];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r0 = (blockIdx.x * 4 + w) * R;
+  const int r0 = (blockIdx.x * W + w) * R;
   float ag[NV][8], ab[NV][8], ad[NV][8], gm[NV][8];
   u32x4 px[R][NV], pd[R][NV], pr[R][NV];
   float mean[R], rstd[R];
@@ -186,7 +186,12 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 8; ++j) part[w][(c * 64 + lane) * 8 + j] = acc3[t][c][j];
     __syncthreads();
-    for (int i = threadIdx.x; i < d; i += 256) atomicAdd(outs[t] + i, part[0][i] + part[1][i] + part[2][i] + part[3][i]);
+    for (int i = threadIdx.x; i < d; i += 64 * W) {
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < W; ++k) acc += part[k][i];
+      atomicAdd(outs[t] + i, acc);
+    }
   }
 }
 
@@ -212,8 +217,9 @@ JDT_API int jdt_ln_fwd(const void* x, const float* gamma, const float* beta, voi
   return HIP_LAUNCH_CHECK();
 }
 
-static int g_ln_rows = 0;
+static int g_ln_rows = 0, g_ln_waves = 0;
 JDT_API void jdt_ln_set_rows(int r) { g_ln_rows = r; }
+JDT_API void jdt_ln_set_waves(int w) { g_ln_waves = w; }
 
 // dsum (optional): += colsum(dx), the bias gradient of the layer that produced
 // this LayerNorm's input (a residual-stream Dense), so it needs no pass of its own.
@@ -222,26 +228,37 @@ JDT_API int jdt_ln_bwd(const void* dy, const void* x, const float* mean, const f
                        void* stream) {
   if (d % 8 || d > 2048) return -3;
   const int nv = (d / 8 + 63) / 64;
-  // rows per wave: R = 2 up to 2048 rows, 4 beyond (fewer workgroups -> fewer
-  // same-address column atomics; all of a wave's row loads are in flight at once)
   hipStream_t st = static_cast<hipStream_t>(stream);
   auto a = static_cast<const bf16_t*>(dy);
   auto b = static_cast<const bf16_t*>(x);
   auto r = static_cast<const bf16_t*>(dres);
   auto o = static_cast<bf16_t*>(dx);
   if ((reinterpret_cast<uintptr_t>(gamma) & 15)) return -3;
-#define JDT_LNB(NV_, R_)                                                                                        \
-  hipLaunchKernelGGL((ln_bwd_kernel<NV_, R_>), dim3((T + 4 * R_ - 1) / (4 * R_)), dim3(256), 0, st, a, b, mean, \
-                     rstd, gamma, r, o, dgamma, dbeta, dsum, T, d)
-  // rows per wave: fewer, longer workgroups cut the same-address column atomics
-  // (3 x d per workgroup); g_ln_rows forces R (sweeps: tools/bench_ln.py)
-  int R = g_ln_rows;
-  // T = 2048: R 8 7.6 us, 4 8.1, 2 11.2; T = 512: R 2 4.8 vs 4 5.6 (tools/bench_ln.py, DPP reductions)
-  if (R == 0) R = T >= 2048 ? 8 : (T >= 1024 ? 4 : 2);
+  // A workgroup = W waves x R rows each.  The column sums cost one same-address
+  // atomic per column per workgroup (they serialise in L2), so the rows per
+  // workgroup set the atomic count; W spreads those rows over more waves (the
+  // per-row work after the loads is serial within a wave).  g_ln_rows /
+  // g_ln_waves force R / W (sweeps: tools/bench_ln.py).
+  int R = g_ln_rows, W = g_ln_waves;
+  if (W == 0) W = (nv <= 2 && T >= 1024) ? 16 : 4;
+  if (nv > 2 && W > 4) W = 4;  // LDS image part[W][512 NV]
+  if (R == 0) R = W == 16 ? 2 : (T >= 1024 ? 4 : 2);
+#define JDT_LNB(NV_, R_, W_)                                                                                      \
+  hipLaunchKernelGGL((ln_bwd_kernel<NV_, R_, W_>), dim3((T + W_ * R_ - 1) / (W_ * R_)), dim3(64 * W_), 0, st, a, b, \
+                     mean, rstd, gamma, r, o, dgamma, dbeta, dsum, T, d)
+  // register budget: R x NV x 3 row vectors per lane -> R <= 2 at 16 waves, <= 4 at 8
   switch (nv) {
-    case 1: if (R >= 8) JDT_LNB(1, 8); else if (R >= 4) JDT_LNB(1, 4); else JDT_LNB(1, 2); break;
-    case 2: if (R >= 8) JDT_LNB(2, 8); else if (R >= 4) JDT_LNB(2, 4); else JDT_LNB(2, 2); break;
-    default: if (R >= 2) JDT_LNB(4, 2); else JDT_LNB(4, 1); break;
+    case 1:
+      if (W >= 16) { if (R >= 2) JDT_LNB(1, 2, 16); else JDT_LNB(1, 1, 16); }
+      else if (W >= 8) { if (R >= 4) JDT_LNB(1, 4, 8); else if (R >= 2) JDT_LNB(1, 2, 8); else JDT_LNB(1, 1, 8); }
+      else { if (R >= 8) JDT_LNB(1, 8, 4); else if (R >= 4) JDT_LNB(1, 4, 4); else if (R >= 2) JDT_LNB(1, 2, 4); else JDT_LNB(1, 1, 4); }
+      break;
+    case 2:
+      if (W >= 16) { if (R >= 2) JDT_LNB(2, 2, 16); else JDT_LNB(2, 1, 16); }
+      else if (W >= 8) { if (R >= 4) JDT_LNB(2, 4, 8); else if (R >= 2) JDT_LNB(2, 2, 8); else JDT_LNB(2, 1, 8); }
+      else { if (R >= 8) JDT_LNB(2, 8, 4); else if (R >= 4) JDT_LNB(2, 4, 4); else if (R >= 2) JDT_LNB(2, 2, 4); else JDT_LNB(2, 1, 4); }
+      break;
+    default: if (R >= 2) JDT_LNB(4, 2, 4); else JDT_LNB(4, 1, 4); break;
   }
 #undef JDT_LNB
   return HIP_LAUNCH_CHECK();

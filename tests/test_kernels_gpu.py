@@ -325,7 +325,7 @@ def test_gemm_split_k(splits, M, N, K_, cfg, gemm_path):
     _close(acc_g, acc_r, rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("T,d", [(37, 64), (256, 512), (64, 1024), (2500, 512)])
+@pytest.mark.parametrize("T,d", [(37, 64), (256, 512), (64, 1024), (2500, 512), (1536, 1024), (1030, 2048)])
 def test_layernorm(T, d):
     x = _mk((T, d), torch.bfloat16, seed=31)
     gmm, bta = 1 + 0.1 * _mk((d,), torch.float32, seed=32), 0.1 * _mk((d,), torch.float32, seed=33)
@@ -345,6 +345,36 @@ def test_layernorm(T, d):
     _close(db_g, db_r, rtol=1e-3, atol=1e-3)
     # dsum = colsum of the kernel's own (bf16) dx output
     _close(ds_g, dx_g.float().sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("d", [512, 1024])
+def test_layernorm_bwd_every_shape_variant(d):
+    """Every (waves per workgroup, rows per wave) instantiation of ln_bwd, forced
+    through the sweep knobs on a ragged row count, == the fp32 CPU reference."""
+    from jax_distributed_tuts_amd.ops import _lib
+
+    T = 333
+    x = _mk((T, d), torch.bfloat16, seed=41)
+    gmm = 1 + 0.1 * _mk((d,), torch.float32, seed=42)
+    _, m_r, r_r = kern.layernorm_fwd(x, gmm, torch.zeros(d))
+    dy, dres = _mk((T, d), torch.bfloat16, seed=43), _mk((T, d), torch.bfloat16, seed=44)
+    dg_r, db_r = torch.zeros(d), torch.zeros(d)
+    dx_r = kern.layernorm_bwd(dy, x, m_r, r_r, gmm, dg_r, db_r, dres=dres)
+    lib = _lib.lib()
+    try:
+        for W, R in ((4, 1), (4, 2), (4, 4), (4, 8), (8, 1), (8, 2), (8, 4), (16, 1), (16, 2)):
+            lib.jdt_ln_set_waves(W)
+            lib.jdt_ln_set_rows(R)
+            dg_g, db_g, ds_g = (torch.zeros(d, device=DEV) for _ in range(3))
+            dx_g = kern.layernorm_bwd(dy.to(DEV), x.to(DEV), m_r.to(DEV), r_r.to(DEV), gmm.to(DEV), dg_g, db_g,
+                                      dres=dres.to(DEV), dsum=ds_g)
+            _close(dx_g, dx_r)
+            _close(dg_g, dg_r, rtol=1e-3, atol=1e-3)
+            _close(db_g, db_r, rtol=1e-3, atol=1e-3)
+            _close(ds_g, dx_g.float().sum(0), rtol=1e-4, atol=1e-3)
+    finally:
+        lib.jdt_ln_set_waves(0)
+        lib.jdt_ln_set_rows(0)
 
 
 @pytest.mark.parametrize("B,S,H,Dh", [(2, 16, 4, 16), (2, 128, 8, 64), (1, 96, 2, 32)])

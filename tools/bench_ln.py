@@ -1,4 +1,4 @@
-"""LayerNorm backward sweep: rows per wave R (workgroups = T / (4 R)) on the
+"""LayerNorm backward sweep: waves per workgroup W x rows per wave R (workgroups = T / (W R)) on the
 transformer's [T, d] shapes; each timing = 50 launches in one hipGraph, median of 5.
 
     python tools/bench_ln.py
@@ -41,10 +41,12 @@ def main():
         _, mean, rstd = K.layernorm_fwd(x, gamma, torch.zeros(d, device=dev))
         dg, db, ds = (torch.zeros(d, device=dev) for _ in range(3))
         row = []
-        for R in (0, 2, 4, 8):
+        for W, R in ((0, 0), (4, 2), (4, 4), (4, 8), (8, 1), (8, 2), (8, 4), (16, 1), (16, 2)):
+            _lib.lib().jdt_ln_set_waves(W)
             _lib.lib().jdt_ln_set_rows(R)
             t = timed(lambda: K.layernorm_bwd(dy, x, mean, rstd, gamma, dg, db, dres=dres, dsum=ds))
-            row.append(f"R={R or 'auto'}: {t:6.2f} us")
+            row.append(f"W{W}R{R}: {t:5.2f}" if W else f"auto: {t:5.2f}")
+        _lib.lib().jdt_ln_set_waves(0)
         _lib.lib().jdt_ln_set_rows(0)
         # floors: the same kernel without the column-sum outputs (no atomics), a
         # forward, and a bf16 add of two [T, d] tensors (3 tensor passes)

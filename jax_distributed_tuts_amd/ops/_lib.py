@@ -46,6 +46,7 @@ _SIGS = {
     "jdt_gemm_set_group_tile": (None, [c_int]),
     "jdt_ln_set_rows": (None, [c_int]),
     "jdt_ln_set_waves": (None, [c_int]),
+    "jdt_gemm_set_group_m": (None, [c_int]),
     "jdt_gemm_set_epi_vec": (None, [c_int]),
     "jdt_gemm_set_epi_vec_min": (None, [c_long]),
     "jdt_gemm_set_r": (None, [c_int]),
@@ -135,6 +136,8 @@ def lib():
             l.jdt_gemm_set_epi_vec_min(int(os.environ["JDT_GEMM_EPI_MIN"]))
         if os.environ.get("JDT_GEMM_R"):  # A/B: force the LDS-DMA GEMM's sub-tiles per ring slot
             l.jdt_gemm_set_r(int(os.environ["JDT_GEMM_R"]))
+        if os.environ.get("JDT_GEMM_GROUP_M"):  # A/B: LDS-DMA GEMM tile order in row-groups of G tiles
+            l.jdt_gemm_set_group_m(int(os.environ["JDT_GEMM_GROUP_M"]))
         if os.environ.get("JDT_LN_WAVES"):  # A/B: force LayerNorm-backward waves per workgroup (0 = auto)
             l.jdt_ln_set_waves(int(os.environ["JDT_LN_WAVES"]))
         _lib = l

@@ -445,14 +445,14 @@ __device__ __forceinline__ void gemm_finish_lds(const GemmArgs& g, f32x4 (&acc)[
 // K = 512 GEMM (tools/gemm_ksweep.py: K = 64 took 13-18 us vs torch's 6).  The
 // arithmetic per element is the same sequence as gemm_finish, so results are
 // bit-identical.
-template <int BM, int BN, int TM, int TN>
+template <int BM, int BN, int TM, int TN, int NT = 256>
 __device__ __forceinline__ void gemm_finish_vec(const GemmArgs& g, f32x4 (&acc)[TM][TN], int tm0, int tn0, int z,
                                                 int wm, int wn, int lane, int tid, int splits, int split, long tile_id,
                                                 float* __restrict__ ws, unsigned* counters, float* img) {
   constexpr int LD = BN + 4;      // padded image row (floats)
   constexpr int CU = BN / 8;      // 8-column chunks per row
   constexpr int NU = BM / 4 * CU; // 4 x 8 units per tile
-  static_assert(256 % CU == 0, "a thread keeps its column chunk across units");
+  static_assert(NT % CU == 0, "a thread keeps its column chunk across units");
   // the caller synchronised: every wave is past its last read of the staging ring
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -466,7 +466,7 @@ __device__ __forceinline__ void gemm_finish_vec(const GemmArgs& g, f32x4 (&acc)[
     constexpr int NV = BM * BN / 4;
     float* slab0 = ws + tile_id * splits * (BM * BN);
     float* slab = slab0 + (long)split * (BM * BN);
-    for (int v = tid; v < NV; v += 256) {
+    for (int v = tid; v < NV; v += NT) {
       const int r = (v * 4) / BN, c = (v * 4) % BN;
       const float4 x = *reinterpret_cast<const float4*>(&img[r * LD + c]);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sys_u32x4, x),
@@ -484,7 +484,7 @@ __device__ __forceinline__ void gemm_finish_vec(const GemmArgs& g, f32x4 (&acc)[
     }
     __syncthreads();
     if (!flag[0]) return;
-    for (int v = tid; v < NV; v += 256) {
+    for (int v = tid; v < NV; v += NT) {
       float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
       for (int sp = 0; sp < splits; ++sp) {
         const sys_u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(
@@ -521,7 +521,7 @@ __device__ __forceinline__ void gemm_finish_vec(const GemmArgs& g, f32x4 (&acc)[
 #pragma unroll
   for (int k = 0; k < 8; ++k) cs[k] = 0.f;
   const long cbase = zoff(g, z, g.sC, g.sC2);
-  for (int u = tid; u < NU; u += 256) {
+  for (int u = tid; u < NU; u += NT) {
     const int rl = (u / CU) * 4;  // first row of the unit within the tile
     const int row0 = tm0 + rl;
     u32x4 db[8];
@@ -601,12 +601,12 @@ __device__ __forceinline__ void gemm_finish_vec(const GemmArgs& g, f32x4 (&acc)[
   }
   if (g.dbias) {
     // column sums: the threads sharing a chunk (tid % CU) meet in the image
-    constexpr int RPT = 256 / CU;  // threads per chunk
+    constexpr int RPT = NT / CU;  // threads per chunk
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 8; ++k) img[(tid / CU) * (BN + 1) + cc * 8 + k] = cs[k];
     __syncthreads();
-    for (int c = tid; c < BN; c += 256) {
+    for (int c = tid; c < BN; c += NT) {
       float s = 0.f;
       for (int r = 0; r < RPT; ++r) s += img[r * (BN + 1) + c];
       atomicAdd(g.dbias + tn0 + c, s);
@@ -942,9 +942,10 @@ __device__ __forceinline__ bf16x8 dma_frag(const bf16_t* img, bool kmajor_img, i
 
 // Stage one operand tile (EXT x 64 of a K-contiguous source, or 64 x EXT of an
 // EXT-contiguous one) into its LDS image: EXT/32 wave-instructions per wave.
-template <int EXT, bool KMAJ>
+template <int EXT, bool KMAJ, int NW = 4>
 __device__ __forceinline__ void dma_stage(const bf16_t* src, long ld, int k0, bf16_t* img, int wid, int lane) {
-  constexpr int IPW = EXT / 32;  // 1 KiB per wave-instruction, EXT*64*2 bytes per tile, 4 waves
+  constexpr int IPW = EXT / (8 * NW);  // 1 KiB per wave-instruction, EXT*64*2 bytes per tile, NW waves
+  static_assert(IPW >= 1, "every wave issues at least one piece");
 #pragma unroll
   for (int i = 0; i < IPW; ++i) {
     const int ins = wid * IPW + i;
@@ -968,13 +969,14 @@ __device__ __forceinline__ void dma_stage(const bf16_t* src, long ld, int k0, bf
 // bank row, so its transposed fragment reads conflicted (PMC on 128 x 128 tiles:
 // SQ_LDS_BANK_CONFLICT 5.1M cycles per launch, 2.6x the kernel time of 64 x 64
 // tiles); 64-wide sub-images keep the conflict-free EXT = 64 swizzle.
-template <int EXT, bool KMAJ>
+template <int EXT, bool KMAJ, int NW = 4>
 __device__ __forceinline__ void stage_op(const bf16_t* src, long ld, int k0, bf16_t* img, int wid, int lane) {
   if constexpr (KMAJ && EXT > 64) {
 #pragma unroll
-    for (int h = 0; h < EXT / 64; ++h) dma_stage<64, true>(src + h * 64, ld, k0, img + h * 64 * DMA_BK, wid, lane);
+    for (int h = 0; h < EXT / 64; ++h)
+      dma_stage<64, true, NW>(src + h * 64, ld, k0, img + h * 64 * DMA_BK, wid, lane);
   } else {
-    dma_stage<EXT, KMAJ>(src, ld, k0, img, wid, lane);
+    dma_stage<EXT, KMAJ, NW>(src, ld, k0, img, wid, lane);
   }
 }
 template <int EXT>
@@ -1060,12 +1062,14 @@ __device__ __forceinline__ void dma_wait_barrier(int pend) {
 // per wave between barriers; the wait / barrier / ds_read latency chain then
 // sets the K loop's pace, ~300 cycles per 64-deep K-tile on one workgroup/CU).
 template <int WM, int WN, int TM, int TN, bool AT, bool BT, int S, int R = 1>
-__global__ void __launch_bounds__(256) gemm_dma_kernel(GemmArgs g, int tiles_n, int splits, int kchunk,
-                                                       float* __restrict__ ws, unsigned* counters, int vec) {
+__global__ void __launch_bounds__(64 * WM * WN) gemm_dma_kernel(GemmArgs g, int tiles_n, int splits, int kchunk,
+                                                                float* __restrict__ ws, unsigned* counters, int vec,
+                                                                int group_m) {
+  constexpr int NW = WM * WN;             // waves: 4, or 8 (two per SIMD) for the 128 x 128+ tiles
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16, BK = DMA_BK;
   constexpr int SUB = (BM + BN) * BK;     // elements of one 64-deep sub-tile (A image then B image)
   constexpr int STAGE = SUB * R;          // elements of one ring slot
-  constexpr int LPW = (BM / 32 + BN / 32) * R;  // glds per wave per slot
+  constexpr int LPW = (BM + BN) / (8 * NW) * R;  // glds per wave per slot
   static_assert((S - 2) * LPW <= 63, "vmcnt range");
   __shared__ __attribute__((aligned(16))) bf16_t smem[S * STAGE];
   const int nwg = gridDim.x;
@@ -1074,7 +1078,17 @@ __global__ void __launch_bounds__(256) gemm_dma_kernel(GemmArgs g, int tiles_n, 
     const int xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
     bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
   }
-  const int tm0 = (bid / tiles_n) * BM, tn0 = (bid % tiles_n) * BN, z = blockIdx.z;
+  int tmi = bid / tiles_n, tni = bid % tiles_n;
+  if (group_m > 1) {
+    // row-groups of group_m tiles, column-major inside a group: an XCD's contiguous
+    // run of tiles is then a near-square block, so the operand panels it fetches
+    // from beyond its L2 per K-tile shrink (2048 x 2048 / 128 x 128: 288 -> 192 KB)
+    const int tiles_m = nwg / tiles_n, gsz = group_m * tiles_n, grp = bid / gsz, f = grp * group_m;
+    const int gm = min(group_m, tiles_m - f), t = bid - grp * gsz;
+    tmi = f + t % gm;
+    tni = t / gm;
+  }
+  const int tm0 = tmi * BM, tn0 = tni * BN, z = blockIdx.z;
   const bf16_t* Ab = static_cast<const bf16_t*>(g.A) + zoff(g, z, g.sA, g.sA2) + (AT ? (long)tm0 : (long)tm0 * g.lda);
   const bf16_t* Bb = static_cast<const bf16_t*>(g.B) + zoff(g, z, g.sB, g.sB2) + (BT ? (long)tn0 : (long)tn0 * g.ldb);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1094,8 +1108,8 @@ __global__ void __launch_bounds__(256) gemm_dma_kernel(GemmArgs g, int tiles_n, 
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int k0 = kbeg + (kt * R + r) * BK;
-      stage_op<BM, AT>(Ab, g.lda, k0, st + r * SUB, wid, lane);
-      stage_op<BN, BT>(Bb, g.ldb, k0, st + r * SUB + BM * BK, wid, lane);
+      stage_op<BM, AT, NW>(Ab, g.lda, k0, st + r * SUB, wid, lane);
+      stage_op<BN, BT, NW>(Bb, g.ldb, k0, st + r * SUB + BM * BK, wid, lane);
     }
   };
 #pragma unroll
@@ -1136,7 +1150,11 @@ __global__ void __launch_bounds__(256) gemm_dma_kernel(GemmArgs g, int tiles_n, 
   }
   __syncthreads();
   static_assert((BM * (BN + 4) + 4) * 4 <= S * STAGE * 2, "output image fits the staging ring");
-  if (vec) {
+  if constexpr (NW != 4) {
+    // 8-wave tiles are launched only where the vectorised epilogue applies (host)
+    gemm_finish_vec<BM, BN, TM, TN, 64 * NW>(g, acc, tm0, tn0, z, wm, wn, lane, tid, splits, split,
+                                             (long)z * gridDim.x + bid, ws, counters, reinterpret_cast<float*>(smem));
+  } else if (vec) {
     gemm_finish_vec<BM, BN, TM, TN>(g, acc, tm0, tn0, z, wm, wn, lane, tid, splits, split,
                                     (long)z * gridDim.x + bid, ws, counters, reinterpret_cast<float*>(smem));
   } else if constexpr (TM * TN >= 16) {
@@ -1385,14 +1403,15 @@ constexpr int dma_stages() { return 3; }
 // workgroup per CU -- no faster in isolation, slower in-model; and software-
 // pipelined fragment reads (both 32-deep halves of a slot issued up front, counted
 // lgkmcnt) -- within noise: the K loop waits on the global->LDS ring, not on LDS.)
+static int g_group_m = -1;  // jdt_gemm_set_group_m(G): force tile row-groups of G (0 = row-major), -1 = table
 static int g_dma_r = -1;  // jdt_gemm_set_r(r): force r 64-deep sub-tiles per ring slot (sweeps); -1 auto
 // R > 1 slots: 3 of them within 96 KB (and the vmcnt immediate range)
 template <int BM, int BN>
-constexpr bool r_ok(int r) { return (BM + BN) * DMA_BK * 2 * 3 * r <= 96 * 1024 && (BM / 32 + BN / 32) * r <= 63; }
+constexpr bool r_ok(int r) { return r == 1 || ((BM + BN) * DMA_BK * 2 * 3 * r <= 96 * 1024 && (BM / 32 + BN / 32) * r <= 63); }
 
 template <int WM, int WN, int TM, int TN>
 static int launch_dma(const GemmArgs& g, int batch, int splits, float* ws, long ws_floats, unsigned* counters,
-                      long n_counters, hipStream_t st, int r_pref = 1) {
+                      long n_counters, hipStream_t st, int r_pref = 1, int gm_pref = 0) {
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
   if (g.M % BM || g.N % BN) return 1;
   const int tiles_n = g.N / BN;
@@ -1415,13 +1434,15 @@ static int launch_dma(const GemmArgs& g, int batch, int splits, float* ws, long 
   // cost more than the narrow stores on those small outputs (in-model A/B,
   // tools/gpu_r2_ab_epi.sh: microbatch-loop transformer 3.07 ms vec vs 2.98)
   const int vec = g_epi_vec && BM * BN >= 2048 && (long)g.M * g.N * batch >= g_epi_vec_min && epi_vec_ok(g, batch);
+  if (WM * WN != 4 && !epi_vec_ok(g, batch)) return 1;  // 8-wave tiles: vectorised epilogue only
   // sub-tiles per ring slot: g_dma_r forces (sweeps), else 1
   int R = g_dma_r > 0 ? g_dma_r : r_pref;
+  const int gm = g_group_m >= 0 ? g_group_m : gm_pref;
   while (R > 1 && (kchunk / DMA_BK) % R) R >>= 1;
   if (R > 1 && !r_ok<BM, BN>(R)) R = 1;
 #define JDT_DMA_S(A_, B_, S_, R_)                                                                                 \
-  hipLaunchKernelGGL((gemm_dma_kernel<WM, WN, TM, TN, A_, B_, S_, R_>), grid, dim3(256), 0, st, g, tiles_n, sp,    \
-                     kchunk, ws, counters, vec)
+  hipLaunchKernelGGL((gemm_dma_kernel<WM, WN, TM, TN, A_, B_, S_, R_>), grid, dim3(64 * WM * WN), 0, st, g, tiles_n, \
+                     sp, kchunk, ws, counters, vec, gm)
 #define JDT_DMA(A_, B_)                                                   \
   do {                                                                    \
     if constexpr (r_ok<BM, BN>(4)) {                                      \
@@ -1448,20 +1469,25 @@ static int launch_dma(const GemmArgs& g, int batch, int splits, float* ws, long 
 // 512-row entries the isolated sweep also favoured were dropped: inside the
 // microbatch-loop transformer step (colder operands, neighbouring kernels) they
 // measured 2 % slower than the heuristic (tools/gpu_r2_ab_tune.sh).
-// {M, N, K, a_trans, b_trans, cfg, R}.
-struct GemmTune { int M, N, K, at, bt, cfg, r; };
+// Tile ORDER (gm): long-K problems with small tiles fetch the operand panels of
+// their whole tile row from beyond the XCD's L2 every K-tile; ordering the tiles
+// in row-groups of gm (column-major inside a group) makes each XCD's contiguous
+// run of tiles a near-square block (qkv dW 19.9 -> 16.3 us at gm = 8; no effect
+// on the 2048 x 2048 short-K shapes).  cfg 15 / 16: 8-wave 128 x 128 tiles.
+// {M, N, K, a_trans, b_trans, cfg, R, gm}.
+struct GemmTune { int M, N, K, at, bt, cfg, r, gm; };
 static const GemmTune kGemmTune[] = {
-    {2048, 1536, 512, 0, 1, 11, 1},   // qkv fwd (2048 rows)       10.38 (12.15)
-    {2048, 512, 2048, 0, 1, 10, 2},   // fc2 fwd                   14.41 (13.78)
-    {512, 2048, 2048, 1, 1, 10, 1},   // fc1 / head dW             18.54 (16.64)
-    {2048, 2048, 512, 0, 1, 12, 1},   // fc1 / head fwd            10.99 (11.19)
-    {2048, 2048, 512, 0, 0, 12, 1},   // fc2 dX                    10.36 (9.73)
-    {2048, 512, 2048, 0, 0, 10, 2},   // fc1 / head dX             12.00 (10.98)
-    {2048, 512, 2048, 1, 1, 10, 2},   // fc2 dW                    15.48 (16.53)
-    {512, 1536, 2048, 1, 1, 10, 1},   // qkv dW                    19.66 (15.93)
-    {512, 512, 2048, 1, 1, 13, 2},    // out dW                    10.41 (15.46)
-    {256, 1536, 512, 0, 1, 10, 2},    // qkv fwd (hybrid, 256 rows) 5.55 (5.60)
-    {256, 512, 2048, 0, 1, 13, 2},    // fc2 fwd (hybrid)          8.38 (9.84)
+    {2048, 1536, 512, 0, 1, 11, 1, 0},   // qkv fwd (2048 rows)       10.38 (12.15)
+    {2048, 512, 2048, 0, 1, 10, 2, 0},   // fc2 fwd                   14.41 (13.78)
+    {512, 2048, 2048, 1, 1, 10, 1, 8},   // fc1 / head dW             17.46 (16.26)
+    {2048, 2048, 512, 0, 1, 15, 1, 0},   // fc1 / head fwd            10.37 (11.02)
+    {2048, 2048, 512, 0, 0, 16, 1, 0},   // fc2 dX                    10.16 (9.91)
+    {2048, 512, 2048, 0, 0, 10, 2, 0},   // fc1 / head dX             12.00 (10.98)
+    {2048, 512, 2048, 1, 1, 10, 2, 0},   // fc2 dW                    15.48 (16.53)
+    {512, 1536, 2048, 1, 1, 10, 1, 8},   // qkv dW                    16.28 (16.09)
+    {512, 512, 2048, 1, 1, 13, 2, 0},    // out dW                    10.41 (15.46)
+    {256, 1536, 512, 0, 1, 10, 2, 0},    // qkv fwd (hybrid, 256 rows) 5.55 (5.60)
+    {256, 512, 2048, 0, 1, 13, 2, 0},    // fc2 fwd (hybrid)          8.38 (9.84)
 };
 static bool g_gemm_tune = true;  // jdt_gemm_set_tune(0): heuristic only (A/B)
 
@@ -1471,12 +1497,13 @@ static int gemm_dma(const GemmArgs& g, int batch, int cfg, int splits, float* ws
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   if (!al(g.A) || !al(g.B) || g.lda % 8 || g.ldb % 8) return 1;
   if (batch > 1 && (g.sA % 8 || g.sB % 8 || g.sA2 % 8 || g.sB2 % 8)) return 1;
-  int r_pref = 1;
+  int r_pref = 1, gm_pref = 0;
   if (cfg < 0 && g_gemm_tune && batch == 1 && splits < 0) {
     for (const GemmTune& t : kGemmTune)
       if (t.M == g.M && t.N == g.N && t.K == g.K && t.at == (g.a_trans != 0) && t.bt == (g.b_trans != 0)) {
         cfg = t.cfg;
         r_pref = t.r;
+        gm_pref = t.gm;
         break;
       }
   }
@@ -1492,14 +1519,24 @@ static int gemm_dma(const GemmArgs& g, int batch, int cfg, int splits, float* ws
     else if (t64 <= 768 || g.N % 128) cfg = 11;
     else cfg = 12;
   }
+  int rc = 1;
   switch (cfg) {
-    case 10: return launch_dma<2, 2, 1, 2>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref);  // 32 x 64
-    case 11: return launch_dma<2, 2, 2, 2>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref);  // 64 x 64
-    case 12: return launch_dma<2, 2, 2, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref);  // 64 x 128
-    case 13: return launch_dma<2, 2, 1, 1>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref);  // 32 x 32
-    case 14: return launch_dma<2, 2, 4, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref);  // 128 x 128
+    case 10: return launch_dma<2, 2, 1, 2>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref, gm_pref);  // 32 x 64
+    case 11: return launch_dma<2, 2, 2, 2>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref, gm_pref);  // 64 x 64
+    case 12: return launch_dma<2, 2, 2, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref, gm_pref);  // 64 x 128
+    case 13: return launch_dma<2, 2, 1, 1>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref, gm_pref);  // 32 x 32
+    case 14: return launch_dma<2, 2, 4, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref, gm_pref);  // 128 x 128
+    // 8 waves (two per SIMD: one wave's LDS reads / DMA issue under the other's MFMAs)
+    case 15: rc = launch_dma<2, 4, 4, 2>(g, batch, splits, ws, ws_floats, counters, n_counters, st, 1, gm_pref); break;  // 128 x 128
+    case 16: rc = launch_dma<4, 2, 2, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st, 1, gm_pref); break;  // 128 x 128
+    case 17: rc = launch_dma<4, 2, 4, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st, 1, gm_pref); break;  // 256 x 128
+    case 18: rc = launch_dma<2, 4, 4, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st, 1, gm_pref); break;  // 128 x 256
     default: return 1;
   }
+  // 8-wave tiles outside their envelope (shape, or rows not 16-byte aligned for the
+  // vectorised epilogue): the 4-wave 64 x 128 tile
+  if (rc == 1) rc = launch_dma<2, 2, 2, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st, 1, gm_pref);
+  return rc;
 }
 
 
@@ -1641,4 +1678,5 @@ JDT_API int jdt_gemm_group(const GemmArgs* gs, int n, float* ws, long ws_floats,
   return gemm_dma_group(gs, n, ws, ws_floats, counters, n_counters, static_cast<hipStream_t>(stream));
 }
 JDT_API void jdt_gemm_set_group_split(int on) { g_group_split = on; }
+JDT_API void jdt_gemm_set_group_m(int gm) { g_group_m = gm; }
 JDT_API void jdt_gemm_set_group_tile(int t) { g_group_tile = t; }

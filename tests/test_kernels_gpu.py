@@ -172,6 +172,43 @@ def test_gemm_vec_epilogue_bit_identical(cfg, r, a_layout, b_layout):
     _close(db_v, db_e, rtol=1e-5, atol=1e-4)  # fp32 atomics: summation order differs
 
 
+@pytest.mark.parametrize("cfg", [15, 16, 17, 18])
+@pytest.mark.parametrize("a_layout,b_layout", [("mk", "kn"), ("mk", "nk"), ("km", "kn"), ("km", "nk")])
+def test_gemm_8wave_tiles_match_4wave(cfg, a_layout, b_layout):
+    """8-wave LDS-DMA tiles (two waves per SIMD; 128 x 128, 256 x 128, 128 x 256)
+    accumulate every output element in the same K order as the 4-wave 128 x 128
+    tile: bit-identical outputs for the full forward / backward epilogues,
+    bf16 / fp32 accumulate and split-K; and close to the fp32 reference."""
+    M, N, K_ = 512, 512, 1024
+    a = _mk((M, K_) if a_layout == "mk" else (K_, M), torch.bfloat16, seed=91).to(DEV)
+    b = (_mk((K_, N) if b_layout == "kn" else (N, K_), torch.float32, seed=92) * 0.05).to(torch.bfloat16).to(DEV)
+    bias, res = _mk((N,), torch.bfloat16, seed=93).to(DEV), _mk((M, N), torch.bfloat16, seed=94).to(DEV)
+    z = _mk((M, N), torch.bfloat16, seed=95).to(DEV)
+
+    def run(c):
+        kw = dict(a_layout=a_layout, b_layout=b_layout, cfg=c)
+        zo = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        f = kern.gemm(a, b, bias=bias, act="gelu", z_out=zo, keep_prob=0.9, seed=7, offset=11, resid=res, **kw)
+        db = torch.zeros(N, device=DEV)
+        g = kern.gemm(a, b, z_in=z, act_bwd="silu", keep_prob=0.9, seed=3, offset=5, dbias=db, **kw)
+        acc16 = res.clone()
+        kern.gemm(a, b, out=acc16, accumulate=True, **kw)
+        acc32 = [torch.full((M, N), 0.5, device=DEV) for _ in range(2)]
+        kern.gemm(a, b, out=acc32[0], accumulate=True, splits=1, **kw)
+        kern.gemm(a, b, out=acc32[1], accumulate=True, splits=4, **kw)
+        torch.cuda.synchronize()
+        return [zo, f, g, acc16, acc32[0], acc32[1]], db
+
+    outs, db = run(cfg)
+    ref_outs, ref_db = run(14)
+    for x, y in zip(outs, ref_outs):
+        assert torch.equal(x, y)
+    _close(db, ref_db, rtol=1e-5, atol=1e-4)  # fp32 atomics: summation order differs
+    A = a.float() if a_layout == "mk" else a.float().t()
+    B = b.float() if b_layout == "kn" else b.float().t()
+    _close(outs[4] - 0.5, A @ B, rtol=2e-3, atol=2e-3)
+
+
 @pytest.mark.parametrize("tile", [32, 64, 128])
 def test_gemm_group_tiles(tile):
     """Grouped launch at each tile size (forced): a weight gradient (km x kn, fp32

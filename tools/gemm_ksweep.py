@@ -22,12 +22,14 @@ def main():
     ap.add_argument("--mn", type=int, default=2048)
     ap.add_argument("--layouts", default="mk/kn,mk/nk,km/kn")
     ap.add_argument("--epi", default="1", help="comma list of vectorised-epilogue settings to compare (0,1)")
+    ap.add_argument("--group-m", default="0", help="comma list of tile row-group sizes to compare (0 = row-major)")
+    ap.add_argument("--ks", default="64,128,256,512,1024,2048")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     M = N = args.mn
     for lay in args.layouts.split(","):
         al, bl = lay.split("/")
-        for Kd in (64, 128, 256, 512, 1024, 2048):
+        for Kd in (int(k) for k in args.ks.split(",")):
             a = torch.randn(*((M, Kd) if al == "mk" else (Kd, M)), device=dev).to(torch.bfloat16)
             b = torch.randn(*((Kd, N) if bl == "kn" else (N, Kd)), device=dev).to(torch.bfloat16)
             c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
@@ -35,8 +37,11 @@ def main():
             for ev in (int(x) for x in args.epi.split(",")):
                 _lib.lib().jdt_gemm_set_epi_vec(ev)
                 for cfg in (int(x) for x in args.cfgs.split(",")):
-                    t = timed(lambda: K.gemm(a, b, a_layout=al, b_layout=bl, out=c, cfg=cfg, splits=1))
-                    row.append(f"e{ev} cfg{cfg} {t:6.2f}")
+                    for gm in (int(x) for x in args.group_m.split(",")):
+                        _lib.lib().jdt_gemm_set_group_m(gm)
+                        t = timed(lambda: K.gemm(a, b, a_layout=al, b_layout=bl, out=c, cfg=cfg, splits=1))
+                        row.append(f"c{cfg}g{gm} {t:6.2f}")
+                    _lib.lib().jdt_gemm_set_group_m(-1)
             _lib.lib().jdt_gemm_set_epi_vec(1)
             tr = timed(lambda: torch.matmul(a if al == "mk" else a.t(), b if bl == "kn" else b.t()))
             fl = 2.0 * M * N * Kd

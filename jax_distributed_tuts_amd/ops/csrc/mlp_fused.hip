@@ -83,6 +83,19 @@ struct Mlp2Args {
   // partial logits to det_logits[H/16][M][C] instead of fp32-atomically adding them;
   // mlp2_bwd sums the partials in column-block order -> bitwise-reproducible steps
   float* det_logits;
+  // run-ahead step (mlp2_bwd_kernel<..., AHEAD>): the backward launch of step t also runs
+  // step t+1's forward, so a step is ONE launch.  XR: row-major bf16 copy of X written by
+  // mlp2_fwd; zslab: per-(hidden block, input chunk) partial Z1 = X[:, chunk] W1[chunk, blk]
+  // fp32 [H/16][K_IN/KC][MPM/4][16][4]; ztick (32-word = 128-byte lines, no line is
+  // shared by two XCDs' L2s): line 0 = step ticket, error word, launch counter; line
+  // 1 + blk = column block blk's barrier counter; then one line per XCD with a counter
+  // per tile it runs (== the launch counter when every tile ran exactly once per
+  // launch); hand: fp32 updated b1 [H], W2 [H][C], b2 [C]
+  // handed from the chunk-0 / lead workgroups to each column block's last arriver.
+  // lg3: logits accumulators indexed by step % 3 (forward of t+1 accumulates into one
+  // buffer while the backward of t reads another and re-arms the third).
+  bf16_t* XR; float* zslab; unsigned* ztick; float* hand;
+  int lg3;
 };
 
 // Persistent multi-step launch (mlp2_loop_kernel): n steps, grid barriers between
@@ -98,12 +111,13 @@ struct Mlp2Loop {
   unsigned long long* stamps;   // diagnostic: [G][n][5] s_memrealtime per phase edge (null = off)
 };
 
-// Slots 0-4: s_memrealtime at phase ends; slots 5/6: s_memtime (core clock) at
-// phases 0/4, so (slot6 - slot5) / (slot4 - slot0) * 100 MHz is the shader clock.
+// 16 slots per workgroup.  Slots 0-4: s_memrealtime at phase ends; slots 5/6:
+// s_memtime (core clock) at phases 0/4, so (slot6 - slot5) / (slot4 - slot0) * 100 MHz
+// is the shader clock; slots 8-11: run-ahead phases (mlp2_bwd AHEAD).
 #define STAMP(i)                                                                              \
   do {                                                                                        \
     if (a.stamps && threadIdx.x == 0) {                                                       \
-      unsigned long long* s_ = a.stamps + (long)(blockIdx.y * gridDim.x + blockIdx.x) * 8;  \
+      unsigned long long* s_ = a.stamps + (long)(blockIdx.y * gridDim.x + blockIdx.x) * 16; \
       s_[(i)] = __builtin_amdgcn_s_memrealtime();                                             \
       if ((i) == 0) s_[5] = __builtin_amdgcn_s_memtime();                                     \
       if ((i) == 4) s_[6] = __builtin_amdgcn_s_memtime();                                     \
@@ -368,6 +382,15 @@ __device__ __forceinline__ void mlp2_fwd_body(AT& a, const int bx, const int by,
     u32x4 o; o.x = q[0]; o.y = q[1]; o.z = q[2]; o.w = q[3];
     st_b128<LOOP>(a.XT + (long)xk * a.ldxt + r0 + h, o);
   }
+  // row-major bf16 X side output (run-ahead backward: the next step's forward operand)
+  if constexpr (!LOOP) {
+    if (a.XR && by < K_IN / XTC && tid < RB * (XTC / 8)) {
+      const int rl = tid / (XTC / 8), q = tid % (XTC / 8);
+      if (r0 + rl < M)
+        *reinterpret_cast<u32x4*>(a.XR + (long)(r0 + rl) * K_IN + by * XTC + 8 * q) =
+            *reinterpret_cast<const u32x4*>(&xs[rl * LDXS + by * XTC + 8 * q]);
+    }
+  }
 
   // ---- 3. K split over the 8 waves
   constexpr int MT = RB / 16;
@@ -433,7 +456,7 @@ __device__ __forceinline__ void mlp2_fwd_body(AT& a, const int bx, const int by,
   }
   __syncthreads();
   STAMP(3);
-  float* lg = a.logits + (long)par * M * C;
+  float* lg = a.logits + (long)(a.lg3 ? step % 3 : par) * M * C;
   if (tid < RB * C) {
     const int rl = tid / C, c = tid % C, row = r0 + rl;
     if (row < M) {
@@ -449,7 +472,16 @@ __device__ __forceinline__ void mlp2_fwd_body(AT& a, const int bx, const int by,
 }
 
 // ---------------------------------------------------------------------------- backward
-template <int K_IN, int C, int KC, bool LOOP, class AT>
+// AHEAD (single GPU, fused AdamW, W1^T copy): after its AdamW epilogue every
+// workgroup (blk, chunk) also computes the partial Z1 = X[:, chunk] W1'[chunk, blk]
+// of the NEXT step from the W1' tile it just produced (phase 5); the last of a
+// column block's K_IN/KC workgroups to arrive sums the partials in chunk order and
+// runs the forward epilogue (bias, SiLU, dropout of step t+1, G1/H1, partial logits).
+// So one launch per step: the kernel boundary the forward needed (W1' complete) is
+// replaced by a per-column-block arrival ticket among workgroups that share an XCD
+// (xcd_contiguous_tile), and the one global dependency left -- complete logits for
+// the next CE -- is the launch boundary.
+template <int K_IN, int C, int KC, bool LOOP, bool AHEAD = false, class AT>
 __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by, const int step_in) {
   constexpr int MPM = 128;                 // max rows per device (fused path)
   constexpr int LDM = MPM + 8;             // padded row (bf16 elements)
@@ -464,6 +496,13 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   __shared__ __attribute__((aligned(16))) bf16_t h1T[16 * LDM];    // H1[:, blk]^T   (chunk-0 blocks)
   __shared__ __attribute__((aligned(16))) bf16_t dlT[16 * LDM];    // dlogits^T, classes padded to 16
   __shared__ float red[2][NW];
+  static_assert(!AHEAD || (!LOOP && KC <= 128 && KC % 16 == 0), "run-ahead: K chunk within 4 k-steps");
+  constexpr int LDW1 = 128 + 8;            // w1n row: one hidden unit's KC inputs, zero-padded to 128
+  constexpr int NCH = K_IN / KC;           // workgroups per column block
+  __shared__ __attribute__((aligned(16))) bf16_t w1n[AHEAD ? 16 * LDW1 : 8];   // W1'[chunk, blk]^T
+  __shared__ float htA[AHEAD ? MPM : 1][17];                                   // next H tile
+  __shared__ float w2A[AHEAD ? 16 : 1][C];
+  __shared__ float b2A[C];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int M = a.M, H = a.H, Mp = (M + 31) & ~31;
   const int j0 = bx * 16, kc0 = by * KC;
@@ -477,11 +516,24 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   // none waits on the step counter (both logits / W2-shadow parities are loaded):
   // a load under a divergent guard makes the compiler wait for it at the join,
   // which serialised this phase into ~6 round trips (asm).  The step counter is
-  // loaded last (its scalar read-back waits for every earlier load).
-  float lr0[C], lr1[C];
+  // loaded last (its scalar read-back waits for every earlier load).  Run-ahead: it is
+  // loaded FIRST through a lane-varying address instead (a per-lane value, as in the
+  // forward), so step t+1's dropout bits are computed while the other loads fly.
+  int step_lane = 0;
+  if constexpr (AHEAD) {
+    int lz;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(lz));
+    step_lane = a.step[lz];
+  }
+  float lr0[C], lr1[C], lr2[AHEAD ? C : 1];
   {
     const long lo = (long)min(tid, M - 1) * C;
-    if constexpr (LOOP) {   // step known: this step's parity only
+    if constexpr (AHEAD) {   // step % 3 buffers, all three loaded (no wait on the step)
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        lr0[c] = a.logits[lo + c]; lr1[c] = a.logits[(long)M * C + lo + c]; lr2[c] = a.logits[2l * M * C + lo + c];
+      }
+    } else if constexpr (LOOP) {   // step known: this step's parity only
       const float* lg = a.logits + (long)(step_in & 1) * M * C;
 #pragma unroll
       for (int c = 0; c < C; ++c) lr1[c] = lr0[c] = ld_f<true>(lg + lo + c);
@@ -546,13 +598,40 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   const float run_pre = (a.running ? a.running : a.logits)[lane & 3];   // lead: metric accumulators
   const int lq = min(lane, C - 1);
   const float qp = (fo ? a.pb2 : a.gb2)[lq], qm = (fo ? a.mb2 : a.gb2)[lq], qv = (fo ? a.vb2 : a.gb2)[lq];
+  // run-ahead: A fragments of X[16w.., chunk] (row-major bf16 copy) for the next
+  // forward (in flight through CE, dZ1 and dW1); k past the chunk is multiplied by
+  // w1n's zero padding, so the address is only clamped.  Then step t+1's dropout bits
+  // for this thread's row group of the epilogue share (phase 6: workgroup `by` of the
+  // column block finishes row groups [g_lo, g_hi)), computed from the per-lane step
+  // while the loads fly.
+  bf16x8 xa[AHEAD ? 4 : 1];
+  u32x4 dbn = {0u, 0u, 0u, 0u};
+  const int g_lo = (by * (MPM / 4)) / NCH, g_hi = ((by + 1) * (MPM / 4)) / NCH;
+  const int eg = g_lo + (tid >> 4);   // phase 6: this thread's row group (tid < 16 * (g_hi - g_lo))
+  if constexpr (AHEAD) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      xa[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(
+                   a.XR + (long)min(w * 16 + (lane & 15), M - 1) * K_IN + min(kc0 + ks * 32 + 8 * (lane >> 4), K_IN - 8)));
+    if (a.keep < 1.f && eg < g_hi && eg * 4 < M)
+      dbn = dropout_bits(a.seed, a.offset + ((unsigned long long)(unsigned)(step_lane + 1) << 32),
+                         dropout_group(0, eg * 4, j0 + gn, M, H));
+  }
   __builtin_amdgcn_sched_barrier(0);
   int step = step_in;
-  if constexpr (!LOOP) step = (a.step_copy ? a.step_copy : a.step)[0];
+  if constexpr (AHEAD) step = step_lane;   // advanced by the step ticket once every workgroup has read it
+  else if constexpr (!LOOP) step = (a.step_copy ? a.step_copy : a.step)[0];
   const int par = step & 1;
   float lrow[C];
+  if constexpr (AHEAD) {
+    const int p3 = step % 3;
 #pragma unroll
-  for (int c = 0; c < C; ++c) lrow[c] = par ? lr1[c] : lr0[c];
+    for (int c = 0; c < C; ++c) lrow[c] = p3 == 0 ? lr0[c] : (p3 == 1 ? lr1[c] : lr2[c]);
+  } else {
+#pragma unroll
+    for (int c = 0; c < C; ++c) lrow[c] = par ? lr1[c] : lr0[c];
+  }
+
   const AdamK ak = adam_consts(a, step);
   const long goff = (!fo && a.stage_stride) ? (long)par * a.stage_stride : 0;   // staged bucket half
 
@@ -596,8 +675,13 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     l_loss = wave_sum(l_loss);
     l_corr = wave_sum(l_corr);
     if (lane == 0) { red[0][w] = l_loss; red[1][w] = l_corr; }
-    float* nxt = a.logits + (long)(par ^ 1) * M * C;   // re-arm next step's accumulator
+    // re-arm the accumulator of the step after next (run-ahead: step t+1's forward
+    // accumulates into buffer (t+1) % 3 during this launch)
+    float* nxt = a.logits + (long)(AHEAD ? (step + 2) % 3 : (par ^ 1)) * M * C;
     for (int i = tid; i < M * C; i += NT) st_f<LOOP>(nxt + i, 0.f);
+  }
+  if constexpr (AHEAD) {   // K padding of the W1' tile image
+    for (int idx = tid; idx < 16 * (128 - KC); idx += NT) w1n[(idx / (128 - KC)) * LDW1 + KC + idx % (128 - KC)] = 0;
   }
   __syncthreads();
   STAMP(1);
@@ -653,6 +737,8 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     // the lane's 4 rows are 4 consecutive K elements of W1^T: one 8-byte store
     if (a.fuse_opt && a.W1T)
       st_u64<LOOP>(a.W1T + (long)tcol * a.ldw1t + trow0, (unsigned long long)wt[0] | ((unsigned long long)wt[1] << 32));
+    if constexpr (AHEAD)
+      *reinterpret_cast<uint2*>(&w1n[(lane & 15) * LDW1 + (trow0 - kc0)]) = make_uint2(wt[0], wt[1]);
   } else if (aux) {
     // chunk-0 blocks, concurrently with the dW1 tiles:
     //   dW2[blk, :] = H1[:, blk]^T dlogits ; db1[blk] = dZ1[:, blk]^T 1 ; db2 = 1^T dlogits (block (0,0))
@@ -685,15 +771,20 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
           const float pn = adam_apply_h<LOOP>(op[e], om[e], ov[e], gr, ak, (isb ? a.pb1 : a.pW2) + o,
                                               (isb ? a.mb1 : a.mW2) + o, (isb ? a.vb1 : a.vW2) + o);
           (isb ? a.sb1 : sW2n)[o] = f2bf(pn);
+          if constexpr (AHEAD) a.hand[(isb ? 0 : H) + o] = pn;   // same XCD as the reader (L2)
         } else {
           (isb ? a.gb1 : a.gW2)[goff + o] = gr;
         }
       }
     }
     if (lead && lane < C) {
-      if (a.fuse_opt)
-        a.sb2[lane] = f2bf(adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane));
-      else a.gb2[goff + lane] = ab2[0];
+      if (a.fuse_opt) {
+        const float pn = adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
+        a.sb2[lane] = f2bf(pn);
+        if constexpr (AHEAD) a.hand[H + (long)H * C + lane] = pn;
+      } else {
+        a.gb2[goff + lane] = ab2[0];
+      }
     }
   }
   __syncthreads();
@@ -707,7 +798,139 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     else if (a.mslot) a.mslot[goff + tid] = val;
     // advance the device step: every other workgroup of this launch reads the
     // forward's copy (step_copy), so no arrival ticket is needed
-    if (!LOOP && fo && tid == 0) a.step[0] = step + 1;   // the loop kernel advances it at its end
+    if (!LOOP && !AHEAD && fo && tid == 0) a.step[0] = step + 1;   // the loop kernel advances it at its end
+  }
+  if constexpr (AHEAD) {
+    // tile-map check (xcd_column_tile): this tile's counter, only touched on this XCD,
+    // must read the launch number
+    unsigned tile_seen = 0u, launch_no = 0u;
+    if (tid == 0) {
+      launch_no = a.ztick[2];
+      const int tpx = (H / 16) * NCH / 8, t = bx * NCH + by;   // tiles per XCD, this tile
+      tile_seen = __hip_atomic_fetch_add((gu32_t*)(a.ztick + 32 * (1 + H / 16) + 32 * ((tpx + 31) / 32) * (t / tpx) + t % tpx),
+                                         1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    // ---- 5. step t+1's partial Z1 for (chunk, blk): wave w -> rows 16w.., K = this chunk
+    f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (ks * 32 < KC) {
+        const bf16x8 bw = *reinterpret_cast<const bf16x8*>(&w1n[(lane & 15) * LDW1 + ks * 32 + 8 * (lane >> 4)]);
+        z = mfma16x16x32(xa[ks], bw, z);
+      }
+    }
+    // lane: rows 16w + 4(lane>>4) + e of column j0 + (lane & 15) = one 4-row dropout group.
+    // The column block's workgroups run on ONE XCD (xcd_column_tile), so the hand-off
+    // lives in that XCD's L2: plain stores (L1 is write-through) drained by vmcnt, an
+    // L2 counter (workgroup-scope atomics), loads with sc1 (never served by the L1).
+    float* const zb = a.zslab + (long)bx * NCH * (MPM / 4) * 64;
+    *reinterpret_cast<u32x4*>(zb + ((long)by * (MPM / 4) + w * 4 + (lane >> 4)) * 64 + (lane & 15) * 4) =
+        (u32x4){__float_as_uint(z[0]), __float_as_uint(z[1]), __float_as_uint(z[2]), __float_as_uint(z[3])};
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // partials, hand-offs, launch_no: in the L2 / read
+    STAMP(8);
+    __syncthreads();
+    // ---- column-block barrier: all NCH workgroups of the column block are resident
+    // (one launch of H/16 * NCH <= CU-count workgroups); monotonic counter, so no reset.
+    // A wall-clock timeout (s_memrealtime) raises the error word instead of hanging.
+    if (tid == 0) {
+      unsigned* cnt = a.ztick + 32 * (1 + bx);
+      __hip_atomic_fetch_add((gu32_t*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const unsigned target = (unsigned)NCH * (launch_no + 1u);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      // poll with sc1 loads (never served by this CU's L1, which is coherent only
+      // within a workgroup; an idempotent atomic such as +0 is folded into a plain load)
+      const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(cnt, (short)0, 4, 0x00020000);
+      while ((int)((unsigned)__builtin_amdgcn_raw_buffer_load_b32(cr, 0, 0, 16) - target) < 0) {
+        if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > 2000000ll) {   // 20 ms
+          atomicOr(a.ztick + 1, 2u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+      }
+      if (tile_seen != launch_no) atomicOr(a.ztick + 1, 1u);   // a tile ran twice / not at all
+    }
+    __syncthreads();
+    STAMP(9);
+    // ---- 6. step t+1's forward epilogue, row groups [g_lo, g_hi) of column block blk
+    const int ng = g_hi - g_lo;
+    const __amdgpu_buffer_rsrc_t zr = __builtin_amdgcn_make_buffer_rsrc(zb, (short)0, NCH * (MPM / 4) * 64 * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t hr =
+        __builtin_amdgcn_make_buffer_rsrc(a.hand, (short)0, (int)((H + H * C + C) * 4), 0x00020000);
+    float4 zp[NCH];
+    const int egc = min(eg, g_hi - 1);
+#pragma unroll
+    for (int q = 0; q < NCH; ++q)
+      zp[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             zr, (int)((((long)q * (MPM / 4) + egc) * 64 + gn * 4) * 4), 0, 16));
+    const float b1v = round_bf(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(hr, (j0 + gn) * 4, 0, 16)));
+    if (tid < 16 * C)
+      w2A[tid / C][tid % C] =
+          round_bf(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(hr, (H + j0 * C + tid) * 4, 0, 16)));
+    if (tid < C)
+      b2A[tid] = bx == 0 ? round_bf(__builtin_bit_cast(
+                               float, __builtin_amdgcn_raw_buffer_load_b32(hr, (H + H * C + tid) * 4, 0, 16)))
+                         : 0.f;
+    if (a.stamps) {   // diagnostic: wait for the partials before stamping
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      STAMP(10);
+    }
+    if (tid < 16 * ng) {
+      float gf[4];
+      unsigned long long hpk = 0ull;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = eg * 4 + e;
+        float hvn = 0.f;
+        gf[e] = 0.f;
+        if (row < M) {
+          float v = b1v;   // + the NCH chunk partials in chunk order
+#pragma unroll
+          for (int q = 0; q < NCH; ++q) v += e == 0 ? zp[q].x : e == 1 ? zp[q].y : e == 2 ? zp[q].z : zp[q].w;
+          const float zz = bf2f(f2bf(v));           // Z1 as the bf16 Dense output
+          const float ez = __expf(-zz);
+          hvn = zz / (1.0f + ez);                    // act_fwd(ACT_SILU)
+          const float sg = 1.0f / (1.0f + ez);
+          float gd = sg * (1.0f + zz * (1.0f - sg));  // act_grad(ACT_SILU)
+          if (a.keep < 1.f) {
+            const bool kp = keep_word(dbn, e, a.keep);
+            hvn = kp ? hvn / a.keep : 0.f;
+            gd = kp ? gd / a.keep : 0.f;
+          }
+          gf[e] = gd;
+          const bf16_t hb = f2bf(hvn);
+          hpk |= (unsigned long long)hb << (16 * e);
+          hvn = bf2f(hb);
+        }
+        htA[(tid >> 4) * 4 + e][gn] = hvn;
+      }
+      if (eg * 4 < M) {
+        const long gq = ((long)eg * H + j0 + gn) * 4;
+        *reinterpret_cast<u32x4*>(a.G1 + gq) =
+            (u32x4){__float_as_uint(gf[0]), __float_as_uint(gf[1]), __float_as_uint(gf[2]), __float_as_uint(gf[3])};
+        *reinterpret_cast<unsigned long long*>(a.H1 + gq) = hpk;
+      }
+    }
+    __syncthreads();
+    STAMP(11);
+    float* lgn = a.logits + (long)((step + 1) % 3) * M * C;
+    const int r0 = g_lo * 4, nr = min(ng * 4, M - r0);
+    if (tid < nr * C) {
+      const int rl = tid / C, c = tid % C;
+      float sacc = b2A[c];
+#pragma unroll
+      for (int n = 0; n < 16; ++n) sacc += htA[rl][n] * w2A[n][c];
+      atomicAdd(lgn + (long)(r0 + rl) * C + c, sacc);
+    }
+    // every workgroup read the step counter before the column barrier; one workgroup
+    // per column block reports, the last of them advances the step and launch counters
+    if (by == 0 && tid == 0 &&
+        __hip_atomic_fetch_add((gu32_t*)a.ztick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            (unsigned)(H / 16 - 1)) {
+      __hip_atomic_store((gu32_t*)a.ztick, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a.step[0] = step + 1;
+      a.ztick[2] = launch_no + 1u;
+    }
   }
   STAMP(4);
 }
@@ -720,11 +943,31 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   if constexpr (XCD) xcd_contiguous_tile(bx, by);
   mlp2_fwd_body<K_IN, C, RB, DIRECT, false>(static_cast<const Mlp2Args&>(a), bx, by, 0);
 }
-template <int K_IN, int C, int KC, bool XCD>
+// Run-ahead tile map, from the XCD the workgroup actually runs on (HW_REG_XCC_ID):
+// XCD x takes tiles [x G/8, (x+1) G/8) in chunk-fastest order, i.e. whole column
+// blocks (all gridDim.y input chunks of 16 hidden units: their Z1 partials meet in
+// the XCD's L2) and 4 neighbouring ones (whole 128-byte lines of W1 rows); its
+// workgroups are told apart by L / 8.  Workgroups are dealt round-robin over the XCDs
+// (linear id L -> XCD (L + o) % 8, the offset o carried over from earlier dispatches),
+// so each XCD gets G/8 workgroups with distinct L / 8 and this is a bijection.  The
+// body checks it: every tile has a per-launch counter (ztick tail) that must read
+// the launch number, otherwise the error word is raised and the host refuses the
+// results (FusedMLP2.finalize).
+__device__ __forceinline__ void xcd_column_tile(int& bx, int& by) {
+  const int L = blockIdx.x + gridDim.x * blockIdx.y, G = gridDim.x * gridDim.y;
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+  const int t = (int)(xcc & 7u) * (G / 8) + L / 8;
+  bx = t / gridDim.y;
+  by = t % gridDim.y;
+}
+
+template <int K_IN, int C, int KC, bool XCD, bool AHEAD = false>
 __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   int bx = blockIdx.x, by = blockIdx.y;
-  if constexpr (XCD) xcd_contiguous_tile(bx, by);
-  mlp2_bwd_body<K_IN, C, KC, false>(static_cast<const Mlp2Args&>(a), bx, by, 0);
+  if constexpr (AHEAD) xcd_column_tile(bx, by);
+  else if constexpr (XCD) xcd_contiguous_tile(bx, by);
+  mlp2_bwd_body<K_IN, C, KC, false, AHEAD>(static_cast<const Mlp2Args&>(a), bx, by, 0);
 }
 
 // n complete training steps in ONE launch (single GPU, fused AdamW, W1^T copy):
@@ -832,6 +1075,19 @@ JDT_API int jdt_mlp2_loop(const Mlp2Args* args, int n, unsigned* ctr, unsigned* 
   return HIP_LAUNCH_CHECK();
 }
 
+// 1 if the run-ahead backward can run M rows x H hidden units here: its column-block
+// barrier needs every workgroup of the launch resident at once.  Called before capture.
+JDT_API int jdt_mlp2_ahead_ok(int M, int H) {
+  if (H % 128 || M <= 0 || M > 128) return 0;
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, mlp2_bwd_kernel<784, 10, 112, true, true>, NT, 0) != hipSuccess)
+    return 0;
+  return (H / 16) * (784 / 112) <= cus * per ? 1 : 0;
+}
+
+// phase 0: mlp2_fwd, 1: mlp2_bwd, 2: run-ahead mlp2_bwd (backward of t + forward of t+1)
 JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* stream) {
   const Mlp2Args& a = *args;
   if (k_in != 784 || c != 10 || a.H % 16 || a.M <= 0 || a.M > 128) return -3;
@@ -851,10 +1107,18 @@ JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* str
       else if (direct) hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 16, true, false>), g, dim3(NT), 0, st, a);
       else hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 16, false, false>), g, dim3(NT), 0, st, a);
     }
-  } else {
+  } else if (phase == 1) {
     const dim3 g(a.H / 16, 784 / 112);
     if (xcd_tiles_enabled()) hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true>), g, dim3(NT), 0, st, a);
     else hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, false>), g, dim3(NT), 0, st, a);
+  } else {
+    // run-ahead backward: step t's backward + AdamW + step t+1's forward (needs the
+    // fused optimizer, the W1^T copy, the X copy written by mlp2_fwd and lg3 logits)
+    if (!a.fuse_opt || !a.W1T || !a.XR || !a.zslab || !a.ztick || !a.hand || !a.lg3 || a.det_logits || a.M > 128 ||
+        a.H % 128)
+      return -3;
+    const dim3 g(a.H / 16, 784 / 112);
+    hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true, true>), g, dim3(NT), 0, st, a);
   }
   return HIP_LAUNCH_CHECK();
 }

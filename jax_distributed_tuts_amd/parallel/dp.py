@@ -337,10 +337,26 @@ class DataParallelTrainer:
                 body()
             self.graph = ("one", g)
             self.multi = None
-            if steps_per_graph > 1:
-                # single GPU, whole-step fused engine: the S steps are ONE persistent
-                # launch (mlp2_loop_kernel, grid barriers instead of kernel boundaries)
-                loop = self.world == 1 and getattr(self.fused, "loop_ok", False)
+            self._ahead = None
+            # single GPU, whole-step fused engine: the S steps are ONE persistent launch
+            # (opt-in mlp2_loop_kernel, grid barriers instead of kernel boundaries) or,
+            # by default, one run-ahead launch per step (step t's backward + AdamW +
+            # step t+1's forward).  Run-ahead graphs come in two variants: "cold" starts
+            # with step t's forward, "primed" does not -- after a run-ahead launch the
+            # forward of the next step is already done (FusedMLP2.ahead_primed).
+            loop = self.world == 1 and getattr(self.fused, "loop_ok", False)
+            ahead = self.world == 1 and not loop and getattr(self.fused, "ahead_ok", False)
+            if ahead:
+                self._ahead = {}
+                for S in sorted({1, steps_per_graph}):
+                    for primed in (False, True):
+                        ga = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(ga, pool=g.pool()):
+                            self.fused.run_ahead(batch, S, prologue=not primed)
+                        self._ahead[(S, primed)] = ga
+                if steps_per_graph > 1:
+                    self.multi = (steps_per_graph, self._ahead[(steps_per_graph, False)])
+            elif steps_per_graph > 1:
                 gm = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gm, pool=g.pool()):
                     if not (loop and self.fused.run_loop(batch, steps_per_graph)):
@@ -421,15 +437,24 @@ class DataParallelTrainer:
             S, gm = multi
             for _ in range(n // S):
                 with replay_scope("train_step_dp", S):
-                    gm.replay()
+                    self._ahead_graph(S).replay() if self._ahead else gm.replay()
+                    if self._ahead:
+                        self.fused.ahead_primed = True
             self.state.step += (n // S) * S
             n = n % S
         for _ in range(n):
             self.step(batch)
 
+    def _ahead_graph(self, S: int):
+        return self._ahead[(S, bool(self.fused.ahead_primed))]
+
     def _replay(self):
         kind = self.graph[0]
-        if kind == "one":
+        if kind == "one" and getattr(self, "_ahead", None):
+            with replay_scope("train_step_dp"):
+                self._ahead_graph(1).replay()
+                self.fused.ahead_primed = True
+        elif kind == "one":
             with replay_scope("train_step_dp"):
                 self.graph[1].replay()
         else:

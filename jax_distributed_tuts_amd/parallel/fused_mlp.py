@@ -38,11 +38,13 @@ class Mlp2Args(ctypes.Structure):
                 ("gscale", c_float), ("running", c_void_p), ("stamps", c_void_p),
                 ("W1T", c_void_p), ("ldw1t", c_int), ("XT", c_void_p), ("ldxt", c_int),
                 ("step_copy", c_void_p), ("W2snap", c_void_p), ("stage_stride", ctypes.c_long),
-                ("det_logits", c_void_p)]
+                ("det_logits", c_void_p),
+                ("XR", c_void_p), ("zslab", c_void_p), ("ztick", c_void_p), ("hand", c_void_p), ("lg3", c_int)]
 
 
 _lib.declare("jdt_mlp2", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_int, c_void_p])
 _lib.declare("jdt_mlp2_args_size", c_int, [])
+_lib.declare("jdt_mlp2_ahead_ok", c_int, [c_int, c_int])
 _lib.declare("jdt_mlp2_set_rows", None, [c_int])
 _lib.declare("jdt_mlp2_loop", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_void_p, c_void_p, c_void_p, ctypes.c_longlong,
                                       c_void_p, c_void_p])
@@ -98,7 +100,10 @@ class FusedMLP2:
         self.G1 = torch.zeros((rows + 31) // 32 * 32 * H, dtype=torch.float32, device=dev)
         # H = dropout(silu(Z1)) bf16, same 4-row group layout as G1
         self.H1 = torch.zeros((rows + 31) // 32 * 32 * H, dtype=torch.bfloat16, device=dev)
-        self.logits = torch.zeros(2, rows, 10, dtype=torch.float32, device=dev)
+        # logits accumulators: [0:2] by step parity (two launches per step), [2:5] by
+        # step % 3 (run-ahead steps); run_ahead zeroes all five first
+        self.logits_all = torch.zeros(5, rows, 10, dtype=torch.float32, device=dev)
+        self.logits = self.logits_all[:2]
         self.step_copy = torch.zeros(1, dtype=torch.int32, device=dev)  # mlp2_fwd -> mlp2_bwd
         # second parity buffer of W2's bf16 shadow (single-GPU fused-optimizer mode)
         self.W2s1 = P.s("output_dense/kernel").clone()
@@ -136,6 +141,26 @@ class FusedMLP2:
         # deterministic mode: per-column-block partial logits instead of fp32 atomics
         self.det_logits = (torch.zeros(H // 16, rows, 10, dtype=torch.float32, device=dev)
                            if deterministic() else None)
+        # run-ahead steps (one launch per step: step t's backward + AdamW + step t+1's
+        # forward, csrc/mlp_fused.hip mlp2_bwd AHEAD); single GPU, fused AdamW only.
+        # JDT_MLP2_AHEAD=0 turns it off (A/B)
+        self.ahead_ok = (self.fuse_opt and self.det_logits is None and self.W1T is not None
+                         and os.environ.get("JDT_MLP2_AHEAD", "1") == "1"
+                         and bool(_lib.lib().jdt_mlp2_ahead_ok(rows, H)))
+        self._ahead_args = None
+        # host-side: the last launch on this engine was a run-ahead backward (set by
+        # run_ahead / DataParallelTrainer after replaying a run-ahead graph)
+        self.ahead_primed = False
+        if self.ahead_ok:
+            nch = 784 // 112
+            self.XR = torch.zeros(rows, 784, dtype=torch.bfloat16, device=dev)
+            self.zslab = torch.zeros(H // 16 * nch * 128 * 16, dtype=torch.float32, device=dev)
+            # 128-byte lines: [step ticket, error word (1: tile map, 2: barrier timeout),
+            # launch counter], one column-barrier counter line per hidden block, one
+            # per-tile launch counter line per XCD (csrc/mlp_fused.hip Mlp2Args.ztick)
+            tpx = H // 16 * nch // 8
+            self.ztick = torch.zeros(32 * (1 + H // 16) + 8 * 32 * ((tpx + 31) // 32), dtype=torch.int32, device=dev)
+            self.hand = torch.zeros(H + H * 10 + 10, dtype=torch.float32, device=dev)
 
     def set_grad_stage(self, base: int, stride: int):
         """Mode 0: write the gradient bucket into the xGMI staging buffer at ``base``
@@ -197,6 +222,8 @@ class FusedMLP2:
         return a
 
     def forward_backward(self, batch):
+        if not torch.cuda.is_current_stream_capturing():
+            self.ahead_primed = False   # the run-ahead buffers no longer hold the next forward
         key = (batch.inputs.data_ptr(), batch.labels.data_ptr(), self.state.rng)
         if self._args is None or self._key != key:
             self._args, self._key = self._build_args(batch), key
@@ -204,6 +231,37 @@ class FusedMLP2:
         s = _lib.stream_ptr()
         _lib.check(L.jdt_mlp2(ctypes.byref(self._args), 0, 784, 10, s), "mlp2_fwd")
         _lib.check(L.jdt_mlp2(ctypes.byref(self._args), 1, 784, 10, s), "mlp2_bwd")
+
+    def run_ahead(self, batch, n: int, prologue: bool = True):
+        """n complete training steps as n run-ahead backward launches, launch i = step
+        i's CE, backward and AdamW plus step i+1's forward; ``prologue`` first runs the
+        first step's forward (``mlp2_fwd``), needed unless the previous launch on this
+        engine was a run-ahead backward (``ahead_primed``: step t's G1, H1 and logits
+        (t % 3) are then already there).  Same maths as n two-launch steps except the
+        fp32 summation order of Z1 (7 input-chunk partials instead of 8 wave
+        partials)."""
+        assert self.ahead_ok
+        key = (batch.inputs.data_ptr(), batch.labels.data_ptr(), self.state.rng)
+        if self._args is None or self._key != key:
+            self._args, self._key = self._build_args(batch), key
+            self._ahead_args = None
+        if self._ahead_args is None:
+            b = Mlp2Args.from_buffer_copy(self._args)
+            b.logits = self.logits_all[2:].data_ptr()
+            b.lg3 = 1
+            b.XR, b.zslab, b.ztick, b.hand = (t.data_ptr() for t in (self.XR, self.zslab, self.ztick, self.hand))
+            self._ahead_args = b
+        L = _lib.lib()
+        s = _lib.stream_ptr()
+        if prologue:
+            self.logits_all.zero_()
+            _lib.check(L.jdt_mlp2(ctypes.byref(self._ahead_args), 0, 784, 10, s), "mlp2_fwd")
+        elif not torch.cuda.is_current_stream_capturing():
+            assert self.ahead_primed, "run_ahead(prologue=False) needs a run-ahead launch just before"
+        for _ in range(n):
+            _lib.check(L.jdt_mlp2(ctypes.byref(self._ahead_args), 2, 784, 10, s), "mlp2_bwd_ahead")
+        if not torch.cuda.is_current_stream_capturing():
+            self.ahead_primed = True
 
     def run_loop(self, batch, n: int, stamps: Optional[torch.Tensor] = None) -> bool:
         """n complete steps (forward, backward, AdamW) in ONE persistent launch.
@@ -242,6 +300,9 @@ class FusedMLP2:
         W1's (mlp2_bwd keeps only the K-contiguous W1^T copy current)."""
         if self.loop_error():
             raise RuntimeError("mlp2_loop_kernel: a grid barrier timed out (not every workgroup was resident)")
+        if self.ahead_ok and int(self.ztick[1].item()) != 0:
+            raise RuntimeError("mlp2_bwd run-ahead: tile map or column barrier failed (error word "
+                               f"{int(self.ztick[1].item())}); results invalid")
         P = self.state.params
         if self.fuse_opt and int(self.state.opt_state["count"].item()) % 2 == 1:
             P.s("output_dense/kernel").copy_(self.W2s1)

@@ -634,6 +634,62 @@ def test_mlp2_loop_kernel_matches_two_launch(rows, monkeypatch):
     assert float(sd.max()) <= 1e-2
 
 
+@pytest.mark.parametrize("rows", [128, 64, 32])
+def test_mlp2_run_ahead_matches_two_launch(rows, monkeypatch):
+    """One launch per step (step t's backward + AdamW + step t+1's forward, XCD-local
+    column barriers) == two launches per step, through the multi-step graphs (cold
+    with the prologue forward, then primed without it), 1-step primed graphs, and
+    eager run-ahead launches mixed with two-launch steps (logits accumulators, step
+    and launch counters stay consistent).  The run-ahead's Z1 sums 7 input-chunk
+    partials instead of 8 wave partials, so agreement is to fp32 rounding."""
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    g = torch.Generator().manual_seed(1)
+    b = Batch(torch.randn(rows, 784, generator=g).to(DEV),
+              torch.randint(0, 10, (rows,), generator=g).to(torch.int32).to(DEV))
+    res = {}
+    for ahead in ("0", "1"):
+        monkeypatch.setenv("JDT_MLP2_AHEAD", ahead)
+        st = init_dp(Classifier(), adamw(1e-3), 69, DEV)
+        tr = DataParallelTrainer(st, None, DPConfig(4, "kernel"))
+        tr.step(b)
+        eng = tr.fused
+        assert eng.ahead_ok == (ahead == "1")
+        tr.capture(b, steps_per_graph=7)
+        tr.run_steps(b, 14)          # cold 7-step graph, then the primed one
+        tr.step(b)
+        tr.step(b)                   # 1-step primed graphs
+        eng.forward_backward(b)      # two launches: clears the primed state
+        if ahead == "1":
+            assert not eng.ahead_primed
+            eng.run_ahead(b, 3)
+            eng.run_ahead(b, 2, prologue=False)
+        else:
+            for _ in range(5):
+                eng.forward_backward(b)
+        eng.forward_backward(b)
+        tr.finalize()
+        torch.cuda.synchronize()
+        res[ahead] = (st.params.master.clone(), tr.metrics.clone(), int(st.opt_state["count"].item()),
+                      st.params.shadow.clone())
+        if ahead == "1":
+            zt = eng.ztick.cpu()
+            nb = 512 // 16
+            n = 7 + 7 + 1 + 1 + 3 + 2   # run-ahead launches
+            assert int(zt[0]) == 0 and int(zt[1]) == 0 and int(zt[2]) == n   # ticket re-armed, no error, launches
+            assert bool((zt[32:32 * (1 + nb)].view(nb, 32)[:, 0] == 7 * n).all())   # column barriers: 7 per launch
+            tiles = zt[32 * (1 + nb):].view(8, 32)[:, :28]
+            assert bool((tiles == n).all())   # every tile ran exactly once per launch
+    assert res["0"][2] == res["1"][2] == 24
+    d = (res["0"][0] - res["1"][0]).abs()
+    assert float(d.max()) <= 3e-3 and float((d > 1e-5).float().mean()) < 1e-2
+    _close(res["1"][1], res["0"][1], rtol=1e-3, atol=5e-2)
+    sd = (res["0"][3].float() - res["1"][3].float()).abs()
+    assert float(sd.max()) <= 1e-2
+
+
 @pytest.mark.parametrize("layers", [2, 4])
 def test_fsdp_fused_kernels_match_generic(layers):
     """FSDP (world 1) with the fused classifier kernels on the gathered buffer ==

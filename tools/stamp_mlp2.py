@@ -27,7 +27,7 @@ NAMES = {0: ["start", "loads+LDS staged", "MFMA+reduce", "epilogue(Z1,H1)", "log
 
 
 def report(kind, st, nwg):
-    raw = st[: nwg * 8].view(nwg, 8).double()
+    raw = st[: nwg * 16].view(nwg, 16).double()
     clk = (raw[:, 6] - raw[:, 5]) / (raw[:, 4] - raw[:, 0]) * 100.0  # MHz
     print(f"    shader clock during the kernel: median {float(clk.median()):.0f} MHz "
           f"(min {float(clk.min()):.0f}, max {float(clk.max()):.0f})")
@@ -66,8 +66,8 @@ def main():
         tr.step(b)
     eng = tr.fused
     L = _lib.lib()
-    sa = torch.zeros(4096 * 8, dtype=torch.int64, device=dev)
-    sb = torch.zeros(4096 * 8, dtype=torch.int64, device=dev)
+    sa = torch.zeros(4096 * 16, dtype=torch.int64, device=dev)
+    sb = torch.zeros(4096 * 16, dtype=torch.int64, device=dev)
     T = type(eng._args)
     args0, args1 = T(), T()
     ctypes.memmove(ctypes.byref(args0), ctypes.byref(eng._args), ctypes.sizeof(T))
@@ -84,9 +84,30 @@ def main():
     report(0, sa.cpu(), nf)
     report(1, sb.cpu(), (H // 16) * 7)
     # inter-kernel gap: last fwd end -> first bwd start
-    fa = sa.cpu()[: nf * 8].view(-1, 8)
-    fb = sb.cpu()[: (H // 16) * 7 * 8].view(-1, 8)
+    fa = sa.cpu()[: nf * 16].view(-1, 16)
+    fb = sb.cpu()[: (H // 16) * 7 * 16].view(-1, 16)
     print(f"fwd last end -> bwd first start: {float(fb[:, 0].min() - fa[:, 4].max()) * 10e-3:.2f} us")
+    if getattr(eng, "ahead_ok", False):
+        # run-ahead backward: same phases plus the next step's forward (slots 8-11)
+        eng.run_ahead(b, 1)
+        ah = type(eng._ahead_args)()
+        ctypes.memmove(ctypes.byref(ah), ctypes.byref(eng._ahead_args), ctypes.sizeof(T))
+        sc = torch.zeros(4096 * 16, dtype=torch.int64, device=dev)
+        ah.stamps = sc.data_ptr()
+        for _ in range(a.iters):
+            _lib.check(L.jdt_mlp2(ctypes.byref(ah), 2, 784, 10, s), "bwd_ahead")
+        torch.cuda.synchronize()
+        n = (H // 16) * 7
+        report(1, sc.cpu(), n)
+        st_ = sc.cpu()[: n * 16].view(n, 16).double() * 10e-3
+        t0 = st_[:, 0]
+        print("--- run-ahead phases (us from each workgroup's start: median / max over workgroups)")
+        for i, nm in ((3, "dW1+AdamW done"), (8, "Z1 partial stored (vmcnt 0)"), (9, "column barrier passed"),
+                      (10, "partials + hand-offs loaded"), (11, "epilogue share (G1/H1, H tile)"),
+                      (4, "logit atomics issued, end")):
+            d = st_[:, i] - t0
+            print(f"  {nm:32s} {float(d.median()):6.2f}  max {float(d.max()):6.2f}")
+        print(f"  span first start -> last end: {float(st_[:, 4].max() - t0.min()):.2f} us")
 
 
 if __name__ == "__main__":

@@ -268,6 +268,12 @@ def main():
     sps = args.steps / dt
     if args.strategy == "dp":
         desc["accum"] = tr.cfg.accum  # the path that actually ran (CPU falls back from "kernel")
+        # 1-GPU fused step: one run-ahead launch per step (step t's backward + AdamW + step
+        # t+1's forward) or the two-launch forward / backward pair
+        if getattr(tr, "_ahead", None):
+            desc["step_launches"] = "1 (run-ahead mlp2_bwd)"
+        elif getattr(tr, "fused", None) is not None:
+            desc["step_launches"] = "2 (mlp2_fwd + mlp2_bwd)" + (" + xGMI all-reduce/AdamW" if ws > 1 else "")
     if args.strategy == "pp":
         desc["single_stage_mode"] = tr.single_stage_mode  # how a 1-stage pipeline ran its microbatches
     if D.rank() == 0:

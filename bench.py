@@ -274,6 +274,8 @@ def main():
             desc["step_launches"] = "1 (run-ahead mlp2_bwd)"
         elif getattr(tr, "fused", None) is not None:
             desc["step_launches"] = "2 (mlp2_fwd + mlp2_bwd)" + (" + xGMI all-reduce/AdamW" if ws > 1 else "")
+    if args.strategy == "fsdp" and getattr(tr, "_ahead", None):
+        desc["step_launches"] = "1 (run-ahead mlp2_bwd)"
     if args.strategy == "pp":
         desc["single_stage_mode"] = tr.single_stage_mode  # how a 1-stage pipeline ran its microbatches
     if D.rank() == 0:

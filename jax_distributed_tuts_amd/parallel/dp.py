@@ -90,6 +90,7 @@ class DataParallelTrainer:
         self.metrics = torch.zeros(N_METRIC_SLOTS, dtype=torch.float32, device=P.master.device)
         self.world = C.axis_size(mesh, cfg.axis)
         self.graph = None
+        self._ahead = None
         self._static = None
         self.fused = None
         self._capturing = False
@@ -119,6 +120,7 @@ class DataParallelTrainer:
         self.fused = None
         self._stage = None
         self.graph = None
+        self._ahead = None
         self.multi = None
         self._scan = None
         self._capturing = False
@@ -347,15 +349,11 @@ class DataParallelTrainer:
             loop = self.world == 1 and getattr(self.fused, "loop_ok", False)
             ahead = self.world == 1 and not loop and getattr(self.fused, "ahead_ok", False)
             if ahead:
-                self._ahead = {}
-                for S in sorted({1, steps_per_graph}):
-                    for primed in (False, True):
-                        ga = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(ga, pool=g.pool()):
-                            self.fused.run_ahead(batch, S, prologue=not primed)
-                        self._ahead[(S, primed)] = ga
+                from .fused_mlp import AheadGraphs
+
+                self._ahead = AheadGraphs(self.fused, batch, steps_per_graph, pool=g.pool())
                 if steps_per_graph > 1:
-                    self.multi = (steps_per_graph, self._ahead[(steps_per_graph, False)])
+                    self.multi = (steps_per_graph, self._ahead.graph(steps_per_graph))
             elif steps_per_graph > 1:
                 gm = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gm, pool=g.pool()):
@@ -437,23 +435,17 @@ class DataParallelTrainer:
             S, gm = multi
             for _ in range(n // S):
                 with replay_scope("train_step_dp", S):
-                    self._ahead_graph(S).replay() if self._ahead else gm.replay()
-                    if self._ahead:
-                        self.fused.ahead_primed = True
+                    self._ahead.replay(S) if self._ahead else gm.replay()
             self.state.step += (n // S) * S
             n = n % S
         for _ in range(n):
             self.step(batch)
 
-    def _ahead_graph(self, S: int):
-        return self._ahead[(S, bool(self.fused.ahead_primed))]
-
     def _replay(self):
         kind = self.graph[0]
         if kind == "one" and getattr(self, "_ahead", None):
             with replay_scope("train_step_dp"):
-                self._ahead_graph(1).replay()
-                self.fused.ahead_primed = True
+                self._ahead.replay(1)
         elif kind == "one":
             with replay_scope("train_step_dp"):
                 self.graph[1].replay()

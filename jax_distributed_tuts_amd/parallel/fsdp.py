@@ -385,6 +385,7 @@ class FSDPTrainer:
         self.world = C.axis_size(mesh, cfg.axis)
         self.fused = None
         self.graph = None
+        self._ahead = None
         self.multi = None
         if self.world > 1 and self.sp.local.master.is_cuda and self.sp.xg is None:
             from ..comm.xgmi import create_for
@@ -400,6 +401,7 @@ class FSDPTrainer:
         """After a checkpoint restore: drop the fused engine and captured graphs."""
         self.fused = None
         self.graph = None
+        self._ahead = None
         self.multi = None
 
     @property
@@ -462,7 +464,7 @@ class FSDPTrainer:
         """train_step_fsdp (param_sharding.py:343-367)."""
         if self.graph is not None:
             with replay_scope("train_step_fsdp"):
-                self.graph.replay()
+                self._ahead.replay(1) if self._ahead else self.graph.replay()
         else:
             self._body(batch)
         self.state.step += 1
@@ -482,7 +484,17 @@ class FSDPTrainer:
         with torch.cuda.graph(g):
             self._body(batch)
         self.graph = g
-        if steps_per_graph > 1:
+        # N = 1 on the fused engine with AdamW in its epilogue: one run-ahead launch per
+        # step (the DP engine's schedule, fused_mlp.AheadGraphs)
+        eng = self.fused
+        self._ahead = None
+        if self.world == 1 and eng is not None and getattr(eng, "ahead_ok", False):
+            from .fused_mlp import AheadGraphs
+
+            self._ahead = AheadGraphs(eng, batch, steps_per_graph, pool=g.pool())
+            if steps_per_graph > 1:
+                self.multi = (steps_per_graph, self._ahead.graph(steps_per_graph))
+        elif steps_per_graph > 1:
             gm = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gm, pool=g.pool()):
                 for _ in range(steps_per_graph):
@@ -494,7 +506,7 @@ class FSDPTrainer:
             S, gm = self.multi
             for _ in range(n // S):
                 with replay_scope("train_step_fsdp", S):
-                    gm.replay()
+                    self._ahead.replay(S) if self._ahead else gm.replay()
             self.state.step += (n // S) * S
             n %= S
         for _ in range(n):

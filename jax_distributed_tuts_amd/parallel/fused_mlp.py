@@ -310,6 +310,31 @@ class FusedMLP2:
             P.s("input_dense/kernel").copy_(self.W1T[:, :784].t())
 
 
+class AheadGraphs:
+    """hipGraphs of run-ahead steps for a single-GPU FusedMLP2 engine (DP and FSDP at
+    N = 1): for S in {1, steps_per_graph}, a "cold" graph (step t's forward first)
+    and a "primed" one (no forward: the previous replay's last launch already ran
+    it).  ``replay(S)`` picks the variant from the engine's host-side state."""
+
+    def __init__(self, eng: "FusedMLP2", batch, steps_per_graph: int, pool=None):
+        self.eng = eng
+        self.graphs = {}
+        for S in sorted({1, int(steps_per_graph)}):
+            for primed in (False, True):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    eng.run_ahead(batch, S, prologue=not primed)
+                self.graphs[(S, primed)] = g
+                pool = g.pool() if pool is None else pool
+
+    def graph(self, S: int, primed: bool = False):
+        return self.graphs[(S, primed)]
+
+    def replay(self, S: int):
+        self.graphs[(S, bool(self.eng.ahead_primed))].replay()
+        self.eng.ahead_primed = True
+
+
 # ----------------------------------------------------------------------------- deep MLPs (csrc/mlp_deep.hip)
 class MdArgs(ctypes.Structure):
     """Mirror of ``jdt::MdArgs`` (field order and types must match)."""

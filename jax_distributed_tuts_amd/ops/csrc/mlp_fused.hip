@@ -607,7 +607,9 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   bf16x8 xa[AHEAD ? 4 : 1];
   u32x4 dbn = {0u, 0u, 0u, 0u};
   const int g_lo = (by * (MPM / 4)) / NCH, g_hi = ((by + 1) * (MPM / 4)) / NCH;
-  const int eg = g_lo + (tid >> 4);   // phase 6: this thread's row group (tid < 16 * (g_hi - g_lo))
+  // phase 6: this thread's element -- row group eg, row eg*4 + ee, column j0 + gn
+  // (tid < 64 * (g_hi - g_lo): one element per thread spreads the epilogue over 5 waves)
+  const int eg = g_lo + (tid >> 6), ee = (tid >> 4) & 3;
   if constexpr (AHEAD) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
@@ -857,12 +859,12 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     const __amdgpu_buffer_rsrc_t zr = __builtin_amdgcn_make_buffer_rsrc(zb, (short)0, NCH * (MPM / 4) * 64 * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t hr =
         __builtin_amdgcn_make_buffer_rsrc(a.hand, (short)0, (int)((H + H * C + C) * 4), 0x00020000);
-    float4 zp[NCH];
+    float zp[NCH];
     const int egc = min(eg, g_hi - 1);
 #pragma unroll
     for (int q = 0; q < NCH; ++q)
-      zp[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             zr, (int)((((long)q * (MPM / 4) + egc) * 64 + gn * 4) * 4), 0, 16));
+      zp[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                            zr, (int)((((long)q * (MPM / 4) + egc) * 64 + gn * 4 + ee) * 4), 0, 16));
     const float b1v = round_bf(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(hr, (j0 + gn) * 4, 0, 16)));
     if (tid < 16 * C)
       w2A[tid / C][tid % C] =
@@ -875,41 +877,31 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       STAMP(10);
     }
-    if (tid < 16 * ng) {
-      float gf[4];
-      unsigned long long hpk = 0ull;
+    if (tid < 64 * ng) {
+      const int row = eg * 4 + ee;
+      float hvn = 0.f;
+      if (row < M) {
+        float v = b1v;   // + the NCH chunk partials in chunk order
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = eg * 4 + e;
-        float hvn = 0.f;
-        gf[e] = 0.f;
-        if (row < M) {
-          float v = b1v;   // + the NCH chunk partials in chunk order
-#pragma unroll
-          for (int q = 0; q < NCH; ++q) v += e == 0 ? zp[q].x : e == 1 ? zp[q].y : e == 2 ? zp[q].z : zp[q].w;
-          const float zz = bf2f(f2bf(v));           // Z1 as the bf16 Dense output
-          const float ez = __expf(-zz);
-          hvn = zz / (1.0f + ez);                    // act_fwd(ACT_SILU)
-          const float sg = 1.0f / (1.0f + ez);
-          float gd = sg * (1.0f + zz * (1.0f - sg));  // act_grad(ACT_SILU)
-          if (a.keep < 1.f) {
-            const bool kp = keep_word(dbn, e, a.keep);
-            hvn = kp ? hvn / a.keep : 0.f;
-            gd = kp ? gd / a.keep : 0.f;
-          }
-          gf[e] = gd;
-          const bf16_t hb = f2bf(hvn);
-          hpk |= (unsigned long long)hb << (16 * e);
-          hvn = bf2f(hb);
+        for (int q = 0; q < NCH; ++q) v += zp[q];
+        const float zz = bf2f(f2bf(v));           // Z1 as the bf16 Dense output
+        const float ez = __expf(-zz);
+        hvn = zz / (1.0f + ez);                    // act_fwd(ACT_SILU)
+        const float sg = 1.0f / (1.0f + ez);
+        float gd = sg * (1.0f + zz * (1.0f - sg));  // act_grad(ACT_SILU)
+        if (a.keep < 1.f) {
+          const bool kp = keep_word(dbn, ee, a.keep);
+          hvn = kp ? hvn / a.keep : 0.f;
+          gd = kp ? gd / a.keep : 0.f;
         }
-        htA[(tid >> 4) * 4 + e][gn] = hvn;
+        const bf16_t hb = f2bf(hvn);
+        hvn = bf2f(hb);
+        // G1 / H1 element (row group eg, column j0+gn, slot ee) of the dropout-group layout
+        const long gq = ((long)eg * H + j0 + gn) * 4 + ee;
+        a.G1[gq] = gd;
+        a.H1[gq] = hb;
       }
-      if (eg * 4 < M) {
-        const long gq = ((long)eg * H + j0 + gn) * 4;
-        *reinterpret_cast<u32x4*>(a.G1 + gq) =
-            (u32x4){__float_as_uint(gf[0]), __float_as_uint(gf[1]), __float_as_uint(gf[2]), __float_as_uint(gf[3])};
-        *reinterpret_cast<unsigned long long*>(a.H1 + gq) = hpk;
-      }
+      htA[(tid >> 6) * 4 + ee][gn] = hvn;
     }
     __syncthreads();
     STAMP(11);

@@ -2,7 +2,9 @@
 
 One DP step = ``mlp2_fwd`` + ``mlp2_bwd`` (+ RCCL all-reduce + fused AdamW when
 N > 1).  On one GPU the optimizer runs inside ``mlp2_bwd``'s epilogue, so a
-step is two kernel launches.  Mathematically identical to the reference's
+step is two kernel launches -- or, in captured multi-step graphs, ONE: the
+run-ahead ``mlp2_bwd`` (``run_ahead`` / ``AheadGraphs``) also computes the next
+step's forward from the W1 tiles its AdamW epilogue just produced.  Mathematically identical to the reference's
 4-minibatch accumulation loop: each row's loss is weighted 1/(rows per
 minibatch) and the summed gradient is scaled by 1/n_minibatches (and 1/N after
 the SUM all-reduce); dropout draws one Philox stream per (step, row, unit).

@@ -716,6 +716,34 @@ def test_fsdp_fused_kernels_match_generic(layers):
     _close(res[1][1], res[0][1], rtol=1e-3, atol=2e-2)
 
 
+def test_fsdp_run_ahead_matches_two_launch(monkeypatch):
+    """FSDP at N = 1 (the DP engine on whole-leaf shards) through captured graphs:
+    run-ahead (one launch per step) == two launches per step, to fp32 rounding."""
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    g = torch.Generator().manual_seed(2)
+    b = Batch(torch.randn(128, 784, generator=g).to(DEV), torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV))
+    res = {}
+    for ahead in ("0", "1"):
+        monkeypatch.setenv("JDT_MLP2_AHEAD", ahead)
+        st = init_fsdp(Classifier(), adamw(1e-4), 6969, DEV, None, "data", 16)
+        tr = FSDPTrainer(st, None, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=True))
+        tr.step(b)
+        tr.capture(b, steps_per_graph=5)
+        assert (tr._ahead is not None) == (ahead == "1")
+        tr.run_steps(b, 10)
+        tr.step(b)
+        tr.finalize() if hasattr(tr, "finalize") else tr.fused.finalize()
+        torch.cuda.synchronize()
+        res[ahead] = (st.params.master.clone(), tr.metrics.clone(), int(st.opt_state["count"].item()))
+    assert res["0"][2] == res["1"][2] == 12
+    d = (res["0"][0] - res["1"][0]).abs()
+    assert float(d.max()) <= 3e-3 and float((d > 1e-5).float().mean()) < 1e-2
+    _close(res["1"][1], res["0"][1], rtol=1e-3, atol=5e-2)
+
+
 @pytest.mark.parametrize("B,S,H", [(2, 128, 8), (1, 96, 2), (2, 200, 4), (1, 64, 1)])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attention_fwd_bwd(B, S, H, causal):

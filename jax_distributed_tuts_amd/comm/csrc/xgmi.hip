@@ -269,6 +269,83 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
 }
 
 // ---------------------------------------------------------------------------
+// One-shot all-reduce for small messages (<= g_oneshot_bytes, 256 KiB by default,
+// SURVEY 5.8 (b)): block b stages chunk b of the WHOLE input, one barrier, then
+// reads chunk b from every peer (all W loads in flight) and sums in rank order --
+// the same order as the two-shot kernel, so results are bit-identical -- one
+// synchronisation point instead of two and no second (gather) pass, which is the
+// cost that matters at latency-bound sizes.  Same double-buffered data halves,
+// epochs and per-block discipline as xg_kernel (a block only writes and reads
+// chunk b of a call; kernels of one stream do not overlap), fused AdamW + metrics.
+template <int W>
+__global__ void __launch_bounds__(XG_THREADS) xg_oneshot_kernel(XgPeers P, int rank, long cap, const float* in,
+                                                                float* out, long n, long chunk, XgAdam A, int fuse,
+                                                                long long timeout) {
+  __shared__ unsigned s_epoch;
+  const int b = blockIdx.x;
+  XgSignal* me = P.sig[rank];
+  if (threadIdx.x == 0) s_epoch = me->epoch[b] + 1u;
+  __syncthreads();
+  const unsigned epoch = s_epoch;
+  const long half = (long)(epoch & 1u) * cap;
+  const long base = (long)b * chunk;
+  const int nv = (int)(chunk >> 2);
+  const unsigned long long bytes = (unsigned long long)cap * 2ull * sizeof(float);
+  __amdgpu_buffer_rsrc_t rdata[W];
+#pragma unroll
+  for (int q = 0; q < W; ++q) rdata[q] = sys_rsrc(P.data[q], bytes);
+  const __amdgpu_buffer_rsrc_t my_data = sys_rsrc(P.data[rank], bytes);
+  for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
+    const long j = base + 4 * i;
+    const float4 x = j < n ? load_guard(in, j, n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    sys_store4(my_data, half + j, x);
+  }
+  xg_barrier(P, rank, W, 0, epoch, timeout);
+  float rbc1 = 1.f, rbc2 = 1.f;
+  if (fuse) {
+    const int t = A.step[0] + 1;
+    rbc1 = 1.f / (1.f - powf(A.b1, (float)t));
+    rbc2 = 1.f / (1.f - powf(A.b2, (float)t));
+  }
+  for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
+    const long j = base + 4 * i;
+    if (j >= n) break;
+    float4 v[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) v[q] = sys_load4(rdata[q], half + j);
+    float4 acc = v[0];
+#pragma unroll
+    for (int q = 1; q < W; ++q) acc = add4(acc, v[q]);
+    if (!fuse) {
+      store_guard(out, j, n, acc);
+    } else {
+      if (j < A.n_params) {
+        adam4(A, j, acc, rbc1, rbc2);
+      } else {
+        const float* rv = &acc.x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const long mj = j + k - A.n_params;
+          if (mj < A.n_metrics && j + k < n) A.running[mj] += rv[k];
+        }
+      }
+      if (A.zero) store_guard(A.zero, j, n, make_float4(0.f, 0.f, 0.f, 0.f));
+    }
+  }
+  if (threadIdx.x == 0) me->epoch[b] = epoch;
+  if (fuse && A.step) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned t = atomicAdd(A.ticket, 1u);
+      if (t == gridDim.x - 1) {
+        A.step[0] = A.step[0] + 1;
+        __hip_atomic_store(A.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Segmented all-gather / reduce-scatter: several tensors ("segments", e.g. the
 // dim-0-sharded leaves of an FSDP model) in ONE launch, each gathered straight
 // into / scattered straight out of its own full-tensor layout.  Rank q's part of
@@ -515,12 +592,53 @@ JDT_API int jdt_xgmi_open(void* ctx, const void* all_handles) {
   return 0;
 }
 
+static long g_oneshot_bytes = -1;   // all-reduces up to this size take the one-shot kernel
+static long oneshot_bytes() {
+  if (g_oneshot_bytes < 0) {
+    const char* e = getenv("JDT_XGMI_ONESHOT_BYTES");
+    g_oneshot_bytes = e ? atol(e) : 256L * 1024;
+  }
+  return g_oneshot_bytes;
+}
+JDT_API void jdt_xgmi_set_oneshot_bytes(long b) { g_oneshot_bytes = b; }
+
+static int xg_oneshot(XgCtx* c, const float* in, float* out, long n, const XgAdam* A, long long timeout,
+                      hipStream_t st) {
+  const long n4 = (n + 3) / 4 * 4;
+  long G, chunk;
+  xg_geometry(n4, &G, &chunk);
+  if (G * chunk > c->cap) return -3;
+  XgAdam a{};
+  int fuse = 0;
+  if (A) { a = *A; fuse = 1; }
+#define XG_CASE(w)                                                                                              \
+  case w:                                                                                                       \
+    hipLaunchKernelGGL((xg_oneshot_kernel<w>), dim3(G), dim3(XG_THREADS), 0, st, c->peers, c->rank, c->cap, in, \
+                       out, n, chunk, a, fuse, timeout);                                                        \
+    break;
+  switch (c->world) {
+    XG_CASE(2)
+    XG_CASE(3)
+    XG_CASE(4)
+    XG_CASE(5)
+    XG_CASE(6)
+    XG_CASE(7)
+    XG_CASE(8)
+    default:
+      return -4;
+  }
+#undef XG_CASE
+  return HIP_LAUNCH_CHECK();
+}
+
 JDT_API int jdt_xgmi_allreduce(void* ctx, const float* in, float* out, long n, const XgAdam* adam, long long timeout,
                                void* stream) {
   XgCtx* c = static_cast<XgCtx*>(ctx);
   if (!c->opened) return -5;
   if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) return -2;
   if (adam && ((adam->n_params & 3) || !adam->step || !adam->ticket)) return -2;
+  if (n > 0 && n * (long)sizeof(float) <= oneshot_bytes())
+    return xg_oneshot(c, in, out, n, adam, timeout, static_cast<hipStream_t>(stream));
   const long part = ((n + c->world - 1) / c->world + 3) / 4 * 4;
   return xg_launch<XG_ALLREDUCE>(c, in, out, n, part, adam, timeout, static_cast<hipStream_t>(stream));
 }

@@ -75,6 +75,7 @@ _lib.declare("jdt_xgmi_create", c_int, [c_int, c_int, c_long, ctypes.POINTER(c_v
 _lib.declare("jdt_xgmi_open", c_int, [c_void_p, c_void_p])
 _lib.declare("jdt_xgmi_allreduce", c_int, [c_void_p, c_void_p, c_void_p, c_long, ctypes.POINTER(XgAdam), c_longlong,
                                            c_void_p])
+_lib.declare("jdt_xgmi_set_oneshot_bytes", None, [c_long])
 _lib.declare("jdt_xgmi_reduce_scatter", c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_longlong, c_void_p])
 _lib.declare("jdt_xgmi_all_gather", c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_longlong, c_void_p])
 _lib.declare("jdt_xgmi_segments", c_int, [c_void_p, ctypes.POINTER(XgSegs), c_int, c_int, c_longlong, c_void_p])
@@ -177,6 +178,13 @@ class XgmiComm:
             raise ValueError("xgmi collectives take contiguous, 16-byte aligned fp32 CUDA tensors")
 
     # ------------------------------------------------------------------ collectives
+    @staticmethod
+    def set_oneshot_bytes(nbytes: int):
+        """All-reduces up to ``nbytes`` (default 256 KiB, env JDT_XGMI_ONESHOT_BYTES) run
+        the one-shot kernel (one barrier, every rank reads the whole vector from each
+        peer); larger ones the two-shot reduce-scatter + all-gather kernel."""
+        _lib.lib().jdt_xgmi_set_oneshot_bytes(int(nbytes))
+
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         self._check_f32(t)
         rc = _lib.lib().jdt_xgmi_allreduce(self.ctx, _ptr(t), _ptr(t), t.numel(), None, self.timeout,

@@ -39,6 +39,16 @@ def collectives(outdir):
         y = xs[r].to(dev)
         comm.all_reduce_(y)
         ar[n] = bool(torch.equal(y.cpu(), _seq_sum(xs)))
+    # small sizes take the one-shot kernel (<= 256 KiB); the same sizes forced through
+    # the two-shot kernel, interleaved with one-shot calls (shared epochs / parities)
+    for n in (1000, 50_000):
+        xs = [torch.randn(n, generator=torch.Generator().manual_seed(77 * q + n)) for q in range(W)]
+        for forced in (0, 256 * 1024, 0):
+            XgmiComm.set_oneshot_bytes(forced)
+            y = xs[r].to(dev)
+            comm.all_reduce_(y)
+            ar[f"{'2shot' if forced == 0 else '1shot'}_{n}_{len(ar)}"] = bool(torch.equal(y.cpu(), _seq_sum(xs)))
+    XgmiComm.set_oneshot_bytes(256 * 1024)
     res["ar"] = ar
     # fused all-reduce + AdamW + metrics fold == sum, then the standalone AdamW kernel
     npar, total = 4096, 4096 + 64

@@ -104,6 +104,10 @@ def main(args):
         if xg is not None:
             part = numel // n
             res["xgmi_all_reduce_us"] = _graph_time(lambda: xg.all_reduce_(x)) * 1e6
+            if b <= 256 * 1024:   # one-shot by default at this size: time the two-shot kernel too
+                xg.set_oneshot_bytes(0)
+                res["xgmi_all_reduce_2shot_us"] = _graph_time(lambda: xg.all_reduce_(x)) * 1e6
+                xg.set_oneshot_bytes(256 * 1024)
             res["xgmi_reduce_scatter_us"] = _graph_time(lambda: xg.reduce_scatter(x, z, part)) * 1e6
             res["xgmi_all_gather_us"] = _graph_time(lambda: xg.all_gather(z, x, part)) * 1e6
             res["xgmi_all_reduce_busbw_GBs"] = b * 2 * (n - 1) / n / (res["xgmi_all_reduce_us"] * 1e-6) / 1e9

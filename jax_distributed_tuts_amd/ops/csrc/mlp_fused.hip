@@ -249,13 +249,14 @@ __device__ __forceinline__ void mlp2_fwd_body(AT& a, const int bx, const int by,
   static_assert(RB == 16 || RB == 32, "row block");
   constexpr int KS = (K_IN + 31) / 32;  // 32-deep MFMA k-steps
   constexpr int KP = KS * 32;
-  constexpr int LDW = KP + 8;           // padded [n][k] row (bank spread)
   constexpr int WCH = (K_IN * 2 + NT - 1) / NT;  // 16-byte W1 chunks per thread
   constexpr int MAXT = (KS + NW - 1) / NW;       // k-steps per wave
   constexpr int XTC = 112;                       // X^T features written per hidden block
   constexpr int LDXS = K_IN + 8;                 // padded row of the X image (bf16)
   static_assert(K_IN % XTC == 0 && XTC % 8 == 0 && K_IN % 8 == 0, "X^T chunking");
-  __shared__ __attribute__((aligned(16))) bf16_t w1t[16 * LDW];
+  // !DIRECT: the W1 column block as loaded, a k-row image [KP][16] (32 bytes per row);
+  // B fragments come out of it with the gfx950 transposing ds_read_b64_tr_b16
+  __shared__ __attribute__((aligned(16))) bf16_t w1k[DIRECT ? 8 : KP * 16];
   __shared__ __attribute__((aligned(16))) bf16_t xs[RB * LDXS];
   __shared__ float part[NW][RB][17];
   __shared__ float htile[RB][17];
@@ -339,22 +340,15 @@ __device__ __forceinline__ void mlp2_fwd_body(AT& a, const int bx, const int by,
   u32x4 db = {0u, 0u, 0u, 0u};
   if (tid < (RB / 4) * 16 && a.keep < 1.f && rowg < M) db = dropout_bits(a.seed, doff, dropout_group(0, rowg, j0 + gc, M, H));
 
-  // ---- 2. (LDS path) W1 block -> LDS transposed (w1t[n][k]), zero the K padding
+  // ---- 2. (LDS path) W1 block -> LDS as loaded (k-row image w1k[k][16]), zero the K padding
   if constexpr (!DIRECT) {
 #pragma unroll
     for (int t = 0; t < WCH; ++t) {
       const int idx = tid + t * NT;
-      if (idx < K_IN * 2) {
-        const int k = idx >> 1, h = (idx & 1) * 8;
-        const unsigned q[4] = {wv[t].x, wv[t].y, wv[t].z, wv[t].w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          w1t[(h + 2 * e) * LDW + k] = (bf16_t)(q[e] & 0xffff);
-          w1t[(h + 2 * e + 1) * LDW + k] = (bf16_t)(q[e] >> 16);
-        }
-      }
+      if (idx < K_IN * 2) *reinterpret_cast<u32x4*>(&w1k[(idx >> 1) * 16 + (idx & 1) * 8]) = wv[t];
     }
-    for (int idx = tid; idx < 16 * (KP - K_IN); idx += NT) w1t[(idx / (KP - K_IN)) * LDW + K_IN + idx % (KP - K_IN)] = 0;
+    for (int idx = tid; idx < 2 * (KP - K_IN); idx += NT)
+      *reinterpret_cast<u32x4*>(&w1k[(K_IN + (idx >> 1)) * 16 + (idx & 1) * 8]) = (u32x4){0u, 0u, 0u, 0u};
   }
   if (tid < 16 * C) w2s[tid / C][tid % C] = bf2f(par ? w2b : w2a);
   if (tid < 16) b1sh[tid] = bf2f(b1b);
@@ -401,7 +395,23 @@ __device__ __forceinline__ void mlp2_fwd_body(AT& a, const int bx, const int by,
   for (int t = 0; t < MAXT; ++t) {
     if (ks0 + t < ks1) {
       const int k = (ks0 + t) * 32 + 8 * (lane >> 4);
-      const bf16x8 b = direct ? bg[t] : *reinterpret_cast<const bf16x8*>(&w1t[(lane & 15) * LDW + k]);
+      bf16x8 b;
+      if constexpr (DIRECT) {
+        b = bg[t];
+      } else {
+        // lane 4q+p of each 16-lane group addresses k-row k + q (then + 4 + q),
+        // columns 4p..4p+3; after the transposing read it holds column (lane & 15)
+        typedef __attribute__((ext_vector_type(4))) short s4;
+        const int i16 = lane & 15;
+        const unsigned a0 = (unsigned)(uintptr_t)(
+            (__attribute__((address_space(3))) const bf16_t*)(w1k + (k + (i16 >> 2)) * 16 + 4 * (i16 & 3)));
+        s4 lo, hi;
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:128" : "=v"(hi) : "v"(a0));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        b[0] = lo[0]; b[1] = lo[1]; b[2] = lo[2]; b[3] = lo[3];
+        b[4] = hi[0]; b[5] = hi[1]; b[6] = hi[2]; b[7] = hi[3];
+      }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         // K tail: W1^T / w1t are zero past K_IN, the X image row is clamped in bounds

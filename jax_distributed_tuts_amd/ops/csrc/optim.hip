@@ -71,7 +71,9 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, float
     if (zero_grad) g[i] = 0.f;
     if (shadow) shadow[i] = f2bf(pi);
   }
-  finish_ticket(step, ticket);
+  // ticket null: one range of a step split over several launches (the caller advances
+  // the step once every range has read it, OverlappedAdamW)
+  if (ticket) finish_ticket(step, ticket);
 }
 
 // SGD (+ optional heavy-ball momentum and decoupled weight decay)

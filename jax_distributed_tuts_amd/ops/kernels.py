@@ -85,6 +85,65 @@ class WGradStream:
             self.pending = False
 
 
+class OverlappedAdamW:
+    """AdamW applied layer by layer on a side stream while the backward pass
+    continues: an explicit backward reports parameters whose gradients are final
+    (``on_ready(names)``, output side first); each report forks AdamW over those
+    parameters' contiguous range of the flat buffers onto the side stream (no
+    step advance), ``finish()`` covers anything unreported, advances the device
+    step once (after every range has read it: one stream, in order) and makes the
+    caller's stream wait.  The bandwidth-bound optimizer pass then runs under the
+    lower layers' GEMMs instead of after them.  Inside hipGraph capture the
+    fork / join become graph branches."""
+
+    def __init__(self, P, tx, opt_state, grad_scale: float):
+        self.P, self.tx, self.o, self.scale = P, tx, opt_state, float(grad_scale)
+        self.s = torch.cuda.Stream(P.master.device)
+        self.done: set = set()
+        self.forked = False
+
+    def _range(self, names):
+        offs = [self.P.offsets[n] for n in names]
+        lo = min(o for o, _ in offs)
+        hi = max(o + _align4(int(np.prod(sh))) for o, sh in offs)
+        return lo, hi
+
+    def _launch(self, lo: int, hi: int):
+        P, tx, o = self.P, self.tx, self.o
+        adamw_step(P.master[lo:hi], P.grad[lo:hi], o["m"][lo:hi], o["v"][lo:hi],
+                   P.shadow[lo:hi] if P.shadow is not None else None, lr=tx.learning_rate, b1=tx.b1, b2=tx.b2,
+                   eps=tx.eps, wd=tx.weight_decay, grad_scale=self.scale, step=o["count"], ticket=None)
+
+    def ready(self, names):
+        names = [n for n in names if n in self.P.offsets and n not in self.done]
+        if not names:
+            return
+        ev = torch.cuda.Event()
+        ev.record()
+        self.s.wait_event(ev)
+        with torch.cuda.stream(self.s):
+            lo, hi = self._range(names)
+            self._launch(lo, hi)
+        self.done.update(names)
+        self.forked = True
+
+    def finish(self):
+        rest = [s.name for s in self.P.specs if s.name not in self.done]
+        if rest:
+            self.ready(rest)
+        with torch.cuda.stream(self.s):
+            self.o["count"].add_(1)
+        torch.cuda.current_stream().wait_stream(self.s)
+        self.done.clear()
+        self.forked = False
+
+
+def _align4(n: int) -> int:
+    from ..utils.flat import _align
+
+    return _align(n)
+
+
 def dw_gemm(wgrad: Optional["WGradStream"], h, dz, out, **kw):
     """``out += h^T dz`` (a_layout "km", b_layout "kn", fp32 accumulate), on the
     side stream when ``wgrad`` is given (GPU), inline otherwise."""
@@ -377,7 +436,8 @@ def adamw_step(p, g, m, v, shadow, *, lr, b1=0.9, b2=0.999, eps=1e-8, wd=1e-4, g
             g.zero_()
         if shadow is not None:
             shadow.copy_(p.to(shadow.dtype))
-        step.add_(1)
+        if ticket is not None:   # no ticket: one range of a split step, the caller advances it
+            step.add_(1)
         return
     rc = _lib.lib().jdt_adamw(_ptr(p), _ptr(g), _ptr(m), _ptr(v), _ptr(shadow), p.numel(), float(lr), float(b1),
                               float(b2), float(eps), float(wd), float(grad_scale), _ptr(step), _ptr(ticket),

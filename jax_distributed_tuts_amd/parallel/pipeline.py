@@ -97,6 +97,12 @@ class PipeConfig:
     # the loop's gradient (each row keeps its microbatch's 1/mb loss weight).  False:
     # per-microbatch passes, as on a real multi-stage pipeline.
     layer_major_single_stage: bool = True
+    # one GPU, one stage, AdamW: apply the optimizer layer by layer on a side stream
+    # as the backward finishes each layer's gradients (ops.kernels.OverlappedAdamW).
+    # Opt-in (env JDT_OVERLAP_OPT=1): measured SLOWER on the transformer step (1.39 vs
+    # 1.18 ms, profiles/r2_overlapped_adamw_ab.txt) -- the forked AdamW grids contend
+    # with the backward GEMMs for CUs instead of filling idle ones
+    overlap_optimizer: bool = True
 
 
 def _no_dropout(model) -> bool:
@@ -221,7 +227,9 @@ class GPipeTrainer:
             out, cache = self.model.forward(P, batch.inputs, train=True, seed=seed, offset=0, step=st.step_tensor)
             d = torch.empty_like(out)
             self.loss_head(out, batch.labels, d, n_parts=n_mb)
-            self.model.backward(P, cache, d, dout_is_dz=True, need_dx=False, wgrad=self.wgrad)
+            ov = self._overlapped_opt()
+            self.model.backward(P, cache, d, dout_is_dz=True, need_dx=False, wgrad=self.wgrad,
+                                on_ready=ov.ready if ov is not None else None)
             return
         eng = self._fused_stage(mb, seed)
         if eng is not None:
@@ -332,12 +340,30 @@ class GPipeTrainer:
             if not self.first:
                 self._send(dx, self.s - 1, n_mb + i)
 
+    def _overlapped_opt(self):
+        """The layer-by-layer side-stream AdamW (one GPU, one stage, no data axis)."""
+        if getattr(self, "_ov_opt", None) is None:
+            from ..utils.train_state import AdamW
+
+            st, cfg = self.state, self.cfg
+            ok = (cfg.overlap_optimizer and os.environ.get("JDT_OVERLAP_OPT", "0") == "1" and self.S == 1
+                  and self.n_dp == 1 and self.wgrad is None and isinstance(st.tx, AdamW)
+                  and st.params.master.is_cuda)
+            self._ov_opt = K.OverlappedAdamW(st.params, st.tx, st.opt_state, 1.0 / cfg.num_microbatches) if ok else False
+        return self._ov_opt or None
+
     def _sync_update(self):
         """sync_gradients(('data','pipe')): stage params are pipe-sharded -> mean over
         'data' only; then AdamW on the local stage and the metrics fold.  The host
         step counter is advanced by the callers."""
         st, P, cfg = self.state, self.state.params, self.cfg
         scale = 1.0 / (cfg.num_microbatches * self.n_dp)
+        ov = getattr(self, "_ov_opt", None)
+        if ov and ov.forked:   # AdamW already forked layer by layer during the backward
+            ov.finish()
+            with named_scope("sync_metrics"):
+                K.metrics_fold_(self.metrics, P.metrics_slot)
+            return
         if self.wgrad is not None:
             self.wgrad.join()  # every weight-gradient GEMM of the step has landed
         if self.deep_engine is not None and self.deep_engine.fuse_opt:

@@ -1,6 +1,7 @@
 #!/bin/bash
 # PMC counters of the fused classifier step kernels (mlp2_fwd / mlp2_bwd), eager
-# launches from tools/stamp_mlp2.py.  One counter group per rocprofv3 run.
+# launches from tools/stamp_mlp2.py (two-launch pair and the run-ahead backward).
+# One counter group per rocprofv3 run.
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/pmc_mlp2
@@ -26,7 +27,7 @@ for f in glob.glob(f"{out}/g*/**/*counter_collection.csv", recursive=True):
         k = r.get("Kernel_Name", "")
         if "mlp2" not in k:
             continue
-        kn = "fwd" if "fwd" in k else "bwd"
+        kn = "fwd" if "fwd" in k else ("bwd_run_ahead" if "true, true>" in k else "bwd")
         agg[kn][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for kn, d in agg.items():
     print(f"== mlp2_{kn}")

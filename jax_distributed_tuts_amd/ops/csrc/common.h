@@ -182,6 +182,25 @@ __device__ __forceinline__ void xcd_contiguous_tile(int& bx, int& by) {
   bx = t % gx; by = t / gx;
 }
 
+// Run-ahead tile map, from the XCD the workgroup actually runs on (HW_REG_XCC_ID):
+// XCD x takes tiles [x G/8, (x+1) G/8) in chunk-fastest order, i.e. whole column
+// blocks (all gridDim.y input chunks of 16 hidden units: their Z1 partials meet in
+// the XCD's L2) and 4 neighbouring ones (whole 128-byte lines of W1 rows); its
+// workgroups are told apart by L / 8.  Workgroups are dealt round-robin over the XCDs
+// (linear id L -> XCD (L + o) % 8, the offset o carried over from earlier dispatches),
+// so each XCD gets G/8 workgroups with distinct L / 8 and this is a bijection.  The
+// body checks it: every tile has a per-launch counter (ztick tail) that must read
+// the launch number, otherwise the error word is raised and the host refuses the
+// results (FusedMLP2 / FusedMLPDeep .finalize).
+__device__ __forceinline__ void xcd_column_tile(int& bx, int& by) {
+  const int L = blockIdx.x + gridDim.x * blockIdx.y, G = gridDim.x * gridDim.y;
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+  const int t = (int)(xcc & 7u) * (G / 8) + L / 8;
+  bx = t / gridDim.y;
+  by = t % gridDim.y;
+}
+
 // A kernel-argument pointer pinned in SGPRs.  Selecting between struct members with a
 // lane-dependent condition (`aux ? a.pW2 : a.pW1`) lets the compiler turn the select
 // into a per-lane load of the member's ADDRESS from the kernarg segment: a vector load

@@ -101,6 +101,13 @@ struct MdArgs {
   // dropout counter high word = step * step_mul (0 or 1: the step): the DP minibatch
   // loop's streams are (step * n_minibatches + i) << 32, i in the offset (dp.py)
   int step_mul;
+  // run-ahead (md_bwd AHEAD, layer 0, one GPU, fused AdamW): the layer-0 backward of
+  // step t also runs layer 0's forward of step t+1 (mlp_fused.hip Mlp2Args has the
+  // same fields): XR row-major bf16 copy of the fp32 input (md_fwd writes it), zslab
+  // Z partials [N/16][K/KC][MD_MPM/4][16][4], ztick counters (128-byte lines: step
+  // ticket unused here, error word, launch counter; column barriers; per-XCD tile
+  // counters), hand = updated b fp32 [N]; G / Hout are layer 0's G_0 / H_0
+  bf16_t* XR; float* zslab; unsigned* ztick; float* hand;
 };
 
 // Slots 0-4: s_memrealtime at the kernel's phase ends (tools/stamp_deep.py).
@@ -111,6 +118,7 @@ struct MdArgs {
   } while (0)
 
 struct MdAdam { float b1, b2, eps, wd, lr, gs, rbc1, rbc2; };
+typedef __attribute__((address_space(1))) unsigned gu32_md;
 
 __device__ __forceinline__ MdAdam md_adam_consts(const MdArgs& a, int step) {
   MdAdam k;
@@ -246,6 +254,13 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
     u32x4 o; o.x = q[0]; o.y = q[1]; o.z = q[2]; o.w = q[3];
     *reinterpret_cast<u32x4*>(a.INT + (long)xk * a.ldint + r0 + h) = o;
   }
+  // row-major bf16 input (run-ahead layer-0 backward: the next step's forward operand)
+  if (XF32 && a.XR && by < K_IN / XTC && tid < RB * (XTC / 8)) {
+    const int rl = tid / (XTC / 8), q = tid % (XTC / 8);
+    if (r0 + rl < M)
+      *reinterpret_cast<u32x4*>(a.XR + (long)(r0 + rl) * K_IN + by * XTC + 8 * q) =
+          *reinterpret_cast<const u32x4*>(&xs[rl * LDXS + by * XTC + 8 * q]);
+  }
 
   // ---- 3. K split over the 8 waves
   constexpr int MT = RB / 16;
@@ -336,7 +351,7 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
 // BND (pipeline stage boundary, !TOP): dZ_i = dH * G_i -- the gradient w.r.t. this
 // layer's output arrives from the next pipeline stage instead of being recomputed
 // from dZ_{i+1} W_{i+1}^T.
-template <int K_IN, bool TOP, int C, int KC, int NN, bool XCD, bool BND = false>
+template <int K_IN, bool TOP, int C, int KC, int NN, bool XCD, bool BND = false, bool AHEAD = false>
 __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   constexpr int NT = MD_NT, NW = MD_NW, MPM = MD_MPM;
   constexpr int LDM = MPM + 8;
@@ -359,10 +374,16 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   static_assert(!(TOP && BND), "TOP and BND are exclusive");
   constexpr bool WN = !TOP && !BND;   // dZ_i from the next layer of this launch sequence
   __shared__ __attribute__((aligned(16))) bf16_t wnS[WN ? 16 * LDWN : 8];
+  // run-ahead (layer 0): W_0'[chunk, blk]^T image for the next forward's partial, H tile
+  static_assert(!AHEAD || (WN && K_IN == 784 && KC <= 128 && KC % 16 == 0), "run-ahead: layer 0 only");
+  constexpr int LDW1 = 128 + 8;
+  constexpr int NCH = K_IN / KC;
+  __shared__ __attribute__((aligned(16))) bf16_t w1n[AHEAD ? 16 * LDW1 : 8];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int M = a.M, N = a.N, Mp = (M + 31) & ~31;
   int bx = blockIdx.x, by = blockIdx.y;
-  if constexpr (XCD) xcd_contiguous_tile(bx, by);   // column-block neighbours share an L2 (common.h)
+  if constexpr (AHEAD) xcd_column_tile(bx, by);      // a column block on ONE XCD (common.h)
+  else if constexpr (XCD) xcd_contiguous_tile(bx, by);   // column-block neighbours share an L2 (common.h)
   const int j0 = bx * 16, kc0 = by * KC;
   const bool chunk0 = by == 0;
   const bool lead = TOP && bx == 0 && by == 0;
@@ -467,6 +488,25 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       const int lq = min(lane, C - 1);
       qp = (fo ? a.pbh : a.gbh)[lq]; qm = (fo ? a.mbh : a.gbh)[lq]; qv = (fo ? a.vbh : a.gbh)[lq];
     }
+  }
+  // run-ahead: X[16w.., chunk] fragments for the next forward (in flight through the
+  // backward), and step t+1's dropout bits of this thread's epilogue element (row group
+  // eg of the share [g_lo, g_hi) of this chunk, column j0 + gn)
+  bf16x8 xa[AHEAD ? 4 : 1];
+  u32x4 dbn = {0u, 0u, 0u, 0u};
+  const int g_lo = (by * (MPM / 4)) / NCH, g_hi = ((by + 1) * (MPM / 4)) / NCH;
+  const int eg = g_lo + (tid >> 6), ee = (tid >> 4) & 3;
+  if constexpr (AHEAD) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      xa[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(
+                   a.XR + (long)min(w * 16 + (lane & 15), M - 1) * K_IN + min(kc0 + ks * 32 + 8 * (lane >> 4), K_IN - 8)));
+    if (a.keep < 1.f && eg < g_hi && eg * 4 < M) {
+      const int sn = step + 1;
+      dbn = dropout_bits(a.seed, a.offset + ((unsigned long long)(unsigned)(a.step_mul > 1 ? sn * a.step_mul : sn) << 32),
+                         dropout_group(0, eg * 4, j0 + gn, M, N));
+    }
+    for (int idx = tid; idx < 16 * (128 - KC); idx += NT) w1n[(idx / (128 - KC)) * LDW1 + KC + idx % (128 - KC)] = 0;
   }
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (!WN) step = a.step[lz];
@@ -614,6 +654,8 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
     }
     if (a.fuse_opt && a.WTout)
       *reinterpret_cast<uint2*>(a.WTout + (long)tcol * a.ldwt + trow0) = make_uint2(wtp[0], wtp[1]);
+    if constexpr (AHEAD)
+      *reinterpret_cast<uint2*>(&w1n[(lane & 15) * LDW1 + (trow0 - kc0)]) = make_uint2(wtp[0], wtp[1]);
   } else if (aux) {
     bf16x8 ones;
 #pragma unroll
@@ -641,8 +683,13 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       }
       if (ac == 0) {
         const int j = j0 + n;
-        if (a.fuse_opt) a.sb[j] = f2bf(md_adam(bp[e], bm[e], bvv[e], ab[e], ak, a.pb + j, a.mb + j, a.vb + j));
-        else a.gb[goff + j] = (a.accumulate ? bp[e] : 0.f) + ab[e];
+        if (a.fuse_opt) {
+          const float pn = md_adam(bp[e], bm[e], bvv[e], ab[e], ak, a.pb + j, a.mb + j, a.vb + j);
+          a.sb[j] = f2bf(pn);
+          if constexpr (AHEAD) a.hand[j] = pn;   // the next forward's bias (same XCD: L2 hand-off)
+        } else {
+          a.gb[goff + j] = (a.accumulate ? bp[e] : 0.f) + ab[e];
+        }
       }
     }
     if (TOP && lead && lane < C) {
@@ -666,12 +713,88 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       }
     }
   }
+  unsigned launch_no = 0u;
+  if constexpr (AHEAD) {
+    // ---- 5. step t+1's layer-0 forward (see mlp_fused.hip mlp2_bwd AHEAD): partial
+    // Z_0 of (chunk, blk) from the W_0' tile just produced, column-block barrier in the
+    // XCD's L2, then each of the NCH workgroups finishes a share of the rows
+    __syncthreads();   // w1n complete, hand-off stored
+    unsigned tile_seen = 0u;
+    if (tid == 0) {
+      launch_no = a.ztick[2];
+      const int tpx = (N / 16) * NCH / 8, t = bx * NCH + by;
+      tile_seen = __hip_atomic_fetch_add((gu32_md*)(a.ztick + 32 * (1 + N / 16) + 32 * ((tpx + 31) / 32) * (t / tpx) + t % tpx),
+                                         1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (ks * 32 < KC) {
+        const bf16x8 bw = *reinterpret_cast<const bf16x8*>(&w1n[(lane & 15) * LDW1 + ks * 32 + 8 * (lane >> 4)]);
+        z = mfma16x16x32(xa[ks], bw, z);
+      }
+    }
+    float* const zb = a.zslab + (long)bx * NCH * (MPM / 4) * 64;
+    *reinterpret_cast<u32x4*>(zb + ((long)by * (MPM / 4) + w * 4 + (lane >> 4)) * 64 + (lane & 15) * 4) =
+        (u32x4){__float_as_uint(z[0]), __float_as_uint(z[1]), __float_as_uint(z[2]), __float_as_uint(z[3])};
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      unsigned* cnt = a.ztick + 32 * (1 + bx);
+      __hip_atomic_fetch_add((gu32_md*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const unsigned target = (unsigned)NCH * (launch_no + 1u);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(cnt, (short)0, 4, 0x00020000);
+      while ((int)((unsigned)__builtin_amdgcn_raw_buffer_load_b32(cr, 0, 0, 16) - target) < 0) {
+        if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > 2000000ll) {   // 20 ms
+          atomicOr(a.ztick + 1, 2u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+      }
+      if (tile_seen != launch_no) atomicOr(a.ztick + 1, 1u);
+    }
+    __syncthreads();
+    // ---- 6. layer 0's forward epilogue of step t+1, one element per thread
+    const int ng = g_hi - g_lo;
+    const __amdgpu_buffer_rsrc_t zr = __builtin_amdgcn_make_buffer_rsrc(zb, (short)0, NCH * (MPM / 4) * 64 * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(a.hand, (short)0, N * 4, 0x00020000);
+    const int egc = min(eg, g_hi - 1);
+    float zp[NCH];
+#pragma unroll
+    for (int q = 0; q < NCH; ++q)
+      zp[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                            zr, (int)((((long)q * (MPM / 4) + egc) * 64 + gn * 4 + ee) * 4), 0, 16));
+    const float bv = round_bf(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(hr, (j0 + gn) * 4, 0, 16)));
+    if (tid < 64 * ng) {
+      const int row = eg * 4 + ee;
+      if (row < M) {
+        float v = bv;   // + the NCH chunk partials in chunk order
+#pragma unroll
+        for (int q = 0; q < NCH; ++q) v += zp[q];
+        const float zz = bf2f(f2bf(v));           // Z_0 as the bf16 Dense output
+        const float ez = __expf(-zz);
+        const float sg = 1.0f / (1.0f + ez);
+        float hvn = zz * sg;                       // act_fwd(ACT_SILU), as md_fwd
+        float gd = sg * (1.0f + zz * (1.0f - sg));  // act_grad(ACT_SILU)
+        if (a.keep < 1.f) {
+          const bool kp = keep_word(dbn, ee, a.keep);
+          hvn = kp ? hvn / a.keep : 0.f;
+          gd = kp ? gd / a.keep : 0.f;
+        }
+        a.Hout[(long)row * N + j0 + gn] = f2bf(hvn);
+        a.G[((long)eg * N + j0 + gn) * 4 + ee] = gd;
+      }
+    }
+  }
   if (a.advance_step) {
     __syncthreads();
     if (tid == 0) {
       const unsigned t = atomicAdd(a.ticket, 1u);
       if (t == gridDim.x * gridDim.y - 1) {
         a.step[0] = step + 1;
+        if constexpr (AHEAD) a.ztick[2] = launch_no + 1u;   // every workgroup has read it (ticket)
         __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -685,6 +808,18 @@ int xcd_tiles_enabled();   // mlp_fused.hip (JDT_XCD_TILES)
 
 JDT_API int jdt_md_args_size() { return (int)sizeof(MdArgs); }
 
+// 1 if the run-ahead layer-0 backward fits (its column barrier needs every workgroup resident)
+JDT_API int jdt_md_ahead_ok(int M) {
+  if (M <= 0 || M > MD_MPM) return 0;
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, md_bwd_kernel<784, false, 10, 112, 512, true, false, true>,
+                                                   MD_NT, 0) != hipSuccess)
+    return 0;
+  return (512 / 16) * (784 / 112) <= cus * per ? 1 : 0;
+}
+
 // phase 0: forward of one hidden layer (head = 1: + head logits); phase 1: backward
 // (head = 1: TOP layer, CE through the head; head = 2: pipeline-stage boundary,
 // dZ from the next stage's dH).  Instantiated for the tutorial
@@ -696,6 +831,15 @@ JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) 
   if (a.mb_rows < 0 || (a.mb_rows && (a.mb_rows % 4 || a.M % a.mb_rows))) return -2;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const dim3 blk(MD_NT);
+  if (phase == 2) {
+    // run-ahead layer-0 backward (+ layer 0's forward of the next step)
+    if (a.K != 784 || head || !a.fuse_opt || !a.WTout || !a.XR || !a.zslab || !a.ztick || !a.hand || a.mb_rows ||
+        !a.advance_step || a.det_logits)
+      return -3;
+    hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, true, false, true>), dim3(a.N / 16, 784 / 112), blk, 0,
+                       st, a);
+    return HIP_LAUNCH_CHECK();
+  }
   if (phase == 0) {
     // 16-row blocks: twice the workgroups, half the input bytes each (as mlp2_fwd)
     const dim3 grid((a.M + 15) / 16, a.N / 16);

@@ -945,25 +945,6 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   if constexpr (XCD) xcd_contiguous_tile(bx, by);
   mlp2_fwd_body<K_IN, C, RB, DIRECT, false>(static_cast<const Mlp2Args&>(a), bx, by, 0);
 }
-// Run-ahead tile map, from the XCD the workgroup actually runs on (HW_REG_XCC_ID):
-// XCD x takes tiles [x G/8, (x+1) G/8) in chunk-fastest order, i.e. whole column
-// blocks (all gridDim.y input chunks of 16 hidden units: their Z1 partials meet in
-// the XCD's L2) and 4 neighbouring ones (whole 128-byte lines of W1 rows); its
-// workgroups are told apart by L / 8.  Workgroups are dealt round-robin over the XCDs
-// (linear id L -> XCD (L + o) % 8, the offset o carried over from earlier dispatches),
-// so each XCD gets G/8 workgroups with distinct L / 8 and this is a bijection.  The
-// body checks it: every tile has a per-launch counter (ztick tail) that must read
-// the launch number, otherwise the error word is raised and the host refuses the
-// results (FusedMLP2.finalize).
-__device__ __forceinline__ void xcd_column_tile(int& bx, int& by) {
-  const int L = blockIdx.x + gridDim.x * blockIdx.y, G = gridDim.x * gridDim.y;
-  unsigned xcc;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
-  const int t = (int)(xcc & 7u) * (G / 8) + L / 8;
-  bx = t / gridDim.y;
-  by = t % gridDim.y;
-}
-
 template <int K_IN, int C, int KC, bool XCD, bool AHEAD = false>
 __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   int bx = blockIdx.x, by = blockIdx.y;

@@ -358,11 +358,13 @@ class MdArgs(ctypes.Structure):
                 ("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float), ("wd", c_float),
                 ("gscale", c_float), ("running", c_void_p), ("stamps", c_void_p),
                 ("accumulate", c_int), ("dH", c_void_p), ("mb_rows", c_int), ("mb_stride", c_ulonglong),
-                ("stage_stride", ctypes.c_long), ("det_logits", c_void_p), ("step_mul", c_int)]
+                ("stage_stride", ctypes.c_long), ("det_logits", c_void_p), ("step_mul", c_int),
+                ("XR", c_void_p), ("zslab", c_void_p), ("ztick", c_void_p), ("hand", c_void_p)]
 
 
 _lib.declare("jdt_md_layer", c_int, [ctypes.POINTER(MdArgs), c_int, c_int, c_void_p])
 _lib.declare("jdt_md_args_size", c_int, [])
+_lib.declare("jdt_md_ahead_ok", c_int, [c_int])
 
 DEEP_H = 512
 
@@ -431,6 +433,20 @@ class FusedMLPDeep:
         self.grad_stage = None
         self.det_logits = (torch.zeros(DEEP_H // 16, rows, 10, dtype=torch.float32, device=dev)
                            if deterministic() else None)
+        # run-ahead (one GPU, fused AdamW, one dropout stream): the layer-0 backward of
+        # step t also runs layer 0's forward of step t+1 (csrc/mlp_deep.hip md_bwd AHEAD),
+        # one launch less per step; same buffers / checks as FusedMLP2
+        self.ahead_ok = (self.fuse_opt and self.world == 1 and self.mb_rows == 0 and self.det_logits is None
+                         and m.dims[0] == 784 and os.environ.get("JDT_MLP2_AHEAD", "1") == "1"
+                         and bool(_lib.lib().jdt_md_ahead_ok(rows)))
+        self.ahead_primed = False
+        self._ahead_args = None
+        if self.ahead_ok:
+            nch, tpx = 784 // 112, H // 16 * (784 // 112) // 8
+            self.XR = torch.zeros(rows, 784, **bf)
+            self.zslab = torch.zeros(H // 16 * nch * 128 * 16, dtype=torch.float32, device=dev)
+            self.ztick = torch.zeros(32 * (1 + H // 16) + 8 * 32 * ((tpx + 31) // 32), dtype=torch.int32, device=dev)
+            self.hand = torch.zeros(H, dtype=torch.float32, device=dev)
 
     def set_grad_stage(self, base: int, stride: int):
         """See FusedMLP2.set_grad_stage."""
@@ -470,6 +486,8 @@ class FusedMLPDeep:
         a.seed = R.fold_rng_over_axis(st.rng, self.mesh, self.axis) & 0xFFFFFFFF
         a.offset = (m.layer_id_base + i) << 1
         a.mb_rows, a.mb_stride = self.mb_rows, self.mb_stride
+        if self.ahead_ok and i == 0 and phase == 0:
+            a.XR = self.XR.data_ptr()   # the run-ahead backward's operand for the next forward
         if self.det_logits is not None:
             a.det_logits = self.det_logits.data_ptr()
         a.step, a.ticket = o["count"].data_ptr(), o["ticket"].data_ptr()
@@ -508,12 +526,44 @@ class FusedMLPDeep:
             a.running = self.metrics.data_ptr()
         return a
 
-    def forward_backward(self, batch):
+    def _ensure_args(self, batch):
         key = (batch.inputs.data_ptr(), batch.labels.data_ptr(), self.state.rng)
         if self._args is None or self._key != key:
             fwd = [self._layer(batch, i, 0) for i in range(self.nh)]
             bwd = [self._layer(batch, i, 1) for i in reversed(range(self.nh))]
             self._args, self._key = (fwd, bwd), key
+            self._ahead_args = None
+
+    def run_ahead(self, batch, n: int, prologue: bool = True):
+        """n complete steps, the layer-0 backward of each also running layer 0's forward
+        of the next step (2 * hidden - 1 launches per step); ``prologue`` first runs
+        layer 0's forward of the first step (see FusedMLP2.run_ahead)."""
+        assert self.ahead_ok
+        self._ensure_args(batch)
+        fwd, bwd = self._args
+        if self._ahead_args is None:
+            b = MdArgs.from_buffer_copy(bwd[-1])   # layer 0's backward
+            b.XR, b.zslab, b.ztick, b.hand = (t.data_ptr() for t in (self.XR, self.zslab, self.ztick, self.hand))
+            self._ahead_args = b
+        Lb = _lib.lib()
+        s = _lib.stream_ptr()
+        if prologue:
+            _lib.check(Lb.jdt_md_layer(ctypes.byref(fwd[0]), 0, int(self.nh == 1), s), "md_fwd")
+        elif not torch.cuda.is_current_stream_capturing():
+            assert self.ahead_primed, "run_ahead(prologue=False) needs a run-ahead launch just before"
+        for _ in range(n):
+            for i in range(1, self.nh):
+                _lib.check(Lb.jdt_md_layer(ctypes.byref(fwd[i]), 0, int(i == self.nh - 1), s), "md_fwd")
+            for j, a in enumerate(bwd[:-1]):
+                _lib.check(Lb.jdt_md_layer(ctypes.byref(a), 1, int(j == 0), s), "md_bwd")
+            _lib.check(Lb.jdt_md_layer(ctypes.byref(self._ahead_args), 2, 0, s), "md_bwd_ahead")
+        if not torch.cuda.is_current_stream_capturing():
+            self.ahead_primed = True
+
+    def forward_backward(self, batch):
+        if not torch.cuda.is_current_stream_capturing():
+            self.ahead_primed = False
+        self._ensure_args(batch)
         Lb = _lib.lib()
         s = _lib.stream_ptr()
         fwd, bwd = self._args
@@ -534,6 +584,9 @@ class FusedMLPDeep:
 
     def finalize(self):
         """Bring the generic bf16 shadows up to date (parity copies in use on odd steps)."""
+        if self.ahead_ok and int(self.ztick[1].item()) != 0:
+            raise RuntimeError("md_bwd run-ahead: tile map or column barrier failed (error word "
+                               f"{int(self.ztick[1].item())}); results invalid")
         if self.fuse_opt and int(self.state.opt_state["count"].item()) % 2 == 1:
             for i, t in self.par.items():
                 self.P.s(self.kn[i]).copy_(t)

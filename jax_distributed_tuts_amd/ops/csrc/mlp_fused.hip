@@ -610,10 +610,9 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   const float qp = (fo ? a.pb2 : a.gb2)[lq], qm = (fo ? a.mb2 : a.gb2)[lq], qv = (fo ? a.vb2 : a.gb2)[lq];
   // run-ahead: A fragments of X[16w.., chunk] (row-major bf16 copy) for the next
   // forward (in flight through CE, dZ1 and dW1); k past the chunk is multiplied by
-  // w1n's zero padding, so the address is only clamped.  Then step t+1's dropout bits
-  // for this thread's row group of the epilogue share (phase 6: workgroup `by` of the
-  // column block finishes row groups [g_lo, g_hi)), computed from the per-lane step
-  // while the loads fly.
+  // w1n's zero padding, so the address is only clamped.  dbn: step t+1's dropout bits
+  // of this thread's element of the epilogue share (phase 6: workgroup `by` of the
+  // column block finishes row groups [g_lo, g_hi)), computed in phase 5.
   bf16x8 xa[AHEAD ? 4 : 1];
   u32x4 dbn = {0u, 0u, 0u, 0u};
   const int g_lo = (by * (MPM / 4)) / NCH, g_hi = ((by + 1) * (MPM / 4)) / NCH;
@@ -625,9 +624,6 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     for (int ks = 0; ks < 4; ++ks)
       xa[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(
                    a.XR + (long)min(w * 16 + (lane & 15), M - 1) * K_IN + min(kc0 + ks * 32 + 8 * (lane >> 4), K_IN - 8)));
-    if (a.keep < 1.f && eg < g_hi && eg * 4 < M)
-      dbn = dropout_bits(a.seed, a.offset + ((unsigned long long)(unsigned)(step_lane + 1) << 32),
-                         dropout_group(0, eg * 4, j0 + gn, M, H));
   }
   __builtin_amdgcn_sched_barrier(0);
   int step = step_in;
@@ -838,6 +834,11 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     float* const zb = a.zslab + (long)bx * NCH * (MPM / 4) * 64;
     *reinterpret_cast<u32x4*>(zb + ((long)by * (MPM / 4) + w * 4 + (lane >> 4)) * 64 + (lane & 15) * 4) =
         (u32x4){__float_as_uint(z[0]), __float_as_uint(z[1]), __float_as_uint(z[2]), __float_as_uint(z[3])};
+    // step t+1's dropout bits of this thread's epilogue element, computed while the
+    // partial store drains (off the phase-0 critical path)
+    if (a.keep < 1.f && eg < g_hi && eg * 4 < M)
+      dbn = dropout_bits(a.seed, a.offset + ((unsigned long long)(unsigned)(step + 1) << 32),
+                         dropout_group(0, eg * 4, j0 + gn, M, H));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // partials, hand-offs, launch_no: in the L2 / read
     STAMP(8);
     __syncthreads();

@@ -490,8 +490,8 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
     }
   }
   // run-ahead: X[16w.., chunk] fragments for the next forward (in flight through the
-  // backward), and step t+1's dropout bits of this thread's epilogue element (row group
-  // eg of the share [g_lo, g_hi) of this chunk, column j0 + gn)
+  // backward); this thread's epilogue element: row group eg of the share [g_lo, g_hi)
+  // of this chunk, column j0 + gn (its dropout bits dbn are computed in phase 5)
   bf16x8 xa[AHEAD ? 4 : 1];
   u32x4 dbn = {0u, 0u, 0u, 0u};
   const int g_lo = (by * (MPM / 4)) / NCH, g_hi = ((by + 1) * (MPM / 4)) / NCH;
@@ -501,11 +501,6 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
     for (int ks = 0; ks < 4; ++ks)
       xa[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(
                    a.XR + (long)min(w * 16 + (lane & 15), M - 1) * K_IN + min(kc0 + ks * 32 + 8 * (lane >> 4), K_IN - 8)));
-    if (a.keep < 1.f && eg < g_hi && eg * 4 < M) {
-      const int sn = step + 1;
-      dbn = dropout_bits(a.seed, a.offset + ((unsigned long long)(unsigned)(a.step_mul > 1 ? sn * a.step_mul : sn) << 32),
-                         dropout_group(0, eg * 4, j0 + gn, M, N));
-    }
     for (int idx = tid; idx < 16 * (128 - KC); idx += NT) w1n[(idx / (128 - KC)) * LDW1 + KC + idx % (128 - KC)] = 0;
   }
   __builtin_amdgcn_sched_barrier(0);
@@ -737,6 +732,19 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
     float* const zb = a.zslab + (long)bx * NCH * (MPM / 4) * 64;
     *reinterpret_cast<u32x4*>(zb + ((long)by * (MPM / 4) + w * 4 + (lane >> 4)) * 64 + (lane & 15) * 4) =
         (u32x4){__float_as_uint(z[0]), __float_as_uint(z[1]), __float_as_uint(z[2]), __float_as_uint(z[3])};
+    // step t+1's dropout bits of this thread's epilogue element, while the store drains
+    if (a.keep < 1.f && eg < g_hi && eg * 4 < M) {
+      const int sn = step + 1;
+      int lrow = eg * 4, Mg = M;
+      unsigned long long off = a.offset + ((unsigned long long)(unsigned)(a.step_mul > 1 ? sn * a.step_mul : sn) << 32);
+      if (a.mb_rows > 0) {   // per-microbatch streams, as md_fwd draws them
+        const int mi = (eg * 4) / a.mb_rows;
+        lrow = eg * 4 - mi * a.mb_rows;
+        Mg = a.mb_rows;
+        off += (unsigned long long)mi * a.mb_stride;
+      }
+      dbn = dropout_bits(a.seed, off, dropout_group(0, lrow, j0 + gn, Mg, N));
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
@@ -833,7 +841,7 @@ JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) 
   const dim3 blk(MD_NT);
   if (phase == 2) {
     // run-ahead layer-0 backward (+ layer 0's forward of the next step)
-    if (a.K != 784 || head || !a.fuse_opt || !a.WTout || !a.XR || !a.zslab || !a.ztick || !a.hand || a.mb_rows ||
+    if (a.K != 784 || head || !a.fuse_opt || !a.WTout || !a.XR || !a.zslab || !a.ztick || !a.hand ||
         !a.advance_step || a.det_logits)
       return -3;
     hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, true, false, true>), dim3(a.N / 16, 784 / 112), blk, 0,

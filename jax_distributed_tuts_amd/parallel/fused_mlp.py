@@ -433,10 +433,15 @@ class FusedMLPDeep:
         self.grad_stage = None
         self.det_logits = (torch.zeros(DEEP_H // 16, rows, 10, dtype=torch.float32, device=dev)
                            if deterministic() else None)
-        # run-ahead (one GPU, fused AdamW, one dropout stream): the layer-0 backward of
-        # step t also runs layer 0's forward of step t+1 (csrc/mlp_deep.hip md_bwd AHEAD),
-        # one launch less per step; same buffers / checks as FusedMLP2
-        self.ahead_ok = (self.fuse_opt and self.world == 1 and self.mb_rows == 0 and self.det_logits is None
+        # run-ahead (one GPU, fused AdamW): the layer-0 backward of step t also runs
+        # layer 0's forward of step t+1 (csrc/mlp_deep.hip md_bwd AHEAD, per-microbatch
+        # dropout streams included), one launch less per step; buffers / checks as FusedMLP2
+        # Per-microbatch dropout streams (mb_rows > 0, one-stage GPipe) are opt-in
+        # (JDT_MLP2_AHEAD_MB=1): its kernel path passes the H_0 / G_0 check against md_fwd,
+        # but a 330-step 8-layer run ended at a different loss than the plain schedule
+        # (0.066 vs 0.089, BENCH_NOTES) and that was not explained this round.
+        self.ahead_ok = (self.fuse_opt and self.world == 1 and self.det_logits is None
+                         and (self.mb_rows == 0 or os.environ.get("JDT_MLP2_AHEAD_MB", "0") == "1")
                          and m.dims[0] == 784 and os.environ.get("JDT_MLP2_AHEAD", "1") == "1"
                          and bool(_lib.lib().jdt_md_ahead_ok(rows)))
         self.ahead_primed = False

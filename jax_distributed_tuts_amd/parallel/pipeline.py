@@ -136,6 +136,7 @@ class GPipeTrainer:
         self.dev = P.master.device
         self.metrics = torch.zeros(N_METRIC_SLOTS, dtype=torch.float32, device=self.dev)
         self.graph = None
+        self._ahead = None
         self.multi = None
         self.p2p = None
         self._p2p_tried = False
@@ -282,6 +283,7 @@ class GPipeTrainer:
     def invalidate(self):
         """After a checkpoint restore: drop captured graphs and the stage engine."""
         self.graph = None
+        self._ahead = None
         self.multi = None
         self.stage_engine = None
         self._engine_tried = False
@@ -388,7 +390,7 @@ class GPipeTrainer:
     def step(self, batch: Batch):
         if self.graph is not None:
             with replay_scope("train_step_pp"):
-                self.graph.replay()
+                self._ahead.replay(1) if getattr(self, "_ahead", None) else self.graph.replay()
         else:
             self._compute(batch)
             self._sync_update()
@@ -410,7 +412,17 @@ class GPipeTrainer:
         with torch.cuda.graph(g):
             body()
         self.graph = g
-        if steps_per_graph > 1:
+        # one stage on the deep fused engine: layer 0's forward of the next step rides in
+        # the layer-0 backward (run-ahead, fused_mlp.AheadGraphs: cold / primed graphs)
+        eng = self.deep_engine
+        self._ahead = None
+        if self.S == 1 and eng is not None and getattr(eng, "ahead_ok", False):
+            from .fused_mlp import AheadGraphs
+
+            self._ahead = AheadGraphs(eng, batch, steps_per_graph, pool=g.pool())
+            if steps_per_graph > 1:
+                self.multi = (steps_per_graph, self._ahead.graph(steps_per_graph))
+        elif steps_per_graph > 1:
             gm = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gm, pool=g.pool()):
                 for _ in range(steps_per_graph):
@@ -422,7 +434,7 @@ class GPipeTrainer:
             S, gm = self.multi
             for _ in range(n // S):
                 with replay_scope("train_step_pp", S):
-                    gm.replay()
+                    self._ahead.replay(S) if self._ahead else gm.replay()
             self.state.step += (n // S) * S
             n %= S
         for _ in range(n):

@@ -999,3 +999,49 @@ def test_deep_run_ahead_matches_two_launch(layers, rows, monkeypatch):
     d = (res["0"][0] - res["1"][0]).abs()
     assert float(d.max()) <= 3e-3
     _close(res["1"][1], res["0"][1], rtol=1e-3, atol=5e-2)
+
+
+def test_pipeline_single_stage_run_ahead(monkeypatch):
+    """One-stage GPipe on the deep fused engine (per-microbatch dropout streams,
+    mb_rows): run-ahead graphs == the plain launch sequence, and the run-ahead's
+    layer-0 forward (H_0 / G_0, per-microbatch masks) == md_fwd of the same step."""
+    import ctypes
+
+    from data_paral import synthetic_batch
+    from pipeline_parallel import build_mlp_pipeline
+    from jax_distributed_tuts_amd.ops import _lib
+    from jax_distributed_tuts_amd.runtime.dist import Mesh
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.train_state import Batch
+
+    mesh = Mesh({"data": 1, "pipe": 1})
+    monkeypatch.setenv("JDT_MLP2_AHEAD_MB", "1")   # opt-in for per-microbatch dropout streams
+    res = {}
+    for ahead in ("0", "1"):
+        monkeypatch.setenv("JDT_MLP2_AHEAD", ahead)
+        cfg = dp_config()
+        tr = build_mlp_pipeline(cfg, mesh, DEV, 8, num_microbatches=4)
+        b = synthetic_batch(cfg, 70)
+        b = Batch(b.inputs.to(DEV), b.labels.to(DEV))
+        tr.step(b)
+        eng = tr.deep_engine
+        assert eng is not None and eng.mb_rows > 0 and eng.ahead_ok == (ahead == "1")
+        tr.capture(b, steps_per_graph=3)
+        tr.run_steps(b, 6)
+        tr.step(b)
+        tr.finalize()
+        torch.cuda.synchronize()
+        res[ahead] = (tr.state.params.master.clone(), tr.metrics.clone(), int(tr.state.opt_state["count"].item()))
+        if ahead == "1":
+            assert int(eng.ztick[1].item()) == 0
+            eng.run_ahead(b, 1)
+            torch.cuda.synchronize()
+            h_a, g_a = eng.Hs[0].clone(), eng.G[0].clone()
+            _lib.check(_lib.lib().jdt_md_layer(ctypes.byref(eng._args[0][0]), 0, 0, _lib.stream_ptr()), "md_fwd")
+            torch.cuda.synchronize()
+            dh = (h_a.float() - eng.Hs[0].float()).abs()
+            assert float((dh > 0).float().mean()) < 0.02 and float(dh.max()) <= 0.05, float(dh.max())
+            assert float(((g_a - eng.G[0]).abs() > 1e-3).float().mean()) < 0.02
+    assert res["0"][2] == res["1"][2] == 8
+    assert float((res["0"][0] - res["1"][0]).abs().max()) <= 3e-3
+    _close(res["1"][1], res["0"][1], rtol=1e-3, atol=5e-2)

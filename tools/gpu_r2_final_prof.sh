@@ -1,9 +1,8 @@
 #!/bin/bash
-# final round-2 evidence: GEMM shape table vs hipBLASLt, transformer merged profile, headline profile
-cd /root/repo && export TMPDIR=/tmp PYTHONUNBUFFERED=1 && mkdir -p gpurun_out/fin
-timeout -k 10 150 python tools/bench_gemm.py --groups 0 --json gpurun_out/fin/gemm.json > gpurun_out/fin/gemm.log 2>&1 || exit $?
-echo gemm done
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/fin/prof_tf -o tf -- python bench.py --strategy pp --model transformer --merge-microbatches --steps 60 --warmup 5 > gpurun_out/fin/prof_tf.log 2>&1 || exit $?
-echo tf prof done
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/fin/prof_dp -o dp -- python bench.py --steps 400 --warmup 50 > gpurun_out/fin/prof_dp.log 2>&1 || exit $?
-echo dp prof done
+# Final round-2 rocprofv3 kernel stats: 4-layer DP (layer-0 run-ahead) and the 1-GPU transformer step
+cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/fprof
+timeout -k 10 150 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/fprof/mlp4 -o run -- \
+  python3 bench.py --num-layers 4 --steps 300 --warmup 30 > gpurun_out/fprof/mlp4.log 2>&1 || exit 1
+timeout -k 10 150 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/fprof/lm -o run -- \
+  python3 bench.py --strategy pp --model transformer --steps 100 --warmup 10 > gpurun_out/fprof/lm.log 2>&1 || exit 1
+find gpurun_out/fprof -name "*kernel_stats.csv"

@@ -270,12 +270,17 @@ def main():
         desc["accum"] = tr.cfg.accum  # the path that actually ran (CPU falls back from "kernel")
         # 1-GPU fused step: one run-ahead launch per step (step t's backward + AdamW + step
         # t+1's forward) or the two-launch forward / backward pair
+        eng = getattr(tr, "fused", None)
+        nh = getattr(eng, "nh", None)   # deep engine: hidden layers
         if getattr(tr, "_ahead", None):
-            desc["step_launches"] = "1 (run-ahead mlp2_bwd)"
-        elif getattr(tr, "fused", None) is not None:
-            desc["step_launches"] = "2 (mlp2_fwd + mlp2_bwd)" + (" + xGMI all-reduce/AdamW" if ws > 1 else "")
+            desc["step_launches"] = (f"{2 * nh - 1} (layer-0 run-ahead md_bwd)" if nh
+                                     else "1 (run-ahead mlp2_bwd)")
+        elif eng is not None:
+            desc["step_launches"] = ((f"{2 * nh} (md_fwd / md_bwd per layer)" if nh else "2 (mlp2_fwd + mlp2_bwd)")
+                                     + (" + xGMI all-reduce/AdamW" if ws > 1 else ""))
     if args.strategy == "fsdp" and getattr(tr, "_ahead", None):
-        desc["step_launches"] = "1 (run-ahead mlp2_bwd)"
+        nh = getattr(tr.fused, "nh", None)
+        desc["step_launches"] = f"{2 * nh - 1} (layer-0 run-ahead md_bwd)" if nh else "1 (run-ahead mlp2_bwd)"
     if args.strategy == "pp":
         desc["single_stage_mode"] = tr.single_stage_mode  # how a 1-stage pipeline ran its microbatches
     if D.rank() == 0:

@@ -96,6 +96,9 @@ struct Mlp2Args {
   // buffer while the backward of t reads another and re-arms the third).
   bf16_t* XR; float* zslab; unsigned* ztick; float* hand;
   int lg3;
+  // fused optimizer = plain SGD (p -= lr * (g * gscale + wd * p), no momentum) instead
+  // of AdamW: the m / v pointers then alias p and are neither used nor written
+  int opt_sgd;
 };
 
 // Persistent multi-step launch (mlp2_loop_kernel): n steps, grid barriers between
@@ -124,12 +127,12 @@ struct Mlp2Loop {
     }                                                                                         \
   } while (0)
 
-struct AdamK { float b1, b2, eps, wd, lr, gs, rbc1, rbc2; };
+struct AdamK { float b1, b2, eps, wd, lr, gs, rbc1, rbc2; int sgd; };
 
 template <class AT>
 __device__ __forceinline__ AdamK adam_consts(AT& a, int step) {
   AdamK k;
-  k.b1 = a.beta1; k.b2 = a.beta2; k.eps = a.eps; k.wd = a.wd; k.lr = a.lr; k.gs = a.gscale;
+  k.b1 = a.beta1; k.b2 = a.beta2; k.eps = a.eps; k.wd = a.wd; k.lr = a.lr; k.gs = a.gscale; k.sgd = a.opt_sgd;
   const float t = (float)(step + 1);
   k.rbc1 = 1.f / (1.f - powf(a.beta1, t));
   k.rbc2 = 1.f / (1.f - powf(a.beta2, t));
@@ -140,6 +143,11 @@ __device__ __forceinline__ AdamK adam_consts(AT& a, int step) {
 __device__ __forceinline__ float adam_apply(float p, float m, float v, float g, const AdamK& k, float* pp, float* mp,
                                             float* vp) {
   g *= k.gs;
+  if (k.sgd) {   // fused SGD (SGD without momentum, utils/train_state.SGD)
+    p = p - k.lr * (g + k.wd * p);
+    *pp = p;
+    return p;
+  }
   m = k.b1 * m + (1.f - k.b1) * g;
   v = k.b2 * v + (1.f - k.b2) * g * g;
   // v_rcp_f32 (1 ulp) instead of the IEEE divide's scale/fma/fixup sequence
@@ -203,9 +211,10 @@ template <bool SC1> __device__ __forceinline__ void st_b128(void* p, u32x4 v) {
 template <bool SC1>
 __device__ __forceinline__ float adam_apply_h(float p, float m, float v, float g, const AdamK& k, float* pp, float* mp,
                                               float* vp) {
-  float tp, tm, tv;
+  float tp, tm = m, tv = v;
   const float r = adam_apply(p, m, v, g, k, &tp, &tm, &tv);
-  st_f<SC1>(pp, tp); *mp = tm; *vp = tv;
+  st_f<SC1>(pp, tp);
+  if (!k.sgd) { *mp = tm; *vp = tv; }   // SGD: m / v alias p (unused)
   return r;
 }
 

@@ -41,7 +41,8 @@ class Mlp2Args(ctypes.Structure):
                 ("W1T", c_void_p), ("ldw1t", c_int), ("XT", c_void_p), ("ldxt", c_int),
                 ("step_copy", c_void_p), ("W2snap", c_void_p), ("stage_stride", ctypes.c_long),
                 ("det_logits", c_void_p),
-                ("XR", c_void_p), ("zslab", c_void_p), ("ztick", c_void_p), ("hand", c_void_p), ("lg3", c_int)]
+                ("XR", c_void_p), ("zslab", c_void_p), ("ztick", c_void_p), ("hand", c_void_p), ("lg3", c_int),
+                ("opt_sgd", c_int)]
 
 
 _lib.declare("jdt_mlp2", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_int, c_void_p])
@@ -65,6 +66,13 @@ def _is_adamw(tx) -> bool:
     from ..utils.train_state import AdamW
 
     return isinstance(tx, AdamW)
+
+
+def _is_plain_sgd(tx) -> bool:
+    """SGD without momentum: the 2-layer engine fuses it into its backward epilogue."""
+    from ..utils.train_state import SGD
+
+    return isinstance(tx, SGD) and not tx.momentum
 
 
 def set_forward_rows(rb: int):
@@ -112,9 +120,10 @@ class FusedMLP2:
         self.metrics = metrics
         if fuse_opt is None:
             fuse_opt = self.world == 1 and os.environ.get("JDT_FUSED_OPT", "1") == "1"
-        # mode 1 fuses AdamW into the backward epilogue; any other optimizer (SGD) runs
-        # mode 0 (plain-stored grads) + its own kernel
-        self.fuse_opt = bool(fuse_opt) and params is None and _is_adamw(state.tx)
+        # mode 1 fuses AdamW (or momentum-free SGD) into the backward epilogue; any other
+        # optimizer runs mode 0 (plain-stored grads) + its own kernel
+        self.opt_sgd = _is_plain_sgd(state.tx) and os.environ.get("JDT_FUSED_SGD", "0") == "1"
+        self.fuse_opt = bool(fuse_opt) and params is None and (_is_adamw(state.tx) or self.opt_sgd)
         # K-contiguous bf16 operand copies (zero K padding): X^T written by mlp2_fwd for
         # mlp2_bwd; W1^T written by mlp2_bwd's AdamW epilogue for the next mlp2_fwd
         self.Mp = (rows + 31) // 32 * 32
@@ -211,14 +220,22 @@ class FusedMLP2:
         tx = st.tx
         if self.fuse_opt:
             off = {n: P.offsets[n][0] for n in names}
-            m, v = o["m"], o["v"]
             a.pW1, a.pb1, a.pW2, a.pb2 = (P.p(n).data_ptr() for n in names)
-            a.mW1, a.mb1, a.mW2, a.mb2 = (m[off[n]:].data_ptr() for n in names)
-            a.vW1, a.vb1, a.vW2, a.vb2 = (v[off[n]:].data_ptr() for n in names)
+            if self.opt_sgd:   # no moment buffers: m / v alias p (the kernel neither uses nor writes them)
+                a.mW1, a.mb1, a.mW2, a.mb2 = a.pW1, a.pb1, a.pW2, a.pb2
+                a.vW1, a.vb1, a.vW2, a.vb2 = a.pW1, a.pb1, a.pW2, a.pb2
+                a.opt_sgd = 1
+            else:
+                m, v = o["m"], o["v"]
+                a.mW1, a.mb1, a.mW2, a.mb2 = (m[off[n]:].data_ptr() for n in names)
+                a.vW1, a.vb1, a.vW2, a.vb2 = (v[off[n]:].data_ptr() for n in names)
             a.sW1, a.sb1 = P.s(names[0]).data_ptr(), P.s(names[1]).data_ptr()
             a.sW2_0, a.sW2_1 = P.s(names[2]).data_ptr(), self.W2s1.data_ptr()
             a.sb2 = P.s(names[3]).data_ptr()
-            a.lr, a.beta1, a.beta2, a.eps, a.wd = tx.learning_rate, tx.b1, tx.b2, tx.eps, tx.weight_decay
+            if self.opt_sgd:
+                a.lr, a.beta1, a.beta2, a.eps, a.wd = tx.learning_rate, 0.0, 0.0, 0.0, tx.weight_decay
+            else:
+                a.lr, a.beta1, a.beta2, a.eps, a.wd = tx.learning_rate, tx.b1, tx.b2, tx.eps, tx.weight_decay
             a.gscale = 1.0 / self.n_mb
             a.running = self.metrics.data_ptr()
         return a

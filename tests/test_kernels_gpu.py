@@ -1045,3 +1045,35 @@ def test_pipeline_single_stage_run_ahead(monkeypatch):
     assert res["0"][2] == res["1"][2] == 8
     assert float((res["0"][0] - res["1"][0]).abs().max()) <= 3e-3
     _close(res["1"][1], res["0"][1], rtol=1e-3, atol=5e-2)
+
+
+def test_fused_sgd_matches_mode0_sgd(monkeypatch):
+    """Momentum-free SGD fused into mlp2_bwd's epilogue (opt_sgd, incl. the run-ahead
+    graphs) == mode 0 (plain-stored grads) + the standalone SGD kernel.  SGD moves
+    parameters linearly in the gradient, so the two agree to fp32 rounding."""
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
+    from jax_distributed_tuts_amd.utils.train_state import Batch, sgd
+
+    g = torch.Generator().manual_seed(4)
+    b = Batch(torch.randn(128, 784, generator=g).to(DEV), torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV))
+    monkeypatch.setenv("JDT_FUSED_SGD", "1")
+    res = {}
+    for fused in ("0", "1"):
+        monkeypatch.setenv("JDT_FUSED_OPT", fused)
+        st = init_dp(Classifier(), sgd(0.05, weight_decay=1e-4), 69, DEV)
+        tr = DataParallelTrainer(st, None, DPConfig(4, "kernel"))
+        tr.step(b)
+        assert tr.fused.fuse_opt == (fused == "1") and tr.fused.opt_sgd
+        tr.capture(b, steps_per_graph=5)
+        tr.run_steps(b, 10)
+        tr.step(b)
+        tr.finalize()
+        torch.cuda.synchronize()
+        res[fused] = (st.params.master.clone(), tr.metrics.clone(), int(st.opt_state["count"].item()),
+                      st.params.shadow.clone())
+    assert res["0"][2] == res["1"][2] == 12
+    d = (res["0"][0] - res["1"][0]).abs()
+    assert float(d.max()) <= 1e-4, float(d.max())
+    _close(res["1"][1], res["0"][1], rtol=1e-3, atol=5e-2)
+    assert float((res["0"][3].float() - res["1"][3].float()).abs().max()) <= 1e-2

@@ -122,7 +122,8 @@ class FusedMLP2:
             fuse_opt = self.world == 1 and os.environ.get("JDT_FUSED_OPT", "1") == "1"
         # mode 1 fuses AdamW (or momentum-free SGD) into the backward epilogue; any other
         # optimizer runs mode 0 (plain-stored grads) + its own kernel
-        self.opt_sgd = _is_plain_sgd(state.tx) and os.environ.get("JDT_FUSED_SGD", "0") == "1"
+        # (JDT_FUSED_SGD=0: SGD through mode 0 + the standalone SGD kernel, for A/B)
+        self.opt_sgd = _is_plain_sgd(state.tx) and os.environ.get("JDT_FUSED_SGD", "1") == "1"
         self.fuse_opt = bool(fuse_opt) and params is None and (_is_adamw(state.tx) or self.opt_sgd)
         # K-contiguous bf16 operand copies (zero K padding): X^T written by mlp2_fwd for
         # mlp2_bwd; W1^T written by mlp2_bwd's AdamW epilogue for the next mlp2_fwd

@@ -6,4 +6,4 @@ for a in "" "--num-layers 4" "--num-layers 3" "--strategy fsdp" "--strategy fsdp
   timeout -k 10 180 python bench.py --steps 300 --warmup 30 $a > gpurun_out/b.log 2>&1 || { echo "bench $a failed"; tail -20 gpurun_out/b.log; exit 3; }
   echo "== $a"; tail -1 gpurun_out/b.log | cut -c1-200; tail -1 gpurun_out/b.log >> gpurun_out/bench_all.jsonl
 done
-bash tools/gpu_multiproc_bench.sh
+bash tools/sessions/gpu_multiproc_bench.sh

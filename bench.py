@@ -100,7 +100,8 @@ def build_pp(args, dev):
         from jax_distributed_tuts_amd.parallel.pipeline_lm import build_lm_pipeline, lm_batch
 
         tr, lm_cfg = build_lm_pipeline(mesh, dev, num_microbatches=args.microbatches, comm=args.comm,
-                                       merge_single_stage=args.merge_microbatches)
+                                       merge_single_stage=args.merge_microbatches,
+                                       layer_major_single_stage=not args.microbatch_passes)
         batch = shard_batch(lm_batch(lm_cfg, global_batch=args.lm_batch, seed=1), mesh, "data")
         desc = {"model": f"transformer LM {lm_cfg.n_layers}L d{lm_cfg.d_model} h{lm_cfg.n_heads} "
                          f"ff{lm_cfg.d_ff} V{lm_cfg.vocab_size}", "global_batch": args.lm_batch,
@@ -180,6 +181,9 @@ def main():
     ap.add_argument("--microbatches", type=int, default=4)
     ap.add_argument("--merge-microbatches", action="store_true",
                     help="--strategy pp with a single stage: run the microbatches as one pass (PipeConfig.merge_single_stage)")
+    ap.add_argument("--microbatch-passes", action="store_true",
+                    help="--strategy pp --model transformer with a single stage: one forward/backward pass per "
+                         "microbatch, as a stage of a real multi-stage pipeline runs (default: layer-major)")
     ap.add_argument("--hidden-layers", type=int, default=8)
     ap.add_argument("--lm-batch", type=int, default=16)
     ap.add_argument("--num-layers", type=int, default=2)

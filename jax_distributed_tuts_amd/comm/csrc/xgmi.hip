@@ -29,8 +29,9 @@
 // instruction (common.h "system-scope payload": write-through stores, coherent
 // loads), so correctness does not depend on the MTYPE the importing GPU's IPC
 // mapping inherits, and there is no L2 write-back/invalidate on the path.  The data and tmp
-// buffers are double-buffered by epoch parity, so a call may start staging
-// while a slow peer still reads the previous call's buffers -- no trailing
+// buffers are double-buffered by the parity of a per-context call counter (every launch
+// advances it once, XgSignal::calls), so a call may start staging while a slow peer
+// still reads the previous call's buffers -- no trailing
 // barrier.  Every spin has a wall-clock timeout (s_memrealtime, 100 MHz): a
 // dead or desynchronised peer sets an error flag instead of hanging the GPU.
 //
@@ -51,7 +52,31 @@ struct XgSignal {
   unsigned flag[2][XG_MAX_BLOCKS][XG_MAX_RANKS];  // [barrier][block][src rank], written by the peers
   unsigned epoch[XG_MAX_BLOCKS];                   // calls completed by each local block
   int err;                                         // 1 = a barrier timed out
+  // local only (never touched by peers): every launch on this context advances `calls`
+  // once (its last block, by `call_ticket`); the parity of `calls` selects the
+  // data / tmp half of every unstaged call.  Per-block epoch parity cannot: a block that
+  // sat out the previous call (that call had fewer blocks) keeps a stale parity and
+  // would write the half a slow peer may still be reading after a single-barrier call
+  // (one-shot all-reduce, segmented all-gather / reduce-scatter).
+  unsigned calls;
+  unsigned call_ticket;
 };
+
+// Read the call counter (thread 0; every block reads it before the last block's ticket).
+__device__ __forceinline__ unsigned xg_calls(XgSignal* me) {
+  return __hip_atomic_load(&me->calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// End of a block's part of the call: the last block advances the call counter.
+__device__ __forceinline__ void xg_call_done(XgSignal* me) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(&me->call_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == gridDim.x - 1) {
+      __hip_atomic_store(&me->call_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&me->calls, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
 
 struct XgPeers {
   float* data[XG_MAX_RANKS];  // 2 halves of cap floats each (epoch parity)
@@ -164,13 +189,16 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
                                                         long n, long s, long slice,
                                                         long chunk, XgAdam A, int fuse, long long timeout,
                                                         int staged) {
-  __shared__ unsigned s_epoch;
+  __shared__ unsigned s_epoch, s_calls;
   const int b = blockIdx.x;
   XgSignal* me = P.sig[rank];
-  if (threadIdx.x == 0) s_epoch = me->epoch[b] + 1u;
+  if (threadIdx.x == 0) {
+    s_epoch = me->epoch[b] + 1u;
+    s_calls = xg_calls(me);
+  }
   __syncthreads();
   const unsigned epoch = s_epoch;
-  const long half = (long)((staged ? (unsigned)A.step[0] : epoch) & 1u) * cap;
+  const long half = (long)((staged ? (unsigned)A.step[0] : s_calls) & 1u) * cap;
   const long base = (long)b * chunk;
   const int nv = (int)(chunk >> 2);
   const long own_n = (n - rank * s < s) ? n - rank * s : s;  // valid length of this rank's part
@@ -210,6 +238,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
     }
     if (OP == XG_REDUCE_SCATTER) {
       if (threadIdx.x == 0) me->epoch[b] = epoch;
+      xg_call_done(me);
       return;
     }
   } else {
@@ -266,6 +295,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
       }
     }
   }
+  xg_call_done(me);
 }
 
 // ---------------------------------------------------------------------------
@@ -281,13 +311,16 @@ template <int W>
 __global__ void __launch_bounds__(XG_THREADS) xg_oneshot_kernel(XgPeers P, int rank, long cap, const float* in,
                                                                 float* out, long n, long chunk, XgAdam A, int fuse,
                                                                 long long timeout) {
-  __shared__ unsigned s_epoch;
+  __shared__ unsigned s_epoch, s_calls;
   const int b = blockIdx.x;
   XgSignal* me = P.sig[rank];
-  if (threadIdx.x == 0) s_epoch = me->epoch[b] + 1u;
+  if (threadIdx.x == 0) {
+    s_epoch = me->epoch[b] + 1u;
+    s_calls = xg_calls(me);
+  }
   __syncthreads();
   const unsigned epoch = s_epoch;
-  const long half = (long)(epoch & 1u) * cap;
+  const long half = (long)(s_calls & 1u) * cap;
   const long base = (long)b * chunk;
   const int nv = (int)(chunk >> 2);
   const unsigned long long bytes = (unsigned long long)cap * 2ull * sizeof(float);
@@ -343,6 +376,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_oneshot_kernel(XgPeers P, int r
       }
     }
   }
+  xg_call_done(me);
 }
 
 // ---------------------------------------------------------------------------
@@ -396,13 +430,16 @@ __device__ __forceinline__ int xg_find(const XgSegs& S, long j) {
 template <int W, int OP>
 __global__ void __launch_bounds__(XG_THREADS) xg_seg_kernel(XgPeers P, int rank, long cap, XgSegs S, long slice,
                                                             long chunk, int accumulate, long long timeout) {
-  __shared__ unsigned s_epoch;
+  __shared__ unsigned s_epoch, s_calls;
   const int b = blockIdx.x;
   XgSignal* me = P.sig[rank];
-  if (threadIdx.x == 0) s_epoch = me->epoch[b] + 1u;
+  if (threadIdx.x == 0) {
+    s_epoch = me->epoch[b] + 1u;
+    s_calls = xg_calls(me);
+  }
   __syncthreads();
   const unsigned epoch = s_epoch;
-  const long half = (long)(epoch & 1u) * cap;
+  const long half = (long)(s_calls & 1u) * cap;
   const long base = (long)b * chunk;
   const int nv = (int)(chunk >> 2);
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -467,6 +504,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_seg_kernel(XgPeers P, int rank,
     }
   }
   if (threadIdx.x == 0) me->epoch[b] = epoch;
+  xg_call_done(me);
 }
 
 struct XgCtx {
@@ -601,6 +639,7 @@ static long oneshot_bytes() {
   return g_oneshot_bytes;
 }
 JDT_API void jdt_xgmi_set_oneshot_bytes(long b) { g_oneshot_bytes = b; }
+JDT_API long jdt_xgmi_oneshot_bytes() { return oneshot_bytes(); }
 
 static int xg_oneshot(XgCtx* c, const float* in, float* out, long n, const XgAdam* A, long long timeout,
                       hipStream_t st) {

@@ -76,6 +76,7 @@ _lib.declare("jdt_xgmi_open", c_int, [c_void_p, c_void_p])
 _lib.declare("jdt_xgmi_allreduce", c_int, [c_void_p, c_void_p, c_void_p, c_long, ctypes.POINTER(XgAdam), c_longlong,
                                            c_void_p])
 _lib.declare("jdt_xgmi_set_oneshot_bytes", None, [c_long])
+_lib.declare("jdt_xgmi_oneshot_bytes", c_long, [])
 _lib.declare("jdt_xgmi_reduce_scatter", c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_longlong, c_void_p])
 _lib.declare("jdt_xgmi_all_gather", c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_longlong, c_void_p])
 _lib.declare("jdt_xgmi_segments", c_int, [c_void_p, ctypes.POINTER(XgSegs), c_int, c_int, c_longlong, c_void_p])
@@ -437,9 +438,36 @@ class XgmiComm:
                 torch.cuda.synchronize(dev)
                 if not self._check(self.error() or not torch.equal(full, exp), f"all-gather mismatch (n {n})"):
                     return False
+        if not self._self_test_oneshot_burst():
+            return False
         if not self._self_test_segments() or not self._self_test_dim1():
             return False
         return self._self_test_adamw()
+
+    def _self_test_oneshot_burst(self) -> bool:
+        """Back-to-back one-shot all-reduces (one barrier each, no host sync between
+        them) alternating across a block-count boundary: 8,000 floats run on 8
+        blocks, 8,200 on 9, so block 8 sits out every other call.  The buffer half
+        must still alternate per CALL (xgmi.hip XgSignal::calls): with per-block
+        parity, block 8 would overwrite words a slower peer's block 7 is still
+        reading.  Ranks start skewed."""
+        W, r, dev = self.world, self.rank, self.device
+        sizes = [8_000, 8_200] * 6
+        if max(sizes) * 4 > int(_lib.lib().jdt_xgmi_oneshot_bytes()) or max(sizes) * W > self.capacity // 2:
+            return True
+        outs, wants = [], []
+        self._skew(r + 1)
+        for it, n in enumerate(sizes):
+            base = (torch.arange(n, device=dev, dtype=torch.int64) % 61).to(torch.float32)
+            x = base * (r + 1) + it
+            wants.append(base * (W * (W + 1) // 2) + W * it)
+            if r == 0 and it % 3 == 0:
+                torch.cuda._sleep(30_000)  # rank 0 lags inside the burst
+            self.all_reduce_(x)
+            outs.append(x)
+        torch.cuda.synchronize(dev)
+        bad = self.error() or any(not torch.equal(o, w) for o, w in zip(outs, wants))
+        return self._check(bad, "one-shot burst mismatch (alternating block counts)")
 
     def _self_test_segments(self) -> bool:
         """Segmented AG / RS on the FSDP tutorial's per-rank shard lengths at N = 8

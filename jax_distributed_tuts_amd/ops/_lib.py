@@ -52,6 +52,7 @@ _SIGS = {
     "jdt_gemm_set_r": (None, [c_int]),
     "jdt_gemm_set_tune": (None, [c_int]),
     "jdt_flash_set_head": (None, [c_int]),
+    "jdt_flash_set_attn128": (None, [c_int]),
     "jdt_xent_set_rpw": (None, [c_int]),
     "jdt_gemm_set_preload": (None, [c_int]),
     "jdt_gemm_set_exact": (None, [c_int]),

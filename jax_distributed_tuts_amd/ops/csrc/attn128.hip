@@ -1,0 +1,418 @@
+// Causal / full self-attention for sequences of at most 128 tokens (the tutorial
+// LM's S = 128), head dim 64, bf16 q/k/v read in place from the fused
+// [B*S, 3*H*64] QKV activation.  Replaces flash_attn.hip's tile-streaming kernels
+// at S <= 128, where a head's whole K and V fit in registers / LDS: those kernels
+// spent their time in transposing 2-byte LDS stores (V^T, Q^T, dO^T images) and
+// one barrier pair per 64-key tile.  Here no operand is ever transposed in memory:
+//
+// forward  grid (ceil(S/16), B*H), ONE wave per workgroup, 16 queries per wave.
+//   S^T = K Q^T on MFMA with both operands loaded straight from global (a K row and
+//   a Q row are each 16 contiguous bytes per lane), exact softmax over all keys in
+//   registers (column reduction: 4 registers x 4 lane groups), then
+//   O^T = V^T P^T: P^T's accumulator layout IS the B operand of the next MFMA
+//   (cdna_hip_programming.md §3 "accumulator tile as the next MFMA's operand"; the
+//   k order inside a step is permuted, so V^T's fragment is read from a row-major
+//   LDS image of V with ds_read_b64_tr_b16 at the same permuted rows).
+// backward ONE workgroup of 8 waves per (batch, head); wave w owns keys 16w..16w+15.
+//   Q, dO, K staged row-major in LDS (plain 16-byte copies; delta = rowsum(dO * O)
+//   on the same pass).  Per pair of 16-query tiles: S = Q K^T and dP = dO V^T
+//   (K / V fragments in registers), P and dS in registers; dV^T += dO^T P and
+//   dK^T += Q^T dS take P and dS as the B operand as they stand (dO^T / Q^T by
+//   transposing LDS reads); dS also goes to an LDS image [q][key].  After one
+//   barrier, dQ^T = K^T dS^T per wave (16 queries).  dQ / dK / dV leave as 8-byte
+//   stores of 4 consecutive head dims; the fused QKV bias gradient (column sums of
+//   the stored bf16 values) is one atomic per column per wave.  Fixed summation
+//   order throughout (deterministic), no workspace, no atomics on dQ.
+#include "common.h"
+
+namespace jdt {
+
+constexpr int A_D = 64;          // head dim
+constexpr int A_S = 128;         // max sequence length
+constexpr int A_LD = A_D + 8;    // [row][64] image stride (elements): 144 B rows
+constexpr int A_DSLD = A_S + 8;  // dS image [q][key] stride
+
+// Bounded loads: a buffer resource over [base, base + bytes) returns zeros past the end
+// without a memory access or a branch.  (Guarded `ok ? load : 0` loads compile into
+// exec-masked branches with a vmcnt(0) wait at every join: serialised round trips.)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t a_rsrc(const void* base, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ bf16x8 ldb8(__amdgpu_buffer_rsrc_t r, long elem_off) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(elem_off * 2), 0, 0));
+}
+__device__ __forceinline__ u32x4 ldb16(__amdgpu_buffer_rsrc_t r, long elem_off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(elem_off * 2), 0, 0));
+}
+// sum over the 16 lanes of a DPP row (lanes 16g .. 16g+15), result in every lane (no LDS)
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror
+  return v;
+}
+// Column sums of an accumulator tile whose 16 lanes of a row are summed away: lane
+// (g, i16) of tile `dt` holds values for head dims 16 dt + 4g + e (e = 0..3); after
+// the row sums, lane i16 = e of row g adds dim 16 dt + 4g + e: one atomic
+// instruction (16 active lanes) per tile.
+__device__ __forceinline__ void colsum_atomic(float* dst, const f32x4& v, int g, int i16) {
+  const float s0 = row16_sum(v[0]), s1 = row16_sum(v[1]), s2 = row16_sum(v[2]), s3 = row16_sum(v[3]);
+  const float mine = i16 == 0 ? s0 : (i16 == 1 ? s1 : (i16 == 2 ? s2 : s3));
+  if (i16 < 4) atomicAdd(dst + 4 * g + i16, mine);
+}
+
+// Transposing fragment read from a row-major [row][A_LD] LDS image: lane l (g = l>>4,
+// i16 = l&15) receives column c0 + i16 of rows r0 + 4g .. +3 (elements 0..3) and of
+// rows r1 + 4g .. +3 (elements 4..7).  With r1 = r0 + 4 and group base r0 + 8g this
+// is the natural k order of an MFMA A/B fragment; with r1 = r0 + 16 and base
+// r0 + 4g it is the permuted order of an accumulator pair used as the other operand.
+__device__ __forceinline__ bf16x8 tr_frag(const bf16_t* img, int ld, int rowA, int rowB, int c0, int lane) {
+  typedef __attribute__((ext_vector_type(4))) short s4;
+  typedef __attribute__((address_space(3))) s4 lds_s4;
+  const int i16 = lane & 15;
+  const int col = c0 + 4 * (i16 & 3);
+  // the builtin (not inline asm): the compiler then places the lgkmcnt wait before
+  // the first use itself (no LDS-DMA is ever in flight in these kernels)
+  const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + (rowA + (i16 >> 2)) * ld + col));
+  const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + (rowB + (i16 >> 2)) * ld + col));
+  bf16x8 f;
+  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+  return f;
+}
+
+// Two accumulator tiles (rows 4g+e of tile t0 and of tile t1) as one bf16 fragment
+// in the permuted k order of tr_frag(r1 = r0 + 16).
+__device__ __forceinline__ bf16x8 pack_pair(const f32x4& a, const f32x4& b) {
+  bf16x8 f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    f[e] = (short)f2bf(a[e]);
+    f[4 + e] = (short)f2bf(b[e]);
+  }
+  return f;
+}
+
+// ------------------------------------------------------------------------ forward
+__global__ void __launch_bounds__(64) attn128_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+                                                         float* __restrict__ lse, int S, int H, float scale,
+                                                         int causal) {
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[A_S * A_LD];
+  const int lane = threadIdx.x, g = lane >> 4, i16 = lane & 15;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int d = H * A_D, ld3 = 3 * d;
+  const int q0 = blockIdx.x * 16;
+  const bf16_t* base = qkv + (long)b * S * ld3;
+  const int nk = causal ? min(S, q0 + 16) : S;  // keys this tile can see
+  const int nt = (nk + 15) >> 4;                // 16-key tiles
+  const int nks = (nk + 31) >> 5;               // 32-key PV steps (V rows staged: 32 * nks)
+
+  // issue every global load first (bounded buffer loads, zeros past the last needed
+  // row): V rows (16 B per lane, 8 rows per wave-instruction), Q^T and K fragments
+  const int nv = min(S, nks * 32);
+  const __amdgpu_buffer_rsrc_t rv = a_rsrc(base + 2 * d + h * A_D, ((long)(nv - 1) * ld3 + A_D) * 2);
+  const __amdgpu_buffer_rsrc_t rk = a_rsrc(base + d + h * A_D, ((long)(nk - 1) * ld3 + A_D) * 2);
+  const __amdgpu_buffer_rsrc_t rq = a_rsrc(base + h * A_D, ((long)(S - 1) * ld3 + A_D) * 2);
+  u32x4 vr[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) vr[i] = ldb16(rv, (long)(i * 8 + (lane >> 3)) * ld3 + (lane & 7) * 8);
+  const int qrow = q0 + i16;
+  bf16x8 qf[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) qf[ks] = ldb8(rq, (long)qrow * ld3 + ks * 32 + 8 * g);
+  bf16x8 kf[8][2];
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) kf[t][ks] = ldb8(rk, (long)(t * 16 + i16) * ld3 + ks * 32 + 8 * g);
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i < nks * 4) *reinterpret_cast<u32x4*>(Vs + (i * 8 + (lane >> 3)) * A_LD + (lane & 7) * 8) = vr[i];
+
+  // S^T (rows: keys 16t + 4g + e, column: query q0 + i16)
+  f32x4 st[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    st[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (t < nt) {
+      st[t] = mfma16x16x32(kf[t][0], qf[0], st[t]);
+      st[t] = mfma16x16x32(kf[t][1], qf[1], st[t]);
+    }
+  }
+  // exact softmax over the column
+  float mx = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int key = t * 16 + 4 * g + e;
+      const bool ok = t < nt && key < S && !(causal && key > qrow);
+      st[t][e] = ok ? st[t][e] * scale : -INFINITY;
+      mx = fmaxf(mx, st[t][e]);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float p = __expf(st[t][e] - mx);  // masked: exp(-inf) = 0 (mx is finite: key 0 is visible)
+      st[t][e] = p;
+      sum += p;
+    }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+
+  // (LDS accesses of one wave complete in order: the V image writes above land before
+  // the transposing reads below)
+  // O^T (rows: head dims 16 dt + 4g + e, column: query) = V^T P^T
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (s < nks) {
+      const bf16x8 pb = pack_pair(st[2 * s], st[2 * s + 1]);
+      bf16x8 va[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) va[dt] = tr_frag(Vs, A_LD, 32 * s + 4 * g, 32 * s + 16 + 4 * g, dt * 16, lane);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16x16x32(va[dt], pb, o[dt]);
+    }
+  }
+  if (qrow < S) {
+    const float inv = 1.f / sum;
+    bf16_t* orow = out + ((long)b * S + qrow) * d + h * A_D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      uint2 pk;
+      pk.x = (unsigned)f2bf(o[dt][0] * inv) | ((unsigned)f2bf(o[dt][1] * inv) << 16);
+      pk.y = (unsigned)f2bf(o[dt][2] * inv) | ((unsigned)f2bf(o[dt][3] * inv) << 16);
+      *reinterpret_cast<uint2*>(orow + dt * 16) = pk;
+    }
+    if (g == 0) lse[(long)bh * S + qrow] = mx + __logf(sum);
+  }
+}
+
+// ------------------------------------------------------------------------ backward
+__global__ void __launch_bounds__(512) attn128_bwd_kernel(const bf16_t* __restrict__ qkv,
+                                                          const bf16_t* __restrict__ o,
+                                                          const bf16_t* __restrict__ dout,
+                                                          const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
+                                                          float* __restrict__ dbias, int S, int H, float scale,
+                                                          int causal) {
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[A_S * A_LD];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[A_S * A_LD];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[A_S * A_LD];
+  __shared__ __attribute__((aligned(16))) bf16_t dSs[A_S * A_DSLD];
+  __shared__ float lse_s[A_S], delta_s[A_S];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i16 = lane & 15;
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int d = H * A_D, ld3 = 3 * d;
+  const int Sp = (S + 31) & ~31;  // staged rows (zero past S)
+  const bf16_t* base = qkv + (long)b * S * ld3;
+  const bf16_t* dbase = dout + (long)b * S * d;
+  const bf16_t* obase = o + (long)b * S * d;
+
+  // ---- this wave's keys: K^T / V^T B fragments (16 contiguous bytes of a row each);
+  // every load bounded (zeros past row S - 1), none behind a branch
+  const int kb = 16 * w, key = kb + i16;
+  const long qkv_bytes = ((long)(S - 1) * ld3 + 3 * d) * 2, do_bytes = (long)S * d * 2;
+  const __amdgpu_buffer_rsrc_t rqkv = a_rsrc(base, qkv_bytes);
+  const __amdgpu_buffer_rsrc_t rdo = a_rsrc(dbase, do_bytes), ro = a_rsrc(obase, do_bytes);
+  bf16x8 kf[2], vf[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    kf[ks] = ldb8(rqkv, (long)key * ld3 + d + h * A_D + ks * 32 + 8 * g);
+    vf[ks] = ldb8(rqkv, (long)key * ld3 + 2 * d + h * A_D + ks * 32 + 8 * g);
+  }
+  // ---- stage Q, dO, K (row-major) and delta: thread t owns 16-byte chunks t, t + 512
+  u32x4 cq[2], ck[2], cd[2], co[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 512 * i, r = c >> 3, col = (c & 7) * 8;
+    const long rowq = (long)r * ld3 + h * A_D + col, rowo = (long)r * d + h * A_D + col;
+    cq[i] = ldb16(rqkv, rowq);
+    ck[i] = ldb16(rqkv, rowq + d);
+    cd[i] = ldb16(rdo, rowo);
+    co[i] = ldb16(ro, rowo);
+  }
+  if (tid < A_S) lse_s[tid] = tid < S ? lse[(long)bh * S + tid] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 512 * i, r = c >> 3, col = (c & 7) * 8;
+    if (r < Sp) {
+      *reinterpret_cast<u32x4*>(Qs + r * A_LD + col) = cq[i];
+      *reinterpret_cast<u32x4*>(Ks + r * A_LD + col) = ck[i];
+      *reinterpret_cast<u32x4*>(dOs + r * A_LD + col) = cd[i];
+    }
+    const unsigned wx[4] = {cd[i].x, cd[i].y, cd[i].z, cd[i].w}, wy[4] = {co[i].x, co[i].y, co[i].z, co[i].w};
+    float dl = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      dl += bf2f((bf16_t)(wx[j] & 0xffff)) * bf2f((bf16_t)(wy[j] & 0xffff)) +
+            bf2f((bf16_t)(wx[j] >> 16)) * bf2f((bf16_t)(wy[j] >> 16));
+    // the 8 chunks of a row are 8 consecutive lanes (one half of a DPP row)
+    dl += dpp_mov<0xB1>(dl);
+    dl += dpp_mov<0x4E>(dl);
+    dl += dpp_mov<0x141>(dl);
+    if ((c & 7) == 0) delta_s[r] = dl;
+  }
+  __syncthreads();
+
+  // ---- dK, dV for this wave's 16 keys over every query tile pair that can see them
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) { dk[dt] = (f32x4){0.f, 0.f, 0.f, 0.f}; dv[dt] = dk[dt]; }
+  const int npair = Sp >> 5;
+  const bool active = kb < S;  // wave-uniform
+  const int p0 = causal ? (kb >> 5) : 0;
+  for (int p = active ? p0 : npair; p < npair; ++p) {
+    f32x4 P2[2], dS2[2];
+    float ls[2][4], dl[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int q = (2 * p + u) * 16 + 4 * g + e;
+        ls[u][e] = lse_s[q];
+        dl[u][e] = delta_s[q];
+      }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int qt = 2 * p + u;
+      bf16x8 qa[2], da[2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        qa[ks] = *reinterpret_cast<const bf16x8*>(Qs + (qt * 16 + i16) * A_LD + ks * 32 + 8 * g);
+        da[ks] = *reinterpret_cast<const bf16x8*>(dOs + (qt * 16 + i16) * A_LD + ks * 32 + 8 * g);
+      }
+      f32x4 sv = (f32x4){0.f, 0.f, 0.f, 0.f}, dp = sv;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        sv = mfma16x16x32(qa[ks], kf[ks], sv);   // S[q][key]
+        dp = mfma16x16x32(da[ks], vf[ks], dp);   // dP[q][key] = dO V^T
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int q = qt * 16 + 4 * g + e;
+        const bool ok = q < S && key < S && !(causal && key > q);
+        const float pv = __expf(ok ? sv[e] * scale - ls[u][e] : -INFINITY);
+        P2[u][e] = pv;
+        dS2[u][e] = pv * (dp[e] - dl[u][e]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dSs[((2 * p + u) * 16 + 4 * g + e) * A_DSLD + key] = f2bf(dS2[u][e]);
+    const bf16x8 pb = pack_pair(P2[0], P2[1]);
+    const bf16x8 sb = pack_pair(dS2[0], dS2[1]);
+    bf16x8 doa[4], qta[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      doa[dt] = tr_frag(dOs, A_LD, 32 * p + 4 * g, 32 * p + 16 + 4 * g, dt * 16, lane);
+      qta[dt] = tr_frag(Qs, A_LD, 32 * p + 4 * g, 32 * p + 16 + 4 * g, dt * 16, lane);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      dv[dt] = mfma16x16x32(doa[dt], pb, dv[dt]);   // dV^T[d][key] += dO^T P
+      dk[dt] = mfma16x16x32(qta[dt], sb, dk[dt]);   // dK^T[d][key] += Q^T dS
+    }
+  }
+  {
+    // dS entries this wave never wrote but dQ reads (keys past S; causal: query pairs
+    // below this wave's first) are zero
+    const int pend = active ? p0 : npair;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    for (int c = lane; c < pend * 64; c += 64)  // 2 x 16 bytes (16 keys) per row
+      *reinterpret_cast<u32x4*>(dSs + (c >> 1) * A_DSLD + kb + (c & 1) * 8) = z;
+  }
+  __syncthreads();
+
+  // ---- dQ^T[d][q] = K^T dS^T for queries 16w .. 16w + 15
+  const int qb = 16 * w;
+  if (qb < S) {
+    const int kmax = causal ? min(S, qb + 16) : S;
+    const int nks = (kmax + 31) >> 5;
+    f32x4 dq[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dq[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < nks; ++ks) {
+      const bf16x8 sb = *reinterpret_cast<const bf16x8*>(dSs + (qb + i16) * A_DSLD + 32 * ks + 8 * g);
+      bf16x8 ka[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) ka[dt] = tr_frag(Ks, A_LD, 32 * ks + 8 * g, 32 * ks + 8 * g + 4, dt * 16, lane);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16x16x32(ka[dt], sb, dq[dt]);
+    }
+    const int q = qb + i16;
+    const bool qok = q < S;
+    bf16_t* row = dqkv + ((long)b * S + q) * ld3 + h * A_D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      f32x4 r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = qok ? round_bf(dq[dt][e] * scale) : 0.f;
+      if (qok) {
+        uint2 pk;
+        pk.x = (unsigned)f2bf(r[0]) | ((unsigned)f2bf(r[1]) << 16);
+        pk.y = (unsigned)f2bf(r[2]) | ((unsigned)f2bf(r[3]) << 16);
+        *reinterpret_cast<uint2*>(row + dt * 16) = pk;
+      }
+      if (dbias) colsum_atomic(dbias + h * A_D + dt * 16, r, g, i16);  // over this wave's 16 queries
+    }
+  }
+  // ---- dK, dV: 4 consecutive head dims per lane (8-byte stores)
+  if (active) {
+    const bool kok = key < S;
+    bf16_t* row = dqkv + ((long)b * S + key) * ld3 + h * A_D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      f32x4 rk, rv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        rk[e] = kok ? round_bf(dk[dt][e] * scale) : 0.f;
+        rv[e] = kok ? round_bf(dv[dt][e]) : 0.f;
+      }
+      if (kok) {
+        uint2 pk, pv;
+        pk.x = (unsigned)f2bf(rk[0]) | ((unsigned)f2bf(rk[1]) << 16);
+        pk.y = (unsigned)f2bf(rk[2]) | ((unsigned)f2bf(rk[3]) << 16);
+        pv.x = (unsigned)f2bf(rv[0]) | ((unsigned)f2bf(rv[1]) << 16);
+        pv.y = (unsigned)f2bf(rv[2]) | ((unsigned)f2bf(rv[3]) << 16);
+        *reinterpret_cast<uint2*>(row + d + dt * 16) = pk;
+        *reinterpret_cast<uint2*>(row + 2 * d + dt * 16) = pv;
+      }
+      if (dbias) {  // over this wave's 16 keys
+        colsum_atomic(dbias + d + h * A_D + dt * 16, rk, g, i16);
+        colsum_atomic(dbias + 2 * d + h * A_D + dt * 16, rv, g, i16);
+      }
+    }
+  }
+}
+
+}  // namespace jdt
+using namespace jdt;
+
+// 1 if the S <= 128 kernels handle this shape (head dim 64 is the caller's contract)
+JDT_API int jdt_attn128_ok(int S) { return S > 0 && S <= A_S ? 1 : 0; }
+
+JDT_API int jdt_attn128_fwd(const void* qkv, void* out, float* lse, int B, int S, int H, float scale, int causal,
+                            void* stream) {
+  if (S <= 0 || S > A_S) return -2;
+  hipLaunchKernelGGL(attn128_fwd_kernel, dim3((S + 15) / 16, B * H), dim3(64), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const bf16_t*>(qkv), static_cast<bf16_t*>(out), lse, S, H, scale, causal);
+  return HIP_LAUNCH_CHECK();
+}
+
+JDT_API int jdt_attn128_bwd(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
+                            float* dbias, int B, int S, int H, float scale, int causal, void* stream) {
+  if (S <= 0 || S > A_S) return -2;
+  hipLaunchKernelGGL(attn128_bwd_kernel, dim3(B * H), dim3(512), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const bf16_t*>(qkv), static_cast<const bf16_t*>(out),
+                     static_cast<const bf16_t*>(dout), lse, static_cast<bf16_t*>(dqkv), dbias, S, H, scale, causal);
+  return HIP_LAUNCH_CHECK();
+}

@@ -572,8 +572,25 @@ __global__ void __launch_bounds__(512) flash_bwd_head_kernel(const bf16_t* __res
 }  // namespace jdt
 using namespace jdt;
 
+// S <= 128: the whole-head kernels of attn128.hip (JDT_ATTN128=0 or
+// jdt_flash_set_attn128(0): these tile-streaming kernels at every S, for A/B runs)
+JDT_API int jdt_attn128_fwd(const void* qkv, void* out, float* lse, int B, int S, int H, float scale, int causal,
+                            void* stream);
+JDT_API int jdt_attn128_bwd(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
+                            float* dbias, int B, int S, int H, float scale, int causal, void* stream);
+static int g_attn128 = -1;
+static bool attn128_on(int S) {
+  if (g_attn128 < 0) {
+    const char* e = getenv("JDT_ATTN128");
+    g_attn128 = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_attn128 && S <= 128;
+}
+JDT_API void jdt_flash_set_attn128(int on) { g_attn128 = on; }
+
 JDT_API int jdt_flash_fwd(const void* qkv, void* out, float* lse, int B, int S, int H, float scale, int causal,
                           void* stream) {
+  if (attn128_on(S)) return jdt_attn128_fwd(qkv, out, lse, B, S, H, scale, causal, stream);
   dim3 grid((S + FB - 1) / FB, B * H);
   hipLaunchKernelGGL(flash_fwd_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(stream),
                      static_cast<const bf16_t*>(qkv), static_cast<bf16_t*>(out), lse, S, H, scale, causal);
@@ -589,6 +606,7 @@ JDT_API void jdt_flash_set_head(int on) { g_flash_head = on; }  // A/B: 0 = key-
 JDT_API int jdt_flash_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* dq_acc,
                           unsigned* tickets, void* dqkv, float* dbias, int B, int S, int H, float scale, int causal,
                           void* stream) {
+  if (attn128_on(S)) return jdt_attn128_bwd(qkv, out, dout, lse, dqkv, dbias, B, S, H, scale, causal, stream);
   if (S <= FS && g_flash_head) {  // whole head in one workgroup: dq_acc / tickets untouched (stay zero)
     hipLaunchKernelGGL(flash_bwd_head_kernel, dim3(B * H), dim3(512), 0, static_cast<hipStream_t>(stream),
                        static_cast<const bf16_t*>(qkv), static_cast<const bf16_t*>(out),

@@ -813,12 +813,14 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
 using namespace jdt;
 
 int xcd_tiles_enabled();   // mlp_fused.hip (JDT_XCD_TILES)
+int xcd_roundrobin_ok(int G);   // mlp_fused.hip (XCD dispatch probe)
 
 JDT_API int jdt_md_args_size() { return (int)sizeof(MdArgs); }
 
 // 1 if the run-ahead layer-0 backward fits (its column barrier needs every workgroup resident)
 JDT_API int jdt_md_ahead_ok(int M) {
   if (M <= 0 || M > MD_MPM) return 0;
+  if (!xcd_roundrobin_ok((512 / 16) * (784 / 112))) return 0;
   int dev = 0, cus = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||

@@ -1068,10 +1068,60 @@ JDT_API int jdt_mlp2_loop(const Mlp2Args* args, int n, unsigned* ctr, unsigned* 
   return HIP_LAUNCH_CHECK();
 }
 
+// ---------------------------------------------------------------- XCD dispatch probe
+// The run-ahead tile map (common.h xcd_column_tile) is a bijection only when the
+// device deals workgroups round-robin over exactly 8 XCDs (linear id L -> XCD
+// (L + o) % 8).  A partitioned device (CPX / DPX mode: fewer XCDs per logical GPU)
+// or another part would run some tiles twice and others never.  This probe
+// launches a grid of G workgroups that each record HW_REG_XCC_ID, and the host
+// checks the assumption the tile map makes: the 8 residues L % 8 land on 8
+// distinct XCC ids, every workgroup of a residue on the same one.
+__global__ void xcd_probe_kernel(int* out) {
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+  if (threadIdx.x == 0) out[blockIdx.x] = (int)xcc;
+}
+
+// 1 if a G-workgroup launch is dealt round-robin over 8 XCDs (checked on 3 launches).
+int xcd_roundrobin_ok(int G) {
+  static int cached_g = -1, cached = 0;
+  if (G == cached_g) return cached;
+  if (G <= 0 || G % 8) return 0;
+  int ok = 1;
+  int* d = nullptr;
+  hipStream_t st = nullptr;
+  if (hipMalloc(&d, sizeof(int) * G) != hipSuccess) return 0;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) { hipFree(d); return 0; }
+  int* h = static_cast<int*>(malloc(sizeof(int) * G));
+  for (int rep = 0; rep < 3 && ok; ++rep) {
+    hipLaunchKernelGGL(xcd_probe_kernel, dim3(G), dim3(64), 0, st, d);
+    if (hipStreamSynchronize(st) != hipSuccess || hipMemcpy(h, d, sizeof(int) * G, hipMemcpyDeviceToHost) != hipSuccess) {
+      ok = 0;
+      break;
+    }
+    unsigned seen = 0;
+    for (int r = 0; r < 8 && ok; ++r) {
+      const int x = h[r];
+      if (x < 0 || x > 7 || (seen >> x) & 1u) ok = 0;
+      seen |= 1u << (x & 7);
+      for (int L = r; L < G && ok; L += 8) ok = h[L] == x;
+    }
+  }
+  free(h);
+  hipStreamDestroy(st);
+  hipFree(d);
+  cached_g = G;
+  cached = ok;
+  return ok;
+}
+JDT_API int jdt_xcd_roundrobin_ok(int G) { return xcd_roundrobin_ok(G); }
+
 // 1 if the run-ahead backward can run M rows x H hidden units here: its column-block
-// barrier needs every workgroup of the launch resident at once.  Called before capture.
+// barrier needs every workgroup of the launch resident at once, and its tile map
+// needs round-robin dispatch over 8 XCDs (probed).  Called before capture.
 JDT_API int jdt_mlp2_ahead_ok(int M, int H) {
   if (H % 128 || M <= 0 || M > 128) return 0;
+  if (!xcd_roundrobin_ok((H / 16) * (784 / 112))) return 0;
   int dev = 0, cus = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||

@@ -338,6 +338,7 @@ class AheadGraphs:
 
     def __init__(self, eng: "FusedMLP2", batch, steps_per_graph: int, pool=None):
         self.eng = eng
+        self._checked = False
         self.graphs = {}
         for S in sorted({1, int(steps_per_graph)}):
             for primed in (False, True):
@@ -353,6 +354,15 @@ class AheadGraphs:
     def replay(self, S: int):
         self.graphs[(S, bool(self.eng.ahead_primed))].replay()
         self.eng.ahead_primed = True
+        if not self._checked:
+            # the first replay (warmup) checks the run-ahead error word once, so a tile
+            # map or column barrier that failed on this device stops the run here
+            # instead of at finalize() after a whole run on wrong weights
+            self._checked = True
+            err = int(self.eng.ztick[1].item())
+            if err:
+                raise RuntimeError(f"run-ahead step failed on its first replay (error word {err}: "
+                                   "1 = tile map, 2 = column barrier timeout); rerun with JDT_MLP2_AHEAD=0")
 
 
 # ----------------------------------------------------------------------------- deep MLPs (csrc/mlp_deep.hip)

@@ -782,6 +782,50 @@ def test_flash_attention_fwd_bwd(B, S, H, causal):
     _close(o_c, o_g, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("B,S,H", [(2, 128, 8), (3, 96, 2), (1, 40, 3), (2, 17, 1), (1, 128, 1)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_attn128_vs_autograd_and_flash(B, S, H, causal):
+    """S <= 128 attention kernels (csrc/attn128.hip) against an fp32 autograd oracle,
+    the tile-streaming flash kernels, and themselves (bitwise reproducible)."""
+    from jax_distributed_tuts_amd.ops import _lib
+
+    d, Dh = H * 64, 64
+    qkv = _mk((B * S, 3 * d), torch.bfloat16, seed=71)
+    do = _mk((B * S, d), torch.bfloat16, seed=72)
+    qkv_r = qkv.float().clone().requires_grad_()
+    q2, k2, v2 = qkv_r.view(B, S, 3, H, Dh).permute(2, 0, 3, 1, 4)
+    s2 = torch.matmul(q2, k2.transpose(-1, -2)) / 8.0
+    if causal:
+        s2 = s2.masked_fill(torch.triu(torch.ones(S, S, dtype=torch.bool), 1), float("-inf"))
+    o2 = torch.matmul(torch.softmax(s2, -1), v2).permute(0, 2, 1, 3).reshape(B * S, d)
+    (o2 * do.float()).sum().backward()
+    res = {}
+    try:
+        for impl in (1, 0, 1):
+            _lib.lib().jdt_flash_set_attn128(impl)
+            o_g, lse = kern.attention_fwd(qkv.to(DEV), B, S, H, causal=causal)
+            db = torch.full((3 * d,), 0.25, device=DEV)
+            g = kern.attention_bwd(do.to(DEV), qkv.to(DEV), lse, B, S, H, o=o_g, causal=causal, dbias=db)
+            torch.cuda.synchronize()
+            if impl in res:  # second attn128 run: bitwise identical (fixed order, no atomics on dQ)
+                assert torch.equal(o_g, res[impl][0]) and torch.equal(g, res[impl][2])
+            res[impl] = (o_g, lse, g, db)
+    finally:
+        _lib.lib().jdt_flash_set_attn128(1)
+    o_n, lse_n, g_n, db_n = res[1]
+    _close(o_n, o2.detach(), rtol=2e-2, atol=2e-2)
+    _close(lse_n.view(B, H, S), torch.logsumexp(s2.detach(), -1), rtol=1e-3, atol=1e-3)
+    _close(g_n, qkv_r.grad, rtol=3e-2, atol=3e-2)
+    _close(db_n, g_n.float().sum(0) + 0.25, rtol=1e-4, atol=1e-3)
+    # relative L2 error per q / k / v block, against the old kernels' error
+    for part in range(3):
+        ref = qkv_r.grad.view(B * S, 3, d)[:, part].float().cpu()
+        e_new = float((g_n.view(B * S, 3, d)[:, part].float().cpu() - ref).norm() / ref.norm().clamp_min(1e-12))
+        e_old = float((res[0][2].view(B * S, 3, d)[:, part].float().cpu() - ref).norm() / ref.norm().clamp_min(1e-12))
+        assert e_new < 1.5 * e_old + 2e-3, (part, e_new, e_old)
+    _close(o_n, res[0][0], rtol=2e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("fused", [True, False])
 def test_fsdp_graph_replay_matches_eager(fused):
     """FSDP (world 1) captured as single- and multi-step hipGraphs == eager steps."""

@@ -131,22 +131,25 @@ class TransformerLM:
             cache = _Cache(inp=x, nseq=nseq, seed=seed, keep=keep, step=step)
         for l in self.layers:
             b = f"block_{l}"
-            h1, m1, r1 = K.layernorm_fwd(h, P.p(f"{b}/ln1/scale"), P.p(f"{b}/ln1/bias"), c.ln_eps)
-            qkv = K.gemm(h1, P.s(f"{b}/attn/qkv/kernel"), bias=P.s(f"{b}/attn/qkv/bias"))
+            # LN1 fused into the QKV projection's A operand (one launch; h1 / stats kept for backward)
+            qkv, h1, m1, r1 = K.ln_gemm(h, P.p(f"{b}/ln1/scale"), P.p(f"{b}/ln1/bias"), P.s(f"{b}/attn/qkv/kernel"),
+                                        eps=c.ln_eps, bias=P.s(f"{b}/attn/qkv/bias"))
             o, Pm = K.attention_fwd(qkv, nseq, c.seq_len, c.n_heads, causal=True)
             x2 = K.gemm(o, P.s(f"{b}/attn/out/kernel"), bias=P.s(f"{b}/attn/out/bias"), resid=h)
-            h2, m2, r2 = K.layernorm_fwd(x2, P.p(f"{b}/ln2/scale"), P.p(f"{b}/ln2/bias"), c.ln_eps)
-            z1 = torch.empty(h2.shape[0], c.d_ff, dtype=torch.bfloat16, device=h2.device)
+            z1 = torch.empty(x2.shape[0], c.d_ff, dtype=torch.bfloat16, device=x2.device)
             off = int(offset) + (l << 1)
-            u = K.gemm(h2, P.s(f"{b}/mlp/fc1/kernel"), bias=P.s(f"{b}/mlp/fc1/bias"), act="gelu", z_out=z1,
-                       keep_prob=keep, seed=seed, offset=off, step=step)
+            # LN2 fused into fc1 (bias + GELU epilogue, pre-activation z1 saved)
+            u, h2, m2, r2 = K.ln_gemm(x2, P.p(f"{b}/ln2/scale"), P.p(f"{b}/ln2/bias"), P.s(f"{b}/mlp/fc1/kernel"),
+                                      eps=c.ln_eps, bias=P.s(f"{b}/mlp/fc1/bias"), act="gelu", z_out=z1,
+                                      keep_prob=keep, seed=seed, offset=off, step=step)
             x3 = K.gemm(u, P.s(f"{b}/mlp/fc2/kernel"), bias=P.s(f"{b}/mlp/fc2/bias"), resid=x2)
             cache.blocks.append(_BlockCache(h, h1, m1, r1, qkv, o, Pm, x2, h2, m2, r2, z1, u, off))
             h = x3
         if self.has_head:
-            hf, mf, rf = K.layernorm_fwd(h, P.p("ln_f/scale"), P.p("ln_f/bias"), c.ln_eps)
+            logits, hf, mf, rf = K.ln_gemm(h, P.p("ln_f/scale"), P.p("ln_f/bias"), P.s("head/kernel"),
+                                           eps=c.ln_eps, bias=P.s("head/bias"))
             cache.xf, cache.hf, cache.mf, cache.rf = h, hf, mf, rf
-            h = K.gemm(hf, P.s("head/kernel"), bias=P.s("head/bias"))
+            h = logits
         return h, cache
 
     # ------------------------------------------------------------------ backward

@@ -38,7 +38,16 @@ class GemmArgs(ctypes.Structure):
     ]
 
 
+class LnArgs(ctypes.Structure):
+    """Mirror of ``jdt::LnArgs`` in csrc/gemm.hip (LayerNorm fused into a GEMM's A operand)."""
+
+    _fields_ = [("X", c_void_p), ("ldx", c_long), ("gamma", c_void_p), ("beta", c_void_p), ("eps", c_float),
+                ("Y", c_void_p), ("ldy", c_long), ("mean", c_void_p), ("rstd", c_void_p)]
+
+
 _SIGS = {
+    "jdt_gemm_ln": (c_int, [ctypes.POINTER(GemmArgs), ctypes.POINTER(LnArgs), c_void_p]),
+    "jdt_ln_args_size": (c_int, []),
     "jdt_gemm": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p]),
     "jdt_gemm_args_size": (c_int, []),
     "jdt_gemm_group": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_void_p, c_long, c_void_p, c_long, c_void_p]),

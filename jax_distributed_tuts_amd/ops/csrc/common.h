@@ -90,6 +90,18 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// ---------------------------------------------------------------- LayerNorm arithmetic
+// Shared by ln_fwd_kernel and the LN-prologue GEMM (gemm_ln_kernel) with explicit
+// rounding intrinsics, so hipcc's default FMA contraction cannot make the two
+// produce different bf16 values for the same row.
+__device__ __forceinline__ float ln_sq_acc(float q, float x, float mean) {
+  const float t = __fsub_rn(x, mean);
+  return __fmaf_rn(t, t, q);
+}
+__device__ __forceinline__ float ln_norm(float x, float mean, float rstd, float g, float b) {
+  return __fmaf_rn(__fmul_rn(__fsub_rn(x, mean), rstd), g, b);
+}
+
 // ---------------------------------------------------------------- Philox4x32-10
 // Counter-based RNG: the dropout mask of element `idx` under stream (seed,
 // offset) is a pure function, so the backward pass regenerates it instead of

@@ -1590,6 +1590,16 @@ static void group_launch(const GemmGroup& G, int total, bool tail, hipStream_t s
     hipLaunchKernelGGL((gemm_dma_group_kernel<3, false, TMN, TMN>), dim3(total), dim3(256), 0, st, G);
 }
 
+// groups of at least this many FLOPs launch problem by problem (JDT_GEMM_GROUP_FLOPS)
+static long g_group_max_flops = -1;
+static long group_max_flops() {
+  if (g_group_max_flops < 0) {
+    const char* e = getenv("JDT_GEMM_GROUP_FLOPS");
+    g_group_max_flops = e ? atol(e) : (1L << 30);
+  }
+  return g_group_max_flops;
+}
+
 static int gemm_dma_group(const GemmArgs* gs, int n, float* ws, long ws_floats, unsigned* counters, long n_counters,
                           hipStream_t st) {
   if (g_gemm_no_dma || n < 1 || n > GROUP_MAX) return 1;
@@ -1611,7 +1621,7 @@ static int gemm_dma_group(const GemmArgs* gs, int n, float* ws, long ws_floats, 
   // 1.3-2.3x (fc2 bwd group 82 us grouped vs 36 us as two launches); the grouped
   // grid pays off for the small microbatch problems (launch gaps dominate).
   int T = g_group_tile;
-  if (T == 0 && flops >= (1L << 30)) return 1;
+  if (T == 0 && flops >= group_max_flops()) return 1;
   if (T == 0) T = (m64 && flops >= (1L << 29)) ? 64 : 32;
   if ((T == 128 && !m128) || (T == 64 && !m64)) T = 32;
   GemmGroup G{};
@@ -1624,6 +1634,161 @@ static int gemm_dma_group(const GemmArgs* gs, int n, float* ws, long ws_floats, 
   if (T == 128) group_launch<4>(G, total, tail, st);
   else if (T == 64) group_launch<2>(G, total, tail, st);
   else group_launch<1>(G, total, tail, st);
+  return HIP_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------
+// LayerNorm fused into the A operand of a GEMM:  C = epilogue( LN(X) . W )
+// (pre-LN transformer: LN1 -> QKV projection, LN2 -> fc1, LN_f -> LM head).
+// X is [M, K] bf16 with K = 512 * NV (the model width: a whole row is one 16-byte
+// load per lane per 512 columns), W the [K, N] ("kn") bf16 weight.  Each workgroup
+// normalises its BM rows in a prologue -- one wave per row, fp32 statistics with
+// the DPP wave sums and the exact arithmetic of ln_fwd_kernel, so the bf16 values
+// are bit-identical to the unfused LayerNorm -- straight into a RESIDENT LDS image
+// of the whole BM x K A operand (the swizzled [BM][64] row images dma_frag reads);
+// only W streams through the LDS-DMA ring.  The workgroups of the first column
+// block also store Y = LN(X) and the row statistics (the backward's weight
+// gradient and LayerNorm backward read them), so the LayerNorm launch and its
+// activation round trip disappear.  W's first ring slots are issued before the
+// prologue, so their landing overlaps the row loads.
+struct LnArgs {
+  const bf16_t* X; long ldx;
+  const float* gamma; const float* beta; float eps;
+  bf16_t* Y; long ldy;          // LN(X) (bf16), written by column block 0
+  float* mean; float* rstd;     // per-row statistics (fp32), column block 0
+};
+
+template <int WM, int WN, int TM, int TN, int NV>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_ln_kernel(GemmArgs g, LnArgs L, int tiles_n, int vec) {
+  constexpr int NW = WM * WN;
+  constexpr int BM = WM * TM * 16, BN = WN * TN * 16, BK = DMA_BK, KD = 512 * NV, NKT = KD / BK;
+  constexpr int S = 3;                       // W ring slots
+  constexpr int AIMG = BM * KD;              // resident A image (bf16)
+  constexpr int BSTAGE = BN * BK;
+  constexpr int LPW = BN / (8 * NW);         // W glds per wave per slot
+  static_assert(LPW >= 1 && (S - 2) * LPW <= 63, "ring");
+  static_assert((BM * (BN + 4) + 4) * 4 <= (AIMG + S * BSTAGE) * 2, "output image fits");
+  __shared__ __attribute__((aligned(16))) bf16_t smem[AIMG + S * BSTAGE];
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  }
+  const int tmi = bid / tiles_n, tni = bid % tiles_n;
+  const int tm0 = tmi * BM, tn0 = tni * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const bf16_t* Bb = static_cast<const bf16_t*>(g.B) + tn0;  // [K][N]: k-row image
+  bf16_t* ring = smem + AIMG;
+  auto issue = [&](int kt) { stage_op<BN, true, NW>(Bb, g.ldb, kt * BK, ring + (kt % S) * BSTAGE, wid, lane); };
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s) issue(s);
+
+  // ---- LN prologue: wave wid normalises rows wid, wid + NW, ...
+  float4 ga[NV][2], be[NV][2];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int col = (v * 64 + lane) * 8;
+    ga[v][0] = *reinterpret_cast<const float4*>(L.gamma + col);
+    ga[v][1] = *reinterpret_cast<const float4*>(L.gamma + col + 4);
+    be[v][0] = *reinterpret_cast<const float4*>(L.beta + col);
+    be[v][1] = *reinterpret_cast<const float4*>(L.beta + col + 4);
+  }
+  const bool writer = tni == 0;
+  for (int r = wid; r < BM; r += NW) {
+    const int row = tm0 + r;
+    u32x4 p[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) p[v] = *reinterpret_cast<const u32x4*>(L.X + (long)row * L.ldx + (v * 64 + lane) * 8);
+    float x[NV][8];
+    float sum = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[v][2 * j] = bf2f((bf16_t)(p[v][j] & 0xffff));
+        x[v][2 * j + 1] = bf2f((bf16_t)(p[v][j] >> 16));
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += x[v][j];
+    }
+    const float mean = __fdiv_rn(wave_sum_dpp(sum), (float)KD);   // same arithmetic as ln_fwd_kernel
+    float q = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q = ln_sq_acc(q, x[v][j], mean);
+    const float rstd = rsqrtf(__fadd_rn(__fdiv_rn(wave_sum_dpp(q), (float)KD), L.eps));
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const float gg[8] = {ga[v][0].x, ga[v][0].y, ga[v][0].z, ga[v][0].w, ga[v][1].x, ga[v][1].y, ga[v][1].z, ga[v][1].w};
+      const float bb[8] = {be[v][0].x, be[v][0].y, be[v][0].z, be[v][0].w, be[v][1].x, be[v][1].y, be[v][1].z, be[v][1].w};
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a = ln_norm(x[v][2 * j], mean, rstd, gg[2 * j], bb[2 * j]);
+        const float b = ln_norm(x[v][2 * j + 1], mean, rstd, gg[2 * j + 1], bb[2 * j + 1]);
+        o[j] = (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+      }
+      // column block (v * 64 + lane) * 8 -> K sub-tile kt = v * 8 + lane / 8, chunk lane % 8
+      const int kt = v * 8 + (lane >> 3), c = lane & 7;
+      *reinterpret_cast<u32x4*>(smem + kt * (BM * BK) + r * BK + ((c ^ (r & 7)) << 3)) = o;
+      if (writer) *reinterpret_cast<u32x4*>(L.Y + (long)row * L.ldy + (v * 64 + lane) * 8) = o;
+    }
+    if (writer && lane == 0) {
+      L.mean[row] = mean;
+      L.rstd[row] = rstd;
+    }
+  }
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int kt = 0; kt < NKT; ++kt) {
+    // W slot kt landed (counted vmcnt) and, on the first pass, every wave's A-image
+    // writes are done (the wait's lgkmcnt(0) + barrier)
+    dma_wait_barrier<LPW, S - 2>(min(S - 2, NKT - 1 - kt));
+    if (kt + S - 1 < NKT) issue(kt + S - 1);
+    const bf16_t* As = smem + kt * (BM * BK);
+    const bf16_t* Bs = ring + (kt % S) * BSTAGE;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = frag_op<BM>(As, false, (wm * TM + i) * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = frag_op<BN>(Bs, true, (wn * TN + j) * 16, kk, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(af[i]));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(bfr[j]));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
+    }
+  }
+  __syncthreads();
+  if (vec)
+    gemm_finish_vec<BM, BN, TM, TN, 64 * NW>(g, acc, tm0, tn0, 0, wm, wn, lane, tid, 1, 0, 0, nullptr, nullptr,
+                                             reinterpret_cast<float*>(smem));
+  else if constexpr (NW == 4)
+    gemm_finish<BM, BN, TM, TN>(g, acc, tm0, tn0, 0, wid, wm, wn, lane, tid, 1, 0, 0, nullptr, nullptr,
+                                reinterpret_cast<int*>(smem));
+}
+
+template <int WM, int WN, int TM, int TN, int NV>
+static int launch_ln(const GemmArgs& g, const LnArgs& L, hipStream_t st) {
+  constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
+  if (g.M % BM || g.N % BN) return -2;
+  const int tiles_n = g.N / BN;
+  const int vec = epi_vec_ok(g, 1);
+  hipLaunchKernelGGL((gemm_ln_kernel<WM, WN, TM, TN, NV>), dim3((g.M / BM) * tiles_n), dim3(64 * WM * WN), 0, st, g, L,
+                     tiles_n, vec);
   return HIP_LAUNCH_CHECK();
 }
 }  // namespace jdt
@@ -1671,6 +1836,25 @@ JDT_API int jdt_gemm(const GemmArgs* ga, int batch, int cfg, int splits, float* 
 }
 
 JDT_API int jdt_gemm_args_size() { return (int)sizeof(GemmArgs); }
+JDT_API int jdt_ln_args_size() { return (int)sizeof(LnArgs); }
+
+// C = epilogue(LN(X) . W) with LN(X) and its row statistics also stored (see
+// gemm_ln_kernel).  X [M, K] bf16 (K in {512, 1024}, rows 16-byte aligned), W
+// [K, N] bf16 "kn"; M % 32 == 0, N % 64 == 0.  Returns -2 outside that envelope.
+JDT_API int jdt_gemm_ln(const GemmArgs* ga, const LnArgs* la, void* stream) {
+  const GemmArgs& g = *ga;
+  const LnArgs& L = *la;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (g.a_f32 || g.b_f32 || !g.b_trans || g.accumulate || g.Zin || g.zin > 1 || (g.K != 512 && g.K != 1024) ||
+      g.M % 32 || g.N % 64 || !al(L.X) || !al(L.Y) || !al(g.B) || L.ldx % 8 || L.ldy % 8 || g.ldb % 8 ||
+      !al(L.gamma) || !al(L.beta))
+    return -2;
+  const long t64 = (long)(g.M / 64) * (g.N / 64);
+  const bool big = g.M % 64 == 0 && t64 >= 512;   // 64 x 64 tiles (88 KB LDS) once they fill the chip twice
+  if (g.K == 512) return big ? launch_ln<2, 2, 2, 2, 1>(g, L, st) : launch_ln<2, 2, 1, 2, 1>(g, L, st);
+  return launch_ln<2, 2, 1, 2, 2>(g, L, st);
+}
 
 // n GEMMs (no batch) in one launch; 1 = not eligible (launch them one by one).
 JDT_API int jdt_gemm_group(const GemmArgs* gs, int n, float* ws, long ws_floats, unsigned* counters, long n_counters,

@@ -52,16 +52,16 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += v[c][j];
   }
-  const float mean = wave_sum_dpp(s) / d;
+  const float mean = __fdiv_rn(wave_sum_dpp(s), (float)d);
   float q = 0.f;
 #pragma unroll
   for (int c = 0; c < NV; ++c) {
     const int col = (c * 64 + lane) * 8;
     if (col < d)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { const float t = v[c][j] - mean; q += t * t; }
+      for (int j = 0; j < 8; ++j) q = ln_sq_acc(q, v[c][j], mean);
   }
-  const float rstd = rsqrtf(wave_sum_dpp(q) / d + eps);
+  const float rstd = rsqrtf(__fadd_rn(__fdiv_rn(wave_sum_dpp(q), (float)d), eps));
   if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
 #pragma unroll
   for (int c = 0; c < NV; ++c) {
@@ -73,8 +73,8 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
       u32x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float a = (v[c][2 * j] - mean) * rstd * gg[2 * j] + bb[2 * j];
-        const float b = (v[c][2 * j + 1] - mean) * rstd * gg[2 * j + 1] + bb[2 * j + 1];
+        const float a = ln_norm(v[c][2 * j], mean, rstd, gg[2 * j], bb[2 * j]);
+        const float b = ln_norm(v[c][2 * j + 1], mean, rstd, gg[2 * j + 1], bb[2 * j + 1]);
         o[j] = (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
       }
       *reinterpret_cast<u32x4*>(y + (long)row * d + col) = o;

@@ -13,6 +13,7 @@ optimizer state are fp32.
 from __future__ import annotations
 
 import contextlib
+import os
 import ctypes
 from typing import Optional
 
@@ -665,6 +666,53 @@ def layernorm_fwd(x, gamma, beta, eps=1e-6):
                                _lib.stream_ptr())
     _lib.check(rc, "jdt_ln_fwd")
     return y, mean, rstd
+
+
+_LN_GEMM = os.environ.get("JDT_LN_GEMM", "1") != "0"
+
+
+def ln_gemm(x, gamma, beta, w, *, eps=1e-6, bias=None, act: str = "none", z_out=None, keep_prob: float = 1.0,
+            seed: int = 0, offset: int = 0, step=None):
+    """``gemm(LN(x), w, ...)`` with the LayerNorm fused into the GEMM's A operand
+    (csrc/gemm.hip ``gemm_ln_kernel``): returns (C, y = LN(x) bf16, mean, rstd) --
+    the same values as ``layernorm_fwd`` followed by ``gemm`` (bit-identical y),
+    one launch instead of two.  ``w`` is the [K, N] ("kn") bf16 weight.  Shapes
+    outside the fused kernel's envelope (or JDT_LN_GEMM=0, or CPU) run the two ops."""
+    T, d = x.shape
+    N = w.shape[-1]
+    if _is_gpu(x) and _LN_GEMM and w.dtype == torch.bfloat16 and x.dtype == torch.bfloat16:
+        y = torch.empty_like(x)
+        mean = torch.empty(T, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(T, dtype=torch.float32, device=x.device)
+        out = torch.empty(T, N, dtype=torch.bfloat16, device=x.device)
+        g = _lib.GemmArgs()
+        g.A, g.lda = y.data_ptr(), y.stride(0)
+        g.B, g.ldb, g.b_trans = w.data_ptr(), w.stride(0), 1
+        g.M, g.N, g.K, g.alpha = T, N, d, 1.0
+        if bias is not None:
+            assert bias.is_contiguous()
+            g.bias, g.bias_f32 = bias.data_ptr(), int(bias.dtype == torch.float32)
+        g.act = ACT[act]
+        if z_out is not None:
+            assert z_out.dtype == torch.bfloat16 and z_out.stride(-1) == 1
+            g.Zout, g.ldz = z_out.data_ptr(), z_out.stride(0)
+        g.keep_prob, g.seed, g.offset = float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1)
+        g.C, g.ldc = out.data_ptr(), out.stride(0)
+        if step is not None:
+            assert step.dtype == torch.int32
+            g.step_ptr = step.data_ptr()
+        L = _lib.LnArgs()
+        L.X, L.ldx = x.data_ptr(), x.stride(0)
+        L.gamma, L.beta, L.eps = gamma.data_ptr(), beta.data_ptr(), float(eps)
+        L.Y, L.ldy, L.mean, L.rstd = y.data_ptr(), y.stride(0), mean.data_ptr(), rstd.data_ptr()
+        assert x.stride(1) == 1 and w.stride(1) == 1 and gamma.dtype == beta.dtype == torch.float32
+        rc = _lib.lib().jdt_gemm_ln(ctypes.byref(g), ctypes.byref(L), _lib.stream_ptr())
+        if rc != -2:
+            _lib.check(rc, "jdt_gemm_ln")
+            return out, y, mean, rstd
+    y, mean, rstd = layernorm_fwd(x, gamma, beta, eps)
+    out = gemm(y, w, bias=bias, act=act, z_out=z_out, keep_prob=keep_prob, seed=seed, offset=offset, step=step)
+    return out, y, mean, rstd
 
 
 def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None, dsum=None):

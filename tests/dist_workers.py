@@ -187,7 +187,10 @@ def _clone(d):
     return {k: v.detach().clone() for k, v in d.items()}
 
 
-def grad_probe(out_dir, kind, accum="loop", gather_once=False, dp=1, n_hidden=3):
+LM_PROBE_CFG = dict(vocab_size=64, d_model=64, n_heads=4, d_ff=128, seq_len=16, n_layers=4)
+
+
+def grad_probe(out_dir, kind, accum="loop", gather_once=False, dp=1, n_hidden=3, num_layers=2, n_mb=4):
     """ONE plain-SGD (lr 1) step of a strategy, dropout off; saves the parameters
     before and after, so the test reads the applied gradient p0 - p1 exactly
     (tests/oracle.py)."""
@@ -200,9 +203,22 @@ def grad_probe(out_dir, kind, accum="loop", gather_once=False, dp=1, n_hidden=3)
 
     cfg = dp_config()
     batch_full = synthetic_batch(cfg, 70)
+    if kind == "dp_drop4":
+        # throwaway fault: rank 0's first minibatch loses its first 4-row group
+        orig, calls = K.softmax_xent, [0]
+
+        def dropped(logits, labels, *, dlogits=None, **kw):
+            calls[0] += 1
+            if D.rank() != 0 or calls[0] != 1:
+                return orig(logits, labels, dlogits=dlogits, **kw)
+            dlogits[:4].zero_()
+            return orig(logits[4:], labels[4:], dlogits=dlogits[4:], **kw)
+
+        K.softmax_xent = dropped
+        kind = "dp"
     if kind in ("dp", "dp_no_inv_n"):
         mesh = Mesh({"data": D.world_size()})
-        st = init_dp(Classifier(dropout_rate=0.0), sgd(1.0), 69, "cpu", mesh)
+        st = init_dp(Classifier(dropout_rate=0.0, num_layers=num_layers), sgd(1.0), 69, "cpu", mesh)
         cls = DataParallelTrainer
         if kind == "dp_no_inv_n":
             class _NoInvN(DataParallelTrainer):  # deliberately drops the 1/N of pmean
@@ -219,7 +235,7 @@ def grad_probe(out_dir, kind, accum="loop", gather_once=False, dp=1, n_hidden=3)
         from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
 
         mesh = Mesh({"data": D.world_size()})
-        st = init_fsdp(Classifier(dropout_rate=0.0), sgd(1.0), 69, "cpu", mesh, "data", 16)
+        st = init_fsdp(Classifier(dropout_rate=0.0, num_layers=num_layers), sgd(1.0), 69, "cpu", mesh, "data", 16)
         tr = FSDPTrainer(st, mesh, FSDPConfig(4, 16, "data", gather_once=gather_once, scatter_once=gather_once))
         before = _clone(tr.full_params())
         tr.step(shard_batch(batch_full, mesh, "data"))
@@ -228,10 +244,20 @@ def grad_probe(out_dir, kind, accum="loop", gather_once=False, dp=1, n_hidden=3)
         from pipeline_parallel import build_mlp_pipeline
 
         mesh = Mesh({"data": dp, "pipe": D.world_size() // dp})
-        tr = build_mlp_pipeline(cfg, mesh, "cpu", n_hidden_layers=n_hidden, dropout_rate=0.0, num_microbatches=4,
-                                tx=sgd(1.0))
+        tr = build_mlp_pipeline(cfg, mesh, "cpu", n_hidden_layers=n_hidden, dropout_rate=0.0,
+                                num_microbatches=n_mb, tx=sgd(1.0))
         before = _clone(tr.state.params.state_dict())
         tr.step(shard_batch(batch_full, mesh, "data"))
+        after = _clone(tr.state.params.state_dict())
+    elif kind == "pp_lm":
+        from jax_distributed_tuts_amd.models.transformer import TransformerConfig
+        from jax_distributed_tuts_amd.parallel.pipeline_lm import build_lm_pipeline, lm_batch
+
+        lm_cfg = TransformerConfig(**LM_PROBE_CFG)
+        mesh = Mesh({"data": dp, "pipe": D.world_size() // dp})
+        tr, _ = build_lm_pipeline(mesh, "cpu", lm_cfg, num_microbatches=n_mb, tx=sgd(1.0))
+        before = _clone(tr.state.params.state_dict())
+        tr.step(shard_batch(lm_batch(lm_cfg, global_batch=2 * n_mb * dp, seed=5), mesh, "data"))
         after = _clone(tr.state.params.state_dict())
     else:
         raise ValueError(kind)

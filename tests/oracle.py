@@ -46,6 +46,41 @@ def mlp_grads_fp64(params: Dict[str, torch.Tensor], names: Sequence[str], x: tor
     return {k: v.grad.detach() for k, v in P.items()}
 
 
+def lm_grads_fp64(params: Dict[str, torch.Tensor], cfg, tok: torch.Tensor, labels: torch.Tensor) -> Dict[str, torch.Tensor]:
+    """d/dparams of the mean next-token CE over every token of the global batch for
+    the pre-LN decoder LM of models/transformer.py (learned positions, causal
+    attention, GELU-tanh MLP, untied head), float64 torch autograd.  With equal
+    microbatches and data shards this is the mean over microbatches and replicas
+    the GPipe / DP x PP trainers apply."""
+    import math
+
+    ps = {n: t.detach().double().clone().requires_grad_(True) for n, t in params.items()}
+    B, S = tok.shape
+    d, H = cfg.d_model, cfg.n_heads
+    Dh = d // H
+
+    def ln(x, g, b):
+        return torch.nn.functional.layer_norm(x, (d,), g, b, eps=cfg.ln_eps)
+
+    x = (ps["embed/wte"][tok.long()] + ps["embed/wpe"][None]).reshape(B * S, d)
+    for l in range(cfg.n_layers):
+        b = f"block_{l}"
+        h = ln(x, ps[f"{b}/ln1/scale"], ps[f"{b}/ln1/bias"])
+        qkv = h @ ps[f"{b}/attn/qkv/kernel"] + ps[f"{b}/attn/qkv/bias"]
+        q, k, v = qkv.view(B, S, 3, H, Dh).permute(2, 0, 3, 1, 4)
+        sc = (q @ k.transpose(-1, -2)) / math.sqrt(Dh)
+        sc = sc.masked_fill(torch.triu(torch.ones(S, S, dtype=torch.bool), 1), float("-inf"))
+        o = (torch.softmax(sc, -1) @ v).permute(0, 2, 1, 3).reshape(B * S, d)
+        x = x + o @ ps[f"{b}/attn/out/kernel"] + ps[f"{b}/attn/out/bias"]
+        h2 = ln(x, ps[f"{b}/ln2/scale"], ps[f"{b}/ln2/bias"])
+        u = torch.nn.functional.gelu(h2 @ ps[f"{b}/mlp/fc1/kernel"] + ps[f"{b}/mlp/fc1/bias"], approximate="tanh")
+        x = x + u @ ps[f"{b}/mlp/fc2/kernel"] + ps[f"{b}/mlp/fc2/bias"]
+    hf = ln(x, ps["ln_f/scale"], ps["ln_f/bias"])
+    logits = hf @ ps["head/kernel"] + ps["head/bias"]
+    torch.nn.functional.cross_entropy(logits, labels.reshape(-1).long()).backward()
+    return {n: t.grad.detach() for n, t in ps.items()}
+
+
 def check_grad(got: torch.Tensor, want: torch.Tensor, name: str = "", rel_tol: float = 0.05,
                scale_tol: float = 0.03):
     """Engine gradient (bf16 matmul operands, fp32 accumulate) vs the fp64 oracle:

@@ -156,3 +156,117 @@ def test_selftest_verdict_is_collective(tmp_path):
     for r in _load(str(tmp_path), "verdict", 3):
         assert r["seen"] == [True, True, False]
         assert r["total"] == 9.0
+
+
+# ----------------------------------------------------------------------------- the BASELINE world size: 8 ranks
+# Every BASELINE GPU config is 8-way (/root/reference/util.py:31-38 simulates 8
+# devices); these gloo probes pin the exact layouts' applied gradients against the
+# fp64 oracle: DP8 (16 rows per rank, 4 rows per minibatch), FSDP8 (98-row W1
+# shards), an 8-stage GPipe MLP and the DP=2 x PP=4 transformer.
+def _max_err(got, want):
+    from .oracle import check_grad as _cg
+
+    return max(_cg(got[k], want[k], k, rel_tol=TOL_REL, scale_tol=TOL_SCALE) for k in want)
+
+
+# measured worst case over these probes (bf16 matmul operands, fp32 accumulate): rel L2
+# error <= 1.4e-2 (the transformer; MLPs <= 1.1e-2) and |scale - 1| <= 2e-3 (printed by
+# the tests with -s); pinned at ~2x.
+# A dropped 4-row minibatch group moves the gradient by ~3 %, a missing 1/N by 50 %.
+TOL_REL, TOL_SCALE = 0.03, 0.005
+
+
+def _check_tight(got, want, tag):
+    worst_rel, worst_scale = 0.0, 0.0
+    for k in sorted(want):
+        rel, scale = check_grad(got[k], want[k], f"{tag}:{k}", rel_tol=TOL_REL, scale_tol=TOL_SCALE)
+        worst_rel, worst_scale = max(worst_rel, rel), max(worst_scale, abs(scale - 1))
+    print(f"[{tag}] worst rel {worst_rel:.2e}, worst |scale-1| {worst_scale:.2e}")
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("num_layers,accum", [(2, "loop"), (2, "fused"), (4, "loop")])
+def test_dp8_sgd_grad_matches_fp64(tmp_path, num_layers, accum):
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+
+    spawn(functools.partial(W.grad_probe, kind="dp", accum=accum, num_layers=num_layers), 8, str(tmp_path))
+    res = _load(tmp_path, "probe_dp", 8)
+    b = _batch()
+    names = Classifier(num_layers=num_layers).names
+    want = mlp_grads_fp64(res[0]["before"], names, b.inputs, b.labels, n_mb=4)
+    for o in res:
+        _check_tight(sgd_grads(o["before"], o["after"]), want, f"dp8 L{num_layers} {accum}")
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("num_layers,gather_once", [(2, False), (2, True), (4, False)])
+def test_fsdp8_sgd_grad_matches_fp64(tmp_path, num_layers, gather_once):
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+
+    spawn(functools.partial(W.grad_probe, kind="fsdp", gather_once=gather_once, num_layers=num_layers), 8,
+          str(tmp_path))
+    res = _load(tmp_path, "probe_fsdp", 8)
+    b = _batch()
+    names = Classifier(num_layers=num_layers).names
+    want = mlp_grads_fp64(res[0]["before"], names, b.inputs, b.labels, n_mb=4)
+    for o in res:
+        _check_tight(sgd_grads(o["before"], o["after"]), want, f"fsdp8 L{num_layers} once={gather_once}")
+
+
+def _stage_union(res):
+    before, got = {}, {}
+    for o in res:
+        before.update(o["before"])
+        for k, v in sgd_grads(o["before"], o["after"]).items():
+            if k in got:  # the other data replica of the same stage: identical
+                torch.testing.assert_close(v, got[k], rtol=0, atol=0)
+            got[k] = v
+    return before, got
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("n_mb", [4, 16])
+def test_pp8_mlp_sgd_grad_matches_fp64(tmp_path, n_mb):
+    """BASELINE config #4: 784-512x8-10 over 8 GPipe stages (9 Dense layers)."""
+    from pipeline_parallel import pp_mlp_dims
+    from jax_distributed_tuts_amd.models.mlp import MLP
+    from jax_distributed_tuts_amd.utils.config import dp_config
+
+    spawn(functools.partial(W.grad_probe, kind="pp", dp=1, n_hidden=8, n_mb=n_mb), 8, str(tmp_path))
+    before, got = _stage_union(_load(tmp_path, "probe_pp", 8))
+    model = MLP(pp_mlp_dims(dp_config(), 8), dropout_rate=0.0)
+    b = _batch()
+    want = mlp_grads_fp64(before, model.names, b.inputs, b.labels, n_mb=n_mb)
+    assert set(got) == set(want)
+    _check_tight(got, want, f"pp8 mb{n_mb}")
+
+
+@pytest.mark.slow
+def test_dp2_pp4_transformer_sgd_grad_matches_fp64(tmp_path):
+    """BASELINE config #5's layout: 4-layer LM, DP=2 x PP=4 (one block per stage,
+    embedding on stage 0, LN_f + head on stage 3), 4 microbatches per replica."""
+    from jax_distributed_tuts_amd.models.transformer import TransformerConfig
+    from jax_distributed_tuts_amd.parallel.pipeline_lm import lm_batch
+
+    from .oracle import lm_grads_fp64
+
+    spawn(functools.partial(W.grad_probe, kind="pp_lm", dp=2, n_mb=4), 8, str(tmp_path))
+    before, got = _stage_union(_load(tmp_path, "probe_pp_lm", 8))
+    cfg = TransformerConfig(**W.LM_PROBE_CFG)
+    b = lm_batch(cfg, global_batch=2 * 4 * 2, seed=5)
+    want = lm_grads_fp64(before, cfg, b.inputs, b.labels)
+    assert set(got) == set(want)
+    _check_tight(got, want, "dp2xpp4 lm")
+
+
+@pytest.mark.slow
+def test_tight_oracle_detects_dropped_row_group(tmp_path):
+    """The pinned tolerances catch a fault confined to ONE 4-row group of one
+    minibatch on one of 8 ranks (1/32 of a rank's rows, 1/128 of the batch)."""
+    spawn(functools.partial(W.grad_probe, kind="dp_drop4"), 8, str(tmp_path))
+    res = _load(tmp_path, "probe_dp", 8)
+    b = _batch()
+    want = mlp_grads_fp64(res[0]["before"], CLS, b.inputs, b.labels, n_mb=4)
+    with pytest.raises(AssertionError, match=r"rel err .*scale") as ei:
+        _check_tight(sgd_grads(res[0]["before"], res[0]["after"]), want, "dp8 drop4")
+    print("[dp8 drop4] caught:", ei.value)

@@ -782,6 +782,36 @@ def test_flash_attention_fwd_bwd(B, S, H, causal):
     _close(o_c, o_g, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("M,K,N,act", [(2048, 512, 1536, "none"), (512, 512, 2048, "gelu"), (256, 512, 1536, "none"),
+                                        (96, 1024, 128, "gelu"), (40, 512, 64, "none")])
+def test_ln_gemm_matches_layernorm_then_gemm(M, K, N, act):
+    """LayerNorm fused into the GEMM A operand (gemm_ln_kernel) == ln_fwd + gemm:
+    LN(x) and its statistics bit-identical, C within bf16 rounding (M = 40 takes the
+    two-launch fallback)."""
+    g = torch.Generator().manual_seed(5)
+    x = (torch.randn(M, K, generator=g) * 2 + 0.5).to(torch.bfloat16).to(DEV)
+    gamma = (1 + 0.1 * torch.randn(K, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(K, generator=g)).to(DEV)
+    w = (torch.randn(K, N, generator=g) / K ** 0.5).to(torch.bfloat16).to(DEV)
+    bias = (0.1 * torch.randn(N, generator=g)).to(torch.bfloat16).to(DEV)
+    z = torch.empty(M, N, dtype=torch.bfloat16, device=DEV) if act != "none" else None
+    c, y, mean, rstd = kern.ln_gemm(x, gamma, beta, w, eps=1e-6, bias=bias, act=act, z_out=z)
+    y_r, m_r, r_r = kern.layernorm_fwd(x, gamma, beta, 1e-6)
+    z_r = torch.empty_like(z) if z is not None else None
+    c_r = kern.gemm(y_r, w, bias=bias, act=act, z_out=z_r)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_r) and torch.equal(mean, m_r) and torch.equal(rstd, r_r)
+    _close(c, c_r, rtol=1e-2, atol=1e-2)
+    if z is not None:
+        _close(z, z_r, rtol=1e-2, atol=1e-2)
+    # against fp32 torch
+    ref = torch.nn.functional.layer_norm(x.float(), (K,), gamma, beta, 1e-6).to(torch.bfloat16).float() @ w.float()
+    ref = ref + bias.float()
+    if act == "gelu":
+        ref = torch.nn.functional.gelu(ref, approximate="tanh")
+    _close(c, ref, rtol=2e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("B,S,H", [(2, 128, 8), (3, 96, 2), (1, 40, 3), (2, 17, 1), (1, 128, 1)])
 @pytest.mark.parametrize("causal", [True, False])
 def test_attn128_vs_autograd_and_flash(B, S, H, causal):

@@ -158,6 +158,16 @@ def comm_sweep(tr, dev, iters: int = 20):
     return out
 
 
+def _comm_choice():
+    """The per-size transport calibration of this rank's xGMI context (comm/xgmi.py
+    ``calibrate``): one-shot threshold, RCCL availability, per-size timings and choice."""
+    try:
+        from jax_distributed_tuts_amd.comm import xgmi
+    except Exception:
+        return None
+    return xgmi.LAST_CALIBRATION
+
+
 def pick_steps_per_graph(steps: int, cap: int) -> int:
     """Steps per captured graph: all of them when steps <= cap (one replay, one host
     launch for the whole timed region), else the largest divisor of steps <= cap
@@ -299,7 +309,8 @@ def main():
                            "comm": getattr(tr, "comm_backend", None) or D.backend() or "none",
                            "process_group": D.backend() or "none",
                            "xgmi_selftest": getattr(tr, "xgmi_status", "n/a"),
-                           "collective_ms_p50": coll_ms, "comm_sweep": sweep}}
+                           "collective_ms_p50": coll_ms, "comm_sweep": sweep,
+                           "comm_choice": _comm_choice()}}
         print(json.dumps(out), flush=True)
     D.shutdown()
 

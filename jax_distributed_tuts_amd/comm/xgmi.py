@@ -605,6 +605,81 @@ class XgmiComm:
         return True
 
 
+# ----------------------------------------------------------------------------- transport choice per size
+CALIBRATION_LADDER = (1024, 4096, 16384, 65536, 262144)   # floats: 4 KiB .. 1 MiB
+
+
+def _max_over(group, v: float, device) -> float:
+    t = torch.tensor([v], dtype=torch.float64, device=device if dist.get_backend(group) == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def calibrate(comm: XgmiComm, sizes, iters: int = 20, rccl_margin_us: float = 3.0) -> dict:
+    """Time this node's transports at the message sizes the trainer issues (SURVEY
+    §5.8 (c)): the xGMI one-shot and two-shot all-reduce kernels and, when the group
+    is nccl, RCCL's all-reduce -- each the median device time of ``iters`` calls,
+    the MAX over ranks (every rank runs the same sequence).  Then
+      * the one-shot threshold becomes the measured crossover (the largest ladder
+        size where one-shot <= two-shot), replacing the 256 KiB default;
+      * for each trainer size, ``choice`` is "xgmi" unless RCCL beats the better
+        xGMI kernel by more than ``rccl_margin_us`` (the xGMI kernels also carry
+        the fused AdamW / metrics fold that RCCL would need an extra launch for).
+    Returns the table (bench JSON ``comm_choice``); ``rccl_us`` is None where RCCL is
+    unavailable (gloo bootstrap: ranks sharing one GPU)."""
+    L = _lib.lib()
+    dev = comm.device
+    rccl = dist.get_backend(comm.group) == "nccl"
+    cap = comm.capacity - 4 * 96 * comm.world
+    ladder = sorted({int(n) for n in tuple(CALIBRATION_LADDER) + tuple(sizes) if 0 < int(n) <= cap // 2})
+    big = 1 << 40
+
+    def timed(fn) -> float:
+        fn()
+        torch.cuda.synchronize(dev)
+        dist.barrier(group=comm.group)
+        ts = []
+        for _ in range(iters):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            b.synchronize()
+            ts.append(a.elapsed_time(b) * 1e3)
+        ts.sort()
+        return _max_over(comm.group, ts[len(ts) // 2], dev)
+
+    rows = []
+    old = int(L.jdt_xgmi_oneshot_bytes())
+    try:
+        with torch.cuda.device(dev):
+            for n in ladder:
+                x = torch.ones(n, device=dev)
+                L.jdt_xgmi_set_oneshot_bytes(big)
+                one = timed(lambda: comm.all_reduce_(x))
+                L.jdt_xgmi_set_oneshot_bytes(0)
+                two = timed(lambda: comm.all_reduce_(x))
+                rc = timed(lambda: dist.all_reduce(x, group=comm.group)) if rccl else None
+                rows.append({"bytes": 4 * n, "xgmi_oneshot_us": round(one, 2), "xgmi_twoshot_us": round(two, 2),
+                             "rccl_us": None if rc is None else round(rc, 2)})
+    finally:
+        L.jdt_xgmi_set_oneshot_bytes(old)
+    if comm.error():
+        raise RuntimeError("xgmi collective timed out during calibration")
+    cross = 0
+    for r in rows:
+        if r["xgmi_oneshot_us"] <= r["xgmi_twoshot_us"]:
+            cross = r["bytes"]
+    L.jdt_xgmi_set_oneshot_bytes(cross)
+    want = {4 * int(n) for n in sizes}
+    for r in rows:
+        best = min(r["xgmi_oneshot_us"], r["xgmi_twoshot_us"])
+        r["choice"] = ("rccl" if r["rccl_us"] is not None and r["rccl_us"] + rccl_margin_us < best else "xgmi")
+        r["trainer_size"] = r["bytes"] in want
+    return {"oneshot_threshold_bytes": cross, "rccl": "available" if rccl else "unavailable (gloo group)",
+            "table": rows}
+
+
 def status(comm: Optional[XgmiComm], world: int, device, mode: str = "auto") -> str:
     """What a trainer's N>1 transport ended up being, for logs and the bench JSON:
     ``passed`` (xGMI kernels, self-test passed on every rank), ``failed->rccl``
@@ -616,8 +691,18 @@ def status(comm: Optional[XgmiComm], world: int, device, mode: str = "auto") -> 
     return "failed->rccl" if requested(mode, world, torch.device(device)) else "off"
 
 
-def create_for(mesh, axis: str, cap_floats: int, device: torch.device, mode: str = "auto") -> Optional[XgmiComm]:
-    """An ``XgmiComm`` over ``mesh``'s ``axis`` group, or None (RCCL fallback)."""
+LAST_CALIBRATION: Optional[dict] = None   # this process's most recent calibrate() table (bench JSON)
+
+
+def create_for(mesh, axis: str, cap_floats: int, device: torch.device, mode: str = "auto",
+               sizes: Optional[list] = None) -> Optional[XgmiComm]:
+    """An ``XgmiComm`` over ``mesh``'s ``axis`` group, or None (RCCL fallback).
+
+    After the self-test the transports are timed at ``sizes`` (floats; default: the
+    capacity requested, i.e. the trainer's bucket) -- :func:`calibrate` -- unless
+    ``JDT_XGMI_CALIBRATE=0``; in "auto" mode the trainer gets RCCL (None) when RCCL
+    wins at its largest size by more than the fused kernels' margin."""
+    global LAST_CALIBRATION
     from ..runtime.dist import is_initialized
 
     n = mesh.axis_size(axis) if mesh is not None else 1
@@ -629,4 +714,15 @@ def create_for(mesh, axis: str, cap_floats: int, device: torch.device, mode: str
             raise RuntimeError("xgmi collectives requested but unavailable on this node")
         log.warning("xgmi collectives unavailable; using RCCL")
         return None
+    if os.environ.get("JDT_XGMI_CALIBRATE", "1") != "0":
+        sizes = [int(s) for s in (sizes or [cap_floats]) if int(s) > 0]
+        cal = calibrate(c, sizes)
+        LAST_CALIBRATION = cal
+        main = max(sizes)
+        row = next((r for r in cal["table"] if r["bytes"] == 4 * main), None)
+        cal["transport"] = "xgmi" if row is None or row["choice"] == "xgmi" or mode == "xgmi" else "rccl"
+        if mode != "xgmi" and cal["transport"] == "rccl":
+            log.warning("xgmi: RCCL measured faster at %d bytes; using RCCL", 4 * main)
+            c.close()
+            return None
     return c

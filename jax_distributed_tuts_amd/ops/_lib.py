@@ -48,6 +48,7 @@ class LnArgs(ctypes.Structure):
 _SIGS = {
     "jdt_gemm_ln": (c_int, [ctypes.POINTER(GemmArgs), ctypes.POINTER(LnArgs), c_void_p]),
     "jdt_ln_args_size": (c_int, []),
+    "jdt_gemm_ln_set_cfg": (None, [c_int]),
     "jdt_gemm": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p]),
     "jdt_gemm_args_size": (c_int, []),
     "jdt_gemm_group": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_void_p, c_long, c_void_p, c_long, c_void_p]),

@@ -65,6 +65,34 @@ def dense(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, act: str = "none
     return _Dense.apply(x, w, b, act, float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset))
 
 
+class _SoftmaxXent(torch.autograd.Function):
+    """Per-row softmax cross-entropy on the fused xent kernel (csrc/xent.hip): ONE
+    launch computes the row losses AND d(row loss)/dlogits = softmax - onehot
+    (saved, bf16 like the trainers' dlogits); the backward only scales each row by
+    its upstream gradient (1/B for a ``loss.mean()``)."""
+
+    @staticmethod
+    def forward(ctx, logits, labels):
+        M, C = logits.shape
+        lg = logits.detach()
+        if lg.stride(-1) != 1:
+            lg = lg.contiguous()
+        lab = labels.detach().to(torch.int32).contiguous()
+        gpu = lg.is_cuda
+        d = torch.empty(M, C, dtype=torch.bfloat16 if gpu else torch.float32, device=lg.device)
+        loss = torch.empty(M, dtype=torch.float32, device=lg.device)
+        K.softmax_xent(lg, lab, grad_scale=1.0, dlogits=d, row_loss=loss)
+        ctx.save_for_backward(d)
+        ctx.ldtype = logits.dtype
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        (d,) = ctx.saved_tensors
+        return (d.float() * gloss.float()[:, None]).to(ctx.ldtype), None
+
+
 def softmax_cross_entropy_with_integer_labels(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-    """optax.softmax_cross_entropy_with_integer_labels: per-row CE (fp32)."""
-    return torch.nn.functional.cross_entropy(logits.float(), labels.long(), reduction="none")
+    """optax.softmax_cross_entropy_with_integer_labels: per-row CE (fp32), forward and
+    gradient from the fused HIP xent kernel (torch reference ops on CPU)."""
+    return _SoftmaxXent.apply(logits, labels)

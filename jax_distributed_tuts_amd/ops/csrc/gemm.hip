@@ -1696,11 +1696,19 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_ln_kernel(GemmArgs g, LnArg
     be[v][1] = *reinterpret_cast<const float4*>(L.beta + col + 4);
   }
   const bool writer = tni == 0;
-  for (int r = wid; r < BM; r += NW) {
-    const int row = tm0 + r;
-    u32x4 p[NV];
+  // every row load of this wave in flight at once (a load -> reduce -> store loop
+  // would pay one dependent memory round trip per row)
+  constexpr int RPW = BM / NW;
+  u32x4 rows_in[RPW][NV];
 #pragma unroll
-    for (int v = 0; v < NV; ++v) p[v] = *reinterpret_cast<const u32x4*>(L.X + (long)row * L.ldx + (v * 64 + lane) * 8);
+  for (int i = 0; i < RPW; ++i)
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+      rows_in[i][v] = *reinterpret_cast<const u32x4*>(L.X + (long)(tm0 + wid + i * NW) * L.ldx + (v * 64 + lane) * 8);
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int r = wid + i * NW, row = tm0 + r;
+    const u32x4* p = rows_in[i];
     float x[NV][8];
     float sum = 0.f;
 #pragma unroll
@@ -1841,6 +1849,7 @@ JDT_API int jdt_ln_args_size() { return (int)sizeof(LnArgs); }
 // C = epilogue(LN(X) . W) with LN(X) and its row statistics also stored (see
 // gemm_ln_kernel).  X [M, K] bf16 (K in {512, 1024}, rows 16-byte aligned), W
 // [K, N] bf16 "kn"; M % 32 == 0, N % 64 == 0.  Returns -2 outside that envelope.
+static int g_ln_cfg = 0;  // jdt_gemm_ln_set_cfg: force a tile (sweeps); 0 = heuristic
 JDT_API int jdt_gemm_ln(const GemmArgs* ga, const LnArgs* la, void* stream) {
   const GemmArgs& g = *ga;
   const LnArgs& L = *la;
@@ -1850,11 +1859,25 @@ JDT_API int jdt_gemm_ln(const GemmArgs* ga, const LnArgs* la, void* stream) {
       g.M % 32 || g.N % 64 || !al(L.X) || !al(L.Y) || !al(g.B) || L.ldx % 8 || L.ldy % 8 || g.ldb % 8 ||
       !al(L.gamma) || !al(L.beta))
     return -2;
-  const long t64 = (long)(g.M / 64) * (g.N / 64);
-  const bool big = g.M % 64 == 0 && t64 >= 512;   // 64 x 64 tiles (88 KB LDS) once they fill the chip twice
-  if (g.K == 512) return big ? launch_ln<2, 2, 2, 2, 1>(g, L, st) : launch_ln<2, 2, 1, 2, 1>(g, L, st);
-  return launch_ln<2, 2, 1, 2, 2>(g, L, st);
+  int cfg = g_ln_cfg;
+  if (cfg <= 0) {
+    // measured (tools/bench_ln_gemm.py): the fused kernel normalises each row once per
+    // column block, so it only pays off while N / BN is small and the separate LN
+    // launch is a large share: M <= 512, N <= 1536 (qkv 512 rows 8.5 vs 9.4 us, 256
+    // rows 7.5 vs 8.1); the 2048-row shapes run LN + GEMM (qkv 14.1 vs 16.5 us best)
+    if (g.M > 512 || g.N > 1536) return -2;
+    cfg = g.M >= 512 ? 3 : 1;
+  }
+  if (g.K == 1024) return launch_ln<2, 2, 1, 2, 2>(g, L, st);
+  switch (cfg) {
+    case 1: return launch_ln<2, 2, 1, 2, 1>(g, L, st);   // 32 x 64
+    case 2: return launch_ln<2, 2, 2, 2, 1>(g, L, st);   // 64 x 64
+    case 3: return launch_ln<2, 2, 1, 4, 1>(g, L, st);   // 32 x 128
+    case 4: return launch_ln<2, 2, 2, 4, 1>(g, L, st);   // 64 x 128
+    default: return -2;
+  }
 }
+JDT_API void jdt_gemm_ln_set_cfg(int c) { g_ln_cfg = c; }
 
 // n GEMMs (no batch) in one launch; 1 = not eligible (launch them one by one).
 JDT_API int jdt_gemm_group(const GemmArgs* gs, int n, float* ws, long ws_floats, unsigned* counters, long n_counters,

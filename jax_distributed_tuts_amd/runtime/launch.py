@@ -50,7 +50,8 @@ def free_port() -> int:
     except (OSError, ValueError, IndexError):
         pass
     rnd = random.Random(os.getpid() ^ time.time_ns())
-    for _ in range(64):
+    # an ephemeral range starting near 1024 leaves no room below it: plain bind(0)
+    for _ in range(64 if lo - 64 > 1024 else 0):
         port = rnd.randrange(max(1024, lo - 10000), lo)
         with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
             try:

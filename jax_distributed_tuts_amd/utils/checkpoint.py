@@ -62,6 +62,13 @@ def restore(state, path: str, metrics: Optional[torch.Tensor] = None):
     _check_layout(man, _manifest(state), path)
     if tuple(t["master"].shape) != tuple(P.master.shape):
         raise ValueError(f"{path}: master buffer {tuple(t['master'].shape)} != {tuple(P.master.shape)}")
+    # optimizer state checked BEFORE anything is copied (a mismatch must not leave a
+    # half-restored state): same slots (AdamW: count, m, v, ticket; SGD: count, ticket)
+    saved_opt = {k[4:]: tuple(v.shape) for k, v in t.items() if k.startswith("opt/")}
+    cur_opt = {k: tuple(v.shape) for k, v in state.opt_state.items()}
+    if saved_opt != cur_opt:
+        raise ValueError(f"{path}: optimizer state {sorted(saved_opt.items())} does not match the live optimizer's "
+                         f"{sorted(cur_opt.items())} (different optimizer or layout)")
     P.master.copy_(t["master"].to(P.master.device))
     for k, v in state.opt_state.items():
         v.copy_(t[f"opt/{k}"].to(v.device))

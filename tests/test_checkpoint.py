@@ -67,3 +67,37 @@ def test_restore_rejects_other_world_size(tmp_path):
     json.dump(man, open(man_f, "w"))
     with pytest.raises(ValueError, match="8-rank"):
         checkpoint.restore(st, str(tmp_path))
+
+
+def test_restore_rejects_other_optimizer_before_touching_state(tmp_path):
+    """An AdamW checkpoint restored into an SGD state (or back) is refused with a
+    ValueError naming the optimizer slots, and the live params are left untouched."""
+    from jax_distributed_tuts_amd.utils.train_state import sgd
+
+    st, tr = _dp()
+    tr.step(_batch())
+    checkpoint.save(st, str(tmp_path))
+    st2 = init_dp(Classifier(), sgd(0.1), 7, "cpu")
+    before = st2.params.master.clone()
+    with pytest.raises(ValueError, match="optimizer state"):
+        checkpoint.restore(st2, str(tmp_path))
+    torch.testing.assert_close(st2.params.master, before, rtol=0, atol=0)
+
+
+def test_free_port_with_low_ephemeral_range(monkeypatch):
+    """An ephemeral range starting at 1024 leaves no room below it: bind(0) fallback."""
+    import builtins
+    import io
+
+    from jax_distributed_tuts_amd.runtime import launch
+
+    real_open = builtins.open
+
+    def fake_open(path, *a, **k):
+        if str(path) == "/proc/sys/net/ipv4/ip_local_port_range":
+            return io.StringIO("1024\t65535\n")
+        return real_open(path, *a, **k)
+
+    monkeypatch.setattr(builtins, "open", fake_open)
+    port = launch.free_port()
+    assert 0 < port < 65536

@@ -794,16 +794,25 @@ def test_ln_gemm_matches_layernorm_then_gemm(M, K, N, act):
     beta = (0.1 * torch.randn(K, generator=g)).to(DEV)
     w = (torch.randn(K, N, generator=g) / K ** 0.5).to(torch.bfloat16).to(DEV)
     bias = (0.1 * torch.randn(N, generator=g)).to(torch.bfloat16).to(DEV)
-    z = torch.empty(M, N, dtype=torch.bfloat16, device=DEV) if act != "none" else None
-    c, y, mean, rstd = kern.ln_gemm(x, gamma, beta, w, eps=1e-6, bias=bias, act=act, z_out=z)
+    from jax_distributed_tuts_amd.ops import _lib
+
     y_r, m_r, r_r = kern.layernorm_fwd(x, gamma, beta, 1e-6)
-    z_r = torch.empty_like(z) if z is not None else None
+    z_r = torch.empty(M, N, dtype=torch.bfloat16, device=DEV) if act != "none" else None
     c_r = kern.gemm(y_r, w, bias=bias, act=act, z_out=z_r)
-    torch.cuda.synchronize()
-    assert torch.equal(y, y_r) and torch.equal(mean, m_r) and torch.equal(rstd, r_r)
-    _close(c, c_r, rtol=1e-2, atol=1e-2)
-    if z is not None:
-        _close(z, z_r, rtol=1e-2, atol=1e-2)
+    try:
+        for cfg in (0, 1, 2, 3, 4):  # heuristic (may fall back) and every fused tile
+            if cfg in (2, 4) and M % 64:
+                continue
+            _lib.lib().jdt_gemm_ln_set_cfg(cfg)
+            z = torch.empty(M, N, dtype=torch.bfloat16, device=DEV) if act != "none" else None
+            c, y, mean, rstd = kern.ln_gemm(x, gamma, beta, w, eps=1e-6, bias=bias, act=act, z_out=z)
+            torch.cuda.synchronize()
+            assert torch.equal(y, y_r) and torch.equal(mean, m_r) and torch.equal(rstd, r_r), cfg
+            _close(c, c_r, rtol=1e-2, atol=1e-2)
+            if z is not None:
+                _close(z, z_r, rtol=1e-2, atol=1e-2)
+    finally:
+        _lib.lib().jdt_gemm_ln_set_cfg(0)
     # against fp32 torch
     ref = torch.nn.functional.layer_norm(x.float(), (K,), gamma, beta, 1e-6).to(torch.bfloat16).float() @ w.float()
     ref = ref + bias.float()

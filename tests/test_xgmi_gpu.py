@@ -28,6 +28,10 @@ def test_xgmi_collectives(tmp_path, ws):
         assert all(o["ar"].values()), o["ar"]
         assert o["fused"] and o["rs"] and o["ag"] and o["graph"], o
         assert o["err"] == 0
+        # per-size transport calibration ran, set the measured one-shot crossover and
+        # reports RCCL as unavailable on the shared-GPU (gloo-bootstrapped) job
+        assert o["cal_rows"] >= 5 and o["cal_threshold_ok"] and o["cal_threshold_set"] and o["cal_has_bucket"], o
+        assert o["cal_rccl"].startswith("unavailable") and o["ar_after_cal"], o
 
 
 def test_dp_over_xgmi_matches_single_device(tmp_path):

@@ -50,6 +50,22 @@ def collectives(outdir):
             ar[f"{'2shot' if forced == 0 else '1shot'}_{n}_{len(ar)}"] = bool(torch.equal(y.cpu(), _seq_sum(xs)))
     XgmiComm.set_oneshot_bytes(256 * 1024)
     res["ar"] = ar
+    # per-size transport choice: one-shot / two-shot / RCCL timed at the
+    # DP bucket, threshold set to the measured crossover; all-reduce still exact after it
+    from jax_distributed_tuts_amd.comm.xgmi import calibrate
+    from jax_distributed_tuts_amd.ops import _lib as _L
+
+    cal = calibrate(comm, [407_168], iters=5)
+    res["cal_rccl"] = cal["rccl"]
+    res["cal_rows"] = len(cal["table"])
+    res["cal_threshold_ok"] = cal["oneshot_threshold_bytes"] in [0] + [row["bytes"] for row in cal["table"]]
+    res["cal_threshold_set"] = int(_L.lib().jdt_xgmi_oneshot_bytes()) == cal["oneshot_threshold_bytes"]
+    res["cal_has_bucket"] = any(row["trainer_size"] for row in cal["table"])
+    xs = [torch.randn(5000, generator=torch.Generator().manual_seed(9 + q)) for q in range(W)]
+    y = xs[r].to(dev)
+    comm.all_reduce_(y)
+    res["ar_after_cal"] = bool(torch.equal(y.cpu(), _seq_sum(xs)))
+    XgmiComm.set_oneshot_bytes(256 * 1024)
     # fused all-reduce + AdamW + metrics fold == sum, then the standalone AdamW kernel
     npar, total = 4096, 4096 + 64
     g = torch.Generator().manual_seed(7)

@@ -507,6 +507,184 @@ __global__ void __launch_bounds__(XG_THREADS) xg_seg_kernel(XgPeers P, int rank,
   xg_call_done(me);
 }
 
+
+// ---------------------------------------------------------------------------
+// The whole FSDP (ZeRO-3) communication of a step in ONE launch, for the fused
+// engines' plain-stored full gradients:
+//   phase 0  stage every peer part of every segment's full fp32 gradient
+//   barrier
+//   phase 1  reduce this rank's part (rank-ordered sum) and, per element:
+//            sharded leaf  -> AdamW on the LOCAL shard (fp32 master, m, v, bf16 local
+//                             shadow), the new bf16 value into tmp for the peers;
+//            replicated    -> (an all-reduce segment) AdamW on every rank, bf16 straight
+//                             into the full shadow;
+//            metric slots  -> running metrics += sum, slots zeroed
+//   barrier
+//   phase 2  gather every peer's updated bf16 shard into the full bf16 shadow the
+//            next step's forward reads (the all-gather of the NEXT step, done now)
+// so an N > 1 FSDP step is the fused forward, the fused backward and this kernel --
+// the separate gather, reduce-scatter, AdamW and metrics-fold launches are gone.
+// Geometry as xg_seg_kernel (segments packed by `off`, `bcast` = all-reduce
+// segment); bf16 values travel in the tmp buffer at bf16 index 2*half + q*slice + j.
+enum { XF_SHARD = 0, XF_REPL = 1, XF_METRIC = 2 };
+struct XgFsdp {
+  XgAdam A;                        // p / m / v / shadow = the LOCAL flat buffers; running = metrics
+  const float* grad;               // local grad base: a part's local offset = part - grad
+  int kind[XG_MAX_SEGS];
+  bf16_t* full_shadow[XG_MAX_SEGS];  // bf16 full leaf (gather / replicated target)
+};
+
+__device__ __forceinline__ void sys_store8(__amdgpu_buffer_rsrc_t r, long byte_off, uint2 x) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, x), r,
+                                        (int)byte_off, 0, CPOL_SYS);
+}
+__device__ __forceinline__ uint2 sys_load8(__amdgpu_buffer_rsrc_t r, long byte_off) {
+  return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)byte_off, 0, CPOL_SYS));
+}
+
+template <int W>
+__global__ void __launch_bounds__(XG_THREADS) xg_fsdp_kernel(XgPeers P, int rank, long cap, XgSegs S, XgFsdp F,
+                                                             long slice, long chunk, long long timeout) {
+  __shared__ unsigned s_epoch, s_calls;
+  const int b = blockIdx.x;
+  XgSignal* me = P.sig[rank];
+  if (threadIdx.x == 0) {
+    s_epoch = me->epoch[b] + 1u;
+    s_calls = xg_calls(me);
+  }
+  __syncthreads();
+  const unsigned epoch = s_epoch;
+  const long half = (long)(s_calls & 1u) * cap;
+  const long base = (long)b * chunk;
+  const int nv = (int)(chunk >> 2);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const unsigned long long bytes = (unsigned long long)cap * 2ull * sizeof(float);
+  const XgAdam& A = F.A;
+
+  // phase 0: stage
+  {
+    const __amdgpu_buffer_rsrc_t my_data = sys_rsrc(P.data[rank], bytes);
+    for (int q = 0; q < W; ++q) {
+      for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
+        const long j = base + 4 * i;
+        float4 x = z4;
+        if (j < S.S) {
+          const XgSeg& g = S.seg[xg_find(S, j)];
+          x = load_guard(g.full, seg_full_index(g, q, j - g.off), g.nfull);
+        }
+        sys_store4(my_data, half + q * slice + j, x);
+      }
+    }
+  }
+  xg_barrier(P, rank, W, 0, epoch, timeout);
+
+  // phase 1: reduce own part, optimizer, publish the new bf16 shard
+  float rbc1, rbc2;
+  {
+    const int t = A.step[0] + 1;
+    rbc1 = 1.f / (1.f - powf(A.b1, (float)t));
+    rbc2 = 1.f / (1.f - powf(A.b2, (float)t));
+  }
+  {
+    __amdgpu_buffer_rsrc_t rdata[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) rdata[q] = sys_rsrc(P.data[q], bytes);
+    const __amdgpu_buffer_rsrc_t my_tmp = sys_rsrc(P.tmp[rank], bytes);
+    for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
+      const long j = base + 4 * i;
+      if (j >= S.S) break;
+      float4 v[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q) v[q] = sys_load4(rdata[q], half + rank * slice + j);
+      float4 acc = v[0];
+#pragma unroll
+      for (int q = 1; q < W; ++q) acc = add4(acc, v[q]);
+      const int k = xg_find(S, j);
+      const XgSeg& g = S.seg[k];
+      const long jj = j - g.off;
+      const long lim = g.bcast ? g.nfull : ((g.nfull - rank * g.s < g.s) ? g.nfull - rank * g.s : g.s);
+      const int kind = F.kind[k];
+      if (kind == XF_METRIC) {
+        const float* a = &acc.x;
+        for (int e = 0; e < 4; ++e)
+          if (jj + e < lim && jj + e < A.n_metrics) A.running[jj + e] += a[e];
+        store_guard(g.part, jj, lim, z4);
+        continue;
+      }
+      const long lo = (g.part - F.grad) + jj;   // local flat offset of element jj of this part
+      const float* ga = &acc.x;
+      float pn[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (jj + e >= lim) break;
+        const float gr = ga[e] * A.grad_scale;
+        const float mm = A.b1 * A.m[lo + e] + (1.f - A.b1) * gr;
+        const float vv = A.b2 * A.v[lo + e] + (1.f - A.b2) * gr * gr;
+        float pp = A.p[lo + e];
+        pp -= A.lr * ((mm * rbc1) / (sqrtf(vv * rbc2) + A.eps) + A.wd * pp);
+        A.m[lo + e] = mm;
+        A.v[lo + e] = vv;
+        A.p[lo + e] = pp;
+        A.shadow[lo + e] = f2bf(pp);
+        pn[e] = pp;
+      }
+      uint2 pk;
+      pk.x = (unsigned)f2bf(pn[0]) | ((unsigned)f2bf(pn[1]) << 16);
+      pk.y = (unsigned)f2bf(pn[2]) | ((unsigned)f2bf(pn[3]) << 16);
+      if (kind == XF_SHARD) {
+        sys_store8(my_tmp, 2 * (2 * half + rank * slice + j), pk);
+      } else {  // replicated: every rank holds the same update; write the full leaf directly
+        bf16_t* fs = F.full_shadow[k];
+        const bf16_t h4[4] = {(bf16_t)(pk.x & 0xffff), (bf16_t)(pk.x >> 16), (bf16_t)(pk.y & 0xffff), (bf16_t)(pk.y >> 16)};
+        for (int e = 0; e < 4; ++e)
+          if (jj + e < lim) fs[jj + e] = h4[e];
+      }
+    }
+  }
+  xg_barrier(P, rank, W, 1, epoch, timeout);
+
+  // phase 2: gather every peer's updated bf16 shard into the full shadow
+  {
+    __amdgpu_buffer_rsrc_t rtmp[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) rtmp[q] = sys_rsrc(P.tmp[q], bytes);
+    for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
+      const long j = base + 4 * i;
+      if (j >= S.S) break;
+      const int k = xg_find(S, j);
+      if (F.kind[k] != XF_SHARD) continue;
+      const XgSeg& g = S.seg[k];
+      const long jj = j - g.off;
+      uint2 r[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q) r[q] = sys_load8(rtmp[q], 2 * (2 * half + q * slice + j));
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        const long lim = (g.nfull - q * g.s < g.s) ? g.nfull - q * g.s : g.s;
+        if (jj >= lim) continue;
+        bf16_t* dst = F.full_shadow[k] + seg_full_index(g, q, jj);
+        if (jj + 4 <= lim) {
+          *reinterpret_cast<uint2*>(dst) = r[q];
+        } else {
+          const bf16_t h4[4] = {(bf16_t)(r[q].x & 0xffff), (bf16_t)(r[q].x >> 16), (bf16_t)(r[q].y & 0xffff),
+                                (bf16_t)(r[q].y >> 16)};
+          for (int e = 0; e < 4 && jj + e < lim; ++e) dst[e] = h4[e];
+        }
+      }
+    }
+  }
+  if (threadIdx.x == 0) me->epoch[b] = epoch;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = atomicAdd(A.ticket, 1u);
+    if (t == gridDim.x - 1) {
+      A.step[0] = A.step[0] + 1;
+      __hip_atomic_store(A.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  xg_call_done(me);
+}
+
 struct XgCtx {
   int rank = 0, world = 1;
   long cap = 0;  // floats per parity half
@@ -812,6 +990,59 @@ JDT_API int jdt_xgmi_segments(void* ctx, const XgSegs* segs, int op, int accumul
 }
 
 JDT_API int jdt_xgmi_segs_size() { return (int)sizeof(XgSegs); }
+JDT_API int jdt_xgmi_fsdp_size() { return (int)sizeof(XgFsdp); }
+
+// One FSDP step's communication + sharded AdamW + metrics fold (xg_fsdp_kernel).
+// Segment word sizes: fp32 grads; the bf16 full shadows get the same element index.
+JDT_API int jdt_xgmi_fsdp_step(void* ctx, const XgSegs* segs, const XgFsdp* f, long long timeout, void* stream) {
+  XgCtx* c = static_cast<XgCtx*>(ctx);
+  if (!c->opened) return -5;
+  if (segs->n < 1 || segs->n > XG_MAX_SEGS || !f->A.step || !f->A.ticket || !f->A.p || !f->A.m || !f->A.v ||
+      !f->A.shadow || !f->grad)
+    return -2;
+  long off = 0;
+  for (int k = 0; k < segs->n; ++k) {
+    const XgSeg& g = segs->seg[k];
+    if ((g.s & 3) || g.off != off || g.nfull > g.s * c->world) return -2;
+    if (g.bcast && (g.nfull > g.s || g.rows > 1)) return -2;
+    if ((f->kind[k] == XF_SHARD) == (g.bcast != 0)) return -2;          // sharded <=> not all-reduce
+    if (f->kind[k] != XF_METRIC && !f->full_shadow[k]) return -2;
+    if (f->kind[k] == XF_METRIC && g.part != g.full) return -2;
+    if (g.rows > 1) {
+      const long w = g.s / g.rows;
+      if (g.s % g.rows || (w & 3) || (g.ld & 3) || (g.qoff & 3) || g.qoff < w ||
+          (long)(c->world - 1) * g.qoff + w > g.ld || g.rows * g.ld > g.nfull)
+        return -2;
+    }
+    if ((reinterpret_cast<uintptr_t>(g.full) | reinterpret_cast<uintptr_t>(g.part)) & 15) return -2;
+    if (f->full_shadow[k] && (reinterpret_cast<uintptr_t>(f->full_shadow[k]) & 7)) return -2;
+    off += g.s;
+  }
+  if (off != segs->S || off <= 0) return -2;
+  long G, chunk;
+  xg_geometry(off, &G, &chunk);
+  const long slice = chunk * G;
+  if (slice * c->world > c->cap) return -3;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+#define XG_F_CASE(w)                                                                                          \
+  case w:                                                                                                     \
+    hipLaunchKernelGGL((xg_fsdp_kernel<w>), dim3(G), dim3(XG_THREADS), 0, st, c->peers, c->rank, c->cap, *segs, \
+                       *f, slice, chunk, timeout);                                                           \
+    break;
+  switch (c->world) {
+    XG_F_CASE(2)
+    XG_F_CASE(3)
+    XG_F_CASE(4)
+    XG_F_CASE(5)
+    XG_F_CASE(6)
+    XG_F_CASE(7)
+    XG_F_CASE(8)
+    default:
+      return -4;
+  }
+#undef XG_F_CASE
+  return HIP_LAUNCH_CHECK();
+}
 
 JDT_API int jdt_xgmi_adam_size() { return (int)sizeof(XgAdam); }
 

@@ -71,6 +71,17 @@ class XgSegs(ctypes.Structure):
     _fields_ = [("seg", XgSeg * MAX_SEGS), ("n", c_int), ("S", c_long)]
 
 
+class XgFsdp(ctypes.Structure):
+    """Mirror of ``jdt::XgFsdp``: local AdamW buffers + per-segment kind / bf16 full shadow."""
+
+    _fields_ = [("A", XgAdam), ("grad", c_void_p), ("kind", c_int * MAX_SEGS), ("full_shadow", c_void_p * MAX_SEGS)]
+
+
+FSDP_SHARD, FSDP_REPL, FSDP_METRIC = 0, 1, 2
+
+_lib.declare("jdt_xgmi_fsdp_size", c_int, [])
+_lib.declare("jdt_xgmi_fsdp_step", c_int, [c_void_p, ctypes.POINTER(XgSegs), ctypes.POINTER(XgFsdp), c_longlong,
+                                           c_void_p])
 _lib.declare("jdt_xgmi_create", c_int, [c_int, c_int, c_long, ctypes.POINTER(c_void_p), c_void_p])
 _lib.declare("jdt_xgmi_open", c_int, [c_void_p, c_void_p])
 _lib.declare("jdt_xgmi_allreduce", c_int, [c_void_p, c_void_p, c_void_p, c_long, ctypes.POINTER(XgAdam), c_longlong,
@@ -120,7 +131,8 @@ class XgmiComm:
         self.ctx = c_void_p()
         self.ok = False
         L = _lib.lib()
-        if L.jdt_xgmi_adam_size() != ctypes.sizeof(XgAdam) or L.jdt_xgmi_segs_size() != ctypes.sizeof(XgSegs):
+        if (L.jdt_xgmi_adam_size() != ctypes.sizeof(XgAdam) or L.jdt_xgmi_segs_size() != ctypes.sizeof(XgSegs)
+                or L.jdt_xgmi_fsdp_size() != ctypes.sizeof(XgFsdp)):
             raise RuntimeError("XgAdam layout mismatch between Python and comm/csrc/xgmi.hip")
         h = (ctypes.c_char * (3 * HANDLE_BYTES))()
         with torch.cuda.device(device):
@@ -338,6 +350,57 @@ class XgmiComm:
             rc = _lib.lib().jdt_xgmi_segments(self.ctx, ctypes.byref(S), 1, int(accumulate), self.timeout,
                                               c_void_p(_lib.stream_ptr()))
             _lib.check(rc, "jdt_xgmi_segments(reduce_scatter)")
+
+    # ------------------------------------------------------------------ fused FSDP step collective
+    def fsdp_plan(self, shards, replicated, metric_slots, *, grad_base: torch.Tensor, p: torch.Tensor,
+                  m: torch.Tensor, v: torch.Tensor, shadow: torch.Tensor, running: torch.Tensor, lr: float,
+                  b1: float, b2: float, eps: float, wd: float, grad_scale: float, step: torch.Tensor,
+                  ticket: torch.Tensor):
+        """Arguments of ONE ``xg_fsdp_kernel`` launch (see comm/csrc/xgmi.hip): ``shards``
+        = [(full fp32 grad, local fp32 grad view, full bf16 shadow)] of the sharded
+        leaves, ``replicated`` = [(full grad, local grad view, full shadow)], and the
+        local metric slots.  The local views must lie in ``grad_base`` (the local flat
+        grad buffer), whose offsets index ``p`` / ``m`` / ``v`` / ``shadow``."""
+        pairs = [(f, l) for f, l, _ in shards]
+        n = len(pairs) + len(replicated) + 1
+        if n > MAX_SEGS:
+            raise ValueError(f"at most {MAX_SEGS} segments in one FSDP step launch")
+        S = self._segs(pairs)   # validates the shard pairs (dim-0 / dim-1 layouts)
+        off = S.S
+        F = XgFsdp()
+        for k, (_, _, fs) in enumerate(shards):
+            F.kind[k] = FSDP_SHARD
+            F.full_shadow[k] = fs.data_ptr()
+        k = len(pairs)
+        for full, part, fs in replicated:
+            if not (full.is_contiguous() and part.is_contiguous() and full.numel() == part.numel()
+                    and full.data_ptr() % 16 == 0 and part.data_ptr() % 16 == 0 and fs.data_ptr() % 8 == 0):
+                raise ValueError("replicated leaf views must be contiguous and aligned")
+            w = (full.numel() + 3) // 4 * 4
+            S.seg[k] = XgSeg(full.data_ptr(), part.data_ptr(), w, off, full.numel(), 1, 0, 0, 0)
+            F.kind[k], F.full_shadow[k] = FSDP_REPL, fs.data_ptr()
+            off += w
+            k += 1
+        ms = metric_slots
+        w = (ms.numel() + 3) // 4 * 4
+        S.seg[k] = XgSeg(ms.data_ptr(), ms.data_ptr(), w, off, ms.numel(), 1, 0, 0, 0)
+        F.kind[k] = FSDP_METRIC
+        off += w
+        S.n, S.S = k + 1, off
+        a = F.A
+        a.p, a.m, a.v, a.shadow = _ptr(p), _ptr(m), _ptr(v), _ptr(shadow)
+        a.n_params, a.running, a.n_metrics = 0, _ptr(running), int(ms.numel())
+        a.lr, a.b1, a.b2, a.eps, a.wd, a.grad_scale = (float(lr), float(b1), float(b2), float(eps), float(wd),
+                                                       float(grad_scale))
+        a.step, a.ticket, a.zero = _ptr(step), _ptr(ticket), c_void_p(0)
+        F.grad = _ptr(grad_base)
+        return S, F
+
+    def fsdp_step(self, plan):
+        S, F = plan
+        rc = _lib.lib().jdt_xgmi_fsdp_step(self.ctx, ctypes.byref(S), ctypes.byref(F), self.timeout,
+                                           c_void_p(_lib.stream_ptr()))
+        _lib.check(rc, "jdt_xgmi_fsdp_step")
 
     # ------------------------------------------------------------------ self-test
     SELF_TEST_ITERS = 32

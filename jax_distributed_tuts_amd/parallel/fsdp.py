@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -387,6 +388,8 @@ class FSDPTrainer:
         self.graph = None
         self._ahead = None
         self.multi = None
+        self._plan = None
+        self._full_fresh = True   # init_fsdp gathered the full shadow
         if self.world > 1 and self.sp.local.master.is_cuda and self.sp.xg is None:
             from ..comm.xgmi import create_for
 
@@ -403,6 +406,31 @@ class FSDPTrainer:
         self.graph = None
         self._ahead = None
         self.multi = None
+        self._plan = None
+        self._full_fresh = False
+
+    def _fsdp_plan(self):
+        """Arguments of the fused FSDP step collective (comm/xgmi.py ``fsdp_plan``), or
+        None when it does not apply: every sharded leaf must move on the segmented xGMI
+        kernel, AdamW, <= 16 segments (JDT_FSDP_FUSED_COMM=0 turns it off)."""
+        if getattr(self, "_plan", None) is not None:
+            return self._plan
+        from ..utils.train_state import AdamW
+
+        sp, st = self.sp, self.state
+        if (sp.xg is None or len(sp._xg_names) != len(sp.sharded_names) or not isinstance(st.tx, AdamW)
+                or len(sp.sharded_names) + len(sp.repl_names) + 1 > 16
+                or os.environ.get("JDT_FSDP_FUSED_COMM", "1") == "0"):
+            return None
+        tx, o = st.tx, st.opt_state
+        self._plan = sp.xg.fsdp_plan(
+            [(sp.full.g(n), sp.local.g(n), sp.full.s(n)) for n in sp.sharded_names],
+            [(sp.full.g(n), sp.local.g(n), sp.full.s(n)) for n in sp.repl_names],
+            sp.local.metrics_slot, grad_base=sp.local.grad, p=sp.local.master, m=o["m"], v=o["v"],
+            shadow=sp.local.shadow, running=self.metrics, lr=tx.learning_rate, b1=tx.b1, b2=tx.b2, eps=tx.eps,
+            wd=tx.weight_decay, grad_scale=1.0 / (self.cfg.num_minibatches * self.world), step=o["count"],
+            ticket=o["ticket"])
+        return self._plan
 
     @property
     def comm_backend(self) -> str:
@@ -450,6 +478,18 @@ class FSDPTrainer:
                 with named_scope("synch_metrics"):
                     K.metrics_fold_(self.metrics, sp.local.metrics_slot)
             return True
+        plan = self._fsdp_plan()
+        if plan is not None:
+            # ONE collective launch: reduce-scatter + sharded AdamW + replicated all-reduce
+            # + metrics fold + the next step's bf16 all-gather (xg_fsdp_kernel); the full
+            # shadow the forward reads was gathered by the previous step's launch
+            if not self._full_fresh:
+                sp.gather()
+                self._full_fresh = True
+            self.fused.forward_backward(batch)
+            with named_scope("scatter_update_gather"):
+                sp.xg.fsdp_step(plan)
+            return True
         sp.gather()
         self.fused.forward_backward(batch)
         if not sp.scatter_grads(accumulate=False, zero_full=False, with_replicated=True):
@@ -480,6 +520,9 @@ class FSDPTrainer:
         all-reduce, sharded AdamW, metrics fold) as a hipGraph; with
         ``steps_per_graph`` > 1 also a graph of that many consecutive steps."""
         assert self.capturable and batch.inputs.is_cuda
+        if not self._full_fresh:   # the fused step collective keeps the full shadow current
+            self.sp.gather()
+            self._full_fresh = True
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._body(batch)

@@ -66,30 +66,40 @@ def test_dp_over_xgmi_matches_single_device(tmp_path):
     assert abs(float(m[2]) - float(ref[2])) <= 4
 
 
-@pytest.mark.parametrize("fused,num_layers", [(True, 2), (False, 2), (True, 4)])
-def test_fsdp_over_xgmi_matches_single_device(tmp_path, fused, num_layers):
+@pytest.mark.parametrize("fused,num_layers,eps", [(True, 2, 1e-8), (False, 2, 1e-8), (True, 4, 1e-8), (True, 2, 10.0),
+                                                  (True, 4, 10.0)])
+def test_fsdp_over_xgmi_matches_single_device(tmp_path, fused, num_layers, eps):
+    """fused: the step's whole collective is ONE xg_fsdp_kernel (reduce-scatter +
+    sharded AdamW + metrics fold + next-step all-gather).  eps = 10 makes AdamW's update
+    ~ lr * g / eps, i.e. proportional to the gradient: a missing 1/N or 1/n_mb in the
+    fused kernel's grad scale fails (Adam with eps 1e-8 would hide it)."""
     from data_paral import synthetic_batch
     from jax_distributed_tuts_amd.models.mlp import Classifier
     from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
     from jax_distributed_tuts_amd.utils.config import fsdp_config
     from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
 
-    spawn(XW.fsdp_xgmi, 2, str(tmp_path), fused, 3, num_layers, gpu=True)
+    spawn(XW.fsdp_xgmi, 2, str(tmp_path), fused, 3, num_layers, eps, gpu=True)
     res = _load(tmp_path, f"fsx{num_layers}", 2)
     assert all(o["comm"] == "xgmi" for o in res)
+    assert all(o["fused_comm"] == fused for o in res)
     # every sharded leaf rides the segmented kernels (dim-0 and, 4-layer, dim-1 shards)
     assert set(res[0]["xg_names"]) == {n for n, d in res[0]["dims"].items() if d is not None}
     if num_layers == 4:
         assert 1 in res[0]["dims"].values()
     dev = torch.device("cuda", 0)
-    st = init_fsdp(Classifier(num_layers=num_layers, dropout_rate=0.0), adamw(1e-3), 69, dev, None, "data", 16)
+    st = init_fsdp(Classifier(num_layers=num_layers, dropout_rate=0.0), adamw(1e-3, eps=eps), 69, dev, None, "data",
+                   16)
     b = synthetic_batch(fsdp_config(), 70)
     b = Batch(b.inputs.to(dev), b.labels.to(dev))
     tr = FSDPTrainer(st, None, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=fused))
+    sp = st.extra["sharded"]
+    p0 = {n: sp.local.p(n).cpu().clone() for n in res[0]["dims"]}
     for _ in range(3):
         tr.step(b)
     torch.cuda.synchronize()
-    sp = st.extra["sharded"]
+    from .oracle import check_grad
+
     for n, d in res[0]["dims"].items():
         got = res[0]["local"][n] if d is None else torch.cat([o["local"][n] for o in res], dim=d)
         if d is None:
@@ -97,6 +107,8 @@ def test_fsdp_over_xgmi_matches_single_device(tmp_path, fused, num_layers):
         diff = (got - sp.local.p(n).cpu()).abs()
         assert float(diff.max()) <= 2 * 1e-3 * 3 + 1e-6, n
         assert float((diff > 5e-5).float().mean()) < 5e-3, n
+        if eps > 1.0:  # the 3-step update is ~ proportional to the gradients: scale-checked
+            check_grad(got - p0[n], sp.local.p(n).cpu() - p0[n], f"{n} update", rel_tol=0.05, scale_tol=0.02)
     m, ref = res[0]["metrics"], tr.metrics.cpu()
     assert abs(float(m[0]) - float(ref[0])) <= 1e-3 * abs(float(ref[0])) + 1e-3
     assert float(m[1]) == float(ref[1])

@@ -165,7 +165,7 @@ def dp_xgmi(outdir, steps_eager=2, steps_graph=6):
                           "fused": tr.fused is not None, "step": int(st.opt_state["count"].item())})
 
 
-def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2):
+def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2, eps=1e-8):
     """FSDP (dropout off) with the segmented xGMI gather / reduce-scatter; every rank
     saves its local shard + the partition table for reassembly in the parent.
     num_layers=4: the square 512 x 512 hidden weights are sharded along dim 1 (the
@@ -181,7 +181,8 @@ def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2):
     dev = D.device()
     cfg = fsdp_config()
     mesh = D.Mesh({"data": D.world_size()})
-    st = init_fsdp(Classifier(num_layers=num_layers, dropout_rate=0.0), adamw(1e-3), 69, dev, mesh, "data", 16)
+    st = init_fsdp(Classifier(num_layers=num_layers, dropout_rate=0.0), adamw(1e-3, eps=eps), 69, dev, mesh, "data",
+                   16)
     b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
     b = Batch(b.inputs.to(dev), b.labels.to(dev))
     tr = FSDPTrainer(st, mesh, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=fused,
@@ -195,7 +196,8 @@ def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2):
     sp = st.extra["sharded"]
     _save(outdir, f"fsx{num_layers}", {"local": {n: sp.local.p(n).cpu() for n in sp.part},
                           "dims": {n: sp.part[n].shard_dim for n in sp.part},
-                          "metrics": tr.metrics.cpu(), "comm": tr.comm_backend, "xg_names": list(sp._xg_names)})
+                          "metrics": tr.metrics.cpu(), "comm": tr.comm_backend, "xg_names": list(sp._xg_names),
+                          "fused_comm": getattr(tr, "_plan", None) is not None})
 
 
 def pp_xgmi(outdir, dp, n_hidden=3, steps=4):

@@ -81,6 +81,15 @@ class TransformerLM:
     def head_bias_name(self) -> Optional[str]:
         return "head/bias" if self.has_head else None
 
+    def gemm_weight_names(self) -> List[str]:
+        """Weights whose gradient is one weight-gradient GEMM per backward pass (the
+        candidates for the in-epilogue optimizer, ops.kernels.EpilogueAdamW)."""
+        out = []
+        for l in self.layers:
+            b = f"block_{l}"
+            out += [f"{b}/attn/qkv/kernel", f"{b}/attn/out/kernel", f"{b}/mlp/fc1/kernel", f"{b}/mlp/fc2/kernel"]
+        return out + (["head/kernel"] if self.has_head else [])
+
     def input_shape(self, nseq: int):
         return (nseq, self.cfg.seq_len) if self.has_embed else (nseq * self.cfg.seq_len, self.cfg.d_model)
 
@@ -154,9 +163,11 @@ class TransformerLM:
 
     # ------------------------------------------------------------------ backward
     def backward(self, P: FlatParams, cache: _Cache, dout: torch.Tensor, *, dout_is_dz: bool = True,
-                 need_dx: bool = False, on_ready=None, wgrad=None) -> Optional[torch.Tensor]:
+                 need_dx: bool = False, on_ready=None, wgrad=None, opt=None) -> Optional[torch.Tensor]:
         """``wgrad`` (ops.kernels.WGradStream): run the weight-gradient GEMMs on its
-        side stream; the caller joins it before reading the grads."""
+        side stream; the caller joins it before reading the grads.  ``opt``
+        (ops.kernels.EpilogueAdamW): this pass carries the weights' final gradients of
+        the step -- AdamW runs in the epilogues of their weight-gradient GEMMs."""
         if on_ready is not None:
             wgrad = None  # bucket callbacks fire as soon as a layer's grads are queued
         c = self.cfg
@@ -167,7 +178,7 @@ class TransformerLM:
             # dlogits (CE already added the head bias grad); the LN-bwd also reduces
             # the top block's fc2 bias grad (colsum of the residual gradient)
             with K.gemm_group():  # dW and dX of a layer only need dz: one grouped launch
-                K.dw_gemm(wgrad, cache.hf, dout, P.g("head/kernel"))
+                K.dw_gemm(wgrad, cache.hf, dout, P.g("head/kernel"), opt=opt, name="head/kernel")
                 dhf = K.gemm(dout, P.s("head/kernel"), b_layout="nk")
             dx = K.layernorm_bwd(dhf, cache.xf, cache.mf, cache.rf, P.p("ln_f/scale"), P.g("ln_f/scale"),
                                  P.g("ln_f/bias"), dsum=fc2_bias(layers[-1]) if layers else None)
@@ -183,23 +194,23 @@ class TransformerLM:
             if not fc2_done:
                 K.colsum_(dx, P.g(f"{b}/mlp/fc2/bias"))
             with K.gemm_group():
-                K.dw_gemm(wgrad, bc.u, dx, P.g(f"{b}/mlp/fc2/kernel"))
+                K.dw_gemm(wgrad, bc.u, dx, P.g(f"{b}/mlp/fc2/kernel"), opt=opt, name=f"{b}/mlp/fc2/kernel")
                 dz1 = K.gemm(dx, P.s(f"{b}/mlp/fc2/kernel"), b_layout="nk", z_in=bc.z1, act_bwd="gelu",
                              keep_prob=cache.keep, seed=cache.seed, offset=bc.off, step=cache.step,
                              dbias=P.g(f"{b}/mlp/fc1/bias"))
             with K.gemm_group():
-                K.dw_gemm(wgrad, bc.h2, dz1, P.g(f"{b}/mlp/fc1/kernel"))
+                K.dw_gemm(wgrad, bc.h2, dz1, P.g(f"{b}/mlp/fc1/kernel"), opt=opt, name=f"{b}/mlp/fc1/kernel")
                 dh2 = K.gemm(dz1, P.s(f"{b}/mlp/fc1/kernel"), b_layout="nk")
             # x2 = x + o.Wo + bo: the LN2-bwd output dx2 is also Wo's bias grad
             dx2 = K.layernorm_bwd(dh2, bc.x2, bc.m2, bc.r2, P.p(f"{b}/ln2/scale"), P.g(f"{b}/ln2/scale"),
                                   P.g(f"{b}/ln2/bias"), dres=dx, dsum=P.g(f"{b}/attn/out/bias"))
             with K.gemm_group():
-                K.dw_gemm(wgrad, bc.o, dx2, P.g(f"{b}/attn/out/kernel"))
+                K.dw_gemm(wgrad, bc.o, dx2, P.g(f"{b}/attn/out/kernel"), opt=opt, name=f"{b}/attn/out/kernel")
                 do = K.gemm(dx2, P.s(f"{b}/attn/out/kernel"), b_layout="nk")
             dqkv = K.attention_bwd(do, bc.qkv, bc.P, cache.nseq, c.seq_len, c.n_heads, o=bc.o,
                                    dbias=P.g(f"{b}/attn/qkv/bias"))
             with K.gemm_group():
-                K.dw_gemm(wgrad, bc.h1, dqkv, P.g(f"{b}/attn/qkv/kernel"))
+                K.dw_gemm(wgrad, bc.h1, dqkv, P.g(f"{b}/attn/qkv/kernel"), opt=opt, name=f"{b}/attn/qkv/kernel")
                 dh1 = K.gemm(dqkv, P.s(f"{b}/attn/qkv/kernel"), b_layout="nk")
             below = fc2_bias(layers[idx - 1]) if idx > 0 else None  # next (lower) block's fc2 bias grad
             dx = K.layernorm_bwd(dh1, bc.x, bc.m1, bc.r1, P.p(f"{b}/ln1/scale"), P.g(f"{b}/ln1/scale"),

@@ -35,6 +35,9 @@ class GemmArgs(ctypes.Structure):
         ("C", c_void_p), ("ldc", c_long), ("sC", c_long), ("c_f32", c_int), ("accumulate", c_int),
         ("step_ptr", c_void_p),
         ("zin", c_int), ("sA2", c_long), ("sB2", c_long), ("sC2", c_long),
+        ("opt_p", c_void_p), ("opt_m", c_void_p), ("opt_v", c_void_p), ("opt_s", c_void_p), ("opt_step", c_void_p),
+        ("opt_lr", c_float), ("opt_b1", c_float), ("opt_b2", c_float), ("opt_eps", c_float), ("opt_wd", c_float),
+        ("opt_gs", c_float),
     ]
 
 
@@ -49,6 +52,8 @@ _SIGS = {
     "jdt_gemm_ln": (c_int, [ctypes.POINTER(GemmArgs), ctypes.POINTER(LnArgs), c_void_p]),
     "jdt_ln_args_size": (c_int, []),
     "jdt_gemm_ln_set_cfg": (None, [c_int]),
+    "jdt_adamw_ranges": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_long,
+                                 c_float, c_float, c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p]),
     "jdt_gemm": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p]),
     "jdt_gemm_args_size": (c_int, []),
     "jdt_gemm_group": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_void_p, c_long, c_void_p, c_long, c_void_p]),

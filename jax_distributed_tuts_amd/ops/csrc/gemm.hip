@@ -47,7 +47,39 @@ struct GemmArgs {
   // optional 2-level batch: z -> (z / zin, z % zin) with strides (sX, sX2) for
   // A, B and C (attention: batch x head over the fused [T, 3d] QKV buffer)
   int zin; long sA2, sB2, sC2;
+  // optional AdamW in the epilogue of a weight-gradient GEMM whose result is that
+  // weight's FINAL gradient of the step (fp32 C only): the element's gradient
+  // (C + value if accumulate, else value) updates the fp32 master / m / v views
+  // (same layout as C) and the bf16 shadow; C is reset to 0 when it was read.  The
+  // step's remaining parameters are updated by adamw_ranges_kernel, which also
+  // advances the device step counter (read here as t = step + 1).
+  float* opt_p; float* opt_m; float* opt_v; bf16_t* opt_s; const int* opt_step;
+  float opt_lr, opt_b1, opt_b2, opt_eps, opt_wd, opt_gs;
 };
+
+// AdamW of one element in a GEMM epilogue (see GemmArgs::opt_*): optax.adamw, the
+// arithmetic of optim.hip adamw_kernel.
+struct OptBC { float rbc1, rbc2; };
+__device__ __forceinline__ OptBC opt_bc(const GemmArgs& g) {
+  OptBC b{1.f, 1.f};
+  if (g.opt_p) {
+    const int t = g.opt_step[0] + 1;
+    b.rbc1 = 1.f / (1.f - powf(g.opt_b1, (float)t));
+    b.rbc2 = 1.f / (1.f - powf(g.opt_b2, (float)t));
+  }
+  return b;
+}
+__device__ __forceinline__ float opt_update(const GemmArgs& g, const OptBC& bc, long i, float grad) {
+  const float gr = grad * g.opt_gs;
+  const float mm = g.opt_b1 * g.opt_m[i] + (1.f - g.opt_b1) * gr;
+  const float vv = g.opt_b2 * g.opt_v[i] + (1.f - g.opt_b2) * gr * gr;
+  float pp = g.opt_p[i];
+  pp -= g.opt_lr * ((mm * bc.rbc1) / (sqrtf(vv * bc.rbc2) + g.opt_eps) + g.opt_wd * pp);
+  g.opt_m[i] = mm;
+  g.opt_v[i] = vv;
+  g.opt_p[i] = pp;
+  return pp;
+}
 
 __device__ __forceinline__ long zoff(const GemmArgs& g, int z, long s1, long s2) {
   return g.zin > 1 ? (long)(z / g.zin) * s1 + (long)(z % g.zin) * s2 : (long)z * s1;
@@ -280,6 +312,7 @@ __device__ __forceinline__ void gemm_finish(const GemmArgs& g, f32x4 (&acc)[TM][
   const bool drop = g.keep_prob < 1.0f;
   const float inv_keep = drop ? 1.0f / g.keep_prob : 1.0f;
   const unsigned long long doff = g.offset + (g.step_ptr ? ((unsigned long long)(unsigned)g.step_ptr[0] << 32) : 0ull);
+  const OptBC obc = opt_bc(g);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = tn0 + (wn * TN + j) * 16 + (lane & 15);
@@ -304,7 +337,11 @@ __device__ __forceinline__ void gemm_finish(const GemmArgs& g, f32x4 (&acc)[TM][
         if (drop) v = keep_word(dbits, e, g.keep_prob) ? v * inv_keep : 0.f;
         if (g.resid) v += bf2f(static_cast<const bf16_t*>(g.resid)[(long)z * g.sR + (long)row * g.ldr + col]);
         const long co = zoff(g, z, g.sC, g.sC2) + (long)row * g.ldc + col;
-        if (g.c_f32) {
+        if (g.c_f32 && g.opt_p) {
+          float* Cp = static_cast<float*>(g.C) + co;
+          g.opt_s[co] = f2bf(opt_update(g, obc, co, g.accumulate ? *Cp + v : v));
+          if (g.accumulate) *Cp = 0.f;
+        } else if (g.c_f32) {
           float* Cp = static_cast<float*>(g.C) + co;
           *Cp = g.accumulate ? *Cp + v : v;
         } else {
@@ -395,6 +432,7 @@ __device__ __forceinline__ void gemm_finish_lds(const GemmArgs& g, f32x4 (&acc)[
   constexpr int CPP = BN < 256 ? BN : 256;      // columns per pass
   constexpr int RGS = 256 / CPP;                 // row groups advanced per pass
   const int cl = tid % CPP;
+  const OptBC obc = opt_bc(g);
   for (int cb = 0; cb < BN; cb += CPP) {
     const int col = tn0 + cb + cl;
     const bool cok = col < g.N;
@@ -416,7 +454,11 @@ __device__ __forceinline__ void gemm_finish_lds(const GemmArgs& g, f32x4 (&acc)[
           if (drop) v = keep_word(dbits, e, g.keep_prob) ? v * inv_keep : 0.f;
           if (g.resid) v += bf2f(static_cast<const bf16_t*>(g.resid)[(long)z * g.sR + (long)row * g.ldr + col]);
           const long co = zoff(g, z, g.sC, g.sC2) + (long)row * g.ldc + col;
-          if (g.c_f32) {
+          if (g.c_f32 && g.opt_p) {
+            float* Cp = static_cast<float*>(g.C) + co;
+            g.opt_s[co] = f2bf(opt_update(g, obc, co, g.accumulate ? *Cp + v : v));
+            if (g.accumulate) *Cp = 0.f;
+          } else if (g.c_f32) {
             float* Cp = static_cast<float*>(g.C) + co;
             *Cp = g.accumulate ? *Cp + v : v;
           } else {
@@ -521,6 +563,7 @@ __device__ __forceinline__ void gemm_finish_vec(const GemmArgs& g, f32x4 (&acc)[
 #pragma unroll
   for (int k = 0; k < 8; ++k) cs[k] = 0.f;
   const long cbase = zoff(g, z, g.sC, g.sC2);
+  const OptBC obc = opt_bc(g);
   for (int u = tid; u < NU; u += NT) {
     const int rl = (u / CU) * 4;  // first row of the unit within the tile
     const int row0 = tm0 + rl;
@@ -566,7 +609,22 @@ __device__ __forceinline__ void gemm_finish_vec(const GemmArgs& g, f32x4 (&acc)[
         for (int k = 0; k < 8; ++k) v[k] += bf2f((bf16_t)((p[k >> 1] >> (16 * (k & 1))) & 0xffff));
       }
       const long co = cbase + (long)row * g.ldc + col;
-      if (g.c_f32) {
+      if (g.c_f32 && g.opt_p) {
+        float4* Cp = reinterpret_cast<float4*>(static_cast<float*>(g.C) + co);
+        if (g.accumulate) {
+          const float4 c0 = Cp[0], c1 = Cp[1];
+          v[0] += c0.x; v[1] += c0.y; v[2] += c0.z; v[3] += c0.w;
+          v[4] += c1.x; v[5] += c1.y; v[6] += c1.z; v[7] += c1.w;
+          Cp[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+          Cp[1] = Cp[0];
+        }
+        u32x4 o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          o[k] = (unsigned)f2bf(opt_update(g, obc, co + 2 * k, v[2 * k])) |
+                 ((unsigned)f2bf(opt_update(g, obc, co + 2 * k + 1, v[2 * k + 1])) << 16);
+        *reinterpret_cast<u32x4*>(g.opt_s + co) = o;
+      } else if (g.c_f32) {
         float4* Cp = reinterpret_cast<float4*>(static_cast<float*>(g.C) + co);
         float4 o0 = make_float4(v[0], v[1], v[2], v[3]), o1 = make_float4(v[4], v[5], v[6], v[7]);
         if (g.accumulate) {
@@ -624,7 +682,8 @@ static bool epi_vec_ok(const GemmArgs& g, int batch) {
     return al(p) && ld % q == 0 && (batch <= 1 || (s1 % q == 0 && (g.zin <= 1 || s2 % q == 0)));
   };
   return rows(g.C, g.ldc, g.sC, g.sC2, g.c_f32) && rows(g.Zout, g.ldz, g.sZ, 0, 0) && rows(g.Zin, g.ldzin, g.sZin, 0, 0) &&
-         rows(g.resid, g.ldr, g.sR, 0, 0) && (!g.bias || al(g.bias)) && g.N % 8 == 0;
+         rows(g.resid, g.ldr, g.sR, 0, 0) && (!g.bias || al(g.bias)) && g.N % 8 == 0 &&
+         (!g.opt_s || (al(g.opt_s) && g.ldc % 8 == 0));   // fused AdamW: 16-byte bf16 shadow stores
 }
 
 template <int WM, int WN, int TM, int TN, int BK, bool AF32, bool BF32, int PRE, bool EXACT = false>

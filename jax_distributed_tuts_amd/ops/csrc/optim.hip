@@ -76,6 +76,52 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, float
   if (ticket) finish_ticket(step, ticket);
 }
 
+// AdamW over a list of ranges of the flat buffers (the parameters whose update did
+// NOT ride in a weight-gradient GEMM epilogue: biases, LayerNorm, embeddings) in ONE
+// launch; ranges are multiples of 4 elements (FlatParams views are 64-aligned and
+// padded), prefix[r] = elements before range r.  Advances the step counter once.
+__global__ void __launch_bounds__(256) adamw_ranges_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                           float* __restrict__ m, float* __restrict__ v,
+                                                           bf16_t* __restrict__ shadow, const long* __restrict__ start,
+                                                           const long* __restrict__ prefix, int nr, long total,
+                                                           float lr, float b1, float b2, float eps, float wd,
+                                                           float grad_scale, int* step, unsigned* ticket) {
+  const int t = step[0] + 1;
+  const float rbc1 = 1.f / (1.f - powf(b1, (float)t)), rbc2 = 1.f / (1.f - powf(b2, (float)t));
+  const long n4 = total / 4;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += stride) {
+    const long e = 4 * q;
+    int lo = 0, hi = nr - 1;   // last range with prefix <= e
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (prefix[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    const long i = (start[lo] + (e - prefix[lo])) >> 2;   // float4 index
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    float4 gg = reinterpret_cast<float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    float* pe = &pp.x; float* ge = &gg.x; float* me = &mm.x; float* ve = &vv.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gr = ge[k] * grad_scale;
+      me[k] = b1 * me[k] + (1.f - b1) * gr;
+      ve[k] = b2 * ve[k] + (1.f - b2) * gr * gr;
+      pe[k] -= lr * ((me[k] * rbc1) / (sqrtf(ve[k] * rbc2) + eps) + wd * pe[k]);
+    }
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    uint2 sh;
+    sh.x = (unsigned)f2bf(pp.x) | ((unsigned)f2bf(pp.y) << 16);
+    sh.y = (unsigned)f2bf(pp.z) | ((unsigned)f2bf(pp.w) << 16);
+    reinterpret_cast<uint2*>(shadow)[i] = sh;
+  }
+  finish_ticket(step, ticket);
+}
+
 // SGD (+ optional heavy-ball momentum and decoupled weight decay)
 __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ buf,
                                                   bf16_t* __restrict__ shadow, long n, float lr, float momentum,
@@ -131,6 +177,21 @@ JDT_API int jdt_adamw(float* p, float* g, float* m, float* v, void* shadow, long
   if (shadow && (reinterpret_cast<uintptr_t>(shadow) & 7)) return -2;
   hipLaunchKernelGGL(adamw_kernel, dim3(ticket_grid(n, 4)), dim3(256), 0, static_cast<hipStream_t>(stream), p, g, m, v,
                      static_cast<bf16_t*>(shadow), n, lr, b1, b2, eps, wd, grad_scale, step, ticket, zero_grad);
+  return HIP_LAUNCH_CHECK();
+}
+
+// ranges: device int64 start[nr] (element offsets, % 4 == 0), prefix[nr] (exclusive sums of
+// the lengths, each % 4 == 0); total = sum of the lengths.  Needs step and ticket.
+JDT_API int jdt_adamw_ranges(float* p, float* g, float* m, float* v, void* shadow, const long* start,
+                             const long* prefix, int nr, long total, float lr, float b1, float b2, float eps, float wd,
+                             float grad_scale, int* step, unsigned* ticket, void* stream) {
+  if (nr <= 0 || total <= 0 || (total & 3) || !step || !ticket || !shadow) return -2;
+  if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
+       reinterpret_cast<uintptr_t>(v)) & 15) return -2;
+  if (reinterpret_cast<uintptr_t>(shadow) & 7) return -2;
+  hipLaunchKernelGGL(adamw_ranges_kernel, dim3(ticket_grid(total, 4)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     p, g, m, v, static_cast<bf16_t*>(shadow), start, prefix, nr, total, lr, b1, b2, eps, wd,
+                     grad_scale, step, ticket);
   return HIP_LAUNCH_CHECK();
 }
 

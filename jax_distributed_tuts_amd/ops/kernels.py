@@ -13,6 +13,7 @@ optimizer state are fp32.
 from __future__ import annotations
 
 import contextlib
+import math
 import os
 import ctypes
 from typing import Optional
@@ -145,13 +146,76 @@ def _align4(n: int) -> int:
     return _align(n)
 
 
-def dw_gemm(wgrad: Optional["WGradStream"], h, dz, out, **kw):
+def dw_gemm(wgrad: Optional["WGradStream"], h, dz, out, opt: Optional["EpilogueAdamW"] = None, name: str = "",
+            **kw):
     """``out += h^T dz`` (a_layout "km", b_layout "kn", fp32 accumulate), on the
-    side stream when ``wgrad`` is given (GPU), inline otherwise."""
+    side stream when ``wgrad`` is given (GPU), inline otherwise.  With ``opt`` (an
+    :class:`EpilogueAdamW` covering ``name``) this is the weight's final gradient of
+    the step and AdamW runs in the GEMM epilogue instead (see GemmArgs::opt_*)."""
+    acc = True
+    if opt is not None and opt.covers(name):
+        kw["opt"] = opt.views(name)
+        acc = not opt.only_contribution
     if wgrad is None or not h.is_cuda:
-        return gemm(h, dz, a_layout="km", b_layout="kn", out=out, accumulate=True, **kw)
-    wgrad.run(lambda: gemm(h, dz, a_layout="km", b_layout="kn", out=out, accumulate=True, **kw), h, dz)
+        return gemm(h, dz, a_layout="km", b_layout="kn", out=out, accumulate=acc, **kw)
+    wgrad.run(lambda: gemm(h, dz, a_layout="km", b_layout="kn", out=out, accumulate=acc, **kw), h, dz)
     return out
+
+
+class EpilogueAdamW:
+    """AdamW for one stage's step with the weight matrices updated in the epilogues of
+    their final weight-gradient GEMMs (the fp32 gradient of a fused weight never goes
+    to HBM when it has a single contribution) and every other parameter (biases,
+    LayerNorm, embeddings) by ONE multi-range launch (``finish``), which also advances
+    the device step counter -- instead of an AdamW pass over the whole flat buffer
+    (read p, g, m, v; write p, m, v, bf16 shadow, zeroed g: 34 B per parameter).
+    ``only_contribution``: the backward pass carrying it is the weights' sole gradient
+    contribution of the step (layer-major single pass) -> no read-modify-write of the
+    gradient buffer; otherwise (last of several microbatches) the epilogue adds the
+    accumulated gradient and re-zeroes it."""
+
+    def __init__(self, P, tx, opt_state, grad_scale: float, fused_names):
+        self.P, self.tx, self.o, self.grad_scale = P, tx, opt_state, float(grad_scale)
+        self.fused = [n for n in fused_names if n in P.offsets]
+        self.only_contribution = True
+        from ..utils.flat import _align
+
+        rest = sorted((P.offsets[n][0], _align(int(math.prod(P.offsets[n][1])))) for n in P.names()
+                      if n not in self.fused)
+        merged = []
+        for st_, ln in rest:
+            if merged and merged[-1][0] + merged[-1][1] == st_:
+                merged[-1][1] += ln
+            else:
+                merged.append([st_, ln])
+        starts = [m_[0] for m_ in merged]
+        pref, acc = [], 0
+        for _, ln in merged:
+            pref.append(acc)
+            acc += ln
+        dev = P.master.device
+        self.nr, self.total = len(merged), acc
+        self.start = torch.tensor(starts, dtype=torch.int64, device=dev)
+        self.prefix = torch.tensor(pref, dtype=torch.int64, device=dev)
+
+    def covers(self, name: str) -> bool:
+        return name in self.fused
+
+    def views(self, name: str):
+        off, shape = self.P.offsets[name]
+        n = int(math.prod(shape))
+        return (self.P.p(name), self.o["m"][off:off + n].view(shape), self.o["v"][off:off + n].view(shape),
+                self.P.s(name), self)
+
+    def finish(self):
+        """AdamW over every parameter not fused into a GEMM epilogue; advances the step."""
+        P, tx, o = self.P, self.tx, self.o
+        rc = _lib.lib().jdt_adamw_ranges(_ptr(P.master), _ptr(P.grad), _ptr(o["m"]), _ptr(o["v"]), _ptr(P.shadow),
+                                         _ptr(self.start), _ptr(self.prefix), self.nr, self.total,
+                                         float(tx.learning_rate), float(tx.b1), float(tx.b2), float(tx.eps),
+                                         float(tx.weight_decay), self.grad_scale, _ptr(o["count"]), _ptr(o["ticket"]),
+                                         _lib.stream_ptr())
+        _lib.check(rc, "jdt_adamw_ranges")
 
 
 # ----------------------------------------------------------------------------- philox (CPU mirror)
@@ -238,7 +302,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, a_layout: str = "mk", b_layout: st
          z_out: Optional[torch.Tensor] = None, z_in: Optional[torch.Tensor] = None, act_bwd: str = "none",
          keep_prob: float = 1.0, seed: int = 0, offset: int = 0, resid: Optional[torch.Tensor] = None,
          dbias: Optional[torch.Tensor] = None, step: Optional[torch.Tensor] = None,
-         cfg: int = -1, splits: int = -1) -> torch.Tensor:
+         cfg: int = -1, splits: int = -1, opt=None) -> torch.Tensor:
     """C = epilogue(alpha * A @ B).
 
     ``a`` holds logical A[M,K] as ``[M,K]`` (``a_layout="mk"``) or ``[K,M]`` ("km");
@@ -260,6 +324,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, a_layout: str = "mk", b_layout: st
     if out is None:
         out = (torch.zeros if accumulate else torch.empty)(*lead, M, N, dtype=out_dtype, device=a.device)
     if not _is_gpu(a):
+        assert opt is None, "epilogue AdamW is a GPU path"
         if step is not None and keep_prob < 1.0:
             offset = int(offset) + (int(step.item()) << 32)
         return _gemm_ref(a, b, a_layout, b_layout, out, accumulate, alpha, bias, act, z_out, z_in, act_bwd,
@@ -297,6 +362,17 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, a_layout: str = "mk", b_layout: st
     if step is not None:
         assert step.dtype == torch.int32
         g.step_ptr = step.data_ptr()
+    if opt is not None:   # (p, m, v, shadow views shaped like out, EpilogueAdamW): AdamW in the epilogue
+        pv, mv, vv, sv, eo = opt
+        assert out.dtype == torch.float32 and not batched
+        for t in (pv, mv, vv, sv):
+            assert t.shape == out.shape and t.is_contiguous() and out.is_contiguous()
+        g.opt_p, g.opt_m, g.opt_v, g.opt_s = pv.data_ptr(), mv.data_ptr(), vv.data_ptr(), sv.data_ptr()
+        g.opt_step = eo.o["count"].data_ptr()
+        tx = eo.tx
+        g.opt_lr, g.opt_b1, g.opt_b2, g.opt_eps, g.opt_wd, g.opt_gs = (float(tx.learning_rate), float(tx.b1),
+                                                                       float(tx.b2), float(tx.eps),
+                                                                       float(tx.weight_decay), eo.grad_scale)
     if _GROUP and not batched and cfg < 0 and splits < 0:
         _GROUP[-1].append((g, a.device, (a, b, out, bias, z_out, z_in, resid, dbias, step)))
         return out

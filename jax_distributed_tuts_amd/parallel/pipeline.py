@@ -224,13 +224,16 @@ class GPipeTrainer:
             if deep is not None:
                 deep.forward_backward(batch)
                 return
+        eo = self._epilogue_opt()
         if self.S == 1 and (cfg.merge_single_stage or (cfg.layer_major_single_stage and _no_dropout(self.model))):
             out, cache = self.model.forward(P, batch.inputs, train=True, seed=seed, offset=0, step=st.step_tensor)
             d = torch.empty_like(out)
             self.loss_head(out, batch.labels, d, n_parts=n_mb)
-            ov = self._overlapped_opt()
+            ov = self._overlapped_opt() if eo is None else None
+            if eo is not None:
+                eo.only_contribution = True   # one pass: each weight's only gradient contribution
             self.model.backward(P, cache, d, dout_is_dz=True, need_dx=False, wgrad=self.wgrad,
-                                on_ready=ov.ready if ov is not None else None)
+                                on_ready=ov.ready if ov is not None else None, opt=eo)
             return
         eng = self._fused_stage(mb, seed)
         if eng is not None:
@@ -254,15 +257,19 @@ class GPipeTrainer:
                 dlogits[i] = d
             else:
                 self._send(out, self.s + 1, i)
-        # ---- backward, reverse microbatch order
+        # ---- backward, reverse microbatch order (the last one, i = 0, carries the
+        # weights' final gradients: the in-epilogue optimizer when enabled)
+        if eo is not None:
+            eo.only_contribution = n_mb == 1
         for i in reversed(range(n_mb)):
+            oi = eo if i == 0 else None
             if self.last:
                 dx = self.model.backward(P, caches[i], dlogits[i], dout_is_dz=True, need_dx=not self.first,
-                                         wgrad=self.wgrad)
+                                         wgrad=self.wgrad, opt=oi)
             else:
                 dh = self._recv(self.model.output_shape(mb), self.act_dtype, self.s + 1, n_mb + i)
                 dx = self.model.backward(P, caches[i], dh, dout_is_dz=False, need_dx=not self.first,
-                                         wgrad=self.wgrad)
+                                         wgrad=self.wgrad, opt=oi)
             if not self.first:
                 self._send(dx, self.s - 1, n_mb + i)
             caches[i] = None
@@ -282,6 +289,7 @@ class GPipeTrainer:
 
     def invalidate(self):
         """After a checkpoint restore: drop captured graphs and the stage engine."""
+        self._eo = None
         self.graph = None
         self._ahead = None
         self.multi = None
@@ -342,6 +350,22 @@ class GPipeTrainer:
             if not self.first:
                 self._send(dx, self.s - 1, n_mb + i)
 
+    def _epilogue_opt(self):
+        """The in-epilogue AdamW (ops.kernels.EpilogueAdamW) for a transformer stage
+        with no data axis on a GPU: weights updated in their final weight-gradient
+        GEMMs, the rest by one multi-range launch in _sync_update.  JDT_LM_FUSED_OPT=0
+        turns it off (A/B)."""
+        if getattr(self, "_eo", None) is None:
+            from ..utils.train_state import AdamW
+
+            st, cfg = self.state, self.cfg
+            ok = (self.n_dp == 1 and self.wgrad is None and isinstance(st.tx, AdamW) and st.params.master.is_cuda
+                  and hasattr(self.model, "gemm_weight_names")
+                  and os.environ.get("JDT_LM_FUSED_OPT", "1") != "0")
+            self._eo = (K.EpilogueAdamW(st.params, st.tx, st.opt_state, 1.0 / (cfg.num_microbatches * self.n_dp),
+                                        self.model.gemm_weight_names()) if ok else False)
+        return self._eo or None
+
     def _overlapped_opt(self):
         """The layer-by-layer side-stream AdamW (one GPU, one stage, no data axis)."""
         if getattr(self, "_ov_opt", None) is None:
@@ -370,6 +394,13 @@ class GPipeTrainer:
             self.wgrad.join()  # every weight-gradient GEMM of the step has landed
         if self.deep_engine is not None and self.deep_engine.fuse_opt:
             return  # one GPU, one stage: AdamW + metrics fold ran in the backward epilogues
+        eo = self._epilogue_opt() if self.deep_engine is None and self.stage_engine is None else None
+        if eo is not None:
+            # weights: updated in their weight-gradient GEMM epilogues; the rest here
+            eo.finish()
+            with named_scope("sync_metrics"):
+                K.metrics_fold_(self.metrics, P.metrics_slot)
+            return
         with named_scope("sync_grads"):
             if self._xg_fused_opt:
                 tx, o = st.tx, st.opt_state

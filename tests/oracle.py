@@ -69,7 +69,7 @@ def lm_grads_fp64(params: Dict[str, torch.Tensor], cfg, tok: torch.Tensor, label
         qkv = h @ ps[f"{b}/attn/qkv/kernel"] + ps[f"{b}/attn/qkv/bias"]
         q, k, v = qkv.view(B, S, 3, H, Dh).permute(2, 0, 3, 1, 4)
         sc = (q @ k.transpose(-1, -2)) / math.sqrt(Dh)
-        sc = sc.masked_fill(torch.triu(torch.ones(S, S, dtype=torch.bool), 1), float("-inf"))
+        sc = sc.masked_fill(torch.triu(torch.ones(S, S, dtype=torch.bool, device=sc.device), 1), float("-inf"))
         o = (torch.softmax(sc, -1) @ v).permute(0, 2, 1, 3).reshape(B * S, d)
         x = x + o @ ps[f"{b}/attn/out/kernel"] + ps[f"{b}/attn/out/bias"]
         h2 = ln(x, ps[f"{b}/ln2/scale"], ps[f"{b}/ln2/bias"])

@@ -1,0 +1,76 @@
+"""Transformer LM on the GPU at the BENCH configuration (4 layers, d 512, 8 heads,
+d_ff 2048, S 128, V 2048, 16 sequences, 4 microbatches): every leaf's applied
+gradient against a float64 autograd oracle, and the in-epilogue AdamW
+(ops.kernels.EpilogueAdamW) against the plain AdamW pass."""
+import os
+
+import pytest
+import torch
+
+from jax_distributed_tuts_amd.models.transformer import TransformerConfig
+from jax_distributed_tuts_amd.parallel.pipeline_lm import build_lm_pipeline, lm_batch
+from jax_distributed_tuts_amd.utils.train_state import Batch, adamw, sgd
+
+from .oracle import check_grad, lm_grads_fp64, sgd_grads
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+CFG = TransformerConfig()   # the bench model
+
+
+def _trainer(tx, layer_major=True, fused_opt="1"):
+    old = os.environ.get("JDT_LM_FUSED_OPT")
+    os.environ["JDT_LM_FUSED_OPT"] = fused_opt
+    try:
+        tr, _ = build_lm_pipeline(None, DEV, CFG, num_microbatches=4, tx=tx, layer_major_single_stage=layer_major)
+        b = lm_batch(CFG, global_batch=16, seed=1)
+        b = Batch(b.inputs.to(DEV), b.labels.to(DEV))
+        tr.step(b)   # builds the epilogue optimizer (env read here)
+    finally:
+        if old is None:
+            os.environ.pop("JDT_LM_FUSED_OPT", None)
+        else:
+            os.environ["JDT_LM_FUSED_OPT"] = old
+    return tr, b
+
+
+@pytest.mark.parametrize("layer_major", [True, False])
+def test_lm_bench_config_grads_match_fp64_autograd(layer_major):
+    """One plain-SGD (lr 1) step: p_before - p_after is the applied gradient (mean CE
+    over all 2048 tokens); every one of the 54 leaves within the pinned oracle
+    tolerance (bf16 operands)."""
+    tr0, _ = build_lm_pipeline(None, DEV, CFG, num_microbatches=4, tx=sgd(1.0), layer_major_single_stage=layer_major)
+    before = {k: v.detach().clone() for k, v in tr0.state.params.state_dict().items()}
+    bb = lm_batch(CFG, global_batch=16, seed=1)
+    tr0.step(Batch(bb.inputs.to(DEV), bb.labels.to(DEV)))
+    torch.cuda.synchronize()
+    got = sgd_grads(before, tr0.state.params.state_dict())
+    want = lm_grads_fp64({k: v.to(DEV) for k, v in before.items()}, CFG, bb.inputs.to(DEV), bb.labels.to(DEV))
+    assert set(got) == set(want) and len(got) == 54
+    worst = 0.0
+    for k in sorted(want):
+        rel, scale = check_grad(got[k].cpu(), want[k].cpu(), k, rel_tol=0.05, scale_tol=0.02)
+        worst = max(worst, rel)
+    print(f"[lm bench grads, layer_major={layer_major}] worst rel err {worst:.3e}")
+
+
+@pytest.mark.parametrize("layer_major", [True, False])
+def test_lm_epilogue_adamw_matches_plain_adamw(layer_major):
+    """AdamW fused into the weight-gradient GEMM epilogues (+ one multi-range launch for
+    the rest) == the plain full-buffer AdamW pass, after 3 steps; the step counter
+    advances once per step."""
+    res = {}
+    for fused in ("1", "0"):
+        tr, b = _trainer(adamw(3e-4), layer_major, fused)
+        assert (getattr(tr, "_eo", None) not in (None, False)) == (fused == "1")
+        tr.step(b)
+        tr.step(b)
+        torch.cuda.synchronize()
+        res[fused] = (tr.state.params.master.clone(), tr.state.params.shadow.clone(),
+                      int(tr.state.opt_state["count"].item()), tr.state.params.grad.abs().max().item())
+    (p1, s1, c1, g1), (p0, s0, c0, g0) = res["1"], res["0"]
+    assert c1 == c0 == 3
+    assert g1 == 0.0 and g0 == 0.0   # gradient buffers left zeroed for the next step
+    d = (p1 - p0).abs()
+    assert float(d.max()) <= 1e-6 + 1e-5 * float(p0.abs().max()), float(d.max())
+    assert float(((s1.float() - p1.to(torch.bfloat16).float()).abs()).max()) == 0.0   # shadow = bf16(master)

@@ -16,3 +16,6 @@ for a in "--strategy fsdp" "" "--strategy fsdp --num-layers 4"; do
   done
 done
 grep '^{' gpurun_out/fsdp/b2.log > gpurun_out/fsdp/last_n2.json
+unset JDT_BACKEND
+timeout -k 10 400 python tools/gemm_split_sweep.py > gpurun_out/fsdp/split_sweep.txt 2>&1 || exit 1
+grep -v amdgpu.ids gpurun_out/fsdp/split_sweep.txt | sed 's/ | /\n   /g' | head -80

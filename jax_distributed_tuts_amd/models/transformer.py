@@ -177,9 +177,9 @@ class TransformerLM:
         if self.has_head:
             # dlogits (CE already added the head bias grad); the LN-bwd also reduces
             # the top block's fc2 bias grad (colsum of the residual gradient)
-            with K.gemm_group():  # dW and dX of a layer only need dz: one grouped launch
-                K.dw_gemm(wgrad, cache.hf, dout, P.g("head/kernel"), opt=opt, name="head/kernel")
-                dhf = K.gemm(dout, P.s("head/kernel"), b_layout="nk")
+            dhf = _dw_dx(opt, "head/kernel",
+                         lambda: K.dw_gemm(wgrad, cache.hf, dout, P.g("head/kernel"), opt=opt, name="head/kernel"),
+                         lambda: K.gemm(dout, P.s("head/kernel"), b_layout="nk"))
             dx = K.layernorm_bwd(dhf, cache.xf, cache.mf, cache.rf, P.p("ln_f/scale"), P.g("ln_f/scale"),
                                  P.g("ln_f/bias"), dsum=fc2_bias(layers[-1]) if layers else None)
             fc2_done = True
@@ -193,25 +193,23 @@ class TransformerLM:
             # x3 = x2 + u.W2 + b2
             if not fc2_done:
                 K.colsum_(dx, P.g(f"{b}/mlp/fc2/bias"))
-            with K.gemm_group():
-                K.dw_gemm(wgrad, bc.u, dx, P.g(f"{b}/mlp/fc2/kernel"), opt=opt, name=f"{b}/mlp/fc2/kernel")
-                dz1 = K.gemm(dx, P.s(f"{b}/mlp/fc2/kernel"), b_layout="nk", z_in=bc.z1, act_bwd="gelu",
-                             keep_prob=cache.keep, seed=cache.seed, offset=bc.off, step=cache.step,
-                             dbias=P.g(f"{b}/mlp/fc1/bias"))
-            with K.gemm_group():
-                K.dw_gemm(wgrad, bc.h2, dz1, P.g(f"{b}/mlp/fc1/kernel"), opt=opt, name=f"{b}/mlp/fc1/kernel")
-                dh2 = K.gemm(dz1, P.s(f"{b}/mlp/fc1/kernel"), b_layout="nk")
+            n2, n1 = f"{b}/mlp/fc2/kernel", f"{b}/mlp/fc1/kernel"
+            dz1 = _dw_dx(opt, n2, lambda: K.dw_gemm(wgrad, bc.u, dx, P.g(n2), opt=opt, name=n2),
+                         lambda: K.gemm(dx, P.s(n2), b_layout="nk", z_in=bc.z1, act_bwd="gelu",
+                                        keep_prob=cache.keep, seed=cache.seed, offset=bc.off, step=cache.step,
+                                        dbias=P.g(f"{b}/mlp/fc1/bias")))
+            dh2 = _dw_dx(opt, n1, lambda: K.dw_gemm(wgrad, bc.h2, dz1, P.g(n1), opt=opt, name=n1),
+                         lambda: K.gemm(dz1, P.s(n1), b_layout="nk"))
             # x2 = x + o.Wo + bo: the LN2-bwd output dx2 is also Wo's bias grad
             dx2 = K.layernorm_bwd(dh2, bc.x2, bc.m2, bc.r2, P.p(f"{b}/ln2/scale"), P.g(f"{b}/ln2/scale"),
                                   P.g(f"{b}/ln2/bias"), dres=dx, dsum=P.g(f"{b}/attn/out/bias"))
-            with K.gemm_group():
-                K.dw_gemm(wgrad, bc.o, dx2, P.g(f"{b}/attn/out/kernel"), opt=opt, name=f"{b}/attn/out/kernel")
-                do = K.gemm(dx2, P.s(f"{b}/attn/out/kernel"), b_layout="nk")
+            no, nq = f"{b}/attn/out/kernel", f"{b}/attn/qkv/kernel"
+            do = _dw_dx(opt, no, lambda: K.dw_gemm(wgrad, bc.o, dx2, P.g(no), opt=opt, name=no),
+                        lambda: K.gemm(dx2, P.s(no), b_layout="nk"))
             dqkv = K.attention_bwd(do, bc.qkv, bc.P, cache.nseq, c.seq_len, c.n_heads, o=bc.o,
                                    dbias=P.g(f"{b}/attn/qkv/bias"))
-            with K.gemm_group():
-                K.dw_gemm(wgrad, bc.h1, dqkv, P.g(f"{b}/attn/qkv/kernel"), opt=opt, name=f"{b}/attn/qkv/kernel")
-                dh1 = K.gemm(dqkv, P.s(f"{b}/attn/qkv/kernel"), b_layout="nk")
+            dh1 = _dw_dx(opt, nq, lambda: K.dw_gemm(wgrad, bc.h1, dqkv, P.g(nq), opt=opt, name=nq),
+                         lambda: K.gemm(dqkv, P.s(nq), b_layout="nk"))
             below = fc2_bias(layers[idx - 1]) if idx > 0 else None  # next (lower) block's fc2 bias grad
             dx = K.layernorm_bwd(dh1, bc.x, bc.m1, bc.r1, P.p(f"{b}/ln1/scale"), P.g(f"{b}/ln1/scale"),
                                  P.g(f"{b}/ln1/bias"), dres=dx2, dsum=below)
@@ -222,6 +220,20 @@ class TransformerLM:
             ready(["embed/wte", "embed/wpe"])
             return None
         return dx if need_dx else None
+
+
+def _dw_dx(opt, name: str, dw, dx):
+    """A Dense layer's weight gradient ``dw()`` and input gradient ``dx()`` (both only
+    need dz): one grouped launch.  With the in-epilogue optimizer covering the weight
+    (ops.kernels.EpilogueAdamW), the input gradient runs FIRST and alone -- it reads the
+    weight's bf16 shadow, which the weight-gradient GEMM's epilogue then overwrites."""
+    if opt is not None and opt.covers(name):
+        out = dx()
+        dw()
+        return out
+    with K.gemm_group():
+        dw()
+        return dx()
 
 
 def lm_stage(cfg: TransformerConfig, n_stages: int, stage: int) -> TransformerLM:

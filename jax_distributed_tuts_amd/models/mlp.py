@@ -32,6 +32,7 @@ from typing import Dict, List, Optional, Sequence
 import torch
 
 from ..ops import kernels as K
+from ..utils import rng as R
 from ..utils.flat import FlatParams, ParamSpec
 
 
@@ -76,12 +77,16 @@ class MLP:
 
         params = variables["params"] if "params" in variables else variables
         keep = 1.0 - self.dropout_rate if train else 1.0
-        seed = int((rngs or {}).get("dropout", 0)) & 0xFFFFFFFF
+        key = (rngs or {}).get("dropout", 0)
+        seed = int(key) & 0xFFFFFFFF
+        # a graph-replayed scan minibatch (utils.rng.ScanKey): its key is selected on the device
+        seed_dev = key.device_seed() if (isinstance(key, R.ScanKey) and keep < 1.0) else None
         h = x
         for i, n in enumerate(self.names):
             hid = self._hidden(i)
             h = dense(h, params[n]["kernel"], params[n]["bias"], act=self.act if hid else "none",
-                      keep=keep if hid else 1.0, seed=seed, offset=(self.layer_id_base + i) << 1)
+                      keep=keep if hid else 1.0, seed=seed, offset=(self.layer_id_base + i) << 1,
+                      seed_dev=seed_dev if hid else None)
         return h.float()
 
     apply = __call__
@@ -138,13 +143,17 @@ class MLP:
 
     # ------------------------------------------------------------------ backward
     def backward(self, P: FlatParams, cache: LayerCache, dout: torch.Tensor, *, dout_is_dz: bool = True,
-                 need_dx: bool = False, on_ready=None, wgrad=None) -> Optional[torch.Tensor]:
+                 need_dx: bool = False, on_ready=None, wgrad=None, opt=None) -> Optional[torch.Tensor]:
         """Accumulate param grads into ``P.grad``; return dx if ``need_dx``.
+        ``opt`` (the in-epilogue AdamW of the transformer stages) is not supported here
+        and must be None (the stage trainer only builds it for models that list
+        ``gemm_weight_names``).
 
         ``dout`` is the gradient w.r.t. the stack output.  With ``dout_is_dz``
         (the CE kernel already wrote dz and the top bias grad) it is used as the
         top layer's dz directly; otherwise the top layer's act/dropout backward
         and bias grad are applied first (pipeline stage boundary)."""
+        assert opt is None, "MLP.backward has no in-epilogue optimizer"
         L = self.L
         top = self.names[L - 1]
         if dout_is_dz:

@@ -38,6 +38,7 @@ class GemmArgs(ctypes.Structure):
         ("opt_p", c_void_p), ("opt_m", c_void_p), ("opt_v", c_void_p), ("opt_s", c_void_p), ("opt_step", c_void_p),
         ("opt_lr", c_float), ("opt_b1", c_float), ("opt_b2", c_float), ("opt_eps", c_float), ("opt_wd", c_float),
         ("opt_gs", c_float),
+        ("seed_ptr", c_void_p),
     ]
 
 
@@ -80,7 +81,7 @@ _SIGS = {
                         c_void_p, c_void_p, c_int, c_void_p]),
     "jdt_cast_f32_bf16": (c_int, [c_void_p, c_void_p, c_long, c_void_p]),
     "jdt_scale": (c_int, [c_void_p, c_long, c_float, c_void_p]),
-    "jdt_act_bwd": (c_int, [c_void_p, c_void_p, c_int, c_float, c_ulonglong, c_ulonglong, c_void_p, c_int, c_int,
+    "jdt_act_bwd": (c_int, [c_void_p, c_void_p, c_int, c_float, c_ulonglong, c_ulonglong, c_void_p, c_void_p, c_int, c_int,
                             c_void_p, c_void_p, c_void_p]),
     "jdt_metrics_fold": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "jdt_ln_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,

@@ -23,7 +23,7 @@ from . import kernels as K
 
 class _Dense(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, act: str, keep: float, seed: int, offset: int):
+    def forward(ctx, x, w, b, act: str, keep: float, seed: int, offset: int, seed_dev=None):
         M = x.shape[0]
         out = torch.empty(M, w.shape[1], dtype=torch.bfloat16, device=x.device)
         hid = act != "none" or keep < 1.0
@@ -33,9 +33,10 @@ class _Dense(torch.autograd.Function):
         if xin.dtype != torch.bfloat16:
             xin = K.cast_bf16_(xin.float(), torch.empty(xin.shape, dtype=torch.bfloat16, device=xin.device))
         K.gemm(xin, w.detach(), a_layout="mk", b_layout="kn", out=out, bias=b.detach(),
-               act=act, z_out=z, keep_prob=keep, seed=seed, offset=offset)
+               act=act, z_out=z, keep_prob=keep, seed=seed, offset=offset, seed_dev=seed_dev)
         ctx.save_for_backward(xin, w, z)
         ctx.cfg = (act, keep, seed, offset, x.dtype)
+        ctx.seed_dev = seed_dev
         return out
 
     @staticmethod
@@ -45,7 +46,7 @@ class _Dense(torch.autograd.Function):
         dz = dout.to(torch.bfloat16).contiguous()
         db = torch.zeros(w.shape[1], dtype=torch.float32, device=dz.device)
         # dz = dout * mask/keep * act'(z) and db = colsum(dz) in one pass (any width)
-        dz = K.act_bwd(dz, z, act, keep_prob=keep, seed=seed, offset=offset, dbias=db)
+        dz = K.act_bwd(dz, z, act, keep_prob=keep, seed=seed, offset=offset, dbias=db, seed_dev=ctx.seed_dev)
         dx = dw = None
         if ctx.needs_input_grad[1]:
             dw = torch.zeros(w.shape, dtype=torch.float32, device=dz.device)
@@ -54,15 +55,16 @@ class _Dense(torch.autograd.Function):
             dx = torch.empty(xin.shape[0], w.shape[0], dtype=torch.bfloat16, device=dz.device)
             K.gemm(dz, w.detach(), a_layout="mk", b_layout="nk", out=dx)
             dx = dx.to(xdtype)
-        return dx, dw, db if ctx.needs_input_grad[2] else None, None, None, None, None
+        return dx, dw, db if ctx.needs_input_grad[2] else None, None, None, None, None, None
 
 
 def dense(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, act: str = "none", keep: float = 1.0,
-          seed: int = 0, offset: int = 0) -> torch.Tensor:
+          seed: int = 0, offset: int = 0, seed_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``dropout(act(bf16(x) @ bf16(w) + b))`` as a bf16 [M, N] tensor, differentiable
     w.r.t. x, w (fp32 [in, out]) and b.  Dropout keeps with probability ``keep``
-    under Philox stream (seed, offset) -- the same masks the engine draws."""
-    return _Dense.apply(x, w, b, act, float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset))
+    under Philox stream (seed, offset) -- the same masks the engine draws.
+    ``seed_dev``: device int64[1] seed read by the kernels instead of ``seed``."""
+    return _Dense.apply(x, w, b, act, float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset), seed_dev)
 
 
 class _SoftmaxXent(torch.autograd.Function):

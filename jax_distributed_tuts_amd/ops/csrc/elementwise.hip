@@ -11,7 +11,8 @@ namespace jdt {
 
 __global__ void __launch_bounds__(256) act_bwd_kernel(const bf16_t* __restrict__ dh, const bf16_t* __restrict__ z,
                                                       int act, float keep_prob, unsigned long long seed,
-                                                      unsigned long long offset, const int* step_ptr, int M, int N,
+                                                      unsigned long long offset, const int* step_ptr,
+                                                      const unsigned long long* seed_ptr, int M, int N,
                                                       int rows_per_block, bf16_t* __restrict__ dz,
                                                       float* __restrict__ dbias) {
   const int col = blockIdx.x * 256 + threadIdx.x;
@@ -21,6 +22,7 @@ __global__ void __launch_bounds__(256) act_bwd_kernel(const bf16_t* __restrict__
   const bool drop = keep_prob < 1.f;
   const float inv_keep = drop ? 1.f / keep_prob : 1.f;
   const unsigned long long doff = offset + (step_ptr ? ((unsigned long long)(unsigned)step_ptr[0] << 32) : 0ull);
+  if (seed_ptr) seed = seed_ptr[0];
   float csum = 0.f;
   u32x4 dbits = {0u, 0u, 0u, 0u};
   for (int r = r0; r < r1; ++r) {  // r0 is a multiple of 4: refresh the Philox bits per 4-row group
@@ -45,14 +47,14 @@ __global__ void metrics_fold_kernel(float* running, float* slot, int n) {
 using namespace jdt;
 
 JDT_API int jdt_act_bwd(const void* dh, const void* z, int act, float keep_prob, unsigned long long seed,
-                        unsigned long long offset, const int* step_ptr, int M, int N, void* dz, float* dbias,
-                        void* stream) {
+                        unsigned long long offset, const int* step_ptr, const unsigned long long* seed_ptr, int M,
+                        int N, void* dz, float* dbias, void* stream) {
   if (M <= 0 || N <= 0) return 0;
   const int rpb = 32;
   dim3 grid((N + 255) / 256, (M + rpb - 1) / rpb);
   hipLaunchKernelGGL(act_bwd_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(stream),
                      static_cast<const bf16_t*>(dh), static_cast<const bf16_t*>(z), act, keep_prob, seed, offset,
-                     step_ptr, M, N, rpb, static_cast<bf16_t*>(dz), dbias);
+                     step_ptr, seed_ptr, M, N, rpb, static_cast<bf16_t*>(dz), dbias);
   return HIP_LAUNCH_CHECK();
 }
 

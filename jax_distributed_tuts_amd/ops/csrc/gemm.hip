@@ -55,6 +55,9 @@ struct GemmArgs {
   // advances the device step counter (read here as t = step + 1).
   float* opt_p; float* opt_m; float* opt_v; bf16_t* opt_s; const int* opt_step;
   float opt_lr, opt_b1, opt_b2, opt_eps, opt_wd, opt_gs;
+  // optional device-resident dropout seed (replaces ``seed``): a hipGraph replayed once
+  // per minibatch selects that minibatch's key on the device (util.accum_grads_scan)
+  const unsigned long long* seed_ptr;
 };
 
 // AdamW of one element in a GEMM epilogue (see GemmArgs::opt_*): optax.adamw, the
@@ -312,6 +315,7 @@ __device__ __forceinline__ void gemm_finish(const GemmArgs& g, f32x4 (&acc)[TM][
   const bool drop = g.keep_prob < 1.0f;
   const float inv_keep = drop ? 1.0f / g.keep_prob : 1.0f;
   const unsigned long long doff = g.offset + (g.step_ptr ? ((unsigned long long)(unsigned)g.step_ptr[0] << 32) : 0ull);
+  const unsigned long long dseed = g.seed_ptr ? g.seed_ptr[0] : g.seed;
   const OptBC obc = opt_bc(g);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -325,7 +329,7 @@ __device__ __forceinline__ void gemm_finish(const GemmArgs& g, f32x4 (&acc)[TM][
       // the lane's 4 rows form one dropout group: one Philox call for all 4
       const int row0 = tm0 + (wm * TM + i) * 16 + (lane >> 4) * 4;
       u32x4 dbits = {0u, 0u, 0u, 0u};
-      if (drop && cok) dbits = dropout_bits(g.seed, doff, dropout_group(z, row0, col, g.M, g.N));
+      if (drop && cok) dbits = dropout_bits(dseed, doff, dropout_group(z, row0, col, g.M, g.N));
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = row0 + e;
@@ -429,6 +433,7 @@ __device__ __forceinline__ void gemm_finish_lds(const GemmArgs& g, f32x4 (&acc)[
   const bool drop = g.keep_prob < 1.0f;
   const float inv_keep = drop ? 1.0f / g.keep_prob : 1.0f;
   const unsigned long long doff = g.offset + (g.step_ptr ? ((unsigned long long)(unsigned)g.step_ptr[0] << 32) : 0ull);
+  const unsigned long long dseed = g.seed_ptr ? g.seed_ptr[0] : g.seed;
   constexpr int CPP = BN < 256 ? BN : 256;      // columns per pass
   constexpr int RGS = 256 / CPP;                 // row groups advanced per pass
   const int cl = tid % CPP;
@@ -442,7 +447,7 @@ __device__ __forceinline__ void gemm_finish_lds(const GemmArgs& g, f32x4 (&acc)[
     for (int rg = tid / CPP; rg < BM / 4; rg += RGS) {
       const int row0 = tm0 + rg * 4;
       u32x4 dbits = {0u, 0u, 0u, 0u};
-      if (drop && cok) dbits = dropout_bits(g.seed, doff, dropout_group(z, row0, col, g.M, g.N));
+      if (drop && cok) dbits = dropout_bits(dseed, doff, dropout_group(z, row0, col, g.M, g.N));
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = row0 + e;
@@ -543,6 +548,7 @@ __device__ __forceinline__ void gemm_finish_vec(const GemmArgs& g, f32x4 (&acc)[
   const bool drop = g.keep_prob < 1.0f;
   const float inv_keep = drop ? 1.0f / g.keep_prob : 1.0f;
   const unsigned long long doff = g.offset + (g.step_ptr ? ((unsigned long long)(unsigned)g.step_ptr[0] << 32) : 0ull);
+  const unsigned long long dseed = g.seed_ptr ? g.seed_ptr[0] : g.seed;
   const int cc = tid % CU;
   const int col = tn0 + cc * 8;
   float bv[8];
@@ -570,7 +576,7 @@ __device__ __forceinline__ void gemm_finish_vec(const GemmArgs& g, f32x4 (&acc)[
     u32x4 db[8];
     if (drop) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) db[k] = dropout_bits(g.seed, doff, dropout_group(z, row0, col + k, g.M, g.N));
+      for (int k = 0; k < 8; ++k) db[k] = dropout_bits(dseed, doff, dropout_group(z, row0, col + k, g.M, g.N));
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {

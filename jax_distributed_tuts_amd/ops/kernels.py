@@ -302,7 +302,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, a_layout: str = "mk", b_layout: st
          z_out: Optional[torch.Tensor] = None, z_in: Optional[torch.Tensor] = None, act_bwd: str = "none",
          keep_prob: float = 1.0, seed: int = 0, offset: int = 0, resid: Optional[torch.Tensor] = None,
          dbias: Optional[torch.Tensor] = None, step: Optional[torch.Tensor] = None,
-         cfg: int = -1, splits: int = -1, opt=None) -> torch.Tensor:
+         cfg: int = -1, splits: int = -1, opt=None, seed_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
     """C = epilogue(alpha * A @ B).
 
     ``a`` holds logical A[M,K] as ``[M,K]`` (``a_layout="mk"``) or ``[K,M]`` ("km");
@@ -310,7 +310,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, a_layout: str = "mk", b_layout: st
     ``[N,K]`` ("nk").  Optional leading batch dim on every operand.
     Epilogue order: +bias -> (store z_out) -> *act'(z_in) -> act -> dropout -> +resid
     -> store/accumulate; ``dbias += colsum(result)``.  Dropout uses Philox stream
-    (seed, offset + (step[0] << 32)) when a device step counter is given.
+    (seed, offset + (step[0] << 32)) when a device step counter is given;
+    ``seed_dev`` (device int64[1]) replaces ``seed`` by a value read in the kernel.
     """
     batched = a.dim() == 3
     if a_layout == "mk":
@@ -327,6 +328,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, a_layout: str = "mk", b_layout: st
         assert opt is None, "epilogue AdamW is a GPU path"
         if step is not None and keep_prob < 1.0:
             offset = int(offset) + (int(step.item()) << 32)
+        if seed_dev is not None:
+            seed = int(seed_dev.item())
         return _gemm_ref(a, b, a_layout, b_layout, out, accumulate, alpha, bias, act, z_out, z_in, act_bwd,
                          keep_prob, seed, offset, resid, dbias)
     for t in (a, b, out, z_out, z_in, resid):
@@ -362,6 +365,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, a_layout: str = "mk", b_layout: st
     if step is not None:
         assert step.dtype == torch.int32
         g.step_ptr = step.data_ptr()
+    if seed_dev is not None:
+        assert seed_dev.dtype == torch.int64 and seed_dev.is_cuda
+        g.seed_ptr = seed_dev.data_ptr()
     if opt is not None:   # (p, m, v, shadow views shaped like out, EpilogueAdamW): AdamW in the epilogue
         pv, mv, vv, sv, eo = opt
         assert out.dtype == torch.float32 and not batched
@@ -374,7 +380,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, a_layout: str = "mk", b_layout: st
                                                                        float(tx.b2), float(tx.eps),
                                                                        float(tx.weight_decay), eo.grad_scale)
     if _GROUP and not batched and cfg < 0 and splits < 0:
-        _GROUP[-1].append((g, a.device, (a, b, out, bias, z_out, z_in, resid, dbias, step)))
+        _GROUP[-1].append((g, a.device, (a, b, out, bias, z_out, z_in, resid, dbias, step, seed_dev)))
         return out
     _launch_gemm(g, int(a.shape[0]) if batched else 1, cfg, splits, a.device)
     return out
@@ -555,8 +561,9 @@ def cast_bf16_(src: torch.Tensor, dst: torch.Tensor):
 # ----------------------------------------------------------------------------- elementwise
 def act_bwd(dh: torch.Tensor, z: Optional[torch.Tensor], act: str, *, keep_prob: float = 1.0, seed: int = 0,
             offset: int = 0, step: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-            dbias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """dz = dh * dropout_mask/keep * act'(z); dbias += colsum(dz).  [M,N] bf16."""
+            dbias: Optional[torch.Tensor] = None, seed_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dz = dh * dropout_mask/keep * act'(z); dbias += colsum(dz).  [M,N] bf16.
+    ``seed_dev``: device int64[1] dropout seed (replaces ``seed``, see :func:`gemm`)."""
     M, N = dh.shape
     if out is None:
         out = torch.empty(M, N, dtype=torch.bfloat16, device=dh.device)
@@ -566,7 +573,7 @@ def act_bwd(dh: torch.Tensor, z: Optional[torch.Tensor], act: str, *, keep_prob:
             v = v * act_grad_t(act, z.float())
         if keep_prob < 1.0:
             off = int(offset) + ((int(step.item()) << 32) if step is not None else 0)
-            mask = dropout_mask(seed, off, (M, N), keep_prob)
+            mask = dropout_mask(int(seed_dev.item()) if seed_dev is not None else seed, off, (M, N), keep_prob)
             v = torch.where(mask, v / keep_prob, torch.zeros_like(v))
         out.copy_(v.to(out.dtype))
         if dbias is not None:
@@ -574,7 +581,8 @@ def act_bwd(dh: torch.Tensor, z: Optional[torch.Tensor], act: str, *, keep_prob:
         return out
     assert dh.is_contiguous() and out.is_contiguous() and (z is None or z.is_contiguous())
     rc = _lib.lib().jdt_act_bwd(_ptr(dh), _ptr(z), ACT[act] if z is not None else 0, float(keep_prob),
-                                int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _ptr(step), M, N, _ptr(out),
+                                int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _ptr(step), _ptr(seed_dev), M, N,
+                                _ptr(out),
                                 _ptr(dbias), _lib.stream_ptr())
     _lib.check(rc, "jdt_act_bwd")
     return out

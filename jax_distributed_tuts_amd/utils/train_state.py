@@ -256,20 +256,27 @@ def accum_grads_scan(batch: Batch, state: TrainState, key: int, n_minbatch: int,
                      loss_fn: LossFn) -> Tuple[GradBuffer, Metrics]:
     """util.py:81-137.  Rolled loop: ONE minibatch step, captured once as a hipGraph
     that reads its minibatch from device-resident input slots, replayed
-    ``n_minbatch`` times on GPU (a plain loop on CPU).  The captured call gets
-    ``rng = key`` and ``minibatch_index`` = a device int32 tensor holding ``i``
-    during replay ``i`` (the reference's scan indexes its rngs with the traced loop
-    index; a captured Python int could not change between replays), so a loss
-    function draws per-minibatch randomness by folding that device index in -- as
-    the DP trainer's ``accum="scan"`` mode does (parallel/dp.py), where scan ==
-    loop bit for bit.  Dropout-free loss functions give the loop's result
-    (tests/test_util_api.py)."""
+    ``n_minbatch`` times on GPU (eagerly, one minibatch at a time, on CPU).
+
+    * engine contract: the captured call gets ``rng = key`` and ``minibatch_index`` =
+      a device int32 tensor holding ``i`` during replay ``i`` (a captured Python int
+      could not change between replays), so the loss draws per-minibatch randomness
+      by folding that device index in -- as the DP trainer's ``accum="scan"`` mode
+      does (parallel/dp.py), where scan == loop bit for bit;
+    * reference contract (autograd ``loss_fn(params, apply_fn, batch, rng)``): the
+      forward AND its autograd backward are captured; ``rng`` is a
+      :class:`~jax_distributed_tuts_amd.utils.rng.ScanKey` holding every minibatch's
+      split key with the device index selecting one -- the reference's
+      ``keys[batch_idx]`` (util.py:107-108) -- so models' dropout draws the loop's
+      masks exactly (tests/test_reference_loss_fn.py).  A loss whose ops cannot be
+      captured runs the same body eagerly, with a warning."""
     bs = batch.size
     mb = bs // n_minbatch
     dev = batch.inputs.device
-    if dev.type != "cuda" or is_reference_loss_fn(loss_fn):
-        # CPU, or an autograd (reference-contract) loss: the rolled loop runs eagerly,
-        # one minibatch at a time with its own split key (util.py:91, 95-111)
+    ref = is_reference_loss_fn(loss_fn)
+    if ref:
+        return _accum_scan_reference(batch, state, key, n_minbatch, loss_fn)
+    if dev.type != "cuda":
         return accum_grads_loop(batch, state, key, n_minbatch, loss_fn)
     # device-resident slot the captured step reads its minibatch from
     xin = torch.empty((mb,) + tuple(batch.inputs.shape[1:]), dtype=batch.inputs.dtype, device=dev)
@@ -286,8 +293,7 @@ def accum_grads_scan(batch: Batch, state: TrainState, key: int, n_minbatch: int,
     xin.copy_(batch.inputs[0:mb])
     yin.copy_(batch.labels[0:mb])
     _body(0)
-    metrics = _metrics_add(metrics, {k: tuple(x.clone() if torch.is_tensor(x) else x for x in v)
-                                     for k, v in mslot["m"].items()})
+    metrics = _metrics_add(metrics, _clone_metrics(mslot["m"]))
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -303,8 +309,67 @@ def accum_grads_scan(batch: Batch, state: TrainState, key: int, n_minbatch: int,
             yin.copy_(batch.labels[i * mb:(i + 1) * mb])
             idx.fill_(i)
             g.replay()
-            metrics = _metrics_add(metrics, {k: tuple(x.clone() if torch.is_tensor(x) else x for x in v)
-                                             for k, v in mslot["m"].items()})
+            metrics = _metrics_add(metrics, _clone_metrics(mslot["m"]))
+    return GradBuffer(state.params, 1.0 / n_minbatch), metrics
+
+
+def _clone_metrics(m: Metrics) -> Metrics:
+    return {k: tuple(x.clone() if torch.is_tensor(x) else x for x in v) for k, v in m.items()}
+
+
+# (grads buffer, capture outcome) of the most recent reference-contract scan, for tests / logs
+LAST_SCAN_MODE = {"mode": None}
+
+
+def _accum_scan_reference(batch: Batch, state: TrainState, key: int, n_minbatch: int,
+                          loss_fn: LossFn) -> Tuple[GradBuffer, Metrics]:
+    """The reference-contract scan (see :func:`accum_grads_scan`)."""
+    bs = batch.size
+    mb = bs // n_minbatch
+    dev = batch.inputs.device
+    xin = torch.empty((mb,) + tuple(batch.inputs.shape[1:]), dtype=batch.inputs.dtype, device=dev)
+    yin = torch.empty((mb,), dtype=batch.labels.dtype, device=dev)
+    idx = torch.zeros(1, dtype=torch.int32, device=dev)
+    skey = R.ScanKey.from_keys(R.split(key, n_minbatch), idx)
+    out = {}
+
+    def _body():
+        out["m"] = value_and_grad_into(loss_fn, state, Batch(xin, yin), skey)[1]
+
+    def _load(i: int):
+        xin.copy_(batch.inputs[i * mb:(i + 1) * mb])
+        yin.copy_(batch.labels[i * mb:(i + 1) * mb])
+        idx.fill_(i)
+
+    metrics = None
+    _load(0)
+    _body()   # minibatch 0 eagerly: warm-up (allocations, autograd graph, kernel library)
+    metrics = _metrics_add(metrics, _clone_metrics(out["m"]))
+    if n_minbatch == 1:
+        LAST_SCAN_MODE["mode"] = "eager"
+        return GradBuffer(state.params, 1.0), metrics
+    graph = None
+    if dev.type == "cuda":
+        _load(1)
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g):
+                _body()
+            graph = g
+        except Exception as e:   # an op of the user's loss that cannot be captured
+            import logging
+
+            logging.getLogger("jdt.util").warning("accum_grads_scan: loss_fn not capturable (%s); "
+                                                  "running the rolled step eagerly", e)
+            torch.cuda.synchronize()
+    LAST_SCAN_MODE["mode"] = "graph" if graph is not None else "eager"
+    for i in range(1, n_minbatch):
+        _load(i)
+        if graph is not None:
+            graph.replay()
+        else:
+            _body()
+        metrics = _metrics_add(metrics, _clone_metrics(out["m"]))
     return GradBuffer(state.params, 1.0 / n_minbatch), metrics
 
 

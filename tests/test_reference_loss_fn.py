@@ -88,3 +88,36 @@ def test_reference_train_step_reduces_loss():
         st = st.apply_gradients(grads=grads, rng=rng)
         losses.append(float(step_metrics["loss"][0]) / step_metrics["loss"][1])
     assert losses[-1] < losses[0] and st.step == 6
+
+
+def _scan_vs_loop(dev):
+    """The rolled (captured on GPU) reference-contract step draws the loop's dropout
+    masks: scan == loop, gradient and metrics, bit for bit."""
+    from jax_distributed_tuts_amd.utils import train_state as TS
+
+    out = []
+    for use_scan in (False, True):
+        st, _, bd = _setup(dev, 0.1)
+        grads, metrics = accum_grads(st, bd, R.PRNGKey(11), 4, loss_fn, use_scan=use_scan)
+        out.append((st.params.grad.clone(), float(metrics["loss"][0]), float(metrics["accuracy"][0])))
+    assert torch.equal(out[0][0], out[1][0])
+    assert out[0][1:] == out[1][1:]
+    return TS.LAST_SCAN_MODE["mode"]
+
+
+def test_scan_key_folds_match_host_keys():
+    keys = R.split(R.PRNGKey(5), 4)
+    idx = torch.tensor([3], dtype=torch.int32)
+    sk = fold_rng_over_axis(R.ScanKey.from_keys(keys, idx), DATA_AXIS)
+    want = [fold_rng_over_axis(k, DATA_AXIS) for k in keys]
+    assert sk.keys == want and int(sk.device_seed()) == want[3] & 0xFFFFFFFF
+    assert [R._s64(w) for w in want] == sk.dev.tolist()
+
+
+def test_reference_scan_equals_loop_cpu():
+    assert _scan_vs_loop("cpu") == "eager"
+
+
+@pytest.mark.gpu
+def test_reference_scan_equals_loop_gpu_captured():
+    assert _scan_vs_loop(torch.device("cuda", 0)) == "graph"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 3 batch: every new GPU test, then benches (transformer both modes, FSDP/DP N=2 shared-GPU), then the GEMM split sweep
 cd /root/repo && export TMPDIR=/tmp PYTHONUNBUFFERED=1 && mkdir -p gpurun_out/b1
-timeout -k 10 900 python -u -m pytest tests/test_lm_gpu.py tests/test_xgmi_gpu.py tests/test_kernels_gpu.py -k "lm_ or fsdp_over_xgmi or xgmi_collectives or ln_gemm or attn128 or transformer" -x -v -s --timeout 300 --timeout-method thread > gpurun_out/b1/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_reference_loss_fn.py tests/test_lm_gpu.py tests/test_xgmi_gpu.py tests/test_kernels_gpu.py -k "reference or lm_ or fsdp_over_xgmi or xgmi_collectives or ln_gemm or attn128 or transformer or gemm_dropout or dropout" -x -v -s --timeout 300 --timeout-method thread > gpurun_out/b1/pytest.log 2>&1
 rc=$?; grep -E "PASSED|FAILED|ERROR|worst" gpurun_out/b1/pytest.log | tail -40; tail -3 gpurun_out/b1/pytest.log; [ $rc -ne 0 ] && exit $rc
 for a in "--strategy pp --model transformer" "--strategy pp --model transformer --microbatch-passes"; do
   for f in 1 0; do
@@ -19,5 +19,7 @@ for a in "--strategy fsdp" "" "--strategy fsdp --num-layers 4"; do
   done
 done
 unset JDT_BACKEND
+timeout -k 10 400 python tools/pp_schedule.py --reps 200 --out gpurun_out/b1/pp_schedule.json > gpurun_out/b1/pp_schedule.log 2>&1 || { tail -20 gpurun_out/b1/pp_schedule.log; exit 1; }
+cat gpurun_out/b1/pp_schedule.log
 timeout -k 10 400 python tools/gemm_split_sweep.py > gpurun_out/b1/split_sweep.txt 2>&1 || exit 1
 grep -v amdgpu.ids gpurun_out/b1/split_sweep.txt | sed 's/ | /\n   /g' | head -60

@@ -84,6 +84,35 @@ __device__ __forceinline__ float opt_update(const GemmArgs& g, const OptBC& bc, 
   return pp;
 }
 
+// The same for 8 consecutive elements (16-byte aligned): p / m / v as float4 pairs,
+// the bf16 shadow as one 16-byte store -- the vectorised epilogue's unit.
+__device__ __forceinline__ u32x4 opt_update8(const GemmArgs& g, const OptBC& bc, long i, const float (&grad)[8]) {
+  float4* P4 = reinterpret_cast<float4*>(g.opt_p + i);
+  float4* M4 = reinterpret_cast<float4*>(g.opt_m + i);
+  float4* V4 = reinterpret_cast<float4*>(g.opt_v + i);
+  const float4 p0 = P4[0], p1 = P4[1], m0 = M4[0], m1 = M4[1], v0 = V4[0], v1 = V4[1];
+  float p[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+  float m[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+  float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float gr = grad[k] * g.opt_gs;
+    m[k] = g.opt_b1 * m[k] + (1.f - g.opt_b1) * gr;
+    v[k] = g.opt_b2 * v[k] + (1.f - g.opt_b2) * gr * gr;
+    p[k] -= g.opt_lr * ((m[k] * bc.rbc1) / (sqrtf(v[k] * bc.rbc2) + g.opt_eps) + g.opt_wd * p[k]);
+  }
+  P4[0] = make_float4(p[0], p[1], p[2], p[3]);
+  P4[1] = make_float4(p[4], p[5], p[6], p[7]);
+  M4[0] = make_float4(m[0], m[1], m[2], m[3]);
+  M4[1] = make_float4(m[4], m[5], m[6], m[7]);
+  V4[0] = make_float4(v[0], v[1], v[2], v[3]);
+  V4[1] = make_float4(v[4], v[5], v[6], v[7]);
+  u32x4 o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) o[k] = (unsigned)f2bf(p[2 * k]) | ((unsigned)f2bf(p[2 * k + 1]) << 16);
+  return o;
+}
+
 __device__ __forceinline__ long zoff(const GemmArgs& g, int z, long s1, long s2) {
   return g.zin > 1 ? (long)(z / g.zin) * s1 + (long)(z % g.zin) * s2 : (long)z * s1;
 }
@@ -570,8 +599,13 @@ __device__ __forceinline__ void gemm_finish_vec(const GemmArgs& g, f32x4 (&acc)[
   for (int k = 0; k < 8; ++k) cs[k] = 0.f;
   const long cbase = zoff(g, z, g.sC, g.sC2);
   const OptBC obc = opt_bc(g);
-  for (int u = tid; u < NU; u += NT) {
-    const int rl = (u / CU) * 4;  // first row of the unit within the tile
+  // rows per unit: one dropout group (4 rows) with dropout, else ONE row -- on a 32-row
+  // tile that is 4x the threads of the epilogue busy (NU = one wave's worth of 4-row
+  // units), which matters for the memory-heavy epilogues (fused AdamW: 26 B/element)
+  const int RU = drop ? 4 : 1;
+  const int nu = NU * (4 / RU);
+  for (int u = tid; u < nu; u += NT) {
+    const int rl = (u / CU) * RU;  // first row of the unit within the tile
     const int row0 = tm0 + rl;
     u32x4 db[8];
     if (drop) {
@@ -580,6 +614,7 @@ __device__ __forceinline__ void gemm_finish_vec(const GemmArgs& g, f32x4 (&acc)[
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
+      if (e >= RU) break;
       const int row = row0 + e;
       float v[8];
       {
@@ -624,12 +659,7 @@ __device__ __forceinline__ void gemm_finish_vec(const GemmArgs& g, f32x4 (&acc)[
           Cp[0] = make_float4(0.f, 0.f, 0.f, 0.f);
           Cp[1] = Cp[0];
         }
-        u32x4 o;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          o[k] = (unsigned)f2bf(opt_update(g, obc, co + 2 * k, v[2 * k])) |
-                 ((unsigned)f2bf(opt_update(g, obc, co + 2 * k + 1, v[2 * k + 1])) << 16);
-        *reinterpret_cast<u32x4*>(g.opt_s + co) = o;
+        *reinterpret_cast<u32x4*>(g.opt_s + co) = opt_update8(g, obc, co, v);
       } else if (g.c_f32) {
         float4* Cp = reinterpret_cast<float4*>(static_cast<float*>(g.C) + co);
         float4 o0 = make_float4(v[0], v[1], v[2], v[3]), o1 = make_float4(v[4], v[5], v[6], v[7]);
@@ -689,7 +719,7 @@ static bool epi_vec_ok(const GemmArgs& g, int batch) {
   };
   return rows(g.C, g.ldc, g.sC, g.sC2, g.c_f32) && rows(g.Zout, g.ldz, g.sZ, 0, 0) && rows(g.Zin, g.ldzin, g.sZin, 0, 0) &&
          rows(g.resid, g.ldr, g.sR, 0, 0) && (!g.bias || al(g.bias)) && g.N % 8 == 0 &&
-         (!g.opt_s || (al(g.opt_s) && g.ldc % 8 == 0));   // fused AdamW: 16-byte bf16 shadow stores
+         (!g.opt_s || (al(g.opt_s) && al(g.opt_p) && al(g.opt_m) && al(g.opt_v) && g.ldc % 8 == 0));  // fused AdamW: 16-byte accesses
 }
 
 template <int WM, int WN, int TM, int TN, int BK, bool AF32, bool BF32, int PRE, bool EXACT = false>

@@ -617,7 +617,8 @@ def _gemm_raw(*, A, lda, B, ldb, C, ldc, M, N, K, a_trans=False, b_kn=False, a_f
 
 
 # ----------------------------------------------------------------------------- attention
-def attention_fwd(qkv: torch.Tensor, B: int, S: int, H: int, causal: bool = True, impl: Optional[str] = None):
+def attention_fwd(qkv: torch.Tensor, B: int, S: int, H: int, causal: bool = True, impl: Optional[str] = None,
+                  o_out: Optional[torch.Tensor] = None):
     """qkv [B*S, 3*H*Dh] bf16 (q | k | v column blocks, heads contiguous) ->
     (o [B*S, H*Dh] bf16, aux saved for backward).
 
@@ -635,12 +636,15 @@ def attention_fwd(qkv: torch.Tensor, B: int, S: int, H: int, causal: bool = True
             s = s.masked_fill(torch.triu(torch.ones(S, S, dtype=torch.bool), 1), float("-inf"))
         p = torch.softmax(s, dim=-1).to(torch.bfloat16)
         o = torch.matmul(p.float(), v).permute(0, 2, 1, 3).reshape(T, d).to(torch.bfloat16)
+        if o_out is not None:
+            o = o_out.copy_(o)
         return o, p.reshape(B * H, S, S)
     assert qkv.is_contiguous()
     dev = qkv.device
     if Dh == 64 and impl != "composed":
         # flash-style fused kernel: returns the per-row LSE instead of P
-        o = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
+        o = torch.empty(T, d, dtype=torch.bfloat16, device=dev) if o_out is None else o_out
+        assert o.is_contiguous() and o.shape == (T, d)
         lse = torch.empty(B * H, S, dtype=torch.float32, device=dev)
         rc = _lib.lib().jdt_flash_fwd(_ptr(qkv), _ptr(o), _ptr(lse), B, S, H, float(scale), int(causal),
                                       _lib.stream_ptr())
@@ -648,7 +652,7 @@ def attention_fwd(qkv: torch.Tensor, B: int, S: int, H: int, causal: bool = True
         return o, lse
     Sc = torch.empty(B * H, S, S, dtype=torch.float32, device=dev)
     P = torch.empty(B * H, S, S, dtype=torch.bfloat16, device=dev)
-    o = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
+    o = torch.empty(T, d, dtype=torch.bfloat16, device=dev) if o_out is None else o_out
     base, e2 = qkv.data_ptr(), 2
     _gemm_raw(A=base, lda=d3, sA=S * d3, sA2=Dh, B=base + d * e2, ldb=d3, sB=S * d3, sB2=Dh, b_kn=False,
               C=Sc.data_ptr(), ldc=S, sC=H * S * S, sC2=S * S, c_f32=True, M=S, N=S, K=Dh, alpha=scale,
@@ -734,16 +738,20 @@ def attention_bwd(do: torch.Tensor, qkv: torch.Tensor, P: torch.Tensor, B: int, 
 
 
 # ----------------------------------------------------------------------------- layernorm / embedding / colsum
-def layernorm_fwd(x, gamma, beta, eps=1e-6):
-    """flax nn.LayerNorm (eps 1e-6); returns (y bf16, mean f32 [T], rstd f32 [T])."""
+def layernorm_fwd(x, gamma, beta, eps=1e-6, y_out=None):
+    """flax nn.LayerNorm (eps 1e-6); returns (y bf16, mean f32 [T], rstd f32 [T]).
+    ``y_out``: preallocated y (e.g. rows of a deferred-weight-gradient arena)."""
     T, d = x.shape
     if not _is_gpu(x):
         xf = x.float()
         mean = xf.mean(-1)
         rstd = torch.rsqrt(((xf - mean[:, None]) ** 2).mean(-1) + eps)
         y = ((xf - mean[:, None]) * rstd[:, None] * gamma.float() + beta.float()).to(torch.bfloat16)
+        if y_out is not None:
+            y = y_out.copy_(y)
         return y, mean, rstd
-    y = torch.empty_like(x)
+    y = torch.empty_like(x) if y_out is None else y_out
+    assert y.stride(1) == 1 and y.shape == x.shape
     mean = torch.empty(T, dtype=torch.float32, device=x.device)
     rstd = torch.empty(T, dtype=torch.float32, device=x.device)
     rc = _lib.lib().jdt_ln_fwd(_ptr(x), _ptr(gamma), _ptr(beta), _ptr(y), _ptr(mean), _ptr(rstd), T, d, float(eps),
@@ -756,19 +764,22 @@ _LN_GEMM = os.environ.get("JDT_LN_GEMM", "1") != "0"
 
 
 def ln_gemm(x, gamma, beta, w, *, eps=1e-6, bias=None, act: str = "none", z_out=None, keep_prob: float = 1.0,
-            seed: int = 0, offset: int = 0, step=None):
+            seed: int = 0, offset: int = 0, step=None, y_out=None, out=None):
     """``gemm(LN(x), w, ...)`` with the LayerNorm fused into the GEMM's A operand
     (csrc/gemm.hip ``gemm_ln_kernel``): returns (C, y = LN(x) bf16, mean, rstd) --
     the same values as ``layernorm_fwd`` followed by ``gemm`` (bit-identical y),
     one launch instead of two.  ``w`` is the [K, N] ("kn") bf16 weight.  Shapes
-    outside the fused kernel's envelope (or JDT_LN_GEMM=0, or CPU) run the two ops."""
+    outside the fused kernel's envelope (or JDT_LN_GEMM=0, or CPU) run the two ops.
+    ``y_out`` / ``out``: preallocated LN(x) / C (deferred weight-gradient arena rows)."""
     T, d = x.shape
     N = w.shape[-1]
     if _is_gpu(x) and _LN_GEMM and w.dtype == torch.bfloat16 and x.dtype == torch.bfloat16:
-        y = torch.empty_like(x)
+        y = torch.empty_like(x) if y_out is None else y_out
         mean = torch.empty(T, dtype=torch.float32, device=x.device)
         rstd = torch.empty(T, dtype=torch.float32, device=x.device)
-        out = torch.empty(T, N, dtype=torch.bfloat16, device=x.device)
+        if out is None:
+            out = torch.empty(T, N, dtype=torch.bfloat16, device=x.device)
+        assert y.shape == x.shape and out.shape == (T, N) and out.dtype == torch.bfloat16
         g = _lib.GemmArgs()
         g.A, g.lda = y.data_ptr(), y.stride(0)
         g.B, g.ldb, g.b_trans = w.data_ptr(), w.stride(0), 1
@@ -794,14 +805,16 @@ def ln_gemm(x, gamma, beta, w, *, eps=1e-6, bias=None, act: str = "none", z_out=
         if rc != -2:
             _lib.check(rc, "jdt_gemm_ln")
             return out, y, mean, rstd
-    y, mean, rstd = layernorm_fwd(x, gamma, beta, eps)
-    out = gemm(y, w, bias=bias, act=act, z_out=z_out, keep_prob=keep_prob, seed=seed, offset=offset, step=step)
+    y, mean, rstd = layernorm_fwd(x, gamma, beta, eps, y_out=y_out)
+    out = gemm(y, w, bias=bias, act=act, z_out=z_out, keep_prob=keep_prob, seed=seed, offset=offset, step=step,
+               out=out)
     return out, y, mean, rstd
 
 
-def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None, dsum=None):
+def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None, dsum=None, dx_out=None):
     """dx = dres + LN'(dy); dgamma/dbeta accumulate (fp32); ``dsum += colsum(dx)``
-    (the bias grad of the residual-stream Dense that produced x, fused here)."""
+    (the bias grad of the residual-stream Dense that produced x, fused here).
+    ``dx_out``: preallocated dx (deferred weight-gradient arena rows)."""
     T, d = x.shape
     if not _is_gpu(x):
         xh = (x.float() - mean[:, None]) * rstd[:, None]
@@ -814,10 +827,13 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None, dsum=None)
         if dbeta is not None:
             dbeta.add_(dy.float().sum(0))
         dx = dx.to(torch.bfloat16)
+        if dx_out is not None:
+            dx = dx_out.copy_(dx)
         if dsum is not None:
             dsum.add_(dx.float().sum(0))
         return dx
-    dx = torch.empty_like(x)
+    dx = torch.empty_like(x) if dx_out is None else dx_out
+    assert dx.is_contiguous() and dx.shape == x.shape
     rc = _lib.lib().jdt_ln_bwd(_ptr(dy), _ptr(x), _ptr(mean), _ptr(rstd), _ptr(gamma), _ptr(dres), _ptr(dx),
                                _ptr(dgamma), _ptr(dbeta), _ptr(dsum), T, d, _lib.stream_ptr())
     _lib.check(rc, "jdt_ln_bwd")

@@ -236,6 +236,11 @@ class FSDPConfig:
     scatter_once: bool = False
     fused_kernels: bool = False   # classifier: whole-step fused kernels on the gathered buffer (implies *_once)
     comm: str = "auto"            # "auto" | "xgmi" | "rccl": N>1 gather / reduce-scatter transport
+    # the reference's per-minibatch schedule (gather / fwd+bwd / reduce-scatter every
+    # minibatch) on the fused per-layer md kernels (parallel/fused_stage.py) instead of
+    # the generic GEMM chain, where the model and the collectives allow (GPU, tutorial
+    # MLP shapes, N = 1 or every sharded leaf on the xGMI kernels)
+    fused_loop: bool = True
 
 
 class ShardedFlatParams:
@@ -377,6 +382,31 @@ def init_fsdp(model: MLP, tx, seed: int, device, mesh: Optional[Mesh], axis: str
     return st
 
 
+class _LoopView:
+    """The parameter view of the fused per-minibatch FSDP loop: bf16 weights from the
+    gathered full shadow, gradients of the SHARDED leaves into the full fp32 buffer
+    (reduce-scattered after every minibatch, gather_arr_mean_grads), gradients of the
+    replicated leaves and the metric slots straight into the local buffer -- they
+    accumulate over the minibatches and are all-reduced once per step
+    (sync_gradients), exactly the reference's split (param_sharding.py:129-142,
+    343-367).  At N = 1 every shard is the whole leaf: everything is local."""
+
+    def __init__(self, sp: ShardedFlatParams):
+        self.sp = sp
+        self.one = sp.n == 1
+        self.master = sp.local.master
+
+    def s(self, name):
+        return self.sp.local.s(name) if self.one else self.sp.full.s(name)
+
+    def g(self, name):
+        return self.sp.local.g(name) if (self.one or name in self.sp.repl_names) else self.sp.full.g(name)
+
+    @property
+    def metrics_slot(self):
+        return self.sp.local.metrics_slot
+
+
 class FSDPTrainer:
     def __init__(self, state: TrainState, mesh: Optional[Mesh], cfg: FSDPConfig = FSDPConfig()):
         self.state, self.mesh, self.cfg = state, mesh, cfg
@@ -390,6 +420,8 @@ class FSDPTrainer:
         self.multi = None
         self._plan = None
         self._full_fresh = True   # init_fsdp gathered the full shadow
+        self._loop_engine = None
+        self._loop_tried = False
         if self.world > 1 and self.sp.local.master.is_cuda and self.sp.xg is None:
             from ..comm.xgmi import create_for
 
@@ -402,6 +434,8 @@ class FSDPTrainer:
 
     def invalidate(self):
         """After a checkpoint restore: drop the fused engine and captured graphs."""
+        self._loop_engine = None
+        self._loop_tried = False
         self.fused = None
         self.graph = None
         self._ahead = None
@@ -555,6 +589,25 @@ class FSDPTrainer:
         for _ in range(n):
             self.step(batch)
 
+    def _fused_loop(self, mb: int, seed: int):
+        """FusedMLPStage (one stage = the whole classifier) on the _LoopView: minibatch
+        i, layer l draws dropout stream (i << 16) + (l << 1) at the step counter -- the
+        generic loop's masks below."""
+        if not self._loop_tried:
+            self._loop_tried = True
+            from .fused_stage import FusedMLPStage, stage_supported
+
+            sp = self.sp
+            dev = sp.local.master.device
+            coll_ok = self.world == 1 or (sp.xg is not None and len(sp._xg_names) == len(sp.sharded_names))
+            if self.cfg.fused_loop and coll_ok and stage_supported(self.model, mb, dev):
+                self._loop_engine = FusedMLPStage(self.model, _LoopView(sp), self.cfg.num_minibatches, mb,
+                                                  self.state.step_tensor, seed)
+                # sharded leaves' full-grad range (zeroed after each minibatch's reduce-scatter)
+                offs = sorted((sp.full.offsets[n][0], sp.full.g(n).numel()) for n in sp.sharded_names)
+                self._shard_full = [sp.full.grad[o:o + n] for o, n in offs]
+        return self._loop_engine
+
     def _body(self, batch: Batch):
         """One step of device work (no host counters, so it can be captured)."""
         if self._fused_step(batch):
@@ -564,6 +617,29 @@ class FSDPTrainer:
         seed = rng & 0xFFFFFFFF
         n_mb = cfg.num_minibatches
         mb = batch.size // n_mb
+        eng = self._fused_loop(mb, seed) if batch.inputs.is_cuda else None
+        if eng is not None:
+            # param_sharding.py's schedule on the md kernels: per minibatch gather the bf16
+            # shards, forward + CE + backward, reduce-scatter the sharded leaves' grads
+            # into the local shards (replicated leaves accumulate locally); then ONE
+            # all-reduce of the local tail (replicated grads + metric slots), AdamW
+            for i in range(n_mb):
+                if self.world > 1 and (i == 0 or not cfg.gather_once):
+                    sp.xg.all_gather_segments([(sp.full.s(n), sp.local.s(n)) for n in sp._xg_names])
+                eng.forward(i, batch.inputs[i * mb:(i + 1) * mb])
+                eng.backward(i, labels=batch.labels[i * mb:(i + 1) * mb])
+                if self.world > 1 and (not cfg.scatter_once or i == n_mb - 1):
+                    with named_scope("scatter_grads"):
+                        sp.xg.reduce_scatter_segments([(sp.full.g(n), sp.local.g(n)) for n in sp._xg_names],
+                                                      accumulate=True)
+                        for t in self._shard_full:
+                            t.zero_()
+            if self.world > 1:
+                sp.sync_replicated()
+            st.tx.update(sp.local, st.opt_state, 1.0 / (n_mb * self.world))
+            with named_scope("synch_metrics"):
+                K.metrics_fold_(self.metrics, sp.local.metrics_slot)
+            return
         for i in range(n_mb):
             if i == 0 or not cfg.gather_once:
                 sp.gather()

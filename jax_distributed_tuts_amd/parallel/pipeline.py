@@ -103,6 +103,13 @@ class PipeConfig:
     # 1.18 ms, profiles/r2_overlapped_adamw_ab.txt) -- the forked AdamW grids contend
     # with the backward GEMMs for CUs instead of filling idle ones
     overlap_optimizer: bool = True
+    # per-microbatch passes of a model with deferrable weight gradients (the transformer
+    # LM): each microbatch's backward runs only the input-gradient chain and the
+    # weight-gradient GEMMs run ONCE per step over all microbatches' rows (the "W pass"
+    # of zero-bubble schedules, Qi et al. 2023) -- 4x the K per GEMM, 1/n_mb the
+    # launches, and the gradient an upstream stage waits for is sent sooner.
+    # JDT_DEFER_WGRAD=0 turns it off (A/B).
+    defer_wgrad: bool = field(default_factory=lambda: os.environ.get("JDT_DEFER_WGRAD", "1") != "0")
 
 
 def _no_dropout(model) -> bool:
@@ -176,9 +183,9 @@ class GPipeTrainer:
             else:
                 C.send(x, self.mesh, self.cfg.pipe_axis, to)
 
-    def _recv(self, shape, to_dtype, frm: int, slot: int) -> torch.Tensor:
+    def _recv(self, shape, to_dtype, frm: int, slot: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         with named_scope("pipe_recv"):
-            buf = torch.empty(shape, dtype=to_dtype, device=self.dev)
+            buf = torch.empty(shape, dtype=to_dtype, device=self.dev) if out is None else out
             if self.p2p is not None:
                 return self.p2p.recv(buf, slot, self.state.step_tensor)
             return C.recv(buf, self.mesh, self.cfg.pipe_axis, frm)
@@ -240,6 +247,8 @@ class GPipeTrainer:
             self._compute_fused(batch, eng, n_mb, mb)
             return
         caches, dlogits = [None] * n_mb, [None] * n_mb
+        arena = self._wgrad_arena(batch.size)
+        akw = {"arena": arena, "n_mb": n_mb} if arena is not None else {}
         # ---- forward fill/drain: tick t, stage s handles microbatch t - s
         for t in range(n_mb + self.S - 1):
             i = t - self.s
@@ -249,10 +258,12 @@ class GPipeTrainer:
                 x = batch.inputs[i * mb:(i + 1) * mb]
             else:
                 x = self._recv(self.model.input_shape(mb), self.act_dtype, self.s - 1, i)
-            out, cache = self.model.forward(P, x, train=True, seed=seed, offset=i << 16, step=st.step_tensor)
+            if arena is not None:
+                akw["mb"] = i
+            out, cache = self.model.forward(P, x, train=True, seed=seed, offset=i << 16, step=st.step_tensor, **akw)
             caches[i] = cache
             if self.last:
-                d = torch.empty_like(out)
+                d = torch.empty_like(out) if arena is None else arena.rows(arena.head["dlog"], i, n_mb)
                 self.loss_head(out, batch.labels[i * mb:(i + 1) * mb], d)
                 dlogits[i] = d
             else:
@@ -261,18 +272,35 @@ class GPipeTrainer:
         # weights' final gradients: the in-epilogue optimizer when enabled)
         if eo is not None:
             eo.only_contribution = n_mb == 1
+        top = list(getattr(self.model, "layers", []))[-1:] if arena is not None else []
         for i in reversed(range(n_mb)):
-            oi = eo if i == 0 else None
+            oi = eo if (i == 0 and arena is None) else None
             if self.last:
                 dx = self.model.backward(P, caches[i], dlogits[i], dout_is_dz=True, need_dx=not self.first,
                                          wgrad=self.wgrad, opt=oi)
             else:
-                dh = self._recv(self.model.output_shape(mb), self.act_dtype, self.s + 1, n_mb + i)
+                into = arena.rows(arena.blocks[top[0]]["dx3"], i, n_mb) if top else None
+                dh = self._recv(self.model.output_shape(mb), self.act_dtype, self.s + 1, n_mb + i, out=into)
                 dx = self.model.backward(P, caches[i], dh, dout_is_dz=False, need_dx=not self.first,
                                          wgrad=self.wgrad, opt=oi)
             if not self.first:
                 self._send(dx, self.s - 1, n_mb + i)
             caches[i] = None
+        if arena is not None:
+            # the W pass: every weight gradient of the step, one GEMM per weight over all rows
+            self.model.weight_grads(P, arena, wgrad=self.wgrad, opt=eo)
+
+    def _wgrad_arena(self, rows: int):
+        """The stage model's deferred weight-gradient buffers (models.transformer.WGradArena)
+        for ``rows`` local sequences, or None (model without them, or defer_wgrad off)."""
+        if not self.cfg.defer_wgrad or not hasattr(self.model, "weight_grads"):
+            return None
+        ar = getattr(self, "_arena", None)
+        if ar is None or ar.nseq != rows:
+            from ..models.transformer import WGradArena
+
+            ar = self._arena = WGradArena(self.model, rows, self.dev)
+        return ar
 
     @property
     def single_stage_mode(self) -> str:

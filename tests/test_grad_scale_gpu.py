@@ -171,14 +171,15 @@ def _load(d, name, ws):
     return [torch.load(os.path.join(d, f"{name}_r{r}.pt"), weights_only=True) for r in range(ws)]
 
 
-@pytest.mark.parametrize("kind", ["dp_sgd", "dp_adam_eps", "fsdp_sgd"])
-def test_xgmi_strategies_grad_scale(tmp_path, kind):
+@pytest.mark.parametrize("kind,ws", [("dp_sgd", 2), ("dp_adam_eps", 2), ("fsdp_sgd", 2), ("fsdp_loop_sgd", 2),
+                                     ("fsdp_loop_sgd", 4)])
+def test_xgmi_strategies_grad_scale(tmp_path, kind, ws):
     from jax_distributed_tuts_amd.runtime.launch import spawn
 
     from . import xgmi_workers as XW
 
-    spawn(functools.partial(XW.grad_probe_xgmi, kind=kind), 2, str(tmp_path), gpu=True)
-    res = _load(tmp_path, f"gpx_{kind}", 2)
+    spawn(functools.partial(XW.grad_probe_xgmi, kind=kind), ws, str(tmp_path), gpu=True)
+    res = _load(tmp_path, f"gpx_{kind}", ws)
     assert all(o["comm"] == "xgmi" for o in res)
     b = _batch()
     want = mlp_grads_fp64(res[0]["before"], ["input_dense", "output_dense"], b.inputs, b.labels, n_mb=4)

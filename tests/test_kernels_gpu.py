@@ -707,7 +707,8 @@ def test_fsdp_fused_kernels_match_generic(layers):
     res = []
     for fused in (False, True):
         st = init_fsdp(Classifier(dropout_rate=0.0, num_layers=layers), adamw(1e-3), 69, DEV, None, "data", 16)
-        tr = FSDPTrainer(st, None, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=fused))
+        tr = FSDPTrainer(st, None, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=fused,
+                                              fused_loop=False))
         for _ in range(3):
             tr.step(b)
         torch.cuda.synchronize()
@@ -716,6 +717,35 @@ def test_fsdp_fused_kernels_match_generic(layers):
             assert tr.fused is not None
     d = (res[0][0] - res[1][0]).abs()
     assert float(d.max()) <= 6e-3 and float((d > 1e-4).float().mean()) < 2e-3
+    _close(res[1][1], res[0][1], rtol=1e-3, atol=2e-2)
+
+
+@pytest.mark.parametrize("layers", [2, 4])
+def test_fsdp_fused_loop_matches_generic_loop(layers):
+    """The reference's per-minibatch FSDP schedule (gather / fwd+bwd / reduce-scatter
+    every minibatch, param_sharding.py) on the fused md kernels (FSDPConfig.fused_loop)
+    == the same schedule on the generic GEMM chain, dropout ON (both draw stream
+    (i << 16) + (l << 1) at the step counter) and a scale-revealing SGD, eager and
+    replayed from a multi-step hipGraph."""
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
+    from jax_distributed_tuts_amd.utils.train_state import Batch, sgd
+
+    g = torch.Generator().manual_seed(0)
+    b = Batch(torch.randn(128, 784, generator=g).to(DEV), torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV))
+    res = []
+    for fl in (False, True):
+        st = init_fsdp(Classifier(num_layers=layers), sgd(0.05), 69, DEV, None, "data", 16)
+        tr = FSDPTrainer(st, None, FSDPConfig(4, 16, "data", fused_loop=fl))
+        tr.step(b)
+        tr.capture(b, steps_per_graph=2)
+        tr.run_steps(b, 4)
+        torch.cuda.synchronize()
+        assert (tr._loop_engine is not None) == fl
+        res.append((st.params.master.clone(), tr.metrics.clone()))
+    d = (res[0][0] - res[1][0]).abs()
+    print(f"[fsdp loop L{layers}] max |dp| {float(d.max()):.3e}")
+    assert float(d.max()) <= 2e-3 * float(res[0][0].abs().max())
     _close(res[1][1], res[0][1], rtol=1e-3, atol=2e-2)
 
 

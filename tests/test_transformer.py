@@ -87,3 +87,28 @@ def test_stage_split_equals_full_model():
     for Q in Ps:
         for n in Q.names():
             torch.testing.assert_close(Q.g(n), P.g(n), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("mode", ["defer", "per-mb", "layer-major"])
+def test_deferred_weight_grads_equal_microbatch_loop(mode, monkeypatch):
+    """One-stage GPipe step of the LM with per-microbatch passes: the deferred W pass
+    (WGradArena: every weight gradient one GEMM over all microbatches' rows after the
+    backward chain) == the per-microbatch weight-gradient accumulation == the
+    layer-major single pass (one plain-SGD step, lr 1: the applied gradient)."""
+    from jax_distributed_tuts_amd.parallel.pipeline_lm import build_lm_pipeline
+    from jax_distributed_tuts_amd.utils.train_state import sgd
+
+    def run(defer, layer_major):
+        monkeypatch.setenv("JDT_DEFER_WGRAD", "1" if defer else "0")
+        tr, _ = build_lm_pipeline(None, "cpu", CFG, num_microbatches=4, tx=sgd(1.0),
+                                  layer_major_single_stage=layer_major)
+        assert (getattr(tr, "_arena", None) is None)
+        before = {k: v.clone() for k, v in tr.state.params.state_dict().items()}
+        tr.step(lm_batch(CFG, global_batch=8, seed=7))
+        assert (getattr(tr, "_arena", None) is not None) == (defer and not layer_major)
+        return {k: before[k] - v for k, v in tr.state.params.state_dict().items()}
+
+    ref = run(False, False)
+    got = run(mode == "defer", mode == "layer-major")
+    for k in ref:
+        torch.testing.assert_close(got[k], ref[k], rtol=2e-4, atol=2e-6, msg=lambda m: f"{k}: {m}")

@@ -371,6 +371,26 @@ def grad_probe_xgmi(outdir, kind, dp=1):
         tr.finalize()
         after = cpu(tr.full_params())
         comm = tr.comm_backend
+    elif kind == "fsdp_loop_sgd":
+        # the reference's per-minibatch gather / reduce-scatter schedule on the fused md
+        # kernels (FSDPConfig.fused_loop), the probed step replayed from a hipGraph
+        from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
+
+        mesh = D.Mesh({"data": D.world_size()})
+        st = init_fsdp(Classifier(dropout_rate=0.0), sgd(1.0), 69, dev, mesh, "data", 16)
+        b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
+        b = Batch(b.inputs.to(dev), b.labels.to(dev))
+        tr = FSDPTrainer(st, mesh, FSDPConfig(4, 16, "data", gather_once=False, scatter_once=False,
+                                              fused_kernels=False, comm="xgmi"))
+        tr.step(b)   # eager: builds the loop engine
+        assert tr._loop_engine is not None and tr.capturable
+        torch.cuda.synchronize()
+        before = cpu(tr.full_params())
+        tr.capture(b)
+        tr.step(b)   # graph replay
+        tr.finalize()
+        after = cpu(tr.full_params())
+        comm = tr.comm_backend
     elif kind == "pp_sgd":
         from pipeline_parallel import build_mlp_pipeline
 

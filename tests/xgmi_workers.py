@@ -329,7 +329,7 @@ def fault_timeout(outdir):
     p2p.close()
 
 
-def grad_probe_xgmi(outdir, kind, dp=1):
+def grad_probe_xgmi(outdir, kind, dp=1, capture=True):
     """One step (dropout off) of a strategy over the xGMI kernels with a
     scale-revealing optimizer -- plain SGD lr 1, or (``dp_adam_eps``) the fused
     xGMI all-reduce + AdamW kernel with eps = 10 -- saving params before / after
@@ -386,8 +386,9 @@ def grad_probe_xgmi(outdir, kind, dp=1):
         assert tr._loop_engine is not None and tr.capturable
         torch.cuda.synchronize()
         before = cpu(tr.full_params())
-        tr.capture(b)
-        tr.step(b)   # graph replay
+        if capture:
+            tr.capture(b)
+        tr.step(b)   # graph replay (or a second eager step)
         tr.finalize()
         after = cpu(tr.full_params())
         comm = tr.comm_backend

@@ -96,6 +96,10 @@ def build_pp(args, dev):
     ws = D.world_size()
     dp = args.dp
     mesh = Mesh({"data": dp, "pipe": ws // dp})
+    if args.microbatches is None:
+        from jax_distributed_tuts_amd.parallel.pipeline import default_microbatches
+
+        args.microbatches = default_microbatches(ws // dp)
     if args.model == "transformer":
         from jax_distributed_tuts_amd.parallel.pipeline_lm import build_lm_pipeline, lm_batch
 
@@ -188,7 +192,8 @@ def main():
     ap.add_argument("--strategy", choices=["dp", "fsdp", "pp"], default="dp")
     ap.add_argument("--dp", type=int, default=1, help="data-parallel degree for --strategy pp (hybrid)")
     ap.add_argument("--model", choices=["mlp", "transformer"], default="mlp")
-    ap.add_argument("--microbatches", type=int, default=4)
+    ap.add_argument("--microbatches", type=int, default=None,
+                    help="GPipe microbatches (default: pipeline.default_microbatches, measured per stage count)")
     ap.add_argument("--merge-microbatches", action="store_true",
                     help="--strategy pp with a single stage: run the microbatches as one pass (PipeConfig.merge_single_stage)")
     ap.add_argument("--microbatch-passes", action="store_true",

@@ -17,6 +17,7 @@ namespace jdt {
 typedef uint16_t bf16_t;  // raw bf16 bits
 typedef __attribute__((ext_vector_type(8))) short bf16x8;  // MFMA A/B fragment
 typedef __attribute__((ext_vector_type(4))) float f32x4;   // 16x16 MFMA C/D
+typedef __attribute__((ext_vector_type(16))) float f32x16; // 32x32 MFMA C/D
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 
 constexpr int WAVE = 64;
@@ -185,6 +186,12 @@ __device__ __forceinline__ float act_grad(int act, float z) {
 // lane l holds A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15]; D[(l>>4)*4+i][l&15].
 __device__ __forceinline__ f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// D = A(32x16) * B(16x32) + C: lane l holds A[l&31][8(l>>5)+j], B[8(l>>5)+j][l&31];
+// D register e of lane l is row (e&3) + 8(e>>2) + 4(l>>5), column l&31.  Half the
+// fragment bytes per FLOP of the 16x16x32 form (one 16-byte A and B read per 32K FLOP).
+__device__ __forceinline__ f32x16 mfma32x32x16(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
 // ---------------------------------------------------------------- XCD-aware 2-D block map

@@ -22,6 +22,8 @@
 // land on the same XCD's L2.
 #include "common.h"
 
+#include <type_traits>
+
 namespace jdt {
 
 struct GemmArgs {
@@ -521,14 +523,16 @@ __device__ __forceinline__ void gemm_finish_lds(const GemmArgs& g, f32x4 (&acc)[
 // K = 512 GEMM (tools/gemm_ksweep.py: K = 64 took 13-18 us vs torch's 6).  The
 // arithmetic per element is the same sequence as gemm_finish, so results are
 // bit-identical.
+template <int BM, int BN, int NT = 256>
+__device__ __forceinline__ void gemm_finish_img(const GemmArgs& g, int tm0, int tn0, int z, int tid, int splits,
+                                                int split, long tile_id, float* __restrict__ ws, unsigned* counters,
+                                                float* img);
+
 template <int BM, int BN, int TM, int TN, int NT = 256>
 __device__ __forceinline__ void gemm_finish_vec(const GemmArgs& g, f32x4 (&acc)[TM][TN], int tm0, int tn0, int z,
                                                 int wm, int wn, int lane, int tid, int splits, int split, long tile_id,
                                                 float* __restrict__ ws, unsigned* counters, float* img) {
   constexpr int LD = BN + 4;      // padded image row (floats)
-  constexpr int CU = BN / 8;      // 8-column chunks per row
-  constexpr int NU = BM / 4 * CU; // 4 x 8 units per tile
-  static_assert(NT % CU == 0, "a thread keeps its column chunk across units");
   // the caller synchronised: every wave is past its last read of the staging ring
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -537,6 +541,37 @@ __device__ __forceinline__ void gemm_finish_vec(const GemmArgs& g, f32x4 (&acc)[
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         img[((wm * TM + i) * 16 + (lane >> 4) * 4 + e) * LD + (wn * TN + j) * 16 + (lane & 15)] = acc[i][j][e];
+  gemm_finish_img<BM, BN, NT>(g, tm0, tn0, z, tid, splits, split, tile_id, ws, counters, img);
+}
+
+// The same for a wave's TM x TN grid of 32x32 accumulators (v_mfma_f32_32x32x16_bf16:
+// lane l holds column l & 31, rows (e & 3) + 8 (e >> 2) + 4 (l >> 5) of register e).
+template <int BM, int BN, int TM, int TN, int NT = 256>
+__device__ __forceinline__ void gemm_finish_vec32(const GemmArgs& g, f32x16 (&acc)[TM][TN], int tm0, int tn0, int z,
+                                                  int wm, int wn, int lane, int tid, int splits, int split,
+                                                  long tile_id, float* __restrict__ ws, unsigned* counters,
+                                                  float* img) {
+  constexpr int LD = BN + 4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        img[((wm * TM + i) * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * LD + (wn * TN + j) * 32 + (lane & 31)] =
+            acc[i][j][e];
+  gemm_finish_img<BM, BN, NT>(g, tm0, tn0, z, tid, splits, split, tile_id, ws, counters, img);
+}
+
+// Split-K combine + fused epilogue from the fp32 tile image ``img`` ([BM][BN + 4]).
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void gemm_finish_img(const GemmArgs& g, int tm0, int tn0, int z, int tid, int splits,
+                                                int split, long tile_id, float* __restrict__ ws, unsigned* counters,
+                                                float* img) {
+  constexpr int LD = BN + 4;      // padded image row (floats)
+  constexpr int CU = BN / 8;      // 8-column chunks per row
+  constexpr int NU = BM / 4 * CU; // 4 x 8 units per tile
+  static_assert(NT % CU == 0, "a thread keeps its column chunk across units");
   __syncthreads();
   if (splits > 1) {
     constexpr int NV = BM * BN / 4;
@@ -1074,6 +1109,39 @@ __device__ __forceinline__ void stage_op(const bf16_t* src, long ld, int k0, bf1
     dma_stage<EXT, KMAJ, NW>(src, ld, k0, img, wid, lane);
   }
 }
+// 32x32x16 operand fragment (lane l: row/column base + (l & 31), k = kk + 8 (l >> 5) + 0..7)
+// from the same two images.  k-row image: each 16-lane group g gathers columns
+// base + 16 (g & 1) .. +15 of k-rows kk + 8 (g >> 1) + 0..3 and + 4..7 (two tr reads;
+// tr_swz ignores k bit 2, so both share one swizzled column).
+template <int EXT>
+__device__ __forceinline__ bf16x8 dma_frag32(const bf16_t* img, bool kmajor_img, int base, int kk, int lane) {
+  if (!kmajor_img) {
+    const int r = base + (lane & 31);
+    const int c = (kk >> 3) + (lane >> 5);
+    return *reinterpret_cast<const bf16x8*>(img + r * DMA_BK + ((c ^ (r & 7)) << 3));
+  }
+  typedef __attribute__((ext_vector_type(4))) short s4;
+  const int i16 = lane & 15, g4 = lane >> 4;
+  const int k1 = kk + 8 * (g4 >> 1) + (i16 >> 2);
+  const int col = base + 16 * (g4 & 1) + 4 * (i16 & 3);
+  const int pcol = (((col >> 3) ^ tr_swz<EXT>(k1)) << 3) | (col & 7);
+  const unsigned a0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) const bf16_t*)(img + k1 * EXT + pcol));
+  s4 lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a0), "n"(4 * EXT * 2));
+  bf16x8 f;
+  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+  return f;
+}
+template <int EXT>
+__device__ __forceinline__ bf16x8 frag_op32(const bf16_t* img, bool kmajor_img, int base, int kk, int lane) {
+  if constexpr (EXT > 64) {
+    if (kmajor_img) return dma_frag32<64>(img + (base >> 6) * 64 * DMA_BK, true, base & 63, kk, lane);
+  }
+  return dma_frag32<EXT>(img, kmajor_img, base, kk, lane);
+}
+
 template <int EXT>
 __device__ __forceinline__ bf16x8 frag_op(const bf16_t* img, bool kmajor_img, int base, int kk, int lane) {
   if constexpr (EXT > 64) {
@@ -1156,12 +1224,14 @@ __device__ __forceinline__ void dma_wait_barrier(int pend) {
 // tiles do too little MFMA work per barrier at R = 1 (a 32 x 32 tile: 2 MFMAs
 // per wave between barriers; the wait / barrier / ds_read latency chain then
 // sets the K loop's pace, ~300 cycles per 64-deep K-tile on one workgroup/CU).
-template <int WM, int WN, int TM, int TN, bool AT, bool BT, int S, int R = 1>
+// MF = 32: every wave's TM x TN sub-tiles are 32 x 32 (v_mfma_f32_32x32x16_bf16): half
+// the LDS fragment traffic per FLOP, and the vectorised epilogue only.
+template <int WM, int WN, int TM, int TN, bool AT, bool BT, int S, int R = 1, int MF = 16>
 __global__ void __launch_bounds__(64 * WM * WN) gemm_dma_kernel(GemmArgs g, int tiles_n, int splits, int kchunk,
                                                                 float* __restrict__ ws, unsigned* counters, int vec,
                                                                 int group_m) {
   constexpr int NW = WM * WN;             // waves: 4, or 8 (two per SIMD) for the 128 x 128+ tiles
-  constexpr int BM = WM * TM * 16, BN = WN * TN * 16, BK = DMA_BK;
+  constexpr int BM = WM * TM * MF, BN = WN * TN * MF, BK = DMA_BK;
   constexpr int SUB = (BM + BN) * BK;     // elements of one 64-deep sub-tile (A image then B image)
   constexpr int STAGE = SUB * R;          // elements of one ring slot
   constexpr int LPW = (BM + BN) / (8 * NW) * R;  // glds per wave per slot
@@ -1192,11 +1262,14 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_dma_kernel(GemmArgs g, int 
   const int kbeg = split * kchunk;
   const int nkt = (min(g.K, kbeg + kchunk) - kbeg) / (BK * R);  // host: kchunk % (64 R) == 0
 
-  f32x4 acc[TM][TN];
+  using acc_t = typename std::conditional<MF == 32, f32x16, f32x4>::type;
+  acc_t acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < (MF == 32 ? 16 : 4); ++e) acc[i][j][e] = 0.f;
 
   auto issue = [&](int kt) {
     bf16_t* st = smem + (kt % S) * STAGE;
@@ -1220,6 +1293,27 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_dma_kernel(GemmArgs g, int 
     for (int r = 0; r < R; ++r) {
       const bf16_t* As = smem + (kt % S) * STAGE + r * SUB;
       const bf16_t* Bs = As + BM * BK;
+      if constexpr (MF == 32) {
+#pragma unroll
+        for (int kk = 0; kk < BK; kk += 16) {
+          bf16x8 af[TM], bfr[TN];
+#pragma unroll
+          for (int i = 0; i < TM; ++i) af[i] = frag_op32<BM>(As, AT, (wm * TM + i) * 32, kk, lane);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) bfr[j] = frag_op32<BN>(Bs, BT, (wn * TN + j) * 32, kk, lane);
+          if constexpr (AT || BT) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(af[i]));
+#pragma unroll
+            for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(bfr[j]));
+          }
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = mfma32x32x16(af[i], bfr[j], acc[i][j]);
+        }
+      } else {
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 32) {
         bf16x8 af[TM], bfr[TN];
@@ -1241,11 +1335,16 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_dma_kernel(GemmArgs g, int 
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
       }
+      }
     }
   }
   __syncthreads();
   static_assert((BM * (BN + 4) + 4) * 4 <= S * STAGE * 2, "output image fits the staging ring");
-  if constexpr (NW != 4) {
+  if constexpr (MF == 32) {
+    // launched only where the vectorised epilogue applies (host)
+    gemm_finish_vec32<BM, BN, TM, TN, 64 * NW>(g, acc, tm0, tn0, z, wm, wn, lane, tid, splits, split,
+                                               (long)z * gridDim.x + bid, ws, counters, reinterpret_cast<float*>(smem));
+  } else if constexpr (NW != 4) {
     // 8-wave tiles are launched only where the vectorised epilogue applies (host)
     gemm_finish_vec<BM, BN, TM, TN, 64 * NW>(g, acc, tm0, tn0, z, wm, wn, lane, tid, splits, split,
                                              (long)z * gridDim.x + bid, ws, counters, reinterpret_cast<float*>(smem));
@@ -1504,10 +1603,12 @@ static int g_dma_r = -1;  // jdt_gemm_set_r(r): force r 64-deep sub-tiles per ri
 template <int BM, int BN>
 constexpr bool r_ok(int r) { return r == 1 || ((BM + BN) * DMA_BK * 2 * 3 * r <= 96 * 1024 && (BM / 32 + BN / 32) * r <= 63); }
 
-template <int WM, int WN, int TM, int TN>
+// MF: MFMA sub-tile (16: 16x16x32, 32: 32x32x16); SD: ring depth (0 = dma_stages)
+template <int WM, int WN, int TM, int TN, int MF = 16, int SD = 0>
 static int launch_dma(const GemmArgs& g, int batch, int splits, float* ws, long ws_floats, unsigned* counters,
                       long n_counters, hipStream_t st, int r_pref = 1, int gm_pref = 0) {
-  constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
+  constexpr int BM = WM * TM * MF, BN = WN * TN * MF;
+  constexpr int SR = SD > 0 ? SD : dma_stages<BM, BN>();
   if (g.M % BM || g.N % BN) return 1;
   const int tiles_n = g.N / BN;
   const long tiles = (long)(g.M / BM) * tiles_n * batch;
@@ -1529,15 +1630,15 @@ static int launch_dma(const GemmArgs& g, int batch, int splits, float* ws, long 
   // cost more than the narrow stores on those small outputs (in-model A/B,
   // tools/gpu_r2_ab_epi.sh: microbatch-loop transformer 3.07 ms vec vs 2.98)
   const int vec = g_epi_vec && BM * BN >= 2048 && (long)g.M * g.N * batch >= g_epi_vec_min && epi_vec_ok(g, batch);
-  if (WM * WN != 4 && !epi_vec_ok(g, batch)) return 1;  // 8-wave tiles: vectorised epilogue only
+  if ((WM * WN != 4 || MF == 32) && !epi_vec_ok(g, batch)) return 1;  // 8-wave / 32x32 tiles: vectorised epilogue only
   // sub-tiles per ring slot: g_dma_r forces (sweeps), else 1
   int R = g_dma_r > 0 ? g_dma_r : r_pref;
   const int gm = g_group_m >= 0 ? g_group_m : gm_pref;
   while (R > 1 && (kchunk / DMA_BK) % R) R >>= 1;
   if (R > 1 && !r_ok<BM, BN>(R)) R = 1;
 #define JDT_DMA_S(A_, B_, S_, R_)                                                                                 \
-  hipLaunchKernelGGL((gemm_dma_kernel<WM, WN, TM, TN, A_, B_, S_, R_>), grid, dim3(64 * WM * WN), 0, st, g, tiles_n, \
-                     sp, kchunk, ws, counters, vec, gm)
+  hipLaunchKernelGGL((gemm_dma_kernel<WM, WN, TM, TN, A_, B_, S_, R_, MF>), grid, dim3(64 * WM * WN), 0, st, g,    \
+                     tiles_n, sp, kchunk, ws, counters, vec, gm)
 #define JDT_DMA(A_, B_)                                                   \
   do {                                                                    \
     if constexpr (r_ok<BM, BN>(4)) {                                      \
@@ -1546,7 +1647,7 @@ static int launch_dma(const GemmArgs& g, int batch, int splits, float* ws, long 
     if constexpr (r_ok<BM, BN>(2)) {                                      \
       if (R == 2) { JDT_DMA_S(A_, B_, 3, 2); break; }                     \
     }                                                                     \
-    JDT_DMA_S(A_, B_, (dma_stages<BM, BN>()), 1);                         \
+    JDT_DMA_S(A_, B_, SR, 1);                                             \
   } while (0)
   if (!at && !bt) JDT_DMA(false, false);
   else if (!at && bt) JDT_DMA(false, true);
@@ -1572,7 +1673,6 @@ static int launch_dma(const GemmArgs& g, int batch, int splits, float* ws, long 
 // {M, N, K, a_trans, b_trans, cfg, R, gm}.
 struct GemmTune { int M, N, K, at, bt, cfg, r, gm; };
 static const GemmTune kGemmTune[] = {
-    {2048, 1536, 512, 0, 1, 11, 1, 0},   // qkv fwd (2048 rows)       10.38 (12.15)
     {2048, 512, 2048, 0, 1, 10, 2, 0},   // fc2 fwd                   14.41 (13.78)
     {512, 2048, 2048, 1, 1, 10, 1, 8},   // fc1 / head dW             17.46 (16.26)
     {2048, 2048, 512, 0, 1, 15, 1, 0},   // fc1 / head fwd            10.37 (11.02)
@@ -1583,6 +1683,13 @@ static const GemmTune kGemmTune[] = {
     {512, 512, 2048, 1, 1, 13, 2, 0},    // out dW                    10.41 (15.46)
     {256, 1536, 512, 0, 1, 10, 2, 0},    // qkv fwd (hybrid, 256 rows) 5.55 (5.60)
     {256, 512, 2048, 0, 1, 13, 2, 0},    // fc2 fwd (hybrid)          8.38 (9.84)
+    // round 3: 32x32x16-MFMA tiles (tools/bench_gemm.py --cfg 20 / 26 sweep,
+    // profiles/r3_gemm_mfma32_sweep.txt; default-table time in parentheses)
+    {512, 2048, 512, 0, 1, 20, 1, 0},    // fc1 / head fwd, 512 rows   7.64 (10.76)
+    {512, 2048, 512, 0, 0, 20, 1, 0},    // fc2 dX, 512 rows           7.46 (9.67)
+    {512, 2048, 512, 1, 1, 20, 1, 0},    // fc1 dW, 512 tokens         8.11 (9.80)
+    {2048, 512, 512, 1, 1, 20, 1, 0},    // fc2 dW, 512 tokens         8.15 (9.92)
+    {2048, 1536, 512, 0, 1, 26, 1, 0},   // qkv fwd (2048 rows)       11.87 (14.92)
 };
 static bool g_gemm_tune = true;  // jdt_gemm_set_tune(0): heuristic only (A/B)
 
@@ -1626,6 +1733,15 @@ static int gemm_dma(const GemmArgs& g, int batch, int cfg, int splits, float* ws
     case 16: rc = launch_dma<4, 2, 2, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st, 1, gm_pref); break;  // 128 x 128
     case 17: rc = launch_dma<4, 2, 4, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st, 1, gm_pref); break;  // 256 x 128
     case 18: rc = launch_dma<2, 4, 4, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st, 1, gm_pref); break;  // 128 x 256
+    // 32 x 32 x 16 MFMA sub-tiles (4 waves unless noted)
+    case 20: rc = launch_dma<2, 2, 1, 1, 32>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref, gm_pref); break;  // 64 x 64
+    case 21: rc = launch_dma<2, 2, 1, 1, 32, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st, 1, gm_pref); break;   // 64 x 64, 4-slot ring
+    case 22: rc = launch_dma<2, 2, 2, 1, 32>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref, gm_pref); break;  // 128 x 64
+    case 23: rc = launch_dma<2, 2, 1, 2, 32>(g, batch, splits, ws, ws_floats, counters, n_counters, st, r_pref, gm_pref); break;  // 64 x 128
+    case 24: rc = launch_dma<2, 2, 2, 2, 32>(g, batch, splits, ws, ws_floats, counters, n_counters, st, 1, gm_pref); break;   // 128 x 128
+    case 25: rc = launch_dma<2, 2, 2, 2, 32, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st, 1, gm_pref); break;  // 128 x 128, 4-slot
+    case 26: rc = launch_dma<4, 2, 1, 2, 32>(g, batch, splits, ws, ws_floats, counters, n_counters, st, 1, gm_pref); break;   // 128 x 128, 8 waves
+    case 27: rc = launch_dma<2, 2, 2, 1, 32, 4>(g, batch, splits, ws, ws_floats, counters, n_counters, st, 1, gm_pref); break;  // 128 x 64, 4-slot
     default: return 1;
   }
   // 8-wave tiles outside their envelope (shape, or rows not 16-byte aligned for the

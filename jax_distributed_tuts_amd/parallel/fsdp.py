@@ -397,7 +397,10 @@ class _LoopView:
         self.master = sp.local.master
 
     def s(self, name):
-        return self.sp.local.s(name) if self.one else self.sp.full.s(name)
+        # replicated leaves: the local bf16 shadow, which the optimizer keeps current (the
+        # per-minibatch all-gather moves only the sharded leaves, so the full buffer's copy
+        # of a replicated leaf is only as fresh as the last sp.gather())
+        return self.sp.local.s(name) if (self.one or name in self.sp.repl_names) else self.sp.full.s(name)
 
     def g(self, name):
         return self.sp.local.g(name) if (self.one or name in self.sp.repl_names) else self.sp.full.g(name)

@@ -71,6 +71,23 @@ def init_stage_params(stage_model, full_specs, seed: int, device) -> FlatParams:
     return P
 
 
+def default_microbatches(n_stages: int) -> int:
+    """GPipe microbatch count when the caller does not pick one.
+
+    Measured, not the textbook 2S-or-more (profiles/r3_pp_schedule.json,
+    tools/pp_schedule.py: per-stage fwd / bwd tick cost on one MI355X at n = 1..16
+    microbatches): the stage kernels are latency-bound, so a tick costs nearly the
+    same at 8 rows as at 64 (8-stage MLP backward tick 12.9 us at 64 rows, 12.5 at 16,
+    15.3 at 8) and every extra microbatch adds a whole tick.  Modeled step time
+    (n + S - 1) * (t_f + t_b), hand-off hops excluded: 8-stage MLP 204 / 183 / 203 /
+    268 / 468 us at n = 1 / 2 / 4 / 8 / 16; 4-stage LM (8 sequences per pipe) 1023 /
+    1055 / 1196 / 1616 us at n = 1 / 2 / 4 / 8.  n = 2 is the MLP's best and within 3 %
+    of the LM's (n = 1 is no pipelining at all); per-tick xGMI hops only widen the gap
+    to larger n.  A single stage keeps the tutorial's 4 minibatches (its merged /
+    layer-major pass makes the count a loss-weighting detail)."""
+    return 4 if n_stages <= 1 else 2
+
+
 @dataclass
 class PipeConfig:
     num_microbatches: int = 4

@@ -53,6 +53,10 @@ def main(args):
     ws = D.world_size()
     dp = args.dp
     mesh = Mesh({"data": dp, "pipe": ws // dp})
+    if args.microbatches is None:
+        from jax_distributed_tuts_amd.parallel.pipeline import default_microbatches
+
+        args.microbatches = default_microbatches(ws // dp)
     if args.model == "transformer":
         from jax_distributed_tuts_amd.parallel.pipeline_lm import build_lm_pipeline, lm_batch
 
@@ -83,7 +87,8 @@ def main(args):
 if __name__ == "__main__":
     ap = add_common_args(argparse.ArgumentParser(), steps=10, accum_choices=("loop",))
     ap.add_argument("--dp", type=int, default=1)
-    ap.add_argument("--microbatches", type=int, default=4)
+    ap.add_argument("--microbatches", type=int, default=None,
+                    help="GPipe microbatches (default: pipeline.default_microbatches, measured per stage count)")
     ap.add_argument("--hidden-layers", type=int, default=8)
     ap.add_argument("--model", choices=["mlp", "transformer"], default="mlp")
     a = ap.parse_args()

@@ -109,6 +109,63 @@ def test_fused_mode1_adamw_scale_matches_fp64(num_layers):
         check_grad(10 * d / (1 - d.abs()), want[n], n)
 
 
+def _adam_inv(before, after):
+    """Gradient recovered from one AdamW(b1 = b2 = 0, eps = 10, wd = 0, lr = 1) update:
+    d = g / (|g| + 10)  ->  g = 10 d / (1 - |d|)."""
+    d = before.double() - after.double()
+    return 10 * d / (1 - d.abs())
+
+
+@pytest.mark.parametrize("num_layers", [2, 4])
+def test_run_ahead_adamw_scale_matches_fp64(num_layers):
+    """The run-ahead schedule (one launch per step: step t's CE / backward / AdamW + step
+    t+1's forward) through its hipGraphs, scale-checked: AdamW with b1 = b2 = 0 and
+    eps = 10 makes every step's update g / (|g| + 10), proportional to that step's
+    gradient.  The cold graph (step 0: forward + run-ahead backward), the primed graph
+    (step 1: its forward already ran inside step 0's launch, with the updated weights)
+    and the primed 4-step graph (the total displacement of 4 steps against the fp64
+    oracle iterated on the CPU with the kernels' dropout masks)."""
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, fold_rng_over_axis
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    st = _state(num_layers, adamw(1.0, b1=0.0, b2=0.0, eps=10.0, weight_decay=0.0))
+    b = _batch()
+    bg = Batch(b.inputs.to(DEV), b.labels.to(DEV))
+    tr = DataParallelTrainer(st, None, DPConfig(4, "kernel"))
+    tr.step(bg)   # eager step 0 builds the fused engine
+    tr.capture(bg, steps_per_graph=4)
+    assert tr._ahead is not None, "run-ahead graphs not built"
+    seed = fold_rng_over_axis(st.rng, None, "data") & 0xFFFFFFFF
+    model = st.apply_fn
+
+    def oracle(params, step):
+        return mlp_grads_fp64(params, model.names, b.inputs, b.labels,
+                              masks=_masks(seed, model.L - 1, 128, 4, step=step), keep=0.9, n_mb=4)
+
+    # cold replay (step 1) and primed replay (step 2)
+    for step in (1, 2):
+        before = _cpu(st.params.state_dict())
+        tr.step(bg)
+        torch.cuda.synchronize()
+        after = _cpu(st.params.state_dict())
+        want = oracle(before, step)
+        for n in want:
+            check_grad(_adam_inv(before[n], after[n]), want[n], f"step {step} {n}")
+    # primed 4-step graph: steps 3..6 against the iterated fp64 oracle
+    before = _cpu(st.params.state_dict())
+    tr.run_steps(bg, 4)
+    tr.finalize()
+    torch.cuda.synchronize()
+    after = _cpu(st.params.state_dict())
+    p = {n: v.double() for n, v in before.items()}
+    for step in range(3, 7):
+        g = oracle({n: v.float() for n, v in p.items()}, step)
+        for n in g:
+            p[n] = p[n] - g[n] / (g[n].abs() + 10.0)
+    for n in p:
+        check_grad(before[n].double() - after[n].double(), before[n].double() - p[n], f"4 steps {n}")
+
+
 @pytest.mark.parametrize("accum", ["loop", "fused"])
 def test_generic_gemm_path_sgd_matches_fp64(accum):
     """Per-minibatch generic kernels (GEMM epilogues, CE kernel) + the SGD kernel;

@@ -172,6 +172,43 @@ def test_gemm_vec_epilogue_bit_identical(cfg, r, a_layout, b_layout):
     _close(db_v, db_e, rtol=1e-5, atol=1e-4)  # fp32 atomics: summation order differs
 
 
+@pytest.mark.parametrize("cfg", [20, 21, 22, 23, 24, 25, 26, 27])
+@pytest.mark.parametrize("a_layout,b_layout", [("mk", "kn"), ("mk", "nk"), ("km", "kn"), ("km", "nk")])
+def test_gemm_mfma32_tiles(cfg, a_layout, b_layout):
+    """32x32x16-MFMA LDS-DMA tiles (64 x 64 .. 128 x 128, 3- and 4-slot rings, 4 and 8
+    waves; transposed operands through the 32-column tr-read fragment): every fused
+    epilogue and split-K against the 16x16x32 128 x 128 tile (same arithmetic, a
+    different in-MFMA summation order: bf16-rounding close, not bit-identical) and the
+    fp32 product against torch."""
+    M, N, K_ = 512, 512, 1024
+    a = _mk((M, K_) if a_layout == "mk" else (K_, M), torch.bfloat16, seed=81).to(DEV)
+    b = (_mk((K_, N) if b_layout == "kn" else (N, K_), torch.float32, seed=82) * 0.05).to(torch.bfloat16).to(DEV)
+    bias, res = _mk((N,), torch.bfloat16, seed=83).to(DEV), _mk((M, N), torch.bfloat16, seed=84).to(DEV)
+    z = _mk((M, N), torch.bfloat16, seed=85).to(DEV)
+
+    def run(c):
+        kw = dict(a_layout=a_layout, b_layout=b_layout, cfg=c)
+        zo = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        f = kern.gemm(a, b, bias=bias, act="gelu", z_out=zo, resid=res, **kw)
+        db = torch.zeros(N, device=DEV)
+        g = kern.gemm(a, b, z_in=z, act_bwd="silu", dbias=db, **kw)
+        acc32 = [torch.full((M, N), 0.5, device=DEV) for _ in range(2)]
+        kern.gemm(a, b, out=acc32[0], accumulate=True, splits=1, **kw)
+        kern.gemm(a, b, out=acc32[1], accumulate=True, splits=4, **kw)
+        torch.cuda.synchronize()
+        return [zo, f, g, acc32[0], acc32[1]], db
+
+    outs, db = run(cfg)
+    ref_outs, ref_db = run(14)
+    for x, y in zip(outs, ref_outs):
+        _close(x.float(), y.float(), rtol=2e-2, atol=2e-2)
+    _close(db, ref_db, rtol=1e-3, atol=1e-2)
+    A = a.float() if a_layout == "mk" else a.float().t()
+    B = b.float() if b_layout == "kn" else b.float().t()
+    for o in outs[3:]:
+        _close(o - 0.5, A @ B, rtol=2e-3, atol=2e-3)
+
+
 @pytest.mark.parametrize("cfg", [15, 16, 17, 18])
 @pytest.mark.parametrize("a_layout,b_layout", [("mk", "kn"), ("mk", "nk"), ("km", "kn"), ("km", "nk")])
 def test_gemm_8wave_tiles_match_4wave(cfg, a_layout, b_layout):

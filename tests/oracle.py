@@ -15,6 +15,9 @@ gradient, so a missing 1/N or 1/n_minibatch shows up as a scale error.
 """
 from __future__ import annotations
 
+import json
+import os
+
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -81,17 +84,28 @@ def lm_grads_fp64(params: Dict[str, torch.Tensor], cfg, tok: torch.Tensor, label
     return {n: t.grad.detach() for n, t in ps.items()}
 
 
-def check_grad(got: torch.Tensor, want: torch.Tensor, name: str = "", rel_tol: float = 0.05,
-               scale_tol: float = 0.03):
+def check_grad(got: torch.Tensor, want: torch.Tensor, name: str = "", rel_tol: float = 0.02,
+               scale_tol: float = 0.005):
     """Engine gradient (bf16 matmul operands, fp32 accumulate) vs the fp64 oracle:
     relative L2 error below ``rel_tol`` AND the least-squares scale
     <got, want> / <want, want> within ``1 +- scale_tol`` (a factor-2 error can
-    never pass)."""
+    never pass).
+
+    Defaults pinned at about twice the largest error measured on the MLP kernel
+    paths (JDT_ORACLE_LOG over the whole GPU suite, profiles/r3_oracle_errors.txt):
+    fused per-layer / run-ahead / generic / xGMI-strategy / GPipe paths max rel 0.0088,
+    max |scale - 1| 0.0011 (dropout on, 8-row microbatches the worst).  A dropped
+    4-row group of a 128-row batch is a 3 % scale error; a missing 1/N is 50 %."""
     g, w = got.double().flatten(), want.double().flatten()
     wn = float(w.norm())
     assert wn > 0, f"{name}: zero oracle gradient"
     rel = float((g - w).norm()) / wn
     scale = float(g @ w) / float(w @ w)
+    log = os.environ.get("JDT_ORACLE_LOG")
+    if log:   # measured error per (test, leaf): the data the pinned tolerances come from
+        with open(log, "a") as f:
+            f.write(json.dumps({"test": os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0], "name": name,
+                                "rel": rel, "scale": scale, "rel_tol": rel_tol, "scale_tol": scale_tol}) + "\n")
     assert rel < rel_tol and abs(scale - 1.0) < scale_tol, f"{name}: rel err {rel:.4f}, scale {scale:.4f}"
     return rel, scale
 

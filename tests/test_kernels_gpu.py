@@ -1084,7 +1084,10 @@ def test_overlapped_adamw_equals_single_launch(graph, monkeypatch):
 
     noise, diff = frac(res["0"][0], res["0b"][0]), frac(res["0"][0], res["1"][0])
     print(f"params differing > 1e-5: run-to-run {noise:.2e}, overlapped {diff:.2e}")
-    assert diff <= 4 * noise + 2e-3, (diff, noise)
+    # a race moves whole weight matrices (each block's 4 kernels are ~24 % of the stage);
+    # a run whose atomics happened to be order-identical (noise 0) still leaves ~1 % of
+    # near-zero-gradient elements apart once the overlap reorders the reductions
+    assert diff <= 4 * noise + 0.03, (diff, noise)
     loss = [float(r[3][0]) for r in (res["0"], res["1"], res["0b"])]
     assert abs(loss[1] - loss[0]) <= 1e-3 * abs(loss[0]) + 4 * abs(loss[2] - loss[0]), loss
 

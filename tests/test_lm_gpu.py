@@ -49,7 +49,7 @@ def test_lm_bench_config_grads_match_fp64_autograd(layer_major):
     assert set(got) == set(want) and len(got) == 54
     worst = 0.0
     for k in sorted(want):
-        rel, scale = check_grad(got[k].cpu(), want[k].cpu(), k, rel_tol=0.05, scale_tol=0.02)
+        rel, scale = check_grad(got[k].cpu(), want[k].cpu(), k, rel_tol=0.025, scale_tol=0.004)  # measured max 0.0126 / 0.0015
         worst = max(worst, rel)
     print(f"[lm bench grads, layer_major={layer_major}] worst rel err {worst:.3e}")
 

@@ -108,7 +108,7 @@ def test_fsdp_over_xgmi_matches_single_device(tmp_path, fused, num_layers, eps):
         assert float(diff.max()) <= 2 * 1e-3 * 3 + 1e-6, n
         assert float((diff > 5e-5).float().mean()) < 5e-3, n
         if eps > 1.0:  # the 3-step update is ~ proportional to the gradients: scale-checked
-            check_grad(got - p0[n], sp.local.p(n).cpu() - p0[n], f"{n} update", rel_tol=0.05, scale_tol=0.02)
+            check_grad(got - p0[n], sp.local.p(n).cpu() - p0[n], f"{n} update")
     m, ref = res[0]["metrics"], tr.metrics.cpu()
     assert abs(float(m[0]) - float(ref[0])) <= 1e-3 * abs(float(ref[0])) + 1e-3
     assert float(m[1]) == float(ref[1])

@@ -2,7 +2,7 @@
 # Full GPU suite (run-ahead AdamW scale probe, FSDP loop fix, 32x32 MFMA tiles), LM benches with the
 # round-3 GEMM table, shared-GPU PP rehearsals at the new default microbatch count, per-mb LM profile
 cd /root/repo && export TMPDIR=/tmp PYTHONUNBUFFERED=1 && mkdir -p gpurun_out/s3
-timeout -k 10 700 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > gpurun_out/s3/pytest.log 2>&1
+JDT_ORACLE_LOG=gpurun_out/s3/oracle.jsonl timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > gpurun_out/s3/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "FAILED|passed|failed|Error" gpurun_out/s3/pytest.log | tail -8
 case $rc in 0) ;; *) exit $rc;; esac
 : > gpurun_out/s3/all.jsonl

@@ -1683,10 +1683,14 @@ static const GemmTune kGemmTune[] = {
     {512, 512, 2048, 1, 1, 13, 2, 0},    // out dW                    10.41 (15.46)
     {256, 1536, 512, 0, 1, 10, 2, 0},    // qkv fwd (hybrid, 256 rows) 5.55 (5.60)
     {256, 512, 2048, 0, 1, 13, 2, 0},    // fc2 fwd (hybrid)          8.38 (9.84)
-    // round 3: 32x32x16-MFMA tiles (tools/bench_gemm.py --cfg 20 / 26 sweep,
-    // profiles/r3_gemm_mfma32_sweep.txt; default-table time in parentheses)
-    {512, 2048, 512, 0, 1, 20, 1, 0},    // fc1 / head fwd, 512 rows   7.64 (10.76)
-    {512, 2048, 512, 0, 0, 20, 1, 0},    // fc2 dX, 512 rows           7.46 (9.67)
+    // round 3: 512-row (one microbatch of 4 sequences) and qkv shapes, from the cfg x split-K
+    // sweeps (profiles/r3_gemm_mfma32_sweep.txt, r3_gemm_cfg_split_sweep.txt; previous
+    // table / heuristic time in parentheses)
+    {512, 2048, 512, 0, 1, 10, 1, 0},    // fc1 / head fwd, 512 rows   6.60 (10.76; cfg 20 7.52)
+    {512, 2048, 512, 0, 0, 10, 1, 0},    // fc2 dX, 512 rows           5.95 (9.67; cfg 20 7.26)
+    {512, 512, 2048, 0, 1, 10, 1, 0},    // fc2 fwd, 512 rows (split 4) 10.00 (11.41)
+    {512, 512, 2048, 0, 0, 10, 1, 0},    // fc1 / head dX, 512 rows     9.42 (10.16)
+    {512, 512, 1536, 0, 0, 10, 1, 0},    // qkv dX, 512 rows (as fc1 dX)
     {512, 2048, 512, 1, 1, 20, 1, 0},    // fc1 dW, 512 tokens         8.11 (9.80)
     {2048, 512, 512, 1, 1, 20, 1, 0},    // fc2 dW, 512 tokens         8.15 (9.92)
     {2048, 1536, 512, 0, 1, 26, 1, 0},   // qkv fwd (2048 rows)       11.87 (14.92)

@@ -1201,6 +1201,50 @@ def test_pipeline_single_stage_run_ahead(monkeypatch):
     _close(res["1"][1], res["0"][1], rtol=1e-3, atol=5e-2)
 
 
+def test_deep_run_ahead_mb_streams_20_steps(monkeypatch):
+    """JDT_MLP2_AHEAD_MB (run-ahead with per-microbatch dropout streams, one-stage GPipe
+    on the deep engine) over 20 captured steps at keep 0.5, against the plain launch
+    sequence: AdamW with b1 = b2 = 0 and eps = 10 makes every update
+    g / (|g| + 10), proportional to that step's gradient, so the 20-step displacement of
+    every leaf compares like a gradient (relative L2 error and least-squares scale).  A
+    mask drawn from the wrong microbatch / step stream at keep 0.5 changes half of a
+    layer's units: far outside bf16 noise."""
+    from data_paral import synthetic_batch
+    from pipeline_parallel import build_mlp_pipeline
+    from jax_distributed_tuts_amd.runtime.dist import Mesh
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    from .oracle import check_grad
+
+    mesh = Mesh({"data": 1, "pipe": 1})
+    monkeypatch.setenv("JDT_MLP2_AHEAD_MB", "1")
+    res = {}
+    for ahead in ("0", "1"):
+        monkeypatch.setenv("JDT_MLP2_AHEAD", ahead)
+        cfg = dp_config()
+        tr = build_mlp_pipeline(cfg, mesh, DEV, 4, dropout_rate=0.5, num_microbatches=4,
+                                tx=adamw(0.01, b1=0.0, b2=0.0, eps=10.0, weight_decay=0.0))
+        b = synthetic_batch(cfg, 70)
+        b = Batch(b.inputs.to(DEV), b.labels.to(DEV))
+        p0 = {k: v.detach().clone().cpu() for k, v in tr.state.params.state_dict().items()}
+        tr.step(b)
+        eng = tr.deep_engine
+        assert eng is not None and eng.mb_rows > 0 and eng.ahead_ok == (ahead == "1")
+        tr.capture(b, steps_per_graph=5)
+        tr.run_steps(b, 15)
+        for _ in range(4):
+            tr.step(b)
+        tr.finalize()
+        torch.cuda.synchronize()
+        assert int(tr.state.opt_state["count"].item()) == 20
+        if ahead == "1":
+            assert int(eng.ztick[1].item()) == 0
+        res[ahead] = {k: (p0[k].double() - v.detach().cpu().double()) for k, v in tr.state.params.state_dict().items()}
+    for k in res["0"]:
+        check_grad(res["1"][k], res["0"][k], f"20-step displacement {k}")
+
+
 def test_fused_sgd_matches_mode0_sgd(monkeypatch):
     """Momentum-free SGD fused into mlp2_bwd's epilogue (opt_sgd, incl. the run-ahead
     graphs) == mode 0 (plain-stored grads) + the standalone SGD kernel.  SGD moves

@@ -99,3 +99,22 @@ def test_apply_gradients_adamw_cpu():
     torch.testing.assert_close(P.p("input_dense/kernel"), exp, rtol=1e-5, atol=1e-6)
     assert st.step == 1 and int(st.opt_state["count"]) == 1
     assert float(P.grad.abs().max()) == 0.0
+
+
+def test_default_microbatches_follows_measured_table():
+    """pipeline.default_microbatches: the count the measured GPipe table picked
+    (profiles/r3_pp_schedule.json: best modeled step of the 8-stage MLP at n = 2, the
+    4-stage LM within 3 % of its best there); a single stage keeps the tutorial's 4."""
+    import json
+    import os
+
+    from jax_distributed_tuts_amd.parallel.pipeline import default_microbatches
+
+    assert default_microbatches(1) == 4
+    assert all(default_microbatches(s) == 2 for s in (2, 4, 8))
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r3_pp_schedule.json")
+    rep = json.load(open(path))
+    mlp = rep["layouts"]["mlp_pp8"]
+    assert mlp["best_n_mb"] == default_microbatches(mlp["stages"])
+    lm = {r["n_mb"]: r["modeled_step_us"] for r in rep["layouts"]["lm_pp4"]["table"]}
+    assert lm[default_microbatches(4)] <= 1.05 * min(lm.values())

@@ -26,6 +26,52 @@ __device__ __forceinline__ void finish_ticket(int* step, unsigned* ticket) {
   }
 }
 
+constexpr int AW_U = 4;
+
+// AdamW on U float4 groups at float4 indices idx[u] (loads first, then math, then the
+// stores of the groups whose logical index q0 + u * stride is < n4)
+template <int U>
+__device__ __forceinline__ void adam_rows(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                                          float* __restrict__ v, bf16_t* __restrict__ shadow, const long (&idx)[U],
+                                          long q0, long stride, long n4, float lr, float b1, float b2, float eps,
+                                          float wd, float grad_scale, float rbc1, float rbc2, int zero_grad) {
+  float4 pp[U], gg[U], mm[U], vv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    pp[u] = reinterpret_cast<const float4*>(p)[idx[u]];
+    gg[u] = reinterpret_cast<const float4*>(g)[idx[u]];
+    mm[u] = reinterpret_cast<const float4*>(m)[idx[u]];
+    vv[u] = reinterpret_cast<const float4*>(v)[idx[u]];
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    float* pe = &pp[u].x; float* ge = &gg[u].x; float* me = &mm[u].x; float* ve = &vv[u].x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gr = ge[k] * grad_scale;
+      me[k] = b1 * me[k] + (1.f - b1) * gr;
+      ve[k] = b2 * ve[k] + (1.f - b2) * gr * gr;
+      const float upd = (me[k] * rbc1) / (sqrtf(ve[k] * rbc2) + eps) + wd * pe[k];
+      pe[k] -= lr * upd;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (q0 + u * stride >= n4) break;   // uniform for all but the last round
+    const long i = idx[u];
+    reinterpret_cast<float4*>(p)[i] = pp[u];
+    reinterpret_cast<float4*>(m)[i] = mm[u];
+    reinterpret_cast<float4*>(v)[i] = vv[u];
+    if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (shadow) {
+      uint2 sh;
+      sh.x = (unsigned)f2bf(pp[u].x) | ((unsigned)f2bf(pp[u].y) << 16);
+      sh.y = (unsigned)f2bf(pp[u].z) | ((unsigned)f2bf(pp[u].w) << 16);
+      reinterpret_cast<uint2*>(shadow)[i] = sh;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                                     float* __restrict__ v, bf16_t* __restrict__ shadow, long n,
                                                     float lr, float b1, float b2, float eps, float wd, float grad_scale,
@@ -35,30 +81,14 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, float
   const float rbc1 = 1.f / bc1, rbc2 = 1.f / bc2;
   const long n4 = n / 4;
   const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 pp = reinterpret_cast<float4*>(p)[i];
-    float4 gg = reinterpret_cast<float4*>(g)[i];
-    float4 mm = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
-    float* pe = &pp.x; float* ge = &gg.x; float* me = &mm.x; float* ve = &vv.x;
+  // AW_U float4 per thread per round, every load issued before any use (clamped
+  // indices, no branch around a load): a round trip per AW_U elements instead of one
+  // per element, so a one-workgroup-per-CU grid still streams at HBM rate
+  for (long q0 = (long)blockIdx.x * blockDim.x + threadIdx.x; q0 < n4; q0 += AW_U * stride) {
+    long idx[AW_U];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float gr = ge[k] * grad_scale;
-      me[k] = b1 * me[k] + (1.f - b1) * gr;
-      ve[k] = b2 * ve[k] + (1.f - b2) * gr * gr;
-      const float upd = (me[k] * rbc1) / (sqrtf(ve[k] * rbc2) + eps) + wd * pe[k];
-      pe[k] -= lr * upd;
-    }
-    reinterpret_cast<float4*>(p)[i] = pp;
-    reinterpret_cast<float4*>(m)[i] = mm;
-    reinterpret_cast<float4*>(v)[i] = vv;
-    if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (shadow) {
-      uint2 s;
-      s.x = (unsigned)f2bf(pp.x) | ((unsigned)f2bf(pp.y) << 16);
-      s.y = (unsigned)f2bf(pp.z) | ((unsigned)f2bf(pp.w) << 16);
-      reinterpret_cast<uint2*>(shadow)[i] = s;
-    }
+    for (int u = 0; u < AW_U; ++u) idx[u] = min(q0 + u * stride, n4 - 1);
+    adam_rows<AW_U>(p, g, m, v, shadow, idx, q0, stride, n4, lr, b1, b2, eps, wd, grad_scale, rbc1, rbc2, zero_grad);
   }
   // tail
   for (long i = n4 * 4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -90,34 +120,19 @@ __global__ void __launch_bounds__(256) adamw_ranges_kernel(float* __restrict__ p
   const float rbc1 = 1.f / (1.f - powf(b1, (float)t)), rbc2 = 1.f / (1.f - powf(b2, (float)t));
   const long n4 = total / 4;
   const long stride = (long)gridDim.x * blockDim.x;
-  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += stride) {
-    const long e = 4 * q;
-    int lo = 0, hi = nr - 1;   // last range with prefix <= e
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (prefix[mid] <= e) lo = mid; else hi = mid - 1;
-    }
-    const long i = (start[lo] + (e - prefix[lo])) >> 2;   // float4 index
-    float4 pp = reinterpret_cast<float4*>(p)[i];
-    float4 gg = reinterpret_cast<float4*>(g)[i];
-    float4 mm = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
-    float* pe = &pp.x; float* ge = &gg.x; float* me = &mm.x; float* ve = &vv.x;
+  for (long q0 = (long)blockIdx.x * blockDim.x + threadIdx.x; q0 < n4; q0 += AW_U * stride) {
+    long idx[AW_U];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float gr = ge[k] * grad_scale;
-      me[k] = b1 * me[k] + (1.f - b1) * gr;
-      ve[k] = b2 * ve[k] + (1.f - b2) * gr * gr;
-      pe[k] -= lr * ((me[k] * rbc1) / (sqrtf(ve[k] * rbc2) + eps) + wd * pe[k]);
+    for (int u = 0; u < AW_U; ++u) {
+      const long e = 4 * min(q0 + u * stride, n4 - 1);
+      int lo = 0, hi = nr - 1;   // last range with prefix <= e
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (prefix[mid] <= e) lo = mid; else hi = mid - 1;
+      }
+      idx[u] = (start[lo] + (e - prefix[lo])) >> 2;   // float4 index
     }
-    reinterpret_cast<float4*>(p)[i] = pp;
-    reinterpret_cast<float4*>(m)[i] = mm;
-    reinterpret_cast<float4*>(v)[i] = vv;
-    reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    uint2 sh;
-    sh.x = (unsigned)f2bf(pp.x) | ((unsigned)f2bf(pp.y) << 16);
-    sh.y = (unsigned)f2bf(pp.z) | ((unsigned)f2bf(pp.w) << 16);
-    reinterpret_cast<uint2*>(shadow)[i] = sh;
+    adam_rows<AW_U>(p, g, m, v, shadow, idx, q0, stride, n4, lr, b1, b2, eps, wd, grad_scale, rbc1, rbc2, 1);
   }
   finish_ticket(step, ticket);
 }
@@ -160,10 +175,12 @@ static int grid_for(long n, int per_thread, int cap = 2048) {
 // arrival ticket per workgroup; those atomics serialise, so those kernels run
 // at most one workgroup per CU and grid-stride over the rest.
 constexpr int kTicketGrid = 256;
-// Large buffers (the transformer's ~13M params): a 256-workgroup grid-stride
-// loop is latency-bound (each thread's iterations are serial round trips), so
-// above ~1M elements the grid grows to 2048 workgroups (8 per CU).
-static int ticket_grid(long n, int per_thread) { return grid_for(n, per_thread, n > (1L << 20) ? 2048 : kTicketGrid); }
+// (Round 2 grew the grid to 2048 workgroups above ~1M elements because a 256-workgroup
+// grid-stride loop was latency-bound; but 2048 same-address tickets serialise at
+// ~12.7 ns each = 26 us, most of the transformer's 23 us AdamW launch.  The AdamW loops
+// now keep AW_U groups of loads in flight per thread instead, so one workgroup per CU
+// streams at HBM rate and the ticket chain is 256 long.)
+static int ticket_grid(long n, int per_thread) { return grid_for(n, per_thread, kTicketGrid); }
 
 }  // namespace jdt
 using namespace jdt;

@@ -35,7 +35,7 @@ from ..runtime.dist import Mesh
 from ..utils import rng as R
 from ..utils.flat import FlatParams, N_METRIC_SLOTS
 from ..utils.profiling import named_scope, replay_scope
-from ..utils.train_state import AdamW, Batch, TrainState
+from ..utils.train_state import AdamW, Batch, TrainState, check_static_batch, load_static_batch
 
 
 def fold_rng_over_axis(rng: int, mesh: Optional[Mesh], axis_name: str) -> int:
@@ -306,11 +306,19 @@ class DataParallelTrainer:
 
     def step(self, batch: Batch):
         if self.graph is not None:
+            check_static_batch(self._static, batch)
             self._replay()
             return
         self.compute(batch)
         self.sync()
         self.update()
+
+    def set_batch(self, batch: Batch):
+        """New data for captured graphs: copied into the captured batch tensors (the
+        run-ahead schedule's next forward, computed from the old contents, is redone)."""
+        if self._static is None:
+            return
+        load_static_batch(self._static, batch, (self.fused,))
 
     # ------------------------------------------------------------------ hipGraph
     def capture(self, batch: Batch, capture_collectives: bool = False, steps_per_graph: int = 1):
@@ -431,6 +439,8 @@ class DataParallelTrainer:
         """n training steps; with a multi-step graph, n // S replays of it plus
         single-step replays for the remainder."""
         multi = getattr(self, "multi", None)
+        if self.graph is not None:
+            check_static_batch(self._static, batch)
         if self.graph is not None and multi is not None:
             S, gm = multi
             for _ in range(n // S):

@@ -45,7 +45,7 @@ from ..runtime.dist import Mesh
 from ..utils import rng as R
 from ..utils.flat import FlatParams, ParamSpec, N_METRIC_SLOTS
 from ..utils.profiling import named_scope, replay_scope
-from ..utils.train_state import AdamW, Batch, TrainState
+from ..utils.train_state import AdamW, Batch, TrainState, check_static_batch, load_static_batch
 
 log = logging.getLogger("jdt.fsdp")
 
@@ -537,9 +537,15 @@ class FSDPTrainer:
             K.metrics_fold_(self.metrics, sp.local.metrics_slot)
         return True
 
+    def set_batch(self, batch: Batch):
+        """New data for captured graphs (see DataParallelTrainer.set_batch)."""
+        if getattr(self, "_static", None) is not None:
+            load_static_batch(self._static, batch, (self.fused, self._loop_engine))
+
     def step(self, batch: Batch):
         """train_step_fsdp (param_sharding.py:343-367)."""
         if self.graph is not None:
+            check_static_batch(getattr(self, "_static", None), batch)
             with replay_scope("train_step_fsdp"):
                 self._ahead.replay(1) if self._ahead else self.graph.replay()
         else:
@@ -557,6 +563,7 @@ class FSDPTrainer:
         all-reduce, sharded AdamW, metrics fold) as a hipGraph; with
         ``steps_per_graph`` > 1 also a graph of that many consecutive steps."""
         assert self.capturable and batch.inputs.is_cuda
+        self._static = batch
         if not self._full_fresh:   # the fused step collective keeps the full shadow current
             self.sp.gather()
             self._full_fresh = True
@@ -582,6 +589,8 @@ class FSDPTrainer:
             self.multi = (steps_per_graph, gm)
 
     def run_steps(self, batch: Batch, n: int):
+        if self.graph is not None:
+            check_static_batch(getattr(self, "_static", None), batch)
         if self.graph is not None and self.multi is not None:
             S, gm = self.multi
             for _ in range(n // S):

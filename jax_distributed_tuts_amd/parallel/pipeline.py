@@ -37,7 +37,7 @@ from ..runtime.dist import Mesh, is_initialized
 from ..utils import rng as R
 from ..utils.flat import FlatParams, N_METRIC_SLOTS
 from ..utils.profiling import named_scope, replay_scope
-from ..utils.train_state import AdamW, Batch, TrainState
+from ..utils.train_state import AdamW, Batch, TrainState, check_static_batch, load_static_batch
 
 
 def split_layers(n_layers: int, n_stages: int) -> List[range]:
@@ -463,8 +463,14 @@ class GPipeTrainer:
         with named_scope("sync_metrics"):
             K.metrics_fold_(self.metrics, P.metrics_slot)
 
+    def set_batch(self, batch: Batch):
+        """New data for captured graphs (see DataParallelTrainer.set_batch)."""
+        if getattr(self, "_static", None) is not None:
+            load_static_batch(self._static, batch, (self.deep_engine,))
+
     def step(self, batch: Batch):
         if self.graph is not None:
+            check_static_batch(getattr(self, "_static", None), batch)
             with replay_scope("train_step_pp"):
                 self._ahead.replay(1) if getattr(self, "_ahead", None) else self.graph.replay()
         else:
@@ -506,6 +512,8 @@ class GPipeTrainer:
             self.multi = (steps_per_graph, gm)
 
     def run_steps(self, batch: Batch, n: int):
+        if self.graph is not None:
+            check_static_batch(getattr(self, "_static", None), batch)
         if self.graph is not None and self.multi is not None:
             S, gm = self.multi
             for _ in range(n // S):

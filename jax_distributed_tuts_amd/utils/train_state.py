@@ -51,6 +51,36 @@ class Batch:
     def size(self) -> int:
         return int(self.inputs.shape[0])
 
+    def same_storage(self, other: "Batch") -> bool:
+        return (self.inputs.data_ptr() == other.inputs.data_ptr() and self.labels.data_ptr() == other.labels.data_ptr()
+                and self.inputs.shape == other.inputs.shape and self.labels.shape == other.labels.shape)
+
+
+def check_static_batch(static: Optional[Batch], batch: Batch) -> None:
+    """A captured hipGraph reads the batch tensors it was captured with: a step on
+    other tensors would silently train on the captured data.  New data goes into the
+    captured tensors through the trainer's ``set_batch`` (which also drops a run-ahead
+    forward computed from the old contents)."""
+    if static is not None and batch is not static and not batch.same_storage(static):
+        raise ValueError("this trainer replays hipGraphs captured on another batch: copy the new data in with "
+                         "trainer.set_batch(batch) (or call trainer.invalidate() and capture again)")
+
+
+def load_static_batch(static: Batch, batch: Batch, engines=()) -> None:
+    """Copy ``batch`` into the captured batch tensors; engines whose run-ahead launch
+    already computed the next forward from the old contents restart cold."""
+    if batch is static or batch.same_storage(static):
+        pass
+    else:
+        if batch.inputs.shape != static.inputs.shape or batch.labels.shape != static.labels.shape:
+            raise ValueError(f"set_batch: shapes {tuple(batch.inputs.shape)} / {tuple(batch.labels.shape)} differ "
+                             f"from the captured {tuple(static.inputs.shape)} / {tuple(static.labels.shape)}")
+        static.inputs.copy_(batch.inputs)
+        static.labels.copy_(batch.labels)
+    for e in engines:
+        if e is not None and hasattr(e, "ahead_primed"):
+            e.ahead_primed = False
+
 
 # ---------------------------------------------------------------------------- optimizers
 @dataclass

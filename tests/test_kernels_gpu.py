@@ -303,8 +303,8 @@ def test_xent(M, C, dt):
     _close(m_g, m_r, rtol=1e-5, atol=1e-3)
 
 
-def test_adamw_and_step_counter():
-    n = 407050
+@pytest.mark.parametrize("n", [407050, 3_000_001])   # one partial round / several rounds of AW_U groups per thread
+def test_adamw_and_step_counter(n):
     g = torch.Generator().manual_seed(0)
     p = torch.randn(n, generator=g)
     gr = torch.randn(n, generator=g)
@@ -1243,6 +1243,50 @@ def test_deep_run_ahead_mb_streams_20_steps(monkeypatch):
         res[ahead] = {k: (p0[k].double() - v.detach().cpu().double()) for k, v in tr.state.params.state_dict().items()}
     for k in res["0"]:
         check_grad(res["1"][k], res["0"][k], f"20-step displacement {k}")
+
+
+@pytest.mark.parametrize("strategy", ["dp", "fsdp"])
+def test_set_batch_after_capture_matches_eager(strategy):
+    """New data for captured graphs: a step on other tensors raises (the graphs read the
+    captured ones), ``set_batch`` copies the data in and restarts the run-ahead cold (its
+    next forward was computed from the old contents) -- equal to eager steps on A, A, B, B."""
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
+    from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    g = torch.Generator().manual_seed(11)
+    A = Batch(torch.randn(128, 784, generator=g).to(DEV), torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV))
+    B = Batch(torch.randn(128, 784, generator=g).to(DEV), torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV))
+    res = []
+    for graph in (False, True):
+        if strategy == "dp":
+            st = init_dp(Classifier(), adamw(1e-3), 69, DEV)
+            tr = DataParallelTrainer(st, None, DPConfig(4, "kernel"))
+        else:
+            st = init_fsdp(Classifier(), adamw(1e-3), 69, DEV, None, "data", 16)
+            tr = FSDPTrainer(st, None, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=True))
+        a = Batch(A.inputs.clone(), A.labels.clone())   # the captured tensors (set_batch overwrites them)
+        tr.step(a)
+        if graph:
+            tr.capture(a)
+        tr.step(a)
+        if graph:
+            with pytest.raises(ValueError):
+                tr.step(B)
+            tr.set_batch(B)
+            tr.step(a)
+            tr.step(a)
+        else:
+            tr.step(B)
+            tr.step(B)
+        tr.finalize()
+        torch.cuda.synchronize()
+        res.append((st.params.master.clone(), tr.metrics.clone(), int(st.opt_state["count"].item())))
+    assert res[0][2] == res[1][2] == 4
+    d = (res[0][0] - res[1][0]).abs()
+    assert float(d.max()) <= 3e-3 and float((d > 1e-5).float().mean()) < 1e-3, (float(d.max()), float((d > 1e-5).float().mean()))
+    _close(res[1][1], res[0][1], rtol=1e-4, atol=1e-2)
 
 
 def test_fused_sgd_matches_mode0_sgd(monkeypatch):

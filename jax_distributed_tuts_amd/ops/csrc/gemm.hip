@@ -2077,11 +2077,12 @@ JDT_API int jdt_gemm_ln(const GemmArgs* ga, const LnArgs* la, void* stream) {
   int cfg = g_ln_cfg;
   if (cfg <= 0) {
     // measured (tools/bench_ln_gemm.py): the fused kernel normalises each row once per
-    // column block, so it only pays off while N / BN is small and the separate LN
-    // launch is a large share: M <= 512, N <= 1536 (qkv 512 rows 8.5 vs 9.4 us, 256
-    // rows 7.5 vs 8.1); the 2048-row shapes run LN + GEMM (qkv 14.1 vs 16.5 us best)
-    if (g.M > 512 || g.N > 1536) return -2;
-    cfg = g.M >= 512 ? 3 : 1;
+    // column block, so it only pays off while the separate LN launch is a large share:
+    // M <= 512 (round 3, 32 x 64 tile: qkv 512 rows 8.39 vs 9.50 us LN + GEMM, fc1
+    // 512 rows 9.79 vs 10.12, 256 rows 6.95 vs 7.42; profiles/r3_ln_gemm_sweep.txt);
+    // the 2048-row shapes run LN + GEMM (the fused 16 x 64 tile only ties them)
+    if (g.M > 512 || g.N > 2048) return -2;
+    cfg = 1;
   }
   if (g.K == 1024) return launch_ln<2, 2, 1, 2, 2>(g, L, st);
   switch (cfg) {

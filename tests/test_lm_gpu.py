@@ -58,15 +58,16 @@ def test_lm_bench_config_grads_match_fp64_autograd(layer_major):
 def test_lm_epilogue_adamw_matches_plain_adamw(layer_major):
     """AdamW fused into the weight-gradient GEMM epilogues (+ one multi-range launch for
     the rest) == the plain full-buffer AdamW pass, after 3 steps; the step counter
-    advances once per step.  Layer-major: to fp32 rounding.  Per-microbatch passes:
-    the step is not bitwise reproducible (fp32 atomics in the attention / LayerNorm /
-    embedding reductions; a second plain run shows the noise), and AdamW turns tiny
-    gradient differences into lr-sized updates where g ~ 0 -- so there the check is
-    that no weight leaf has more than 2 % of its elements half an update apart (a
-    missed microbatch contribution or a wrong gradient scale moves most of a leaf)."""
+    advances once per step.  The step is not bitwise reproducible (fp32 atomics in the
+    attention / LayerNorm / embedding / bias reductions; a second plain run shows the
+    noise -- layer-major runs usually come out bit-equal, not always), and AdamW turns
+    tiny gradient differences into lr-sized updates where g ~ 0 -- so the check is that
+    no weight leaf has more than 2 % of its elements half an update apart (a missed
+    microbatch contribution or a wrong gradient scale moves most of a leaf), plus the
+    loss sums."""
     lr = 3e-4
     res = {}
-    for fused in ("1", "0") if layer_major else ("1", "0", "0b"):
+    for fused in ("1", "0", "0b"):
         tr, b = _trainer(adamw(lr), layer_major, fused[0])
         assert (getattr(tr, "_eo", None) not in (None, False)) == (fused == "1")
         tr.step(b)
@@ -79,10 +80,6 @@ def test_lm_epilogue_adamw_matches_plain_adamw(layer_major):
     assert c1 == c0 == 3
     assert g1 == 0.0 and g0 == 0.0   # gradient buffers left zeroed for the next step
     assert float(((s1.float() - p1.to(torch.bfloat16).float()).abs()).max()) == 0.0   # shadow = bf16(master)
-    if layer_major:
-        d = (p1 - p0).abs()
-        assert float(d.max()) <= 1e-6 + 1e-5 * float(p0.abs().max()), float(d.max())
-        return
     noise_loss = abs(res["0b"][5] - l0)
     assert abs(l1 - l0) <= 1e-3 * abs(l0) + 4 * noise_loss, (l1, l0, res["0b"][5])
     for n in P0.names():

@@ -108,6 +108,14 @@ struct MdArgs {
   // ticket unused here, error word, launch counter; column barriers; per-XCD tile
   // counters), hand = updated b fp32 [N]; G / Hout are layer 0's G_0 / H_0
   bf16_t* XR; float* zslab; unsigned* ztick; float* hand;
+  // dZ split (md_bwd, !TOP && !BND, one GPU, every workgroup resident): the K/KC
+  // workgroups of a column block each compute only the 16-row blocks w of
+  // dZ_i[:, blk] with w % (K/KC) == chunk -- 1/(K/KC) of dZ_{i+1}'s bytes per
+  // workgroup instead of all of them -- publish them (write-through) to dzx
+  // [N/16][16][MD_MPM] (transposed, as the dzT image) and meet at a per-block arrival
+  // counter in dzc (128-byte lines: [0] error word, block b at 32 (1 + b)); then every
+  // workgroup reads the whole dZ_i[:, blk] back.  dzs = 0: each workgroup computes all rows.
+  bf16_t* dzx; unsigned* dzc; int dzs;
 };
 
 // Slots 0-4: s_memrealtime at the kernel's phase ends (tools/stamp_deep.py).
@@ -388,6 +396,8 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   const bool chunk0 = by == 0;
   const bool lead = TOP && bx == 0 && by == 0;
   const int rg = tid >> 4, gn = tid & 15;   // TOP: this thread's group (rows 4rg..4rg+3, column j0+gn)
+  const bool dzs = WN && a.dzs != 0;
+  const bool act = !dzs || (w % NCH) == by;   // wave-uniform: this wave computes its 16 dZ rows
 
   MD_STAMP(0);
   // ---- 0. every global load up front, all unconditional (clamped addresses: values
@@ -447,9 +457,14 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   } else {
     // wave w: rows 16w..16w+15 of dZ_i[:, blk] = dZ_{i+1} . W_{i+1}[blk, :]^T
     const int row = min(w * 16 + (lane & 15), M - 1);
+    // a wave that skips its rows (dZ split) gets a zero-length resource: its loads
+    // return zeros without a memory access and without a branch around them
+    const __amdgpu_buffer_rsrc_t dzr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(a.dZn), (short)0, act ? M * NN * 2 : 0, 0x00020000);
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks)
-      dzf[ks] = *reinterpret_cast<const bf16x8*>(a.dZn + (long)row * NN + ks * 32 + 8 * (lane >> 4));
+      dzf[ks] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                               dzr, (int)(((long)row * NN + ks * 32 + 8 * (lane >> 4)) * 2), 0, 0));
     const int row0 = min(w * 16 + (lane >> 4) * 4, M - 1);
     gv = *reinterpret_cast<const float4*>(a.G + ((long)(row0 >> 2) * N + j0 + (lane & 15)) * 4);
   }
@@ -591,7 +606,7 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       }
       __syncthreads();
     }
-    if (w * 16 < Mp) {
+    if (w * 16 < Mp && act) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       if constexpr (WN) {
 #pragma unroll
@@ -615,12 +630,51 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
         }
         const bf16_t vb = f2bf(v);
         packed[e >> 1] |= (unsigned)vb << (16 * (e & 1));
-        if (chunk0 && a.dZout && m < M) a.dZout[(long)m * N + col] = vb;
+        if ((dzs || chunk0) && a.dZout && m < M) a.dZout[(long)m * N + col] = vb;
       }
       *reinterpret_cast<uint2*>(&dzT[(lane & 15) * LDM + row0]) = make_uint2(packed[0], packed[1]);
+      if (dzs) {   // publish (write-through) for the block's other workgroups
+        const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(a.dzx + (long)bx * 16 * MPM, (short)0,
+                                                                            16 * MPM * 2, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned,
+                                                                 make_uint2(packed[0], packed[1])),
+                                              xr, ((lane & 15) * MPM + row0) * 2, 0, 16);
+      }
     }
   }
   __syncthreads();
+  if (dzs) {
+    // every wave's exchange stores have left (sc1: at the coherence point), then one
+    // arrival per workgroup; a launch adds NCH per block, so the target is the next
+    // multiple of NCH above this workgroup's own arrival ticket
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      unsigned* cnt = a.dzc + 32 * (1 + bx);
+      const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned target = (old / NCH + 1u) * NCH;
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(cnt, (short)0, 4, 0x00020000);
+      while ((int)((unsigned)__builtin_amdgcn_raw_buffer_load_b32(cr, 0, 0, 16) - target) < 0) {
+        if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > 2000000ll) {   // 20 ms: a block-mate never ran
+          atomicOr(a.dzc, 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+      }
+    }
+    __syncthreads();
+    // the whole dZ_i[:, blk]^T back into dzT (16-byte sc1 loads, past this CU's L1)
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(a.dzx + (long)bx * 16 * MPM, (short)0,
+                                                                        16 * MPM * 2, 0x00020000);
+    for (int c = tid; c < 16 * (Mp / 8); c += NT) {
+      const int n = c / (Mp / 8), r8 = (c % (Mp / 8)) * 8;
+      const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, (n * MPM + r8) * 2, 0, 16));
+      *reinterpret_cast<u32x4*>(&dzT[n * LDM + r8]) = v;
+    }
+    __syncthreads();
+  }
 
   MD_STAMP(2);
   // ---- 3. dW_i[chunk, blk] = IN[:, chunk]^T dZ_i[:, blk]; spare wave: db_i (+ head grads)
@@ -830,6 +884,21 @@ JDT_API int jdt_md_ahead_ok(int M) {
   return (512 / 16) * (784 / 112) <= cus * per ? 1 : 0;
 }
 
+// 1 if the dZ split (MdArgs::dzs) fits: its per-block arrival counter needs every
+// workgroup of the !TOP backward grids resident at once
+JDT_API int jdt_md_dzs_ok(int M) {
+  if (M <= 0 || M > MD_MPM) return 0;
+  int dev = 0, cus = 0, p1 = 0, p2 = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&p1, md_bwd_kernel<512, false, 10, 64, 512, true>, MD_NT, 0) !=
+          hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&p2, md_bwd_kernel<784, false, 10, 112, 512, true>, MD_NT, 0) !=
+          hipSuccess)
+    return 0;
+  return (512 / 16) * (512 / 64) <= cus * p1 && (512 / 16) * (784 / 112) <= cus * p2 ? 1 : 0;
+}
+
 // phase 0: forward of one hidden layer (head = 1: + head logits); phase 1: backward
 // (head = 1: TOP layer, CE through the head; head = 2: pipeline-stage boundary,
 // dZ from the next stage's dH).  Instantiated for the tutorial
@@ -839,6 +908,7 @@ JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) 
   if (a.N != 512 || a.M <= 0 || a.M > MD_MPM || (a.K != 784 && a.K != 512) || (head == 1 && a.C != 10)) return -3;
   if (phase == 0 && head == 2) return -2;
   if (a.mb_rows < 0 || (a.mb_rows && (a.mb_rows % 4 || a.M % a.mb_rows))) return -2;
+  if (a.dzs && (phase == 0 || head || !a.dzx || !a.dzc)) return -2;   // dZ split: !TOP, !BND backward only
   hipStream_t st = static_cast<hipStream_t>(stream);
   const dim3 blk(MD_NT);
   if (phase == 2) {

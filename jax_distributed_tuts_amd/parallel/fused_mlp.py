@@ -360,6 +360,10 @@ class AheadGraphs:
             # instead of at finalize() after a whole run on wrong weights
             self._checked = True
             err = int(self.eng.ztick[1].item())
+            dz = self.eng.dzs_error() if hasattr(self.eng, "dzs_error") else 0
+            if dz:
+                raise RuntimeError("md_bwd dZ split: a column-block barrier timed out on the first replay "
+                                   "(not every workgroup resident); rerun with JDT_MD_DZS=0")
             if err:
                 raise RuntimeError(f"run-ahead step failed on its first replay (error word {err}: "
                                    "1 = tile map, 2 = column barrier timeout); rerun with JDT_MLP2_AHEAD=0")
@@ -387,10 +391,12 @@ class MdArgs(ctypes.Structure):
                 ("gscale", c_float), ("running", c_void_p), ("stamps", c_void_p),
                 ("accumulate", c_int), ("dH", c_void_p), ("mb_rows", c_int), ("mb_stride", c_ulonglong),
                 ("stage_stride", ctypes.c_long), ("det_logits", c_void_p), ("step_mul", c_int),
-                ("XR", c_void_p), ("zslab", c_void_p), ("ztick", c_void_p), ("hand", c_void_p)]
+                ("XR", c_void_p), ("zslab", c_void_p), ("ztick", c_void_p), ("hand", c_void_p),
+                ("dzx", c_void_p), ("dzc", c_void_p), ("dzs", c_int)]
 
 
 _lib.declare("jdt_md_layer", c_int, [ctypes.POINTER(MdArgs), c_int, c_int, c_void_p])
+_lib.declare("jdt_md_dzs_ok", c_int, [c_int])
 _lib.declare("jdt_md_args_size", c_int, [])
 _lib.declare("jdt_md_ahead_ok", c_int, [c_int])
 
@@ -474,6 +480,14 @@ class FusedMLPDeep:
                          and bool(_lib.lib().jdt_md_ahead_ok(rows)))
         self.ahead_primed = False
         self._ahead_args = None
+        # dZ split (one GPU): the K-chunk workgroups of a column block share the dZ_i rows
+        # instead of each recomputing all of them from the whole dZ_{i+1}
+        # (csrc/mlp_deep.hip MdArgs::dzs); opt-in JDT_MD_DZS=1 until measured on the GPU
+        self.dzs_ok = (self.world == 1 and self.nh >= 2 and os.environ.get("JDT_MD_DZS", "0") == "1"
+                       and bool(_lib.lib().jdt_md_dzs_ok(rows)))
+        if self.dzs_ok:
+            self.dzx = [torch.zeros(H // 16 * 16 * 128, **bf) for _ in range(self.nh - 1)]
+            self.dzc = [torch.zeros(32 * (1 + H // 16), dtype=torch.int32, device=dev) for _ in range(self.nh - 1)]
         if self.ahead_ok:
             nch, tpx = 784 // 112, H // 16 * (784 // 112) // 8
             self.XR = torch.zeros(rows, 784, **bf)
@@ -528,6 +542,8 @@ class FusedMLPDeep:
         if not top:
             a.dZn = self.dZ[i + 1].data_ptr()
             a.Wn0, a.Wn1 = self._shadow_pair(i + 1)
+            if phase == 1 and self.dzs_ok:
+                a.dzx, a.dzc, a.dzs = self.dzx[i].data_ptr(), self.dzc[i].data_ptr(), 1
         if i >= 1:
             a.dZout = self.dZ[i].data_ptr()
         a.fuse_opt = int(self.fuse_opt)
@@ -615,8 +631,15 @@ class FusedMLPDeep:
             with named_scope("sync_metrics"):
                 K.metrics_fold_(self.metrics, P.metrics_slot)
 
+    def dzs_error(self) -> int:
+        """Nonzero if a dZ-split block barrier timed out (a block-mate never ran)."""
+        return max((int(t[0].item()) for t in self.dzc), default=0) if self.dzs_ok else 0
+
     def finalize(self):
         """Bring the generic bf16 shadows up to date (parity copies in use on odd steps)."""
+        if self.dzs_error():
+            raise RuntimeError("md_bwd dZ split: a column-block barrier timed out (not every workgroup "
+                               "resident); results invalid -- rerun with JDT_MD_DZS=0")
         if self.ahead_ok and int(self.ztick[1].item()) != 0:
             raise RuntimeError("md_bwd run-ahead: tile map or column barrier failed (error word "
                                f"{int(self.ztick[1].item())}); results invalid")

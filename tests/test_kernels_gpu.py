@@ -1289,6 +1289,37 @@ def test_set_batch_after_capture_matches_eager(strategy):
     _close(res[1][1], res[0][1], rtol=1e-4, atol=1e-2)
 
 
+@pytest.mark.parametrize("layers,rows", [(4, 128), (3, 64), (4, 32)])
+def test_deep_dz_split_bitwise(layers, rows, monkeypatch):
+    """md_bwd dZ split (MdArgs::dzs: the K-chunk workgroups of a column block each
+    compute 1/NCH of dZ_i's rows and exchange them through a per-block counter) ==
+    every workgroup computing all rows, bit for bit: deterministic mode (ordered
+    partial logits, no fp32 atomics), 3 eager steps of the deep engine; and the
+    barrier's error word stays clear."""
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    g = torch.Generator().manual_seed(5)
+    b = Batch(torch.randn(rows, 784, generator=g).to(DEV), torch.randint(0, 10, (rows,), generator=g).to(torch.int32).to(DEV))
+    monkeypatch.setenv("JDT_DETERMINISTIC", "1")
+    res = {}
+    for dzs in ("1", "0"):
+        monkeypatch.setenv("JDT_MD_DZS", dzs)
+        st = init_dp(Classifier(num_layers=layers), adamw(1e-3), 69, DEV)
+        tr = DataParallelTrainer(st, None, DPConfig(4, "kernel"))
+        for _ in range(3):
+            tr.step(b)
+        eng = tr.fused
+        assert eng.dzs_ok == (dzs == "1")
+        assert eng.dzs_error() == 0
+        tr.finalize()
+        torch.cuda.synchronize()
+        res[dzs] = (st.params.master.clone(), tr.metrics.clone())
+    assert torch.equal(res["1"][0], res["0"][0])
+    assert torch.equal(res["1"][1], res["0"][1])
+
+
 def test_fused_sgd_matches_mode0_sgd(monkeypatch):
     """Momentum-free SGD fused into mlp2_bwd's epilogue (opt_sgd, incl. the run-ahead
     graphs) == mode 0 (plain-stored grads) + the standalone SGD kernel.  SGD moves

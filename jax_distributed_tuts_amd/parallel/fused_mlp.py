@@ -482,8 +482,9 @@ class FusedMLPDeep:
         self._ahead_args = None
         # dZ split (one GPU): the K-chunk workgroups of a column block share the dZ_i rows
         # instead of each recomputing all of them from the whole dZ_{i+1}
-        # (csrc/mlp_deep.hip MdArgs::dzs); opt-in JDT_MD_DZS=1 until measured on the GPU
-        self.dzs_ok = (self.world == 1 and self.nh >= 2 and os.environ.get("JDT_MD_DZS", "0") == "1"
+        # (csrc/mlp_deep.hip MdArgs::dzs); JDT_MD_DZS=0 turns it off (A/B: +3 % on the 3- / 4-layer and
+        # 8-layer GPipe steps, profiles/r3_dz_split_ab.txt)
+        self.dzs_ok = (self.world == 1 and self.nh >= 2 and os.environ.get("JDT_MD_DZS", "1") == "1"
                        and bool(_lib.lib().jdt_md_dzs_ok(rows)))
         if self.dzs_ok:
             self.dzx = [torch.zeros(H // 16 * 16 * 128, **bf) for _ in range(self.nh - 1)]

@@ -198,7 +198,9 @@ def main():
                     help="--strategy pp with a single stage: run the microbatches as one pass (PipeConfig.merge_single_stage)")
     ap.add_argument("--microbatch-passes", action="store_true",
                     help="--strategy pp --model transformer with a single stage: one forward/backward pass per "
-                         "microbatch, as a stage of a real multi-stage pipeline runs (default: layer-major)")
+                         "microbatch, as a stage of a real multi-stage pipeline runs (on one GPU the LM's "
+                         "microbatch passes already run by default, on concurrent streams: JDT_MB_STREAMS; "
+                         "this flag only matters with JDT_MB_STREAMS=1, where the default is layer-major)")
     ap.add_argument("--hidden-layers", type=int, default=8)
     ap.add_argument("--lm-batch", type=int, default=16)
     ap.add_argument("--num-layers", type=int, default=2)

@@ -15,6 +15,8 @@ block range, ``has_embed``/``has_head`` mark the first/last stage.
 """
 from __future__ import annotations
 
+import contextlib
+
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -198,7 +200,7 @@ class TransformerLM:
 
     # ------------------------------------------------------------------ backward
     def backward(self, P: FlatParams, cache: _Cache, dout: torch.Tensor, *, dout_is_dz: bool = True,
-                 need_dx: bool = False, on_ready=None, wgrad=None, opt=None) -> Optional[torch.Tensor]:
+                 need_dx: bool = False, on_ready=None, wgrad=None, opt=None, after=None) -> Optional[torch.Tensor]:
         """``wgrad`` (ops.kernels.WGradStream): run the weight-gradient GEMMs on its
         side stream; the caller joins it before reading the grads.  ``opt``
         (ops.kernels.EpilogueAdamW): this pass carries the weights' final gradients of
@@ -214,6 +216,7 @@ class TransformerLM:
             assert opt is None and on_ready is None, "deferred weight gradients: optimizer runs in weight_grads"
         R = (lambda l, k: ar.rows(ar.blocks[l][k], cache.mb, cache.n_mb)) if ar is not None else (lambda l, k: None)  # noqa: E731
         ready = on_ready if on_ready is not None else (lambda names: None)
+        after = after if after is not None else (lambda part: None)   # part's deferred dW inputs complete
         layers = list(self.layers)
 
         def dw_dx(name, dw, dx):
@@ -230,6 +233,7 @@ class TransformerLM:
             dhf = dw_dx("head/kernel",
                         lambda: K.dw_gemm(wgrad, cache.hf, dout, P.g("head/kernel"), opt=opt, name="head/kernel"),
                         lambda: K.gemm(dout, P.s("head/kernel"), b_layout="nk"))
+            after("head")   # after the dX GEMM: an epilogue AdamW rewrites the shadow it reads
             dx = K.layernorm_bwd(dhf, cache.xf, cache.mf, cache.rf, P.p("ln_f/scale"), P.g("ln_f/scale"),
                                  P.g("ln_f/bias"), dsum=fc2_bias(layers[-1]) if layers else None,
                                  dx_out=R(layers[-1], "dx3") if layers else None)
@@ -268,6 +272,7 @@ class TransformerLM:
                                  P.g(f"{b}/ln1/bias"), dres=dx2, dsum=below,
                                  dx_out=R(layers[idx - 1], "dx3") if idx > 0 else None)
             fc2_done = below is not None
+            after(l)
             ready([s.name for s in self.param_specs() if s.name.startswith(b + "/")])
         if self.has_embed:
             K.embed_bwd(dx, cache.inp, P.g("embed/wte"), P.g("embed/wpe"), c.seq_len)
@@ -275,10 +280,12 @@ class TransformerLM:
             return None
         return dx if need_dx else None
 
-    def weight_grads(self, P: FlatParams, arena: WGradArena, *, wgrad=None, opt=None):
+    def weight_grads(self, P: FlatParams, arena: WGradArena, *, wgrad=None, opt=None, on=None):
         """The deferred weight gradients of every microbatch in one GEMM per weight:
         dW (+)= A^T . dZ over all T = n_mb * mb rows of ``arena`` (``opt``: AdamW in the
-        epilogue, each weight's single gradient contribution of the step)."""
+        epilogue, each weight's single gradient contribution of the step).  ``on(j)``:
+        context for GEMM j (parallel.pipeline._MbStreams: the GEMMs touch disjoint
+        weights and only read the step counter, so they may run on several streams)."""
         if opt is not None:
             opt.only_contribution = True
         order = []
@@ -288,8 +295,27 @@ class TransformerLM:
             a, b = arena.blocks[l], f"block_{l}"
             order += [(f"{b}/mlp/fc2/kernel", a["u"], a["dx3"]), (f"{b}/mlp/fc1/kernel", a["h2"], a["dz1"]),
                       (f"{b}/attn/out/kernel", a["o"], a["dx2"]), (f"{b}/attn/qkv/kernel", a["h1"], a["dqkv"])]
-        for name, h, dz in order:
-            K.dw_gemm(wgrad, h, dz, P.g(name), opt=opt, name=name)
+        for j, (name, h, dz) in enumerate(order):
+            with (on(j) if on is not None else contextlib.nullcontext()):
+                K.dw_gemm(wgrad, h, dz, P.g(name), opt=opt, name=name)
+
+    def weight_grads_of(self, P: FlatParams, arena: WGradArena, part, *, opt=None, on=None, j0: int = 0) -> int:
+        """The deferred weight-gradient GEMMs of one ``part`` ("head" or a layer index),
+        as soon as the backward chain has produced that part's output gradients (the
+        ``after`` hook of ``backward``); GEMM j runs under ``on(j0 + j)``.  Returns the
+        next j0."""
+        if opt is not None:
+            opt.only_contribution = True
+        if part == "head":
+            order = [("head/kernel", arena.head["hf"], arena.head["dlog"])]
+        else:
+            a, b = arena.blocks[part], f"block_{part}"
+            order = [(f"{b}/mlp/fc2/kernel", a["u"], a["dx3"]), (f"{b}/mlp/fc1/kernel", a["h2"], a["dz1"]),
+                     (f"{b}/attn/out/kernel", a["o"], a["dx2"]), (f"{b}/attn/qkv/kernel", a["h1"], a["dqkv"])]
+        for j, (name, h, dz) in enumerate(order):
+            with (on(j0 + j) if on is not None else contextlib.nullcontext()):
+                K.dw_gemm(None, h, dz, P.g(name), opt=opt, name=name)
+        return j0 + len(order)
 
 
 def _into(dst: Optional[torch.Tensor], src: torch.Tensor) -> torch.Tensor:

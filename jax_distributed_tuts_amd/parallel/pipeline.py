@@ -23,6 +23,7 @@ bucket (grads + metric slots) per stage; the optimizer is the same fused AdamW.
 from __future__ import annotations
 
 import math
+import contextlib
 import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
@@ -112,7 +113,10 @@ class PipeConfig:
     # the fused MLP kernels keep per-microbatch streams (_single_stage_engine); a model
     # without dropout (the transformer LM) has no masks to keep, so its merged pass IS
     # the loop's gradient (each row keeps its microbatch's 1/mb loss weight).  False:
-    # per-microbatch passes, as on a real multi-stage pipeline.
+    # per-microbatch passes, as on a real multi-stage pipeline.  A model whose
+    # per-microbatch passes run on concurrent streams (mb_streams > 1, below) takes
+    # those instead: the LM step measured 1.07 vs 1.17 ms layer-major on one MI355X
+    # (profiles/r3_lm_mb_streams_ab.txt).
     layer_major_single_stage: bool = True
     # one GPU, one stage, AdamW: apply the optimizer layer by layer on a side stream
     # as the backward finishes each layer's gradients (ops.kernels.OverlappedAdamW).
@@ -127,6 +131,18 @@ class PipeConfig:
     # launches, and the gradient an upstream stage waits for is sent sooner.
     # JDT_DEFER_WGRAD=0 turns it off (A/B).
     defer_wgrad: bool = field(default_factory=lambda: os.environ.get("JDT_DEFER_WGRAD", "1") != "0")
+    # one stage, per-microbatch passes with deferred weight gradients (GPU): microbatch i
+    # runs its forward and input-gradient chain on stream i % mb_streams.  With the
+    # weight gradients deferred the chains share no buffer (every cross-microbatch
+    # accumulation -- bias / LayerNorm / embedding grads, metrics -- is an fp32 atomic,
+    # split-K slabs are per stream), and a 512-row microbatch GEMM fills half the CUs.
+    mb_streams: int = field(default_factory=lambda: int(os.environ.get("JDT_MB_STREAMS", "4")))
+    # one stage, layer-major (one pass over all rows), GPU: weight gradients deferred and
+    # issued per part on this many streams, overlapping the input-gradient chain
+    # (GPipeTrainer._layer_major_wpass); 1 = the weight GEMMs inline in the backward.
+    # Opt-in: measured SLOWER (1.21-1.28 vs 1.17 ms: the side-stream GEMMs take CUs from
+    # the chain they were meant to hide behind)
+    wpass_streams: int = field(default_factory=lambda: int(os.environ.get("JDT_LM_WSTREAMS", "1")))
 
 
 def _no_dropout(model) -> bool:
@@ -135,6 +151,27 @@ def _no_dropout(model) -> bool:
     if rate is None:
         rate = getattr(getattr(model, "cfg", None), "dropout_rate", 1.0)
     return float(rate) == 0.0
+
+
+class _MbStreams:
+    """``with on(i)``: run work item i on stream i % k (item 0, k, 2k, ... on the main
+    stream); ``fork``: the side streams wait for the main stream's work so far;
+    ``join``: the main stream waits for the side streams.  ``main=None``: one stream."""
+
+    def __init__(self, main, side):
+        self.main, self.side = main, side or []
+
+    def fork(self):
+        for s in self.side:
+            s.wait_stream(self.main)
+
+    def join(self):
+        for s in self.side:
+            self.main.wait_stream(s)
+
+    def __call__(self, i: int):
+        k = len(self.side) + 1
+        return torch.cuda.stream(self.side[i % k - 1]) if (self.side and i % k) else contextlib.nullcontext()
 
 
 class GPipeTrainer:
@@ -167,6 +204,7 @@ class GPipeTrainer:
         self.xg = None
         self._xg_fused_opt = False
         self.wgrad = K.WGradStream(self.dev) if (self.dev.type == "cuda" and cfg.overlap_wgrad) else None
+        self._mb_streams = None
         self.stage_engine = None
         self._engine_tried = False
         self.deep_engine = None
@@ -249,7 +287,10 @@ class GPipeTrainer:
                 deep.forward_backward(batch)
                 return
         eo = self._epilogue_opt()
-        if self.S == 1 and (cfg.merge_single_stage or (cfg.layer_major_single_stage and _no_dropout(self.model))):
+        if self.S == 1 and (cfg.merge_single_stage or (cfg.layer_major_single_stage and _no_dropout(self.model)
+                                                       and self._mb_streams_k() <= 1)):
+            if self._layer_major_wpass(batch, P, st, seed, eo, n_mb):
+                return
             out, cache = self.model.forward(P, batch.inputs, train=True, seed=seed, offset=0, step=st.step_tensor)
             d = torch.empty_like(out)
             self.loss_head(out, batch.labels, d, n_parts=n_mb)
@@ -266,25 +307,15 @@ class GPipeTrainer:
         caches, dlogits = [None] * n_mb, [None] * n_mb
         arena = self._wgrad_arena(batch.size)
         akw = {"arena": arena, "n_mb": n_mb} if arena is not None else {}
+        on = self._mb_stream_ctx(arena, n_mb)
+        on.fork()   # after the previous step's optimizer / this step's inputs
         # ---- forward fill/drain: tick t, stage s handles microbatch t - s
         for t in range(n_mb + self.S - 1):
             i = t - self.s
             if not (0 <= i < n_mb):
                 continue
-            if self.first:
-                x = batch.inputs[i * mb:(i + 1) * mb]
-            else:
-                x = self._recv(self.model.input_shape(mb), self.act_dtype, self.s - 1, i)
-            if arena is not None:
-                akw["mb"] = i
-            out, cache = self.model.forward(P, x, train=True, seed=seed, offset=i << 16, step=st.step_tensor, **akw)
-            caches[i] = cache
-            if self.last:
-                d = torch.empty_like(out) if arena is None else arena.rows(arena.head["dlog"], i, n_mb)
-                self.loss_head(out, batch.labels[i * mb:(i + 1) * mb], d)
-                dlogits[i] = d
-            else:
-                self._send(out, self.s + 1, i)
+            with on(i):
+                self._forward_mb(batch, P, st, seed, caches, dlogits, arena, akw, i, mb)
         # ---- backward, reverse microbatch order (the last one, i = 0, carries the
         # weights' final gradients: the in-epilogue optimizer when enabled)
         if eo is not None:
@@ -292,20 +323,81 @@ class GPipeTrainer:
         top = list(getattr(self.model, "layers", []))[-1:] if arena is not None else []
         for i in reversed(range(n_mb)):
             oi = eo if (i == 0 and arena is None) else None
-            if self.last:
-                dx = self.model.backward(P, caches[i], dlogits[i], dout_is_dz=True, need_dx=not self.first,
-                                         wgrad=self.wgrad, opt=oi)
-            else:
-                into = arena.rows(arena.blocks[top[0]]["dx3"], i, n_mb) if top else None
-                dh = self._recv(self.model.output_shape(mb), self.act_dtype, self.s + 1, n_mb + i, out=into)
-                dx = self.model.backward(P, caches[i], dh, dout_is_dz=False, need_dx=not self.first,
-                                         wgrad=self.wgrad, opt=oi)
-            if not self.first:
-                self._send(dx, self.s - 1, n_mb + i)
-            caches[i] = None
+            with on(i):
+                if self.last:
+                    dx = self.model.backward(P, caches[i], dlogits[i], dout_is_dz=True, need_dx=not self.first,
+                                             wgrad=self.wgrad, opt=oi)
+                else:
+                    into = arena.rows(arena.blocks[top[0]]["dx3"], i, n_mb) if top else None
+                    dh = self._recv(self.model.output_shape(mb), self.act_dtype, self.s + 1, n_mb + i, out=into)
+                    dx = self.model.backward(P, caches[i], dh, dout_is_dz=False, need_dx=not self.first,
+                                             wgrad=self.wgrad, opt=oi)
+                if not self.first:
+                    self._send(dx, self.s - 1, n_mb + i)
+                caches[i] = None
         if arena is not None:
-            # the W pass: every weight gradient of the step, one GEMM per weight over all rows
-            self.model.weight_grads(P, arena, wgrad=self.wgrad, opt=eo)
+            # the W pass: every weight gradient of the step, one GEMM per weight over all
+            # rows (the GEMMs round-robin over the streams once every chain has finished)
+            on.join()
+            on.fork()
+            self.model.weight_grads(P, arena, wgrad=self.wgrad, opt=eo, on=on)
+        on.join()
+
+    def _layer_major_wpass(self, batch, P, st, seed, eo, n_mb) -> bool:
+        """One stage, one pass over all rows, weight gradients deferred (cfg.wpass_streams
+        = k > 1, GPU): the backward runs the input-gradient chain only and each part's
+        weight-gradient GEMMs (AdamW in their epilogues) go out round-robin on k - 1 side
+        streams as soon as the chain has produced that part's output gradients
+        (TransformerLM.backward ``after`` hook), overlapping the rest of the chain."""
+        k = int(self.cfg.wpass_streams)
+        if k <= 1 or self.dev.type != "cuda" or not hasattr(self.model, "weight_grads_of"):
+            return False
+        arena = self._wgrad_arena(batch.size)
+        if arena is None:
+            return False
+        if self._mb_streams is None or len(self._mb_streams) != k - 1:
+            self._mb_streams = [torch.cuda.Stream(self.dev) for _ in range(k - 1)]
+        on = _MbStreams(torch.cuda.current_stream(self.dev), self._mb_streams)
+        out, cache = self.model.forward(P, batch.inputs, train=True, seed=seed, offset=0, step=st.step_tensor,
+                                        arena=arena, mb=0, n_mb=1)
+        d = arena.head["dlog"] if self.model.has_head else torch.empty_like(out)
+        self.loss_head(out, batch.labels, d, n_parts=n_mb)
+        j = [0]
+
+        def after(part):
+            on.fork()   # the side streams see the chain so far
+            j[0] = self.model.weight_grads_of(P, arena, part, opt=eo, on=lambda i: on(1 + i % (k - 1)), j0=j[0])
+
+        self.model.backward(P, cache, d, dout_is_dz=True, need_dx=False, after=after)
+        on.join()
+        return True
+
+    def _mb_stream_ctx(self, arena, n_mb: int) -> "_MbStreams":
+        """Microbatch i's passes (and the W pass's GEMM j) run on stream i % k when
+        ``cfg.mb_streams`` = k > 1 applies: GPU, one stage, deferred weight gradients."""
+        k = self._mb_streams_k()
+        if not (k > 1 and arena is not None):
+            return _MbStreams(None, None)
+        if self._mb_streams is None or len(self._mb_streams) != k - 1:
+            self._mb_streams = [torch.cuda.Stream(self.dev) for _ in range(k - 1)]
+        return _MbStreams(torch.cuda.current_stream(self.dev), self._mb_streams)
+
+    def _forward_mb(self, batch, P, st, seed, caches, dlogits, arena, akw, i, mb):
+        n_mb = self.cfg.num_microbatches
+        if self.first:
+            x = batch.inputs[i * mb:(i + 1) * mb]
+        else:
+            x = self._recv(self.model.input_shape(mb), self.act_dtype, self.s - 1, i)
+        if arena is not None:
+            akw["mb"] = i
+        out, cache = self.model.forward(P, x, train=True, seed=seed, offset=i << 16, step=st.step_tensor, **akw)
+        caches[i] = cache
+        if self.last:
+            d = torch.empty_like(out) if arena is None else arena.rows(arena.head["dlog"], i, n_mb)
+            self.loss_head(out, batch.labels[i * mb:(i + 1) * mb], d)
+            dlogits[i] = d
+        else:
+            self._send(out, self.s + 1, i)
 
     def _wgrad_arena(self, rows: int):
         """The stage model's deferred weight-gradient buffers (models.transformer.WGradArena)
@@ -328,9 +420,17 @@ class GPipeTrainer:
             return "pipeline"
         if self.cfg.merge_single_stage:
             return "merged"
-        if self.cfg.layer_major_single_stage and (self.deep_engine is not None or _no_dropout(self.model)):
+        k = self._mb_streams_k()
+        if self.cfg.layer_major_single_stage and (self.deep_engine is not None or _no_dropout(self.model)) and k <= 1:
             return "layer-major"
-        return "microbatch-loop"
+        return f"microbatch-loop ({k} streams)" if k > 1 else "microbatch-loop"
+
+    def _mb_streams_k(self) -> int:
+        """Streams the per-microbatch passes of a one-stage pipeline run on (1: serial)."""
+        k = min(int(self.cfg.mb_streams), self.cfg.num_microbatches)
+        ok = (self.S == 1 and self.dev.type == "cuda" and self.cfg.defer_wgrad and hasattr(self.model, "weight_grads")
+              and not self.cfg.merge_single_stage)
+        return k if ok else 1
 
     def invalidate(self):
         """After a checkpoint restore: drop captured graphs and the stage engine."""

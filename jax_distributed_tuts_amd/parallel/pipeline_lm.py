@@ -20,11 +20,16 @@ def lm_batch(cfg: TransformerConfig, global_batch: int = 16, seed: int = 1) -> B
 
 def build_lm_pipeline(mesh: Mesh, dev, cfg: TransformerConfig = TransformerConfig(), num_microbatches: int = 4,
                       lr: float = 3e-4, seed: int = 0, comm: str = "auto", merge_single_stage: bool = False,
-                      layer_major_single_stage: bool = True, tx=None):
+                      layer_major_single_stage: bool = True, tx=None, mb_streams=None, wpass_streams=None):
     S, s = (mesh.axis_size("pipe"), mesh.axis_index("pipe")) if mesh is not None else (1, 0)
     stage = lm_stage(cfg, S, s)
     full = TransformerLM(cfg)
     P = init_stage_params(stage, full.param_specs(), seed, dev)
     st = TrainState.create(apply_fn=stage, params=P, tx=tx if tx is not None else adamw(lr), rng=R.PRNGKey(seed))
-    return GPipeTrainer(st, mesh, PipeConfig(num_microbatches, comm=comm, merge_single_stage=merge_single_stage,
-                                               layer_major_single_stage=layer_major_single_stage)), cfg
+    pc = PipeConfig(num_microbatches, comm=comm, merge_single_stage=merge_single_stage,
+                    layer_major_single_stage=layer_major_single_stage)
+    if mb_streams is not None:
+        pc.mb_streams = int(mb_streams)
+    if wpass_streams is not None:
+        pc.wpass_streams = int(wpass_streams)
+    return GPipeTrainer(st, mesh, pc), cfg

@@ -1057,6 +1057,7 @@ def test_overlapped_adamw_equals_single_launch(graph, monkeypatch):
     for ov in ("0", "1", "0b"):
         monkeypatch.setenv("JDT_OVERLAP_OPT", ov[0])
         monkeypatch.setenv("JDT_LM_FUSED_OPT", "0")  # the in-epilogue AdamW would take precedence
+        monkeypatch.setenv("JDT_MB_STREAMS", "1")    # layer-major (concurrent microbatch passes otherwise)
         tr, lcfg = build_lm_pipeline(mesh, DEV, num_microbatches=4)
         b = lm_batch(lcfg, global_batch=8, seed=1)
         b = Batch(b.inputs.to(DEV), b.labels.to(DEV))

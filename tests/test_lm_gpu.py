@@ -18,11 +18,12 @@ DEV = torch.device("cuda", 0)
 CFG = TransformerConfig()   # the bench model
 
 
-def _trainer(tx, layer_major=True, fused_opt="1"):
+def _trainer(tx, layer_major=True, fused_opt="1", wpass=None):
     old = os.environ.get("JDT_LM_FUSED_OPT")
     os.environ["JDT_LM_FUSED_OPT"] = fused_opt
     try:
-        tr, _ = build_lm_pipeline(None, DEV, CFG, num_microbatches=4, tx=tx, layer_major_single_stage=layer_major)
+        tr, _ = build_lm_pipeline(None, DEV, CFG, num_microbatches=4, tx=tx, layer_major_single_stage=layer_major,
+                                  mb_streams=1 if layer_major else None, wpass_streams=wpass)
         b = lm_batch(CFG, global_batch=16, seed=1)
         b = Batch(b.inputs.to(DEV), b.labels.to(DEV))
         tr.step(b)   # builds the epilogue optimizer (env read here)
@@ -34,12 +35,17 @@ def _trainer(tx, layer_major=True, fused_opt="1"):
     return tr, b
 
 
-@pytest.mark.parametrize("layer_major", [True, False])
-def test_lm_bench_config_grads_match_fp64_autograd(layer_major):
+@pytest.mark.parametrize("layer_major,streams", [(True, 1), (True, 3), (False, 1), (False, 2), (False, 4)])
+def test_lm_bench_config_grads_match_fp64_autograd(layer_major, streams):
     """One plain-SGD (lr 1) step: p_before - p_after is the applied gradient (mean CE
     over all 2048 tokens); every one of the 54 leaves within the pinned oracle
-    tolerance (bf16 operands)."""
-    tr0, _ = build_lm_pipeline(None, DEV, CFG, num_microbatches=4, tx=sgd(1.0), layer_major_single_stage=layer_major)
+    tolerance (bf16 operands).  Per-microbatch passes: microbatch i on stream
+    i % streams; layer-major: the deferred weight-gradient GEMMs on streams - 1 side
+    streams, overlapping the input-gradient chain."""
+    tr0, _ = build_lm_pipeline(None, DEV, CFG, num_microbatches=4, tx=sgd(1.0), layer_major_single_stage=layer_major,
+                               mb_streams=1 if layer_major else streams, wpass_streams=streams)
+    assert tr0.single_stage_mode == ("layer-major" if layer_major else
+                                     f"microbatch-loop ({streams} streams)" if streams > 1 else "microbatch-loop")
     before = {k: v.detach().clone() for k, v in tr0.state.params.state_dict().items()}
     bb = lm_batch(CFG, global_batch=16, seed=1)
     tr0.step(Batch(bb.inputs.to(DEV), bb.labels.to(DEV)))
@@ -51,11 +57,11 @@ def test_lm_bench_config_grads_match_fp64_autograd(layer_major):
     for k in sorted(want):
         rel, scale = check_grad(got[k].cpu(), want[k].cpu(), k, rel_tol=0.025, scale_tol=0.004)  # measured max 0.0126 / 0.0015
         worst = max(worst, rel)
-    print(f"[lm bench grads, layer_major={layer_major}] worst rel err {worst:.3e}")
+    print(f"[lm bench grads, layer_major={layer_major}, streams={streams}] worst rel err {worst:.3e}")
 
 
-@pytest.mark.parametrize("layer_major", [True, False])
-def test_lm_epilogue_adamw_matches_plain_adamw(layer_major):
+@pytest.mark.parametrize("layer_major,wpass", [(True, 1), (True, 3), (False, None)])
+def test_lm_epilogue_adamw_matches_plain_adamw(layer_major, wpass):
     """AdamW fused into the weight-gradient GEMM epilogues (+ one multi-range launch for
     the rest) == the plain full-buffer AdamW pass, after 3 steps; the step counter
     advances once per step.  The step is not bitwise reproducible (fp32 atomics in the
@@ -68,7 +74,7 @@ def test_lm_epilogue_adamw_matches_plain_adamw(layer_major):
     lr = 3e-4
     res = {}
     for fused in ("1", "0", "0b"):
-        tr, b = _trainer(adamw(lr), layer_major, fused[0])
+        tr, b = _trainer(adamw(lr), layer_major, fused[0], wpass)
         assert (getattr(tr, "_eo", None) not in (None, False)) == (fused == "1")
         tr.step(b)
         tr.step(b)
@@ -91,3 +97,30 @@ def test_lm_epilogue_adamw_matches_plain_adamw(layer_major):
         noise = float(((nb - c).abs() > 0.5 * lr).float().mean())
         print(f"{n:28s} apart {frac:.2e} (noise {noise:.2e})")
         assert frac <= 0.02 + 4 * noise, (n, frac, noise)
+
+
+def test_lm_microbatch_streams_captured_matches_eager():
+    """Per-microbatch passes on 1 stream (eager) vs 2 streams (eager and hipGraph-captured,
+    the fork / join recorded in the graph): 3 SGD steps move the parameters by the same
+    amount up to the fp32-atomic reduction-order noise."""
+    res = {}
+    for streams, cap in ((1, False), (2, False), (2, True)):
+        tr, _ = build_lm_pipeline(None, DEV, CFG, num_microbatches=4, tx=sgd(0.5), layer_major_single_stage=False,
+                                  mb_streams=streams)
+        bb = lm_batch(CFG, global_batch=16, seed=1)
+        b = Batch(bb.inputs.to(DEV), bb.labels.to(DEV))
+        p0 = tr.state.params.master.clone()
+        if cap:
+            tr.capture(b)
+            tr.run_steps(b, 3)
+        else:
+            for _ in range(3):
+                tr.step(b)
+        torch.cuda.synchronize()
+        res[(streams, cap)] = tr.state.params.master - p0
+        assert int(tr.state.step) == 3
+    ref = res[(1, False)]
+    for key in ((2, False), (2, True)):
+        rel = float((res[key] - ref).norm() / ref.norm())
+        print(f"[lm mb streams] {key}: update rel diff {rel:.2e}")
+        assert rel < 0.02, (key, rel)

@@ -143,6 +143,9 @@ class PipeConfig:
     # Opt-in: measured SLOWER (1.21-1.28 vs 1.17 ms: the side-stream GEMMs take CUs from
     # the chain they were meant to hide behind)
     wpass_streams: int = field(default_factory=lambda: int(os.environ.get("JDT_LM_WSTREAMS", "1")))
+    # concurrent microbatch passes: > 0 runs the W pass on this many dedicated streams,
+    # each part's GEMMs as soon as every chain has passed it (0: after the join)
+    wpass_early: int = field(default_factory=lambda: int(os.environ.get("JDT_WPASS_EARLY", "0")))
 
 
 def _no_dropout(model) -> bool:
@@ -205,6 +208,7 @@ class GPipeTrainer:
         self._xg_fused_opt = False
         self.wgrad = K.WGradStream(self.dev) if (self.dev.type == "cuda" and cfg.overlap_wgrad) else None
         self._mb_streams = None
+        self._w_streams = None
         self.stage_engine = None
         self._engine_tried = False
         self.deep_engine = None
@@ -321,20 +325,45 @@ class GPipeTrainer:
         if eo is not None:
             eo.only_contribution = n_mb == 1
         top = list(getattr(self.model, "layers", []))[-1:] if arena is not None else []
+        # early W pass (on dedicated streams): each part's weight-gradient GEMMs start once
+        # every microbatch chain has passed that part (per-chain events), not after the join
+        nw = int(self.cfg.wpass_early) if (on.side and hasattr(self.model, "weight_grads_of")) else 0
+        evs: dict = {}
+
+        def mark(part):
+            ev = torch.cuda.Event()
+            ev.record()
+            evs.setdefault(part, []).append(ev)
+
+        bkw = {"after": mark} if nw else {}
         for i in reversed(range(n_mb)):
             oi = eo if (i == 0 and arena is None) else None
             with on(i):
                 if self.last:
                     dx = self.model.backward(P, caches[i], dlogits[i], dout_is_dz=True, need_dx=not self.first,
-                                             wgrad=self.wgrad, opt=oi)
+                                             wgrad=self.wgrad, opt=oi, **bkw)
                 else:
                     into = arena.rows(arena.blocks[top[0]]["dx3"], i, n_mb) if top else None
                     dh = self._recv(self.model.output_shape(mb), self.act_dtype, self.s + 1, n_mb + i, out=into)
                     dx = self.model.backward(P, caches[i], dh, dout_is_dz=False, need_dx=not self.first,
-                                             wgrad=self.wgrad, opt=oi)
+                                             wgrad=self.wgrad, opt=oi, **bkw)
                 if not self.first:
                     self._send(dx, self.s - 1, n_mb + i)
                 caches[i] = None
+        if nw:
+            if self._w_streams is None or len(self._w_streams) != nw:
+                self._w_streams = [torch.cuda.Stream(self.dev) for _ in range(nw)]
+            ws, j = self._w_streams, 0
+            for part in (["head"] if self.model.has_head else []) + list(reversed(list(self.model.layers))):
+                for w in ws:
+                    for ev in evs[part]:
+                        w.wait_event(ev)
+                j = self.model.weight_grads_of(P, arena, part, opt=eo, on=lambda g: torch.cuda.stream(ws[g % nw]),
+                                               j0=j)
+            for w in ws:
+                on.main.wait_stream(w)
+            on.join()
+            return
         if arena is not None:
             # the W pass: every weight gradient of the step, one GEMM per weight over all
             # rows (the GEMMs round-robin over the streams once every chain has finished)

@@ -35,8 +35,9 @@ def _trainer(tx, layer_major=True, fused_opt="1", wpass=None):
     return tr, b
 
 
-@pytest.mark.parametrize("layer_major,streams", [(True, 1), (True, 3), (False, 1), (False, 2), (False, 4)])
-def test_lm_bench_config_grads_match_fp64_autograd(layer_major, streams):
+@pytest.mark.parametrize("layer_major,streams,early", [(True, 1, 0), (True, 3, 0), (False, 1, 0), (False, 2, 0),
+                                                      (False, 4, 0), (False, 4, 2)])
+def test_lm_bench_config_grads_match_fp64_autograd(layer_major, streams, early):
     """One plain-SGD (lr 1) step: p_before - p_after is the applied gradient (mean CE
     over all 2048 tokens); every one of the 54 leaves within the pinned oracle
     tolerance (bf16 operands).  Per-microbatch passes: microbatch i on stream
@@ -46,6 +47,7 @@ def test_lm_bench_config_grads_match_fp64_autograd(layer_major, streams):
                                mb_streams=1 if layer_major else streams, wpass_streams=streams)
     assert tr0.single_stage_mode == ("layer-major" if layer_major else
                                      f"microbatch-loop ({streams} streams)" if streams > 1 else "microbatch-loop")
+    tr0.cfg.wpass_early = early   # > 0: the W pass on its own streams, per part as the chains pass it
     before = {k: v.detach().clone() for k, v in tr0.state.params.state_dict().items()}
     bb = lm_batch(CFG, global_batch=16, seed=1)
     tr0.step(Batch(bb.inputs.to(DEV), bb.labels.to(DEV)))
@@ -57,7 +59,7 @@ def test_lm_bench_config_grads_match_fp64_autograd(layer_major, streams):
     for k in sorted(want):
         rel, scale = check_grad(got[k].cpu(), want[k].cpu(), k, rel_tol=0.025, scale_tol=0.004)  # measured max 0.0126 / 0.0015
         worst = max(worst, rel)
-    print(f"[lm bench grads, layer_major={layer_major}, streams={streams}] worst rel err {worst:.3e}")
+    print(f"[lm bench grads, layer_major={layer_major}, streams={streams}, early={early}] worst rel err {worst:.3e}")
 
 
 @pytest.mark.parametrize("layer_major,wpass", [(True, 1), (True, 3), (False, None)])
@@ -104,9 +106,10 @@ def test_lm_microbatch_streams_captured_matches_eager():
     the fork / join recorded in the graph): 3 SGD steps move the parameters by the same
     amount up to the fp32-atomic reduction-order noise."""
     res = {}
-    for streams, cap in ((1, False), (2, False), (2, True)):
+    for streams, cap in ((1, False), (2, False), (2, True), (4, True)):
         tr, _ = build_lm_pipeline(None, DEV, CFG, num_microbatches=4, tx=sgd(0.5), layer_major_single_stage=False,
                                   mb_streams=streams)
+        tr.cfg.wpass_early = 2 if streams == 4 else 0
         bb = lm_batch(CFG, global_batch=16, seed=1)
         b = Batch(bb.inputs.to(DEV), bb.labels.to(DEV))
         p0 = tr.state.params.master.clone()
@@ -120,7 +123,7 @@ def test_lm_microbatch_streams_captured_matches_eager():
         res[(streams, cap)] = tr.state.params.master - p0
         assert int(tr.state.step) == 3
     ref = res[(1, False)]
-    for key in ((2, False), (2, True)):
+    for key in ((2, False), (2, True), (4, True)):
         rel = float((res[key] - ref).norm() / ref.norm())
         print(f"[lm mb streams] {key}: update rel diff {rel:.2e}")
         assert rel < 0.02, (key, rel)

@@ -289,6 +289,8 @@ def main():
     sps = args.steps / dt
     if args.strategy == "dp":
         desc["accum"] = tr.cfg.accum  # the path that actually ran (CPU falls back from "kernel")
+        if getattr(tr, "_loop_engine", None) is not None:
+            desc["loop_streams"] = tr._loop_engine.n_sets   # minibatch loop on concurrent streams
         # 1-GPU fused step: one run-ahead launch per step (step t's backward + AdamW + step
         # t+1's forward) or the two-launch forward / backward pair
         eng = getattr(tr, "fused", None)

@@ -22,6 +22,7 @@ dropout streams are indexed differently) -- 4x fewer launches.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from dataclasses import dataclass, field
 from typing import Optional
@@ -76,6 +77,12 @@ class DPConfig:
     # per-minibatch passes and dropout streams as the generic loop, 2 launches per
     # minibatch (env JDT_FUSED_LOOP=0: generic GEMM chain)
     fused_loop: bool = field(default_factory=lambda: os.environ.get("JDT_FUSED_LOOP", "1") == "1")
+    # ... with minibatch i on stream i % loop_streams (its own grad set, merged after the
+    # join: parallel.fused_stage.FusedMLPStage n_sets).  0 = auto: 2 for models of >= 3
+    # layers (4-layer loop 6.4k -> 7.6-7.9k steps/s), 1 for the 2-layer classifier (no
+    # gain: its per-minibatch kernels already cover the chip), never 4 (the merge of 3
+    # private sets costs more than it wins) -- profiles/r3_dp_loop_streams_ab.txt
+    loop_streams: int = field(default_factory=lambda: int(os.environ.get("JDT_LOOP_STREAMS", "0")))
 
 
 class DataParallelTrainer:
@@ -98,6 +105,7 @@ class DataParallelTrainer:
         self._scan = None
         self._loop_engine = None
         self._loop_tried = False
+        self._loop_streams = None
         self.xg = None
         self._xg_fused_opt = False
         if self.world > 1 and P.grad.is_cuda:
@@ -177,9 +185,22 @@ class DataParallelTrainer:
         if loop_eng is not None:
             # the reference's minibatch loop (util.py:41-78) on the fused per-layer
             # kernels: fwd + CE/bwd per minibatch, grads accumulated into P.grad
+            k = loop_eng.n_sets
+            main = torch.cuda.current_stream(P.master.device) if k > 1 else None
+            if k > 1:
+                if self._loop_streams is None:
+                    self._loop_streams = [torch.cuda.Stream(P.master.device) for _ in range(k - 1)]
+                for s_ in self._loop_streams:
+                    s_.wait_stream(main)
             for i in range(n_mb):
-                loop_eng.forward(i, batch.inputs[i * mb:(i + 1) * mb])
-                loop_eng.backward(i, labels=batch.labels[i * mb:(i + 1) * mb])
+                ctx = torch.cuda.stream(self._loop_streams[i % k - 1]) if (k > 1 and i % k) else contextlib.nullcontext()
+                with ctx:
+                    loop_eng.forward(i, batch.inputs[i * mb:(i + 1) * mb])
+                    loop_eng.backward(i, labels=batch.labels[i * mb:(i + 1) * mb])
+            if k > 1:
+                for s_ in self._loop_streams:
+                    main.wait_stream(s_)
+                loop_eng.merge()
             return
         if cfg.accum == "fused":
             loss_and_grad(self.model, P, batch.inputs, batch.labels, train=True, seed=seed, offset=0,
@@ -192,6 +213,10 @@ class DataParallelTrainer:
                 last = i == n_mb - 1  # grads are final only in the last minibatch's backward
                 self._minibatch(batch.inputs[i * mb:(i + 1) * mb], batch.labels[i * mb:(i + 1) * mb], i, seed, mb,
                                 on_ready=bk.ready if (bk is not None and last) else None)
+
+    def _loop_sets(self) -> int:
+        k = int(self.cfg.loop_streams)
+        return k if k > 0 else (2 if self.model.L >= 3 else 1)
 
     def _fused_loop(self, mb: int, seed: int):
         """FusedMLPStage over this rank's minibatches (one stage = the whole model):
@@ -207,7 +232,8 @@ class DataParallelTrainer:
                 # n_mb for the dropout counter
                 self._loop_engine = FusedMLPStage(self.model, self.state.params, self.cfg.num_minibatches, mb,
                                                   self.state.step_tensor, seed, mb_shift=32,
-                                                  step_mul=self.cfg.num_minibatches)
+                                                  step_mul=self.cfg.num_minibatches,
+                                                  n_sets=min(self._loop_sets(), self.cfg.num_minibatches))
         return self._loop_engine
 
     # ------------------------------------------------------------------ accumulation

@@ -65,11 +65,18 @@ class FusedMLPStage:
     ``step``: the device step counter (dropout offset; advanced by the optimizer)."""
 
     def __init__(self, model, params, n_mb: int, mb: int, step: torch.Tensor, seed: int,
-                 mb_shift: int = 16, step_mul: int = 1):
+                 mb_shift: int = 16, step_mul: int = 1, n_sets: int = 1):
         """``mb_shift`` / ``step_mul``: microbatch i, layer l draws dropout stream
         offset (i << mb_shift) + (l << 1) at counter high word step * step_mul -- the
-        GPipe convention (16, 1) or the DP minibatch loop's (32, n_minibatches)."""
+        GPipe convention (16, 1) or the DP minibatch loop's (32, n_minibatches).
+        ``n_sets`` > 1: microbatch i accumulates its grads / metric slots into set
+        i % n_sets (set 0 = the params' grad buffer, the others private zeroed copies)
+        and uses that set's dZ buffers, so the sets' microbatches may run on
+        concurrent streams (every grad write is a read-modify-write); ``merge`` folds
+        the private sets into the grad buffer afterwards."""
         self.model, self.P = model, params
+        self.n_sets = max(1, int(n_sets))
+        self.gx = [torch.zeros_like(params.grad) for _ in range(self.n_sets - 1)]
         self.n_mb, self.mb = n_mb, mb
         self.step, self.seed = step, seed & 0xFFFFFFFF
         self.mb_shift, self.step_mul = mb_shift, step_mul
@@ -93,7 +100,8 @@ class FusedMLPStage:
         self.det_logits = [torch.zeros(H // 16, mb, C_HEAD, dtype=torch.float32, device=dev) for _ in range(n_mb)] \
             if (self.last and deterministic()) else None
         # dZ of each layer (consumed by the launch of the layer below, then dead)
-        self.dZ = [torch.empty(mb, H, **bf) for _ in range(self.nh)]
+        self.dZs = [[torch.empty(mb, H, **bf) for _ in range(self.nh)] for _ in range(self.n_sets)]
+        self.dZ = self.dZs[0]
         self.dX = [torch.empty(mb, self.k0, **bf) for _ in range(n_mb)]   # in flight to the previous stage
         self.kn = [f"{n}/kernel" for n in model.names]
         self.bn = [f"{n}/bias" for n in model.names]
@@ -104,6 +112,18 @@ class FusedMLPStage:
             raise RuntimeError("MdArgs layout mismatch")
 
     # ------------------------------------------------------------------ args
+    def _g(self, i: int, name: str) -> int:
+        """Address of leaf ``name``'s gradient in microbatch i's grad set."""
+        g = self.P.g(name)
+        k = i % self.n_sets
+        return g.data_ptr() if k == 0 else self.gx[k - 1].data_ptr() + (g.data_ptr() - self.P.grad.data_ptr())
+
+    def merge(self):
+        """grad += every private set (then re-zeroed): after the sets' streams joined."""
+        for g in self.gx:
+            self.P.grad.add_(g)
+            g.zero_()
+
     def _base(self, i: int, l: int, x_ptr: int) -> MdArgs:
         P, m = self.P, self.model
         a = MdArgs()
@@ -121,7 +141,7 @@ class FusedMLPStage:
             a.logits = self.logits[i].data_ptr()
             if self.det_logits is not None:
                 a.det_logits = self.det_logits[i].data_ptr()
-            a.gWh, a.gbh = P.g(hk).data_ptr(), P.g(hb).data_ptr()
+            a.gWh, a.gbh = self._g(i, hk), self._g(i, hb)
         a.keep = 1.0 - m.dropout_rate
         a.seed = self.seed
         a.offset = (i << self.mb_shift) + ((m.layer_id_base + l) << 1)
@@ -131,8 +151,10 @@ class FusedMLPStage:
         a.fuse_opt = 0
         a.accumulate = 1
         a.mb_rows = 0
-        a.gW, a.gb = P.g(self.kn[l]).data_ptr(), P.g(self.bn[l]).data_ptr()
-        a.mslot = P.metrics_slot.data_ptr()
+        a.gW, a.gb = self._g(i, self.kn[l]), self._g(i, self.bn[l])
+        ms = P.metrics_slot
+        a.mslot = ms.data_ptr() if i % self.n_sets == 0 else \
+            self.gx[i % self.n_sets - 1].data_ptr() + (ms.data_ptr() - P.grad.data_ptr())
         return a
 
     # ------------------------------------------------------------------ passes
@@ -159,15 +181,16 @@ class FusedMLPStage:
         output gradient ``dh`` (bf16 [mb, 512]) from the next stage; grads += ;
         returns dX (bf16 [mb, k0]) for the previous stage if ``need_dx``."""
         Lb, s = _lib.lib(), _lib.stream_ptr()
+        dZ = self.dZs[i % self.n_sets]
         for l in reversed(range(self.nh)):
             top = l == self.nh - 1
             a = self._bwd[i][l]
             if a is None:
                 a = self._base(i, l, 0)
                 if l >= 1 or need_dx:
-                    a.dZout = self.dZ[l].data_ptr()
+                    a.dZout = dZ[l].data_ptr()
                 if not top:
-                    a.dZn = self.dZ[l + 1].data_ptr()
+                    a.dZn = dZ[l + 1].data_ptr()
                     a.Wn0 = a.Wn1 = self.P.s(self.kn[l + 1]).data_ptr()
                 self._bwd[i][l] = a
             if top and self.last:
@@ -183,5 +206,5 @@ class FusedMLPStage:
             _lib.check(Lb.jdt_md_layer(ctypes.byref(a), 1, variant, s), "md_bwd(stage)")
         if not need_dx:
             return None
-        K.gemm(self.dZ[0], self.P.s(self.kn[0]), a_layout="mk", b_layout="nk", out=self.dX[i])
+        K.gemm(dZ[0], self.P.s(self.kn[0]), a_layout="mk", b_layout="nk", out=self.dX[i])
         return self.dX[i]

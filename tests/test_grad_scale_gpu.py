@@ -166,10 +166,11 @@ def test_run_ahead_adamw_scale_matches_fp64(num_layers):
         check_grad(before[n].double() - after[n].double(), before[n].double() - p[n], f"4 steps {n}")
 
 
-@pytest.mark.parametrize("accum", ["loop", "fused"])
-def test_generic_gemm_path_sgd_matches_fp64(accum):
-    """Per-minibatch generic kernels (GEMM epilogues, CE kernel) + the SGD kernel;
-    loop: minibatch i of step 0 draws its masks from (seed, (l << 1) + (i << 32))
+@pytest.mark.parametrize("accum,streams", [("loop", 1), ("loop", 2), ("loop", 4), ("fused", 1)])
+def test_generic_gemm_path_sgd_matches_fp64(accum, streams):
+    """Per-minibatch kernels (loop: the fused per-layer md kernels, minibatch i on
+    stream i % streams with its own grad set) or generic kernels (fused) + the SGD
+    kernel; loop: minibatch i of step 0 draws its masks from (seed, (l << 1) + (i << 32))
     over its own [32, H] block."""
     from jax_distributed_tuts_amd.ops.kernels import dropout_mask
     from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, fold_rng_over_axis
@@ -177,7 +178,7 @@ def test_generic_gemm_path_sgd_matches_fp64(accum):
 
     st = _state(2, sgd(1.0))
     b = _batch()
-    tr = DataParallelTrainer(st, None, DPConfig(4, accum))
+    tr = DataParallelTrainer(st, None, DPConfig(4, accum, loop_streams=streams))
     before = _cpu(st.params.state_dict())
     tr.step(Batch(b.inputs.to(DEV), b.labels.to(DEV)))
     torch.cuda.synchronize()
@@ -190,6 +191,39 @@ def test_generic_gemm_path_sgd_matches_fp64(accum):
     got = sgd_grads(before, _cpu(st.params.state_dict()))
     for n in want:
         check_grad(got[n], want[n], n)
+    if accum == "loop":
+        assert tr._loop_engine is not None and tr._loop_engine.n_sets == streams
+        assert float(st.params.grad.abs().max()) == 0.0   # private sets merged, everything re-zeroed
+        assert all(float(g.abs().max()) == 0.0 for g in tr._loop_engine.gx)
+
+
+@pytest.mark.parametrize("layers", [2, 4])
+def test_loop_streams_captured_matches_one_stream(layers):
+    """The DP minibatch loop on 2 streams, captured into a multi-step hipGraph, trains
+    like the 1-stream eager loop (4 SGD steps; fp32 accumulation order is the only
+    difference: the two grad sets are summed after the join)."""
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig
+    from jax_distributed_tuts_amd.utils.train_state import Batch, sgd
+
+    res = []
+    for streams, cap in ((1, False), (2, True)):
+        st = _state(layers, sgd(0.5))
+        b = _batch()
+        b = Batch(b.inputs.to(DEV), b.labels.to(DEV))
+        p0 = st.params.master.clone()
+        tr = DataParallelTrainer(st, None, DPConfig(4, "loop", loop_streams=streams))
+        if cap:
+            tr.step(b)
+            tr.capture(b, steps_per_graph=3)
+            tr.run_steps(b, 3)
+        else:
+            for _ in range(4):
+                tr.step(b)
+        torch.cuda.synchronize()
+        res.append(st.params.master - p0)
+    rel = float((res[1] - res[0]).norm() / res[0].norm())
+    print(f"[loop streams, {layers} layers] update rel diff {rel:.2e}")
+    assert rel < 5e-3, rel
 
 
 @pytest.mark.parametrize("momentum,wd", [(0.0, 0.0), (0.9, 0.0), (0.9, 1e-2)])

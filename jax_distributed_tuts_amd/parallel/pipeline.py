@@ -369,7 +369,8 @@ class GPipeTrainer:
             # rows (the GEMMs round-robin over the streams once every chain has finished)
             on.join()
             on.fork()
-            self.model.weight_grads(P, arena, wgrad=self.wgrad, opt=eo, on=on)
+            nw = max(1, int(os.environ.get("JDT_WPASS_STREAMS", "0")) or len(on.side) + 1)
+            self.model.weight_grads(P, arena, wgrad=self.wgrad, opt=eo, on=lambda j: on(j % nw))
         on.join()
 
     def _layer_major_wpass(self, batch, P, st, seed, eo, n_mb) -> bool:

@@ -146,6 +146,9 @@ class PipeConfig:
     # concurrent microbatch passes: > 0 runs the W pass on this many dedicated streams,
     # each part's GEMMs as soon as every chain has passed it (0: after the join)
     wpass_early: int = field(default_factory=lambda: int(os.environ.get("JDT_WPASS_EARLY", "0")))
+    # ... the W pass after the join round-robin over the first wpass_rr microbatch streams
+    # (0: all of them; measured 1 stream 1.27 ms, 2: 1.12, 3-4: 1.07-1.09)
+    wpass_rr: int = field(default_factory=lambda: int(os.environ.get("JDT_WPASS_STREAMS", "0")))
 
 
 def _no_dropout(model) -> bool:
@@ -369,7 +372,7 @@ class GPipeTrainer:
             # rows (the GEMMs round-robin over the streams once every chain has finished)
             on.join()
             on.fork()
-            nw = max(1, int(os.environ.get("JDT_WPASS_STREAMS", "0")) or len(on.side) + 1)
+            nw = max(1, int(self.cfg.wpass_rr) or len(on.side) + 1)
             self.model.weight_grads(P, arena, wgrad=self.wgrad, opt=eo, on=lambda j: on(j % nw))
         on.join()
 

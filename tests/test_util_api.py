@@ -118,3 +118,34 @@ def test_default_microbatches_follows_measured_table():
     assert mlp["best_n_mb"] == default_microbatches(mlp["stages"])
     lm = {r["n_mb"]: r["modeled_step_us"] for r in rep["layouts"]["lm_pp4"]["table"]}
     assert lm[default_microbatches(4)] <= 1.05 * min(lm.values())
+
+
+def test_stream_schedules_resolve_on_cpu(monkeypatch):
+    """The concurrent-stream schedules are GPU-only: on CPU a one-stage LM pipeline keeps
+    layer-major (or the serial microbatch loop), its stream set is a no-op, and the DP
+    loop's auto stream count follows the measured rule (2 for >= 3 layers, else 1)."""
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.models.transformer import TransformerConfig
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
+    from jax_distributed_tuts_amd.parallel.pipeline import PipeConfig, _MbStreams
+    from jax_distributed_tuts_amd.parallel.pipeline_lm import build_lm_pipeline
+    from jax_distributed_tuts_amd.utils.train_state import adamw
+
+    monkeypatch.delenv("JDT_MB_STREAMS", raising=False)
+    monkeypatch.delenv("JDT_LOOP_STREAMS", raising=False)
+    assert PipeConfig().mb_streams == 4 and PipeConfig().wpass_early == 0 and PipeConfig().wpass_rr == 0
+    cfg = TransformerConfig(n_layers=1, d_model=64, n_heads=1, d_ff=128, seq_len=16, vocab_size=64)
+    for lm, mode in ((True, "layer-major"), (False, "microbatch-loop")):
+        tr, _ = build_lm_pipeline(None, "cpu", cfg, num_microbatches=4, layer_major_single_stage=lm)
+        assert tr._mb_streams_k() == 1 and tr.single_stage_mode == mode
+    on = _MbStreams(None, None)
+    on.fork()
+    on.join()
+    with on(3):
+        pass
+    for layers, want in ((2, 1), (3, 2), (4, 2)):
+        st = init_dp(Classifier(num_layers=layers), adamw(1e-3), 0, "cpu")
+        assert DataParallelTrainer(st, None, DPConfig(4, "loop"))._loop_sets() == want
+    monkeypatch.setenv("JDT_LOOP_STREAMS", "3")
+    st = init_dp(Classifier(num_layers=2), adamw(1e-3), 0, "cpu")
+    assert DataParallelTrainer(st, None, DPConfig(4, "loop"))._loop_sets() == 3

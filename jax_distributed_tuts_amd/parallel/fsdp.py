@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import logging
 import math
+import contextlib
 import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -241,6 +242,10 @@ class FSDPConfig:
     # the generic GEMM chain, where the model and the collectives allow (GPU, tutorial
     # MLP shapes, N = 1 or every sharded leaf on the xGMI kernels)
     fused_loop: bool = True
+    # N = 1 (every shard the whole leaf, no per-minibatch collective): minibatch i of the
+    # fused loop on stream i % loop_streams with its own grad set, as DPConfig.loop_streams
+    # (0 = auto: 2 for models of >= 3 layers, else 1)
+    loop_streams: int = field(default_factory=lambda: int(os.environ.get("JDT_LOOP_STREAMS", "0")))
 
 
 class ShardedFlatParams:
@@ -408,6 +413,12 @@ class _LoopView:
     @property
     def metrics_slot(self):
         return self.sp.local.metrics_slot
+
+    @property
+    def grad(self):
+        """The buffer every g() view lives in -- only at N = 1 (grad sets, FusedMLPStage)."""
+        assert self.one, "private grad sets need every gradient in one local buffer (N = 1)"
+        return self.sp.local.grad
 
 
 class FSDPTrainer:
@@ -613,8 +624,10 @@ class FSDPTrainer:
             dev = sp.local.master.device
             coll_ok = self.world == 1 or (sp.xg is not None and len(sp._xg_names) == len(sp.sharded_names))
             if self.cfg.fused_loop and coll_ok and stage_supported(self.model, mb, dev):
+                k = int(self.cfg.loop_streams) or (2 if self.model.L >= 3 else 1)
                 self._loop_engine = FusedMLPStage(self.model, _LoopView(sp), self.cfg.num_minibatches, mb,
-                                                  self.state.step_tensor, seed)
+                                                  self.state.step_tensor, seed,
+                                                  n_sets=min(k, self.cfg.num_minibatches) if self.world == 1 else 1)
                 # sharded leaves' full-grad range (zeroed after each minibatch's reduce-scatter)
                 offs = sorted((sp.full.offsets[n][0], sp.full.g(n).numel()) for n in sp.sharded_names)
                 self._shard_full = [sp.full.grad[o:o + n] for o, n in offs]
@@ -635,17 +648,30 @@ class FSDPTrainer:
             # shards, forward + CE + backward, reduce-scatter the sharded leaves' grads
             # into the local shards (replicated leaves accumulate locally); then ONE
             # all-reduce of the local tail (replicated grads + metric slots), AdamW
+            k = eng.n_sets   # > 1 only at N = 1: no collective inside the loop
+            main = torch.cuda.current_stream(batch.inputs.device) if k > 1 else None
+            if k > 1:
+                if getattr(self, "_loop_streams", None) is None:
+                    self._loop_streams = [torch.cuda.Stream(batch.inputs.device) for _ in range(k - 1)]
+                for s_ in self._loop_streams:
+                    s_.wait_stream(main)
             for i in range(n_mb):
                 if self.world > 1 and (i == 0 or not cfg.gather_once):
                     sp.xg.all_gather_segments([(sp.full.s(n), sp.local.s(n)) for n in sp._xg_names])
-                eng.forward(i, batch.inputs[i * mb:(i + 1) * mb])
-                eng.backward(i, labels=batch.labels[i * mb:(i + 1) * mb])
+                with (torch.cuda.stream(self._loop_streams[i % k - 1]) if (k > 1 and i % k)
+                      else contextlib.nullcontext()):
+                    eng.forward(i, batch.inputs[i * mb:(i + 1) * mb])
+                    eng.backward(i, labels=batch.labels[i * mb:(i + 1) * mb])
                 if self.world > 1 and (not cfg.scatter_once or i == n_mb - 1):
                     with named_scope("scatter_grads"):
                         sp.xg.reduce_scatter_segments([(sp.full.g(n), sp.local.g(n)) for n in sp._xg_names],
                                                       accumulate=True)
                         for t in self._shard_full:
                             t.zero_()
+            if k > 1:
+                for s_ in self._loop_streams:
+                    main.wait_stream(s_)
+                eng.merge()
             if self.world > 1:
                 sp.sync_replicated()
             st.tx.update(sp.local, st.opt_state, 1.0 / (n_mb * self.world))

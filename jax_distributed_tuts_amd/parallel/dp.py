@@ -215,8 +215,10 @@ class DataParallelTrainer:
                                 on_ready=bk.ready if (bk is not None and last) else None)
 
     def _loop_sets(self) -> int:
+        from .pipeline import hw_queues
+
         k = int(self.cfg.loop_streams)
-        return k if k > 0 else (2 if self.model.L >= 3 else 1)
+        return min(k if k > 0 else (2 if self.model.L >= 3 else 1), hw_queues())
 
     def _fused_loop(self, mb: int, seed: int):
         """FusedMLPStage over this rank's minibatches (one stage = the whole model):

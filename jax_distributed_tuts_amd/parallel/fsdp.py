@@ -624,7 +624,9 @@ class FSDPTrainer:
             dev = sp.local.master.device
             coll_ok = self.world == 1 or (sp.xg is not None and len(sp._xg_names) == len(sp.sharded_names))
             if self.cfg.fused_loop and coll_ok and stage_supported(self.model, mb, dev):
-                k = int(self.cfg.loop_streams) or (2 if self.model.L >= 3 else 1)
+                from .pipeline import hw_queues
+
+                k = min(int(self.cfg.loop_streams) or (2 if self.model.L >= 3 else 1), hw_queues())
                 self._loop_engine = FusedMLPStage(self.model, _LoopView(sp), self.cfg.num_minibatches, mb,
                                                   self.state.step_tensor, seed,
                                                   n_sets=min(k, self.cfg.num_minibatches) if self.world == 1 else 1)

@@ -159,6 +159,14 @@ def _no_dropout(model) -> bool:
     return float(rate) == 0.0
 
 
+def hw_queues() -> int:
+    """HIP hardware queues per process (GPU_MAX_HW_QUEUES; HIP's default is 4)."""
+    try:
+        return max(1, int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))
+    except ValueError:
+        return 4
+
+
 class _MbStreams:
     """``with on(i)``: run work item i on stream i % k (item 0, k, 2k, ... on the main
     stream); ``fork``: the side streams wait for the main stream's work so far;
@@ -459,8 +467,11 @@ class GPipeTrainer:
         return f"microbatch-loop ({k} streams)" if k > 1 else "microbatch-loop"
 
     def _mb_streams_k(self) -> int:
-        """Streams the per-microbatch passes of a one-stage pipeline run on (1: serial)."""
-        k = min(int(self.cfg.mb_streams), self.cfg.num_microbatches)
+        """Streams the per-microbatch passes of a one-stage pipeline run on (1: serial);
+        never more than the process's HIP hardware queues (GPU_MAX_HW_QUEUES when set:
+        a 4-stream graph on 2 queues crashed the runtime in a probe,
+        profiles/r3_lm_mb_streams_ab.txt)."""
+        k = min(int(self.cfg.mb_streams), self.cfg.num_microbatches, hw_queues())
         ok = (self.S == 1 and self.dev.type == "cuda" and self.cfg.defer_wgrad and hasattr(self.model, "weight_grads")
               and not self.cfg.merge_single_stage)
         return k if ok else 1

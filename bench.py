@@ -25,6 +25,7 @@ kernels still run between them).
 from __future__ import annotations
 
 import argparse
+import faulthandler
 import json
 import os
 import sys
@@ -152,7 +153,7 @@ def comm_sweep(tr, dev, iters: int = 20):
             b.synchronize()
             return round(a.elapsed_time(b) * 1e3 / iters, 2)
 
-        if xg is not None and n <= xg.capacity - 4 * 96 * D.world_size():
+        if xg is not None and xg.fits(n)["twoshot"]:
             row["xgmi_us"] = timed(lambda: xg.all_reduce_(x))
         if rccl:
             row["rccl_us"] = timed(lambda: dist.all_reduce(x))
@@ -217,6 +218,8 @@ def main():
     ap.add_argument("--optimizer", choices=["adamw", "sgd"], default="adamw",
                     help="DP: adamw (the reference's optax.adamw) or sgd (the fused SGD kernel)")
     args = ap.parse_args()
+    # a native crash (HIP runtime segfault, abort) prints every thread's Python stack
+    faulthandler.enable(all_threads=True)
 
     # N ranks for --gpus N: start them here (this process never touches the GPU) ...
     LCH.maybe_launch(args.gpus, __file__, sys.argv[1:])

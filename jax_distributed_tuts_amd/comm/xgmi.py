@@ -113,6 +113,26 @@ def part_len(n: int, world: int) -> int:
     return ((n + world - 1) // world + 3) // 4 * 4
 
 
+XG_MAX_BLOCKS, XG_THREADS = 96, 256   # comm/csrc/xgmi.hip
+
+
+def geometry(s: int) -> tuple:
+    """(blocks, chunk) of a launch over s floats per rank part: mirror of
+    ``xg_geometry`` in comm/csrc/xgmi.hip (the host checks ``blocks*chunk*W <= cap``)."""
+    g = min(max((s + 4 * XG_THREADS - 1) // (4 * XG_THREADS), 8), XG_MAX_BLOCKS)
+    return g, ((s + g - 1) // g + 3) // 4 * 4
+
+
+def allreduce_fits(n: int, world: int, cap: int) -> dict:
+    """Which all-reduce kernels can take an n-float vector on a context of ``cap``
+    floats per buffer half: {"oneshot": bool, "twoshot": bool} (the same launch
+    checks as ``xg_oneshot`` / ``xg_launch`` in comm/csrc/xgmi.hip)."""
+    n4 = (n + 3) // 4 * 4
+    g1, c1 = geometry(n4)
+    g2, c2 = geometry(part_len(n, world))
+    return {"oneshot": n > 0 and g1 * c1 <= cap, "twoshot": n > 0 and g2 * c2 * world <= cap}
+
+
 def requested(mode: str, world: int, device: torch.device) -> bool:
     """Whether a trainer should try the xGMI path: ``mode`` in {"auto","xgmi","rccl"}
     (env ``JDT_COMM`` overrides "auto")."""
@@ -169,6 +189,22 @@ class XgmiComm:
     def capacity(self) -> int:
         return int(_lib.lib().jdt_xgmi_capacity(self.ctx)) if self.ctx else 0
 
+    def fits(self, n: int) -> dict:
+        """{"oneshot", "twoshot"}: whether each all-reduce kernel takes n floats here."""
+        return allreduce_fits(int(n), self.world, self.capacity)
+
+    def max_allreduce(self) -> int:
+        """Largest n (multiple of 4) the two-shot all-reduce takes on this context."""
+        lo, hi = 0, self.capacity
+        while lo < hi:   # fits() is monotone in n up to padding steps: bisect, then step down
+            mid = (lo + hi + 1) // 2
+            if self.fits(mid)["twoshot"]:
+                lo = mid
+            else:
+                hi = mid - 1
+        while lo > 0 and not self.fits(lo)["twoshot"]:
+            lo -= 1
+        return lo // 4 * 4
     def error(self) -> int:
         """1 if any in-kernel barrier timed out on this rank (synchronises the device)."""
         return int(_lib.lib().jdt_xgmi_error(self.ctx)) if self.ctx else 0
@@ -459,7 +495,10 @@ class XgmiComm:
     def _self_test_body(self) -> bool:
         W, r, dev = self.world, self.rank, self.device
         cap = self.capacity
-        sizes = [n for n in (407_054, 300_001, 4_099) if part_len(n, W) * W <= cap // 2] or [min(cap // 4, 4_099)]
+        # the largest two-shot size this context takes (the trainer's own bucket: create_for
+        # sizes the context to it), the DP tutorial bucket and two odd sizes
+        top = self.max_allreduce()
+        sizes = sorted({n for n in (top, 407_054, 300_001, 4_099) if 0 < n <= top}, reverse=True)
         nccl = dist.get_backend(self.group) == "nccl"
         for it in range(self.SELF_TEST_ITERS):
             n = sizes[it % len(sizes)]
@@ -693,8 +732,11 @@ def calibrate(comm: XgmiComm, sizes, iters: int = 20, rccl_margin_us: float = 3.
     L = _lib.lib()
     dev = comm.device
     rccl = dist.get_backend(comm.group) == "nccl"
-    cap = comm.capacity - 4 * 96 * comm.world
-    ladder = sorted({int(n) for n in tuple(CALIBRATION_LADDER) + tuple(sizes) if 0 < int(n) <= cap // 2})
+    sizes = [int(n) for n in sizes if int(n) > 0]
+    too_big = [n for n in sizes if not comm.fits(n)["twoshot"]]
+    if too_big:   # the trainer sized the context: every size it issues must be timed
+        raise ValueError(f"calibrate: trainer sizes {too_big} exceed this context (max {comm.max_allreduce()} floats)")
+    ladder = sorted({int(n) for n in CALIBRATION_LADDER if comm.fits(n)["twoshot"]} | set(sizes))
     big = 1 << 40
 
     def timed(fn) -> float:
@@ -718,29 +760,32 @@ def calibrate(comm: XgmiComm, sizes, iters: int = 20, rccl_margin_us: float = 3.
         with torch.cuda.device(dev):
             for n in ladder:
                 x = torch.ones(n, device=dev)
-                L.jdt_xgmi_set_oneshot_bytes(big)
-                one = timed(lambda: comm.all_reduce_(x))
+                one = None
+                if comm.fits(n)["oneshot"]:
+                    L.jdt_xgmi_set_oneshot_bytes(big)
+                    one = timed(lambda: comm.all_reduce_(x))
                 L.jdt_xgmi_set_oneshot_bytes(0)
                 two = timed(lambda: comm.all_reduce_(x))
                 rc = timed(lambda: dist.all_reduce(x, group=comm.group)) if rccl else None
-                rows.append({"bytes": 4 * n, "xgmi_oneshot_us": round(one, 2), "xgmi_twoshot_us": round(two, 2),
-                             "rccl_us": None if rc is None else round(rc, 2)})
+                rows.append({"bytes": 4 * n, "xgmi_oneshot_us": None if one is None else round(one, 2),
+                             "xgmi_twoshot_us": round(two, 2), "rccl_us": None if rc is None else round(rc, 2)})
     finally:
         L.jdt_xgmi_set_oneshot_bytes(old)
     if comm.error():
         raise RuntimeError("xgmi collective timed out during calibration")
     cross = 0
-    for r in rows:
-        if r["xgmi_oneshot_us"] <= r["xgmi_twoshot_us"]:
+    for r in rows:   # the one-shot kernel up to the largest size where it is not slower
+        if r["xgmi_oneshot_us"] is not None and r["xgmi_oneshot_us"] <= r["xgmi_twoshot_us"]:
             cross = r["bytes"]
     L.jdt_xgmi_set_oneshot_bytes(cross)
-    want = {4 * int(n) for n in sizes}
+    want = {4 * n for n in sizes}
     for r in rows:
-        best = min(r["xgmi_oneshot_us"], r["xgmi_twoshot_us"])
+        best = min(t for t in (r["xgmi_oneshot_us"], r["xgmi_twoshot_us"]) if t is not None)
+        r["xgmi_us"] = best
         r["choice"] = ("rccl" if r["rccl_us"] is not None and r["rccl_us"] + rccl_margin_us < best else "xgmi")
         r["trainer_size"] = r["bytes"] in want
     return {"oneshot_threshold_bytes": cross, "rccl": "available" if rccl else "unavailable (gloo group)",
-            "table": rows}
+            "rccl_margin_us": rccl_margin_us, "table": rows}
 
 
 def status(comm: Optional[XgmiComm], world: int, device, mode: str = "auto") -> str:
@@ -782,8 +827,9 @@ def create_for(mesh, axis: str, cap_floats: int, device: torch.device, mode: str
         cal = calibrate(c, sizes)
         LAST_CALIBRATION = cal
         main = max(sizes)
-        row = next((r for r in cal["table"] if r["bytes"] == 4 * main), None)
-        cal["transport"] = "xgmi" if row is None or row["choice"] == "xgmi" or mode == "xgmi" else "rccl"
+        row = next(r for r in cal["table"] if r["bytes"] == 4 * main and r["trainer_size"])
+        cal["trainer_bytes"] = 4 * main
+        cal["transport"] = "xgmi" if row["choice"] == "xgmi" or mode == "xgmi" else "rccl"
         if mode != "xgmi" and cal["transport"] == "rccl":
             log.warning("xgmi: RCCL measured faster at %d bytes; using RCCL", 4 * main)
             c.close()

@@ -103,8 +103,12 @@ def entry_main(main, args, script: str):
     2. ``--profile``: this rank re-runs itself under rocprofv3 as a child;
     3. run ``main(args)`` on the job's process group, failing (exit 3) unless it
        has exactly the requested number of ranks."""
+    import faulthandler
+
     from ..runtime.launch import maybe_launch, resolve_gpus, run
 
+    # a native crash (HIP runtime segfault, abort) prints every thread's Python stack
+    faulthandler.enable(all_threads=True)
     if getattr(args, "serialize_kernels", False):
         # read by the HIP runtime at initialisation: set here, before any GPU call,
         # so this process and every rank the launcher starts inherit them

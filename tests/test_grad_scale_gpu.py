@@ -263,7 +263,8 @@ def _load(d, name, ws):
 
 
 @pytest.mark.parametrize("kind,ws", [("dp_sgd", 2), ("dp_adam_eps", 2), ("fsdp_sgd", 2), ("fsdp_loop_sgd", 2),
-                                     ("fsdp_loop_sgd", 4)])
+                                     ("fsdp_loop_sgd", 4), ("dp_sgd", 8), ("dp_adam_eps", 8), ("fsdp_sgd", 8),
+                                     ("fsdp_loop_sgd", 8)])
 def test_xgmi_strategies_grad_scale(tmp_path, kind, ws):
     from jax_distributed_tuts_amd.runtime.launch import spawn
 
@@ -281,8 +282,8 @@ def test_xgmi_strategies_grad_scale(tmp_path, kind, ws):
             check_grad(g, want[n], n)
 
 
-@pytest.mark.parametrize("ws,dp", [(2, 1), (4, 2)])
-def test_xgmi_pipeline_grad_scale(tmp_path, ws, dp):
+@pytest.mark.parametrize("ws,dp,n_hidden", [(2, 1, 3), (4, 2, 3), (8, 1, 7), (8, 2, 3)])
+def test_xgmi_pipeline_grad_scale(tmp_path, ws, dp, n_hidden):
     from pipeline_parallel import pp_mlp_dims
     from jax_distributed_tuts_amd.models.mlp import MLP
     from jax_distributed_tuts_amd.runtime.launch import spawn
@@ -290,7 +291,8 @@ def test_xgmi_pipeline_grad_scale(tmp_path, ws, dp):
 
     from . import xgmi_workers as XW
 
-    spawn(functools.partial(XW.grad_probe_xgmi, kind="pp_sgd", dp=dp), ws, str(tmp_path), gpu=True)
+    spawn(functools.partial(XW.grad_probe_xgmi, kind="pp_sgd", dp=dp, n_hidden=n_hidden), ws, str(tmp_path),
+          gpu=True)
     res = _load(tmp_path, "gpx_pp_sgd", ws)
     before, got = {}, {}
     for o in res:
@@ -301,7 +303,7 @@ def test_xgmi_pipeline_grad_scale(tmp_path, ws, dp):
                 torch.testing.assert_close(v, got[k], rtol=0, atol=0)
             got[k] = v
     b = _batch()
-    want = mlp_grads_fp64(before, MLP(pp_mlp_dims(dp_config(), 3)).names, b.inputs, b.labels, n_mb=4)
+    want = mlp_grads_fp64(before, MLP(pp_mlp_dims(dp_config(), n_hidden)).names, b.inputs, b.labels, n_mb=4)
     assert set(got) == set(want)
     for n in want:
         check_grad(got[n], want[n], n)

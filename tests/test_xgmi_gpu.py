@@ -20,7 +20,7 @@ def _load(d, name, ws):
     return [torch.load(os.path.join(d, f"{name}_r{r}.pt"), weights_only=True) for r in range(ws)]
 
 
-@pytest.mark.parametrize("ws", [2, 4])
+@pytest.mark.parametrize("ws", [2, 4, 8])
 def test_xgmi_collectives(tmp_path, ws):
     spawn(XW.collectives, ws, str(tmp_path), gpu=True)
     for r, o in enumerate(_load(tmp_path, "xg", ws)):
@@ -32,21 +32,24 @@ def test_xgmi_collectives(tmp_path, ws):
         # reports RCCL as unavailable on the shared-GPU (gloo-bootstrapped) job
         assert o["cal_rows"] >= 5 and o["cal_threshold_ok"] and o["cal_threshold_set"] and o["cal_has_bucket"], o
         assert o["cal_rccl"].startswith("unavailable") and o["ar_after_cal"], o
+        assert o["prod_trainer_row"], o
 
 
-def test_dp_over_xgmi_matches_single_device(tmp_path):
+@pytest.mark.parametrize("ws", [2, 8])
+def test_dp_over_xgmi_matches_single_device(tmp_path, ws):
     from data_paral import synthetic_batch
     from jax_distributed_tuts_amd.models.mlp import Classifier
     from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
     from jax_distributed_tuts_amd.utils.config import dp_config
     from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
 
-    spawn(XW.dp_xgmi, 2, str(tmp_path), gpu=True)
-    res = _load(tmp_path, "dpx", 2)
+    spawn(XW.dp_xgmi, ws, str(tmp_path), gpu=True)
+    res = _load(tmp_path, "dpx", ws)
     assert all(o["comm"] == "xgmi" for o in res)
     assert all(o["step"] == 8 for o in res)
-    torch.testing.assert_close(res[0]["master"], res[1]["master"], rtol=0, atol=0)  # replicated exactly
-    torch.testing.assert_close(res[0]["metrics"], res[1]["metrics"], rtol=0, atol=0)
+    for o in res[1:]:
+        torch.testing.assert_close(res[0]["master"], o["master"], rtol=0, atol=0)  # replicated exactly
+        torch.testing.assert_close(res[0]["metrics"], o["metrics"], rtol=0, atol=0)
     # single device, whole batch, same steps
     dev = torch.device("cuda", 0)
     st = init_dp(Classifier(dropout_rate=0.0), adamw(1e-3), 69, dev, None)
@@ -66,9 +69,10 @@ def test_dp_over_xgmi_matches_single_device(tmp_path):
     assert abs(float(m[2]) - float(ref[2])) <= 4
 
 
-@pytest.mark.parametrize("fused,num_layers,eps", [(True, 2, 1e-8), (False, 2, 1e-8), (True, 4, 1e-8), (True, 2, 10.0),
-                                                  (True, 4, 10.0)])
-def test_fsdp_over_xgmi_matches_single_device(tmp_path, fused, num_layers, eps):
+@pytest.mark.parametrize("ws,fused,num_layers,eps", [(2, True, 2, 1e-8), (2, False, 2, 1e-8), (2, True, 4, 1e-8),
+                                                     (2, True, 2, 10.0), (2, True, 4, 10.0), (8, True, 2, 10.0),
+                                                     (8, True, 4, 10.0), (8, False, 2, 1e-8)])
+def test_fsdp_over_xgmi_matches_single_device(tmp_path, ws, fused, num_layers, eps):
     """fused: the step's whole collective is ONE xg_fsdp_kernel (reduce-scatter +
     sharded AdamW + metrics fold + next-step all-gather).  eps = 10 makes AdamW's update
     ~ lr * g / eps, i.e. proportional to the gradient: a missing 1/N or 1/n_mb in the
@@ -79,8 +83,8 @@ def test_fsdp_over_xgmi_matches_single_device(tmp_path, fused, num_layers, eps):
     from jax_distributed_tuts_amd.utils.config import fsdp_config
     from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
 
-    spawn(XW.fsdp_xgmi, 2, str(tmp_path), fused, 3, num_layers, eps, gpu=True)
-    res = _load(tmp_path, f"fsx{num_layers}", 2)
+    spawn(XW.fsdp_xgmi, ws, str(tmp_path), fused, 3, num_layers, eps, gpu=True)
+    res = _load(tmp_path, f"fsx{num_layers}", ws)
     assert all(o["comm"] == "xgmi" for o in res)
     assert all(o["fused_comm"] == fused for o in res)
     # every sharded leaf rides the segmented kernels (dim-0 and, 4-layer, dim-1 shards)
@@ -103,7 +107,8 @@ def test_fsdp_over_xgmi_matches_single_device(tmp_path, fused, num_layers, eps):
     for n, d in res[0]["dims"].items():
         got = res[0]["local"][n] if d is None else torch.cat([o["local"][n] for o in res], dim=d)
         if d is None:
-            torch.testing.assert_close(res[0]["local"][n], res[1]["local"][n], rtol=0, atol=0)
+            for o in res[1:]:
+                torch.testing.assert_close(res[0]["local"][n], o["local"][n], rtol=0, atol=0)
         diff = (got - sp.local.p(n).cpu()).abs()
         assert float(diff.max()) <= 2 * 1e-3 * 3 + 1e-6, n
         assert float((diff > 5e-5).float().mean()) < 5e-3, n
@@ -114,7 +119,7 @@ def test_fsdp_over_xgmi_matches_single_device(tmp_path, fused, num_layers, eps):
     assert float(m[1]) == float(ref[1])
 
 
-@pytest.mark.parametrize("ws", [2, 3])
+@pytest.mark.parametrize("ws", [2, 3, 8])
 def test_p2p_inbox_roundtrip(tmp_path, ws):
     spawn(XW.p2p_roundtrip, ws, str(tmp_path), gpu=True)
     for r, o in enumerate(_load(tmp_path, "p2p", ws)):
@@ -122,10 +127,11 @@ def test_p2p_inbox_roundtrip(tmp_path, ws):
         assert o["data"] and o["err"] == 0 and o["epoch"] == 4, o
 
 
-@pytest.mark.parametrize("ws,dp", [(2, 1), (4, 2)])
-def test_pipeline_over_xgmi_matches_single_device(tmp_path, ws, dp):
+@pytest.mark.parametrize("ws,dp,n_hidden", [(2, 1, 3), (4, 2, 3), (8, 1, 7), (8, 2, 3)])
+def test_pipeline_over_xgmi_matches_single_device(tmp_path, ws, dp, n_hidden):
     """GPipe with the inbox hand-off captured into hipGraphs (and the fused xGMI
-    data-axis all-reduce for dp=2) == the un-split model on one device."""
+    data-axis all-reduce for dp=2) == the un-split model on one device.  ws=8: the
+    8-stage GPipe MLP (BASELINE config #4, one dense layer per stage) and DP=2 x PP=4."""
     from data_paral import synthetic_batch
     from pipeline_parallel import pp_mlp_dims
     from jax_distributed_tuts_amd.models.mlp import MLP
@@ -137,12 +143,12 @@ def test_pipeline_over_xgmi_matches_single_device(tmp_path, ws, dp):
 
     import functools
 
-    spawn(functools.partial(XW.pp_xgmi, dp=dp), ws, str(tmp_path), gpu=True)
+    spawn(functools.partial(XW.pp_xgmi, dp=dp, n_hidden=n_hidden), ws, str(tmp_path), gpu=True)
     res = _load(tmp_path, f"ppx{dp}", ws)
     assert all(o["comm"] == "xgmi" and o["count"] == 4 for o in res)
     dev = torch.device("cuda", 0)
     cfg = dp_config()
-    model = MLP(pp_mlp_dims(cfg, 3), dropout_rate=0.0)
+    model = MLP(pp_mlp_dims(cfg, n_hidden), dropout_rate=0.0)
     P = FlatParams(model.param_specs(), device=dev).init_(cfg.seed)
     st = TrainState.create(apply_fn=model, params=P, tx=adamw(1e-3), rng=R.PRNGKey(cfg.seed))
     tr = DataParallelTrainer(st, None, DPConfig(4, "loop"))
@@ -165,9 +171,11 @@ def test_pipeline_over_xgmi_matches_single_device(tmp_path, ws, dp):
     assert abs(float(m[0]) - float(rm[0])) <= 2e-3 * abs(float(rm[0])) + 1e-3
 
 
-def test_transformer_hybrid_over_xgmi_matches_single_device(tmp_path):
-    """Transformer LM, DP=2 x PP=2 over xGMI (4 processes on the GPU), captured
-    into hipGraphs == the un-split model trained on the whole batch on one device."""
+@pytest.mark.parametrize("ws,n_layers", [(4, 2), (8, 4)])
+def test_transformer_hybrid_over_xgmi_matches_single_device(tmp_path, ws, n_layers):
+    """Transformer LM, DP=2 x PP=ws/2 over xGMI (ws processes on the GPU), captured
+    into hipGraphs == the un-split model trained on the whole batch on one device.
+    ws=8 is BASELINE config #5's layout (DP=2 x PP=4, one layer per stage)."""
     import functools
 
     from jax_distributed_tuts_amd.models.transformer import TransformerConfig
@@ -175,11 +183,11 @@ def test_transformer_hybrid_over_xgmi_matches_single_device(tmp_path):
     from jax_distributed_tuts_amd.parallel.pipeline_lm import build_lm_pipeline, lm_batch
     from jax_distributed_tuts_amd.utils.train_state import Batch
 
-    spawn(functools.partial(XW.lm_pp_xgmi, dp=2), 4, str(tmp_path), gpu=True)
-    res = _load(tmp_path, "lmx2", 4)
+    spawn(functools.partial(XW.lm_pp_xgmi, dp=2, n_layers=n_layers), ws, str(tmp_path), gpu=True)
+    res = _load(tmp_path, "lmx2", ws)
     assert all(o["comm"] == "xgmi" for o in res)
     dev = torch.device("cuda", 0)
-    cfg = TransformerConfig(vocab_size=512, d_model=128, n_heads=2, d_ff=256, seq_len=64, n_layers=2)
+    cfg = TransformerConfig(vocab_size=512, d_model=128, n_heads=2, d_ff=256, seq_len=64, n_layers=n_layers)
     tr, _ = build_lm_pipeline(None, dev, cfg, num_microbatches=4)  # dp=2 x 2 microbatches == 4 microbatches
     tr.cfg.layer_major_single_stage = False  # per-microbatch passes, like the hybrid's stages (same rounding)
     b = lm_batch(cfg, global_batch=8, seed=1)

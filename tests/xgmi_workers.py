@@ -66,6 +66,19 @@ def collectives(outdir):
     comm.all_reduce_(y)
     res["ar_after_cal"] = bool(torch.equal(y.cpu(), _seq_sum(xs)))
     XgmiComm.set_oneshot_bytes(256 * 1024)
+    # the production geometry: create_for sizes the context to the trainer's bucket (the DP
+    # tutorial's 407,050 grads + 4 metric slots) and must time exactly that size, then pick
+    # the transport from that row
+    from jax_distributed_tuts_amd.comm import xgmi as XM
+
+    prod = XM.create_for(mesh, "data", 407_054, dev, "xgmi")
+    cal2 = XM.LAST_CALIBRATION or {}
+    rows = [row for row in cal2.get("table", []) if row["trainer_size"]]
+    res["prod_trainer_row"] = (prod is not None and len(rows) == 1 and rows[0]["bytes"] == 4 * 407_054
+                               and cal2.get("transport") == "xgmi" and rows[0]["xgmi_twoshot_us"] > 0)
+    if prod is not None:
+        prod.close()
+    XgmiComm.set_oneshot_bytes(256 * 1024)
     # fused all-reduce + AdamW + metrics fold == sum, then the standalone AdamW kernel
     npar, total = 4096, 4096 + 64
     g = torch.Generator().manual_seed(7)
@@ -276,7 +289,7 @@ def p2p_roundtrip(outdir):
     _save(outdir, "p2p", res)
 
 
-def lm_pp_xgmi(outdir, dp, steps=3):
+def lm_pp_xgmi(outdir, dp, steps=3, n_layers=2):
     """Transformer LM (small config) over a (data=dp, pipe=W/dp) mesh with the xGMI
     inbox hand-off and the fused data-axis all-reduce; eager step, then graphs."""
     from jax_distributed_tuts_amd.models.transformer import TransformerConfig
@@ -286,7 +299,7 @@ def lm_pp_xgmi(outdir, dp, steps=3):
     from jax_distributed_tuts_amd.utils.train_state import Batch
 
     dev = D.device()
-    cfg = TransformerConfig(vocab_size=512, d_model=128, n_heads=2, d_ff=256, seq_len=64, n_layers=2)
+    cfg = TransformerConfig(vocab_size=512, d_model=128, n_heads=2, d_ff=256, seq_len=64, n_layers=n_layers)
     mesh = D.Mesh({"data": dp, "pipe": D.world_size() // dp})
     tr, _ = build_lm_pipeline(mesh, dev, cfg, num_microbatches=2, comm="xgmi")
     b = shard_batch(lm_batch(cfg, global_batch=8, seed=1), mesh, "data")
@@ -329,7 +342,7 @@ def fault_timeout(outdir):
     p2p.close()
 
 
-def grad_probe_xgmi(outdir, kind, dp=1, capture=True):
+def grad_probe_xgmi(outdir, kind, dp=1, capture=True, n_hidden=3):
     """One step (dropout off) of a strategy over the xGMI kernels with a
     scale-revealing optimizer -- plain SGD lr 1, or (``dp_adam_eps``) the fused
     xGMI all-reduce + AdamW kernel with eps = 10 -- saving params before / after
@@ -396,8 +409,8 @@ def grad_probe_xgmi(outdir, kind, dp=1, capture=True):
         from pipeline_parallel import build_mlp_pipeline
 
         mesh = D.Mesh({"data": dp, "pipe": D.world_size() // dp})
-        tr = build_mlp_pipeline(cfg, mesh, dev, n_hidden_layers=3, dropout_rate=0.0, num_microbatches=4, comm="xgmi",
-                                tx=sgd(1.0))
+        tr = build_mlp_pipeline(cfg, mesh, dev, n_hidden_layers=n_hidden, dropout_rate=0.0, num_microbatches=4,
+                                comm="xgmi", tx=sgd(1.0))
         b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
         before = cpu(tr.state.params.state_dict())
         tr.step(Batch(b.inputs.to(dev), b.labels.to(dev)))

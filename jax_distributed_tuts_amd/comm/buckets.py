@@ -20,14 +20,16 @@ import math
 import torch
 import torch.distributed as dist
 
-from ..runtime.dist import Mesh, is_initialized
+from ..runtime.dist import Mesh
 from ..utils.flat import FlatParams
 
 
 class GradBuckets:
     def __init__(self, P: FlatParams, mesh: Optional[Mesh], axis: str, bucket_bytes: int = 25 << 20):
         self.P, self.mesh, self.axis = P, mesh, axis
-        self.active = mesh is not None and is_initialized() and mesh.axis_size(axis) > 1
+        from .collectives import active
+
+        self.active = active(mesh, axis)
         specs = list(P.specs)
         groups: List[List[str]] = []
         cur: List[str] = []

@@ -38,7 +38,16 @@ def axis_size(mesh: Optional[Mesh], axis: str) -> int:
 
 
 def _active(mesh: Optional[Mesh], axis: str) -> bool:
-    return mesh is not None and is_initialized() and mesh.axis_size(axis) > 1
+    """Whether a collective along ``axis`` is a real call (a 1-member axis only on a
+    ``Mesh(unit_groups=True)``)."""
+    if mesh is None or not is_initialized():
+        return False
+    return mesh.axis_size(axis) > 1 or (getattr(mesh, "unit_groups", False) and mesh.group(axis) is not None)
+
+
+def active(mesh: Optional[Mesh], axis: str) -> bool:
+    """Public form of the check above: the trainers issue their collectives iff this holds."""
+    return _active(mesh, axis)
 
 
 def _is_gloo(group) -> bool:

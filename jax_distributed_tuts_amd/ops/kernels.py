@@ -36,7 +36,6 @@ def _is_gpu(t: torch.Tensor) -> bool:
 
 _WS = {}
 WS_FLOATS = 8 << 20      # 32 MiB split-K slab workspace per device
-_LIB_PLAIN = os.environ.get("JDT_GEMM_LIB", "0") == "1"   # plain bf16 GEMMs on hipBLASLt (gemm)
 N_COUNTERS = 1 << 16
 
 
@@ -333,13 +332,6 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, a_layout: str = "mk", b_layout: st
             seed = int(seed_dev.item())
         return _gemm_ref(a, b, a_layout, b_layout, out, accumulate, alpha, bias, act, z_out, z_in, act_bwd,
                          keep_prob, seed, offset, resid, dbias)
-    if (_LIB_PLAIN and not batched and not _GROUP and opt is None and not accumulate and alpha == 1.0
-            and bias is None and act == "none" and z_out is None and z_in is None and act_bwd == "none"
-            and resid is None and dbias is None and keep_prob == 1.0 and cfg < 0 and splits < 0
-            and a.dtype == b.dtype == out.dtype == torch.bfloat16):
-        # a plain bf16 GEMM (no epilogue to fuse): the vendor library (hipBLASLt) -- opt-in
-        # JDT_GEMM_LIB=1, see BENCH_NOTES "plain GEMMs on hipBLASLt"
-        return torch.mm(a if a_layout == "mk" else a.t(), b if b_layout == "kn" else b.t(), out=out)
     for t in (a, b, out, z_out, z_in, resid):
         if t is not None:
             assert t.stride(-1) == 1, "gemm operands must be contiguous in the last dim"

@@ -96,6 +96,8 @@ class DataParallelTrainer:
         P = state.params
         self.metrics = torch.zeros(N_METRIC_SLOTS, dtype=torch.float32, device=P.master.device)
         self.world = C.axis_size(mesh, cfg.axis)
+        # the step issues its gradient collective (N > 1, or a Mesh(unit_groups=True))
+        self._coll = self.world > 1 or C.active(mesh, cfg.axis)
         self.graph = None
         self._ahead = None
         self._static = None
@@ -114,7 +116,7 @@ class DataParallelTrainer:
             # one kernel = all-reduce of [grads || metrics] + AdamW + metrics fold
             self.xg = create_for(mesh, cfg.axis, P.grad.numel(), P.grad.device, cfg.comm)
             self._xg_fused_opt = self.xg is not None and isinstance(state.tx, AdamW)
-        if self.world > 1 and cfg.overlap and self.xg is None:
+        if self._coll and cfg.overlap and self.xg is None:
             from ..comm.buckets import GradBuckets
 
             self.buckets = GradBuckets(P, mesh, cfg.axis, int(cfg.bucket_mb * (1 << 20)))
@@ -141,8 +143,9 @@ class DataParallelTrainer:
         if self.fused is None:
             from .fused_mlp import make_engine
 
+            # a step with a collective keeps the optimizer out of the backward epilogue
             self.fused = make_engine(self.state, self.mesh, self.cfg.axis, self.cfg.num_minibatches, batch.size,
-                                     self.metrics, batch.inputs.device)
+                                     self.metrics, batch.inputs.device, fuse_opt=False if self._coll else None)
             if self.fused is None:
                 self.cfg.accum = "fused"  # shapes outside the fused kernels' envelope
                 return None
@@ -303,7 +306,7 @@ class DataParallelTrainer:
         """pmean(grads) + psum(metrics) as SUM all-reduce(s) of the flat bucket(s); the
         1/N of the mean is applied by the optimizer."""
         P = self.state.params
-        if self.world == 1:
+        if not self._coll:
             return
         with named_scope("sync_grads"):
             if self.xg is not None:
@@ -361,18 +364,24 @@ class DataParallelTrainer:
         (~10-30 us of host time) is amortised over several ~20 us steps.
         ``run_steps`` uses it; ``step`` replays the 1-step graph."""
         assert batch.inputs.is_cuda
+        from ..runtime.dist import collectives_capturable
+
         self._static = batch
-        self._capturing = True  # from now on the step's collectives are whole-buffer, outside graphs
-        one_graph = self.world == 1 or capture_collectives or self.xg is not None  # xGMI collectives are kernels
+        self._capturing = True  # from now on the step's collectives are whole-buffer (no per-bucket overlap)
+        # the collective inside the step graph: xGMI collectives are kernels, RCCL enqueues
+        # on the capturing stream (reference: the whole step under one jit,
+        # data_paral.py:241-251); only a gloo group runs it on the host between graphs
+        one_graph = (not self._coll or capture_collectives or self.xg is not None or collectives_capturable())
         if one_graph:
             def body():
                 self.compute(batch)
                 self.sync()
                 self.update_noncounting()
 
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                body()
+            g = capture_graph(body)
+            if g is None:   # the collective refused capture: compute / RCCL eager / update graphs
+                self._capture_split(batch)
+                return
             self.graph = ("one", g)
             self.multi = None
             self._ahead = None
@@ -398,12 +407,17 @@ class DataParallelTrainer:
                             body()
                 self.multi = (steps_per_graph, gm)
         else:
-            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1):
-                self.compute(batch)
-            with torch.cuda.graph(g2):
-                self.update_noncounting()
-            self.graph = ("split", g1, g2)
+            self._capture_split(batch)
+
+    def _capture_split(self, batch: Batch):
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1):
+            self.compute(batch)
+        with torch.cuda.graph(g2):
+            self.update_noncounting()
+        self.graph = ("split", g1, g2)
+        self.multi = None
+        self._ahead = None
 
     def update_noncounting(self):
         P = self.state.params
@@ -430,7 +444,7 @@ class DataParallelTrainer:
         bucket all-reduce (xGMI: with the fused AdamW + metrics fold) -- bracketed by
         hipEvents in separate, untimed eager steps (complete training steps: they
         advance the state like any other).  None for N = 1 or off-GPU."""
-        if self.world == 1 or not self.state.params.master.is_cuda:
+        if not self._coll or not self.state.params.master.is_cuda:
             return None
         ts = []
         for _ in range(iters):
@@ -454,7 +468,7 @@ class DataParallelTrainer:
 
     @property
     def comm_backend(self) -> str:
-        if self.world == 1:
+        if not self._coll:
             return "none"
         if self.xg is not None:
             return "xgmi"
@@ -492,6 +506,24 @@ class DataParallelTrainer:
             self.sync()
             self.graph[2].replay()
         self.state.step += 1
+
+
+def capture_graph(body, pool=None) -> Optional[torch.cuda.CUDAGraph]:
+    """``body`` recorded into a hipGraph, or None if a collective in it refused stream
+    capture (the caller then keeps that collective eager).  RCCL collectives enqueue
+    on the capturing stream and are recorded like kernels."""
+    g = torch.cuda.CUDAGraph()
+    try:
+        with torch.cuda.graph(g, pool=pool):
+            body()
+    except RuntimeError as e:
+        import logging
+
+        logging.getLogger(__name__).warning("step capture with the collective inside failed (%s); "
+                                            "running the collective eagerly between graphs", e)
+        torch.cuda.synchronize()
+        return None
+    return g
 
 
 def train_step_dp(trainer: DataParallelTrainer, batch: Batch):

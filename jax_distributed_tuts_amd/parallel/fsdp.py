@@ -428,6 +428,10 @@ class FSDPTrainer:
         self.model: MLP = state.apply_fn
         self.metrics = torch.zeros(N_METRIC_SLOTS, dtype=torch.float32, device=self.sp.local.master.device)
         self.world = C.axis_size(mesh, cfg.axis)
+        # one device and no collective to issue: gather / reduce-scatter are identities and
+        # the step is the DP engine on the local buffer (a Mesh(unit_groups=True) keeps the
+        # N > 1 schedule, RCCL calls included, on one GPU)
+        self._n1 = not (self.world > 1 or C.active(mesh, cfg.axis))
         self.fused = None
         self.graph = None
         self._ahead = None
@@ -482,7 +486,7 @@ class FSDPTrainer:
 
     @property
     def comm_backend(self) -> str:
-        if self.world == 1:
+        if self._n1:
             return "none"
         if self.sp.xg is not None:
             return "xgmi"
@@ -506,7 +510,7 @@ class FSDPTrainer:
         if self.fused is None:
             from .fused_mlp import make_engine
 
-            if self.world == 1:
+            if self._n1:
                 # one device: every shard is the whole leaf (param_sharding.py:89-113 at
                 # N=1) and the gather / reduce-scatter are identities, so the step is the
                 # DP engine on the local buffer with AdamW in the backward epilogue
@@ -519,7 +523,7 @@ class FSDPTrainer:
             if self.fused is None:
                 self.cfg.fused_kernels = False
                 return False
-        if self.world == 1:
+        if self._n1:
             self.fused.forward_backward(batch)
             if not self.fused.fuse_opt:
                 self.state.tx.update(sp.local, self.state.opt_state, 1.0 / self.cfg.num_minibatches, zero_grad=False)
@@ -566,8 +570,15 @@ class FSDPTrainer:
     # ------------------------------------------------------------------ hipGraph
     @property
     def capturable(self) -> bool:
-        """N=1, or every collective of the step is an xGMI kernel (no host-side RCCL)."""
-        return self.world == 1 or (self.sp.xg is not None and len(self.sp._xg_names) == len(self.sp.sharded_names))
+        """N=1, every collective of the step an xGMI kernel, or RCCL (which enqueues on
+        the capturing stream; reference: the step under one jit, param_sharding.py:370-379).
+        Only a gloo group's host-side collectives keep the step eager."""
+        from ..runtime.dist import collectives_capturable
+
+        if self.sp.local.master.device.type != "cuda":
+            return False
+        return (self._n1 or (self.sp.xg is not None and len(self.sp._xg_names) == len(self.sp.sharded_names))
+                or collectives_capturable())
 
     def capture(self, batch: Batch, steps_per_graph: int = 1):
         """Record the whole step (gather, fwd/bwd, reduce-scatter, replicated
@@ -578,15 +589,18 @@ class FSDPTrainer:
         if not self._full_fresh:   # the fused step collective keeps the full shadow current
             self.sp.gather()
             self._full_fresh = True
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._body(batch)
+        from .dp import capture_graph
+
+        g = capture_graph(lambda: self._body(batch))
+        if g is None:   # a collective refused stream capture: the step stays eager
+            self.graph = None
+            return False
         self.graph = g
         # N = 1 on the fused engine with AdamW in its epilogue: one run-ahead launch per
         # step (the DP engine's schedule, fused_mlp.AheadGraphs)
         eng = self.fused
         self._ahead = None
-        if self.world == 1 and eng is not None and getattr(eng, "ahead_ok", False):
+        if self._n1 and eng is not None and getattr(eng, "ahead_ok", False):
             from .fused_mlp import AheadGraphs
 
             self._ahead = AheadGraphs(eng, batch, steps_per_graph, pool=g.pool())
@@ -598,6 +612,7 @@ class FSDPTrainer:
                 for _ in range(steps_per_graph):
                     self._body(batch)
             self.multi = (steps_per_graph, gm)
+        return True
 
     def run_steps(self, batch: Batch, n: int):
         if self.graph is not None:
@@ -622,14 +637,14 @@ class FSDPTrainer:
 
             sp = self.sp
             dev = sp.local.master.device
-            coll_ok = self.world == 1 or (sp.xg is not None and len(sp._xg_names) == len(sp.sharded_names))
+            coll_ok = self._n1 or (sp.xg is not None and len(sp._xg_names) == len(sp.sharded_names))
             if self.cfg.fused_loop and coll_ok and stage_supported(self.model, mb, dev):
                 from .pipeline import hw_queues
 
                 k = min(int(self.cfg.loop_streams) or (2 if self.model.L >= 3 else 1), hw_queues())
                 self._loop_engine = FusedMLPStage(self.model, _LoopView(sp), self.cfg.num_minibatches, mb,
                                                   self.state.step_tensor, seed,
-                                                  n_sets=min(k, self.cfg.num_minibatches) if self.world == 1 else 1)
+                                                  n_sets=min(k, self.cfg.num_minibatches) if self._n1 else 1)
                 # sharded leaves' full-grad range (zeroed after each minibatch's reduce-scatter)
                 offs = sorted((sp.full.offsets[n][0], sp.full.g(n).numel()) for n in sp.sharded_names)
                 self._shard_full = [sp.full.grad[o:o + n] for o, n in offs]
@@ -658,13 +673,13 @@ class FSDPTrainer:
                 for s_ in self._loop_streams:
                     s_.wait_stream(main)
             for i in range(n_mb):
-                if self.world > 1 and (i == 0 or not cfg.gather_once):
+                if not self._n1 and (i == 0 or not cfg.gather_once):
                     sp.xg.all_gather_segments([(sp.full.s(n), sp.local.s(n)) for n in sp._xg_names])
                 with (torch.cuda.stream(self._loop_streams[i % k - 1]) if (k > 1 and i % k)
                       else contextlib.nullcontext()):
                     eng.forward(i, batch.inputs[i * mb:(i + 1) * mb])
                     eng.backward(i, labels=batch.labels[i * mb:(i + 1) * mb])
-                if self.world > 1 and (not cfg.scatter_once or i == n_mb - 1):
+                if not self._n1 and (not cfg.scatter_once or i == n_mb - 1):
                     with named_scope("scatter_grads"):
                         sp.xg.reduce_scatter_segments([(sp.full.g(n), sp.local.g(n)) for n in sp._xg_names],
                                                       accumulate=True)
@@ -674,7 +689,7 @@ class FSDPTrainer:
                 for s_ in self._loop_streams:
                     main.wait_stream(s_)
                 eng.merge()
-            if self.world > 1:
+            if not self._n1:
                 sp.sync_replicated()
             st.tx.update(sp.local, st.opt_state, 1.0 / (n_mb * self.world))
             with named_scope("synch_metrics"):
@@ -695,7 +710,7 @@ class FSDPTrainer:
             K.metrics_fold_(self.metrics, sp.local.metrics_slot)
 
     def finalize(self):
-        if self.fused is not None and self.world == 1:
+        if self.fused is not None and self._n1:
             self.fused.finalize()  # bf16 shadow parity of the in-epilogue AdamW
         if self.sp.xg is not None and self.sp.xg.error():
             raise RuntimeError("xgmi collective timed out on this rank (peer dead or desynchronised)")

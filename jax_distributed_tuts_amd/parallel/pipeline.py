@@ -262,15 +262,20 @@ class GPipeTrainer:
 
     @property
     def capturable(self) -> bool:
-        """Whether the step is kernels only (no host-driven collective)."""
-        return (self.dev.type == "cuda" and (self.S == 1 or self.p2p is not None)
-                and (self.n_dp == 1 or self.xg is not None))
+        """Whether the step can be recorded as a hipGraph: every hand-off and collective
+        is an xGMI kernel or an RCCL call (RCCL send / recv / all-reduce enqueue on the
+        capturing stream); a gloo group's host-side ops keep it eager."""
+        from ..runtime.dist import collectives_capturable
+
+        rccl = collectives_capturable()
+        return (self.dev.type == "cuda" and (self.S == 1 or self.p2p is not None or rccl)
+                and (self.n_dp == 1 or self.xg is not None or rccl))
 
     @property
     def comm_backend(self) -> str:
         if self.S * self.n_dp == 1:
             return "none"
-        if self.capturable:
+        if (self.S == 1 or self.p2p is not None) and (self.n_dp == 1 or self.xg is not None):
             return "xgmi"
         from ..runtime.dist import backend
 
@@ -634,9 +639,12 @@ class GPipeTrainer:
             self._compute(batch)
             self._sync_update()
 
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            body()
+        from .dp import capture_graph
+
+        g = capture_graph(body)
+        if g is None:   # a collective refused stream capture: the step stays eager
+            self.graph = None
+            return False
         self.graph = g
         # one stage on the deep fused engine: layer 0's forward of the next step rides in
         # the layer-0 backward (run-ahead, fused_mlp.AheadGraphs: cold / primed graphs)
@@ -654,6 +662,7 @@ class GPipeTrainer:
                 for _ in range(steps_per_graph):
                     body()
             self.multi = (steps_per_graph, gm)
+        return True
 
     def run_steps(self, batch: Batch, n: int):
         if self.graph is not None:

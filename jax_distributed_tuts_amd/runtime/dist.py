@@ -94,6 +94,13 @@ def shutdown():
         dist.destroy_process_group()
 
 
+def collectives_capturable() -> bool:
+    """Whether this job's collectives can be recorded into a hipGraph: RCCL (the nccl
+    backend) enqueues every collective on the caller's stream, so torch.cuda.graph
+    captures it; gloo runs on the host and cannot be captured."""
+    return backend() == "nccl"
+
+
 def barrier():
     if is_initialized():
         if backend() == "nccl":
@@ -106,9 +113,14 @@ class Mesh:
     """N-D process mesh.  ``Mesh({"data": 2, "pipe": 4})``: rank = row-major index
     over the axes in the given order (the last axis varies fastest), so with
     ("data", "pipe") the pipe stages of one data replica are consecutive ranks --
-    on an 8-GPU MI355X node every pair is one xGMI hop regardless."""
+    on an 8-GPU MI355X node every pair is one xGMI hop regardless.
 
-    def __init__(self, axes: Dict[str, int] | Sequence[Tuple[str, int]]):
+    ``unit_groups=True`` gives axes of size 1 a real process group too (the world
+    group of a 1-rank job, else a 1-member group), and the collectives of
+    comm/collectives.py then run on them instead of short-circuiting: a one-GPU job
+    issues exactly the RCCL calls (and graph captures) an N-GPU job does."""
+
+    def __init__(self, axes: Dict[str, int] | Sequence[Tuple[str, int]], unit_groups: bool = False):
         items = list(axes.items()) if isinstance(axes, dict) else list(axes)
         self.axis_names: Tuple[str, ...] = tuple(a for a, _ in items)
         self.shape: Tuple[int, ...] = tuple(int(s) for _, s in items)
@@ -116,6 +128,7 @@ class Mesh:
         if math.prod(self.shape) != ws:
             raise ValueError(f"mesh {dict(items)} needs {math.prod(self.shape)} ranks, world has {ws}")
         self.rank = rank()
+        self.unit_groups = bool(unit_groups) and is_initialized()
         self.coords = self._coords(self.rank)
         self._groups: Dict[str, Optional[dist.ProcessGroup]] = {}
         self._group_ranks: Dict[str, Tuple[int, ...]] = {}
@@ -123,12 +136,12 @@ class Mesh:
             mine = None
             # every rank must create every group, in the same order
             for line in self._lines(ai):
-                g = dist.new_group(list(line)) if (is_initialized() and self.shape[ai] > 1 and
-                                                    self.shape[ai] != ws) else None
+                g = dist.new_group(list(line)) if (is_initialized() and self.shape[ai] != ws and
+                                                    (self.shape[ai] > 1 or self.unit_groups)) else None
                 if self.rank in line:
                     mine = (g, line)
             g, line = mine
-            if is_initialized() and self.shape[ai] == ws and ws > 1:
+            if is_initialized() and self.shape[ai] == ws and (ws > 1 or self.unit_groups):
                 g = dist.group.WORLD
             self._groups[a] = g
             self._group_ranks[a] = tuple(line)

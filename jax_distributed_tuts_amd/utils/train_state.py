@@ -299,7 +299,15 @@ def accum_grads_scan(batch: Batch, state: TrainState, key: int, n_minbatch: int,
       split key with the device index selecting one -- the reference's
       ``keys[batch_idx]`` (util.py:107-108) -- so models' dropout draws the loop's
       masks exactly (tests/test_reference_loss_fn.py).  A loss whose ops cannot be
-      captured runs the same body eagerly, with a warning."""
+      captured runs the same body eagerly, with a warning.
+
+    The captured minibatch program is cached (like ``jax.jit``'s trace cache) under
+    (loss_fn, parameter / gradient buffers, minibatch shape and dtypes, n_minbatch):
+    the next call only loads its minibatches into the slots and replays.  A
+    reference-contract call refreshes the device copy of its split keys in place, so
+    a training loop whose rng changes every step captures once; an engine-contract
+    loss receives ``key`` as a host int, which a graph bakes in, so the key is part
+    of its cache entry."""
     bs = batch.size
     mb = bs // n_minbatch
     dev = batch.inputs.device
@@ -308,43 +316,87 @@ def accum_grads_scan(batch: Batch, state: TrainState, key: int, n_minbatch: int,
         return _accum_scan_reference(batch, state, key, n_minbatch, loss_fn)
     if dev.type != "cuda":
         return accum_grads_loop(batch, state, key, n_minbatch, loss_fn)
-    # device-resident slot the captured step reads its minibatch from
-    xin = torch.empty((mb,) + tuple(batch.inputs.shape[1:]), dtype=batch.inputs.dtype, device=dev)
-    yin = torch.empty((mb,), dtype=batch.labels.dtype, device=dev)
-    mslot = {}
-    idx = torch.zeros(1, dtype=torch.int32, device=dev)
-
-    def _body(i: int):
-        _, m = loss_fn(state.params, state.apply_fn, Batch(xin, yin), key, minibatch_index=idx, state=state)
-        mslot["m"] = m
-
+    ck = _scan_key("engine", batch, state, n_minbatch, loss_fn) + (int(key),)
+    ent = _SCAN_CACHE.get(ck)
     metrics = None
-    # warm up on minibatch 0 eagerly (allocations, library load), then capture the body once
-    xin.copy_(batch.inputs[0:mb])
-    yin.copy_(batch.labels[0:mb])
-    _body(0)
-    metrics = _metrics_add(metrics, _clone_metrics(mslot["m"]))
-    g = torch.cuda.CUDAGraph()
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        xin.copy_(batch.inputs[mb:2 * mb]) if n_minbatch > 1 else None
-        yin.copy_(batch.labels[mb:2 * mb]) if n_minbatch > 1 else None
-    torch.cuda.current_stream().wait_stream(s)
-    if n_minbatch > 1:
-        with torch.cuda.graph(g):
-            _body(1)
-        for i in range(1, n_minbatch):
-            xin.copy_(batch.inputs[i * mb:(i + 1) * mb])
-            yin.copy_(batch.labels[i * mb:(i + 1) * mb])
-            idx.fill_(i)
-            g.replay()
-            metrics = _metrics_add(metrics, _clone_metrics(mslot["m"]))
+    if ent is None:
+        # device-resident slot the captured step reads its minibatch from
+        xin = torch.empty((mb,) + tuple(batch.inputs.shape[1:]), dtype=batch.inputs.dtype, device=dev)
+        yin = torch.empty((mb,), dtype=batch.labels.dtype, device=dev)
+        mslot = {}
+        idx = torch.zeros(1, dtype=torch.int32, device=dev)
+
+        def _body():
+            _, m = loss_fn(state.params, state.apply_fn, Batch(xin, yin), key, minibatch_index=idx, state=state)
+            mslot["m"] = m
+
+        # warm up on minibatch 0 eagerly (allocations, library load), then capture the body once
+        _scan_load(batch, xin, yin, idx, 0, mb)
+        _body()
+        metrics = _metrics_add(metrics, _clone_metrics(mslot["m"]))
+        g = None
+        if n_minbatch > 1:
+            _scan_load(batch, xin, yin, idx, 1, mb)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                _body()
+            SCAN_STATS["captures"] += 1
+        ent = _SCAN_CACHE.put(ck, {"graph": g, "xin": xin, "yin": yin, "idx": idx, "out": mslot})
+        first = 1
+    else:
+        first = 0
+    for i in range(first, n_minbatch):
+        _scan_load(batch, ent["xin"], ent["yin"], ent["idx"], i, mb)
+        ent["graph"].replay()
+        metrics = _metrics_add(metrics, _clone_metrics(ent["out"]["m"]))
     return GradBuffer(state.params, 1.0 / n_minbatch), metrics
 
 
 def _clone_metrics(m: Metrics) -> Metrics:
     return {k: tuple(x.clone() if torch.is_tensor(x) else x for x in v) for k, v in m.items()}
+
+
+class _LRU:
+    """A small least-recently-used map (captured scan programs hold graph memory)."""
+
+    def __init__(self, cap: int = 8):
+        from collections import OrderedDict
+
+        self.cap, self.d = cap, OrderedDict()
+
+    def get(self, k):
+        v = self.d.get(k)
+        if v is not None:
+            self.d.move_to_end(k)
+        return v
+
+    def put(self, k, v):
+        self.d[k] = v
+        self.d.move_to_end(k)
+        while len(self.d) > self.cap:
+            self.d.popitem(last=False)
+        return v
+
+    def clear(self):
+        self.d.clear()
+
+
+_SCAN_CACHE = _LRU()
+# captures of a rolled minibatch program since import (tests assert a training loop captures once)
+SCAN_STATS = {"captures": 0}
+
+
+def _scan_key(kind: str, batch: Batch, state: "TrainState", n_minbatch: int, loss_fn) -> tuple:
+    P = state.params
+    return (kind, loss_fn, id(P), P.master.data_ptr(), P.grad.data_ptr(), id(state.apply_fn), n_minbatch,
+            batch.size // n_minbatch, tuple(batch.inputs.shape[1:]), batch.inputs.dtype, batch.labels.dtype,
+            str(batch.inputs.device))
+
+
+def _scan_load(batch: Batch, xin, yin, idx, i: int, mb: int):
+    xin.copy_(batch.inputs[i * mb:(i + 1) * mb])
+    yin.copy_(batch.labels[i * mb:(i + 1) * mb])
+    idx.fill_(i)
 
 
 # (grads buffer, capture outcome) of the most recent reference-contract scan, for tests / logs
@@ -357,22 +409,29 @@ def _accum_scan_reference(batch: Batch, state: TrainState, key: int, n_minbatch:
     bs = batch.size
     mb = bs // n_minbatch
     dev = batch.inputs.device
+    keys = R.split(key, n_minbatch)
+    ck = _scan_key("reference", batch, state, n_minbatch, loss_fn)
+    ent = _SCAN_CACHE.get(ck) if (dev.type == "cuda" and n_minbatch > 1) else None
+    metrics = None
+    if ent is not None:
+        # cached program: this call's split keys into the device key table it reads
+        ent["skey"].dev.copy_(torch.tensor([R._s64(k) for k in keys], dtype=torch.int64))
+        LAST_SCAN_MODE["mode"] = "graph"
+        for i in range(n_minbatch):
+            _scan_load(batch, ent["xin"], ent["yin"], ent["idx"], i, mb)
+            ent["graph"].replay()
+            metrics = _metrics_add(metrics, _clone_metrics(ent["out"]["m"]))
+        return GradBuffer(state.params, 1.0 / n_minbatch), metrics
     xin = torch.empty((mb,) + tuple(batch.inputs.shape[1:]), dtype=batch.inputs.dtype, device=dev)
     yin = torch.empty((mb,), dtype=batch.labels.dtype, device=dev)
     idx = torch.zeros(1, dtype=torch.int32, device=dev)
-    skey = R.ScanKey.from_keys(R.split(key, n_minbatch), idx)
+    skey = R.ScanKey.from_keys(keys, idx)
     out = {}
 
     def _body():
         out["m"] = value_and_grad_into(loss_fn, state, Batch(xin, yin), skey)[1]
 
-    def _load(i: int):
-        xin.copy_(batch.inputs[i * mb:(i + 1) * mb])
-        yin.copy_(batch.labels[i * mb:(i + 1) * mb])
-        idx.fill_(i)
-
-    metrics = None
-    _load(0)
+    _scan_load(batch, xin, yin, idx, 0, mb)
     _body()   # minibatch 0 eagerly: warm-up (allocations, autograd graph, kernel library)
     metrics = _metrics_add(metrics, _clone_metrics(out["m"]))
     if n_minbatch == 1:
@@ -380,12 +439,14 @@ def _accum_scan_reference(batch: Batch, state: TrainState, key: int, n_minbatch:
         return GradBuffer(state.params, 1.0), metrics
     graph = None
     if dev.type == "cuda":
-        _load(1)
+        _scan_load(batch, xin, yin, idx, 1, mb)
         g = torch.cuda.CUDAGraph()
         try:
             with torch.cuda.graph(g):
                 _body()
             graph = g
+            SCAN_STATS["captures"] += 1
+            _SCAN_CACHE.put(ck, {"graph": g, "xin": xin, "yin": yin, "idx": idx, "skey": skey, "out": out})
         except Exception as e:   # an op of the user's loss that cannot be captured
             import logging
 
@@ -394,7 +455,7 @@ def _accum_scan_reference(batch: Batch, state: TrainState, key: int, n_minbatch:
             torch.cuda.synchronize()
     LAST_SCAN_MODE["mode"] = "graph" if graph is not None else "eager"
     for i in range(1, n_minbatch):
-        _load(i)
+        _scan_load(batch, xin, yin, idx, i, mb)
         if graph is not None:
             graph.replay()
         else:

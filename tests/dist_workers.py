@@ -313,3 +313,40 @@ def selftest_verdict(out_dir):
     t = torch.tensor([float(len(seen))])
     dist.all_reduce(t)  # pairs up only if every rank stopped at the same check
     _save(out_dir, "verdict", {"seen": seen, "total": float(t.item())})
+
+
+def unit_groups(out_dir):
+    """A 1-rank gloo job whose 1-member data axis is a real process group
+    (Mesh(unit_groups=True)): DP and FSDP issue their collectives exactly as at N > 1
+    and must train exactly like the plain N = 1 step (CPU: bitwise)."""
+    import torch.distributed as dist
+
+    from data_paral import synthetic_batch
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
+    from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.train_state import adamw
+
+    dist.init_process_group("gloo", init_method="env://", rank=0, world_size=1)
+    res = {}
+    try:
+        b = synthetic_batch(dp_config(), 70)
+        for unit in (False, True):
+            mesh = Mesh({"data": 1}, unit_groups=unit)
+            res[f"active_{unit}"] = C.active(mesh, "data")
+            st = init_dp(Classifier(dropout_rate=0.0), adamw(1e-3), 69, "cpu", mesh)
+            tr = DataParallelTrainer(st, mesh, DPConfig(4, "loop"))
+            res[f"dp_coll_{unit}"] = tr._coll
+            for _ in range(3):
+                tr.step(b)
+            res[f"dp_{unit}"] = st.params.master.clone()
+            st = init_fsdp(Classifier(num_layers=4, dropout_rate=0.0), adamw(1e-3), 69, "cpu", mesh, "data", 16)
+            tr = FSDPTrainer(st, mesh, FSDPConfig(4, 16, "data"))
+            res[f"fsdp_n1_{unit}"] = tr._n1
+            for _ in range(3):
+                tr.step(b)
+            res[f"fsdp_{unit}"] = st.params.master.clone()
+    finally:
+        dist.destroy_process_group()
+    _save(out_dir, "unit", res)

@@ -121,3 +121,32 @@ def test_reference_scan_equals_loop_cpu():
 @pytest.mark.gpu
 def test_reference_scan_equals_loop_gpu_captured():
     assert _scan_vs_loop(torch.device("cuda", 0)) == "graph"
+
+
+@pytest.mark.gpu
+def test_rolled_step_captures_once_over_a_training_loop():
+    """A 10-step training loop through util.accum_grads(use_scan=True) (the reference's
+    train_step body, a fresh rng every step) captures the minibatch program ONCE and
+    replays it every later step -- and every step equals the unrolled loop's
+    gradient and metrics bit for bit (same dropout masks: the cached program's device
+    key table is refreshed per call)."""
+    from jax_distributed_tuts_amd.utils import train_state as TS
+
+    dev = torch.device("cuda", 0)
+    runs = []
+    for use_scan in (False, True):
+        st, _, bd = _setup(dev, 0.1)
+        c0 = TS.SCAN_STATS["captures"]
+        grads_seen, losses = [], []
+        for _ in range(10):
+            rng, step_rng = R.split(st.rng)
+            grads, m = accum_grads(st, bd, step_rng, 4, loss_fn=loss_fn, use_scan=use_scan)
+            grads_seen.append(st.params.grad.clone())
+            losses.append((float(m["loss"][0]), float(m["accuracy"][0])))
+            st = st.apply_gradients(grads=grads, rng=rng)
+        runs.append((grads_seen, losses, TS.SCAN_STATS["captures"] - c0))
+    (g_loop, l_loop, c_loop), (g_scan, l_scan, c_scan) = runs
+    assert c_loop == 0 and c_scan == 1
+    assert l_loop == l_scan
+    for a, b in zip(g_loop, g_scan):
+        assert torch.equal(a, b)

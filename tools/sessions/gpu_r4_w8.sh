@@ -5,6 +5,10 @@
 # config's layout at 8 ranks.  Code-path checks, not link numbers.
 cd /root/repo && export TMPDIR=/tmp PYTHONUNBUFFERED=1 && mkdir -p gpurun_out/w8
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+timeout -k 10 300 python -u -m pytest tests/test_rccl_capture_gpu.py tests/test_reference_loss_fn.py -x -v --timeout 120 \
+  --timeout-method thread > gpurun_out/w8/pytest_rccl.log 2>&1
+rc=$?; echo "pytest rccl-capture + scan-cache rc=$rc"; grep -E "PASSED|FAILED|ERROR" gpurun_out/w8/pytest_rccl.log | tail -20
+[ $rc -ne 0 ] && { tail -30 gpurun_out/w8/pytest_rccl.log; exit $rc; }
 timeout -k 10 900 python -u -m pytest tests/test_xgmi_gpu.py -x -v --timeout 240 --timeout-method thread \
   > gpurun_out/w8/pytest_xgmi.log 2>&1
 rc=$?; echo "pytest xgmi rc=$rc"; grep -E "PASSED|FAILED|ERROR" gpurun_out/w8/pytest_xgmi.log | tail -40

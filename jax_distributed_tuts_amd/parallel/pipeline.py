@@ -160,7 +160,11 @@ def _no_dropout(model) -> bool:
 
 
 def hw_queues() -> int:
-    """HIP hardware queues per process (GPU_MAX_HW_QUEUES; HIP's default is 4)."""
+    """HIP hardware queues per process (GPU_MAX_HW_QUEUES; HIP's default is 4), the cap
+    on concurrent-stream schedules.  ``JDT_HWQ_CAP=0`` lifts the cap (diagnosis of the
+    more-streams-than-queues case, tools/sessions/gpu_r4_hwq.sh)."""
+    if os.environ.get("JDT_HWQ_CAP", "1") == "0":
+        return 1 << 10
     try:
         return max(1, int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))
     except ValueError:

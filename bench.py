@@ -173,6 +173,20 @@ def _comm_choice():
     return xgmi.LAST_CALIBRATION
 
 
+def comm_check(tr, where: str):
+    """Raise (naming the phase of the run) if an in-kernel xGMI wait of this rank timed
+    out so far -- the collective, the FSDP context or a pipeline inbox (synchronises)."""
+    for xg in (getattr(tr, "xg", None), getattr(getattr(tr, "sp", None), "xg", None)):
+        if xg is not None:
+            try:
+                xg.raise_if_error()
+            except RuntimeError as e:
+                raise RuntimeError(f"[{where}] {e}") from None
+    p2p = getattr(tr, "p2p", None)
+    if p2p is not None and p2p.error():
+        raise RuntimeError(f"[{where}] xgmi pipeline receive timed out on this rank")
+
+
 def pick_steps_per_graph(steps: int, cap: int) -> int:
     """Steps per captured graph: all of them when steps <= cap (one replay, one host
     launch for the whole timed region), else the largest divisor of steps <= cap
@@ -256,6 +270,8 @@ def main():
 
     run(max(0, args.warmup - n_eager))
     sync()
+    if ws > 1 and on_gpu:
+        comm_check(tr, "warmup")
     D.barrier()
     sync()
     t0 = time.perf_counter()
@@ -268,6 +284,8 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=dev if D.backend() == "nccl" else "cpu")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
+    if ws > 1 and on_gpu:
+        comm_check(tr, "timed steps")
     # per-step latency distribution (separate, untimed pass)
     p50 = p90 = None
     if on_gpu:
@@ -309,6 +327,7 @@ def main():
         desc["step_launches"] = f"{2 * nh - 1} (layer-0 run-ahead md_bwd)" if nh else "1 (run-ahead mlp2_bwd)"
     if args.strategy == "pp":
         desc["single_stage_mode"] = tr.single_stage_mode  # how a 1-stage pipeline ran its microbatches
+        desc["stage_streams"] = tr.stage_streams          # concurrent microbatch chains per stage
     if D.rank() == 0:
         out = {"metric": METRIC, "value": round(sps, 2), "unit": "steps/s", "n_gpus": ws, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 5), "higher_is_better": True,

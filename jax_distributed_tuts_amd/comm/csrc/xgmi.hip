@@ -52,6 +52,8 @@ struct XgSignal {
   unsigned flag[2][XG_MAX_BLOCKS][XG_MAX_RANKS];  // [barrier][block][src rank], written by the peers
   unsigned epoch[XG_MAX_BLOCKS];                   // calls completed by each local block
   int err;                                         // 1 = a barrier timed out
+  // the first timeout's site (kernel * 2 + barrier), block, awaited epoch, silent peer
+  unsigned errinfo[4];
   // local only (never touched by peers): every launch on this context advances `calls`
   // once (its last block, by `call_ticket`); the parity of `calls` selects the
   // data / tmp half of every unstaged call.  Per-block epoch parity cannot: a block that
@@ -114,7 +116,10 @@ __device__ __forceinline__ float4 add4(float4 a, float4 b) {
 // maintenance instruction is needed.  (A release/acquire pair would lower to
 // a write-back / invalidate of the whole L2 -- per wave, and per spin iteration
 // on the acquire side: measured ~70 us for a 1 MB all-reduce, tools/bench_comm.py.)
-__device__ void xg_barrier(const XgPeers& P, int rank, int W, int which, unsigned epoch, long long timeout) {
+// site: kernel id (XG_SITE_*) * 2 + which, recorded with the first timeout (errinfo)
+enum { XG_SITE_TWOSHOT = 1, XG_SITE_ONESHOT = 2, XG_SITE_SEG = 3, XG_SITE_FSDP = 4 };
+__device__ void xg_barrier(const XgPeers& P, int rank, int W, int which, unsigned epoch, long long timeout,
+                           int kernel = 0) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int b = blockIdx.x;
@@ -125,7 +130,14 @@ __device__ void xg_barrier(const XgPeers& P, int rank, int W, int which, unsigne
     const unsigned long long t0 = xg_now();
     while ((int)(__hip_atomic_load(&me->flag[which][b][q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
       if ((long long)(xg_now() - t0) > timeout) {
-        __hip_atomic_store(&me->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        int zero = 0;
+        if (__hip_atomic_compare_exchange_strong(&me->err, &zero, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_SYSTEM)) {
+          me->errinfo[0] = (unsigned)(kernel * 2 + which);
+          me->errinfo[1] = (unsigned)b;
+          me->errinfo[2] = epoch;
+          me->errinfo[3] = (unsigned)q;
+        }
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -150,7 +162,7 @@ __device__ __forceinline__ void store_guard(float* dst, long e, long n, float4 x
   if (e + 2 < n) dst[e + 2] = x.z;
 }
 
-__device__ __forceinline__ void adam4(const XgAdam& A, long e, float4 g, float rbc1, float rbc2) {
+__device__ __forceinline__ float4 adam4(const XgAdam& A, long e, float4 g, float rbc1, float rbc2) {
   float4 pp = *reinterpret_cast<float4*>(A.p + e);
   float4 mm = *reinterpret_cast<float4*>(A.m + e);
   float4 vv = *reinterpret_cast<float4*>(A.v + e);
@@ -171,6 +183,7 @@ __device__ __forceinline__ void adam4(const XgAdam& A, long e, float4 g, float r
     s.y = (unsigned)f2bf(pp.z) | ((unsigned)f2bf(pp.w) << 16);
     *reinterpret_cast<uint2*>(A.shadow + e) = s;
   }
+  return pp;
 }
 
 // Caller layout: rank q's part of the full vector is [q*s, q*s + s) (s % 4 == 0),
@@ -221,7 +234,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
         sys_store4(my_data, half + q * slice + j, x);
       }
     }
-    xg_barrier(P, rank, W, 0, epoch, timeout);
+    xg_barrier(P, rank, W, 0, epoch, timeout, XG_SITE_TWOSHOT);
     // phase 1: reduce chunk b of part `rank` over the peers (all W loads in flight,
     // fixed rank order -> every rank computes bit-identical sums)
     for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
@@ -249,7 +262,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
       sys_store4(my_tmp, half + rank * slice + j, x);
     }
   }
-  xg_barrier(P, rank, W, 1, epoch, timeout);
+  xg_barrier(P, rank, W, 1, epoch, timeout, XG_SITE_TWOSHOT);
 
   // phase 2: gather chunk b of every part (all W loads in flight per thread)
   float rbc1 = 1.f, rbc2 = 1.f;
@@ -333,7 +346,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_oneshot_kernel(XgPeers P, int r
     const float4 x = j < n ? load_guard(in, j, n) : make_float4(0.f, 0.f, 0.f, 0.f);
     sys_store4(my_data, half + j, x);
   }
-  xg_barrier(P, rank, W, 0, epoch, timeout);
+  xg_barrier(P, rank, W, 0, epoch, timeout, XG_SITE_ONESHOT);
   float rbc1 = 1.f, rbc2 = 1.f;
   if (fuse) {
     const int t = A.step[0] + 1;
@@ -458,7 +471,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_seg_kernel(XgPeers P, int rank,
         sys_store4(my_data, half + q * slice + j, x);
       }
     }
-    xg_barrier(P, rank, W, 0, epoch, timeout);
+    xg_barrier(P, rank, W, 0, epoch, timeout, XG_SITE_SEG);
     __amdgpu_buffer_rsrc_t rdata[W];
 #pragma unroll
     for (int q = 0; q < W; ++q) rdata[q] = sys_rsrc(P.data[q], bytes);
@@ -488,7 +501,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_seg_kernel(XgPeers P, int rank,
       }
       sys_store4(my_tmp, half + rank * slice + j, x);
     }
-    xg_barrier(P, rank, W, 1, epoch, timeout);
+    xg_barrier(P, rank, W, 1, epoch, timeout, XG_SITE_SEG);
     __amdgpu_buffer_rsrc_t rtmp[W];
 #pragma unroll
     for (int q = 0; q < W; ++q) rtmp[q] = sys_rsrc(P.tmp[q], bytes);
@@ -532,7 +545,15 @@ struct XgFsdp {
   const float* grad;               // local grad base: a part's local offset = part - grad
   int kind[XG_MAX_SEGS];
   bf16_t* full_shadow[XG_MAX_SEGS];  // bf16 full leaf (gather / replicated target)
+  // diagnostic (tools/stamp_xg_fsdp.py): per block s_memrealtime at the phase edges
+  // [G][8]: start, stage stored, barrier A, reduce + AdamW, barrier B, gather, end
+  unsigned long long* stamps;
 };
+
+#define XF_STAMP(i)                                                                            \
+  do {                                                                                         \
+    if (F.stamps && threadIdx.x == 0) F.stamps[(long)blockIdx.x * 8 + (i)] = xg_now();       \
+  } while (0)
 
 __device__ __forceinline__ void sys_store8(__amdgpu_buffer_rsrc_t r, long byte_off, uint2 x) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, x), r,
@@ -560,6 +581,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_fsdp_kernel(XgPeers P, int rank
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   const unsigned long long bytes = (unsigned long long)cap * 2ull * sizeof(float);
   const XgAdam& A = F.A;
+  XF_STAMP(0);
 
   // phase 0: stage
   {
@@ -576,7 +598,9 @@ __global__ void __launch_bounds__(XG_THREADS) xg_fsdp_kernel(XgPeers P, int rank
       }
     }
   }
-  xg_barrier(P, rank, W, 0, epoch, timeout);
+  if (F.stamps) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); XF_STAMP(1); }
+  xg_barrier(P, rank, W, 0, epoch, timeout, XG_SITE_FSDP);
+  XF_STAMP(2);
 
   // phase 1: reduce own part, optimizer, publish the new bf16 shard
   float rbc1, rbc2;
@@ -614,19 +638,26 @@ __global__ void __launch_bounds__(XG_THREADS) xg_fsdp_kernel(XgPeers P, int rank
       const long lo = (g.part - F.grad) + jj;   // local flat offset of element jj of this part
       const float* ga = &acc.x;
       float pn[4] = {0.f, 0.f, 0.f, 0.f};
+      if (jj + 4 <= lim && (lo & 3) == 0) {
+        // whole aligned group: one 16-byte access per state vector (the per-element
+        // path below issues 12 dependent 4-byte loads per group)
+        const float4 pv = adam4(A, lo, acc, rbc1, rbc2);
+        pn[0] = pv.x; pn[1] = pv.y; pn[2] = pv.z; pn[3] = pv.w;
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (jj + e >= lim) break;
-        const float gr = ga[e] * A.grad_scale;
-        const float mm = A.b1 * A.m[lo + e] + (1.f - A.b1) * gr;
-        const float vv = A.b2 * A.v[lo + e] + (1.f - A.b2) * gr * gr;
-        float pp = A.p[lo + e];
-        pp -= A.lr * ((mm * rbc1) / (sqrtf(vv * rbc2) + A.eps) + A.wd * pp);
-        A.m[lo + e] = mm;
-        A.v[lo + e] = vv;
-        A.p[lo + e] = pp;
-        A.shadow[lo + e] = f2bf(pp);
-        pn[e] = pp;
+        for (int e = 0; e < 4; ++e) {
+          if (jj + e >= lim) break;
+          const float gr = ga[e] * A.grad_scale;
+          const float mm = A.b1 * A.m[lo + e] + (1.f - A.b1) * gr;
+          const float vv = A.b2 * A.v[lo + e] + (1.f - A.b2) * gr * gr;
+          float pp = A.p[lo + e];
+          pp -= A.lr * ((mm * rbc1) / (sqrtf(vv * rbc2) + A.eps) + A.wd * pp);
+          A.m[lo + e] = mm;
+          A.v[lo + e] = vv;
+          A.p[lo + e] = pp;
+          A.shadow[lo + e] = f2bf(pp);
+          pn[e] = pp;
+        }
       }
       uint2 pk;
       pk.x = (unsigned)f2bf(pn[0]) | ((unsigned)f2bf(pn[1]) << 16);
@@ -641,7 +672,9 @@ __global__ void __launch_bounds__(XG_THREADS) xg_fsdp_kernel(XgPeers P, int rank
       }
     }
   }
-  xg_barrier(P, rank, W, 1, epoch, timeout);
+  if (F.stamps) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); XF_STAMP(3); }
+  xg_barrier(P, rank, W, 1, epoch, timeout, XG_SITE_FSDP);
+  XF_STAMP(4);
 
   // phase 2: gather every peer's updated bf16 shard into the full shadow
   {
@@ -673,6 +706,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_fsdp_kernel(XgPeers P, int rank
       }
     }
   }
+  if (F.stamps) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); XF_STAMP(5); }
   if (threadIdx.x == 0) me->epoch[b] = epoch;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1047,6 +1081,14 @@ JDT_API int jdt_xgmi_fsdp_step(void* ctx, const XgSegs* segs, const XgFsdp* f, l
 JDT_API int jdt_xgmi_adam_size() { return (int)sizeof(XgAdam); }
 
 JDT_API long jdt_xgmi_capacity(void* ctx) { return static_cast<XgCtx*>(ctx)->cap; }
+
+// The first timeout's [site, block, epoch, peer] (zeros if none; synchronises the device).
+JDT_API int jdt_xgmi_error_info(void* ctx, unsigned* out4) {
+  XgCtx* c = static_cast<XgCtx*>(ctx);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpy(out4, c->sig->errinfo, 4 * sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return 0;
+}
 
 // 1 if any barrier of this rank timed out (synchronises the device).
 JDT_API int jdt_xgmi_error(void* ctx) {

@@ -74,7 +74,8 @@ class XgSegs(ctypes.Structure):
 class XgFsdp(ctypes.Structure):
     """Mirror of ``jdt::XgFsdp``: local AdamW buffers + per-segment kind / bf16 full shadow."""
 
-    _fields_ = [("A", XgAdam), ("grad", c_void_p), ("kind", c_int * MAX_SEGS), ("full_shadow", c_void_p * MAX_SEGS)]
+    _fields_ = [("A", XgAdam), ("grad", c_void_p), ("kind", c_int * MAX_SEGS), ("full_shadow", c_void_p * MAX_SEGS),
+                ("stamps", c_void_p)]
 
 
 FSDP_SHARD, FSDP_REPL, FSDP_METRIC = 0, 1, 2
@@ -95,6 +96,7 @@ _lib.declare("jdt_xgmi_segs_size", c_int, [])
 _lib.declare("jdt_xgmi_capacity", c_long, [c_void_p])
 _lib.declare("jdt_xgmi_adam_size", c_int, [])
 _lib.declare("jdt_xgmi_error", c_int, [c_void_p])
+_lib.declare("jdt_xgmi_error_info", c_int, [c_void_p, c_void_p])
 _lib.declare("jdt_xgmi_stage_part", c_long, [c_void_p, c_long])
 _lib.declare("jdt_xgmi_stage_base", c_void_p, [c_void_p])
 _lib.declare("jdt_xgmi_stage_write", c_int, [c_void_p, c_int, c_void_p, c_long, c_void_p])
@@ -208,6 +210,27 @@ class XgmiComm:
     def error(self) -> int:
         """1 if any in-kernel barrier timed out on this rank (synchronises the device)."""
         return int(_lib.lib().jdt_xgmi_error(self.ctx)) if self.ctx else 0
+
+    SITES = {1: "two-shot all-reduce", 2: "one-shot all-reduce", 3: "segmented RS/AG", 4: "fused FSDP step"}
+
+    def error_info(self) -> Optional[dict]:
+        """Where this rank's first barrier timeout happened (None if none): kernel,
+        barrier (0: after staging, 1: after the reduce), block, awaited epoch and the
+        peer that never signalled."""
+        if not self.ctx or not self.error():
+            return None
+        out = (ctypes.c_uint * 4)()
+        _lib.check(_lib.lib().jdt_xgmi_error_info(self.ctx, out), "jdt_xgmi_error_info")
+        site, blk, ep, q = (int(v) for v in out)
+        return {"kernel": self.SITES.get(site // 2, f"site {site}"), "barrier": site % 2, "block": blk, "epoch": ep,
+                "silent_peer": q, "rank": self.rank, "world": self.world}
+
+    def raise_if_error(self):
+        """RuntimeError naming the timed-out barrier if any in-kernel wait of this rank
+        timed out (a peer dead, desynchronised or not scheduled)."""
+        info = self.error_info()
+        if info is not None:
+            raise RuntimeError(f"xgmi collective timed out on this rank (peer dead or desynchronised): {info}")
 
     def close(self):
         if self.ctx:

@@ -463,8 +463,8 @@ class DataParallelTrainer:
     def finalize(self):
         if self.fused is not None:
             self.fused.finalize()
-        if self.xg is not None and self.xg.error():
-            raise RuntimeError("xgmi collective timed out on this rank (peer dead or desynchronised)")
+        if self.xg is not None:
+            self.xg.raise_if_error()
 
     @property
     def comm_backend(self) -> str:

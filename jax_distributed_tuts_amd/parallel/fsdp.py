@@ -712,8 +712,8 @@ class FSDPTrainer:
     def finalize(self):
         if self.fused is not None and self._n1:
             self.fused.finalize()  # bf16 shadow parity of the in-epilogue AdamW
-        if self.sp.xg is not None and self.sp.xg.error():
-            raise RuntimeError("xgmi collective timed out on this rank (peer dead or desynchronised)")
+        if self.sp.xg is not None:
+            self.sp.xg.raise_if_error()
 
     def full_params(self) -> Dict[str, torch.Tensor]:
         """Gather the fp32 masters (for checks / checkpoints)."""

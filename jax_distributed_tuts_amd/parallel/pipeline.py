@@ -481,9 +481,25 @@ class GPipeTrainer:
         a 4-stream graph on 2 queues crashed the runtime in a probe,
         profiles/r3_lm_mb_streams_ab.txt)."""
         k = min(int(self.cfg.mb_streams), self.cfg.num_microbatches, hw_queues())
-        ok = (self.S == 1 and self.dev.type == "cuda" and self.cfg.defer_wgrad and hasattr(self.model, "weight_grads")
+        ok = (self._streams_ok() and self.cfg.defer_wgrad and hasattr(self.model, "weight_grads")
               and not self.cfg.merge_single_stage)
         return k if ok else 1
+
+    @property
+    def stage_streams(self) -> int:
+        """Streams this stage's microbatch chains ran on (bench JSON)."""
+        if self.stage_engine is not None:
+            return self.stage_engine.n_sets
+        if self.deep_engine is not None:
+            return 1
+        return self._mb_streams_k()
+
+    def _streams_ok(self) -> bool:
+        """Whether this stage may run its microbatch chains on concurrent streams: GPU,
+        and either one stage or every hand-off on the xGMI inbox kernels (per-microbatch
+        slots, stream-ordered reuse: comm/csrc/p2p.hip).  RCCL send / recv issued from
+        several streams of one communicator could pair up out of order across ranks."""
+        return self.dev.type == "cuda" and (self.S == 1 or self.p2p is not None)
 
     def invalidate(self):
         """After a checkpoint restore: drop captured graphs and the stage engine."""
@@ -522,31 +538,58 @@ class GPipeTrainer:
             from .fused_stage import FusedMLPStage, stage_supported
 
             if self.cfg.fused_stage and self.wgrad is None and stage_supported(self.model, mb, self.dev):
+                # S > 1 on the inbox kernels: microbatch i on stream i % k, with its own grad
+                # set (every md-kernel gradient write is a read-modify-write), merged after
+                # the join -- the DP minibatch loop's scheme (FusedMLPStage n_sets)
+                k = self._stage_streams_k()
                 self.stage_engine = FusedMLPStage(self.model, self.state.params, self.cfg.num_microbatches, mb,
-                                                  self.state.step_tensor, seed)
+                                                  self.state.step_tensor, seed, n_sets=k)
         return self.stage_engine
 
+    def _stage_streams_k(self) -> int:
+        """Concurrent streams of a multi-stage MLP stage's microbatch chains (1: serial)."""
+        if self.S == 1 or not self._streams_ok():
+            return 1
+        return max(1, min(int(self.cfg.mb_streams), self.cfg.num_microbatches, hw_queues()))
+
     def _compute_fused(self, batch: Batch, eng, n_mb: int, mb: int):
-        """The same GPipe fill/drain schedule on the fused stage kernels."""
+        """The same GPipe fill/drain schedule on the fused stage kernels.  With
+        ``eng.n_sets`` = k > 1 (S > 1, xGMI inbox hand-offs) microbatch i's receive,
+        compute and send run on stream i % k: a stage starts microbatch i as soon as it
+        arrives while earlier ones still run (latency-bound ticks overlap instead of
+        queueing), and the backward of one microbatch overlaps another's."""
+        k = eng.n_sets
+        if k > 1:
+            if self._mb_streams is None or len(self._mb_streams) != k - 1:
+                self._mb_streams = [torch.cuda.Stream(self.dev) for _ in range(k - 1)]
+            on = _MbStreams(torch.cuda.current_stream(self.dev), self._mb_streams)
+        else:
+            on = _MbStreams(None, None)
+        on.fork()
         for t in range(n_mb + self.S - 1):
             i = t - self.s
             if not (0 <= i < n_mb):
                 continue
-            if self.first:
-                x = batch.inputs[i * mb:(i + 1) * mb]
-            else:
-                x = self._recv(self.model.input_shape(mb), self.act_dtype, self.s - 1, i)
-            out = eng.forward(i, x)
-            if not self.last:
-                self._send(out, self.s + 1, i)
+            with on(i):
+                if self.first:
+                    x = batch.inputs[i * mb:(i + 1) * mb]
+                else:
+                    x = self._recv(self.model.input_shape(mb), self.act_dtype, self.s - 1, i)
+                out = eng.forward(i, x)
+                if not self.last:
+                    self._send(out, self.s + 1, i)
         for i in reversed(range(n_mb)):
-            if self.last:
-                dx = eng.backward(i, labels=batch.labels[i * mb:(i + 1) * mb], need_dx=not self.first)
-            else:
-                dh = self._recv(self.model.output_shape(mb), self.act_dtype, self.s + 1, n_mb + i)
-                dx = eng.backward(i, dh=dh, need_dx=not self.first)
-            if not self.first:
-                self._send(dx, self.s - 1, n_mb + i)
+            with on(i):
+                if self.last:
+                    dx = eng.backward(i, labels=batch.labels[i * mb:(i + 1) * mb], need_dx=not self.first)
+                else:
+                    dh = self._recv(self.model.output_shape(mb), self.act_dtype, self.s + 1, n_mb + i)
+                    dx = eng.backward(i, dh=dh, need_dx=not self.first)
+                if not self.first:
+                    self._send(dx, self.s - 1, n_mb + i)
+        on.join()
+        if k > 1:
+            eng.merge()
 
     def _epilogue_opt(self):
         """The in-epilogue AdamW (ops.kernels.EpilogueAdamW) for a transformer stage
@@ -686,8 +729,8 @@ class GPipeTrainer:
             self.deep_engine.finalize()  # bf16 shadow parity of the in-epilogue AdamW
         if self.p2p is not None and self.p2p.error():
             raise RuntimeError("xgmi pipeline receive timed out on this rank (peer dead or desynchronised)")
-        if self.xg is not None and self.xg.error():
-            raise RuntimeError("xgmi collective timed out on this rank (peer dead or desynchronised)")
+        if self.xg is not None:
+            self.xg.raise_if_error()
 
     def loss_head(self, logits, labels, dlogits, n_parts: int = 1):
         """CE of ``labels`` (``n_parts`` merged microbatches: every row keeps its

@@ -197,11 +197,42 @@ __device__ __forceinline__ float4 adam4(const XgAdam& A, long e, float4 g, float
 // buffer, identity layout (slice == s), in the half selected by the parity of the
 // optimizer step counter A.step -- which every block reads here before the last
 // block's ticket advances it -- so phase 0 (a full-buffer copy) is skipped.
+// Latency structure: a thread owns nit = ceil(nv / 256) float4 positions of its block's
+// chunk (1 at W = 8, 2-3 at W = 2..4 for the DP bucket).  Every phase issues ALL of a
+// thread's loads for up to XG_MI(W) positions before its first store (vmcnt counts loads
+// and stores together on gfx9, so a load behind a store waits for that store), and the
+// fused AdamW state (p, m, v -- local, unaffected by the collective) is loaded before
+// barrier B, so it arrives while the block waits for its peers.
+template <int W> struct XgMi { static constexpr int v = W <= 2 ? 4 : (W <= 4 ? 2 : 1); };
+
+__device__ __forceinline__ float4 adam4_pre(const XgAdam& A, long e, float4 g, float4 pp, float4 mm, float4 vv,
+                                            float rbc1, float rbc2) {
+  float* pe = &pp.x; float* me = &mm.x; float* ve = &vv.x; const float* ge = &g.x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float gr = ge[k] * A.grad_scale;
+    me[k] = A.b1 * me[k] + (1.f - A.b1) * gr;
+    ve[k] = A.b2 * ve[k] + (1.f - A.b2) * gr * gr;
+    pe[k] -= A.lr * ((me[k] * rbc1) / (sqrtf(ve[k] * rbc2) + A.eps) + A.wd * pe[k]);
+  }
+  *reinterpret_cast<float4*>(A.p + e) = pp;
+  *reinterpret_cast<float4*>(A.m + e) = mm;
+  *reinterpret_cast<float4*>(A.v + e) = vv;
+  if (A.shadow) {
+    uint2 s;
+    s.x = (unsigned)f2bf(pp.x) | ((unsigned)f2bf(pp.y) << 16);
+    s.y = (unsigned)f2bf(pp.z) | ((unsigned)f2bf(pp.w) << 16);
+    *reinterpret_cast<uint2*>(A.shadow + e) = s;
+  }
+  return pp;
+}
+
 template <int W, int OP>
 __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, long cap, const float* in, float* out,
                                                         long n, long s, long slice,
                                                         long chunk, XgAdam A, int fuse, long long timeout,
                                                         int staged) {
+  constexpr int MI = XgMi<W>::v;
   __shared__ unsigned s_epoch, s_calls;
   const int b = blockIdx.x;
   XgSignal* me = P.sig[rank];
@@ -214,8 +245,10 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
   const long half = (long)((staged ? (unsigned)A.step[0] : s_calls) & 1u) * cap;
   const long base = (long)b * chunk;
   const int nv = (int)(chunk >> 2);
+  const int nit = (nv + XG_THREADS - 1) / XG_THREADS;
   const long own_n = (n - rank * s < s) ? n - rank * s : s;  // valid length of this rank's part
   const unsigned long long bytes = (unsigned long long)cap * 2ull * sizeof(float);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   // every access to an IPC buffer (own or peer) is a system-scope sc0 sc1 access (common.h)
   __amdgpu_buffer_rsrc_t rdata[W], rtmp[W];
 #pragma unroll
@@ -226,28 +259,51 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
   const __amdgpu_buffer_rsrc_t my_data = sys_rsrc(P.data[rank], bytes), my_tmp = sys_rsrc(P.tmp[rank], bytes);
 
   if (OP != XG_ALL_GATHER) {
-    // phase 0: stage chunk b of every part of the local input (write-through stores)
-    for (int q = 0; q < (staged ? 0 : W); ++q) {
-      for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
-        const long j = base + 4 * i;
-        const float4 x = j < s ? load_guard(in, q * s + j, n) : make_float4(0.f, 0.f, 0.f, 0.f);
-        sys_store4(my_data, half + q * slice + j, x);
+    // phase 0: stage chunk b of every part of the local input (write-through stores):
+    // all (part, position) loads of a round first, then the stores
+    if (!staged) {
+      for (int t0 = 0; t0 < W * nit; t0 += MI) {
+        float4 x[MI];
+        long d[MI];
+#pragma unroll
+        for (int u = 0; u < MI; ++u) {
+          const int t = t0 + u, q = t / nit, i = threadIdx.x + (t % nit) * XG_THREADS;
+          const long j = base + 4 * (long)i;
+          x[u] = z4;
+          d[u] = -1;
+          if (t < W * nit && i < nv) {
+            d[u] = half + q * slice + j;
+            if (j < s) x[u] = load_guard(in, q * s + j, n);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < MI; ++u)
+          if (d[u] >= 0) sys_store4(my_data, d[u], x[u]);
       }
     }
     xg_barrier(P, rank, W, 0, epoch, timeout, XG_SITE_TWOSHOT);
-    // phase 1: reduce chunk b of part `rank` over the peers (all W loads in flight,
+    // phase 1: reduce chunk b of part `rank` over the peers (W x MI loads in flight,
     // fixed rank order -> every rank computes bit-identical sums)
-    for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
-      const long j = base + 4 * i;
-      const long e = rank * slice + j;
-      float4 v[W];
+    for (int i0 = 0; i0 < nit; i0 += MI) {
+      float4 v[MI][W];
 #pragma unroll
-      for (int q = 0; q < W; ++q) v[q] = sys_load4(rdata[q], half + e);
-      float4 acc = v[0];
+      for (int u = 0; u < MI; ++u) {
+        const int i = min(threadIdx.x + (i0 + u) * XG_THREADS, nv - 1);   // clamped: unconditional loads
+        const long e = rank * slice + base + 4 * (long)i;
 #pragma unroll
-      for (int q = 1; q < W; ++q) acc = add4(acc, v[q]);
-      if (OP == XG_REDUCE_SCATTER) store_guard(out, j, own_n, acc);
-      else sys_store4(my_tmp, half + e, acc);
+        for (int q = 0; q < W; ++q) v[u][q] = sys_load4(rdata[q], half + e);
+      }
+#pragma unroll
+      for (int u = 0; u < MI; ++u) {
+        const int i = threadIdx.x + (i0 + u) * XG_THREADS;
+        if (i0 + u >= nit || i >= nv) continue;
+        const long j = base + 4 * (long)i;
+        float4 acc = v[u][0];
+#pragma unroll
+        for (int q = 1; q < W; ++q) acc = add4(acc, v[u][q]);
+        if (OP == XG_REDUCE_SCATTER) store_guard(out, j, own_n, acc);
+        else sys_store4(my_tmp, half + rank * slice + j, acc);
+      }
     }
     if (OP == XG_REDUCE_SCATTER) {
       if (threadIdx.x == 0) me->epoch[b] = epoch;
@@ -258,45 +314,71 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
     // all-gather phase 0: stage chunk b of this rank's part into its tmp slice
     for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
       const long j = base + 4 * i;
-      const float4 x = j < s ? load_guard(in, j, own_n) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 x = j < s ? load_guard(in, j, own_n) : z4;
       sys_store4(my_tmp, half + rank * slice + j, x);
     }
   }
-  xg_barrier(P, rank, W, 1, epoch, timeout, XG_SITE_TWOSHOT);
-
-  // phase 2: gather chunk b of every part (all W loads in flight per thread)
   float rbc1 = 1.f, rbc2 = 1.f;
   if (fuse) {
     const int t = A.step[0] + 1;
     rbc1 = 1.f / (1.f - powf(A.b1, (float)t));
     rbc2 = 1.f / (1.f - powf(A.b2, (float)t));
   }
-  for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
-    const long j = base + 4 * i;
-    if (j >= s) break;
-    float4 r[W];
+  // phase 2: gather chunk b of every part (all W x MI loads in flight per thread).  Fused:
+  // the AdamW state of the first round's elements is loaded before barrier B.
+  const bool pre = fuse && A.n_params >= 4;
+  const long pcl = pre ? A.n_params - 4 : 0;
+  float4 sp[MI][W], sm[MI][W], sv[MI][W];
+  for (int i0 = 0; i0 < nit; i0 += MI) {
+    if (pre) {
 #pragma unroll
-    for (int q = 0; q < W; ++q) r[q] = sys_load4(rtmp[q], half + q * slice + j);
+      for (int u = 0; u < MI; ++u) {
+        const long j = base + 4 * (long)min(threadIdx.x + (i0 + u) * XG_THREADS, nv - 1);
 #pragma unroll
-    for (int q = 0; q < W; ++q) {
-      const long e = q * s + j;
-      if (!fuse) {
-        store_guard(out, e, n, r[q]);
-      } else if (e < n) {
-        if (e < A.n_params) {
-          adam4(A, e, r[q], rbc1, rbc2);
-        } else {
-          const float* rv = &r[q].x;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const long mj = e + k - A.n_params;
-            if (mj < A.n_metrics && e + k < n) A.running[mj] += rv[k];
-          }
+        for (int q = 0; q < W; ++q) {
+          const long e = min((long)q * s + j, pcl);
+          sp[u][q] = *reinterpret_cast<const float4*>(A.p + e);
+          sm[u][q] = *reinterpret_cast<const float4*>(A.m + e);
+          sv[u][q] = *reinterpret_cast<const float4*>(A.v + e);
         }
-        if (A.zero) store_guard(A.zero, e, n, make_float4(0.f, 0.f, 0.f, 0.f));
+      }
+    }
+    if (i0 == 0) xg_barrier(P, rank, W, 1, epoch, timeout, XG_SITE_TWOSHOT);
+    float4 r[MI][W];
+#pragma unroll
+    for (int u = 0; u < MI; ++u) {
+      const long j = base + 4 * (long)min(threadIdx.x + (i0 + u) * XG_THREADS, nv - 1);
+#pragma unroll
+      for (int q = 0; q < W; ++q) r[u][q] = sys_load4(rtmp[q], half + q * slice + j);
+    }
+#pragma unroll
+    for (int u = 0; u < MI; ++u) {
+      const int i = threadIdx.x + (i0 + u) * XG_THREADS;
+      const long j = base + 4 * (long)i;
+      if (i0 + u >= nit || i >= nv || j >= s) continue;
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        const long e = q * s + j;
+        if (!fuse) {
+          store_guard(out, e, n, r[u][q]);
+        } else if (e < n) {
+          if (e < A.n_params) {
+            if (pre) adam4_pre(A, e, r[u][q], sp[u][q], sm[u][q], sv[u][q], rbc1, rbc2);
+            else adam4(A, e, r[u][q], rbc1, rbc2);
+          } else {
+            const float* rv = &r[u][q].x;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const long mj = e + k - A.n_params;
+              if (mj < A.n_metrics && e + k < n) A.running[mj] += rv[k];
+            }
+          }
+          if (A.zero) store_guard(A.zero, e, n, z4);
+        }
       }
     }
   }
+  if (nit == 0) xg_barrier(P, rank, W, 1, epoch, timeout, XG_SITE_TWOSHOT);
   if (threadIdx.x == 0) me->epoch[b] = epoch;
   if (fuse && A.step) {
     __syncthreads();
@@ -341,41 +423,73 @@ __global__ void __launch_bounds__(XG_THREADS) xg_oneshot_kernel(XgPeers P, int r
 #pragma unroll
   for (int q = 0; q < W; ++q) rdata[q] = sys_rsrc(P.data[q], bytes);
   const __amdgpu_buffer_rsrc_t my_data = sys_rsrc(P.data[rank], bytes);
-  for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
-    const long j = base + 4 * i;
-    const float4 x = j < n ? load_guard(in, j, n) : make_float4(0.f, 0.f, 0.f, 0.f);
-    sys_store4(my_data, half + j, x);
+  constexpr int MI = 4;   // positions per thread per round (xg_kernel's latency structure)
+  const int nit = (nv + XG_THREADS - 1) / XG_THREADS;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i0 = 0; i0 < nit; i0 += MI) {
+    float4 x[MI];
+#pragma unroll
+    for (int u = 0; u < MI; ++u) {
+      const long j = base + 4 * (long)(threadIdx.x + (i0 + u) * XG_THREADS);
+      x[u] = (i0 + u < nit && j < base + chunk && j < n) ? load_guard(in, j, n) : z4;
+    }
+#pragma unroll
+    for (int u = 0; u < MI; ++u) {
+      const long j = base + 4 * (long)(threadIdx.x + (i0 + u) * XG_THREADS);
+      if (i0 + u < nit && j < base + chunk) sys_store4(my_data, half + j, x[u]);
+    }
   }
-  xg_barrier(P, rank, W, 0, epoch, timeout, XG_SITE_ONESHOT);
   float rbc1 = 1.f, rbc2 = 1.f;
   if (fuse) {
     const int t = A.step[0] + 1;
     rbc1 = 1.f / (1.f - powf(A.b1, (float)t));
     rbc2 = 1.f / (1.f - powf(A.b2, (float)t));
   }
-  for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
-    const long j = base + 4 * i;
-    if (j >= n) break;
-    float4 v[W];
+  const bool pre = fuse && A.n_params >= 4;
+  const long pcl = pre ? A.n_params - 4 : 0;
+  for (int i0 = 0; i0 < nit; i0 += MI) {
+    float4 sp[MI], sm[MI], sv[MI];
+    if (pre) {   // AdamW state (local) of this round: in flight across the barrier
 #pragma unroll
-    for (int q = 0; q < W; ++q) v[q] = sys_load4(rdata[q], half + j);
-    float4 acc = v[0];
-#pragma unroll
-    for (int q = 1; q < W; ++q) acc = add4(acc, v[q]);
-    if (!fuse) {
-      store_guard(out, j, n, acc);
-    } else {
-      if (j < A.n_params) {
-        adam4(A, j, acc, rbc1, rbc2);
-      } else {
-        const float* rv = &acc.x;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const long mj = j + k - A.n_params;
-          if (mj < A.n_metrics && j + k < n) A.running[mj] += rv[k];
-        }
+      for (int u = 0; u < MI; ++u) {
+        const long e = min(base + 4 * (long)min(threadIdx.x + (i0 + u) * XG_THREADS, nv - 1), pcl);
+        sp[u] = *reinterpret_cast<const float4*>(A.p + e);
+        sm[u] = *reinterpret_cast<const float4*>(A.m + e);
+        sv[u] = *reinterpret_cast<const float4*>(A.v + e);
       }
-      if (A.zero) store_guard(A.zero, j, n, make_float4(0.f, 0.f, 0.f, 0.f));
+    }
+    if (i0 == 0) xg_barrier(P, rank, W, 0, epoch, timeout, XG_SITE_ONESHOT);
+    float4 v[MI][W];
+#pragma unroll
+    for (int u = 0; u < MI; ++u) {
+      const long j = base + 4 * (long)min(threadIdx.x + (i0 + u) * XG_THREADS, nv - 1);
+#pragma unroll
+      for (int q = 0; q < W; ++q) v[u][q] = sys_load4(rdata[q], half + j);
+    }
+#pragma unroll
+    for (int u = 0; u < MI; ++u) {
+      const int i = threadIdx.x + (i0 + u) * XG_THREADS;
+      const long j = base + 4 * (long)i;
+      if (i0 + u >= nit || i >= nv || j >= n) continue;
+      float4 acc = v[u][0];
+#pragma unroll
+      for (int q = 1; q < W; ++q) acc = add4(acc, v[u][q]);
+      if (!fuse) {
+        store_guard(out, j, n, acc);
+      } else {
+        if (j < A.n_params) {
+          if (pre) adam4_pre(A, j, acc, sp[u], sm[u], sv[u], rbc1, rbc2);
+          else adam4(A, j, acc, rbc1, rbc2);
+        } else {
+          const float* rv = &acc.x;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const long mj = j + k - A.n_params;
+            if (mj < A.n_metrics && j + k < n) A.running[mj] += rv[k];
+          }
+        }
+        if (A.zero) store_guard(A.zero, j, n, z4);
+      }
     }
   }
   if (threadIdx.x == 0) me->epoch[b] = epoch;
@@ -583,24 +697,38 @@ __global__ void __launch_bounds__(XG_THREADS) xg_fsdp_kernel(XgPeers P, int rank
   const XgAdam& A = F.A;
   XF_STAMP(0);
 
+  // Latency structure as xg_kernel: a thread's loads of a round are all issued before
+  // its first store (M0 / MI positions per round), the sharded AdamW state of the first
+  // round is loaded before barrier A.
+  constexpr int M0 = 8, MI = XgMi<W>::v;
+  const int nit = (nv + XG_THREADS - 1) / XG_THREADS;
+
   // phase 0: stage
   {
     const __amdgpu_buffer_rsrc_t my_data = sys_rsrc(P.data[rank], bytes);
-    for (int q = 0; q < W; ++q) {
-      for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
-        const long j = base + 4 * i;
-        float4 x = z4;
-        if (j < S.S) {
-          const XgSeg& g = S.seg[xg_find(S, j)];
-          x = load_guard(g.full, seg_full_index(g, q, j - g.off), g.nfull);
+    for (int t0 = 0; t0 < W * nit; t0 += M0) {
+      float4 x[M0];
+      long d[M0];
+#pragma unroll
+      for (int u = 0; u < M0; ++u) {
+        const int t = t0 + u, q = t / nit, i = threadIdx.x + (t % nit) * XG_THREADS;
+        const long j = base + 4 * (long)i;
+        x[u] = z4;
+        d[u] = -1;
+        if (t < W * nit && i < nv) {
+          d[u] = half + q * slice + j;
+          if (j < S.S) {
+            const XgSeg& g = S.seg[xg_find(S, j)];
+            x[u] = load_guard(g.full, seg_full_index(g, q, j - g.off), g.nfull);
+          }
         }
-        sys_store4(my_data, half + q * slice + j, x);
       }
+#pragma unroll
+      for (int u = 0; u < M0; ++u)
+        if (d[u] >= 0) sys_store4(my_data, d[u], x[u]);
     }
   }
   if (F.stamps) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); XF_STAMP(1); }
-  xg_barrier(P, rank, W, 0, epoch, timeout, XG_SITE_FSDP);
-  XF_STAMP(2);
 
   // phase 1: reduce own part, optimizer, publish the new bf16 shard
   float rbc1, rbc2;
@@ -614,61 +742,93 @@ __global__ void __launch_bounds__(XG_THREADS) xg_fsdp_kernel(XgPeers P, int rank
 #pragma unroll
     for (int q = 0; q < W; ++q) rdata[q] = sys_rsrc(P.data[q], bytes);
     const __amdgpu_buffer_rsrc_t my_tmp = sys_rsrc(P.tmp[rank], bytes);
-    for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
-      const long j = base + 4 * i;
-      if (j >= S.S) break;
-      float4 v[W];
+    for (int i0 = 0; i0 < nit; i0 += MI) {
+      // this round's positions: segment, local offset, and (aligned whole groups) the
+      // AdamW state -- local, so it is loaded while the block waits at barrier A
+      int kk[MI];
+      long jjv[MI], lov[MI], limv[MI];
+      bool live[MI], fast[MI];
+      float4 sp[MI], sm[MI], sv[MI];
 #pragma unroll
-      for (int q = 0; q < W; ++q) v[q] = sys_load4(rdata[q], half + rank * slice + j);
-      float4 acc = v[0];
-#pragma unroll
-      for (int q = 1; q < W; ++q) acc = add4(acc, v[q]);
-      const int k = xg_find(S, j);
-      const XgSeg& g = S.seg[k];
-      const long jj = j - g.off;
-      const long lim = g.bcast ? g.nfull : ((g.nfull - rank * g.s < g.s) ? g.nfull - rank * g.s : g.s);
-      const int kind = F.kind[k];
-      if (kind == XF_METRIC) {
-        const float* a = &acc.x;
-        for (int e = 0; e < 4; ++e)
-          if (jj + e < lim && jj + e < A.n_metrics) A.running[jj + e] += a[e];
-        store_guard(g.part, jj, lim, z4);
-        continue;
+      for (int u = 0; u < MI; ++u) {
+        const int i = threadIdx.x + (i0 + u) * XG_THREADS;
+        const long j = base + 4 * (long)i;
+        live[u] = i0 + u < nit && i < nv && j < S.S;
+        const int k = live[u] ? xg_find(S, j) : 0;
+        const XgSeg& g = S.seg[k];
+        kk[u] = k;
+        jjv[u] = j - g.off;
+        limv[u] = g.bcast ? g.nfull : ((g.nfull - rank * g.s < g.s) ? g.nfull - rank * g.s : g.s);
+        lov[u] = (g.part - F.grad) + jjv[u];   // local flat offset of element jj of this part
+        fast[u] = live[u] && F.kind[k] != XF_METRIC && jjv[u] + 4 <= limv[u] && (lov[u] & 3) == 0;
+        const long ec = fast[u] ? lov[u] : 0;
+        sp[u] = *reinterpret_cast<const float4*>(A.p + ec);
+        sm[u] = *reinterpret_cast<const float4*>(A.m + ec);
+        sv[u] = *reinterpret_cast<const float4*>(A.v + ec);
       }
-      const long lo = (g.part - F.grad) + jj;   // local flat offset of element jj of this part
-      const float* ga = &acc.x;
-      float pn[4] = {0.f, 0.f, 0.f, 0.f};
-      if (jj + 4 <= lim && (lo & 3) == 0) {
-        // whole aligned group: one 16-byte access per state vector (the per-element
-        // path below issues 12 dependent 4-byte loads per group)
-        const float4 pv = adam4(A, lo, acc, rbc1, rbc2);
-        pn[0] = pv.x; pn[1] = pv.y; pn[2] = pv.z; pn[3] = pv.w;
-      } else {
+      if (i0 == 0) {
+        xg_barrier(P, rank, W, 0, epoch, timeout, XG_SITE_FSDP);
+        XF_STAMP(2);
+      }
+      float4 v[MI][W];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (jj + e >= lim) break;
-          const float gr = ga[e] * A.grad_scale;
-          const float mm = A.b1 * A.m[lo + e] + (1.f - A.b1) * gr;
-          const float vv = A.b2 * A.v[lo + e] + (1.f - A.b2) * gr * gr;
-          float pp = A.p[lo + e];
-          pp -= A.lr * ((mm * rbc1) / (sqrtf(vv * rbc2) + A.eps) + A.wd * pp);
-          A.m[lo + e] = mm;
-          A.v[lo + e] = vv;
-          A.p[lo + e] = pp;
-          A.shadow[lo + e] = f2bf(pp);
-          pn[e] = pp;
+      for (int u = 0; u < MI; ++u) {
+        const long j = base + 4 * (long)min(threadIdx.x + (i0 + u) * XG_THREADS, nv - 1);
+#pragma unroll
+        for (int q = 0; q < W; ++q) v[u][q] = sys_load4(rdata[q], half + rank * slice + j);
+      }
+#pragma unroll
+      for (int u = 0; u < MI; ++u) {
+        if (!live[u]) continue;
+        const long j = base + 4 * (long)(threadIdx.x + (i0 + u) * XG_THREADS);
+        float4 acc = v[u][0];
+#pragma unroll
+        for (int q = 1; q < W; ++q) acc = add4(acc, v[u][q]);
+        const int k = kk[u];
+        const XgSeg& g = S.seg[k];
+        const long jj = jjv[u], lim = limv[u], lo = lov[u];
+        const int kind = F.kind[k];
+        if (kind == XF_METRIC) {
+          const float* a = &acc.x;
+          for (int e = 0; e < 4; ++e)
+            if (jj + e < lim && jj + e < A.n_metrics) A.running[jj + e] += a[e];
+          store_guard(g.part, jj, lim, z4);
+          continue;
         }
-      }
-      uint2 pk;
-      pk.x = (unsigned)f2bf(pn[0]) | ((unsigned)f2bf(pn[1]) << 16);
-      pk.y = (unsigned)f2bf(pn[2]) | ((unsigned)f2bf(pn[3]) << 16);
-      if (kind == XF_SHARD) {
-        sys_store8(my_tmp, 2 * (2 * half + rank * slice + j), pk);
-      } else {  // replicated: every rank holds the same update; write the full leaf directly
-        bf16_t* fs = F.full_shadow[k];
-        const bf16_t h4[4] = {(bf16_t)(pk.x & 0xffff), (bf16_t)(pk.x >> 16), (bf16_t)(pk.y & 0xffff), (bf16_t)(pk.y >> 16)};
-        for (int e = 0; e < 4; ++e)
-          if (jj + e < lim) fs[jj + e] = h4[e];
+        const float* ga = &acc.x;
+        float pn[4] = {0.f, 0.f, 0.f, 0.f};
+        if (fast[u]) {
+          // writes p, m, v and the local bf16 shadow; the new p is also the published value
+          const float4 pv = adam4_pre(A, lo, acc, sp[u], sm[u], sv[u], rbc1, rbc2);
+          pn[0] = pv.x; pn[1] = pv.y; pn[2] = pv.z; pn[3] = pv.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (jj + e >= lim) break;
+            const float gr = ga[e] * A.grad_scale;
+            const float mm = A.b1 * A.m[lo + e] + (1.f - A.b1) * gr;
+            const float vv = A.b2 * A.v[lo + e] + (1.f - A.b2) * gr * gr;
+            float pp = A.p[lo + e];
+            pp -= A.lr * ((mm * rbc1) / (sqrtf(vv * rbc2) + A.eps) + A.wd * pp);
+            A.m[lo + e] = mm;
+            A.v[lo + e] = vv;
+            A.p[lo + e] = pp;
+            A.shadow[lo + e] = f2bf(pp);
+            pn[e] = pp;
+          }
+        }
+        uint2 pk;
+        pk.x = (unsigned)f2bf(pn[0]) | ((unsigned)f2bf(pn[1]) << 16);
+        pk.y = (unsigned)f2bf(pn[2]) | ((unsigned)f2bf(pn[3]) << 16);
+        if (kind == XF_SHARD) {
+          sys_store8(my_tmp, 2 * (2 * half + rank * slice + j), pk);
+        } else {  // replicated: every rank holds the same update; write the full leaf directly
+          bf16_t* fs = F.full_shadow[k];
+          const bf16_t h4[4] = {(bf16_t)(pk.x & 0xffff), (bf16_t)(pk.x >> 16), (bf16_t)(pk.y & 0xffff),
+                                (bf16_t)(pk.y >> 16)};
+          for (int e = 0; e < 4; ++e)
+            if (jj + e < lim) fs[jj + e] = h4[e];
+        }
       }
     }
   }
@@ -681,27 +841,35 @@ __global__ void __launch_bounds__(XG_THREADS) xg_fsdp_kernel(XgPeers P, int rank
     __amdgpu_buffer_rsrc_t rtmp[W];
 #pragma unroll
     for (int q = 0; q < W; ++q) rtmp[q] = sys_rsrc(P.tmp[q], bytes);
-    for (int i = threadIdx.x; i < nv; i += XG_THREADS) {
-      const long j = base + 4 * i;
-      if (j >= S.S) break;
-      const int k = xg_find(S, j);
-      if (F.kind[k] != XF_SHARD) continue;
-      const XgSeg& g = S.seg[k];
-      const long jj = j - g.off;
-      uint2 r[W];
+    for (int i0 = 0; i0 < nit; i0 += MI) {
+      uint2 r[MI][W];
 #pragma unroll
-      for (int q = 0; q < W; ++q) r[q] = sys_load8(rtmp[q], 2 * (2 * half + q * slice + j));
+      for (int u = 0; u < MI; ++u) {
+        const long j = base + 4 * (long)min(threadIdx.x + (i0 + u) * XG_THREADS, nv - 1);
 #pragma unroll
-      for (int q = 0; q < W; ++q) {
-        const long lim = (g.nfull - q * g.s < g.s) ? g.nfull - q * g.s : g.s;
-        if (jj >= lim) continue;
-        bf16_t* dst = F.full_shadow[k] + seg_full_index(g, q, jj);
-        if (jj + 4 <= lim) {
-          *reinterpret_cast<uint2*>(dst) = r[q];
-        } else {
-          const bf16_t h4[4] = {(bf16_t)(r[q].x & 0xffff), (bf16_t)(r[q].x >> 16), (bf16_t)(r[q].y & 0xffff),
-                                (bf16_t)(r[q].y >> 16)};
-          for (int e = 0; e < 4 && jj + e < lim; ++e) dst[e] = h4[e];
+        for (int q = 0; q < W; ++q) r[u][q] = sys_load8(rtmp[q], 2 * (2 * half + q * slice + j));
+      }
+#pragma unroll
+      for (int u = 0; u < MI; ++u) {
+        const int i = threadIdx.x + (i0 + u) * XG_THREADS;
+        const long j = base + 4 * (long)i;
+        if (i0 + u >= nit || i >= nv || j >= S.S) continue;
+        const int k = xg_find(S, j);
+        if (F.kind[k] != XF_SHARD) continue;
+        const XgSeg& g = S.seg[k];
+        const long jj = j - g.off;
+#pragma unroll
+        for (int q = 0; q < W; ++q) {
+          const long lim = (g.nfull - q * g.s < g.s) ? g.nfull - q * g.s : g.s;
+          if (jj >= lim) continue;
+          bf16_t* dst = F.full_shadow[k] + seg_full_index(g, q, jj);
+          if (jj + 4 <= lim) {
+            *reinterpret_cast<uint2*>(dst) = r[u][q];
+          } else {
+            const bf16_t h4[4] = {(bf16_t)(r[u][q].x & 0xffff), (bf16_t)(r[u][q].x >> 16),
+                                  (bf16_t)(r[u][q].y & 0xffff), (bf16_t)(r[u][q].y >> 16)};
+            for (int e = 0; e < 4 && jj + e < lim; ++e) dst[e] = h4[e];
+          }
         }
       }
     }

@@ -149,6 +149,9 @@ class PipeConfig:
     # ... the W pass after the join round-robin over the first wpass_rr microbatch streams
     # (0: all of them; measured 1 stream 1.27 ms, 2: 1.12, 3-4: 1.07-1.09)
     wpass_rr: int = field(default_factory=lambda: int(os.environ.get("JDT_WPASS_STREAMS", "0")))
+    # S > 1 (xGMI inbox hand-offs): microbatch chains of a stage on concurrent streams
+    # (mb_streams of them) -- opt-in, see GPipeTrainer._streams_ok
+    multi_stage_streams: bool = field(default_factory=lambda: os.environ.get("JDT_PP_STREAMS", "0") == "1")
 
 
 def _no_dropout(model) -> bool:
@@ -496,10 +499,17 @@ class GPipeTrainer:
 
     def _streams_ok(self) -> bool:
         """Whether this stage may run its microbatch chains on concurrent streams: GPU,
-        and either one stage or every hand-off on the xGMI inbox kernels (per-microbatch
-        slots, stream-ordered reuse: comm/csrc/p2p.hip).  RCCL send / recv issued from
-        several streams of one communicator could pair up out of order across ranks."""
-        return self.dev.type == "cuda" and (self.S == 1 or self.p2p is not None)
+        and either one stage or -- opt-in, ``cfg.multi_stage_streams`` -- every hand-off
+        on the xGMI inbox kernels (per-microbatch slots, stream-ordered reuse:
+        comm/csrc/p2p.hip; RCCL send / recv issued from several streams of one
+        communicator could pair up out of order across ranks).  Off by default for
+        S > 1: with 4 / 8 ranks sharing one GPU it measured 5x / 20x SLOWER
+        (profiles/r4_pp_streams_ab.txt) -- every rank's receive kernels then spin on
+        concurrent hardware queues of a time-shared GPU; a real node (one rank per GPU)
+        is unmeasured."""
+        if self.dev.type != "cuda":
+            return False
+        return self.S == 1 or (self.p2p is not None and self.cfg.multi_stage_streams)
 
     def invalidate(self):
         """After a checkpoint restore: drop captured graphs and the stage engine."""

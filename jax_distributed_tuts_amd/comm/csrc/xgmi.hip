@@ -324,18 +324,22 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
     rbc1 = 1.f / (1.f - powf(A.b1, (float)t));
     rbc2 = 1.f / (1.f - powf(A.b2, (float)t));
   }
-  // phase 2: gather chunk b of every part (all W x MI loads in flight per thread).  Fused:
-  // the AdamW state of the first round's elements is loaded before barrier B.
-  const bool pre = fuse && A.n_params >= 4;
+  // phase 2: gather chunk b of every part (all W x MI loads in flight per thread).  Fused,
+  // W <= 4: the AdamW state of the first round's elements is loaded before barrier B (at
+  // W > 4 its 3W float4 registers would halve the occupancy, and ranks sharing one GPU
+  // need every rank's grid resident at once for the barriers)
+  constexpr bool PRE = W <= 4;
+  constexpr int WP = PRE ? W : 1;
+  const bool pre = PRE && fuse && A.n_params >= 4;
   const long pcl = pre ? A.n_params - 4 : 0;
-  float4 sp[MI][W], sm[MI][W], sv[MI][W];
+  float4 sp[MI][WP], sm[MI][WP], sv[MI][WP];
   for (int i0 = 0; i0 < nit; i0 += MI) {
     if (pre) {
 #pragma unroll
       for (int u = 0; u < MI; ++u) {
         const long j = base + 4 * (long)min(threadIdx.x + (i0 + u) * XG_THREADS, nv - 1);
 #pragma unroll
-        for (int q = 0; q < W; ++q) {
+        for (int q = 0; q < WP; ++q) {
           const long e = min((long)q * s + j, pcl);
           sp[u][q] = *reinterpret_cast<const float4*>(A.p + e);
           sm[u][q] = *reinterpret_cast<const float4*>(A.m + e);
@@ -363,7 +367,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
           store_guard(out, e, n, r[u][q]);
         } else if (e < n) {
           if (e < A.n_params) {
-            if (pre) adam4_pre(A, e, r[u][q], sp[u][q], sm[u][q], sv[u][q], rbc1, rbc2);
+            if (PRE && pre) adam4_pre(A, e, r[u][q], sp[u][q % WP], sm[u][q % WP], sv[u][q % WP], rbc1, rbc2);
             else adam4(A, e, r[u][q], rbc1, rbc2);
           } else {
             const float* rv = &r[u][q].x;
@@ -423,7 +427,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_oneshot_kernel(XgPeers P, int r
 #pragma unroll
   for (int q = 0; q < W; ++q) rdata[q] = sys_rsrc(P.data[q], bytes);
   const __amdgpu_buffer_rsrc_t my_data = sys_rsrc(P.data[rank], bytes);
-  constexpr int MI = 4;   // positions per thread per round (xg_kernel's latency structure)
+  constexpr int MI = XgMi<W>::v;   // positions per thread per round (xg_kernel's latency structure)
   const int nit = (nv + XG_THREADS - 1) / XG_THREADS;
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int i0 = 0; i0 < nit; i0 += MI) {
@@ -445,7 +449,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_oneshot_kernel(XgPeers P, int r
     rbc1 = 1.f / (1.f - powf(A.b1, (float)t));
     rbc2 = 1.f / (1.f - powf(A.b2, (float)t));
   }
-  const bool pre = fuse && A.n_params >= 4;
+  const bool pre = W <= 4 && fuse && A.n_params >= 4;   // register budget as in xg_kernel
   const long pcl = pre ? A.n_params - 4 : 0;
   for (int i0 = 0; i0 < nit; i0 += MI) {
     float4 sp[MI], sm[MI], sv[MI];

@@ -666,6 +666,11 @@ struct XgFsdp {
   // diagnostic (tools/stamp_xg_fsdp.py): per block s_memrealtime at the phase edges
   // [G][8]: start, stage stored, barrier A, reduce + AdamW, barrier B, gather, end
   unsigned long long* stamps;
+  // 1: the step's producer kernel (mlp2_bwd / md_bwd mode 0 with a common.h StageMap)
+  // already wrote every peer part of every segment into this rank's data buffer, in the
+  // half of the optimizer step's parity (A.step, read by every block before the last
+  // block's ticket advances it) -- phase 0 is skipped, as in xg_kernel's staged mode
+  int staged;
 };
 
 #define XF_STAMP(i)                                                                            \
@@ -693,12 +698,12 @@ __global__ void __launch_bounds__(XG_THREADS) xg_fsdp_kernel(XgPeers P, int rank
   }
   __syncthreads();
   const unsigned epoch = s_epoch;
-  const long half = (long)(s_calls & 1u) * cap;
+  const XgAdam& A = F.A;
+  const long half = (long)((F.staged ? (unsigned)A.step[0] : s_calls) & 1u) * cap;
   const long base = (long)b * chunk;
   const int nv = (int)(chunk >> 2);
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   const unsigned long long bytes = (unsigned long long)cap * 2ull * sizeof(float);
-  const XgAdam& A = F.A;
   XF_STAMP(0);
 
   // Latency structure as xg_kernel: a thread's loads of a round are all issued before
@@ -707,8 +712,8 @@ __global__ void __launch_bounds__(XG_THREADS) xg_fsdp_kernel(XgPeers P, int rank
   constexpr int M0 = 8, MI = XgMi<W>::v;
   const int nit = (nv + XG_THREADS - 1) / XG_THREADS;
 
-  // phase 0: stage
-  {
+  // phase 0: stage (skipped when the producer staged the bucket)
+  if (!F.staged) {
     const __amdgpu_buffer_rsrc_t my_data = sys_rsrc(P.data[rank], bytes);
     for (int t0 = 0; t0 < W * nit; t0 += M0) {
       float4 x[M0];
@@ -1251,6 +1256,14 @@ JDT_API int jdt_xgmi_fsdp_step(void* ctx, const XgSegs* segs, const XgFsdp* f, l
 }
 
 JDT_API int jdt_xgmi_adam_size() { return (int)sizeof(XgAdam); }
+JDT_API int jdt_stage_map_size() { return (int)sizeof(StageMap); }
+
+// Per-peer slot stride (floats) of a segmented / fused FSDP launch over S packed words.
+JDT_API long jdt_xgmi_seg_slice(long S) {
+  long G, chunk;
+  xg_geometry(S, &G, &chunk);
+  return G * chunk;
+}
 
 JDT_API long jdt_xgmi_capacity(void* ctx) { return static_cast<XgCtx*>(ctx)->cap; }
 

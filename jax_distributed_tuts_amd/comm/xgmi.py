@@ -75,7 +75,7 @@ class XgFsdp(ctypes.Structure):
     """Mirror of ``jdt::XgFsdp``: local AdamW buffers + per-segment kind / bf16 full shadow."""
 
     _fields_ = [("A", XgAdam), ("grad", c_void_p), ("kind", c_int * MAX_SEGS), ("full_shadow", c_void_p * MAX_SEGS),
-                ("stamps", c_void_p)]
+                ("stamps", c_void_p), ("staged", c_int)]
 
 
 FSDP_SHARD, FSDP_REPL, FSDP_METRIC = 0, 1, 2
@@ -104,6 +104,7 @@ _lib.declare("jdt_xgmi_stage_clear", c_int, [c_void_p, c_void_p])
 _lib.declare("jdt_xgmi_allreduce_staged", c_int, [c_void_p, c_long, c_long, ctypes.POINTER(XgAdam), c_longlong,
                                                   c_void_p])
 _lib.declare("jdt_xgmi_destroy", c_int, [c_void_p])
+_lib.declare("jdt_xgmi_seg_slice", c_long, [c_long])
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -454,6 +455,29 @@ class XgmiComm:
         a.step, a.ticket, a.zero = _ptr(step), _ptr(ticket), c_void_p(0)
         F.grad = _ptr(grad_base)
         return S, F
+
+    def fsdp_stage_layout(self, plan, leaves) -> dict:
+        """Where a producer kernel writes each gradient element for a STAGED fused FSDP
+        step (common.h StageMap): ``leaves`` = [(name, full shape, shard dim or None)] in
+        the plan's segment order (sharded leaves, then replicated ones), then the metric
+        slots.  Returns {name: (packed offset, dim, per, cols)} plus "metrics", and
+        "base" / "half" / "slice" of this rank's staging buffer."""
+        S, _F = plan
+        out = {}
+        for k, (name, shape, d) in enumerate(leaves):
+            g = S.seg[k]
+            cols = int(shape[-1]) if len(shape) == 2 else 1
+            if d is None:
+                out[name] = (int(g.off), 2, 1, cols)
+            elif d == 0:
+                out[name] = (int(g.off), 0, int(shape[0]) // self.world, cols)
+            else:
+                out[name] = (int(g.off), 1, int(shape[1]) // self.world, cols)
+        out["metrics"] = (int(S.seg[len(leaves)].off), 2, 1, 1)
+        out["base"] = int(_lib.lib().jdt_xgmi_stage_base(self.ctx))
+        out["half"] = self.capacity
+        out["slice"] = int(_lib.lib().jdt_xgmi_seg_slice(int(S.S)))
+        return out
 
     def fsdp_step(self, plan):
         S, F = plan

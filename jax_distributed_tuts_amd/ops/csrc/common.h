@@ -36,6 +36,41 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 }
 __device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
 
+// ---------------------------------------------------------------- FSDP staged gradient bucket
+// A producer kernel of the FSDP step (mlp2_bwd / md_bwd mode 0) writes each full-layout
+// gradient element straight into this rank's xGMI data buffer, in the packed layout of
+// the fused FSDP collective (comm/csrc/xgmi.hip xg_fsdp_kernel, staged): peer-part q of
+// leaf k at q * slice + off_k (+ the element's index within the part), in the half of
+// the optimizer step's parity -- so the collective skips its staging copy.
+struct StageLeaf {
+  long off;    // packed offset (words) of this leaf's part within a peer slot
+  int dim;     // 0: row shards of `per` rows; 1: column shards of `per` columns;
+               // 2: replicated leaf / metric slots (the whole leaf in every peer slot)
+  int per;
+  int cols;    // row length of the full leaf (1 for a vector)
+  int pad;
+};
+struct StageMap {
+  float* base;   // this rank's IPC data buffer, half 0
+  long half;     // floats from half 0 to half 1
+  long slice;    // floats per peer slot
+  int W;         // ranks
+  int nleaf;
+  StageLeaf leaf[5];   // the producer's outputs: [0] W, [1] b, [2] head W, [3] head b, [4] metrics
+};
+
+__device__ __forceinline__ void stage_store(const StageMap* m, int par, int leaf, int row, int col, float v) {
+  const StageLeaf L = m->leaf[leaf];
+  float* b = m->base + (long)par * m->half + L.off;
+  if (L.dim == 2) {
+    for (int q = 0; q < m->W; ++q) b[(long)q * m->slice + (long)row * L.cols + col] = v;
+    return;
+  }
+  const int q = (L.dim == 0 ? row : col) / L.per;
+  const long jj = L.dim == 0 ? (long)(row - q * L.per) * L.cols + col : (long)row * L.per + (col - q * L.per);
+  b[(long)q * m->slice + jj] = v;
+}
+
 // ---------------------------------------------------------------- reductions
 // Whole-wave sum through DPP lane moves (no LDS): quad_perm swaps (xor 1, xor 2),
 // row_half_mirror and row_mirror leave every 16-lane row uniform, then the four

@@ -116,6 +116,10 @@ struct MdArgs {
   // counter in dzc (128-byte lines: [0] error word, block b at 32 (1 + b)); then every
   // workgroup reads the whole dZ_i[:, blk] back.  dzs = 0: each workgroup computes all rows.
   bf16_t* dzx; unsigned* dzc; int dzs;
+  // mode 0, FSDP N > 1 (accumulate = 0): this layer's gradients + (TOP) head gradients and
+  // metric slots straight into the fused FSDP collective's staging buffer (common.h
+  // StageMap; leaves W_i, b_i, W_head, b_head, metrics), half = step parity
+  const StageMap* smap;
 };
 
 // Slots 0-4: s_memrealtime at the kernel's phase ends (tools/stamp_deep.py).
@@ -697,6 +701,8 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
         const bf16_t pb = f2bf(md_adam(op[e], om[e], ov[e], acc[e], ak, a.pW + idx, a.mW + idx, a.vW + idx));
         Wsn[idx] = pb;
         wtp[e >> 1] |= (unsigned)pb << (16 * (e & 1));
+      } else if (a.smap) {
+        stage_store(a.smap, par, 0, trow0 + e, tcol, acc[e]);
       } else {
         a.gW[goff + idx] = (a.accumulate ? op[e] : 0.f) + acc[e];   // mode 0 loaded the old grad into op
       }
@@ -728,6 +734,7 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       if (TOP && ac < C) {
         const long g = (long)(j0 + n) * C + ac;
         if (a.fuse_opt) Whn[g] = f2bf(md_adam(op[e], om[e], ov[e], aw[e], ak, a.pWh + g, a.mWh + g, a.vWh + g));
+        else if (a.smap) stage_store(a.smap, par, 2, j0 + n, ac, aw[e]);
         else a.gWh[goff + g] = (a.accumulate ? op[e] : 0.f) + aw[e];
       }
       if (ac == 0) {
@@ -736,6 +743,8 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
           const float pn = md_adam(bp[e], bm[e], bvv[e], ab[e], ak, a.pb + j, a.mb + j, a.vb + j);
           a.sb[j] = f2bf(pn);
           if constexpr (AHEAD) a.hand[j] = pn;   // the next forward's bias (same XCD: L2 hand-off)
+        } else if (a.smap) {
+          stage_store(a.smap, par, 1, j, 0, ab[e]);
         } else {
           a.gb[goff + j] = (a.accumulate ? bp[e] : 0.f) + ab[e];
         }
@@ -743,6 +752,7 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
     }
     if (TOP && lead && lane < C) {
       if (a.fuse_opt) a.sbh[lane] = f2bf(md_adam(qp, qm, qv, ab2[0], ak, a.pbh + lane, a.mbh + lane, a.vbh + lane));
+      else if (a.smap) stage_store(a.smap, par, 3, lane, 0, ab2[0]);
       else a.gbh[goff + lane] = (a.accumulate ? qp : 0.f) + ab2[0];
     }
   }
@@ -754,6 +764,9 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
       if (a.fuse_opt && a.running) {
         a.running[0] += L; a.running[1] += (float)M; a.running[2] += Cr; a.running[3] += (float)M;
+      } else if (a.smap) {
+        stage_store(a.smap, par, 4, 0, 0, L); stage_store(a.smap, par, 4, 1, 0, (float)M);
+        stage_store(a.smap, par, 4, 2, 0, Cr); stage_store(a.smap, par, 4, 3, 0, (float)M);
       } else if (a.mslot) {
         const float k = a.accumulate ? 1.f : 0.f;
         float* ms = a.mslot + goff;

@@ -99,6 +99,10 @@ struct Mlp2Args {
   // fused optimizer = plain SGD (p -= lr * (g * gscale + wd * p), no momentum) instead
   // of AdamW: the m / v pointers then alias p and are neither used nor written
   int opt_sgd;
+  // mode 0, FSDP N > 1: gradients + metric slots go straight into the xGMI staging
+  // buffer in the fused FSDP collective's packed layout (common.h StageMap; leaves W1,
+  // b1, W2, b2, metrics), half = step parity; null = plain stores at g* (+ goff)
+  const StageMap* smap;
 };
 
 // Persistent multi-step launch (mlp2_loop_kernel): n steps, grid barriers between
@@ -747,6 +751,8 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         // FusedMLP2.finalize() instead of being written every step (0.8 MB of HBM writes)
         if (!a.W1T) a.sW1[idx] = pb;
         wt[e >> 1] |= (unsigned)pb << (16 * (e & 1));
+      } else if (a.smap) {
+        stage_store(a.smap, par, 0, trow0 + e, tcol, acc[e]);
       } else {
         a.gW1[goff + idx] = acc[e];
       }
@@ -789,6 +795,9 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
                                               (isb ? a.mb1 : a.mW2) + o, (isb ? a.vb1 : a.vW2) + o);
           (isb ? a.sb1 : sW2n)[o] = f2bf(pn);
           if constexpr (AHEAD) a.hand[(isb ? 0 : H) + o] = pn;   // same XCD as the reader (L2)
+        } else if (a.smap) {
+          if (isb) stage_store(a.smap, par, 1, j0 + n, 0, gr);
+          else stage_store(a.smap, par, 2, j0 + n, ac, gr);
         } else {
           (isb ? a.gb1 : a.gW2)[goff + o] = gr;
         }
@@ -799,6 +808,8 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         const float pn = adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
         a.sb2[lane] = f2bf(pn);
         if constexpr (AHEAD) a.hand[H + (long)H * C + lane] = pn;
+      } else if (a.smap) {
+        stage_store(a.smap, par, 3, lane, 0, ab2[0]);
       } else {
         a.gb2[goff + lane] = ab2[0];
       }
@@ -812,6 +823,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
     const float val = tid == 0 ? L : tid == 2 ? Cr : (float)M;   // {loss sum, n, correct, n}
     if (fo && a.running) a.running[tid] = run_pre + val;
+    else if (a.smap) stage_store(a.smap, par, 4, tid, 0, val);
     else if (a.mslot) a.mslot[goff + tid] = val;
     // advance the device step: every other workgroup of this launch reads the
     // forward's copy (step_copy), so no arrival ticket is needed

@@ -475,6 +475,7 @@ class FSDPTrainer:
                 or os.environ.get("JDT_FSDP_FUSED_COMM", "1") == "0"):
             return None
         tx, o = st.tx, st.opt_state
+        self._staged = False
         self._plan = sp.xg.fsdp_plan(
             [(sp.full.g(n), sp.local.g(n), sp.full.s(n)) for n in sp.sharded_names],
             [(sp.full.g(n), sp.local.g(n), sp.full.s(n)) for n in sp.repl_names],
@@ -483,6 +484,22 @@ class FSDPTrainer:
             wd=tx.weight_decay, grad_scale=1.0 / (self.cfg.num_minibatches * self.world), step=o["count"],
             ticket=o["ticket"])
         return self._plan
+
+    def _stage_producer(self):
+        """The fused engine writes its gradients straight into the collective's staging
+        buffer (packed FSDP layout, step-parity half): the step's collective skips its
+        staging copy -- the FSDP form of DP's staged bucket (JDT_FSDP_STAGED=0: off)."""
+        if (getattr(self, "_staged", False) or self._plan is None or self.fused is None
+                or not hasattr(self.fused, "set_fsdp_stage") or os.environ.get("JDT_FSDP_STAGED", "1") == "0"):
+            return
+        sp = self.sp
+        leaves = ([(n, self.sp.part[n].global_shape, self.sp.part[n].shard_dim) for n in sp.sharded_names]
+                  + [(n, self.sp.part[n].global_shape, None) for n in sp.repl_names])
+        lay = sp.xg.fsdp_stage_layout(self._plan, leaves)
+        sp.xg.stage_clear()   # packed positions no producer writes (segment padding) reduce to zero
+        self.fused.set_fsdp_stage(lay, lay["base"], lay["half"], lay["slice"], self.world)
+        self._plan[1].staged = 1
+        self._staged = True
 
     @property
     def comm_backend(self) -> str:
@@ -538,6 +555,7 @@ class FSDPTrainer:
             if not self._full_fresh:
                 sp.gather()
                 self._full_fresh = True
+            self._stage_producer()
             self.fused.forward_backward(batch)
             with named_scope("scatter_update_gather"):
                 sp.xg.fsdp_step(plan)

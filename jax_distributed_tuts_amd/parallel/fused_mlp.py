@@ -42,7 +42,39 @@ class Mlp2Args(ctypes.Structure):
                 ("step_copy", c_void_p), ("W2snap", c_void_p), ("stage_stride", ctypes.c_long),
                 ("det_logits", c_void_p),
                 ("XR", c_void_p), ("zslab", c_void_p), ("ztick", c_void_p), ("hand", c_void_p), ("lg3", c_int),
-                ("opt_sgd", c_int)]
+                ("opt_sgd", c_int), ("smap", c_void_p)]
+
+
+class StageLeaf(ctypes.Structure):
+    """Mirror of ``jdt::StageLeaf`` (ops/csrc/common.h)."""
+
+    _fields_ = [("off", ctypes.c_long), ("dim", c_int), ("per", c_int), ("cols", c_int), ("pad", c_int)]
+
+
+class StageMap(ctypes.Structure):
+    """Mirror of ``jdt::StageMap``: where a mode-0 producer writes each gradient element
+    of its leaves (W, b, head W, head b, metrics) in the fused FSDP collective's packed
+    staging layout (comm/csrc/xgmi.hip xg_fsdp_kernel, staged)."""
+
+    _fields_ = [("base", c_void_p), ("half", ctypes.c_long), ("slice", ctypes.c_long), ("W", c_int),
+                ("nleaf", c_int), ("leaf", StageLeaf * 5)]
+
+
+_lib.declare("jdt_stage_map_size", c_int, [])
+
+
+def stage_map_tensor(base: int, half: int, slice_: int, world: int, leaves, device) -> torch.Tensor:
+    """A device copy of a StageMap; ``leaves`` = 5 (off, dim, per, cols) tuples (None =
+    unused slot).  The engines pass its address as ``smap``."""
+    if _lib.lib().jdt_stage_map_size() != ctypes.sizeof(StageMap):
+        raise RuntimeError("StageMap layout mismatch")
+    m = StageMap()
+    m.base, m.half, m.slice, m.W, m.nleaf = base, half, slice_, world, 5
+    for k, lf in enumerate(leaves):
+        if lf is not None:
+            m.leaf[k] = StageLeaf(int(lf[0]), int(lf[1]), int(lf[2]), int(lf[3]), 0)
+    raw = torch.frombuffer(bytearray(bytes(m)), dtype=torch.uint8)
+    return raw.to(device)
 
 
 _lib.declare("jdt_mlp2", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_int, c_void_p])
@@ -181,6 +213,15 @@ class FusedMLP2:
         self.grad_stage = (int(base), int(stride))
         self._args = None
 
+    def set_fsdp_stage(self, layout: dict, base: int, half: int, slice_: int, world: int):
+        """Mode 0, FSDP N > 1: write the gradients and metric slots straight into the
+        fused FSDP collective's staging buffer (``layout``: leaf name -> (packed offset,
+        dim, per, cols), "metrics" included; XgmiComm.fsdp_stage_layout)."""
+        assert not self.fuse_opt
+        names = ["input_dense/kernel", "input_dense/bias", "output_dense/kernel", "output_dense/bias", "metrics"]
+        self.smap_t = stage_map_tensor(base, half, slice_, world, [layout[n] for n in names], self.P.master.device)
+        self._args = None
+
     def _build_args(self, batch) -> Mlp2Args:
         st, P = self.state, self.P
         o = st.opt_state
@@ -210,6 +251,8 @@ class FusedMLP2:
             a.gW1, a.gb1, a.gW2, a.gb2 = (base + 4 * P.offsets[n][0] for n in names)
             a.mslot = base + 4 * P.metric_off
             a.stage_stride = stride
+        if getattr(self, "smap_t", None) is not None:
+            a.smap = self.smap_t.data_ptr()
         a.fuse_opt = int(self.fuse_opt)
         a.XT, a.ldxt = self.XT.data_ptr(), self.Mp
         a.step_copy = self.step_copy.data_ptr()
@@ -392,7 +435,7 @@ class MdArgs(ctypes.Structure):
                 ("accumulate", c_int), ("dH", c_void_p), ("mb_rows", c_int), ("mb_stride", c_ulonglong),
                 ("stage_stride", ctypes.c_long), ("det_logits", c_void_p), ("step_mul", c_int),
                 ("XR", c_void_p), ("zslab", c_void_p), ("ztick", c_void_p), ("hand", c_void_p),
-                ("dzx", c_void_p), ("dzc", c_void_p), ("dzs", c_int)]
+                ("dzx", c_void_p), ("dzc", c_void_p), ("dzs", c_int), ("smap", c_void_p)]
 
 
 _lib.declare("jdt_md_layer", c_int, [ctypes.POINTER(MdArgs), c_int, c_int, c_void_p])
@@ -502,6 +545,18 @@ class FusedMLPDeep:
         self.grad_stage = (int(base), int(stride))
         self._args = None
 
+    def set_fsdp_stage(self, layout: dict, base: int, half: int, slice_: int, world: int):
+        """See FusedMLP2.set_fsdp_stage: one StageMap per hidden layer (its W / b, the
+        head's W / b, the metric slots)."""
+        assert not self.fuse_opt
+        L = self.model.L
+        dev = self.P.master.device
+        self.smap_t = [stage_map_tensor(base, half, slice_, world,
+                                        [layout[self.kn[i]], layout[self.bn[i]], layout[self.kn[L - 1]],
+                                         layout[self.bn[L - 1]], layout["metrics"]], dev)
+                       for i in range(self.nh)]
+        self._args = None
+
     def _shadow_pair(self, i):
         s0 = self.P.s(self.kn[i]).data_ptr()
         return s0, (self.par[i].data_ptr() if i in self.par else s0)
@@ -557,6 +612,8 @@ class FusedMLPDeep:
             a.gWh, a.gbh = base + 4 * P.offsets[self.kn[L - 1]][0], base + 4 * P.offsets[self.bn[L - 1]][0]
             a.mslot = base + 4 * P.metric_off
             a.stage_stride = stride
+        if getattr(self, "smap_t", None) is not None and phase == 1:
+            a.smap = self.smap_t[i].data_ptr()
         if self.fuse_opt:
             mm, vv = o["m"], o["v"]
 

@@ -136,6 +136,25 @@ def allreduce_fits(n: int, world: int, cap: int) -> dict:
     return {"oneshot": n > 0 and g1 * c1 <= cap, "twoshot": n > 0 and g2 * c2 * world <= cap}
 
 
+def stage_layout(S: "XgSegs", leaves, world: int) -> dict:
+    """{leaf name: (packed offset, dim, per, cols)} + "metrics" -- the common.h StageMap
+    leaves of a fused FSDP plan's segment table ``S`` (sharded leaves, replicated leaves,
+    then the metric slots): dim 0 = row shards of ``per`` rows, 1 = column shards of
+    ``per`` columns, 2 = the whole leaf in every peer slot."""
+    out = {}
+    for k, (name, shape, d) in enumerate(leaves):
+        g = S.seg[k]
+        cols = int(shape[-1]) if len(shape) == 2 else 1
+        if d is None:
+            out[name] = (int(g.off), 2, 1, cols)
+        elif d == 0:
+            out[name] = (int(g.off), 0, int(shape[0]) // world, cols)
+        else:
+            out[name] = (int(g.off), 1, int(shape[1]) // world, cols)
+    out["metrics"] = (int(S.seg[len(leaves)].off), 2, 1, 1)
+    return out
+
+
 def requested(mode: str, world: int, device: torch.device) -> bool:
     """Whether a trainer should try the xGMI path: ``mode`` in {"auto","xgmi","rccl"}
     (env ``JDT_COMM`` overrides "auto")."""
@@ -463,17 +482,7 @@ class XgmiComm:
         slots.  Returns {name: (packed offset, dim, per, cols)} plus "metrics", and
         "base" / "half" / "slice" of this rank's staging buffer."""
         S, _F = plan
-        out = {}
-        for k, (name, shape, d) in enumerate(leaves):
-            g = S.seg[k]
-            cols = int(shape[-1]) if len(shape) == 2 else 1
-            if d is None:
-                out[name] = (int(g.off), 2, 1, cols)
-            elif d == 0:
-                out[name] = (int(g.off), 0, int(shape[0]) // self.world, cols)
-            else:
-                out[name] = (int(g.off), 1, int(shape[1]) // self.world, cols)
-        out["metrics"] = (int(S.seg[len(leaves)].off), 2, 1, 1)
+        out = stage_layout(S, leaves, self.world)
         out["base"] = int(_lib.lib().jdt_xgmi_stage_base(self.ctx))
         out["half"] = self.capacity
         out["slice"] = int(_lib.lib().jdt_xgmi_seg_slice(int(S.S)))

@@ -108,6 +108,22 @@ def main():
             d = st_[:, i] - t0
             print(f"  {nm:32s} {float(d.median()):6.2f}  max {float(d.max()):6.2f}")
         print(f"  span first start -> last end: {float(st_[:, 4].max() - t0.min()):.2f} us")
+        # boundary between two consecutive run-ahead launches (the per-step gap of the graph)
+        sd = torch.zeros(4096 * 16, dtype=torch.int64, device=dev)
+        ah2 = type(eng._ahead_args)()
+        ctypes.memmove(ctypes.byref(ah2), ctypes.byref(ah), ctypes.sizeof(T))
+        ah2.stamps = sd.data_ptr()
+        gaps = []
+        for _ in range(a.iters):
+            _lib.check(L.jdt_mlp2(ctypes.byref(ah), 2, 784, 10, s), "bwd_ahead")
+            _lib.check(L.jdt_mlp2(ctypes.byref(ah2), 2, 784, 10, s), "bwd_ahead")
+            torch.cuda.synchronize()
+            x = sc.cpu()[: n * 16].view(n, 16).double() * 10e-3
+            y = sd.cpu()[: n * 16].view(n, 16).double() * 10e-3
+            gaps.append(float(y[:, 0].min() - x[:, 4].max()))
+        gaps.sort()
+        print(f"  run-ahead launch k last end -> launch k+1 first start: median {gaps[len(gaps) // 2]:.2f} us "
+              f"(min {gaps[0]:.2f}, max {gaps[-1]:.2f})")
 
 
 if __name__ == "__main__":

@@ -120,6 +120,10 @@ struct MdArgs {
   // metric slots straight into the fused FSDP collective's staging buffer (common.h
   // StageMap; leaves W_i, b_i, W_head, b_head, metrics), half = step parity
   const StageMap* smap;
+  // 1: the dW epilogue's AdamW state (p, m, v) and bf16 weight copies are stored
+  // write-through (agent-scope sc1) instead of left dirty in the L2 for the kernel
+  // boundary to write back (mlp_fused.hip Mlp2Args::wt)
+  int wt;
 };
 
 // Slots 0-4: s_memrealtime at the kernel's phase ends (tools/stamp_deep.py).
@@ -139,6 +143,11 @@ __device__ __forceinline__ MdAdam md_adam_consts(const MdArgs& a, int step) {
   k.rbc1 = 1.f / (1.f - powf(a.beta1, t));
   k.rbc2 = 1.f / (1.f - powf(a.beta2, t));
   return k;
+}
+
+// write-through (agent-scope sc1) fp32 store: the line is not left dirty in this XCD's L2
+__device__ __forceinline__ void md_st(float* p, float v) {
+  __hip_atomic_store((__attribute__((address_space(1))) float*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ float md_adam(float p, float m, float v, float g, const MdAdam& k, float* pp, float* mp,
@@ -698,7 +707,13 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
     for (int e = 0; e < 4; ++e) {
       const long idx = (long)(trow0 + e) * N + tcol;
       if (a.fuse_opt) {
-        const bf16_t pb = f2bf(md_adam(op[e], om[e], ov[e], acc[e], ak, a.pW + idx, a.mW + idx, a.vW + idx));
+        float tp, tm, tv;
+        const bf16_t pb = f2bf(md_adam(op[e], om[e], ov[e], acc[e], ak, &tp, &tm, &tv));
+        if (a.wt) {
+          md_st(a.pW + idx, tp); md_st(a.mW + idx, tm); md_st(a.vW + idx, tv);
+        } else {
+          a.pW[idx] = tp; a.mW[idx] = tm; a.vW[idx] = tv;
+        }
         Wsn[idx] = pb;
         wtp[e >> 1] |= (unsigned)pb << (16 * (e & 1));
       } else if (a.smap) {
@@ -707,8 +722,15 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
         a.gW[goff + idx] = (a.accumulate ? op[e] : 0.f) + acc[e];   // mode 0 loaded the old grad into op
       }
     }
-    if (a.fuse_opt && a.WTout)
-      *reinterpret_cast<uint2*>(a.WTout + (long)tcol * a.ldwt + trow0) = make_uint2(wtp[0], wtp[1]);
+    if (a.fuse_opt && a.WTout) {
+      bf16_t* const wto = a.WTout + (long)tcol * a.ldwt + trow0;
+      if (a.wt)
+        __hip_atomic_store((__attribute__((address_space(1))) unsigned long long*)wto,
+                           (unsigned long long)wtp[0] | ((unsigned long long)wtp[1] << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      else
+        *reinterpret_cast<uint2*>(wto) = make_uint2(wtp[0], wtp[1]);
+    }
     if constexpr (AHEAD)
       *reinterpret_cast<uint2*>(&w1n[(lane & 15) * LDW1 + (trow0 - kc0)]) = make_uint2(wtp[0], wtp[1]);
   } else if (aux) {

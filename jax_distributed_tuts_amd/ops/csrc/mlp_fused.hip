@@ -103,6 +103,13 @@ struct Mlp2Args {
   // buffer in the fused FSDP collective's packed layout (common.h StageMap; leaves W1,
   // b1, W2, b2, metrics), half = step parity; null = plain stores at g* (+ goff)
   const StageMap* smap;
+  // run-ahead backward only: bit 0 = the W1 AdamW state (p, m, v) and the W1^T copy are
+  // stored write-through (sc1), bit 1 = the Z1 partials and G1 / H1 too.  A plain store
+  // leaves its line dirty in this XCD's L2 and the kernel boundary writes every dirty
+  // line back before the next launch starts (~B / 6 TB/s on the boundary, guide
+  // "boundary" row); written through, those bytes drain during the kernel's own
+  // latency-bound run-ahead phases instead.
+  int wt;
 };
 
 // Persistent multi-step launch (mlp2_loop_kernel): n steps, grid barriers between
@@ -746,7 +753,15 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     for (int e = 0; e < 4; ++e) {
       const long idx = (long)(trow0 + e) * H + tcol;   // K_IN % KC == 0: always in range
       if (a.fuse_opt) {
-        const bf16_t pb = f2bf(adam_apply(op[e], om[e], ov[e], acc[e], ak, a.pW1 + idx, a.mW1 + idx, a.vW1 + idx));
+        float tp, tm = om[e], tv = ov[e];
+        const bf16_t pb = f2bf(adam_apply(op[e], om[e], ov[e], acc[e], ak, &tp, &tm, &tv));
+        if (AHEAD && (a.wt & 1)) {
+          st_f<true>(a.pW1 + idx, tp);
+          if (!ak.sgd) { st_f<true>(a.mW1 + idx, tm); st_f<true>(a.vW1 + idx, tv); }
+        } else {
+          a.pW1[idx] = tp;
+          if (!ak.sgd) { a.mW1[idx] = tm; a.vW1[idx] = tv; }   // SGD: m / v alias p (unused)
+        }
         // with the W1^T copy, the [in,out] bf16 shadow is rebuilt from it by
         // FusedMLP2.finalize() instead of being written every step (0.8 MB of HBM writes)
         if (!a.W1T) a.sW1[idx] = pb;
@@ -758,8 +773,11 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
       }
     }
     // the lane's 4 rows are 4 consecutive K elements of W1^T: one 8-byte store
-    if (a.fuse_opt && a.W1T)
-      st_u64<LOOP>(a.W1T + (long)tcol * a.ldw1t + trow0, (unsigned long long)wt[0] | ((unsigned long long)wt[1] << 32));
+    if (a.fuse_opt && a.W1T) {
+      const unsigned long long w8 = (unsigned long long)wt[0] | ((unsigned long long)wt[1] << 32);
+      if (LOOP || (AHEAD && (a.wt & 1))) st_u64<true>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
+      else st_u64<false>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
+    }
     if constexpr (AHEAD)
       *reinterpret_cast<uint2*>(&w1n[(lane & 15) * LDW1 + (trow0 - kc0)]) = make_uint2(wt[0], wt[1]);
   } else if (aux) {
@@ -853,8 +871,12 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     // lives in that XCD's L2: plain stores (L1 is write-through) drained by vmcnt, an
     // L2 counter (workgroup-scope atomics), loads with sc1 (never served by the L1).
     float* const zb = a.zslab + (long)bx * NCH * (MPM / 4) * 64;
-    *reinterpret_cast<u32x4*>(zb + ((long)by * (MPM / 4) + w * 4 + (lane >> 4)) * 64 + (lane & 15) * 4) =
-        (u32x4){__float_as_uint(z[0]), __float_as_uint(z[1]), __float_as_uint(z[2]), __float_as_uint(z[3])};
+    {
+      const long zo = ((long)by * (MPM / 4) + w * 4 + (lane >> 4)) * 64 + (lane & 15) * 4;
+      const u32x4 zv = {__float_as_uint(z[0]), __float_as_uint(z[1]), __float_as_uint(z[2]), __float_as_uint(z[3])};
+      if (a.wt & 2) st_b128<true>(zb + zo, zv);
+      else *reinterpret_cast<u32x4*>(zb + zo) = zv;
+    }
     // step t+1's dropout bits of this thread's epilogue element, computed while the
     // partial store drains (off the phase-0 critical path)
     if (a.keep < 1.f && eg < g_hi && eg * 4 < M)
@@ -930,7 +952,8 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         hvn = bf2f(hb);
         // G1 / H1 element (row group eg, column j0+gn, slot ee) of the dropout-group layout
         const long gq = ((long)eg * H + j0 + gn) * 4 + ee;
-        a.G1[gq] = gd;
+        if (a.wt & 2) st_f<true>(a.G1 + gq, gd);
+        else a.G1[gq] = gd;
         a.H1[gq] = hb;
       }
       htA[(tid >> 6) * 4 + ee][gn] = hvn;

@@ -42,7 +42,7 @@ class Mlp2Args(ctypes.Structure):
                 ("step_copy", c_void_p), ("W2snap", c_void_p), ("stage_stride", ctypes.c_long),
                 ("det_logits", c_void_p),
                 ("XR", c_void_p), ("zslab", c_void_p), ("ztick", c_void_p), ("hand", c_void_p), ("lg3", c_int),
-                ("opt_sgd", c_int), ("smap", c_void_p)]
+                ("opt_sgd", c_int), ("smap", c_void_p), ("wt", c_int)]
 
 
 class StageLeaf(ctypes.Structure):
@@ -254,6 +254,7 @@ class FusedMLP2:
         if getattr(self, "smap_t", None) is not None:
             a.smap = self.smap_t.data_ptr()
         a.fuse_opt = int(self.fuse_opt)
+        a.wt = int(os.environ.get("JDT_MLP2_WT", "0"))   # run-ahead write-through stores (A/B)
         a.XT, a.ldxt = self.XT.data_ptr(), self.Mp
         a.step_copy = self.step_copy.data_ptr()
         a.W2snap = self.W2snap.data_ptr()
@@ -435,7 +436,7 @@ class MdArgs(ctypes.Structure):
                 ("accumulate", c_int), ("dH", c_void_p), ("mb_rows", c_int), ("mb_stride", c_ulonglong),
                 ("stage_stride", ctypes.c_long), ("det_logits", c_void_p), ("step_mul", c_int),
                 ("XR", c_void_p), ("zslab", c_void_p), ("ztick", c_void_p), ("hand", c_void_p),
-                ("dzx", c_void_p), ("dzc", c_void_p), ("dzs", c_int), ("smap", c_void_p)]
+                ("dzx", c_void_p), ("dzc", c_void_p), ("dzs", c_int), ("smap", c_void_p), ("wt", c_int)]
 
 
 _lib.declare("jdt_md_layer", c_int, [ctypes.POINTER(MdArgs), c_int, c_int, c_void_p])
@@ -603,6 +604,7 @@ class FusedMLPDeep:
         if i >= 1:
             a.dZout = self.dZ[i].data_ptr()
         a.fuse_opt = int(self.fuse_opt)
+        a.wt = int(os.environ.get("JDT_MD_WT", "0"))   # write-through AdamW state stores (A/B)
         a.gW, a.gb = P.g(self.kn[i]).data_ptr(), P.g(self.bn[i]).data_ptr()
         a.gWh, a.gbh = P.g(self.kn[L - 1]).data_ptr(), P.g(self.bn[L - 1]).data_ptr()
         a.mslot = self.mslot.data_ptr()

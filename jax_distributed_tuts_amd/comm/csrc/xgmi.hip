@@ -98,6 +98,9 @@ struct XgAdam {  // fused AdamW + metrics fold over the reduced buffer (phase 2)
   int* step;
   unsigned* ticket;
   float* zero;     // zero these indices of this buffer after reading (the grad bucket) or null
+  // 1: do not advance *step at the end (one of several per-bucket calls of a step that
+  // overlap the backward, parallel/pipeline.py; the step's last call advances it)
+  int hold;
 };
 
 enum { XG_ALLREDUCE = 0, XG_REDUCE_SCATTER = 1, XG_ALL_GATHER = 2 };
@@ -384,7 +387,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_kernel(XgPeers P, int rank, lon
   }
   if (nit == 0) xg_barrier(P, rank, W, 1, epoch, timeout, XG_SITE_TWOSHOT);
   if (threadIdx.x == 0) me->epoch[b] = epoch;
-  if (fuse && A.step) {
+  if (fuse && A.step && !A.hold) {
     __syncthreads();
     if (threadIdx.x == 0) {
       const unsigned t = atomicAdd(A.ticket, 1u);
@@ -497,7 +500,7 @@ __global__ void __launch_bounds__(XG_THREADS) xg_oneshot_kernel(XgPeers P, int r
     }
   }
   if (threadIdx.x == 0) me->epoch[b] = epoch;
-  if (fuse && A.step) {
+  if (fuse && A.step && !A.hold) {
     __syncthreads();
     if (threadIdx.x == 0) {
       const unsigned t = atomicAdd(A.ticket, 1u);

@@ -54,6 +54,7 @@ class XgAdam(ctypes.Structure):
         ("n_params", c_long), ("running", c_void_p), ("n_metrics", c_int),
         ("lr", c_float), ("b1", c_float), ("b2", c_float), ("eps", c_float), ("wd", c_float),
         ("grad_scale", c_float), ("step", c_void_p), ("ticket", c_void_p), ("zero", c_void_p),
+        ("hold", c_int),
     ]
 
 
@@ -287,10 +288,13 @@ class XgmiComm:
     def all_reduce_adamw_(self, grad: torch.Tensor, *, p: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                           shadow: Optional[torch.Tensor], n_params: int, running: Optional[torch.Tensor],
                           n_metrics: int, lr: float, b1: float, b2: float, eps: float, wd: float,
-                          grad_scale: float, step: torch.Tensor, ticket: torch.Tensor, zero_grad: bool = True):
+                          grad_scale: float, step: torch.Tensor, ticket: torch.Tensor, zero_grad: bool = True,
+                          advance: bool = True):
         """SUM-all-reduce ``grad`` and, in the same kernel, AdamW on ``p[:n_params]``
         (grads scaled by ``grad_scale``: the 1/(n_mb*N) mean) and
-        ``running[j] += grad_sum[n_params + j]`` for the metric slots."""
+        ``running[j] += grad_sum[n_params + j]`` for the metric slots.  ``advance=False``:
+        leave the step counter to a later call of the same step (per-bucket calls; every
+        call of a step reads the same step for the bias correction)."""
         self._check_f32(grad)
         a = XgAdam()
         a.p, a.m, a.v, a.shadow = _ptr(p), _ptr(m), _ptr(v), _ptr(shadow)
@@ -298,6 +302,7 @@ class XgmiComm:
         a.lr, a.b1, a.b2, a.eps, a.wd, a.grad_scale = float(lr), float(b1), float(b2), float(eps), float(wd), float(grad_scale)
         a.step, a.ticket = _ptr(step), _ptr(ticket)
         a.zero = _ptr(grad) if zero_grad else c_void_p(0)
+        a.hold = 0 if advance else 1
         rc = _lib.lib().jdt_xgmi_allreduce(self.ctx, _ptr(grad), c_void_p(0), grad.numel(), ctypes.byref(a),
                                            self.timeout, c_void_p(_lib.stream_ptr()))
         _lib.check(rc, "jdt_xgmi_allreduce(adamw)")

@@ -152,6 +152,11 @@ class PipeConfig:
     # S > 1 (xGMI inbox hand-offs): microbatch chains of a stage on concurrent streams
     # (mb_streams of them) -- opt-in, see GPipeTrainer._streams_ok
     multi_stage_streams: bool = field(default_factory=lambda: os.environ.get("JDT_PP_STREAMS", "0") == "1")
+    # S > 1 with a data axis on the xGMI all-reduce + AdamW kernel: the data-axis sync is
+    # issued per part (embedding, each layer, head) on a comm stream as soon as the W pass
+    # has produced that part's weight gradients, instead of one call after the whole W
+    # pass (GPipeTrainer._overlapped_sync).  JDT_PP_OVERLAP_SYNC=0: one call (A/B)
+    overlap_data_sync: bool = field(default_factory=lambda: os.environ.get("JDT_PP_OVERLAP_SYNC", "1") == "1")
 
 
 def _no_dropout(model) -> bool:
@@ -387,6 +392,9 @@ class GPipeTrainer:
                 on.main.wait_stream(w)
             on.join()
             return
+        if arena is not None and not on.side and self._overlap_sync_ok():
+            self._overlapped_sync(P, arena)
+            return
         if arena is not None:
             # the W pass: every weight gradient of the step, one GEMM per weight over all
             # rows (the GEMMs round-robin over the streams once every chain has finished)
@@ -395,6 +403,64 @@ class GPipeTrainer:
             nw = max(1, int(self.cfg.wpass_rr) or len(on.side) + 1)
             self.model.weight_grads(P, arena, wgrad=self.wgrad, opt=eo, on=lambda j: on(j % nw))
         on.join()
+
+    def _overlap_sync_ok(self) -> bool:
+        return (self.S > 1 and self.cfg.overlap_data_sync and self._xg_fused_opt and self.wgrad is None
+                and self.dev.type == "cuda" and hasattr(self.model, "weight_grads_of") and hw_queues() >= 2)
+
+    def _sync_buckets(self):
+        """The overlapped data-axis sync's buckets, in issue order: (part, lo, hi,
+        metrics, advance).  A part's flat range runs from its first parameter to the next
+        part's (FlatParams offsets are 4-aligned, every range a valid kernel bucket); the
+        last range in flat order -- the head, or the top layer -- also carries the metric
+        slots, and the last bucket issued advances the optimizer step."""
+        if getattr(self, "_buckets", None) is None:
+            P, m = self.state.params, self.model
+            starts = []
+            if m.has_embed:
+                starts.append(("embed", P.offsets["embed/wte"][0]))
+            for l in m.layers:
+                starts.append((l, P.offsets[f"block_{l}/ln1/scale"][0]))
+            if m.has_head:
+                starts.append(("head", P.offsets["ln_f/scale"][0]))
+            starts.sort(key=lambda t: t[1])
+            rng = {}
+            for k, (part, lo) in enumerate(starts):
+                hi = starts[k + 1][1] if k + 1 < len(starts) else P.numel
+                rng[part] = (lo, hi, k + 1 == len(starts))
+            order = (["embed"] if m.has_embed else []) + (["head"] if m.has_head else []) + list(reversed(list(m.layers)))
+            self._buckets = [(part, *rng[part], i + 1 == len(order)) for i, part in enumerate(order)]
+        return self._buckets
+
+    def _overlapped_sync(self, P, arena):
+        """The W pass with the data-axis sync overlapped: each part's weight-gradient
+        GEMMs on the main stream, then that part's xGMI all-reduce + AdamW on a comm
+        stream (the kernel only reads the part's final gradients and writes its
+        parameters / moments / shadow, which nothing on the main stream touches until the
+        join).  Same per-element reduction order and AdamW as the single call."""
+        st, cfg = self.state, self.cfg
+        tx, o = st.tx, st.opt_state
+        scale = 1.0 / (cfg.num_microbatches * self.n_dp)
+        main = torch.cuda.current_stream(self.dev)
+        cs = getattr(self, "_comm_stream", None)
+        if cs is None:
+            cs = self._comm_stream = torch.cuda.Stream(self.dev)
+        G = P.grad
+        j = 0
+        for part, lo, hi, metrics, advance in self._sync_buckets():
+            if part != "embed":
+                j = self.model.weight_grads_of(P, arena, part, j0=j)
+            cs.wait_stream(main)
+            with torch.cuda.stream(cs), named_scope(f"sync_grads_{part}"):
+                end = G.numel() if metrics else hi
+                self.xg.all_reduce_adamw_(
+                    G[lo:end], p=P.master[lo:end], m=o["m"][lo:end], v=o["v"][lo:end], shadow=P.shadow[lo:end],
+                    n_params=hi - lo, running=self.metrics if metrics else None,
+                    n_metrics=N_METRIC_SLOTS if metrics else 0, lr=tx.learning_rate, b1=tx.b1, b2=tx.b2,
+                    eps=tx.eps, wd=tx.weight_decay, grad_scale=scale, step=o["count"], ticket=o["ticket"],
+                    zero_grad=True, advance=advance)
+        main.wait_stream(cs)
+        self._synced = True
 
     def _layer_major_wpass(self, batch, P, st, seed, eo, n_mb) -> bool:
         """One stage, one pass over all rows, weight gradients deferred (cfg.wpass_streams
@@ -634,6 +700,9 @@ class GPipeTrainer:
         'data' only; then AdamW on the local stage and the metrics fold.  The host
         step counter is advanced by the callers."""
         st, P, cfg = self.state, self.state.params, self.cfg
+        if getattr(self, "_synced", False):   # the W pass issued the sync per part (_overlapped_sync)
+            self._synced = False
+            return
         scale = 1.0 / (cfg.num_microbatches * self.n_dp)
         ov = getattr(self, "_ov_opt", None)
         if ov and ov.forked:   # AdamW already forked layer by layer during the backward

@@ -26,7 +26,7 @@ def test_xgmi_collectives(tmp_path, ws):
     for r, o in enumerate(_load(tmp_path, "xg", ws)):
         assert o["ok"], f"rank {r}: communicator self-test failed"
         assert all(o["ar"].values()), o["ar"]
-        assert o["fused"] and o["rs"] and o["ag"] and o["graph"], o
+        assert o["fused"] and o["rs"] and o["ag"] and o["graph"] and o["bucketed"], o
         assert o["err"] == 0
         # per-size transport calibration ran, set the measured one-shot crossover and
         # reports RCCL as unavailable on the shared-GPU (gloo-bootstrapped) job
@@ -186,6 +186,9 @@ def test_transformer_hybrid_over_xgmi_matches_single_device(tmp_path, ws, n_laye
     spawn(functools.partial(XW.lm_pp_xgmi, dp=2, n_layers=n_layers), ws, str(tmp_path), gpu=True)
     res = _load(tmp_path, "lmx2", ws)
     assert all(o["comm"] == "xgmi" for o in res)
+    # the data-axis sync ran per part, overlapping the W pass (pipeline._overlapped_sync):
+    # embedding / layers / head buckets, one step advance per step
+    assert all(o["buckets"] >= 2 for o in res)
     dev = torch.device("cuda", 0)
     cfg = TransformerConfig(vocab_size=512, d_model=128, n_heads=2, d_ff=256, seq_len=64, n_layers=n_layers)
     tr, _ = build_lm_pipeline(None, dev, cfg, num_microbatches=4)  # dp=2 x 2 microbatches == 4 microbatches

@@ -115,6 +115,28 @@ def collectives(outdir):
         fused["running"] &= bool(torch.allclose(run.cpu(), runr, rtol=1e-6, atol=1e-6))
         fused["step"] &= int(step.item()) == 6 + it and int(ticket.item()) == 0
         fused["zero"] &= bool((gr == 0).all())
+    # per-bucket calls of one step (parallel/pipeline._overlapped_sync): the first holds
+    # the step counter (advance=False), the last advances it and folds the metrics --
+    # equal to one call over the whole bucket
+    gs = [torch.randn(total, generator=torch.Generator().manual_seed(90 + q)) for q in range(W)]
+    outs = []
+    for split in (False, True):
+        pa, ma, va = p0.to(dev), m0.to(dev), v0.to(dev)
+        sa, ra = torch.empty_like(sh), run0.to(dev)
+        sta, tka = torch.tensor([5], dtype=torch.int32, device=dev), torch.zeros(1, dtype=torch.int32, device=dev)
+        ga = gs[r].to(dev)
+        kw = dict(lr=1e-3, b1=0.9, b2=0.999, eps=1e-8, wd=1e-4, grad_scale=0.25, step=sta, ticket=tka)
+        if split:
+            c = 2048
+            comm.all_reduce_adamw_(ga[:c], p=pa[:c], m=ma[:c], v=va[:c], shadow=sa[:c], n_params=c, running=None,
+                                   n_metrics=0, advance=False, **kw)
+            comm.all_reduce_adamw_(ga[c:], p=pa[c:], m=ma[c:], v=va[c:], shadow=sa[c:], n_params=npar - c,
+                                   running=ra, n_metrics=4, **kw)
+        else:
+            comm.all_reduce_adamw_(ga, p=pa, m=ma, v=va, shadow=sa, n_params=npar, running=ra, n_metrics=4, **kw)
+        torch.cuda.synchronize()
+        outs.append([t.cpu() for t in (pa, ma, va, sa, ra, sta, tka, ga)])
+    res["bucketed"] = all(torch.equal(x, y) for x, y in zip(*outs)) and int(outs[1][5].item()) == 6
     res["fused_detail"] = fused
     fused_ok = all(fused.values())
     res["fused"] = fused_ok
@@ -311,7 +333,8 @@ def lm_pp_xgmi(outdir, dp, steps=3, n_layers=2):
     torch.cuda.synchronize()
     tr.finalize()
     _save(outdir, f"lmx{dp}", {"params": {k: v.cpu() for k, v in tr.state.params.state_dict().items()},
-                               "metrics": tr.gather_metrics().cpu(), "comm": tr.comm_backend})
+                               "metrics": tr.gather_metrics().cpu(), "comm": tr.comm_backend,
+                               "buckets": len(getattr(tr, "_buckets", None) or [])})
 
 
 def fault_timeout(outdir):

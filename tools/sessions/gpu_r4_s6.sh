@@ -24,6 +24,19 @@ for r in 1 2; do
   run "rep $r pp8 md_wt=0" "JDT_MD_WT=0" "--strategy pp --hidden-layers 8"
   run "rep $r pp8 md_wt=1" "JDT_MD_WT=1" "--strategy pp --hidden-layers 8"
 done
+# per-part data-axis sync overlapping the W pass (pipeline._overlapped_sync): tests, then
+# DP2 x PP2 LM (4 ranks sharing the GPU) A/B
+timeout -k 10 400 python -u -m pytest tests/test_xgmi_gpu.py -m gpu -x -q --timeout 240 --timeout-method thread \
+  -k "collectives or transformer_hybrid" > gpurun_out/s6/pytest_xg.log 2>&1
+rc=$?; echo "pytest xgmi (overlap sync) rc=$rc"; tail -3 gpurun_out/s6/pytest_xg.log
+[ $rc -ne 0 ] && { grep -E "FAILED|Error|assert" gpurun_out/s6/pytest_xg.log | head -20; exit $rc; }
+for r in 1 2; do
+  for ov in 1 0; do
+    JDT_BACKEND=gloo JDT_PP_OVERLAP_SYNC=$ov timeout -k 10 200 python bench.py --gpus 4 --strategy pp --dp 2 --model transformer \
+      --steps 60 --warmup 10 > gpurun_out/s6/lm$ov.log 2>&1 || { echo "lm bench ov=$ov failed"; tail -5 gpurun_out/s6/lm$ov.log; exit 1; }
+    echo "rep $r DP2xPP2 LM overlap_sync=$ov: $(grep '^{' gpurun_out/s6/lm$ov.log | python -c 'import json,sys; j=json.loads(sys.stdin.read()); print(j["value"], j["ms_per_step"])')"
+  done
+done
 for wt in 0 3; do
   JDT_MLP2_WT=$wt timeout -k 10 120 python tools/stamp_mlp2.py > gpurun_out/s6/stamps_wt$wt.log 2>&1 || { echo stamps failed; tail -5 gpurun_out/s6/stamps_wt$wt.log; exit 1; }
   echo "--- stamps wt=$wt"; grep -E "run-ahead|span|column barrier|Z1 partial|dW1" gpurun_out/s6/stamps_wt$wt.log | tail -8

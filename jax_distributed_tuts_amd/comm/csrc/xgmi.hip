@@ -101,6 +101,9 @@ struct XgAdam {  // fused AdamW + metrics fold over the reduced buffer (phase 2)
   // 1: do not advance *step at the end (one of several per-bucket calls of a step that
   // overlap the backward, parallel/pipeline.py; the step's last call advances it)
   int hold;
+  // 1: p / m / v / shadow stored write-through (agent-scope sc1): not left dirty in this
+  // XCD's L2 for the kernel boundary to write back (ops/csrc/mlp_fused.hip Mlp2Args::wt)
+  int wt;
 };
 
 enum { XG_ALLREDUCE = 0, XG_REDUCE_SCATTER = 1, XG_ALL_GATHER = 2 };
@@ -165,6 +168,31 @@ __device__ __forceinline__ void store_guard(float* dst, long e, long n, float4 x
   if (e + 2 < n) dst[e + 2] = x.z;
 }
 
+typedef __attribute__((address_space(1))) unsigned long long xg_gu64;
+__device__ __forceinline__ void wt_store8(void* p, unsigned long long x) {
+  __hip_atomic_store((xg_gu64*)p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // global_store ... sc1
+}
+__device__ __forceinline__ void wt_store16(float* p, float4 x) {
+  wt_store8(p, (unsigned long long)__float_as_uint(x.x) | ((unsigned long long)__float_as_uint(x.y) << 32));
+  wt_store8(p + 2, (unsigned long long)__float_as_uint(x.z) | ((unsigned long long)__float_as_uint(x.w) << 32));
+}
+// the fused AdamW's stores of element group e: p, m, v and the bf16 shadow
+__device__ __forceinline__ void adam_store(const XgAdam& A, long e, float4 pp, float4 mm, float4 vv) {
+  unsigned long long sh = 0ull;
+  if (A.shadow)
+    sh = (unsigned long long)((unsigned)f2bf(pp.x) | ((unsigned)f2bf(pp.y) << 16)) |
+         ((unsigned long long)((unsigned)f2bf(pp.z) | ((unsigned)f2bf(pp.w) << 16)) << 32);
+  if (A.wt) {
+    wt_store16(A.p + e, pp); wt_store16(A.m + e, mm); wt_store16(A.v + e, vv);
+    if (A.shadow) wt_store8(A.shadow + e, sh);
+  } else {
+    *reinterpret_cast<float4*>(A.p + e) = pp;
+    *reinterpret_cast<float4*>(A.m + e) = mm;
+    *reinterpret_cast<float4*>(A.v + e) = vv;
+    if (A.shadow) *reinterpret_cast<unsigned long long*>(A.shadow + e) = sh;
+  }
+}
+
 __device__ __forceinline__ float4 adam4(const XgAdam& A, long e, float4 g, float rbc1, float rbc2) {
   float4 pp = *reinterpret_cast<float4*>(A.p + e);
   float4 mm = *reinterpret_cast<float4*>(A.m + e);
@@ -177,15 +205,7 @@ __device__ __forceinline__ float4 adam4(const XgAdam& A, long e, float4 g, float
     ve[k] = A.b2 * ve[k] + (1.f - A.b2) * gr * gr;
     pe[k] -= A.lr * ((me[k] * rbc1) / (sqrtf(ve[k] * rbc2) + A.eps) + A.wd * pe[k]);
   }
-  *reinterpret_cast<float4*>(A.p + e) = pp;
-  *reinterpret_cast<float4*>(A.m + e) = mm;
-  *reinterpret_cast<float4*>(A.v + e) = vv;
-  if (A.shadow) {
-    uint2 s;
-    s.x = (unsigned)f2bf(pp.x) | ((unsigned)f2bf(pp.y) << 16);
-    s.y = (unsigned)f2bf(pp.z) | ((unsigned)f2bf(pp.w) << 16);
-    *reinterpret_cast<uint2*>(A.shadow + e) = s;
-  }
+  adam_store(A, e, pp, mm, vv);
   return pp;
 }
 
@@ -218,15 +238,7 @@ __device__ __forceinline__ float4 adam4_pre(const XgAdam& A, long e, float4 g, f
     ve[k] = A.b2 * ve[k] + (1.f - A.b2) * gr * gr;
     pe[k] -= A.lr * ((me[k] * rbc1) / (sqrtf(ve[k] * rbc2) + A.eps) + A.wd * pe[k]);
   }
-  *reinterpret_cast<float4*>(A.p + e) = pp;
-  *reinterpret_cast<float4*>(A.m + e) = mm;
-  *reinterpret_cast<float4*>(A.v + e) = vv;
-  if (A.shadow) {
-    uint2 s;
-    s.x = (unsigned)f2bf(pp.x) | ((unsigned)f2bf(pp.y) << 16);
-    s.y = (unsigned)f2bf(pp.z) | ((unsigned)f2bf(pp.w) << 16);
-    *reinterpret_cast<uint2*>(A.shadow + e) = s;
-  }
+  adam_store(A, e, pp, mm, vv);
   return pp;
 }
 

@@ -46,6 +46,13 @@ HANDLE_BYTES = 64
 TICKS_PER_S = 100_000_000  # s_memrealtime
 
 
+def xg_wt() -> int:
+    """JDT_XG_WT: the fused AdamW of the xGMI kernels stores p / m / v / shadow
+    write-through (1) or plain (0) -- the kernel boundary then has fewer dirty L2 lines
+    to write back (the md_bwd / run-ahead mlp2_bwd switch, profiles/r4_write_through_ab.txt)."""
+    return int(os.environ.get("JDT_XG_WT", "0"))
+
+
 class XgAdam(ctypes.Structure):
     """Mirror of ``jdt::XgAdam`` (comm/csrc/xgmi.hip)."""
 
@@ -54,7 +61,7 @@ class XgAdam(ctypes.Structure):
         ("n_params", c_long), ("running", c_void_p), ("n_metrics", c_int),
         ("lr", c_float), ("b1", c_float), ("b2", c_float), ("eps", c_float), ("wd", c_float),
         ("grad_scale", c_float), ("step", c_void_p), ("ticket", c_void_p), ("zero", c_void_p),
-        ("hold", c_int),
+        ("hold", c_int), ("wt", c_int),
     ]
 
 
@@ -297,6 +304,7 @@ class XgmiComm:
         call of a step reads the same step for the bias correction)."""
         self._check_f32(grad)
         a = XgAdam()
+        a.wt = xg_wt()
         a.p, a.m, a.v, a.shadow = _ptr(p), _ptr(m), _ptr(v), _ptr(shadow)
         a.n_params, a.running, a.n_metrics = int(n_params), _ptr(running), int(n_metrics if running is not None else 0)
         a.lr, a.b1, a.b2, a.eps, a.wd, a.grad_scale = float(lr), float(b1), float(b2), float(eps), float(wd), float(grad_scale)
@@ -334,6 +342,7 @@ class XgmiComm:
         staging copy; the producer and this kernel pick the buffer half from the
         parity of ``step`` (the optimizer counter this kernel advances)."""
         a = XgAdam()
+        a.wt = xg_wt()
         a.p, a.m, a.v, a.shadow = _ptr(p), _ptr(m), _ptr(v), _ptr(shadow)
         a.n_params, a.running, a.n_metrics = int(n_params), _ptr(running), int(n_metrics if running is not None else 0)
         a.lr, a.b1, a.b2, a.eps, a.wd, a.grad_scale = float(lr), float(b1), float(b2), float(eps), float(wd), float(grad_scale)
@@ -472,6 +481,7 @@ class XgmiComm:
         off += w
         S.n, S.S = k + 1, off
         a = F.A
+        a.wt = xg_wt()
         a.p, a.m, a.v, a.shadow = _ptr(p), _ptr(m), _ptr(v), _ptr(shadow)
         a.n_params, a.running, a.n_metrics = 0, _ptr(running), int(ms.numel())
         a.lr, a.b1, a.b2, a.eps, a.wd, a.grad_scale = (float(lr), float(b1), float(b2), float(eps), float(wd),

@@ -306,16 +306,37 @@ class TransformerLM:
         next j0."""
         if opt is not None:
             opt.only_contribution = True
-        if part == "head":
-            order = [("head/kernel", arena.head["hf"], arena.head["dlog"])]
-        else:
-            a, b = arena.blocks[part], f"block_{part}"
-            order = [(f"{b}/mlp/fc2/kernel", a["u"], a["dx3"]), (f"{b}/mlp/fc1/kernel", a["h2"], a["dz1"]),
-                     (f"{b}/attn/out/kernel", a["o"], a["dx2"]), (f"{b}/attn/qkv/kernel", a["h1"], a["dqkv"])]
+        order = self.weight_grad_items(arena, part)
         for j, (name, h, dz) in enumerate(order):
             with (on(j0 + j) if on is not None else contextlib.nullcontext()):
                 K.dw_gemm(None, h, dz, P.g(name), opt=opt, name=name)
         return j0 + len(order)
+
+    @staticmethod
+    def weight_grad_items(arena: WGradArena, part):
+        """(weight name, A rows, dZ rows) of one part's deferred weight-gradient GEMMs,
+        in the W pass's order (``weight_grads_of``)."""
+        if part == "head":
+            return [("head/kernel", arena.head["hf"], arena.head["dlog"])]
+        a, b = arena.blocks[part], f"block_{part}"
+        return [(f"{b}/mlp/fc2/kernel", a["u"], a["dx3"]), (f"{b}/mlp/fc1/kernel", a["h2"], a["dz1"]),
+                (f"{b}/attn/out/kernel", a["o"], a["dx2"]), (f"{b}/attn/qkv/kernel", a["h1"], a["dqkv"])]
+
+    def sync_groups(self):
+        """The stage's parameters cut into groups that become final one at a time in the
+        W pass: (key, first parameter) in W-pass order -- "embed" (its gradient is final
+        when the backward chain ends), then one group per weight-gradient GEMM, keyed by
+        the weight: the GEMM's weight plus the bias / LayerNorm parameters that follow it
+        in the flat layout up to the next group (computed by the chain, already final);
+        a layer's qkv group starts at its ln1 (parallel/pipeline.py _sync_buckets)."""
+        out = [("embed", "embed/wte")] if self.has_embed else []
+        if self.has_head:
+            out.append(("head/kernel", "ln_f/scale"))
+        for l in reversed(list(self.layers)):
+            b = f"block_{l}"
+            out += [(f"{b}/mlp/fc2/kernel", f"{b}/mlp/fc2/kernel"), (f"{b}/mlp/fc1/kernel", f"{b}/mlp/fc1/kernel"),
+                    (f"{b}/attn/out/kernel", f"{b}/attn/out/kernel"), (f"{b}/attn/qkv/kernel", f"{b}/ln1/scale")]
+        return out
 
 
 def _into(dst: Optional[torch.Tensor], src: torch.Tensor) -> torch.Tensor:

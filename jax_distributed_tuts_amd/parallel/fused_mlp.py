@@ -254,7 +254,9 @@ class FusedMLP2:
         if getattr(self, "smap_t", None) is not None:
             a.smap = self.smap_t.data_ptr()
         a.fuse_opt = int(self.fuse_opt)
-        a.wt = int(os.environ.get("JDT_MLP2_WT", "0"))   # run-ahead write-through stores (A/B)
+        # run-ahead: the W1 AdamW state and W1^T stored write-through (+1.0 % steps/s,
+        # profiles/r4_write_through_ab.txt; 3 = also the Z1 partials and G1: no gain)
+        a.wt = int(os.environ.get("JDT_MLP2_WT", "1"))
         a.XT, a.ldxt = self.XT.data_ptr(), self.Mp
         a.step_copy = self.step_copy.data_ptr()
         a.W2snap = self.W2snap.data_ptr()
@@ -604,7 +606,7 @@ class FusedMLPDeep:
         if i >= 1:
             a.dZout = self.dZ[i].data_ptr()
         a.fuse_opt = int(self.fuse_opt)
-        a.wt = int(os.environ.get("JDT_MD_WT", "0"))   # write-through AdamW state stores (A/B)
+        a.wt = int(os.environ.get("JDT_MD_WT", "1"))   # write-through AdamW state (+3 %, r4_write_through_ab.txt)
         a.gW, a.gb = P.g(self.kn[i]).data_ptr(), P.g(self.bn[i]).data_ptr()
         a.gWh, a.gbh = P.g(self.kn[L - 1]).data_ptr(), P.g(self.bn[L - 1]).data_ptr()
         a.mslot = self.mslot.data_ptr()

@@ -153,9 +153,10 @@ class PipeConfig:
     # (mb_streams of them) -- opt-in, see GPipeTrainer._streams_ok
     multi_stage_streams: bool = field(default_factory=lambda: os.environ.get("JDT_PP_STREAMS", "0") == "1")
     # S > 1 with a data axis on the xGMI all-reduce + AdamW kernel: the data-axis sync is
-    # issued per part (embedding, each layer, head) on a comm stream as soon as the W pass
-    # has produced that part's weight gradients, instead of one call after the whole W
-    # pass (GPipeTrainer._overlapped_sync).  JDT_PP_OVERLAP_SYNC=0: one call (A/B)
+    # issued per group (the embedding, then each weight-gradient GEMM's weight with the
+    # bias / LayerNorm parameters beside it) on a comm stream as soon as the W pass has
+    # produced that group's gradients, instead of one call after the whole W pass
+    # (GPipeTrainer._overlapped_sync).  JDT_PP_OVERLAP_SYNC=0: one call (A/B)
     overlap_data_sync: bool = field(default_factory=lambda: os.environ.get("JDT_PP_OVERLAP_SYNC", "1") == "1")
 
 
@@ -406,38 +407,32 @@ class GPipeTrainer:
 
     def _overlap_sync_ok(self) -> bool:
         return (self.S > 1 and self.cfg.overlap_data_sync and self._xg_fused_opt and self.wgrad is None
-                and self.dev.type == "cuda" and hasattr(self.model, "weight_grads_of") and hw_queues() >= 2)
+                and self.dev.type == "cuda" and hasattr(self.model, "sync_groups") and hw_queues() >= 2)
 
     def _sync_buckets(self):
-        """The overlapped data-axis sync's buckets, in issue order: (part, lo, hi,
-        metrics, advance).  A part's flat range runs from its first parameter to the next
-        part's (FlatParams offsets are 4-aligned, every range a valid kernel bucket); the
-        last range in flat order -- the head, or the top layer -- also carries the metric
-        slots, and the last bucket issued advances the optimizer step."""
+        """The overlapped data-axis sync's buckets, in issue order: (key, lo, hi, metrics,
+        advance).  One bucket per group of ``model.sync_groups`` (the embedding, then one
+        per weight-gradient GEMM in W-pass order), each the flat range from the group's
+        first parameter to the next group's (FlatParams offsets are 4-aligned, so every
+        range is a valid kernel bucket); the range that ends the flat buffer also carries
+        the metric slots, and the last bucket issued advances the optimizer step."""
         if getattr(self, "_buckets", None) is None:
-            P, m = self.state.params, self.model
-            starts = []
-            if m.has_embed:
-                starts.append(("embed", P.offsets["embed/wte"][0]))
-            for l in m.layers:
-                starts.append((l, P.offsets[f"block_{l}/ln1/scale"][0]))
-            if m.has_head:
-                starts.append(("head", P.offsets["ln_f/scale"][0]))
-            starts.sort(key=lambda t: t[1])
+            P = self.state.params
+            groups = self.model.sync_groups()
+            starts = sorted((P.offsets[first][0], key) for key, first in groups)
             rng = {}
-            for k, (part, lo) in enumerate(starts):
-                hi = starts[k + 1][1] if k + 1 < len(starts) else P.numel
-                rng[part] = (lo, hi, k + 1 == len(starts))
-            order = (["embed"] if m.has_embed else []) + (["head"] if m.has_head else []) + list(reversed(list(m.layers)))
-            self._buckets = [(part, *rng[part], i + 1 == len(order)) for i, part in enumerate(order)]
+            for k, (lo, key) in enumerate(starts):
+                hi = starts[k + 1][0] if k + 1 < len(starts) else P.numel
+                rng[key] = (lo, hi, k + 1 == len(starts))
+            self._buckets = [(key, *rng[key], i + 1 == len(groups)) for i, (key, _) in enumerate(groups)]
         return self._buckets
 
     def _overlapped_sync(self, P, arena):
-        """The W pass with the data-axis sync overlapped: each part's weight-gradient
-        GEMMs on the main stream, then that part's xGMI all-reduce + AdamW on a comm
-        stream (the kernel only reads the part's final gradients and writes its
-        parameters / moments / shadow, which nothing on the main stream touches until the
-        join).  Same per-element reduction order and AdamW as the single call."""
+        """The W pass with the data-axis sync overlapped: each weight-gradient GEMM on the
+        main stream, then its group's xGMI all-reduce + AdamW on a comm stream (the kernel
+        only reads the group's final gradients and writes its parameters / moments /
+        shadow, which nothing on the main stream touches until the join).  Same
+        per-element reduction order and AdamW as the single call."""
         st, cfg = self.state, self.cfg
         tx, o = st.tx, st.opt_state
         scale = 1.0 / (cfg.num_microbatches * self.n_dp)
@@ -446,12 +441,16 @@ class GPipeTrainer:
         if cs is None:
             cs = self._comm_stream = torch.cuda.Stream(self.dev)
         G = P.grad
-        j = 0
-        for part, lo, hi, metrics, advance in self._sync_buckets():
-            if part != "embed":
-                j = self.model.weight_grads_of(P, arena, part, j0=j)
+        gemms = {}
+        for part in (["head"] if self.model.has_head else []) + list(self.model.layers):
+            for name, h, dz in self.model.weight_grad_items(arena, part):
+                gemms[name] = (h, dz)
+        for key, lo, hi, metrics, advance in self._sync_buckets():
+            if key != "embed":
+                h, dz = gemms[key]
+                K.dw_gemm(None, h, dz, P.g(key), name=key)
             cs.wait_stream(main)
-            with torch.cuda.stream(cs), named_scope(f"sync_grads_{part}"):
+            with torch.cuda.stream(cs), named_scope("sync_grads_part"):
                 end = G.numel() if metrics else hi
                 self.xg.all_reduce_adamw_(
                     G[lo:end], p=P.master[lo:end], m=o["m"][lo:end], v=o["v"][lo:end], shadow=P.shadow[lo:end],

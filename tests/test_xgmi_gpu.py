@@ -187,8 +187,8 @@ def test_transformer_hybrid_over_xgmi_matches_single_device(tmp_path, ws, n_laye
     res = _load(tmp_path, "lmx2", ws)
     assert all(o["comm"] == "xgmi" for o in res)
     # the data-axis sync ran per part, overlapping the W pass (pipeline._overlapped_sync):
-    # embedding / layers / head buckets, one step advance per step
-    assert all(o["buckets"] >= 2 for o in res)
+    # a bucket per weight-gradient GEMM (+ embedding), one step advance per step
+    assert all(o["buckets"] >= 4 for o in res)
     dev = torch.device("cuda", 0)
     cfg = TransformerConfig(vocab_size=512, d_model=128, n_heads=2, d_ff=256, seq_len=64, n_layers=n_layers)
     tr, _ = build_lm_pipeline(None, dev, cfg, num_microbatches=4)  # dp=2 x 2 microbatches == 4 microbatches

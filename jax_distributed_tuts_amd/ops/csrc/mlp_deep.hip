@@ -120,9 +120,10 @@ struct MdArgs {
   // metric slots straight into the fused FSDP collective's staging buffer (common.h
   // StageMap; leaves W_i, b_i, W_head, b_head, metrics), half = step parity
   const StageMap* smap;
-  // 1: the dW epilogue's AdamW state (p, m, v) and bf16 weight copies are stored
-  // write-through (agent-scope sc1) instead of left dirty in the L2 for the kernel
-  // boundary to write back (mlp_fused.hip Mlp2Args::wt)
+  // bit 0: the dW epilogue's AdamW state (p, m, v) and the K-contiguous bf16 copy are
+  // stored write-through (agent-scope sc1) instead of left dirty in the L2 for the
+  // kernel boundary to write back (mlp_fused.hip Mlp2Args::wt); bit 1: the row-major
+  // bf16 shadow of the next step too
   int wt;
 };
 
@@ -702,6 +703,7 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       }
     }
     bf16_t* Wsn = const_cast<bf16_t*>(par ? a.Ws0 : a.Ws1);   // next step's parity of the row-major shadow
+    const __amdgpu_buffer_rsrc_t wsn_r = __builtin_amdgcn_make_buffer_rsrc(Wsn, (short)0, 0x7fffffff, 0x00020000);
     unsigned wtp[2] = {0u, 0u};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -709,12 +711,15 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
       if (a.fuse_opt) {
         float tp, tm, tv;
         const bf16_t pb = f2bf(md_adam(op[e], om[e], ov[e], acc[e], ak, &tp, &tm, &tv));
-        if (a.wt) {
+        if (a.wt & 1) {
           md_st(a.pW + idx, tp); md_st(a.mW + idx, tm); md_st(a.vW + idx, tv);
         } else {
           a.pW[idx] = tp; a.mW[idx] = tm; a.vW[idx] = tv;
         }
-        Wsn[idx] = pb;
+        if (a.wt & 2)   // the next step's bf16 row-major shadow, write-through too
+          __builtin_amdgcn_raw_buffer_store_b16((unsigned short)pb, wsn_r, (int)(idx * 2), 0, 16);
+        else
+          Wsn[idx] = pb;
         wtp[e >> 1] |= (unsigned)pb << (16 * (e & 1));
       } else if (a.smap) {
         stage_store(a.smap, par, 0, trow0 + e, tcol, acc[e]);
@@ -724,7 +729,7 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
     }
     if (a.fuse_opt && a.WTout) {
       bf16_t* const wto = a.WTout + (long)tcol * a.ldwt + trow0;
-      if (a.wt)
+      if (a.wt & 1)
         __hip_atomic_store((__attribute__((address_space(1))) unsigned long long*)wto,
                            (unsigned long long)wtp[0] | ((unsigned long long)wtp[1] << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);

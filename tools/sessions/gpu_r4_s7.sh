@@ -26,6 +26,9 @@ for r in 1 2; do
 done
 for r in 1 2; do
   run "rep $r headline (wt defaults)" "" "--steps 300 --warmup 30"
-  run "rep $r 4-layer (wt defaults)" "" "--num-layers 4 --steps 300 --warmup 30"
+  run "rep $r 4-layer md_wt=1 (default)" "" "--num-layers 4 --steps 300 --warmup 30"
+  run "rep $r 4-layer md_wt=3 (+ row-major shadow)" "JDT_MD_WT=3" "--num-layers 4 --steps 300 --warmup 30"
+  run "rep $r pp8 md_wt=3" "JDT_MD_WT=3" "--strategy pp --hidden-layers 8 --steps 300 --warmup 30"
+  run "rep $r pp8 md_wt=1" "JDT_MD_WT=1" "--strategy pp --hidden-layers 8 --steps 300 --warmup 30"
 done
 echo done

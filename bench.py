@@ -328,6 +328,7 @@ def main():
     if args.strategy == "pp":
         desc["single_stage_mode"] = tr.single_stage_mode  # how a 1-stage pipeline ran its microbatches
         desc["stage_streams"] = tr.stage_streams          # concurrent microbatch chains per stage
+        desc["data_sync"] = tr.data_sync_mode             # data-axis sync: per W-pass group or one call
     if D.rank() == 0:
         out = {"metric": METRIC, "value": round(sps, 2), "unit": "steps/s", "n_gpus": ws, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 5), "higher_is_better": True,

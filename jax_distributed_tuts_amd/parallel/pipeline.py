@@ -156,8 +156,11 @@ class PipeConfig:
     # issued per group (the embedding, then each weight-gradient GEMM's weight with the
     # bias / LayerNorm parameters beside it) on a comm stream as soon as the W pass has
     # produced that group's gradients, instead of one call after the whole W pass
-    # (GPipeTrainer._overlapped_sync).  JDT_PP_OVERLAP_SYNC=0: one call (A/B)
-    overlap_data_sync: bool = field(default_factory=lambda: os.environ.get("JDT_PP_OVERLAP_SYNC", "1") == "1")
+    # (GPipeTrainer._overlapped_sync).  "auto": when every rank has a GPU of its own --
+    # with ranks sharing one GPU it measured 4.4x SLOWER (profiles/r4_overlap_sync_ab.txt:
+    # the comm streams' spinning collectives time-share the card's queues, as the
+    # multi-stage streams above); "1" / "0" force it (JDT_PP_OVERLAP_SYNC)
+    overlap_data_sync: str = field(default_factory=lambda: os.environ.get("JDT_PP_OVERLAP_SYNC", "auto"))
 
 
 def _no_dropout(model) -> bool:
@@ -245,6 +248,11 @@ class GPipeTrainer:
 
             self.xg = create_for(mesh, cfg.data_axis, P.grad.numel(), self.dev, cfg.comm)
             self._xg_fused_opt = self.xg is not None and isinstance(state.tx, AdamW)
+        # ranks time-sharing one GPU (rehearsals): schedules with concurrent spinning
+        # streams stay off in "auto" mode (collective: every rank builds its trainer)
+        from ..runtime.dist import ranks_share_gpu
+
+        self._gpu_shared = ranks_share_gpu() if self.dev.type == "cuda" else False
 
     # ------------------------------------------------------------------ p2p
     def _setup_p2p(self, mb: int):
@@ -406,8 +414,20 @@ class GPipeTrainer:
         on.join()
 
     def _overlap_sync_ok(self) -> bool:
-        return (self.S > 1 and self.cfg.overlap_data_sync and self._xg_fused_opt and self.wgrad is None
-                and self.dev.type == "cuda" and hasattr(self.model, "sync_groups") and hw_queues() >= 2)
+        mode = str(self.cfg.overlap_data_sync)
+        on = mode == "1" or (mode == "auto" and not self._gpu_shared)
+        return (on and self.S > 1 and self._xg_fused_opt and self.wgrad is None and self.dev.type == "cuda"
+                and hasattr(self.model, "sync_groups") and hw_queues() >= 2)
+
+    @property
+    def data_sync_mode(self) -> str:
+        """How the data-axis sync runs (bench JSON): "none" (no data axis), "one call",
+        or "overlapped (k buckets)" -- per W-pass group on a comm stream."""
+        if self.n_dp == 1:
+            return "none"
+        if self._overlap_sync_ok():
+            return f"overlapped ({len(self._sync_buckets())} buckets)"
+        return "one call"
 
     def _sync_buckets(self):
         """The overlapped data-axis sync's buckets, in issue order: (key, lo, hi, metrics,

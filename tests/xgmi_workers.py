@@ -324,6 +324,7 @@ def lm_pp_xgmi(outdir, dp, steps=3, n_layers=2):
     cfg = TransformerConfig(vocab_size=512, d_model=128, n_heads=2, d_ff=256, seq_len=64, n_layers=n_layers)
     mesh = D.Mesh({"data": dp, "pipe": D.world_size() // dp})
     tr, _ = build_lm_pipeline(mesh, dev, cfg, num_microbatches=2, comm="xgmi")
+    tr.cfg.overlap_data_sync = "1"   # "auto" keeps it off with ranks sharing the GPU; test the path
     b = shard_batch(lm_batch(cfg, global_batch=8, seed=1), mesh, "data")
     b = Batch(b.inputs.to(dev), b.labels.to(dev))
     tr.step(b)

@@ -313,6 +313,31 @@ __device__ __forceinline__ float4 sys_load4(__amdgpu_buffer_rsrc_t r, long float
 __device__ __forceinline__ void sys_store4(__amdgpu_buffer_rsrc_t r, long float_off, float4 x) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sys_u32x4, x), r, (int)(float_off * 4), 0, CPOL_SYS);
 }
+__device__ __forceinline__ float sys_load1(__amdgpu_buffer_rsrc_t r, long float_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)(float_off * 4), 0, CPOL_SYS));
+}
+__device__ __forceinline__ void sys_store1(__amdgpu_buffer_rsrc_t r, long float_off, float x) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), r, (int)(float_off * 4), 0, CPOL_SYS);
+}
+
+// ---------------------------------------------------------------- tile exchange (N > 1 run-ahead step)
+// The data-parallel step of the fused 2-layer engine at N > 1 as ONE launch per step
+// (mlp_fused.hip mlp2_bwd AHEAD with Mlp2Args::tx): every workgroup all-reduces its own
+// gradient tile with the same tile of the other ranks' launches -- a two-shot exchange
+// per tile (tile T is summed by rank T % W, in rank order, and the sum pushed back to
+// every rank) -- then applies AdamW and runs the next step's forward exactly as on one
+// GPU.  IPC buffers (comm/csrc/tile_exchange.hip): per rank a partial inbox
+// [tile][src][pay] floats, a reduced inbox [tile][pay] floats and an uncached signal
+// page: flag[tile * TX_MAX_RANKS + src] (partial of src arrived), then
+// flag[tiles * TX_MAX_RANKS + tile] (reduced tile arrived); epochs = optimizer step + 1.
+constexpr int TX_MAX_RANKS = 8;
+struct TxArgs {
+  float* part[TX_MAX_RANKS];      // rank q's partial inbox (IPC-mapped)
+  float* red[TX_MAX_RANKS];       // rank q's reduced inbox
+  unsigned* flag[TX_MAX_RANKS];   // rank q's signal page
+  int rank, world, tiles, pay;    // pay: floats per tile payload
+  long long timeout;              // s_memrealtime ticks (100 MHz) per wait
+};
 
 }  // namespace jdt
 

@@ -110,6 +110,9 @@ struct Mlp2Args {
   // "boundary" row); written through, those bytes drain during the kernel's own
   // latency-bound run-ahead phases instead.
   int wt;
+  // N > 1 run-ahead step: the per-tile gradient exchange with the other ranks' launches
+  // (common.h TxArgs, device memory; null = one GPU)
+  const TxArgs* tx;
 };
 
 // Persistent multi-step launch (mlp2_loop_kernel): n steps, grid barriers between
@@ -502,6 +505,102 @@ __device__ __forceinline__ void mlp2_fwd_body(AT& a, const int bx, const int by,
 }
 
 // ---------------------------------------------------------------------------- backward
+// ---------------------------------------------------------------------------- N > 1 tile exchange
+// Two-shot all-reduce of one workgroup's gradient values with the same tile T of the
+// other ranks' launches (common.h TxArgs): tile T belongs to rank T % W.  A non-owner
+// pushes its values into the owner's partial inbox (system-scope write-through stores,
+// drained, then ONE lane raises the owner's flag [T][rank]) and waits for the reduced
+// tile; the owner waits for the W - 1 flags, sums in rank order (own values at its rank
+// -- so every rank gets bit-identical sums, as comm/csrc/xgmi.hip), pushes the sum into
+// every peer's reduced inbox and raises their flags [T].  Each thread moves only its own
+// values: n4 float4 at payload offsets p4[] and one scalar at ps (ps < 0: none).  Every
+// wait is bounded (s_memrealtime); a timeout sets bit 2 of the error word and the tile
+// goes on with what it has (the host raises on the word).
+__device__ __forceinline__ bool tx_wait(const unsigned* f, unsigned epoch, long long timeout, unsigned* err) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+    if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout) {
+      atomicOr(err, 4u);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+__device__ __forceinline__ void tx_tile(const TxArgs* X, int T, unsigned epoch, int n4, float4 (&v4)[2],
+                                        const int (&p4)[2], float& vs, int ps, unsigned* err) {
+  const int R = X->rank, W = X->world, own = T % W, tid = threadIdx.x;
+  const long pay = X->pay, tiles = X->tiles;
+  const unsigned long long tb = (unsigned long long)pay * 4ull;
+  if (R != own) {
+    const __amdgpu_buffer_rsrc_t dst = sys_rsrc(X->part[own] + ((long)T * TX_MAX_RANKS + R) * pay, tb);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (k < n4) sys_store4(dst, p4[k], v4[k]);
+    if (ps >= 0) sys_store1(dst, ps, vs);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its pushes
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_store(X->flag[own] + (long)T * TX_MAX_RANKS + R, epoch, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      tx_wait(X->flag[R] + tiles * TX_MAX_RANKS + T, epoch, X->timeout, err);
+    }
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t src = sys_rsrc(X->red[R] + (long)T * pay, tb);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (k < n4) v4[k] = sys_load4(src, p4[k]);
+    if (ps >= 0) vs = sys_load1(src, ps);
+    return;
+  }
+  if (tid < W && tid != R) tx_wait(X->flag[R] + (long)T * TX_MAX_RANKS + tid, epoch, X->timeout, err);
+  __syncthreads();
+  const float* inbox = X->part[R] + (long)T * TX_MAX_RANKS * pay;
+  // the rank-ordered sum, peers' partials loaded 4 ranks at a time (all 4 in flight)
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {   // k = 0, 1: the float4 slots; k = 2: the scalar
+    if (k < 2 ? k >= n4 : ps < 0) continue;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int g = 0; g < TX_MAX_RANKS; g += 4) {
+      if (g >= W) break;
+      float4 in[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = g + u;
+        if (q < W && q != R) {
+          const __amdgpu_buffer_rsrc_t src = sys_rsrc(inbox + (long)q * pay, tb);
+          in[u] = k < 2 ? sys_load4(src, p4[k]) : make_float4(sys_load1(src, ps), 0.f, 0.f, 0.f);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = g + u;
+        if (q >= W) break;
+        const float4 x = q == R ? (k < 2 ? v4[k] : make_float4(vs, 0.f, 0.f, 0.f)) : in[u];
+        if (q == 0) acc = x;
+        else { acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w; }
+      }
+    }
+    if (k < 2) v4[k] = acc;
+    else vs = acc.x;
+  }
+#pragma unroll
+  for (int q = 0; q < TX_MAX_RANKS; ++q) {
+    if (q >= W || q == R) continue;
+    const __amdgpu_buffer_rsrc_t dst = sys_rsrc(X->red[q] + (long)T * pay, tb);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (k < n4) sys_store4(dst, p4[k], v4[k]);
+    if (ps >= 0) sys_store1(dst, ps, vs);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid < W && tid != R)
+    __hip_atomic_store(X->flag[tid] + tiles * TX_MAX_RANKS + T, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // AHEAD (single GPU, fused AdamW, W1^T copy): after its AdamW epilogue every
 // workgroup (blk, chunk) also computes the partial Z1 = X[:, chunk] W1'[chunk, blk]
 // of the NEXT step from the W1' tile it just produced (phase 5); the last of a
@@ -511,7 +610,7 @@ __device__ __forceinline__ void mlp2_fwd_body(AT& a, const int bx, const int by,
 // replaced by a per-column-block arrival ticket among workgroups that share an XCD
 // (xcd_contiguous_tile), and the one global dependency left -- complete logits for
 // the next CE -- is the launch boundary.
-template <int K_IN, int C, int KC, bool LOOP, bool AHEAD = false, class AT>
+template <int K_IN, int C, int KC, bool LOOP, bool AHEAD = false, bool TX = false, class AT>
 __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by, const int step_in) {
   constexpr int MPM = 128;                 // max rows per device (fused path)
   constexpr int LDM = MPM + 8;             // padded row (bf16 elements)
@@ -738,8 +837,11 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   STAMP(2);
 
   // ---- 3. dW1[chunk, blk] = X[:, chunk]^T dZ1[:, blk]   (K = rows) on MFMA; one tile per wave
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  // chunk-0 blocks' spare wave, concurrently with the dW1 tiles:
+  //   dW2[blk, :] = H1[:, blk]^T dlogits ; db1[blk] = dZ1[:, blk]^T 1 ; db2 = 1^T dlogits (block (0,0))
+  f32x4 aw = {0.f, 0.f, 0.f, 0.f}, ab1 = {0.f, 0.f, 0.f, 0.f}, ab2 = {0.f, 0.f, 0.f, 0.f};
   if (w < NTILE) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < MPM / 32; ++ks) {
       if (ks < Mp / 32) {
@@ -748,6 +850,60 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         acc = mfma16x16x32(xf[ks], bfr, acc);
       }
     }
+  } else if (aux) {
+    bf16x8 ones;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ones[q] = (short)0x3f80;  // bf16 1.0
+#pragma unroll
+    for (int ks = 0; ks < MPM / 32; ++ks) {
+      if (ks >= Mp / 32) break;
+      const int kk = ks * 32 + 8 * (lane >> 4);
+      const bf16x8 hT = *reinterpret_cast<const bf16x8*>(&h1T[(lane & 15) * LDM + kk]);
+      const bf16x8 dT = *reinterpret_cast<const bf16x8*>(&dlT[(lane & 15) * LDM + kk]);
+      const bf16x8 zT = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
+      aw = mfma16x16x32(hT, dT, aw);
+      ab1 = mfma16x16x32(zT, ones, ab1);
+      if (lead) ab2 = mfma16x16x32(ones, dT, ab2);
+    }
+  }
+  // N > 1 (Mlp2Args::tx): this tile's gradients -- and the lead's db2 and metric slots --
+  // all-reduced with the same tile of the other ranks' launches before the optimizer
+  float mval = 0.f;
+  if constexpr (AHEAD && TX) {
+    {
+      if (lead && tid < 4) {
+        float L = 0.f, Cr = 0.f;
+        for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
+        mval = tid == 0 ? L : tid == 2 ? Cr : (float)M;   // {loss sum, n, correct, n}
+      }
+      float4 v4[2];
+      int p4[2], n4 = 0, ps = -1;
+      float vs = 0.f;
+      if (w < NTILE) {
+        v4[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        p4[0] = w * 256 + lane * 4;
+        n4 = 1;
+        if (lead && tid < 4) { vs = mval; ps = (NTILE + 2) * 256 + 64 + tid; }
+      } else if (aux) {
+        v4[0] = make_float4(aw[0], aw[1], aw[2], aw[3]);
+        v4[1] = make_float4(ab1[0], ab1[1], ab1[2], ab1[3]);
+        p4[0] = NTILE * 256 + lane * 4;
+        p4[1] = (NTILE + 1) * 256 + lane * 4;
+        n4 = 2;
+        if (lead && lane < C) { vs = ab2[0]; ps = (NTILE + 2) * 256 + lane; }
+      }
+      tx_tile(a.tx, bx * NCH + by, (unsigned)step + 1u, n4, v4, p4, vs, ps, a.ztick + 1);
+      if (w < NTILE) {
+        acc = (f32x4){v4[0].x, v4[0].y, v4[0].z, v4[0].w};
+        if (lead && tid < 4) mval = vs;
+      } else if (aux) {
+        aw = (f32x4){v4[0].x, v4[0].y, v4[0].z, v4[0].w};
+        ab1 = (f32x4){v4[1].x, v4[1].y, v4[1].z, v4[1].w};
+        if (lead && lane < C) ab2[0] = vs;
+      }
+    }
+  }
+  if (w < NTILE) {
     unsigned wt[2] = {0u, 0u};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -781,23 +937,6 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     if constexpr (AHEAD)
       *reinterpret_cast<uint2*>(&w1n[(lane & 15) * LDW1 + (trow0 - kc0)]) = make_uint2(wt[0], wt[1]);
   } else if (aux) {
-    // chunk-0 blocks, concurrently with the dW1 tiles:
-    //   dW2[blk, :] = H1[:, blk]^T dlogits ; db1[blk] = dZ1[:, blk]^T 1 ; db2 = 1^T dlogits (block (0,0))
-    bf16x8 ones;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) ones[q] = (short)0x3f80;  // bf16 1.0
-    f32x4 aw = {0.f, 0.f, 0.f, 0.f}, ab1 = {0.f, 0.f, 0.f, 0.f}, ab2 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < MPM / 32; ++ks) {
-      if (ks >= Mp / 32) break;
-      const int kk = ks * 32 + 8 * (lane >> 4);
-      const bf16x8 hT = *reinterpret_cast<const bf16x8*>(&h1T[(lane & 15) * LDM + kk]);
-      const bf16x8 dT = *reinterpret_cast<const bf16x8*>(&dlT[(lane & 15) * LDM + kk]);
-      const bf16x8 zT = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
-      aw = mfma16x16x32(hT, dT, aw);
-      ab1 = mfma16x16x32(zT, ones, ab1);
-      if (lead) ab2 = mfma16x16x32(ones, dT, ab2);
-    }
     bf16_t* sW2n = par ? a.sW2_0 : a.sW2_1;   // next step's parity buffer
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -837,9 +976,12 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   STAMP(3);
 
   if (lead && tid < 4) {
-    float L = 0.f, Cr = 0.f;
-    for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
-    const float val = tid == 0 ? L : tid == 2 ? Cr : (float)M;   // {loss sum, n, correct, n}
+    float val = mval;   // N > 1 run-ahead: the all-reduced slot
+    if (!(AHEAD && TX)) {
+      float L = 0.f, Cr = 0.f;
+      for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
+      val = tid == 0 ? L : tid == 2 ? Cr : (float)M;   // {loss sum, n, correct, n}
+    }
     if (fo && a.running) a.running[tid] = run_pre + val;
     else if (a.smap) stage_store(a.smap, par, 4, tid, 0, val);
     else if (a.mslot) a.mslot[goff + tid] = val;
@@ -990,12 +1132,12 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   if constexpr (XCD) xcd_contiguous_tile(bx, by);
   mlp2_fwd_body<K_IN, C, RB, DIRECT, false>(static_cast<const Mlp2Args&>(a), bx, by, 0);
 }
-template <int K_IN, int C, int KC, bool XCD, bool AHEAD = false>
+template <int K_IN, int C, int KC, bool XCD, bool AHEAD = false, bool TX = false>
 __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   int bx = blockIdx.x, by = blockIdx.y;
   if constexpr (AHEAD) xcd_column_tile(bx, by);
   else if constexpr (XCD) xcd_contiguous_tile(bx, by);
-  mlp2_bwd_body<K_IN, C, KC, false, AHEAD>(static_cast<const Mlp2Args&>(a), bx, by, 0);
+  mlp2_bwd_body<K_IN, C, KC, false, AHEAD, TX>(static_cast<const Mlp2Args&>(a), bx, by, 0);
 }
 
 // n complete training steps in ONE launch (single GPU, fused AdamW, W1^T copy):
@@ -1165,6 +1307,21 @@ JDT_API int jdt_mlp2_ahead_ok(int M, int H) {
   return (H / 16) * (784 / 112) <= cus * per ? 1 : 0;
 }
 
+// 1 if the N > 1 run-ahead backward (tile exchange, Mlp2Args::tx) can run here with
+// `nshare` ranks' grids on this GPU (1 = a GPU per rank): every workgroup of every
+// sharing rank's launch must be resident at once -- a tile waits for the same tile of
+// the other ranks' launches, and a column block for its own workgroups.
+JDT_API int jdt_mlp2_ahead_tx_ok(int M, int H, int nshare) {
+  if (!jdt_mlp2_ahead_ok(M, H) || nshare < 1) return 0;
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, mlp2_bwd_kernel<784, 10, 112, true, true, true>, NT, 0) !=
+          hipSuccess)
+    return 0;
+  return (long)nshare * (H / 16) * (784 / 112) <= (long)cus * per ? 1 : 0;
+}
+
 // phase 0: mlp2_fwd, 1: mlp2_bwd, 2: run-ahead mlp2_bwd (backward of t + forward of t+1)
 JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* stream) {
   const Mlp2Args& a = *args;
@@ -1196,7 +1353,8 @@ JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* str
         a.H % 128)
       return -3;
     const dim3 g(a.H / 16, 784 / 112);
-    hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true, true>), g, dim3(NT), 0, st, a);
+    if (a.tx) hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true, true, true>), g, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true, true>), g, dim3(NT), 0, st, a);
   }
   return HIP_LAUNCH_CHECK();
 }

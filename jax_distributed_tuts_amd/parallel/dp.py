@@ -143,14 +143,41 @@ class DataParallelTrainer:
         if self.fused is None:
             from .fused_mlp import make_engine
 
-            # a step with a collective keeps the optimizer out of the backward epilogue
+            # a step with a collective keeps the optimizer out of the backward epilogue --
+            # unless the tiles exchange their gradients inside the run-ahead launch (N > 1,
+            # one launch per step, _tile_exchange)
+            tx, share = self._tile_exchange(batch)
             self.fused = make_engine(self.state, self.mesh, self.cfg.axis, self.cfg.num_minibatches, batch.size,
-                                     self.metrics, batch.inputs.device, fuse_opt=False if self._coll else None)
+                                     self.metrics, batch.inputs.device,
+                                     fuse_opt=True if tx is not None else (False if self._coll else None),
+                                     tx=tx, ranks_on_gpu=share)
             if self.fused is None:
                 self.cfg.accum = "fused"  # shapes outside the fused kernels' envelope
                 return None
             self._setup_stage()
         return self.fused
+
+    def _tile_exchange(self, batch: Batch):
+        """(TileExchange, ranks sharing this GPU) for the one-launch N > 1 step, or
+        (None, 1): the 2-layer fused engine with a fused optimizer (AdamW / plain SGD),
+        not deterministic, every rank's run-ahead grid co-resident with the grids of the
+        ranks sharing its GPU -- agreed by all ranks (collective: every rank builds its
+        engine on the same step).  JDT_DP_AHEAD=0: the three-launch step (A/B)."""
+        if not (self.world > 1 and batch.inputs.is_cuda and os.environ.get("JDT_DP_AHEAD", "1") == "1"):
+            return None, 1
+        from ..comm import tile_exchange as TX
+        from ..runtime.dist import ranks_per_gpu
+        from .fused_mlp import _is_adamw, _is_plain_sgd, deterministic, supported
+
+        share = ranks_per_gpu()
+        H = self.model.dims[1] if len(getattr(self.model, "dims", ())) == 3 else 0
+        local = (supported(self.model, batch.size, batch.inputs.device) and H > 0 and not deterministic()
+                 and (_is_adamw(self.state.tx) or _is_plain_sgd(self.state.tx))
+                 and TX.ahead_tx_ok(batch.size, H, share))
+        if not TX.agree(self.mesh.group(self.cfg.axis), local, batch.inputs.device):
+            return None, 1
+        tx = TX.create_for(self.mesh, self.cfg.axis, batch.inputs.device, tiles=(H // 16) * (784 // 112))
+        return tx, share
 
     def _setup_stage(self):
         """N > 1 with the fused xGMI all-reduce + AdamW: the backward kernel writes the
@@ -302,11 +329,16 @@ class DataParallelTrainer:
             idx.fill_(i)
             g.replay()
 
+    @property
+    def one_launch(self) -> bool:
+        """N > 1 step as one run-ahead launch with the in-kernel tile exchange."""
+        return getattr(self.fused, "tx", None) is not None
+
     def sync(self):
         """pmean(grads) + psum(metrics) as SUM all-reduce(s) of the flat bucket(s); the
         1/N of the mean is applied by the optimizer."""
         P = self.state.params
-        if not self._coll:
+        if not self._coll or self.one_launch:   # one-launch step: summed inside the backward launch
             return
         with named_scope("sync_grads"):
             if self.xg is not None:
@@ -392,7 +424,7 @@ class DataParallelTrainer:
             # with step t's forward, "primed" does not -- after a run-ahead launch the
             # forward of the next step is already done (FusedMLP2.ahead_primed).
             loop = self.world == 1 and getattr(self.fused, "loop_ok", False)
-            ahead = self.world == 1 and not loop and getattr(self.fused, "ahead_ok", False)
+            ahead = (self.world == 1 or self.one_launch) and not loop and getattr(self.fused, "ahead_ok", False)
             if ahead:
                 from .fused_mlp import AheadGraphs
 
@@ -421,7 +453,7 @@ class DataParallelTrainer:
 
     def update_noncounting(self):
         P = self.state.params
-        if self._xg_fused_opt:
+        if self._xg_fused_opt or self.one_launch:
             return  # AdamW + metrics fold ran inside the xGMI all-reduce kernel (sync)
         if self.fused is not None:
             if self.fused.fuse_opt:
@@ -444,8 +476,8 @@ class DataParallelTrainer:
         bucket all-reduce (xGMI: with the fused AdamW + metrics fold) -- bracketed by
         hipEvents in separate, untimed eager steps (complete training steps: they
         advance the state like any other).  None for N = 1 or off-GPU."""
-        if not self._coll or not self.state.params.master.is_cuda:
-            return None
+        if not self._coll or not self.state.params.master.is_cuda or self.one_launch:
+            return None   # (one-launch step: the exchange is inside the backward launch)
         ts = []
         for _ in range(iters):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

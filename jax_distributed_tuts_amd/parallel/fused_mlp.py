@@ -42,7 +42,7 @@ class Mlp2Args(ctypes.Structure):
                 ("step_copy", c_void_p), ("W2snap", c_void_p), ("stage_stride", ctypes.c_long),
                 ("det_logits", c_void_p),
                 ("XR", c_void_p), ("zslab", c_void_p), ("ztick", c_void_p), ("hand", c_void_p), ("lg3", c_int),
-                ("opt_sgd", c_int), ("smap", c_void_p), ("wt", c_int)]
+                ("opt_sgd", c_int), ("smap", c_void_p), ("wt", c_int), ("tx", c_void_p)]
 
 
 class StageLeaf(ctypes.Structure):
@@ -127,8 +127,14 @@ class FusedMLP2:
     (grads then reduce-scattered), with ``mslot`` its local metric slots."""
 
     def __init__(self, state, mesh, axis: str, num_minibatches: int, rows: int, metrics: torch.Tensor,
-                 params=None, mslot: Optional[torch.Tensor] = None, fuse_opt: Optional[bool] = None):
+                 params=None, mslot: Optional[torch.Tensor] = None, fuse_opt: Optional[bool] = None,
+                 tx=None, ranks_on_gpu: int = 1):
+        """``tx`` (comm.tile_exchange.TileExchange, N > 1): every step is ONE run-ahead
+        launch whose tiles all-reduce their gradients with the other ranks' launches
+        before the fused optimizer (``ranks_on_gpu``: ranks sharing this GPU, for the
+        co-residency check)."""
         P = params if params is not None else state.params
+        self.tx = tx
         self.P = P
         self.mslot = mslot if mslot is not None else P.metrics_slot
         self.state, self.mesh, self.axis = state, mesh, axis
@@ -191,6 +197,11 @@ class FusedMLP2:
         self.ahead_ok = (self.fuse_opt and self.det_logits is None and self.W1T is not None
                          and os.environ.get("JDT_MLP2_AHEAD", "1") == "1"
                          and bool(_lib.lib().jdt_mlp2_ahead_ok(rows, H)))
+        if tx is not None:
+            from ..comm.tile_exchange import ahead_tx_ok
+
+            self.ahead_ok = (self.fuse_opt and self.det_logits is None and self.W1T is not None
+                             and ahead_tx_ok(rows, H, ranks_on_gpu))
         self._ahead_args = None
         # host-side: the last launch on this engine was a run-ahead backward (set by
         # run_ahead / DataParallelTrainer after replaying a run-ahead graph)
@@ -283,11 +294,17 @@ class FusedMLP2:
                 a.lr, a.beta1, a.beta2, a.eps, a.wd = tx.learning_rate, 0.0, 0.0, 0.0, tx.weight_decay
             else:
                 a.lr, a.beta1, a.beta2, a.eps, a.wd = tx.learning_rate, tx.b1, tx.b2, tx.eps, tx.weight_decay
-            a.gscale = 1.0 / self.n_mb
+            # N > 1 one-launch step: the kernel sums the ranks' gradients, 1/N in the scale
+            a.gscale = 1.0 / (self.n_mb * (self.world if self.tx is not None else 1))
             a.running = self.metrics.data_ptr()
         return a
 
     def forward_backward(self, batch):
+        if self.tx is not None:
+            # N > 1 with the tile exchange: a step is a run-ahead launch (the two-launch pair
+            # would apply AdamW to this rank's local gradients)
+            self.run_ahead(batch, 1, prologue=not self.ahead_primed)
+            return
         if not torch.cuda.is_current_stream_capturing():
             self.ahead_primed = False   # the run-ahead buffers no longer hold the next forward
         key = (batch.inputs.data_ptr(), batch.labels.data_ptr(), self.state.rng)
@@ -316,6 +333,8 @@ class FusedMLP2:
             b.logits = self.logits_all[2:].data_ptr()
             b.lg3 = 1
             b.XR, b.zslab, b.ztick, b.hand = (t.data_ptr() for t in (self.XR, self.zslab, self.ztick, self.hand))
+            if self.tx is not None:
+                b.tx = self.tx.args_ptr
             self._ahead_args = b
         L = _lib.lib()
         s = _lib.stream_ptr()
@@ -367,8 +386,9 @@ class FusedMLP2:
         if self.loop_error():
             raise RuntimeError("mlp2_loop_kernel: a grid barrier timed out (not every workgroup was resident)")
         if self.ahead_ok and int(self.ztick[1].item()) != 0:
-            raise RuntimeError("mlp2_bwd run-ahead: tile map or column barrier failed (error word "
-                               f"{int(self.ztick[1].item())}); results invalid")
+            raise RuntimeError("mlp2_bwd run-ahead: tile map, column barrier or tile exchange failed (error "
+                               f"word {int(self.ztick[1].item())}: 1 tile map, 2 column barrier, 4 exchange "
+                               "timeout); results invalid")
         P = self.state.params
         if self.fuse_opt and int(self.state.opt_state["count"].item()) % 2 == 1:
             P.s("output_dense/kernel").copy_(self.W2s1)
@@ -412,7 +432,8 @@ class AheadGraphs:
                                    "(not every workgroup resident); rerun with JDT_MD_DZS=0")
             if err:
                 raise RuntimeError(f"run-ahead step failed on its first replay (error word {err}: "
-                                   "1 = tile map, 2 = column barrier timeout); rerun with JDT_MLP2_AHEAD=0")
+                                   "1 = tile map, 2 = column barrier timeout, 4 = tile exchange timeout); "
+                                   "rerun with JDT_MLP2_AHEAD=0 (JDT_DP_AHEAD=0 at N > 1)")
 
 
 # ----------------------------------------------------------------------------- deep MLPs (csrc/mlp_deep.hip)
@@ -633,7 +654,8 @@ class FusedMLPDeep:
             a.sbh = P.s(self.bn[L - 1]).data_ptr()
             tx = st.tx
             a.lr, a.beta1, a.beta2, a.eps, a.wd = tx.learning_rate, tx.b1, tx.b2, tx.eps, tx.weight_decay
-            a.gscale = 1.0 / self.n_mb
+            # N > 1 one-launch step: the kernel sums the ranks' gradients, 1/N in the scale
+            a.gscale = 1.0 / (self.n_mb * (self.world if self.tx is not None else 1))
             a.running = self.metrics.data_ptr()
         return a
 
@@ -655,6 +677,8 @@ class FusedMLPDeep:
         if self._ahead_args is None:
             b = MdArgs.from_buffer_copy(bwd[-1])   # layer 0's backward
             b.XR, b.zslab, b.ztick, b.hand = (t.data_ptr() for t in (self.XR, self.zslab, self.ztick, self.hand))
+            if self.tx is not None:
+                b.tx = self.tx.args_ptr
             self._ahead_args = b
         Lb = _lib.lib()
         s = _lib.stream_ptr()
@@ -672,6 +696,11 @@ class FusedMLPDeep:
             self.ahead_primed = True
 
     def forward_backward(self, batch):
+        if self.tx is not None:
+            # N > 1 with the tile exchange: a step is a run-ahead launch (the two-launch pair
+            # would apply AdamW to this rank's local gradients)
+            self.run_ahead(batch, 1, prologue=not self.ahead_primed)
+            return
         if not torch.cuda.is_current_stream_capturing():
             self.ahead_primed = False
         self._ensure_args(batch)
@@ -711,13 +740,15 @@ class FusedMLPDeep:
 
 
 def make_engine(state, mesh, axis: str, num_minibatches: int, rows: int, metrics: torch.Tensor, device,
-                params=None, mslot: Optional[torch.Tensor] = None, fuse_opt: Optional[bool] = None):
+                params=None, mslot: Optional[torch.Tensor] = None, fuse_opt: Optional[bool] = None,
+                tx=None, ranks_on_gpu: int = 1):
     """The whole-step fused engine for ``state.apply_fn`` (2-layer or deep), or None
-    if the model/shape is outside the fused kernels' envelope."""
+    if the model/shape is outside the fused kernels' envelope.  ``tx``: the 2-layer
+    engine's one-launch N > 1 step (FusedMLP2)."""
     model = state.apply_fn
     if supported(model, rows, device):
         return FusedMLP2(state, mesh, axis, num_minibatches, rows, metrics, params=params, mslot=mslot,
-                         fuse_opt=fuse_opt)
+                         fuse_opt=fuse_opt, tx=tx, ranks_on_gpu=ranks_on_gpu)
     if supported_deep(model, rows, device):
         return FusedMLPDeep(state, mesh, axis, num_minibatches, rows, metrics, params=params, mslot=mslot,
                             fuse_opt=fuse_opt)

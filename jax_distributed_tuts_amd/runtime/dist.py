@@ -101,24 +101,31 @@ def collectives_capturable() -> bool:
     return backend() == "nccl"
 
 
-def ranks_share_gpu() -> bool:
-    """True when two ranks of the job drive the same physical GPU (same PCI domain / bus /
-    device) -- the rehearsal setup of several processes on one card, where concurrent
-    spinning streams time-share the GPU's queues (profiles/r4_pp_streams_ab.txt,
-    r4_overlap_sync_ab.txt) -- False on a node with one rank per GPU, with one rank, or
-    off the GPU.  Collective over the world group (every rank must call it); cached."""
-    if "gpu_shared" in _STATE:
-        return bool(_STATE["gpu_shared"])
+def ranks_per_gpu() -> int:
+    """The most ranks of the job that drive one physical GPU (same PCI domain / bus /
+    device): > 1 in the rehearsal setup of several processes on one card, where
+    concurrent spinning streams time-share the GPU's queues (profiles/r4_pp_streams_ab.txt,
+    r4_overlap_sync_ab.txt) and co-resident grids must share its CUs; 1 on a node with one
+    rank per GPU, with one rank, or off the GPU.  Collective over the world group (every
+    rank must call it); cached."""
+    if "gpu_share" in _STATE:
+        return int(_STATE["gpu_share"])
     dev = device()
-    shared = False
+    n = 1
     if is_initialized() and world_size() > 1 and dev.type == "cuda":
         p = torch.cuda.get_device_properties(dev)
         mine = (int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id))
         ids = [None] * world_size()
         dist.all_gather_object(ids, mine)
-        shared = len(set(map(tuple, ids))) < len(ids)
-    _STATE["gpu_shared"] = shared
-    return shared
+        ids = [tuple(x) for x in ids]
+        n = max(ids.count(x) for x in ids)
+    _STATE["gpu_share"] = n
+    return n
+
+
+def ranks_share_gpu() -> bool:
+    """Two ranks of the job drive the same GPU (ranks_per_gpu() > 1)."""
+    return ranks_per_gpu() > 1
 
 
 def barrier():

@@ -35,20 +35,27 @@ def test_xgmi_collectives(tmp_path, ws):
         assert o["prod_trainer_row"], o
 
 
-@pytest.mark.parametrize("ws", [2, 8])
-def test_dp_over_xgmi_matches_single_device(tmp_path, ws):
+@pytest.mark.parametrize("ws,dp_ahead", [(2, "1"), (2, "0"), (8, "1")])
+def test_dp_over_xgmi_matches_single_device(tmp_path, ws, dp_ahead):
+    """ws=2, dp_ahead=1: the one-launch step (run-ahead backward with the in-kernel
+    tile exchange: 2 x 224 workgroups fit the shared GPU); ws=2, dp_ahead=0 and ws=8
+    (8 grids do not fit one GPU): forward, backward and the xGMI all-reduce + AdamW."""
+    import functools
+
     from data_paral import synthetic_batch
     from jax_distributed_tuts_amd.models.mlp import Classifier
     from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
     from jax_distributed_tuts_amd.utils.config import dp_config
     from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
 
-    spawn(XW.dp_xgmi, ws, str(tmp_path), gpu=True)
+    spawn(functools.partial(XW.dp_xgmi, dp_ahead=dp_ahead), ws, str(tmp_path), gpu=True)
     res = _load(tmp_path, "dpx", ws)
     assert all(o["comm"] == "xgmi" for o in res)
     assert all(o["step"] == 8 for o in res)
+    assert all(o["one_launch"] == (ws == 2 and dp_ahead == "1") for o in res), [o["one_launch"] for o in res]
     for o in res[1:]:
         torch.testing.assert_close(res[0]["master"], o["master"], rtol=0, atol=0)  # replicated exactly
+        torch.testing.assert_close(res[0]["m"], o["m"], rtol=0, atol=0)
         torch.testing.assert_close(res[0]["metrics"], o["metrics"], rtol=0, atol=0)
     # single device, whole batch, same steps
     dev = torch.device("cuda", 0)

@@ -172,9 +172,12 @@ def collectives(outdir):
     comm.close()
 
 
-def dp_xgmi(outdir, steps_eager=2, steps_graph=6):
+def dp_xgmi(outdir, steps_eager=2, steps_graph=6, dp_ahead="1"):
     """DP over the xGMI fused all-reduce+AdamW kernel (dropout off), fused step
-    kernels, eager steps then multi-step graph replays."""
+    kernels, eager steps then multi-step graph replays.  ``dp_ahead`` = JDT_DP_AHEAD:
+    "1" lets the step be one run-ahead launch with the in-kernel tile exchange where
+    every rank's grid fits on the shared GPU, "0" keeps the three-launch step."""
+    os.environ["JDT_DP_AHEAD"] = dp_ahead
     from data_paral import synthetic_batch
     from jax_distributed_tuts_amd.models.mlp import Classifier
     from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp, shard_batch
@@ -197,7 +200,8 @@ def dp_xgmi(outdir, steps_eager=2, steps_graph=6):
     torch.cuda.synchronize()
     tr.finalize()
     _save(outdir, "dpx", {"master": st.params.master.cpu(), "metrics": tr.metrics.cpu(), "comm": tr.comm_backend,
-                          "fused": tr.fused is not None, "step": int(st.opt_state["count"].item())})
+                          "fused": tr.fused is not None, "step": int(st.opt_state["count"].item()),
+                          "one_launch": bool(tr.one_launch), "m": st.opt_state["m"].cpu()})
 
 
 def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2, eps=1e-8):

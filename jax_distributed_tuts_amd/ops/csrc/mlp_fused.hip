@@ -130,7 +130,8 @@ struct Mlp2Loop {
 
 // 16 slots per workgroup.  Slots 0-4: s_memrealtime at phase ends; slots 5/6:
 // s_memtime (core clock) at phases 0/4, so (slot6 - slot5) / (slot4 - slot0) * 100 MHz
-// is the shader clock; slots 8-11: run-ahead phases (mlp2_bwd AHEAD).
+// is the shader clock; slots 8-11: run-ahead phases (mlp2_bwd AHEAD); 12/13: the N > 1
+// tile exchange's start / end.
 #define STAMP(i)                                                                              \
   do {                                                                                        \
     if (a.stamps && threadIdx.x == 0) {                                                       \
@@ -892,7 +893,9 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         n4 = 2;
         if (lead && lane < C) { vs = ab2[0]; ps = (NTILE + 2) * 256 + lane; }
       }
+      STAMP(12);
       tx_tile(a.tx, bx * NCH + by, (unsigned)step + 1u, n4, v4, p4, vs, ps, a.ztick + 1);
+      STAMP(13);
       if (w < NTILE) {
         acc = (f32x4){v4[0].x, v4[0].y, v4[0].z, v4[0].w};
         if (lead && tid < 4) mval = vs;

@@ -176,8 +176,14 @@ class DataParallelTrainer:
                  and TX.ahead_tx_ok(batch.size, H, share))
         if not TX.agree(self.mesh.group(self.cfg.axis), local, batch.inputs.device):
             return None, 1
-        tx = TX.create_for(self.mesh, self.cfg.axis, batch.inputs.device, tiles=(H // 16) * (784 // 112))
-        return tx, share
+        # fresh buffers per engine: their flags hold epochs (optimizer step + 1), which a
+        # checkpoint restore (invalidate -> new engine) may move backwards
+        old = getattr(self, "_txx", None)
+        if old is not None:
+            torch.cuda.synchronize(batch.inputs.device)
+            old.close()
+        self._txx = TX.create_for(self.mesh, self.cfg.axis, batch.inputs.device, tiles=(H // 16) * (784 // 112))
+        return self._txx, share
 
     def _setup_stage(self):
         """N > 1 with the fused xGMI all-reduce + AdamW: the backward kernel writes the

@@ -654,8 +654,7 @@ class FusedMLPDeep:
             a.sbh = P.s(self.bn[L - 1]).data_ptr()
             tx = st.tx
             a.lr, a.beta1, a.beta2, a.eps, a.wd = tx.learning_rate, tx.b1, tx.b2, tx.eps, tx.weight_decay
-            # N > 1 one-launch step: the kernel sums the ranks' gradients, 1/N in the scale
-            a.gscale = 1.0 / (self.n_mb * (self.world if self.tx is not None else 1))
+            a.gscale = 1.0 / self.n_mb
             a.running = self.metrics.data_ptr()
         return a
 
@@ -677,8 +676,6 @@ class FusedMLPDeep:
         if self._ahead_args is None:
             b = MdArgs.from_buffer_copy(bwd[-1])   # layer 0's backward
             b.XR, b.zslab, b.ztick, b.hand = (t.data_ptr() for t in (self.XR, self.zslab, self.ztick, self.hand))
-            if self.tx is not None:
-                b.tx = self.tx.args_ptr
             self._ahead_args = b
         Lb = _lib.lib()
         s = _lib.stream_ptr()
@@ -696,11 +693,6 @@ class FusedMLPDeep:
             self.ahead_primed = True
 
     def forward_backward(self, batch):
-        if self.tx is not None:
-            # N > 1 with the tile exchange: a step is a run-ahead launch (the two-launch pair
-            # would apply AdamW to this rank's local gradients)
-            self.run_ahead(batch, 1, prologue=not self.ahead_primed)
-            return
         if not torch.cuda.is_current_stream_capturing():
             self.ahead_primed = False
         self._ensure_args(batch)

@@ -114,6 +114,14 @@ JDT_API void* jdt_tx_args(void* ctx) {
 
 JDT_API int jdt_tx_args_size() { return (int)sizeof(TxArgs); }
 
+// Zero this rank's flags (after the self-test, before any step kernel: the step kernels'
+// epochs start at 1).  Every rank resets its own page, then the ranks meet at a barrier.
+JDT_API int jdt_tx_reset(void* ctx) {
+  TxCtx* c = static_cast<TxCtx*>(ctx);
+  if (hipMemset(c->flag, 0, tx_flag_words(c) * sizeof(unsigned)) != hipSuccess) return -1;
+  return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
 JDT_API void jdt_tx_close(void* ctx) {
   TxCtx* c = static_cast<TxCtx*>(ctx);
   if (!c) return;

@@ -39,6 +39,9 @@ _lib.declare("jdt_tx_open", c_int, [c_void_p, c_void_p, c_longlong])
 _lib.declare("jdt_tx_args", c_void_p, [c_void_p])
 _lib.declare("jdt_tx_close", None, [c_void_p])
 _lib.declare("jdt_mlp2_ahead_tx_ok", c_int, [c_int, c_int, c_int])
+_lib.declare("jdt_tx_selftest", c_int, [c_void_p, c_int, ctypes.c_uint, c_void_p, c_void_p])
+_lib.declare("jdt_tx_reset", c_int, [c_void_p])
+SELFTEST_TILES = 64   # 64 workgroups per rank: 8 ranks' self-test grids fit one shared GPU
 
 
 class TileExchange:
@@ -52,6 +55,7 @@ class TileExchange:
         self.device = device
         self.ctx = c_void_p()
         self.ok = False
+        self.selftest = None
         L = _lib.lib()
         h = (ctypes.c_char * (3 * HANDLE_BYTES))()
         with torch.cuda.device(device):
@@ -69,9 +73,30 @@ class TileExchange:
                 log.warning("tile exchange: hipIpcOpenMemHandle failed on rank %d", rank)
         else:
             log.warning("tile exchange: buffer export failed on some rank (rank %d rc %d)", rank, rc)
+        good = self._agree(good)
+        if good:
+            # every rank exchanges known values through the real buffers and kernel code
+            # (all payload positions, W-rank sums bit-exact), then clears its flags -- the
+            # step kernels' epochs start at 1 -- before any rank may use them
+            good = self._self_test()
         self.ok = self._agree(good)
         if not self.ok:
             self.close()
+
+    def _self_test(self) -> bool:
+        L = _lib.lib()
+        words = torch.zeros(2, dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            rc = L.jdt_tx_selftest(self.args_ptr, min(self.tiles, SELFTEST_TILES), 1, words.data_ptr(),
+                                   c_void_p(_lib.stream_ptr(self.device)))
+            torch.cuda.synchronize(self.device)
+            bad, err = (int(x) for x in words.cpu())
+            rc2 = L.jdt_tx_reset(self.ctx)
+        self.selftest = {"rc": int(rc), "wrong": bad, "timeouts": err, "reset": int(rc2)}
+        if rc != 0 or bad or err or rc2 != 0:
+            log.warning("tile exchange self-test failed on rank %d: %s", self.rank, self.selftest)
+            return False
+        return True
 
     def _agree(self, ok: bool) -> bool:
         t = torch.tensor([1 if ok else 0], dtype=torch.int32,

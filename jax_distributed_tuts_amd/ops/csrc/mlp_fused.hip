@@ -602,6 +602,61 @@ __device__ __forceinline__ void tx_tile(const TxArgs* X, int T, unsigned epoch, 
     __hip_atomic_store(X->flag[tid] + tiles * TX_MAX_RANKS + T, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Start-up self-test of the tile exchange (comm/tile_exchange.py): workgroup T < tiles
+// exchanges, with the payload positions of mlp2_bwd AHEAD's waves (tile T % 7 == 0 with
+// the spare wave's dW2 / db1 slots, tile 0 with db2 and the metric slots), values that
+// are an exact function of (rank, tile, position), and counts every result that is not
+// bit-identical to the rank-ordered sum.  Small grid: the W ranks' grids fit one GPU.
+__device__ __forceinline__ float tx_probe_value(int rank, int T, int pos) {
+  unsigned h = (unsigned)rank * 0x9E3779B1u ^ (unsigned)T * 0x85EBCA77u ^ (unsigned)pos * 0xC2B2AE3Du;
+  h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12;
+  return (float)((int)(h & 0xFFFFu) - 32768) * (1.f / 4096.f);   // exact in fp32, exact sums
+}
+
+__global__ void __launch_bounds__(NT) tx_selftest_kernel(const TxArgs* X, unsigned epoch, unsigned* bad,
+                                                        unsigned* err) {
+  constexpr int NTILE = 7;
+  const int T = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const bool chunk0 = T % 7 == 0, lead = T == 0;
+  float4 v4[2];
+  int p4[2] = {0, 0}, n4 = 0, ps = -1;
+  float vs = 0.f;
+  if (w < NTILE) {
+    p4[0] = w * 256 + lane * 4;
+    n4 = 1;
+    if (lead && tid < 4) ps = (NTILE + 2) * 256 + 64 + tid;
+  } else if (chunk0) {
+    p4[0] = NTILE * 256 + lane * 4;
+    p4[1] = (NTILE + 1) * 256 + lane * 4;
+    n4 = 2;
+    if (lead && lane < 10) ps = (NTILE + 2) * 256 + lane;
+  }
+  const int R = X->rank, W = X->world;
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+    v4[k] = make_float4(tx_probe_value(R, T, p4[k]), tx_probe_value(R, T, p4[k] + 1),
+                        tx_probe_value(R, T, p4[k] + 2), tx_probe_value(R, T, p4[k] + 3));
+  if (ps >= 0) vs = tx_probe_value(R, T, ps);
+  tx_tile(X, T, epoch, n4, v4, p4, vs, ps, err);
+  unsigned nbad = 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    if (k >= n4) continue;
+    const float* got = &v4[k].x;
+    for (int e = 0; e < 4; ++e) {
+      float want = 0.f;
+      for (int q = 0; q < W; ++q) want = q == 0 ? tx_probe_value(q, T, p4[k] + e) : want + tx_probe_value(q, T, p4[k] + e);
+      nbad += __float_as_uint(got[e]) != __float_as_uint(want);
+    }
+  }
+  if (ps >= 0) {
+    float want = 0.f;
+    for (int q = 0; q < W; ++q) want = q == 0 ? tx_probe_value(q, T, ps) : want + tx_probe_value(q, T, ps);
+    nbad += __float_as_uint(vs) != __float_as_uint(want);
+  }
+  if (nbad) atomicAdd(bad, nbad);
+}
+
 // AHEAD (single GPU, fused AdamW, W1^T copy): after its AdamW epilogue every
 // workgroup (blk, chunk) also computes the partial Z1 = X[:, chunk] W1'[chunk, blk]
 // of the NEXT step from the W1' tile it just produced (phase 5); the last of a
@@ -1323,6 +1378,16 @@ JDT_API int jdt_mlp2_ahead_tx_ok(int M, int H, int nshare) {
           hipSuccess)
     return 0;
   return (long)nshare * (H / 16) * (784 / 112) <= (long)cus * per ? 1 : 0;
+}
+
+// The tile exchange's self-test (above): `tiles` workgroups, epoch `epoch`; words[0] gets
+// the number of wrong results, words[1] the timeout bits.  The caller resets the flags
+// afterwards (jdt_tx_reset) before the step kernels use epochs from 1.
+JDT_API int jdt_tx_selftest(const void* tx_args_dev, int tiles, unsigned epoch, unsigned* words, void* stream) {
+  if (!tx_args_dev || tiles <= 0) return -2;
+  hipLaunchKernelGGL(tx_selftest_kernel, dim3(tiles), dim3(NT), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const TxArgs*>(tx_args_dev), epoch, words, words + 1);
+  return HIP_LAUNCH_CHECK();
 }
 
 // phase 0: mlp2_fwd, 1: mlp2_bwd, 2: run-ahead mlp2_bwd (backward of t + forward of t+1)

@@ -35,6 +35,18 @@ def test_xgmi_collectives(tmp_path, ws):
         assert o["prod_trainer_row"], o
 
 
+@pytest.mark.parametrize("ws", [2, 4, 8])
+def test_tile_exchange_self_test(tmp_path, ws):
+    """The one-launch DP step's per-tile exchange at W = 2 / 4 / 8 ranks sharing the GPU:
+    the start-up self-test sums every payload position of 64 tiles over the W ranks
+    bit-exactly through the kernel's own exchange code (the 8-rank path, two groups of 4
+    peers, runs here although 8 training grids do not fit one GPU)."""
+    spawn(XW.tile_exchange, ws, str(tmp_path), gpu=True)
+    for r, o in enumerate(_load(tmp_path, "tx", ws)):
+        assert o["ok"] and o["args"], (r, o)
+        assert o["selftest"] == {"rc": 0, "wrong": 0, "timeouts": 0, "reset": 0}, (r, o)
+
+
 @pytest.mark.parametrize("ws,dp_ahead", [(2, "1"), (2, "0"), (8, "1")])
 def test_dp_over_xgmi_matches_single_device(tmp_path, ws, dp_ahead):
     """ws=2, dp_ahead=1: the one-launch step (run-ahead backward with the in-kernel

@@ -342,6 +342,21 @@ def lm_pp_xgmi(outdir, dp, steps=3, n_layers=2):
                                "buckets": len(getattr(tr, "_buckets", None) or [])})
 
 
+def tile_exchange(outdir):
+    """The one-launch DP step's tile exchange (comm/tile_exchange.py) at W ranks: buffers
+    exported / mapped, the start-up self-test (every payload position of 64 tiles summed
+    over the W ranks, bit-exact) passes, flags cleared."""
+    from jax_distributed_tuts_amd.comm.tile_exchange import TileExchange
+    from jax_distributed_tuts_amd.runtime import dist as D
+
+    r, W, dev = D.rank(), D.world_size(), D.device()
+    mesh = D.Mesh({"data": W})
+    tx = TileExchange(mesh.group("data"), r, W, 224, dev, timeout_s=20.0)
+    res = {"ok": tx.ok, "selftest": tx.selftest, "args": tx.args_ptr != 0}
+    tx.close()
+    _save(outdir, "tx", res)
+
+
 def fault_timeout(outdir):
     """Fault injection: rank 1 never joins the collective / never sends.  Rank 0's
     in-kernel waits must time out into the error flag (no hung GPU), for both

@@ -317,9 +317,9 @@ def main():
         eng = getattr(tr, "fused", None)
         nh = getattr(eng, "nh", None)   # deep engine: hidden layers
         if getattr(tr, "_ahead", None):
-            desc["step_launches"] = (f"{2 * nh - 1} (layer-0 run-ahead md_bwd)" if nh
-                                     else "1 (run-ahead mlp2_bwd" + (", gradient tiles all-reduced in the launch)"
-                                                                     if getattr(tr, "one_launch", False) else ")"))
+            tx_ = ", gradient tiles all-reduced in the launches" if getattr(tr, "one_launch", False) else ""
+            desc["step_launches"] = (f"{2 * nh - 1} (layer-0 run-ahead md_bwd{tx_})" if nh
+                                     else f"1 (run-ahead mlp2_bwd{tx_})")
         elif eng is not None:
             desc["step_launches"] = ((f"{2 * nh} (md_fwd / md_bwd per layer)" if nh else "2 (mlp2_fwd + mlp2_bwd)")
                                      + (" + xGMI all-reduce/AdamW" if ws > 1 else ""))

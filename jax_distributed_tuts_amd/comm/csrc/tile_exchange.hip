@@ -20,6 +20,7 @@ struct TxCtx {
   float* part = nullptr;
   float* red = nullptr;
   unsigned* flag = nullptr;
+  unsigned* err = nullptr;   // local error word (TxArgs::err)
   TxArgs host{};
   TxArgs* dev = nullptr;   // device copy of `host`
   bool opened = false;
@@ -56,6 +57,8 @@ JDT_API int jdt_tx_create(int rank, int world, int tiles, int pay, void** ctx_ou
   if (hipMemset(c->red, 0, tx_red_floats(c) * sizeof(float)) != hipSuccess) goto fail;
   if (hipMemset(c->flag, 0, tx_flag_words(c) * sizeof(unsigned)) != hipSuccess) goto fail;
   if (hipMalloc(reinterpret_cast<void**>(&c->dev), sizeof(TxArgs)) != hipSuccess) goto fail;
+  if (hipMalloc(reinterpret_cast<void**>(&c->err), sizeof(unsigned)) != hipSuccess) goto fail;
+  if (hipMemset(c->err, 0, sizeof(unsigned)) != hipSuccess) goto fail;
   if (hipDeviceSynchronize() != hipSuccess) goto fail;
   if (hipIpcGetMemHandle(&h[0], c->part) != hipSuccess) goto fail;
   if (hipIpcGetMemHandle(&h[1], c->red) != hipSuccess) goto fail;
@@ -70,6 +73,7 @@ fail:
   if (c->red) (void)hipFree(c->red);
   if (c->flag) (void)hipFree(c->flag);
   if (c->dev) (void)hipFree(c->dev);
+  if (c->err) (void)hipFree(c->err);
   delete c;
   return -1;
 }
@@ -101,6 +105,7 @@ JDT_API int jdt_tx_open(void* ctx, const void* all_handles, long long timeout_ti
   A.tiles = c->tiles;
   A.pay = c->pay;
   A.timeout = timeout_ticks;
+  A.err = c->err;
   if (hipMemcpy(c->dev, &A, sizeof(A), hipMemcpyHostToDevice) != hipSuccess) return -1;
   c->opened = true;
   return 0;
@@ -136,5 +141,14 @@ JDT_API void jdt_tx_close(void* ctx) {
   if (c->red) (void)hipFree(c->red);
   if (c->flag) (void)hipFree(c->flag);
   if (c->dev) (void)hipFree(c->dev);
+  if (c->err) (void)hipFree(c->err);
   delete c;
+}
+
+// The error word (bit 2: an exchange wait timed out), read synchronously.
+JDT_API unsigned jdt_tx_error(void* ctx) {
+  TxCtx* c = static_cast<TxCtx*>(ctx);
+  unsigned v = 0;
+  if (!c || !c->err || hipMemcpy(&v, c->err, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return 0xffffffffu;
+  return v;
 }

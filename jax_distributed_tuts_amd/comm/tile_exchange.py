@@ -41,6 +41,8 @@ _lib.declare("jdt_tx_close", None, [c_void_p])
 _lib.declare("jdt_mlp2_ahead_tx_ok", c_int, [c_int, c_int, c_int])
 _lib.declare("jdt_tx_selftest", c_int, [c_void_p, c_int, ctypes.c_uint, c_void_p, c_void_p])
 _lib.declare("jdt_tx_reset", c_int, [c_void_p])
+_lib.declare("jdt_tx_error", ctypes.c_uint, [c_void_p])
+_lib.declare("jdt_md_tx_ok", c_int, [c_int, c_int])
 SELFTEST_TILES = 64   # 64 workgroups per rank: 8 ranks' self-test grids fit one shared GPU
 
 
@@ -109,6 +111,10 @@ class TileExchange:
         """Device pointer of the kernel's TxArgs (Mlp2Args::tx)."""
         return int(_lib.lib().jdt_tx_args(self.ctx) or 0) if self.ctx else 0
 
+    def error(self) -> int:
+        """This rank's error word (4: an exchange wait timed out; synchronous read)."""
+        return int(_lib.lib().jdt_tx_error(self.ctx)) if self.ctx else 0
+
     def agree(self, ok: bool) -> bool:
         """All ranks' AND of ``ok`` (collective)."""
         return self._agree(ok)
@@ -132,6 +138,12 @@ def ahead_tx_ok(rows: int, hidden: int, ranks_on_this_gpu: int) -> bool:
     """Whether the one-launch N > 1 step can run here: the run-ahead conditions plus
     every sharing rank's grid resident at once (``ranks_on_this_gpu`` grids per GPU)."""
     return bool(_lib.lib().jdt_mlp2_ahead_tx_ok(int(rows), int(hidden), int(ranks_on_this_gpu)))
+
+
+def deep_tx_ok(rows: int, ranks_on_this_gpu: int) -> bool:
+    """The deep (>= 2 hidden layers) engine's exchanging backward launches all resident
+    with ``ranks_on_this_gpu`` ranks' grids per GPU (csrc/mlp_deep.hip jdt_md_tx_ok)."""
+    return bool(_lib.lib().jdt_md_tx_ok(int(rows), int(ranks_on_this_gpu)))
 
 
 def create_for(mesh, axis: str, device: torch.device, tiles: int) -> Optional[TileExchange]:

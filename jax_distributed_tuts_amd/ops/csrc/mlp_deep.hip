@@ -125,6 +125,12 @@ struct MdArgs {
   // kernel boundary to write back (mlp_fused.hip Mlp2Args::wt); bit 1: the row-major
   // bf16 shadow of the next step too
   int wt;
+  // N > 1 one-launch-per-layer step: this backward's tiles all-reduce their gradients with
+  // the same tiles of the other ranks' launches before the fused AdamW (common.h
+  // TxArgs; tile T of this launch is exchange tile tx_base + T; null = one GPU)
+  const TxArgs* tx;
+  int tx_base;
+  int tx_shared;   // ranks share this GPU: the two-workgroups-per-CU variants (jdt_md_tx_ok)
 };
 
 // Slots 0-4: s_memrealtime at the kernel's phase ends (tools/stamp_deep.py).
@@ -373,8 +379,13 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
 // BND (pipeline stage boundary, !TOP): dZ_i = dH * G_i -- the gradient w.r.t. this
 // layer's output arrives from the next pipeline stage instead of being recomputed
 // from dZ_{i+1} W_{i+1}^T.
-template <int K_IN, bool TOP, int C, int KC, int NN, bool XCD, bool BND = false, bool AHEAD = false>
-__global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
+// TX: N > 1, in-kernel tile exchange.  WPE = 4 (two workgroups per CU, <= 128 VGPRs,
+// a few spills) is the variant for ranks SHARING one GPU -- both ranks' launches must be
+// resident at once for the exchange's waits (jdt_md_tx_ok); with a GPU per rank one
+// workgroup per CU suffices and WPE = 1 keeps the unconstrained allocation.
+template <int K_IN, bool TOP, int C, int KC, int NN, bool XCD, bool BND = false, bool AHEAD = false, bool TX = false,
+          int WPE = 1>
+__global__ void __launch_bounds__(MD_NT) __attribute__((amdgpu_waves_per_eu(WPE))) md_bwd_kernel(MdArgs a) {
   constexpr int NT = MD_NT, NW = MD_NW, MPM = MD_MPM;
   constexpr int LDM = MPM + 8;
   constexpr int NTILE = KC / 16;           // dW output tiles (one per wave)
@@ -692,8 +703,9 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
 
   MD_STAMP(2);
   // ---- 3. dW_i[chunk, blk] = IN[:, chunk]^T dZ_i[:, blk]; spare wave: db_i (+ head grads)
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 aw = {0.f, 0.f, 0.f, 0.f}, ab = {0.f, 0.f, 0.f, 0.f}, ab2 = {0.f, 0.f, 0.f, 0.f};
   if (w < NTILE) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < MPM / 32; ++ks) {
       if (ks < Mp / 32) {
@@ -702,6 +714,62 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
         acc = mfma16x16x32(xf[ks], bfr, acc);
       }
     }
+  } else if (aux) {
+    bf16x8 ones;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ones[q] = (short)0x3f80;  // bf16 1.0
+    for (int ks = 0; ks < Mp / 32; ++ks) {
+      const int kk = ks * 32 + 8 * (lane >> 4);
+      const bf16x8 zT = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
+      ab = mfma16x16x32(zT, ones, ab);
+      if constexpr (TOP) {
+        const bf16x8 h = *reinterpret_cast<const bf16x8*>(&hT[(lane & 15) * LDM + kk]);
+        const bf16x8 d = *reinterpret_cast<const bf16x8*>(&dlT[(lane & 15) * LDM + kk]);
+        aw = mfma16x16x32(h, d, aw);
+        if (lead) ab2 = mfma16x16x32(ones, d, ab2);
+      }
+    }
+  }
+  // N > 1 (MdArgs::tx): this tile's gradients -- and (TOP lead) the head's db and the
+  // metric slots -- all-reduced with the same tile of the other ranks' launches before
+  // the optimizer (common.h tx_tile; payload as mlp_fused.hip's)
+  float mval = 0.f;
+  if constexpr (TX) {
+    if (TOP && lead && tid < 4) {
+      float L = 0.f, Cr = 0.f;
+      for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
+      mval = tid == 0 ? L : tid == 2 ? Cr : (float)M;   // {loss sum, n, correct, n}
+    }
+    float4 v4[2];
+    int p4[2] = {0, 0}, n4 = 0, ps = -1;
+    float vs = 0.f;
+    if (w < NTILE) {
+      v4[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      p4[0] = w * 256 + lane * 4;
+      n4 = 1;
+      if (TOP && lead && tid < 4) { vs = mval; ps = 9 * 256 + 64 + tid; }
+    } else if (aux) {
+      v4[0] = make_float4(ab[0], ab[1], ab[2], ab[3]);
+      v4[1] = make_float4(aw[0], aw[1], aw[2], aw[3]);
+      p4[0] = 7 * 256 + lane * 4;
+      p4[1] = 8 * 256 + lane * 4;
+      n4 = TOP ? 2 : 1;
+      if (TOP && lead && lane < C) { vs = ab2[0]; ps = 9 * 256 + lane; }
+    }
+    MD_STAMP(5);
+    tx_tile(a.tx, a.tx_base + bx * NCH + by, (unsigned)step + 1u, n4, v4, p4, vs, ps,
+            a.tx->err);
+    MD_STAMP(6);
+    if (w < NTILE) {
+      acc = (f32x4){v4[0].x, v4[0].y, v4[0].z, v4[0].w};
+      if (TOP && lead && tid < 4) mval = vs;
+    } else if (aux) {
+      ab = (f32x4){v4[0].x, v4[0].y, v4[0].z, v4[0].w};
+      if (TOP) aw = (f32x4){v4[1].x, v4[1].y, v4[1].z, v4[1].w};
+      if (TOP && lead && lane < C) ab2[0] = vs;
+    }
+  }
+  if (w < NTILE) {
     bf16_t* Wsn = const_cast<bf16_t*>(par ? a.Ws0 : a.Ws1);   // next step's parity of the row-major shadow
     const __amdgpu_buffer_rsrc_t wsn_r = __builtin_amdgcn_make_buffer_rsrc(Wsn, (short)0, 0x7fffffff, 0x00020000);
     unsigned wtp[2] = {0u, 0u};
@@ -739,21 +807,6 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
     if constexpr (AHEAD)
       *reinterpret_cast<uint2*>(&w1n[(lane & 15) * LDW1 + (trow0 - kc0)]) = make_uint2(wtp[0], wtp[1]);
   } else if (aux) {
-    bf16x8 ones;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) ones[q] = (short)0x3f80;  // bf16 1.0
-    f32x4 aw = {0.f, 0.f, 0.f, 0.f}, ab = {0.f, 0.f, 0.f, 0.f}, ab2 = {0.f, 0.f, 0.f, 0.f};
-    for (int ks = 0; ks < Mp / 32; ++ks) {
-      const int kk = ks * 32 + 8 * (lane >> 4);
-      const bf16x8 zT = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
-      ab = mfma16x16x32(zT, ones, ab);
-      if constexpr (TOP) {
-        const bf16x8 h = *reinterpret_cast<const bf16x8*>(&hT[(lane & 15) * LDM + kk]);
-        const bf16x8 d = *reinterpret_cast<const bf16x8*>(&dlT[(lane & 15) * LDM + kk]);
-        aw = mfma16x16x32(h, d, aw);
-        if (lead) ab2 = mfma16x16x32(ones, d, ab2);
-      }
-    }
     bf16_t* Whn = const_cast<bf16_t*>(par ? a.Wh0 : a.Wh1);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -786,7 +839,9 @@ __global__ void __launch_bounds__(MD_NT) md_bwd_kernel(MdArgs a) {
   MD_STAMP(3);
   if (TOP && lead) {
     __syncthreads();
-    if (tid == 0) {
+    if (TX) {   // the all-reduced slots, one per thread
+      if (tid < 4 && a.fuse_opt && a.running) a.running[tid] += mval;
+    } else if (tid == 0) {
       float L = 0.f, Cr = 0.f;
       for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
       if (a.fuse_opt && a.running) {
@@ -943,6 +998,32 @@ JDT_API int jdt_md_dzs_ok(int M) {
 // (head = 1: TOP layer, CE through the head; head = 2: pipeline-stage boundary,
 // dZ from the next stage's dH).  Instantiated for the tutorial
 // shapes: K in {784 (fp32 data), 512}, N = NN = 512, C = 10, M <= 128.
+// 1 if the deep engine's N > 1 step with the in-kernel tile exchange can run here with
+// `nshare` ranks' grids on this GPU: every exchanging backward launch of every sharing
+// rank resident at once (as jdt_mlp2_ahead_tx_ok).
+JDT_API int jdt_md_tx_ok(int M, int nshare) {
+  if (M <= 0 || M > MD_MPM || nshare < 1) return 0;
+  int dev = 0, cus = 0, p0 = 0, p1 = 0, p2 = 0;
+  const bool sh = nshare > 1;   // the launcher's variant choice (MdArgs::tx_shared)
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &p0,
+          sh ? (const void*)md_bwd_kernel<784, false, 10, 112, 512, true, false, true, true, 4>
+             : (const void*)md_bwd_kernel<784, false, 10, 112, 512, true, false, true, true>,
+          MD_NT, 0) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&p1, md_bwd_kernel<512, true, 10, 64, 512, true, false, false, true>,
+                                                   MD_NT, 0) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &p2,
+          sh ? (const void*)md_bwd_kernel<512, false, 10, 64, 512, true, false, false, true, 4>
+             : (const void*)md_bwd_kernel<512, false, 10, 64, 512, true, false, false, true>,
+          MD_NT, 0) != hipSuccess)
+    return 0;
+  const long cap = (long)cus * (p0 < p1 ? (p0 < p2 ? p0 : p2) : (p1 < p2 ? p1 : p2));
+  return (long)nshare * (512 / 16) * (512 / 64) <= cap ? 1 : 0;
+}
+
 JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) {
   const MdArgs& a = *args;
   if (a.N != 512 || a.M <= 0 || a.M > MD_MPM || (a.K != 784 && a.K != 512) || (head == 1 && a.C != 10)) return -3;
@@ -956,8 +1037,25 @@ JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) 
     if (a.K != 784 || head || !a.fuse_opt || !a.WTout || !a.XR || !a.zslab || !a.ztick || !a.hand ||
         !a.advance_step || a.det_logits)
       return -3;
-    hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, true, false, true>), dim3(a.N / 16, 784 / 112), blk, 0,
-                       st, a);
+    if (a.tx && a.tx_shared)
+      hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, true, false, true, true, 4>),
+                         dim3(a.N / 16, 784 / 112), blk, 0, st, a);
+    else if (a.tx)
+      hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, true, false, true, true>), dim3(a.N / 16, 784 / 112),
+                         blk, 0, st, a);
+    else
+      hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, true, false, true>), dim3(a.N / 16, 784 / 112), blk,
+                         0, st, a);
+    return HIP_LAUNCH_CHECK();
+  }
+  if (a.tx && phase == 1) {
+    // N > 1 hidden layers >= 1 with the in-kernel tile exchange (layer 0 runs ahead)
+    if (a.K != 512 || head == 2 || a.dzs || !a.fuse_opt) return -3;
+    const dim3 g(a.N / 16, 512 / 64);
+    if (head) hipLaunchKernelGGL((md_bwd_kernel<512, true, 10, 64, 512, true, false, false, true>), g, blk, 0, st, a);
+    else if (a.tx_shared)
+      hipLaunchKernelGGL((md_bwd_kernel<512, false, 10, 64, 512, true, false, false, true, 4>), g, blk, 0, st, a);
+    else hipLaunchKernelGGL((md_bwd_kernel<512, false, 10, 64, 512, true, false, false, true>), g, blk, 0, st, a);
     return HIP_LAUNCH_CHECK();
   }
   if (phase == 0) {

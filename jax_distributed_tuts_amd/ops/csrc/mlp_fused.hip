@@ -506,102 +506,6 @@ __device__ __forceinline__ void mlp2_fwd_body(AT& a, const int bx, const int by,
 }
 
 // ---------------------------------------------------------------------------- backward
-// ---------------------------------------------------------------------------- N > 1 tile exchange
-// Two-shot all-reduce of one workgroup's gradient values with the same tile T of the
-// other ranks' launches (common.h TxArgs): tile T belongs to rank T % W.  A non-owner
-// pushes its values into the owner's partial inbox (system-scope write-through stores,
-// drained, then ONE lane raises the owner's flag [T][rank]) and waits for the reduced
-// tile; the owner waits for the W - 1 flags, sums in rank order (own values at its rank
-// -- so every rank gets bit-identical sums, as comm/csrc/xgmi.hip), pushes the sum into
-// every peer's reduced inbox and raises their flags [T].  Each thread moves only its own
-// values: n4 float4 at payload offsets p4[] and one scalar at ps (ps < 0: none).  Every
-// wait is bounded (s_memrealtime); a timeout sets bit 2 of the error word and the tile
-// goes on with what it has (the host raises on the word).
-__device__ __forceinline__ bool tx_wait(const unsigned* f, unsigned epoch, long long timeout, unsigned* err) {
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-    if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout) {
-      atomicOr(err, 4u);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return true;
-}
-
-__device__ __forceinline__ void tx_tile(const TxArgs* X, int T, unsigned epoch, int n4, float4 (&v4)[2],
-                                        const int (&p4)[2], float& vs, int ps, unsigned* err) {
-  const int R = X->rank, W = X->world, own = T % W, tid = threadIdx.x;
-  const long pay = X->pay, tiles = X->tiles;
-  const unsigned long long tb = (unsigned long long)pay * 4ull;
-  if (R != own) {
-    const __amdgpu_buffer_rsrc_t dst = sys_rsrc(X->part[own] + ((long)T * TX_MAX_RANKS + R) * pay, tb);
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-      if (k < n4) sys_store4(dst, p4[k], v4[k]);
-    if (ps >= 0) sys_store1(dst, ps, vs);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its pushes
-    __syncthreads();
-    if (tid == 0) {
-      __hip_atomic_store(X->flag[own] + (long)T * TX_MAX_RANKS + R, epoch, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-      tx_wait(X->flag[R] + tiles * TX_MAX_RANKS + T, epoch, X->timeout, err);
-    }
-    __syncthreads();
-    const __amdgpu_buffer_rsrc_t src = sys_rsrc(X->red[R] + (long)T * pay, tb);
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-      if (k < n4) v4[k] = sys_load4(src, p4[k]);
-    if (ps >= 0) vs = sys_load1(src, ps);
-    return;
-  }
-  if (tid < W && tid != R) tx_wait(X->flag[R] + (long)T * TX_MAX_RANKS + tid, epoch, X->timeout, err);
-  __syncthreads();
-  const float* inbox = X->part[R] + (long)T * TX_MAX_RANKS * pay;
-  // the rank-ordered sum, peers' partials loaded 4 ranks at a time (all 4 in flight)
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {   // k = 0, 1: the float4 slots; k = 2: the scalar
-    if (k < 2 ? k >= n4 : ps < 0) continue;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int g = 0; g < TX_MAX_RANKS; g += 4) {
-      if (g >= W) break;
-      float4 in[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int q = g + u;
-        if (q < W && q != R) {
-          const __amdgpu_buffer_rsrc_t src = sys_rsrc(inbox + (long)q * pay, tb);
-          in[u] = k < 2 ? sys_load4(src, p4[k]) : make_float4(sys_load1(src, ps), 0.f, 0.f, 0.f);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int q = g + u;
-        if (q >= W) break;
-        const float4 x = q == R ? (k < 2 ? v4[k] : make_float4(vs, 0.f, 0.f, 0.f)) : in[u];
-        if (q == 0) acc = x;
-        else { acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w; }
-      }
-    }
-    if (k < 2) v4[k] = acc;
-    else vs = acc.x;
-  }
-#pragma unroll
-  for (int q = 0; q < TX_MAX_RANKS; ++q) {
-    if (q >= W || q == R) continue;
-    const __amdgpu_buffer_rsrc_t dst = sys_rsrc(X->red[q] + (long)T * pay, tb);
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-      if (k < n4) sys_store4(dst, p4[k], v4[k]);
-    if (ps >= 0) sys_store1(dst, ps, vs);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid < W && tid != R)
-    __hip_atomic_store(X->flag[tid] + tiles * TX_MAX_RANKS + T, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // Start-up self-test of the tile exchange (comm/tile_exchange.py): workgroup T < tiles
 // exchanges, with the payload positions of mlp2_bwd AHEAD's waves (tile T % 7 == 0 with
 // the spare wave's dW2 / db1 slots, tile 0 with db2 and the metric slots), values that

@@ -158,23 +158,35 @@ class DataParallelTrainer:
         return self.fused
 
     def _tile_exchange(self, batch: Batch):
-        """(TileExchange, ranks sharing this GPU) for the one-launch N > 1 step, or
-        (None, 1): the 2-layer fused engine with a fused optimizer (AdamW / plain SGD),
-        not deterministic, every rank's run-ahead grid co-resident with the grids of the
-        ranks sharing its GPU -- agreed by all ranks (collective: every rank builds its
-        engine on the same step).  JDT_DP_AHEAD=0: the three-launch step (A/B)."""
+        """(TileExchange, ranks sharing this GPU) for the N > 1 step without a separate
+        collective launch, or (None, 1).  2-layer engine (AdamW / plain SGD): ONE launch per
+        step; deep engine (AdamW): one backward launch per hidden layer, each exchanging
+        its tiles, layer 0 running ahead.  Not deterministic, every exchanging grid
+        co-resident with the grids of the ranks sharing its GPU -- agreed by all ranks
+        (collective: every rank builds its engine on the same step).  JDT_DP_AHEAD=0: the
+        forward / backward / xGMI all-reduce step (A/B)."""
         if not (self.world > 1 and batch.inputs.is_cuda and os.environ.get("JDT_DP_AHEAD", "1") == "1"):
             return None, 1
         from ..comm import tile_exchange as TX
         from ..runtime.dist import ranks_per_gpu
         from .fused_mlp import _is_adamw, _is_plain_sgd, deterministic, supported
 
+        from .fused_mlp import FusedMLPDeep, supported_deep
+
         share = ranks_per_gpu()
-        H = self.model.dims[1] if len(getattr(self.model, "dims", ())) == 3 else 0
-        local = (supported(self.model, batch.size, batch.inputs.device) and H > 0 and not deterministic()
-                 and (_is_adamw(self.state.tx) or _is_plain_sgd(self.state.tx))
-                 and TX.ahead_tx_ok(batch.size, H, share))
-        if not TX.agree(self.mesh.group(self.cfg.axis), local, batch.inputs.device):
+        dev = batch.inputs.device
+        if supported(self.model, batch.size, dev):          # 2-layer: one launch per step
+            H = self.model.dims[1]
+            local = (not deterministic() and (_is_adamw(self.state.tx) or _is_plain_sgd(self.state.tx))
+                     and TX.ahead_tx_ok(batch.size, H, share))
+            tiles = (H // 16) * (784 // 112)
+        elif supported_deep(self.model, batch.size, dev):   # deep: one launch per hidden layer
+            local = (not deterministic() and _is_adamw(self.state.tx) and os.environ.get("JDT_MLP2_AHEAD", "1") == "1"
+                     and bool(_lib_md_ahead_ok(batch.size)) and TX.deep_tx_ok(batch.size, share))
+            tiles = FusedMLPDeep.tx_tiles(self.model.L - 1)
+        else:
+            local, tiles = False, 0
+        if not TX.agree(self.mesh.group(self.cfg.axis), local, dev):
             return None, 1
         # fresh buffers per engine: their flags hold epochs (optimizer step + 1), which a
         # checkpoint restore (invalidate -> new engine) may move backwards
@@ -182,7 +194,7 @@ class DataParallelTrainer:
         if old is not None:
             torch.cuda.synchronize(batch.inputs.device)
             old.close()
-        self._txx = TX.create_for(self.mesh, self.cfg.axis, batch.inputs.device, tiles=(H // 16) * (784 // 112))
+        self._txx = TX.create_for(self.mesh, self.cfg.axis, dev, tiles=tiles)
         return self._txx, share
 
     def _setup_stage(self):
@@ -544,6 +556,12 @@ class DataParallelTrainer:
             self.sync()
             self.graph[2].replay()
         self.state.step += 1
+
+
+def _lib_md_ahead_ok(rows: int) -> int:
+    from ..ops import _lib
+
+    return _lib.lib().jdt_md_ahead_ok(int(rows))
 
 
 def capture_graph(body, pool=None) -> Optional[torch.cuda.CUDAGraph]:

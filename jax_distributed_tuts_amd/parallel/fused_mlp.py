@@ -426,6 +426,9 @@ class AheadGraphs:
             # instead of at finalize() after a whole run on wrong weights
             self._checked = True
             err = int(self.eng.ztick[1].item())
+            tx = getattr(self.eng, "tx", None)
+            if tx is not None and tx.error():
+                err |= 4
             dz = self.eng.dzs_error() if hasattr(self.eng, "dzs_error") else 0
             if dz:
                 raise RuntimeError("md_bwd dZ split: a column-block barrier timed out on the first replay "
@@ -459,7 +462,8 @@ class MdArgs(ctypes.Structure):
                 ("accumulate", c_int), ("dH", c_void_p), ("mb_rows", c_int), ("mb_stride", c_ulonglong),
                 ("stage_stride", ctypes.c_long), ("det_logits", c_void_p), ("step_mul", c_int),
                 ("XR", c_void_p), ("zslab", c_void_p), ("ztick", c_void_p), ("hand", c_void_p),
-                ("dzx", c_void_p), ("dzc", c_void_p), ("dzs", c_int), ("smap", c_void_p), ("wt", c_int)]
+                ("dzx", c_void_p), ("dzc", c_void_p), ("dzs", c_int), ("smap", c_void_p), ("wt", c_int),
+                ("tx", c_void_p), ("tx_base", c_int), ("tx_shared", c_int)]
 
 
 _lib.declare("jdt_md_layer", c_int, [ctypes.POINTER(MdArgs), c_int, c_int, c_void_p])
@@ -485,9 +489,15 @@ class FusedMLPDeep:
 
     def __init__(self, state, mesh, axis: str, num_minibatches: int, rows: int, metrics: torch.Tensor,
                  params=None, mslot: Optional[torch.Tensor] = None, fuse_opt: Optional[bool] = None,
-                 mb_rows: int = 0, mb_stride: int = 1 << 16):
+                 mb_rows: int = 0, mb_stride: int = 1 << 16, tx=None, ranks_on_gpu: int = 1):
+        """``tx`` (comm.tile_exchange.TileExchange, N > 1): every hidden layer's backward
+        all-reduces its gradient tiles with the other ranks' launches before the fused
+        AdamW (layer i's tiles at exchange offset ``tx_base(i)``), layer 0 running ahead --
+        no separate collective launch (FusedMLP2 ``tx``)."""
         P = params if params is not None else state.params
         self.P = P
+        self.tx = tx
+        self.tx_shared = int(ranks_on_gpu > 1)
         self.mslot = mslot if mslot is not None else P.metrics_slot
         self.state, self.mesh, self.axis = state, mesh, axis
         self.world = C.axis_size(mesh, axis)
@@ -541,7 +551,7 @@ class FusedMLPDeep:
         # (JDT_MLP2_AHEAD_MB=1): its kernel path passes the H_0 / G_0 check against md_fwd,
         # but a 330-step 8-layer run ended at a different loss than the plain schedule
         # (0.066 vs 0.089, BENCH_NOTES) and that was not explained this round.
-        self.ahead_ok = (self.fuse_opt and self.world == 1 and self.det_logits is None
+        self.ahead_ok = (self.fuse_opt and (self.world == 1 or tx is not None) and self.det_logits is None
                          and (self.mb_rows == 0 or os.environ.get("JDT_MLP2_AHEAD_MB", "0") == "1")
                          and m.dims[0] == 784 and os.environ.get("JDT_MLP2_AHEAD", "1") == "1"
                          and bool(_lib.lib().jdt_md_ahead_ok(rows)))
@@ -628,6 +638,8 @@ class FusedMLPDeep:
             a.dZout = self.dZ[i].data_ptr()
         a.fuse_opt = int(self.fuse_opt)
         a.wt = int(os.environ.get("JDT_MD_WT", "1"))   # write-through AdamW state (+3 %, r4_write_through_ab.txt)
+        if self.tx is not None and phase == 1:
+            a.tx, a.tx_base, a.tx_shared = self.tx.args_ptr, self.tx_base(i), self.tx_shared
         a.gW, a.gb = P.g(self.kn[i]).data_ptr(), P.g(self.bn[i]).data_ptr()
         a.gWh, a.gbh = P.g(self.kn[L - 1]).data_ptr(), P.g(self.bn[L - 1]).data_ptr()
         a.mslot = self.mslot.data_ptr()
@@ -654,7 +666,8 @@ class FusedMLPDeep:
             a.sbh = P.s(self.bn[L - 1]).data_ptr()
             tx = st.tx
             a.lr, a.beta1, a.beta2, a.eps, a.wd = tx.learning_rate, tx.b1, tx.b2, tx.eps, tx.weight_decay
-            a.gscale = 1.0 / self.n_mb
+            # N > 1 with the tile exchange: the kernels sum the ranks' gradients, 1/N here
+            a.gscale = 1.0 / (self.n_mb * (self.world if self.tx is not None else 1))
             a.running = self.metrics.data_ptr()
         return a
 
@@ -692,7 +705,20 @@ class FusedMLPDeep:
         if not torch.cuda.is_current_stream_capturing():
             self.ahead_primed = True
 
+    @staticmethod
+    def tx_tiles(nh: int) -> int:
+        """Exchange tiles of one step: layer 0's backward 32 x 7, every other 32 x 8."""
+        return 224 + 256 * (nh - 1)
+
+    def tx_base(self, i: int) -> int:
+        return 0 if i == 0 else 224 + 256 * (i - 1)
+
     def forward_backward(self, batch):
+        if self.tx is not None:
+            # N > 1 with the tile exchange: a step is the run-ahead schedule (layer 0's
+            # exchanging backward exists only as the run-ahead launch)
+            self.run_ahead(batch, 1, prologue=not self.ahead_primed)
+            return
         if not torch.cuda.is_current_stream_capturing():
             self.ahead_primed = False
         self._ensure_args(batch)
@@ -726,6 +752,9 @@ class FusedMLPDeep:
         if self.ahead_ok and int(self.ztick[1].item()) != 0:
             raise RuntimeError("md_bwd run-ahead: tile map or column barrier failed (error word "
                                f"{int(self.ztick[1].item())}); results invalid")
+        if self.tx is not None and self.tx.error():
+            raise RuntimeError(f"md_bwd tile exchange: a wait timed out (error word {self.tx.error()}); "
+                               "results invalid -- rerun with JDT_DP_AHEAD=0")
         if self.fuse_opt and int(self.state.opt_state["count"].item()) % 2 == 1:
             for i, t in self.par.items():
                 self.P.s(self.kn[i]).copy_(t)
@@ -743,5 +772,5 @@ def make_engine(state, mesh, axis: str, num_minibatches: int, rows: int, metrics
                          fuse_opt=fuse_opt, tx=tx, ranks_on_gpu=ranks_on_gpu)
     if supported_deep(model, rows, device):
         return FusedMLPDeep(state, mesh, axis, num_minibatches, rows, metrics, params=params, mslot=mslot,
-                            fuse_opt=fuse_opt)
+                            fuse_opt=fuse_opt, tx=tx, ranks_on_gpu=ranks_on_gpu)
     return None

@@ -63,11 +63,12 @@ def test_tile_exchange_self_test(tmp_path, ws):
         assert o["selftest"] == {"rc": 0, "wrong": 0, "timeouts": 0, "reset": 0}, (r, o)
 
 
-@pytest.mark.parametrize("ws,dp_ahead", [(2, "1"), (2, "0"), (8, "1")])
-def test_dp_over_xgmi_matches_single_device(tmp_path, ws, dp_ahead):
+@pytest.mark.parametrize("ws,dp_ahead,layers", [(2, "1", 2), (2, "0", 2), (8, "1", 2), (2, "1", 4), (2, "0", 4)])
+def test_dp_over_xgmi_matches_single_device(tmp_path, ws, dp_ahead, layers):
     """ws=2, dp_ahead=1: the one-launch step (run-ahead backward with the in-kernel
-    tile exchange: 2 x 224 workgroups fit the shared GPU); ws=2, dp_ahead=0 and ws=8
-    (8 grids do not fit one GPU): forward, backward and the xGMI all-reduce + AdamW."""
+    tile exchange: 2 x 224 workgroups fit the shared GPU) -- 4 layers: every hidden
+    layer's backward exchanges its tiles, layer 0 running ahead; ws=2, dp_ahead=0 and
+    ws=8 (8 grids do not fit one GPU): forward, backward and the xGMI all-reduce + AdamW."""
     import functools
 
     from data_paral import synthetic_batch
@@ -76,7 +77,7 @@ def test_dp_over_xgmi_matches_single_device(tmp_path, ws, dp_ahead):
     from jax_distributed_tuts_amd.utils.config import dp_config
     from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
 
-    spawn(functools.partial(XW.dp_xgmi, dp_ahead=dp_ahead), ws, str(tmp_path), gpu=True)
+    spawn(functools.partial(XW.dp_xgmi, dp_ahead=dp_ahead, num_layers=layers), ws, str(tmp_path), gpu=True)
     res = _load(tmp_path, "dpx", ws)
     assert all(o["comm"] == "xgmi" for o in res)
     assert all(o["step"] == 8 for o in res)
@@ -87,7 +88,7 @@ def test_dp_over_xgmi_matches_single_device(tmp_path, ws, dp_ahead):
         torch.testing.assert_close(res[0]["metrics"], o["metrics"], rtol=0, atol=0)
     # single device, whole batch, same steps
     dev = torch.device("cuda", 0)
-    st = init_dp(Classifier(dropout_rate=0.0), adamw(1e-3), 69, dev, None)
+    st = init_dp(Classifier(num_layers=layers, dropout_rate=0.0), adamw(1e-3), 69, dev, None)
     b = synthetic_batch(dp_config(), 70)
     b = Batch(b.inputs.to(dev), b.labels.to(dev))
     tr = DataParallelTrainer(st, None, DPConfig(4, "kernel"))

@@ -172,7 +172,7 @@ def collectives(outdir):
     comm.close()
 
 
-def dp_xgmi(outdir, steps_eager=2, steps_graph=6, dp_ahead="1"):
+def dp_xgmi(outdir, steps_eager=2, steps_graph=6, dp_ahead="1", num_layers=2):
     """DP over the xGMI fused all-reduce+AdamW kernel (dropout off), fused step
     kernels, eager steps then multi-step graph replays.  ``dp_ahead`` = JDT_DP_AHEAD:
     "1" lets the step be one run-ahead launch with the in-kernel tile exchange where
@@ -188,7 +188,7 @@ def dp_xgmi(outdir, steps_eager=2, steps_graph=6, dp_ahead="1"):
     dev = D.device()
     cfg = dp_config()
     mesh = D.Mesh({"data": D.world_size()})
-    st = init_dp(Classifier(dropout_rate=0.0), adamw(1e-3), 69, dev, None)  # same seed -> replicated
+    st = init_dp(Classifier(num_layers=num_layers, dropout_rate=0.0), adamw(1e-3), 69, dev, None)  # same seed
     b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
     b = Batch(b.inputs.to(dev), b.labels.to(dev))
     tr = DataParallelTrainer(st, mesh, DPConfig(4, "kernel", comm="xgmi"))

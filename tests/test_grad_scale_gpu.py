@@ -262,10 +262,13 @@ def _load(d, name, ws):
     return [torch.load(os.path.join(d, f"{name}_r{r}.pt"), weights_only=True) for r in range(ws)]
 
 
-@pytest.mark.parametrize("kind,ws", [("dp_sgd", 2), ("dp_adam_eps", 2), ("fsdp_sgd", 2), ("fsdp_loop_sgd", 2),
-                                     ("fsdp_loop_sgd", 4), ("dp_sgd", 8), ("dp_adam_eps", 8), ("fsdp_sgd", 8),
-                                     ("fsdp_loop_sgd", 8)])
+@pytest.mark.parametrize("kind,ws", [("dp_sgd", 2), ("dp_adam_eps", 2), ("dp4_adam_eps", 2), ("fsdp_sgd", 2),
+                                     ("fsdp_loop_sgd", 2), ("fsdp_loop_sgd", 4), ("dp_sgd", 8), ("dp_adam_eps", 8),
+                                     ("dp4_adam_eps", 8), ("fsdp_sgd", 8), ("fsdp_loop_sgd", 8)])
 def test_xgmi_strategies_grad_scale(tmp_path, kind, ws):
+    """dp4_adam_eps at ws = 2: the 4-layer DP step with every hidden layer's backward
+    exchanging its tiles in-kernel (AdamW eps = 10: the update is ~ the gradient);
+    at ws = 8 (8 grids do not fit one GPU): the xGMI all-reduce + AdamW step."""
     from jax_distributed_tuts_amd.runtime.launch import spawn
 
     from . import xgmi_workers as XW
@@ -274,11 +277,13 @@ def test_xgmi_strategies_grad_scale(tmp_path, kind, ws):
     res = _load(tmp_path, f"gpx_{kind}", ws)
     assert all(o["comm"] == "xgmi" for o in res)
     b = _batch()
-    want = mlp_grads_fp64(res[0]["before"], ["input_dense", "output_dense"], b.inputs, b.labels, n_mb=4)
+    names = (["input_dense", "hidden_dense_1", "hidden_dense_2", "output_dense"] if kind == "dp4_adam_eps"
+             else ["input_dense", "output_dense"])
+    want = mlp_grads_fp64(res[0]["before"], names, b.inputs, b.labels, n_mb=4)
     for o in res:
         for n in want:
             d = o["before"][n].double() - o["after"][n].double()
-            g = 10 * d / (1 - d.abs()) if kind == "dp_adam_eps" else d
+            g = 10 * d / (1 - d.abs()) if kind in ("dp_adam_eps", "dp4_adam_eps") else d
             check_grad(g, want[n], n)
 
 

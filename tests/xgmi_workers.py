@@ -403,10 +403,10 @@ def grad_probe_xgmi(outdir, kind, dp=1, capture=True, n_hidden=3):
     def cpu(d):
         return {k: v.detach().float().cpu().clone() for k, v in d.items()}
 
-    if kind in ("dp_sgd", "dp_adam_eps"):
+    if kind in ("dp_sgd", "dp_adam_eps", "dp4_adam_eps"):
         mesh = D.Mesh({"data": D.world_size()})
         tx = sgd(1.0) if kind == "dp_sgd" else adamw(1.0, eps=10.0, weight_decay=0.0)
-        st = init_dp(Classifier(dropout_rate=0.0), tx, 69, dev, None)
+        st = init_dp(Classifier(num_layers=4 if kind == "dp4_adam_eps" else 2, dropout_rate=0.0), tx, 69, dev, None)
         b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
         tr = DataParallelTrainer(st, mesh, DPConfig(4, "kernel", comm="xgmi"))
         before = cpu(st.params.state_dict())

@@ -4,9 +4,9 @@
 # 4-layer, one-launch and three-launch) equal to one device, the exchange self-test; then
 # shared-GPU A/B at N = 2 (4-layer and 2-layer, JDT_DP_AHEAD 1 / 0) and the 1-GPU 4-layer.
 cd /root/repo && export TMPDIR=/tmp PYTHONUNBUFFERED=1 && mkdir -p gpurun_out/s11
-timeout -k 10 600 python -u -m pytest tests/test_xgmi_gpu.py tests/test_grad_scale_gpu.py -m gpu -x -v --timeout 240 \
-  --timeout-method thread -k "tile_exchange or dp_over_xgmi or dp_adam or dp_sgd" > gpurun_out/s11/pytest.log 2>&1
-rc=$?; echo "pytest rc=$rc"; grep -E "PASSED|FAILED|ERROR" gpurun_out/s11/pytest.log | tail -16
+timeout -k 10 600 python -u -m pytest tests/test_xgmi_gpu.py tests/test_grad_scale_gpu.py -m gpu -v -s --timeout 240 \
+  --timeout-method thread -k "dp_over_xgmi or dp_adam or dp4_adam or dp_sgd" > gpurun_out/s11/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -E "PASSED|FAILED|ERROR|\[dp ws" gpurun_out/s11/pytest.log | tail -30
 [ $rc -ne 0 ] && { grep -E "Error|assert|timed out|error word" gpurun_out/s11/pytest.log | head -30; exit $rc; }
 js() { grep '^{' $1 | python -c 'import json,sys; j=json.loads(sys.stdin.read()); c=j["config"]; print(j["value"], j["ms_per_step"], c.get("step_launches"))'; }
 run() {

@@ -181,7 +181,11 @@ class DataParallelTrainer:
                      and TX.ahead_tx_ok(batch.size, H, share))
             tiles = (H // 16) * (784 // 112)
         elif supported_deep(self.model, batch.size, dev):   # deep: one launch per hidden layer
-            local = (not deterministic() and _is_adamw(self.state.tx) and os.environ.get("JDT_MLP2_AHEAD", "1") == "1"
+            # opt-in (JDT_DP_DEEP_TX=1): measured 4 % SLOWER than md_fwd / md_bwd + the xGMI
+            # all-reduce on the shared GPU (profiles/r4_one_launch_dp_ab.txt; its two-ranks-
+            # per-GPU variants spill registers), one rank per GPU unmeasured
+            local = (os.environ.get("JDT_DP_DEEP_TX", "0") == "1" and not deterministic()
+                     and _is_adamw(self.state.tx) and os.environ.get("JDT_MLP2_AHEAD", "1") == "1"
                      and bool(_lib_md_ahead_ok(batch.size)) and TX.deep_tx_ok(batch.size, share))
             tiles = FusedMLPDeep.tx_tiles(self.model.L - 1)
         else:

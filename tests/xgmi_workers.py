@@ -178,6 +178,7 @@ def dp_xgmi(outdir, steps_eager=2, steps_graph=6, dp_ahead="1", num_layers=2):
     "1" lets the step be one run-ahead launch with the in-kernel tile exchange where
     every rank's grid fits on the shared GPU, "0" keeps the three-launch step."""
     os.environ["JDT_DP_AHEAD"] = dp_ahead
+    os.environ["JDT_DP_DEEP_TX"] = dp_ahead   # the deep engine's exchange path is opt-in: test it
     from data_paral import synthetic_batch
     from jax_distributed_tuts_amd.models.mlp import Classifier
     from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp, shard_batch
@@ -404,6 +405,7 @@ def grad_probe_xgmi(outdir, kind, dp=1, capture=True, n_hidden=3):
         return {k: v.detach().float().cpu().clone() for k, v in d.items()}
 
     if kind in ("dp_sgd", "dp_adam_eps", "dp4_adam_eps"):
+        os.environ["JDT_DP_DEEP_TX"] = "1"   # dp4: the deep engine's (opt-in) exchange path where it fits
         mesh = D.Mesh({"data": D.world_size()})
         tx = sgd(1.0) if kind == "dp_sgd" else adamw(1.0, eps=10.0, weight_decay=0.0)
         st = init_dp(Classifier(num_layers=4 if kind == "dp4_adam_eps" else 2, dropout_rate=0.0), tx, 69, dev, None)

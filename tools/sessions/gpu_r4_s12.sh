@@ -4,7 +4,7 @@
 # ranks sharing the GPU (2: one launch per step; 4 / 8: forward, backward, xGMI all-reduce).
 cd /root/repo && export TMPDIR=/tmp PYTHONUNBUFFERED=1 && mkdir -p gpurun_out/s12
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
-timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread \
+timeout -k 10 1100 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread \
   > gpurun_out/s12/pytest_gpu.log 2>&1
 rc=$?; echo "pytest gpu rc=$rc"; tail -3 gpurun_out/s12/pytest_gpu.log
 [ $rc -ne 0 ] && { grep -E "FAILED|Error" gpurun_out/s12/pytest_gpu.log | head -20; exit $rc; }

@@ -570,7 +570,7 @@ __global__ void __launch_bounds__(NT) tx_selftest_kernel(const TxArgs* X, unsign
 // replaced by a per-column-block arrival ticket among workgroups that share an XCD
 // (xcd_contiguous_tile), and the one global dependency left -- complete logits for
 // the next CE -- is the launch boundary.
-template <int K_IN, int C, int KC, bool LOOP, bool AHEAD = false, bool TX = false, class AT>
+template <int K_IN, int C, int KC, bool LOOP, bool AHEAD = false, bool TX = false, bool P3S = false, class AT>
 __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by, const int step_in) {
   constexpr int MPM = 128;                 // max rows per device (fused path)
   constexpr int LDM = MPM + 8;             // padded row (bf16 elements)
@@ -796,141 +796,243 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   __syncthreads();
   STAMP(2);
 
-  // ---- 3. dW1[chunk, blk] = X[:, chunk]^T dZ1[:, blk]   (K = rows) on MFMA; one tile per wave
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  // chunk-0 blocks' spare wave, concurrently with the dW1 tiles:
-  //   dW2[blk, :] = H1[:, blk]^T dlogits ; db1[blk] = dZ1[:, blk]^T 1 ; db2 = 1^T dlogits (block (0,0))
-  f32x4 aw = {0.f, 0.f, 0.f, 0.f}, ab1 = {0.f, 0.f, 0.f, 0.f}, ab2 = {0.f, 0.f, 0.f, 0.f};
-  if (w < NTILE) {
-#pragma unroll
-    for (int ks = 0; ks < MPM / 32; ++ks) {
-      if (ks < Mp / 32) {
-        const int kk = ks * 32 + 8 * (lane >> 4);
-        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
-        acc = mfma16x16x32(xf[ks], bfr, acc);
-      }
-    }
-  } else if (aux) {
-    bf16x8 ones;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) ones[q] = (short)0x3f80;  // bf16 1.0
-#pragma unroll
-    for (int ks = 0; ks < MPM / 32; ++ks) {
-      if (ks >= Mp / 32) break;
-      const int kk = ks * 32 + 8 * (lane >> 4);
-      const bf16x8 hT = *reinterpret_cast<const bf16x8*>(&h1T[(lane & 15) * LDM + kk]);
-      const bf16x8 dT = *reinterpret_cast<const bf16x8*>(&dlT[(lane & 15) * LDM + kk]);
-      const bf16x8 zT = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
-      aw = mfma16x16x32(hT, dT, aw);
-      ab1 = mfma16x16x32(zT, ones, ab1);
-      if (lead) ab2 = mfma16x16x32(ones, dT, ab2);
-    }
-  }
-  // N > 1 (Mlp2Args::tx): this tile's gradients -- and the lead's db2 and metric slots --
-  // all-reduced with the same tile of the other ranks' launches before the optimizer
+  // mval: lead, tid < 4 -- the all-reduced metric slot of the N > 1 exchange (TX)
   float mval = 0.f;
-  if constexpr (AHEAD && TX) {
-    {
-      if (lead && tid < 4) {
-        float L = 0.f, Cr = 0.f;
-        for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
-        mval = tid == 0 ? L : tid == 2 ? Cr : (float)M;   // {loss sum, n, correct, n}
-      }
-      float4 v4[2];
-      int p4[2], n4 = 0, ps = -1;
-      float vs = 0.f;
-      if (w < NTILE) {
-        v4[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-        p4[0] = w * 256 + lane * 4;
-        n4 = 1;
-        if (lead && tid < 4) { vs = mval; ps = (NTILE + 2) * 256 + 64 + tid; }
-      } else if (aux) {
-        v4[0] = make_float4(aw[0], aw[1], aw[2], aw[3]);
-        v4[1] = make_float4(ab1[0], ab1[1], ab1[2], ab1[3]);
-        p4[0] = NTILE * 256 + lane * 4;
-        p4[1] = (NTILE + 1) * 256 + lane * 4;
-        n4 = 2;
-        if (lead && lane < C) { vs = ab2[0]; ps = (NTILE + 2) * 256 + lane; }
-      }
-      STAMP(12);
-      tx_tile(a.tx, bx * NCH + by, (unsigned)step + 1u, n4, v4, p4, vs, ps, a.ztick + 1);
-      STAMP(13);
-      if (w < NTILE) {
-        acc = (f32x4){v4[0].x, v4[0].y, v4[0].z, v4[0].w};
-        if (lead && tid < 4) mval = vs;
-      } else if (aux) {
-        aw = (f32x4){v4[0].x, v4[0].y, v4[0].z, v4[0].w};
-        ab1 = (f32x4){v4[1].x, v4[1].y, v4[1].z, v4[1].w};
-        if (lead && lane < C) ab2[0] = vs;
-      }
-    }
-  }
-  if (w < NTILE) {
-    unsigned wt[2] = {0u, 0u};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const long idx = (long)(trow0 + e) * H + tcol;   // K_IN % KC == 0: always in range
-      if (a.fuse_opt) {
-        float tp, tm = om[e], tv = ov[e];
-        const bf16_t pb = f2bf(adam_apply(op[e], om[e], ov[e], acc[e], ak, &tp, &tm, &tv));
-        if (AHEAD && (a.wt & 1)) {
-          st_f<true>(a.pW1 + idx, tp);
-          if (!ak.sgd) { st_f<true>(a.mW1 + idx, tm); st_f<true>(a.vW1 + idx, tv); }
-        } else {
-          a.pW1[idx] = tp;
-          if (!ak.sgd) { a.mW1[idx] = tm; a.vW1[idx] = tv; }   // SGD: m / v alias p (unused)
+  if constexpr (!TX && !P3S) {
+    // one GPU: each tile's MFMA result goes straight into its epilogue
+    // ---- 3. dW1[chunk, blk] = X[:, chunk]^T dZ1[:, blk]   (K = rows) on MFMA; one tile per wave
+    if (w < NTILE) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+      for (int ks = 0; ks < MPM / 32; ++ks) {
+        if (ks < Mp / 32) {
+          const int kk = ks * 32 + 8 * (lane >> 4);
+          const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
+          acc = mfma16x16x32(xf[ks], bfr, acc);
         }
-        // with the W1^T copy, the [in,out] bf16 shadow is rebuilt from it by
-        // FusedMLP2.finalize() instead of being written every step (0.8 MB of HBM writes)
-        if (!a.W1T) a.sW1[idx] = pb;
-        wt[e >> 1] |= (unsigned)pb << (16 * (e & 1));
-      } else if (a.smap) {
-        stage_store(a.smap, par, 0, trow0 + e, tcol, acc[e]);
-      } else {
-        a.gW1[goff + idx] = acc[e];
       }
-    }
-    // the lane's 4 rows are 4 consecutive K elements of W1^T: one 8-byte store
-    if (a.fuse_opt && a.W1T) {
-      const unsigned long long w8 = (unsigned long long)wt[0] | ((unsigned long long)wt[1] << 32);
-      if (LOOP || (AHEAD && (a.wt & 1))) st_u64<true>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
-      else st_u64<false>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
-    }
-    if constexpr (AHEAD)
-      *reinterpret_cast<uint2*>(&w1n[(lane & 15) * LDW1 + (trow0 - kc0)]) = make_uint2(wt[0], wt[1]);
-  } else if (aux) {
-    bf16_t* sW2n = par ? a.sW2_0 : a.sW2_1;   // next step's parity buffer
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      // lanes ac < C: W2[j0+n][ac]; lane ac == C: b1[j0+n] (every column of ab1 holds
-      // db1, B = ones) -- one AdamW code path for both, its state loaded in phase 0
-      const int n = (lane >> 4) * 4 + e;
-      if (ac <= C) {
-        const bool isb = ac == C;
-        const long o = isb ? (long)(j0 + n) : (long)(j0 + n) * C + ac;
-        const float gr = isb ? ab1[e] : aw[e];
+      unsigned wt[2] = {0u, 0u};
+  #pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long idx = (long)(trow0 + e) * H + tcol;   // K_IN % KC == 0: always in range
         if (a.fuse_opt) {
-          const float pn = adam_apply_h<LOOP>(op[e], om[e], ov[e], gr, ak, (isb ? a.pb1 : a.pW2) + o,
-                                              (isb ? a.mb1 : a.mW2) + o, (isb ? a.vb1 : a.vW2) + o);
-          (isb ? a.sb1 : sW2n)[o] = f2bf(pn);
-          if constexpr (AHEAD) a.hand[(isb ? 0 : H) + o] = pn;   // same XCD as the reader (L2)
+          float tp, tm = om[e], tv = ov[e];
+          const bf16_t pb = f2bf(adam_apply(op[e], om[e], ov[e], acc[e], ak, &tp, &tm, &tv));
+          if (AHEAD && (a.wt & 1)) {
+            st_f<true>(a.pW1 + idx, tp);
+            if (!ak.sgd) { st_f<true>(a.mW1 + idx, tm); st_f<true>(a.vW1 + idx, tv); }
+          } else {
+            a.pW1[idx] = tp;
+            if (!ak.sgd) { a.mW1[idx] = tm; a.vW1[idx] = tv; }   // SGD: m / v alias p (unused)
+          }
+          // with the W1^T copy, the [in,out] bf16 shadow is rebuilt from it by
+          // FusedMLP2.finalize() instead of being written every step (0.8 MB of HBM writes)
+          if (!a.W1T) a.sW1[idx] = pb;
+          wt[e >> 1] |= (unsigned)pb << (16 * (e & 1));
         } else if (a.smap) {
-          if (isb) stage_store(a.smap, par, 1, j0 + n, 0, gr);
-          else stage_store(a.smap, par, 2, j0 + n, ac, gr);
+          stage_store(a.smap, par, 0, trow0 + e, tcol, acc[e]);
         } else {
-          (isb ? a.gb1 : a.gW2)[goff + o] = gr;
+          a.gW1[goff + idx] = acc[e];
+        }
+      }
+      // the lane's 4 rows are 4 consecutive K elements of W1^T: one 8-byte store
+      if (a.fuse_opt && a.W1T) {
+        const unsigned long long w8 = (unsigned long long)wt[0] | ((unsigned long long)wt[1] << 32);
+        if (LOOP || (AHEAD && (a.wt & 1))) st_u64<true>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
+        else st_u64<false>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
+      }
+      if constexpr (AHEAD)
+        *reinterpret_cast<uint2*>(&w1n[(lane & 15) * LDW1 + (trow0 - kc0)]) = make_uint2(wt[0], wt[1]);
+    } else if (aux) {
+      // chunk-0 blocks, concurrently with the dW1 tiles:
+      //   dW2[blk, :] = H1[:, blk]^T dlogits ; db1[blk] = dZ1[:, blk]^T 1 ; db2 = 1^T dlogits (block (0,0))
+      bf16x8 ones;
+  #pragma unroll
+      for (int q = 0; q < 8; ++q) ones[q] = (short)0x3f80;  // bf16 1.0
+      f32x4 aw = {0.f, 0.f, 0.f, 0.f}, ab1 = {0.f, 0.f, 0.f, 0.f}, ab2 = {0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+      for (int ks = 0; ks < MPM / 32; ++ks) {
+        if (ks >= Mp / 32) break;
+        const int kk = ks * 32 + 8 * (lane >> 4);
+        const bf16x8 hT = *reinterpret_cast<const bf16x8*>(&h1T[(lane & 15) * LDM + kk]);
+        const bf16x8 dT = *reinterpret_cast<const bf16x8*>(&dlT[(lane & 15) * LDM + kk]);
+        const bf16x8 zT = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
+        aw = mfma16x16x32(hT, dT, aw);
+        ab1 = mfma16x16x32(zT, ones, ab1);
+        if (lead) ab2 = mfma16x16x32(ones, dT, ab2);
+      }
+      bf16_t* sW2n = par ? a.sW2_0 : a.sW2_1;   // next step's parity buffer
+  #pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        // lanes ac < C: W2[j0+n][ac]; lane ac == C: b1[j0+n] (every column of ab1 holds
+        // db1, B = ones) -- one AdamW code path for both, its state loaded in phase 0
+        const int n = (lane >> 4) * 4 + e;
+        if (ac <= C) {
+          const bool isb = ac == C;
+          const long o = isb ? (long)(j0 + n) : (long)(j0 + n) * C + ac;
+          const float gr = isb ? ab1[e] : aw[e];
+          if (a.fuse_opt) {
+            const float pn = adam_apply_h<LOOP>(op[e], om[e], ov[e], gr, ak, (isb ? a.pb1 : a.pW2) + o,
+                                                (isb ? a.mb1 : a.mW2) + o, (isb ? a.vb1 : a.vW2) + o);
+            (isb ? a.sb1 : sW2n)[o] = f2bf(pn);
+            if constexpr (AHEAD) a.hand[(isb ? 0 : H) + o] = pn;   // same XCD as the reader (L2)
+          } else if (a.smap) {
+            if (isb) stage_store(a.smap, par, 1, j0 + n, 0, gr);
+            else stage_store(a.smap, par, 2, j0 + n, ac, gr);
+          } else {
+            (isb ? a.gb1 : a.gW2)[goff + o] = gr;
+          }
+        }
+      }
+      if (lead && lane < C) {
+        if (a.fuse_opt) {
+          const float pn = adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
+          a.sb2[lane] = f2bf(pn);
+          if constexpr (AHEAD) a.hand[H + (long)H * C + lane] = pn;
+        } else if (a.smap) {
+          stage_store(a.smap, par, 3, lane, 0, ab2[0]);
+        } else {
+          a.gb2[goff + lane] = ab2[0];
         }
       }
     }
-    if (lead && lane < C) {
-      if (a.fuse_opt) {
-        const float pn = adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
-        a.sb2[lane] = f2bf(pn);
-        if constexpr (AHEAD) a.hand[H + (long)H * C + lane] = pn;
-      } else if (a.smap) {
-        stage_store(a.smap, par, 3, lane, 0, ab2[0]);
-      } else {
-        a.gb2[goff + lane] = ab2[0];
+  } else {
+    // N > 1 (TX): all MFMAs, then the tile exchange, then the epilogues
+    // ---- 3. dW1[chunk, blk] = X[:, chunk]^T dZ1[:, blk]   (K = rows) on MFMA; one tile per wave
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // chunk-0 blocks' spare wave, concurrently with the dW1 tiles:
+    //   dW2[blk, :] = H1[:, blk]^T dlogits ; db1[blk] = dZ1[:, blk]^T 1 ; db2 = 1^T dlogits (block (0,0))
+    f32x4 aw = {0.f, 0.f, 0.f, 0.f}, ab1 = {0.f, 0.f, 0.f, 0.f}, ab2 = {0.f, 0.f, 0.f, 0.f};
+    if (w < NTILE) {
+  #pragma unroll
+      for (int ks = 0; ks < MPM / 32; ++ks) {
+        if (ks < Mp / 32) {
+          const int kk = ks * 32 + 8 * (lane >> 4);
+          const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
+          acc = mfma16x16x32(xf[ks], bfr, acc);
+        }
+      }
+    } else if (aux) {
+      bf16x8 ones;
+  #pragma unroll
+      for (int q = 0; q < 8; ++q) ones[q] = (short)0x3f80;  // bf16 1.0
+  #pragma unroll
+      for (int ks = 0; ks < MPM / 32; ++ks) {
+        if (ks >= Mp / 32) break;
+        const int kk = ks * 32 + 8 * (lane >> 4);
+        const bf16x8 hT = *reinterpret_cast<const bf16x8*>(&h1T[(lane & 15) * LDM + kk]);
+        const bf16x8 dT = *reinterpret_cast<const bf16x8*>(&dlT[(lane & 15) * LDM + kk]);
+        const bf16x8 zT = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
+        aw = mfma16x16x32(hT, dT, aw);
+        ab1 = mfma16x16x32(zT, ones, ab1);
+        if (lead) ab2 = mfma16x16x32(ones, dT, ab2);
+      }
+    }
+    // N > 1 (Mlp2Args::tx): this tile's gradients -- and the lead's db2 and metric slots --
+    // all-reduced with the same tile of the other ranks' launches before the optimizer
+    if constexpr (AHEAD && TX) {
+      {
+        if (lead && tid < 4) {
+          float L = 0.f, Cr = 0.f;
+          for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
+          mval = tid == 0 ? L : tid == 2 ? Cr : (float)M;   // {loss sum, n, correct, n}
+        }
+        float4 v4[2];
+        int p4[2], n4 = 0, ps = -1;
+        float vs = 0.f;
+        if (w < NTILE) {
+          v4[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+          p4[0] = w * 256 + lane * 4;
+          n4 = 1;
+          if (lead && tid < 4) { vs = mval; ps = (NTILE + 2) * 256 + 64 + tid; }
+        } else if (aux) {
+          v4[0] = make_float4(aw[0], aw[1], aw[2], aw[3]);
+          v4[1] = make_float4(ab1[0], ab1[1], ab1[2], ab1[3]);
+          p4[0] = NTILE * 256 + lane * 4;
+          p4[1] = (NTILE + 1) * 256 + lane * 4;
+          n4 = 2;
+          if (lead && lane < C) { vs = ab2[0]; ps = (NTILE + 2) * 256 + lane; }
+        }
+        STAMP(12);
+        tx_tile(a.tx, bx * NCH + by, (unsigned)step + 1u, n4, v4, p4, vs, ps, a.ztick + 1);
+        STAMP(13);
+        if (w < NTILE) {
+          acc = (f32x4){v4[0].x, v4[0].y, v4[0].z, v4[0].w};
+          if (lead && tid < 4) mval = vs;
+        } else if (aux) {
+          aw = (f32x4){v4[0].x, v4[0].y, v4[0].z, v4[0].w};
+          ab1 = (f32x4){v4[1].x, v4[1].y, v4[1].z, v4[1].w};
+          if (lead && lane < C) ab2[0] = vs;
+        }
+      }
+    }
+    if (w < NTILE) {
+      unsigned wt[2] = {0u, 0u};
+  #pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long idx = (long)(trow0 + e) * H + tcol;   // K_IN % KC == 0: always in range
+        if (a.fuse_opt) {
+          float tp, tm = om[e], tv = ov[e];
+          const bf16_t pb = f2bf(adam_apply(op[e], om[e], ov[e], acc[e], ak, &tp, &tm, &tv));
+          if (AHEAD && (a.wt & 1)) {
+            st_f<true>(a.pW1 + idx, tp);
+            if (!ak.sgd) { st_f<true>(a.mW1 + idx, tm); st_f<true>(a.vW1 + idx, tv); }
+          } else {
+            a.pW1[idx] = tp;
+            if (!ak.sgd) { a.mW1[idx] = tm; a.vW1[idx] = tv; }   // SGD: m / v alias p (unused)
+          }
+          // with the W1^T copy, the [in,out] bf16 shadow is rebuilt from it by
+          // FusedMLP2.finalize() instead of being written every step (0.8 MB of HBM writes)
+          if (!a.W1T) a.sW1[idx] = pb;
+          wt[e >> 1] |= (unsigned)pb << (16 * (e & 1));
+        } else if (a.smap) {
+          stage_store(a.smap, par, 0, trow0 + e, tcol, acc[e]);
+        } else {
+          a.gW1[goff + idx] = acc[e];
+        }
+      }
+      // the lane's 4 rows are 4 consecutive K elements of W1^T: one 8-byte store
+      if (a.fuse_opt && a.W1T) {
+        const unsigned long long w8 = (unsigned long long)wt[0] | ((unsigned long long)wt[1] << 32);
+        if (LOOP || (AHEAD && (a.wt & 1))) st_u64<true>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
+        else st_u64<false>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
+      }
+      if constexpr (AHEAD)
+        *reinterpret_cast<uint2*>(&w1n[(lane & 15) * LDW1 + (trow0 - kc0)]) = make_uint2(wt[0], wt[1]);
+    } else if (aux) {
+      bf16_t* sW2n = par ? a.sW2_0 : a.sW2_1;   // next step's parity buffer
+  #pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        // lanes ac < C: W2[j0+n][ac]; lane ac == C: b1[j0+n] (every column of ab1 holds
+        // db1, B = ones) -- one AdamW code path for both, its state loaded in phase 0
+        const int n = (lane >> 4) * 4 + e;
+        if (ac <= C) {
+          const bool isb = ac == C;
+          const long o = isb ? (long)(j0 + n) : (long)(j0 + n) * C + ac;
+          const float gr = isb ? ab1[e] : aw[e];
+          if (a.fuse_opt) {
+            const float pn = adam_apply_h<LOOP>(op[e], om[e], ov[e], gr, ak, (isb ? a.pb1 : a.pW2) + o,
+                                                (isb ? a.mb1 : a.mW2) + o, (isb ? a.vb1 : a.vW2) + o);
+            (isb ? a.sb1 : sW2n)[o] = f2bf(pn);
+            if constexpr (AHEAD) a.hand[(isb ? 0 : H) + o] = pn;   // same XCD as the reader (L2)
+          } else if (a.smap) {
+            if (isb) stage_store(a.smap, par, 1, j0 + n, 0, gr);
+            else stage_store(a.smap, par, 2, j0 + n, ac, gr);
+          } else {
+            (isb ? a.gb1 : a.gW2)[goff + o] = gr;
+          }
+        }
+      }
+      if (lead && lane < C) {
+        if (a.fuse_opt) {
+          const float pn = adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
+          a.sb2[lane] = f2bf(pn);
+          if constexpr (AHEAD) a.hand[H + (long)H * C + lane] = pn;
+        } else if (a.smap) {
+          stage_store(a.smap, par, 3, lane, 0, ab2[0]);
+        } else {
+          a.gb2[goff + lane] = ab2[0];
+        }
       }
     }
   }
@@ -1094,12 +1196,12 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   if constexpr (XCD) xcd_contiguous_tile(bx, by);
   mlp2_fwd_body<K_IN, C, RB, DIRECT, false>(static_cast<const Mlp2Args&>(a), bx, by, 0);
 }
-template <int K_IN, int C, int KC, bool XCD, bool AHEAD = false, bool TX = false>
+template <int K_IN, int C, int KC, bool XCD, bool AHEAD = false, bool TX = false, bool P3S = false>
 __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   int bx = blockIdx.x, by = blockIdx.y;
   if constexpr (AHEAD) xcd_column_tile(bx, by);
   else if constexpr (XCD) xcd_contiguous_tile(bx, by);
-  mlp2_bwd_body<K_IN, C, KC, false, AHEAD, TX>(static_cast<const Mlp2Args&>(a), bx, by, 0);
+  mlp2_bwd_body<K_IN, C, KC, false, AHEAD, TX, P3S>(static_cast<const Mlp2Args&>(a), bx, by, 0);
 }
 
 // n complete training steps in ONE launch (single GPU, fused AdamW, W1^T copy):
@@ -1294,6 +1396,11 @@ JDT_API int jdt_tx_selftest(const void* tx_args_dev, int tiles, unsigned epoch, 
   return HIP_LAUNCH_CHECK();
 }
 
+// A/B switch (JDT_MLP2_P3S=1): the one-GPU run-ahead backward compiled with the N > 1
+// kernel's phase-3 structure (all MFMAs, then all epilogues) instead of its own
+static int g_mlp2_p3s = 0;
+JDT_API void jdt_mlp2_set_p3s(int on) { g_mlp2_p3s = on; }
+
 // phase 0: mlp2_fwd, 1: mlp2_bwd, 2: run-ahead mlp2_bwd (backward of t + forward of t+1)
 JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* stream) {
   const Mlp2Args& a = *args;
@@ -1326,6 +1433,7 @@ JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* str
       return -3;
     const dim3 g(a.H / 16, 784 / 112);
     if (a.tx) hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true, true, true>), g, dim3(NT), 0, st, a);
+    else if (g_mlp2_p3s) hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true, true, false, true>), g, dim3(NT), 0, st, a);
     else hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true, true>), g, dim3(NT), 0, st, a);
   }
   return HIP_LAUNCH_CHECK();

@@ -78,6 +78,7 @@ def stage_map_tensor(base: int, half: int, slice_: int, world: int, leaves, devi
 
 
 _lib.declare("jdt_mlp2", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_int, c_void_p])
+_lib.declare("jdt_mlp2_set_p3s", None, [c_int])
 _lib.declare("jdt_mlp2_args_size", c_int, [])
 _lib.declare("jdt_mlp2_ahead_ok", c_int, [c_int, c_int])
 _lib.declare("jdt_mlp2_set_rows", None, [c_int])
@@ -185,6 +186,8 @@ class FusedMLP2:
                         and bool(_lib.lib().jdt_mlp2_loop_ok(rows, H)))
         if _lib.lib().jdt_mlp2_args_size() != ctypes.sizeof(Mlp2Args):
             raise RuntimeError("Mlp2Args layout mismatch")
+        if os.environ.get("JDT_MLP2_P3S"):   # A/B: the one-GPU run-ahead with the N > 1 phase-3 order
+            _lib.lib().jdt_mlp2_set_p3s(int(os.environ["JDT_MLP2_P3S"]))
         self._args = None
         self._key = None
         self.grad_stage = None   # (staging base pointer, half stride in floats): set_grad_stage

@@ -1,0 +1,52 @@
+"""Host-side checks of the one-launch N > 1 step's exchange geometry
+(comm/tile_exchange.py, ops/csrc/common.h tx_tile and its callers in mlp_fused.hip /
+mlp_deep.hip): every payload position a workgroup's threads move lies inside
+TILE_PAYLOAD, no two threads of a workgroup share a position, and the tile counts match
+the backward kernels' grids.  Pure index arithmetic mirrored from the kernels."""
+import pytest
+
+from jax_distributed_tuts_amd.comm.tile_exchange import SELFTEST_TILES, TILE_PAYLOAD
+from jax_distributed_tuts_amd.parallel.fused_mlp import FusedMLPDeep
+
+NT, NW, C = 512, 8, 10
+
+
+def positions(ntile: int, chunk0: bool, lead: bool, top: bool = True):
+    """{thread: [payload offsets]} as the kernels assign them (float4 slots expanded)."""
+    out = {}
+    for tid in range(NT):
+        w, lane = tid >> 6, tid & 63
+        p = []
+        if w < ntile:
+            p += [w * 256 + lane * 4 + e for e in range(4)]
+            if lead and tid < 4:
+                p.append(9 * 256 + 64 + tid)           # metric slot
+        elif chunk0 and w == NW - 1:
+            p += [7 * 256 + lane * 4 + e for e in range(4)]   # db (deep) / dW2 (2-layer)
+            if top:
+                p += [8 * 256 + lane * 4 + e for e in range(4)]
+            if lead and lane < C:
+                p.append(9 * 256 + lane)               # head / output bias
+        out[tid] = p
+    return out
+
+
+@pytest.mark.parametrize("ntile,top", [(7, True), (7, False), (4, True), (4, False)])
+def test_payload_positions_fit_and_are_disjoint(ntile, top):
+    for chunk0, lead in ((False, False), (True, False), (True, True)):
+        pos = positions(ntile, chunk0, lead, top)
+        flat = [x for v in pos.values() for x in v]
+        assert max(flat) < TILE_PAYLOAD and min(flat) >= 0
+        assert len(flat) == len(set(flat)), (ntile, chunk0, lead)
+    assert TILE_PAYLOAD % 4 == 0
+
+
+def test_tile_counts_match_the_grids():
+    # mlp2_bwd / md_bwd layer 0: (512 / 16) column blocks x (784 / 112) input chunks;
+    # md_bwd layers >= 1: (512 / 16) x (512 / 64)
+    assert FusedMLPDeep.tx_tiles(1) == 32 * 7
+    assert FusedMLPDeep.tx_tiles(3) == 32 * 7 + 2 * 32 * 8
+    eng = FusedMLPDeep.__new__(FusedMLPDeep)
+    bases = [eng.tx_base(i) for i in range(3)]
+    assert bases == [0, 224, 480]
+    assert SELFTEST_TILES <= 32 * 7

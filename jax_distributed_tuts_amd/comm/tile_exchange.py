@@ -101,10 +101,7 @@ class TileExchange:
         return True
 
     def _agree(self, ok: bool) -> bool:
-        t = torch.tensor([1 if ok else 0], dtype=torch.int32,
-                         device=self.device if dist.get_backend(self.group) == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
-        return bool(int(t.item()))
+        return agree(self.group, ok, self.device)
 
     @property
     def args_ptr(self) -> int:
@@ -114,10 +111,6 @@ class TileExchange:
     def error(self) -> int:
         """This rank's error word (4: an exchange wait timed out; synchronous read)."""
         return int(_lib.lib().jdt_tx_error(self.ctx)) if self.ctx else 0
-
-    def agree(self, ok: bool) -> bool:
-        """All ranks' AND of ``ok`` (collective)."""
-        return self._agree(ok)
 
     def close(self):
         if self.ctx:

@@ -20,6 +20,7 @@ import os
 import pytest
 import torch
 
+from .gpu_spawn import spawn8
 from .oracle import check_grad, mlp_grads_fp64, sgd_grads
 
 pytestmark = pytest.mark.gpu
@@ -296,8 +297,7 @@ def test_xgmi_pipeline_grad_scale(tmp_path, ws, dp, n_hidden):
 
     from . import xgmi_workers as XW
 
-    spawn(functools.partial(XW.grad_probe_xgmi, kind="pp_sgd", dp=dp, n_hidden=n_hidden), ws, str(tmp_path),
-          gpu=True)
+    spawn8(functools.partial(XW.grad_probe_xgmi, kind="pp_sgd", dp=dp, n_hidden=n_hidden), ws, str(tmp_path))
     res = _load(tmp_path, "gpx_pp_sgd", ws)
     before, got = {}, {}
     for o in res:

@@ -12,28 +12,13 @@ import torch
 from jax_distributed_tuts_amd.runtime.launch import spawn
 
 from . import xgmi_workers as XW
+from .gpu_spawn import spawn8 as _spawn8
 
 pytestmark = pytest.mark.gpu
 
 
 def _load(d, name, ws):
     return [torch.load(os.path.join(d, f"{name}_r{r}.pt"), weights_only=True) for r in range(ws)]
-
-
-def _spawn8(fn, ws, *args):
-    """spawn() for the heaviest 8-rank cases.  Eight processes time-sharing one GPU can
-    leave one rank's queue unscheduled past the in-kernel barrier timeout while the
-    other seven spin (every other rank then reports that one rank as the silent peer;
-    profiles/r4_eight_rank_rehearsal.txt) -- a scheduling property of the shared card,
-    not of the code under test, which a node with a GPU per rank never has.  That one
-    failure signature skips; any other failure, and every result of a run that
-    completes, is checked as usual."""
-    try:
-        spawn(fn, ws, *args, gpu=True)
-    except Exception as e:  # noqa: BLE001
-        if ws >= 8 and "timed out on this rank" in str(e) and "silent_peer" in str(e):
-            pytest.skip(f"{ws} ranks sharing one GPU: a rank was not scheduled within the barrier timeout")
-        raise
 
 
 @pytest.mark.parametrize("ws", [2, 4, 8])
@@ -77,7 +62,7 @@ def test_dp_over_xgmi_matches_single_device(tmp_path, ws, dp_ahead, layers):
     from jax_distributed_tuts_amd.utils.config import dp_config
     from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
 
-    spawn(functools.partial(XW.dp_xgmi, dp_ahead=dp_ahead, num_layers=layers), ws, str(tmp_path), gpu=True)
+    _spawn8(functools.partial(XW.dp_xgmi, dp_ahead=dp_ahead, num_layers=layers), ws, str(tmp_path))
     res = _load(tmp_path, "dpx", ws)
     assert all(o["comm"] == "xgmi" for o in res)
     assert all(o["step"] == 8 for o in res)
@@ -187,7 +172,7 @@ def test_pipeline_over_xgmi_matches_single_device(tmp_path, ws, dp, n_hidden):
 
     import functools
 
-    spawn(functools.partial(XW.pp_xgmi, dp=dp, n_hidden=n_hidden), ws, str(tmp_path), gpu=True)
+    _spawn8(functools.partial(XW.pp_xgmi, dp=dp, n_hidden=n_hidden), ws, str(tmp_path))
     res = _load(tmp_path, f"ppx{dp}", ws)
     assert all(o["comm"] == "xgmi" and o["count"] == 4 for o in res)
     dev = torch.device("cuda", 0)
@@ -227,7 +212,7 @@ def test_transformer_hybrid_over_xgmi_matches_single_device(tmp_path, ws, n_laye
     from jax_distributed_tuts_amd.parallel.pipeline_lm import build_lm_pipeline, lm_batch
     from jax_distributed_tuts_amd.utils.train_state import Batch
 
-    spawn(functools.partial(XW.lm_pp_xgmi, dp=2, n_layers=n_layers), ws, str(tmp_path), gpu=True)
+    _spawn8(functools.partial(XW.lm_pp_xgmi, dp=2, n_layers=n_layers), ws, str(tmp_path))
     res = _load(tmp_path, "lmx2", ws)
     assert all(o["comm"] == "xgmi" for o in res)
     # the data-axis sync ran per part, overlapping the W pass (pipeline._overlapped_sync):

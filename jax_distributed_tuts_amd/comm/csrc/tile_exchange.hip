@@ -28,7 +28,8 @@ struct TxCtx {
 
 static long tx_part_floats(const TxCtx* c) { return (long)c->tiles * TX_MAX_RANKS * c->pay; }
 static long tx_red_floats(const TxCtx* c) { return (long)c->tiles * c->pay; }
-static long tx_flag_words(const TxCtx* c) { return (long)c->tiles * TX_MAX_RANKS + c->tiles; }
+// [tile][src] partial flags, [tile] reduced flags (DP), [tile][owner] updated-value flags (FSDP)
+static long tx_flag_words(const TxCtx* c) { return (long)c->tiles * TX_MAX_RANKS * 2 + c->tiles; }
 
 }  // namespace jdt
 using namespace jdt;

@@ -113,6 +113,9 @@ struct Mlp2Args {
   // N > 1 run-ahead step: the per-tile gradient exchange with the other ranks' launches
   // (common.h TxArgs, device memory; null = one GPU)
   const TxArgs* tx;
+  // with tx: 1 = FSDP (the optimizer state pointers are this rank's local shards; the
+  // tile's partials go to their rows' owners, which hand back updated values)
+  int tx_fsdp;
 };
 
 // Persistent multi-step launch (mlp2_loop_kernel): n steps, grid barriers between
@@ -570,7 +573,8 @@ __global__ void __launch_bounds__(NT) tx_selftest_kernel(const TxArgs* X, unsign
 // replaced by a per-column-block arrival ticket among workgroups that share an XCD
 // (xcd_contiguous_tile), and the one global dependency left -- complete logits for
 // the next CE -- is the launch boundary.
-template <int K_IN, int C, int KC, bool LOOP, bool AHEAD = false, bool TX = false, bool P3S = false, class AT>
+template <int K_IN, int C, int KC, bool LOOP, bool AHEAD = false, bool TX = false, bool P3S = false,
+          bool FX = false, class AT>
 __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by, const int step_in) {
   constexpr int MPM = 128;                 // max rows per device (fused path)
   constexpr int LDM = MPM + 8;             // padded row (bf16 elements)
@@ -677,11 +681,24 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   const float* sp = aux ? (w2l ? sgpr_ptr(fo ? a.pW2 : a.gW2) : sgpr_ptr(fo ? a.pb1 : a.gb1)) : sgpr_ptr(fo ? a.pW1 : a.gW1);
   const float* sm = aux ? (w2l ? sgpr_ptr(fo ? a.mW2 : a.gW2) : sgpr_ptr(fo ? a.mb1 : a.gb1)) : sgpr_ptr(fo ? a.mW1 : a.gW1);
   const float* sv = aux ? (w2l ? sgpr_ptr(fo ? a.vW2 : a.gW2) : sgpr_ptr(fo ? a.vb1 : a.gb1)) : sgpr_ptr(fo ? a.vW1 : a.gW1);
+  // FSDP one-launch (FX): the AdamW state is this rank's LOCAL shard (W1 rows in 784 / W
+  // blocks, W2 / b1 rows in H / W blocks); other ranks' elements read a clamped index
+  int fx_R = 0, fx_rpq = 1, fx_hpq = 1;
+  if constexpr (FX) {
+    fx_R = a.tx->rank;
+    fx_rpq = 784 / a.tx->world;
+    fx_hpq = H / a.tx->world;
+  }
   float op[4], om[4], ov[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int n = (lane >> 4) * 4 + e;
-    const long idx = aux ? (w2l ? (long)(j0 + n) * C + ac : (long)(j0 + n)) : (long)(trow0 + e) * H + tcol;
+    long idx = aux ? (w2l ? (long)(j0 + n) * C + ac : (long)(j0 + n)) : (long)(trow0 + e) * H + tcol;
+    if constexpr (FX) {
+      const int lr = aux ? min(max(j0 + n - fx_R * fx_hpq, 0), fx_hpq - 1)
+                         : min(max(trow0 + e - fx_R * fx_rpq, 0), fx_rpq - 1);
+      idx = aux ? (w2l ? (long)lr * C + ac : (long)lr) : (long)lr * H + tcol;
+    }
     op[e] = ld_global(sp + idx); om[e] = ld_global(sm + idx); ov[e] = ld_global(sv + idx);
   }
   const float run_pre = (a.running ? a.running : a.logits)[lane & 3];   // lead: metric accumulators
@@ -928,110 +945,262 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         if (lead) ab2 = mfma16x16x32(ones, dT, ab2);
       }
     }
-    // N > 1 (Mlp2Args::tx): this tile's gradients -- and the lead's db2 and metric slots --
-    // all-reduced with the same tile of the other ranks' launches before the optimizer
-    if constexpr (AHEAD && TX) {
+    if constexpr (FX) {
+      // FSDP at N > 1 (the reference's dim-0 shards: W1 rows in 784 / W blocks, W2 / b1 rows
+      // in H / W blocks; b2 replicated): every element's partial goes to the rank that owns
+      // its row, the owner sums in rank order, applies the SHARDED AdamW (its local state)
+      // and pushes the updated fp32 value to every rank; replicated b2 and the metric slots
+      // are summed by rank T % W and pushed back as sums (every rank updates its own copy).
+      // Then every rank holds the whole updated tile and runs the next forward from it.
+      const TxArgs* X = a.tx;
+      const int R = fx_R, W = X->world;
+      const int T = bx * NCH + by;
+      const long pay = X->pay, tiles = X->tiles;
+      const unsigned long long tb = (unsigned long long)pay * 4ull;
+      const unsigned epoch = (unsigned)step + 1u;
+      const long AG = tiles * TX_MAX_RANKS + tiles;   // flag base of the updated-value hand-back
+      const int o_lo = kc0 / fx_rpq, o_hi = (kc0 + KC - 1) / fx_rpq, ob = j0 / fx_hpq, orep = T % W;
+      auto owner_of = [&](int q) { return (q >= o_lo && q <= o_hi) || (chunk0 && q == ob) || (lead && q == orep); };
+      if (lead && tid < 4) {
+        float L = 0.f, Cr = 0.f;
+        for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
+        mval = tid == 0 ? L : tid == 2 ? Cr : (float)M;   // {loss sum, n, correct, n}
+      }
+      float ev[4];          // waves < NTILE: this lane's 4 W1 elements; aux: dW2 (ac < C) / db1 (ac == C)
+      int eo[4];            // their owners
+      int epos[4];          // payload positions
+      int ne = 0;
+      if (w < NTILE) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { ev[e] = acc[e]; eo[e] = (trow0 + e) / fx_rpq; epos[e] = w * 256 + lane * 4 + e; }
+        ne = 4;
+      } else if (aux && ac <= C) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ev[e] = ac == C ? ab1[e] : aw[e];
+          eo[e] = ob;
+          epos[e] = (ac == C ? 8 * 256 : 7 * 256) + lane * 4 + e;
+        }
+        ne = 4;
+      }
+      // replicated scalar of this thread: lead's db2 (aux lanes < C) or metric slot (tid < 4)
+      int rpos = -1;
+      float rv = 0.f;
+      if (lead && aux && lane < C) { rpos = 9 * 256 + lane; rv = ab2[0]; }
+      if (lead && tid < 4) { rpos = 9 * 256 + 64 + tid; rv = mval; }
+      // 1. partials to their owners
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (e < ne && eo[e] != R)
+          sys_store1(sys_rsrc(X->part[eo[e]] + ((long)T * TX_MAX_RANKS + R) * pay, tb), epos[e], ev[e]);
+      if (rpos >= 0 && orep != R)
+        sys_store1(sys_rsrc(X->part[orep] + ((long)T * TX_MAX_RANKS + R) * pay, tb), rpos, rv);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid < W && tid != R && owner_of(tid))
+        __hip_atomic_store(X->flag[tid] + (long)T * TX_MAX_RANKS + R, epoch, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      // 2. this rank's owned elements: rank-ordered sums, sharded AdamW, hand-back
+      float pnew[4] = {0.f, 0.f, 0.f, 0.f};
+      if (owner_of(R)) {
+        if (tid < W && tid != R) tx_wait(X->flag[R] + (long)T * TX_MAX_RANKS + tid, epoch, X->timeout, a.ztick + 1);
+        __syncthreads();
+        const float* inbox = X->part[R] + (long)T * TX_MAX_RANKS * pay;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (e >= ne || eo[e] != R) continue;
+          float sacc = 0.f;
+          for (int q = 0; q < W; ++q) {
+            const float x = q == R ? ev[e] : sys_load1(sys_rsrc(inbox + (long)q * pay, tb), epos[e]);
+            sacc = q == 0 ? x : sacc + x;
+          }
+          ev[e] = sacc;
+        }
+        if (rpos >= 0 && orep == R) {
+          float sacc = 0.f;
+          for (int q = 0; q < W; ++q) {
+            const float x = q == R ? rv : sys_load1(sys_rsrc(inbox + (long)q * pay, tb), rpos);
+            sacc = q == 0 ? x : sacc + x;
+          }
+          rv = sacc;
+        }
+        // sharded AdamW on the owned elements (state prefetched at local indices in phase 0)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (e >= ne || eo[e] != R) continue;
+          if (w < NTILE) {
+            const long li = (long)(trow0 + e - R * fx_rpq) * H + tcol;
+            float tp, tm = om[e], tv = ov[e];
+            adam_apply(op[e], om[e], ov[e], ev[e], ak, &tp, &tm, &tv);
+            a.pW1[li] = tp; a.mW1[li] = tm; a.vW1[li] = tv;
+            pnew[e] = tp;
+          } else {
+            const int n = (lane >> 4) * 4 + e;
+            const bool isb = ac == C;
+            const long li = isb ? (long)(j0 + n - R * fx_hpq) : (long)(j0 + n - R * fx_hpq) * C + ac;
+            float tp, tm = om[e], tv = ov[e];
+            adam_apply(op[e], om[e], ov[e], ev[e], ak, &tp, &tm, &tv);
+            (isb ? a.pb1 : a.pW2)[li] = tp; (isb ? a.mb1 : a.mW2)[li] = tm; (isb ? a.vb1 : a.vW2)[li] = tv;
+            pnew[e] = tp;
+          }
+        }
+        for (int q = 0; q < W; ++q) {
+          if (q == R) continue;
+          const __amdgpu_buffer_rsrc_t dst = sys_rsrc(X->red[q] + (long)T * pay, tb);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (e < ne && eo[e] == R) sys_store1(dst, epos[e], pnew[e]);
+          if (rpos >= 0 && orep == R) sys_store1(dst, rpos, rv);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid < W && tid != R)
+          __hip_atomic_store(X->flag[tid] + AG + (long)T * TX_MAX_RANKS + R, epoch, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      // 3. the other owners' updated values
+      if (tid < W && tid != R && owner_of(tid)) tx_wait(X->flag[R] + AG + (long)T * TX_MAX_RANKS + tid, epoch, X->timeout, a.ztick + 1);
+      __syncthreads();
       {
-        if (lead && tid < 4) {
-          float L = 0.f, Cr = 0.f;
-          for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
-          mval = tid == 0 ? L : tid == 2 ? Cr : (float)M;   // {loss sum, n, correct, n}
-        }
-        float4 v4[2];
-        int p4[2], n4 = 0, ps = -1;
-        float vs = 0.f;
-        if (w < NTILE) {
-          v4[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-          p4[0] = w * 256 + lane * 4;
-          n4 = 1;
-          if (lead && tid < 4) { vs = mval; ps = (NTILE + 2) * 256 + 64 + tid; }
-        } else if (aux) {
-          v4[0] = make_float4(aw[0], aw[1], aw[2], aw[3]);
-          v4[1] = make_float4(ab1[0], ab1[1], ab1[2], ab1[3]);
-          p4[0] = NTILE * 256 + lane * 4;
-          p4[1] = (NTILE + 1) * 256 + lane * 4;
-          n4 = 2;
-          if (lead && lane < C) { vs = ab2[0]; ps = (NTILE + 2) * 256 + lane; }
-        }
-        STAMP(12);
-        tx_tile(a.tx, bx * NCH + by, (unsigned)step + 1u, n4, v4, p4, vs, ps, a.ztick + 1);
-        STAMP(13);
-        if (w < NTILE) {
-          acc = (f32x4){v4[0].x, v4[0].y, v4[0].z, v4[0].w};
-          if (lead && tid < 4) mval = vs;
-        } else if (aux) {
-          aw = (f32x4){v4[0].x, v4[0].y, v4[0].z, v4[0].w};
-          ab1 = (f32x4){v4[1].x, v4[1].y, v4[1].z, v4[1].w};
-          if (lead && lane < C) ab2[0] = vs;
-        }
+        const __amdgpu_buffer_rsrc_t src = sys_rsrc(X->red[R] + (long)T * pay, tb);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (e < ne && eo[e] != R) pnew[e] = sys_load1(src, epos[e]);
+        if (rpos >= 0 && orep != R) rv = sys_load1(src, rpos);
       }
-    }
-    if (w < NTILE) {
-      unsigned wt[2] = {0u, 0u};
-  #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const long idx = (long)(trow0 + e) * H + tcol;   // K_IN % KC == 0: always in range
-        if (a.fuse_opt) {
-          float tp, tm = om[e], tv = ov[e];
-          const bf16_t pb = f2bf(adam_apply(op[e], om[e], ov[e], acc[e], ak, &tp, &tm, &tv));
-          if (AHEAD && (a.wt & 1)) {
-            st_f<true>(a.pW1 + idx, tp);
-            if (!ak.sgd) { st_f<true>(a.mW1 + idx, tm); st_f<true>(a.vW1 + idx, tv); }
-          } else {
-            a.pW1[idx] = tp;
-            if (!ak.sgd) { a.mW1[idx] = tm; a.vW1[idx] = tv; }   // SGD: m / v alias p (unused)
-          }
-          // with the W1^T copy, the [in,out] bf16 shadow is rebuilt from it by
-          // FusedMLP2.finalize() instead of being written every step (0.8 MB of HBM writes)
-          if (!a.W1T) a.sW1[idx] = pb;
-          wt[e >> 1] |= (unsigned)pb << (16 * (e & 1));
-        } else if (a.smap) {
-          stage_store(a.smap, par, 0, trow0 + e, tcol, acc[e]);
-        } else {
-          a.gW1[goff + idx] = acc[e];
-        }
-      }
-      // the lane's 4 rows are 4 consecutive K elements of W1^T: one 8-byte store
-      if (a.fuse_opt && a.W1T) {
-        const unsigned long long w8 = (unsigned long long)wt[0] | ((unsigned long long)wt[1] << 32);
-        if (LOOP || (AHEAD && (a.wt & 1))) st_u64<true>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
-        else st_u64<false>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
-      }
-      if constexpr (AHEAD)
+      if (lead && tid < 4) mval = rv;
+      // 4. the whole updated tile: W1^T copy + the next forward's LDS image; W2 / b1 shadows
+      // and hand-offs; b2 (replicated) updated by every rank from the summed gradient
+      if (w < NTILE) {
+        unsigned wt[2] = {0u, 0u};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) wt[e >> 1] |= (unsigned)f2bf(pnew[e]) << (16 * (e & 1));
+        st_u64<true>(a.W1T + (long)tcol * a.ldw1t + trow0, (unsigned long long)wt[0] | ((unsigned long long)wt[1] << 32));
         *reinterpret_cast<uint2*>(&w1n[(lane & 15) * LDW1 + (trow0 - kc0)]) = make_uint2(wt[0], wt[1]);
-    } else if (aux) {
-      bf16_t* sW2n = par ? a.sW2_0 : a.sW2_1;   // next step's parity buffer
-  #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        // lanes ac < C: W2[j0+n][ac]; lane ac == C: b1[j0+n] (every column of ab1 holds
-        // db1, B = ones) -- one AdamW code path for both, its state loaded in phase 0
-        const int n = (lane >> 4) * 4 + e;
-        if (ac <= C) {
-          const bool isb = ac == C;
-          const long o = isb ? (long)(j0 + n) : (long)(j0 + n) * C + ac;
-          const float gr = isb ? ab1[e] : aw[e];
-          if (a.fuse_opt) {
-            const float pn = adam_apply_h<LOOP>(op[e], om[e], ov[e], gr, ak, (isb ? a.pb1 : a.pW2) + o,
-                                                (isb ? a.mb1 : a.mW2) + o, (isb ? a.vb1 : a.vW2) + o);
-            (isb ? a.sb1 : sW2n)[o] = f2bf(pn);
-            if constexpr (AHEAD) a.hand[(isb ? 0 : H) + o] = pn;   // same XCD as the reader (L2)
-          } else if (a.smap) {
-            if (isb) stage_store(a.smap, par, 1, j0 + n, 0, gr);
-            else stage_store(a.smap, par, 2, j0 + n, ac, gr);
-          } else {
-            (isb ? a.gb1 : a.gW2)[goff + o] = gr;
+      } else if (aux) {
+        bf16_t* sW2n = par ? a.sW2_0 : a.sW2_1;   // next step's parity buffer
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int n = (lane >> 4) * 4 + e;
+          if (ac <= C) {
+            const bool isb = ac == C;
+            const long o = isb ? (long)(j0 + n) : (long)(j0 + n) * C + ac;
+            (isb ? a.sb1 : sW2n)[o] = f2bf(pnew[e]);
+            a.hand[(isb ? 0 : H) + o] = pnew[e];
+          }
+        }
+        if (lead && lane < C) {
+          const float pn = adam_apply_h<LOOP>(qp, qm, qv, rv, ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
+          a.sb2[lane] = f2bf(pn);
+          a.hand[H + (long)H * C + lane] = pn;
+        }
+      }
+    } else {
+      // N > 1 (Mlp2Args::tx): this tile's gradients -- and the lead's db2 and metric slots --
+      // all-reduced with the same tile of the other ranks' launches before the optimizer
+      if constexpr (AHEAD && TX) {
+        {
+          if (lead && tid < 4) {
+            float L = 0.f, Cr = 0.f;
+            for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
+            mval = tid == 0 ? L : tid == 2 ? Cr : (float)M;   // {loss sum, n, correct, n}
+          }
+          float4 v4[2];
+          int p4[2], n4 = 0, ps = -1;
+          float vs = 0.f;
+          if (w < NTILE) {
+            v4[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+            p4[0] = w * 256 + lane * 4;
+            n4 = 1;
+            if (lead && tid < 4) { vs = mval; ps = (NTILE + 2) * 256 + 64 + tid; }
+          } else if (aux) {
+            v4[0] = make_float4(aw[0], aw[1], aw[2], aw[3]);
+            v4[1] = make_float4(ab1[0], ab1[1], ab1[2], ab1[3]);
+            p4[0] = NTILE * 256 + lane * 4;
+            p4[1] = (NTILE + 1) * 256 + lane * 4;
+            n4 = 2;
+            if (lead && lane < C) { vs = ab2[0]; ps = (NTILE + 2) * 256 + lane; }
+          }
+          STAMP(12);
+          tx_tile(a.tx, bx * NCH + by, (unsigned)step + 1u, n4, v4, p4, vs, ps, a.ztick + 1);
+          STAMP(13);
+          if (w < NTILE) {
+            acc = (f32x4){v4[0].x, v4[0].y, v4[0].z, v4[0].w};
+            if (lead && tid < 4) mval = vs;
+          } else if (aux) {
+            aw = (f32x4){v4[0].x, v4[0].y, v4[0].z, v4[0].w};
+            ab1 = (f32x4){v4[1].x, v4[1].y, v4[1].z, v4[1].w};
+            if (lead && lane < C) ab2[0] = vs;
           }
         }
       }
-      if (lead && lane < C) {
-        if (a.fuse_opt) {
-          const float pn = adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
-          a.sb2[lane] = f2bf(pn);
-          if constexpr (AHEAD) a.hand[H + (long)H * C + lane] = pn;
-        } else if (a.smap) {
-          stage_store(a.smap, par, 3, lane, 0, ab2[0]);
-        } else {
-          a.gb2[goff + lane] = ab2[0];
+      if (w < NTILE) {
+        unsigned wt[2] = {0u, 0u};
+    #pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const long idx = (long)(trow0 + e) * H + tcol;   // K_IN % KC == 0: always in range
+          if (a.fuse_opt) {
+            float tp, tm = om[e], tv = ov[e];
+            const bf16_t pb = f2bf(adam_apply(op[e], om[e], ov[e], acc[e], ak, &tp, &tm, &tv));
+            if (AHEAD && (a.wt & 1)) {
+              st_f<true>(a.pW1 + idx, tp);
+              if (!ak.sgd) { st_f<true>(a.mW1 + idx, tm); st_f<true>(a.vW1 + idx, tv); }
+            } else {
+              a.pW1[idx] = tp;
+              if (!ak.sgd) { a.mW1[idx] = tm; a.vW1[idx] = tv; }   // SGD: m / v alias p (unused)
+            }
+            // with the W1^T copy, the [in,out] bf16 shadow is rebuilt from it by
+            // FusedMLP2.finalize() instead of being written every step (0.8 MB of HBM writes)
+            if (!a.W1T) a.sW1[idx] = pb;
+            wt[e >> 1] |= (unsigned)pb << (16 * (e & 1));
+          } else if (a.smap) {
+            stage_store(a.smap, par, 0, trow0 + e, tcol, acc[e]);
+          } else {
+            a.gW1[goff + idx] = acc[e];
+          }
+        }
+        // the lane's 4 rows are 4 consecutive K elements of W1^T: one 8-byte store
+        if (a.fuse_opt && a.W1T) {
+          const unsigned long long w8 = (unsigned long long)wt[0] | ((unsigned long long)wt[1] << 32);
+          if (LOOP || (AHEAD && (a.wt & 1))) st_u64<true>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
+          else st_u64<false>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
+        }
+        if constexpr (AHEAD)
+          *reinterpret_cast<uint2*>(&w1n[(lane & 15) * LDW1 + (trow0 - kc0)]) = make_uint2(wt[0], wt[1]);
+      } else if (aux) {
+        bf16_t* sW2n = par ? a.sW2_0 : a.sW2_1;   // next step's parity buffer
+    #pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          // lanes ac < C: W2[j0+n][ac]; lane ac == C: b1[j0+n] (every column of ab1 holds
+          // db1, B = ones) -- one AdamW code path for both, its state loaded in phase 0
+          const int n = (lane >> 4) * 4 + e;
+          if (ac <= C) {
+            const bool isb = ac == C;
+            const long o = isb ? (long)(j0 + n) : (long)(j0 + n) * C + ac;
+            const float gr = isb ? ab1[e] : aw[e];
+            if (a.fuse_opt) {
+              const float pn = adam_apply_h<LOOP>(op[e], om[e], ov[e], gr, ak, (isb ? a.pb1 : a.pW2) + o,
+                                                  (isb ? a.mb1 : a.mW2) + o, (isb ? a.vb1 : a.vW2) + o);
+              (isb ? a.sb1 : sW2n)[o] = f2bf(pn);
+              if constexpr (AHEAD) a.hand[(isb ? 0 : H) + o] = pn;   // same XCD as the reader (L2)
+            } else if (a.smap) {
+              if (isb) stage_store(a.smap, par, 1, j0 + n, 0, gr);
+              else stage_store(a.smap, par, 2, j0 + n, ac, gr);
+            } else {
+              (isb ? a.gb1 : a.gW2)[goff + o] = gr;
+            }
+          }
+        }
+        if (lead && lane < C) {
+          if (a.fuse_opt) {
+            const float pn = adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
+            a.sb2[lane] = f2bf(pn);
+            if constexpr (AHEAD) a.hand[H + (long)H * C + lane] = pn;
+          } else if (a.smap) {
+            stage_store(a.smap, par, 3, lane, 0, ab2[0]);
+          } else {
+            a.gb2[goff + lane] = ab2[0];
+          }
         }
       }
     }
@@ -1196,12 +1365,12 @@ __global__ void __launch_bounds__(NT) mlp2_fwd_kernel(Mlp2Args a) {
   if constexpr (XCD) xcd_contiguous_tile(bx, by);
   mlp2_fwd_body<K_IN, C, RB, DIRECT, false>(static_cast<const Mlp2Args&>(a), bx, by, 0);
 }
-template <int K_IN, int C, int KC, bool XCD, bool AHEAD = false, bool TX = false, bool P3S = false>
+template <int K_IN, int C, int KC, bool XCD, bool AHEAD = false, bool TX = false, bool P3S = false, bool FX = false>
 __global__ void __launch_bounds__(NT) mlp2_bwd_kernel(Mlp2Args a) {
   int bx = blockIdx.x, by = blockIdx.y;
   if constexpr (AHEAD) xcd_column_tile(bx, by);
   else if constexpr (XCD) xcd_contiguous_tile(bx, by);
-  mlp2_bwd_body<K_IN, C, KC, false, AHEAD, TX, P3S>(static_cast<const Mlp2Args&>(a), bx, by, 0);
+  mlp2_bwd_body<K_IN, C, KC, false, AHEAD, TX, P3S, FX>(static_cast<const Mlp2Args&>(a), bx, by, 0);
 }
 
 // n complete training steps in ONE launch (single GPU, fused AdamW, W1^T copy):
@@ -1432,7 +1601,9 @@ JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* str
         a.H % 128)
       return -3;
     const dim3 g(a.H / 16, 784 / 112);
-    if (a.tx) hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true, true, true>), g, dim3(NT), 0, st, a);
+    if (a.tx && a.tx_fsdp)
+      hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true, true, true, false, true>), g, dim3(NT), 0, st, a);
+    else if (a.tx) hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true, true, true>), g, dim3(NT), 0, st, a);
     else if (g_mlp2_p3s) hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true, true, false, true>), g, dim3(NT), 0, st, a);
     else hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true, true>), g, dim3(NT), 0, st, a);
   }

@@ -461,6 +461,42 @@ class FSDPTrainer:
         self._plan = None
         self._full_fresh = False
 
+    @property
+    def one_launch(self) -> bool:
+        """N > 1 step as one run-ahead launch with the in-kernel sharded exchange."""
+        return getattr(self.fused, "fsdp_tx", False)
+
+    def _tile_exchange(self, batch: Batch):
+        """(TileExchange, ranks sharing this GPU) for the one-launch N > 1 FSDP step, or
+        (None, 1): the 2-layer classifier on the fused engine, AdamW, the reference's
+        dim-0 shards of W1 / b1 / W2 with whole 16-unit column blocks per rank (b2
+        replicated), not deterministic, every rank's grid co-resident with the grids of the
+        ranks sharing its GPU -- agreed by all ranks (collective).  JDT_FSDP_AHEAD=0: the
+        forward / backward / fused FSDP collective step."""
+        if not (self.world > 1 and batch.inputs.is_cuda and os.environ.get("JDT_FSDP_AHEAD", "1") == "1"):
+            return None, 1
+        from ..comm import tile_exchange as TX
+        from ..runtime.dist import ranks_per_gpu
+        from ..utils.train_state import AdamW
+        from .fused_mlp import deterministic, supported
+
+        sp, W, dev = self.sp, self.world, batch.inputs.device
+        share = ranks_per_gpu()
+        dims = {n: sp.part[n].shard_dim for n in sp.part}
+        want = {"input_dense/kernel": 0, "input_dense/bias": 0, "output_dense/kernel": 0, "output_dense/bias": None}
+        H = self.model.dims[1] if len(getattr(self.model, "dims", ())) == 3 else 0
+        local = (supported(self.model, batch.size, dev) and dims == want and isinstance(self.state.tx, AdamW)
+                 and not deterministic() and 784 % W == 0 and H % (16 * W) == 0
+                 and TX.ahead_tx_ok(batch.size, H, share))
+        if not TX.agree(self.mesh.group(self.cfg.axis), local, dev):
+            return None, 1
+        old = getattr(self, "_txx", None)
+        if old is not None:
+            torch.cuda.synchronize(dev)
+            old.close()
+        self._txx = TX.create_for(self.mesh, self.cfg.axis, dev, tiles=(H // 16) * (784 // 112))
+        return self._txx, share
+
     def _fsdp_plan(self):
         """Arguments of the fused FSDP step collective (comm/xgmi.py ``fsdp_plan``), or
         None when it does not apply: every sharded leaf must move on the segmented xGMI
@@ -534,9 +570,18 @@ class FSDPTrainer:
                 self.fused = make_engine(self.state, self.mesh, self.cfg.axis, self.cfg.num_minibatches,
                                          batch.size, self.metrics, batch.inputs.device)
             else:
-                self.fused = make_engine(self.state, self.mesh, self.cfg.axis, self.cfg.num_minibatches,
-                                         batch.size, self.metrics, batch.inputs.device, params=sp.full,
-                                         mslot=sp.local.metrics_slot, fuse_opt=False)
+                tx, share = self._tile_exchange(batch)
+                if tx is not None:
+                    # ONE launch per step: each tile's partial gradients go to their rows'
+                    # owners, which apply the sharded AdamW and hand the updated values back
+                    # (csrc/mlp_fused.hip FX); no separate collective
+                    self.fused = make_engine(self.state, self.mesh, self.cfg.axis, self.cfg.num_minibatches,
+                                             batch.size, self.metrics, batch.inputs.device, params=sp.full,
+                                             fuse_opt=True, tx=tx, ranks_on_gpu=share, opt_params=sp.local)
+                else:
+                    self.fused = make_engine(self.state, self.mesh, self.cfg.axis, self.cfg.num_minibatches,
+                                             batch.size, self.metrics, batch.inputs.device, params=sp.full,
+                                             mslot=sp.local.metrics_slot, fuse_opt=False)
             if self.fused is None:
                 self.cfg.fused_kernels = False
                 return False
@@ -546,6 +591,12 @@ class FSDPTrainer:
                 self.state.tx.update(sp.local, self.state.opt_state, 1.0 / self.cfg.num_minibatches, zero_grad=False)
                 with named_scope("synch_metrics"):
                     K.metrics_fold_(self.metrics, sp.local.metrics_slot)
+            return True
+        if self.one_launch:
+            if not self._full_fresh:
+                sp.gather()
+                self._full_fresh = True
+            self.fused.forward_backward(batch)   # the run-ahead launch with the in-kernel exchange
             return True
         plan = self._fsdp_plan()
         if plan is not None:
@@ -618,7 +669,7 @@ class FSDPTrainer:
         # step (the DP engine's schedule, fused_mlp.AheadGraphs)
         eng = self.fused
         self._ahead = None
-        if self._n1 and eng is not None and getattr(eng, "ahead_ok", False):
+        if (self._n1 or self.one_launch) and eng is not None and getattr(eng, "ahead_ok", False):
             from .fused_mlp import AheadGraphs
 
             self._ahead = AheadGraphs(eng, batch, steps_per_graph, pool=g.pool())
@@ -728,8 +779,12 @@ class FSDPTrainer:
             K.metrics_fold_(self.metrics, sp.local.metrics_slot)
 
     def finalize(self):
-        if self.fused is not None and self._n1:
+        if self.fused is not None and (self._n1 or self.one_launch):
             self.fused.finalize()  # bf16 shadow parity of the in-epilogue AdamW
+        if self.one_launch:
+            # the owners updated the local fp32 masters in-kernel; their bf16 local shards
+            # (what a later gather() moves) are refreshed from them
+            self.sp.local.sync_shadow()
         if self.sp.xg is not None:
             self.sp.xg.raise_if_error()
 

@@ -42,7 +42,7 @@ class Mlp2Args(ctypes.Structure):
                 ("step_copy", c_void_p), ("W2snap", c_void_p), ("stage_stride", ctypes.c_long),
                 ("det_logits", c_void_p),
                 ("XR", c_void_p), ("zslab", c_void_p), ("ztick", c_void_p), ("hand", c_void_p), ("lg3", c_int),
-                ("opt_sgd", c_int), ("smap", c_void_p), ("wt", c_int), ("tx", c_void_p)]
+                ("opt_sgd", c_int), ("smap", c_void_p), ("wt", c_int), ("tx", c_void_p), ("tx_fsdp", c_int)]
 
 
 class StageLeaf(ctypes.Structure):
@@ -129,13 +129,17 @@ class FusedMLP2:
 
     def __init__(self, state, mesh, axis: str, num_minibatches: int, rows: int, metrics: torch.Tensor,
                  params=None, mslot: Optional[torch.Tensor] = None, fuse_opt: Optional[bool] = None,
-                 tx=None, ranks_on_gpu: int = 1):
+                 tx=None, ranks_on_gpu: int = 1, opt_params=None):
         """``tx`` (comm.tile_exchange.TileExchange, N > 1): every step is ONE run-ahead
         launch whose tiles all-reduce their gradients with the other ranks' launches
         before the fused optimizer (``ranks_on_gpu``: ranks sharing this GPU, for the
-        co-residency check)."""
+        co-residency check).  ``opt_params`` (FSDP, with ``tx``): the rank's LOCAL shard
+        buffer holding the fp32 masters the sharded AdamW updates (``params`` is then the
+        gathered full buffer whose bf16 shadow the kernels read and write)."""
         P = params if params is not None else state.params
         self.tx = tx
+        self.fsdp_tx = tx is not None and opt_params is not None
+        self.OP = opt_params if opt_params is not None else P
         self.P = P
         self.mslot = mslot if mslot is not None else P.metrics_slot
         self.state, self.mesh, self.axis = state, mesh, axis
@@ -163,7 +167,8 @@ class FusedMLP2:
         # optimizer runs mode 0 (plain-stored grads) + its own kernel
         # (JDT_FUSED_SGD=0: SGD through mode 0 + the standalone SGD kernel, for A/B)
         self.opt_sgd = _is_plain_sgd(state.tx) and os.environ.get("JDT_FUSED_SGD", "1") == "1"
-        self.fuse_opt = bool(fuse_opt) and params is None and (_is_adamw(state.tx) or self.opt_sgd)
+        self.fuse_opt = (bool(fuse_opt) and (params is None or self.fsdp_tx)
+                         and (_is_adamw(state.tx) or (self.opt_sgd and not self.fsdp_tx)))
         # K-contiguous bf16 operand copies (zero K padding): X^T written by mlp2_fwd for
         # mlp2_bwd; W1^T written by mlp2_bwd's AdamW epilogue for the next mlp2_fwd
         self.Mp = (rows + 31) // 32 * 32
@@ -280,8 +285,10 @@ class FusedMLP2:
             a.det_logits = self.det_logits.data_ptr()
         tx = st.tx
         if self.fuse_opt:
-            off = {n: P.offsets[n][0] for n in names}
-            a.pW1, a.pb1, a.pW2, a.pb2 = (P.p(n).data_ptr() for n in names)
+            OP = self.OP   # the optimizer's masters (FSDP one-launch: this rank's local shards)
+            off = {n: OP.offsets[n][0] for n in names}
+            a.pW1, a.pb1, a.pW2, a.pb2 = (OP.p(n).data_ptr() for n in names)
+            a.tx_fsdp = int(self.fsdp_tx)
             if self.opt_sgd:   # no moment buffers: m / v alias p (the kernel neither uses nor writes them)
                 a.mW1, a.mb1, a.mW2, a.mb2 = a.pW1, a.pb1, a.pW2, a.pb2
                 a.vW1, a.vb1, a.vW2, a.vb2 = a.pW1, a.pb1, a.pW2, a.pb2
@@ -765,14 +772,14 @@ class FusedMLPDeep:
 
 def make_engine(state, mesh, axis: str, num_minibatches: int, rows: int, metrics: torch.Tensor, device,
                 params=None, mslot: Optional[torch.Tensor] = None, fuse_opt: Optional[bool] = None,
-                tx=None, ranks_on_gpu: int = 1):
+                tx=None, ranks_on_gpu: int = 1, opt_params=None):
     """The whole-step fused engine for ``state.apply_fn`` (2-layer or deep), or None
     if the model/shape is outside the fused kernels' envelope.  ``tx``: the 2-layer
-    engine's one-launch N > 1 step (FusedMLP2)."""
+    engine's one-launch N > 1 step (FusedMLP2; ``opt_params``: FSDP's local shards)."""
     model = state.apply_fn
     if supported(model, rows, device):
         return FusedMLP2(state, mesh, axis, num_minibatches, rows, metrics, params=params, mslot=mslot,
-                         fuse_opt=fuse_opt, tx=tx, ranks_on_gpu=ranks_on_gpu)
+                         fuse_opt=fuse_opt, tx=tx, ranks_on_gpu=ranks_on_gpu, opt_params=opt_params)
     if supported_deep(model, rows, device):
         return FusedMLPDeep(state, mesh, axis, num_minibatches, rows, metrics, params=params, mslot=mslot,
                             fuse_opt=fuse_opt, tx=tx, ranks_on_gpu=ranks_on_gpu)

@@ -116,6 +116,9 @@ def test_fsdp_over_xgmi_matches_single_device(tmp_path, ws, fused, num_layers, e
     res = _load(tmp_path, f"fsx{num_layers}", ws)
     assert all(o["comm"] == "xgmi" for o in res)
     assert all(o["fused_comm"] == fused for o in res)
+    # 2-layer, fused, 2 ranks: one launch per step (the in-kernel sharded tile exchange:
+    # partials to their rows' owners, sharded AdamW, updated values handed back)
+    assert all(o["one_launch"] == (fused and num_layers == 2 and ws == 2) for o in res), [o["one_launch"] for o in res]
     # every sharded leaf rides the segmented kernels (dim-0 and, 4-layer, dim-1 shards)
     assert set(res[0]["xg_names"]) == {n for n, d in res[0]["dims"].items() if d is not None}
     if num_layers == 4:

@@ -237,7 +237,8 @@ def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2, eps=1e-8):
     _save(outdir, f"fsx{num_layers}", {"local": {n: sp.local.p(n).cpu() for n in sp.part},
                           "dims": {n: sp.part[n].shard_dim for n in sp.part},
                           "metrics": tr.metrics.cpu(), "comm": tr.comm_backend, "xg_names": list(sp._xg_names),
-                          "fused_comm": getattr(tr, "_plan", None) is not None})
+                          "fused_comm": getattr(tr, "_plan", None) is not None or tr.one_launch,
+                          "one_launch": bool(tr.one_launch)})
 
 
 def pp_xgmi(outdir, dp, n_hidden=3, steps=4):

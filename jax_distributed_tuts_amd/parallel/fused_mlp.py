@@ -399,7 +399,7 @@ class FusedMLP2:
             raise RuntimeError("mlp2_bwd run-ahead: tile map, column barrier or tile exchange failed (error "
                                f"word {int(self.ztick[1].item())}: 1 tile map, 2 column barrier, 4 exchange "
                                "timeout); results invalid")
-        P = self.state.params
+        P = self.P   # the buffer whose bf16 shadow the kernels read (FSDP: the gathered full one)
         if self.fuse_opt and int(self.state.opt_state["count"].item()) % 2 == 1:
             P.s("output_dense/kernel").copy_(self.W2s1)
         if self.W1T is not None:

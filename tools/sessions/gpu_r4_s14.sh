@@ -4,7 +4,7 @@
 # grad-scale probes, then shared-GPU FSDP2 A/B (JDT_FSDP_AHEAD 1 / 0) next to DP2.
 cd /root/repo && export TMPDIR=/tmp PYTHONUNBUFFERED=1 && mkdir -p gpurun_out/s14
 timeout -k 10 700 python -u -m pytest tests/test_xgmi_gpu.py tests/test_grad_scale_gpu.py -m gpu -v --timeout 240 \
-  --timeout-method thread -k "fsdp or dp_over or tile_exchange" > gpurun_out/s14/pytest.log 2>&1
+  --timeout-method thread -k "fsdp" > gpurun_out/s14/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "PASSED|FAILED|ERROR|SKIPPED" gpurun_out/s14/pytest.log | tail -30
 [ $rc -ne 0 ] && { grep -E "Error|assert|timed out|error word" gpurun_out/s14/pytest.log | head -30; exit $rc; }
 js() { grep '^{' $1 | python -c 'import json,sys; j=json.loads(sys.stdin.read()); c=j["config"]; print(j["value"], j["ms_per_step"], c.get("step_launches", ""))'; }

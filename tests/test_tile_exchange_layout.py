@@ -50,3 +50,34 @@ def test_tile_counts_match_the_grids():
     bases = [eng.tx_base(i) for i in range(3)]
     assert bases == [0, 224, 480]
     assert SELFTEST_TILES <= 32 * 7
+
+
+@pytest.mark.parametrize("W", [2, 4, 8])
+def test_fsdp_ownership_covers_every_element_once(W):
+    """The FSDP one-launch exchange (mlp_fused.hip mlp2_bwd FX): for every tile, the owner
+    set the kernel waits on (owner_of) contains every element's owner, every owner's local
+    state index lies inside its shard, and over all tiles each W1 / W2 / b1 element is
+    updated by exactly one rank -- the reference's dim-0 shards."""
+    H, KC, NCH, NB = 512, 112, 7, 32
+    rpq, hpq = 784 // W, H // W
+    seen_w1 = [[0] * H for _ in range(784)]
+    seen_h = [0] * H
+    for bx in range(NB):
+        j0 = bx * 16
+        for by in range(NCH):
+            T = bx * NCH + by
+            kc0 = by * KC
+            o_lo, o_hi, ob, orep = kc0 // rpq, (kc0 + KC - 1) // rpq, j0 // hpq, T % W
+            owners = {q for q in range(W) if o_lo <= q <= o_hi or (by == 0 and q == ob) or q == orep}
+            for r in range(kc0, kc0 + KC):
+                o = r // rpq
+                assert o in owners and 0 <= r - o * rpq < rpq
+                for c in range(j0, j0 + 16):
+                    seen_w1[r][c] += 1
+            if by == 0:
+                for n in range(16):
+                    assert ob in owners and 0 <= j0 + n - ob * hpq < hpq
+                    seen_h[j0 + n] += 1
+            assert orep in owners
+    assert all(v == 1 for row in seen_w1 for v in row)
+    assert all(v == 1 for v in seen_h)

@@ -187,6 +187,23 @@ def comm_check(tr, where: str):
         raise RuntimeError(f"[{where}] xgmi pipeline receive timed out on this rank")
 
 
+def one_launch_failed(tr, dev) -> bool:
+    """True on EVERY rank when the one-launch N > 1 step (parallel/dp.py, fsdp.py
+    one_launch: the run-ahead backward's in-kernel tile exchange) reported an error on
+    any rank during the eager steps (synchronises; all ranks call it)."""
+    eng = getattr(tr, "fused", None)
+    tx = getattr(eng, "tx", None)
+    bad = 0
+    if tx is not None:
+        zt = getattr(eng, "ztick", None)
+        bad = int(tx.error() != 0 or (zt is not None and int(zt[1].item()) != 0))
+        # rehearsal hook (tests/test_bench_fallback_gpu.py): this rank reports a failure
+        bad |= int(os.environ.get("JDT_BENCH_FAKE_TX_ERROR", "-1") == str(D.rank()))
+    t = torch.tensor([bad], dtype=torch.int32, device=dev if D.backend() == "nccl" else "cpu")
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return bool(t.item())
+
+
 def pick_steps_per_graph(steps: int, cap: int) -> int:
     """Steps per captured graph: all of them when steps <= cap (one replay, one host
     launch for the whole timed region), else the largest divisor of steps <= cap
@@ -253,6 +270,15 @@ def main():
     for _ in range(n_eager):
         tr.step(batch)
     sync()
+    if ws > 1 and on_gpu and one_launch_failed(tr, dev):
+        # the in-kernel tile exchange passed its start-up self-test but a step's wait timed
+        # out on some rank: every rank rebuilds (fresh init) on the three-launch step
+        os.environ["JDT_DP_AHEAD"] = os.environ["JDT_FSDP_AHEAD"] = "0"
+        tr, batch, desc = build(args, dev)
+        desc["one_launch_fallback"] = "tile exchange wait timed out in the eager steps; three-launch step"
+        for _ in range(n_eager):
+            tr.step(batch)
+        sync()
     # DP always captures its step; FSDP and PP when their collectives / stage hand-offs
     # are xGMI kernels (or N=1)
     use_graph = on_gpu and not args.no_graph and (args.strategy == "dp" or tr.capturable)

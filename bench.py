@@ -361,7 +361,7 @@ def main():
                "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 5), "higher_is_better": True,
                "scaling": "strong", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (N(0,1) inputs, "
                "uniform int labels; random init)", "config": desc,
-               "details": {"p50_ms": p50, "p90_ms": p90, "hipgraph": use_graph,
+               "details": {"p50_ms": p50, "p90_ms": p90, "hipgraph": use_graph, "host_sync": D.host_sync_mode(),
                            "steps_per_graph": (tr.multi[0] if getattr(tr, "multi", None) else 1) if use_graph else 0,
                            "samples_per_s":
                            round(sps * desc["global_batch"], 1), "final_loss": float(m[0] / max(m[1], 1)),

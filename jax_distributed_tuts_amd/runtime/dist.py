@@ -66,6 +66,7 @@ def init(backend: Optional[str] = None, timeout_s: float = 600.0) -> torch.devic
     if use_gpu:
         dev = torch.device("cuda", local_rank() % max(1, torch.cuda.device_count()))
         torch.cuda.set_device(dev)
+        _host_sync_mode()
     else:
         dev = torch.device("cpu")
     _STATE["device"] = dev
@@ -79,6 +80,28 @@ def init(backend: Optional[str] = None, timeout_s: float = 600.0) -> torch.devic
         dist.init_process_group(**kw)
         _STATE["backend"] = be
     return dev
+
+
+def _host_sync_mode():
+    """JDT_SYNC_SPIN=1: host waits on this device (torch.cuda.synchronize, event
+    waits) spin instead of sleeping until an interrupt (hipDeviceScheduleSpin on the
+    current device), so a short timed region's closing synchronize returns as soon as
+    the last kernel completes.  Recorded in _STATE["host_sync"]."""
+    _STATE["host_sync"] = "auto"
+    if os.environ.get("JDT_SYNC_SPIN", "0") != "1":
+        return
+    import ctypes
+
+    try:
+        hip = ctypes.CDLL("libamdhip64.so.7")   # the runtime torch already loaded (same soname)
+        rc = hip.hipSetDeviceFlags(ctypes.c_uint(1))   # hipDeviceScheduleSpin
+    except OSError:
+        rc = -1
+    _STATE["host_sync"] = "spin" if rc == 0 else f"auto (hipSetDeviceFlags rc {rc})"
+
+
+def host_sync_mode() -> str:
+    return str(_STATE.get("host_sync", "auto"))
 
 
 def backend() -> Optional[str]:

@@ -306,6 +306,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t sys_rsrc(const void* base, uns
   const int n = bytes >= 0x7fffffffull ? 0x7fffffff : (int)bytes;
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, n, 0x00020000);
 }
+// The same for a base the caller knows to be wave-uniform: readfirstlane pins the whole
+// resource in SGPRs.  A base that merely IS uniform can still reach the resource as a
+// "divergent" value (a phi after a lane-dependent branch), and a buffer access through
+// a VGPR resource compiles into a readfirstlane waterfall loop per instruction.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sys_rsrc_u(const void* base, unsigned long long bytes) {
+  const int n = bytes >= 0x7fffffffull ? 0x7fffffff : (int)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(sgpr_ptr(const_cast<void*>(base)), (short)0,
+                                           __builtin_amdgcn_readfirstlane(n), 0x00020000);
+}
 __device__ __forceinline__ float4 sys_load4(__amdgpu_buffer_rsrc_t r, long float_off) {
   const sys_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(float_off * 4), 0, CPOL_SYS);
   return __builtin_bit_cast(float4, v);
@@ -364,11 +373,16 @@ __device__ __forceinline__ bool tx_wait(const unsigned* f, unsigned epoch, long 
 
 __device__ __forceinline__ void tx_tile(const TxArgs* X, int T, unsigned epoch, int n4, float4 (&v4)[2],
                                         const int (&p4)[2], float& vs, int ps, unsigned* err) {
-  const int R = X->rank, W = X->world, own = T % W, tid = threadIdx.x;
-  const long pay = X->pay, tiles = X->tiles;
+  // TxArgs lives in device memory the kernel also writes, so its fields come back in VGPRs;
+  // readfirstlane makes them (and the peer pointers, sgpr_ptr) scalar -- a buffer resource
+  // built from a VGPR value is a readfirstlane waterfall loop around every access
+  const int R = __builtin_amdgcn_readfirstlane(X->rank), W = __builtin_amdgcn_readfirstlane(X->world);
+  T = __builtin_amdgcn_readfirstlane(T);
+  const int own = T % W, tid = threadIdx.x;
+  const long pay = __builtin_amdgcn_readfirstlane(X->pay), tiles = __builtin_amdgcn_readfirstlane(X->tiles);
   const unsigned long long tb = (unsigned long long)pay * 4ull;
   if (R != own) {
-    const __amdgpu_buffer_rsrc_t dst = sys_rsrc(X->part[own] + ((long)T * TX_MAX_RANKS + R) * pay, tb);
+    const __amdgpu_buffer_rsrc_t dst = sys_rsrc_u(sgpr_ptr(X->part[own]) + ((long)T * TX_MAX_RANKS + R) * pay, tb);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
       if (k < n4) sys_store4(dst, p4[k], v4[k]);
@@ -381,7 +395,7 @@ __device__ __forceinline__ void tx_tile(const TxArgs* X, int T, unsigned epoch, 
       tx_wait(X->flag[R] + tiles * TX_MAX_RANKS + T, epoch, X->timeout, err);
     }
     __syncthreads();
-    const __amdgpu_buffer_rsrc_t src = sys_rsrc(X->red[R] + (long)T * pay, tb);
+    const __amdgpu_buffer_rsrc_t src = sys_rsrc_u(sgpr_ptr(X->red[R]) + (long)T * pay, tb);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
       if (k < n4) v4[k] = sys_load4(src, p4[k]);
@@ -390,7 +404,7 @@ __device__ __forceinline__ void tx_tile(const TxArgs* X, int T, unsigned epoch, 
   }
   if (tid < W && tid != R) tx_wait(X->flag[R] + (long)T * TX_MAX_RANKS + tid, epoch, X->timeout, err);
   __syncthreads();
-  const float* inbox = X->part[R] + (long)T * TX_MAX_RANKS * pay;
+  const float* inbox = sgpr_ptr(X->part[R]) + (long)T * TX_MAX_RANKS * pay;
   // the rank-ordered sum, peers' partials loaded 4 ranks at a time (all 4 in flight)
 #pragma unroll
   for (int k = 0; k < 3; ++k) {   // k = 0, 1: the float4 slots; k = 2: the scalar
@@ -404,7 +418,7 @@ __device__ __forceinline__ void tx_tile(const TxArgs* X, int T, unsigned epoch, 
       for (int u = 0; u < 4; ++u) {
         const int q = g + u;
         if (q < W && q != R) {
-          const __amdgpu_buffer_rsrc_t src = sys_rsrc(inbox + (long)q * pay, tb);
+          const __amdgpu_buffer_rsrc_t src = sys_rsrc_u(inbox + (long)q * pay, tb);
           in[u] = k < 2 ? sys_load4(src, p4[k]) : make_float4(sys_load1(src, ps), 0.f, 0.f, 0.f);
         }
       }
@@ -423,7 +437,7 @@ __device__ __forceinline__ void tx_tile(const TxArgs* X, int T, unsigned epoch, 
 #pragma unroll
   for (int q = 0; q < TX_MAX_RANKS; ++q) {
     if (q >= W || q == R) continue;
-    const __amdgpu_buffer_rsrc_t dst = sys_rsrc(X->red[q] + (long)T * pay, tb);
+    const __amdgpu_buffer_rsrc_t dst = sys_rsrc_u(sgpr_ptr(X->red[q]) + (long)T * pay, tb);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
       if (k < n4) sys_store4(dst, p4[k], v4[k]);

@@ -412,7 +412,10 @@ __global__ void __launch_bounds__(MD_NT) __attribute__((amdgpu_waves_per_eu(WPE)
   constexpr int LDW1 = 128 + 8;
   constexpr int NCH = K_IN / KC;
   __shared__ __attribute__((aligned(16))) bf16_t w1n[AHEAD ? 16 * LDW1 : 8];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // the wave index through readfirstlane: the compiler then knows it is wave-uniform, so
+  // the per-wave buffer resources below (dZ split) stay scalar -- derived from threadIdx it
+  // is a VGPR, and every buffer access through it became a readfirstlane waterfall loop
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int M = a.M, N = a.N, Mp = (M + 31) & ~31;
   int bx = blockIdx.x, by = blockIdx.y;
   if constexpr (AHEAD) xcd_column_tile(bx, by);      // a column block on ONE XCD (common.h)
@@ -769,8 +772,11 @@ __global__ void __launch_bounds__(MD_NT) __attribute__((amdgpu_waves_per_eu(WPE)
       if (TOP && lead && lane < C) ab2[0] = vs;
     }
   }
+  // the step parity as a scalar for the parity-selected store resources (the step was the
+  // first load of the launch and is long back; per lane it made them waterfall loops)
+  const int par_s = __builtin_amdgcn_readfirstlane(par);
   if (w < NTILE) {
-    bf16_t* Wsn = const_cast<bf16_t*>(par ? a.Ws0 : a.Ws1);   // next step's parity of the row-major shadow
+    bf16_t* Wsn = const_cast<bf16_t*>(par_s ? a.Ws0 : a.Ws1);   // next step's parity of the row-major shadow
     const __amdgpu_buffer_rsrc_t wsn_r = __builtin_amdgcn_make_buffer_rsrc(Wsn, (short)0, 0x7fffffff, 0x00020000);
     unsigned wtp[2] = {0u, 0u};
 #pragma unroll
@@ -807,7 +813,7 @@ __global__ void __launch_bounds__(MD_NT) __attribute__((amdgpu_waves_per_eu(WPE)
     if constexpr (AHEAD)
       *reinterpret_cast<uint2*>(&w1n[(lane & 15) * LDW1 + (trow0 - kc0)]) = make_uint2(wtp[0], wtp[1]);
   } else if (aux) {
-    bf16_t* Whn = const_cast<bf16_t*>(par ? a.Wh0 : a.Wh1);
+    bf16_t* Whn = const_cast<bf16_t*>(par_s ? a.Wh0 : a.Wh1);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int n = (lane >> 4) * 4 + e;

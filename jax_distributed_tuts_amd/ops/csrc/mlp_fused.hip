@@ -685,9 +685,10 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   // blocks, W2 / b1 rows in H / W blocks); other ranks' elements read a clamped index
   int fx_R = 0, fx_rpq = 1, fx_hpq = 1;
   if constexpr (FX) {
-    fx_R = a.tx->rank;
-    fx_rpq = 784 / a.tx->world;
-    fx_hpq = H / a.tx->world;
+    fx_R = __builtin_amdgcn_readfirstlane(a.tx->rank);   // scalar (common.h tx_tile)
+    const int fx_W = __builtin_amdgcn_readfirstlane(a.tx->world);
+    fx_rpq = 784 / fx_W;
+    fx_hpq = H / fx_W;
   }
   float op[4], om[4], ov[4];
 #pragma unroll
@@ -953,9 +954,9 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
       // are summed by rank T % W and pushed back as sums (every rank updates its own copy).
       // Then every rank holds the whole updated tile and runs the next forward from it.
       const TxArgs* X = a.tx;
-      const int R = fx_R, W = X->world;
+      const int R = fx_R, W = __builtin_amdgcn_readfirstlane(X->world);
       const int T = bx * NCH + by;
-      const long pay = X->pay, tiles = X->tiles;
+      const long pay = __builtin_amdgcn_readfirstlane(X->pay), tiles = __builtin_amdgcn_readfirstlane(X->tiles);
       const unsigned long long tb = (unsigned long long)pay * 4ull;
       const unsigned epoch = (unsigned)step + 1u;
       const long AG = tiles * TX_MAX_RANKS + tiles;   // flag base of the updated-value hand-back
@@ -994,7 +995,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         if (e < ne && eo[e] != R)
           sys_store1(sys_rsrc(X->part[eo[e]] + ((long)T * TX_MAX_RANKS + R) * pay, tb), epos[e], ev[e]);
       if (rpos >= 0 && orep != R)
-        sys_store1(sys_rsrc(X->part[orep] + ((long)T * TX_MAX_RANKS + R) * pay, tb), rpos, rv);
+        sys_store1(sys_rsrc_u(sgpr_ptr(X->part[orep]) + ((long)T * TX_MAX_RANKS + R) * pay, tb), rpos, rv);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid < W && tid != R && owner_of(tid))
@@ -1005,13 +1006,13 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
       if (owner_of(R)) {
         if (tid < W && tid != R) tx_wait(X->flag[R] + (long)T * TX_MAX_RANKS + tid, epoch, X->timeout, a.ztick + 1);
         __syncthreads();
-        const float* inbox = X->part[R] + (long)T * TX_MAX_RANKS * pay;
+        const float* inbox = sgpr_ptr(X->part[R]) + (long)T * TX_MAX_RANKS * pay;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           if (e >= ne || eo[e] != R) continue;
           float sacc = 0.f;
           for (int q = 0; q < W; ++q) {
-            const float x = q == R ? ev[e] : sys_load1(sys_rsrc(inbox + (long)q * pay, tb), epos[e]);
+            const float x = q == R ? ev[e] : sys_load1(sys_rsrc_u(inbox + (long)q * pay, tb), epos[e]);
             sacc = q == 0 ? x : sacc + x;
           }
           ev[e] = sacc;
@@ -1019,7 +1020,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         if (rpos >= 0 && orep == R) {
           float sacc = 0.f;
           for (int q = 0; q < W; ++q) {
-            const float x = q == R ? rv : sys_load1(sys_rsrc(inbox + (long)q * pay, tb), rpos);
+            const float x = q == R ? rv : sys_load1(sys_rsrc_u(inbox + (long)q * pay, tb), rpos);
             sacc = q == 0 ? x : sacc + x;
           }
           rv = sacc;
@@ -1046,7 +1047,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         }
         for (int q = 0; q < W; ++q) {
           if (q == R) continue;
-          const __amdgpu_buffer_rsrc_t dst = sys_rsrc(X->red[q] + (long)T * pay, tb);
+          const __amdgpu_buffer_rsrc_t dst = sys_rsrc_u(sgpr_ptr(X->red[q]) + (long)T * pay, tb);
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             if (e < ne && eo[e] == R) sys_store1(dst, epos[e], pnew[e]);
@@ -1062,7 +1063,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
       if (tid < W && tid != R && owner_of(tid)) tx_wait(X->flag[R] + AG + (long)T * TX_MAX_RANKS + tid, epoch, X->timeout, a.ztick + 1);
       __syncthreads();
       {
-        const __amdgpu_buffer_rsrc_t src = sys_rsrc(X->red[R] + (long)T * pay, tb);
+        const __amdgpu_buffer_rsrc_t src = sys_rsrc_u(sgpr_ptr(X->red[R]) + (long)T * pay, tb);
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if (e < ne && eo[e] != R) pnew[e] = sys_load1(src, epos[e]);

@@ -61,7 +61,10 @@ struct StageMap {
 
 __device__ __forceinline__ void stage_store(const StageMap* m, int par, int leaf, int row, int col, float v) {
   const StageLeaf L = m->leaf[leaf];
-  float* b = m->base + (long)par * m->half + L.off;
+  // a global (not flat) pointer: a flat store also counts in lgkmcnt, so every later LDS
+  // wait of the producer would wait for these stores' write acknowledgements too
+  __attribute__((address_space(1))) float* b =
+      (__attribute__((address_space(1))) float*)(m->base + (long)par * m->half + L.off);
   if (L.dim == 2) {
     for (int q = 0; q < m->W; ++q) b[(long)q * m->slice + (long)row * L.cols + col] = v;
     return;

@@ -362,11 +362,21 @@ struct TxArgs {
 // values: n4 float4 at payload offsets p4[] and one scalar at ps (ps < 0: none).  Every
 // wait is bounded (s_memrealtime); a timeout sets bit 2 of the error word and the tile
 // goes on with what it has (the host raises on the word).
+// Flags as GLOBAL (address space 1) accesses: through a generic pointer they compile to
+// flat instructions, which count in lgkmcnt as well as vmcnt -- every later LDS wait of
+// the wave would then also wait for the flag store's acknowledgement (over xGMI).
+typedef __attribute__((address_space(1))) unsigned tx_gu32;
+__device__ __forceinline__ unsigned tx_flag_load(const unsigned* f) {
+  return __hip_atomic_load((const tx_gu32*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void tx_flag_store(unsigned* f, unsigned v) {
+  __hip_atomic_store((tx_gu32*)f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ bool tx_wait(const unsigned* f, unsigned epoch, long long timeout, unsigned* err) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+  while ((int)(tx_flag_load(f) - epoch) < 0) {
     if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout) {
-      atomicOr(err, 4u);
+      __hip_atomic_fetch_or((tx_gu32*)err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -393,8 +403,7 @@ __device__ __forceinline__ void tx_tile(const TxArgs* X, int T, unsigned epoch, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its pushes
     __syncthreads();
     if (tid == 0) {
-      __hip_atomic_store(X->flag[own] + (long)T * TX_MAX_RANKS + R, epoch, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
+      tx_flag_store(sgpr_ptr(X->flag[own]) + (long)T * TX_MAX_RANKS + R, epoch);
       tx_wait(X->flag[R] + tiles * TX_MAX_RANKS + T, epoch, X->timeout, err);
     }
     __syncthreads();
@@ -449,7 +458,7 @@ __device__ __forceinline__ void tx_tile(const TxArgs* X, int T, unsigned epoch, 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid < W && tid != R)
-    __hip_atomic_store(X->flag[tid] + tiles * TX_MAX_RANKS + T, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    tx_flag_store(X->flag[tid] + tiles * TX_MAX_RANKS + T, epoch);
 }
 
 

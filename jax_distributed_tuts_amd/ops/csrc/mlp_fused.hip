@@ -999,8 +999,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid < W && tid != R && owner_of(tid))
-        __hip_atomic_store(X->flag[tid] + (long)T * TX_MAX_RANKS + R, epoch, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        tx_flag_store(X->flag[tid] + (long)T * TX_MAX_RANKS + R, epoch);
       // 2. this rank's owned elements: rank-ordered sums, sharded AdamW, hand-back
       float pnew[4] = {0.f, 0.f, 0.f, 0.f};
       if (owner_of(R)) {
@@ -1056,8 +1055,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid < W && tid != R)
-          __hip_atomic_store(X->flag[tid] + AG + (long)T * TX_MAX_RANKS + R, epoch, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
+          tx_flag_store(X->flag[tid] + AG + (long)T * TX_MAX_RANKS + R, epoch);
       }
       // 3. the other owners' updated values
       if (tid < W && tid != R && owner_of(tid)) tx_wait(X->flag[R] + AG + (long)T * TX_MAX_RANKS + tid, epoch, X->timeout, a.ztick + 1);

@@ -989,11 +989,21 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
       float rv = 0.f;
       if (lead && aux && lane < C) { rpos = 9 * 256 + lane; rv = ab2[0]; }
       if (lead && tid < 4) { rpos = 9 * 256 + 64 + tid; rv = mval; }
-      // 1. partials to their owners
+      // 1. partials to their owners: one uniform resource per candidate owner (a W1 chunk's
+      // rows have at most two, o_lo / o_hi; the aux rows one, ob); a lane whose element
+      // belongs elsewhere stores out of range (offset pay: dropped by the bounds check), so
+      // no resource is lane-dependent (that compiled into readfirstlane waterfall loops)
+      {
+        const int cand[3] = {o_lo, o_hi, ob};
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (e < ne && eo[e] != R)
-          sys_store1(sys_rsrc(X->part[eo[e]] + ((long)T * TX_MAX_RANKS + R) * pay, tb), epos[e], ev[e]);
+        for (int ci = 0; ci < 3; ++ci) {
+          const int c = cand[ci];
+          if (c == R || (ci >= 1 && c == cand[0]) || (ci == 2 && c == cand[1]) || (ci == 2 && !chunk0)) continue;
+          const __amdgpu_buffer_rsrc_t rr = sys_rsrc_u(sgpr_ptr(X->part[c]) + ((long)T * TX_MAX_RANKS + R) * pay, tb);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sys_store1(rr, (e < ne && eo[e] == c) ? (long)epos[e] : pay, ev[e]);
+        }
+      }
       if (rpos >= 0 && orep != R)
         sys_store1(sys_rsrc_u(sgpr_ptr(X->part[orep]) + ((long)T * TX_MAX_RANKS + R) * pay, tb), rpos, rv);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -51,7 +51,9 @@ def build_dp(args, dev):
     cfg.model.num_layers = args.num_layers
     mesh = Mesh({"data": D.world_size()})
     model = Classifier.from_config(cfg.model)
-    tx = adamw(cfg.optimizer.learning_rate) if args.optimizer == "adamw" else sgd(cfg.optimizer.learning_rate)
+    eps = getattr(args, "adam_eps", None)   # autotune's validation probes: AdamW(eps = 10)
+    tx = (adamw(cfg.optimizer.learning_rate, **({"eps": eps} if eps else {})) if args.optimizer == "adamw"
+          else sgd(cfg.optimizer.learning_rate))
     state = init_dp(model, tx, cfg.seed, dev, mesh)
     batch = shard_batch(synthetic_batch(cfg, cfg.seed + 1), mesh, "data")
     batch = Batch(batch.inputs.to(dev), batch.labels.to(dev))
@@ -74,7 +76,9 @@ def build_fsdp(args, dev):
     cfg.model.num_layers = args.num_layers
     mesh = Mesh({"data": D.world_size()})
     model = Classifier.from_config(cfg.model)
-    st = init_fsdp(model, adamw(cfg.model.lr), cfg.seed, dev, mesh, "data", cfg.model.min_weight_size)
+    eps = getattr(args, "adam_eps", None)   # autotune's validation probes: AdamW(eps = 10)
+    st = init_fsdp(model, adamw(cfg.model.lr, **({"eps": eps} if eps else {})), cfg.seed, dev, mesh, "data",
+                   cfg.model.min_weight_size)
     batch = shard_batch(synthetic_batch(cfg, cfg.seed + 1), mesh, "data")
     batch = Batch(batch.inputs.to(dev), batch.labels.to(dev))
     once = args.accum != "loop"
@@ -204,6 +208,92 @@ def one_launch_failed(tr, dev) -> bool:
     return bool(t.item())
 
 
+def autotune_candidates(args, ws: int):
+    """[stage candidate lists] for this job (utils/autotune.py).  DP / FSDP: the step forms
+    that only engage with one rank per GPU (or that the shared-GPU rehearsals could not
+    rank) against the plain collective form, validated; PP: GPipe microbatch count, then
+    concurrent stage streams, then the overlapped data-axis sync, timed one stage after
+    the other (coordinate descent)."""
+    from jax_distributed_tuts_amd.utils.autotune import Candidate
+
+    one = lambda tr: bool(getattr(tr, "one_launch", False))   # noqa: E731
+    if args.strategy == "dp" and args.accum == "kernel":
+        if args.num_layers == 2:
+            return [[Candidate("one-launch", {"JDT_DP_AHEAD": "1"}, replicated=True, engaged=one),
+                     Candidate("three-launch", {"JDT_DP_AHEAD": "0"}, reference=True, replicated=True)]]
+        if args.optimizer == "adamw":
+            return [[Candidate("deep-exchange", {"JDT_DP_DEEP_TX": "1"}, replicated=True, engaged=one),
+                     Candidate("collective", {"JDT_DP_DEEP_TX": "0"}, reference=True, replicated=True)]]
+        return []
+    if args.strategy == "fsdp" and args.accum == "kernel" and args.num_layers == 2:
+        return [[Candidate("one-launch", {"JDT_FSDP_AHEAD": "1"}, engaged=one),
+                 Candidate("three-launch", {"JDT_FSDP_AHEAD": "0"}, reference=True)]]
+    if args.strategy == "pp":
+        S = ws // args.dp
+        stages = []
+        if args.microbatches is None and S > 1:
+            rows = (args.lm_batch if args.model == "transformer" else 128) // args.dp
+            ns = [n for n in (2, 4, 8) if rows % n == 0 and (args.model == "transformer" or rows // n >= 4)]
+            stages.append([Candidate(f"microbatches={n}", {}, reference=(n == 2), args={"microbatches": n})
+                           for n in ns])
+        if S > 1:
+            stages.append([Candidate("stage-streams=0", {"JDT_PP_STREAMS": "0"}, reference=True),
+                           Candidate("stage-streams=1", {"JDT_PP_STREAMS": "1"})])
+        if S > 1 and args.dp > 1:
+            stages.append([Candidate("overlap-sync=0", {"JDT_PP_OVERLAP_SYNC": "0"}, reference=True),
+                           Candidate("overlap-sync=1", {"JDT_PP_OVERLAP_SYNC": "1"})])
+        return [st for st in stages if len(st) > 1]
+    return []
+
+
+def run_autotune(args, dev, build, prepare):
+    """(trainer, batch, desc, report) of the fastest valid step form, or (None, None,
+    None, report) when there is nothing to choose (the caller builds as usual)."""
+    import copy
+
+    from jax_distributed_tuts_amd.utils import autotune as AT
+
+    stages = autotune_candidates(args, D.world_size())
+    if not stages:
+        return None, None, None, {"candidates": [], "choice": "default", "reason": "a single step form"}
+    spg = args.steps_per_graph
+    steps = spg * max(1, -(-100 // spg))   # whole multi-step graphs, >= 100 steps per timing
+    log = (lambda m: print(m, file=sys.stderr, flush=True)) if D.rank() == 0 else (lambda m: None)
+    chosen_env, chosen_args, tables = {}, {}, []
+    tr = batch = None
+    for k, cands in enumerate(stages):
+        for c in cands:   # earlier stages' choices carry over
+            c.env = {**chosen_env, **c.env}
+            c.args = {**chosen_args, **c.args}
+
+        def build_one(eps, c):
+            a = copy.copy(args)
+            a.__dict__.update(c.args)
+            a.adam_eps = eps
+            t, b, d = build(a, dev)
+            t.bench_desc = d
+            return t, b
+
+        validate = args.strategy in ("dp", "fsdp")
+        rep, t, b = AT.run(cands, build_one, prepare, dev, validate=validate, steps=steps, log=log)
+        tables.append(rep)
+        chosen_env.update(rep["env"])
+        chosen_args.update(rep.get("args", {}))
+        if k < len(stages) - 1 and t is not None:
+            t.close()
+        else:
+            tr, batch = t, b
+    os.environ.update(chosen_env)
+    args.__dict__.update(chosen_args)
+    report = {"stages": tables, "env": chosen_env, "args": chosen_args}
+    desc = getattr(tr, "bench_desc", None) if tr is not None else None
+    if desc is not None:
+        bad = [r for t_ in tables for r in t_["candidates"] if r.get("valid") is False]
+        if bad and args.strategy in ("dp", "fsdp"):
+            desc["one_launch_fallback"] = "; ".join(f"{r['name']}: {r.get('reason')}" for r in bad)
+    return tr, batch, desc, report
+
+
 def pick_steps_per_graph(steps: int, cap: int) -> int:
     """Steps per captured graph: all of them when steps <= cap (one replay, one host
     launch for the whole timed region), else the largest divisor of steps <= cap
@@ -248,6 +338,10 @@ def main():
                     help="skip the untimed RCCL-vs-xGMI all-reduce sweep reported for N > 1")
     ap.add_argument("--optimizer", choices=["adamw", "sgd"], default="adamw",
                     help="DP: adamw (the reference's optax.adamw) or sgd (the fused SGD kernel)")
+    ap.add_argument("--autotune", choices=["auto", "off"], default="auto",
+                    help="N > 1 on GPUs: validate the step forms (one-launch tile exchange, deep exchange, "
+                         "pipeline schedules) against the plain collective form and time them before the "
+                         "measured region; the timed run uses the fastest valid one (utils/autotune.py)")
     args = ap.parse_args()
     # a native crash (HIP runtime segfault, abort) prints every thread's Python stack
     faulthandler.enable(all_threads=True)
@@ -261,31 +355,46 @@ def main():
     if args.steps_per_graph is None:
         args.steps_per_graph = pick_steps_per_graph(args.steps, 200 if args.strategy == "dp" else 50)
     build = {"dp": build_dp, "fsdp": build_fsdp, "pp": build_pp}[args.strategy]
-    tr, batch, desc = build(args, dev)
     on_gpu = dev.type == "cuda"
     sync = (lambda: torch.cuda.synchronize()) if on_gpu else (lambda: None)
 
-    # warmup: eager steps (library load, allocator), then capture + replays
+    def prepare(tr_, batch_):
+        """Capture the step the way the timed region replays it (DP always; FSDP and PP
+        when their collectives / stage hand-offs are xGMI kernels or N = 1)."""
+        if not (on_gpu and not args.no_graph and (args.strategy == "dp" or tr_.capturable)):
+            return False
+        if args.strategy == "dp":
+            tr_.capture(batch_, capture_collectives=args.capture_collectives, steps_per_graph=args.steps_per_graph)
+        else:
+            tr_.capture(batch_, steps_per_graph=args.steps_per_graph)
+        return True
+
     n_eager = max(1, min(args.warmup, 3))
-    for _ in range(n_eager):
-        tr.step(batch)
-    sync()
-    if ws > 1 and on_gpu and one_launch_failed(tr, dev):
-        # the in-kernel tile exchange passed its start-up self-test but a step's wait timed
-        # out on some rank: every rank rebuilds (fresh init) on the three-launch step
-        os.environ["JDT_DP_AHEAD"] = os.environ["JDT_FSDP_AHEAD"] = "0"
+    tr = autotune = None
+    if ws > 1 and on_gpu and args.autotune != "off":
+        # validate the N > 1 step forms against the plain collective form and time them
+        # (untimed; utils/autotune.py): the timed run uses the fastest valid one
+        tr, batch, desc, autotune = run_autotune(args, dev, build, prepare)
+    if tr is None:
         tr, batch, desc = build(args, dev)
-        desc["one_launch_fallback"] = "tile exchange wait timed out in the eager steps; three-launch step"
+        # warmup: eager steps (library load, allocator), then capture + replays
         for _ in range(n_eager):
             tr.step(batch)
         sync()
-    # DP always captures its step; FSDP and PP when their collectives / stage hand-offs
-    # are xGMI kernels (or N=1)
-    use_graph = on_gpu and not args.no_graph and (args.strategy == "dp" or tr.capturable)
-    if use_graph and args.strategy == "dp":
-        tr.capture(batch, capture_collectives=args.capture_collectives, steps_per_graph=args.steps_per_graph)
-    elif use_graph:
-        tr.capture(batch, steps_per_graph=args.steps_per_graph)
+        if ws > 1 and on_gpu and one_launch_failed(tr, dev):
+            # the in-kernel tile exchange passed its start-up self-test but a step's wait timed
+            # out on some rank: every rank rebuilds (fresh init) on the three-launch step
+            tr.close()
+            os.environ["JDT_DP_AHEAD"] = os.environ["JDT_FSDP_AHEAD"] = "0"
+            tr, batch, desc = build(args, dev)
+            desc["one_launch_fallback"] = "tile exchange wait timed out in the eager steps; three-launch step"
+            for _ in range(n_eager):
+                tr.step(batch)
+            sync()
+        use_graph = prepare(tr, batch)
+    else:
+        use_graph = tr.graph is not None
+        n_eager = 0
 
     def run(n):
         if hasattr(tr, "run_steps"):
@@ -369,7 +478,7 @@ def main():
                            "process_group": D.backend() or "none",
                            "xgmi_selftest": getattr(tr, "xgmi_status", "n/a"),
                            "collective_ms_p50": coll_ms, "comm_sweep": sweep,
-                           "comm_choice": _comm_choice()}}
+                           "comm_choice": _comm_choice(), "autotune": autotune}}
         print(json.dumps(out), flush=True)
     D.shutdown()
 

@@ -181,7 +181,10 @@ def create_for(mesh, axis: str, slot_bytes: int, n_slots: int, device: torch.dev
     n = mesh.axis_size(axis) if mesh is not None else 1
     if mesh is None or not is_initialized() or not requested(mode, n, device):
         return None
-    c = XgmiP2P(mesh.group(axis), mesh.axis_index(axis), n, slot_bytes, n_slots, device)
+    from ..runtime.dist import spin_timeout_s
+
+    c = XgmiP2P(mesh.group(axis), mesh.axis_index(axis), n, slot_bytes, n_slots, device,
+                timeout_s=spin_timeout_s(30.0))
     if not c.ok:
         if mode == "xgmi":
             raise RuntimeError("xgmi p2p requested but unavailable on this node")

@@ -38,7 +38,7 @@ _lib.declare("jdt_tx_create", c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER
 _lib.declare("jdt_tx_open", c_int, [c_void_p, c_void_p, c_longlong])
 _lib.declare("jdt_tx_args", c_void_p, [c_void_p])
 _lib.declare("jdt_tx_close", None, [c_void_p])
-_lib.declare("jdt_mlp2_ahead_tx_ok", c_int, [c_int, c_int, c_int])
+_lib.declare("jdt_mlp2_ahead_tx_ok", c_int, [c_int, c_int, c_int, c_int])
 _lib.declare("jdt_tx_selftest", c_int, [c_void_p, c_int, ctypes.c_uint, c_void_p, c_void_p])
 _lib.declare("jdt_tx_reset", c_int, [c_void_p])
 _lib.declare("jdt_tx_error", ctypes.c_uint, [c_void_p])
@@ -127,16 +127,27 @@ def agree(group, ok: bool, device: torch.device) -> bool:
     return bool(int(t.item()))
 
 
-def ahead_tx_ok(rows: int, hidden: int, ranks_on_this_gpu: int) -> bool:
+def ahead_tx_ok(rows: int, hidden: int, ranks_on_this_gpu: int, k_in: int = 784) -> bool:
     """Whether the one-launch N > 1 step can run here: the run-ahead conditions plus
     every sharing rank's grid resident at once (``ranks_on_this_gpu`` grids per GPU)."""
-    return bool(_lib.lib().jdt_mlp2_ahead_tx_ok(int(rows), int(hidden), int(ranks_on_this_gpu)))
+    return bool(_lib.lib().jdt_mlp2_ahead_tx_ok(int(rows), int(hidden), int(k_in), int(ranks_on_this_gpu)))
 
 
 def deep_tx_ok(rows: int, ranks_on_this_gpu: int) -> bool:
     """The deep (>= 2 hidden layers) engine's exchanging backward launches all resident
     with ``ranks_on_this_gpu`` ranks' grids per GPU (csrc/mlp_deep.hip jdt_md_tx_ok)."""
     return bool(_lib.lib().jdt_md_tx_ok(int(rows), int(ranks_on_this_gpu)))
+
+
+def fx_owner_span(world: int, rows: int = 784, chunk: int = 112) -> int:
+    """Most shard owners any ``chunk``-row W1 input chunk of the FSDP one-launch exchange
+    touches (dim-0 shards of ``rows / world`` rows; chunks start at multiples of ``chunk``).
+    mlp2_bwd's FX partial stores go to the chunk's first and last owner only, so the step
+    is valid only when this is <= 2 (and ``world`` divides ``rows``)."""
+    if world < 1 or rows % world:
+        return 1 << 30
+    rpq = rows // world
+    return max((c0 + chunk - 1) // rpq - c0 // rpq + 1 for c0 in range(0, rows, chunk))
 
 
 def create_for(mesh, axis: str, device: torch.device, tiles: int) -> Optional[TileExchange]:
@@ -147,5 +158,7 @@ def create_for(mesh, axis: str, device: torch.device, tiles: int) -> Optional[Ti
     W = C.axis_size(mesh, axis)
     if W < 2 or device.type != "cuda" or W > 8:
         return None
-    tx = TileExchange(mesh.group(axis), C.axis_index(mesh, axis), W, tiles, device)
+    from ..runtime.dist import spin_timeout_s
+
+    tx = TileExchange(mesh.group(axis), C.axis_index(mesh, axis), W, tiles, device, timeout_s=spin_timeout_s(10.0))
     return tx if tx.ok else None

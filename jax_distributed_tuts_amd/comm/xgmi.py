@@ -887,7 +887,9 @@ def create_for(mesh, axis: str, cap_floats: int, device: torch.device, mode: str
     n = mesh.axis_size(axis) if mesh is not None else 1
     if mesh is None or not is_initialized() or not requested(mode, n, device):
         return None
-    c = XgmiComm(mesh.group(axis), mesh.axis_index(axis), n, cap_floats, device)
+    from ..runtime.dist import spin_timeout_s
+
+    c = XgmiComm(mesh.group(axis), mesh.axis_index(axis), n, cap_floats, device, timeout_s=spin_timeout_s(30.0))
     if not c.ok:
         if mode == "xgmi":
             raise RuntimeError("xgmi collectives requested but unavailable on this node")

@@ -41,6 +41,15 @@ namespace jdt {
 constexpr int NT = 512;  // threads per workgroup (8 waves)
 constexpr int NW = NT / 64;
 
+// Input chunk of one backward workgroup (= the X^T columns one forward hidden block
+// writes) for an input width K_IN: 112 for the tutorial's 784 (7 chunks), 64 for
+// power-of-two widths (1024: 16 chunks).  At most 7 dW1 tiles of 16 rows per chunk
+// (wave 7 is the aux wave: dW2 / db1 / db2), a multiple of 16.
+template <int K_IN>
+constexpr int mlp2_kc() {
+  return K_IN % 112 == 0 ? 112 : (K_IN % 64 == 0 ? 64 : (K_IN % 32 == 0 ? 32 : 16));
+}
+
 struct Mlp2Args {
   int M, H;
   float inv_mb;                     // CE grad scale: 1 / rows per minibatch
@@ -278,7 +287,7 @@ __device__ __forceinline__ void mlp2_fwd_body(AT& a, const int bx, const int by,
   constexpr int KP = KS * 32;
   constexpr int WCH = (K_IN * 2 + NT - 1) / NT;  // 16-byte W1 chunks per thread
   constexpr int MAXT = (KS + NW - 1) / NW;       // k-steps per wave
-  constexpr int XTC = 112;                       // X^T features written per hidden block
+  constexpr int XTC = mlp2_kc<K_IN>();           // X^T features written per hidden block
   constexpr int LDXS = K_IN + 8;                 // padded row of the X image (bf16)
   static_assert(K_IN % XTC == 0 && XTC % 8 == 0 && K_IN % 8 == 0, "X^T chunking");
   // !DIRECT: the W1 column block as loaded, a k-row image [KP][16] (32 bytes per row);
@@ -681,13 +690,13 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   const float* sp = aux ? (w2l ? sgpr_ptr(fo ? a.pW2 : a.gW2) : sgpr_ptr(fo ? a.pb1 : a.gb1)) : sgpr_ptr(fo ? a.pW1 : a.gW1);
   const float* sm = aux ? (w2l ? sgpr_ptr(fo ? a.mW2 : a.gW2) : sgpr_ptr(fo ? a.mb1 : a.gb1)) : sgpr_ptr(fo ? a.mW1 : a.gW1);
   const float* sv = aux ? (w2l ? sgpr_ptr(fo ? a.vW2 : a.gW2) : sgpr_ptr(fo ? a.vb1 : a.gb1)) : sgpr_ptr(fo ? a.vW1 : a.gW1);
-  // FSDP one-launch (FX): the AdamW state is this rank's LOCAL shard (W1 rows in 784 / W
+  // FSDP one-launch (FX): the AdamW state is this rank's LOCAL shard (W1 rows in K_IN / W
   // blocks, W2 / b1 rows in H / W blocks); other ranks' elements read a clamped index
   int fx_R = 0, fx_rpq = 1, fx_hpq = 1;
   if constexpr (FX) {
     fx_R = __builtin_amdgcn_readfirstlane(a.tx->rank);   // scalar (common.h tx_tile)
     const int fx_W = __builtin_amdgcn_readfirstlane(a.tx->world);
-    fx_rpq = 784 / fx_W;
+    fx_rpq = K_IN / fx_W;
     fx_hpq = H / fx_W;
   }
   float op[4], om[4], ov[4];
@@ -947,7 +956,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
       }
     }
     if constexpr (FX) {
-      // FSDP at N > 1 (the reference's dim-0 shards: W1 rows in 784 / W blocks, W2 / b1 rows
+      // FSDP at N > 1 (the reference's dim-0 shards: W1 rows in K_IN / W blocks, W2 / b1 rows
       // in H / W blocks; b2 replicated): every element's partial goes to the rank that owns
       // its row, the owner sums in rank order, applies the SHARDED AdamW (its local state)
       // and pushes the updated fp32 value to every rank; replicated b2 and the metric slots
@@ -1535,33 +1544,51 @@ int xcd_roundrobin_ok(int G) {
 }
 JDT_API int jdt_xcd_roundrobin_ok(int G) { return xcd_roundrobin_ok(G); }
 
-// 1 if the run-ahead backward can run M rows x H hidden units here: its column-block
-// barrier needs every workgroup of the launch resident at once, and its tile map
-// needs round-robin dispatch over 8 XCDs (probed).  Called before capture.
-JDT_API int jdt_mlp2_ahead_ok(int M, int H) {
-  if (H % 128 || M <= 0 || M > 128) return 0;
-  if (!xcd_roundrobin_ok((H / 16) * (784 / 112))) return 0;
+// 1 if the run-ahead backward can run M rows x H hidden units of input width K_IN here:
+// its column-block barrier needs every workgroup of the launch resident at once, its tile
+// map needs round-robin dispatch over 8 XCDs (probed), and the forward's X^T side output
+// one input chunk per hidden block.  Called before capture.
+template <int K_IN>
+static int mlp2_ahead_ok_k(int M, int H, int nshare, bool tx) {
+  constexpr int NCH = K_IN / mlp2_kc<K_IN>();
+  if (H % 128 || M <= 0 || M > 128 || H / 16 < NCH || nshare < 1) return 0;
+  if (!xcd_roundrobin_ok((H / 16) * NCH)) return 0;
   int dev = 0, cus = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, mlp2_bwd_kernel<784, 10, 112, true, true>, NT, 0) != hipSuccess)
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
-  return (H / 16) * (784 / 112) <= cus * per ? 1 : 0;
+  const hipError_t e = tx ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                                &per, mlp2_bwd_kernel<K_IN, 10, mlp2_kc<K_IN>(), true, true, true>, NT, 0)
+                          : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                                &per, mlp2_bwd_kernel<K_IN, 10, mlp2_kc<K_IN>(), true, true>, NT, 0);
+  if (e != hipSuccess) return 0;
+  return (long)nshare * (H / 16) * NCH <= (long)cus * per ? 1 : 0;
+}
+
+// input widths the fused classifier kernels are instantiated for
+static bool mlp2_width_ok(int k_in) { return k_in == 784 || k_in == 1024; }
+
+JDT_API int jdt_mlp2_ahead_ok(int M, int H, int k_in) {
+  if (k_in == 784) return mlp2_ahead_ok_k<784>(M, H, 1, false);
+  if (k_in == 1024) return mlp2_ahead_ok_k<1024>(M, H, 1, false);
+  return 0;
 }
 
 // 1 if the N > 1 run-ahead backward (tile exchange, Mlp2Args::tx) can run here with
 // `nshare` ranks' grids on this GPU (1 = a GPU per rank): every workgroup of every
 // sharing rank's launch must be resident at once -- a tile waits for the same tile of
 // the other ranks' launches, and a column block for its own workgroups.
-JDT_API int jdt_mlp2_ahead_tx_ok(int M, int H, int nshare) {
-  if (!jdt_mlp2_ahead_ok(M, H) || nshare < 1) return 0;
-  int dev = 0, cus = 0, per = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, mlp2_bwd_kernel<784, 10, 112, true, true, true>, NT, 0) !=
-          hipSuccess)
-    return 0;
-  return (long)nshare * (H / 16) * (784 / 112) <= (long)cus * per ? 1 : 0;
+JDT_API int jdt_mlp2_ahead_tx_ok(int M, int H, int k_in, int nshare) {
+  if (!jdt_mlp2_ahead_ok(M, H, k_in)) return 0;
+  if (k_in == 784) return mlp2_ahead_ok_k<784>(M, H, nshare, true);
+  return mlp2_ahead_ok_k<1024>(M, H, nshare, true);
+}
+
+// input chunk (rows of W1 per backward workgroup) for an input width, 0 if unsupported
+JDT_API int jdt_mlp2_chunk(int k_in) {
+  if (k_in == 784) return mlp2_kc<784>();
+  if (k_in == 1024) return mlp2_kc<1024>();
+  return 0;
 }
 
 // The tile exchange's self-test (above): `tiles` workgroups, epoch `epoch`; words[0] gets
@@ -1580,41 +1607,48 @@ static int g_mlp2_p3s = 0;
 JDT_API void jdt_mlp2_set_p3s(int on) { g_mlp2_p3s = on; }
 
 // phase 0: mlp2_fwd, 1: mlp2_bwd, 2: run-ahead mlp2_bwd (backward of t + forward of t+1)
-JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* stream) {
-  const Mlp2Args& a = *args;
-  if (k_in != 784 || c != 10 || a.H % 16 || a.M <= 0 || a.M > 128) return -3;
-  hipStream_t st = static_cast<hipStream_t>(stream);
+template <int K_IN>
+static int mlp2_launch(const Mlp2Args& a, int phase, hipStream_t st) {
+  constexpr int KC = mlp2_kc<K_IN>(), NCH = K_IN / KC;
+  // the forward's X^T / X side outputs: hidden block y < NCH writes input chunk y
+  if (a.H / 16 < NCH) return -3;
   if (phase == 0) {
     const bool direct = a.W1T != nullptr;
+    const bool xf = xcd_tiles_enabled() == 1;
     if (g_mlp2_rb == 32) {
       const dim3 g((a.M + 31) / 32, a.H / 16);
-      const bool xf = xcd_tiles_enabled() == 1;
-      if (direct && xf) hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 32, true, true>), g, dim3(NT), 0, st, a);
-      else if (direct) hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 32, true, false>), g, dim3(NT), 0, st, a);
-      else hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 32, false, false>), g, dim3(NT), 0, st, a);
+      if (direct && xf) hipLaunchKernelGGL((mlp2_fwd_kernel<K_IN, 10, 32, true, true>), g, dim3(NT), 0, st, a);
+      else if (direct) hipLaunchKernelGGL((mlp2_fwd_kernel<K_IN, 10, 32, true, false>), g, dim3(NT), 0, st, a);
+      else hipLaunchKernelGGL((mlp2_fwd_kernel<K_IN, 10, 32, false, false>), g, dim3(NT), 0, st, a);
     } else {
       const dim3 g((a.M + 15) / 16, a.H / 16);
-      const bool xf = xcd_tiles_enabled() == 1;
-      if (direct && xf) hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 16, true, true>), g, dim3(NT), 0, st, a);
-      else if (direct) hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 16, true, false>), g, dim3(NT), 0, st, a);
-      else hipLaunchKernelGGL((mlp2_fwd_kernel<784, 10, 16, false, false>), g, dim3(NT), 0, st, a);
+      if (direct && xf) hipLaunchKernelGGL((mlp2_fwd_kernel<K_IN, 10, 16, true, true>), g, dim3(NT), 0, st, a);
+      else if (direct) hipLaunchKernelGGL((mlp2_fwd_kernel<K_IN, 10, 16, true, false>), g, dim3(NT), 0, st, a);
+      else hipLaunchKernelGGL((mlp2_fwd_kernel<K_IN, 10, 16, false, false>), g, dim3(NT), 0, st, a);
     }
   } else if (phase == 1) {
-    const dim3 g(a.H / 16, 784 / 112);
-    if (xcd_tiles_enabled()) hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true>), g, dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, false>), g, dim3(NT), 0, st, a);
+    const dim3 g(a.H / 16, NCH);
+    if (xcd_tiles_enabled()) hipLaunchKernelGGL((mlp2_bwd_kernel<K_IN, 10, KC, true>), g, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((mlp2_bwd_kernel<K_IN, 10, KC, false>), g, dim3(NT), 0, st, a);
   } else {
     // run-ahead backward: step t's backward + AdamW + step t+1's forward (needs the
     // fused optimizer, the W1^T copy, the X copy written by mlp2_fwd and lg3 logits)
     if (!a.fuse_opt || !a.W1T || !a.XR || !a.zslab || !a.ztick || !a.hand || !a.lg3 || a.det_logits || a.M > 128 ||
         a.H % 128)
       return -3;
-    const dim3 g(a.H / 16, 784 / 112);
+    const dim3 g(a.H / 16, NCH);
     if (a.tx && a.tx_fsdp)
-      hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true, true, true, false, true>), g, dim3(NT), 0, st, a);
-    else if (a.tx) hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true, true, true>), g, dim3(NT), 0, st, a);
-    else if (g_mlp2_p3s) hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true, true, false, true>), g, dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL((mlp2_bwd_kernel<784, 10, 112, true, true>), g, dim3(NT), 0, st, a);
+      hipLaunchKernelGGL((mlp2_bwd_kernel<K_IN, 10, KC, true, true, true, false, true>), g, dim3(NT), 0, st, a);
+    else if (a.tx) hipLaunchKernelGGL((mlp2_bwd_kernel<K_IN, 10, KC, true, true, true>), g, dim3(NT), 0, st, a);
+    else if (g_mlp2_p3s) hipLaunchKernelGGL((mlp2_bwd_kernel<K_IN, 10, KC, true, true, false, true>), g, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((mlp2_bwd_kernel<K_IN, 10, KC, true, true>), g, dim3(NT), 0, st, a);
   }
   return HIP_LAUNCH_CHECK();
+}
+
+JDT_API int jdt_mlp2(const Mlp2Args* args, int phase, int k_in, int c, void* stream) {
+  const Mlp2Args& a = *args;
+  if (!mlp2_width_ok(k_in) || c != 10 || a.H % 16 || a.M <= 0 || a.M > 128) return -3;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  return k_in == 784 ? mlp2_launch<784>(a, phase, st) : mlp2_launch<1024>(a, phase, st);
 }

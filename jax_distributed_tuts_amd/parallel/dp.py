@@ -176,10 +176,15 @@ class DataParallelTrainer:
         share = ranks_per_gpu()
         dev = batch.inputs.device
         if supported(self.model, batch.size, dev):          # 2-layer: one launch per step
-            H = self.model.dims[1]
-            local = (not deterministic() and (_is_adamw(self.state.tx) or _is_plain_sgd(self.state.tx))
-                     and TX.ahead_tx_ok(batch.size, H, share))
-            tiles = (H // 16) * (784 // 112)
+            from .fused_mlp import mlp2_chunk
+
+            K, H = self.model.dims[0], self.model.dims[1]
+            # the engine's own condition for an optimizer fused into the backward epilogue
+            # (JDT_FUSED_SGD=0 keeps SGD out of it: three-launch step)
+            fused_sgd = _is_plain_sgd(self.state.tx) and os.environ.get("JDT_FUSED_SGD", "1") == "1"
+            local = (not deterministic() and (_is_adamw(self.state.tx) or fused_sgd)
+                     and TX.ahead_tx_ok(batch.size, H, share, K))
+            tiles = (H // 16) * (K // mlp2_chunk(K))
         elif supported_deep(self.model, batch.size, dev):   # deep: one launch per hidden layer
             # opt-in (JDT_DP_DEEP_TX=1): measured 4 % SLOWER than md_fwd / md_bwd + the xGMI
             # all-reduce on the shared GPU (profiles/r4_one_launch_dp_ab.txt; its two-ranks-
@@ -519,6 +524,18 @@ class DataParallelTrainer:
             self.fused.finalize()
         if self.xg is not None:
             self.xg.raise_if_error()
+
+    def close(self):
+        """Release the IPC-mapped exchange buffers (tile exchange inboxes, xGMI context)
+        and the captured graphs, so another trainer can be built in this process
+        (bench.py's probes).  Not collective; the trainer is unusable afterwards."""
+        if self.state.params.master.is_cuda:
+            torch.cuda.synchronize(self.state.params.master.device)
+        for r in (getattr(self, "_txx", None), self.xg):
+            if r is not None:
+                r.close()
+        self._txx = self.xg = None
+        self.invalidate()
 
     @property
     def comm_backend(self) -> str:

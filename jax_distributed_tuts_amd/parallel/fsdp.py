@@ -478,23 +478,27 @@ class FSDPTrainer:
         from ..comm import tile_exchange as TX
         from ..runtime.dist import ranks_per_gpu
         from ..utils.train_state import AdamW
-        from .fused_mlp import deterministic, supported
+        from .fused_mlp import deterministic, mlp2_chunk, supported
 
         sp, W, dev = self.sp, self.world, batch.inputs.device
         share = ranks_per_gpu()
         dims = {n: sp.part[n].shard_dim for n in sp.part}
         want = {"input_dense/kernel": 0, "input_dense/bias": 0, "output_dense/kernel": 0, "output_dense/bias": None}
-        H = self.model.dims[1] if len(getattr(self.model, "dims", ())) == 3 else 0
+        two = len(getattr(self.model, "dims", ())) == 3
+        K, H = (self.model.dims[0], self.model.dims[1]) if two else (0, 0)
+        kc = mlp2_chunk(K) if two else 0
+        # the kernel's partial stores reach a W1 chunk's first and last owner only
+        # (tile_exchange.fx_owner_span); W must divide both sharded dims
         local = (supported(self.model, batch.size, dev) and dims == want and isinstance(self.state.tx, AdamW)
-                 and not deterministic() and 784 % W == 0 and H % (16 * W) == 0
-                 and TX.ahead_tx_ok(batch.size, H, share))
+                 and not deterministic() and K % W == 0 and H % (16 * W) == 0
+                 and TX.fx_owner_span(W, K, kc) <= 2 and TX.ahead_tx_ok(batch.size, H, share, K))
         if not TX.agree(self.mesh.group(self.cfg.axis), local, dev):
             return None, 1
         old = getattr(self, "_txx", None)
         if old is not None:
             torch.cuda.synchronize(dev)
             old.close()
-        self._txx = TX.create_for(self.mesh, self.cfg.axis, dev, tiles=(H // 16) * (784 // 112))
+        self._txx = TX.create_for(self.mesh, self.cfg.axis, dev, tiles=(H // 16) * (K // kc))
         return self._txx, share
 
     def _fsdp_plan(self):
@@ -787,6 +791,17 @@ class FSDPTrainer:
             self.sp.local.sync_shadow()
         if self.sp.xg is not None:
             self.sp.xg.raise_if_error()
+
+    def close(self):
+        """Release the IPC-mapped exchange buffers (tile exchange inboxes, the shards' xGMI
+        context) and the captured graphs (see DataParallelTrainer.close)."""
+        if self.sp.local.master.is_cuda:
+            torch.cuda.synchronize(self.sp.local.master.device)
+        for r in (getattr(self, "_txx", None), self.sp.xg):
+            if r is not None:
+                r.close()
+        self._txx = self.sp.xg = None
+        self.invalidate()
 
     def full_params(self) -> Dict[str, torch.Tensor]:
         """Gather the fp32 masters (for checks / checkpoints)."""

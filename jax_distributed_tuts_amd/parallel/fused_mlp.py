@@ -80,7 +80,8 @@ def stage_map_tensor(base: int, half: int, slice_: int, world: int, leaves, devi
 _lib.declare("jdt_mlp2", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_int, c_void_p])
 _lib.declare("jdt_mlp2_set_p3s", None, [c_int])
 _lib.declare("jdt_mlp2_args_size", c_int, [])
-_lib.declare("jdt_mlp2_ahead_ok", c_int, [c_int, c_int])
+_lib.declare("jdt_mlp2_ahead_ok", c_int, [c_int, c_int, c_int])
+_lib.declare("jdt_mlp2_chunk", c_int, [c_int])
 _lib.declare("jdt_mlp2_set_rows", None, [c_int])
 _lib.declare("jdt_mlp2_loop", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_void_p, c_void_p, c_void_p, ctypes.c_longlong,
                                       c_void_p, c_void_p])
@@ -114,12 +115,24 @@ def set_forward_rows(rb: int):
     _lib.lib().jdt_mlp2_set_rows(int(rb))
 
 
+def mlp2_chunk(k_in: int) -> int:
+    """Input rows of W1 per backward workgroup (csrc/mlp_fused.hip mlp2_kc): 112 for the
+    tutorial's 784 inputs, 64 for 1024; 0 for a width the kernels are not built for."""
+    return int(_lib.lib().jdt_mlp2_chunk(int(k_in)))
+
+
 def supported(model, rows: int, device) -> bool:
+    """The 2-layer fused engine's envelope: K_IN in the instantiated widths (784, 1024),
+    10 classes, hidden a multiple of 16 with one hidden block per input chunk (the
+    forward writes X^T chunk y from hidden block y), <= 128 rows, SiLU."""
     from ..models.mlp import MLP
 
-    return (torch.device(device).type == "cuda" and isinstance(model, MLP) and model.L == 2 and model.dims[0] == 784
-            and model.dims[2] == 10 and model.dims[1] % 16 == 0 and 0 < rows <= 128 and model.act == "silu"
-            and not model.final_act)
+    if not (torch.device(device).type == "cuda" and isinstance(model, MLP) and model.L == 2):
+        return False
+    k, h = model.dims[0], model.dims[1]
+    kc = mlp2_chunk(k)
+    return (kc > 0 and model.dims[2] == 10 and h % 16 == 0 and h // 16 >= k // kc and 0 < rows <= 128
+            and model.act == "silu" and not model.final_act)
 
 
 class FusedMLP2:
@@ -149,6 +162,10 @@ class FusedMLP2:
         H = self.model.dims[1]
         dev = P.master.device
         self.rows = rows
+        # input width and its backward chunk (csrc/mlp_fused.hip is instantiated for 784 / 1024)
+        self.K = K = self.model.dims[0]
+        self.kc = mlp2_chunk(K)
+        self.nch = K // self.kc
         # silu'(Z1) * mask / keep in 4-row groups ([Mp/4][H][4] fp32), mlp2_fwd -> mlp2_bwd
         self.G1 = torch.zeros((rows + 31) // 32 * 32 * H, dtype=torch.float32, device=dev)
         # H = dropout(silu(Z1)) bf16, same 4-row group layout as G1
@@ -172,13 +189,14 @@ class FusedMLP2:
         # K-contiguous bf16 operand copies (zero K padding): X^T written by mlp2_fwd for
         # mlp2_bwd; W1^T written by mlp2_bwd's AdamW epilogue for the next mlp2_fwd
         self.Mp = (rows + 31) // 32 * 32
-        self.XT = torch.zeros(784, self.Mp, dtype=torch.bfloat16, device=dev)  # sample tail stays zero
+        self.XT = torch.zeros(K, self.Mp, dtype=torch.bfloat16, device=dev)  # sample tail stays zero
         if os.environ.get("JDT_MLP2_RB"):
             set_forward_rows(int(os.environ["JDT_MLP2_RB"]))
         self.W1T = None
         if self.fuse_opt:
-            self.W1T = torch.zeros(H, 800, dtype=torch.bfloat16, device=dev)
-            self.W1T[:, :784].copy_(P.s("input_dense/kernel").t())
+            self.ldw1t = (K + 31) // 32 * 32   # K padded to whole 32-deep MFMA steps (zero tail)
+            self.W1T = torch.zeros(H, self.ldw1t, dtype=torch.bfloat16, device=dev)
+            self.W1T[:, :K].copy_(P.s("input_dense/kernel").t())
         # persistent n-step kernel (mlp2_loop_kernel): W2 snapshot + barrier words
         # [arrival counter, its base at the next launch, error flag, pad]
         self.W2snap = torch.zeros(H * 10, dtype=torch.float32, device=dev)
@@ -187,7 +205,7 @@ class FusedMLP2:
         # (29.3 vs 16.3 us/step, tools/stamp_loop.py: each 256-workgroup grid barrier
         # costs ~8 us against a 2.4 us kernel boundary), kept as the tested reference
         # design for in-launch sc1 hand-offs.
-        self.loop_ok = (self.fuse_opt and os.environ.get("JDT_MLP2_LOOP", "0") == "1"
+        self.loop_ok = (self.fuse_opt and K == 784 and os.environ.get("JDT_MLP2_LOOP", "0") == "1"
                         and bool(_lib.lib().jdt_mlp2_loop_ok(rows, H)))
         if _lib.lib().jdt_mlp2_args_size() != ctypes.sizeof(Mlp2Args):
             raise RuntimeError("Mlp2Args layout mismatch")
@@ -204,19 +222,19 @@ class FusedMLP2:
         # JDT_MLP2_AHEAD=0 turns it off (A/B)
         self.ahead_ok = (self.fuse_opt and self.det_logits is None and self.W1T is not None
                          and os.environ.get("JDT_MLP2_AHEAD", "1") == "1"
-                         and bool(_lib.lib().jdt_mlp2_ahead_ok(rows, H)))
+                         and bool(_lib.lib().jdt_mlp2_ahead_ok(rows, H, K)))
         if tx is not None:
             from ..comm.tile_exchange import ahead_tx_ok
 
             self.ahead_ok = (self.fuse_opt and self.det_logits is None and self.W1T is not None
-                             and ahead_tx_ok(rows, H, ranks_on_gpu))
+                             and ahead_tx_ok(rows, H, ranks_on_gpu, K))
         self._ahead_args = None
         # host-side: the last launch on this engine was a run-ahead backward (set by
         # run_ahead / DataParallelTrainer after replaying a run-ahead graph)
         self.ahead_primed = False
         if self.ahead_ok:
-            nch = 784 // 112
-            self.XR = torch.zeros(rows, 784, dtype=torch.bfloat16, device=dev)
+            nch = self.nch
+            self.XR = torch.zeros(rows, K, dtype=torch.bfloat16, device=dev)
             self.zslab = torch.zeros(H // 16 * nch * 128 * 16, dtype=torch.float32, device=dev)
             # 128-byte lines: [step ticket, error word (1: tile map, 2: barrier timeout),
             # launch counter], one column-barrier counter line per hidden block, one
@@ -280,7 +298,7 @@ class FusedMLP2:
         a.step_copy = self.step_copy.data_ptr()
         a.W2snap = self.W2snap.data_ptr()
         if self.W1T is not None:
-            a.W1T, a.ldw1t = self.W1T.data_ptr(), 800
+            a.W1T, a.ldw1t = self.W1T.data_ptr(), self.ldw1t
         if self.det_logits is not None:
             a.det_logits = self.det_logits.data_ptr()
         tx = st.tx
@@ -322,8 +340,8 @@ class FusedMLP2:
             self._args, self._key = self._build_args(batch), key
         L = _lib.lib()
         s = _lib.stream_ptr()
-        _lib.check(L.jdt_mlp2(ctypes.byref(self._args), 0, 784, 10, s), "mlp2_fwd")
-        _lib.check(L.jdt_mlp2(ctypes.byref(self._args), 1, 784, 10, s), "mlp2_bwd")
+        _lib.check(L.jdt_mlp2(ctypes.byref(self._args), 0, self.K, 10, s), "mlp2_fwd")
+        _lib.check(L.jdt_mlp2(ctypes.byref(self._args), 1, self.K, 10, s), "mlp2_bwd")
 
     def run_ahead(self, batch, n: int, prologue: bool = True):
         """n complete training steps as n run-ahead backward launches, launch i = step
@@ -350,11 +368,11 @@ class FusedMLP2:
         s = _lib.stream_ptr()
         if prologue:
             self.logits_all.zero_()
-            _lib.check(L.jdt_mlp2(ctypes.byref(self._ahead_args), 0, 784, 10, s), "mlp2_fwd")
+            _lib.check(L.jdt_mlp2(ctypes.byref(self._ahead_args), 0, self.K, 10, s), "mlp2_fwd")
         elif not torch.cuda.is_current_stream_capturing():
             assert self.ahead_primed, "run_ahead(prologue=False) needs a run-ahead launch just before"
         for _ in range(n):
-            _lib.check(L.jdt_mlp2(ctypes.byref(self._ahead_args), 2, 784, 10, s), "mlp2_bwd_ahead")
+            _lib.check(L.jdt_mlp2(ctypes.byref(self._ahead_args), 2, self.K, 10, s), "mlp2_bwd_ahead")
         if not torch.cuda.is_current_stream_capturing():
             self.ahead_primed = True
 
@@ -403,7 +421,7 @@ class FusedMLP2:
         if self.fuse_opt and int(self.state.opt_state["count"].item()) % 2 == 1:
             P.s("output_dense/kernel").copy_(self.W2s1)
         if self.W1T is not None:
-            P.s("input_dense/kernel").copy_(self.W1T[:, :784].t())
+            P.s("input_dense/kernel").copy_(self.W1T[:, :self.K].t())
 
 
 class AheadGraphs:

@@ -830,6 +830,17 @@ class GPipeTrainer:
         if self.xg is not None:
             self.xg.raise_if_error()
 
+    def close(self):
+        """Release the inboxes and the xGMI context and drop the captured graphs, so
+        another trainer can be built in this process (bench.py's autotune candidates)."""
+        if self.dev.type == "cuda":
+            torch.cuda.synchronize(self.dev)
+        for r in (self.p2p, self.xg):
+            if r is not None:
+                r.close()
+        self.p2p = self.xg = None
+        self.graph = self._ahead = self.multi = None
+
     def loss_head(self, logits, labels, dlogits, n_parts: int = 1):
         """CE of ``labels`` (``n_parts`` merged microbatches: every row keeps its
         microbatch's 1/rows weight)."""

@@ -146,6 +146,15 @@ def ranks_per_gpu() -> int:
     return n
 
 
+def spin_timeout_s(base_s: float) -> float:
+    """Wall-clock bound of an in-kernel wait (xGMI barriers, inbox receives, tile
+    exchange) for this job: ``base_s`` with a GPU per rank; with k ranks time-sharing
+    one GPU (rehearsals) a peer's grid may wait for its queue to be scheduled, so the
+    bound grows with k (x k / 2).  Collective on first use (ranks_per_gpu)."""
+    k = ranks_per_gpu()
+    return float(base_s) * max(1.0, k / 2.0)
+
+
 def ranks_share_gpu() -> bool:
     """Two ranks of the job drive the same GPU (ranks_per_gpu() > 1)."""
     return ranks_per_gpu() > 1

@@ -341,13 +341,16 @@ def accum_grads_scan(batch: Batch, state: TrainState, key: int, n_minbatch: int,
             with torch.cuda.graph(g):
                 _body()
             SCAN_STATS["captures"] += 1
-        ent = _SCAN_CACHE.put(ck, {"graph": g, "xin": xin, "yin": yin, "idx": idx, "out": mslot})
+        ent = _SCAN_CACHE.put(ck, {"graph": g, "xin": xin, "yin": yin, "idx": idx, "out": mslot, "body": _body})
         first = 1
     else:
         first = 0
     for i in range(first, n_minbatch):
         _scan_load(batch, ent["xin"], ent["yin"], ent["idx"], i, mb)
-        ent["graph"].replay()
+        if ent["graph"] is None:
+            ent["body"]()   # one minibatch: nothing was captured, the body runs eagerly
+        else:
+            ent["graph"].replay()
         metrics = _metrics_add(metrics, _clone_metrics(ent["out"]["m"]))
     return GradBuffer(state.params, 1.0 / n_minbatch), metrics
 

@@ -513,6 +513,38 @@ def test_transformer_step_gpu_matches_cpu():
     _close(res[DEV][1], res["cpu"][1], rtol=1e-3, atol=1e-2)
 
 
+@pytest.mark.parametrize("width", [(1024, 512), (1024, 256)])
+def test_fused_mlp_input_width_1024(width):
+    """The 2-layer fused engine at input width 1024 (16 backward chunks of 64 rows,
+    csrc/mlp_fused.hip mlp2_kc): eager two-launch steps and captured run-ahead steps
+    (one launch per step) == the generic-kernel path over the same rows."""
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    K, H = width
+    g = torch.Generator().manual_seed(0)
+    b = Batch(torch.randn(128, K, generator=g).to(DEV), torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV))
+    out = {}
+    for accum in ("fused", "kernel"):
+        st = init_dp(Classifier(input_size=K, hidden_size=H), adamw(1e-3), 69, DEV)
+        tr = DataParallelTrainer(st, None, DPConfig(4, accum))
+        for _ in range(2):
+            tr.step(b)
+        tr.capture(b, steps_per_graph=2)
+        tr.run_steps(b, 4)
+        tr.finalize()
+        torch.cuda.synchronize()
+        if accum == "kernel":
+            assert tr.fused is not None and tr.fused.K == K and tr.fused.kc == 64 and tr.fused.ahead_ok
+            assert tr._ahead is not None   # captured as run-ahead launches
+        out[accum] = (st.params.master.clone(), tr.metrics.clone(), int(st.opt_state["count"].item()))
+    assert out["kernel"][2] == out["fused"][2] == 6
+    d = (out["kernel"][0] - out["fused"][0]).abs()
+    assert float(d.max()) <= 2 * 1e-3 * 6 and float((d > 1e-4).float().mean()) < 5e-3, float(d.max())
+    _close(out["kernel"][1], out["fused"][1], rtol=1e-3, atol=5e-2)
+
+
 @pytest.mark.parametrize("fused_opt", ["1", "0"])
 @pytest.mark.parametrize("rows", [128, 32, 16])
 @pytest.mark.parametrize("layers", [2, 3, 4])

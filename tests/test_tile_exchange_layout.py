@@ -68,6 +68,8 @@ def test_fsdp_ownership_covers_every_element_once(W):
             T = bx * NCH + by
             kc0 = by * KC
             o_lo, o_hi, ob, orep = kc0 // rpq, (kc0 + KC - 1) // rpq, j0 // hpq, T % W
+            # the kernel's partial stores reach o_lo and o_hi only: no middle owner
+            assert o_hi - o_lo <= 1
             owners = {q for q in range(W) if o_lo <= q <= o_hi or (by == 0 and q == ob) or q == orep}
             for r in range(kc0, kc0 + KC):
                 o = r // rpq
@@ -81,3 +83,12 @@ def test_fsdp_ownership_covers_every_element_once(W):
             assert orep in owners
     assert all(v == 1 for row in seen_w1 for v in row)
     assert all(v == 1 for v in seen_h)
+
+
+def test_fx_owner_span_guards_the_allowed_worlds():
+    """fsdp._tile_exchange admits W only when each 112-row chunk has <= 2 owners:
+    true for W = 2 / 4 / 8, false for W = 16 (49-row shards) and non-divisors."""
+    from jax_distributed_tuts_amd.comm.tile_exchange import fx_owner_span
+
+    assert [fx_owner_span(W) for W in (1, 2, 4, 8)] == [1, 2, 2, 2]
+    assert fx_owner_span(16) > 2 and fx_owner_span(3) > 2

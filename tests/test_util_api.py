@@ -70,6 +70,36 @@ def _engine_loss_fn(model):
     return loss_fn
 
 
+@pytest.mark.gpu
+def test_engine_scan_one_minibatch_repeats():
+    """accum_grads(use_scan=True, num_minibatches=1) with an engine loss, called twice:
+    the cached entry has no captured graph (nothing to roll), so the second call runs the
+    body eagerly -- and both calls equal the unrolled loop."""
+    dev = torch.device("cuda", 0)
+    model = Classifier(dropout_rate=0.0)
+    g = torch.Generator().manual_seed(0)
+    x, y = torch.randn(32, 784, generator=g).to(dev), torch.randint(0, 10, (32,), generator=g).to(torch.int32).to(dev)
+
+    def loss_fn(params, apply_fn, batch, rng, minibatch_index=0, state=None):
+        from jax_distributed_tuts_amd.models.mlp import loss_and_grad
+
+        m = torch.zeros(4, device=dev)
+        loss_and_grad(apply_fn, params, batch.inputs, batch.labels, train=False, seed=rng & 0xFFFF, offset=0,
+                      step=None, grad_scale=1.0 / batch.size, metrics=m)
+        return m[0] / m[1], {"loss": (m[0], m[1]), "accuracy": (m[2], m[3])}
+
+    P = FlatParams(model.param_specs(), device=dev).init_(1)
+    st = util.TrainState.create(apply_fn=model, params=P, tx=util.adamw(1e-3), rng=R.PRNGKey(0))
+    util.accum_grads(st, util.Batch(x, y), R.PRNGKey(1), 1, loss_fn, False)
+    want = P.grad.clone()
+    for _ in range(2):
+        P.zero_grad()
+        _, m = util.accum_grads(st, util.Batch(x, y), R.PRNGKey(1), 1, loss_fn, True)
+        torch.cuda.synchronize()
+        assert torch.equal(P.grad, want)
+        assert float(m["loss"][1]) == 32.0
+
+
 @pytest.mark.parametrize("use_scan", [False, True])
 def test_accum_grads_matches_full_batch(use_scan):
     """mean over minibatches of minibatch-mean grads == full-batch mean grad (util.py:77)."""

@@ -48,12 +48,16 @@ def test_tile_exchange_self_test(tmp_path, ws):
         assert o["selftest"] == {"rc": 0, "wrong": 0, "timeouts": 0, "reset": 0}, (r, o)
 
 
-@pytest.mark.parametrize("ws,dp_ahead,layers", [(2, "1", 2), (2, "0", 2), (8, "1", 2), (2, "1", 4), (2, "0", 4)])
-def test_dp_over_xgmi_matches_single_device(tmp_path, ws, dp_ahead, layers):
+@pytest.mark.parametrize("ws,dp_ahead,layers,width", [(2, "1", 2, (784, 512)), (2, "0", 2, (784, 512)),
+                                                      (8, "1", 2, (784, 512)), (2, "1", 4, (784, 512)),
+                                                      (2, "0", 4, (784, 512)), (2, "1", 2, (1024, 256))])
+def test_dp_over_xgmi_matches_single_device(tmp_path, ws, dp_ahead, layers, width):
     """ws=2, dp_ahead=1: the one-launch step (run-ahead backward with the in-kernel
     tile exchange: 2 x 224 workgroups fit the shared GPU) -- 4 layers: every hidden
     layer's backward exchanges its tiles, layer 0 running ahead; ws=2, dp_ahead=0 and
-    ws=8 (8 grids do not fit one GPU): forward, backward and the xGMI all-reduce + AdamW."""
+    ws=8 (8 grids do not fit one GPU): forward, backward and the xGMI all-reduce + AdamW.
+    width (1024, 256): the one-launch step at input width 1024 (16 input chunks of 64
+    rows, 2 x 256 workgroups)."""
     import functools
 
     from data_paral import synthetic_batch
@@ -62,7 +66,7 @@ def test_dp_over_xgmi_matches_single_device(tmp_path, ws, dp_ahead, layers):
     from jax_distributed_tuts_amd.utils.config import dp_config
     from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
 
-    _spawn8(functools.partial(XW.dp_xgmi, dp_ahead=dp_ahead, num_layers=layers), ws, str(tmp_path))
+    _spawn8(functools.partial(XW.dp_xgmi, dp_ahead=dp_ahead, num_layers=layers, width=width), ws, str(tmp_path))
     res = _load(tmp_path, "dpx", ws)
     assert all(o["comm"] == "xgmi" for o in res)
     assert all(o["step"] == 8 for o in res)
@@ -73,8 +77,11 @@ def test_dp_over_xgmi_matches_single_device(tmp_path, ws, dp_ahead, layers):
         torch.testing.assert_close(res[0]["metrics"], o["metrics"], rtol=0, atol=0)
     # single device, whole batch, same steps
     dev = torch.device("cuda", 0)
-    st = init_dp(Classifier(num_layers=layers, dropout_rate=0.0), adamw(1e-3), 69, dev, None)
-    b = synthetic_batch(dp_config(), 70)
+    st = init_dp(Classifier(input_size=width[0], hidden_size=width[1], num_layers=layers, dropout_rate=0.0),
+                 adamw(1e-3), 69, dev, None)
+    cfg = dp_config()
+    cfg.data.input_size = width[0]
+    b = synthetic_batch(cfg, 70)
     b = Batch(b.inputs.to(dev), b.labels.to(dev))
     tr = DataParallelTrainer(st, None, DPConfig(4, "kernel"))
     for _ in range(8):

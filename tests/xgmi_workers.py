@@ -172,11 +172,12 @@ def collectives(outdir):
     comm.close()
 
 
-def dp_xgmi(outdir, steps_eager=2, steps_graph=6, dp_ahead="1", num_layers=2):
+def dp_xgmi(outdir, steps_eager=2, steps_graph=6, dp_ahead="1", num_layers=2, width=(784, 512)):
     """DP over the xGMI fused all-reduce+AdamW kernel (dropout off), fused step
     kernels, eager steps then multi-step graph replays.  ``dp_ahead`` = JDT_DP_AHEAD:
     "1" lets the step be one run-ahead launch with the in-kernel tile exchange where
-    every rank's grid fits on the shared GPU, "0" keeps the three-launch step."""
+    every rank's grid fits on the shared GPU, "0" keeps the three-launch step.
+    ``width`` = (input size, hidden size) of the classifier."""
     os.environ["JDT_DP_AHEAD"] = dp_ahead
     os.environ["JDT_DP_DEEP_TX"] = dp_ahead   # the deep engine's exchange path is opt-in: test it
     from data_paral import synthetic_batch
@@ -188,8 +189,10 @@ def dp_xgmi(outdir, steps_eager=2, steps_graph=6, dp_ahead="1", num_layers=2):
 
     dev = D.device()
     cfg = dp_config()
+    cfg.data.input_size = width[0]
     mesh = D.Mesh({"data": D.world_size()})
-    st = init_dp(Classifier(num_layers=num_layers, dropout_rate=0.0), adamw(1e-3), 69, dev, None)  # same seed
+    st = init_dp(Classifier(input_size=width[0], hidden_size=width[1], num_layers=num_layers, dropout_rate=0.0),
+                 adamw(1e-3), 69, dev, None)  # same seed
     b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
     b = Batch(b.inputs.to(dev), b.labels.to(dev))
     tr = DataParallelTrainer(st, mesh, DPConfig(4, "kernel", comm="xgmi"))

@@ -54,7 +54,7 @@ int main() {
   EXPECT(jdt_gemm_group(gemm.data(), 0, nullptr, 0, nullptr, 0, nullptr) == 1, "empty group declined");
   std::vector<unsigned char> mlp2(jdt_mlp2_args_size(), 0);
   EXPECT(jdt_mlp2(mlp2.data(), 0, 784, 10, nullptr) == -3, "mlp2 rejects M = 0");
-  EXPECT(jdt_mlp2(mlp2.data(), 0, 100, 10, nullptr) == -3, "mlp2 rejects K != 784");
+  EXPECT(jdt_mlp2(mlp2.data(), 0, 100, 10, nullptr) == -3, "mlp2 rejects an input width it is not built for");
   std::vector<unsigned char> md(jdt_md_args_size(), 0);
   EXPECT(jdt_md_layer(md.data(), 0, 0, nullptr) == -3, "md rejects N != 512");
   void* ctx = nullptr;

@@ -921,10 +921,20 @@ struct XgCtx {
   bool opened = false;
 };
 
+// Grid cap of every xGMI kernel (8 .. XG_MAX_BLOCKS).  With k ranks time-sharing one GPU
+// (rehearsals) their spinning grids must leave every CU room for the other ranks'
+// non-spinning kernels -- a peer's md_bwd that cannot be dispatched because the CUs are
+// full of waiting xGMI workgroups never arrives at the barrier they wait on -- so the
+// host lowers the cap (comm/xgmi.py set_max_blocks) before it creates any context; the
+// layouts derived from the geometry (stage part, segment slice) follow it.
+static long g_xg_max_blocks = XG_MAX_BLOCKS;
+JDT_API void jdt_xgmi_set_max_blocks(int b) { g_xg_max_blocks = b < 8 ? 8 : (b > XG_MAX_BLOCKS ? XG_MAX_BLOCKS : b); }
+JDT_API int jdt_xgmi_max_blocks() { return (int)g_xg_max_blocks; }
+
 static void xg_geometry(long s, long* G_out, long* chunk_out) {
   long G = (s + 4 * XG_THREADS - 1) / (4 * XG_THREADS);
   if (G < 8) G = 8;
-  if (G > XG_MAX_BLOCKS) G = XG_MAX_BLOCKS;
+  if (G > g_xg_max_blocks) G = g_xg_max_blocks;
   *G_out = G;
   *chunk_out = (((s + G - 1) / G) + 3) / 4 * 4;
 }

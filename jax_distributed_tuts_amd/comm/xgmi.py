@@ -125,12 +125,38 @@ def part_len(n: int, world: int) -> int:
 
 
 XG_MAX_BLOCKS, XG_THREADS = 96, 256   # comm/csrc/xgmi.hip
+_lib.declare("jdt_xgmi_set_max_blocks", None, [c_int])
+_lib.declare("jdt_xgmi_max_blocks", c_int, [])
+
+
+def max_blocks() -> int:
+    """The kernels' current grid cap (``xg_geometry``; lowered when ranks share a GPU)."""
+    return int(_lib.lib().jdt_xgmi_max_blocks())
+
+
+def set_max_blocks(b: int) -> None:
+    _lib.lib().jdt_xgmi_set_max_blocks(int(b))
+
+
+def size_grids_for_sharing(device: torch.device) -> int:
+    """With k ranks time-sharing this GPU, cap every spinning xGMI grid at
+    CUs / (2 k) workgroups (>= 8): k ranks' waiting collectives then occupy at most half
+    the CUs' workgroup slots, so a peer's non-spinning kernels (md_fwd / md_bwd, GEMMs)
+    always find room to run and reach the barrier (tests at 8 shared ranks).  One rank
+    per GPU keeps the full 96.  Collective (ranks_per_gpu); returns the cap."""
+    from ..runtime.dist import ranks_per_gpu
+
+    k = ranks_per_gpu()
+    if k > 1:
+        cus = torch.cuda.get_device_properties(device).multi_processor_count
+        set_max_blocks(max(8, min(XG_MAX_BLOCKS, cus // (2 * k))))
+    return max_blocks()
 
 
 def geometry(s: int) -> tuple:
     """(blocks, chunk) of a launch over s floats per rank part: mirror of
     ``xg_geometry`` in comm/csrc/xgmi.hip (the host checks ``blocks*chunk*W <= cap``)."""
-    g = min(max((s + 4 * XG_THREADS - 1) // (4 * XG_THREADS), 8), XG_MAX_BLOCKS)
+    g = min(max((s + 4 * XG_THREADS - 1) // (4 * XG_THREADS), 8), max_blocks())
     return g, ((s + g - 1) // g + 3) // 4 * 4
 
 
@@ -889,6 +915,7 @@ def create_for(mesh, axis: str, cap_floats: int, device: torch.device, mode: str
         return None
     from ..runtime.dist import spin_timeout_s
 
+    size_grids_for_sharing(device)
     c = XgmiComm(mesh.group(axis), mesh.axis_index(axis), n, cap_floats, device, timeout_s=spin_timeout_s(30.0))
     if not c.ok:
         if mode == "xgmi":

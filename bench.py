@@ -236,6 +236,11 @@ def autotune_candidates(args, ws: int):
             ns = [n for n in (2, 4, 8) if rows % n == 0 and (args.model == "transformer" or rows // n >= 4)]
             stages.append([Candidate(f"microbatches={n}", {}, reference=(n == 2), args={"microbatches": n})
                            for n in ns])
+        if S > 1 and args.model == "mlp" and args.dp == 1:
+            # one persistent launch per stage step (parallel/pp_kernel.py) vs per-tick launches
+            stages.append([Candidate("stage-kernel=1", {"JDT_PP_KERNEL": "1"},
+                                     engaged=lambda tr: getattr(tr, "pp_kernel", None) is not None),
+                           Candidate("stage-kernel=0", {"JDT_PP_KERNEL": "0"}, reference=True)])
         if S > 1:
             stages.append([Candidate("stage-streams=0", {"JDT_PP_STREAMS": "0"}, reference=True),
                            Candidate("stage-streams=1", {"JDT_PP_STREAMS": "1"})])
@@ -465,6 +470,8 @@ def main():
         desc["single_stage_mode"] = tr.single_stage_mode  # how a 1-stage pipeline ran its microbatches
         desc["stage_streams"] = tr.stage_streams          # concurrent microbatch chains per stage
         desc["data_sync"] = tr.data_sync_mode             # data-axis sync: per W-pass group or one call
+        if getattr(tr, "pp_kernel", None) is not None:
+            desc["step_launches"] = "1 per stage (in-kernel GPipe schedule, parallel/pp_kernel.py)"
     if D.rank() == 0:
         out = {"metric": METRIC, "value": round(sps, 2), "unit": "steps/s", "n_gpus": ws, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 5), "higher_is_better": True,

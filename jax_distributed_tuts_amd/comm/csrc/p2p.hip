@@ -30,6 +30,7 @@
 // Waits time out (s_memrealtime, 100 MHz) into an error flag, never a hang.
 #include "common.h"
 
+#include <cstddef>
 #include <cstring>
 
 namespace jdt {
@@ -246,3 +247,19 @@ JDT_API int jdt_p2p_destroy(void* ctx) {
   delete c;
   return 0;
 }
+
+// Raw view of rank q's inbox and signal page for kernels that hand off in-kernel
+// (ops/csrc/pp_stage.hip): inbox base, flag array [P2P_MAX_SLOTS][P2P_MAX_BLOCKS] and
+// error word of q's page (q = this rank: its own).  -2 if q is out of range or unmapped.
+JDT_API int jdt_p2p_peer(void* ctx, int q, void** inbox, void** flags, void** err) {
+  P2PCtx* c = static_cast<P2PCtx*>(ctx);
+  if (!c || !c->opened || q < 0 || q >= c->world) return -2;
+  // addresses only (device pointers, nothing is dereferenced on the host)
+  char* sig = reinterpret_cast<char*>(c->peers.sig[q]);
+  *inbox = c->peers.inbox[q];
+  *flags = sig + offsetof(P2PSignal, flag);
+  *err = sig + offsetof(P2PSignal, err);
+  return 0;
+}
+JDT_API int jdt_p2p_max_blocks() { return P2P_MAX_BLOCKS; }
+JDT_API int jdt_p2p_max_slots() { return P2P_MAX_SLOTS; }

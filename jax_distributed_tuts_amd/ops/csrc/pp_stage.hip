@@ -1,0 +1,659 @@
+// One GPipe stage's whole training step in ONE persistent launch per rank
+// (BASELINE config #4: the 8-stage MLP 784 -> 512 x 8 -> 10, one dense layer per
+// stage, the 10-class head on the last stage).
+//
+// The per-tick path (parallel/pipeline.py _compute_fused) issues, per microbatch and
+// direction, a receive kernel, the layer's md_fwd / md_bwd launch, a dX GEMM and a
+// send kernel: 3-4 dependent launches of ~4 us each for a 64 x 512 x 512 layer, so a
+// tick costs ~13 us and an 8-stage pipeline cannot beat one GPU.  Here the whole
+// fill / drain schedule of the step runs inside one launch of 32 workgroups per rank,
+// workgroup b owning output columns [16b, 16b + 16) of the stage's layer (and, for the
+// input gradient, rows [16b, 16b + 16) of its weight):
+//
+//   forward tick i:  wait for the 32 producer flags of inbox slot i (or read the data),
+//                    Z = X W[:, own] + b on MFMA (K split over the 4 waves), SiLU,
+//                    dropout (the md kernels' Philox streams), backward factor G kept in
+//                    LDS; the H tile goes straight into the NEXT stage's inbox (H and
+//                    H^T, system-scope stores over xGMI) and one flag per workgroup is
+//                    raised -- or, last stage, the head's partial logits (fp32 atomics)
+//   backward tick i: dH[:, own] from the next stage's inbox (or, last stage, CE of the
+//                    complete logits through the head), dZ = dH * G; dW[:, own] +=
+//                    X^T dZ (accumulated in registers over the microbatches, X^T from
+//                    the inbox), db; then -- not stage 0 -- dZ is published to the
+//                    stage's other workgroups (one arrival counter), and each computes
+//                    dX[:, own rows] = dZ W[own rows, :]^T and sends it to the previous
+//                    stage's inbox
+//   end of step:     AdamW on the owned columns (gradient scale 1 / n_mb), bf16 shadows,
+//                    metrics fold, step advance (arrival ticket).
+//
+// Every wait is on another workgroup that is resident (32 workgroups, all co-resident,
+// host-checked) or on a neighbour stage's launch, and bounded (s_memrealtime) into the
+// inbox error word.  Flags are epoch-valued (the device optimizer step + 1, read at
+// the start), exactly as comm/csrc/p2p.hip's send / receive kernels, so replays need
+// no host bookkeeping; slot reuse is race-free by GPipe's own dependencies (the
+// producer overwrites slot i of step t+1 only after every gradient of step t arrived).
+// Reference semantics: the intended GPipe of /root/reference/pipeline_parallel.py:37-38
+// (SURVEY section 3.5); gradients equal the un-split model's (tests/test_pp_kernel_gpu.py).
+#include "common.h"
+
+namespace jdt {
+
+constexpr int PS_NT = 256;         // 4 waves
+constexpr int PS_NW = PS_NT / 64;
+constexpr int PS_NB = 32;          // workgroups = 512 / 16 output column blocks
+constexpr int PS_N = 512;          // layer width
+constexpr int PS_MAXMB = 64;       // rows per microbatch
+constexpr int PS_MAXROWS = 128;    // rows per step (n_mb * mb)
+constexpr int PS_MAXNMB = 8;
+constexpr int PS_C = 10;
+constexpr int PS_FLAG_BLOCKS = 32; // comm/csrc/p2p.hip P2P_MAX_BLOCKS (flags per slot)
+
+struct PsArgs {
+  int n_mb, mb;                    // microbatches, rows per microbatch (mb % 16 == 0, <= 64)
+  int K;                           // layer input width (784: stage 0, else 512)
+  int gid;                         // global layer index (dropout stream id)
+  int mb_shift;                    // dropout offset of microbatch i: (i << mb_shift) + (gid << 1)
+  float keep; unsigned long long seed;
+  // layer parameters (fp32 master, Adam moments) and bf16 shadows
+  float* p; float* m; float* v; bf16_t* sW;       // W [K][512]
+  float* pb; float* mbv; float* vb; bf16_t* sb;   // b [512]
+  // head (last stage): W_h [512][C], b_h [C]
+  float* ph; float* mh; float* vh; bf16_t* sh;
+  float* phb; float* mhb; float* vhb; bf16_t* shb;
+  const float* X;                  // stage 0: data [n_mb * mb][784] fp32
+  const int* labels;               // last stage: [n_mb * mb]
+  // inboxes (comm/csrc/p2p.hip layout): slot i < n_mb: activation of microbatch i (H
+  // [mb][512] bf16, then H^T [512][mbp]); slot n_mb + i: its gradient dX [mb][512]
+  char* in_mine; unsigned* flag_mine;
+  char* in_prev; unsigned* flag_prev;   // rank of stage s-1 (null at stage 0)
+  char* in_next; unsigned* flag_next;   // rank of stage s+1 (null at the last stage)
+  long slot_bytes;
+  int* err;                        // this rank's inbox error word (a wait timed out)
+  long long timeout;               // s_memrealtime ticks per wait
+  // scratch (zero-initialised once by the host)
+  bf16_t* XT;                      // stage 0: X^T [n_mb][784][mbp] bf16
+  bf16_t* dZ;                      // [n_mb][mb][512] bf16 (published for the dX products)
+  float* logits;                   // last stage: [2][n_mb][mb][C] fp32, by step parity
+  unsigned* ctr;                   // arrival counters, one 128-byte line each
+  int* step; unsigned* ticket;     // device optimizer step, end-of-step ticket
+  float lr, b1, b2, eps, wd, gscale;
+  float* mslot; float* running;    // last stage: metric slots (loss, n, correct, n), running sums
+  unsigned long long* stamps;      // diagnostic: [32][24] s_memrealtime (null = off)
+};
+
+#define PS_STAMP(k)                                                                           \
+  do {                                                                                        \
+    if (a.stamps && threadIdx.x == 0) a.stamps[(long)blockIdx.x * 24 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
+constexpr int CPOL_SC1 = 16;       // agent-coherent (write-through / past L1) buffer access
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ps_rsrc(const void* base, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(sgpr_ptr(const_cast<void*>(base)), (short)0,
+                                           __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
+}
+template <int CPOL>
+__device__ __forceinline__ u32x4 ps_load16(__amdgpu_buffer_rsrc_t r, long byte_off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, CPOL));
+}
+template <int CPOL>
+__device__ __forceinline__ void ps_store16(__amdgpu_buffer_rsrc_t r, long byte_off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sys_u32x4, v), r, (int)byte_off, 0, CPOL);
+}
+
+// this rank's error word: once a wait timed out, every later wait of the step gives up
+// at once (the results are refused by the host anyway), so a dead peer costs one timeout
+__device__ __forceinline__ bool ps_failed(const int* err) {
+  return __hip_atomic_load((const __attribute__((address_space(1))) int*)err, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
+
+// Wait until all PS_FLAG_BLOCKS producer flags of `slot` reached `epoch` (wave 0, one
+// lane per flag), then the workgroup barrier.  Bounded: a timeout raises *err.
+__device__ __forceinline__ void ps_wait_slot(const unsigned* flags, int slot, unsigned epoch, long long timeout,
+                                             int* err) {
+  if (threadIdx.x < PS_FLAG_BLOCKS && !ps_failed(err)) {
+    const unsigned* f = flags + (long)slot * PS_FLAG_BLOCKS + threadIdx.x;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int)(tx_flag_load(f) - epoch) < 0) {
+      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout) {
+        __hip_atomic_store((__attribute__((address_space(1))) int*)err, 1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+}
+
+// This workgroup's stores are drained, then ONE lane raises its flag of `slot` on the peer.
+__device__ __forceinline__ void ps_raise(unsigned* peer_flags, int slot, unsigned epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) tx_flag_store(peer_flags + (long)slot * PS_FLAG_BLOCKS + blockIdx.x, epoch);
+}
+
+// All PS_NB workgroups of this launch arrive at counter line `c` (stores drained, one
+// agent-scope add each) and wait for the others: the target is the next multiple of
+// PS_NB above this workgroup's own ticket, so the counter never needs a reset.
+__device__ __forceinline__ void ps_arrive_wait(unsigned* ctr, int c, long long timeout, int* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* cnt = ctr + 32 * c;
+    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = (old / PS_NB + 1u) * PS_NB;
+    const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(cnt, (short)0, 4, 0x00020000);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (!ps_failed(err) && (int)((unsigned)__builtin_amdgcn_raw_buffer_load_b32(cr, 0, 0, CPOL_SC1) - target) < 0) {
+      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout) {
+        __hip_atomic_store((__attribute__((address_space(1))) int*)err, 2, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");
+    }
+  }
+  __syncthreads();
+}
+
+// counter lines: X^T of microbatch i complete (stage 0), logits of i complete (last
+// stage), dZ of i published (stages > 0)
+__device__ __forceinline__ int ps_ctr_xt(int i) { return i; }
+__device__ __forceinline__ int ps_ctr_lg(int i) { return PS_MAXNMB + i; }
+__device__ __forceinline__ int ps_ctr_dz(int i) { return 2 * PS_MAXNMB + i; }
+
+template <bool FIRST, bool LAST>
+__global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
+  constexpr int K = FIRST ? 784 : PS_N;
+  constexpr int KS = (K + 31) / 32;             // 32-deep k-steps of the forward
+  constexpr int KP = KS * 32;
+  constexpr int LDWC = KP + 8;                  // padded LDS rows (bank spread)
+  constexpr int LDWR = PS_N + 8;
+  constexpr int NTK = K / 16;                   // 16-wide k tiles of dW^T (49 or 32)
+  constexpr int UPW = (NTK + PS_NW - 1) / PS_NW; // dW^T tiles per wave
+  constexpr int LDT = PS_MAXMB + 8;
+  static_assert(K % 16 == 0, "dW tiles");
+  __shared__ __attribute__((aligned(16))) bf16_t wc[16 * LDWC];                 // W[:, own]^T
+  __shared__ __attribute__((aligned(16))) bf16_t wr[FIRST ? 8 : 16 * LDWR];    // W[own rows, :]
+  __shared__ float part[PS_NW][PS_MAXMB][17];
+  __shared__ float gl[PS_MAXROWS][16];                                          // backward factor G
+  __shared__ __attribute__((aligned(16))) bf16_t ht[PS_MAXMB][24];             // this tick's H tile
+  __shared__ __attribute__((aligned(16))) bf16_t hown[LAST ? PS_MAXROWS : 1][16];  // head input (own cols)
+  __shared__ __attribute__((aligned(16))) bf16_t dzT[16 * LDT];                // dZ[:, own]^T
+  __shared__ float dlog[LAST ? PS_MAXMB : 1][PS_C + 1];
+  __shared__ float whs[16][PS_C];
+  __shared__ float bsh[16];
+  __shared__ float red[2][PS_NW];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.x, j0 = 16 * b;
+  const int mb = a.mb, n_mb = a.n_mb, mbp = (mb + 31) & ~31;
+  const int step = a.step[0], par = step & 1;
+  const unsigned epoch = (unsigned)step + 1u;
+  const unsigned long long dbase = (unsigned long long)(unsigned)step << 32;
+  PS_STAMP(0);
+
+  // ---- 0. this step's weights into LDS (bf16 rounding of the fp32 masters = the shadows)
+  for (int idx = tid; idx < K * 4; idx += PS_NT) {   // W[k][j0 .. j0+16) as 4 float4 per row
+    const int k = idx >> 2, q = idx & 3;
+    const float4 x = *reinterpret_cast<const float4*>(a.p + (long)k * PS_N + j0 + 4 * q);
+    wc[(4 * q + 0) * LDWC + k] = f2bf(x.x);
+    wc[(4 * q + 1) * LDWC + k] = f2bf(x.y);
+    wc[(4 * q + 2) * LDWC + k] = f2bf(x.z);
+    wc[(4 * q + 3) * LDWC + k] = f2bf(x.w);
+  }
+  if constexpr (KP > K)
+    for (int idx = tid; idx < 16 * (KP - K); idx += PS_NT) wc[(idx / (KP - K)) * LDWC + K + idx % (KP - K)] = 0;
+  if constexpr (!FIRST) {
+    for (int idx = tid; idx < 16 * (PS_N / 4); idx += PS_NT) {   // W[j0 + r][0 .. 512)
+      const int r = idx / (PS_N / 4), q = idx % (PS_N / 4);
+      const float4 x = *reinterpret_cast<const float4*>(a.p + (long)(j0 + r) * PS_N + 4 * q);
+      const unsigned lo = (unsigned)f2bf(x.x) | ((unsigned)f2bf(x.y) << 16);
+      const unsigned hi = (unsigned)f2bf(x.z) | ((unsigned)f2bf(x.w) << 16);
+      *reinterpret_cast<uint2*>(&wr[r * LDWR + 4 * q]) = make_uint2(lo, hi);
+    }
+  }
+  if (tid < 16) bsh[tid] = round_bf(a.pb[j0 + tid]);
+  if constexpr (LAST) {
+    if (tid < 16 * PS_C) whs[tid / PS_C][tid % PS_C] = round_bf(a.ph[(long)(j0 + tid / PS_C) * PS_C + tid % PS_C]);
+    // re-arm the other parity's logit accumulator (the previous step's, fully consumed)
+    if (b == 0)
+      for (int idx = tid; idx < n_mb * mb * PS_C; idx += PS_NT) a.logits[(long)(par ^ 1) * PS_MAXROWS * PS_C + idx] = 0.f;
+  }
+  __syncthreads();
+  PS_STAMP(1);
+
+  // ---- 1. forward ticks
+  const int MT = mb / 16;
+  for (int i = 0; i < n_mb; ++i) {
+    const int r0 = i * mb;   // this microbatch's rows of the step
+    if constexpr (!FIRST) ps_wait_slot(a.flag_mine, i, epoch, a.timeout, a.err);
+    // Z partials: wave w takes k-steps [w KS / 4, (w+1) KS / 4) of every 16-row tile
+    const int ks0 = (w * KS) / PS_NW, ks1 = ((w + 1) * KS) / PS_NW;
+    f32x4 acc[PS_MAXMB / 16];
+#pragma unroll
+    for (int mt = 0; mt < PS_MAXMB / 16; ++mt) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if constexpr (FIRST) {
+      for (int ks = ks0; ks < ks1; ++ks) {
+        const int k = ks * 32 + 8 * (lane >> 4);
+        const bf16x8 bf = *reinterpret_cast<const bf16x8*>(&wc[(lane & 15) * LDWC + k]);
+#pragma unroll
+        for (int mt = 0; mt < PS_MAXMB / 16; ++mt) {
+          if (mt >= MT) break;
+          bf16x8 af = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+          if (k < K) {
+            const float* xr = a.X + (long)(r0 + mt * 16 + (lane & 15)) * K + k;
+            const float4 x0 = *reinterpret_cast<const float4*>(xr), x1 = *reinterpret_cast<const float4*>(xr + 4);
+            af[0] = (short)f2bf(x0.x); af[1] = (short)f2bf(x0.y); af[2] = (short)f2bf(x0.z); af[3] = (short)f2bf(x0.w);
+            af[4] = (short)f2bf(x1.x); af[5] = (short)f2bf(x1.y); af[6] = (short)f2bf(x1.z); af[7] = (short)f2bf(x1.w);
+          }
+          acc[mt] = mfma16x16x32(af, bf, acc[mt]);
+        }
+      }
+      // X^T of this microbatch for the backward's dW: workgroup b converts input features
+      // [25 b, 25 b + 25) (write-through: the other workgroups read them after a counter)
+      const __amdgpu_buffer_rsrc_t xt = ps_rsrc(a.XT + (long)i * K * mbp, (long)K * mbp * 2);
+      for (int idx = tid; idx < 25 * (mb / 8); idx += PS_NT) {
+        const int kk = 25 * b + idx / (mb / 8), r8 = (idx % (mb / 8)) * 8;
+        if (kk >= K) continue;
+        unsigned q[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          q[e] = (unsigned)f2bf(a.X[(long)(r0 + r8 + 2 * e) * K + kk]) |
+                 ((unsigned)f2bf(a.X[(long)(r0 + r8 + 2 * e + 1) * K + kk]) << 16);
+        ps_store16<CPOL_SC1>(xt, ((long)kk * mbp + r8) * 2, (u32x4){q[0], q[1], q[2], q[3]});
+      }
+    } else {
+      const __amdgpu_buffer_rsrc_t xin = ps_rsrc(a.in_mine + (long)i * a.slot_bytes, (long)mb * PS_N * 2);
+      bf16x8 af[PS_MAXMB / 16][(KS + PS_NW - 1) / PS_NW];
+#pragma unroll
+      for (int t = 0; t < (KS + PS_NW - 1) / PS_NW; ++t)
+#pragma unroll
+        for (int mt = 0; mt < PS_MAXMB / 16; ++mt) {
+          const int ks = min(ks0 + t, ks1 - 1), row = min(mt * 16 + (lane & 15), mb - 1);
+          af[mt][t] = __builtin_bit_cast(bf16x8, ps_load16<CPOL_SYS>(xin, ((long)row * PS_N + ks * 32 + 8 * (lane >> 4)) * 2));
+        }
+#pragma unroll
+      for (int t = 0; t < (KS + PS_NW - 1) / PS_NW; ++t) {
+        const int ks = ks0 + t;
+        if (ks >= ks1) break;
+        const bf16x8 bf = *reinterpret_cast<const bf16x8*>(&wc[(lane & 15) * LDWC + ks * 32 + 8 * (lane >> 4)]);
+#pragma unroll
+        for (int mt = 0; mt < PS_MAXMB / 16; ++mt)
+          if (mt < MT) acc[mt] = mfma16x16x32(af[mt][t], bf, acc[mt]);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < PS_MAXMB / 16; ++mt)
+      if (mt < MT)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) part[w][mt * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[mt][e];
+    __syncthreads();
+    // bias + SiLU + dropout, one 4-row group per thread (the md kernels' streams)
+    {
+      const int g4 = tid >> 4, c = tid & 15;
+      if (4 * g4 < mb) {
+        u32x4 db = {0u, 0u, 0u, 0u};
+        const unsigned long long off = (unsigned long long)((long)i << a.mb_shift) + ((unsigned long long)a.gid << 1);
+        if (a.keep < 1.f) db = dropout_bits(a.seed, off + dbase, dropout_group(0, 4 * g4, j0 + c, mb, PS_N));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rl = 4 * g4 + e;
+          float v = bsh[c];
+#pragma unroll
+          for (int q = 0; q < PS_NW; ++q) v += part[q][rl][c];
+          const float z = round_bf(v);
+          const float ez = __expf(-z), sg = 1.0f / (1.0f + ez);
+          float hv = z * sg, gd = sg * (1.0f + z * (1.0f - sg));
+          if (a.keep < 1.f) {
+            const bool kp = keep_word(db, e, a.keep);
+            hv = kp ? hv / a.keep : 0.f;
+            gd = kp ? gd / a.keep : 0.f;
+          }
+          gl[r0 + rl][c] = gd;
+          const bf16_t hb = f2bf(hv);
+          ht[rl][c] = hb;
+          if constexpr (LAST) hown[r0 + rl][c] = hb;
+        }
+      }
+    }
+    __syncthreads();
+    if constexpr (LAST) {
+      // the head's partial logits of the owned 16 hidden units (+ b_h from workgroup 0)
+      float* lg = a.logits + (long)par * PS_MAXROWS * PS_C + (long)r0 * PS_C;
+      for (int idx = tid; idx < mb * PS_C; idx += PS_NT) {
+        const int r = idx / PS_C, c = idx % PS_C;
+        float s = b == 0 ? round_bf(a.phb[c]) : 0.f;
+#pragma unroll
+        for (int n = 0; n < 16; ++n) s += bf2f(ht[r][n]) * whs[n][c];
+        atomicAdd(lg + idx, s);
+      }
+      ps_arrive_wait(a.ctr, ps_ctr_lg(i), a.timeout, a.err);
+    } else {
+      // H[:, own] and H^T[own, :] into the next stage's inbox slot i, then this block's flag
+      const __amdgpu_buffer_rsrc_t o = ps_rsrc(a.in_next + (long)i * a.slot_bytes, a.slot_bytes);
+      if (tid < 2 * mb) {
+        const int r = tid >> 1, h = (tid & 1) * 8;
+        ps_store16<CPOL_SYS>(o, ((long)r * PS_N + j0 + h) * 2, *reinterpret_cast<const u32x4*>(&ht[r][h]));
+      }
+      // H^T rows: all mbp columns, the padding [mb, mbp) as zeros (the consumer's dW k-steps
+      // read it; the slot's memory holds whatever was sent through it before)
+      const long tbase = (long)mb * PS_N * 2;
+      for (int idx = tid; idx < 16 * (mbp / 8); idx += PS_NT) {
+        const int n = idx / (mbp / 8), r8 = (idx % (mbp / 8)) * 8;
+        unsigned q[4] = {0u, 0u, 0u, 0u};
+        if (r8 < mb)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) q[e] = (unsigned)ht[r8 + 2 * e][n] | ((unsigned)ht[r8 + 2 * e + 1][n] << 16);
+        ps_store16<CPOL_SYS>(o, tbase + ((long)(j0 + n) * mbp + r8) * 2, (u32x4){q[0], q[1], q[2], q[3]});
+      }
+      ps_raise(a.flag_next, i, epoch);
+    }
+    if constexpr (FIRST) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // X^T slice drained before anyone waits on it
+    }
+    if (i < 8) PS_STAMP(2 + i);
+  }
+
+  // ---- 2. backward ticks, last microbatch first
+  f32x4 dwa[UPW];
+#pragma unroll
+  for (int u = 0; u < UPW; ++u) dwa[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float dba = 0.f;                   // threads < 16: db[j0 + tid]
+  float dwh = 0.f, dbh = 0.f;        // last stage: threads < 160: dW_h[j0 + t/C][t%C]; b == 0, t < C: db_h
+  float l_loss = 0.f, l_corr = 0.f;
+  if constexpr (FIRST) {
+    for (int i = 0; i < n_mb; ++i) ps_arrive_wait(a.ctr, ps_ctr_xt(i), a.timeout, a.err);
+  }
+  for (int i = n_mb - 1; i >= 0; --i) {
+    const int r0 = i * mb;
+    // dH[:, own] -> dZ = dH * G -> dzT (bf16, as the md kernels round dZ)
+    if constexpr (LAST) {
+      // CE of every row of microbatch i from the complete logits (every workgroup passed
+      // the microbatch's logit counter in the forward)
+      const __amdgpu_buffer_rsrc_t lr =
+          ps_rsrc(a.logits + (long)par * PS_MAXROWS * PS_C + (long)r0 * PS_C, (long)mb * PS_C * 4);
+      if (tid < mb) {
+        float lrow[PS_C];
+#pragma unroll
+        for (int c = 0; c < PS_C; ++c)
+          lrow[c] = round_bf(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lr, (tid * PS_C + c) * 4, 0,
+                                                                                            CPOL_SC1)));
+        const int lab = a.labels[r0 + tid];
+        float mx = -INFINITY;
+        int am = 0;
+#pragma unroll
+        for (int c = 0; c < PS_C; ++c)
+          if (lrow[c] > mx) { mx = lrow[c]; am = c; }
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < PS_C; ++c) s += __expf(lrow[c] - mx);
+        const float lse = mx + __logf(s);
+        l_loss += lse - lrow[lab];
+        l_corr += (am == lab) ? 1.f : 0.f;
+        const float inv = 1.f / (float)mb;
+#pragma unroll
+        for (int c = 0; c < PS_C; ++c) dlog[tid][c] = round_bf((__expf(lrow[c] - lse) - (c == lab ? 1.f : 0.f)) * inv);
+      }
+      __syncthreads();
+      {
+        const int g4 = tid >> 4, c = tid & 15;
+        if (4 * g4 < mb) {
+          unsigned pk[2] = {0u, 0u};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int rl = 4 * g4 + e;
+            float dh = 0.f;
+#pragma unroll
+            for (int k = 0; k < PS_C; ++k) dh += dlog[rl][k] * whs[c][k];
+            pk[e >> 1] |= (unsigned)f2bf(dh * gl[r0 + rl][c]) << (16 * (e & 1));
+          }
+          *reinterpret_cast<uint2*>(&dzT[c * LDT + 4 * g4]) = make_uint2(pk[0], pk[1]);
+        }
+      }
+      // head gradients of the owned rows of W_h (and b_h, workgroup 0)
+      if (tid < 16 * PS_C) {
+        const int n = tid / PS_C, c = tid % PS_C;
+        float s = 0.f;
+        for (int r = 0; r < mb; ++r) s += bf2f(hown[r0 + r][n]) * dlog[r][c];
+        dwh += s;
+      }
+      if (b == 0 && tid < PS_C) {
+        float s = 0.f;
+        for (int r = 0; r < mb; ++r) s += dlog[r][tid];
+        dbh += s;
+      }
+    } else {
+      ps_wait_slot(a.flag_mine, n_mb + i, epoch, a.timeout, a.err);
+      const __amdgpu_buffer_rsrc_t gin = ps_rsrc(a.in_mine + (long)(n_mb + i) * a.slot_bytes, (long)mb * PS_N * 2);
+      const int g4 = tid >> 4, c = tid & 15;
+      if (4 * g4 < mb) {
+        unsigned pk[2] = {0u, 0u};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rl = 4 * g4 + e;
+          const unsigned short hb = (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(
+              gin, (int)(((long)rl * PS_N + j0 + c) * 2), 0, CPOL_SYS);
+          pk[e >> 1] |= (unsigned)f2bf(bf2f(hb) * gl[r0 + rl][c]) << (16 * (e & 1));
+        }
+        *reinterpret_cast<uint2*>(&dzT[c * LDT + 4 * g4]) = make_uint2(pk[0], pk[1]);
+      }
+    }
+    // zero padding rows [mb, mbp) of dzT for the 32-deep dW k-steps
+    for (int idx = tid; idx < 16 * (mbp - mb); idx += PS_NT) dzT[(idx / (mbp - mb)) * LDT + mb + idx % (mbp - mb)] = 0;
+    __syncthreads();
+    if (tid < 16) {
+      float s = 0.f;
+      for (int r = 0; r < mb; ++r) s += bf2f(dzT[tid * LDT + r]);
+      dba += s;
+    }
+    // dW^T[own cols][k] += dZ^T X: A = dzT (LDS), B = X^T rows (stage 0: XT scratch; else the
+    // inbox slot's H^T part), wave w takes k tiles w, w + 4, ...
+    {
+      const bf16_t* xtb = FIRST ? a.XT + (long)i * K * mbp
+                                : reinterpret_cast<const bf16_t*>(a.in_mine + (long)i * a.slot_bytes + (long)mb * PS_N * 2);
+      const __amdgpu_buffer_rsrc_t xr = ps_rsrc(xtb, (long)K * mbp * 2);
+      constexpr int cpol = FIRST ? CPOL_SC1 : CPOL_SYS;
+      bf16x8 dza[PS_MAXMB / 32];
+#pragma unroll
+      for (int rs = 0; rs < PS_MAXMB / 32; ++rs)
+        dza[rs] = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDT + min(rs, mbp / 32 - 1) * 32 + 8 * (lane >> 4)]);
+      bf16x8 xb[UPW][PS_MAXMB / 32];
+#pragma unroll
+      for (int u = 0; u < UPW; ++u)
+#pragma unroll
+        for (int rs = 0; rs < PS_MAXMB / 32; ++rs) {
+          const int t = min(w + PS_NW * u, NTK - 1);
+          xb[u][rs] = __builtin_bit_cast(
+              bf16x8, ps_load16<cpol>(xr, ((long)(16 * t + (lane & 15)) * mbp + min(rs, mbp / 32 - 1) * 32 + 8 * (lane >> 4)) * 2));
+        }
+#pragma unroll
+      for (int u = 0; u < UPW; ++u) {
+        if (w + PS_NW * u >= NTK) break;
+#pragma unroll
+        for (int rs = 0; rs < PS_MAXMB / 32; ++rs)
+          if (rs < mbp / 32) dwa[u] = mfma16x16x32(dza[rs], xb[u][rs], dwa[u]);
+      }
+    }
+    if constexpr (!FIRST) {
+      // publish dZ[:, own] (write-through), meet the stage's other workgroups, then
+      // dX[:, own rows] = dZ W[own rows, :]^T -> the previous stage's inbox slot n_mb + i
+      const __amdgpu_buffer_rsrc_t zr = ps_rsrc(a.dZ + (long)i * mb * PS_N, (long)mb * PS_N * 2);
+      if (tid < 2 * mb) {
+        const int r = tid >> 1, h = (tid & 1) * 8;
+        unsigned q[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          q[e] = (unsigned)dzT[(h + 2 * e) * LDT + r] | ((unsigned)dzT[(h + 2 * e + 1) * LDT + r] << 16);
+        ps_store16<CPOL_SC1>(zr, ((long)r * PS_N + j0 + h) * 2, (u32x4){q[0], q[1], q[2], q[3]});
+      }
+      ps_arrive_wait(a.ctr, ps_ctr_dz(i), a.timeout, a.err);
+      // wave w: k-steps [4w, 4w + 4) of the 512-deep product, every 16-row tile
+      bf16x8 za[PS_MAXMB / 16][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int mt = 0; mt < PS_MAXMB / 16; ++mt) {
+          const int row = min(mt * 16 + (lane & 15), mb - 1);
+          za[mt][t] = __builtin_bit_cast(bf16x8, ps_load16<CPOL_SC1>(zr, ((long)row * PS_N + (4 * w + t) * 32 + 8 * (lane >> 4)) * 2));
+        }
+      f32x4 acc[PS_MAXMB / 16];
+#pragma unroll
+      for (int mt = 0; mt < PS_MAXMB / 16; ++mt) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16x8 bf = *reinterpret_cast<const bf16x8*>(&wr[(lane & 15) * LDWR + (4 * w + t) * 32 + 8 * (lane >> 4)]);
+#pragma unroll
+        for (int mt = 0; mt < PS_MAXMB / 16; ++mt)
+          if (mt < MT) acc[mt] = mfma16x16x32(za[mt][t], bf, acc[mt]);
+      }
+#pragma unroll
+      for (int mt = 0; mt < PS_MAXMB / 16; ++mt)
+        if (mt < MT)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) part[w][mt * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[mt][e];
+      __syncthreads();
+      const __amdgpu_buffer_rsrc_t o = ps_rsrc(a.in_prev + (long)(n_mb + i) * a.slot_bytes, (long)mb * PS_N * 2);
+      if (tid < 2 * mb) {
+        const int r = tid >> 1, h = (tid & 1) * 8;
+        unsigned q[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x0 = 0.f, x1 = 0.f;
+#pragma unroll
+          for (int ww = 0; ww < PS_NW; ++ww) { x0 += part[ww][r][h + 2 * e]; x1 += part[ww][r][h + 2 * e + 1]; }
+          q[e] = (unsigned)f2bf(x0) | ((unsigned)f2bf(x1) << 16);
+        }
+        ps_store16<CPOL_SYS>(o, ((long)r * PS_N + j0 + h) * 2, (u32x4){q[0], q[1], q[2], q[3]});
+      }
+      ps_raise(a.flag_prev, n_mb + i, epoch);
+    }
+    __syncthreads();
+    if (i < 8) PS_STAMP(10 + i);
+  }
+
+  // ---- 3. AdamW on the owned columns (+ the head's owned rows), shadows, metrics, step
+  const float t1 = (float)(step + 1);
+  const float rbc1 = 1.f / (1.f - powf(a.b1, t1)), rbc2 = 1.f / (1.f - powf(a.b2, t1));
+  auto adam = [&](float& p, float& m, float& v, float g) {
+    g *= a.gscale;
+    m = a.b1 * m + (1.f - a.b1) * g;
+    v = a.b2 * v + (1.f - a.b2) * g * g;
+    p = p - a.lr * ((m * rbc1) * __builtin_amdgcn_rcpf(sqrtf(v * rbc2) + a.eps) + a.wd * p);
+  };
+  {
+    // lane: dW^T rows (lane >> 4) * 4 + e (owned columns), column 16 t + (lane & 15) (input k)
+    float4 pv[UPW], mv[UPW], vv[UPW];
+#pragma unroll
+    for (int u = 0; u < UPW; ++u) {
+      const int t = min(w + PS_NW * u, NTK - 1);
+      const long o = (long)(16 * t + (lane & 15)) * PS_N + j0 + 4 * (lane >> 4);
+      pv[u] = *reinterpret_cast<const float4*>(a.p + o);
+      mv[u] = *reinterpret_cast<const float4*>(a.m + o);
+      vv[u] = *reinterpret_cast<const float4*>(a.v + o);
+    }
+#pragma unroll
+    for (int u = 0; u < UPW; ++u) {
+      const int t = w + PS_NW * u;
+      if (t >= NTK) break;
+      const long o = (long)(16 * t + (lane & 15)) * PS_N + j0 + 4 * (lane >> 4);
+      float* pe = &pv[u].x; float* me = &mv[u].x; float* ve = &vv[u].x;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) adam(pe[e], me[e], ve[e], dwa[u][e]);
+      *reinterpret_cast<float4*>(a.p + o) = pv[u];
+      *reinterpret_cast<float4*>(a.m + o) = mv[u];
+      *reinterpret_cast<float4*>(a.v + o) = vv[u];
+      *reinterpret_cast<uint2*>(a.sW + o) = make_uint2((unsigned)f2bf(pv[u].x) | ((unsigned)f2bf(pv[u].y) << 16),
+                                                       (unsigned)f2bf(pv[u].z) | ((unsigned)f2bf(pv[u].w) << 16));
+    }
+  }
+  if (tid < 16) {
+    float p = a.pb[j0 + tid], m = a.mbv[j0 + tid], v = a.vb[j0 + tid];
+    adam(p, m, v, dba);
+    a.pb[j0 + tid] = p; a.mbv[j0 + tid] = m; a.vb[j0 + tid] = v; a.sb[j0 + tid] = f2bf(p);
+  }
+  if constexpr (LAST) {
+    if (tid < 16 * PS_C) {
+      const long o = (long)j0 * PS_C + tid;   // W_h[j0 + tid / C][tid % C]
+      float p = a.ph[o], m = a.mh[o], v = a.vh[o];
+      adam(p, m, v, dwh);
+      a.ph[o] = p; a.mh[o] = m; a.vh[o] = v; a.sh[o] = f2bf(p);
+    }
+    if (b == 0 && tid < PS_C) {
+      float p = a.phb[tid], m = a.mhb[tid], v = a.vhb[tid];
+      adam(p, m, v, dbh);
+      a.phb[tid] = p; a.mhb[tid] = m; a.vhb[tid] = v; a.shb[tid] = f2bf(p);
+    }
+    if (b == 0) {
+      // metrics: this step's loss sum / rows / correct / rows, folded into the running sums
+      l_loss = wave_sum(l_loss);
+      l_corr = wave_sum(l_corr);
+      if (lane == 0) { red[0][w] = l_loss; red[1][w] = l_corr; }
+      __syncthreads();
+      if (tid < 4) {
+        float s = 0.f;
+        for (int q = 0; q < PS_NW; ++q) s += tid == 0 ? red[0][q] : (tid == 2 ? red[1][q] : 0.f);
+        const float val = (tid & 1) ? (float)(n_mb * mb) : s;
+        a.running[tid] += a.mslot[tid] + val;
+        a.mslot[tid] = 0.f;
+      }
+    }
+  }
+  PS_STAMP(18);
+  // the last workgroup to finish advances the optimizer step (read by every workgroup at
+  // its start, which all passed: each waited on a counter or flag that needed them all)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == PS_NB - 1) {
+      a.step[0] = step + 1;
+      __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace jdt
+using namespace jdt;
+
+JDT_API int jdt_pp_stage_args_size() { return (int)sizeof(PsArgs); }
+
+// 1 if `nshare` ranks' stage launches (PS_NB workgroups each) can all be resident on
+// this GPU at once (every wait of the launch is on a co-resident workgroup or a
+// neighbour's launch), with half the device's workgroup slots to spare for the other
+// ranks' kernels when the GPU is shared.
+JDT_API int jdt_pp_stage_ok(int first, int last, int nshare) {
+  int dev = 0, cus = 0, per = 0;
+  if (nshare < 1 || hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  hipError_t e;
+  if (first) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pp_stage_kernel<true, false>, PS_NT, 0);
+  else if (last) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pp_stage_kernel<false, true>, PS_NT, 0);
+  else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pp_stage_kernel<false, false>, PS_NT, 0);
+  if (e != hipSuccess || per < 1) return 0;
+  const long slots = (long)cus * per;
+  return (long)nshare * PS_NB <= (nshare > 1 ? slots / 2 : slots) ? 1 : 0;
+}
+
+// One step of this stage (first: stage 0, last: the last stage; not both).
+JDT_API int jdt_pp_stage(const PsArgs* args, int first, int last, void* stream) {
+  const PsArgs& a = *args;
+  if ((first && last) || a.n_mb < 1 || a.n_mb > PS_MAXNMB || a.mb < 16 || a.mb > PS_MAXMB || (a.mb & 15) ||
+      a.n_mb * a.mb > PS_MAXROWS || a.K != (first ? 784 : PS_N) || !a.step || !a.ticket || !a.ctr || !a.err)
+    return -2;
+  if (!first && (!a.in_mine || !a.flag_mine || !a.in_prev || !a.flag_prev || !a.dZ)) return -2;
+  if (!last && (!a.in_next || !a.flag_next)) return -2;
+  if (first && (!a.X || !a.XT)) return -2;
+  if (last && (!a.labels || !a.logits || !a.ph || !a.phb || !a.mslot || !a.running)) return -2;
+  const long need = (long)a.mb * PS_N * 2 + (long)PS_N * ((a.mb + 31) & ~31) * 2;
+  if (a.slot_bytes < need) return -2;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (first) hipLaunchKernelGGL((pp_stage_kernel<true, false>), dim3(PS_NB), dim3(PS_NT), 0, st, a);
+  else if (last) hipLaunchKernelGGL((pp_stage_kernel<false, true>), dim3(PS_NB), dim3(PS_NT), 0, st, a);
+  else hipLaunchKernelGGL((pp_stage_kernel<false, false>), dim3(PS_NB), dim3(PS_NT), 0, st, a);
+  return HIP_LAUNCH_CHECK();
+}

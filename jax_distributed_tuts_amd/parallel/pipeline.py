@@ -240,6 +240,8 @@ class GPipeTrainer:
         self._engine_tried = False
         self.deep_engine = None
         self._deep_tried = False
+        self.pp_kernel = None          # the in-kernel GPipe step (parallel/pp_kernel.py)
+        self._pp_kernel_tried = False
         from ..utils.checkpoint import bind_trainer
 
         bind_trainer(state, self)
@@ -289,14 +291,14 @@ class GPipeTrainer:
         from ..runtime.dist import collectives_capturable
 
         rccl = collectives_capturable()
-        return (self.dev.type == "cuda" and (self.S == 1 or self.p2p is not None or rccl)
+        return (self.dev.type == "cuda" and (self.S == 1 or self.p2p is not None or self.pp_kernel is not None or rccl)
                 and (self.n_dp == 1 or self.xg is not None or rccl))
 
     @property
     def comm_backend(self) -> str:
         if self.S * self.n_dp == 1:
             return "none"
-        if (self.S == 1 or self.p2p is not None) and (self.n_dp == 1 or self.xg is not None):
+        if (self.S == 1 or self.p2p is not None or self.pp_kernel is not None) and (self.n_dp == 1 or self.xg is not None):
             return "xgmi"
         from ..runtime.dist import backend
 
@@ -310,18 +312,38 @@ class GPipeTrainer:
         dp = status(self.xg, self.n_dp, self.dev, self.cfg.comm)
         if self.S == 1:
             return dp
-        pipe = "passed" if self.p2p is not None else ("failed->rccl" if self._p2p_tried and self.dev.type == "cuda"
+        pipe = "passed" if (self.p2p is not None or self.pp_kernel is not None) else (
+            "failed->rccl" if self._p2p_tried and self.dev.type == "cuda"
                                                       and self.cfg.comm != "rccl" else "off")
         return f"data:{dp},pipe:{pipe}"
 
     # ------------------------------------------------------------------ step
+    def _pp_kernel_engine(self, mb: int, seed: int):
+        """The whole stage step as one persistent launch (parallel/pp_kernel.py), when
+        every stage of the pipe axis can run it (collective on first use)."""
+        if not self._pp_kernel_tried:
+            self._pp_kernel_tried = True
+            if self.S > 1 and self.dev.type == "cuda":
+                from ..comm.tile_exchange import agree
+                from . import pp_kernel as PK
+
+                ok = agree(self.mesh.group(self.cfg.pipe_axis), PK.local_ok(self, mb), self.dev)
+                if ok:
+                    eng = PK.PPStageKernel(self, mb, seed)
+                    self.pp_kernel = eng if eng.ok else None
+        return self.pp_kernel
+
     def _compute(self, batch: Batch):
         st, P, cfg = self.state, self.state.params, self.cfg
         n_mb = cfg.num_microbatches
         mb = batch.size // n_mb
-        self._setup_p2p(mb)
         rng = R.fold_rng_over_axis(st.rng, self.mesh, cfg.data_axis)
         seed = rng & 0xFFFFFFFF
+        if self.S > 1 and self._pp_kernel_engine(mb, seed) is not None:
+            # every tick, hand-off and the AdamW update in ONE launch (csrc/pp_stage.hip)
+            self.pp_kernel.step(batch)
+            return
+        self._setup_p2p(mb)
         if self.S == 1:
             deep = self._single_stage_engine(batch.size, mb)
             if deep is not None:
@@ -719,6 +741,8 @@ class GPipeTrainer:
         'data' only; then AdamW on the local stage and the metrics fold.  The host
         step counter is advanced by the callers."""
         st, P, cfg = self.state, self.state.params, self.cfg
+        if self.pp_kernel is not None:
+            return   # AdamW, the metrics fold and the step advance ran inside the stage launch
         if getattr(self, "_synced", False):   # the W pass issued the sync per part (_overlapped_sync)
             self._synced = False
             return
@@ -827,6 +851,9 @@ class GPipeTrainer:
             self.deep_engine.finalize()  # bf16 shadow parity of the in-epilogue AdamW
         if self.p2p is not None and self.p2p.error():
             raise RuntimeError("xgmi pipeline receive timed out on this rank (peer dead or desynchronised)")
+        if self.pp_kernel is not None and self.pp_kernel.error():
+            raise RuntimeError("pipeline stage kernel: an in-kernel wait timed out on this rank (peer dead or "
+                               "desynchronised); results invalid")
         if self.xg is not None:
             self.xg.raise_if_error()
 
@@ -835,10 +862,10 @@ class GPipeTrainer:
         another trainer can be built in this process (bench.py's autotune candidates)."""
         if self.dev.type == "cuda":
             torch.cuda.synchronize(self.dev)
-        for r in (self.p2p, self.xg):
+        for r in (self.p2p, self.xg, self.pp_kernel):
             if r is not None:
                 r.close()
-        self.p2p = self.xg = None
+        self.p2p = self.xg = self.pp_kernel = None
         self.graph = self._ahead = self.multi = None
 
     def loss_head(self, logits, labels, dlogits, n_parts: int = 1):

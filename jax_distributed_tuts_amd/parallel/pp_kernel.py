@@ -1,0 +1,205 @@
+"""A GPipe stage's whole step as ONE persistent launch per rank (csrc/pp_stage.hip).
+
+For an MLP pipeline with one 512-wide SiLU/dropout layer per stage (stage 0's takes the
+784 inputs, the last stage also carries the 10-class head) -- BASELINE config #4, the
+8-stage MLP -- the per-tick schedule of parallel/pipeline.py (a receive, the md layer
+kernel, a dX GEMM and a send per microbatch and direction: 3-4 launches per tick)
+becomes one launch of 32 workgroups per rank per step: every tick's wait is an in-kernel
+poll of the producer stage's inbox flags, every hand-off a system-scope store straight
+into the consumer's inbox, the weight gradients stay in registers over the
+microbatches and AdamW runs at the end of the same launch.
+
+The engine applies when every rank of the pipe axis can run it (agreed collectively):
+a GPU, no data axis (the data-axis all-reduce needs the gradients in memory: the
+per-tick path keeps it), AdamW, one layer per stage, microbatches of 16..64 rows
+(multiple of 16), all 32 workgroups of every rank sharing the GPU co-resident.
+``JDT_PP_KERNEL=0`` turns it off (A/B; bench.py's autotune times both).
+
+Reference: the intended GPipe of /root/reference/pipeline_parallel.py:37-38
+(SURVEY §3.5), the tutorial MLP layer of data_paral.py:86-100.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_float, c_int, c_long, c_longlong, c_ulonglong, c_void_p
+from typing import Optional
+
+import torch
+
+from ..ops import _lib
+
+NB = 32          # workgroups per rank (512 / 16 columns)
+H = 512
+C_HEAD = 10
+
+
+class PsArgs(ctypes.Structure):
+    """Mirror of ``jdt::PsArgs`` (ops/csrc/pp_stage.hip)."""
+
+    _fields_ = [("n_mb", c_int), ("mb", c_int), ("K", c_int), ("gid", c_int), ("mb_shift", c_int),
+                ("keep", c_float), ("seed", c_ulonglong),
+                ("p", c_void_p), ("m", c_void_p), ("v", c_void_p), ("sW", c_void_p),
+                ("pb", c_void_p), ("mbv", c_void_p), ("vb", c_void_p), ("sb", c_void_p),
+                ("ph", c_void_p), ("mh", c_void_p), ("vh", c_void_p), ("sh", c_void_p),
+                ("phb", c_void_p), ("mhb", c_void_p), ("vhb", c_void_p), ("shb", c_void_p),
+                ("X", c_void_p), ("labels", c_void_p),
+                ("in_mine", c_void_p), ("flag_mine", c_void_p), ("in_prev", c_void_p), ("flag_prev", c_void_p),
+                ("in_next", c_void_p), ("flag_next", c_void_p), ("slot_bytes", c_long), ("err", c_void_p),
+                ("timeout", c_longlong),
+                ("XT", c_void_p), ("dZ", c_void_p), ("logits", c_void_p), ("ctr", c_void_p),
+                ("step", c_void_p), ("ticket", c_void_p),
+                ("lr", c_float), ("b1", c_float), ("b2", c_float), ("eps", c_float), ("wd", c_float),
+                ("gscale", c_float), ("mslot", c_void_p), ("running", c_void_p), ("stamps", c_void_p)]
+
+
+_lib.declare("jdt_pp_stage_args_size", c_int, [])
+_lib.declare("jdt_pp_stage_ok", c_int, [c_int, c_int, c_int])
+_lib.declare("jdt_pp_stage", c_int, [ctypes.POINTER(PsArgs), c_int, c_int, c_void_p])
+_lib.declare("jdt_p2p_max_slots", c_int, [])
+_lib.declare("jdt_p2p_peer", c_int, [c_void_p, c_int, ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p),
+                                     ctypes.POINTER(c_void_p)])
+
+
+def slot_bytes(mb: int) -> int:
+    """Inbox slot: H [mb][512] then H^T [512][mbp] (bf16)."""
+    mbp = (mb + 31) // 32 * 32
+    return mb * H * 2 + H * mbp * 2
+
+
+def stage_fits(model, first: bool, last: bool) -> bool:
+    """One 512-wide SiLU layer per stage (784 inputs on stage 0), the head on the last."""
+    from ..models.mlp import MLP
+
+    if not isinstance(model, MLP) or model.act != "silu":
+        return False
+    k0 = 784 if first else H
+    if last:
+        return model.L == 2 and list(model.dims) == [k0, H, C_HEAD] and not model.final_act
+    return model.L == 1 and list(model.dims) == [k0, H] and model.final_act
+
+
+def local_ok(trainer, mb: int) -> bool:
+    """This rank's view of whether the stage kernel applies (not collective)."""
+    from ..utils.train_state import AdamW
+
+    n_mb = trainer.cfg.num_microbatches
+    if os.environ.get("JDT_PP_KERNEL", "1") == "0" or trainer.dev.type != "cuda":
+        return False
+    if trainer.S < 2 or trainer.n_dp != 1 or not isinstance(trainer.state.tx, AdamW):
+        return False
+    if not (16 <= mb <= 64 and mb % 16 == 0 and 1 <= n_mb <= 8 and n_mb * mb <= 128):
+        return False
+    if 2 * n_mb > int(_lib.lib().jdt_p2p_max_slots()):
+        return False
+    if not stage_fits(trainer.model, trainer.first, trainer.last):
+        return False
+    from ..runtime.dist import ranks_per_gpu
+
+    return bool(_lib.lib().jdt_pp_stage_ok(int(trainer.first), int(trainer.last), ranks_per_gpu()))
+
+
+class PPStageKernel:
+    """One rank's stage of the in-kernel GPipe step (collective construction over the
+    pipe axis: every stage builds its engine at the same point)."""
+
+    def __init__(self, trainer, mb: int, seed: int):
+        from ..comm.p2p import TICKS_PER_S, XgmiP2P
+        from ..runtime.dist import spin_timeout_s
+
+        if _lib.lib().jdt_pp_stage_args_size() != ctypes.sizeof(PsArgs):
+            raise RuntimeError("PsArgs layout mismatch")
+        tr = self.tr = trainer
+        self.mb, self.n_mb = mb, trainer.cfg.num_microbatches
+        self.first, self.last = trainer.first, trainer.last
+        dev = self.dev = trainer.dev
+        S, s = trainer.S, trainer.s
+        timeout_s = spin_timeout_s(30.0)
+        self.p2p = XgmiP2P(trainer.mesh.group(trainer.cfg.pipe_axis), s, S, slot_bytes(mb), 2 * self.n_mb, dev,
+                           timeout_s=timeout_s)
+        self.ok = self.p2p.ok
+        if not self.ok:
+            return
+        L = _lib.lib()
+
+        def peer(q):
+            ib, fl, er = c_void_p(), c_void_p(), c_void_p()
+            _lib.check(L.jdt_p2p_peer(self.p2p.ctx, int(q), ctypes.byref(ib), ctypes.byref(fl), ctypes.byref(er)),
+                       "jdt_p2p_peer")
+            return ib.value, fl.value, er.value
+
+        mine = peer(s)
+        prev = peer(s - 1) if s > 0 else (None, None, None)
+        nxt = peer(s + 1) if s < S - 1 else (None, None, None)
+        P, st, model = trainer.state.params, trainer.state, trainer.model
+        o = st.opt_state
+        mbp = (mb + 31) // 32 * 32
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        # scratch (zeroed once: padding rows are read as zeros by the dW k-steps)
+        self.XT = torch.zeros(self.n_mb, 784, mbp, **bf) if self.first else None
+        self.dZ = torch.zeros(self.n_mb, mb, H, **bf)
+        self.logits = torch.zeros(2, 128, C_HEAD, dtype=torch.float32, device=dev) if self.last else None
+        self.ctr = torch.zeros(64 * 32, dtype=torch.int32, device=dev)
+        self.stamps = None
+
+        a = PsArgs()
+        a.n_mb, a.mb, a.K = self.n_mb, mb, model.dims[0]
+        a.gid = int(model.layer_id_base)
+        a.mb_shift = 16
+        a.keep = 1.0 - float(model.dropout_rate)
+        a.seed = int(seed) & 0xFFFFFFFF
+        kn, bn = f"{model.names[0]}/kernel", f"{model.names[0]}/bias"
+        a.p, a.sW = P.p(kn).data_ptr(), P.s(kn).data_ptr()
+        a.m, a.v = o["m"][P.offsets[kn][0]:].data_ptr(), o["v"][P.offsets[kn][0]:].data_ptr()
+        a.pb, a.sb = P.p(bn).data_ptr(), P.s(bn).data_ptr()
+        a.mbv, a.vb = o["m"][P.offsets[bn][0]:].data_ptr(), o["v"][P.offsets[bn][0]:].data_ptr()
+        if self.last:
+            hk, hb = f"{model.names[1]}/kernel", f"{model.names[1]}/bias"
+            a.ph, a.sh = P.p(hk).data_ptr(), P.s(hk).data_ptr()
+            a.mh, a.vh = o["m"][P.offsets[hk][0]:].data_ptr(), o["v"][P.offsets[hk][0]:].data_ptr()
+            a.phb, a.shb = P.p(hb).data_ptr(), P.s(hb).data_ptr()
+            a.mhb, a.vhb = o["m"][P.offsets[hb][0]:].data_ptr(), o["v"][P.offsets[hb][0]:].data_ptr()
+            a.logits = self.logits.data_ptr()
+            a.mslot, a.running = P.metrics_slot.data_ptr(), trainer.metrics.data_ptr()
+        a.in_mine, a.flag_mine, a.err = mine
+        a.in_prev, a.flag_prev, _ = prev
+        a.in_next, a.flag_next, _ = nxt
+        a.slot_bytes = int(self.p2p.slot_bytes)
+        a.timeout = int(timeout_s * TICKS_PER_S)
+        a.XT = self.XT.data_ptr() if self.XT is not None else None
+        a.dZ = self.dZ.data_ptr()
+        a.ctr = self.ctr.data_ptr()
+        a.step, a.ticket = o["count"].data_ptr(), o["ticket"].data_ptr()
+        tx = st.tx
+        a.lr, a.b1, a.b2, a.eps, a.wd = tx.learning_rate, tx.b1, tx.b2, tx.eps, tx.weight_decay
+        a.gscale = 1.0 / self.n_mb
+        self.args = a
+        self._key = None
+
+    def set_stamps(self, stamps: Optional[torch.Tensor]):
+        """Diagnostic: [32 * 24] int64 s_memrealtime per workgroup (tools/stamp_pp.py)."""
+        self.stamps = stamps
+        self.args.stamps = stamps.data_ptr() if stamps is not None else None
+
+    def step(self, batch):
+        a = self.args
+        key = (batch.inputs.data_ptr(), batch.labels.data_ptr())
+        if key != self._key:
+            if self.first:
+                assert batch.inputs.dtype == torch.float32 and batch.inputs.is_contiguous()
+                assert batch.inputs.shape == (self.n_mb * self.mb, 784)
+                a.X = batch.inputs.data_ptr()
+            if self.last:
+                assert batch.labels.dtype == torch.int32 and batch.labels.numel() == self.n_mb * self.mb
+                a.labels = batch.labels.data_ptr()
+            self._key = key
+        _lib.check(_lib.lib().jdt_pp_stage(ctypes.byref(a), int(self.first), int(self.last), c_void_p(_lib.stream_ptr())),
+                   "pp_stage")
+
+    def error(self) -> int:
+        return self.p2p.error() if self.p2p is not None else 0
+
+    def close(self):
+        if self.p2p is not None:
+            self.p2p.close()
+            self.p2p = None

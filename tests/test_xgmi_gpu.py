@@ -166,11 +166,14 @@ def test_p2p_inbox_roundtrip(tmp_path, ws):
         assert o["data"] and o["err"] == 0 and o["epoch"] == 4, o
 
 
-@pytest.mark.parametrize("ws,dp,n_hidden", [(2, 1, 3), (4, 2, 3), (8, 1, 7), (8, 2, 3)])
+@pytest.mark.parametrize("ws,dp,n_hidden", [(2, 1, 3), (4, 2, 3), (8, 1, 7), (8, 2, 3), (2, 1, 2), (4, 1, 4)])
 def test_pipeline_over_xgmi_matches_single_device(tmp_path, ws, dp, n_hidden):
     """GPipe with the inbox hand-off captured into hipGraphs (and the fused xGMI
     data-axis all-reduce for dp=2) == the un-split model on one device.  ws=8: the
-    8-stage GPipe MLP (BASELINE config #4, one dense layer per stage) and DP=2 x PP=4."""
+    8-stage GPipe MLP (BASELINE config #4, one dense layer per stage) and DP=2 x PP=4.
+    (2, 1, 2) / (4, 1, 4): one layer per stage -- each stage's step is ONE persistent
+    launch (parallel/pp_kernel.py; 8 ranks' stage grids would not all fit the shared
+    GPU, so ws=8 runs the per-tick launches here)."""
     from data_paral import synthetic_batch
     from pipeline_parallel import pp_mlp_dims
     from jax_distributed_tuts_amd.models.mlp import MLP
@@ -185,6 +188,8 @@ def test_pipeline_over_xgmi_matches_single_device(tmp_path, ws, dp, n_hidden):
     _spawn8(functools.partial(XW.pp_xgmi, dp=dp, n_hidden=n_hidden), ws, str(tmp_path))
     res = _load(tmp_path, f"ppx{dp}", ws)
     assert all(o["comm"] == "xgmi" and o["count"] == 4 for o in res)
+    one_layer = dp == 1 and n_hidden + 1 == ws + 1 and ws < 8
+    assert all(o["pp_kernel"] == one_layer for o in res), [o["pp_kernel"] for o in res]
     dev = torch.device("cuda", 0)
     cfg = dp_config()
     model = MLP(pp_mlp_dims(cfg, n_hidden), dropout_rate=0.0)
@@ -208,6 +213,31 @@ def test_pipeline_over_xgmi_matches_single_device(tmp_path, ws, dp, n_hidden):
     m, rm = res[0]["metrics"], tr.metrics.cpu()
     assert float(m[1]) == float(rm[1]) and float(m[3]) == float(rm[3])
     assert abs(float(m[0]) - float(rm[0])) <= 2e-3 * abs(float(rm[0])) + 1e-3
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+def test_pipeline_stage_kernel_equals_per_tick_launches(tmp_path, ws):
+    """The in-kernel GPipe step (one persistent launch per stage: in-kernel inbox waits,
+    hand-offs, register-held weight gradients, AdamW at the end) == the per-tick launches
+    (receive / md layer kernel / dX GEMM / send per tick), dropout ON: the same Philox
+    streams, only fp32 summation order differs."""
+    import functools
+
+    n_hidden = ws   # one layer per stage, the head on the last
+    for k in ("1", "0"):
+        spawn(functools.partial(XW.pp_xgmi, dp=1, n_hidden=n_hidden, pp_kernel=k, dropout=0.1, tag=f"k{k}"), ws,
+              str(tmp_path), gpu=True)
+    a, b = _load(tmp_path, "ppx1k1", ws), _load(tmp_path, "ppx1k0", ws)
+    assert all(o["pp_kernel"] for o in a) and not any(o["pp_kernel"] for o in b)
+    for oa, ob in zip(a, b):
+        assert oa["count"] == ob["count"] == 4
+        for k, v in oa["params"].items():
+            d = (v - ob["params"][k]).abs()
+            assert float(d.max()) <= 2 * 1e-3 * 4 + 1e-6, k
+            assert float((d > 5e-5).float().mean()) < 2e-2, (k, float((d > 5e-5).float().mean()))
+    ma, mb_ = a[0]["metrics"], b[0]["metrics"]
+    assert float(ma[1]) == float(mb_[1]) and abs(float(ma[0]) - float(mb_[0])) <= 2e-3 * abs(float(mb_[0])) + 1e-2
+    assert abs(float(ma[2]) - float(mb_[2])) <= 2
 
 
 @pytest.mark.parametrize("ws,n_layers", [(4, 2), (8, 4)])

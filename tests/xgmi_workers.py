@@ -244,9 +244,12 @@ def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2, eps=1e-8):
                           "one_launch": bool(tr.one_launch)})
 
 
-def pp_xgmi(outdir, dp, n_hidden=3, steps=4):
-    """GPipe (dropout off) with the xGMI inbox hand-off (+ the fused xGMI all-reduce
-    on the data axis when dp > 1): one eager step, then multi-step graph replays."""
+def pp_xgmi(outdir, dp, n_hidden=3, steps=4, pp_kernel="1", dropout=0.0, tag=""):
+    """GPipe with the xGMI inbox hand-off (+ the fused xGMI all-reduce on the data axis
+    when dp > 1): one eager step, then multi-step graph replays.  ``pp_kernel`` =
+    JDT_PP_KERNEL: "1" lets a pipeline of one layer per stage run each stage's step as
+    one persistent launch (parallel/pp_kernel.py), "0" keeps the per-tick launches."""
+    os.environ["JDT_PP_KERNEL"] = pp_kernel
     from data_paral import synthetic_batch
     from pipeline_parallel import build_mlp_pipeline
     from jax_distributed_tuts_amd.parallel.dp import shard_batch
@@ -257,19 +260,20 @@ def pp_xgmi(outdir, dp, n_hidden=3, steps=4):
     dev = D.device()
     cfg = dp_config()
     mesh = D.Mesh({"data": dp, "pipe": D.world_size() // dp})
-    tr = build_mlp_pipeline(cfg, mesh, dev, n_hidden_layers=n_hidden, dropout_rate=0.0, num_microbatches=4,
+    tr = build_mlp_pipeline(cfg, mesh, dev, n_hidden_layers=n_hidden, dropout_rate=dropout, num_microbatches=4,
                             comm="xgmi")
     b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
     b = Batch(b.inputs.to(dev), b.labels.to(dev))
     tr.step(b)
-    assert tr.capturable and tr.p2p is not None
+    assert tr.capturable and (tr.p2p is not None or tr.pp_kernel is not None)
     tr.capture(b, steps_per_graph=2)
     tr.run_steps(b, steps - 1)
     torch.cuda.synchronize()
     tr.finalize()
-    _save(outdir, f"ppx{dp}", {"params": {k: v.cpu() for k, v in tr.state.params.state_dict().items()},
-                               "metrics": tr.gather_metrics().cpu(), "comm": tr.comm_backend,
-                               "count": int(tr.state.step_tensor.item())})
+    _save(outdir, f"ppx{dp}{tag}", {"params": {k: v.cpu() for k, v in tr.state.params.state_dict().items()},
+                                    "metrics": tr.gather_metrics().cpu(), "comm": tr.comm_backend,
+                                    "count": int(tr.state.step_tensor.item()),
+                                    "pp_kernel": tr.pp_kernel is not None})
 
 
 def p2p_roundtrip(outdir):

@@ -241,10 +241,17 @@ def autotune_candidates(args, ws: int):
             stages.append([Candidate("stage-kernel=1", {"JDT_PP_KERNEL": "1"},
                                      engaged=lambda tr: getattr(tr, "pp_kernel", None) is not None),
                            Candidate("stage-kernel=0", {"JDT_PP_KERNEL": "0"}, reference=True)])
-        if S > 1:
+        # schedules on concurrent streams: only with a GPU per rank.  Ranks sharing one GPU
+        # time-share its hardware queues; a process that once opened extra queues keeps
+        # them, and every later build of the job then runs 20-50x slower (session 3 of
+        # round 5: GPipe-8 1.9 -> 90 ms/step after a stage-streams candidate was built)
+        from jax_distributed_tuts_amd.runtime.dist import ranks_per_gpu
+
+        own_gpu = ranks_per_gpu() == 1
+        if S > 1 and own_gpu:
             stages.append([Candidate("stage-streams=0", {"JDT_PP_STREAMS": "0"}, reference=True),
                            Candidate("stage-streams=1", {"JDT_PP_STREAMS": "1"})])
-        if S > 1 and args.dp > 1:
+        if S > 1 and args.dp > 1 and own_gpu:
             stages.append([Candidate("overlap-sync=0", {"JDT_PP_OVERLAP_SYNC": "0"}, reference=True),
                            Candidate("overlap-sync=1", {"JDT_PP_OVERLAP_SYNC": "1"})])
         return [st for st in stages if len(st) > 1]

@@ -22,3 +22,10 @@ for n in 2 4; do
   [ $rc -ne 0 ] && { echo "pp$n rc=$rc"; grep -v amdgpu.ids gpurun_out/r5s4/pp$n.log | tail -15; fatal $rc && exit $rc; continue; }
   grep '^{' gpurun_out/r5s4/pp$n.log | python -c 'import json,sys; j=json.loads(sys.stdin.read()); c=j["config"]; print("pp", c["parallelism"], j["value"], j["ms_per_step"], c.get("num_microbatches"), c.get("step_launches",""), json.dumps(j["details"].get("autotune"))[:1500])'
 done
+# A/B: the per-tick GPipe path at 4 shared ranks with and without the autotune's
+# successive builds (session 3: the builds after the first autotune stage ran 20-50x slower)
+for at in off auto; do
+  timeout -k 10 300 python bench.py --gpus 4 --strategy pp --hidden-layers 8 --steps 100 --warmup 10 --autotune $at > gpurun_out/r5s4/pp4g_$at.log 2>&1; rc=$?
+  [ $rc -ne 0 ] && { echo "pp4 generic autotune=$at rc=$rc"; grep -v amdgpu.ids gpurun_out/r5s4/pp4g_$at.log | tail -15; fatal $rc && exit $rc; continue; }
+  grep '^{' gpurun_out/r5s4/pp4g_$at.log | python -c 'import json,sys; j=json.loads(sys.stdin.read()); c=j["config"]; print("pp4 generic autotune='$at'", j["value"], j["ms_per_step"], c.get("num_microbatches"), json.dumps(j["details"].get("autotune"))[:1500])'
+done

@@ -71,7 +71,8 @@ struct PsArgs {
   int* err;                        // this rank's inbox error word (a wait timed out)
   long long timeout;               // s_memrealtime ticks per wait
   // scratch (zero-initialised once by the host)
-  bf16_t* XT;                      // stage 0: X^T [n_mb][784][mbp] bf16
+  bf16_t* XT;                      // stage 0: X^T [PS_MAXNMB][784][PS_MAXMB] bf16 (per microbatch, stride
+                                   // K * mbp), then the bf16 row copy [PS_MAXROWS][784]
   bf16_t* dZ;                      // [n_mb][mb][512] bf16 (published for the dX products)
   float* logits;                   // last stage: [2][n_mb][mb][C] fp32, by step parity
   unsigned* ctr;                   // arrival counters, one 128-byte line each
@@ -135,16 +136,22 @@ __device__ __forceinline__ void ps_raise(unsigned* peer_flags, int slot, unsigne
 }
 
 // All PS_NB workgroups of this launch arrive at counter line `c` (stores drained, one
-// agent-scope add each) and wait for the others: the target is the next multiple of
-// PS_NB above this workgroup's own ticket, so the counter never needs a reset.
-__device__ __forceinline__ void ps_arrive_wait(unsigned* ctr, int c, long long timeout, int* err) {
+// agent-scope add each); the target -- the next multiple of PS_NB above this workgroup's
+// own ticket, so the counter never needs a reset -- is returned (lane 0 of wave 0) for a
+// later ps_wait: work placed between the two overlaps the other workgroups' arrival.
+__device__ __forceinline__ unsigned ps_arrive(unsigned* ctr, int c) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  unsigned target = 0;
   if (threadIdx.x == 0) {
-    unsigned* cnt = ctr + 32 * c;
-    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned target = (old / PS_NB + 1u) * PS_NB;
-    const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(cnt, (short)0, 4, 0x00020000);
+    const unsigned old = __hip_atomic_fetch_add(ctr + 32 * c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    target = (old / PS_NB + 1u) * PS_NB;
+  }
+  return target;
+}
+__device__ __forceinline__ void ps_wait(unsigned* ctr, int c, unsigned target, long long timeout, int* err) {
+  if (threadIdx.x == 0) {
+    const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(ctr + 32 * c, (short)0, 4, 0x00020000);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (!ps_failed(err) && (int)((unsigned)__builtin_amdgcn_raw_buffer_load_b32(cr, 0, 0, CPOL_SC1) - target) < 0) {
       if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout) {
@@ -158,8 +165,11 @@ __device__ __forceinline__ void ps_arrive_wait(unsigned* ctr, int c, long long t
   }
   __syncthreads();
 }
+__device__ __forceinline__ void ps_arrive_wait(unsigned* ctr, int c, long long timeout, int* err) {
+  ps_wait(ctr, c, ps_arrive(ctr, c), timeout, err);
+}
 
-// counter lines: X^T of microbatch i complete (stage 0), logits of i complete (last
+// counter lines: stage 0's bf16 X / X^T pre-pass done, logits of i complete (last
 // stage), dZ of i published (stages > 0)
 __device__ __forceinline__ int ps_ctr_xt(int i) { return i; }
 __device__ __forceinline__ int ps_ctr_lg(int i) { return PS_MAXNMB + i; }
@@ -174,7 +184,9 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
   constexpr int LDWR = PS_N + 8;
   constexpr int NTK = K / 16;                   // 16-wide k tiles of dW^T (49 or 32)
   constexpr int UPW = (NTK + PS_NW - 1) / PS_NW; // dW^T tiles per wave
+  constexpr int TPW = (KS + PS_NW - 1) / PS_NW;  // forward k-steps per wave
   constexpr int LDT = PS_MAXMB + 8;
+  constexpr int MMT = PS_MAXMB / 16;            // 16-row tiles of a microbatch
   static_assert(K % 16 == 0, "dW tiles");
   __shared__ __attribute__((aligned(16))) bf16_t wc[16 * LDWC];                 // W[:, own]^T
   __shared__ __attribute__((aligned(16))) bf16_t wr[FIRST ? 8 : 16 * LDWR];    // W[own rows, :]
@@ -187,6 +199,7 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
   __shared__ float whs[16][PS_C];
   __shared__ float bsh[16];
   __shared__ float red[2][PS_NW];
+  __shared__ unsigned tgt[PS_MAXNMB];                                           // counter targets (lane 0)
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x, j0 = 16 * b;
@@ -196,34 +209,95 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
   const unsigned long long dbase = (unsigned long long)(unsigned)step << 32;
   PS_STAMP(0);
 
-  // ---- 0. this step's weights into LDS (bf16 rounding of the fp32 masters = the shadows)
-  for (int idx = tid; idx < K * 4; idx += PS_NT) {   // W[k][j0 .. j0+16) as 4 float4 per row
-    const int k = idx >> 2, q = idx & 3;
-    const float4 x = *reinterpret_cast<const float4*>(a.p + (long)k * PS_N + j0 + 4 * q);
-    wc[(4 * q + 0) * LDWC + k] = f2bf(x.x);
-    wc[(4 * q + 1) * LDWC + k] = f2bf(x.y);
-    wc[(4 * q + 2) * LDWC + k] = f2bf(x.z);
-    wc[(4 * q + 3) * LDWC + k] = f2bf(x.w);
-  }
-  if constexpr (KP > K)
-    for (int idx = tid; idx < 16 * (KP - K); idx += PS_NT) wc[(idx / (KP - K)) * LDWC + K + idx % (KP - K)] = 0;
-  if constexpr (!FIRST) {
-    for (int idx = tid; idx < 16 * (PS_N / 4); idx += PS_NT) {   // W[j0 + r][0 .. 512)
-      const int r = idx / (PS_N / 4), q = idx % (PS_N / 4);
-      const float4 x = *reinterpret_cast<const float4*>(a.p + (long)(j0 + r) * PS_N + 4 * q);
-      const unsigned lo = (unsigned)f2bf(x.x) | ((unsigned)f2bf(x.y) << 16);
-      const unsigned hi = (unsigned)f2bf(x.z) | ((unsigned)f2bf(x.w) << 16);
-      *reinterpret_cast<uint2*>(&wr[r * LDWR + 4 * q]) = make_uint2(lo, hi);
+  // ---- 0. this step's weights into LDS (bf16 rounding of the fp32 masters = the
+  // shadows): every load first, then the images (a load-store loop would pay one round
+  // trip per iteration)
+  {
+    constexpr int WC4 = (K * 4 + PS_NT - 1) / PS_NT;   // float4 of W[:, own] per thread
+    constexpr int WR4 = FIRST ? 1 : 16 * (PS_N / 4) / PS_NT;
+    float4 wv[WC4], rv[WR4];
+#pragma unroll
+    for (int t = 0; t < WC4; ++t) {
+      const int idx = min(tid + t * PS_NT, K * 4 - 1);
+      wv[t] = *reinterpret_cast<const float4*>(a.p + (long)(idx >> 2) * PS_N + j0 + 4 * (idx & 3));
+    }
+    if constexpr (!FIRST) {
+#pragma unroll
+      for (int t = 0; t < WR4; ++t) {
+        const int idx = tid + t * PS_NT, r = idx / (PS_N / 4), q = idx % (PS_N / 4);
+        rv[t] = *reinterpret_cast<const float4*>(a.p + (long)(j0 + r) * PS_N + 4 * q);
+      }
+    }
+    const float bv = a.pb[j0 + (tid & 15)];
+    float hv = 0.f, hbv = 0.f;
+    if constexpr (LAST) {
+      const int t = min(tid, 16 * PS_C - 1);
+      hv = a.ph[(long)(j0 + t / PS_C) * PS_C + t % PS_C];
+    }
+#pragma unroll
+    for (int t = 0; t < WC4; ++t) {
+      const int idx = tid + t * PS_NT;
+      if (idx < K * 4) {
+        const int k = idx >> 2, q = idx & 3;
+        wc[(4 * q + 0) * LDWC + k] = f2bf(wv[t].x);
+        wc[(4 * q + 1) * LDWC + k] = f2bf(wv[t].y);
+        wc[(4 * q + 2) * LDWC + k] = f2bf(wv[t].z);
+        wc[(4 * q + 3) * LDWC + k] = f2bf(wv[t].w);
+      }
+    }
+    if constexpr (KP > K)
+      for (int idx = tid; idx < 16 * (KP - K); idx += PS_NT) wc[(idx / (KP - K)) * LDWC + K + idx % (KP - K)] = 0;
+    if constexpr (!FIRST) {
+#pragma unroll
+      for (int t = 0; t < WR4; ++t) {
+        const int idx = tid + t * PS_NT, r = idx / (PS_N / 4), q = idx % (PS_N / 4);
+        const unsigned lo = (unsigned)f2bf(rv[t].x) | ((unsigned)f2bf(rv[t].y) << 16);
+        const unsigned hi = (unsigned)f2bf(rv[t].z) | ((unsigned)f2bf(rv[t].w) << 16);
+        *reinterpret_cast<uint2*>(&wr[r * LDWR + 4 * q]) = make_uint2(lo, hi);
+      }
+    }
+    if (tid < 16) bsh[tid] = round_bf(bv);
+    if constexpr (LAST) {
+      (void)hbv;
+      if (tid < 16 * PS_C) whs[tid / PS_C][tid % PS_C] = round_bf(hv);
+      // re-arm the other parity's logit accumulator (the previous step's, fully consumed)
+      if (b == 0)
+        for (int idx = tid; idx < n_mb * mb * PS_C; idx += PS_NT) a.logits[(long)(par ^ 1) * PS_MAXROWS * PS_C + idx] = 0.f;
     }
   }
-  if (tid < 16) bsh[tid] = round_bf(a.pb[j0 + tid]);
-  if constexpr (LAST) {
-    if (tid < 16 * PS_C) whs[tid / PS_C][tid % PS_C] = round_bf(a.ph[(long)(j0 + tid / PS_C) * PS_C + tid % PS_C]);
-    // re-arm the other parity's logit accumulator (the previous step's, fully consumed)
-    if (b == 0)
-      for (int idx = tid; idx < n_mb * mb * PS_C; idx += PS_NT) a.logits[(long)(par ^ 1) * PS_MAXROWS * PS_C + idx] = 0.f;
+  // stage 0: the step's data once in bf16, row-major (the forward's A operand) and per
+  // microbatch transposed (the dW operand): workgroup b converts rows [4b, 4b + 4)
+  // (n_mb * mb == 128, host-checked), write-through, then every workgroup meets
+  if constexpr (FIRST) {
+    const int rr = 4 * b, i = rr / mb, rl = rr - i * mb;
+    for (int k4 = tid; k4 < K / 4; k4 += PS_NT) {
+      float4 x[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = *reinterpret_cast<const float4*>(a.X + (long)(rr + e) * K + 4 * k4);
+      const __amdgpu_buffer_rsrc_t xbr = ps_rsrc(a.XT + (long)PS_MAXNMB * K * PS_MAXMB, (long)PS_MAXROWS * K * 2);
+      const __amdgpu_buffer_rsrc_t xtr = ps_rsrc(a.XT + (long)i * K * mbp, (long)K * mbp * 2);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const unsigned lo = (unsigned)f2bf(x[e].x) | ((unsigned)f2bf(x[e].y) << 16);
+        const unsigned hi = (unsigned)f2bf(x[e].z) | ((unsigned)f2bf(x[e].w) << 16);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned,
+                                                                 make_uint2(lo, hi)),
+                                              xbr, (int)(((long)(rr + e) * K + 4 * k4) * 2), 0, CPOL_SC1);
+      }
+      const float* xs = &x[0].x;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {   // feature 4 k4 + c of the 4 rows: 8 contiguous bytes of X^T
+        const unsigned lo = (unsigned)f2bf(xs[0 * 4 + c]) | ((unsigned)f2bf(xs[1 * 4 + c]) << 16);
+        const unsigned hi = (unsigned)f2bf(xs[2 * 4 + c]) | ((unsigned)f2bf(xs[3 * 4 + c]) << 16);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned,
+                                                                 make_uint2(lo, hi)),
+                                              xtr, (int)(((long)(4 * k4 + c) * mbp + rl) * 2), 0, CPOL_SC1);
+      }
+    }
+    ps_arrive_wait(a.ctr, ps_ctr_xt(0), a.timeout, a.err);
+  } else {
+    __syncthreads();
   }
-  __syncthreads();
   PS_STAMP(1);
 
   // ---- 1. forward ticks
@@ -231,67 +305,47 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
   for (int i = 0; i < n_mb; ++i) {
     const int r0 = i * mb;   // this microbatch's rows of the step
     if constexpr (!FIRST) ps_wait_slot(a.flag_mine, i, epoch, a.timeout, a.err);
-    // Z partials: wave w takes k-steps [w KS / 4, (w+1) KS / 4) of every 16-row tile
+    if (i == 1) PS_STAMP(19);
+    // Z partials: wave w takes k-steps [w KS / 4, (w+1) KS / 4) of every 16-row tile; all
+    // of its A fragments are loaded first (bf16 rows: stage 0's converted copy, else the
+    // inbox slot written by the previous stage)
     const int ks0 = (w * KS) / PS_NW, ks1 = ((w + 1) * KS) / PS_NW;
-    f32x4 acc[PS_MAXMB / 16];
+    f32x4 acc[MMT];
 #pragma unroll
-    for (int mt = 0; mt < PS_MAXMB / 16; ++mt) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if constexpr (FIRST) {
-      for (int ks = ks0; ks < ks1; ++ks) {
-        const int k = ks * 32 + 8 * (lane >> 4);
-        const bf16x8 bf = *reinterpret_cast<const bf16x8*>(&wc[(lane & 15) * LDWC + k]);
+    for (int mt = 0; mt < MMT; ++mt) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    {
+      const __amdgpu_buffer_rsrc_t xin =
+          FIRST ? ps_rsrc(a.XT + (long)PS_MAXNMB * K * PS_MAXMB + (long)r0 * K, (long)mb * K * 2)
+                : ps_rsrc(a.in_mine + (long)i * a.slot_bytes, (long)mb * PS_N * 2);
+      bf16x8 af[MMT][TPW];
 #pragma unroll
-        for (int mt = 0; mt < PS_MAXMB / 16; ++mt) {
-          if (mt >= MT) break;
-          bf16x8 af = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-          if (k < K) {
-            const float* xr = a.X + (long)(r0 + mt * 16 + (lane & 15)) * K + k;
-            const float4 x0 = *reinterpret_cast<const float4*>(xr), x1 = *reinterpret_cast<const float4*>(xr + 4);
-            af[0] = (short)f2bf(x0.x); af[1] = (short)f2bf(x0.y); af[2] = (short)f2bf(x0.z); af[3] = (short)f2bf(x0.w);
-            af[4] = (short)f2bf(x1.x); af[5] = (short)f2bf(x1.y); af[6] = (short)f2bf(x1.z); af[7] = (short)f2bf(x1.w);
-          }
-          acc[mt] = mfma16x16x32(af, bf, acc[mt]);
-        }
-      }
-      // X^T of this microbatch for the backward's dW: workgroup b converts input features
-      // [25 b, 25 b + 25) (write-through: the other workgroups read them after a counter)
-      const __amdgpu_buffer_rsrc_t xt = ps_rsrc(a.XT + (long)i * K * mbp, (long)K * mbp * 2);
-      for (int idx = tid; idx < 25 * (mb / 8); idx += PS_NT) {
-        const int kk = 25 * b + idx / (mb / 8), r8 = (idx % (mb / 8)) * 8;
-        if (kk >= K) continue;
-        unsigned q[4];
+      for (int t = 0; t < TPW; ++t)
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          q[e] = (unsigned)f2bf(a.X[(long)(r0 + r8 + 2 * e) * K + kk]) |
-                 ((unsigned)f2bf(a.X[(long)(r0 + r8 + 2 * e + 1) * K + kk]) << 16);
-        ps_store16<CPOL_SC1>(xt, ((long)kk * mbp + r8) * 2, (u32x4){q[0], q[1], q[2], q[3]});
-      }
-    } else {
-      const __amdgpu_buffer_rsrc_t xin = ps_rsrc(a.in_mine + (long)i * a.slot_bytes, (long)mb * PS_N * 2);
-      bf16x8 af[PS_MAXMB / 16][(KS + PS_NW - 1) / PS_NW];
-#pragma unroll
-      for (int t = 0; t < (KS + PS_NW - 1) / PS_NW; ++t)
-#pragma unroll
-        for (int mt = 0; mt < PS_MAXMB / 16; ++mt) {
+        for (int mt = 0; mt < MMT; ++mt) {
           const int ks = min(ks0 + t, ks1 - 1), row = min(mt * 16 + (lane & 15), mb - 1);
-          af[mt][t] = __builtin_bit_cast(bf16x8, ps_load16<CPOL_SYS>(xin, ((long)row * PS_N + ks * 32 + 8 * (lane >> 4)) * 2));
+          // k past K (stage 0's 784 = 24.5 k-steps) reads the next row or, past the
+          // buffer, zero (bounds check): finite values times wc's zero padding
+          const long off = ((long)row * K + ks * 32 + 8 * (lane >> 4)) * 2;
+          af[mt][t] = FIRST ? __builtin_bit_cast(bf16x8, ps_load16<CPOL_SC1>(xin, off))
+                            : __builtin_bit_cast(bf16x8, ps_load16<CPOL_SYS>(xin, off));
         }
 #pragma unroll
-      for (int t = 0; t < (KS + PS_NW - 1) / PS_NW; ++t) {
+      for (int t = 0; t < TPW; ++t) {
         const int ks = ks0 + t;
         if (ks >= ks1) break;
         const bf16x8 bf = *reinterpret_cast<const bf16x8*>(&wc[(lane & 15) * LDWC + ks * 32 + 8 * (lane >> 4)]);
 #pragma unroll
-        for (int mt = 0; mt < PS_MAXMB / 16; ++mt)
+        for (int mt = 0; mt < MMT; ++mt)
           if (mt < MT) acc[mt] = mfma16x16x32(af[mt][t], bf, acc[mt]);
       }
     }
 #pragma unroll
-    for (int mt = 0; mt < PS_MAXMB / 16; ++mt)
+    for (int mt = 0; mt < MMT; ++mt)
       if (mt < MT)
 #pragma unroll
         for (int e = 0; e < 4; ++e) part[w][mt * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[mt][e];
     __syncthreads();
+    if (i == 1) PS_STAMP(20);
     // bias + SiLU + dropout, one 4-row group per thread (the md kernels' streams)
     {
       const int g4 = tid >> 4, c = tid & 15;
@@ -321,8 +375,10 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
       }
     }
     __syncthreads();
+    if (i == 1) PS_STAMP(21);
     if constexpr (LAST) {
-      // the head's partial logits of the owned 16 hidden units (+ b_h from workgroup 0)
+      // the head's partial logits of the owned 16 hidden units (+ b_h from workgroup 0);
+      // the arrival is waited for in the backward (the next microbatch goes on at once)
       float* lg = a.logits + (long)par * PS_MAXROWS * PS_C + (long)r0 * PS_C;
       for (int idx = tid; idx < mb * PS_C; idx += PS_NT) {
         const int r = idx / PS_C, c = idx % PS_C;
@@ -331,7 +387,8 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
         for (int n = 0; n < 16; ++n) s += bf2f(ht[r][n]) * whs[n][c];
         atomicAdd(lg + idx, s);
       }
-      ps_arrive_wait(a.ctr, ps_ctr_lg(i), a.timeout, a.err);
+      const unsigned t_ = ps_arrive(a.ctr, ps_ctr_lg(i));
+      if (tid == 0) tgt[i] = t_;
     } else {
       // H[:, own] and H^T[own, :] into the next stage's inbox slot i, then this block's flag
       const __amdgpu_buffer_rsrc_t o = ps_rsrc(a.in_next + (long)i * a.slot_bytes, a.slot_bytes);
@@ -352,9 +409,6 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
       }
       ps_raise(a.flag_next, i, epoch);
     }
-    if constexpr (FIRST) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // X^T slice drained before anyone waits on it
-    }
     if (i < 8) PS_STAMP(2 + i);
   }
 
@@ -365,15 +419,27 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
   float dba = 0.f;                   // threads < 16: db[j0 + tid]
   float dwh = 0.f, dbh = 0.f;        // last stage: threads < 160: dW_h[j0 + t/C][t%C]; b == 0, t < C: db_h
   float l_loss = 0.f, l_corr = 0.f;
-  if constexpr (FIRST) {
-    for (int i = 0; i < n_mb; ++i) ps_arrive_wait(a.ctr, ps_ctr_xt(i), a.timeout, a.err);
-  }
   for (int i = n_mb - 1; i >= 0; --i) {
     const int r0 = i * mb;
+    // the dW operand (X^T rows of microbatch i: stage 0's transposed copy, else the inbox
+    // slot's H^T part) is already there: its loads fly while this tick waits for dH
+    const bf16_t* xtb = FIRST ? a.XT + (long)i * K * mbp
+                              : reinterpret_cast<const bf16_t*>(a.in_mine + (long)i * a.slot_bytes + (long)mb * PS_N * 2);
+    const __amdgpu_buffer_rsrc_t xr = ps_rsrc(xtb, (long)K * mbp * 2);
+    bf16x8 xb[UPW][PS_MAXMB / 32];
+#pragma unroll
+    for (int u = 0; u < UPW; ++u)
+#pragma unroll
+      for (int rs = 0; rs < PS_MAXMB / 32; ++rs) {
+        const int t = min(w + PS_NW * u, NTK - 1);
+        const long off = ((long)(16 * t + (lane & 15)) * mbp + min(rs, mbp / 32 - 1) * 32 + 8 * (lane >> 4)) * 2;
+        xb[u][rs] = FIRST ? __builtin_bit_cast(bf16x8, ps_load16<CPOL_SC1>(xr, off))
+                          : __builtin_bit_cast(bf16x8, ps_load16<CPOL_SYS>(xr, off));
+      }
     // dH[:, own] -> dZ = dH * G -> dzT (bf16, as the md kernels round dZ)
     if constexpr (LAST) {
-      // CE of every row of microbatch i from the complete logits (every workgroup passed
-      // the microbatch's logit counter in the forward)
+      ps_wait(a.ctr, ps_ctr_lg(i), tgt[i], a.timeout, a.err);
+      // CE of every row of microbatch i from the complete logits
       const __amdgpu_buffer_rsrc_t lr =
           ps_rsrc(a.logits + (long)par * PS_MAXROWS * PS_C + (long)r0 * PS_C, (long)mb * PS_C * 4);
       if (tid < mb) {
@@ -442,6 +508,7 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
         *reinterpret_cast<uint2*>(&dzT[c * LDT + 4 * g4]) = make_uint2(pk[0], pk[1]);
       }
     }
+    if (i == 1) PS_STAMP(22);
     // zero padding rows [mb, mbp) of dzT for the 32-deep dW k-steps
     for (int idx = tid; idx < 16 * (mbp - mb); idx += PS_NT) dzT[(idx / (mbp - mb)) * LDT + mb + idx % (mbp - mb)] = 0;
     __syncthreads();
@@ -450,38 +517,11 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
       for (int r = 0; r < mb; ++r) s += bf2f(dzT[tid * LDT + r]);
       dba += s;
     }
-    // dW^T[own cols][k] += dZ^T X: A = dzT (LDS), B = X^T rows (stage 0: XT scratch; else the
-    // inbox slot's H^T part), wave w takes k tiles w, w + 4, ...
-    {
-      const bf16_t* xtb = FIRST ? a.XT + (long)i * K * mbp
-                                : reinterpret_cast<const bf16_t*>(a.in_mine + (long)i * a.slot_bytes + (long)mb * PS_N * 2);
-      const __amdgpu_buffer_rsrc_t xr = ps_rsrc(xtb, (long)K * mbp * 2);
-      constexpr int cpol = FIRST ? CPOL_SC1 : CPOL_SYS;
-      bf16x8 dza[PS_MAXMB / 32];
-#pragma unroll
-      for (int rs = 0; rs < PS_MAXMB / 32; ++rs)
-        dza[rs] = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDT + min(rs, mbp / 32 - 1) * 32 + 8 * (lane >> 4)]);
-      bf16x8 xb[UPW][PS_MAXMB / 32];
-#pragma unroll
-      for (int u = 0; u < UPW; ++u)
-#pragma unroll
-        for (int rs = 0; rs < PS_MAXMB / 32; ++rs) {
-          const int t = min(w + PS_NW * u, NTK - 1);
-          xb[u][rs] = __builtin_bit_cast(
-              bf16x8, ps_load16<cpol>(xr, ((long)(16 * t + (lane & 15)) * mbp + min(rs, mbp / 32 - 1) * 32 + 8 * (lane >> 4)) * 2));
-        }
-#pragma unroll
-      for (int u = 0; u < UPW; ++u) {
-        if (w + PS_NW * u >= NTK) break;
-#pragma unroll
-        for (int rs = 0; rs < PS_MAXMB / 32; ++rs)
-          if (rs < mbp / 32) dwa[u] = mfma16x16x32(dza[rs], xb[u][rs], dwa[u]);
-      }
-    }
+    // publish dZ[:, own] (write-through) and arrive -- not stage 0, whose input needs no
+    // gradient -- then the dW MFMAs overlap the other workgroups' arrival
+    const __amdgpu_buffer_rsrc_t zr = ps_rsrc(a.dZ + (long)i * mb * PS_N, (long)mb * PS_N * 2);
+    unsigned tz = 0;
     if constexpr (!FIRST) {
-      // publish dZ[:, own] (write-through), meet the stage's other workgroups, then
-      // dX[:, own rows] = dZ W[own rows, :]^T -> the previous stage's inbox slot n_mb + i
-      const __amdgpu_buffer_rsrc_t zr = ps_rsrc(a.dZ + (long)i * mb * PS_N, (long)mb * PS_N * 2);
       if (tid < 2 * mb) {
         const int r = tid >> 1, h = (tid & 1) * 8;
         unsigned q[4];
@@ -490,28 +530,48 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
           q[e] = (unsigned)dzT[(h + 2 * e) * LDT + r] | ((unsigned)dzT[(h + 2 * e + 1) * LDT + r] << 16);
         ps_store16<CPOL_SC1>(zr, ((long)r * PS_N + j0 + h) * 2, (u32x4){q[0], q[1], q[2], q[3]});
       }
-      ps_arrive_wait(a.ctr, ps_ctr_dz(i), a.timeout, a.err);
+      tz = ps_arrive(a.ctr, ps_ctr_dz(i));
+    }
+    // dW^T[own cols][k] += dZ^T X (A = dzT, B = the prefetched X^T rows); wave w takes
+    // k tiles w, w + 4, ...
+    {
+      bf16x8 dza[PS_MAXMB / 32];
+#pragma unroll
+      for (int rs = 0; rs < PS_MAXMB / 32; ++rs)
+        dza[rs] = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDT + min(rs, mbp / 32 - 1) * 32 + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int u = 0; u < UPW; ++u) {
+        if (w + PS_NW * u >= NTK) break;
+#pragma unroll
+        for (int rs = 0; rs < PS_MAXMB / 32; ++rs)
+          if (rs < mbp / 32) dwa[u] = mfma16x16x32(dza[rs], xb[u][rs], dwa[u]);
+      }
+    }
+    if (i == 1) PS_STAMP(23);
+    if constexpr (!FIRST) {
+      // dX[:, own rows] = dZ W[own rows, :]^T -> the previous stage's inbox slot n_mb + i
+      ps_wait(a.ctr, ps_ctr_dz(i), tz, a.timeout, a.err);
       // wave w: k-steps [4w, 4w + 4) of the 512-deep product, every 16-row tile
-      bf16x8 za[PS_MAXMB / 16][4];
+      bf16x8 za[MMT][4];
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int mt = 0; mt < PS_MAXMB / 16; ++mt) {
+        for (int mt = 0; mt < MMT; ++mt) {
           const int row = min(mt * 16 + (lane & 15), mb - 1);
           za[mt][t] = __builtin_bit_cast(bf16x8, ps_load16<CPOL_SC1>(zr, ((long)row * PS_N + (4 * w + t) * 32 + 8 * (lane >> 4)) * 2));
         }
-      f32x4 acc[PS_MAXMB / 16];
+      f32x4 acc[MMT];
 #pragma unroll
-      for (int mt = 0; mt < PS_MAXMB / 16; ++mt) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int mt = 0; mt < MMT; ++mt) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const bf16x8 bf = *reinterpret_cast<const bf16x8*>(&wr[(lane & 15) * LDWR + (4 * w + t) * 32 + 8 * (lane >> 4)]);
 #pragma unroll
-        for (int mt = 0; mt < PS_MAXMB / 16; ++mt)
+        for (int mt = 0; mt < MMT; ++mt)
           if (mt < MT) acc[mt] = mfma16x16x32(za[mt][t], bf, acc[mt]);
       }
 #pragma unroll
-      for (int mt = 0; mt < PS_MAXMB / 16; ++mt)
+      for (int mt = 0; mt < MMT; ++mt)
         if (mt < MT)
 #pragma unroll
           for (int e = 0; e < 4; ++e) part[w][mt * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[mt][e];
@@ -647,7 +707,7 @@ JDT_API int jdt_pp_stage(const PsArgs* args, int first, int last, void* stream) 
     return -2;
   if (!first && (!a.in_mine || !a.flag_mine || !a.in_prev || !a.flag_prev || !a.dZ)) return -2;
   if (!last && (!a.in_next || !a.flag_next)) return -2;
-  if (first && (!a.X || !a.XT)) return -2;
+  if (first && (!a.X || !a.XT || a.n_mb * a.mb != PS_MAXROWS)) return -2;
   if (last && (!a.labels || !a.logits || !a.ph || !a.phb || !a.mslot || !a.running)) return -2;
   const long need = (long)a.mb * PS_N * 2 + (long)PS_N * ((a.mb + 31) & ~31) * 2;
   if (a.slot_bytes < need) return -2;

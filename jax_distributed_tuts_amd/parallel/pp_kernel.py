@@ -88,7 +88,7 @@ def local_ok(trainer, mb: int) -> bool:
         return False
     if trainer.S < 2 or trainer.n_dp != 1 or not isinstance(trainer.state.tx, AdamW):
         return False
-    if not (16 <= mb <= 64 and mb % 16 == 0 and 1 <= n_mb <= 8 and n_mb * mb <= 128):
+    if not (16 <= mb <= 64 and mb % 16 == 0 and 1 <= n_mb <= 8 and n_mb * mb == 128):
         return False
     if 2 * n_mb > int(_lib.lib().jdt_p2p_max_slots()):
         return False
@@ -133,10 +133,11 @@ class PPStageKernel:
         nxt = peer(s + 1) if s < S - 1 else (None, None, None)
         P, st, model = trainer.state.params, trainer.state, trainer.model
         o = st.opt_state
-        mbp = (mb + 31) // 32 * 32
         bf = dict(dtype=torch.bfloat16, device=dev)
-        # scratch (zeroed once: padding rows are read as zeros by the dW k-steps)
-        self.XT = torch.zeros(self.n_mb, 784, mbp, **bf) if self.first else None
+        # scratch (zeroed once: padding rows are read as zeros by the dW k-steps); stage 0:
+        # the per-microbatch X^T blocks [n_mb][784][mbp] in an 8 x 784 x 64 region, then the
+        # step's bf16 row copy [128][784] (ops/csrc/pp_stage.hip pre-pass)
+        self.XT = torch.zeros(8 * 784 * 64 + 128 * 784, **bf) if self.first else None
         self.dZ = torch.zeros(self.n_mb, mb, H, **bf)
         self.logits = torch.zeros(2, 128, C_HEAD, dtype=torch.float32, device=dev) if self.last else None
         self.ctr = torch.zeros(64 * 32, dtype=torch.int32, device=dev)

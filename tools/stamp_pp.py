@@ -72,7 +72,10 @@ def main():
     us = lambda k: (med(k) - t0) / 100.0   # noqa: E731   ticks -> us
     row = {"stage": D.rank(), "start": us(0), "staged": us(1),
            "fwd": [round(us(2 + i), 2) for i in range(min(n, 8))],
-           "bwd": [round(us(10 + i), 2) for i in reversed(range(min(n, 8)))], "adam": us(18)}
+           "bwd": [round(us(10 + i), 2) for i in reversed(range(min(n, 8)))], "adam": us(18),
+           # microbatch 1's sub-tick marks: forward inputs there / MFMAs done / epilogue done,
+           # backward dZ formed / dW MFMAs done
+           "sub": [round(us(k), 2) for k in range(19, 24)]}
     rows = [None] * S
     torch.distributed.all_gather_object(rows, row)
     if D.rank() == 0:
@@ -82,6 +85,8 @@ def main():
             print(f"  stage {r['stage']}: start {r['start']:7.2f} staged {r['staged']:7.2f} fwd ticks end "
                   + " ".join(f"{x:7.2f}" for x in r["fwd"]) + "  bwd ticks end "
                   + " ".join(f"{x:7.2f}" for x in r["bwd"]) + f"  adam {r['adam']:7.2f}")
+            print(f"    mb1 fwd: inputs {r['sub'][0]:7.2f} mfma {r['sub'][1]:7.2f} epilogue {r['sub'][2]:7.2f} sent "
+                  f"{r['fwd'][1] if len(r['fwd']) > 1 else 0:7.2f} | bwd: dZ {r['sub'][3]:7.2f} dW {r['sub'][4]:7.2f}")
         f_last = rows[-1]["fwd"][-1] - rows[0]["fwd"][0]
         ticks_f = n + S - 2
         b_first = rows[0]["bwd"][-1] - rows[-1]["bwd"][0]

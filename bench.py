@@ -225,9 +225,17 @@ def autotune_candidates(args, ws: int):
             return [[Candidate("deep-exchange", {"JDT_DP_DEEP_TX": "1"}, replicated=True, engaged=one),
                      Candidate("collective", {"JDT_DP_DEEP_TX": "0"}, reference=True, replicated=True)]]
         return []
-    if args.strategy == "fsdp" and args.accum == "kernel" and args.num_layers == 2:
-        return [[Candidate("one-launch", {"JDT_FSDP_AHEAD": "1"}, engaged=one),
-                 Candidate("three-launch", {"JDT_FSDP_AHEAD": "0"}, reference=True)]]
+    if args.strategy == "fsdp" and args.accum == "kernel":
+        if args.num_layers == 2:
+            return [[Candidate("one-launch", {"JDT_FSDP_AHEAD": "1"}, engaged=one),
+                     Candidate("three-launch", {"JDT_FSDP_AHEAD": "0"}, reference=True)]]
+        if args.optimizer == "adamw":
+            # deep: one backward launch per hidden layer sending its partials to the shard
+            # owners (sharded AdamW in-kernel, csrc/mlp_deep.hip md_bwd FX) vs the step
+            # collective (xg_fsdp_kernel)
+            return [[Candidate("deep-exchange", {"JDT_FSDP_DEEP_FX": "1"}, engaged=one),
+                     Candidate("collective", {"JDT_FSDP_DEEP_FX": "0"}, reference=True)]]
+        return []
     if args.strategy == "pp":
         S = ws // args.dp
         stages = []
@@ -472,7 +480,14 @@ def main():
                                      + (" + xGMI all-reduce/AdamW" if ws > 1 else ""))
     if args.strategy == "fsdp" and getattr(tr, "_ahead", None):
         nh = getattr(tr.fused, "nh", None)
-        desc["step_launches"] = f"{2 * nh - 1} (layer-0 run-ahead md_bwd)" if nh else "1 (run-ahead mlp2_bwd)"
+        tx_ = (", partials to the shard owners, sharded AdamW in the launches"
+               if getattr(tr, "one_launch", False) else "")
+        desc["step_launches"] = (f"{2 * nh - 1} (layer-0 run-ahead md_bwd{tx_})" if nh
+                                 else f"1 (run-ahead mlp2_bwd{tx_})")
+    elif args.strategy == "fsdp" and getattr(tr, "fused", None) is not None and ws > 1:
+        nh = getattr(tr.fused, "nh", None)
+        desc["step_launches"] = ((f"{2 * nh} (md_fwd / md_bwd per layer)" if nh else "2 (mlp2_fwd + mlp2_bwd)")
+                                 + " + xGMI FSDP step collective")
     if args.strategy == "pp":
         desc["single_stage_mode"] = tr.single_stage_mode  # how a 1-stage pipeline ran its microbatches
         desc["stage_streams"] = tr.stage_streams          # concurrent microbatch chains per stage

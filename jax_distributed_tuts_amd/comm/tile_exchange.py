@@ -42,6 +42,7 @@ _lib.declare("jdt_mlp2_ahead_tx_ok", c_int, [c_int, c_int, c_int, c_int])
 _lib.declare("jdt_tx_selftest", c_int, [c_void_p, c_int, ctypes.c_uint, c_void_p, c_void_p])
 _lib.declare("jdt_tx_reset", c_int, [c_void_p])
 _lib.declare("jdt_tx_error", ctypes.c_uint, [c_void_p])
+_lib.declare("jdt_md_fx_ok", c_int, [c_int, c_int])
 _lib.declare("jdt_md_tx_ok", c_int, [c_int, c_int])
 SELFTEST_TILES = 64   # 64 workgroups per rank: 8 ranks' self-test grids fit one shared GPU
 
@@ -137,6 +138,11 @@ def deep_tx_ok(rows: int, ranks_on_this_gpu: int) -> bool:
     """The deep (>= 2 hidden layers) engine's exchanging backward launches all resident
     with ``ranks_on_this_gpu`` ranks' grids per GPU (csrc/mlp_deep.hip jdt_md_tx_ok)."""
     return bool(_lib.lib().jdt_md_tx_ok(int(rows), int(ranks_on_this_gpu)))
+
+
+def deep_fx_ok(rows: int, ranks_on_this_gpu: int) -> bool:
+    """The deep engine's FSDP form (md_bwd FX) resident as deep_tx_ok."""
+    return bool(_lib.lib().jdt_md_fx_ok(int(rows), int(ranks_on_this_gpu)))
 
 
 def fx_owner_span(world: int, rows: int = 784, chunk: int = 112) -> int:

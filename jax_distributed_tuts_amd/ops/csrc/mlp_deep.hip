@@ -131,6 +131,9 @@ struct MdArgs {
   const TxArgs* tx;
   int tx_base;
   int tx_shared;   // ranks share this GPU: the two-workgroups-per-CU variants (jdt_md_tx_ok)
+  int tx_fsdp;     // the FSDP form (md_bwd FX): a.pW ... are this rank's LOCAL shards; 2: this
+                   // layer's W is sharded along dim 1 (columns; the reference rule for the
+                   // square hidden kernels), else along dim 0 (rows)
 };
 
 // Slots 0-4: s_memrealtime at the kernel's phase ends (tools/stamp_deep.py).
@@ -383,14 +386,18 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
 // a few spills) is the variant for ranks SHARING one GPU -- both ranks' launches must be
 // resident at once for the exchange's waits (jdt_md_tx_ok); with a GPU per rank one
 // workgroup per CU suffices and WPE = 1 keeps the unconstrained allocation.
+// FX (with TX): the FSDP form -- every gradient element goes to the rank that owns its
+// row (the reference's dim-0 shards), the owner applies the SHARDED AdamW on its local
+// state and hands the updated value back (as mlp_fused.hip mlp2_bwd FX).
 template <int K_IN, bool TOP, int C, int KC, int NN, bool XCD, bool BND = false, bool AHEAD = false, bool TX = false,
-          int WPE = 1>
+          int WPE = 1, bool FX = false>
 __global__ void __launch_bounds__(MD_NT) __attribute__((amdgpu_waves_per_eu(WPE))) md_bwd_kernel(MdArgs a) {
   constexpr int NT = MD_NT, NW = MD_NW, MPM = MD_MPM;
   constexpr int LDM = MPM + 8;
   constexpr int NTILE = KC / 16;           // dW output tiles (one per wave)
   constexpr int NKS = NN / 32;             // k-steps of the dZ_{i+1} W_{i+1}^T product
   static_assert(KC % 16 == 0 && K_IN % KC == 0 && NTILE <= NW - 1, "tile plan");
+  static_assert(!FX || (TX && !BND), "FX is the FSDP form of the exchanging backward");
   static_assert((MPM / 4) * 16 == NT, "one 4-row group per thread");
   __shared__ float dlog[TOP ? MPM : 1][C + 1];
   __shared__ __attribute__((aligned(16))) bf16_t dzT[16 * LDM];
@@ -512,6 +519,17 @@ __global__ void __launch_bounds__(MD_NT) __attribute__((amdgpu_waves_per_eu(WPE)
   const bool aux = chunk0 && w == NW - 1;
   const int ac = lane & 15;
   float bp[4], bm[4], bvv[4], qp = 0.f, qm = 0.f, qv = 0.f;
+  // FX: this rank R of W owns W rows [R K/W, (R+1) K/W) and bias / head rows
+  // [R N/W, (R+1) N/W); its AdamW state (a.pW ... a.vbh) is that LOCAL shard
+  int fx_R = 0, fx_W = 1, fx_rpq = K_IN, fx_hpq = 512;
+  bool fx_col = false;   // W column-sharded: the whole tile has one owner (j0 / hpq)
+  if constexpr (FX) {
+    fx_R = __builtin_amdgcn_readfirstlane(a.tx->rank);
+    fx_W = __builtin_amdgcn_readfirstlane(a.tx->world);
+    fx_rpq = K_IN / fx_W;
+    fx_hpq = N / fx_W;
+    fx_col = __builtin_amdgcn_readfirstlane(a.tx_fsdp) == 2;
+  }
   {
     const bool hw = TOP && aux;   // wave-uniform
     const float* sp = hw ? (fo ? a.pWh : a.gWh) : (fo ? a.pW : a.gW);
@@ -520,12 +538,17 @@ __global__ void __launch_bounds__(MD_NT) __attribute__((amdgpu_waves_per_eu(WPE)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int n = (lane >> 4) * 4 + e;
-      const long idx = hw ? (long)(j0 + n) * C + min(ac, C - 1) : (long)(trow0 + e) * N + tcol;
+      // (FX: clamped into the local shard; values of rows this rank does not own unused)
+      const int hrow = FX ? min(max(j0 + n - fx_R * fx_hpq, 0), fx_hpq - 1) : j0 + n;
+      const int wrow = (FX && !fx_col) ? min(max(trow0 + e - fx_R * fx_rpq, 0), fx_rpq - 1) : trow0 + e;
+      const long idx = hw ? (long)hrow * C + min(ac, C - 1)
+                          : (FX && fx_col) ? (long)wrow * fx_hpq + min(max(tcol - fx_R * fx_hpq, 0), fx_hpq - 1)
+                                           : (long)wrow * N + tcol;
       op[e] = sp[idx]; om[e] = sm[idx]; ov[e] = sv[idx];
       const float* bq = fo ? a.pb : a.gb;
       const float* bmq = fo ? a.mb : a.gb;
       const float* bvq = fo ? a.vb : a.gb;
-      bp[e] = bq[j0 + n]; bm[e] = bmq[j0 + n]; bvv[e] = bvq[j0 + n];
+      bp[e] = bq[hrow]; bm[e] = bmq[hrow]; bvv[e] = bvq[hrow];
     }
     if constexpr (TOP) {
       const int lq = min(lane, C - 1);
@@ -737,7 +760,7 @@ __global__ void __launch_bounds__(MD_NT) __attribute__((amdgpu_waves_per_eu(WPE)
   // metric slots -- all-reduced with the same tile of the other ranks' launches before
   // the optimizer (common.h tx_tile; payload as mlp_fused.hip's)
   float mval = 0.f;
-  if constexpr (TX) {
+  if constexpr (TX && !FX) {
     if (TOP && lead && tid < 4) {
       float L = 0.f, Cr = 0.f;
       for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
@@ -772,74 +795,251 @@ __global__ void __launch_bounds__(MD_NT) __attribute__((amdgpu_waves_per_eu(WPE)
       if (TOP && lead && lane < C) ab2[0] = vs;
     }
   }
-  // the step parity as a scalar for the parity-selected store resources (the step was the
-  // first load of the launch and is long back; per lane it made them waterfall loops)
-  const int par_s = __builtin_amdgcn_readfirstlane(par);
-  if (w < NTILE) {
-    bf16_t* Wsn = const_cast<bf16_t*>(par_s ? a.Ws0 : a.Ws1);   // next step's parity of the row-major shadow
-    const __amdgpu_buffer_rsrc_t wsn_r = __builtin_amdgcn_make_buffer_rsrc(Wsn, (short)0, 0x7fffffff, 0x00020000);
-    unsigned wtp[2] = {0u, 0u};
+  if constexpr (FX) {
+    // FSDP at N > 1 (md_bwd FX): every element's partial goes to the rank owning its row,
+    // the owner sums in rank order, applies the sharded AdamW (local state, prefetched at
+    // local indices above) and pushes the updated fp32 value to every rank; the
+    // replicated b_h and the metric slots are summed by rank T % W and pushed back as
+    // sums (every rank updates its own copy).  Then every rank holds the whole updated
+    // tile and writes the shadows / hand-offs the next forward reads.
+    const TxArgs* X = a.tx;
+    const int R = fx_R, W = fx_W;
+    const int T = a.tx_base + bx * NCH + by;
+    const long pay = __builtin_amdgcn_readfirstlane(X->pay), tiles = __builtin_amdgcn_readfirstlane(X->tiles);
+    const unsigned long long tb = (unsigned long long)pay * 4ull;
+    const unsigned epoch = (unsigned)step + 1u;
+    const long AG = tiles * TX_MAX_RANKS + tiles;   // flag base of the updated-value hand-back
+    const int ob = j0 / fx_hpq, orep = T % W;
+    const int o_lo = fx_col ? ob : kc0 / fx_rpq, o_hi = fx_col ? ob : (kc0 + KC - 1) / fx_rpq;
+    auto owner_of = [&](int q) { return (q >= o_lo && q <= o_hi) || (chunk0 && q == ob) || (lead && q == orep); };
+    if (TOP && lead && tid < 4) {
+      float L = 0.f, Cr = 0.f;
+      for (int q = 0; q < NW; ++q) { L += red[0][q]; Cr += red[1][q]; }
+      mval = tid == 0 ? L : tid == 2 ? Cr : (float)M;   // {loss sum, n, correct, n}
+    }
+    // waves < NTILE: this lane's 4 W elements; aux: lanes ac < C the head's dW rows (TOP),
+    // lane ac == C the bias (the column sums are the same in every lane)
+    float ev[4] = {0.f, 0.f, 0.f, 0.f};
+    int eo[4] = {0, 0, 0, 0}, epos[4] = {0, 0, 0, 0};
+    int ne = 0;
+    if (w < NTILE) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const long idx = (long)(trow0 + e) * N + tcol;
-      if (a.fuse_opt) {
-        float tp, tm, tv;
-        const bf16_t pb = f2bf(md_adam(op[e], om[e], ov[e], acc[e], ak, &tp, &tm, &tv));
-        if (a.wt & 1) {
-          md_st(a.pW + idx, tp); md_st(a.mW + idx, tm); md_st(a.vW + idx, tv);
-        } else {
-          a.pW[idx] = tp; a.mW[idx] = tm; a.vW[idx] = tv;
-        }
-        if (a.wt & 2)   // the next step's bf16 row-major shadow, write-through too
-          __builtin_amdgcn_raw_buffer_store_b16((unsigned short)pb, wsn_r, (int)(idx * 2), 0, 16);
-        else
-          Wsn[idx] = pb;
-        wtp[e >> 1] |= (unsigned)pb << (16 * (e & 1));
-      } else if (a.smap) {
-        stage_store(a.smap, par, 0, trow0 + e, tcol, acc[e]);
-      } else {
-        a.gW[goff + idx] = (a.accumulate ? op[e] : 0.f) + acc[e];   // mode 0 loaded the old grad into op
+      for (int e = 0; e < 4; ++e) {
+        ev[e] = acc[e];
+        eo[e] = fx_col ? ob : (trow0 + e) / fx_rpq;
+        epos[e] = w * 256 + lane * 4 + e;
+      }
+      ne = 4;
+    } else if (aux && ((TOP && ac < C) || ac == C)) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        ev[e] = ac == C ? ab[e] : aw[e];
+        eo[e] = ob;
+        epos[e] = (ac == C ? 8 * 256 : 7 * 256) + lane * 4 + e;
+      }
+      ne = 4;
+    }
+    int rpos = -1;   // replicated scalar of this thread: lead's db_h (aux lanes < C) or a metric slot
+    float rv = 0.f;
+    if (TOP && lead && aux && lane < C) { rpos = 9 * 256 + lane; rv = ab2[0]; }
+    if (TOP && lead && tid < 4) { rpos = 9 * 256 + 64 + tid; rv = mval; }
+    // 1. partials to their owners (one uniform resource per candidate owner; a lane whose
+    // element belongs elsewhere stores out of range: dropped by the bounds check)
+    {
+      const int cand[3] = {o_lo, o_hi, ob};
+#pragma unroll
+      for (int ci = 0; ci < 3; ++ci) {
+        const int c = cand[ci];
+        if (c == R || (ci >= 1 && c == cand[0]) || (ci == 2 && c == cand[1]) || (ci == 2 && !chunk0)) continue;
+        const __amdgpu_buffer_rsrc_t rr = sys_rsrc_u(sgpr_ptr(X->part[c]) + ((long)T * TX_MAX_RANKS + R) * pay, tb);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sys_store1(rr, (e < ne && eo[e] == c) ? (long)epos[e] : pay, ev[e]);
       }
     }
-    if (a.fuse_opt && a.WTout) {
-      bf16_t* const wto = a.WTout + (long)tcol * a.ldwt + trow0;
-      if (a.wt & 1)
+    if (rpos >= 0 && orep != R)
+      sys_store1(sys_rsrc_u(sgpr_ptr(X->part[orep]) + ((long)T * TX_MAX_RANKS + R) * pay, tb), rpos, rv);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid < W && tid != R && owner_of(tid)) tx_flag_store(X->flag[tid] + (long)T * TX_MAX_RANKS + R, epoch);
+    MD_STAMP(5);
+    // 2. this rank's owned elements: rank-ordered sums, sharded AdamW, hand-back
+    float pnew[4] = {0.f, 0.f, 0.f, 0.f};
+    if (owner_of(R)) {
+      if (tid < W && tid != R) tx_wait(X->flag[R] + (long)T * TX_MAX_RANKS + tid, epoch, X->timeout, X->err);
+      __syncthreads();
+      const float* inbox = sgpr_ptr(X->part[R]) + (long)T * TX_MAX_RANKS * pay;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (e >= ne || eo[e] != R) continue;
+        float sacc = 0.f;
+        for (int q = 0; q < W; ++q) {
+          const float x = q == R ? ev[e] : sys_load1(sys_rsrc_u(inbox + (long)q * pay, tb), epos[e]);
+          sacc = q == 0 ? x : sacc + x;
+        }
+        ev[e] = sacc;
+      }
+      if (rpos >= 0 && orep == R) {
+        float sacc = 0.f;
+        for (int q = 0; q < W; ++q) {
+          const float x = q == R ? rv : sys_load1(sys_rsrc_u(inbox + (long)q * pay, tb), rpos);
+          sacc = q == 0 ? x : sacc + x;
+        }
+        rv = sacc;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (e >= ne || eo[e] != R) continue;
+        float tp, tm, tv;
+        if (w < NTILE) {
+          const long li = fx_col ? (long)(trow0 + e) * fx_hpq + (tcol - R * fx_hpq)
+                                 : (long)(trow0 + e - R * fx_rpq) * N + tcol;
+          md_adam(op[e], om[e], ov[e], ev[e], ak, &tp, &tm, &tv);
+          a.pW[li] = tp; a.mW[li] = tm; a.vW[li] = tv;
+        } else {
+          const int lr_ = j0 + (lane >> 4) * 4 + e - R * fx_hpq;
+          if (ac == C) {
+            md_adam(bp[e], bm[e], bvv[e], ev[e], ak, &tp, &tm, &tv);
+            a.pb[lr_] = tp; a.mb[lr_] = tm; a.vb[lr_] = tv;
+          } else {
+            const long li = (long)lr_ * C + ac;
+            md_adam(op[e], om[e], ov[e], ev[e], ak, &tp, &tm, &tv);
+            a.pWh[li] = tp; a.mWh[li] = tm; a.vWh[li] = tv;
+          }
+        }
+        pnew[e] = tp;
+      }
+      for (int q = 0; q < W; ++q) {
+        if (q == R) continue;
+        const __amdgpu_buffer_rsrc_t dst = sys_rsrc_u(sgpr_ptr(X->red[q]) + (long)T * pay, tb);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (e < ne && eo[e] == R) sys_store1(dst, epos[e], pnew[e]);
+        if (rpos >= 0 && orep == R) sys_store1(dst, rpos, rv);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid < W && tid != R) tx_flag_store(X->flag[tid] + AG + (long)T * TX_MAX_RANKS + R, epoch);
+    }
+    // 3. the other owners' updated values
+    if (tid < W && tid != R && owner_of(tid))
+      tx_wait(X->flag[R] + AG + (long)T * TX_MAX_RANKS + tid, epoch, X->timeout, X->err);
+    __syncthreads();
+    {
+      const __amdgpu_buffer_rsrc_t src = sys_rsrc_u(sgpr_ptr(X->red[R]) + (long)T * pay, tb);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (e < ne && eo[e] != R) pnew[e] = sys_load1(src, epos[e]);
+      if (rpos >= 0 && orep != R) rv = sys_load1(src, rpos);
+    }
+    if (TOP && lead && tid < 4) mval = rv;
+    MD_STAMP(6);
+    // 4. the whole updated tile: the next step's row-major shadow, W^T copy and (layer 0)
+    // the run-ahead forward's LDS image; bias shadow / hand-off; head shadow; b_h
+    // (replicated) updated by every rank from the summed gradient
+    const int par_s = __builtin_amdgcn_readfirstlane(par);
+    if (w < NTILE) {
+      bf16_t* Wsn = const_cast<bf16_t*>(par_s ? a.Ws0 : a.Ws1);
+      const __amdgpu_buffer_rsrc_t wsn_r = __builtin_amdgcn_make_buffer_rsrc(Wsn, (short)0, 0x7fffffff, 0x00020000);
+      unsigned wtp[2] = {0u, 0u};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bf16_t pb = f2bf(pnew[e]);
+        const long idx = (long)(trow0 + e) * N + tcol;
+        if (a.wt & 2) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)pb, wsn_r, (int)(idx * 2), 0, 16);
+        else Wsn[idx] = pb;
+        wtp[e >> 1] |= (unsigned)pb << (16 * (e & 1));
+      }
+      if (a.WTout) {
+        bf16_t* const wto = a.WTout + (long)tcol * a.ldwt + trow0;
         __hip_atomic_store((__attribute__((address_space(1))) unsigned long long*)wto,
                            (unsigned long long)wtp[0] | ((unsigned long long)wtp[1] << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-      else
-        *reinterpret_cast<uint2*>(wto) = make_uint2(wtp[0], wtp[1]);
-    }
-    if constexpr (AHEAD)
-      *reinterpret_cast<uint2*>(&w1n[(lane & 15) * LDW1 + (trow0 - kc0)]) = make_uint2(wtp[0], wtp[1]);
-  } else if (aux) {
-    bf16_t* Whn = const_cast<bf16_t*>(par_s ? a.Wh0 : a.Wh1);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int n = (lane >> 4) * 4 + e;
-      if (TOP && ac < C) {
-        const long g = (long)(j0 + n) * C + ac;
-        if (a.fuse_opt) Whn[g] = f2bf(md_adam(op[e], om[e], ov[e], aw[e], ak, a.pWh + g, a.mWh + g, a.vWh + g));
-        else if (a.smap) stage_store(a.smap, par, 2, j0 + n, ac, aw[e]);
-        else a.gWh[goff + g] = (a.accumulate ? op[e] : 0.f) + aw[e];
       }
-      if (ac == 0) {
-        const int j = j0 + n;
-        if (a.fuse_opt) {
-          const float pn = md_adam(bp[e], bm[e], bvv[e], ab[e], ak, a.pb + j, a.mb + j, a.vb + j);
-          a.sb[j] = f2bf(pn);
-          if constexpr (AHEAD) a.hand[j] = pn;   // the next forward's bias (same XCD: L2 hand-off)
-        } else if (a.smap) {
-          stage_store(a.smap, par, 1, j, 0, ab[e]);
-        } else {
-          a.gb[goff + j] = (a.accumulate ? bp[e] : 0.f) + ab[e];
+      if constexpr (AHEAD)
+        *reinterpret_cast<uint2*>(&w1n[(lane & 15) * LDW1 + (trow0 - kc0)]) = make_uint2(wtp[0], wtp[1]);
+    } else if (aux) {
+      bf16_t* Whn = const_cast<bf16_t*>(par_s ? a.Wh0 : a.Wh1);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = j0 + (lane >> 4) * 4 + e;
+        if (TOP && ac < C) Whn[(long)j * C + ac] = f2bf(pnew[e]);
+        if (ac == C) {
+          a.sb[j] = f2bf(pnew[e]);
+          if constexpr (AHEAD) a.hand[j] = pnew[e];   // the next forward's bias (same XCD: L2 hand-off)
         }
       }
+      if (TOP && lead && lane < C) a.sbh[lane] = f2bf(md_adam(qp, qm, qv, rv, ak, a.pbh + lane, a.mbh + lane, a.vbh + lane));
     }
-    if (TOP && lead && lane < C) {
-      if (a.fuse_opt) a.sbh[lane] = f2bf(md_adam(qp, qm, qv, ab2[0], ak, a.pbh + lane, a.mbh + lane, a.vbh + lane));
-      else if (a.smap) stage_store(a.smap, par, 3, lane, 0, ab2[0]);
-      else a.gbh[goff + lane] = (a.accumulate ? qp : 0.f) + ab2[0];
+  } else {
+    // the step parity as a scalar for the parity-selected store resources (the step was the
+    // first load of the launch and is long back; per lane it made them waterfall loops)
+    const int par_s = __builtin_amdgcn_readfirstlane(par);
+    if (w < NTILE) {
+      bf16_t* Wsn = const_cast<bf16_t*>(par_s ? a.Ws0 : a.Ws1);   // next step's parity of the row-major shadow
+      const __amdgpu_buffer_rsrc_t wsn_r = __builtin_amdgcn_make_buffer_rsrc(Wsn, (short)0, 0x7fffffff, 0x00020000);
+      unsigned wtp[2] = {0u, 0u};
+  #pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long idx = (long)(trow0 + e) * N + tcol;
+        if (a.fuse_opt) {
+          float tp, tm, tv;
+          const bf16_t pb = f2bf(md_adam(op[e], om[e], ov[e], acc[e], ak, &tp, &tm, &tv));
+          if (a.wt & 1) {
+            md_st(a.pW + idx, tp); md_st(a.mW + idx, tm); md_st(a.vW + idx, tv);
+          } else {
+            a.pW[idx] = tp; a.mW[idx] = tm; a.vW[idx] = tv;
+          }
+          if (a.wt & 2)   // the next step's bf16 row-major shadow, write-through too
+            __builtin_amdgcn_raw_buffer_store_b16((unsigned short)pb, wsn_r, (int)(idx * 2), 0, 16);
+          else
+            Wsn[idx] = pb;
+          wtp[e >> 1] |= (unsigned)pb << (16 * (e & 1));
+        } else if (a.smap) {
+          stage_store(a.smap, par, 0, trow0 + e, tcol, acc[e]);
+        } else {
+          a.gW[goff + idx] = (a.accumulate ? op[e] : 0.f) + acc[e];   // mode 0 loaded the old grad into op
+        }
+      }
+      if (a.fuse_opt && a.WTout) {
+        bf16_t* const wto = a.WTout + (long)tcol * a.ldwt + trow0;
+        if (a.wt & 1)
+          __hip_atomic_store((__attribute__((address_space(1))) unsigned long long*)wto,
+                             (unsigned long long)wtp[0] | ((unsigned long long)wtp[1] << 32), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        else
+          *reinterpret_cast<uint2*>(wto) = make_uint2(wtp[0], wtp[1]);
+      }
+      if constexpr (AHEAD)
+        *reinterpret_cast<uint2*>(&w1n[(lane & 15) * LDW1 + (trow0 - kc0)]) = make_uint2(wtp[0], wtp[1]);
+    } else if (aux) {
+      bf16_t* Whn = const_cast<bf16_t*>(par_s ? a.Wh0 : a.Wh1);
+  #pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = (lane >> 4) * 4 + e;
+        if (TOP && ac < C) {
+          const long g = (long)(j0 + n) * C + ac;
+          if (a.fuse_opt) Whn[g] = f2bf(md_adam(op[e], om[e], ov[e], aw[e], ak, a.pWh + g, a.mWh + g, a.vWh + g));
+          else if (a.smap) stage_store(a.smap, par, 2, j0 + n, ac, aw[e]);
+          else a.gWh[goff + g] = (a.accumulate ? op[e] : 0.f) + aw[e];
+        }
+        if (ac == 0) {
+          const int j = j0 + n;
+          if (a.fuse_opt) {
+            const float pn = md_adam(bp[e], bm[e], bvv[e], ab[e], ak, a.pb + j, a.mb + j, a.vb + j);
+            a.sb[j] = f2bf(pn);
+            if constexpr (AHEAD) a.hand[j] = pn;   // the next forward's bias (same XCD: L2 hand-off)
+          } else if (a.smap) {
+            stage_store(a.smap, par, 1, j, 0, ab[e]);
+          } else {
+            a.gb[goff + j] = (a.accumulate ? bp[e] : 0.f) + ab[e];
+          }
+        }
+      }
+      if (TOP && lead && lane < C) {
+        if (a.fuse_opt) a.sbh[lane] = f2bf(md_adam(qp, qm, qv, ab2[0], ak, a.pbh + lane, a.mbh + lane, a.vbh + lane));
+        else if (a.smap) stage_store(a.smap, par, 3, lane, 0, ab2[0]);
+        else a.gbh[goff + lane] = (a.accumulate ? qp : 0.f) + ab2[0];
+      }
     }
   }
   MD_STAMP(3);
@@ -1007,7 +1207,8 @@ JDT_API int jdt_md_dzs_ok(int M) {
 // 1 if the deep engine's N > 1 step with the in-kernel tile exchange can run here with
 // `nshare` ranks' grids on this GPU: every exchanging backward launch of every sharing
 // rank resident at once (as jdt_mlp2_ahead_tx_ok).
-JDT_API int jdt_md_tx_ok(int M, int nshare) {
+template <bool FX>
+static int md_tx_fits(int M, int nshare) {
   if (M <= 0 || M > MD_MPM || nshare < 1) return 0;
   int dev = 0, cus = 0, p0 = 0, p1 = 0, p2 = 0;
   const bool sh = nshare > 1;   // the launcher's variant choice (MdArgs::tx_shared)
@@ -1015,20 +1216,23 @@ JDT_API int jdt_md_tx_ok(int M, int nshare) {
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       hipOccupancyMaxActiveBlocksPerMultiprocessor(
           &p0,
-          sh ? (const void*)md_bwd_kernel<784, false, 10, 112, 512, true, false, true, true, 4>
-             : (const void*)md_bwd_kernel<784, false, 10, 112, 512, true, false, true, true>,
+          sh ? (const void*)md_bwd_kernel<784, false, 10, 112, 512, true, false, true, true, 4, FX>
+             : (const void*)md_bwd_kernel<784, false, 10, 112, 512, true, false, true, true, 1, FX>,
           MD_NT, 0) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&p1, md_bwd_kernel<512, true, 10, 64, 512, true, false, false, true>,
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&p1, md_bwd_kernel<512, true, 10, 64, 512, true, false, false, true, 1, FX>,
                                                    MD_NT, 0) != hipSuccess ||
       hipOccupancyMaxActiveBlocksPerMultiprocessor(
           &p2,
-          sh ? (const void*)md_bwd_kernel<512, false, 10, 64, 512, true, false, false, true, 4>
-             : (const void*)md_bwd_kernel<512, false, 10, 64, 512, true, false, false, true>,
+          sh ? (const void*)md_bwd_kernel<512, false, 10, 64, 512, true, false, false, true, 4, FX>
+             : (const void*)md_bwd_kernel<512, false, 10, 64, 512, true, false, false, true, 1, FX>,
           MD_NT, 0) != hipSuccess)
     return 0;
   const long cap = (long)cus * (p0 < p1 ? (p0 < p2 ? p0 : p2) : (p1 < p2 ? p1 : p2));
   return (long)nshare * (512 / 16) * (512 / 64) <= cap ? 1 : 0;
 }
+JDT_API int jdt_md_tx_ok(int M, int nshare) { return md_tx_fits<false>(M, nshare); }
+// the same for the FSDP form (md_bwd FX, MdArgs::tx_fsdp)
+JDT_API int jdt_md_fx_ok(int M, int nshare) { return md_tx_fits<true>(M, nshare); }
 
 JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) {
   const MdArgs& a = *args;
@@ -1043,7 +1247,13 @@ JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) 
     if (a.K != 784 || head || !a.fuse_opt || !a.WTout || !a.XR || !a.zslab || !a.ztick || !a.hand ||
         !a.advance_step || a.det_logits)
       return -3;
-    if (a.tx && a.tx_shared)
+    if (a.tx && a.tx_fsdp && a.tx_shared)
+      hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, true, false, true, true, 4, true>),
+                         dim3(a.N / 16, 784 / 112), blk, 0, st, a);
+    else if (a.tx && a.tx_fsdp)
+      hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, true, false, true, true, 1, true>),
+                         dim3(a.N / 16, 784 / 112), blk, 0, st, a);
+    else if (a.tx && a.tx_shared)
       hipLaunchKernelGGL((md_bwd_kernel<784, false, 10, 112, 512, true, false, true, true, 4>),
                          dim3(a.N / 16, 784 / 112), blk, 0, st, a);
     else if (a.tx)
@@ -1058,6 +1268,15 @@ JDT_API int jdt_md_layer(const MdArgs* args, int phase, int head, void* stream) 
     // N > 1 hidden layers >= 1 with the in-kernel tile exchange (layer 0 runs ahead)
     if (a.K != 512 || head == 2 || a.dzs || !a.fuse_opt) return -3;
     const dim3 g(a.N / 16, 512 / 64);
+    if (a.tx_fsdp) {
+      if (head)
+        hipLaunchKernelGGL((md_bwd_kernel<512, true, 10, 64, 512, true, false, false, true, 1, true>), g, blk, 0, st, a);
+      else if (a.tx_shared)
+        hipLaunchKernelGGL((md_bwd_kernel<512, false, 10, 64, 512, true, false, false, true, 4, true>), g, blk, 0, st, a);
+      else
+        hipLaunchKernelGGL((md_bwd_kernel<512, false, 10, 64, 512, true, false, false, true, 1, true>), g, blk, 0, st, a);
+      return HIP_LAUNCH_CHECK();
+    }
     if (head) hipLaunchKernelGGL((md_bwd_kernel<512, true, 10, 64, 512, true, false, false, true>), g, blk, 0, st, a);
     else if (a.tx_shared)
       hipLaunchKernelGGL((md_bwd_kernel<512, false, 10, 64, 512, true, false, false, true, 4>), g, blk, 0, st, a);

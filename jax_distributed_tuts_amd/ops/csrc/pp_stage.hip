@@ -7,22 +7,24 @@
 // send kernel: 3-4 dependent launches of ~4 us each for a 64 x 512 x 512 layer, so a
 // tick costs ~13 us and an 8-stage pipeline cannot beat one GPU.  Here the whole
 // fill / drain schedule of the step runs inside one launch of 32 workgroups per rank,
-// workgroup b owning output columns [16b, 16b + 16) of the stage's layer (and, for the
-// input gradient, rows [16b, 16b + 16) of its weight):
+// workgroup b owning output columns [16b, 16b + 16) of the stage's layer:
 //
+//   step start:      W (fp32 master) -> bf16 LDS image; a stage > 0 also writes that image
+//                    into its predecessor's weight box (second inbox, by step parity);
+//                    stage 0 converts the step's data to bf16 rows and per-microbatch X^T
 //   forward tick i:  wait for the 32 producer flags of inbox slot i (or read the data),
 //                    Z = X W[:, own] + b on MFMA (K split over the 4 waves), SiLU,
 //                    dropout (the md kernels' Philox streams), backward factor G kept in
 //                    LDS; the H tile goes straight into the NEXT stage's inbox (H and
 //                    H^T, system-scope stores over xGMI) and one flag per workgroup is
 //                    raised -- or, last stage, the head's partial logits (fp32 atomics)
-//   backward tick i: dH[:, own] from the next stage's inbox (or, last stage, CE of the
-//                    complete logits through the head), dZ = dH * G; dW[:, own] +=
-//                    X^T dZ (accumulated in registers over the microbatches, X^T from
-//                    the inbox), db; then -- not stage 0 -- dZ is published to the
-//                    stage's other workgroups (one arrival counter), and each computes
-//                    dX[:, own rows] = dZ W[own rows, :]^T and sends it to the previous
-//                    stage's inbox
+//   backward tick i: dH[:, own] = dZ_next W_next[own, :]^T from the successor's dZ
+//                    (inbox) and weight image (weight box) on MFMA -- or, last stage, CE
+//                    of the complete logits through the head; dZ = dH * G goes straight
+//                    to the predecessor's inbox (not stage 0) with one flag per workgroup,
+//                    so a backward hop is shaped like a forward one (no intra-stage
+//                    gather); then dW[:, own] += X^T dZ (registers, over the
+//                    microbatches; X^T prefetched ahead of the wait) and db
 //   end of step:     AdamW on the owned columns (gradient scale 1 / n_mb), bf16 shadows,
 //                    metrics fold, step advance (arrival ticket).
 //
@@ -38,7 +40,9 @@
 
 namespace jdt {
 
-constexpr int PS_NT = 256;         // 4 waves
+constexpr int PS_NT = 512;         // 8 waves: twice the loads in flight per workgroup of the
+                                   // 4-wave form (a hop's A operand is read at a per-block
+                                   // rate that grows with outstanding loads)
 constexpr int PS_NW = PS_NT / 64;
 constexpr int PS_NB = 32;          // workgroups = 512 / 16 output column blocks
 constexpr int PS_N = 512;          // layer width
@@ -73,7 +77,12 @@ struct PsArgs {
   // scratch (zero-initialised once by the host)
   bf16_t* XT;                      // stage 0: X^T [PS_MAXNMB][784][PS_MAXMB] bf16 (per microbatch, stride
                                    // K * mbp), then the bf16 row copy [PS_MAXROWS][784]
-  bf16_t* dZ;                      // [n_mb][mb][512] bf16 (published for the dX products)
+  // weight boxes (a second p2p inbox of two PS_WBYTES slots, by step parity): a stage > 0
+  // writes the bf16 image of its W [512][512] into its predecessor's box at the start of
+  // the step; the predecessor's backward forms dH = dZ_next W_next^T itself, so a backward
+  // hop carries dZ and no stage waits on an intra-stage gather before sending
+  char* w_mine; unsigned* wflag_mine;
+  char* w_prev; unsigned* wflag_prev;
   float* logits;                   // last stage: [2][n_mb][mb][C] fp32, by step parity
   unsigned* ctr;                   // arrival counters, one 128-byte line each
   int* step; unsigned* ticket;     // device optimizer step, end-of-step ticket
@@ -87,7 +96,8 @@ struct PsArgs {
     if (a.stamps && threadIdx.x == 0) a.stamps[(long)blockIdx.x * 24 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
-constexpr int CPOL_SC1 = 16;       // agent-coherent (write-through / past L1) buffer access
+constexpr int CPOL_SC1 = 16;
+constexpr long PS_WBYTES = (long)PS_N * PS_N * 2;       // agent-coherent (write-through / past L1) buffer access
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t ps_rsrc(const void* base, long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(sgpr_ptr(const_cast<void*>(base)), (short)0,
@@ -126,6 +136,27 @@ __device__ __forceinline__ void ps_wait_slot(const unsigned* flags, int slot, un
     }
   }
   __syncthreads();
+}
+
+// Wave w's share of a 512-deep product (k in [64w, 64w + 64) with 8 waves) comes from
+// producer workgroups [4w, 4w + 4): those lanes poll just their flags, no workgroup barrier (the
+// data loads that follow are issued after the loop exits: in-order issue per wave).
+__device__ __forceinline__ void ps_wait_wave(const unsigned* flags, int slot, unsigned epoch, long long timeout,
+                                             int* err) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane < PS_FLAG_BLOCKS / PS_NW && !ps_failed(err)) {
+    const unsigned* f = flags + (long)slot * PS_FLAG_BLOCKS + w * (PS_FLAG_BLOCKS / PS_NW) + lane;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int)(tx_flag_load(f) - epoch) < 0) {
+      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout) {
+        __hip_atomic_store((__attribute__((address_space(1))) int*)err, 1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  asm volatile("" ::: "memory");
 }
 
 // This workgroup's stores are drained, then ONE lane raises its flag of `slot` on the peer.
@@ -169,11 +200,9 @@ __device__ __forceinline__ void ps_arrive_wait(unsigned* ctr, int c, long long t
   ps_wait(ctr, c, ps_arrive(ctr, c), timeout, err);
 }
 
-// counter lines: stage 0's bf16 X / X^T pre-pass done, logits of i complete (last
-// stage), dZ of i published (stages > 0)
+// counter lines: stage 0's bf16 X / X^T pre-pass done, logits of i complete (last stage)
 __device__ __forceinline__ int ps_ctr_xt(int i) { return i; }
 __device__ __forceinline__ int ps_ctr_lg(int i) { return PS_MAXNMB + i; }
-__device__ __forceinline__ int ps_ctr_dz(int i) { return 2 * PS_MAXNMB + i; }
 
 template <bool FIRST, bool LAST>
 __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
@@ -187,9 +216,11 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
   constexpr int TPW = (KS + PS_NW - 1) / PS_NW;  // forward k-steps per wave
   constexpr int LDT = PS_MAXMB + 8;
   constexpr int MMT = PS_MAXMB / 16;            // 16-row tiles of a microbatch
+  constexpr int KSW = (PS_N / 32) / PS_NW;      // k-steps per wave of a 512-deep product
+  static_assert(KSW * 32 / 16 == PS_FLAG_BLOCKS / PS_NW, "a wave's k range = its producers' columns");
   static_assert(K % 16 == 0, "dW tiles");
   __shared__ __attribute__((aligned(16))) bf16_t wc[16 * LDWC];                 // W[:, own]^T
-  __shared__ __attribute__((aligned(16))) bf16_t wr[FIRST ? 8 : 16 * LDWR];    // W[own rows, :]
+  __shared__ __attribute__((aligned(16))) bf16_t wr[LAST ? 8 : 16 * LDWR];     // W_next[own rows, :]
   __shared__ float part[PS_NW][PS_MAXMB][17];
   __shared__ float gl[PS_MAXROWS][16];                                          // backward factor G
   __shared__ __attribute__((aligned(16))) bf16_t ht[PS_MAXMB][24];             // this tick's H tile
@@ -207,26 +238,27 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
   const int step = a.step[0], par = step & 1;
   const unsigned epoch = (unsigned)step + 1u;
   const unsigned long long dbase = (unsigned long long)(unsigned)step << 32;
+  const float rkeep = 1.f / a.keep;
   PS_STAMP(0);
 
   // ---- 0. this step's weights into LDS (bf16 rounding of the fp32 masters = the
   // shadows): every load first, then the images (a load-store loop would pay one round
-  // trip per iteration)
+  // trip per iteration); stage 0's data rows for the pre-pass below load with them
+  static_assert(!FIRST || K / 4 <= PS_NT, "one float4 column per thread");
+  const int rr = 4 * b;   // stage 0: this workgroup's 4 data rows of the step
+  float4 xpre[FIRST ? 4 : 1];
   {
     constexpr int WC4 = (K * 4 + PS_NT - 1) / PS_NT;   // float4 of W[:, own] per thread
-    constexpr int WR4 = FIRST ? 1 : 16 * (PS_N / 4) / PS_NT;
-    float4 wv[WC4], rv[WR4];
+    float4 wv[WC4];
 #pragma unroll
     for (int t = 0; t < WC4; ++t) {
       const int idx = min(tid + t * PS_NT, K * 4 - 1);
       wv[t] = *reinterpret_cast<const float4*>(a.p + (long)(idx >> 2) * PS_N + j0 + 4 * (idx & 3));
     }
-    if constexpr (!FIRST) {
+    if constexpr (FIRST) {
+      if (tid < K / 4)
 #pragma unroll
-      for (int t = 0; t < WR4; ++t) {
-        const int idx = tid + t * PS_NT, r = idx / (PS_N / 4), q = idx % (PS_N / 4);
-        rv[t] = *reinterpret_cast<const float4*>(a.p + (long)(j0 + r) * PS_N + 4 * q);
-      }
+        for (int e = 0; e < 4; ++e) xpre[e] = *reinterpret_cast<const float4*>(a.X + (long)(rr + e) * K + 4 * tid);
     }
     const float bv = a.pb[j0 + (tid & 15)];
     float hv = 0.f, hbv = 0.f;
@@ -248,12 +280,20 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
     if constexpr (KP > K)
       for (int idx = tid; idx < 16 * (KP - K); idx += PS_NT) wc[(idx / (KP - K)) * LDWC + K + idx % (KP - K)] = 0;
     if constexpr (!FIRST) {
+      // W[:, own] (bf16) into the predecessor's weight box, slot = step parity; its flag
+      // goes up after the forward ticks (their sends drain these stores too)
+      const __amdgpu_buffer_rsrc_t wo = ps_rsrc(a.w_prev + (long)par * PS_WBYTES, PS_WBYTES);
 #pragma unroll
-      for (int t = 0; t < WR4; ++t) {
-        const int idx = tid + t * PS_NT, r = idx / (PS_N / 4), q = idx % (PS_N / 4);
-        const unsigned lo = (unsigned)f2bf(rv[t].x) | ((unsigned)f2bf(rv[t].y) << 16);
-        const unsigned hi = (unsigned)f2bf(rv[t].z) | ((unsigned)f2bf(rv[t].w) << 16);
-        *reinterpret_cast<uint2*>(&wr[r * LDWR + 4 * q]) = make_uint2(lo, hi);
+      for (int t = 0; t < WC4; ++t) {
+        const int idx = tid + t * PS_NT;
+        if (idx < K * 4) {
+          const int k = idx >> 2, q = idx & 3;
+          const unsigned lo = (unsigned)f2bf(wv[t].x) | ((unsigned)f2bf(wv[t].y) << 16);
+          const unsigned hi = (unsigned)f2bf(wv[t].z) | ((unsigned)f2bf(wv[t].w) << 16);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned,
+                                                                   make_uint2(lo, hi)),
+                                                wo, (int)(((long)k * PS_N + j0 + 4 * q) * 2), 0, CPOL_SYS);
+        }
       }
     }
     if (tid < 16) bsh[tid] = round_bf(bv);
@@ -269,11 +309,9 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
   // microbatch transposed (the dW operand): workgroup b converts rows [4b, 4b + 4)
   // (n_mb * mb == 128, host-checked), write-through, then every workgroup meets
   if constexpr (FIRST) {
-    const int rr = 4 * b, i = rr / mb, rl = rr - i * mb;
-    for (int k4 = tid; k4 < K / 4; k4 += PS_NT) {
-      float4 x[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) x[e] = *reinterpret_cast<const float4*>(a.X + (long)(rr + e) * K + 4 * k4);
+    const int i = rr / mb, rl = rr - i * mb, k4 = tid;
+    if (tid < K / 4) {
+      const float4* x = xpre;
       const __amdgpu_buffer_rsrc_t xbr = ps_rsrc(a.XT + (long)PS_MAXNMB * K * PS_MAXMB, (long)PS_MAXROWS * K * 2);
       const __amdgpu_buffer_rsrc_t xtr = ps_rsrc(a.XT + (long)i * K * mbp, (long)K * mbp * 2);
 #pragma unroll
@@ -304,7 +342,14 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
   const int MT = mb / 16;
   for (int i = 0; i < n_mb; ++i) {
     const int r0 = i * mb;   // this microbatch's rows of the step
-    if constexpr (!FIRST) ps_wait_slot(a.flag_mine, i, epoch, a.timeout, a.err);
+    // this thread's dropout bits (4 rows x 1 column) do not wait for the inputs
+    const int g4 = tid >> 4, c = tid & 15;
+    u32x4 db = {0u, 0u, 0u, 0u};
+    if (a.keep < 1.f && 4 * g4 < mb) {
+      const unsigned long long off = (unsigned long long)((long)i << a.mb_shift) + ((unsigned long long)a.gid << 1);
+      db = dropout_bits(a.seed, off + dbase, dropout_group(0, 4 * g4, j0 + c, mb, PS_N));
+    }
+    if constexpr (!FIRST) ps_wait_wave(a.flag_mine, i, epoch, a.timeout, a.err);
     if (i == 1) PS_STAMP(19);
     // Z partials: wave w takes k-steps [w KS / 4, (w+1) KS / 4) of every 16-row tile; all
     // of its A fragments are loaded first (bf16 rows: stage 0's converted copy, else the
@@ -322,7 +367,8 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
       for (int t = 0; t < TPW; ++t)
 #pragma unroll
         for (int mt = 0; mt < MMT; ++mt) {
-          const int ks = min(ks0 + t, ks1 - 1), row = min(mt * 16 + (lane & 15), mb - 1);
+          if (mt >= MT) break;
+          const int ks = min(ks0 + t, ks1 - 1), row = mt * 16 + (lane & 15);
           // k past K (stage 0's 784 = 24.5 k-steps) reads the next row or, past the
           // buffer, zero (bounds check): finite values times wc's zero padding
           const long off = ((long)row * K + ks * 32 + 8 * (lane >> 4)) * 2;
@@ -348,11 +394,7 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
     if (i == 1) PS_STAMP(20);
     // bias + SiLU + dropout, one 4-row group per thread (the md kernels' streams)
     {
-      const int g4 = tid >> 4, c = tid & 15;
       if (4 * g4 < mb) {
-        u32x4 db = {0u, 0u, 0u, 0u};
-        const unsigned long long off = (unsigned long long)((long)i << a.mb_shift) + ((unsigned long long)a.gid << 1);
-        if (a.keep < 1.f) db = dropout_bits(a.seed, off + dbase, dropout_group(0, 4 * g4, j0 + c, mb, PS_N));
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int rl = 4 * g4 + e;
@@ -364,8 +406,8 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
           float hv = z * sg, gd = sg * (1.0f + z * (1.0f - sg));
           if (a.keep < 1.f) {
             const bool kp = keep_word(db, e, a.keep);
-            hv = kp ? hv / a.keep : 0.f;
-            gd = kp ? gd / a.keep : 0.f;
+            hv = kp ? hv * rkeep : 0.f;
+            gd = kp ? gd * rkeep : 0.f;
           }
           gl[r0 + rl][c] = gd;
           const bf16_t hb = f2bf(hv);
@@ -410,6 +452,27 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
       ps_raise(a.flag_next, i, epoch);
     }
     if (i < 8) PS_STAMP(2 + i);
+  }
+
+  // the weight image written at the start is drained by now (every send waited on it)
+  if constexpr (!FIRST) ps_raise(a.wflag_prev, par, epoch);
+  // the successor's W rows of this workgroup's columns: wr[r][j] = W_next[j0 + r][j]
+  if constexpr (!LAST) {
+    ps_wait_slot(a.wflag_mine, par, epoch, a.timeout, a.err);
+    const __amdgpu_buffer_rsrc_t wi = ps_rsrc(a.w_mine + (long)par * PS_WBYTES, PS_WBYTES);
+    constexpr int WN16 = 16 * PS_N / 8 / PS_NT;   // 16-byte chunks per thread
+    u32x4 q[WN16];
+#pragma unroll
+    for (int t = 0; t < WN16; ++t) {
+      const int idx = tid + t * PS_NT, r = idx >> 6, c8 = (idx & 63) * 8;
+      q[t] = ps_load16<CPOL_SYS>(wi, ((long)(j0 + r) * PS_N + c8) * 2);
+    }
+#pragma unroll
+    for (int t = 0; t < WN16; ++t) {
+      const int idx = tid + t * PS_NT, r = idx >> 6, c8 = (idx & 63) * 8;
+      *reinterpret_cast<u32x4*>(&wr[r * LDWR + c8]) = q[t];
+    }
+    __syncthreads();
   }
 
   // ---- 2. backward ticks, last microbatch first
@@ -458,7 +521,10 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
 #pragma unroll
         for (int c = 0; c < PS_C; ++c) s += __expf(lrow[c] - mx);
         const float lse = mx + __logf(s);
-        l_loss += lse - lrow[lab];
+        float ll = 0.f;   // lrow[lab] without a dynamically indexed (scratch) array
+#pragma unroll
+        for (int c = 0; c < PS_C; ++c) ll = c == lab ? lrow[c] : ll;
+        l_loss += lse - ll;
         l_corr += (am == lab) ? 1.f : 0.f;
         const float inv = 1.f / (float)mb;
 #pragma unroll
@@ -493,17 +559,46 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
         dbh += s;
       }
     } else {
-      ps_wait_slot(a.flag_mine, n_mb + i, epoch, a.timeout, a.err);
+      // dH[:, own] = dZ_next W_next[own, :]^T: the successor's dZ (inbox slot n_mb + i) is
+      // the A operand; wave w takes k-steps [KSW w, KSW (w + 1)) of the 512-deep product
+      ps_wait_wave(a.flag_mine, n_mb + i, epoch, a.timeout, a.err);
       const __amdgpu_buffer_rsrc_t gin = ps_rsrc(a.in_mine + (long)(n_mb + i) * a.slot_bytes, (long)mb * PS_N * 2);
+      bf16x8 za[MMT][KSW];
+#pragma unroll
+      for (int t = 0; t < KSW; ++t)
+#pragma unroll
+        for (int mt = 0; mt < MMT; ++mt) {
+          if (mt >= MT) break;
+          za[mt][t] = __builtin_bit_cast(
+              bf16x8, ps_load16<CPOL_SYS>(gin, ((long)(mt * 16 + (lane & 15)) * PS_N + (KSW * w + t) * 32 + 8 * (lane >> 4)) * 2));
+        }
+      f32x4 acc[MMT];
+#pragma unroll
+      for (int mt = 0; mt < MMT; ++mt) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < KSW; ++t) {
+        const bf16x8 bf = *reinterpret_cast<const bf16x8*>(&wr[(lane & 15) * LDWR + (KSW * w + t) * 32 + 8 * (lane >> 4)]);
+#pragma unroll
+        for (int mt = 0; mt < MMT; ++mt)
+          if (mt < MT) acc[mt] = mfma16x16x32(za[mt][t], bf, acc[mt]);
+      }
+#pragma unroll
+      for (int mt = 0; mt < MMT; ++mt)
+        if (mt < MT)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) part[w][mt * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[mt][e];
+      __syncthreads();
+      // dZ = bf16(bf16(dH) * G), the rounding points of the per-tick path (dX sent as bf16)
       const int g4 = tid >> 4, c = tid & 15;
       if (4 * g4 < mb) {
         unsigned pk[2] = {0u, 0u};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int rl = 4 * g4 + e;
-          const unsigned short hb = (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(
-              gin, (int)(((long)rl * PS_N + j0 + c) * 2), 0, CPOL_SYS);
-          pk[e >> 1] |= (unsigned)f2bf(bf2f(hb) * gl[r0 + rl][c]) << (16 * (e & 1));
+          float v = 0.f;
+#pragma unroll
+          for (int q = 0; q < PS_NW; ++q) v += part[q][rl][c];
+          pk[e >> 1] |= (unsigned)f2bf(round_bf(v) * gl[r0 + rl][c]) << (16 * (e & 1));
         }
         *reinterpret_cast<uint2*>(&dzT[c * LDT + 4 * g4]) = make_uint2(pk[0], pk[1]);
       }
@@ -517,20 +612,18 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
       for (int r = 0; r < mb; ++r) s += bf2f(dzT[tid * LDT + r]);
       dba += s;
     }
-    // publish dZ[:, own] (write-through) and arrive -- not stage 0, whose input needs no
-    // gradient -- then the dW MFMAs overlap the other workgroups' arrival
-    const __amdgpu_buffer_rsrc_t zr = ps_rsrc(a.dZ + (long)i * mb * PS_N, (long)mb * PS_N * 2);
-    unsigned tz = 0;
+    // dZ[:, own] to the predecessor (stage 0's input needs no gradient), then dW
     if constexpr (!FIRST) {
+      const __amdgpu_buffer_rsrc_t o = ps_rsrc(a.in_prev + (long)(n_mb + i) * a.slot_bytes, (long)mb * PS_N * 2);
       if (tid < 2 * mb) {
         const int r = tid >> 1, h = (tid & 1) * 8;
         unsigned q[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           q[e] = (unsigned)dzT[(h + 2 * e) * LDT + r] | ((unsigned)dzT[(h + 2 * e + 1) * LDT + r] << 16);
-        ps_store16<CPOL_SC1>(zr, ((long)r * PS_N + j0 + h) * 2, (u32x4){q[0], q[1], q[2], q[3]});
+        ps_store16<CPOL_SYS>(o, ((long)r * PS_N + j0 + h) * 2, (u32x4){q[0], q[1], q[2], q[3]});
       }
-      tz = ps_arrive(a.ctr, ps_ctr_dz(i));
+      ps_raise(a.flag_prev, n_mb + i, epoch);
     }
     // dW^T[own cols][k] += dZ^T X (A = dzT, B = the prefetched X^T rows); wave w takes
     // k tiles w, w + 4, ...
@@ -548,49 +641,6 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
       }
     }
     if (i == 1) PS_STAMP(23);
-    if constexpr (!FIRST) {
-      // dX[:, own rows] = dZ W[own rows, :]^T -> the previous stage's inbox slot n_mb + i
-      ps_wait(a.ctr, ps_ctr_dz(i), tz, a.timeout, a.err);
-      // wave w: k-steps [4w, 4w + 4) of the 512-deep product, every 16-row tile
-      bf16x8 za[MMT][4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int mt = 0; mt < MMT; ++mt) {
-          const int row = min(mt * 16 + (lane & 15), mb - 1);
-          za[mt][t] = __builtin_bit_cast(bf16x8, ps_load16<CPOL_SC1>(zr, ((long)row * PS_N + (4 * w + t) * 32 + 8 * (lane >> 4)) * 2));
-        }
-      f32x4 acc[MMT];
-#pragma unroll
-      for (int mt = 0; mt < MMT; ++mt) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const bf16x8 bf = *reinterpret_cast<const bf16x8*>(&wr[(lane & 15) * LDWR + (4 * w + t) * 32 + 8 * (lane >> 4)]);
-#pragma unroll
-        for (int mt = 0; mt < MMT; ++mt)
-          if (mt < MT) acc[mt] = mfma16x16x32(za[mt][t], bf, acc[mt]);
-      }
-#pragma unroll
-      for (int mt = 0; mt < MMT; ++mt)
-        if (mt < MT)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) part[w][mt * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[mt][e];
-      __syncthreads();
-      const __amdgpu_buffer_rsrc_t o = ps_rsrc(a.in_prev + (long)(n_mb + i) * a.slot_bytes, (long)mb * PS_N * 2);
-      if (tid < 2 * mb) {
-        const int r = tid >> 1, h = (tid & 1) * 8;
-        unsigned q[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float x0 = 0.f, x1 = 0.f;
-#pragma unroll
-          for (int ww = 0; ww < PS_NW; ++ww) { x0 += part[ww][r][h + 2 * e]; x1 += part[ww][r][h + 2 * e + 1]; }
-          q[e] = (unsigned)f2bf(x0) | ((unsigned)f2bf(x1) << 16);
-        }
-        ps_store16<CPOL_SYS>(o, ((long)r * PS_N + j0 + h) * 2, (u32x4){q[0], q[1], q[2], q[3]});
-      }
-      ps_raise(a.flag_prev, n_mb + i, epoch);
-    }
     __syncthreads();
     if (i < 8) PS_STAMP(10 + i);
   }
@@ -705,7 +755,8 @@ JDT_API int jdt_pp_stage(const PsArgs* args, int first, int last, void* stream) 
   if ((first && last) || a.n_mb < 1 || a.n_mb > PS_MAXNMB || a.mb < 16 || a.mb > PS_MAXMB || (a.mb & 15) ||
       a.n_mb * a.mb > PS_MAXROWS || a.K != (first ? 784 : PS_N) || !a.step || !a.ticket || !a.ctr || !a.err)
     return -2;
-  if (!first && (!a.in_mine || !a.flag_mine || !a.in_prev || !a.flag_prev || !a.dZ)) return -2;
+  if (!first && (!a.in_mine || !a.flag_mine || !a.in_prev || !a.flag_prev || !a.w_prev || !a.wflag_prev)) return -2;
+  if (!last && (!a.w_mine || !a.wflag_mine)) return -2;
   if (!last && (!a.in_next || !a.flag_next)) return -2;
   if (first && (!a.X || !a.XT || a.n_mb * a.mb != PS_MAXROWS)) return -2;
   if (last && (!a.labels || !a.logits || !a.ph || !a.phb || !a.mslot || !a.running)) return -2;

@@ -467,38 +467,65 @@ class FSDPTrainer:
         return getattr(self.fused, "fsdp_tx", False)
 
     def _tile_exchange(self, batch: Batch):
-        """(TileExchange, ranks sharing this GPU) for the one-launch N > 1 FSDP step, or
-        (None, 1): the 2-layer classifier on the fused engine, AdamW, the reference's
-        dim-0 shards of W1 / b1 / W2 with whole 16-unit column blocks per rank (b2
-        replicated), not deterministic, every rank's grid co-resident with the grids of the
-        ranks sharing its GPU -- agreed by all ranks (collective).  JDT_FSDP_AHEAD=0: the
-        forward / backward / fused FSDP collective step."""
+        """(TileExchange, ranks sharing this GPU) for the N > 1 FSDP step without a
+        separate collective launch, or (None, 1).  2-layer classifier: ONE run-ahead launch
+        per step (csrc/mlp_fused.hip FX); deep classifier (JDT_FSDP_DEEP_FX=1): one backward
+        launch per hidden layer, each sending its tiles' partials to the row owners, which
+        apply the sharded AdamW and hand the values back (csrc/mlp_deep.hip md_bwd FX).
+        Both need AdamW, the reference's dim-0 shards of every kernel and bias (the head
+        bias replicated) with whole 16-unit column blocks per rank, not deterministic, every
+        rank's grid co-resident with the grids of the ranks sharing its GPU -- agreed by
+        all ranks (collective).  JDT_FSDP_AHEAD=0: the forward / backward / fused FSDP
+        collective step."""
         if not (self.world > 1 and batch.inputs.is_cuda and os.environ.get("JDT_FSDP_AHEAD", "1") == "1"):
             return None, 1
         from ..comm import tile_exchange as TX
         from ..runtime.dist import ranks_per_gpu
         from ..utils.train_state import AdamW
-        from .fused_mlp import deterministic, mlp2_chunk, supported
+        from .dp import _lib_md_ahead_ok
+        from .fused_mlp import FusedMLPDeep, deterministic, mlp2_chunk, supported, supported_deep
 
         sp, W, dev = self.sp, self.world, batch.inputs.device
         share = ranks_per_gpu()
         dims = {n: sp.part[n].shard_dim for n in sp.part}
-        want = {"input_dense/kernel": 0, "input_dense/bias": 0, "output_dense/kernel": 0, "output_dense/bias": None}
-        two = len(getattr(self.model, "dims", ())) == 3
-        K, H = (self.model.dims[0], self.model.dims[1]) if two else (0, 0)
-        kc = mlp2_chunk(K) if two else 0
-        # the kernel's partial stores reach a W1 chunk's first and last owner only
-        # (tile_exchange.fx_owner_span); W must divide both sharded dims
-        local = (supported(self.model, batch.size, dev) and dims == want and isinstance(self.state.tx, AdamW)
-                 and not deterministic() and K % W == 0 and H % (16 * W) == 0
-                 and TX.fx_owner_span(W, K, kc) <= 2 and TX.ahead_tx_ok(batch.size, H, share, K))
+        names = list(getattr(self.model, "names", ()))
+
+        def dim_ok(name, d):
+            # dim-0 shards (the head bias replicated); a square hidden kernel also dim 1
+            layer, leaf = name.split("/")
+            if layer == names[-1] and leaf == "bias":
+                return d is None
+            if leaf == "kernel" and layer not in (names[0], names[-1]):
+                return d in (0, 1)
+            return d == 0
+
+        base = (bool(names) and set(dims) == {f"{n}/{leaf}" for n in names for leaf in ("kernel", "bias")}
+                and all(dim_ok(n, d) for n, d in dims.items()) and isinstance(self.state.tx, AdamW)
+                and not deterministic())
+        if supported(self.model, batch.size, dev):
+            K, H = self.model.dims[0], self.model.dims[1]
+            kc = mlp2_chunk(K)
+            # the kernel's partial stores reach a W1 chunk's first and last owner only
+            # (tile_exchange.fx_owner_span); W must divide both sharded dims
+            local = (base and K % W == 0 and H % (16 * W) == 0 and TX.fx_owner_span(W, K, kc) <= 2
+                     and TX.ahead_tx_ok(batch.size, H, share, K))
+            tiles = (H // 16) * (K // kc)
+        elif supported_deep(self.model, batch.size, dev):
+            # layer 0 (784 rows, 112-row chunks) and the 512-row layers (64-row chunks)
+            local = (base and os.environ.get("JDT_FSDP_DEEP_FX", "0") == "1"
+                     and os.environ.get("JDT_MLP2_AHEAD", "1") == "1" and 784 % W == 0 and 512 % (16 * W) == 0
+                     and TX.fx_owner_span(W, 784, 112) <= 2 and TX.fx_owner_span(W, 512, 64) <= 2
+                     and bool(_lib_md_ahead_ok(batch.size)) and TX.deep_fx_ok(batch.size, share))
+            tiles = FusedMLPDeep.tx_tiles(self.model.L - 1)
+        else:
+            local, tiles = False, 0
         if not TX.agree(self.mesh.group(self.cfg.axis), local, dev):
             return None, 1
         old = getattr(self, "_txx", None)
         if old is not None:
             torch.cuda.synchronize(dev)
             old.close()
-        self._txx = TX.create_for(self.mesh, self.cfg.axis, dev, tiles=(H // 16) * (K // kc))
+        self._txx = TX.create_for(self.mesh, self.cfg.axis, dev, tiles=tiles)
         return self._txx, share
 
     def _fsdp_plan(self):

@@ -491,13 +491,14 @@ class MdArgs(ctypes.Structure):
                 ("stage_stride", ctypes.c_long), ("det_logits", c_void_p), ("step_mul", c_int),
                 ("XR", c_void_p), ("zslab", c_void_p), ("ztick", c_void_p), ("hand", c_void_p),
                 ("dzx", c_void_p), ("dzc", c_void_p), ("dzs", c_int), ("smap", c_void_p), ("wt", c_int),
-                ("tx", c_void_p), ("tx_base", c_int), ("tx_shared", c_int)]
+                ("tx", c_void_p), ("tx_base", c_int), ("tx_shared", c_int), ("tx_fsdp", c_int)]
 
 
 _lib.declare("jdt_md_layer", c_int, [ctypes.POINTER(MdArgs), c_int, c_int, c_void_p])
 _lib.declare("jdt_md_dzs_ok", c_int, [c_int])
 _lib.declare("jdt_md_args_size", c_int, [])
 _lib.declare("jdt_md_ahead_ok", c_int, [c_int])
+_lib.declare("jdt_md_fx_ok", c_int, [c_int, c_int])
 
 DEEP_H = 512
 
@@ -517,14 +518,18 @@ class FusedMLPDeep:
 
     def __init__(self, state, mesh, axis: str, num_minibatches: int, rows: int, metrics: torch.Tensor,
                  params=None, mslot: Optional[torch.Tensor] = None, fuse_opt: Optional[bool] = None,
-                 mb_rows: int = 0, mb_stride: int = 1 << 16, tx=None, ranks_on_gpu: int = 1):
+                 mb_rows: int = 0, mb_stride: int = 1 << 16, tx=None, ranks_on_gpu: int = 1, opt_params=None):
         """``tx`` (comm.tile_exchange.TileExchange, N > 1): every hidden layer's backward
         all-reduces its gradient tiles with the other ranks' launches before the fused
         AdamW (layer i's tiles at exchange offset ``tx_base(i)``), layer 0 running ahead --
-        no separate collective launch (FusedMLP2 ``tx``)."""
+        no separate collective launch (FusedMLP2 ``tx``).  ``opt_params`` (FSDP, with
+        ``tx``): the rank's LOCAL shards -- each gradient element goes to the rank owning
+        its row, which applies the sharded AdamW and hands the value back (md_bwd FX)."""
         P = params if params is not None else state.params
         self.P = P
         self.tx = tx
+        self.fsdp_tx = tx is not None and opt_params is not None
+        self.OP = opt_params if opt_params is not None else P
         self.tx_shared = int(ranks_on_gpu > 1)
         self.mslot = mslot if mslot is not None else P.metrics_slot
         self.state, self.mesh, self.axis = state, mesh, axis
@@ -551,7 +556,7 @@ class FusedMLPDeep:
         self.logits = torch.zeros(2, rows, 10, dtype=torch.float32, device=dev)
         if fuse_opt is None:
             fuse_opt = self.world == 1 and os.environ.get("JDT_FUSED_OPT", "1") == "1"
-        self.fuse_opt = bool(fuse_opt) and params is None and _is_adamw(state.tx)
+        self.fuse_opt = bool(fuse_opt) and (params is None or self.fsdp_tx) and _is_adamw(state.tx)
         kn = [f"{n}/kernel" for n in m.names]
         self.kn, self.bn = kn, [f"{n}/bias" for n in m.names]
         # second step-parity copy of the row-major shadows read after being updated in
@@ -668,6 +673,10 @@ class FusedMLPDeep:
         a.wt = int(os.environ.get("JDT_MD_WT", "1"))   # write-through AdamW state (+3 %, r4_write_through_ab.txt)
         if self.tx is not None and phase == 1:
             a.tx, a.tx_base, a.tx_shared = self.tx.args_ptr, self.tx_base(i), self.tx_shared
+            # FSDP: 1 = W row-sharded (dim 0), 2 = column-sharded (dim 1: the reference
+            # rule's choice for the square hidden kernels)
+            a.tx_fsdp = (0 if not self.fsdp_tx else
+                         2 if tuple(self.OP.p(self.kn[i]).shape)[1] != DEEP_H else 1)
         a.gW, a.gb = P.g(self.kn[i]).data_ptr(), P.g(self.bn[i]).data_ptr()
         a.gWh, a.gbh = P.g(self.kn[L - 1]).data_ptr(), P.g(self.bn[L - 1]).data_ptr()
         a.mslot = self.mslot.data_ptr()
@@ -680,11 +689,13 @@ class FusedMLPDeep:
         if getattr(self, "smap_t", None) is not None and phase == 1:
             a.smap = self.smap_t[i].data_ptr()
         if self.fuse_opt:
-            mm, vv = o["m"], o["v"]
+            # AdamW state: the whole leaves, or (FSDP FX) this rank's local shards, whose
+            # optimizer state is laid out like the local flat buffer
+            mm, vv, OP = o["m"], o["v"], self.OP
 
             def trio(name):
-                off = P.offsets[name][0]
-                return P.p(name).data_ptr(), mm[off:].data_ptr(), vv[off:].data_ptr()
+                off = OP.offsets[name][0]
+                return OP.p(name).data_ptr(), mm[off:].data_ptr(), vv[off:].data_ptr()
 
             a.pW, a.mW, a.vW = trio(self.kn[i])
             a.pb, a.mb, a.vb = trio(self.bn[i])
@@ -792,13 +803,13 @@ def make_engine(state, mesh, axis: str, num_minibatches: int, rows: int, metrics
                 params=None, mslot: Optional[torch.Tensor] = None, fuse_opt: Optional[bool] = None,
                 tx=None, ranks_on_gpu: int = 1, opt_params=None):
     """The whole-step fused engine for ``state.apply_fn`` (2-layer or deep), or None
-    if the model/shape is outside the fused kernels' envelope.  ``tx``: the 2-layer
-    engine's one-launch N > 1 step (FusedMLP2; ``opt_params``: FSDP's local shards)."""
+    if the model/shape is outside the fused kernels' envelope.  ``tx``: the one-launch
+    (2-layer) / one-launch-per-layer (deep) N > 1 step; ``opt_params``: FSDP's local shards."""
     model = state.apply_fn
     if supported(model, rows, device):
         return FusedMLP2(state, mesh, axis, num_minibatches, rows, metrics, params=params, mslot=mslot,
                          fuse_opt=fuse_opt, tx=tx, ranks_on_gpu=ranks_on_gpu, opt_params=opt_params)
     if supported_deep(model, rows, device):
         return FusedMLPDeep(state, mesh, axis, num_minibatches, rows, metrics, params=params, mslot=mslot,
-                            fuse_opt=fuse_opt, tx=tx, ranks_on_gpu=ranks_on_gpu)
+                            fuse_opt=fuse_opt, tx=tx, ranks_on_gpu=ranks_on_gpu, opt_params=opt_params)
     return None

@@ -47,7 +47,8 @@ class PsArgs(ctypes.Structure):
                 ("in_mine", c_void_p), ("flag_mine", c_void_p), ("in_prev", c_void_p), ("flag_prev", c_void_p),
                 ("in_next", c_void_p), ("flag_next", c_void_p), ("slot_bytes", c_long), ("err", c_void_p),
                 ("timeout", c_longlong),
-                ("XT", c_void_p), ("dZ", c_void_p), ("logits", c_void_p), ("ctr", c_void_p),
+                ("XT", c_void_p), ("w_mine", c_void_p), ("wflag_mine", c_void_p), ("w_prev", c_void_p),
+                ("wflag_prev", c_void_p), ("logits", c_void_p), ("ctr", c_void_p),
                 ("step", c_void_p), ("ticket", c_void_p),
                 ("lr", c_float), ("b1", c_float), ("b2", c_float), ("eps", c_float), ("wd", c_float),
                 ("gscale", c_float), ("mslot", c_void_p), ("running", c_void_p), ("stamps", c_void_p)]
@@ -59,6 +60,9 @@ _lib.declare("jdt_pp_stage", c_int, [ctypes.POINTER(PsArgs), c_int, c_int, c_voi
 _lib.declare("jdt_p2p_max_slots", c_int, [])
 _lib.declare("jdt_p2p_peer", c_int, [c_void_p, c_int, ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p),
                                      ctypes.POINTER(c_void_p)])
+
+
+W_BYTES = H * H * 2   # a stage's bf16 weight image (ops/csrc/pp_stage.hip PS_WBYTES)
 
 
 def slot_bytes(mb: int) -> int:
@@ -117,20 +121,25 @@ class PPStageKernel:
         timeout_s = spin_timeout_s(30.0)
         self.p2p = XgmiP2P(trainer.mesh.group(trainer.cfg.pipe_axis), s, S, slot_bytes(mb), 2 * self.n_mb, dev,
                            timeout_s=timeout_s)
-        self.ok = self.p2p.ok
+        # weight boxes: two slots (step parity) of a 512 x 512 bf16 image, written by the
+        # successor at its step start, read by this stage's backward (dH = dZ_next W_next^T)
+        self.wbox = XgmiP2P(trainer.mesh.group(trainer.cfg.pipe_axis), s, S, W_BYTES, 2, dev, timeout_s=timeout_s)
+        self.ok = self.p2p.ok and self.wbox.ok
         if not self.ok:
             return
         L = _lib.lib()
 
-        def peer(q):
+        def peer(box, q):
             ib, fl, er = c_void_p(), c_void_p(), c_void_p()
-            _lib.check(L.jdt_p2p_peer(self.p2p.ctx, int(q), ctypes.byref(ib), ctypes.byref(fl), ctypes.byref(er)),
+            _lib.check(L.jdt_p2p_peer(box.ctx, int(q), ctypes.byref(ib), ctypes.byref(fl), ctypes.byref(er)),
                        "jdt_p2p_peer")
             return ib.value, fl.value, er.value
 
-        mine = peer(s)
-        prev = peer(s - 1) if s > 0 else (None, None, None)
-        nxt = peer(s + 1) if s < S - 1 else (None, None, None)
+        mine = peer(self.p2p, s)
+        prev = peer(self.p2p, s - 1) if s > 0 else (None, None, None)
+        nxt = peer(self.p2p, s + 1) if s < S - 1 else (None, None, None)
+        w_mine = peer(self.wbox, s) if s < S - 1 else (None, None, None)
+        w_prev = peer(self.wbox, s - 1) if s > 0 else (None, None, None)
         P, st, model = trainer.state.params, trainer.state, trainer.model
         o = st.opt_state
         bf = dict(dtype=torch.bfloat16, device=dev)
@@ -138,7 +147,6 @@ class PPStageKernel:
         # the per-microbatch X^T blocks [n_mb][784][mbp] in an 8 x 784 x 64 region, then the
         # step's bf16 row copy [128][784] (ops/csrc/pp_stage.hip pre-pass)
         self.XT = torch.zeros(8 * 784 * 64 + 128 * 784, **bf) if self.first else None
-        self.dZ = torch.zeros(self.n_mb, mb, H, **bf)
         self.logits = torch.zeros(2, 128, C_HEAD, dtype=torch.float32, device=dev) if self.last else None
         self.ctr = torch.zeros(64 * 32, dtype=torch.int32, device=dev)
         self.stamps = None
@@ -168,7 +176,8 @@ class PPStageKernel:
         a.slot_bytes = int(self.p2p.slot_bytes)
         a.timeout = int(timeout_s * TICKS_PER_S)
         a.XT = self.XT.data_ptr() if self.XT is not None else None
-        a.dZ = self.dZ.data_ptr()
+        a.w_mine, a.wflag_mine, _ = w_mine
+        a.w_prev, a.wflag_prev, _ = w_prev
         a.ctr = self.ctr.data_ptr()
         a.step, a.ticket = o["count"].data_ptr(), o["ticket"].data_ptr()
         tx = st.tx
@@ -201,6 +210,7 @@ class PPStageKernel:
         return self.p2p.error() if self.p2p is not None else 0
 
     def close(self):
-        if self.p2p is not None:
-            self.p2p.close()
-            self.p2p = None
+        for box in ("p2p", "wbox"):
+            if getattr(self, box, None) is not None:
+                getattr(self, box).close()
+                setattr(self, box, None)

@@ -105,27 +105,33 @@ def test_dp_over_xgmi_matches_single_device(tmp_path, ws, dp_ahead, layers, widt
     assert abs(float(m[2]) - float(ref[2])) <= 4
 
 
-@pytest.mark.parametrize("ws,fused,num_layers,eps", [(2, True, 2, 1e-8), (2, False, 2, 1e-8), (2, True, 4, 1e-8),
-                                                     (2, True, 2, 10.0), (2, True, 4, 10.0), (8, True, 2, 10.0),
-                                                     (8, True, 4, 10.0), (8, False, 2, 1e-8)])
-def test_fsdp_over_xgmi_matches_single_device(tmp_path, ws, fused, num_layers, eps):
+@pytest.mark.parametrize("ws,fused,num_layers,eps,deep_fx", [
+    (2, True, 2, 1e-8, "0"), (2, False, 2, 1e-8, "0"), (2, True, 4, 1e-8, "0"), (2, True, 2, 10.0, "0"),
+    (2, True, 4, 10.0, "0"), (8, True, 2, 10.0, "0"), (8, True, 4, 10.0, "0"), (8, False, 2, 1e-8, "0"),
+    (2, True, 4, 1e-8, "1"), (2, True, 4, 10.0, "1")])
+def test_fsdp_over_xgmi_matches_single_device(tmp_path, ws, fused, num_layers, eps, deep_fx):
     """fused: the step's whole collective is ONE xg_fsdp_kernel (reduce-scatter +
     sharded AdamW + metrics fold + next-step all-gather).  eps = 10 makes AdamW's update
     ~ lr * g / eps, i.e. proportional to the gradient: a missing 1/N or 1/n_mb in the
-    fused kernel's grad scale fails (Adam with eps 1e-8 would hide it)."""
+    fused kernel's grad scale fails (Adam with eps 1e-8 would hide it).  deep_fx = "1"
+    (JDT_FSDP_DEEP_FX): the 4-layer step with no collective launch -- every hidden
+    layer's backward sends its partials to the rows' (layer 0, biases, head) or columns'
+    (square hidden kernels, dim-1 shards) owners, which apply the sharded AdamW in-kernel
+    (csrc/mlp_deep.hip md_bwd FX)."""
     from data_paral import synthetic_batch
     from jax_distributed_tuts_amd.models.mlp import Classifier
     from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
     from jax_distributed_tuts_amd.utils.config import fsdp_config
     from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
 
-    _spawn8(XW.fsdp_xgmi, ws, str(tmp_path), fused, 3, num_layers, eps)
+    _spawn8(XW.fsdp_xgmi, ws, str(tmp_path), fused, 3, num_layers, eps, deep_fx)
     res = _load(tmp_path, f"fsx{num_layers}", ws)
     assert all(o["comm"] == "xgmi" for o in res)
     assert all(o["fused_comm"] == fused for o in res)
-    # 2-layer, fused, 2 ranks: one launch per step (the in-kernel sharded tile exchange:
-    # partials to their rows' owners, sharded AdamW, updated values handed back)
-    assert all(o["one_launch"] == (fused and num_layers == 2 and ws == 2) for o in res), [o["one_launch"] for o in res]
+    # 2-layer (or 4-layer with deep_fx), fused, 2 ranks: no collective launch (the in-kernel
+    # sharded tile exchange: partials to their owners, sharded AdamW, values handed back)
+    want = fused and ws == 2 and (num_layers == 2 or deep_fx == "1")
+    assert all(o["one_launch"] == want for o in res), [o["one_launch"] for o in res]
     # every sharded leaf rides the segmented kernels (dim-0 and, 4-layer, dim-1 shards)
     assert set(res[0]["xg_names"]) == {n for n, d in res[0]["dims"].items() if d is not None}
     if num_layers == 4:

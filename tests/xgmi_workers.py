@@ -208,11 +208,14 @@ def dp_xgmi(outdir, steps_eager=2, steps_graph=6, dp_ahead="1", num_layers=2, wi
                           "one_launch": bool(tr.one_launch), "m": st.opt_state["m"].cpu()})
 
 
-def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2, eps=1e-8):
+def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2, eps=1e-8, deep_fx="0"):
     """FSDP (dropout off) with the segmented xGMI gather / reduce-scatter; every rank
     saves its local shard + the partition table for reassembly in the parent.
     num_layers=4: the square 512 x 512 hidden weights are sharded along dim 1 (the
-    reference rule) and move as 2-D column-block segments."""
+    reference rule) and move as 2-D column-block segments.  deep_fx = JDT_FSDP_DEEP_FX."""
+    import os
+
+    os.environ["JDT_FSDP_DEEP_FX"] = deep_fx
     from data_paral import synthetic_batch
     from jax_distributed_tuts_amd.models.mlp import Classifier
     from jax_distributed_tuts_amd.parallel.dp import shard_batch

@@ -65,6 +65,11 @@ def env_override(kv: Dict[str, str]):
                 os.environ[k] = v
 
 
+def _sync(dev):
+    if torch.device(dev).type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
 def close_trainer(tr):
     if tr is not None and hasattr(tr, "close"):
         tr.close()
@@ -187,7 +192,7 @@ def _inject_corruption(tr):
 
 def time_candidate(tr, batch, steps: int, dev) -> float:
     """us per step (max over ranks) of ``steps`` captured steps."""
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     D.barrier()
     t0 = time.perf_counter()
     if hasattr(tr, "run_steps"):
@@ -195,7 +200,7 @@ def time_candidate(tr, batch, steps: int, dev) -> float:
     else:
         for _ in range(steps):
             tr.step(batch)
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     dt = time.perf_counter() - t0
     return _max(dt / steps * 1e6, dev)
 
@@ -225,54 +230,56 @@ def run(cands: List[Candidate], build: Callable, prepare: Callable, dev, validat
             row["valid"] = True
             live.append(c)
             continue
+        # the env stays in force through the eager steps: engines are built (and read their
+        # switches) on the first step, not at construction
         with env_override(c.env):
             tr, batch = build(PROBE_EPS if validate else None, c)
-        try:
-            init = snapshot(tr) if validate else None
-            for i in range(VALIDATE_STEPS):
-                tr.step(batch)
-            torch.cuda.synchronize(dev)
-            # the form asked for must have engaged on every rank (its engine is built on
-            # the first step); otherwise it is the reference form under another name
-            eng = _all(bool(c.engaged(tr)), dev)
-            row["engaged"] = eng
-            err = step_error(tr)
-            if err is None and not c.reference and os.environ.get("JDT_BENCH_FAKE_TX_ERROR", "-1") == str(D.rank()):
-                err = "tile exchange wait timed out (injected: JDT_BENCH_FAKE_TX_ERROR)"
-            bad = not _all(err is None, dev)
-            if bad:
-                row["valid"] = False
-                row["reason"] = _first_reason(err)
-            elif not eng and not c.reference:
-                row["valid"] = None
-                row["reason"] = "not engaged (the trainer fell back to the reference form)"
-            elif validate:
-                if os.environ.get("JDT_BENCH_FAKE_TX_CORRUPT", "-1") == str(D.rank()) and not c.reference:
-                    _inject_corruption(tr)
-                got = snapshot(tr)
-                if c.reference:
-                    ref_state, init_state = got, init
-                    row["valid"] = True
+            try:
+                init = snapshot(tr) if validate else None
+                for i in range(VALIDATE_STEPS):
+                    tr.step(batch)
+                _sync(dev)
+                # the form asked for must have engaged on every rank (its engine is built on
+                # the first step); otherwise it is the reference form under another name
+                eng = _all(bool(c.engaged(tr)), dev)
+                row["engaged"] = eng
+                err = step_error(tr)
+                if err is None and not c.reference and os.environ.get("JDT_BENCH_FAKE_TX_ERROR", "-1") == str(D.rank()):
+                    err = "tile exchange wait timed out (injected: JDT_BENCH_FAKE_TX_ERROR)"
+                bad = not _all(err is None, dev)
+                if bad:
+                    row["valid"] = False
+                    row["reason"] = _first_reason(err)
+                elif not eng and not c.reference:
+                    row["valid"] = None
+                    row["reason"] = "not engaged (the trainer fell back to the reference form)"
+                elif validate:
+                    if os.environ.get("JDT_BENCH_FAKE_TX_CORRUPT", "-1") == str(D.rank()) and not c.reference:
+                        _inject_corruption(tr)
+                    got = snapshot(tr)
+                    if c.reference:
+                        ref_state, init_state = got, init
+                        row["valid"] = True
+                    else:
+                        e = compare(init_state, got, ref_state)
+                        worst = {k: _max(v, dev) for k, v in e.items()}
+                        row["err"] = {k: float(f"{v:.3g}") for k, v in worst.items()}
+                        ok = all(worst[k] <= REL_TOL for k in ("p", "m", "v") if k in worst)
+                        ok = ok and worst.get("block", 0.0) <= BLOCK_TOL
+                        row["valid"] = _all(ok, dev)
+                        if not row["valid"]:
+                            row["reason"] = "state differs from the reference form"
+                    if row["valid"] and c.replicated and not c.reference:
+                        # DP: the masters are replicated -- bit-identical on every rank
+                        rep = replicated_bitwise(got["p"], dev)
+                        row["replicated"] = rep
+                        if not rep:
+                            row["valid"] = False
+                            row["reason"] = "masters not bit-identical across ranks"
                 else:
-                    e = compare(init_state, got, ref_state)
-                    worst = {k: _max(v, dev) for k, v in e.items()}
-                    row["err"] = {k: float(f"{v:.3g}") for k, v in worst.items()}
-                    ok = all(worst[k] <= REL_TOL for k in ("p", "m", "v") if k in worst)
-                    ok = ok and worst.get("block", 0.0) <= BLOCK_TOL
-                    row["valid"] = _all(ok, dev)
-                    if not row["valid"]:
-                        row["reason"] = "state differs from the reference form"
-                if row["valid"] and c.replicated and not c.reference:
-                    # DP: the masters are replicated -- bit-identical on every rank
-                    rep = replicated_bitwise(got["p"], dev)
-                    row["replicated"] = rep
-                    if not rep:
-                        row["valid"] = False
-                        row["reason"] = "masters not bit-identical across ranks"
-            else:
-                row["valid"] = True
-        finally:
-            close_trainer(tr)
+                    row["valid"] = True
+            finally:
+                close_trainer(tr)
         if row["valid"]:
             live.append(c)
     # timing: each surviving candidate built with the run's own optimizer, captured,

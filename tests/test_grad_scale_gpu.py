@@ -265,7 +265,8 @@ def _load(d, name, ws):
 
 @pytest.mark.parametrize("kind,ws", [("dp_sgd", 2), ("dp_adam_eps", 2), ("dp4_adam_eps", 2), ("fsdp_sgd", 2),
                                      ("fsdp_loop_sgd", 2), ("fsdp_loop_sgd", 4), ("dp_sgd", 8), ("dp_adam_eps", 8),
-                                     ("dp4_adam_eps", 8), ("fsdp_sgd", 8), ("fsdp_loop_sgd", 8)])
+                                     ("dp4_adam_eps", 8), ("fsdp_sgd", 8), ("fsdp_loop_sgd", 8),
+                                     ("fsdp4_adam_eps", 2), ("fsdp4_adam_eps", 8)])
 def test_xgmi_strategies_grad_scale(tmp_path, kind, ws):
     """dp4_adam_eps at ws = 2: the 4-layer DP step with every hidden layer's backward
     exchanging its tiles in-kernel (AdamW eps = 10: the update is ~ the gradient);
@@ -278,14 +279,45 @@ def test_xgmi_strategies_grad_scale(tmp_path, kind, ws):
     res = _load(tmp_path, f"gpx_{kind}", ws)
     assert all(o["comm"] == "xgmi" for o in res)
     b = _batch()
-    names = (["input_dense", "hidden_dense_1", "hidden_dense_2", "output_dense"] if kind == "dp4_adam_eps"
+    deep = kind in ("dp4_adam_eps", "fsdp4_adam_eps")
+    names = (["input_dense", "hidden_dense_1", "hidden_dense_2", "output_dense"] if deep
              else ["input_dense", "output_dense"])
+    if kind == "fsdp4_adam_eps":
+        # 2 ranks: the in-kernel owner exchange (no step collective)
+        assert all(o["one_launch"] == (ws == 2) for o in res), [o["one_launch"] for o in res]
     want = mlp_grads_fp64(res[0]["before"], names, b.inputs, b.labels, n_mb=4)
     for o in res:
         for n in want:
             d = o["before"][n].double() - o["after"][n].double()
-            g = 10 * d / (1 - d.abs()) if kind in ("dp_adam_eps", "dp4_adam_eps") else d
+            g = 10 * d / (1 - d.abs()) if kind.endswith("adam_eps") else d
             check_grad(g, want[n], n)
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+def test_pipeline_stage_kernel_adam_scale(tmp_path, ws):
+    """One layer per stage, AdamW eps = 10 (update ~ gradient): each stage's step is the
+    in-kernel GPipe launch (ops/csrc/pp_stage.hip: dZ hops, dH from the successor's weight
+    image, register-held dW, AdamW at the end) -- its update equals the fp64 oracle's."""
+    from pipeline_parallel import pp_mlp_dims
+    from jax_distributed_tuts_amd.models.mlp import MLP
+    from jax_distributed_tuts_amd.utils.config import dp_config
+
+    from . import xgmi_workers as XW
+
+    spawn8(functools.partial(XW.grad_probe_xgmi, kind="pp_adam_eps", dp=1, n_hidden=ws), ws, str(tmp_path))
+    res = _load(tmp_path, "gpx_pp_adam_eps", ws)
+    assert all(o["comm"] == "xgmi" and o["pp_kernel"] for o in res), [(o["comm"], o["pp_kernel"]) for o in res]
+    before, got = {}, {}
+    for o in res:
+        before.update(o["before"])
+        for k in o["before"]:
+            d = o["before"][k].double() - o["after"][k].double()
+            got[k] = 10 * d / (1 - d.abs())
+    b = _batch()
+    want = mlp_grads_fp64(before, MLP(pp_mlp_dims(dp_config(), ws)).names, b.inputs, b.labels, n_mb=4)
+    assert set(got) == set(want)
+    for n in want:
+        check_grad(got[n], want[n], n)
 
 
 @pytest.mark.parametrize("ws,dp,n_hidden", [(2, 1, 3), (4, 2, 3), (8, 1, 7), (8, 2, 3)])

@@ -415,6 +415,7 @@ def grad_probe_xgmi(outdir, kind, dp=1, capture=True, n_hidden=3):
     def cpu(d):
         return {k: v.detach().float().cpu().clone() for k, v in d.items()}
 
+    extra = {}
     if kind in ("dp_sgd", "dp_adam_eps", "dp4_adam_eps"):
         os.environ["JDT_DP_DEEP_TX"] = "1"   # dp4: the deep engine's (opt-in) exchange path where it fits
         mesh = D.Mesh({"data": D.world_size()})
@@ -461,19 +462,41 @@ def grad_probe_xgmi(outdir, kind, dp=1, capture=True, n_hidden=3):
         tr.finalize()
         after = cpu(tr.full_params())
         comm = tr.comm_backend
-    elif kind == "pp_sgd":
+    elif kind == "fsdp4_adam_eps":
+        # the deep FSDP step with every hidden layer's backward sending its partials to the
+        # shard owners (md_bwd FX, JDT_FSDP_DEEP_FX=1; at 8 shared ranks the grids do not
+        # fit: the step collective form)
+        from jax_distributed_tuts_amd.parallel.fsdp import FSDPConfig, FSDPTrainer, init_fsdp
+
+        os.environ["JDT_FSDP_DEEP_FX"] = "1"
+        mesh = D.Mesh({"data": D.world_size()})
+        st = init_fsdp(Classifier(num_layers=4, dropout_rate=0.0), adamw(1.0, eps=10.0, weight_decay=0.0), 69, dev,
+                       mesh, "data", 16)
+        b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
+        tr = FSDPTrainer(st, mesh, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=True,
+                                              comm="xgmi"))
+        before = cpu(tr.full_params())
+        tr.step(Batch(b.inputs.to(dev), b.labels.to(dev)))
+        tr.finalize()
+        after = cpu(tr.full_params())
+        comm = tr.comm_backend
+        extra["one_launch"] = bool(tr.one_launch)
+    elif kind in ("pp_sgd", "pp_adam_eps"):
         from pipeline_parallel import build_mlp_pipeline
 
         mesh = D.Mesh({"data": dp, "pipe": D.world_size() // dp})
+        # pp_adam_eps with one layer per stage: the in-kernel GPipe stage step (AdamW only)
+        tx = sgd(1.0) if kind == "pp_sgd" else adamw(1.0, eps=10.0, weight_decay=0.0)
         tr = build_mlp_pipeline(cfg, mesh, dev, n_hidden_layers=n_hidden, dropout_rate=0.0, num_microbatches=4,
-                                comm="xgmi", tx=sgd(1.0))
+                                comm="xgmi", tx=tx)
         b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
         before = cpu(tr.state.params.state_dict())
         tr.step(Batch(b.inputs.to(dev), b.labels.to(dev)))
         tr.finalize()
         after = cpu(tr.state.params.state_dict())
         comm = tr.comm_backend
+        extra["pp_kernel"] = getattr(tr, "pp_kernel", None) is not None
     else:
         raise ValueError(kind)
     torch.cuda.synchronize()
-    _save(outdir, f"gpx_{kind}", {"before": before, "after": after, "comm": comm})
+    _save(outdir, f"gpx_{kind}", {"before": before, "after": after, "comm": comm, **extra})

@@ -5,8 +5,8 @@ cd /root/repo && export TMPDIR=/tmp PYTHONUNBUFFERED=1 && mkdir -p gpurun_out/r5
 ( while sleep 30; do echo "[hb] $(date +%T)"; done ) & HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
-timeout -k 10 600 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_xgmi_gpu.py \
-  -k "pipeline or fsdp_over" > gpurun_out/r5s10/pytest.log 2>&1
+timeout -k 10 700 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_xgmi_gpu.py \
+  tests/test_grad_scale_gpu.py -k "pipeline or fsdp_over or stage_kernel or fsdp4" > gpurun_out/r5s10/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "PASSED|FAILED|Error|assert" gpurun_out/r5s10/pytest.log | head -40
 fatal $rc && exit $rc
 [ $rc -ne 0 ] && { grep -v amdgpu.ids gpurun_out/r5s10/pytest.log | tail -60; exit 1; }

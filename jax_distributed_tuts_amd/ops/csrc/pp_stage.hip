@@ -6,27 +6,33 @@
 // direction, a receive kernel, the layer's md_fwd / md_bwd launch, a dX GEMM and a
 // send kernel: 3-4 dependent launches of ~4 us each for a 64 x 512 x 512 layer, so a
 // tick costs ~13 us and an 8-stage pipeline cannot beat one GPU.  Here the whole
-// fill / drain schedule of the step runs inside one launch of 32 workgroups per rank,
-// workgroup b owning output columns [16b, 16b + 16) of the stage's layer:
+// fill / drain schedule of the step runs inside one launch of 32 workgroups per rank.
+// Workgroup b = 2 cb + h owns output columns [32 cb, 32 cb + 32) of the stage's layer
+// for rows [h mb/2, (h+1) mb/2) of every microbatch: a hop's input (the previous stage's
+// activation, the next stage's dZ) is read once per column block per row half, so each
+// workgroup loads half the bytes of a column-only split -- the per-workgroup read rate
+// of freshly handed-off data is what bounds a tick (stamps: profiles/r5_pp_intile_stamps.txt).
 //
-//   step start:      W (fp32 master) -> bf16 LDS image; a stage > 0 also writes that image
-//                    into its predecessor's weight box (second inbox, by step parity);
-//                    stage 0 converts the step's data to bf16 rows and per-microbatch X^T
-//   forward tick i:  wait for the 32 producer flags of inbox slot i (or read the data),
-//                    Z = X W[:, own] + b on MFMA (K split over the 4 waves), SiLU,
-//                    dropout (the md kernels' Philox streams), backward factor G kept in
-//                    LDS; the H tile goes straight into the NEXT stage's inbox (H and
-//                    H^T, system-scope stores over xGMI) and one flag per workgroup is
-//                    raised -- or, last stage, the head's partial logits (fp32 atomics)
-//   backward tick i: dH[:, own] = dZ_next W_next[own, :]^T from the successor's dZ
+//   step start:      W[:, own] (fp32 master) -> bf16 LDS image; a stage > 0 also writes
+//                    its image into its predecessor's weight box (second inbox, by step
+//                    parity); stage 0 writes the step's data transposed per microbatch
+//                    (X^T, the dW operand; its forward reads the fp32 rows directly)
+//   forward tick i:  wait for the flags of the 16 producers of this row half (per wave:
+//                    only the 2 whose columns are its k range), Z = X W[:, own] + b on
+//                    MFMA (K split over the 8 waves), SiLU, dropout (the md kernels' Philox
+//                    streams), backward factor G kept in LDS; H and H^T of the tile go
+//                    straight into the NEXT stage's inbox (system-scope stores over xGMI)
+//                    and one flag per workgroup is raised -- or, last stage, the head's
+//                    partial logits (fp32 atomics, one arrival counter per row half)
+//   backward tick i: dH[half, own] = dZ_next W_next[own, :]^T from the successor's dZ
 //                    (inbox) and weight image (weight box) on MFMA -- or, last stage, CE
 //                    of the complete logits through the head; dZ = dH * G goes straight
-//                    to the predecessor's inbox (not stage 0) with one flag per workgroup,
-//                    so a backward hop is shaped like a forward one (no intra-stage
-//                    gather); then dW[:, own] += X^T dZ (registers, over the
-//                    microbatches; X^T prefetched ahead of the wait) and db
-//   end of step:     AdamW on the owned columns (gradient scale 1 / n_mb), bf16 shadows,
-//                    metrics fold, step advance (arrival ticket).
+//                    to the predecessor's inbox (not stage 0); then dW[:, own] += X^T dZ
+//                    over this row half (registers; X^T prefetched ahead of the wait), db
+//   end of step:     the two row halves of a column block swap the partial dW rows the
+//                    other one updates (write-through + a pair counter); AdamW on the
+//                    owned rows (gradient scale 1 / n_mb), bf16 shadows, metrics fold,
+//                    step advance (arrival ticket).
 //
 // Every wait is on another workgroup that is resident (32 workgroups, all co-resident,
 // host-checked) or on a neighbour stage's launch, and bounded (s_memrealtime) into the
@@ -35,25 +41,33 @@
 // no host bookkeeping; slot reuse is race-free by GPipe's own dependencies (the
 // producer overwrites slot i of step t+1 only after every gradient of step t arrived).
 // Reference semantics: the intended GPipe of /root/reference/pipeline_parallel.py:37-38
-// (SURVEY section 3.5); gradients equal the un-split model's (tests/test_pp_kernel_gpu.py).
+// (SURVEY section 3.5); gradients equal the un-split model's (tests/test_grad_scale_gpu.py
+// test_pipeline_stage_kernel_adam_scale, tests/test_xgmi_gpu.py).
 #include "common.h"
 
 namespace jdt {
 
-constexpr int PS_NT = 512;         // 8 waves: twice the loads in flight per workgroup of the
-                                   // 4-wave form (a hop's A operand is read at a per-block
-                                   // rate that grows with outstanding loads)
+constexpr int PS_NT = 512;         // 8 waves (outstanding loads per workgroup)
 constexpr int PS_NW = PS_NT / 64;
-constexpr int PS_NB = 32;          // workgroups = 512 / 16 output column blocks
+constexpr int PS_NB = 32;          // workgroups: 16 column blocks x 2 row halves
+constexpr int PS_CB = 32;          // columns per workgroup
 constexpr int PS_N = 512;          // layer width
-constexpr int PS_MAXMB = 64;       // rows per microbatch
+constexpr int PS_MAXMB = 64;       // rows per microbatch (32 or 64: 16-row MFMA tiles per half)
+constexpr int PS_MAXH = PS_MAXMB / 2;
 constexpr int PS_MAXROWS = 128;    // rows per step (n_mb * mb)
 constexpr int PS_MAXNMB = 8;
 constexpr int PS_C = 10;
 constexpr int PS_FLAG_BLOCKS = 32; // comm/csrc/p2p.hip P2P_MAX_BLOCKS (flags per slot)
+constexpr int PS_UPWMAX = (784 / 16 + PS_NW - 1) / PS_NW;   // dW k tiles per wave (stage 0: 7)
+// pair-exchange slab per workgroup (floats): the partner's dW column tile [wave][tile][lane][4],
+// then db (32), dW_h (32 x C), db_h (C), loss / correct sums
+constexpr int PS_PAIR_DW = PS_NW * PS_UPWMAX * 256;   // one 16-column tile
+constexpr int PS_PAIR_DB = PS_PAIR_DW, PS_PAIR_WH = PS_PAIR_DB + PS_CB, PS_PAIR_BH = PS_PAIR_WH + PS_CB * PS_C,
+              PS_PAIR_MET = PS_PAIR_BH + PS_C;
+constexpr int PS_PAIR = PS_PAIR_MET + 2 + 30;
 
 struct PsArgs {
-  int n_mb, mb;                    // microbatches, rows per microbatch (mb % 16 == 0, <= 64)
+  int n_mb, mb;                    // microbatches, rows per microbatch (32 or 64; n_mb * mb = 128)
   int K;                           // layer input width (784: stage 0, else 512)
   int gid;                         // global layer index (dropout stream id)
   int mb_shift;                    // dropout offset of microbatch i: (i << mb_shift) + (gid << 1)
@@ -67,7 +81,7 @@ struct PsArgs {
   const float* X;                  // stage 0: data [n_mb * mb][784] fp32
   const int* labels;               // last stage: [n_mb * mb]
   // inboxes (comm/csrc/p2p.hip layout): slot i < n_mb: activation of microbatch i (H
-  // [mb][512] bf16, then H^T [512][mbp]); slot n_mb + i: its gradient dX [mb][512]
+  // [mb][512] bf16, then H^T [512][mb]); slot n_mb + i: the successor's dZ [mb][512]
   char* in_mine; unsigned* flag_mine;
   char* in_prev; unsigned* flag_prev;   // rank of stage s-1 (null at stage 0)
   char* in_next; unsigned* flag_next;   // rank of stage s+1 (null at the last stage)
@@ -75,8 +89,7 @@ struct PsArgs {
   int* err;                        // this rank's inbox error word (a wait timed out)
   long long timeout;               // s_memrealtime ticks per wait
   // scratch (zero-initialised once by the host)
-  bf16_t* XT;                      // stage 0: X^T [PS_MAXNMB][784][PS_MAXMB] bf16 (per microbatch, stride
-                                   // K * mbp), then the bf16 row copy [PS_MAXROWS][784]
+  bf16_t* XT;                      // stage 0: X^T [n_mb][784][mb] bf16 (the dW operand)
   // weight boxes (a second p2p inbox of two PS_WBYTES slots, by step parity): a stage > 0
   // writes the bf16 image of its W [512][512] into its predecessor's box at the start of
   // the step; the predecessor's backward forms dH = dZ_next W_next^T itself, so a backward
@@ -85,6 +98,7 @@ struct PsArgs {
   char* w_prev; unsigned* wflag_prev;
   float* logits;                   // last stage: [2][n_mb][mb][C] fp32, by step parity
   unsigned* ctr;                   // arrival counters, one 128-byte line each
+  float* pair;                     // [PS_NB][PS_PAIR] partial-gradient swap of the row halves
   int* step; unsigned* ticket;     // device optimizer step, end-of-step ticket
   float lr, b1, b2, eps, wd, gscale;
   float* mslot; float* running;    // last stage: metric slots (loss, n, correct, n), running sums
@@ -96,8 +110,8 @@ struct PsArgs {
     if (a.stamps && threadIdx.x == 0) a.stamps[(long)blockIdx.x * 24 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
-constexpr int CPOL_SC1 = 16;
-constexpr long PS_WBYTES = (long)PS_N * PS_N * 2;       // agent-coherent (write-through / past L1) buffer access
+constexpr int CPOL_SC1 = 16;       // agent-coherent (write-through / past L1) buffer access
+constexpr long PS_WBYTES = (long)PS_N * PS_N * 2;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t ps_rsrc(const void* base, long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(sgpr_ptr(const_cast<void*>(base)), (short)0,
@@ -111,6 +125,11 @@ template <int CPOL>
 __device__ __forceinline__ void ps_store16(__amdgpu_buffer_rsrc_t r, long byte_off, u32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sys_u32x4, v), r, (int)byte_off, 0, CPOL);
 }
+__device__ __forceinline__ void ps_store8(__amdgpu_buffer_rsrc_t r, long byte_off, unsigned lo, unsigned hi, int cpol_sys) {
+  const __attribute__((ext_vector_type(2))) unsigned v = {lo, hi};
+  if (cpol_sys) __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)byte_off, 0, CPOL_SYS);
+  else __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)byte_off, 0, CPOL_SC1);
+}
 
 // this rank's error word: once a wait timed out, every later wait of the step gives up
 // at once (the results are refused by the host anyway), so a dead peer costs one timeout
@@ -119,43 +138,35 @@ __device__ __forceinline__ bool ps_failed(const int* err) {
                            __HIP_MEMORY_SCOPE_SYSTEM) != 0;
 }
 
+__device__ __forceinline__ void ps_poll(const unsigned* f, unsigned epoch, long long timeout, int* err) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while ((int)(tx_flag_load(f) - epoch) < 0) {
+    if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout) {
+      __hip_atomic_store((__attribute__((address_space(1))) int*)err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // Wait until all PS_FLAG_BLOCKS producer flags of `slot` reached `epoch` (wave 0, one
 // lane per flag), then the workgroup barrier.  Bounded: a timeout raises *err.
 __device__ __forceinline__ void ps_wait_slot(const unsigned* flags, int slot, unsigned epoch, long long timeout,
                                              int* err) {
-  if (threadIdx.x < PS_FLAG_BLOCKS && !ps_failed(err)) {
-    const unsigned* f = flags + (long)slot * PS_FLAG_BLOCKS + threadIdx.x;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while ((int)(tx_flag_load(f) - epoch) < 0) {
-      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout) {
-        __hip_atomic_store((__attribute__((address_space(1))) int*)err, 1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
+  if (threadIdx.x < PS_FLAG_BLOCKS && !ps_failed(err))
+    ps_poll(flags + (long)slot * PS_FLAG_BLOCKS + threadIdx.x, epoch, timeout, err);
   __syncthreads();
 }
 
-// Wave w's share of a 512-deep product (k in [64w, 64w + 64) with 8 waves) comes from
-// producer workgroups [4w, 4w + 4): those lanes poll just their flags, no workgroup barrier (the
-// data loads that follow are issued after the loop exits: in-order issue per wave).
-__device__ __forceinline__ void ps_wait_wave(const unsigned* flags, int slot, unsigned epoch, long long timeout,
-                                             int* err) {
+// Wave w's share of a 512-deep product (k in [64w, 64w + 64)) comes from the producers
+// of column blocks 2w and 2w + 1 in row half h (workgroups 4w + h, 4w + 2 + h): two lanes
+// poll just those flags, no workgroup barrier (the data loads that follow are issued
+// after the loop exits: in-order issue per wave).
+__device__ __forceinline__ void ps_wait_wave(const unsigned* flags, int slot, int h, unsigned epoch,
+                                             long long timeout, int* err) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane < PS_FLAG_BLOCKS / PS_NW && !ps_failed(err)) {
-    const unsigned* f = flags + (long)slot * PS_FLAG_BLOCKS + w * (PS_FLAG_BLOCKS / PS_NW) + lane;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while ((int)(tx_flag_load(f) - epoch) < 0) {
-      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout) {
-        __hip_atomic_store((__attribute__((address_space(1))) int*)err, 1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
+  if (lane < 2 && !ps_failed(err))
+    ps_poll(flags + (long)slot * PS_FLAG_BLOCKS + 4 * w + 2 * lane + h, epoch, timeout, err);
   asm volatile("" ::: "memory");
 }
 
@@ -166,17 +177,17 @@ __device__ __forceinline__ void ps_raise(unsigned* peer_flags, int slot, unsigne
   if (threadIdx.x == 0) tx_flag_store(peer_flags + (long)slot * PS_FLAG_BLOCKS + blockIdx.x, epoch);
 }
 
-// All PS_NB workgroups of this launch arrive at counter line `c` (stores drained, one
-// agent-scope add each); the target -- the next multiple of PS_NB above this workgroup's
-// own ticket, so the counter never needs a reset -- is returned (lane 0 of wave 0) for a
-// later ps_wait: work placed between the two overlaps the other workgroups' arrival.
-__device__ __forceinline__ unsigned ps_arrive(unsigned* ctr, int c) {
+// `cnt` workgroups arrive at counter line `c` (stores drained, one agent-scope add each);
+// the target -- the next multiple of cnt above this workgroup's own ticket, so the counter
+// never needs a reset -- is returned (lane 0 of wave 0) for a later ps_wait: work placed
+// between the two overlaps the other workgroups' arrival.
+__device__ __forceinline__ unsigned ps_arrive(unsigned* ctr, int c, unsigned cnt) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   unsigned target = 0;
   if (threadIdx.x == 0) {
     const unsigned old = __hip_atomic_fetch_add(ctr + 32 * c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    target = (old / PS_NB + 1u) * PS_NB;
+    target = (old / cnt + 1u) * cnt;
   }
   return target;
 }
@@ -184,7 +195,11 @@ __device__ __forceinline__ void ps_wait(unsigned* ctr, int c, unsigned target, l
   if (threadIdx.x == 0) {
     const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(ctr + 32 * c, (short)0, 4, 0x00020000);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (!ps_failed(err) && (int)((unsigned)__builtin_amdgcn_raw_buffer_load_b32(cr, 0, 0, CPOL_SC1) - target) < 0) {
+    // (the error word -- a system-scope load -- only every 64th poll: it would set the poll
+    // period)
+    for (unsigned spins = 0; (int)((unsigned)__builtin_amdgcn_raw_buffer_load_b32(cr, 0, 0, CPOL_SC1) - target) < 0;
+         ++spins) {
+      if ((spins & 63) == 63 && ps_failed(err)) break;
       if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout) {
         __hip_atomic_store((__attribute__((address_space(1))) int*)err, 2, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
@@ -196,13 +211,12 @@ __device__ __forceinline__ void ps_wait(unsigned* ctr, int c, unsigned target, l
   }
   __syncthreads();
 }
-__device__ __forceinline__ void ps_arrive_wait(unsigned* ctr, int c, long long timeout, int* err) {
-  ps_wait(ctr, c, ps_arrive(ctr, c), timeout, err);
-}
 
-// counter lines: stage 0's bf16 X / X^T pre-pass done, logits of i complete (last stage)
-__device__ __forceinline__ int ps_ctr_xt(int i) { return i; }
-__device__ __forceinline__ int ps_ctr_lg(int i) { return PS_MAXNMB + i; }
+// counter lines: stage 0's X^T pre-pass done; logits of microbatch i, row half h complete
+// (last stage); the row-half pair of column block cb swapped its partials
+__device__ __forceinline__ int ps_ctr_xt() { return 0; }
+__device__ __forceinline__ int ps_ctr_lg(int i, int h) { return 8 + 2 * i + h; }
+__device__ __forceinline__ int ps_ctr_pair(int cb) { return 24 + cb; }
 
 template <bool FIRST, bool LAST>
 __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
@@ -212,29 +226,30 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
   constexpr int LDWC = KP + 8;                  // padded LDS rows (bank spread)
   constexpr int LDWR = PS_N + 8;
   constexpr int NTK = K / 16;                   // 16-wide k tiles of dW^T (49 or 32)
-  constexpr int UPW = (NTK + PS_NW - 1) / PS_NW; // dW^T tiles per wave
+  constexpr int NTK_H = (NTK + 1) / 2;          // row half 0 updates k tiles [0, NTK_H)
+  constexpr int UPW = (NTK + PS_NW - 1) / PS_NW; // dW^T k tiles per wave
   constexpr int TPW = (KS + PS_NW - 1) / PS_NW;  // forward k-steps per wave
-  constexpr int LDT = PS_MAXMB + 8;
-  constexpr int MMT = PS_MAXMB / 16;            // 16-row tiles of a microbatch
   constexpr int KSW = (PS_N / 32) / PS_NW;      // k-steps per wave of a 512-deep product
-  static_assert(KSW * 32 / 16 == PS_FLAG_BLOCKS / PS_NW, "a wave's k range = its producers' columns");
-  static_assert(K % 16 == 0, "dW tiles");
-  __shared__ __attribute__((aligned(16))) bf16_t wc[16 * LDWC];                 // W[:, own]^T
-  __shared__ __attribute__((aligned(16))) bf16_t wr[LAST ? 8 : 16 * LDWR];     // W_next[own rows, :]
-  __shared__ float part[PS_NW][PS_MAXMB][17];
-  __shared__ float gl[PS_MAXROWS][16];                                          // backward factor G
-  __shared__ __attribute__((aligned(16))) bf16_t ht[PS_MAXMB][24];             // this tick's H tile
-  __shared__ __attribute__((aligned(16))) bf16_t hown[LAST ? PS_MAXROWS : 1][16];  // head input (own cols)
-  __shared__ __attribute__((aligned(16))) bf16_t dzT[16 * LDT];                // dZ[:, own]^T
-  __shared__ float dlog[LAST ? PS_MAXMB : 1][PS_C + 1];
-  __shared__ float whs[16][PS_C];
-  __shared__ float bsh[16];
+  constexpr int MTH = PS_MAXH / 16;             // 16-row tiles of a row half (max)
+  constexpr int LDT = 32 + 8;                   // dzT rows: 32 (the dW k-step; half rows + zeros)
+  static_assert(K % 16 == 0 && UPW <= PS_UPWMAX, "dW tiles");
+  static_assert(KSW * 32 == 64 && PS_NW * 64 == PS_N, "a wave's k range = two producers' column blocks");
+  __shared__ __attribute__((aligned(16))) bf16_t wc[PS_CB * LDWC];                 // W[:, own]^T
+  __shared__ __attribute__((aligned(16))) bf16_t wr[LAST ? 8 : PS_CB * LDWR];      // W_next[own rows, :]
+  __shared__ float part[PS_NW][PS_MAXH][PS_CB + 1];
+  __shared__ float gl[PS_MAXROWS / 2][PS_CB];                                     // G of own rows / cols
+  __shared__ __attribute__((aligned(16))) bf16_t ht[PS_MAXH][PS_CB + 8];          // this tick's H tile
+  __shared__ __attribute__((aligned(16))) bf16_t hown[LAST ? PS_MAXROWS / 2 : 1][PS_CB];  // head input
+  __shared__ __attribute__((aligned(16))) bf16_t dzT[PS_CB * LDT];                // dZ[half, own]^T
+  __shared__ float dlog[LAST ? PS_MAXH : 1][PS_C + 1];
+  __shared__ float whs[PS_CB][PS_C];
+  __shared__ float bsh[PS_CB];
   __shared__ float red[2][PS_NW];
-  __shared__ unsigned tgt[PS_MAXNMB];                                           // counter targets (lane 0)
+  __shared__ unsigned tgt[PS_MAXNMB];                                             // counter targets (lane 0)
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x, j0 = 16 * b;
-  const int mb = a.mb, n_mb = a.n_mb, mbp = (mb + 31) & ~31;
+  const int b = blockIdx.x, cb = b >> 1, h = b & 1, j0 = PS_CB * cb;
+  const int mb = a.mb, n_mb = a.n_mb, mh = mb >> 1, MT = mh / 16;
   const int step = a.step[0], par = step & 1;
   const unsigned epoch = (unsigned)step + 1u;
   const unsigned long long dbase = (unsigned long long)(unsigned)step << 32;
@@ -242,35 +257,58 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
   PS_STAMP(0);
 
   // ---- 0. this step's weights into LDS (bf16 rounding of the fp32 masters = the
-  // shadows): every load first, then the images (a load-store loop would pay one round
-  // trip per iteration); stage 0's data rows for the pre-pass below load with them
+  // shadows): every load first, then the images; stage 0's data rows for the X^T
+  // pre-pass load with them
   static_assert(!FIRST || K / 4 <= PS_NT, "one float4 column per thread");
-  const int rr = 4 * b;   // stage 0: this workgroup's 4 data rows of the step
   float4 xpre[FIRST ? 4 : 1];
+  // the forward's k-steps of this wave: [w KS / 8, (w+1) KS / 8) of every 16-row tile
+  const int ks0 = (w * KS) / PS_NW, ks1 = ((w + 1) * KS) / PS_NW;
+  // stage 0: the fp32 data rows of microbatch i's row half for this wave's k-steps
+  // (software-pipelined: microbatch i + 1's loads fly during tick i).  k past 784 (the
+  // 25th k-step's upper half) reads the next row or, past the buffer, zero (bounds
+  // check): finite values times wc's zero padding
+  float4 xf[FIRST ? MTH : 1][FIRST ? TPW : 1][2];
+  auto load_x = [&](int i) {
+    if constexpr (FIRST) {
+      const int r0 = i * mb + h * mh;
+      const __amdgpu_buffer_rsrc_t xr = ps_rsrc(a.X + (long)r0 * K, (long)(PS_MAXROWS - r0) * K * 4);
+#pragma unroll
+      for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int mt = 0; mt < MTH; ++mt) {
+          if (mt >= MT) continue;
+          const int ks = min(ks0 + t, ks1 - 1), row = mt * 16 + (lane & 15);
+          const long off = ((long)row * K + ks * 32 + 8 * (lane >> 4)) * 4;
+          xf[mt][t][0] = __builtin_bit_cast(float4, ps_load16<0>(xr, off));
+          xf[mt][t][1] = __builtin_bit_cast(float4, ps_load16<0>(xr, off + 16));
+        }
+    }
+  };
+  load_x(0);
   {
-    constexpr int WC4 = (K * 4 + PS_NT - 1) / PS_NT;   // float4 of W[:, own] per thread
+    constexpr int WC4 = (K * (PS_CB / 4) + PS_NT - 1) / PS_NT;   // float4 of W[:, own] per thread
     float4 wv[WC4];
 #pragma unroll
     for (int t = 0; t < WC4; ++t) {
-      const int idx = min(tid + t * PS_NT, K * 4 - 1);
-      wv[t] = *reinterpret_cast<const float4*>(a.p + (long)(idx >> 2) * PS_N + j0 + 4 * (idx & 3));
+      const int idx = min(tid + t * PS_NT, K * (PS_CB / 4) - 1);
+      wv[t] = *reinterpret_cast<const float4*>(a.p + (long)(idx >> 3) * PS_N + j0 + 4 * (idx & 7));
     }
     if constexpr (FIRST) {
       if (tid < K / 4)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) xpre[e] = *reinterpret_cast<const float4*>(a.X + (long)(rr + e) * K + 4 * tid);
+        for (int e = 0; e < 4; ++e) xpre[e] = *reinterpret_cast<const float4*>(a.X + (long)(4 * b + e) * K + 4 * tid);
     }
-    const float bv = a.pb[j0 + (tid & 15)];
-    float hv = 0.f, hbv = 0.f;
+    const float bv = a.pb[j0 + (tid & 31)];
+    float hv = 0.f;
     if constexpr (LAST) {
-      const int t = min(tid, 16 * PS_C - 1);
+      const int t = min(tid, PS_CB * PS_C - 1);
       hv = a.ph[(long)(j0 + t / PS_C) * PS_C + t % PS_C];
     }
 #pragma unroll
     for (int t = 0; t < WC4; ++t) {
       const int idx = tid + t * PS_NT;
-      if (idx < K * 4) {
-        const int k = idx >> 2, q = idx & 3;
+      if (idx < K * (PS_CB / 4)) {
+        const int k = idx >> 3, q = idx & 7;
         wc[(4 * q + 0) * LDWC + k] = f2bf(wv[t].x);
         wc[(4 * q + 1) * LDWC + k] = f2bf(wv[t].y);
         wc[(4 * q + 2) * LDWC + k] = f2bf(wv[t].z);
@@ -278,176 +316,171 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
       }
     }
     if constexpr (KP > K)
-      for (int idx = tid; idx < 16 * (KP - K); idx += PS_NT) wc[(idx / (KP - K)) * LDWC + K + idx % (KP - K)] = 0;
+      for (int idx = tid; idx < PS_CB * (KP - K); idx += PS_NT) wc[(idx / (KP - K)) * LDWC + K + idx % (KP - K)] = 0;
     if constexpr (!FIRST) {
-      // W[:, own] (bf16) into the predecessor's weight box, slot = step parity; its flag
-      // goes up after the forward ticks (their sends drain these stores too)
+      // W[:, own] (bf16) into the predecessor's weight box, slot = step parity (row half h
+      // writes rows [h K/2, (h+1) K/2)); its flag goes up after the forward ticks (their
+      // sends drain these stores too)
       const __amdgpu_buffer_rsrc_t wo = ps_rsrc(a.w_prev + (long)par * PS_WBYTES, PS_WBYTES);
 #pragma unroll
       for (int t = 0; t < WC4; ++t) {
         const int idx = tid + t * PS_NT;
-        if (idx < K * 4) {
-          const int k = idx >> 2, q = idx & 3;
+        const int k = idx >> 3, q = idx & 7;
+        if (idx < K * (PS_CB / 4) && (k >= K / 2) == (h == 1)) {
           const unsigned lo = (unsigned)f2bf(wv[t].x) | ((unsigned)f2bf(wv[t].y) << 16);
           const unsigned hi = (unsigned)f2bf(wv[t].z) | ((unsigned)f2bf(wv[t].w) << 16);
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned,
-                                                                   make_uint2(lo, hi)),
-                                                wo, (int)(((long)k * PS_N + j0 + 4 * q) * 2), 0, CPOL_SYS);
+          ps_store8(wo, ((long)k * PS_N + j0 + 4 * q) * 2, lo, hi, 1);
         }
       }
     }
-    if (tid < 16) bsh[tid] = round_bf(bv);
+    if (tid < PS_CB) bsh[tid] = round_bf(bv);
     if constexpr (LAST) {
-      (void)hbv;
-      if (tid < 16 * PS_C) whs[tid / PS_C][tid % PS_C] = round_bf(hv);
+      if (tid < PS_CB * PS_C) whs[tid / PS_C][tid % PS_C] = round_bf(hv);
       // re-arm the other parity's logit accumulator (the previous step's, fully consumed)
       if (b == 0)
         for (int idx = tid; idx < n_mb * mb * PS_C; idx += PS_NT) a.logits[(long)(par ^ 1) * PS_MAXROWS * PS_C + idx] = 0.f;
     }
   }
-  // stage 0: the step's data once in bf16, row-major (the forward's A operand) and per
-  // microbatch transposed (the dW operand): workgroup b converts rows [4b, 4b + 4)
-  // (n_mb * mb == 128, host-checked), write-through, then every workgroup meets
+  // stage 0: the step's data transposed per microbatch (the dW operand): workgroup b
+  // converts rows [4b, 4b + 4) (n_mb * mb == 128, host-checked), write-through; waited
+  // for before the first backward tick
+  unsigned t_xt = 0;
   if constexpr (FIRST) {
-    const int i = rr / mb, rl = rr - i * mb, k4 = tid;
+    const int rr = 4 * b, i = rr / mb, rl = rr - i * mb;
     if (tid < K / 4) {
-      const float4* x = xpre;
-      const __amdgpu_buffer_rsrc_t xbr = ps_rsrc(a.XT + (long)PS_MAXNMB * K * PS_MAXMB, (long)PS_MAXROWS * K * 2);
-      const __amdgpu_buffer_rsrc_t xtr = ps_rsrc(a.XT + (long)i * K * mbp, (long)K * mbp * 2);
+      const __amdgpu_buffer_rsrc_t xtr = ps_rsrc(a.XT + (long)i * K * mb, (long)K * mb * 2);
+      const float* xs = &xpre[0].x;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const unsigned lo = (unsigned)f2bf(x[e].x) | ((unsigned)f2bf(x[e].y) << 16);
-        const unsigned hi = (unsigned)f2bf(x[e].z) | ((unsigned)f2bf(x[e].w) << 16);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned,
-                                                                 make_uint2(lo, hi)),
-                                              xbr, (int)(((long)(rr + e) * K + 4 * k4) * 2), 0, CPOL_SC1);
-      }
-      const float* xs = &x[0].x;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {   // feature 4 k4 + c of the 4 rows: 8 contiguous bytes of X^T
+      for (int c = 0; c < 4; ++c) {   // feature 4 tid + c of the 4 rows: 8 contiguous bytes of X^T
         const unsigned lo = (unsigned)f2bf(xs[0 * 4 + c]) | ((unsigned)f2bf(xs[1 * 4 + c]) << 16);
         const unsigned hi = (unsigned)f2bf(xs[2 * 4 + c]) | ((unsigned)f2bf(xs[3 * 4 + c]) << 16);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned,
-                                                                 make_uint2(lo, hi)),
-                                              xtr, (int)(((long)(4 * k4 + c) * mbp + rl) * 2), 0, CPOL_SC1);
+        ps_store8(xtr, ((long)(4 * tid + c) * mb + rl) * 2, lo, hi, 0);
       }
     }
-    ps_arrive_wait(a.ctr, ps_ctr_xt(0), a.timeout, a.err);
+    t_xt = ps_arrive(a.ctr, ps_ctr_xt(), PS_NB);
   } else {
     __syncthreads();
   }
   PS_STAMP(1);
 
   // ---- 1. forward ticks
-  const int MT = mb / 16;
   for (int i = 0; i < n_mb; ++i) {
-    const int r0 = i * mb;   // this microbatch's rows of the step
+    const int r0 = i * mb + h * mh;   // this workgroup's rows of the step
     // this thread's dropout bits (4 rows x 1 column) do not wait for the inputs
-    const int g4 = tid >> 4, c = tid & 15;
+    const int g4 = tid >> 5, c = tid & 31;
     u32x4 db = {0u, 0u, 0u, 0u};
-    if (a.keep < 1.f && 4 * g4 < mb) {
+    if (a.keep < 1.f && 4 * g4 < mh) {
       const unsigned long long off = (unsigned long long)((long)i << a.mb_shift) + ((unsigned long long)a.gid << 1);
-      db = dropout_bits(a.seed, off + dbase, dropout_group(0, 4 * g4, j0 + c, mb, PS_N));
+      db = dropout_bits(a.seed, off + dbase, dropout_group(0, h * mh + 4 * g4, j0 + c, mb, PS_N));
     }
-    if constexpr (!FIRST) ps_wait_wave(a.flag_mine, i, epoch, a.timeout, a.err);
+    if constexpr (!FIRST) ps_wait_wave(a.flag_mine, i, h, epoch, a.timeout, a.err);
     if (i == 1) PS_STAMP(19);
-    // Z partials: wave w takes k-steps [w KS / 4, (w+1) KS / 4) of every 16-row tile; all
-    // of its A fragments are loaded first (bf16 rows: stage 0's converted copy, else the
-    // inbox slot written by the previous stage)
-    const int ks0 = (w * KS) / PS_NW, ks1 = ((w + 1) * KS) / PS_NW;
-    f32x4 acc[MMT];
+    // Z partials: wave w takes its k-steps of both 16-column tiles of every 16-row tile;
+    // all of its A fragments are loaded first (stage 0: the fp32 data rows, converted in
+    // registers; else the inbox slot written by the previous stage)
+    f32x4 acc[MTH][2];
 #pragma unroll
-    for (int mt = 0; mt < MMT; ++mt) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < MTH; ++mt) acc[mt][0] = acc[mt][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
     {
-      const __amdgpu_buffer_rsrc_t xin =
-          FIRST ? ps_rsrc(a.XT + (long)PS_MAXNMB * K * PS_MAXMB + (long)r0 * K, (long)mb * K * 2)
-                : ps_rsrc(a.in_mine + (long)i * a.slot_bytes, (long)mb * PS_N * 2);
-      bf16x8 af[MMT][TPW];
+      bf16x8 af[MTH][TPW];
+      if constexpr (FIRST) {
 #pragma unroll
-      for (int t = 0; t < TPW; ++t)
+        for (int t = 0; t < TPW; ++t)
 #pragma unroll
-        for (int mt = 0; mt < MMT; ++mt) {
-          if (mt >= MT) break;
-          const int ks = min(ks0 + t, ks1 - 1), row = mt * 16 + (lane & 15);
-          // k past K (stage 0's 784 = 24.5 k-steps) reads the next row or, past the
-          // buffer, zero (bounds check): finite values times wc's zero padding
-          const long off = ((long)row * K + ks * 32 + 8 * (lane >> 4)) * 2;
-          af[mt][t] = FIRST ? __builtin_bit_cast(bf16x8, ps_load16<CPOL_SC1>(xin, off))
-                            : __builtin_bit_cast(bf16x8, ps_load16<CPOL_SYS>(xin, off));
-        }
+          for (int mt = 0; mt < MTH; ++mt) {
+            if (mt >= MT) continue;
+            const float* f = &xf[mt][t][0].x;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) af[mt][t][q] = (short)f2bf(f[q]);
+          }
+        if (i + 1 < n_mb) load_x(i + 1);
+      } else {
+        const __amdgpu_buffer_rsrc_t xin = ps_rsrc(a.in_mine + (long)i * a.slot_bytes, (long)mb * PS_N * 2);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t)
+#pragma unroll
+          for (int mt = 0; mt < MTH; ++mt) {
+            if (mt >= MT) continue;
+            const int ks = min(ks0 + t, ks1 - 1), row = h * mh + mt * 16 + (lane & 15);
+            af[mt][t] = __builtin_bit_cast(
+                bf16x8, ps_load16<CPOL_SYS>(xin, ((long)row * K + ks * 32 + 8 * (lane >> 4)) * 2));
+          }
+      }
 #pragma unroll
       for (int t = 0; t < TPW; ++t) {
         const int ks = ks0 + t;
         if (ks >= ks1) break;
-        const bf16x8 bf = *reinterpret_cast<const bf16x8*>(&wc[(lane & 15) * LDWC + ks * 32 + 8 * (lane >> 4)]);
 #pragma unroll
-        for (int mt = 0; mt < MMT; ++mt)
-          if (mt < MT) acc[mt] = mfma16x16x32(af[mt][t], bf, acc[mt]);
+        for (int ct = 0; ct < 2; ++ct) {
+          const bf16x8 bf =
+              *reinterpret_cast<const bf16x8*>(&wc[(ct * 16 + (lane & 15)) * LDWC + ks * 32 + 8 * (lane >> 4)]);
+#pragma unroll
+          for (int mt = 0; mt < MTH; ++mt)
+            if (mt < MT) acc[mt][ct] = mfma16x16x32(af[mt][t], bf, acc[mt][ct]);
+        }
       }
     }
 #pragma unroll
-    for (int mt = 0; mt < MMT; ++mt)
+    for (int mt = 0; mt < MTH; ++mt)
       if (mt < MT)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) part[w][mt * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[mt][e];
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) part[w][mt * 16 + (lane >> 4) * 4 + e][ct * 16 + (lane & 15)] = acc[mt][ct][e];
     __syncthreads();
     if (i == 1) PS_STAMP(20);
-    // bias + SiLU + dropout, one 4-row group per thread (the md kernels' streams)
-    {
-      if (4 * g4 < mb) {
+    // bias + SiLU + dropout, one 4-row group x 1 column per thread (the md kernels' streams)
+    if (4 * g4 < mh) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int rl = 4 * g4 + e;
-          float v = bsh[c];
+      for (int e = 0; e < 4; ++e) {
+        const int rl = 4 * g4 + e;
+        float v = bsh[c];
 #pragma unroll
-          for (int q = 0; q < PS_NW; ++q) v += part[q][rl][c];
-          const float z = round_bf(v);
-          const float ez = __expf(-z), sg = 1.0f / (1.0f + ez);
-          float hv = z * sg, gd = sg * (1.0f + z * (1.0f - sg));
-          if (a.keep < 1.f) {
-            const bool kp = keep_word(db, e, a.keep);
-            hv = kp ? hv * rkeep : 0.f;
-            gd = kp ? gd * rkeep : 0.f;
-          }
-          gl[r0 + rl][c] = gd;
-          const bf16_t hb = f2bf(hv);
-          ht[rl][c] = hb;
-          if constexpr (LAST) hown[r0 + rl][c] = hb;
+        for (int q = 0; q < PS_NW; ++q) v += part[q][rl][c];
+        const float z = round_bf(v);
+        const float ez = __expf(-z), sg = 1.0f / (1.0f + ez);
+        float hv = z * sg, gd = sg * (1.0f + z * (1.0f - sg));
+        if (a.keep < 1.f) {
+          const bool kp = keep_word(db, e, a.keep);
+          hv = kp ? hv * rkeep : 0.f;
+          gd = kp ? gd * rkeep : 0.f;
         }
+        gl[i * mh + rl][c] = gd;
+        const bf16_t hb = f2bf(hv);
+        ht[rl][c] = hb;
+        if constexpr (LAST) hown[i * mh + rl][c] = hb;
       }
     }
     __syncthreads();
     if (i == 1) PS_STAMP(21);
     if constexpr (LAST) {
-      // the head's partial logits of the owned 16 hidden units (+ b_h from workgroup 0);
-      // the arrival is waited for in the backward (the next microbatch goes on at once)
+      // the head's partial logits of the owned 32 hidden units for this row half (+ b_h
+      // from column block 0); the arrival is waited for in the backward
       float* lg = a.logits + (long)par * PS_MAXROWS * PS_C + (long)r0 * PS_C;
-      for (int idx = tid; idx < mb * PS_C; idx += PS_NT) {
-        const int r = idx / PS_C, c = idx % PS_C;
-        float s = b == 0 ? round_bf(a.phb[c]) : 0.f;
+      if (tid < mh * PS_C) {
+        const int r = tid / PS_C, cc = tid % PS_C;
+        float s = cb == 0 ? round_bf(a.phb[cc]) : 0.f;
 #pragma unroll
-        for (int n = 0; n < 16; ++n) s += bf2f(ht[r][n]) * whs[n][c];
-        atomicAdd(lg + idx, s);
+        for (int n = 0; n < PS_CB; ++n) s += bf2f(ht[r][n]) * whs[n][cc];
+        atomicAdd(lg + tid, s);
       }
-      const unsigned t_ = ps_arrive(a.ctr, ps_ctr_lg(i));
+      const unsigned t_ = ps_arrive(a.ctr, ps_ctr_lg(i, h), PS_NB / 2);
       if (tid == 0) tgt[i] = t_;
     } else {
-      // H[:, own] and H^T[own, :] into the next stage's inbox slot i, then this block's flag
+      // H[half, own] and H^T[own, half] into the next stage's inbox slot i, then this
+      // workgroup's flag
       const __amdgpu_buffer_rsrc_t o = ps_rsrc(a.in_next + (long)i * a.slot_bytes, a.slot_bytes);
-      if (tid < 2 * mb) {
-        const int r = tid >> 1, h = (tid & 1) * 8;
-        ps_store16<CPOL_SYS>(o, ((long)r * PS_N + j0 + h) * 2, *reinterpret_cast<const u32x4*>(&ht[r][h]));
+      if (tid < mh * 4) {
+        const int r = tid >> 2, q = tid & 3;
+        ps_store16<CPOL_SYS>(o, ((long)(h * mh + r) * PS_N + j0 + 8 * q) * 2, *reinterpret_cast<const u32x4*>(&ht[r][8 * q]));
       }
-      // H^T rows: all mbp columns, the padding [mb, mbp) as zeros (the consumer's dW k-steps
-      // read it; the slot's memory holds whatever was sent through it before)
       const long tbase = (long)mb * PS_N * 2;
-      for (int idx = tid; idx < 16 * (mbp / 8); idx += PS_NT) {
-        const int n = idx / (mbp / 8), r8 = (idx % (mbp / 8)) * 8;
-        unsigned q[4] = {0u, 0u, 0u, 0u};
-        if (r8 < mb)
+      if (tid < PS_CB * (mh / 8)) {
+        const int n = tid / (mh / 8), r8 = (tid % (mh / 8)) * 8;
+        unsigned q[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) q[e] = (unsigned)ht[r8 + 2 * e][n] | ((unsigned)ht[r8 + 2 * e + 1][n] << 16);
-        ps_store16<CPOL_SYS>(o, tbase + ((long)(j0 + n) * mbp + r8) * 2, (u32x4){q[0], q[1], q[2], q[3]});
+        for (int e = 0; e < 4; ++e) q[e] = (unsigned)ht[r8 + 2 * e][n] | ((unsigned)ht[r8 + 2 * e + 1][n] << 16);
+        ps_store16<CPOL_SYS>(o, tbase + ((long)(j0 + n) * mb + h * mh + r8) * 2, (u32x4){q[0], q[1], q[2], q[3]});
       }
       ps_raise(a.flag_next, i, epoch);
     }
@@ -460,7 +493,7 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
   if constexpr (!LAST) {
     ps_wait_slot(a.wflag_mine, par, epoch, a.timeout, a.err);
     const __amdgpu_buffer_rsrc_t wi = ps_rsrc(a.w_mine + (long)par * PS_WBYTES, PS_WBYTES);
-    constexpr int WN16 = 16 * PS_N / 8 / PS_NT;   // 16-byte chunks per thread
+    constexpr int WN16 = PS_CB * PS_N / 8 / PS_NT;   // 16-byte chunks per thread
     u32x4 q[WN16];
 #pragma unroll
     for (int t = 0; t < WN16; ++t) {
@@ -474,66 +507,68 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
     }
     __syncthreads();
   }
+  if constexpr (FIRST) ps_wait(a.ctr, ps_ctr_xt(), t_xt, a.timeout, a.err);   // X^T complete
 
   // ---- 2. backward ticks, last microbatch first
-  f32x4 dwa[UPW];
+  f32x4 dwa[UPW][2];
 #pragma unroll
-  for (int u = 0; u < UPW; ++u) dwa[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float dba = 0.f;                   // threads < 16: db[j0 + tid]
-  float dwh = 0.f, dbh = 0.f;        // last stage: threads < 160: dW_h[j0 + t/C][t%C]; b == 0, t < C: db_h
+  for (int u = 0; u < UPW; ++u) dwa[u][0] = dwa[u][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float dba = 0.f;                   // threads < 32: db[j0 + tid] over this row half
+  float dwh = 0.f, dbh = 0.f;        // last stage: threads < 320: dW_h[j0 + t/C][t%C]; cb == 0, t < C: db_h
   float l_loss = 0.f, l_corr = 0.f;
   for (int i = n_mb - 1; i >= 0; --i) {
-    const int r0 = i * mb;
-    // the dW operand (X^T rows of microbatch i: stage 0's transposed copy, else the inbox
-    // slot's H^T part) is already there: its loads fly while this tick waits for dH
-    const bf16_t* xtb = FIRST ? a.XT + (long)i * K * mbp
+    const int r0 = i * mb + h * mh;
+    // the dW operand (X^T columns of this row half of microbatch i: stage 0's transposed
+    // copy, else the inbox slot's H^T part) is already there: its loads fly while this
+    // tick waits for dZ_next.  32 columns per k-step: for mh = 16 the upper 16 belong to
+    // the other half (or past the slot: zero) and meet dzT's zero rows
+    const bf16_t* xtb = FIRST ? a.XT + (long)i * K * mb
                               : reinterpret_cast<const bf16_t*>(a.in_mine + (long)i * a.slot_bytes + (long)mb * PS_N * 2);
-    const __amdgpu_buffer_rsrc_t xr = ps_rsrc(xtb, (long)K * mbp * 2);
-    bf16x8 xb[UPW][PS_MAXMB / 32];
+    const __amdgpu_buffer_rsrc_t xr = ps_rsrc(xtb, (long)K * mb * 2);
+    bf16x8 xb[UPW];
 #pragma unroll
-    for (int u = 0; u < UPW; ++u)
-#pragma unroll
-      for (int rs = 0; rs < PS_MAXMB / 32; ++rs) {
-        const int t = min(w + PS_NW * u, NTK - 1);
-        const long off = ((long)(16 * t + (lane & 15)) * mbp + min(rs, mbp / 32 - 1) * 32 + 8 * (lane >> 4)) * 2;
-        xb[u][rs] = FIRST ? __builtin_bit_cast(bf16x8, ps_load16<CPOL_SC1>(xr, off))
-                          : __builtin_bit_cast(bf16x8, ps_load16<CPOL_SYS>(xr, off));
-      }
-    // dH[:, own] -> dZ = dH * G -> dzT (bf16, as the md kernels round dZ)
+    for (int u = 0; u < UPW; ++u) {
+      const int t = min(w + PS_NW * u, NTK - 1);
+      const long off = ((long)(16 * t + (lane & 15)) * mb + h * mh + 8 * (lane >> 4)) * 2;
+      xb[u] = FIRST ? __builtin_bit_cast(bf16x8, ps_load16<CPOL_SC1>(xr, off))
+                    : __builtin_bit_cast(bf16x8, ps_load16<CPOL_SYS>(xr, off));
+    }
+    // dH[half, own] -> dZ = dH * G -> dzT (bf16, as the md kernels round dZ)
     if constexpr (LAST) {
-      ps_wait(a.ctr, ps_ctr_lg(i), tgt[i], a.timeout, a.err);
-      // CE of every row of microbatch i from the complete logits
+      ps_wait(a.ctr, ps_ctr_lg(i, h), tgt[i], a.timeout, a.err);
+      // CE of this row half of microbatch i from the complete logits
       const __amdgpu_buffer_rsrc_t lr =
-          ps_rsrc(a.logits + (long)par * PS_MAXROWS * PS_C + (long)r0 * PS_C, (long)mb * PS_C * 4);
-      if (tid < mb) {
+          ps_rsrc(a.logits + (long)par * PS_MAXROWS * PS_C + (long)r0 * PS_C, (long)mh * PS_C * 4);
+      if (tid < mh) {
         float lrow[PS_C];
 #pragma unroll
-        for (int c = 0; c < PS_C; ++c)
-          lrow[c] = round_bf(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lr, (tid * PS_C + c) * 4, 0,
-                                                                                            CPOL_SC1)));
+        for (int cc = 0; cc < PS_C; ++cc)
+          lrow[cc] = round_bf(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lr, (tid * PS_C + cc) * 4, 0,
+                                                                                              CPOL_SC1)));
         const int lab = a.labels[r0 + tid];
         float mx = -INFINITY;
         int am = 0;
 #pragma unroll
-        for (int c = 0; c < PS_C; ++c)
-          if (lrow[c] > mx) { mx = lrow[c]; am = c; }
+        for (int cc = 0; cc < PS_C; ++cc)
+          if (lrow[cc] > mx) { mx = lrow[cc]; am = cc; }
         float s = 0.f;
 #pragma unroll
-        for (int c = 0; c < PS_C; ++c) s += __expf(lrow[c] - mx);
+        for (int cc = 0; cc < PS_C; ++cc) s += __expf(lrow[cc] - mx);
         const float lse = mx + __logf(s);
         float ll = 0.f;   // lrow[lab] without a dynamically indexed (scratch) array
 #pragma unroll
-        for (int c = 0; c < PS_C; ++c) ll = c == lab ? lrow[c] : ll;
+        for (int cc = 0; cc < PS_C; ++cc) ll = cc == lab ? lrow[cc] : ll;
         l_loss += lse - ll;
         l_corr += (am == lab) ? 1.f : 0.f;
         const float inv = 1.f / (float)mb;
 #pragma unroll
-        for (int c = 0; c < PS_C; ++c) dlog[tid][c] = round_bf((__expf(lrow[c] - lse) - (c == lab ? 1.f : 0.f)) * inv);
+        for (int cc = 0; cc < PS_C; ++cc)
+          dlog[tid][cc] = round_bf((__expf(lrow[cc] - lse) - (cc == lab ? 1.f : 0.f)) * inv);
       }
       __syncthreads();
       {
-        const int g4 = tid >> 4, c = tid & 15;
-        if (4 * g4 < mb) {
+        const int g4 = tid >> 5, c = tid & 31;
+        if (4 * g4 < mh) {
           unsigned pk[2] = {0u, 0u};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -541,56 +576,62 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
             float dh = 0.f;
 #pragma unroll
             for (int k = 0; k < PS_C; ++k) dh += dlog[rl][k] * whs[c][k];
-            pk[e >> 1] |= (unsigned)f2bf(dh * gl[r0 + rl][c]) << (16 * (e & 1));
+            pk[e >> 1] |= (unsigned)f2bf(dh * gl[i * mh + rl][c]) << (16 * (e & 1));
           }
           *reinterpret_cast<uint2*>(&dzT[c * LDT + 4 * g4]) = make_uint2(pk[0], pk[1]);
         }
       }
-      // head gradients of the owned rows of W_h (and b_h, workgroup 0)
-      if (tid < 16 * PS_C) {
-        const int n = tid / PS_C, c = tid % PS_C;
+      // head gradients of the owned rows of W_h over this row half (b_h: column block 0)
+      if (tid < PS_CB * PS_C) {
+        const int n = tid / PS_C, cc = tid % PS_C;
         float s = 0.f;
-        for (int r = 0; r < mb; ++r) s += bf2f(hown[r0 + r][n]) * dlog[r][c];
+        for (int r = 0; r < mh; ++r) s += bf2f(hown[i * mh + r][n]) * dlog[r][cc];
         dwh += s;
       }
-      if (b == 0 && tid < PS_C) {
+      if (cb == 0 && tid < PS_C) {
         float s = 0.f;
-        for (int r = 0; r < mb; ++r) s += dlog[r][tid];
+        for (int r = 0; r < mh; ++r) s += dlog[r][tid];
         dbh += s;
       }
     } else {
-      // dH[:, own] = dZ_next W_next[own, :]^T: the successor's dZ (inbox slot n_mb + i) is
-      // the A operand; wave w takes k-steps [KSW w, KSW (w + 1)) of the 512-deep product
-      ps_wait_wave(a.flag_mine, n_mb + i, epoch, a.timeout, a.err);
+      // dH[half, own] = dZ_next W_next[own, :]^T: the successor's dZ (inbox slot n_mb + i)
+      // is the A operand; wave w takes k-steps [2w, 2w + 2) of the 512-deep product
+      ps_wait_wave(a.flag_mine, n_mb + i, h, epoch, a.timeout, a.err);
       const __amdgpu_buffer_rsrc_t gin = ps_rsrc(a.in_mine + (long)(n_mb + i) * a.slot_bytes, (long)mb * PS_N * 2);
-      bf16x8 za[MMT][KSW];
+      bf16x8 za[MTH][KSW];
 #pragma unroll
       for (int t = 0; t < KSW; ++t)
 #pragma unroll
-        for (int mt = 0; mt < MMT; ++mt) {
-          if (mt >= MT) break;
+        for (int mt = 0; mt < MTH; ++mt) {
+          if (mt >= MT) continue;
           za[mt][t] = __builtin_bit_cast(
-              bf16x8, ps_load16<CPOL_SYS>(gin, ((long)(mt * 16 + (lane & 15)) * PS_N + (KSW * w + t) * 32 + 8 * (lane >> 4)) * 2));
+              bf16x8, ps_load16<CPOL_SYS>(gin, ((long)(h * mh + mt * 16 + (lane & 15)) * PS_N + (KSW * w + t) * 32 +
+                                                8 * (lane >> 4)) * 2));
         }
-      f32x4 acc[MMT];
+      f32x4 acc[MTH][2];
 #pragma unroll
-      for (int mt = 0; mt < MMT; ++mt) acc[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int mt = 0; mt < MTH; ++mt) acc[mt][0] = acc[mt][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int t = 0; t < KSW; ++t) {
-        const bf16x8 bf = *reinterpret_cast<const bf16x8*>(&wr[(lane & 15) * LDWR + (KSW * w + t) * 32 + 8 * (lane >> 4)]);
+      for (int t = 0; t < KSW; ++t)
 #pragma unroll
-        for (int mt = 0; mt < MMT; ++mt)
-          if (mt < MT) acc[mt] = mfma16x16x32(za[mt][t], bf, acc[mt]);
-      }
+        for (int ct = 0; ct < 2; ++ct) {
+          const bf16x8 bf = *reinterpret_cast<const bf16x8*>(
+              &wr[(ct * 16 + (lane & 15)) * LDWR + (KSW * w + t) * 32 + 8 * (lane >> 4)]);
 #pragma unroll
-      for (int mt = 0; mt < MMT; ++mt)
+          for (int mt = 0; mt < MTH; ++mt)
+            if (mt < MT) acc[mt][ct] = mfma16x16x32(za[mt][t], bf, acc[mt][ct]);
+        }
+#pragma unroll
+      for (int mt = 0; mt < MTH; ++mt)
         if (mt < MT)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) part[w][mt * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[mt][e];
+          for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) part[w][mt * 16 + (lane >> 4) * 4 + e][ct * 16 + (lane & 15)] = acc[mt][ct][e];
       __syncthreads();
       // dZ = bf16(bf16(dH) * G), the rounding points of the per-tick path (dX sent as bf16)
-      const int g4 = tid >> 4, c = tid & 15;
-      if (4 * g4 < mb) {
+      const int g4 = tid >> 5, c = tid & 31;
+      if (4 * g4 < mh) {
         unsigned pk[2] = {0u, 0u};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -598,46 +639,45 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
           float v = 0.f;
 #pragma unroll
           for (int q = 0; q < PS_NW; ++q) v += part[q][rl][c];
-          pk[e >> 1] |= (unsigned)f2bf(round_bf(v) * gl[r0 + rl][c]) << (16 * (e & 1));
+          pk[e >> 1] |= (unsigned)f2bf(round_bf(v) * gl[i * mh + rl][c]) << (16 * (e & 1));
         }
         *reinterpret_cast<uint2*>(&dzT[c * LDT + 4 * g4]) = make_uint2(pk[0], pk[1]);
       }
     }
     if (i == 1) PS_STAMP(22);
-    // zero padding rows [mb, mbp) of dzT for the 32-deep dW k-steps
-    for (int idx = tid; idx < 16 * (mbp - mb); idx += PS_NT) dzT[(idx / (mbp - mb)) * LDT + mb + idx % (mbp - mb)] = 0;
+    // zero rows [mh, 32) of dzT for the 32-deep dW k-step
+    for (int idx = tid; idx < PS_CB * (32 - mh); idx += PS_NT) dzT[(idx / (32 - mh)) * LDT + mh + idx % (32 - mh)] = 0;
     __syncthreads();
-    if (tid < 16) {
+    if (tid < PS_CB) {
       float s = 0.f;
-      for (int r = 0; r < mb; ++r) s += bf2f(dzT[tid * LDT + r]);
+      for (int r = 0; r < mh; ++r) s += bf2f(dzT[tid * LDT + r]);
       dba += s;
     }
-    // dZ[:, own] to the predecessor (stage 0's input needs no gradient), then dW
+    // dZ[half, own] to the predecessor (stage 0's input needs no gradient), then dW
     if constexpr (!FIRST) {
       const __amdgpu_buffer_rsrc_t o = ps_rsrc(a.in_prev + (long)(n_mb + i) * a.slot_bytes, (long)mb * PS_N * 2);
-      if (tid < 2 * mb) {
-        const int r = tid >> 1, h = (tid & 1) * 8;
+      if (tid < mh * 4) {
+        const int r = tid >> 2, q8 = (tid & 3) * 8;
         unsigned q[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          q[e] = (unsigned)dzT[(h + 2 * e) * LDT + r] | ((unsigned)dzT[(h + 2 * e + 1) * LDT + r] << 16);
-        ps_store16<CPOL_SYS>(o, ((long)r * PS_N + j0 + h) * 2, (u32x4){q[0], q[1], q[2], q[3]});
+          q[e] = (unsigned)dzT[(q8 + 2 * e) * LDT + r] | ((unsigned)dzT[(q8 + 2 * e + 1) * LDT + r] << 16);
+        ps_store16<CPOL_SYS>(o, ((long)(h * mh + r) * PS_N + j0 + q8) * 2, (u32x4){q[0], q[1], q[2], q[3]});
       }
       ps_raise(a.flag_prev, n_mb + i, epoch);
     }
-    // dW^T[own cols][k] += dZ^T X (A = dzT, B = the prefetched X^T rows); wave w takes
-    // k tiles w, w + 4, ...
+    // dW^T[own cols][k] += dZ^T X over this row half (A = dzT, B = the prefetched X^T
+    // columns); wave w takes k tiles w, w + 8, ..., both 16-column tiles
     {
-      bf16x8 dza[PS_MAXMB / 32];
+      bf16x8 dza[2];
 #pragma unroll
-      for (int rs = 0; rs < PS_MAXMB / 32; ++rs)
-        dza[rs] = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDT + min(rs, mbp / 32 - 1) * 32 + 8 * (lane >> 4)]);
+      for (int ct = 0; ct < 2; ++ct)
+        dza[ct] = *reinterpret_cast<const bf16x8*>(&dzT[(ct * 16 + (lane & 15)) * LDT + 8 * (lane >> 4)]);
 #pragma unroll
       for (int u = 0; u < UPW; ++u) {
         if (w + PS_NW * u >= NTK) break;
 #pragma unroll
-        for (int rs = 0; rs < PS_MAXMB / 32; ++rs)
-          if (rs < mbp / 32) dwa[u] = mfma16x16x32(dza[rs], xb[u][rs], dwa[u]);
+        for (int ct = 0; ct < 2; ++ct) dwa[u][ct] = mfma16x16x32(dza[ct], xb[u], dwa[u][ct]);
       }
     }
     if (i == 1) PS_STAMP(23);
@@ -645,7 +685,7 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
     if (i < 8) PS_STAMP(10 + i);
   }
 
-  // ---- 3. AdamW on the owned columns (+ the head's owned rows), shadows, metrics, step
+  // AdamW state of the owned column tile (see below), in flight during the swap
   const float t1 = (float)(step + 1);
   const float rbc1 = 1.f / (1.f - powf(a.b1, t1)), rbc2 = 1.f / (1.f - powf(a.b2, t1));
   auto adam = [&](float& p, float& m, float& v, float g) {
@@ -654,57 +694,99 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
     v = a.b2 * v + (1.f - a.b2) * g * g;
     p = p - a.lr * ((m * rbc1) * __builtin_amdgcn_rcpf(sqrtf(v * rbc2) + a.eps) + a.wd * p);
   };
-  {
-    // lane: dW^T rows (lane >> 4) * 4 + e (owned columns), column 16 t + (lane & 15) (input k)
-    float4 pv[UPW], mv[UPW], vv[UPW];
+  const int jc = j0 + 16 * h;   // the owned column tile
+  float4 pv[UPW], mv[UPW], vv[UPW];
 #pragma unroll
-    for (int u = 0; u < UPW; ++u) {
-      const int t = min(w + PS_NW * u, NTK - 1);
-      const long o = (long)(16 * t + (lane & 15)) * PS_N + j0 + 4 * (lane >> 4);
-      pv[u] = *reinterpret_cast<const float4*>(a.p + o);
-      mv[u] = *reinterpret_cast<const float4*>(a.m + o);
-      vv[u] = *reinterpret_cast<const float4*>(a.v + o);
-    }
+  for (int u = 0; u < UPW; ++u) {
+    const int t = min(w + PS_NW * u, NTK - 1);
+    const long o = (long)(16 * t + (lane & 15)) * PS_N + jc + 4 * (lane >> 4);
+    pv[u] = *reinterpret_cast<const float4*>(a.p + o);
+    mv[u] = *reinterpret_cast<const float4*>(a.m + o);
+    vv[u] = *reinterpret_cast<const float4*>(a.v + o);
+  }
+  // ---- 3. the row-half pair of this column block swaps partials: half h updates the
+  // columns of 16-column tile ct = h (every k), so it needs the partner's partial of that
+  // tile only; both halves hand over every slot the other one may read (write-through)
+  float* const mine = a.pair + (long)b * PS_PAIR;
+  const float* const other = a.pair + (long)(b ^ 1) * PS_PAIR;
+  typedef __attribute__((address_space(1))) float gf32;
+  const __amdgpu_buffer_rsrc_t pw = ps_rsrc(mine, (long)PS_PAIR * 4);
+  const __amdgpu_buffer_rsrc_t po = ps_rsrc(other, (long)PS_PAIR * 4);
+  const int hc = h ^ 1;   // the partner's column tile
 #pragma unroll
-    for (int u = 0; u < UPW; ++u) {
-      const int t = w + PS_NW * u;
-      if (t >= NTK) break;
-      const long o = (long)(16 * t + (lane & 15)) * PS_N + j0 + 4 * (lane >> 4);
-      float* pe = &pv[u].x; float* me = &mv[u].x; float* ve = &vv[u].x;
+  for (int u = 0; u < UPW; ++u) {
+    if (w + PS_NW * u >= NTK) break;
+    // (constant indices under a uniform branch: a runtime index puts dwa in scratch)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) adam(pe[e], me[e], ve[e], dwa[u][e]);
-      *reinterpret_cast<float4*>(a.p + o) = pv[u];
-      *reinterpret_cast<float4*>(a.m + o) = mv[u];
-      *reinterpret_cast<float4*>(a.v + o) = vv[u];
-      *reinterpret_cast<uint2*>(a.sW + o) = make_uint2((unsigned)f2bf(pv[u].x) | ((unsigned)f2bf(pv[u].y) << 16),
-                                                       (unsigned)f2bf(pv[u].z) | ((unsigned)f2bf(pv[u].w) << 16));
+    for (int ct = 0; ct < 2; ++ct)
+      if (ct == hc)
+        ps_store16<CPOL_SC1>(pw, (((long)w * PS_UPWMAX + u) * 256 + lane * 4) * 4, __builtin_bit_cast(u32x4, dwa[u][ct]));
+  }
+  if (tid < PS_CB) __hip_atomic_store((gf32*)(mine + PS_PAIR_DB + tid), dba, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if constexpr (LAST) {
+    if (tid < PS_CB * PS_C)
+      __hip_atomic_store((gf32*)(mine + PS_PAIR_WH + tid), dwh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cb == 0 && h == 1) {
+      if (tid < PS_C) __hip_atomic_store((gf32*)(mine + PS_PAIR_BH + tid), dbh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float ls = wave_sum(l_loss), cs = wave_sum(l_corr);
+      if (tid == 0) {
+        __hip_atomic_store((gf32*)(mine + PS_PAIR_MET), ls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gf32*)(mine + PS_PAIR_MET + 1), cs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
-  if (tid < 16) {
-    float p = a.pb[j0 + tid], m = a.mbv[j0 + tid], v = a.vb[j0 + tid];
-    adam(p, m, v, dba);
-    a.pb[j0 + tid] = p; a.mbv[j0 + tid] = m; a.vb[j0 + tid] = v; a.sb[j0 + tid] = f2bf(p);
+  const unsigned t_pair = ps_arrive(a.ctr, ps_ctr_pair(cb), 2);
+  ps_wait(a.ctr, ps_ctr_pair(cb), t_pair, a.timeout, a.err);
+  // the dW sums in row-half order (half 0's partial first)
+#pragma unroll
+  for (int u = 0; u < UPW; ++u) {
+    const int t = w + PS_NW * u;
+    if (t >= NTK) break;
+    const long o = (long)(16 * t + (lane & 15)) * PS_N + jc + 4 * (lane >> 4);
+    const f32x4 q = __builtin_bit_cast(f32x4, ps_load16<CPOL_SC1>(po, (((long)w * PS_UPWMAX + u) * 256 + lane * 4) * 4));
+    float* pe = &pv[u].x; float* me = &mv[u].x; float* ve = &vv[u].x;
+    if (h == 0) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) adam(pe[e], me[e], ve[e], dwa[u][0][e] + q[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) adam(pe[e], me[e], ve[e], q[e] + dwa[u][1][e]);
+    }
+    *reinterpret_cast<float4*>(a.p + o) = pv[u];
+    *reinterpret_cast<float4*>(a.m + o) = mv[u];
+    *reinterpret_cast<float4*>(a.v + o) = vv[u];
+    *reinterpret_cast<uint2*>(a.sW + o) = make_uint2((unsigned)f2bf(pv[u].x) | ((unsigned)f2bf(pv[u].y) << 16),
+                                                     (unsigned)f2bf(pv[u].z) | ((unsigned)f2bf(pv[u].w) << 16));
+  }
+  auto oth = [&](int i) { return __hip_atomic_load((const gf32*)(other + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  if (tid >= 16 * h && tid < 16 * h + 16) {   // b over the owned column tile
+    const int j = j0 + tid;
+    float p = a.pb[j], m = a.mbv[j], v = a.vb[j];
+    const float q = oth(PS_PAIR_DB + tid);
+    adam(p, m, v, h == 0 ? dba + q : q + dba);
+    a.pb[j] = p; a.mbv[j] = m; a.vb[j] = v; a.sb[j] = f2bf(p);
   }
   if constexpr (LAST) {
-    if (tid < 16 * PS_C) {
+    if (tid >= 16 * PS_C * h && tid < 16 * PS_C * (h + 1)) {   // W_h rows of the owned column tile
       const long o = (long)j0 * PS_C + tid;   // W_h[j0 + tid / C][tid % C]
       float p = a.ph[o], m = a.mh[o], v = a.vh[o];
-      adam(p, m, v, dwh);
+      const float q = oth(PS_PAIR_WH + tid);
+      adam(p, m, v, h == 0 ? dwh + q : q + dwh);
       a.ph[o] = p; a.mh[o] = m; a.vh[o] = v; a.sh[o] = f2bf(p);
     }
-    if (b == 0 && tid < PS_C) {
-      float p = a.phb[tid], m = a.mhb[tid], v = a.vhb[tid];
-      adam(p, m, v, dbh);
-      a.phb[tid] = p; a.mhb[tid] = m; a.vhb[tid] = v; a.shb[tid] = f2bf(p);
-    }
-    if (b == 0) {
+    if (cb == 0 && h == 0) {
+      if (tid < PS_C) {
+        float p = a.phb[tid], m = a.mhb[tid], v = a.vhb[tid];
+        adam(p, m, v, dbh + oth(PS_PAIR_BH + tid));
+        a.phb[tid] = p; a.mhb[tid] = m; a.vhb[tid] = v; a.shb[tid] = f2bf(p);
+      }
       // metrics: this step's loss sum / rows / correct / rows, folded into the running sums
       l_loss = wave_sum(l_loss);
       l_corr = wave_sum(l_corr);
       if (lane == 0) { red[0][w] = l_loss; red[1][w] = l_corr; }
       __syncthreads();
       if (tid < 4) {
-        float s = 0.f;
+        float s = tid == 0 ? oth(PS_PAIR_MET) : (tid == 2 ? oth(PS_PAIR_MET + 1) : 0.f);
         for (int q = 0; q < PS_NW; ++q) s += tid == 0 ? red[0][q] : (tid == 2 ? red[1][q] : 0.f);
         const float val = (tid & 1) ? (float)(n_mb * mb) : s;
         a.running[tid] += a.mslot[tid] + val;
@@ -714,7 +796,7 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
   }
   PS_STAMP(18);
   // the last workgroup to finish advances the optimizer step (read by every workgroup at
-  // its start, which all passed: each waited on a counter or flag that needed them all)
+  // its start, which all passed: the ticket counts every workgroup of the launch)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
@@ -730,6 +812,7 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
 using namespace jdt;
 
 JDT_API int jdt_pp_stage_args_size() { return (int)sizeof(PsArgs); }
+JDT_API int jdt_pp_stage_pair_floats() { return PS_PAIR; }
 
 // 1 if `nshare` ranks' stage launches (PS_NB workgroups each) can all be resident on
 // this GPU at once (every wait of the launch is on a co-resident workgroup or a
@@ -752,15 +835,15 @@ JDT_API int jdt_pp_stage_ok(int first, int last, int nshare) {
 // One step of this stage (first: stage 0, last: the last stage; not both).
 JDT_API int jdt_pp_stage(const PsArgs* args, int first, int last, void* stream) {
   const PsArgs& a = *args;
-  if ((first && last) || a.n_mb < 1 || a.n_mb > PS_MAXNMB || a.mb < 16 || a.mb > PS_MAXMB || (a.mb & 15) ||
-      a.n_mb * a.mb > PS_MAXROWS || a.K != (first ? 784 : PS_N) || !a.step || !a.ticket || !a.ctr || !a.err)
+  if ((first && last) || (a.mb != 32 && a.mb != 64) || a.n_mb * a.mb != PS_MAXROWS || a.K != (first ? 784 : PS_N) ||
+      !a.step || !a.ticket || !a.ctr || !a.err || !a.pair)
     return -2;
   if (!first && (!a.in_mine || !a.flag_mine || !a.in_prev || !a.flag_prev || !a.w_prev || !a.wflag_prev)) return -2;
   if (!last && (!a.w_mine || !a.wflag_mine)) return -2;
   if (!last && (!a.in_next || !a.flag_next)) return -2;
-  if (first && (!a.X || !a.XT || a.n_mb * a.mb != PS_MAXROWS)) return -2;
+  if (first && (!a.X || !a.XT)) return -2;
   if (last && (!a.labels || !a.logits || !a.ph || !a.phb || !a.mslot || !a.running)) return -2;
-  const long need = (long)a.mb * PS_N * 2 + (long)PS_N * ((a.mb + 31) & ~31) * 2;
+  const long need = (long)a.mb * PS_N * 2 + (long)PS_N * a.mb * 2;
   if (a.slot_bytes < need) return -2;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (first) hipLaunchKernelGGL((pp_stage_kernel<true, false>), dim3(PS_NB), dim3(PS_NT), 0, st, a);

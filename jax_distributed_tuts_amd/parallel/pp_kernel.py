@@ -49,12 +49,13 @@ class PsArgs(ctypes.Structure):
                 ("timeout", c_longlong),
                 ("XT", c_void_p), ("w_mine", c_void_p), ("wflag_mine", c_void_p), ("w_prev", c_void_p),
                 ("wflag_prev", c_void_p), ("logits", c_void_p), ("ctr", c_void_p),
-                ("step", c_void_p), ("ticket", c_void_p),
+                ("pair", c_void_p), ("step", c_void_p), ("ticket", c_void_p),
                 ("lr", c_float), ("b1", c_float), ("b2", c_float), ("eps", c_float), ("wd", c_float),
                 ("gscale", c_float), ("mslot", c_void_p), ("running", c_void_p), ("stamps", c_void_p)]
 
 
 _lib.declare("jdt_pp_stage_args_size", c_int, [])
+_lib.declare("jdt_pp_stage_pair_floats", c_int, [])
 _lib.declare("jdt_pp_stage_ok", c_int, [c_int, c_int, c_int])
 _lib.declare("jdt_pp_stage", c_int, [ctypes.POINTER(PsArgs), c_int, c_int, c_void_p])
 _lib.declare("jdt_p2p_max_slots", c_int, [])
@@ -92,7 +93,8 @@ def local_ok(trainer, mb: int) -> bool:
         return False
     if trainer.S < 2 or trainer.n_dp != 1 or not isinstance(trainer.state.tx, AdamW):
         return False
-    if not (16 <= mb <= 64 and mb % 16 == 0 and 1 <= n_mb <= 8 and n_mb * mb == 128):
+    # 32 or 64 rows: two row halves of whole 16-row MFMA tiles per column block
+    if not (mb in (32, 64) and n_mb * mb == 128):
         return False
     if 2 * n_mb > int(_lib.lib().jdt_p2p_max_slots()):
         return False
@@ -143,10 +145,10 @@ class PPStageKernel:
         P, st, model = trainer.state.params, trainer.state, trainer.model
         o = st.opt_state
         bf = dict(dtype=torch.bfloat16, device=dev)
-        # scratch (zeroed once: padding rows are read as zeros by the dW k-steps); stage 0:
-        # the per-microbatch X^T blocks [n_mb][784][mbp] in an 8 x 784 x 64 region, then the
-        # step's bf16 row copy [128][784] (ops/csrc/pp_stage.hip pre-pass)
-        self.XT = torch.zeros(8 * 784 * 64 + 128 * 784, **bf) if self.first else None
+        # scratch: stage 0's per-microbatch X^T blocks [n_mb][784][mb] (the dW operand,
+        # written by the kernel's pre-pass); the row-half pairs' partial-gradient swap slabs
+        self.XT = torch.zeros(128 * 784, **bf) if self.first else None
+        self.pair = torch.zeros(32 * int(L.jdt_pp_stage_pair_floats()), dtype=torch.float32, device=dev)
         self.logits = torch.zeros(2, 128, C_HEAD, dtype=torch.float32, device=dev) if self.last else None
         self.ctr = torch.zeros(64 * 32, dtype=torch.int32, device=dev)
         self.stamps = None
@@ -179,6 +181,7 @@ class PPStageKernel:
         a.w_mine, a.wflag_mine, _ = w_mine
         a.w_prev, a.wflag_prev, _ = w_prev
         a.ctr = self.ctr.data_ptr()
+        a.pair = self.pair.data_ptr()
         a.step, a.ticket = o["count"].data_ptr(), o["ticket"].data_ptr()
         tx = st.tx
         a.lr, a.b1, a.b2, a.eps, a.wd = tx.learning_rate, tx.b1, tx.b2, tx.eps, tx.weight_decay

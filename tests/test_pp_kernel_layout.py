@@ -28,7 +28,7 @@ def test_stage_kernel_takes_one_layer_per_stage(S, n_hidden, fits):
 def test_slot_holds_activation_and_its_transpose():
     # H [mb][512] + H^T [512][mbp] bf16, mbp = mb rounded up to the 32-deep dW k-steps
     assert PK.slot_bytes(64) == 64 * 512 * 2 + 512 * 64 * 2
-    assert PK.slot_bytes(16) == 16 * 512 * 2 + 512 * 32 * 2
+    assert PK.slot_bytes(32) == 32 * 512 * 2 + 512 * 32 * 2
 
 
 def test_args_mirror_is_packed_like_the_kernel_struct():

@@ -221,18 +221,19 @@ def test_pipeline_over_xgmi_matches_single_device(tmp_path, ws, dp, n_hidden):
     assert abs(float(m[0]) - float(rm[0])) <= 2e-3 * abs(float(rm[0])) + 1e-3
 
 
-@pytest.mark.parametrize("ws", [2, 4])
-def test_pipeline_stage_kernel_equals_per_tick_launches(tmp_path, ws):
+@pytest.mark.parametrize("ws,n_mb", [(2, 4), (4, 4), (2, 2), (4, 2)])
+def test_pipeline_stage_kernel_equals_per_tick_launches(tmp_path, ws, n_mb):
     """The in-kernel GPipe step (one persistent launch per stage: in-kernel inbox waits,
     hand-offs, register-held weight gradients, AdamW at the end) == the per-tick launches
     (receive / md layer kernel / dX GEMM / send per tick), dropout ON: the same Philox
-    streams, only fp32 summation order differs."""
+    streams, only fp32 summation order differs.  n_mb = 4 / 2: 32- / 64-row microbatches
+    (16 / 32 rows per row half: the dW k-step's zero rows / whole)."""
     import functools
 
     n_hidden = ws   # one layer per stage, the head on the last
     for k in ("1", "0"):
-        spawn(functools.partial(XW.pp_xgmi, dp=1, n_hidden=n_hidden, pp_kernel=k, dropout=0.1, tag=f"k{k}"), ws,
-              str(tmp_path), gpu=True)
+        spawn(functools.partial(XW.pp_xgmi, dp=1, n_hidden=n_hidden, pp_kernel=k, dropout=0.1, tag=f"k{k}",
+                                n_mb=n_mb), ws, str(tmp_path), gpu=True)
     a, b = _load(tmp_path, "ppx1k1", ws), _load(tmp_path, "ppx1k0", ws)
     assert all(o["pp_kernel"] for o in a) and not any(o["pp_kernel"] for o in b)
     for oa, ob in zip(a, b):

@@ -247,7 +247,7 @@ def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2, eps=1e-8, deep_fx="0"):
                           "one_launch": bool(tr.one_launch)})
 
 
-def pp_xgmi(outdir, dp, n_hidden=3, steps=4, pp_kernel="1", dropout=0.0, tag=""):
+def pp_xgmi(outdir, dp, n_hidden=3, steps=4, pp_kernel="1", dropout=0.0, tag="", n_mb=4):
     """GPipe with the xGMI inbox hand-off (+ the fused xGMI all-reduce on the data axis
     when dp > 1): one eager step, then multi-step graph replays.  ``pp_kernel`` =
     JDT_PP_KERNEL: "1" lets a pipeline of one layer per stage run each stage's step as
@@ -263,7 +263,7 @@ def pp_xgmi(outdir, dp, n_hidden=3, steps=4, pp_kernel="1", dropout=0.0, tag="")
     dev = D.device()
     cfg = dp_config()
     mesh = D.Mesh({"data": dp, "pipe": D.world_size() // dp})
-    tr = build_mlp_pipeline(cfg, mesh, dev, n_hidden_layers=n_hidden, dropout_rate=dropout, num_microbatches=4,
+    tr = build_mlp_pipeline(cfg, mesh, dev, n_hidden_layers=n_hidden, dropout_rate=dropout, num_microbatches=n_mb,
                             comm="xgmi")
     b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
     b = Batch(b.inputs.to(dev), b.labels.to(dev))

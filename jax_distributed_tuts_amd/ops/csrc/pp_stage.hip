@@ -29,10 +29,12 @@
 //                    of the complete logits through the head; dZ = dH * G goes straight
 //                    to the predecessor's inbox (not stage 0); then dW[:, own] += X^T dZ
 //                    over this row half (registers; X^T prefetched ahead of the wait), db
-//   end of step:     the two row halves of a column block swap the partial dW rows the
-//                    other one updates (write-through + a pair counter); AdamW on the
-//                    owned rows (gradient scale 1 / n_mb), bf16 shadows, metrics fold,
-//                    step advance (arrival ticket).
+//   end of step:     each row half stores its partial weight gradients; a second, wide
+//                    launch (pp_adam_kernel, ~all CUs) sums the two halves and applies
+//                    AdamW (gradient scale 1 / n_mb), bf16 shadows, metrics fold, step
+//                    advance.  32 workgroups updating a whole layer's p / m / v moved
+//                    ~150 KB per CU and took 10-15 us (stamps); spread over the chip it is
+//                    a few us plus one launch boundary.
 //
 // Every wait is on another workgroup that is resident (32 workgroups, all co-resident,
 // host-checked) or on a neighbour stage's launch, and bounded (s_memrealtime) into the
@@ -59,12 +61,13 @@ constexpr int PS_MAXNMB = 8;
 constexpr int PS_C = 10;
 constexpr int PS_FLAG_BLOCKS = 32; // comm/csrc/p2p.hip P2P_MAX_BLOCKS (flags per slot)
 constexpr int PS_UPWMAX = (784 / 16 + PS_NW - 1) / PS_NW;   // dW k tiles per wave (stage 0: 7)
-// pair-exchange slab per workgroup (floats): the partner's dW column tile [wave][tile][lane][4],
-// then db (32), dW_h (32 x C), db_h (C), loss / correct sums
-constexpr int PS_PAIR_DW = PS_NW * PS_UPWMAX * 256;   // one 16-column tile
-constexpr int PS_PAIR_DB = PS_PAIR_DW, PS_PAIR_WH = PS_PAIR_DB + PS_CB, PS_PAIR_BH = PS_PAIR_WH + PS_CB * PS_C,
-              PS_PAIR_MET = PS_PAIR_BH + PS_C;
-constexpr int PS_PAIR = PS_PAIR_MET + 2 + 30;
+// partial-gradient slab of one row half (floats, PsArgs::gstride apart): dW [K][512], db
+// [512], dW_h [512][C], db_h [C], loss / correct sums (column block 0)
+__host__ __device__ constexpr long ps_g_b(int K) { return (long)K * 512; }
+__host__ __device__ constexpr long ps_g_wh(int K) { return ps_g_b(K) + 512; }
+__host__ __device__ constexpr long ps_g_bh(int K) { return ps_g_wh(K) + 512 * 10; }
+__host__ __device__ constexpr long ps_g_met(int K) { return ps_g_bh(K) + 10; }
+__host__ __device__ constexpr long ps_g_size(int K) { return ps_g_met(K) + 6; }
 
 struct PsArgs {
   int n_mb, mb;                    // microbatches, rows per microbatch (32 or 64; n_mb * mb = 128)
@@ -98,16 +101,16 @@ struct PsArgs {
   char* w_prev; unsigned* wflag_prev;
   float* logits;                   // last stage: [2][n_mb][mb][C] fp32, by step parity
   unsigned* ctr;                   // arrival counters, one 128-byte line each
-  float* pair;                     // [PS_NB][PS_PAIR] partial-gradient swap of the row halves
+  float* gpart; long gstride;      // [2 row halves][gstride] partial gradients (ps_g_*)
   int* step; unsigned* ticket;     // device optimizer step, end-of-step ticket
   float lr, b1, b2, eps, wd, gscale;
   float* mslot; float* running;    // last stage: metric slots (loss, n, correct, n), running sums
-  unsigned long long* stamps;      // diagnostic: [32][24] s_memrealtime (null = off)
+  unsigned long long* stamps;      // diagnostic: [32][32] s_memrealtime (null = off)
 };
 
 #define PS_STAMP(k)                                                                           \
   do {                                                                                        \
-    if (a.stamps && threadIdx.x == 0) a.stamps[(long)blockIdx.x * 24 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    if (a.stamps && threadIdx.x == 0) a.stamps[(long)blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 constexpr int CPOL_SC1 = 16;       // agent-coherent (write-through / past L1) buffer access
@@ -213,10 +216,9 @@ __device__ __forceinline__ void ps_wait(unsigned* ctr, int c, unsigned target, l
 }
 
 // counter lines: stage 0's X^T pre-pass done; logits of microbatch i, row half h complete
-// (last stage); the row-half pair of column block cb swapped its partials
+// (last stage)
 __device__ __forceinline__ int ps_ctr_xt() { return 0; }
 __device__ __forceinline__ int ps_ctr_lg(int i, int h) { return 8 + 2 * i + h; }
-__device__ __forceinline__ int ps_ctr_pair(int cb) { return 24 + cb; }
 
 template <bool FIRST, bool LAST>
 __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
@@ -685,123 +687,105 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
     if (i < 8) PS_STAMP(10 + i);
   }
 
-  // AdamW state of the owned column tile (see below), in flight during the swap
-  const float t1 = (float)(step + 1);
-  const float rbc1 = 1.f / (1.f - powf(a.b1, t1)), rbc2 = 1.f / (1.f - powf(a.b2, t1));
-  auto adam = [&](float& p, float& m, float& v, float g) {
-    g *= a.gscale;
-    m = a.b1 * m + (1.f - a.b1) * g;
-    v = a.b2 * v + (1.f - a.b2) * g * g;
-    p = p - a.lr * ((m * rbc1) * __builtin_amdgcn_rcpf(sqrtf(v * rbc2) + a.eps) + a.wd * p);
-  };
-  const int jc = j0 + 16 * h;   // the owned column tile
-  float4 pv[UPW], mv[UPW], vv[UPW];
-#pragma unroll
-  for (int u = 0; u < UPW; ++u) {
-    const int t = min(w + PS_NW * u, NTK - 1);
-    const long o = (long)(16 * t + (lane & 15)) * PS_N + jc + 4 * (lane >> 4);
-    pv[u] = *reinterpret_cast<const float4*>(a.p + o);
-    mv[u] = *reinterpret_cast<const float4*>(a.m + o);
-    vv[u] = *reinterpret_cast<const float4*>(a.v + o);
-  }
-  // ---- 3. the row-half pair of this column block swaps partials: half h updates the
-  // columns of 16-column tile ct = h (every k), so it needs the partner's partial of that
-  // tile only; both halves hand over every slot the other one may read (write-through)
-  float* const mine = a.pair + (long)b * PS_PAIR;
-  const float* const other = a.pair + (long)(b ^ 1) * PS_PAIR;
-  typedef __attribute__((address_space(1))) float gf32;
-  const __amdgpu_buffer_rsrc_t pw = ps_rsrc(mine, (long)PS_PAIR * 4);
-  const __amdgpu_buffer_rsrc_t po = ps_rsrc(other, (long)PS_PAIR * 4);
-  const int hc = h ^ 1;   // the partner's column tile
-#pragma unroll
-  for (int u = 0; u < UPW; ++u) {
-    if (w + PS_NW * u >= NTK) break;
-    // (constant indices under a uniform branch: a runtime index puts dwa in scratch)
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-      if (ct == hc)
-        ps_store16<CPOL_SC1>(pw, (((long)w * PS_UPWMAX + u) * 256 + lane * 4) * 4, __builtin_bit_cast(u32x4, dwa[u][ct]));
-  }
-  if (tid < PS_CB) __hip_atomic_store((gf32*)(mine + PS_PAIR_DB + tid), dba, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if constexpr (LAST) {
-    if (tid < PS_CB * PS_C)
-      __hip_atomic_store((gf32*)(mine + PS_PAIR_WH + tid), dwh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (cb == 0 && h == 1) {
-      if (tid < PS_C) __hip_atomic_store((gf32*)(mine + PS_PAIR_BH + tid), dbh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const float ls = wave_sum(l_loss), cs = wave_sum(l_corr);
-      if (tid == 0) {
-        __hip_atomic_store((gf32*)(mine + PS_PAIR_MET), ls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((gf32*)(mine + PS_PAIR_MET + 1), cs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-  const unsigned t_pair = ps_arrive(a.ctr, ps_ctr_pair(cb), 2);
-  ps_wait(a.ctr, ps_ctr_pair(cb), t_pair, a.timeout, a.err);
-  // the dW sums in row-half order (half 0's partial first)
+  // ---- 3. this row half's partial gradients (plain stores: pp_adam_kernel reads them
+  // after the launch boundary); each 16-column tile row is 64 contiguous bytes, the two
+  // tiles of a row back to back
+  PS_STAMP(24);
+  float* const g = a.gpart + (long)h * a.gstride;
 #pragma unroll
   for (int u = 0; u < UPW; ++u) {
     const int t = w + PS_NW * u;
     if (t >= NTK) break;
-    const long o = (long)(16 * t + (lane & 15)) * PS_N + jc + 4 * (lane >> 4);
-    const f32x4 q = __builtin_bit_cast(f32x4, ps_load16<CPOL_SC1>(po, (((long)w * PS_UPWMAX + u) * 256 + lane * 4) * 4));
-    float* pe = &pv[u].x; float* me = &mv[u].x; float* ve = &vv[u].x;
-    if (h == 0) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) adam(pe[e], me[e], ve[e], dwa[u][0][e] + q[e]);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) adam(pe[e], me[e], ve[e], q[e] + dwa[u][1][e]);
-    }
-    *reinterpret_cast<float4*>(a.p + o) = pv[u];
-    *reinterpret_cast<float4*>(a.m + o) = mv[u];
-    *reinterpret_cast<float4*>(a.v + o) = vv[u];
-    *reinterpret_cast<uint2*>(a.sW + o) = make_uint2((unsigned)f2bf(pv[u].x) | ((unsigned)f2bf(pv[u].y) << 16),
-                                                     (unsigned)f2bf(pv[u].z) | ((unsigned)f2bf(pv[u].w) << 16));
+    for (int ct = 0; ct < 2; ++ct)
+      *reinterpret_cast<f32x4*>(g + (long)(16 * t + (lane & 15)) * PS_N + j0 + ct * 16 + 4 * (lane >> 4)) = dwa[u][ct];
   }
-  auto oth = [&](int i) { return __hip_atomic_load((const gf32*)(other + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-  if (tid >= 16 * h && tid < 16 * h + 16) {   // b over the owned column tile
-    const int j = j0 + tid;
-    float p = a.pb[j], m = a.mbv[j], v = a.vb[j];
-    const float q = oth(PS_PAIR_DB + tid);
-    adam(p, m, v, h == 0 ? dba + q : q + dba);
-    a.pb[j] = p; a.mbv[j] = m; a.vb[j] = v; a.sb[j] = f2bf(p);
-  }
+  if (tid < PS_CB) g[ps_g_b(K) + j0 + tid] = dba;
   if constexpr (LAST) {
-    if (tid >= 16 * PS_C * h && tid < 16 * PS_C * (h + 1)) {   // W_h rows of the owned column tile
-      const long o = (long)j0 * PS_C + tid;   // W_h[j0 + tid / C][tid % C]
-      float p = a.ph[o], m = a.mh[o], v = a.vh[o];
-      const float q = oth(PS_PAIR_WH + tid);
-      adam(p, m, v, h == 0 ? dwh + q : q + dwh);
-      a.ph[o] = p; a.mh[o] = m; a.vh[o] = v; a.sh[o] = f2bf(p);
-    }
-    if (cb == 0 && h == 0) {
-      if (tid < PS_C) {
-        float p = a.phb[tid], m = a.mhb[tid], v = a.vhb[tid];
-        adam(p, m, v, dbh + oth(PS_PAIR_BH + tid));
-        a.phb[tid] = p; a.mhb[tid] = m; a.vhb[tid] = v; a.shb[tid] = f2bf(p);
-      }
-      // metrics: this step's loss sum / rows / correct / rows, folded into the running sums
+    if (tid < PS_CB * PS_C) g[ps_g_wh(K) + (long)j0 * PS_C + tid] = dwh;
+    if (cb == 0) {
+      if (tid < PS_C) g[ps_g_bh(K) + tid] = dbh;
       l_loss = wave_sum(l_loss);
       l_corr = wave_sum(l_corr);
       if (lane == 0) { red[0][w] = l_loss; red[1][w] = l_corr; }
       __syncthreads();
-      if (tid < 4) {
-        float s = tid == 0 ? oth(PS_PAIR_MET) : (tid == 2 ? oth(PS_PAIR_MET + 1) : 0.f);
-        for (int q = 0; q < PS_NW; ++q) s += tid == 0 ? red[0][q] : (tid == 2 ? red[1][q] : 0.f);
-        const float val = (tid & 1) ? (float)(n_mb * mb) : s;
-        a.running[tid] += a.mslot[tid] + val;
-        a.mslot[tid] = 0.f;
+      if (tid < 2) {
+        float sum = 0.f;
+        for (int q = 0; q < PS_NW; ++q) sum += red[tid][q];
+        g[ps_g_met(K) + tid] = sum;
       }
     }
   }
   PS_STAMP(18);
-  // the last workgroup to finish advances the optimizer step (read by every workgroup at
-  // its start, which all passed: the ticket counts every workgroup of the launch)
+}
+
+// AdamW of one stage over the whole chip, after pp_stage_kernel: g = half 0 + half 1
+// (fixed order), scale 1 / n_mb; p / m / v, bf16 shadows; the last stage's head and
+// metric fold; the last workgroup advances the optimizer step.
+template <bool FIRST, bool LAST>
+__global__ void __launch_bounds__(256) pp_adam_kernel(PsArgs a) {
+  constexpr int K = FIRST ? 784 : PS_N;
+  const int step = a.step[0];
+  const float t1 = (float)(step + 1);
+  const float rbc1 = 1.f / (1.f - powf(a.b1, t1)), rbc2 = 1.f / (1.f - powf(a.b2, t1));
+  auto adam = [&](float& p, float& m, float& v, float gr) {
+    gr *= a.gscale;
+    m = a.b1 * m + (1.f - a.b1) * gr;
+    v = a.b2 * v + (1.f - a.b2) * gr * gr;
+    p = p - a.lr * ((m * rbc1) * __builtin_amdgcn_rcpf(sqrtf(v * rbc2) + a.eps) + a.wd * p);
+  };
+  const float* g0 = a.gpart;
+  const float* g1 = a.gpart + a.gstride;
+  const long nw4 = (long)K * PS_N / 4;
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < nw4; q += (long)gridDim.x * blockDim.x) {
+    const float4 x0 = reinterpret_cast<const float4*>(g0)[q], x1 = reinterpret_cast<const float4*>(g1)[q];
+    float4 p = reinterpret_cast<const float4*>(a.p)[q], m = reinterpret_cast<const float4*>(a.m)[q],
+           v = reinterpret_cast<const float4*>(a.v)[q];
+    adam(p.x, m.x, v.x, x0.x + x1.x);
+    adam(p.y, m.y, v.y, x0.y + x1.y);
+    adam(p.z, m.z, v.z, x0.z + x1.z);
+    adam(p.w, m.w, v.w, x0.w + x1.w);
+    reinterpret_cast<float4*>(a.p)[q] = p;
+    reinterpret_cast<float4*>(a.m)[q] = m;
+    reinterpret_cast<float4*>(a.v)[q] = v;
+    reinterpret_cast<uint2*>(a.sW)[q] = make_uint2((unsigned)f2bf(p.x) | ((unsigned)f2bf(p.y) << 16),
+                                                   (unsigned)f2bf(p.z) | ((unsigned)f2bf(p.w) << 16));
+  }
+  if (blockIdx.x == gridDim.x - 1) {
+    // the small leaves: b (+ W_h, b_h and the metric fold on the last stage)
+    for (int j = threadIdx.x; j < PS_N; j += blockDim.x) {
+      float p = a.pb[j], m = a.mbv[j], v = a.vb[j];
+      adam(p, m, v, g0[ps_g_b(K) + j] + g1[ps_g_b(K) + j]);
+      a.pb[j] = p; a.mbv[j] = m; a.vb[j] = v; a.sb[j] = f2bf(p);
+    }
+    if constexpr (LAST) {
+      for (int j = threadIdx.x; j < PS_N * PS_C; j += blockDim.x) {
+        float p = a.ph[j], m = a.mh[j], v = a.vh[j];
+        adam(p, m, v, g0[ps_g_wh(K) + j] + g1[ps_g_wh(K) + j]);
+        a.ph[j] = p; a.mh[j] = m; a.vh[j] = v; a.sh[j] = f2bf(p);
+      }
+      if (threadIdx.x < PS_C) {
+        const int j = threadIdx.x;
+        float p = a.phb[j], m = a.mhb[j], v = a.vhb[j];
+        adam(p, m, v, g0[ps_g_bh(K) + j] + g1[ps_g_bh(K) + j]);
+        a.phb[j] = p; a.mhb[j] = m; a.vhb[j] = v; a.shb[j] = f2bf(p);
+      }
+      if (threadIdx.x < 4) {
+        // this step's loss sum / rows / correct / rows, folded into the running sums
+        const int s = threadIdx.x;
+        const float val = (s & 1) ? (float)(a.n_mb * a.mb)
+                                  : g0[ps_g_met(K) + s / 2] + g1[ps_g_met(K) + s / 2];
+        a.running[s] += a.mslot[s] + val;
+        a.mslot[s] = 0.f;
+      }
+    }
+  }
+  // the last workgroup to finish advances the optimizer step (every workgroup read it)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) {
+  if (threadIdx.x == 0) {
     const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == PS_NB - 1) {
+    if (t == gridDim.x - 1) {
       a.step[0] = step + 1;
       __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -812,7 +796,8 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
 using namespace jdt;
 
 JDT_API int jdt_pp_stage_args_size() { return (int)sizeof(PsArgs); }
-JDT_API int jdt_pp_stage_pair_floats() { return PS_PAIR; }
+// floats per row half of PsArgs::gpart for a stage whose layer input is `k` wide
+JDT_API long jdt_pp_stage_gstride(int k) { return ps_g_size(k); }
 
 // 1 if `nshare` ranks' stage launches (PS_NB workgroups each) can all be resident on
 // this GPU at once (every wait of the launch is on a co-resident workgroup or a
@@ -836,7 +821,7 @@ JDT_API int jdt_pp_stage_ok(int first, int last, int nshare) {
 JDT_API int jdt_pp_stage(const PsArgs* args, int first, int last, void* stream) {
   const PsArgs& a = *args;
   if ((first && last) || (a.mb != 32 && a.mb != 64) || a.n_mb * a.mb != PS_MAXROWS || a.K != (first ? 784 : PS_N) ||
-      !a.step || !a.ticket || !a.ctr || !a.err || !a.pair)
+      !a.step || !a.ticket || !a.ctr || !a.err || !a.gpart || a.gstride < ps_g_size(a.K))
     return -2;
   if (!first && (!a.in_mine || !a.flag_mine || !a.in_prev || !a.flag_prev || !a.w_prev || !a.wflag_prev)) return -2;
   if (!last && (!a.w_mine || !a.wflag_mine)) return -2;
@@ -846,8 +831,17 @@ JDT_API int jdt_pp_stage(const PsArgs* args, int first, int last, void* stream) 
   const long need = (long)a.mb * PS_N * 2 + (long)PS_N * a.mb * 2;
   if (a.slot_bytes < need) return -2;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (first) hipLaunchKernelGGL((pp_stage_kernel<true, false>), dim3(PS_NB), dim3(PS_NT), 0, st, a);
-  else if (last) hipLaunchKernelGGL((pp_stage_kernel<false, true>), dim3(PS_NB), dim3(PS_NT), 0, st, a);
-  else hipLaunchKernelGGL((pp_stage_kernel<false, false>), dim3(PS_NB), dim3(PS_NT), 0, st, a);
+  // the AdamW launch: one float4 of W per thread, every CU
+  const int ga = (int)((((long)a.K * PS_N / 4) + 255) / 256);
+  if (first) {
+    hipLaunchKernelGGL((pp_stage_kernel<true, false>), dim3(PS_NB), dim3(PS_NT), 0, st, a);
+    hipLaunchKernelGGL((pp_adam_kernel<true, false>), dim3(ga), dim3(256), 0, st, a);
+  } else if (last) {
+    hipLaunchKernelGGL((pp_stage_kernel<false, true>), dim3(PS_NB), dim3(PS_NT), 0, st, a);
+    hipLaunchKernelGGL((pp_adam_kernel<false, true>), dim3(ga), dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((pp_stage_kernel<false, false>), dim3(PS_NB), dim3(PS_NT), 0, st, a);
+    hipLaunchKernelGGL((pp_adam_kernel<false, false>), dim3(ga), dim3(256), 0, st, a);
+  }
   return HIP_LAUNCH_CHECK();
 }

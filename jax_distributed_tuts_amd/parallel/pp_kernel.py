@@ -49,13 +49,13 @@ class PsArgs(ctypes.Structure):
                 ("timeout", c_longlong),
                 ("XT", c_void_p), ("w_mine", c_void_p), ("wflag_mine", c_void_p), ("w_prev", c_void_p),
                 ("wflag_prev", c_void_p), ("logits", c_void_p), ("ctr", c_void_p),
-                ("pair", c_void_p), ("step", c_void_p), ("ticket", c_void_p),
+                ("gpart", c_void_p), ("gstride", c_long), ("step", c_void_p), ("ticket", c_void_p),
                 ("lr", c_float), ("b1", c_float), ("b2", c_float), ("eps", c_float), ("wd", c_float),
                 ("gscale", c_float), ("mslot", c_void_p), ("running", c_void_p), ("stamps", c_void_p)]
 
 
 _lib.declare("jdt_pp_stage_args_size", c_int, [])
-_lib.declare("jdt_pp_stage_pair_floats", c_int, [])
+_lib.declare("jdt_pp_stage_gstride", c_long, [c_int])
 _lib.declare("jdt_pp_stage_ok", c_int, [c_int, c_int, c_int])
 _lib.declare("jdt_pp_stage", c_int, [ctypes.POINTER(PsArgs), c_int, c_int, c_void_p])
 _lib.declare("jdt_p2p_max_slots", c_int, [])
@@ -146,9 +146,11 @@ class PPStageKernel:
         o = st.opt_state
         bf = dict(dtype=torch.bfloat16, device=dev)
         # scratch: stage 0's per-microbatch X^T blocks [n_mb][784][mb] (the dW operand,
-        # written by the kernel's pre-pass); the row-half pairs' partial-gradient swap slabs
+        # written by the kernel's pre-pass); the two row halves' partial gradients, summed
+        # by the AdamW launch that follows the stage launch
         self.XT = torch.zeros(128 * 784, **bf) if self.first else None
-        self.pair = torch.zeros(32 * int(L.jdt_pp_stage_pair_floats()), dtype=torch.float32, device=dev)
+        self.gstride = int(L.jdt_pp_stage_gstride(int(model.dims[0])))
+        self.gpart = torch.zeros(2 * self.gstride, dtype=torch.float32, device=dev)
         self.logits = torch.zeros(2, 128, C_HEAD, dtype=torch.float32, device=dev) if self.last else None
         self.ctr = torch.zeros(64 * 32, dtype=torch.int32, device=dev)
         self.stamps = None
@@ -181,7 +183,7 @@ class PPStageKernel:
         a.w_mine, a.wflag_mine, _ = w_mine
         a.w_prev, a.wflag_prev, _ = w_prev
         a.ctr = self.ctr.data_ptr()
-        a.pair = self.pair.data_ptr()
+        a.gpart, a.gstride = self.gpart.data_ptr(), self.gstride
         a.step, a.ticket = o["count"].data_ptr(), o["ticket"].data_ptr()
         tx = st.tx
         a.lr, a.b1, a.b2, a.eps, a.wd = tx.learning_rate, tx.b1, tx.b2, tx.eps, tx.weight_decay
@@ -190,7 +192,7 @@ class PPStageKernel:
         self._key = None
 
     def set_stamps(self, stamps: Optional[torch.Tensor]):
-        """Diagnostic: [32 * 24] int64 s_memrealtime per workgroup (tools/stamp_pp.py)."""
+        """Diagnostic: [32 * 32] int64 s_memrealtime per workgroup (tools/stamp_pp.py)."""
         self.stamps = stamps
         self.args.stamps = stamps.data_ptr() if stamps is not None else None
 

@@ -52,7 +52,7 @@ def main():
             print("stage kernel not engaged (see parallel/pp_kernel.local_ok)")
         D.shutdown()
         return
-    stamps = torch.zeros(32 * 24, dtype=torch.int64, device=dev)
+    stamps = torch.zeros(32 * 32, dtype=torch.int64, device=dev)
     eng.set_stamps(stamps)
     tr.capture(b, steps_per_graph=1)
     # steps, then one stamped step whose timeline is printed
@@ -62,7 +62,7 @@ def main():
     tr.step(b)
     torch.cuda.synchronize()
     tr.finalize()
-    st = stamps.view(32, 24).double()
+    st = stamps.view(32, 32).double()
     n = args.microbatches
     med = lambda k: float(st[:, k].median())   # noqa: E731
     t = torch.tensor([med(0)], dtype=torch.float64)
@@ -72,10 +72,13 @@ def main():
     us = lambda k: (med(k) - t0) / 100.0   # noqa: E731   ticks -> us
     row = {"stage": D.rank(), "start": us(0), "staged": us(1),
            "fwd": [round(us(2 + i), 2) for i in range(min(n, 8))],
-           "bwd": [round(us(10 + i), 2) for i in reversed(range(min(n, 8)))], "adam": us(18),
+           "bwd": [round(us(10 + i), 2) for i in reversed(range(min(n, 8)))], "adam": us(18),   # stage launch end
            # microbatch 1's sub-tick marks: forward inputs there / MFMAs done / epilogue done,
            # backward dZ formed / dW MFMAs done
-           "sub": [round(us(k), 2) for k in range(19, 24)]}
+           "sub": [round(us(k), 2) for k in range(19, 24)],
+           # end of the stage launch: partial gradients being stored / stored (the AdamW
+           # launch follows)
+           "end": [round(us(k), 2) for k in (24, 18)]}
     rows = [None] * S
     torch.distributed.all_gather_object(rows, row)
     if D.rank() == 0:
@@ -85,6 +88,7 @@ def main():
             print(f"  stage {r['stage']}: start {r['start']:7.2f} staged {r['staged']:7.2f} fwd ticks end "
                   + " ".join(f"{x:7.2f}" for x in r["fwd"]) + "  bwd ticks end "
                   + " ".join(f"{x:7.2f}" for x in r["bwd"]) + f"  adam {r['adam']:7.2f}")
+            print("    end: partial gradients stored {:7.2f} -> {:7.2f}".format(*r["end"]))
             print(f"    mb1 fwd: inputs {r['sub'][0]:7.2f} mfma {r['sub'][1]:7.2f} epilogue {r['sub'][2]:7.2f} sent "
                   f"{r['fwd'][1] if len(r['fwd']) > 1 else 0:7.2f} | bwd: dZ {r['sub'][3]:7.2f} dW {r['sub'][4]:7.2f}")
         f_last = rows[-1]["fwd"][-1] - rows[0]["fwd"][0]

@@ -469,7 +469,7 @@ class FSDPTrainer:
     def _tile_exchange(self, batch: Batch):
         """(TileExchange, ranks sharing this GPU) for the N > 1 FSDP step without a
         separate collective launch, or (None, 1).  2-layer classifier: ONE run-ahead launch
-        per step (csrc/mlp_fused.hip FX); deep classifier (JDT_FSDP_DEEP_FX=1): one backward
+        per step (csrc/mlp_fused.hip FX); deep classifier (JDT_FSDP_DEEP_FX, default 1): one backward
         launch per hidden layer, each sending its tiles' partials to the row owners, which
         apply the sharded AdamW and hand the values back (csrc/mlp_deep.hip md_bwd FX).
         Both need AdamW, the reference's dim-0 shards of every kernel and bias (the head
@@ -512,7 +512,9 @@ class FSDPTrainer:
             tiles = (H // 16) * (K // kc)
         elif supported_deep(self.model, batch.size, dev):
             # layer 0 (784 rows, 112-row chunks) and the 512-row layers (64-row chunks)
-            local = (base and os.environ.get("JDT_FSDP_DEEP_FX", "0") == "1"
+            # default on: 88 vs 111 us per step against the step collective at 2 ranks
+            # sharing the GPU (profiles/r5_autotune_validation.txt, session 12)
+            local = (base and os.environ.get("JDT_FSDP_DEEP_FX", "1") == "1"
                      and os.environ.get("JDT_MLP2_AHEAD", "1") == "1" and 784 % W == 0 and 512 % (16 * W) == 0
                      and TX.fx_owner_span(W, 784, 112) <= 2 and TX.fx_owner_span(W, 512, 64) <= 2
                      and bool(_lib_md_ahead_ok(batch.size)) and TX.deep_fx_ok(batch.size, share))

@@ -33,8 +33,9 @@ import torch.distributed as dist
 from ..runtime import dist as D
 
 # validation bounds (relative L2 errors vs the reference form after k steps; measured on
-# the shared-GPU rehearsal at W = 2: profiles/r5_autotune_validation.txt)
-REL_TOL = 1e-2          # whole master delta / m / v (measured: 0 -- both forms sum in rank order)
+# the shared-GPU rehearsal at W = 2, profiles/r5_autotune_validation.txt session 12: 4e-8 to
+# 7e-4 whole-tensor, <= 3e-3 per block -- fp32 summation order only)
+REL_TOL = 1e-2          # whole master delta / m / v
 BLOCK_TOL = 0.05        # worst 16 x 16 block of the largest weight's master delta
 VALIDATE_STEPS = 3
 PROBE_EPS = 10.0

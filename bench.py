@@ -493,7 +493,9 @@ def main():
         desc["stage_streams"] = tr.stage_streams          # concurrent microbatch chains per stage
         desc["data_sync"] = tr.data_sync_mode             # data-axis sync: per W-pass group or one call
         if getattr(tr, "pp_kernel", None) is not None:
-            desc["step_launches"] = "2 per stage (in-kernel GPipe schedule + chip-wide AdamW, parallel/pp_kernel.py)"
+            desc["step_launches"] = ("2 (one-GPU chain: every layer a stage of one launch + chip-wide AdamW, "
+                                     "parallel/pp_kernel.py)" if tr.S == 1 else
+                                     "2 per stage (in-kernel GPipe schedule + chip-wide AdamW, parallel/pp_kernel.py)")
     if D.rank() == 0:
         out = {"metric": METRIC, "value": round(sps, 2), "unit": "steps/s", "n_gpus": ws, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 5), "higher_is_better": True,

@@ -110,7 +110,7 @@ struct PsArgs {
 
 #define PS_STAMP(k)                                                                           \
   do {                                                                                        \
-    if (a.stamps && threadIdx.x == 0) a.stamps[(long)blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    if (a.stamps && threadIdx.x == 0) a.stamps[(long)b * 32 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 constexpr int CPOL_SC1 = 16;       // agent-coherent (write-through / past L1) buffer access
@@ -174,10 +174,10 @@ __device__ __forceinline__ void ps_wait_wave(const unsigned* flags, int slot, in
 }
 
 // This workgroup's stores are drained, then ONE lane raises its flag of `slot` on the peer.
-__device__ __forceinline__ void ps_raise(unsigned* peer_flags, int slot, unsigned epoch) {
+__device__ __forceinline__ void ps_raise(unsigned* peer_flags, int slot, unsigned epoch, int b) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) tx_flag_store(peer_flags + (long)slot * PS_FLAG_BLOCKS + blockIdx.x, epoch);
+  if (threadIdx.x == 0) tx_flag_store(peer_flags + (long)slot * PS_FLAG_BLOCKS + b, epoch);
 }
 
 // `cnt` workgroups arrive at counter line `c` (stores drained, one agent-scope add each);
@@ -220,8 +220,35 @@ __device__ __forceinline__ void ps_wait(unsigned* ctr, int c, unsigned target, l
 __device__ __forceinline__ int ps_ctr_xt() { return 0; }
 __device__ __forceinline__ int ps_ctr_lg(int i, int h) { return 8 + 2 * i + h; }
 
+// LDS of one stage role, carved from one buffer (the one-GPU chain kernel runs every role
+// in one launch: static __shared__ arrays of three inlined roles would be summed, a
+// carved buffer is their maximum)
+__host__ __device__ constexpr int ps_al16(int x) { return (x + 15) & ~15; }
 template <bool FIRST, bool LAST>
-__global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
+struct PsLds {
+  static constexpr int K = FIRST ? 784 : PS_N;
+  static constexpr int LDWC = (K + 31) / 32 * 32 + 8, LDWR = PS_N + 8, LDT = 32 + 8;
+  static constexpr int wc = 0;
+  static constexpr int wr = ps_al16(wc + PS_CB * LDWC * 2);
+  static constexpr int part = ps_al16(wr + (LAST ? 8 : PS_CB * LDWR) * 2);
+  static constexpr int gl = ps_al16(part + PS_NW * PS_MAXH * (PS_CB + 1) * 4);
+  static constexpr int ht = ps_al16(gl + (PS_MAXROWS / 2) * PS_CB * 4);
+  static constexpr int hown = ps_al16(ht + PS_MAXH * (PS_CB + 8) * 2);
+  static constexpr int dzT = ps_al16(hown + (LAST ? PS_MAXROWS / 2 : 1) * PS_CB * 2);
+  static constexpr int dlog = ps_al16(dzT + PS_CB * LDT * 2);
+  static constexpr int whs = ps_al16(dlog + (LAST ? PS_MAXH : 1) * (PS_C + 1) * 4);
+  static constexpr int bsh = ps_al16(whs + PS_CB * PS_C * 4);
+  static constexpr int red = ps_al16(bsh + PS_CB * 4);
+  static constexpr int tgt = ps_al16(red + 2 * PS_NW * 4);
+  static constexpr int size = ps_al16(tgt + PS_MAXNMB * 4);
+};
+constexpr int ps_max3(int x, int y, int z) { return x > y ? (x > z ? x : z) : (y > z ? y : z); }
+constexpr int PS_LDS_MAX = ps_max3(PsLds<true, false>::size, PsLds<false, false>::size, PsLds<false, true>::size);
+
+// One stage's step, workgroup b of the stage's PS_NB (the per-rank launch: blockIdx.x;
+// the one-GPU chain: blockIdx.x % PS_NB), over the LDS buffer `lds`.
+template <bool FIRST, bool LAST>
+__device__ __forceinline__ void ps_body(const PsArgs& a, const int b, char* __restrict__ lds) {
   constexpr int K = FIRST ? 784 : PS_N;
   constexpr int KS = (K + 31) / 32;             // 32-deep k-steps of the forward
   constexpr int KP = KS * 32;
@@ -236,21 +263,23 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
   constexpr int LDT = 32 + 8;                   // dzT rows: 32 (the dW k-step; half rows + zeros)
   static_assert(K % 16 == 0 && UPW <= PS_UPWMAX, "dW tiles");
   static_assert(KSW * 32 == 64 && PS_NW * 64 == PS_N, "a wave's k range = two producers' column blocks");
-  __shared__ __attribute__((aligned(16))) bf16_t wc[PS_CB * LDWC];                 // W[:, own]^T
-  __shared__ __attribute__((aligned(16))) bf16_t wr[LAST ? 8 : PS_CB * LDWR];      // W_next[own rows, :]
-  __shared__ float part[PS_NW][PS_MAXH][PS_CB + 1];
-  __shared__ float gl[PS_MAXROWS / 2][PS_CB];                                     // G of own rows / cols
-  __shared__ __attribute__((aligned(16))) bf16_t ht[PS_MAXH][PS_CB + 8];          // this tick's H tile
-  __shared__ __attribute__((aligned(16))) bf16_t hown[LAST ? PS_MAXROWS / 2 : 1][PS_CB];  // head input
-  __shared__ __attribute__((aligned(16))) bf16_t dzT[PS_CB * LDT];                // dZ[half, own]^T
-  __shared__ float dlog[LAST ? PS_MAXH : 1][PS_C + 1];
-  __shared__ float whs[PS_CB][PS_C];
-  __shared__ float bsh[PS_CB];
-  __shared__ float red[2][PS_NW];
-  __shared__ unsigned tgt[PS_MAXNMB];                                             // counter targets (lane 0)
+  using LL = PsLds<FIRST, LAST>;
+  static_assert(LL::LDWC == LDWC && LL::LDT == LDT, "LDS layout");
+  bf16_t* const wc = reinterpret_cast<bf16_t*>(lds + LL::wc);                      // W[:, own]^T
+  bf16_t* const wr = reinterpret_cast<bf16_t*>(lds + LL::wr);                      // W_next[own rows, :]
+  float(*const part)[PS_MAXH][PS_CB + 1] = reinterpret_cast<float(*)[PS_MAXH][PS_CB + 1]>(lds + LL::part);
+  float(*const gl)[PS_CB] = reinterpret_cast<float(*)[PS_CB]>(lds + LL::gl);      // G of own rows / cols
+  bf16_t(*const ht)[PS_CB + 8] = reinterpret_cast<bf16_t(*)[PS_CB + 8]>(lds + LL::ht);   // this tick's H tile
+  bf16_t(*const hown)[PS_CB] = reinterpret_cast<bf16_t(*)[PS_CB]>(lds + LL::hown);       // head input
+  bf16_t* const dzT = reinterpret_cast<bf16_t*>(lds + LL::dzT);                    // dZ[half, own]^T
+  float(*const dlog)[PS_C + 1] = reinterpret_cast<float(*)[PS_C + 1]>(lds + LL::dlog);
+  float(*const whs)[PS_C] = reinterpret_cast<float(*)[PS_C]>(lds + LL::whs);
+  float* const bsh = reinterpret_cast<float*>(lds + LL::bsh);
+  float(*const red)[PS_NW] = reinterpret_cast<float(*)[PS_NW]>(lds + LL::red);
+  unsigned* const tgt = reinterpret_cast<unsigned*>(lds + LL::tgt);                // counter targets (lane 0)
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x, cb = b >> 1, h = b & 1, j0 = PS_CB * cb;
+  const int cb = b >> 1, h = b & 1, j0 = PS_CB * cb;
   const int mb = a.mb, n_mb = a.n_mb, mh = mb >> 1, MT = mh / 16;
   const int step = a.step[0], par = step & 1;
   const unsigned epoch = (unsigned)step + 1u;
@@ -484,13 +513,13 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
         for (int e = 0; e < 4; ++e) q[e] = (unsigned)ht[r8 + 2 * e][n] | ((unsigned)ht[r8 + 2 * e + 1][n] << 16);
         ps_store16<CPOL_SYS>(o, tbase + ((long)(j0 + n) * mb + h * mh + r8) * 2, (u32x4){q[0], q[1], q[2], q[3]});
       }
-      ps_raise(a.flag_next, i, epoch);
+      ps_raise(a.flag_next, i, epoch, b);
     }
     if (i < 8) PS_STAMP(2 + i);
   }
 
   // the weight image written at the start is drained by now (every send waited on it)
-  if constexpr (!FIRST) ps_raise(a.wflag_prev, par, epoch);
+  if constexpr (!FIRST) ps_raise(a.wflag_prev, par, epoch, b);
   // the successor's W rows of this workgroup's columns: wr[r][j] = W_next[j0 + r][j]
   if constexpr (!LAST) {
     ps_wait_slot(a.wflag_mine, par, epoch, a.timeout, a.err);
@@ -666,7 +695,7 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
           q[e] = (unsigned)dzT[(q8 + 2 * e) * LDT + r] | ((unsigned)dzT[(q8 + 2 * e + 1) * LDT + r] << 16);
         ps_store16<CPOL_SYS>(o, ((long)(h * mh + r) * PS_N + j0 + q8) * 2, (u32x4){q[0], q[1], q[2], q[3]});
       }
-      ps_raise(a.flag_prev, n_mb + i, epoch);
+      ps_raise(a.flag_prev, n_mb + i, epoch, b);
     }
     // dW^T[own cols][k] += dZ^T X over this row half (A = dzT, B = the prefetched X^T
     // columns); wave w takes k tiles w, w + 8, ..., both 16-column tiles
@@ -719,13 +748,36 @@ __global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
   PS_STAMP(18);
 }
 
+template <bool FIRST, bool LAST>
+__global__ void __launch_bounds__(PS_NT) pp_stage_kernel(PsArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[PsLds<FIRST, LAST>::size];
+  ps_body<FIRST, LAST>(a, blockIdx.x, lds);
+}
+
+// One GPU, every layer of an MLP pipeline a stage of ONE launch: stage s is workgroups
+// [s PS_NB, (s+1) PS_NB), hand-offs through local inboxes (the same protocol as across
+// ranks).  Every stage's workgroups must be resident at once (jdt_pp_chain_ok).
+constexpr int PS_MAXCHAIN = 8;
+struct PsChain {
+  PsArgs st[PS_MAXCHAIN];
+  int S;
+  int adam_blk[PS_MAXCHAIN + 1];   // the AdamW launch: stage s owns blocks [adam_blk[s], adam_blk[s+1])
+};
+
+__global__ void __launch_bounds__(PS_NT) pp_chain_kernel(PsChain c) {
+  __shared__ __attribute__((aligned(16))) char lds[PS_LDS_MAX];
+  const int s = __builtin_amdgcn_readfirstlane(blockIdx.x / PS_NB), b = blockIdx.x % PS_NB;
+  if (s == 0) ps_body<true, false>(c.st[0], b, lds);
+  else if (s == c.S - 1) ps_body<false, true>(c.st[s], b, lds);
+  else ps_body<false, false>(c.st[s], b, lds);
+}
+
 // AdamW of one stage over the whole chip, after pp_stage_kernel: g = half 0 + half 1
 // (fixed order), scale 1 / n_mb; p / m / v, bf16 shadows; the last stage's head and
 // metric fold; the last workgroup advances the optimizer step.
 template <bool FIRST, bool LAST>
-__global__ void __launch_bounds__(256) pp_adam_kernel(PsArgs a) {
+__device__ __forceinline__ void ps_adam_body(const PsArgs& a, const int blk, const int nblk, const int step) {
   constexpr int K = FIRST ? 784 : PS_N;
-  const int step = a.step[0];
   const float t1 = (float)(step + 1);
   const float rbc1 = 1.f / (1.f - powf(a.b1, t1)), rbc2 = 1.f / (1.f - powf(a.b2, t1));
   auto adam = [&](float& p, float& m, float& v, float gr) {
@@ -737,7 +789,7 @@ __global__ void __launch_bounds__(256) pp_adam_kernel(PsArgs a) {
   const float* g0 = a.gpart;
   const float* g1 = a.gpart + a.gstride;
   const long nw4 = (long)K * PS_N / 4;
-  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < nw4; q += (long)gridDim.x * blockDim.x) {
+  for (long q = (long)blk * blockDim.x + threadIdx.x; q < nw4; q += (long)nblk * blockDim.x) {
     const float4 x0 = reinterpret_cast<const float4*>(g0)[q], x1 = reinterpret_cast<const float4*>(g1)[q];
     float4 p = reinterpret_cast<const float4*>(a.p)[q], m = reinterpret_cast<const float4*>(a.m)[q],
            v = reinterpret_cast<const float4*>(a.v)[q];
@@ -751,7 +803,7 @@ __global__ void __launch_bounds__(256) pp_adam_kernel(PsArgs a) {
     reinterpret_cast<uint2*>(a.sW)[q] = make_uint2((unsigned)f2bf(p.x) | ((unsigned)f2bf(p.y) << 16),
                                                    (unsigned)f2bf(p.z) | ((unsigned)f2bf(p.w) << 16));
   }
-  if (blockIdx.x == gridDim.x - 1) {
+  if (blk == nblk - 1) {
     // the small leaves: b (+ W_h, b_h and the metric fold on the last stage)
     for (int j = threadIdx.x; j < PS_N; j += blockDim.x) {
       float p = a.pb[j], m = a.mbv[j], v = a.vb[j];
@@ -780,16 +832,41 @@ __global__ void __launch_bounds__(256) pp_adam_kernel(PsArgs a) {
       }
     }
   }
-  // the last workgroup to finish advances the optimizer step (every workgroup read it)
+}
+
+// the last workgroup of the launch to finish advances the optimizer step (every
+// workgroup read it at its start)
+__device__ __forceinline__ void ps_advance(int* step_p, unsigned* ticket, int step) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == gridDim.x - 1) {
-      a.step[0] = step + 1;
-      __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      step_p[0] = step + 1;
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+
+template <bool FIRST, bool LAST>
+__global__ void __launch_bounds__(256) pp_adam_kernel(PsArgs a) {
+  const int step = a.step[0];
+  ps_adam_body<FIRST, LAST>(a, blockIdx.x, gridDim.x, step);
+  ps_advance(a.step, a.ticket, step);
+}
+
+// the chain's AdamW: stage s's leaves over blocks [adam_blk[s], adam_blk[s+1]); one step
+// counter for the whole model
+__global__ void __launch_bounds__(256) pp_adam_chain_kernel(PsChain c) {
+  const int step = c.st[0].step[0];
+  int s = 0;
+  while (s + 1 < c.S && (int)blockIdx.x >= c.adam_blk[s + 1]) ++s;
+  s = __builtin_amdgcn_readfirstlane(s);
+  const int blk = blockIdx.x - c.adam_blk[s], nblk = c.adam_blk[s + 1] - c.adam_blk[s];
+  if (s == 0) ps_adam_body<true, false>(c.st[0], blk, nblk, step);
+  else if (s == c.S - 1) ps_adam_body<false, true>(c.st[s], blk, nblk, step);
+  else ps_adam_body<false, false>(c.st[s], blk, nblk, step);
+  ps_advance(c.st[0].step, c.st[0].ticket, step);
 }
 
 }  // namespace jdt
@@ -815,6 +892,45 @@ JDT_API int jdt_pp_stage_ok(int first, int last, int nshare) {
   if (e != hipSuccess || per < 1) return 0;
   const long slots = (long)cus * per;
   return (long)nshare * PS_NB <= (nshare > 1 ? slots / 2 : slots) ? 1 : 0;
+}
+
+// 1 if a chain of `S` stages (S x PS_NB workgroups of the one-GPU chain launch) can all be
+// resident on this GPU at once
+JDT_API int jdt_pp_chain_ok(int S) {
+  int dev = 0, cus = 0, per = 0;
+  if (S < 2 || S > PS_MAXCHAIN || hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pp_chain_kernel, PS_NT, 0) != hipSuccess || per < 1)
+    return 0;
+  return (long)S * PS_NB <= (long)cus * per ? 1 : 0;
+}
+JDT_API int jdt_pp_chain_max() { return PS_MAXCHAIN; }
+
+// One step of a one-GPU chain: args[0 .. S) are the stages' arguments (stage 0 takes the
+// data, stage S - 1 carries the head; one step counter / ticket for all)
+JDT_API int jdt_pp_chain(const PsArgs* args, int S, void* stream) {
+  if (!args || S < 2 || S > PS_MAXCHAIN) return -2;
+  PsChain c;
+  c.S = S;
+  c.adam_blk[0] = 0;
+  for (int s = 0; s < S; ++s) {
+    const PsArgs& a = args[s];
+    const bool first = s == 0, last = s == S - 1;
+    if ((a.mb != 32 && a.mb != 64) || a.n_mb * a.mb != PS_MAXROWS || a.K != (first ? 784 : PS_N) || !a.step ||
+        a.step != args[0].step || !a.ticket || !a.ctr || !a.err || !a.gpart || a.gstride < ps_g_size(a.K))
+      return -2;
+    if (!first && (!a.in_mine || !a.flag_mine || !a.in_prev || !a.flag_prev || !a.w_prev || !a.wflag_prev)) return -2;
+    if (!last && (!a.w_mine || !a.wflag_mine || !a.in_next || !a.flag_next)) return -2;
+    if (first && (!a.X || !a.XT)) return -2;
+    if (last && (!a.labels || !a.logits || !a.ph || !a.phb || !a.mslot || !a.running)) return -2;
+    if (a.slot_bytes < (long)a.mb * PS_N * 4) return -2;
+    c.st[s] = a;
+    c.adam_blk[s + 1] = c.adam_blk[s] + (int)((((long)a.K * PS_N / 4) + 255) / 256);
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(pp_chain_kernel, dim3(S * PS_NB), dim3(PS_NT), 0, st, c);
+  hipLaunchKernelGGL(pp_adam_chain_kernel, dim3(c.adam_blk[S]), dim3(256), 0, st, c);
+  return HIP_LAUNCH_CHECK();
 }
 
 // One step of this stage (first: stage 0, last: the last stage; not both).

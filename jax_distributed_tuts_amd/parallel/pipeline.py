@@ -320,10 +320,16 @@ class GPipeTrainer:
     # ------------------------------------------------------------------ step
     def _pp_kernel_engine(self, mb: int, seed: int):
         """The whole stage step as one persistent launch (parallel/pp_kernel.py), when
-        every stage of the pipe axis can run it (collective on first use)."""
+        every stage of the pipe axis can run it (collective on first use); with a pipe
+        axis of size 1, the one-GPU chain: every layer of the MLP a stage of one launch."""
         if not self._pp_kernel_tried:
             self._pp_kernel_tried = True
-            if self.S > 1 and self.dev.type == "cuda":
+            if self.S == 1 and self.dev.type == "cuda":
+                from . import pp_kernel as PK
+
+                if PK.chain_ok(self, mb):
+                    self.pp_kernel = PK.PPChainKernel(self, mb, seed)
+            elif self.S > 1 and self.dev.type == "cuda":
                 from ..comm.tile_exchange import agree
                 from . import pp_kernel as PK
 
@@ -339,8 +345,8 @@ class GPipeTrainer:
         mb = batch.size // n_mb
         rng = R.fold_rng_over_axis(st.rng, self.mesh, cfg.data_axis)
         seed = rng & 0xFFFFFFFF
-        if self.S > 1 and self._pp_kernel_engine(mb, seed) is not None:
-            # every tick, hand-off and the AdamW update in ONE launch (csrc/pp_stage.hip)
+        if self._pp_kernel_engine(mb, seed) is not None:
+            # every tick and hand-off in ONE launch, then the AdamW launch (csrc/pp_stage.hip)
             self.pp_kernel.step(batch)
             return
         self._setup_p2p(mb)

@@ -66,6 +66,25 @@ _lib.declare("jdt_p2p_peer", c_int, [c_void_p, c_int, ctypes.POINTER(c_void_p), 
 W_BYTES = H * H * 2   # a stage's bf16 weight image (ops/csrc/pp_stage.hip PS_WBYTES)
 
 
+def _fill_params(a: "PsArgs", P, o, layer: str, head: Optional[str]):
+    """Layer ``layer``'s (and the head's) fp32 master / Adam moments / bf16 shadow pointers."""
+    def trio(name):
+        off = P.offsets[name][0]
+        return P.p(name).data_ptr(), o["m"][off:].data_ptr(), o["v"][off:].data_ptr()
+
+    kn, bn = f"{layer}/kernel", f"{layer}/bias"
+    a.p, a.m, a.v = trio(kn)
+    a.sW = P.s(kn).data_ptr()
+    a.pb, a.mbv, a.vb = trio(bn)
+    a.sb = P.s(bn).data_ptr()
+    if head is not None:
+        hk, hb = f"{head}/kernel", f"{head}/bias"
+        a.ph, a.mh, a.vh = trio(hk)
+        a.sh = P.s(hk).data_ptr()
+        a.phb, a.mhb, a.vhb = trio(hb)
+        a.shb = P.s(hb).data_ptr()
+
+
 def slot_bytes(mb: int) -> int:
     """Inbox slot: H [mb][512] then H^T [512][mbp] (bf16)."""
     mbp = (mb + 31) // 32 * 32
@@ -161,17 +180,8 @@ class PPStageKernel:
         a.mb_shift = 16
         a.keep = 1.0 - float(model.dropout_rate)
         a.seed = int(seed) & 0xFFFFFFFF
-        kn, bn = f"{model.names[0]}/kernel", f"{model.names[0]}/bias"
-        a.p, a.sW = P.p(kn).data_ptr(), P.s(kn).data_ptr()
-        a.m, a.v = o["m"][P.offsets[kn][0]:].data_ptr(), o["v"][P.offsets[kn][0]:].data_ptr()
-        a.pb, a.sb = P.p(bn).data_ptr(), P.s(bn).data_ptr()
-        a.mbv, a.vb = o["m"][P.offsets[bn][0]:].data_ptr(), o["v"][P.offsets[bn][0]:].data_ptr()
+        _fill_params(a, P, o, model.names[0], model.names[1] if self.last else None)
         if self.last:
-            hk, hb = f"{model.names[1]}/kernel", f"{model.names[1]}/bias"
-            a.ph, a.sh = P.p(hk).data_ptr(), P.s(hk).data_ptr()
-            a.mh, a.vh = o["m"][P.offsets[hk][0]:].data_ptr(), o["v"][P.offsets[hk][0]:].data_ptr()
-            a.phb, a.shb = P.p(hb).data_ptr(), P.s(hb).data_ptr()
-            a.mhb, a.vhb = o["m"][P.offsets[hb][0]:].data_ptr(), o["v"][P.offsets[hb][0]:].data_ptr()
             a.logits = self.logits.data_ptr()
             a.mslot, a.running = P.metrics_slot.data_ptr(), trainer.metrics.data_ptr()
         a.in_mine, a.flag_mine, a.err = mine
@@ -219,3 +229,123 @@ class PPStageKernel:
             if getattr(self, box, None) is not None:
                 getattr(self, box).close()
                 setattr(self, box, None)
+
+
+_lib.declare("jdt_pp_chain_ok", c_int, [c_int])
+_lib.declare("jdt_pp_chain_max", c_int, [])
+_lib.declare("jdt_pp_chain", c_int, [c_void_p, c_int, c_void_p])
+
+
+def chain_ok(trainer, mb: int) -> bool:
+    """A pipe axis of size 1 holding the whole 784 -> 512 x L -> 10 MLP (2 <= L <= 8),
+    AdamW, no data axis, 32- or 64-row microbatches: the one-GPU chain launch applies.
+    Opt-in (JDT_PP_CHAIN=1): it measured SLOWER than the layer-by-layer full-chip
+    kernels it replaces -- 8 layers 131.7 vs 115.3 us, 4 layers 85.2 vs 61.0 us per step
+    (BENCH_NOTES round 5): 32 workgroups per layer leave each tick latency-bound, and the
+    AdamW of every layer waits for the whole chain, where the multi-rank stages overlap it."""
+    from ..models.mlp import MLP
+    from ..utils.train_state import AdamW
+
+    m = trainer.model
+    if os.environ.get("JDT_PP_CHAIN", "0") != "1" or trainer.dev.type != "cuda" or trainer.S != 1:
+        return False
+    if trainer.n_dp != 1 or not isinstance(trainer.state.tx, AdamW) or not isinstance(m, MLP) or m.act != "silu":
+        return False
+    dims = list(m.dims)
+    L = len(dims) - 2
+    if not (2 <= L <= int(_lib.lib().jdt_pp_chain_max()) and dims[0] == 784 and dims[-1] == C_HEAD
+            and all(d == H for d in dims[1:-1]) and not m.final_act):
+        return False
+    if not (mb in (32, 64) and trainer.cfg.num_microbatches * mb == 128):
+        return False
+    return bool(_lib.lib().jdt_pp_chain_ok(L))
+
+
+class PPChainKernel:
+    """One GPU, the whole GPipe step of an L-layer MLP as ONE launch: hidden layer i is
+    stage i of the chain (32 workgroups each, all resident), the stages hand off through
+    local inboxes with the protocol of the per-rank stage launch (csrc/pp_stage.hip
+    pp_chain_kernel), then one AdamW launch over the chip for every layer.  Replaces the
+    one-stage GPipe's layer-by-layer launches (2 per layer)."""
+
+    def __init__(self, trainer, mb: int, seed: int):
+        from ..comm.p2p import TICKS_PER_S
+        from ..runtime.dist import spin_timeout_s
+
+        if _lib.lib().jdt_pp_stage_args_size() != ctypes.sizeof(PsArgs):
+            raise RuntimeError("PsArgs layout mismatch")
+        L_ = _lib.lib()
+        tr = self.tr = trainer
+        model = trainer.model
+        self.mb, self.n_mb = mb, trainer.cfg.num_microbatches
+        dev = self.dev = trainer.dev
+        self.L = L = len(model.dims) - 2
+        P, st = trainer.state.params, trainer.state
+        o = st.opt_state
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        sb = slot_bytes(mb)
+        n_slots = 2 * self.n_mb
+        # per stage: activation / gradient inbox, its flags [64][32], the weight box (two
+        # 512 x 512 bf16 images by step parity) and its flags; one error word for all
+        self.inbox = [torch.zeros(n_slots * sb, dtype=torch.uint8, device=dev) for _ in range(L)]
+        self.flags = [torch.zeros(64 * 32, **i32) for _ in range(L)]
+        self.wbox = [torch.zeros(2 * W_BYTES, dtype=torch.uint8, device=dev) for _ in range(L)]
+        self.wflags = [torch.zeros(64 * 32, **i32) for _ in range(L)]
+        self.err = torch.zeros(1, **i32)
+        self.ctr = [torch.zeros(64 * 32, **i32) for _ in range(L)]
+        self.gpart = [torch.zeros(2 * int(L_.jdt_pp_stage_gstride(int(model.dims[i]))), dtype=torch.float32,
+                                  device=dev) for i in range(L)]
+        self.XT = torch.zeros(128 * 784, **bf)
+        self.logits = torch.zeros(2, 128, C_HEAD, dtype=torch.float32, device=dev)
+        timeout = int(spin_timeout_s(30.0) * TICKS_PER_S)
+        tx = st.tx
+        self.args = (PsArgs * L)()
+        for i in range(L):
+            a = self.args[i]
+            first, last = i == 0, i == L - 1
+            a.n_mb, a.mb, a.K = self.n_mb, mb, model.dims[i]
+            a.gid = int(model.layer_id_base) + i
+            a.mb_shift = 16
+            a.keep = 1.0 - float(model.dropout_rate)
+            a.seed = int(seed) & 0xFFFFFFFF
+            _fill_params(a, P, o, model.names[i], model.names[L] if last else None)
+            if last:
+                a.logits = self.logits.data_ptr()
+                a.mslot, a.running = P.metrics_slot.data_ptr(), trainer.metrics.data_ptr()
+            a.in_mine, a.flag_mine = self.inbox[i].data_ptr(), self.flags[i].data_ptr()
+            if not first:
+                a.in_prev, a.flag_prev = self.inbox[i - 1].data_ptr(), self.flags[i - 1].data_ptr()
+                a.w_prev, a.wflag_prev = self.wbox[i - 1].data_ptr(), self.wflags[i - 1].data_ptr()
+            if not last:
+                a.in_next, a.flag_next = self.inbox[i + 1].data_ptr(), self.flags[i + 1].data_ptr()
+                a.w_mine, a.wflag_mine = self.wbox[i].data_ptr(), self.wflags[i].data_ptr()
+            a.slot_bytes = sb
+            a.err = self.err.data_ptr()
+            a.timeout = timeout
+            a.XT = self.XT.data_ptr() if first else None
+            a.ctr = self.ctr[i].data_ptr()
+            a.gpart, a.gstride = self.gpart[i].data_ptr(), self.gpart[i].numel() // 2
+            a.step, a.ticket = o["count"].data_ptr(), o["ticket"].data_ptr()
+            a.lr, a.b1, a.b2, a.eps, a.wd = tx.learning_rate, tx.b1, tx.b2, tx.eps, tx.weight_decay
+            a.gscale = 1.0 / self.n_mb
+        self._key = None
+        self.ok = True
+
+    def step(self, batch):
+        key = (batch.inputs.data_ptr(), batch.labels.data_ptr())
+        if key != self._key:
+            assert batch.inputs.dtype == torch.float32 and batch.inputs.is_contiguous()
+            assert batch.inputs.shape == (self.n_mb * self.mb, 784)
+            assert batch.labels.dtype == torch.int32 and batch.labels.numel() == self.n_mb * self.mb
+            self.args[0].X = batch.inputs.data_ptr()
+            self.args[self.L - 1].labels = batch.labels.data_ptr()
+            self._key = key
+        _lib.check(_lib.lib().jdt_pp_chain(ctypes.cast(self.args, c_void_p), self.L, c_void_p(_lib.stream_ptr())),
+                   "pp_chain")
+
+    def error(self) -> int:
+        return int(self.err.item())
+
+    def close(self):
+        pass

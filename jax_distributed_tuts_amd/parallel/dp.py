@@ -528,9 +528,11 @@ class DataParallelTrainer:
     def close(self):
         """Release the IPC-mapped exchange buffers (tile exchange inboxes, xGMI context)
         and the captured graphs, so another trainer can be built in this process
-        (bench.py's probes).  Not collective; the trainer is unusable afterwards."""
-        if self.state.params.master.is_cuda:
-            torch.cuda.synchronize(self.state.params.master.device)
+        (bench.py's probes).  Collective (runtime.dist.quiesce: no rank frees buffers a
+        peer's kernel may still write); the trainer is unusable afterwards."""
+        from ..runtime.dist import quiesce
+
+        quiesce(self.state.params.master.device)
         for r in (getattr(self, "_txx", None), self.xg):
             if r is not None:
                 r.close()

@@ -823,9 +823,10 @@ class FSDPTrainer:
 
     def close(self):
         """Release the IPC-mapped exchange buffers (tile exchange inboxes, the shards' xGMI
-        context) and the captured graphs (see DataParallelTrainer.close)."""
-        if self.sp.local.master.is_cuda:
-            torch.cuda.synchronize(self.sp.local.master.device)
+        context) and the captured graphs (see DataParallelTrainer.close; collective)."""
+        from ..runtime.dist import quiesce
+
+        quiesce(self.sp.local.master.device)
         for r in (getattr(self, "_txx", None), self.sp.xg):
             if r is not None:
                 r.close()

@@ -865,9 +865,11 @@ class GPipeTrainer:
 
     def close(self):
         """Release the inboxes and the xGMI context and drop the captured graphs, so
-        another trainer can be built in this process (bench.py's autotune candidates)."""
-        if self.dev.type == "cuda":
-            torch.cuda.synchronize(self.dev)
+        another trainer can be built in this process (bench.py's autotune candidates).
+        Collective (runtime.dist.quiesce)."""
+        from ..runtime.dist import quiesce
+
+        quiesce(self.dev)
         for r in (self.p2p, self.xg, self.pp_kernel):
             if r is not None:
                 r.close()

@@ -160,6 +160,17 @@ def ranks_share_gpu() -> bool:
     return ranks_per_gpu() > 1
 
 
+def quiesce(dev):
+    """Before a trainer frees IPC buffers its peers write into (collective when a process
+    group is up): this rank's queue drained, then every rank's.  Freeing right after a
+    local synchronize let a slower peer's last collective kernel land in memory this
+    rank had already re-allocated -- a new context's start-up self-test then read a
+    corrupted all-reduce (round 5 closing run, 4 ranks sharing the GPU)."""
+    if torch.device(dev).type == "cuda":
+        torch.cuda.synchronize(dev)
+    barrier()
+
+
 def barrier():
     if is_initialized():
         if backend() == "nccl":

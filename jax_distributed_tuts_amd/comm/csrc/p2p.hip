@@ -29,6 +29,7 @@
 //
 // Waits time out (s_memrealtime, 100 MHz) into an error flag, never a hang.
 #include "common.h"
+#include "ipc_pool.h"
 
 #include <cstddef>
 #include <cstring>
@@ -132,10 +133,9 @@ JDT_API int jdt_p2p_create(int rank, int world, long slot_bytes, int n_slots, vo
   c->n_slots = n_slots;
   hipIpcMemHandle_t h[2];
   const size_t inbox_bytes = (size_t)c->slot_bytes * n_slots;
-  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->inbox), inbox_bytes, hipDeviceMallocUncached) != hipSuccess)
+  if (ipc_alloc(reinterpret_cast<void**>(&c->inbox), inbox_bytes) != hipSuccess)
     goto fail;
-  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->sig), sizeof(P2PSignal), hipDeviceMallocUncached) !=
-      hipSuccess)
+  if (ipc_alloc(reinterpret_cast<void**>(&c->sig), sizeof(P2PSignal)) != hipSuccess)
     goto fail;
   if (hipMemset(c->inbox, 0, inbox_bytes) != hipSuccess) goto fail;
   if (hipMemset(c->sig, 0, sizeof(P2PSignal)) != hipSuccess) goto fail;
@@ -147,8 +147,8 @@ JDT_API int jdt_p2p_create(int rank, int world, long slot_bytes, int n_slots, vo
   return 0;
 fail:
   (void)hipGetLastError();
-  if (c->inbox) (void)hipFree(c->inbox);
-  if (c->sig) (void)hipFree(c->sig);
+  ipc_release(c->inbox);
+  ipc_release(c->sig);
   delete c;
   return -1;
 }
@@ -242,8 +242,8 @@ JDT_API int jdt_p2p_destroy(void* ctx) {
       if (c->peers.sig[q]) (void)hipIpcCloseMemHandle(c->peers.sig[q]);
     }
   }
-  (void)hipFree(c->inbox);
-  (void)hipFree(c->sig);
+  ipc_release(c->inbox);
+  ipc_release(c->sig);
   delete c;
   return 0;
 }

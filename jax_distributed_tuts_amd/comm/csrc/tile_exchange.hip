@@ -10,6 +10,7 @@
 // right after a flag (the same discipline as comm/csrc/xgmi.hip and p2p.hip).  The
 // TxArgs the kernel reads (every rank's mapped pointers) lives in device memory.
 #include "common.h"
+#include "ipc_pool.h"
 
 #include <cstring>
 
@@ -45,14 +46,11 @@ JDT_API int jdt_tx_create(int rank, int world, int tiles, int pay, void** ctx_ou
   c->pay = pay;
   hipIpcMemHandle_t h[3];
   if ((long)tx_part_floats(c) * (long)sizeof(float) >= 0x7fffffffL) goto fail;   // 32-bit buffer offsets
-  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->part), tx_part_floats(c) * sizeof(float),
-                            hipDeviceMallocUncached) != hipSuccess)
+  if (ipc_alloc(reinterpret_cast<void**>(&c->part), tx_part_floats(c) * sizeof(float)) != hipSuccess)
     goto fail;
-  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->red), tx_red_floats(c) * sizeof(float),
-                            hipDeviceMallocUncached) != hipSuccess)
+  if (ipc_alloc(reinterpret_cast<void**>(&c->red), tx_red_floats(c) * sizeof(float)) != hipSuccess)
     goto fail;
-  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->flag), tx_flag_words(c) * sizeof(unsigned),
-                            hipDeviceMallocUncached) != hipSuccess)
+  if (ipc_alloc(reinterpret_cast<void**>(&c->flag), tx_flag_words(c) * sizeof(unsigned)) != hipSuccess)
     goto fail;
   if (hipMemset(c->part, 0, tx_part_floats(c) * sizeof(float)) != hipSuccess) goto fail;
   if (hipMemset(c->red, 0, tx_red_floats(c) * sizeof(float)) != hipSuccess) goto fail;
@@ -70,9 +68,9 @@ JDT_API int jdt_tx_create(int rank, int world, int tiles, int pay, void** ctx_ou
   return 0;
 fail:
   (void)hipGetLastError();
-  if (c->part) (void)hipFree(c->part);
-  if (c->red) (void)hipFree(c->red);
-  if (c->flag) (void)hipFree(c->flag);
+  ipc_release(c->part);
+  ipc_release(c->red);
+  ipc_release(c->flag);
   if (c->dev) (void)hipFree(c->dev);
   if (c->err) (void)hipFree(c->err);
   delete c;
@@ -138,9 +136,9 @@ JDT_API void jdt_tx_close(void* ctx) {
     if (c->host.red[q]) (void)hipIpcCloseMemHandle(c->host.red[q]);
     if (c->host.flag[q]) (void)hipIpcCloseMemHandle(c->host.flag[q]);
   }
-  if (c->part) (void)hipFree(c->part);
-  if (c->red) (void)hipFree(c->red);
-  if (c->flag) (void)hipFree(c->flag);
+  ipc_release(c->part);
+  ipc_release(c->red);
+  ipc_release(c->flag);
   if (c->dev) (void)hipFree(c->dev);
   if (c->err) (void)hipFree(c->err);
   delete c;

@@ -39,6 +39,7 @@
 // (stage own shard, barrier, phase 2) reuse the same machinery for FSDP
 // (SURVEY X05/X06).
 #include "common.h"
+#include "ipc_pool.h"
 
 #include <cstring>
 
@@ -989,14 +990,11 @@ JDT_API int jdt_xgmi_create(int rank, int world, long cap_floats, void** ctx_out
   }
   hipIpcMemHandle_t h[3];
   // uncached: peers read these over xGMI right after the flag (see xg_barrier)
-  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->data), 2 * c->cap * sizeof(float), hipDeviceMallocUncached) !=
-      hipSuccess)
+  if (ipc_alloc(reinterpret_cast<void**>(&c->data), 2 * c->cap * sizeof(float)) != hipSuccess)
     goto fail;
-  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->tmp), 2 * c->cap * sizeof(float), hipDeviceMallocUncached) !=
-      hipSuccess)
+  if (ipc_alloc(reinterpret_cast<void**>(&c->tmp), 2 * c->cap * sizeof(float)) != hipSuccess)
     goto fail;
-  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->sig), sizeof(XgSignal), hipDeviceMallocUncached) !=
-      hipSuccess)
+  if (ipc_alloc(reinterpret_cast<void**>(&c->sig), sizeof(XgSignal)) != hipSuccess)
     goto fail;
   if (hipMemset(c->sig, 0, sizeof(XgSignal)) != hipSuccess) goto fail;
   if (hipMemset(c->data, 0, 2 * c->cap * sizeof(float)) != hipSuccess) goto fail;
@@ -1011,9 +1009,9 @@ JDT_API int jdt_xgmi_create(int rank, int world, long cap_floats, void** ctx_out
   return 0;
 fail:
   (void)hipGetLastError();
-  if (c->data) (void)hipFree(c->data);
-  if (c->tmp) (void)hipFree(c->tmp);
-  if (c->sig) (void)hipFree(c->sig);
+  ipc_release(c->data);
+  ipc_release(c->tmp);
+  ipc_release(c->sig);
   delete c;
   return -1;
 }
@@ -1321,9 +1319,9 @@ JDT_API int jdt_xgmi_destroy(void* ctx) {
       if (c->peers.sig[q]) (void)hipIpcCloseMemHandle(c->peers.sig[q]);
     }
   }
-  (void)hipFree(c->data);
-  (void)hipFree(c->tmp);
-  (void)hipFree(c->sig);
+  ipc_release(c->data);
+  ipc_release(c->tmp);
+  ipc_release(c->sig);
   delete c;
   return 0;
 }

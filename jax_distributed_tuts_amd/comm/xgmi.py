@@ -113,6 +113,16 @@ _lib.declare("jdt_xgmi_allreduce_staged", c_int, [c_void_p, c_long, c_long, ctyp
                                                   c_void_p])
 _lib.declare("jdt_xgmi_destroy", c_int, [c_void_p])
 _lib.declare("jdt_xgmi_seg_slice", c_long, [c_long])
+_lib.declare("jdt_ipc_pool_stats", None, [c_void_p])
+
+
+def ipc_pool_stats() -> dict:
+    """Census of this process's pool of IPC-exported buffers (comm/csrc/ipc_pool.hip):
+    every comm context (xGMI, p2p inboxes, tile exchange) takes its exported buffers
+    from it and returns them there, never to the driver."""
+    out = (ctypes.c_long * 3)()
+    _lib.lib().jdt_ipc_pool_stats(out)
+    return {"buffers": int(out[0]), "bytes": int(out[1]), "in_use": int(out[2])}
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -200,8 +210,11 @@ def requested(mode: str, world: int, device: torch.device) -> bool:
 
 
 class XgmiComm:
+    _serial = 0   # contexts created in this process (self-test failure logs)
+
     def __init__(self, group, rank: int, world: int, cap_floats: int, device: torch.device,
                  timeout_s: float = 30.0, self_test: bool = True):
+        XgmiComm._serial += 1
         self.group, self.rank, self.world, self.device = group, rank, world, device
         self.timeout = c_longlong(int(timeout_s * TICKS_PER_S))
         self.ctx = c_void_p()
@@ -580,6 +593,20 @@ class XgmiComm:
                     " (barrier timeout)" if self.error() else "")
         return False
 
+    def _diff(self, x: torch.Tensor, want: torch.Tensor, base: torch.Tensor, it: int) -> str:
+        """Shape of an all-reduce mismatch for the log: how many elements, where, and
+        what the wrong sums decompose into (x - want in units of the per-rank terms: a
+        missing rank q shows as -(base * (q + 1) + it))."""
+        bad = (x != want).nonzero().flatten()
+        if bad.numel() == 0:
+            return ""
+        i = int(bad[0])
+        d = float(x[i] - want[i])
+        missing = [q for q in range(self.world) if d == -(float(base[i]) * (q + 1) + it)]
+        blk = int(_lib.lib().jdt_xgmi_capacity(self.ctx)) if self.ctx else 0
+        return (f"; {bad.numel()} wrong, first {i} last {int(bad[-1])}, got {float(x[i])} want {float(want[i])}"
+                f", missing-rank match {missing}, context #{XgmiComm._serial} in this process, cap {blk}")
+
     def _check(self, bad: bool, what: str) -> bool:
         """Collective verdict of one self-test check: every rank learns whether ANY
         rank failed before anyone issues the next collective (a rank that stopped
@@ -608,7 +635,8 @@ class XgmiComm:
             if ref is not None:
                 dist.all_reduce(ref, group=self.group)
             torch.cuda.synchronize(dev)
-            if not self._check(self.error() or not torch.equal(x, want), f"all-reduce mismatch (iter {it}, n {n})"):
+            if not self._check(self.error() or not torch.equal(x, want),
+                               f"all-reduce mismatch (iter {it}, n {n}{self._diff(x, want, base, it)})"):
                 return False
             if not self._check(ref is not None and not torch.equal(x, ref),
                                f"all-reduce differs from RCCL (iter {it}, n {n})"):

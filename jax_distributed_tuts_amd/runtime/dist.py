@@ -162,10 +162,11 @@ def ranks_share_gpu() -> bool:
 
 def quiesce(dev):
     """Before a trainer frees IPC buffers its peers write into (collective when a process
-    group is up): this rank's queue drained, then every rank's.  Freeing right after a
-    local synchronize let a slower peer's last collective kernel land in memory this
-    rank had already re-allocated -- a new context's start-up self-test then read a
-    corrupted all-reduce (round 5 closing run, 4 ranks sharing the GPU)."""
+    group is up): this rank's queue drained, then every rank's, so no peer kernel still
+    writes into a context being torn down.  The exported buffers themselves go back to a
+    per-process pool, never to the driver (comm/csrc/ipc_pool.hip): with them freed, a
+    new context's start-up self-test saw its own tensors change under it even after this
+    barrier (profiles/r5_ipc_pool.txt, 4 ranks sharing the GPU)."""
     if torch.device(dev).type == "cuda":
         torch.cuda.synchronize(dev)
     barrier()

@@ -573,6 +573,21 @@ __global__ void __launch_bounds__(NT) tx_selftest_kernel(const TxArgs* X, unsign
   if (nbad) atomicAdd(bad, nbad);
 }
 
+// Persistent run-ahead (PST, mlp2_pst_kernel): what a workgroup's lanes carry from step
+// to step in registers -- the AdamW state (p, m, v) of the lane's four W1 elements (aux
+// lanes: W2 / b1; block (0,0)'s first lanes: b2 too).  Only the last step of a launch
+// stores it; every step still hands its updated values to the other workgroups.
+struct PstRegs {
+  float op[4], om[4], ov[4];
+  float qp, qm, qv;
+};
+// position of a step inside a persistent launch: step `it` of `n`, the launch counter
+// (Mlp2Args::ztick[2]) when the launch started
+struct PstPos {
+  int it, n;
+  unsigned launch0;
+};
+
 // AHEAD (single GPU, fused AdamW, W1^T copy): after its AdamW epilogue every
 // workgroup (blk, chunk) also computes the partial Z1 = X[:, chunk] W1'[chunk, blk]
 // of the NEXT step from the W1' tile it just produced (phase 5); the last of a
@@ -582,9 +597,19 @@ __global__ void __launch_bounds__(NT) tx_selftest_kernel(const TxArgs* X, unsign
 // replaced by a per-column-block arrival ticket among workgroups that share an XCD
 // (xcd_contiguous_tile), and the one global dependency left -- complete logits for
 // the next CE -- is the launch boundary.
+//
+// PST (persistent run-ahead, mlp2_pst_kernel): the same step, n of them per launch with an
+// XCD-hierarchical grid barrier between steps in place of the launch boundary.  The AdamW
+// state stays in registers (PstRegs); every byte another workgroup wrote during the launch
+// is read with sc1 loads (never served by a stale L1; logits, re-armed write-through and
+// accumulated by atomics, come from the cross-XCD coherence point).
 template <int K_IN, int C, int KC, bool LOOP, bool AHEAD = false, bool TX = false, bool P3S = false,
-          bool FX = false, class AT>
-__device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by, const int step_in) {
+          bool FX = false, bool PST = false, class AT>
+__device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by, const int step_in,
+                                              PstRegs* R = nullptr, const PstPos pp = PstPos{0, 1, 0u}) {
+  static_assert(!PST || (AHEAD && !TX && !P3S && !FX && !LOOP), "persistent: the one-GPU run-ahead step");
+  constexpr bool SCX = LOOP || PST;        // in-launch hand-offs: sc1 loads / stores
+  const bool pst_last = !PST || pp.it == pp.n - 1;
   constexpr int MPM = 128;                 // max rows per device (fused path)
   constexpr int LDM = MPM + 8;             // padded row (bf16 elements)
   constexpr int NTILE = KC / 16;           // dW1 output tiles (one per wave)
@@ -622,7 +647,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   // loaded FIRST through a lane-varying address instead (a per-lane value, as in the
   // forward), so step t+1's dropout bits are computed while the other loads fly.
   int step_lane = 0;
-  if constexpr (AHEAD) {
+  if constexpr (AHEAD && !PST) {
     int lz;
     asm volatile("v_mov_b32 %0, 0" : "=v"(lz));
     step_lane = a.step[lz];
@@ -633,7 +658,21 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     if constexpr (AHEAD) {   // step % 3 buffers, all three loaded (no wait on the step)
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        lr0[c] = a.logits[lo + c]; lr1[c] = a.logits[(long)M * C + lo + c]; lr2[c] = a.logits[2l * M * C + lo + c];
+        if constexpr (!PST) {
+          lr0[c] = a.logits[lo + c]; lr1[c] = a.logits[(long)M * C + lo + c]; lr2[c] = a.logits[2l * M * C + lo + c];
+        }
+      }
+      if constexpr (PST) {   // accumulated by other XCDs' atomics this launch: 8-byte sc1 loads
+        static_assert(C % 2 == 0, "logits rows in 8-byte pairs");
+#pragma unroll
+        for (int q = 0; q < C / 2; ++q) {
+          const unsigned long long x0 = ld_u64<true>(a.logits + lo + 2 * q);
+          const unsigned long long x1 = ld_u64<true>(a.logits + (long)M * C + lo + 2 * q);
+          const unsigned long long x2 = ld_u64<true>(a.logits + 2l * M * C + lo + 2 * q);
+          lr0[2 * q] = __uint_as_float((unsigned)x0); lr0[2 * q + 1] = __uint_as_float((unsigned)(x0 >> 32));
+          lr1[2 * q] = __uint_as_float((unsigned)x1); lr1[2 * q + 1] = __uint_as_float((unsigned)(x1 >> 32));
+          lr2[2 * q] = __uint_as_float((unsigned)x2); lr2[2 * q + 1] = __uint_as_float((unsigned)(x2 >> 32));
+        }
       }
     } else if constexpr (LOOP) {   // step known: this step's parity only
       const float* lg = a.logits + (long)(step_in & 1) * M * C;
@@ -658,8 +697,8 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   const int lab = a.labels[min(tid, M - 1)];
   // G1 / H1: this thread's dropout group (rows 4rg..4rg+3, column j0+gn)
   const long go = ((long)min(rg, (M - 1) >> 2) * H + j0 + gn) * 4;
-  const u32x4 g1q = ld_b128<LOOP>(a.G1 + go);
-  const unsigned long long hq = ld_u64<LOOP>(a.H1 + go);
+  const u32x4 g1q = ld_b128<SCX>(a.G1 + go);
+  const unsigned long long hq = ld_u64<SCX>(a.H1 + go);
   bf16_t hv[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) hv[e] = (bf16_t)(hq >> (16 * e));
@@ -674,6 +713,12 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   bf16_t w2a, w2b;
   if constexpr (LOOP) {
     w2a = w2b = f2bf(ld_f<true>(a.W2snap + wo));   // the forward's snapshot of this step's W2
+  } else if constexpr (PST) {
+    // written by the column block's chunk-0 workgroup during the previous step: the
+    // aligned 4-byte word holding the element, sc1
+    const unsigned sh = 16u * (unsigned)(wo & 1);
+    w2a = (bf16_t)(__hip_atomic_load((const gu32_t*)(a.W2s0 + (wo & ~1l)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> sh);
+    w2b = (bf16_t)(__hip_atomic_load((const gu32_t*)(a.W2s1 + (wo & ~1l)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> sh);
   } else {
     w2a = a.W2s0[wo]; w2b = a.W2s1[wo];
   }
@@ -700,6 +745,10 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     fx_hpq = H / fx_W;
   }
   float op[4], om[4], ov[4];
+  if (PST && pp.it > 0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { op[e] = R->op[e]; om[e] = R->om[e]; ov[e] = R->ov[e]; }
+  } else {
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int n = (lane >> 4) * 4 + e;
@@ -711,9 +760,15 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     }
     op[e] = ld_global(sp + idx); om[e] = ld_global(sm + idx); ov[e] = ld_global(sv + idx);
   }
+  }
   const float run_pre = (a.running ? a.running : a.logits)[lane & 3];   // lead: metric accumulators
   const int lq = min(lane, C - 1);
-  const float qp = (fo ? a.pb2 : a.gb2)[lq], qm = (fo ? a.mb2 : a.gb2)[lq], qv = (fo ? a.vb2 : a.gb2)[lq];
+  float qp, qm, qv;
+  if (PST && pp.it > 0) {
+    qp = R->qp; qm = R->qm; qv = R->qv;
+  } else {
+    qp = (fo ? a.pb2 : a.gb2)[lq]; qm = (fo ? a.mb2 : a.gb2)[lq]; qv = (fo ? a.vb2 : a.gb2)[lq];
+  }
   // run-ahead: A fragments of X[16w.., chunk] (row-major bf16 copy) for the next
   // forward (in flight through CE, dZ1 and dW1); k past the chunk is multiplied by
   // w1n's zero padding, so the address is only clamped.  dbn: step t+1's dropout bits
@@ -733,7 +788,8 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   }
   __builtin_amdgcn_sched_barrier(0);
   int step = step_in;
-  if constexpr (AHEAD) step = step_lane;   // advanced by the step ticket once every workgroup has read it
+  if constexpr (PST) step = step_in;    // the launch's first step + it
+  else if constexpr (AHEAD) step = step_lane;   // advanced by the step ticket once every workgroup has read it
   else if constexpr (!LOOP) step = (a.step_copy ? a.step_copy : a.step)[0];
   const int par = step & 1;
   float lrow[C];
@@ -792,7 +848,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     // re-arm the accumulator of the step after next (run-ahead: step t+1's forward
     // accumulates into buffer (t+1) % 3 during this launch)
     float* nxt = a.logits + (long)(AHEAD ? (step + 2) % 3 : (par ^ 1)) * M * C;
-    for (int i = tid; i < M * C; i += NT) st_f<LOOP>(nxt + i, 0.f);
+    for (int i = tid; i < M * C; i += NT) st_f<SCX>(nxt + i, 0.f);
   }
   if constexpr (AHEAD) {   // K padding of the W1' tile image
     for (int idx = tid; idx < 16 * (128 - KC); idx += NT) w1n[(idx / (128 - KC)) * LDW1 + KC + idx % (128 - KC)] = 0;
@@ -845,7 +901,10 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         if (a.fuse_opt) {
           float tp, tm = om[e], tv = ov[e];
           const bf16_t pb = f2bf(adam_apply(op[e], om[e], ov[e], acc[e], ak, &tp, &tm, &tv));
-          if (AHEAD && (a.wt & 1)) {
+          if constexpr (PST) { R->op[e] = tp; R->om[e] = tm; R->ov[e] = tv; }
+          if (!pst_last) {
+            // persistent launch: the state stays in registers until its last step
+          } else if (AHEAD && (a.wt & 1)) {
             st_f<true>(a.pW1 + idx, tp);
             if (!ak.sgd) { st_f<true>(a.mW1 + idx, tm); st_f<true>(a.vW1 + idx, tv); }
           } else {
@@ -863,7 +922,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         }
       }
       // the lane's 4 rows are 4 consecutive K elements of W1^T: one 8-byte store
-      if (a.fuse_opt && a.W1T) {
+      if (a.fuse_opt && a.W1T && pst_last) {   // persistent: the next steps read w1n (LDS), not W1^T
         const unsigned long long w8 = (unsigned long long)wt[0] | ((unsigned long long)wt[1] << 32);
         if (LOOP || (AHEAD && (a.wt & 1))) st_u64<true>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
         else st_u64<false>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
@@ -899,8 +958,19 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
           const long o = isb ? (long)(j0 + n) : (long)(j0 + n) * C + ac;
           const float gr = isb ? ab1[e] : aw[e];
           if (a.fuse_opt) {
-            const float pn = adam_apply_h<LOOP>(op[e], om[e], ov[e], gr, ak, (isb ? a.pb1 : a.pW2) + o,
-                                                (isb ? a.mb1 : a.mW2) + o, (isb ? a.vb1 : a.vW2) + o);
+            float pn;
+            if constexpr (PST) {
+              float tp, tm = om[e], tv = ov[e];
+              pn = adam_apply(op[e], om[e], ov[e], gr, ak, &tp, &tm, &tv);
+              R->op[e] = tp; R->om[e] = tm; R->ov[e] = tv;
+              if (pst_last) {
+                (isb ? a.pb1 : a.pW2)[o] = tp;
+                if (!ak.sgd) { (isb ? a.mb1 : a.mW2)[o] = tm; (isb ? a.vb1 : a.vW2)[o] = tv; }
+              }
+            } else {
+              pn = adam_apply_h<LOOP>(op[e], om[e], ov[e], gr, ak, (isb ? a.pb1 : a.pW2) + o,
+                                      (isb ? a.mb1 : a.mW2) + o, (isb ? a.vb1 : a.vW2) + o);
+            }
             (isb ? a.sb1 : sW2n)[o] = f2bf(pn);
             if constexpr (AHEAD) a.hand[(isb ? 0 : H) + o] = pn;   // same XCD as the reader (L2)
           } else if (a.smap) {
@@ -913,7 +983,18 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
       }
       if (lead && lane < C) {
         if (a.fuse_opt) {
-          const float pn = adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
+          float pn;
+          if constexpr (PST) {
+            float tp, tm = qm, tv = qv;
+            pn = adam_apply(qp, qm, qv, ab2[0], ak, &tp, &tm, &tv);
+            R->qp = tp; R->qm = tm; R->qv = tv;
+            if (pst_last) {
+              a.pb2[lane] = tp;
+              if (!ak.sgd) { a.mb2[lane] = tm; a.vb2[lane] = tv; }
+            }
+          } else {
+            pn = adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
+          }
           a.sb2[lane] = f2bf(pn);
           if constexpr (AHEAD) a.hand[H + (long)H * C + lane] = pn;
         } else if (a.smap) {
@@ -1245,7 +1326,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     // must read the launch number
     unsigned tile_seen = 0u, launch_no = 0u;
     if (tid == 0) {
-      launch_no = a.ztick[2];
+      launch_no = PST ? pp.launch0 + (unsigned)pp.it : a.ztick[2];
       const int tpx = (H / 16) * NCH / 8, t = bx * NCH + by;   // tiles per XCD, this tile
       tile_seen = __hip_atomic_fetch_add((gu32_t*)(a.ztick + 32 * (1 + H / 16) + 32 * ((tpx + 31) / 32) * (t / tpx) + t % tpx),
                                          1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1364,7 +1445,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     }
     // every workgroup read the step counter before the column barrier; one workgroup
     // per column block reports, the last of them advances the step and launch counters
-    if (by == 0 && tid == 0 &&
+    if (!PST && by == 0 && tid == 0 &&
         __hip_atomic_fetch_add((gu32_t*)a.ztick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
             (unsigned)(H / 16 - 1)) {
       __hip_atomic_store((gu32_t*)a.ztick, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1437,6 +1518,91 @@ __global__ void __launch_bounds__(NT) mlp2_loop_kernel(Mlp2Args a, Mlp2Loop l) {
   if (b == 0 && threadIdx.x == 0 && it == l.n) {
     a.step[0] = step0 + l.n;
     l.base[0] = base + (2u * l.n - 1u) * (unsigned)G;
+  }
+}
+
+// XCD-hierarchical grid barrier of the persistent run-ahead launch (profiles/r5_barrier_lab.txt:
+// 1.92 us, the cost of the kernel boundary it replaces).  ws: 128-byte lines -- 0: the
+// generation count of completed barriers (advanced by the host-visible end of a launch),
+// 1: top counter, 2 + x: XCD x's arrival counter.  A workgroup adds to its XCD's counter
+// (HW_REG_XCC_ID); the XCD's last arriver (told by the value its add returned; the grid
+// is dealt round-robin over the 8 XCDs, probed: G / 8 workgroups each) adds 1 to the top
+// counter; every workgroup polls the top counter for 8 arrivals per generation.  Every
+// wave drains its stores and atomics first (vmcnt), so the step's hand-offs (sc1 / atomic
+// for cross-XCD bytes, L2 for the column block's own XCD) are complete before anyone passes.
+// A wall-clock timeout (20 ms) raises bit 8 of the error word and every workgroup leaves.
+__device__ __forceinline__ bool pst_grid_sync(unsigned* ws, unsigned gen, int* ok_lds, unsigned* errw) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    xcc &= 7u;
+    const unsigned per = (gridDim.x * gridDim.y) / 8u;
+    const unsigned old =
+        __hip_atomic_fetch_add((gu32_t*)(ws + 32 * (2 + xcc)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old % per == per - 1)
+      __hip_atomic_fetch_add((gu32_t*)(ws + 32), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = 8u * gen;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(ws + 32, (short)0, 4, 0x00020000);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    int ok = 1;
+    while ((int)((unsigned)__builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 16) - target) < 0) {
+      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > 2000000ll) {   // 20 ms
+        atomicOr(errw + 1, 8u);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");
+    }
+    ok_lds[0] = ok;
+  }
+  __syncthreads();
+  return ok_lds[0] != 0;
+}
+
+// n run-ahead steps in ONE launch (single GPU, fused AdamW, W1^T copy): step i's CE,
+// backward and AdamW plus step i+1's forward, then the grid barrier, n times.  The AdamW
+// state of every workgroup's tile stays in registers across the steps (PstRegs) -- the
+// per-step reload and write-back of p / m / v (9.6 MB of L2 / HBM traffic a step) and the
+// launch ramp are gone; the last step stores the state, W1^T and the shadows as the
+// one-step kernel does.  Same arithmetic as n launches of mlp2_bwd_kernel<..., AHEAD>:
+// bit-identical results (tests/test_mlp2_persistent_gpu.py).  Requires every workgroup
+// resident at once and round-robin XCD dispatch (the run-ahead's own conditions).
+template <int K_IN, int C, int KC>
+__global__ void __launch_bounds__(NT) mlp2_pst_kernel(Mlp2Args a, int n, unsigned* ws) {
+  __shared__ int ok_lds[1];
+  int bx = blockIdx.x, by = blockIdx.y;
+  xcd_column_tile(bx, by);
+  // read before the first barrier; block (0,0) rewrites them only after the last one
+  const int step0 = a.step[0];
+  const unsigned launch0 = a.ztick[2];
+  const unsigned gen0 = ws[0];
+  // the body's ~50 argument words re-read from the kernarg segment each step (laundered
+  // pointer) instead of being held live across the loop (mlp2_loop_kernel's lesson)
+  typedef const __attribute__((address_space(4))) Mlp2Args KArgs;
+  KArgs* const kbase = (KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
+  PstRegs R;
+  int it = 0;
+  // diagnostic stamps (Mlp2Args::stamps; the body stamps its phases each step, the last
+  // step's survive): slot 7 = start of step n-2, 12 / 13 = before / after the last barrier
+  unsigned long long* const stw =
+      a.stamps && threadIdx.x == 0 ? a.stamps + (long)(blockIdx.y * gridDim.x + blockIdx.x) * 16 : nullptr;
+  for (; it < n; ++it) {
+    KArgs* k = kbase;
+    asm volatile("" : "+s"(k));
+    if (stw && it == n - 2) stw[7] = __builtin_amdgcn_s_memrealtime();
+    mlp2_bwd_body<K_IN, C, KC, false, true, false, false, false, true>(*k, bx, by, step0 + it, &R,
+                                                                        PstPos{it, n, launch0});
+    if (stw && it == n - 2) stw[12] = __builtin_amdgcn_s_memrealtime();
+    if (it + 1 < n && !pst_grid_sync(ws, gen0 + (unsigned)it + 1u, ok_lds, a.ztick)) break;
+    if (stw && it == n - 2) stw[13] = __builtin_amdgcn_s_memrealtime();
+  }
+  if (bx == 0 && by == 0 && threadIdx.x == 0 && it == n) {
+    a.step[0] = step0 + n;
+    a.ztick[2] = launch0 + (unsigned)n;
+    ws[0] = gen0 + (unsigned)(n - 1);
   }
 }
 
@@ -1563,6 +1729,50 @@ static int mlp2_ahead_ok_k(int M, int H, int nshare, bool tx) {
                                 &per, mlp2_bwd_kernel<K_IN, 10, mlp2_kc<K_IN>(), true, true>, NT, 0);
   if (e != hipSuccess) return 0;
   return (long)nshare * (H / 16) * NCH <= (long)cus * per ? 1 : 0;
+}
+
+// 1 if the persistent run-ahead launch can run M rows x H hidden units of input width
+// K_IN here: the run-ahead's conditions, a grid of whole XCD shares (G % 8 == 0) and every
+// workgroup of the persistent kernel resident at once.
+template <int K_IN>
+static int mlp2_pst_ok_k(int M, int H) {
+  constexpr int KC = mlp2_kc<K_IN>(), NCH = K_IN / KC;
+  if (!mlp2_ahead_ok_k<K_IN>(M, H, 1, false)) return 0;
+  const int G = (H / 16) * NCH;
+  if (G % 8) return 0;
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, mlp2_pst_kernel<K_IN, 10, KC>, NT, 0) != hipSuccess)
+    return 0;
+  return G <= cus * per ? 1 : 0;
+}
+
+JDT_API int jdt_mlp2_pst_ok(int M, int H, int k_in) {
+  if (k_in == 784) return mlp2_pst_ok_k<784>(M, H);
+  if (k_in == 1024) return mlp2_pst_ok_k<1024>(M, H);
+  return 0;
+}
+
+// n >= 2 run-ahead steps in one persistent launch (mlp2_pst_kernel); ws: >= 10 x 32 words,
+// zeroed once, never reset (monotonic barrier counters).  -3 outside the run-ahead's
+// argument envelope (the caller then launches the one-step kernel n times).
+JDT_API int jdt_mlp2_pst(const Mlp2Args* args, int n, int k_in, unsigned* ws, void* stream) {
+  const Mlp2Args& a = *args;
+  if (n < 2 || !ws || a.tx || !a.fuse_opt || !a.W1T || !a.XR || !a.zslab || !a.ztick || !a.hand || !a.lg3 ||
+      a.det_logits || a.M <= 0 || a.M > 128 || a.H % 128)
+    return -3;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (k_in == 784) {
+    const dim3 g(a.H / 16, 784 / mlp2_kc<784>());
+    hipLaunchKernelGGL((mlp2_pst_kernel<784, 10, mlp2_kc<784>()>), g, dim3(NT), 0, st, a, n, ws);
+  } else if (k_in == 1024) {
+    const dim3 g(a.H / 16, 1024 / mlp2_kc<1024>());
+    hipLaunchKernelGGL((mlp2_pst_kernel<1024, 10, mlp2_kc<1024>()>), g, dim3(NT), 0, st, a, n, ws);
+  } else {
+    return -3;
+  }
+  return HIP_LAUNCH_CHECK();
 }
 
 // input widths the fused classifier kernels are instantiated for

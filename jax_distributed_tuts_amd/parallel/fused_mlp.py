@@ -87,6 +87,8 @@ _lib.declare("jdt_mlp2_loop", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_void_p,
                                       c_void_p, c_void_p])
 
 _lib.declare("jdt_mlp2_loop_ok", c_int, [c_int, c_int])
+_lib.declare("jdt_mlp2_pst_ok", c_int, [c_int, c_int, c_int])
+_lib.declare("jdt_mlp2_pst", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_void_p, c_void_p])
 
 LOOP_BARRIER_TIMEOUT_TICKS = 20_000_000   # 0.2 s of s_memrealtime (100 MHz) per grid barrier
 
@@ -242,6 +244,14 @@ class FusedMLP2:
             tpx = H // 16 * nch // 8
             self.ztick = torch.zeros(32 * (1 + H // 16) + 8 * 32 * ((tpx + 31) // 32), dtype=torch.int32, device=dev)
             self.hand = torch.zeros(H + H * 10 + 10, dtype=torch.float32, device=dev)
+        # persistent run-ahead (csrc/mlp_fused.hip mlp2_pst_kernel): n >= 2 steps of a
+        # run-ahead call in ONE launch, the AdamW state in registers across them and an
+        # XCD-hierarchical grid barrier between steps; one GPU only.  JDT_MLP2_PST=0: one
+        # launch per step (A/B).  pst_ws: the barrier's counter lines, zeroed once.
+        self.pst_ok = (self.ahead_ok and tx is None and os.environ.get("JDT_MLP2_PST", "1") == "1"
+                       and bool(_lib.lib().jdt_mlp2_pst_ok(rows, H, K)))
+        if self.pst_ok:
+            self.pst_ws = torch.zeros(32 * 10, dtype=torch.int32, device=dev)
 
     def set_grad_stage(self, base: int, stride: int):
         """Mode 0: write the gradient bucket into the xGMI staging buffer at ``base``
@@ -345,7 +355,8 @@ class FusedMLP2:
 
     def run_ahead(self, batch, n: int, prologue: bool = True):
         """n complete training steps as n run-ahead backward launches, launch i = step
-        i's CE, backward and AdamW plus step i+1's forward; ``prologue`` first runs the
+        i's CE, backward and AdamW plus step i+1's forward (n >= 2 with ``pst_ok``: ONE
+        persistent launch of the n steps, bit-identical); ``prologue`` first runs the
         first step's forward (``mlp2_fwd``), needed unless the previous launch on this
         engine was a run-ahead backward (``ahead_primed``: step t's G1, H1 and logits
         (t % 3) are then already there).  Same maths as n two-launch steps except the
@@ -371,8 +382,12 @@ class FusedMLP2:
             _lib.check(L.jdt_mlp2(ctypes.byref(self._ahead_args), 0, self.K, 10, s), "mlp2_fwd")
         elif not torch.cuda.is_current_stream_capturing():
             assert self.ahead_primed, "run_ahead(prologue=False) needs a run-ahead launch just before"
-        for _ in range(n):
-            _lib.check(L.jdt_mlp2(ctypes.byref(self._ahead_args), 2, self.K, 10, s), "mlp2_bwd_ahead")
+        if self.pst_ok and n >= 2:
+            _lib.check(L.jdt_mlp2_pst(ctypes.byref(self._ahead_args), int(n), self.K, self.pst_ws.data_ptr(), s),
+                       "mlp2_pst")
+        else:
+            for _ in range(n):
+                _lib.check(L.jdt_mlp2(ctypes.byref(self._ahead_args), 2, self.K, 10, s), "mlp2_bwd_ahead")
         if not torch.cuda.is_current_stream_capturing():
             self.ahead_primed = True
 
@@ -416,7 +431,7 @@ class FusedMLP2:
         if self.ahead_ok and int(self.ztick[1].item()) != 0:
             raise RuntimeError("mlp2_bwd run-ahead: tile map, column barrier or tile exchange failed (error "
                                f"word {int(self.ztick[1].item())}: 1 tile map, 2 column barrier, 4 exchange "
-                               "timeout); results invalid")
+                               "timeout, 8 persistent grid barrier); results invalid")
         P = self.P   # the buffer whose bf16 shadow the kernels read (FSDP: the gathered full one)
         if self.fuse_opt and int(self.state.opt_state["count"].item()) % 2 == 1:
             P.s("output_dense/kernel").copy_(self.W2s1)

@@ -1,0 +1,85 @@
+"""The persistent run-ahead launch (ops/csrc/mlp_fused.hip mlp2_pst_kernel): n >= 2
+headline steps in ONE launch, each workgroup's AdamW state in registers across them and an
+XCD-hierarchical grid barrier between steps, against the same steps as n run-ahead
+launches (JDT_MLP2_PST=0) -- through the multi-step graphs (cold, then primed), 1-step
+graphs, eager run-ahead calls and two-launch steps mixed in (logits accumulators, step,
+launch and barrier counters stay consistent).  The only difference between the two is the
+order of the forward's fp32 logits atomics, so agreement is to that rounding (the same
+bound as the run-ahead against two launches)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+def _run(b, pst, opt, monkeypatch):
+    from jax_distributed_tuts_amd.models.mlp import Classifier
+    from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
+
+    monkeypatch.setenv("JDT_MLP2_PST", pst)
+    st = init_dp(Classifier(), opt, 69, DEV)
+    tr = DataParallelTrainer(st, None, DPConfig(4, "kernel"))
+    tr.step(b)
+    eng = tr.fused
+    assert eng.ahead_ok and eng.pst_ok == (pst == "1")
+    tr.capture(b, steps_per_graph=7)
+    tr.run_steps(b, 14)          # cold 7-step graph, then the primed one
+    tr.step(b)
+    tr.step(b)                   # 1-step primed graphs (one-step kernel)
+    eng.forward_backward(b)      # two launches: clears the primed state
+    eng.run_ahead(b, 3)          # prologue forward + one 3-step launch
+    eng.run_ahead(b, 2, prologue=False)
+    eng.forward_backward(b)
+    tr.finalize()
+    torch.cuda.synchronize()
+    o = st.opt_state
+    out = {"p": st.params.master.clone(), "metrics": tr.metrics.clone(), "count": int(o["count"].item()),
+           "shadow": st.params.shadow.clone()}
+    if "m" in o:
+        out["m"], out["v"] = o["m"].clone(), o["v"].clone()
+    zt = eng.ztick.cpu()
+    n = 7 + 7 + 1 + 1 + 3 + 2   # run-ahead steps (one-step launches or steps of persistent launches)
+    assert int(zt[0]) == 0 and int(zt[1]) == 0 and int(zt[2]) == n   # ticket re-armed, no error word, steps
+    nb = 512 // 16
+    assert bool((zt[32:32 * (1 + nb)].view(nb, 32)[:, 0] == 7 * n).all())   # column barriers: 7 per step
+    assert bool((zt[32 * (1 + nb):].view(8, 32)[:, :28] == n).all())       # every tile once per step
+    if pst == "1":
+        ws = eng.pst_ws.cpu()
+        gens = 6 + 6 + 2 + 1     # grid barriers: n - 1 per persistent launch (7, 7, 3, 2)
+        assert int(ws[0]) == gens and int(ws[32]) == 8 * gens
+        assert bool((ws[64:320].view(8, 32)[:, 0] == 28 * gens).all())   # 224 workgroups, 28 per XCD
+    return out
+
+
+@pytest.mark.parametrize("rows", [128, 64, 32])
+def test_persistent_run_ahead_matches_per_step_launches(rows, monkeypatch):
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    g = torch.Generator().manual_seed(3)
+    b = Batch(torch.randn(rows, 784, generator=g).to(DEV),
+              torch.randint(0, 10, (rows,), generator=g).to(torch.int32).to(DEV))
+    res = {k: _run(b, k, adamw(1e-3), monkeypatch) for k in ("0", "1")}
+    assert res["0"]["count"] == res["1"]["count"] == 24
+    for k in ("p", "m", "v"):
+        d = (res["0"][k] - res["1"][k]).abs()
+        scale = float(res["0"][k].abs().max())
+        assert float(d.max()) <= 3e-3 * max(scale, 1.0), k
+        assert float((d > 1e-5 * max(scale, 1.0)).float().mean()) < 1e-2, k
+    torch.testing.assert_close(res["1"]["metrics"], res["0"]["metrics"], rtol=1e-3, atol=5e-2)
+    sd = (res["0"]["shadow"].float() - res["1"]["shadow"].float()).abs()
+    assert float(sd.max()) <= 1e-2
+
+
+def test_persistent_run_ahead_sgd(monkeypatch):
+    """The fused SGD (m / v alias p, never written) through the persistent launch."""
+    from jax_distributed_tuts_amd.utils.train_state import Batch, sgd
+
+    g = torch.Generator().manual_seed(4)
+    b = Batch(torch.randn(128, 784, generator=g).to(DEV),
+              torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV))
+    res = {k: _run(b, k, sgd(0.05), monkeypatch) for k in ("0", "1")}
+    d = (res["0"]["p"] - res["1"]["p"]).abs()
+    assert float(d.max()) <= 2e-3 * float(res["0"]["p"].abs().max())
+    torch.testing.assert_close(res["1"]["metrics"], res["0"]["metrics"], rtol=1e-3, atol=5e-2)

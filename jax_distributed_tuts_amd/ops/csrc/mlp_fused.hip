@@ -166,6 +166,16 @@ __device__ __forceinline__ AdamK adam_consts(AT& a, int step) {
   return k;
 }
 
+// the same constants with the bias corrections supplied (persistent launch)
+template <class AT>
+__device__ __forceinline__ AdamK adam_consts_pre(AT& a, float rbc1, float rbc2) {
+  AdamK k;
+  k.b1 = a.beta1; k.b2 = a.beta2; k.eps = a.eps; k.wd = a.wd; k.lr = a.lr; k.gs = a.gscale; k.sgd = a.opt_sgd;
+  k.rbc1 = rbc1;
+  k.rbc2 = rbc2;
+  return k;
+}
+
 // AdamW on one element whose (p, m, v) were loaded earlier; writes them back.
 __device__ __forceinline__ float adam_apply(float p, float m, float v, float g, const AdamK& k, float* pp, float* mp,
                                             float* vp) {
@@ -580,6 +590,7 @@ __global__ void __launch_bounds__(NT) tx_selftest_kernel(const TxArgs* X, unsign
 struct PstRegs {
   float op[4], om[4], ov[4];
   float qp, qm, qv;
+  float rbc1, rbc2;   // the step's AdamW bias corrections (computed during the previous barrier)
 };
 // position of a step inside a persistent launch: step `it` of `n`, the launch counter
 // (Mlp2Args::ztick[2]) when the launch started
@@ -609,7 +620,29 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
                                               PstRegs* R = nullptr, const PstPos pp = PstPos{0, 1, 0u}) {
   static_assert(!PST || (AHEAD && !TX && !P3S && !FX && !LOOP), "persistent: the one-GPU run-ahead step");
   constexpr bool SCX = LOOP || PST;        // in-launch hand-offs: sc1 loads / stores
-  const bool pst_last = !PST || pp.it == pp.n - 1;
+  // phase stamps: a persistent launch records step n-2 (a steady step: the last one also
+  // stores the optimizer state)
+  unsigned long long* const stamps_ = (!PST || pp.it + 2 == pp.n) ? a.stamps : nullptr;
+#pragma push_macro("STAMP")
+#undef STAMP
+#define STAMP(i)                                                                              \
+  do {                                                                                        \
+    if (stamps_ && threadIdx.x == 0) {                                                        \
+      unsigned long long* s_ = stamps_ + (long)(blockIdx.y * gridDim.x + blockIdx.x) * 16;    \
+      s_[(i)] = __builtin_amdgcn_s_memrealtime();                                             \
+      if (!PST && (i) == 0) s_[5] = __builtin_amdgcn_s_memtime();                             \
+      if (!PST && (i) == 4) s_[6] = __builtin_amdgcn_s_memtime();                             \
+    }                                                                                         \
+  } while (0)
+  // persistent launches: sub-phase stamps of one lane (slot k), after `dep` is computed
+#define PSTAMP(k, dep)                                                                        \
+  do {                                                                                        \
+    if (PST && stamps_ && lane == 0) {                                                        \
+      const unsigned d_ = __builtin_amdgcn_readfirstlane(__float_as_uint(dep));              \
+      stamps_[(long)(blockIdx.y * gridDim.x + blockIdx.x) * 16 + (k)] =                       \
+          __builtin_amdgcn_s_memrealtime() + (d_ == 0x7fc00001u ? 1ull : 0ull);               \
+    }                                                                                         \
+  } while (0)
   constexpr int MPM = 128;                 // max rows per device (fused path)
   constexpr int LDM = MPM + 8;             // padded row (bf16 elements)
   constexpr int NTILE = KC / 16;           // dW1 output tiles (one per wave)
@@ -745,7 +778,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     fx_hpq = H / fx_W;
   }
   float op[4], om[4], ov[4];
-  if (PST && pp.it > 0) {
+  if constexpr (PST) {   // loaded by the launch's prologue (pst_state_io), carried in registers
 #pragma unroll
     for (int e = 0; e < 4; ++e) { op[e] = R->op[e]; om[e] = R->om[e]; ov[e] = R->ov[e]; }
   } else {
@@ -764,7 +797,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   const float run_pre = (a.running ? a.running : a.logits)[lane & 3];   // lead: metric accumulators
   const int lq = min(lane, C - 1);
   float qp, qm, qv;
-  if (PST && pp.it > 0) {
+  if constexpr (PST) {
     qp = R->qp; qm = R->qm; qv = R->qv;
   } else {
     qp = (fo ? a.pb2 : a.gb2)[lq]; qm = (fo ? a.mb2 : a.gb2)[lq]; qv = (fo ? a.vb2 : a.gb2)[lq];
@@ -802,7 +835,12 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     for (int c = 0; c < C; ++c) lrow[c] = par ? lr1[c] : lr0[c];
   }
 
-  const AdamK ak = adam_consts(a, step);
+  // persistent: the bias corrections (two powf + two divides per lane, ~0.4 us of VALU at
+  // two waves per SIMD on the step's critical path) were computed while this workgroup
+  // waited in the previous grid barrier
+  AdamK ak;
+  if constexpr (PST) ak = adam_consts_pre(a, R->rbc1, R->rbc2);
+  else ak = adam_consts(a, step);
   const long goff = (!fo && a.stage_stride) ? (long)par * a.stage_stride : 0;   // staged bucket half
 
   // ---- 1. CE from the summed logits (rounded like the bf16 Dense output) -> dlogits
@@ -894,6 +932,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
           acc = mfma16x16x32(xf[ks], bfr, acc);
         }
       }
+      if (w == 0) PSTAMP(15, acc[0]);   // wave 0: dW1 tile on MFMA done
       unsigned wt[2] = {0u, 0u};
   #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -901,9 +940,9 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         if (a.fuse_opt) {
           float tp, tm = om[e], tv = ov[e];
           const bf16_t pb = f2bf(adam_apply(op[e], om[e], ov[e], acc[e], ak, &tp, &tm, &tv));
-          if constexpr (PST) { R->op[e] = tp; R->om[e] = tm; R->ov[e] = tv; }
-          if (!pst_last) {
-            // persistent launch: the state stays in registers until its last step
+          if constexpr (PST) {
+            // persistent launch: the state stays in registers (stored after the last step)
+            R->op[e] = tp; R->om[e] = tm; R->ov[e] = tv;
           } else if (AHEAD && (a.wt & 1)) {
             st_f<true>(a.pW1 + idx, tp);
             if (!ak.sgd) { st_f<true>(a.mW1 + idx, tm); st_f<true>(a.vW1 + idx, tv); }
@@ -922,13 +961,14 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         }
       }
       // the lane's 4 rows are 4 consecutive K elements of W1^T: one 8-byte store
-      if (a.fuse_opt && a.W1T && pst_last) {   // persistent: the next steps read w1n (LDS), not W1^T
+      if (!PST && a.fuse_opt && a.W1T) {   // persistent: the next steps read w1n (LDS), not W1^T
         const unsigned long long w8 = (unsigned long long)wt[0] | ((unsigned long long)wt[1] << 32);
         if (LOOP || (AHEAD && (a.wt & 1))) st_u64<true>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
         else st_u64<false>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
       }
       if constexpr (AHEAD)
         *reinterpret_cast<uint2*>(&w1n[(lane & 15) * LDW1 + (trow0 - kc0)]) = make_uint2(wt[0], wt[1]);
+      if (w == 0) PSTAMP(14, __uint_as_float(wt[0]));   // wave 0: AdamW + W1' tile done
     } else if (aux) {
       // chunk-0 blocks, concurrently with the dW1 tiles:
       //   dW2[blk, :] = H1[:, blk]^T dlogits ; db1[blk] = dZ1[:, blk]^T 1 ; db2 = 1^T dlogits (block (0,0))
@@ -963,10 +1003,6 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
               float tp, tm = om[e], tv = ov[e];
               pn = adam_apply(op[e], om[e], ov[e], gr, ak, &tp, &tm, &tv);
               R->op[e] = tp; R->om[e] = tm; R->ov[e] = tv;
-              if (pst_last) {
-                (isb ? a.pb1 : a.pW2)[o] = tp;
-                if (!ak.sgd) { (isb ? a.mb1 : a.mW2)[o] = tm; (isb ? a.vb1 : a.vW2)[o] = tv; }
-              }
             } else {
               pn = adam_apply_h<LOOP>(op[e], om[e], ov[e], gr, ak, (isb ? a.pb1 : a.pW2) + o,
                                       (isb ? a.mb1 : a.mW2) + o, (isb ? a.vb1 : a.vW2) + o);
@@ -988,10 +1024,6 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
             float tp, tm = qm, tv = qv;
             pn = adam_apply(qp, qm, qv, ab2[0], ak, &tp, &tm, &tv);
             R->qp = tp; R->qm = tm; R->qv = tv;
-            if (pst_last) {
-              a.pb2[lane] = tp;
-              if (!ak.sgd) { a.mb2[lane] = tm; a.vb2[lane] = tv; }
-            }
           } else {
             pn = adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
           }
@@ -1003,6 +1035,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
           a.gb2[goff + lane] = ab2[0];
         }
       }
+      PSTAMP(5, aw[0]);   // aux wave: dW2 / db1 / db2 + their AdamW done
     }
   } else {
     // N > 1 (TX): all MFMAs, then the tile exchange, then the epilogues
@@ -1454,6 +1487,8 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     }
   }
   STAMP(4);
+#pragma pop_macro("STAMP")
+#undef PSTAMP
 }
 
 // ---------------------------------------------------------------------------- kernels
@@ -1531,7 +1566,9 @@ __global__ void __launch_bounds__(NT) mlp2_loop_kernel(Mlp2Args a, Mlp2Loop l) {
 // wave drains its stores and atomics first (vmcnt), so the step's hand-offs (sc1 / atomic
 // for cross-XCD bytes, L2 for the column block's own XCD) are complete before anyone passes.
 // A wall-clock timeout (20 ms) raises bit 8 of the error word and every workgroup leaves.
-__device__ __forceinline__ bool pst_grid_sync(unsigned* ws, unsigned gen, int* ok_lds, unsigned* errw) {
+// Arrival: every wave drains, then one lane adds to its XCD's counter (and the XCD's last
+// arriver to the top counter).  The caller may compute between arrival and the wait.
+__device__ __forceinline__ void pst_arrive(unsigned* ws) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1543,6 +1580,11 @@ __device__ __forceinline__ bool pst_grid_sync(unsigned* ws, unsigned gen, int* o
         __hip_atomic_fetch_add((gu32_t*)(ws + 32 * (2 + xcc)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old % per == per - 1)
       __hip_atomic_fetch_add((gu32_t*)(ws + 32), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// Wait: one lane polls the top counter for 8 arrivals per generation (sc1 loads), bounded.
+__device__ __forceinline__ bool pst_wait(unsigned* ws, unsigned gen, int* ok_lds, unsigned* errw) {
+  if (threadIdx.x == 0) {
     const unsigned target = 8u * gen;
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(ws + 32, (short)0, 4, 0x00020000);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -1562,6 +1604,81 @@ __device__ __forceinline__ bool pst_grid_sync(unsigned* ws, unsigned gen, int* o
   return ok_lds[0] != 0;
 }
 
+// The AdamW state a persistent launch carries in registers (PstRegs), loaded before its
+// first step and stored after its last: the elements each lane owns in mlp2_bwd_body's
+// phase-3 epilogues (same indices) -- tile waves 4 W1 elements (plus their W1^T bf16
+// copy), the chunk-0 aux wave W2 / b1 (lanes ac <= C) and, in block (0,0), b2.
+template <int K_IN, int C, int KC, class AT>
+__device__ __forceinline__ void pst_state_io(AT& a, const int bx, const int by, PstRegs& R, const bool store) {
+  constexpr int NTILE = KC / 16;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, H = a.H;
+  const int j0 = bx * 16, kc0 = by * KC;
+  const bool aux = by == 0 && w == NW - 1;
+  const int ac = lane & 15;
+  const bool w2l = aux && ac < C;
+  const int trow0 = kc0 + min(w, NTILE - 1) * 16 + (lane >> 4) * 4, tcol = j0 + (lane & 15);
+  const bool sgd = a.opt_sgd != 0;
+  // argument words as scalar values first, then per-lane selects between those values
+  // (a select between two fields of the by-value argument block made the compiler give
+  // the kernel a private copy of it: a scratch segment, set up at the first launch)
+  float* const pW1 = sgpr_ptr(a.pW1); float* const mW1 = sgpr_ptr(a.mW1); float* const vW1 = sgpr_ptr(a.vW1);
+  float* const pW2 = sgpr_ptr(a.pW2); float* const mW2 = sgpr_ptr(a.mW2); float* const vW2 = sgpr_ptr(a.vW2);
+  float* const pb1 = sgpr_ptr(a.pb1); float* const mb1 = sgpr_ptr(a.mb1); float* const vb1 = sgpr_ptr(a.vb1);
+  float* const pb2 = sgpr_ptr(a.pb2); float* const mb2 = sgpr_ptr(a.mb2); float* const vb2 = sgpr_ptr(a.vb2);
+  if (!store) {
+    float* const sp = aux ? (w2l ? pW2 : pb1) : pW1;
+    float* const sm = aux ? (w2l ? mW2 : mb1) : mW1;
+    float* const sv = aux ? (w2l ? vW2 : vb1) : vW1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = (lane >> 4) * 4 + e;
+      const long idx = aux ? (w2l ? (long)(j0 + n) * C + ac : (long)(j0 + n)) : (long)(trow0 + e) * H + tcol;
+      R.op[e] = ld_global(sp + idx); R.om[e] = ld_global(sm + idx); R.ov[e] = ld_global(sv + idx);
+    }
+    const int lq = min(lane, C - 1);
+    R.qp = ld_global(pb2 + lq); R.qm = ld_global(mb2 + lq); R.qv = ld_global(vb2 + lq);
+    return;
+  }
+  if (w < NTILE) {
+    unsigned wt[2] = {0u, 0u};
+    const bool wt1 = (a.wt & 1) != 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long idx = (long)(trow0 + e) * H + tcol;
+      if (wt1) {
+        st_f<true>(pW1 + idx, R.op[e]);
+        if (!sgd) { st_f<true>(mW1 + idx, R.om[e]); st_f<true>(vW1 + idx, R.ov[e]); }
+      } else {
+        pW1[idx] = R.op[e];
+        if (!sgd) { mW1[idx] = R.om[e]; vW1[idx] = R.ov[e]; }
+      }
+      wt[e >> 1] |= (unsigned)f2bf(R.op[e]) << (16 * (e & 1));
+    }
+    const unsigned long long w8 = (unsigned long long)wt[0] | ((unsigned long long)wt[1] << 32);
+    bf16_t* const W1T = sgpr_ptr(a.W1T);
+    if (wt1) st_u64<true>(W1T + (long)tcol * a.ldw1t + trow0, w8);
+    else st_u64<false>(W1T + (long)tcol * a.ldw1t + trow0, w8);
+  } else if (aux) {
+    if (ac <= C) {
+      const bool isb = ac == C;
+      float* const dp = isb ? pb1 : pW2;
+      float* const dm = isb ? mb1 : mW2;
+      float* const dv = isb ? vb1 : vW2;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = (lane >> 4) * 4 + e;
+        const long o = isb ? (long)(j0 + n) : (long)(j0 + n) * C + ac;
+        dp[o] = R.op[e];
+        if (!sgd) { dm[o] = R.om[e]; dv[o] = R.ov[e]; }
+      }
+    }
+    if (bx == 0 && by == 0 && lane < C) {
+      pb2[lane] = R.qp;
+      if (!sgd) { mb2[lane] = R.qm; vb2[lane] = R.qv; }
+    }
+  }
+}
+
 // n run-ahead steps in ONE launch (single GPU, fused AdamW, W1^T copy): step i's CE,
 // backward and AdamW plus step i+1's forward, then the grid barrier, n times.  The AdamW
 // state of every workgroup's tile stays in registers across the steps (PstRegs) -- the
@@ -1573,6 +1690,7 @@ __device__ __forceinline__ bool pst_grid_sync(unsigned* ws, unsigned gen, int* o
 template <int K_IN, int C, int KC>
 __global__ void __launch_bounds__(NT) mlp2_pst_kernel(Mlp2Args a, int n, unsigned* ws) {
   __shared__ int ok_lds[1];
+  if (n <= 0) return;   // warm-up launch (jdt_mlp2_pst n = 0): touches nothing
   int bx = blockIdx.x, by = blockIdx.y;
   xcd_column_tile(bx, by);
   // read before the first barrier; block (0,0) rewrites them only after the last one
@@ -1580,25 +1698,41 @@ __global__ void __launch_bounds__(NT) mlp2_pst_kernel(Mlp2Args a, int n, unsigne
   const unsigned launch0 = a.ztick[2];
   const unsigned gen0 = ws[0];
   // the body's ~50 argument words re-read from the kernarg segment each step (laundered
-  // pointer) instead of being held live across the loop (mlp2_loop_kernel's lesson)
+  // pointer) instead of being held live across the loop (by value: 107 SGPRs spilled)
   typedef const __attribute__((address_space(4))) Mlp2Args KArgs;
   KArgs* const kbase = (KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
   PstRegs R;
+  pst_state_io<K_IN, C, KC>(a, bx, by, R, false);
+  {
+    const AdamK k0 = adam_consts(*kbase, step0);
+    R.rbc1 = k0.rbc1;
+    R.rbc2 = k0.rbc2;
+  }
   int it = 0;
-  // diagnostic stamps (Mlp2Args::stamps; the body stamps its phases each step, the last
-  // step's survive): slot 7 = start of step n-2, 12 / 13 = before / after the last barrier
+  // diagnostic stamps (Mlp2Args::stamps; the body stamps the phases of step n-2, sub-phases
+  // in slots 5, 14, 15): slot 7 = start of step n-1, 12 / 13 = before / after the barrier
+  // between them, 6 = the tile (bx + 256 * by) this workgroup plays
   unsigned long long* const stw =
       a.stamps && threadIdx.x == 0 ? a.stamps + (long)(blockIdx.y * gridDim.x + blockIdx.x) * 16 : nullptr;
   for (; it < n; ++it) {
     KArgs* k = kbase;
     asm volatile("" : "+s"(k));
-    if (stw && it == n - 2) stw[7] = __builtin_amdgcn_s_memrealtime();
+    if (stw && it == n - 1) stw[7] = __builtin_amdgcn_s_memrealtime();
     mlp2_bwd_body<K_IN, C, KC, false, true, false, false, false, true>(*k, bx, by, step0 + it, &R,
                                                                         PstPos{it, n, launch0});
     if (stw && it == n - 2) stw[12] = __builtin_amdgcn_s_memrealtime();
-    if (it + 1 < n && !pst_grid_sync(ws, gen0 + (unsigned)it + 1u, ok_lds, a.ztick)) break;
+    if (it + 1 < n) {
+      pst_arrive(ws);
+      // the next step's bias corrections, while the other workgroups arrive
+      const AdamK kn = adam_consts(*kbase, step0 + it + 1);
+      R.rbc1 = kn.rbc1;
+      R.rbc2 = kn.rbc2;
+      if (!pst_wait(ws, gen0 + (unsigned)it + 1u, ok_lds, a.ztick)) break;
+    }
     if (stw && it == n - 2) stw[13] = __builtin_amdgcn_s_memrealtime();
   }
+  if (it == n) pst_state_io<K_IN, C, KC>(a, bx, by, R, true);
+  if (stw) stw[6] = (unsigned long long)(bx + 256 * by);
   if (bx == 0 && by == 0 && threadIdx.x == 0 && it == n) {
     a.step[0] = step0 + n;
     a.ztick[2] = launch0 + (unsigned)n;
@@ -1756,10 +1890,13 @@ JDT_API int jdt_mlp2_pst_ok(int M, int H, int k_in) {
 
 // n >= 2 run-ahead steps in one persistent launch (mlp2_pst_kernel); ws: >= 10 x 32 words,
 // zeroed once, never reset (monotonic barrier counters).  -3 outside the run-ahead's
-// argument envelope (the caller then launches the one-step kernel n times).
+// argument envelope (the caller then launches the one-step kernel n times).  n = 0: a
+// launch that returns at once -- done once before any timed or captured use, so the
+// kernel's first-dispatch setup (its private segment, ~100 us) is not paid inside one
+// (bench.py's 20-step driver form measured 51.6k steps/s without it).
 JDT_API int jdt_mlp2_pst(const Mlp2Args* args, int n, int k_in, unsigned* ws, void* stream) {
   const Mlp2Args& a = *args;
-  if (n < 2 || !ws || a.tx || !a.fuse_opt || !a.W1T || !a.XR || !a.zslab || !a.ztick || !a.hand || !a.lg3 ||
+  if (n == 1 || n < 0 || !ws || a.tx || !a.fuse_opt || !a.W1T || !a.XR || !a.zslab || !a.ztick || !a.hand || !a.lg3 ||
       a.det_logits || a.M <= 0 || a.M > 128 || a.H % 128)
     return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);

@@ -252,6 +252,7 @@ class FusedMLP2:
                        and bool(_lib.lib().jdt_mlp2_pst_ok(rows, H, K)))
         if self.pst_ok:
             self.pst_ws = torch.zeros(32 * 10, dtype=torch.int32, device=dev)
+        self._pst_warm = False
 
     def set_grad_stage(self, base: int, stride: int):
         """Mode 0: write the gradient bucket into the xGMI staging buffer at ``base``
@@ -368,13 +369,7 @@ class FusedMLP2:
             self._args, self._key = self._build_args(batch), key
             self._ahead_args = None
         if self._ahead_args is None:
-            b = Mlp2Args.from_buffer_copy(self._args)
-            b.logits = self.logits_all[2:].data_ptr()
-            b.lg3 = 1
-            b.XR, b.zslab, b.ztick, b.hand = (t.data_ptr() for t in (self.XR, self.zslab, self.ztick, self.hand))
-            if self.tx is not None:
-                b.tx = self.tx.args_ptr
-            self._ahead_args = b
+            self._make_ahead_args()
         L = _lib.lib()
         s = _lib.stream_ptr()
         if prologue:
@@ -383,6 +378,8 @@ class FusedMLP2:
         elif not torch.cuda.is_current_stream_capturing():
             assert self.ahead_primed, "run_ahead(prologue=False) needs a run-ahead launch just before"
         if self.pst_ok and n >= 2:
+            if not torch.cuda.is_current_stream_capturing():
+                self.pst_warm()
             _lib.check(L.jdt_mlp2_pst(ctypes.byref(self._ahead_args), int(n), self.K, self.pst_ws.data_ptr(), s),
                        "mlp2_pst")
         else:
@@ -390,6 +387,23 @@ class FusedMLP2:
                 _lib.check(L.jdt_mlp2(ctypes.byref(self._ahead_args), 2, self.K, 10, s), "mlp2_bwd_ahead")
         if not torch.cuda.is_current_stream_capturing():
             self.ahead_primed = True
+
+    def _make_ahead_args(self):
+        b = Mlp2Args.from_buffer_copy(self._args)
+        b.logits = self.logits_all[2:].data_ptr()
+        b.lg3 = 1
+        b.XR, b.zslab, b.ztick, b.hand = (t.data_ptr() for t in (self.XR, self.zslab, self.ztick, self.hand))
+        if self.tx is not None:
+            b.tx = self.tx.args_ptr
+        self._ahead_args = b
+
+    def pst_warm(self):
+        """One no-op dispatch of the persistent kernel (n = 0), once, outside any capture:
+        its first-dispatch setup (private segment) lands here, not in a timed replay."""
+        if self.pst_ok and not self._pst_warm and self._ahead_args is not None:
+            _lib.check(_lib.lib().jdt_mlp2_pst(ctypes.byref(self._ahead_args), 0, self.K, self.pst_ws.data_ptr(),
+                                               _lib.stream_ptr()), "mlp2_pst warm")
+            self._pst_warm = True
 
     def run_loop(self, batch, n: int, stamps: Optional[torch.Tensor] = None) -> bool:
         """n complete steps (forward, backward, AdamW) in ONE persistent launch.
@@ -449,6 +463,13 @@ class AheadGraphs:
         self.eng = eng
         self._checked = False
         self.graphs = {}
+        if int(steps_per_graph) >= 2 and getattr(eng, "pst_ok", False):
+            if eng._ahead_args is None:   # the arguments are built by the first run-ahead call
+                eng._args, eng._key = eng._build_args(batch), (batch.inputs.data_ptr(), batch.labels.data_ptr(),
+                                                              eng.state.rng)
+                eng._ahead_args = None
+                eng._make_ahead_args()
+            eng.pst_warm()
         for S in sorted({1, int(steps_per_graph)}):
             for primed in (False, True):
                 g = torch.cuda.CUDAGraph()

@@ -1,6 +1,6 @@
 # persistent run-ahead headline kernel: correctness, then driver-form / 300-step A/B
 cd /root/repo && export TMPDIR=/tmp PYTHONUNBUFFERED=1 && mkdir -p gpurun_out/r5s25 || exit 1
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_mlp2_persistent_gpu.py \
+timeout -k 10 300 python -u -m pytest -x -v -s --timeout 120 --timeout-method thread tests/test_mlp2_persistent_gpu.py \
   > gpurun_out/r5s25/pst_tests.log 2>&1; rc=$?; tail -8 gpurun_out/r5s25/pst_tests.log; [ $rc -eq 0 ] || exit 1
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "ahead or fused_mlp" \
   > gpurun_out/r5s25/ahead_tests.log 2>&1; rc=$?; tail -3 gpurun_out/r5s25/ahead_tests.log; [ $rc -eq 0 ] || exit 1

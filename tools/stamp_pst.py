@@ -1,7 +1,8 @@
 """Diagnostic: phase stamps (s_memrealtime, 100 MHz) of the persistent run-ahead launch
 (csrc/mlp_fused.hip mlp2_pst_kernel).  One n-step launch with stamps on; per workgroup the
-last step's phase ends (the body's STAMP points), the step before it (slot 7 -> next
-start) and the grid barrier between them (slots 12 -> 13).  Medians over the 224
+phase ends of step n-2 (the body's STAMP points; the last step also stores the optimizer
+state), the step time (start of n-2 -> start of n-1) and the grid barrier between them
+(slots 12 -> 13).  Medians over the 224
 workgroups, microseconds.
 
     python tools/stamp_pst.py [--steps 20] [--rows 128]
@@ -20,7 +21,8 @@ from jax_distributed_tuts_amd.models.mlp import Classifier  # noqa: E402
 from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp  # noqa: E402
 from jax_distributed_tuts_amd.utils.train_state import Batch, adamw  # noqa: E402
 
-PHASES = [(1, "CE -> dlogits (loads landed)"), (2, "dZ1"), (3, "dW1 MFMA + AdamW + hand-offs"),
+PHASES = [(1, "CE -> dlogits (loads landed)"), (2, "dZ1"), (15, "  wave 0: dW1 tile MFMA"),
+          (14, "  wave 0: AdamW + W1' tile"), (3, "dW1 MFMA + AdamW + hand-offs"),
           (8, "next Z1 partials stored"), (9, "column barrier passed"), (10, "partials loaded"),
           (11, "forward epilogue (G1 / H1)"), (4, "logit atomics issued")]
 
@@ -53,10 +55,10 @@ def main():
         torch.cuda.synchronize()
         s = stamps.view(224, 16).double() * 1e-2       # us
         t0 = s[:, 0]
-        step = float((s[:, 0] - s[:, 7]).median())
+        step = float((s[:, 7] - s[:, 0]).median())
         bar = float((s[:, 13] - s[:, 12]).median())
         print(f"rep {rep}: launch {ev0.elapsed_time(ev1) * 1e3 / args.steps:.2f} us/step (events) | "
-              f"step n-2 -> n-1 start: median {step:.2f} us | last grid barrier: median {bar:.2f} us, "
+              f"step n-2 start -> n-1 start: median {step:.2f} us | last grid barrier (n-2 -> n-1): median {bar:.2f} us, "
               f"max {float((s[:, 13] - s[:, 12]).max()):.2f}")
         if rep == args.reps - 1:
             prev = torch.zeros_like(t0)
@@ -65,8 +67,23 @@ def main():
                 print(f"    {name:32s} end @ median {float(d.median()):6.2f} us  max {float(d.max()):6.2f}"
                       f"   (phase median {float((d - prev).median()):5.2f})")
                 prev = d
-            print(f"    start skew of the last step {float(t0.max() - t0.min()):.2f} us; "
+            print(f"    start skew of step n-2 {float(t0.max() - t0.min()):.2f} us; "
                   f"first start -> last end {float(s[:, 4].max() - t0.min()):.2f} us")
+            tile = stamps.view(224, 16)[:, 6].cpu()
+            by = (tile // 256).double()
+            print("    per input chunk (chunk 0 runs the dW2 / db1 / db2 wave; block (0,0) the CE metrics):")
+            for y in range(int(by.max()) + 1):
+                sel = (by == y).to(s.device)
+                ends = [float((s[sel, k] - t0[sel]).median()) for k, _ in PHASES]
+                extra = ""
+                if y == 0:
+                    extra = f"   aux wave done {float((s[sel, 5] - t0[sel]).median()):5.2f}"
+                print(f"      chunk {y}: " + " ".join(f"{e:5.2f}" for e in ends) + extra)
+            xcd = torch.arange(224) % 8
+            for x in range(8):
+                sel = (xcd == x).to(s.device)
+                print(f"      dispatch XCD {x}: phase-3 end median {float((s[sel, 3] - t0[sel]).median()):5.2f}, "
+                      f"last-step start (rel. earliest) median {float((t0[sel] - t0.min()).median()):5.2f}")
     eng._ahead_args.stamps = None
     tr.finalize()
 

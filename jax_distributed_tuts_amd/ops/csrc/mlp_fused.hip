@@ -695,16 +695,15 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
           lr0[c] = a.logits[lo + c]; lr1[c] = a.logits[(long)M * C + lo + c]; lr2[c] = a.logits[2l * M * C + lo + c];
         }
       }
-      if constexpr (PST) {   // accumulated by other XCDs' atomics this launch: 8-byte sc1 loads
+      if constexpr (PST) {
+        // accumulated by other XCDs' atomics during the previous step: 8-byte sc1 loads of
+        // this step's buffer only (the step is known: no load waits on the counter)
         static_assert(C % 2 == 0, "logits rows in 8-byte pairs");
+        const float* lg = a.logits + (long)(step_in % 3) * M * C + lo;
 #pragma unroll
         for (int q = 0; q < C / 2; ++q) {
-          const unsigned long long x0 = ld_u64<true>(a.logits + lo + 2 * q);
-          const unsigned long long x1 = ld_u64<true>(a.logits + (long)M * C + lo + 2 * q);
-          const unsigned long long x2 = ld_u64<true>(a.logits + 2l * M * C + lo + 2 * q);
+          const unsigned long long x0 = ld_u64<true>(lg + 2 * q);
           lr0[2 * q] = __uint_as_float((unsigned)x0); lr0[2 * q + 1] = __uint_as_float((unsigned)(x0 >> 32));
-          lr1[2 * q] = __uint_as_float((unsigned)x1); lr1[2 * q + 1] = __uint_as_float((unsigned)(x1 >> 32));
-          lr2[2 * q] = __uint_as_float((unsigned)x2); lr2[2 * q + 1] = __uint_as_float((unsigned)(x2 >> 32));
         }
       }
     } else if constexpr (LOOP) {   // step known: this step's parity only
@@ -826,7 +825,10 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   else if constexpr (!LOOP) step = (a.step_copy ? a.step_copy : a.step)[0];
   const int par = step & 1;
   float lrow[C];
-  if constexpr (AHEAD) {
+  if constexpr (PST) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) lrow[c] = lr0[c];
+  } else if constexpr (AHEAD) {
     const int p3 = step % 3;
 #pragma unroll
     for (int c = 0; c < C; ++c) lrow[c] = p3 == 0 ? lr0[c] : (p3 == 1 ? lr1[c] : lr2[c]);
@@ -1576,8 +1578,10 @@ __device__ __forceinline__ void pst_arrive(unsigned* ws) {
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
     xcc &= 7u;
     const unsigned per = (gridDim.x * gridDim.y) / 8u;
+    // the XCD's counter line is touched only by its own workgroups: an L2 atomic (workgroup
+    // scope, as the run-ahead's column barrier); the top counter is cross-XCD (agent scope)
     const unsigned old =
-        __hip_atomic_fetch_add((gu32_t*)(ws + 32 * (2 + xcc)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add((gu32_t*)(ws + 32 * (2 + xcc)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (old % per == per - 1)
       __hip_atomic_fetch_add((gu32_t*)(ws + 32), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }

@@ -3,9 +3,11 @@ headline steps in ONE launch, each workgroup's AdamW state in registers across t
 XCD-hierarchical grid barrier between steps, against the same steps as n run-ahead
 launches (JDT_MLP2_PST=0) -- through the multi-step graphs (cold, then primed), 1-step
 graphs, eager run-ahead calls and two-launch steps mixed in (logits accumulators, step,
-launch and barrier counters stay consistent).  The only difference between the two is the
-order of the forward's fp32 logits atomics, so agreement is to that rounding (the same
-bound as the run-ahead against two launches)."""
+launch and barrier counters stay consistent).  Same arithmetic in the same order except the
+forward's fp32 logits atomics (arrival order), so the two agree to that rounding: measured
+bit-identical at 32 / 64 / 128 rows (max |dp| 1.3e-7 in one earlier run).  The bound is
+~100 ulp of the parameters -- far below what one step on stale logits, a stale W2 shadow
+or a lost tile would do (those move a parameter by ~lr = 1e-3)."""
 import pytest
 import torch
 
@@ -70,11 +72,10 @@ def test_persistent_run_ahead_matches_per_step_launches(rows, monkeypatch):
         print(f"[pst rows {rows}] {k}: max |d| {float(d.max()):.3e} (scale {scale:.3e}), "
               f"frac > 1e-5 scale {float((d > 1e-5 * max(scale, 1.0)).float().mean()):.2e}, "
               f"frac != {float((d > 0).float().mean()):.2e}")
-        assert float(d.max()) <= 3e-3 * max(scale, 1.0), k
-        assert float((d > 1e-5 * max(scale, 1.0)).float().mean()) < 1e-2, k
-    torch.testing.assert_close(res["1"]["metrics"], res["0"]["metrics"], rtol=1e-3, atol=5e-2)
+        assert float(d.max()) <= 1e-5 * scale, k
+    torch.testing.assert_close(res["1"]["metrics"], res["0"]["metrics"], rtol=1e-5, atol=1e-3)
     sd = (res["0"]["shadow"].float() - res["1"]["shadow"].float()).abs()
-    assert float(sd.max()) <= 1e-2
+    assert float(sd.max()) <= 1e-3 * float(res["0"]["shadow"].float().abs().max())
 
 
 def test_persistent_run_ahead_sgd(monkeypatch):
@@ -86,5 +87,5 @@ def test_persistent_run_ahead_sgd(monkeypatch):
               torch.randint(0, 10, (128,), generator=g).to(torch.int32).to(DEV))
     res = {k: _run(b, k, sgd(0.05), monkeypatch) for k in ("0", "1")}
     d = (res["0"]["p"] - res["1"]["p"]).abs()
-    assert float(d.max()) <= 2e-3 * float(res["0"]["p"].abs().max())
-    torch.testing.assert_close(res["1"]["metrics"], res["0"]["metrics"], rtol=1e-3, atol=5e-2)
+    assert float(d.max()) <= 1e-5 * float(res["0"]["p"].abs().max())
+    torch.testing.assert_close(res["1"]["metrics"], res["0"]["metrics"], rtol=1e-5, atol=1e-3)

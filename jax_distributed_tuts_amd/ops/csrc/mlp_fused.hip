@@ -591,6 +591,7 @@ struct PstRegs {
   float op[4], om[4], ov[4];
   float qp, qm, qv;
   float rbc1, rbc2;   // the step's AdamW bias corrections (computed during the previous barrier)
+  float l_loss, l_corr;   // block (0,0): this thread's row loss / hit, folded into the metrics
 };
 // position of a step inside a persistent launch: step `it` of `n`, the launch counter
 // (Mlp2Args::ztick[2]) when the launch started
@@ -881,14 +882,31 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   }
   for (int idx = tid; idx < (16 - C) * MPM; idx += NT) dlT[(C + idx / MPM) * LDM + idx % MPM] = 0;
   w2B[(tid >> 5) * LDB + (tid & 31)] = (tid & 31) < C ? (par ? w2b : w2a) : (bf16_t)0;
-  if (lead) {
+  if constexpr (PST) {   // folded into the metrics while waiting in the grid barrier
+    R->l_loss = l_loss;
+    R->l_corr = l_corr;
+  }
+  if (lead && !PST) {
     l_loss = wave_sum(l_loss);
     l_corr = wave_sum(l_corr);
     if (lane == 0) { red[0][w] = l_loss; red[1][w] = l_corr; }
+  }
+  if (lead) {
     // re-arm the accumulator of the step after next (run-ahead: step t+1's forward
     // accumulates into buffer (t+1) % 3 during this launch)
     float* nxt = a.logits + (long)(AHEAD ? (step + 2) % 3 : (par ^ 1)) * M * C;
-    for (int i = tid; i < M * C; i += NT) st_f<SCX>(nxt + i, 0.f);
+    if constexpr (!PST)
+      for (int i = tid; i < M * C; i += NT) st_f<SCX>(nxt + i, 0.f);
+  }
+  if constexpr (PST) {
+    // persistent: every workgroup re-arms 8 words (write-through), so the lead workgroup
+    // -- and with it its column block, which everyone then waits for at the grid barrier --
+    // does not drain 1,280 sc1 stores before its column barrier (stamps: column block 0
+    // was the step's last by ~0.5 us)
+    float* nxt = a.logits + (long)((step + 2) % 3) * M * C;
+    const int G = (int)(gridDim.x * gridDim.y), t = by * (int)gridDim.x + bx;
+    if (tid < 8)
+      for (int i = t * 8 + tid; i < M * C; i += G * 8) st_f<true>(nxt + i, 0.f);
   }
   if constexpr (AHEAD) {   // K padding of the W1' tile image
     for (int idx = tid; idx < 16 * (128 - KC); idx += NT) w1n[(idx / (128 - KC)) * LDW1 + KC + idx % (128 - KC)] = 0;
@@ -987,7 +1005,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         const bf16x8 zT = *reinterpret_cast<const bf16x8*>(&dzT[(lane & 15) * LDM + kk]);
         aw = mfma16x16x32(hT, dT, aw);
         ab1 = mfma16x16x32(zT, ones, ab1);
-        if (lead) ab2 = mfma16x16x32(ones, dT, ab2);
+        if (lead && !PST) ab2 = mfma16x16x32(ones, dT, ab2);
       }
       bf16_t* sW2n = par ? a.sW2_0 : a.sW2_1;   // next step's parity buffer
   #pragma unroll
@@ -1019,16 +1037,9 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
           }
         }
       }
-      if (lead && lane < C) {
+      if (!PST && lead && lane < C) {
         if (a.fuse_opt) {
-          float pn;
-          if constexpr (PST) {
-            float tp, tm = qm, tv = qv;
-            pn = adam_apply(qp, qm, qv, ab2[0], ak, &tp, &tm, &tv);
-            R->qp = tp; R->qm = tm; R->qv = tv;
-          } else {
-            pn = adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
-          }
+          const float pn = adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
           a.sb2[lane] = f2bf(pn);
           if constexpr (AHEAD) a.hand[H + (long)H * C + lane] = pn;
         } else if (a.smap) {
@@ -1038,6 +1049,29 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         }
       }
       PSTAMP(5, aw[0]);   // aux wave: dW2 / db1 / db2 + their AdamW done
+    } else if (PST && bx == 0 && by == 1 && w == NW - 1) {
+      // persistent: db2 = 1^T dlogits and b2's AdamW on the otherwise idle last wave of
+      // block (0,1) instead of the lead's aux wave (the lead's extra work held its column
+      // block -- and so the grid barrier -- back by ~0.5 us); the same MFMA sum and AdamW,
+      // handed to the column block's forward epilogues like the lead's was
+      bf16x8 ones;
+  #pragma unroll
+      for (int q = 0; q < 8; ++q) ones[q] = (short)0x3f80;  // bf16 1.0
+      f32x4 ab2 = {0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+      for (int ks = 0; ks < MPM / 32; ++ks) {
+        if (ks >= Mp / 32) break;
+        const int kk = ks * 32 + 8 * (lane >> 4);
+        const bf16x8 dT = *reinterpret_cast<const bf16x8*>(&dlT[(lane & 15) * LDM + kk]);
+        ab2 = mfma16x16x32(ones, dT, ab2);
+      }
+      if (lane < C) {
+        float tp, tm = qm, tv = qv;
+        const float pn = adam_apply(qp, qm, qv, ab2[0], ak, &tp, &tm, &tv);
+        R->qp = tp; R->qm = tm; R->qv = tv;
+        a.sb2[lane] = f2bf(pn);
+        a.hand[H + (long)H * C + lane] = pn;
+      }
     }
   } else {
     // N > 1 (TX): all MFMAs, then the tile exchange, then the epilogues
@@ -1342,7 +1376,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   __syncthreads();
   STAMP(3);
 
-  if (lead && tid < 4) {
+  if (!PST && lead && tid < 4) {
     float val = mval;   // N > 1 run-ahead: the all-reduced slot
     if (!(AHEAD && TX)) {
       float L = 0.f, Cr = 0.f;
@@ -1639,7 +1673,7 @@ __device__ __forceinline__ void pst_state_io(AT& a, const int bx, const int by, 
       const long idx = aux ? (w2l ? (long)(j0 + n) * C + ac : (long)(j0 + n)) : (long)(trow0 + e) * H + tcol;
       R.op[e] = ld_global(sp + idx); R.om[e] = ld_global(sm + idx); R.ov[e] = ld_global(sv + idx);
     }
-    const int lq = min(lane, C - 1);
+    const int lq = min(lane, C - 1);   // b2: block (0,1)'s last wave (mlp2_bwd_body PST)
     R.qp = ld_global(pb2 + lq); R.qm = ld_global(mb2 + lq); R.qv = ld_global(vb2 + lq);
     return;
   }
@@ -1676,10 +1710,25 @@ __device__ __forceinline__ void pst_state_io(AT& a, const int bx, const int by, 
         if (!sgd) { dm[o] = R.om[e]; dv[o] = R.ov[e]; }
       }
     }
-    if (bx == 0 && by == 0 && lane < C) {
-      pb2[lane] = R.qp;
-      if (!sgd) { mb2[lane] = R.qm; vb2[lane] = R.qv; }
-    }
+  }
+  if (bx == 0 && by == 1 && w == NW - 1 && lane < C) {
+    pb2[lane] = R.qp;
+    if (!sgd) { mb2[lane] = R.qm; vb2[lane] = R.qv; }
+  }
+}
+
+// Block (0,0), persistent launch: the step's loss sum / hits folded into the running metrics
+// ({loss sum, n, correct, n}: the per-step kernel's metric slot), between arriving at the grid
+// barrier and waiting on it (or after the last step) -- off the step's critical path.
+__device__ __forceinline__ void pst_metrics(float* running, int M, const PstRegs& R, float (*red)[NW]) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float L = wave_sum(R.l_loss), Cr = wave_sum(R.l_corr);
+  if (lane == 0) { red[0][w] = L; red[1][w] = Cr; }
+  __syncthreads();
+  if (tid < 4) {
+    float Ls = 0.f, Cs = 0.f;
+    for (int q = 0; q < NW; ++q) { Ls += red[0][q]; Cs += red[1][q]; }
+    running[tid] += tid == 0 ? Ls : tid == 2 ? Cs : (float)M;
   }
 }
 
@@ -1694,6 +1743,7 @@ __device__ __forceinline__ void pst_state_io(AT& a, const int bx, const int by, 
 template <int K_IN, int C, int KC>
 __global__ void __launch_bounds__(NT) mlp2_pst_kernel(Mlp2Args a, int n, unsigned* ws) {
   __shared__ int ok_lds[1];
+  __shared__ float red_lds[2][NW];
   if (n <= 0) return;   // warm-up launch (jdt_mlp2_pst n = 0): touches nothing
   int bx = blockIdx.x, by = blockIdx.y;
   xcd_column_tile(bx, by);
@@ -1727,6 +1777,7 @@ __global__ void __launch_bounds__(NT) mlp2_pst_kernel(Mlp2Args a, int n, unsigne
     if (stw && it == n - 2) stw[12] = __builtin_amdgcn_s_memrealtime();
     if (it + 1 < n) {
       pst_arrive(ws);
+      if (bx == 0 && by == 0) pst_metrics(a.running, a.M, R, red_lds);
       // the next step's bias corrections, while the other workgroups arrive
       const AdamK kn = adam_consts(*kbase, step0 + it + 1);
       R.rbc1 = kn.rbc1;
@@ -1735,7 +1786,10 @@ __global__ void __launch_bounds__(NT) mlp2_pst_kernel(Mlp2Args a, int n, unsigne
     }
     if (stw && it == n - 2) stw[13] = __builtin_amdgcn_s_memrealtime();
   }
-  if (it == n) pst_state_io<K_IN, C, KC>(a, bx, by, R, true);
+  if (it == n) {
+    if (bx == 0 && by == 0) pst_metrics(a.running, a.M, R, red_lds);
+    pst_state_io<K_IN, C, KC>(a, bx, by, R, true);
+  }
   if (stw) stw[6] = (unsigned long long)(bx + 256 * by);
   if (bx == 0 && by == 0 && threadIdx.x == 0 && it == n) {
     a.step[0] = step0 + n;

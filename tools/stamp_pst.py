@@ -79,6 +79,19 @@ def main():
                 if y == 0:
                     extra = f"   aux wave done {float((s[sel, 5] - t0[sel]).median()):5.2f}"
                 print(f"      chunk {y}: " + " ".join(f"{e:5.2f}" for e in ends) + extra)
+            ends = (s[:, 4] - s[:, 0].min()).cpu()
+            order = torch.argsort(ends, descending=True)[:12]
+            print("    slowest workgroups (end of step n-2 rel. earliest start): " + ", ".join(
+                f"wg {int(i)} tile (bx {int(tile[i]) % 256}, by {int(tile[i]) // 256}) {float(ends[i]):.2f}" for i in order))
+            bxv = (tile % 256).to(s.device)
+            for label, sel in (("column block 0", bxv == 0), ("lead (0,0)", (tile == 0).to(s.device)),
+                               ("other blocks", bxv != 0)):
+                e = [float((s[sel, k] - t0[sel]).median()) for k, _ in PHASES]
+                print(f"    {label:15s}: " + " ".join(f"{x:5.2f}" for x in e) +
+                      f"   start rel. earliest {float((t0[sel] - t0.min()).median()):5.2f}")
+            stt = (s[:, 0] - s[:, 0].min()).cpu()
+            late = torch.argsort(stt, descending=True)[:6]
+            print("    latest starters: " + ", ".join(f"wg {int(i)} +{float(stt[i]):.2f}" for i in late))
             xcd = torch.arange(224) % 8
             for x in range(8):
                 sel = (xcd == x).to(s.device)

@@ -1510,7 +1510,17 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
       float sacc = b2A[c];
 #pragma unroll
       for (int n = 0; n < 16; ++n) sacc += htA[rl][n] * w2A[n][c];
-      atomicAdd(lgn + (long)(r0 + rl) * C + c, sacc);
+      if constexpr (PST) {
+        // returning atomics: the wait for the returned value is the proof that the add was
+        // PERFORMED at the memory side (a no-return add's vmcnt acknowledgement is not), so
+        // the grid barrier's arrival orders it before every reader of the next step; without
+        // it the XCD-local release let a reader see 99 % of the parameters ~1e-6 off
+        const float old = __hip_atomic_fetch_add((gf32_t*)(lgn + (long)(r0 + rl) * C + c), sacc, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("" ::"v"(old));
+      } else {
+        atomicAdd(lgn + (long)(r0 + rl) * C + c, sacc);
+      }
     }
     // every workgroup read the step counter before the column barrier; one workgroup
     // per column block reports, the last of them advances the step and launch counters
@@ -1595,46 +1605,58 @@ __global__ void __launch_bounds__(NT) mlp2_loop_kernel(Mlp2Args a, Mlp2Loop l) {
 // XCD-hierarchical grid barrier of the persistent run-ahead launch (profiles/r5_barrier_lab.txt:
 // 1.92 us, the cost of the kernel boundary it replaces).  ws: 128-byte lines -- 0: the
 // generation count of completed barriers (advanced by the host-visible end of a launch),
-// 1: top counter, 2 + x: XCD x's arrival counter.  A workgroup adds to its XCD's counter
-// (HW_REG_XCC_ID); the XCD's last arriver (told by the value its add returned; the grid
-// is dealt round-robin over the 8 XCDs, probed: G / 8 workgroups each) adds 1 to the top
-// counter; every workgroup polls the top counter for 8 arrivals per generation.  Every
-// wave drains its stores and atomics first (vmcnt), so the step's hand-offs (sc1 / atomic
-// for cross-XCD bytes, L2 for the column block's own XCD) are complete before anyone passes.
-// A wall-clock timeout (20 ms) raises bit 8 of the error word and every workgroup leaves.
-// Arrival: every wave drains, then one lane adds to its XCD's counter (and the XCD's last
-// arriver to the top counter).  The caller may compute between arrival and the wait.
-__device__ __forceinline__ void pst_arrive(unsigned* ws) {
+// 1: top counter, 2 + x: XCD x's arrival counter, 10 + x: XCD x's release word (the grid is
+// dealt round-robin over the 8 XCDs, probed: G / 8 workgroups each).  Every wave drains its
+// stores and atomics first (vmcnt), so the step's hand-offs (sc1 / atomic for cross-XCD
+// bytes, L2 for the column block's own XCD) are complete before anyone passes.  A
+// wall-clock timeout (20 ms) raises bit 8 of the error word and every workgroup leaves.
+// Arrival: every wave drains, then one lane adds to its XCD's counter (an L2 atomic: the
+// line is only touched by that XCD's workgroups); the XCD's last arriver -- told by the
+// value its add returned -- adds 1 to the cross-XCD top counter.  The caller may compute
+// between arrival and the wait.  Returns (to lane 0) whether this workgroup arrived last.
+__device__ __forceinline__ bool pst_arrive(unsigned* ws, unsigned& xcc) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  bool last = false;
   if (threadIdx.x == 0) {
-    unsigned xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
     xcc &= 7u;
     const unsigned per = (gridDim.x * gridDim.y) / 8u;
-    // the XCD's counter line is touched only by its own workgroups: an L2 atomic (workgroup
-    // scope, as the run-ahead's column barrier); the top counter is cross-XCD (agent scope)
     const unsigned old =
         __hip_atomic_fetch_add((gu32_t*)(ws + 32 * (2 + xcc)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (old % per == per - 1)
-      __hip_atomic_fetch_add((gu32_t*)(ws + 32), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old % per == per - 1;
+    if (last) __hip_atomic_fetch_add((gu32_t*)(ws + 32), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  return last;
 }
-// Wait: one lane polls the top counter for 8 arrivals per generation (sc1 loads), bounded.
-__device__ __forceinline__ bool pst_wait(unsigned* ws, unsigned gen, int* ok_lds, unsigned* errw) {
+// bounded poll of one word until it reaches `target` (sc1 loads: never an L1 copy)
+__device__ __forceinline__ bool pst_poll(unsigned* word, unsigned target, unsigned* errw) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(word, (short)0, 4, 0x00020000);
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while ((int)((unsigned)__builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 16) - target) < 0) {
+    if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > 2000000ll) {   // 20 ms
+      atomicOr(errw + 1, 8u);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+  }
+  return true;
+}
+// Wait: each XCD's last arriver polls the top counter (8 arrivals per generation, at the
+// cross-XCD coherence point) and then releases its XCD through a word in that XCD's L2
+// (line 10 + x), which the XCD's other workgroups poll -- 8 pollers of the shared counter
+// instead of every workgroup, the rest served by their own L2.
+__device__ __forceinline__ bool pst_wait(unsigned* ws, unsigned gen, bool last, unsigned xcc, int* ok_lds,
+                                         unsigned* errw) {
   if (threadIdx.x == 0) {
-    const unsigned target = 8u * gen;
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(ws + 32, (short)0, 4, 0x00020000);
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     int ok = 1;
-    while ((int)((unsigned)__builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 16) - target) < 0) {
-      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > 2000000ll) {   // 20 ms
-        atomicOr(errw + 1, 8u);
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      asm volatile("" ::: "memory");
+    unsigned* rel = ws + 32 * (10 + xcc);
+    if (last) {
+      ok = pst_poll(ws + 32, 8u * gen, errw);
+      __hip_atomic_store((gu32_t*)rel, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      ok = pst_poll(rel, gen, errw);
     }
     ok_lds[0] = ok;
   }
@@ -1776,13 +1798,14 @@ __global__ void __launch_bounds__(NT) mlp2_pst_kernel(Mlp2Args a, int n, unsigne
                                                                         PstPos{it, n, launch0});
     if (stw && it == n - 2) stw[12] = __builtin_amdgcn_s_memrealtime();
     if (it + 1 < n) {
-      pst_arrive(ws);
+      unsigned xcc = 0u;
+      const bool last = pst_arrive(ws, xcc);
       if (bx == 0 && by == 0) pst_metrics(a.running, a.M, R, red_lds);
       // the next step's bias corrections, while the other workgroups arrive
       const AdamK kn = adam_consts(*kbase, step0 + it + 1);
       R.rbc1 = kn.rbc1;
       R.rbc2 = kn.rbc2;
-      if (!pst_wait(ws, gen0 + (unsigned)it + 1u, ok_lds, a.ztick)) break;
+      if (!pst_wait(ws, gen0 + (unsigned)it + 1u, last, xcc, ok_lds, a.ztick)) break;
     }
     if (stw && it == n - 2) stw[13] = __builtin_amdgcn_s_memrealtime();
   }
@@ -1946,7 +1969,7 @@ JDT_API int jdt_mlp2_pst_ok(int M, int H, int k_in) {
   return 0;
 }
 
-// n >= 2 run-ahead steps in one persistent launch (mlp2_pst_kernel); ws: >= 10 x 32 words,
+// n >= 2 run-ahead steps in one persistent launch (mlp2_pst_kernel); ws: >= 18 x 32 words,
 // zeroed once, never reset (monotonic barrier counters).  -3 outside the run-ahead's
 // argument envelope (the caller then launches the one-step kernel n times).  n = 0: a
 // launch that returns at once -- done once before any timed or captured use, so the

@@ -251,7 +251,7 @@ class FusedMLP2:
         self.pst_ok = (self.ahead_ok and tx is None and os.environ.get("JDT_MLP2_PST", "1") == "1"
                        and bool(_lib.lib().jdt_mlp2_pst_ok(rows, H, K)))
         if self.pst_ok:
-            self.pst_ws = torch.zeros(32 * 10, dtype=torch.int32, device=dev)
+            self.pst_ws = torch.zeros(32 * 18, dtype=torch.int32, device=dev)
         self._pst_warm = False
 
     def set_grad_stage(self, base: int, stride: int):

@@ -52,6 +52,7 @@ def _run(b, pst, opt, monkeypatch):
         gens = 6 + 6 + 2 + 1     # grid barriers: n - 1 per persistent launch (7, 7, 3, 2)
         assert int(ws[0]) == gens and int(ws[32]) == 8 * gens
         assert bool((ws[64:320].view(8, 32)[:, 0] == 28 * gens).all())   # 224 workgroups, 28 per XCD
+        assert bool((ws[320:576].view(8, 32)[:, 0] == gens).all())       # every XCD released each time
     return out
 
 
@@ -75,7 +76,8 @@ def test_persistent_run_ahead_matches_per_step_launches(rows, monkeypatch):
         assert float(d.max()) <= 1e-5 * scale, k
     torch.testing.assert_close(res["1"]["metrics"], res["0"]["metrics"], rtol=1e-5, atol=1e-3)
     sd = (res["0"]["shadow"].float() - res["1"]["shadow"].float()).abs()
-    assert float(sd.max()) <= 1e-3 * float(res["0"]["shadow"].float().abs().max())
+    # the bf16 shadow may round a last-bit fp32 difference to the neighbouring bf16: one ulp
+    assert float(sd.max()) <= 2.0 ** -7 * float(res["0"]["shadow"].float().abs().max())
 
 
 def test_persistent_run_ahead_sgd(monkeypatch):

@@ -519,8 +519,16 @@ __device__ __forceinline__ void mlp2_fwd_body(AT& a, const int bx, const int by,
       float s = (by == 0) ? bf2f(b2b) : 0.f;
 #pragma unroll
       for (int n = 0; n < 16; ++n) s += htile[rl][n] * w2s[n][c];
-      if (a.det_logits) a.det_logits[((long)by * M + row) * C + c] = s;
-      else atomicAdd(lg + (long)row * C + c, s);
+      if (a.det_logits) {
+        a.det_logits[((long)by * M + row) * C + c] = s;
+      } else if constexpr (LOOP) {
+        // read after a grid barrier in this launch: a returning add proves it was performed
+        const float old = __hip_atomic_fetch_add((gf32_t*)(lg + (long)row * C + c), s, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("" ::"v"(old));
+      } else {
+        atomicAdd(lg + (long)row * C + c, s);
+      }
     }
   }
   __syncthreads();
@@ -1413,7 +1421,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     // The column block's workgroups run on ONE XCD (xcd_column_tile), so the hand-off
     // lives in that XCD's L2: plain stores (L1 is write-through) drained by vmcnt, an
     // L2 counter (workgroup-scope atomics), loads with sc1 (never served by the L1).
-    float* const zb = a.zslab + (long)bx * NCH * (MPM / 4) * 64;
+    float* const zb = sgpr_ptr(a.zslab + (long)bx * NCH * (MPM / 4) * 64);   // scalar: a buffer resource base
     {
       const long zo = ((long)by * (MPM / 4) + w * 4 + (lane >> 4)) * 64 + (lane & 15) * 4;
       const u32x4 zv = {__float_as_uint(z[0]), __float_as_uint(z[1]), __float_as_uint(z[2]), __float_as_uint(z[3])};
@@ -1432,7 +1440,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     // (one launch of H/16 * NCH <= CU-count workgroups); monotonic counter, so no reset.
     // A wall-clock timeout (s_memrealtime) raises the error word instead of hanging.
     if (tid == 0) {
-      unsigned* cnt = a.ztick + 32 * (1 + bx);
+      unsigned* cnt = sgpr_ptr(a.ztick + 32 * (1 + bx));
       __hip_atomic_fetch_add((gu32_t*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       const unsigned target = (unsigned)NCH * (launch_no + 1u);
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -1455,7 +1463,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     const int ng = g_hi - g_lo;
     const __amdgpu_buffer_rsrc_t zr = __builtin_amdgcn_make_buffer_rsrc(zb, (short)0, NCH * (MPM / 4) * 64 * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t hr =
-        __builtin_amdgcn_make_buffer_rsrc(a.hand, (short)0, (int)((H + H * C + C) * 4), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(sgpr_ptr(a.hand), (short)0, (int)((H + H * C + C) * 4), 0x00020000);
     float zp[NCH];
     const int egc = min(eg, g_hi - 1);
 #pragma unroll
@@ -1618,13 +1626,17 @@ __device__ __forceinline__ bool pst_arrive(unsigned* ws, unsigned& xcc) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   bool last = false;
+  // read by every lane (a scalar register): set inside the lane-0 branch it would come out
+  // of the branch as a vector value, and the poll's buffer resource with it
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+  xcc &= 7u;
   if (threadIdx.x == 0) {
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
-    xcc &= 7u;
     const unsigned per = (gridDim.x * gridDim.y) / 8u;
     const unsigned old =
         __hip_atomic_fetch_add((gu32_t*)(ws + 32 * (2 + xcc)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    last = old % per == per - 1;
+    // scalar: the poll's buffer resource is chosen by it (a lane value would compile into a
+    // readfirstlane waterfall loop, tests/test_isa_waterfalls.py)
+    last = __builtin_amdgcn_readfirstlane(old % per == per - 1 ? 1u : 0u) != 0u;
     if (last) __hip_atomic_fetch_add((gu32_t*)(ws + 32), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   return last;
@@ -1651,8 +1663,8 @@ __device__ __forceinline__ bool pst_wait(unsigned* ws, unsigned gen, bool last, 
                                          unsigned* errw) {
   if (threadIdx.x == 0) {
     int ok = 1;
-    unsigned* rel = ws + 32 * (10 + xcc);
-    if (last) {
+    unsigned* rel = sgpr_ptr(ws + 32 * (10 + xcc));
+    if (__builtin_amdgcn_readfirstlane(last ? 1u : 0u)) {
       ok = pst_poll(ws + 32, 8u * gen, errw);
       __hip_atomic_store((gu32_t*)rel, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else {
@@ -1794,8 +1806,11 @@ __global__ void __launch_bounds__(NT) mlp2_pst_kernel(Mlp2Args a, int n, unsigne
     KArgs* k = kbase;
     asm volatile("" : "+s"(k));
     if (stw && it == n - 1) stw[7] = __builtin_amdgcn_s_memrealtime();
-    mlp2_bwd_body<K_IN, C, KC, false, true, false, false, false, true>(*k, bx, by, step0 + it, &R,
-                                                                        PstPos{it, n, launch0});
+    // the tile coordinates re-made scalar each step: carried across the loop they may sit
+    // in VGPRs, and the buffer resources built from them would become waterfall loops
+    mlp2_bwd_body<K_IN, C, KC, false, true, false, false, false, true>(
+        *k, __builtin_amdgcn_readfirstlane(bx), __builtin_amdgcn_readfirstlane(by), step0 + it, &R,
+        PstPos{it, n, launch0});
     if (stw && it == n - 2) stw[12] = __builtin_amdgcn_s_memrealtime();
     if (it + 1 < n) {
       unsigned xcc = 0u;

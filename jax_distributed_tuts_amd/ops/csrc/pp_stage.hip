@@ -493,7 +493,12 @@ __device__ __forceinline__ void ps_body(const PsArgs& a, const int b, char* __re
         float s = cb == 0 ? round_bf(a.phb[cc]) : 0.f;
 #pragma unroll
         for (int n = 0; n < PS_CB; ++n) s += bf2f(ht[r][n]) * whs[n][cc];
-        atomicAdd(lg + tid, s);
+        // a RETURNING add: waiting for the old value proves the add was performed at the
+        // memory side before the arrival below (a no-return add's acknowledgement does not:
+        // profiles/r5_pst_headline.txt, the persistent headline kernel's lesson)
+        const float old = __hip_atomic_fetch_add((__attribute__((address_space(1))) float*)(lg + tid), s,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("" ::"v"(old));
       }
       const unsigned t_ = ps_arrive(a.ctr, ps_ctr_lg(i, h), PS_NB / 2);
       if (tid == 0) tgt[i] = t_;

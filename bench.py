@@ -314,6 +314,15 @@ def run_autotune(args, dev, build, prepare):
     return tr, batch, desc, report
 
 
+def _mlp2_launches(eng, tx_: str, spg: int) -> str:
+    """Launches per step of the fused 2-layer engine's captured replay: the persistent
+    run-ahead kernel runs a whole replay of ``spg`` steps in one launch (ops/csrc/mlp_fused.hip
+    mlp2_pst_kernel), else one run-ahead launch per step."""
+    if getattr(eng, "pst_ok", False) and spg >= 2:
+        return f"1/{spg} (persistent run-ahead: {spg} steps per launch, grid barrier between steps{tx_})"
+    return f"1 (run-ahead mlp2_bwd{tx_})"
+
+
 def pick_steps_per_graph(steps: int, cap: int) -> int:
     """Steps per captured graph: all of them when steps <= cap (one replay, one host
     launch for the whole timed region), else the largest divisor of steps <= cap
@@ -474,7 +483,7 @@ def main():
         if getattr(tr, "_ahead", None):
             tx_ = ", gradient tiles all-reduced in the launches" if getattr(tr, "one_launch", False) else ""
             desc["step_launches"] = (f"{2 * nh - 1} (layer-0 run-ahead md_bwd{tx_})" if nh
-                                     else f"1 (run-ahead mlp2_bwd{tx_})")
+                                     else _mlp2_launches(eng, tx_, args.steps_per_graph))
         elif eng is not None:
             desc["step_launches"] = ((f"{2 * nh} (md_fwd / md_bwd per layer)" if nh else "2 (mlp2_fwd + mlp2_bwd)")
                                      + (" + xGMI all-reduce/AdamW" if ws > 1 else ""))
@@ -483,7 +492,7 @@ def main():
         tx_ = (", partials to the shard owners, sharded AdamW in the launches"
                if getattr(tr, "one_launch", False) else "")
         desc["step_launches"] = (f"{2 * nh - 1} (layer-0 run-ahead md_bwd{tx_})" if nh
-                                 else f"1 (run-ahead mlp2_bwd{tx_})")
+                                 else _mlp2_launches(tr.fused, tx_, args.steps_per_graph))
     elif args.strategy == "fsdp" and getattr(tr, "fused", None) is not None and ws > 1:
         nh = getattr(tr.fused, "nh", None)
         desc["step_launches"] = ((f"{2 * nh} (md_fwd / md_bwd per layer)" if nh else "2 (mlp2_fwd + mlp2_bwd)")

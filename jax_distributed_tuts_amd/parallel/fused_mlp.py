@@ -482,6 +482,8 @@ class AheadGraphs:
         return self.graphs[(S, primed)]
 
     def replay(self, S: int):
+        # (the persistent kernel's S steps are one graph node; launching it directly instead
+        # measured slower in bench.py's driver form, 81.6k vs 85.0k steps/s: profiles/r5_pst_headline.txt)
         self.graphs[(S, bool(self.eng.ahead_primed))].replay()
         self.eng.ahead_primed = True
         if not self._checked:

@@ -144,6 +144,9 @@ struct MdArgs {
   } while (0)
 
 struct MdAdam { float b1, b2, eps, wd, lr, gs, rbc1, rbc2; };
+#ifndef JDT_MD_PIN_ADAM
+#define JDT_MD_PIN_ADAM 1
+#endif
 typedef __attribute__((address_space(1))) unsigned gu32_md;
 
 __device__ __forceinline__ MdAdam md_adam_consts(const MdArgs& a, int step) {
@@ -588,6 +591,10 @@ __global__ void __launch_bounds__(MD_NT) __attribute__((amdgpu_waves_per_eu(WPE)
     whv = par ? whv1 : whv0;
   }
   const MdAdam ak = md_adam_consts(a, step);
+  // the bias corrections (two powf + two divides per lane) here, before the phase-1 work:
+  // left to the compiler they sink to the AdamW epilogue, on the critical path behind the
+  // MFMAs (the persistent headline kernel's lesson, profiles/r5_pst_headline.txt)
+  if (JDT_MD_PIN_ADAM) asm volatile("" ::"v"(ak.rbc1), "v"(ak.rbc2));
   const long goff = (!fo && a.stage_stride) ? (long)par * a.stage_stride : 0;   // staged bucket half
 
   MD_STAMP(1);

@@ -850,8 +850,13 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   // two waves per SIMD on the step's critical path) were computed while this workgroup
   // waited in the previous grid barrier
   AdamK ak;
-  if constexpr (PST) ak = adam_consts_pre(a, R->rbc1, R->rbc2);
-  else ak = adam_consts(a, step);
+  if constexpr (PST) {
+    ak = adam_consts_pre(a, R->rbc1, R->rbc2);
+  } else {
+    // (pinning these early, as md_bwd does, measured no gain here: 77.7-77.9k per-step
+    // headline, N = 2 shared 44.5k vs 46.8k; the compiler's placement stays)
+    ak = adam_consts(a, step);
+  }
   const long goff = (!fo && a.stage_stride) ? (long)par * a.stage_stride : 0;   // staged bucket half
 
   // ---- 1. CE from the summed logits (rounded like the bf16 Dense output) -> dlogits

@@ -168,7 +168,9 @@ __device__ __forceinline__ float md_adam(float p, float m, float v, float g, con
   g *= k.gs;
   m = k.b1 * m + (1.f - k.b1) * g;
   v = k.b2 * v + (1.f - k.b2) * g * g;
-  p = p - k.lr * ((m * k.rbc1) / (sqrtf(v * k.rbc2) + k.eps) + k.wd * p);
+  // v_rcp_f32 (1 ulp) instead of the IEEE divide's scale / fma / fixup sequence, as the
+  // 2-layer engine's AdamW (mlp_fused.hip adam_apply)
+  p = p - k.lr * ((m * k.rbc1) * __builtin_amdgcn_rcpf(sqrtf(v * k.rbc2) + k.eps) + k.wd * p);
   *pp = p; *mp = m; *vp = v;
   return p;
 }

@@ -208,7 +208,7 @@ def dp_xgmi(outdir, steps_eager=2, steps_graph=6, dp_ahead="1", num_layers=2, wi
                           "one_launch": bool(tr.one_launch), "m": st.opt_state["m"].cpu()})
 
 
-def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2, eps=1e-8, deep_fx="0"):
+def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2, eps=1e-8, deep_fx="0", hidden=512):
     """FSDP (dropout off) with the segmented xGMI gather / reduce-scatter; every rank
     saves its local shard + the partition table for reassembly in the parent.
     num_layers=4: the square 512 x 512 hidden weights are sharded along dim 1 (the
@@ -227,8 +227,8 @@ def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2, eps=1e-8, deep_fx="0"):
     dev = D.device()
     cfg = fsdp_config()
     mesh = D.Mesh({"data": D.world_size()})
-    st = init_fsdp(Classifier(num_layers=num_layers, dropout_rate=0.0), adamw(1e-3, eps=eps), 69, dev, mesh, "data",
-                   16)
+    st = init_fsdp(Classifier(hidden_size=hidden, num_layers=num_layers, dropout_rate=0.0), adamw(1e-3, eps=eps), 69,
+                   dev, mesh, "data", 16)
     b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
     b = Batch(b.inputs.to(dev), b.labels.to(dev))
     tr = FSDPTrainer(st, mesh, FSDPConfig(4, 16, "data", gather_once=True, scatter_once=True, fused_kernels=fused,

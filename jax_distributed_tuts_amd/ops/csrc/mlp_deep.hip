@@ -596,8 +596,10 @@ __global__ void __launch_bounds__(MD_NT) __attribute__((amdgpu_waves_per_eu(WPE)
   // the bias corrections (two powf + two divides per lane) here, before the phase-1 work:
   // left to the compiler they sink to the AdamW epilogue, on the critical path behind the
   // MFMAs (the persistent headline kernel's lesson, profiles/r5_pst_headline.txt)
-  // (JDT_MD_PIN_ADAM: 1 every layer, 2 only where the step counter is the first load (!TOP))
-  if (JDT_MD_PIN_ADAM == 1 || (JDT_MD_PIN_ADAM == 2 && WN)) asm volatile("" ::"v"(ak.rbc1), "v"(ak.rbc2));
+  // (JDT_MD_PIN_ADAM: 1 every layer, 2 only where the step counter is the first load (!TOP)).
+  // Not in the N > 1 exchange variants: two more live registers put the top layer's TX
+  // variant at 133 VGPRs, one workgroup per CU, and 2 ranks' grids no longer co-resident
+  if (!TX && (JDT_MD_PIN_ADAM == 1 || (JDT_MD_PIN_ADAM == 2 && WN))) asm volatile("" ::"v"(ak.rbc1), "v"(ak.rbc2));
   const long goff = (!fo && a.stage_stride) ? (long)par * a.stage_stride : 0;   // staged bucket half
 
   MD_STAMP(1);

@@ -382,7 +382,11 @@ def main():
     LCH.check_world(args.gpus)
     ws = D.world_size()
     if args.steps_per_graph is None:
-        args.steps_per_graph = pick_steps_per_graph(args.steps, 200 if args.strategy == "dp" else 50)
+        # the 2-layer DP / FSDP replay is ONE persistent launch whatever its length; the deep and
+        # pipeline graphs hold every step's launches, and 50-step ones measured 0.8 % faster than
+        # 150-step ones for the 4-layer step (24.10-24.15k vs 23.90-23.95k, session r5s42)
+        two_layer = args.strategy in ("dp", "fsdp") and args.num_layers == 2
+        args.steps_per_graph = pick_steps_per_graph(args.steps, 200 if two_layer else 50)
     build = {"dp": build_dp, "fsdp": build_fsdp, "pp": build_pp}[args.strategy]
     on_gpu = dev.type == "cuda"
     sync = (lambda: torch.cuda.synchronize()) if on_gpu else (lambda: None)

@@ -4,10 +4,16 @@ XCD-hierarchical grid barrier between steps, against the same steps as n run-ahe
 launches (JDT_MLP2_PST=0) -- through the multi-step graphs (cold, then primed), 1-step
 graphs, eager run-ahead calls and two-launch steps mixed in (logits accumulators, step,
 launch and barrier counters stay consistent).  Same arithmetic in the same order except the
-forward's fp32 logits atomics (arrival order), so the two agree to that rounding: measured
-bit-identical at 32 / 64 / 128 rows (max |dp| 1.3e-7 in one earlier run).  The bound is
-~100 ulp of the parameters -- far below what one step on stale logits, a stale W2 shadow
-or a lost tile would do (those move a parameter by ~lr = 1e-3)."""
+forward's fp32 logits atomics (32 column-block partials per logit, summed in arrival order
+in BOTH forms), so the two agree to that rounding: usually bit-identical at 32 / 64 / 128
+rows, but a different arrival order in either run perturbs a logit by ~1 ulp and AdamW
+carries it on (m / sqrt(v) normalises the perturbation, it does not shrink it): one run
+of 128 rows gave 99 % of the parameters different, median tiny, max |dp| 7.3e-6 = 6e-5 x
+scale.  So the bounds are on the bulk: median |d| <= 1e-5 x scale and the 99.9th percentile
+<= 1e-4 x scale.  A lost or doubly applied gradient tile (1,792 of 401k parameters moved
+by ~lr = 1e-3) breaks the percentile bound; a step on stale logits, a stale W2 shadow or a
+missed barrier moves most parameters by ~1e-5 .. 1e-3 and breaks the median bound.  SGD
+has no normalisation: its rounding stays rounding, and its bound stays on the max."""
 import pytest
 import torch
 
@@ -68,12 +74,14 @@ def test_persistent_run_ahead_matches_per_step_launches(rows, monkeypatch):
     dm = (res["0"]["metrics"] - res["1"]["metrics"]).abs()
     print(f"[pst rows {rows}] metrics {res['0']['metrics'].tolist()} |d| {dm.tolist()}")
     for k in ("p", "m", "v"):
-        d = (res["0"][k] - res["1"][k]).abs()
+        d = (res["0"][k] - res["1"][k]).abs().flatten().float().cpu()
         scale = float(res["0"][k].abs().max())
-        print(f"[pst rows {rows}] {k}: max |d| {float(d.max()):.3e} (scale {scale:.3e}), "
-              f"frac > 1e-5 scale {float((d > 1e-5 * max(scale, 1.0)).float().mean()):.2e}, "
-              f"frac != {float((d > 0).float().mean()):.2e}")
-        assert float(d.max()) <= 1e-5 * scale, k
+        ds = d.sort().values
+        q50, q999 = float(ds[len(ds) // 2]), float(ds[int(0.999 * (len(ds) - 1))])
+        print(f"[pst rows {rows}] {k}: max |d| {float(ds[-1]):.3e} (scale {scale:.3e}), median {q50:.3e}, "
+              f"p99.9 {q999:.3e}, frac != {float((d > 0).float().mean()):.2e}")
+        assert q50 <= 1e-5 * scale, (k, "median", q50)
+        assert q999 <= 1e-4 * scale, (k, "p99.9", q999)
     torch.testing.assert_close(res["1"]["metrics"], res["0"]["metrics"], rtol=1e-5, atol=1e-3)
     sd = (res["0"]["shadow"].float() - res["1"]["shadow"].float()).abs()
     # the bf16 shadow may round a last-bit fp32 difference to the neighbouring bf16: one ulp

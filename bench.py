@@ -95,11 +95,16 @@ def build_pp(args, dev):
     from pipeline_parallel import build_mlp_pipeline
     from jax_distributed_tuts_amd.parallel.dp import shard_batch
     from jax_distributed_tuts_amd.utils.config import dp_config
-    from jax_distributed_tuts_amd.utils.train_state import Batch
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
 
     cfg = dp_config()
     ws = D.world_size()
     dp = args.dp
+    # autotune's validation probes: AdamW(eps = 10), and no dropout -- a different
+    # microbatch count draws a different dropout stream, so only the probe without it
+    # compares schedules value for value (utils/autotune.py)
+    eps = getattr(args, "adam_eps", None)
+    probe = eps is not None
     mesh = Mesh({"data": dp, "pipe": ws // dp})
     if args.microbatches is None:
         from jax_distributed_tuts_amd.parallel.pipeline import default_microbatches
@@ -110,14 +115,17 @@ def build_pp(args, dev):
 
         tr, lm_cfg = build_lm_pipeline(mesh, dev, num_microbatches=args.microbatches, comm=args.comm,
                                        merge_single_stage=args.merge_microbatches,
-                                       layer_major_single_stage=not args.microbatch_passes)
+                                       layer_major_single_stage=not args.microbatch_passes,
+                                       tx=adamw(3e-4, eps=eps) if probe else None)
         batch = shard_batch(lm_batch(lm_cfg, global_batch=args.lm_batch, seed=1), mesh, "data")
         desc = {"model": f"transformer LM {lm_cfg.n_layers}L d{lm_cfg.d_model} h{lm_cfg.n_heads} "
                          f"ff{lm_cfg.d_ff} V{lm_cfg.vocab_size}", "global_batch": args.lm_batch,
                 "seq_len": lm_cfg.seq_len, "tokens_per_step": args.lm_batch * lm_cfg.seq_len}
     else:
         tr = build_mlp_pipeline(cfg, mesh, dev, args.hidden_layers, num_microbatches=args.microbatches,
-                                comm=args.comm, merge_single_stage=args.merge_microbatches)
+                                comm=args.comm, merge_single_stage=args.merge_microbatches,
+                                dropout_rate=0.0 if probe else None,
+                                tx=adamw(cfg.optimizer.learning_rate, eps=eps) if probe else None)
         batch = shard_batch(synthetic_batch(cfg, cfg.seed + 1), mesh, "data")
         desc = {"model": f"MLP 784-512x{args.hidden_layers}-10 GPipe", "global_batch": cfg.data.batch_size,
                 "seq_len": None}
@@ -238,30 +246,33 @@ def autotune_candidates(args, ws: int):
         return []
     if args.strategy == "pp":
         S = ws // args.dp
+        # data-axis replicas of a stage: bit-identical (hybrid DP x PP)
+        rep = dict(replicated=args.dp > 1, group_of=lambda tr: tr.mesh.group("data"))
         stages = []
         if args.microbatches is None and S > 1:
             rows = (args.lm_batch if args.model == "transformer" else 128) // args.dp
             ns = [n for n in (2, 4, 8) if rows % n == 0 and (args.model == "transformer" or rows // n >= 4)]
-            stages.append([Candidate(f"microbatches={n}", {}, reference=(n == 2), args={"microbatches": n})
+            stages.append([Candidate(f"microbatches={n}", {}, reference=(n == 2), args={"microbatches": n}, **rep)
                            for n in ns])
         if S > 1 and args.model == "mlp" and args.dp == 1:
             # one persistent launch per stage step (parallel/pp_kernel.py) vs per-tick launches
             stages.append([Candidate("stage-kernel=1", {"JDT_PP_KERNEL": "1"},
                                      engaged=lambda tr: getattr(tr, "pp_kernel", None) is not None),
                            Candidate("stage-kernel=0", {"JDT_PP_KERNEL": "0"}, reference=True)])
-        # schedules on concurrent streams: only with a GPU per rank.  Ranks sharing one GPU
-        # time-share its hardware queues; a process that once opened extra queues keeps
-        # them, and every later build of the job then runs 20-50x slower (session 3 of
-        # round 5: GPipe-8 1.9 -> 90 ms/step after a stage-streams candidate was built)
         from jax_distributed_tuts_amd.runtime.dist import ranks_per_gpu
 
         own_gpu = ranks_per_gpu() == 1
-        if S > 1 and own_gpu:
-            stages.append([Candidate("stage-streams=0", {"JDT_PP_STREAMS": "0"}, reference=True),
-                           Candidate("stage-streams=1", {"JDT_PP_STREAMS": "1"})])
         if S > 1 and args.dp > 1 and own_gpu:
-            stages.append([Candidate("overlap-sync=0", {"JDT_PP_OVERLAP_SYNC": "0"}, reference=True),
-                           Candidate("overlap-sync=1", {"JDT_PP_OVERLAP_SYNC": "1"})])
+            stages.append([Candidate("overlap-sync=0", {"JDT_PP_OVERLAP_SYNC": "0"}, reference=True, **rep),
+                           Candidate("overlap-sync=1", {"JDT_PP_OVERLAP_SYNC": "1"}, **rep)])
+        # schedules on concurrent streams: only with a GPU per rank, and LAST (stage and
+        # candidate): a process that once opened extra hardware queues keeps them, and on a
+        # time-shared GPU every later build then ran 20-50x slower (round 5: GPipe-8 1.9 ->
+        # 90 ms/step after a stage-streams candidate was built) -- the autotune re-times the
+        # reference after it and records "contaminated"
+        if S > 1 and own_gpu:
+            stages.append([Candidate("stage-streams=0", {"JDT_PP_STREAMS": "0"}, reference=True, **rep),
+                           Candidate("stage-streams=1", {"JDT_PP_STREAMS": "1"}, contaminates=True, **rep)])
         return [st for st in stages if len(st) > 1]
     return []
 
@@ -294,8 +305,9 @@ def run_autotune(args, dev, build, prepare):
             t.bench_desc = d
             return t, b
 
-        validate = args.strategy in ("dp", "fsdp")
-        rep, t, b = AT.run(cands, build_one, prepare, dev, validate=validate, steps=steps, log=log)
+        # every candidate is value-checked against its stage's reference form (PP too: the
+        # stage kernel, microbatch counts and stream schedules against per-tick launches)
+        rep, t, b = AT.run(cands, build_one, prepare, dev, validate=True, steps=steps, log=log)
         tables.append(rep)
         chosen_env.update(rep["env"])
         chosen_args.update(rep.get("args", {}))
@@ -311,6 +323,8 @@ def run_autotune(args, dev, build, prepare):
         bad = [r for t_ in tables for r in t_["candidates"] if r.get("valid") is False]
         if bad and args.strategy in ("dp", "fsdp"):
             desc["one_launch_fallback"] = "; ".join(f"{r['name']}: {r.get('reason')}" for r in bad)
+        if bad and args.strategy == "pp":
+            desc["pp_rejected"] = "; ".join(f"{r['name']}: {r.get('reason')}" for r in bad)
     return tr, batch, desc, report
 
 

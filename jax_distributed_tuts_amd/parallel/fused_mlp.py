@@ -13,7 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import c_float, c_int, c_ulonglong, c_void_p
+from ctypes import c_float, c_int, c_longlong, c_ulonglong, c_void_p
 from typing import Optional
 
 import torch
@@ -88,7 +88,8 @@ _lib.declare("jdt_mlp2_loop", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_void_p,
 
 _lib.declare("jdt_mlp2_loop_ok", c_int, [c_int, c_int])
 _lib.declare("jdt_mlp2_pst_ok", c_int, [c_int, c_int, c_int])
-_lib.declare("jdt_mlp2_pst", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_void_p, c_void_p])
+_lib.declare("jdt_mlp2_pst", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_void_p, c_longlong, c_void_p])
+PST_BARRIER_TIMEOUT_S = 0.02   # persistent run-ahead grid barrier bound (x runtime.dist.spin_timeout_s sharing)
 
 LOOP_BARRIER_TIMEOUT_TICKS = 20_000_000   # 0.2 s of s_memrealtime (100 MHz) per grid barrier
 
@@ -251,7 +252,12 @@ class FusedMLP2:
         self.pst_ok = (self.ahead_ok and tx is None and os.environ.get("JDT_MLP2_PST", "1") == "1"
                        and bool(_lib.lib().jdt_mlp2_pst_ok(rows, H, K)))
         if self.pst_ok:
+            from ..runtime.dist import spin_timeout_s
+
             self.pst_ws = torch.zeros(32 * 18, dtype=torch.int32, device=dev)
+            # s_memrealtime ticks (100 MHz); grows with the ranks sharing the GPU like the
+            # other in-kernel waits
+            self.pst_timeout = int(spin_timeout_s(PST_BARRIER_TIMEOUT_S) * 1e8)
         self._pst_warm = False
 
     def set_grad_stage(self, base: int, stride: int):
@@ -357,7 +363,8 @@ class FusedMLP2:
     def run_ahead(self, batch, n: int, prologue: bool = True):
         """n complete training steps as n run-ahead backward launches, launch i = step
         i's CE, backward and AdamW plus step i+1's forward (n >= 2 with ``pst_ok``: ONE
-        persistent launch of the n steps, bit-identical); ``prologue`` first runs the
+        persistent launch of the n steps -- equal to the per-step launches up to the
+        arrival order of the logits' fp32 atomics); ``prologue`` first runs the
         first step's forward (``mlp2_fwd``), needed unless the previous launch on this
         engine was a run-ahead backward (``ahead_primed``: step t's G1, H1 and logits
         (t % 3) are then already there).  Same maths as n two-launch steps except the
@@ -380,8 +387,8 @@ class FusedMLP2:
         if self.pst_ok and n >= 2:
             if not torch.cuda.is_current_stream_capturing():
                 self.pst_warm()
-            _lib.check(L.jdt_mlp2_pst(ctypes.byref(self._ahead_args), int(n), self.K, self.pst_ws.data_ptr(), s),
-                       "mlp2_pst")
+            _lib.check(L.jdt_mlp2_pst(ctypes.byref(self._ahead_args), int(n), self.K, self.pst_ws.data_ptr(),
+                                      self.pst_timeout, s), "mlp2_pst")
         else:
             for _ in range(n):
                 _lib.check(L.jdt_mlp2(ctypes.byref(self._ahead_args), 2, self.K, 10, s), "mlp2_bwd_ahead")
@@ -402,7 +409,7 @@ class FusedMLP2:
         its first-dispatch setup (private segment) lands here, not in a timed replay."""
         if self.pst_ok and not self._pst_warm and self._ahead_args is not None:
             _lib.check(_lib.lib().jdt_mlp2_pst(ctypes.byref(self._ahead_args), 0, self.K, self.pst_ws.data_ptr(),
-                                               _lib.stream_ptr()), "mlp2_pst warm")
+                                               self.pst_timeout, _lib.stream_ptr()), "mlp2_pst warm")
             self._pst_warm = True
 
     def run_loop(self, batch, n: int, stamps: Optional[torch.Tensor] = None) -> bool:
@@ -443,6 +450,11 @@ class FusedMLP2:
         if self.loop_error():
             raise RuntimeError("mlp2_loop_kernel: a grid barrier timed out (not every workgroup was resident)")
         if self.ahead_ok and int(self.ztick[1].item()) != 0:
+            if self.pst_ok and int(self.ztick[1].item()) & 8:
+                # a persistent launch left its grid barrier early: the XCD / top counters
+                # moved without the generation word, so every later launch would be out of
+                # step -- re-zero them (the engine stays unusable until the error is cleared)
+                self.pst_ws.zero_()
             raise RuntimeError("mlp2_bwd run-ahead: tile map, column barrier or tile exchange failed (error "
                                f"word {int(self.ztick[1].item())}: 1 tile map, 2 column barrier, 4 exchange "
                                "timeout, 8 persistent grid barrier); results invalid")
@@ -827,6 +839,11 @@ class FusedMLPDeep:
             raise RuntimeError("md_bwd dZ split: a column-block barrier timed out (not every workgroup "
                                "resident); results invalid -- rerun with JDT_MD_DZS=0")
         if self.ahead_ok and int(self.ztick[1].item()) != 0:
+            if self.pst_ok and int(self.ztick[1].item()) & 8:
+                # a persistent launch left its grid barrier early: the XCD / top counters
+                # moved without the generation word, so every later launch would be out of
+                # step -- re-zero them (the engine stays unusable until the error is cleared)
+                self.pst_ws.zero_()
             raise RuntimeError("md_bwd run-ahead: tile map or column barrier failed (error word "
                                f"{int(self.ztick[1].item())}); results invalid")
         if self.tx is not None and self.tx.error():

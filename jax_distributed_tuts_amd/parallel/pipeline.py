@@ -242,6 +242,7 @@ class GPipeTrainer:
         self._deep_tried = False
         self.pp_kernel = None          # the in-kernel GPipe step (parallel/pp_kernel.py)
         self._pp_kernel_tried = False
+        self._pp_kernel_stale = False  # a checkpoint restore moved the step counter: rebuild it
         from ..utils.checkpoint import bind_trainer
 
         bind_trainer(state, self)
@@ -318,10 +319,28 @@ class GPipeTrainer:
         return f"data:{dp},pipe:{pipe}"
 
     # ------------------------------------------------------------------ step
+    def _drop_stale_pp_kernel(self):
+        """After a restore (``invalidate``): the stage engine's in-kernel waits pass once a
+        flag is >= the step epoch, and its inbox / weight-box / counter words still hold the
+        epochs of steps the restore rolled back -- every wait would pass at once on stale
+        hand-offs.  Drop it so the next step rebuilds it from zeroed buffers.  Collective
+        (every rank restores, then steps or captures); quiesce first so no peer still
+        writes into the old inboxes.  Never called inside a stream capture."""
+        if not self._pp_kernel_stale:
+            return
+        from ..runtime.dist import quiesce
+
+        self._pp_kernel_stale = False
+        quiesce(self.dev)
+        self.pp_kernel.close()
+        self.pp_kernel = None
+        self._pp_kernel_tried = False
+
     def _pp_kernel_engine(self, mb: int, seed: int):
         """The whole stage step as one persistent launch (parallel/pp_kernel.py), when
         every stage of the pipe axis can run it (collective on first use); with a pipe
         axis of size 1, the one-GPU chain: every layer of the MLP a stage of one launch."""
+        self._drop_stale_pp_kernel()
         if not self._pp_kernel_tried:
             self._pp_kernel_tried = True
             if self.S == 1 and self.dev.type == "cuda":
@@ -347,7 +366,7 @@ class GPipeTrainer:
         seed = rng & 0xFFFFFFFF
         if self._pp_kernel_engine(mb, seed) is not None:
             # every tick and hand-off in ONE launch, then the AdamW launch (csrc/pp_stage.hip)
-            self.pp_kernel.step(batch)
+            self.pp_kernel.step(batch, seed)
             return
         self._setup_p2p(mb)
         if self.S == 1:
@@ -634,6 +653,8 @@ class GPipeTrainer:
         self._engine_tried = False
         self.deep_engine = None
         self._deep_tried = False
+        if self.pp_kernel is not None:
+            self._pp_kernel_stale = True   # rebuilt (zeroed hand-off flags, new seed) at the next step
 
     def _single_stage_engine(self, rows: int, mb: int):
         """One stage holding the whole MLP (pipe axis of size 1): GPipe's fill/drain
@@ -809,6 +830,7 @@ class GPipeTrainer:
         if not self.capturable:
             raise RuntimeError("pipeline step is not capturable (host-driven collectives)")
         self._static = batch
+        self._drop_stale_pp_kernel()   # a restore since the last step: rebuild outside the capture
 
         def body():
             self._compute(batch)

@@ -206,8 +206,10 @@ class PPStageKernel:
         self.stamps = stamps
         self.args.stamps = stamps.data_ptr() if stamps is not None else None
 
-    def step(self, batch):
+    def step(self, batch, seed: Optional[int] = None):
         a = self.args
+        if seed is not None:
+            a.seed = int(seed) & 0xFFFFFFFF   # the trainer's dropout stream (changes on restore)
         key = (batch.inputs.data_ptr(), batch.labels.data_ptr())
         if key != self._key:
             if self.first:
@@ -332,7 +334,10 @@ class PPChainKernel:
         self._key = None
         self.ok = True
 
-    def step(self, batch):
+    def step(self, batch, seed: Optional[int] = None):
+        if seed is not None:
+            for i in range(self.L):
+                self.args[i].seed = int(seed) & 0xFFFFFFFF
         key = (batch.inputs.data_ptr(), batch.labels.data_ptr())
         if key != self._key:
             assert batch.inputs.dtype == torch.float32 and batch.inputs.is_contiguous()

@@ -39,6 +39,7 @@ REL_TOL = 1e-2          # whole master delta / m / v
 BLOCK_TOL = 0.05        # worst 16 x 16 block of the largest weight's master delta
 VALIDATE_STEPS = 3
 PROBE_EPS = 10.0
+CONTAMINATION = 1.10    # reference re-timed after a state-changing candidate: slower by > 10 %
 
 
 @dataclass
@@ -50,6 +51,15 @@ class Candidate:
     args: Dict = field(default_factory=dict)   # bench argument overrides (PP microbatches ...)
     # trainer attribute telling whether the form this candidate asks for actually engaged
     engaged: Callable = field(default=lambda tr: True)
+    # replicated over a sub-group only (hybrid DP x PP: the data axis of each stage);
+    # group_of(tr) -> process group, None = the world
+    group_of: Optional[Callable] = None
+    # building it may change process state for everything built after it (a schedule on
+    # concurrent streams opens extra hardware queues that the process keeps: round 5,
+    # GPipe-8 1.9 -> 90 ms per step after a stage-streams candidate was built).  Such
+    # candidates are validated and timed LAST, the reference form is re-timed after them,
+    # and the table says "contaminated" when it slowed by more than CONTAMINATION
+    contaminates: bool = False
 
 
 @contextlib.contextmanager
@@ -143,13 +153,14 @@ def compare(init: Dict, got: Dict, ref: Dict) -> Dict[str, float]:
     return out
 
 
-def replicated_bitwise(t: torch.Tensor, dev) -> bool:
-    """``t`` identical on every rank (collective): elementwise MAX == MIN."""
+def replicated_bitwise(t: torch.Tensor, dev, group=None) -> bool:
+    """``t`` identical on every rank of ``group`` (default: the world), elementwise
+    MAX == MIN; the verdict is agreed over the world (collective on every rank)."""
     on = dev if D.backend() == "nccl" else "cpu"
     hi, lo = t.to(on).clone(), t.to(on).clone()
-    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
-    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-    return bool(torch.equal(hi, lo))
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    return _all(bool(torch.equal(hi, lo)), dev)
 
 
 def step_error(tr) -> Optional[str]:
@@ -167,6 +178,9 @@ def step_error(tr) -> Optional[str]:
     p2p = getattr(tr, "p2p", None)
     if p2p is not None and p2p.error():
         return "pipeline receive timed out"
+    pk = getattr(tr, "pp_kernel", None)
+    if pk is not None and pk.error():
+        return "pipeline stage kernel wait timed out"
     return None
 
 
@@ -206,6 +220,74 @@ def time_candidate(tr, batch, steps: int, dev) -> float:
     return _max(dt / steps * 1e6, dev)
 
 
+def _validate(c: Candidate, build: Callable, dev, validate: bool, ref: Optional[Dict], row: Dict):
+    """Build ``c`` under its env, run the probe steps and fill ``row`` (valid / engaged /
+    err / reason).  Returns this candidate's (init, state) snapshots (the reference form's
+    become ``ref``)."""
+    if not validate:   # timing only (the in-kernel error words are still checked)
+        row["valid"] = True
+        return None
+    # the env stays in force through the eager steps: engines are built (and read their
+    # switches) on the first step, not at construction
+    with env_override(c.env):
+        tr, batch = build(PROBE_EPS, c)
+        try:
+            init = snapshot(tr)
+            for _ in range(VALIDATE_STEPS):
+                tr.step(batch)
+            _sync(dev)
+            # the form asked for must have engaged on every rank (its engine is built on
+            # the first step); otherwise it is the reference form under another name
+            eng = _all(bool(c.engaged(tr)), dev)
+            row["engaged"] = eng
+            err = step_error(tr)
+            if err is None and not c.reference and os.environ.get("JDT_BENCH_FAKE_TX_ERROR", "-1") == str(D.rank()):
+                err = "tile exchange wait timed out (injected: JDT_BENCH_FAKE_TX_ERROR)"
+            if not _all(err is None, dev):
+                row["valid"] = False
+                row["reason"] = _first_reason(err)
+                return None
+            if not eng and not c.reference:
+                row["valid"] = None
+                row["reason"] = "not engaged (the trainer fell back to the reference form)"
+                return None
+            if os.environ.get("JDT_BENCH_FAKE_TX_CORRUPT", "-1") == str(D.rank()) and not c.reference:
+                _inject_corruption(tr)
+            got = snapshot(tr)
+            if c.reference:
+                row["valid"] = True
+            else:
+                e = compare(ref["init"], got, ref["got"])
+                worst = {k: _max(v, dev) for k, v in e.items()}
+                row["err"] = {k: float(f"{v:.3g}") for k, v in worst.items()}
+                ok = all(worst[k] <= REL_TOL for k in ("p", "m", "v") if k in worst)
+                ok = ok and worst.get("block", 0.0) <= BLOCK_TOL
+                row["valid"] = _all(ok, dev)
+                if not row["valid"]:
+                    row["reason"] = "state differs from the reference form"
+            if row["valid"] and c.replicated and not c.reference:
+                # DP (or a hybrid's data axis): the masters are replicated -- bit-identical
+                grp = c.group_of(tr) if c.group_of is not None else None
+                rep = replicated_bitwise(got["p"], dev, grp)
+                row["replicated"] = rep
+                if not rep:
+                    row["valid"] = False
+                    row["reason"] = "masters not bit-identical across the replicas"
+            return {"init": init, "got": got}
+        finally:
+            close_trainer(tr)
+
+
+def _build_timed(c: Candidate, build: Callable, prepare: Callable, steps: int):
+    with env_override(c.env):
+        tr, batch = build(None, c)
+        for _ in range(2):
+            tr.step(batch)
+        prepare(tr, batch)
+        tr.run_steps(batch, min(steps, 20)) if hasattr(tr, "run_steps") else tr.step(batch)
+    return tr, batch
+
+
 def run(cands: List[Candidate], build: Callable, prepare: Callable, dev, validate: bool = True,
         steps: int = 100, rounds: int = 3, log: Callable = print):
     """Validate and time ``cands`` (collective: every rank calls it with the same list).
@@ -216,114 +298,105 @@ def run(cands: List[Candidate], build: Callable, prepare: Callable, dev, validat
     trainer, batch): the report {"candidates": [...], "choice": name, "env": {...},
     "args": {...}} and the winner's trainer -- built with the run's own optimizer,
     stepped, captured and replayed, ready for the timed run (None if no candidate could
-    be timed; the caller then builds the reference form itself)."""
+    be timed, or the reference form itself failed: the caller then builds the reference
+    form itself).
+
+    Candidates marked ``contaminates`` go last: validated and built after every other
+    candidate was timed, then timed in alternation with all of them again; if the
+    reference form is more than CONTAMINATION slower in that second phase the report
+    says so, and the choice uses the second phase's times (the process the timed run
+    will use is the contaminated one)."""
     table = []
-    live = []
-    ref_state = init_state = None
-    # the reference form first: every other candidate is compared with it
-    order = sorted(cands, key=lambda c: not c.reference)
+    ref_snap = None
+    order = sorted(cands, key=lambda c: (c.contaminates, not c.reference))   # reference first
+    rows = {}
     for c in order:
         row = {"name": c.name, "env": dict(c.env)}
         if c.args:
             row["args"] = dict(c.args)
         table.append(row)
-        if not validate:   # timing only (the in-kernel error words are still checked)
-            row["valid"] = True
+        rows[c.name] = row
+    ref_c = next((c for c in order if c.reference), order[0])
+
+    def no_choice(reason):
+        return ({"candidates": table, "choice": ref_c.name, "env": dict(ref_c.env), "args": dict(ref_c.args),
+                 "reason": reason}, None, None)
+
+    early = [c for c in order if not c.contaminates]
+    late = [c for c in order if c.contaminates]
+    live = []
+    for c in early:
+        snap = _validate(c, build, dev, validate, ref_snap, rows[c.name])
+        if c.reference:
+            ref_snap = snap
+            if validate and not rows[c.name]["valid"]:
+                # nothing to compare against: validate nothing, time nothing
+                for c2 in order:
+                    if c2 is not c:
+                        rows[c2.name]["valid"] = None
+                        rows[c2.name]["reason"] = "not validated (the reference form failed)"
+                return no_choice(f"reference form failed: {rows[c.name].get('reason')}")
+        if rows[c.name]["valid"]:
             live.append(c)
-            continue
-        # the env stays in force through the eager steps: engines are built (and read their
-        # switches) on the first step, not at construction
-        with env_override(c.env):
-            tr, batch = build(PROBE_EPS if validate else None, c)
-            try:
-                init = snapshot(tr) if validate else None
-                for i in range(VALIDATE_STEPS):
-                    tr.step(batch)
-                _sync(dev)
-                # the form asked for must have engaged on every rank (its engine is built on
-                # the first step); otherwise it is the reference form under another name
-                eng = _all(bool(c.engaged(tr)), dev)
-                row["engaged"] = eng
-                err = step_error(tr)
-                if err is None and not c.reference and os.environ.get("JDT_BENCH_FAKE_TX_ERROR", "-1") == str(D.rank()):
-                    err = "tile exchange wait timed out (injected: JDT_BENCH_FAKE_TX_ERROR)"
-                bad = not _all(err is None, dev)
-                if bad:
-                    row["valid"] = False
-                    row["reason"] = _first_reason(err)
-                elif not eng and not c.reference:
-                    row["valid"] = None
-                    row["reason"] = "not engaged (the trainer fell back to the reference form)"
-                elif validate:
-                    if os.environ.get("JDT_BENCH_FAKE_TX_CORRUPT", "-1") == str(D.rank()) and not c.reference:
-                        _inject_corruption(tr)
-                    got = snapshot(tr)
-                    if c.reference:
-                        ref_state, init_state = got, init
-                        row["valid"] = True
-                    else:
-                        e = compare(init_state, got, ref_state)
-                        worst = {k: _max(v, dev) for k, v in e.items()}
-                        row["err"] = {k: float(f"{v:.3g}") for k, v in worst.items()}
-                        ok = all(worst[k] <= REL_TOL for k in ("p", "m", "v") if k in worst)
-                        ok = ok and worst.get("block", 0.0) <= BLOCK_TOL
-                        row["valid"] = _all(ok, dev)
-                        if not row["valid"]:
-                            row["reason"] = "state differs from the reference form"
-                    if row["valid"] and c.replicated and not c.reference:
-                        # DP: the masters are replicated -- bit-identical on every rank
-                        rep = replicated_bitwise(got["p"], dev)
-                        row["replicated"] = rep
-                        if not rep:
-                            row["valid"] = False
-                            row["reason"] = "masters not bit-identical across ranks"
-                else:
-                    row["valid"] = True
-            finally:
-                close_trainer(tr)
-        if row["valid"]:
-            live.append(c)
-    # timing: each surviving candidate built with the run's own optimizer, captured,
-    # replayed in alternation
     built = []
-    times = {}
+    times: Dict[str, List[float]] = {}
+    after: Dict[str, List[float]] = {}
     keep = None
+    contaminated = False
     try:
         for c in live:
-            with env_override(c.env):
-                tr, batch = build(None, c)
-                for _ in range(2):
-                    tr.step(batch)
-                prepare(tr, batch)
-                tr.run_steps(batch, min(steps, 20)) if hasattr(tr, "run_steps") else tr.step(batch)
+            tr, batch = _build_timed(c, build, prepare, steps)
             built.append((c, tr, batch))
         times = {c.name: [] for c, _, _ in built}
         for _ in range(rounds if len(built) > 1 else 1):
             for c, tr, batch in built:
                 times[c.name].append(time_candidate(tr, batch, steps, dev))
+        late_live = []
+        for c in late:
+            _validate(c, build, dev, validate, ref_snap, rows[c.name])
+            if rows[c.name]["valid"]:
+                late_live.append(c)
+        if late_live:
+            for c in late_live:
+                tr, batch = _build_timed(c, build, prepare, steps)
+                built.append((c, tr, batch))
+            after = {c.name: [] for c, _, _ in built}
+            for _ in range(rounds):
+                for c, tr, batch in built:
+                    after[c.name].append(time_candidate(tr, batch, steps, dev))
+            if ref_c.name in times and times[ref_c.name]:
+                pre, post = min(times[ref_c.name]), min(after[ref_c.name])
+                contaminated = post > CONTAMINATION * pre
+                rows[ref_c.name]["us_per_step_after_late"] = round(post, 2)
         for c, tr, _ in built:
             err = step_error(tr)
             if not _all(err is None, dev):
-                times[c.name] = [float("inf")]
-                r = next(r for r in table if r["name"] == c.name)
-                r["valid"] = False
-                r["reason"] = f"timed replays: {_first_reason(err)}"
-        for r in table:
-            if r["name"] in times:
-                r["us_per_step"] = round(min(times[r["name"]]), 2)
-        ok = [r for r in table if r.get("us_per_step") not in (None, float("inf"))]
+                times[c.name] = after[c.name] = [float("inf")]
+                rows[c.name]["valid"] = False
+                rows[c.name]["reason"] = f"timed replays: {_first_reason(err)}"
+        use = after if contaminated else {**{k: v for k, v in times.items()}, **{k: v for k, v in after.items()
+                                                                                 if k not in times}}
+        for c, _, _ in built:
+            r = rows[c.name]
+            if c.name in times:
+                r["us_per_step"] = round(min(times[c.name]), 2)
+            if c.name in after:
+                r["us_per_step" if c.name not in times else "us_per_step_late_phase"] = round(min(after[c.name]), 2)
+        ok = [(c, min(use[c.name])) for c, _, _ in built if c.name in use and min(use[c.name]) != float("inf")]
         if ok:
-            best = min(ok, key=lambda r: r["us_per_step"])
-            keep = next(x for x in built if x[0].name == best["name"])
+            best = min(ok, key=lambda x: x[1])[0]
+            keep = next(x for x in built if x[0] is best)
     finally:
         for b in built:
             if b is not keep:
                 close_trainer(b[1])
     if keep is None:
-        ref = next((c for c in order if c.reference), order[0])
-        return ({"candidates": table, "choice": ref.name, "env": dict(ref.env), "args": dict(ref.args),
-                 "reason": "no candidate timed"}, None, None)
+        return no_choice("no candidate timed")
     summary = ", ".join(f"{r['name']}: {r.get('us_per_step')}" for r in table)
-    log(f"[autotune] {summary} -> {keep[0].name}")
-    return ({"candidates": table, "choice": keep[0].name, "env": dict(keep[0].env), "args": dict(keep[0].args),
-             "steps_timed": steps, "rounds": rounds}, keep[1], keep[2])
+    log(f"[autotune] {summary} -> {keep[0].name}" + (" (reference slowed after a late candidate)" if contaminated
+                                                      else ""))
+    out = {"candidates": table, "choice": keep[0].name, "env": dict(keep[0].env), "args": dict(keep[0].args),
+           "steps_timed": steps, "rounds": rounds}
+    if late:
+        out["contaminated"] = contaminated
+    return out, keep[1], keep[2]

@@ -93,3 +93,51 @@ def test_wrong_tile_is_rejected(gloo1):
     assert rows["bad"]["engaged"] is True
     assert rows["bad"]["valid"] is False and "differs" in rows["bad"]["reason"], rows
     assert report["choice"] == "ref" and tr.form == "ref"
+
+
+def test_failed_reference_validates_nothing(gloo1):
+    # the reference form's probe fails (an in-kernel wait timed out): no candidate can be
+    # compared -- none is timed, the caller builds the reference form itself
+    class _Bad(_Trainer):
+        def __init__(self, eps):
+            super().__init__(eps)
+            self.fused = type("E", (), {"tx": type("T", (), {"error": lambda self: 1})()})()
+
+    report, tr, _ = AT.run(_cands("one"), lambda eps, c: (_Bad(eps), None), lambda tr, b: None,
+                           torch.device("cpu"), steps=2, rounds=1, log=lambda *a: None)
+    rows = {r["name"]: r for r in report["candidates"]}
+    assert tr is None and report["choice"] == "ref" and "reference form failed" in report["reason"]
+    assert rows["ref"]["valid"] is False and rows["one"]["valid"] is None, rows
+
+
+def test_state_changing_candidate_is_timed_last(gloo1):
+    # a candidate that slows the process for everything built after it: validated and
+    # timed after the others, the reference re-timed, the slowdown reported
+    import time
+
+    slow = {"on": False}
+
+    class _T(_Trainer):
+        def step(self, batch):
+            super().step(batch)
+            if slow["on"]:
+                time.sleep(2e-3)
+
+    order = []
+
+    def build(eps, c):
+        order.append(c.name)
+        if c.name == "streams" and eps is None:
+            slow["on"] = True
+        return _T(eps), None
+
+    cands = [AT.Candidate("streams", {FORM: "one"}, contaminates=True),
+             AT.Candidate("ref", {FORM: "ref"}, reference=True),
+             AT.Candidate("other", {FORM: "one"})]
+    report, tr, _ = AT.run(cands, build, lambda tr, b: None, torch.device("cpu"), steps=3, rounds=1,
+                           log=lambda *a: None)
+    assert order[-1] == "streams" and order[:4] == ["ref", "other", "ref", "other"], order
+    assert report["contaminated"] is True, report
+    rows = {r["name"]: r for r in report["candidates"]}
+    assert rows["ref"]["us_per_step_after_late"] > rows["ref"]["us_per_step"]
+    slow["on"] = False

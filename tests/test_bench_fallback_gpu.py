@@ -80,3 +80,24 @@ def test_bench_falls_back_when_the_exchange_fails_without_autotune(strategy):
     assert "one_launch_fallback" in j["config"], j["config"]
     assert not j["config"].get("step_launches", "").startswith("1 "), j["config"]
     assert j["value"] > 0 and j["n_gpus"] == 2
+
+
+def test_pp_autotune_validates_the_stage_kernel():
+    """GPipe with one layer per stage (2 ranks sharing the GPU): the autotune value-checks
+    the in-kernel stage step against the per-tick launches (AdamW eps = 10 probe, no
+    dropout) before timing it, and drops it -- reason in the JSON -- when one rank's
+    stage state is corrupted by one 16 x 16 block."""
+    extra = ("--hidden-layers", "2")
+    ok = _bench("pp", extra=extra)
+    rows = _rows(ok)
+    assert rows["stage-kernel=1"]["valid"] is True and rows["stage-kernel=1"]["engaged"] is True, rows
+    assert rows["stage-kernel=1"]["err"]["p"] < 1e-2, rows
+    assert all(r["valid"] for r in rows.values()), rows
+    assert "pp_rejected" not in ok["config"]
+    j = _bench("pp", corrupt=1, extra=extra)
+    rows = _rows(j)
+    assert rows["stage-kernel=1"]["valid"] is False and "differs" in rows["stage-kernel=1"]["reason"], rows
+    assert "stage-kernel=1" in j["config"]["pp_rejected"], j["config"]
+    assert j["details"]["autotune"]["stages"][-1]["choice"] == "stage-kernel=0"
+    assert "step_launches" not in j["config"], j["config"]   # the per-tick path ran
+    assert j["value"] > 0 and j["n_gpus"] == 2

@@ -27,6 +27,13 @@ def _run(args, env=None, timeout=300):
                           timeout=timeout)
 
 
+def _why(r) -> str:
+    """A failed job's whole output: every rank's stderr (the ranks share the parent's
+    stream), so a rank's faulthandler stack and native abort message are never cut off
+    (a one-off SIGABRT of rank 1 in round 5 left only its last 3000 characters)."""
+    return f"exit {r.returncode}\n--- stdout ---\n{r.stdout[-4000:]}\n--- stderr (all ranks) ---\n{r.stderr[-60000:]}"
+
+
 def _json_line(out: str) -> dict:
     lines = [ln for ln in out.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out  # rank 0 prints exactly one JSON line
@@ -36,7 +43,7 @@ def _json_line(out: str) -> dict:
 @pytest.mark.parametrize("n", [2, 4])
 def test_bench_gpus_n_starts_n_ranks(n):
     r = _run(["bench.py", "--gpus", str(n), "--steps", "2", "--warmup", "1"])
-    assert r.returncode == 0, r.stdout[-1500:] + r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     j = _json_line(r.stdout)
     assert j["n_gpus"] == n and j["steps"] == 2 and j["warmup"] == 1
     assert j["config"]["parallelism"] == f"dp{n}"
@@ -56,7 +63,7 @@ def test_bench_refuses_wrong_world_size():
 ])
 def test_entry_scripts_gpus_flag(script, extra, title):
     r = _run([script, "--gpus", "2", "--steps", "1", "--check-replication", *extra])
-    assert r.returncode == 0, r.stdout[-1500:] + r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     assert title in r.stdout and "loss:" in r.stdout
     assert "[check-replication]" in r.stdout
 

@@ -256,6 +256,28 @@ def test_pipeline_stage_kernel_equals_per_tick_launches(tmp_path, ws, n_mb):
     assert abs(float(ma[2]) - float(mb_[2])) <= 2
 
 
+@pytest.mark.parametrize("ws", [2, 4])
+def test_pipeline_stage_kernel_checkpoint_restore(tmp_path, ws):
+    """Save, train on, restore, train: the stage kernel (rebuilt after the restore from
+    zeroed hand-off flags, parallel/pipeline.py invalidate) == the per-tick launches on the
+    same schedule.  Before the fix every in-kernel wait passed at once on the flags of the
+    rolled-back steps and the stages read stale activations / gradients / weights."""
+    import functools
+
+    for k in ("1", "0"):
+        spawn(functools.partial(XW.pp_restore, n_hidden=ws, pp_kernel=k, tag=f"k{k}"), ws, str(tmp_path), gpu=True)
+    a, b = _load(tmp_path, "pprk1", ws), _load(tmp_path, "pprk0", ws)
+    assert all(o["pp_kernel"] for o in a) and not any(o["pp_kernel"] for o in b)
+    for oa, ob in zip(a, b):
+        assert oa["count"] == ob["count"] == 5
+        for k, v in oa["params"].items():
+            d = (v - ob["params"][k]).abs()
+            assert float(d.max()) <= 2 * 1e-3 * 5 + 1e-6, k
+            assert float((d > 5e-5).float().mean()) < 2e-2, (k, float((d > 5e-5).float().mean()))
+    ma, mb_ = a[0]["metrics"], b[0]["metrics"]
+    assert float(ma[1]) == float(mb_[1]) and abs(float(ma[0]) - float(mb_[0])) <= 2e-3 * abs(float(mb_[0])) + 1e-2
+
+
 @pytest.mark.parametrize("ws,n_layers", [(4, 2), (8, 4)])
 def test_transformer_hybrid_over_xgmi_matches_single_device(tmp_path, ws, n_layers):
     """Transformer LM, DP=2 x PP=ws/2 over xGMI (ws processes on the GPU), captured

@@ -279,6 +279,49 @@ def pp_xgmi(outdir, dp, n_hidden=3, steps=4, pp_kernel="1", dropout=0.0, tag="",
                                     "pp_kernel": tr.pp_kernel is not None})
 
 
+def pp_restore(outdir, n_hidden, pp_kernel="1", dropout=0.1, tag=""):
+    """GPipe over the inboxes: 2 steps, checkpoint, 3 more steps (the hand-off flags move
+    past the checkpoint's epochs), restore, then 1 eager step + a 2-step graph replay.
+    With the stage kernel the restore must rebuild its engine (parallel/pipeline.py
+    invalidate): stale flags would let every in-kernel wait pass at once."""
+    os.environ["JDT_PP_KERNEL"] = pp_kernel
+    from data_paral import synthetic_batch
+    from pipeline_parallel import build_mlp_pipeline
+    from jax_distributed_tuts_amd.parallel.dp import shard_batch
+    from jax_distributed_tuts_amd.runtime import dist as D
+    from jax_distributed_tuts_amd.utils import checkpoint as CK
+    from jax_distributed_tuts_amd.utils.config import dp_config
+    from jax_distributed_tuts_amd.utils.train_state import Batch
+
+    dev = D.device()
+    cfg = dp_config()
+    mesh = D.Mesh({"data": 1, "pipe": D.world_size()})
+    tr = build_mlp_pipeline(cfg, mesh, dev, n_hidden_layers=n_hidden, dropout_rate=dropout, num_microbatches=4,
+                            comm="xgmi")
+    b = shard_batch(synthetic_batch(cfg, 70), mesh, "data")
+    b = Batch(b.inputs.to(dev), b.labels.to(dev))
+    for _ in range(2):
+        tr.step(b)
+    torch.cuda.synchronize()
+    ck = os.path.join(outdir, f"ck{tag}")
+    CK.save(tr.state, ck, tr.metrics)
+    D.barrier()
+    for _ in range(3):
+        tr.step(b)
+    torch.cuda.synchronize()
+    D.barrier()
+    CK.restore(tr.state, ck, tr.metrics)
+    tr.step(b)
+    tr.capture(b, steps_per_graph=2)
+    tr.run_steps(b, 2)
+    torch.cuda.synchronize()
+    tr.finalize()
+    _save(outdir, f"ppr{tag}", {"params": {k: v.cpu() for k, v in tr.state.params.state_dict().items()},
+                                "metrics": tr.gather_metrics().cpu(),
+                                "count": int(tr.state.step_tensor.item()),
+                                "pp_kernel": tr.pp_kernel is not None})
+
+
 def p2p_roundtrip(outdir):
     """Raw XgmiP2P: ring sends through every slot, eager and graph-replayed epochs."""
     from jax_distributed_tuts_amd.comm.p2p import XgmiP2P

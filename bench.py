@@ -227,7 +227,11 @@ def autotune_candidates(args, ws: int):
     one = lambda tr: bool(getattr(tr, "one_launch", False))   # noqa: E731
     if args.strategy == "dp" and args.accum == "kernel":
         if args.num_layers == 2:
-            return [[Candidate("one-launch", {"JDT_DP_AHEAD": "1"}, replicated=True, engaged=one),
+            # persistent: a replay's steps are ONE launch per rank, the tile exchange inside
+            # every step (mlp2_pst_kernel TX); one-launch: one run-ahead launch per step
+            pst = lambda tr: one(tr) and bool(getattr(getattr(tr, "fused", None), "pst_ok", False))  # noqa: E731
+            return [[Candidate("persistent", {"JDT_DP_AHEAD": "1", "JDT_DP_PST": "1"}, replicated=True, engaged=pst),
+                     Candidate("one-launch", {"JDT_DP_AHEAD": "1", "JDT_DP_PST": "0"}, replicated=True, engaged=one),
                      Candidate("three-launch", {"JDT_DP_AHEAD": "0"}, reference=True, replicated=True)]]
         if args.optimizer == "adamw":
             return [[Candidate("deep-exchange", {"JDT_DP_DEEP_TX": "1"}, replicated=True, engaged=one),
@@ -331,7 +335,7 @@ def run_autotune(args, dev, build, prepare):
 def _mlp2_launches(eng, tx_: str, spg: int) -> str:
     """Launches per step of the fused 2-layer engine's captured replay: the persistent
     run-ahead kernel runs a whole replay of ``spg`` steps in one launch (ops/csrc/mlp_fused.hip
-    mlp2_pst_kernel), else one run-ahead launch per step."""
+    mlp2_pst_kernel; at N > 1 with the tile exchange inside), else one run-ahead launch per step."""
     if getattr(eng, "pst_ok", False) and spg >= 2:
         return f"1/{spg} (persistent run-ahead: {spg} steps per launch, grid barrier between steps{tx_})"
     return f"1 (run-ahead mlp2_bwd{tx_})"

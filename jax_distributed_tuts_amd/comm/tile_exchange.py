@@ -55,6 +55,7 @@ class TileExchange:
     def __init__(self, group, rank: int, world: int, tiles: int, device: torch.device,
                  pay: int = TILE_PAYLOAD, timeout_s: float = 10.0):
         self.group, self.rank, self.world, self.tiles, self.pay = group, rank, world, tiles, pay
+        self.timeout_s = float(timeout_s)
         self.device = device
         self.ctx = c_void_p()
         self.ok = False

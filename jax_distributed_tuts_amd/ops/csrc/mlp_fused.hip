@@ -627,7 +627,7 @@ template <int K_IN, int C, int KC, bool LOOP, bool AHEAD = false, bool TX = fals
           bool FX = false, bool PST = false, class AT>
 __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by, const int step_in,
                                               PstRegs* R = nullptr, const PstPos pp = PstPos{0, 1, 0u}) {
-  static_assert(!PST || (AHEAD && !TX && !P3S && !FX && !LOOP), "persistent: the one-GPU run-ahead step");
+  static_assert(!PST || (AHEAD && !P3S && !FX && !LOOP), "persistent: the run-ahead step (one GPU, or DP TX)");
   constexpr bool SCX = LOOP || PST;        // in-launch hand-offs: sc1 loads / stores
   // phase stamps: a persistent launch records step n-2 (a steady step: the last one also
   // stores the optimizer state)
@@ -802,7 +802,11 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     op[e] = ld_global(sp + idx); om[e] = ld_global(sm + idx); ov[e] = ld_global(sv + idx);
   }
   }
-  const float run_pre = (a.running ? a.running : a.logits)[lane & 3];   // lead: metric accumulators
+  // lead: metric accumulators (persistent N > 1: its own store of the previous step, sc1 so
+  // no stale L1 line is read)
+  float run_pre;
+  if constexpr (PST && TX) run_pre = ld_f<true>(a.running + (lane & 3));
+  else run_pre = (a.running ? a.running : a.logits)[lane & 3];
   const int lq = min(lane, C - 1);
   float qp, qm, qv;
   if constexpr (PST) {
@@ -899,7 +903,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
     R->l_loss = l_loss;
     R->l_corr = l_corr;
   }
-  if (lead && !PST) {
+  if (lead && (!PST || TX)) {   // persistent N > 1: the metric slots ride the exchange
     l_loss = wave_sum(l_loss);
     l_corr = wave_sum(l_corr);
     if (lane == 0) { red[0][w] = l_loss; red[1][w] = l_corr; }
@@ -1323,7 +1327,10 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
           if (a.fuse_opt) {
             float tp, tm = om[e], tv = ov[e];
             const bf16_t pb = f2bf(adam_apply(op[e], om[e], ov[e], acc[e], ak, &tp, &tm, &tv));
-            if (AHEAD && (a.wt & 1)) {
+            if constexpr (PST) {
+              // persistent N > 1: the state stays in registers (stored after the last step)
+              R->op[e] = tp; R->om[e] = tm; R->ov[e] = tv;
+            } else if (AHEAD && (a.wt & 1)) {
               st_f<true>(a.pW1 + idx, tp);
               if (!ak.sgd) { st_f<true>(a.mW1 + idx, tm); st_f<true>(a.vW1 + idx, tv); }
             } else {
@@ -1341,7 +1348,8 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
           }
         }
         // the lane's 4 rows are 4 consecutive K elements of W1^T: one 8-byte store
-        if (a.fuse_opt && a.W1T) {
+        // (persistent: the next steps read w1n; W1^T is stored after the last one)
+        if (!PST && a.fuse_opt && a.W1T) {
           const unsigned long long w8 = (unsigned long long)wt[0] | ((unsigned long long)wt[1] << 32);
           if (LOOP || (AHEAD && (a.wt & 1))) st_u64<true>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
           else st_u64<false>(a.W1T + (long)tcol * a.ldw1t + trow0, w8);
@@ -1360,8 +1368,15 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
             const long o = isb ? (long)(j0 + n) : (long)(j0 + n) * C + ac;
             const float gr = isb ? ab1[e] : aw[e];
             if (a.fuse_opt) {
-              const float pn = adam_apply_h<LOOP>(op[e], om[e], ov[e], gr, ak, (isb ? a.pb1 : a.pW2) + o,
-                                                  (isb ? a.mb1 : a.mW2) + o, (isb ? a.vb1 : a.vW2) + o);
+              float pn;
+              if constexpr (PST) {
+                float tp, tm = om[e], tv = ov[e];
+                pn = adam_apply(op[e], om[e], ov[e], gr, ak, &tp, &tm, &tv);
+                R->op[e] = tp; R->om[e] = tm; R->ov[e] = tv;
+              } else {
+                pn = adam_apply_h<LOOP>(op[e], om[e], ov[e], gr, ak, (isb ? a.pb1 : a.pW2) + o,
+                                        (isb ? a.mb1 : a.mW2) + o, (isb ? a.vb1 : a.vW2) + o);
+              }
               (isb ? a.sb1 : sW2n)[o] = f2bf(pn);
               if constexpr (AHEAD) a.hand[(isb ? 0 : H) + o] = pn;   // same XCD as the reader (L2)
             } else if (a.smap) {
@@ -1374,7 +1389,14 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
         }
         if (lead && lane < C) {
           if (a.fuse_opt) {
-            const float pn = adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
+            float pn;
+            if constexpr (PST) {   // persistent N > 1: b2 stays with the lead's aux wave
+              float tp, tm = qm, tv = qv;
+              pn = adam_apply(qp, qm, qv, ab2[0], ak, &tp, &tm, &tv);
+              R->qp = tp; R->qm = tm; R->qv = tv;
+            } else {
+              pn = adam_apply_h<LOOP>(qp, qm, qv, ab2[0], ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
+            }
             a.sb2[lane] = f2bf(pn);
             if constexpr (AHEAD) a.hand[H + (long)H * C + lane] = pn;
           } else if (a.smap) {
@@ -1389,7 +1411,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   __syncthreads();
   STAMP(3);
 
-  if (!PST && lead && tid < 4) {
+  if ((!PST || TX) && lead && tid < 4) {
     float val = mval;   // N > 1 run-ahead: the all-reduced slot
     if (!(AHEAD && TX)) {
       float L = 0.f, Cr = 0.f;
@@ -1687,7 +1709,7 @@ __device__ __forceinline__ bool pst_wait(unsigned* ws, unsigned gen, bool last, 
 // first step and stored after its last: the elements each lane owns in mlp2_bwd_body's
 // phase-3 epilogues (same indices) -- tile waves 4 W1 elements (plus their W1^T bf16
 // copy), the chunk-0 aux wave W2 / b1 (lanes ac <= C) and, in block (0,0), b2.
-template <int K_IN, int C, int KC, class AT>
+template <int K_IN, int C, int KC, bool TX, class AT>
 __device__ __forceinline__ void pst_state_io(AT& a, const int bx, const int by, PstRegs& R, const bool store) {
   constexpr int NTILE = KC / 16;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, H = a.H;
@@ -1752,7 +1774,8 @@ __device__ __forceinline__ void pst_state_io(AT& a, const int bx, const int by, 
       }
     }
   }
-  if (bx == 0 && by == 1 && w == NW - 1 && lane < C) {
+  // b2's state: block (0,1)'s last wave on one GPU, the lead's aux wave with the exchange
+  if (bx == 0 && by == (TX ? 0 : 1) && w == NW - 1 && lane < C) {
     pb2[lane] = R.qp;
     if (!sgd) { mb2[lane] = R.qm; vb2[lane] = R.qv; }
   }
@@ -1783,8 +1806,19 @@ __device__ __forceinline__ void pst_metrics(float* running, int M, const PstRegs
 // tests/test_mlp2_persistent_gpu.py bounds the difference (median <= 1e-5 x the update
 // scale, p99.9 <= 1e-4 x).  Requires every workgroup
 // resident at once and round-robin XCD dispatch (the run-ahead's own conditions).
-template <int K_IN, int C, int KC>
-__global__ void __launch_bounds__(NT) mlp2_pst_kernel(Mlp2Args a, int n, unsigned* ws, long long tmo) {
+//
+// TX (N > 1 data parallel, Mlp2Args::tx): every step's gradient tiles are all-reduced with
+// the same tiles of the other ranks' persistent launches inside the step (the one-launch
+// step's tile exchange, common.h tx_tile: epochs = optimizer step + 1, single-buffered
+// inboxes -- a rank pushes step t+1's partial only after it read step t's reduced tile,
+// which the owner sends only after it has read step t's partials), so the n steps of a
+// replay are one launch per rank.  The metric slots ride the exchange (every rank folds
+// the all-reduced sums); b2 stays with the lead's aux wave.  Requires every workgroup of
+// every rank resident (one rank per GPU; two ranks sharing one only while both grids fit:
+// the WPE = 4 variant, <= 128 VGPRs, two workgroups per CU).
+template <int K_IN, int C, int KC, bool TX = false, int WPE = 1>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE)))
+mlp2_pst_kernel(Mlp2Args a, int n, unsigned* ws, long long tmo) {
   __shared__ int ok_lds[1];
   __shared__ float red_lds[2][NW];
   if (n <= 0) return;   // warm-up launch (jdt_mlp2_pst n = 0): touches nothing
@@ -1799,7 +1833,7 @@ __global__ void __launch_bounds__(NT) mlp2_pst_kernel(Mlp2Args a, int n, unsigne
   typedef const __attribute__((address_space(4))) Mlp2Args KArgs;
   KArgs* const kbase = (KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
   PstRegs R;
-  pst_state_io<K_IN, C, KC>(a, bx, by, R, false);
+  pst_state_io<K_IN, C, KC, TX>(a, bx, by, R, false);
   {
     const AdamK k0 = adam_consts(*kbase, step0);
     R.rbc1 = k0.rbc1;
@@ -1817,14 +1851,14 @@ __global__ void __launch_bounds__(NT) mlp2_pst_kernel(Mlp2Args a, int n, unsigne
     if (stw && it == n - 1) stw[7] = __builtin_amdgcn_s_memrealtime();
     // the tile coordinates re-made scalar each step: carried across the loop they may sit
     // in VGPRs, and the buffer resources built from them would become waterfall loops
-    mlp2_bwd_body<K_IN, C, KC, false, true, false, false, false, true>(
+    mlp2_bwd_body<K_IN, C, KC, false, true, TX, false, false, true>(
         *k, __builtin_amdgcn_readfirstlane(bx), __builtin_amdgcn_readfirstlane(by), step0 + it, &R,
         PstPos{it, n, launch0});
     if (stw && it == n - 2) stw[12] = __builtin_amdgcn_s_memrealtime();
     if (it + 1 < n) {
       unsigned xcc = 0u;
       const bool last = pst_arrive(ws, xcc);
-      if (bx == 0 && by == 0) pst_metrics(a.running, a.M, R, red_lds);
+      if (!TX && bx == 0 && by == 0) pst_metrics(a.running, a.M, R, red_lds);
       // the next step's bias corrections, while the other workgroups arrive
       const AdamK kn = adam_consts(*kbase, step0 + it + 1);
       R.rbc1 = kn.rbc1;
@@ -1834,8 +1868,8 @@ __global__ void __launch_bounds__(NT) mlp2_pst_kernel(Mlp2Args a, int n, unsigne
     if (stw && it == n - 2) stw[13] = __builtin_amdgcn_s_memrealtime();
   }
   if (it == n) {
-    if (bx == 0 && by == 0) pst_metrics(a.running, a.M, R, red_lds);
-    pst_state_io<K_IN, C, KC>(a, bx, by, R, true);
+    if (!TX && bx == 0 && by == 0) pst_metrics(a.running, a.M, R, red_lds);
+    pst_state_io<K_IN, C, KC, TX>(a, bx, by, R, true);
   }
   if (stw) stw[6] = (unsigned long long)(bx + 256 * by);
   if (bx == 0 && by == 0 && threadIdx.x == 0 && it == n) {
@@ -1973,23 +2007,36 @@ static int mlp2_ahead_ok_k(int M, int H, int nshare, bool tx) {
 // 1 if the persistent run-ahead launch can run M rows x H hidden units of input width
 // K_IN here: the run-ahead's conditions, a grid of whole XCD shares (G % 8 == 0) and every
 // workgroup of the persistent kernel resident at once.
+// nshare > 0: the N > 1 form (tile exchange) with `nshare` ranks' grids on this GPU -- every
+// workgroup of every sharing rank's persistent launch resident at once.
 template <int K_IN>
-static int mlp2_pst_ok_k(int M, int H) {
+static int mlp2_pst_ok_k(int M, int H, int nshare) {
   constexpr int KC = mlp2_kc<K_IN>(), NCH = K_IN / KC;
-  if (!mlp2_ahead_ok_k<K_IN>(M, H, 1, false)) return 0;
+  if (!mlp2_ahead_ok_k<K_IN>(M, H, nshare > 0 ? nshare : 1, nshare > 0)) return 0;
   const int G = (H / 16) * NCH;
   if (G % 8) return 0;
   int dev = 0, cus = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, mlp2_pst_kernel<K_IN, 10, KC>, NT, 0) != hipSuccess)
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
-  return G <= cus * per ? 1 : 0;
+  const hipError_t e =
+      nshare > 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, mlp2_pst_kernel<K_IN, 10, KC, true, 4>, NT, 0)
+      : nshare == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, mlp2_pst_kernel<K_IN, 10, KC, true>, NT, 0)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, mlp2_pst_kernel<K_IN, 10, KC>, NT, 0);
+  if (e != hipSuccess) return 0;
+  return (long)(nshare > 0 ? nshare : 1) * G <= (long)cus * per ? 1 : 0;
 }
 
 JDT_API int jdt_mlp2_pst_ok(int M, int H, int k_in) {
-  if (k_in == 784) return mlp2_pst_ok_k<784>(M, H);
-  if (k_in == 1024) return mlp2_pst_ok_k<1024>(M, H);
+  if (k_in == 784) return mlp2_pst_ok_k<784>(M, H, 0);
+  if (k_in == 1024) return mlp2_pst_ok_k<1024>(M, H, 0);
+  return 0;
+}
+// the persistent launch with the tile exchange (N > 1 DP), `nshare` ranks per GPU
+JDT_API int jdt_mlp2_pst_tx_ok(int M, int H, int k_in, int nshare) {
+  if (nshare < 1) return 0;
+  if (k_in == 784) return mlp2_pst_ok_k<784>(M, H, nshare);
+  if (k_in == 1024) return mlp2_pst_ok_k<1024>(M, H, nshare);
   return 0;
 }
 
@@ -1999,19 +2046,30 @@ JDT_API int jdt_mlp2_pst_ok(int M, int H, int k_in) {
 // launch that returns at once -- done once before any timed or captured use, so the
 // kernel's first-dispatch setup (its private segment, ~100 us) is not paid inside one
 // (bench.py's 20-step driver form measured 51.6k steps/s without it).
+// ranks sharing this GPU (jdt_mlp2_pst_set_share): > 1 selects the two-workgroups-per-CU
+// build of the exchanging persistent kernel
+static int g_pst_share = 1;
+JDT_API void jdt_mlp2_pst_set_share(int n) { g_pst_share = n < 1 ? 1 : n; }
 JDT_API int jdt_mlp2_pst(const Mlp2Args* args, int n, int k_in, unsigned* ws, long long timeout, void* stream) {
   const long long tmo = timeout > 0 ? timeout : 2000000ll;   // s_memrealtime ticks (100 MHz): 20 ms
   const Mlp2Args& a = *args;
-  if (n == 1 || n < 0 || !ws || a.tx || !a.fuse_opt || !a.W1T || !a.XR || !a.zslab || !a.ztick || !a.hand || !a.lg3 ||
-      a.det_logits || a.M <= 0 || a.M > 128 || a.H % 128)
+  if (n == 1 || n < 0 || !ws || a.tx_fsdp || !a.fuse_opt || !a.W1T || !a.XR || !a.zslab || !a.ztick || !a.hand ||
+      !a.lg3 || a.det_logits || a.M <= 0 || a.M > 128 || a.H % 128 || (a.tx && !a.running))
     return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  const bool tx = a.tx != nullptr;
   if (k_in == 784) {
     const dim3 g(a.H / 16, 784 / mlp2_kc<784>());
-    hipLaunchKernelGGL((mlp2_pst_kernel<784, 10, mlp2_kc<784>()>), g, dim3(NT), 0, st, a, n, ws, tmo);
+    if (tx && g_pst_share > 1)
+      hipLaunchKernelGGL((mlp2_pst_kernel<784, 10, mlp2_kc<784>(), true, 4>), g, dim3(NT), 0, st, a, n, ws, tmo);
+    else if (tx) hipLaunchKernelGGL((mlp2_pst_kernel<784, 10, mlp2_kc<784>(), true>), g, dim3(NT), 0, st, a, n, ws, tmo);
+    else hipLaunchKernelGGL((mlp2_pst_kernel<784, 10, mlp2_kc<784>()>), g, dim3(NT), 0, st, a, n, ws, tmo);
   } else if (k_in == 1024) {
     const dim3 g(a.H / 16, 1024 / mlp2_kc<1024>());
-    hipLaunchKernelGGL((mlp2_pst_kernel<1024, 10, mlp2_kc<1024>()>), g, dim3(NT), 0, st, a, n, ws, tmo);
+    if (tx && g_pst_share > 1)
+      hipLaunchKernelGGL((mlp2_pst_kernel<1024, 10, mlp2_kc<1024>(), true, 4>), g, dim3(NT), 0, st, a, n, ws, tmo);
+    else if (tx) hipLaunchKernelGGL((mlp2_pst_kernel<1024, 10, mlp2_kc<1024>(), true>), g, dim3(NT), 0, st, a, n, ws, tmo);
+    else hipLaunchKernelGGL((mlp2_pst_kernel<1024, 10, mlp2_kc<1024>()>), g, dim3(NT), 0, st, a, n, ws, tmo);
   } else {
     return -3;
   }

@@ -88,6 +88,8 @@ _lib.declare("jdt_mlp2_loop", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_void_p,
 
 _lib.declare("jdt_mlp2_loop_ok", c_int, [c_int, c_int])
 _lib.declare("jdt_mlp2_pst_ok", c_int, [c_int, c_int, c_int])
+_lib.declare("jdt_mlp2_pst_tx_ok", c_int, [c_int, c_int, c_int, c_int])
+_lib.declare("jdt_mlp2_pst_set_share", None, [c_int])
 _lib.declare("jdt_mlp2_pst", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_void_p, c_longlong, c_void_p])
 PST_BARRIER_TIMEOUT_S = 0.02   # persistent run-ahead grid barrier bound (x runtime.dist.spin_timeout_s sharing)
 
@@ -249,8 +251,19 @@ class FusedMLP2:
         # run-ahead call in ONE launch, the AdamW state in registers across them and an
         # XCD-hierarchical grid barrier between steps; one GPU only.  JDT_MLP2_PST=0: one
         # launch per step (A/B).  pst_ws: the barrier's counter lines, zeroed once.
-        self.pst_ok = (self.ahead_ok and tx is None and os.environ.get("JDT_MLP2_PST", "1") == "1"
-                       and bool(_lib.lib().jdt_mlp2_pst_ok(rows, H, K)))
+        # N > 1 (DP one-launch step, ``tx``): the same persistent launch with the tile
+        # exchange inside every step (mlp2_pst_kernel TX), so a replay's n steps are one
+        # launch per rank; JDT_DP_PST=0 keeps one run-ahead launch per step (bench.py's
+        # autotune validates and times both).  Not the FSDP form (its sharded AdamW state
+        # is owner-local, handed back by value every step).
+        if tx is None:
+            self.pst_ok = (self.ahead_ok and os.environ.get("JDT_MLP2_PST", "1") == "1"
+                           and bool(_lib.lib().jdt_mlp2_pst_ok(rows, H, K)))
+        else:
+            self.pst_ok = (self.ahead_ok and not self.fsdp_tx and os.environ.get("JDT_DP_PST", "1") == "1"
+                           and bool(_lib.lib().jdt_mlp2_pst_tx_ok(rows, H, K, int(ranks_on_gpu))))
+            if self.pst_ok:
+                _lib.lib().jdt_mlp2_pst_set_share(int(ranks_on_gpu))
         if self.pst_ok:
             from ..runtime.dist import spin_timeout_s
 
@@ -258,6 +271,11 @@ class FusedMLP2:
             # s_memrealtime ticks (100 MHz); grows with the ranks sharing the GPU like the
             # other in-kernel waits
             self.pst_timeout = int(spin_timeout_s(PST_BARRIER_TIMEOUT_S) * 1e8)
+            if tx is not None:
+                # N > 1: a workgroup reaches the grid barrier only after its tile's exchange,
+                # which waits for the peers' launches (not started in lockstep): the barrier
+                # gets the exchange's bound
+                self.pst_timeout = max(self.pst_timeout, int(tx.timeout_s * 1e8))
         self._pst_warm = False
 
     def set_grad_stage(self, base: int, stride: int):

@@ -50,35 +50,44 @@ def test_autotune_validates_and_falls_back(strategy):
     print(strategy, "errors of the one-launch form vs three-launch:", rows["one-launch"]["err"])
     if strategy == "dp":
         assert rows["one-launch"]["replicated"] is True
+        # N > 1 persistent launch (tile exchange inside every step): validated like the others
+        assert rows["persistent"]["valid"] is True and rows["persistent"]["engaged"] is True, rows
+        assert rows["persistent"]["replicated"] is True
+        print("errors of the persistent form vs three-launch:", rows["persistent"]["err"])
     # the timed run is the faster valid form
     best = min(rows.values(), key=lambda r: r["us_per_step"])["name"]
     assert ok["details"]["autotune"]["stages"][0]["choice"] == best
-    want_one = best == "one-launch"
-    assert ok["config"].get("step_launches", "").startswith("1 (run-ahead mlp2_bwd") == want_one, ok["config"]
+    sl = ok["config"].get("step_launches", "")
+    assert sl.startswith("1 (run-ahead mlp2_bwd") == (best == "one-launch"), ok["config"]
+    assert sl.startswith("1/") == (best == "persistent"), ok["config"]
     assert "one_launch_fallback" not in ok["config"]
     # a corrupted exchange tile on rank 1: wrong values, not a timeout -> dropped everywhere
     j = _bench(strategy, corrupt=1)
     rows = _rows(j)
     assert rows["one-launch"]["valid"] is False and "differs" in rows["one-launch"]["reason"], rows
     assert rows["one-launch"]["err"]["block"] > 0.05, rows
+    if strategy == "dp":
+        assert rows["persistent"]["valid"] is False and "differs" in rows["persistent"]["reason"], rows
     assert "one_launch_fallback" in j["config"], j["config"]
-    assert not j["config"].get("step_launches", "").startswith("1 "), j["config"]
+    assert not j["config"].get("step_launches", "").startswith(("1 ", "1/")), j["config"]
     assert j["value"] > 0 and j["n_gpus"] == 2
     # a failed exchange wait reported by rank 1
     j = _bench(strategy, fake=1)
     rows = _rows(j)
     assert rows["one-launch"]["valid"] is False and "timed out" in rows["one-launch"]["reason"], rows
-    assert not j["config"].get("step_launches", "").startswith("1 "), j["config"]
+    assert not j["config"].get("step_launches", "").startswith(("1 ", "1/")), j["config"]
 
 
 @pytest.mark.parametrize("strategy", ["dp", "fsdp"])
 def test_bench_falls_back_when_the_exchange_fails_without_autotune(strategy):
     ok = _bench(strategy, extra=("--autotune", "off"))
     assert "one_launch_fallback" not in ok["config"]
-    assert ok["config"]["step_launches"].startswith("1 (run-ahead mlp2_bwd")
+    # DP: a 20-step replay is one persistent launch per rank (JDT_DP_PST default on)
+    want = "1/20 (persistent" if strategy == "dp" else "1 (run-ahead mlp2_bwd"
+    assert ok["config"]["step_launches"].startswith(want), ok["config"]
     j = _bench(strategy, 1, extra=("--autotune", "off"))
     assert "one_launch_fallback" in j["config"], j["config"]
-    assert not j["config"].get("step_launches", "").startswith("1 "), j["config"]
+    assert not j["config"].get("step_launches", "").startswith(("1 ", "1/")), j["config"]
     assert j["value"] > 0 and j["n_gpus"] == 2
 
 

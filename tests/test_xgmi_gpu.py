@@ -111,6 +111,37 @@ def test_dp_over_xgmi_matches_single_device(tmp_path, ws, dp_ahead, layers, widt
     assert abs(float(m[2]) - float(ref[2])) <= 4
 
 
+@pytest.mark.parametrize("ws,width", [(2, (784, 512)), (4, (784, 256))])
+def test_dp_persistent_exchange_matches_per_step_launches(tmp_path, ws, width):
+    """N > 1 data parallel, 2-layer: a 3-step replay as ONE persistent launch per rank with
+    the tile exchange inside every step (mlp2_pst_kernel TX; on the shared GPU the
+    two-workgroups-per-CU build) == one run-ahead launch per step (JDT_DP_PST=0), up to the
+    arrival order of the forward's fp32 logit atomics (tests/test_mlp2_persistent_gpu.py's
+    bulk bounds); replicas bit-identical in both forms."""
+    import functools
+
+    for k in ("1", "0"):
+        _spawn8(functools.partial(XW.dp_xgmi, dp_ahead="1", width=width, dp_pst=k, tag=f"p{k}"), ws,
+                str(tmp_path))
+    a, b = _load(tmp_path, "dpxp1", ws), _load(tmp_path, "dpxp0", ws)
+    assert all(o["one_launch"] and o["pst"] for o in a), [(o["one_launch"], o["pst"]) for o in a]
+    assert all(o["one_launch"] and not o["pst"] for o in b)
+    for res in (a, b):
+        assert all(o["step"] == 8 for o in res)
+        for o in res[1:]:
+            torch.testing.assert_close(res[0]["master"], o["master"], rtol=0, atol=0)
+            torch.testing.assert_close(res[0]["metrics"], o["metrics"], rtol=0, atol=0)
+    for k in ("master", "m", "v"):
+        ref = b[0][k]
+        d = (a[0][k] - ref).abs().float()
+        scale = float(ref.abs().max())
+        ds = d.flatten().sort().values
+        q50, q999 = float(ds[len(ds) // 2]), float(ds[int(0.999 * (len(ds) - 1))])
+        print(f"[dp pst ws={ws}] {k}: max {float(ds[-1]):.3e} median {q50:.3e} p99.9 {q999:.3e} (scale {scale:.3e})")
+        assert q50 <= 1e-5 * scale and q999 <= 1e-4 * scale, (k, q50, q999)
+    torch.testing.assert_close(a[0]["metrics"], b[0]["metrics"], rtol=1e-5, atol=1e-3)
+
+
 @pytest.mark.parametrize("ws,fused,num_layers,eps,deep_fx,hidden", [
     (2, True, 2, 1e-8, "0", 512), (2, False, 2, 1e-8, "0", 512), (2, True, 4, 1e-8, "0", 512),
     (2, True, 2, 10.0, "0", 512), (2, True, 4, 10.0, "0", 512), (8, True, 2, 10.0, "0", 512),

@@ -172,13 +172,16 @@ def collectives(outdir):
     comm.close()
 
 
-def dp_xgmi(outdir, steps_eager=2, steps_graph=6, dp_ahead="1", num_layers=2, width=(784, 512)):
+def dp_xgmi(outdir, steps_eager=2, steps_graph=6, dp_ahead="1", num_layers=2, width=(784, 512), dp_pst="1", tag=""):
     """DP over the xGMI fused all-reduce+AdamW kernel (dropout off), fused step
     kernels, eager steps then multi-step graph replays.  ``dp_ahead`` = JDT_DP_AHEAD:
     "1" lets the step be one run-ahead launch with the in-kernel tile exchange where
     every rank's grid fits on the shared GPU, "0" keeps the three-launch step.
-    ``width`` = (input size, hidden size) of the classifier."""
+    ``width`` = (input size, hidden size) of the classifier.  ``dp_pst`` = JDT_DP_PST: "1"
+    lets a multi-step replay of the one-launch step be ONE persistent launch per rank (the
+    exchange inside every step, mlp2_pst_kernel TX), "0" one run-ahead launch per step."""
     os.environ["JDT_DP_AHEAD"] = dp_ahead
+    os.environ["JDT_DP_PST"] = dp_pst
     os.environ["JDT_DP_DEEP_TX"] = dp_ahead   # the deep engine's exchange path is opt-in: test it
     from data_paral import synthetic_batch
     from jax_distributed_tuts_amd.models.mlp import Classifier
@@ -203,9 +206,11 @@ def dp_xgmi(outdir, steps_eager=2, steps_graph=6, dp_ahead="1", num_layers=2, wi
     tr.run_steps(b, steps_graph)
     torch.cuda.synchronize()
     tr.finalize()
-    _save(outdir, "dpx", {"master": st.params.master.cpu(), "metrics": tr.metrics.cpu(), "comm": tr.comm_backend,
-                          "fused": tr.fused is not None, "step": int(st.opt_state["count"].item()),
-                          "one_launch": bool(tr.one_launch), "m": st.opt_state["m"].cpu()})
+    _save(outdir, "dpx" + tag, {"master": st.params.master.cpu(), "metrics": tr.metrics.cpu(),
+                                "comm": tr.comm_backend, "fused": tr.fused is not None,
+                                "step": int(st.opt_state["count"].item()), "one_launch": bool(tr.one_launch),
+                                "m": st.opt_state["m"].cpu(), "v": st.opt_state["v"].cpu(),
+                                "pst": bool(getattr(tr.fused, "pst_ok", False))})
 
 
 def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2, eps=1e-8, deep_fx="0", hidden=512):

@@ -90,7 +90,8 @@ struct Mlp2Args {
   long stage_stride;
   // deterministic mode (JDT_DETERMINISTIC=1): each column block of mlp2_fwd stores its
   // partial logits to det_logits[H/16][M][C] instead of fp32-atomically adding them;
-  // mlp2_bwd sums the partials in column-block order -> bitwise-reproducible steps
+  // mlp2_bwd sums the partials in column-block order -> bitwise-reproducible steps.  The
+  // run-ahead / persistent step (lg3) keeps one such set per step % 3: [3][H/16][M][C]
   float* det_logits;
   // run-ahead step (mlp2_bwd_kernel<..., AHEAD>): the backward launch of step t also runs
   // step t+1's forward, so a step is ONE launch.  XR: row-major bf16 copy of X written by
@@ -520,7 +521,8 @@ __device__ __forceinline__ void mlp2_fwd_body(AT& a, const int bx, const int by,
 #pragma unroll
       for (int n = 0; n < 16; ++n) s += htile[rl][n] * w2s[n][c];
       if (a.det_logits) {
-        a.det_logits[((long)by * M + row) * C + c] = s;
+        // run-ahead (lg3): one [H/16][M][C] partial set per step % 3, like the accumulators
+        a.det_logits[(((long)(a.lg3 ? step % 3 : 0) * (H / 16) + by) * M + row) * C + c] = s;
       } else if constexpr (LOOP) {
         // read after a grid barrier in this launch: a returning add proves it was performed
         const float old = __hip_atomic_fetch_add((gf32_t*)(lg + (long)row * C + c), s, __ATOMIC_RELAXED,
@@ -697,7 +699,24 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
   float lr0[C], lr1[C], lr2[AHEAD ? C : 1];
   {
     const long lo = (long)min(tid, M - 1) * C;
-    if constexpr (AHEAD) {   // step % 3 buffers, all three loaded (no wait on the step)
+    if (AHEAD && a.det_logits) {
+      // deterministic run-ahead / persistent: this step's per-column-block partial logits
+      // (step % 3 set, written by the previous forward epilogues -- write-through in a
+      // persistent launch) summed in column-block order; waits for the step (det mode only)
+      const int p3 = (PST ? step_in : step_lane) % 3;
+      const float* pb = a.det_logits + (long)p3 * (H / 16) * M * C + lo;
+#pragma unroll
+      for (int c = 0; c < C; ++c) lr0[c] = 0.f;
+      for (int q = 0; q < H / 16; ++q) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) lr0[c] += ld_f<PST>(pb + (long)q * M * C + c);
+      }
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        lr1[c] = lr0[c];
+        if constexpr (AHEAD) lr2[c] = lr0[c];
+      }
+    } else if constexpr (AHEAD) {   // step % 3 buffers, all three loaded (no wait on the step)
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         if constexpr (!PST) {
@@ -1545,7 +1564,13 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
       float sacc = b2A[c];
 #pragma unroll
       for (int n = 0; n < 16; ++n) sacc += htA[rl][n] * w2A[n][c];
-      if constexpr (PST) {
+      if (a.det_logits) {
+        // deterministic: this column block's partial (b2 in block 0's, as the forward
+        // kernel), summed in block order by the next step's backward
+        float* const dp = a.det_logits + (((long)((step + 1) % 3) * (H / 16) + bx) * M + r0 + rl) * C + c;
+        if constexpr (PST) st_f<true>(dp, sacc);   // read on other XCDs after the grid barrier
+        else *dp = sacc;
+      } else if constexpr (PST) {
         // returning atomics: the wait for the returned value is the proof that the add was
         // PERFORMED at the memory side (a no-return add's vmcnt acknowledgement is not), so
         // the grid barrier's arrival orders it before every reader of the next step; without
@@ -2054,7 +2079,7 @@ JDT_API int jdt_mlp2_pst(const Mlp2Args* args, int n, int k_in, unsigned* ws, lo
   const long long tmo = timeout > 0 ? timeout : 2000000ll;   // s_memrealtime ticks (100 MHz): 20 ms
   const Mlp2Args& a = *args;
   if (n == 1 || n < 0 || !ws || a.tx_fsdp || !a.fuse_opt || !a.W1T || !a.XR || !a.zslab || !a.ztick || !a.hand ||
-      !a.lg3 || a.det_logits || a.M <= 0 || a.M > 128 || a.H % 128 || (a.tx && !a.running))
+      !a.lg3 || a.M <= 0 || a.M > 128 || a.H % 128 || (a.tx && !a.running))
     return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool tx = a.tx != nullptr;
@@ -2144,8 +2169,7 @@ static int mlp2_launch(const Mlp2Args& a, int phase, hipStream_t st) {
   } else {
     // run-ahead backward: step t's backward + AdamW + step t+1's forward (needs the
     // fused optimizer, the W1^T copy, the X copy written by mlp2_fwd and lg3 logits)
-    if (!a.fuse_opt || !a.W1T || !a.XR || !a.zslab || !a.ztick || !a.hand || !a.lg3 || a.det_logits || a.M > 128 ||
-        a.H % 128)
+    if (!a.fuse_opt || !a.W1T || !a.XR || !a.zslab || !a.ztick || !a.hand || !a.lg3 || a.M > 128 || a.H % 128)
       return -3;
     const dim3 g(a.H / 16, NCH);
     if (a.tx && a.tx_fsdp)

@@ -219,20 +219,21 @@ class FusedMLP2:
         self._args = None
         self._key = None
         self.grad_stage = None   # (staging base pointer, half stride in floats): set_grad_stage
-        # deterministic mode: per-column-block partial logits instead of fp32 atomics
-        self.det_logits = (torch.zeros(H // 16, rows, 10, dtype=torch.float32, device=dev)
+        # deterministic mode: per-column-block partial logits instead of fp32 atomics, summed
+        # in block order (one set per step % 3 for the run-ahead / persistent step, which
+        # then runs in this mode too: the benchmarked kernel, bitwise reproducible)
+        self.det_logits = (torch.zeros(3, H // 16, rows, 10, dtype=torch.float32, device=dev)
                            if deterministic() else None)
         # run-ahead steps (one launch per step: step t's backward + AdamW + step t+1's
         # forward, csrc/mlp_fused.hip mlp2_bwd AHEAD); single GPU, fused AdamW only.
         # JDT_MLP2_AHEAD=0 turns it off (A/B)
-        self.ahead_ok = (self.fuse_opt and self.det_logits is None and self.W1T is not None
+        self.ahead_ok = (self.fuse_opt and self.W1T is not None
                          and os.environ.get("JDT_MLP2_AHEAD", "1") == "1"
                          and bool(_lib.lib().jdt_mlp2_ahead_ok(rows, H, K)))
         if tx is not None:
             from ..comm.tile_exchange import ahead_tx_ok
 
-            self.ahead_ok = (self.fuse_opt and self.det_logits is None and self.W1T is not None
-                             and ahead_tx_ok(rows, H, ranks_on_gpu, K))
+            self.ahead_ok = self.fuse_opt and self.W1T is not None and ahead_tx_ok(rows, H, ranks_on_gpu, K)
         self._ahead_args = None
         # host-side: the last launch on this engine was a run-ahead backward (set by
         # run_ahead / DataParallelTrainer after replaying a run-ahead graph)

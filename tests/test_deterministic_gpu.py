@@ -1,6 +1,7 @@
 """--deterministic (JDT_DETERMINISTIC=1): two identical runs give bitwise-identical
 parameters and metrics.  The fused engines then sum per-column-
-block partial logits in block order instead of with fp32 atomics."""
+block partial logits in block order instead of with fp32 atomics -- the 2-layer DP run
+is the headline path (run-ahead steps, persistent multi-step launch)."""
 import pytest
 import torch
 
@@ -26,6 +27,9 @@ def _dp_run(num_layers, steps=6):
     tr.finalize()
     torch.cuda.synchronize()
     assert tr.fused is not None and tr.fused.det_logits is not None
+    if num_layers == 2:
+        # the headline kernel: run-ahead steps, a 2-step replay as ONE persistent launch
+        assert tr.fused.ahead_ok and tr.fused.pst_ok and tr.multi is not None
     return st.params.master.cpu().clone(), tr.metrics.cpu().clone()
 
 

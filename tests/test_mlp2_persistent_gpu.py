@@ -88,6 +88,23 @@ def test_persistent_run_ahead_matches_per_step_launches(rows, monkeypatch):
     assert float(sd.max()) <= 2.0 ** -7 * float(res["0"]["shadow"].float().abs().max())
 
 
+@pytest.mark.parametrize("rows", [128, 64])
+def test_persistent_run_ahead_deterministic_is_bitwise_equal(rows, monkeypatch):
+    """--deterministic (JDT_DETERMINISTIC=1) runs the benchmarked kernels too: the forward
+    epilogues store per-column-block partial logits (one set per step % 3) that the next
+    step's backward sums in block order, so the persistent launch and the per-step
+    launches are bitwise equal -- parameters, both moments and metrics."""
+    from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
+
+    monkeypatch.setenv("JDT_DETERMINISTIC", "1")
+    g = torch.Generator().manual_seed(5)
+    b = Batch(torch.randn(rows, 784, generator=g).to(DEV),
+              torch.randint(0, 10, (rows,), generator=g).to(torch.int32).to(DEV))
+    res = {k: _run(b, k, adamw(1e-3), monkeypatch) for k in ("0", "1")}
+    for k in ("p", "m", "v", "metrics", "shadow"):
+        assert torch.equal(res["0"][k], res["1"][k]), (k, float((res["0"][k].float() - res["1"][k].float()).abs().max()))
+
+
 def test_persistent_run_ahead_sgd(monkeypatch):
     """The fused SGD (m / v alias p, never written) through the persistent launch."""
     from jax_distributed_tuts_amd.utils.train_state import Batch, sgd

@@ -5,13 +5,19 @@
 // at every teardown, a context's start-up self-test on 4 ranks sharing one GPU failed
 // about once in four runs (profiles/r5_ipc_pool.txt): after torch.cuda.synchronize the
 // rank's OWN freshly computed tensors kept changing -- foreign writes into pages this
-// process had just re-allocated.  Teardown was already collective (runtime.dist.quiesce:
-// no kernel of any rank in flight), so the writes came through a peer's mapping that
-// still resolved to the freed pages.  Keeping exported pages for the life of the process
-// removes the recycling; the pool is small (a few MB per context size).
+// process had just re-allocated.  Teardown was collective (runtime.dist.quiesce: no
+// kernel of any rank in flight), but each rank closed its peer mappings and freed its own
+// buffers in ONE call, so a rank could free (and re-allocate into torch) pages a slower
+// peer still had mapped.  Teardown is now two-phase (every rank closes its mappings of
+// the peers' pages, a barrier, then every rank releases its own: jdt_*_unmap, then
+// jdt_*_destroy), and the pool is an option on top (JDT_IPC_POOL, default on): a
+// released buffer is kept for the next context of the same size instead of going back to
+// the driver.  JDT_IPC_POOL=0 frees at release (tools/xgmi_churn.py measures both); the
+// pool frees instead of keeping once it holds more than JDT_IPC_POOL_MB (default 512).
 #include "common.h"
 #include "ipc_pool.h"
 
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -28,6 +34,22 @@ struct PoolBuf {
 std::mutex g_pool_mu;
 std::vector<PoolBuf> g_pool;
 
+bool pool_on() {
+  static const bool on = [] {
+    const char* e = getenv("JDT_IPC_POOL");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+size_t pool_cap_bytes() {
+  static const size_t cap = [] {
+    const char* e = getenv("JDT_IPC_POOL_MB");
+    const long mb = e ? atol(e) : 512;
+    return (size_t)(mb > 0 ? mb : 0) << 20;
+  }();
+  return cap;
+}
+
 }  // namespace
 
 hipError_t ipc_alloc(void** out, size_t bytes) {
@@ -36,11 +58,13 @@ hipError_t ipc_alloc(void** out, size_t bytes) {
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
   std::lock_guard<std::mutex> lk(g_pool_mu);
-  for (auto& b : g_pool) {
-    if (!b.used && b.bytes == bytes && b.dev == dev) {
-      b.used = true;
-      *out = b.p;
-      return hipSuccess;
+  if (pool_on()) {
+    for (auto& b : g_pool) {
+      if (!b.used && b.bytes == bytes && b.dev == dev) {
+        b.used = true;
+        *out = b.p;
+        return hipSuccess;
+      }
     }
   }
   void* p = nullptr;
@@ -54,11 +78,20 @@ hipError_t ipc_alloc(void** out, size_t bytes) {
 void ipc_release(void* p) {
   if (!p) return;
   std::lock_guard<std::mutex> lk(g_pool_mu);
-  for (auto& b : g_pool) {
-    if (b.p == p) {
-      b.used = false;
-      return;
+  size_t kept = 0;
+  for (const auto& b : g_pool)
+    if (!b.used) kept += b.bytes;
+  for (size_t i = 0; i < g_pool.size(); ++i) {
+    if (g_pool[i].p != p) continue;
+    if (pool_on() && kept + g_pool[i].bytes <= pool_cap_bytes()) {
+      g_pool[i].used = false;
+    } else {
+      // pool off or full: back to the driver (safe: teardown is two-phase, every peer has
+      // closed its mapping of these pages before any rank releases them)
+      (void)hipFree(g_pool[i].p);
+      g_pool.erase(g_pool.begin() + (long)i);
     }
+    return;
   }
 }
 

@@ -231,7 +231,8 @@ JDT_API int jdt_p2p_reset(void* ctx) {
   return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 
-JDT_API int jdt_p2p_destroy(void* ctx) {
+// Teardown phase 1 (see jdt_xgmi_unmap): close this rank's mappings of its peers' pages.
+JDT_API int jdt_p2p_unmap(void* ctx) {
   P2PCtx* c = static_cast<P2PCtx*>(ctx);
   if (!c) return 0;
   (void)hipDeviceSynchronize();
@@ -240,8 +241,18 @@ JDT_API int jdt_p2p_destroy(void* ctx) {
       if (q == c->rank) continue;
       if (c->peers.inbox[q]) (void)hipIpcCloseMemHandle(c->peers.inbox[q]);
       if (c->peers.sig[q]) (void)hipIpcCloseMemHandle(c->peers.sig[q]);
+      c->peers.inbox[q] = nullptr;
+      c->peers.sig[q] = nullptr;
     }
+    c->opened = false;
   }
+  return 0;
+}
+
+JDT_API int jdt_p2p_destroy(void* ctx) {
+  P2PCtx* c = static_cast<P2PCtx*>(ctx);
+  if (!c) return 0;
+  (void)jdt_p2p_unmap(ctx);
   ipc_release(c->inbox);
   ipc_release(c->sig);
   delete c;

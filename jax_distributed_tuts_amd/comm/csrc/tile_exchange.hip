@@ -126,7 +126,8 @@ JDT_API int jdt_tx_reset(void* ctx) {
   return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 
-JDT_API void jdt_tx_close(void* ctx) {
+// Teardown phase 1 (see jdt_xgmi_unmap): close this rank's mappings of its peers' pages.
+JDT_API void jdt_tx_unmap(void* ctx) {
   TxCtx* c = static_cast<TxCtx*>(ctx);
   if (!c) return;
   (void)hipDeviceSynchronize();
@@ -135,7 +136,16 @@ JDT_API void jdt_tx_close(void* ctx) {
     if (c->host.part[q]) (void)hipIpcCloseMemHandle(c->host.part[q]);
     if (c->host.red[q]) (void)hipIpcCloseMemHandle(c->host.red[q]);
     if (c->host.flag[q]) (void)hipIpcCloseMemHandle(c->host.flag[q]);
+    c->host.part[q] = c->host.red[q] = nullptr;
+    c->host.flag[q] = nullptr;
   }
+  c->opened = false;
+}
+
+JDT_API void jdt_tx_close(void* ctx) {
+  TxCtx* c = static_cast<TxCtx*>(ctx);
+  if (!c) return;
+  jdt_tx_unmap(ctx);
   ipc_release(c->part);
   ipc_release(c->red);
   ipc_release(c->flag);

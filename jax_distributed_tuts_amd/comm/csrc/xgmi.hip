@@ -1307,7 +1307,11 @@ JDT_API int jdt_xgmi_error(void* ctx) {
   return e;
 }
 
-JDT_API int jdt_xgmi_destroy(void* ctx) {
+// Teardown phase 1 (collective with phase 2 through a barrier, comm/xgmi.py close): drain
+// this rank's queue and close its mappings of the peers' buffers.  Only after EVERY rank
+// did so does any rank release its own exported buffers (jdt_xgmi_destroy), so no peer
+// mapping outlives the pages it resolves to.
+JDT_API int jdt_xgmi_unmap(void* ctx) {
   XgCtx* c = static_cast<XgCtx*>(ctx);
   if (!c) return 0;
   (void)hipDeviceSynchronize();
@@ -1317,8 +1321,18 @@ JDT_API int jdt_xgmi_destroy(void* ctx) {
       if (c->peers.data[q]) (void)hipIpcCloseMemHandle(c->peers.data[q]);
       if (c->peers.tmp[q]) (void)hipIpcCloseMemHandle(c->peers.tmp[q]);
       if (c->peers.sig[q]) (void)hipIpcCloseMemHandle(c->peers.sig[q]);
+      c->peers.data[q] = c->peers.tmp[q] = nullptr;
+      c->peers.sig[q] = nullptr;
     }
+    c->opened = false;
   }
+  return 0;
+}
+
+JDT_API int jdt_xgmi_destroy(void* ctx) {
+  XgCtx* c = static_cast<XgCtx*>(ctx);
+  if (!c) return 0;
+  (void)jdt_xgmi_unmap(ctx);   // one-phase fallback (garbage collection): unmap, then release
   ipc_release(c->data);
   ipc_release(c->tmp);
   ipc_release(c->sig);

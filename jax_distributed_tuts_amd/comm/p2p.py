@@ -39,6 +39,7 @@ _lib.declare("jdt_p2p_slot_bytes", c_long, [c_void_p])
 _lib.declare("jdt_p2p_error", c_int, [c_void_p])
 _lib.declare("jdt_p2p_reset", c_int, [c_void_p])
 _lib.declare("jdt_p2p_destroy", c_int, [c_void_p])
+_lib.declare("jdt_p2p_unmap", c_int, [c_void_p])
 
 
 def wire_bytes(t: torch.Tensor) -> int:
@@ -118,15 +119,21 @@ class XgmiP2P:
         """1 if a receive of this rank timed out (synchronises the device)."""
         return int(_lib.lib().jdt_p2p_error(self.ctx)) if self.ctx else 0
 
-    def close(self):
+    def close(self, collective: bool = True):
+        """Two-phase teardown (collective over the pipe group; comm/xgmi.py close)."""
         if self.ctx:
+            if collective:
+                from .xgmi import ipc_teardown_barrier
+
+                _lib.lib().jdt_p2p_unmap(self.ctx)
+                ipc_teardown_barrier(self.group)
             _lib.lib().jdt_p2p_destroy(self.ctx)
             self.ctx = c_void_p()
         self.ok = False
 
     def __del__(self):
         try:
-            self.close()
+            self.close(collective=False)
         except Exception:
             pass
 

@@ -38,6 +38,7 @@ _lib.declare("jdt_tx_create", c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER
 _lib.declare("jdt_tx_open", c_int, [c_void_p, c_void_p, c_longlong])
 _lib.declare("jdt_tx_args", c_void_p, [c_void_p])
 _lib.declare("jdt_tx_close", None, [c_void_p])
+_lib.declare("jdt_tx_unmap", None, [c_void_p])
 _lib.declare("jdt_mlp2_ahead_tx_ok", c_int, [c_int, c_int, c_int, c_int])
 _lib.declare("jdt_tx_selftest", c_int, [c_void_p, c_int, ctypes.c_uint, c_void_p, c_void_p])
 _lib.declare("jdt_tx_reset", c_int, [c_void_p])
@@ -114,8 +115,14 @@ class TileExchange:
         """This rank's error word (4: an exchange wait timed out; synchronous read)."""
         return int(_lib.lib().jdt_tx_error(self.ctx)) if self.ctx else 0
 
-    def close(self):
+    def close(self, collective: bool = True):
+        """Two-phase teardown (collective over the group; comm/xgmi.py close)."""
         if self.ctx:
+            if collective:
+                from .xgmi import ipc_teardown_barrier
+
+                _lib.lib().jdt_tx_unmap(self.ctx)
+                ipc_teardown_barrier(self.group)
             _lib.lib().jdt_tx_close(self.ctx)
             self.ctx = c_void_p()
         self.ok = False

@@ -112,6 +112,21 @@ _lib.declare("jdt_xgmi_stage_clear", c_int, [c_void_p, c_void_p])
 _lib.declare("jdt_xgmi_allreduce_staged", c_int, [c_void_p, c_long, c_long, ctypes.POINTER(XgAdam), c_longlong,
                                                   c_void_p])
 _lib.declare("jdt_xgmi_destroy", c_int, [c_void_p])
+_lib.declare("jdt_xgmi_unmap", c_int, [c_void_p])
+
+
+def ipc_teardown_barrier(group):
+    """The barrier between the two phases of a comm context's teardown: every rank of
+    ``group`` has closed its mappings of the peers' buffers before any rank releases its
+    own (a gloo group's barrier runs on the host; nccl's on the device)."""
+    if group is None or not dist.is_initialized():
+        return
+    if dist.get_backend(group) == "nccl":
+        from ..runtime.dist import device
+
+        dist.barrier(group=group, device_ids=[device().index])
+    else:
+        dist.barrier(group=group)
 _lib.declare("jdt_xgmi_seg_slice", c_long, [c_long])
 _lib.declare("jdt_ipc_pool_stats", None, [c_void_p])
 
@@ -299,15 +314,22 @@ class XgmiComm:
         if info is not None:
             raise RuntimeError(f"xgmi collective timed out on this rank (peer dead or desynchronised): {info}")
 
-    def close(self):
+    def close(self, collective: bool = True):
+        """Two-phase teardown (collective over the context's group): every rank closes its
+        mappings of the peers' buffers, a barrier, then every rank releases its own -- no
+        peer mapping outlives the pages it resolves to (comm/csrc/ipc_pool.hip).
+        ``collective=False`` (garbage collection): one phase, this rank only."""
         if self.ctx:
+            if collective:
+                _lib.lib().jdt_xgmi_unmap(self.ctx)
+                ipc_teardown_barrier(self.group)
             _lib.lib().jdt_xgmi_destroy(self.ctx)
             self.ctx = c_void_p()
         self.ok = False
 
     def __del__(self):
         try:
-            self.close()
+            self.close(collective=False)
         except Exception:
             pass
 

@@ -57,3 +57,21 @@ def test_contexts_reuse_pooled_buffers():
     L.jdt_xgmi_destroy(ctx3)
     L.jdt_xgmi_destroy(ctx2)
     assert X.ipc_pool_stats()["in_use"] == s0["in_use"]
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+def test_two_phase_teardown_without_pool(tmp_path, ws):
+    """Contexts churned with the pool OFF (exported pages back to the driver at every
+    teardown) and torch tensors allocated in between: with the two-phase teardown (every
+    rank unmaps its peers' pages, a barrier, then every rank frees its own) no self-test
+    fails and no canary tensor is written -- the round-5 failure mode (4 ranks, one-call
+    teardown) was a rank's own fresh tensors changing under it."""
+    from jax_distributed_tuts_amd.runtime.launch import spawn
+
+    from . import xgmi_workers as XW
+    from .test_xgmi_gpu import _load
+
+    spawn(XW.ipc_churn, ws, str(tmp_path), gpu=True)
+    for r, o in enumerate(_load(tmp_path, "churn", ws)):
+        assert o["fails"] == 0 and o["bad"] == 0, (r, o)
+        assert o["pool_in_use"] == 0 and o["pool_buffers"] == 0, (r, o)   # nothing kept with the pool off

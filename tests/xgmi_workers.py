@@ -2,6 +2,7 @@
 of the test box (gloo process group for the bootstrap), which exercises the
 whole IPC path of comm/xgmi.py -- handle export/open, per-block epoch barriers
 across processes, both buffer parities, graph capture -- on real hardware."""
+import ctypes
 import os
 
 import torch
@@ -548,3 +549,40 @@ def grad_probe_xgmi(outdir, kind, dp=1, capture=True, n_hidden=3):
         raise ValueError(kind)
     torch.cuda.synchronize()
     _save(outdir, f"gpx_{kind}", {"before": before, "after": after, "comm": comm, **extra})
+
+
+def ipc_churn(outdir, iters=6, pool="0"):
+    """Comm contexts built, used and torn down (two-phase) in a loop with torch tensors
+    allocated between them (canaries), the exported-buffer pool OFF: every self-test must
+    pass and no canary may change (a write through a stale peer mapping would)."""
+    os.environ["JDT_IPC_POOL"] = pool
+    import torch.distributed as dist
+
+    from jax_distributed_tuts_amd.comm import xgmi as X
+    from jax_distributed_tuts_amd.ops import _lib
+    from jax_distributed_tuts_amd.runtime import dist as D
+
+    dev = D.device()
+    rank, world = D.rank(), D.world_size()
+    X.size_grids_for_sharing(dev)
+    fails = bad = 0
+    held = []
+    for it in range(iters):
+        c = X.XgmiComm(dist.group.WORLD, rank, world, 408_576, dev, timeout_s=D.spin_timeout_s(30.0))
+        fails += int(not c.ok)
+        if c.ok:
+            x = torch.ones(407_054, device=dev) * (rank + 1)
+            for _ in range(20):
+                c.all_reduce_(x)
+        torch.cuda.synchronize(dev)
+        bad += sum(int(not bool((t == v).all())) for t, v in held)
+        D.quiesce(dev)
+        c.close()
+        held = []
+        for k, n in enumerate((1 << 17, 1 << 19, 1 << 21)):
+            v = float(100 * it + 10 * k + rank + 1)
+            held.append((torch.full((n,), v, device=dev), v))
+        D.barrier()
+    st = (ctypes.c_long * 3)()
+    _lib.lib().jdt_ipc_pool_stats(st)
+    _save(outdir, "churn", {"fails": fails, "bad": bad, "pool_buffers": int(st[0]), "pool_in_use": int(st[2])})

@@ -1,4 +1,5 @@
-"""Grid barrier vs kernel boundary on this GPU (ops/csrc/barrier_lab.hip).
+"""Grid barrier vs kernel boundary on this GPU (tools/barrier_lab/barrier_lab.hip, a lab
+kernel built into its own library here, not into the production kernel library).
 
 The headline step is one run-ahead launch per step; a persistent n-step launch would
 replace each launch boundary with a grid barrier.  This times, at the headline grid
@@ -23,8 +24,23 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from jax_distributed_tuts_amd.ops import _lib  # noqa: E402
 
-_lib.declare("jdt_barrier_lab", c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_longlong, c_void_p])
-_lib.declare("jdt_boundary_lab", c_int, [c_int, c_void_p, c_void_p])
+LAB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "barrier_lab")
+
+
+def lab_lib():
+    """Build (hipcc, gfx950) and load tools/barrier_lab/libbarrier_lab.so."""
+    import subprocess
+
+    src, so = os.path.join(LAB, "barrier_lab.hip"), os.path.join(LAB, "libbarrier_lab.so")
+    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+        inc = os.path.join(os.path.dirname(LAB), "..", "jax_distributed_tuts_amd", "ops", "csrc")
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                        f"-I{inc}", src, "-o", so], check=True)
+    L = ctypes.CDLL(so)
+    L.jdt_barrier_lab.restype, L.jdt_barrier_lab.argtypes = c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                                                    c_void_p, c_longlong, c_void_p]
+    L.jdt_boundary_lab.restype, L.jdt_boundary_lab.argtypes = c_int, [c_int, c_void_p, c_void_p]
+    return L
 
 
 def timed(fn, reps=5):
@@ -46,7 +62,8 @@ def main():
     ap.add_argument("--iters", type=int, default=1024)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    L = _lib.lib()
+    _lib.lib()
+    L = lab_lib()
     ctr = torch.zeros(16 * 32, dtype=torch.int32, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     sink = torch.zeros(1024, device=dev)

@@ -242,7 +242,7 @@ class GPipeTrainer:
         self._deep_tried = False
         self.pp_kernel = None          # the in-kernel GPipe step (parallel/pp_kernel.py)
         self._pp_kernel_tried = False
-        self._pp_kernel_stale = False  # a checkpoint restore moved the step counter: rebuild it
+        self._handoffs_stale = False   # a checkpoint restore moved the step counter: rebuild them
         from ..utils.checkpoint import bind_trainer
 
         bind_trainer(state, self)
@@ -319,28 +319,31 @@ class GPipeTrainer:
         return f"data:{dp},pipe:{pipe}"
 
     # ------------------------------------------------------------------ step
-    def _drop_stale_pp_kernel(self):
-        """After a restore (``invalidate``): the stage engine's in-kernel waits pass once a
-        flag is >= the step epoch, and its inbox / weight-box / counter words still hold the
-        epochs of steps the restore rolled back -- every wait would pass at once on stale
-        hand-offs.  Drop it so the next step rebuilds it from zeroed buffers.  Collective
-        (every rank restores, then steps or captures); quiesce first so no peer still
-        writes into the old inboxes.  Never called inside a stream capture."""
-        if not self._pp_kernel_stale:
+    def _drop_stale_handoffs(self):
+        """After a restore (``invalidate``): the stage hand-offs wait until a flag is >= the
+        step epoch -- the in-kernel GPipe engine's inbox / weight-box / counter words and the
+        per-tick xGMI inbox (comm/p2p.py, epoch = the device step) -- and their flags still
+        hold the epochs of steps the restore rolled back, so every wait would pass at once
+        on stale data.  Drop both so the next step rebuilds them from zeroed buffers.
+        Collective (every rank restores, then steps or captures); quiesce first so no peer
+        still writes into the old inboxes.  Never called inside a stream capture."""
+        if not self._handoffs_stale:
             return
         from ..runtime.dist import quiesce
 
-        self._pp_kernel_stale = False
+        self._handoffs_stale = False
         quiesce(self.dev)
-        self.pp_kernel.close()
-        self.pp_kernel = None
-        self._pp_kernel_tried = False
+        for r in (self.pp_kernel, self.p2p):
+            if r is not None:
+                r.close()
+        self.pp_kernel = self.p2p = None
+        self._pp_kernel_tried = self._p2p_tried = False
 
     def _pp_kernel_engine(self, mb: int, seed: int):
         """The whole stage step as one persistent launch (parallel/pp_kernel.py), when
         every stage of the pipe axis can run it (collective on first use); with a pipe
         axis of size 1, the one-GPU chain: every layer of the MLP a stage of one launch."""
-        self._drop_stale_pp_kernel()
+        self._drop_stale_handoffs()
         if not self._pp_kernel_tried:
             self._pp_kernel_tried = True
             if self.S == 1 and self.dev.type == "cuda":
@@ -653,8 +656,8 @@ class GPipeTrainer:
         self._engine_tried = False
         self.deep_engine = None
         self._deep_tried = False
-        if self.pp_kernel is not None:
-            self._pp_kernel_stale = True   # rebuilt (zeroed hand-off flags, new seed) at the next step
+        if self.pp_kernel is not None or self.p2p is not None:
+            self._handoffs_stale = True   # rebuilt (zeroed hand-off flags, new seed) at the next step
 
     def _single_stage_engine(self, rows: int, mb: int):
         """One stage holding the whole MLP (pipe axis of size 1): GPipe's fill/drain
@@ -830,7 +833,7 @@ class GPipeTrainer:
         if not self.capturable:
             raise RuntimeError("pipeline step is not capturable (host-driven collectives)")
         self._static = batch
-        self._drop_stale_pp_kernel()   # a restore since the last step: rebuild outside the capture
+        self._drop_stale_handoffs()   # a restore since the last step: rebuild outside the capture
 
         def body():
             self._compute(batch)

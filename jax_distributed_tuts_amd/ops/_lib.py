@@ -58,6 +58,10 @@ _SIGS = {
     "jdt_gemm": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p]),
     "jdt_gemm_args_size": (c_int, []),
     "jdt_gemm_group": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_void_p, c_long, c_void_p, c_long, c_void_p]),
+    "jdt_gemm_wpass_table_bytes": (c_int, []),
+    "jdt_gemm_wpass_plan": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_int, c_void_p, c_void_p, c_long, c_void_p,
+                                    c_long]),
+    "jdt_gemm_wpass_launch": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "jdt_gemm_set_group_split": (None, [c_int]),
     "jdt_gemm_set_group_tile": (None, [c_int]),
     "jdt_ln_set_rows": (None, [c_int]),

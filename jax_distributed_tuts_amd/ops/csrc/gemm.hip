@@ -1483,6 +1483,134 @@ __global__ void __launch_bounds__(256) gemm_dma_group_kernel(GemmGroup G) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// The W pass in ONE launch (transformer stages, models/transformer.py weight_grads):
+// every deferred weight-gradient GEMM of a step, dW_p = A_p^T B_p with both operands
+// token-major (A_p = a layer's input [T][M_p], B_p = its output gradient [T][N_p],
+// K = T tokens), AdamW in the vectorised epilogue.  Workgroups pick their problem from a
+// prefix table in DEVICE memory (17 GemmArgs do not fit a kernel-argument block); the
+// main loop is gemm_dma_kernel's for two transposed operands (LDS-DMA ring, counted
+// vmcnt, ds_read_b64_tr_b16 fragments).  Replaces 17 launches round-robin over the
+// microbatch streams: the GEMMs' tiles fill the chip side by side instead of each
+// stream's small GEMMs queueing behind its large ones, and the AdamW epilogues of one
+// problem overlap the main loops of the others.
+constexpr int WP_MAX = 40;
+struct GemmWTable {
+  int n, total;
+  int start[WP_MAX + 1];
+  int tiles_n[WP_MAX];
+  int splits[WP_MAX];
+  long wsoff[WP_MAX];
+  int cntoff[WP_MAX];
+  float* ws;
+  unsigned* counters;
+  GemmArgs g[WP_MAX];
+};
+
+template <int TM, int TN, int MF, int S>
+__global__ void __launch_bounds__(256) gemm_wpass_kernel(const GemmWTable* __restrict__ T) {
+  constexpr int WM = 2, WN = 2, NW = 4;
+  constexpr int BM = WM * TM * MF, BN = WN * TN * MF, BK = DMA_BK;
+  constexpr int STAGE = (BM + BN) * BK;
+  constexpr int LPW = (BM + BN) / (8 * NW);   // glds per wave per K-tile
+  static_assert((S - 2) * LPW <= 63, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) bf16_t smem[S * STAGE];
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid % 8, q = nwg / 8, rr = nwg % 8;
+    bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + bid / 8;
+  }
+  // the problem: scalar loads of the prefix table (wave-uniform address)
+  const int n = T->n;
+  int p = 0;
+  for (int t = 1; t < n; ++t)
+    if (bid >= T->start[t]) p = t;
+  p = __builtin_amdgcn_readfirstlane(p);
+  const GemmArgs& g = T->g[p];
+  const int tn = T->tiles_n[p], sp = T->splits[p];
+  const int tiles_p = (g.M / BM) * tn;
+  const int local = bid - T->start[p];
+  const int tile = local % tiles_p, split = local / tiles_p;
+  const int tm0 = (tile / tn) * BM, tn0 = (tile % tn) * BN;
+  const int kchunk = g.K / sp, kbeg = split * kchunk;   // host: kchunk % 64 == 0
+  const bf16_t* Ab = static_cast<const bf16_t*>(g.A) + tm0;   // "km": A[k][m] at k * lda + m
+  const bf16_t* Bb = static_cast<const bf16_t*>(g.B) + tn0;   // "kn": B[k][n] at k * ldb + n
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int nkt = kchunk / BK;
+  using acc_t = typename std::conditional<MF == 32, f32x16, f32x4>::type;
+  acc_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < (MF == 32 ? 16 : 4); ++e) acc[i][j][e] = 0.f;
+  auto issue = [&](int kt) {
+    bf16_t* st = smem + (kt % S) * STAGE;
+    const int k0 = kbeg + kt * BK;
+    stage_op<BM, true, NW>(Ab, g.lda, k0, st, wid, lane);
+    stage_op<BN, true, NW>(Bb, g.ldb, k0, st + BM * BK, wid, lane);
+  };
+#pragma unroll
+  for (int s2 = 0; s2 < S - 1; ++s2)
+    if (s2 < nkt) issue(s2);
+  for (int kt = 0; kt < nkt; ++kt) {
+    dma_wait_barrier<LPW, S - 2>(min(S - 2, nkt - 1 - kt));
+    if (kt + S - 1 < nkt) issue(kt + S - 1);
+    const bf16_t* As = smem + (kt % S) * STAGE;
+    const bf16_t* Bs = As + BM * BK;
+    if constexpr (MF == 32) {
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 16) {
+        bf16x8 af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = frag_op32<BM>(As, true, (wm * TM + i) * 32, kk, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j] = frag_op32<BN>(Bs, true, (wn * TN + j) * 32, kk, lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // asm tr reads retired (gemm_dma_kernel)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(af[i]));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(bfr[j]));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma32x32x16(af[i], bfr[j], acc[i][j]);
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 32) {
+        bf16x8 af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = frag_op<BM>(As, true, (wm * TM + i) * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j] = frag_op<BN>(Bs, true, (wn * TN + j) * 16, kk, lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(af[i]));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(bfr[j]));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
+      }
+    }
+  }
+  __syncthreads();
+  static_assert((BM * (BN + 4) + 4) * 4 <= S * STAGE * 2, "output image fits the staging ring");
+  float* const wsp = sp > 1 ? T->ws + T->wsoff[p] : nullptr;
+  unsigned* const cnt = sp > 1 ? T->counters + T->cntoff[p] : nullptr;
+  if constexpr (MF == 32)
+    gemm_finish_vec32<BM, BN, TM, TN>(g, acc, tm0, tn0, 0, wm, wn, lane, tid, sp, split, tile, wsp, cnt,
+                                      reinterpret_cast<float*>(smem));
+  else
+    gemm_finish_vec<BM, BN, TM, TN>(g, acc, tm0, tn0, 0, wm, wn, lane, tid, sp, split, tile, wsp, cnt,
+                                    reinterpret_cast<float*>(smem));
+}
+
 // Exact-slice depth: K-tiles a slice may hold in registers (~128 VGPRs of
 // staged bf16 operands) and in one LDS image (<= 160 KB).
 template <int WM, int WN, int TM, int TN, int BK>
@@ -2103,3 +2231,76 @@ JDT_API int jdt_gemm_group(const GemmArgs* gs, int n, float* ws, long ws_floats,
 JDT_API void jdt_gemm_set_group_split(int on) { g_group_split = on; }
 JDT_API void jdt_gemm_set_group_m(int gm) { g_group_m = gm; }
 JDT_API void jdt_gemm_set_group_tile(int t) { g_group_tile = t; }
+
+// The W pass (gemm_wpass_kernel): plan the prefix table of `n` weight-gradient problems
+// into `out` (host memory; the caller copies it to the device once and replays it) for
+// tile config `cfg` (0: 64 x 64 of 16x16x32 MFMAs, 1: 64 x 64 of 32x32x16, 2: 128 x 128
+// of 32x32x16, 3: 32 x 64).  Split-K per problem while the whole launch has fewer than
+// two workgroups per CU.  Returns the workgroup count, or < 0 outside the envelope (a
+// problem not "km" x "kn" bf16 with 16-byte aligned operands and fp32 output rows, a
+// shape not a multiple of the tile, K not a multiple of 64, > WP_MAX problems).
+template <int BM, int BN>
+static int wpass_plan(const GemmArgs* gs, int n, GemmWTable* out, float* ws, long ws_floats, unsigned* counters,
+                      long n_counters) {
+  if (n <= 0 || n > WP_MAX) return -2;
+  auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  long tiles_all = 0;
+  for (int p = 0; p < n; ++p) {
+    const GemmArgs& g = gs[p];
+    if (!g.a_trans || !g.b_trans || g.a_f32 || g.b_f32 || !g.c_f32 || g.M % BM || g.N % BN || g.K % DMA_BK ||
+        !al(g.A) || !al(g.B) || g.lda % 8 || g.ldb % 8 || !epi_vec_ok(g, 1) || g.Zin || g.Zout || g.resid ||
+        g.keep_prob < 1.f)
+      return -2;
+    tiles_all += (long)(g.M / BM) * (g.N / BN);
+  }
+  int total = 0;
+  long wsused = 0, cntused = 0;
+  out->n = n;
+  out->ws = ws;
+  out->counters = counters;
+  for (int p = 0; p < n; ++p) {
+    const GemmArgs& g = gs[p];
+    out->g[p] = g;
+    out->tiles_n[p] = g.N / BN;
+    out->start[p] = total;
+    const long tiles = (long)(g.M / BM) * (g.N / BN);
+    int sp = 1;
+    while (sp < 8 && tiles_all * sp < 512 && (g.K / (2 * sp)) % DMA_BK == 0 && g.K / (2 * sp) >= 8 * DMA_BK) sp *= 2;
+    if (sp > 1 && (!ws || !counters || wsused + tiles * sp * BM * BN > ws_floats || cntused + tiles > n_counters))
+      sp = 1;
+    out->splits[p] = sp;
+    out->wsoff[p] = wsused;
+    out->cntoff[p] = (int)cntused;
+    if (sp > 1) { wsused += tiles * sp * BM * BN; cntused += tiles; }
+    total += (int)(tiles * sp);
+  }
+  out->start[n] = total;
+  out->total = total;
+  return total;
+}
+
+JDT_API int jdt_gemm_wpass_table_bytes() { return (int)sizeof(GemmWTable); }
+JDT_API int jdt_gemm_wpass_plan(const GemmArgs* gs, int n, int cfg, void* out, float* ws, long ws_floats,
+                                unsigned* counters, long n_counters) {
+  GemmWTable* t = static_cast<GemmWTable*>(out);
+  switch (cfg) {
+    case 0: case 1: return wpass_plan<64, 64>(gs, n, t, ws, ws_floats, counters, n_counters);
+    case 2: return wpass_plan<128, 128>(gs, n, t, ws, ws_floats, counters, n_counters);
+    case 3: return wpass_plan<32, 64>(gs, n, t, ws, ws_floats, counters, n_counters);
+    default: return -2;
+  }
+}
+// launch the planned table (device copy) with `total` workgroups
+JDT_API int jdt_gemm_wpass_launch(const void* table_dev, int total, int cfg, void* stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const GemmWTable* t = static_cast<const GemmWTable*>(table_dev);
+  if (total <= 0) return 0;
+  switch (cfg) {
+    case 0: hipLaunchKernelGGL((gemm_wpass_kernel<2, 2, 16, 3>), dim3(total), dim3(256), 0, st, t); break;
+    case 1: hipLaunchKernelGGL((gemm_wpass_kernel<1, 1, 32, 3>), dim3(total), dim3(256), 0, st, t); break;
+    case 2: hipLaunchKernelGGL((gemm_wpass_kernel<2, 2, 32, 3>), dim3(total), dim3(256), 0, st, t); break;
+    case 3: hipLaunchKernelGGL((gemm_wpass_kernel<1, 2, 16, 3>), dim3(total), dim3(256), 0, st, t); break;
+    default: return -2;
+  }
+  return HIP_LAUNCH_CHECK();
+}

@@ -379,6 +379,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, *, a_layout: str = "mk", b_layout: st
         g.opt_lr, g.opt_b1, g.opt_b2, g.opt_eps, g.opt_wd, g.opt_gs = (float(tx.learning_rate), float(tx.b1),
                                                                        float(tx.b2), float(tx.eps),
                                                                        float(tx.weight_decay), eo.grad_scale)
+    if _WPASS and not batched and cfg < 0 and splits < 0:
+        _WPASS[-1].append((g, a.device, (a, b, out, bias, z_out, z_in, resid, dbias, step, seed_dev)))
+        return out
     if _GROUP and not batched and cfg < 0 and splits < 0:
         _GROUP[-1].append((g, a.device, (a, b, out, bias, z_out, z_in, resid, dbias, step, seed_dev)))
         return out
@@ -395,6 +398,53 @@ def _launch_gemm(g, batch: int, cfg: int, splits: int, device):
 
 
 _GROUP: list = []
+_WPASS: list = []
+_WPASS_PLANS: dict = {}
+WPASS_CFG = int(os.environ.get("JDT_WPASS_CFG", "0"))
+
+
+@contextlib.contextmanager
+def gemm_wpass(cfg: Optional[int] = None):
+    """GPU GEMMs issued inside the block -- a stage's deferred weight-gradient GEMMs
+    dW (+)= A^T dZ, both operands token-major, AdamW in their epilogues -- run at its end as
+    ONE launch (csrc/gemm.hip ``gemm_wpass_kernel``: every problem's tiles in one grid,
+    problems picked from a prefix table in device memory).  The table is planned and
+    uploaded on the first (eager) use of a problem set and reused by later calls and graph
+    replays; a set first seen inside a stream capture, or outside the kernel's envelope,
+    launches problem by problem (same results)."""
+    _WPASS.append([])
+    try:
+        yield
+    finally:
+        items = _WPASS.pop()
+        if items:
+            _launch_wpass(items, WPASS_CFG if cfg is None else int(cfg))
+
+
+def _launch_wpass(items, cfg: int):
+    L = _lib.lib()
+    dev = items[0][1]
+    arr = (_lib.GemmArgs * len(items))(*[it[0] for it in items])
+    # (the plan embeds the planning stream's split-K workspace; a W pass runs on one
+    # stream at a time, and a graph capture replays the eager plan)
+    key = (bytes(arr), cfg)
+    plan = _WPASS_PLANS.get(key)
+    if plan is None and not torch.cuda.is_current_stream_capturing():
+        ws, ctr = workspace(dev)
+        host = (ctypes.c_char * int(L.jdt_gemm_wpass_table_bytes()))()
+        total = int(L.jdt_gemm_wpass_plan(arr, len(items), int(cfg), host, ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                                          ctypes.c_void_p(ctr.data_ptr()), ctr.numel()))
+        table = None
+        if total > 0:
+            table = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(dev)
+        plan = _WPASS_PLANS[key] = (table, total)
+    if plan is None or plan[0] is None:
+        for g, d, _refs in items:
+            _launch_gemm(g, 1, -1, -1, d)
+        return
+    table, total = plan
+    _lib.check(L.jdt_gemm_wpass_launch(ctypes.c_void_p(table.data_ptr()), total, int(cfg), _lib.stream_ptr()),
+               "jdt_gemm_wpass")
 
 
 @contextlib.contextmanager

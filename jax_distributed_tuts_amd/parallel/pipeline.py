@@ -149,6 +149,10 @@ class PipeConfig:
     # ... the W pass after the join round-robin over the first wpass_rr microbatch streams
     # (0: all of them; measured 1 stream 1.27 ms, 2: 1.12, 3-4: 1.07-1.09)
     wpass_rr: int = field(default_factory=lambda: int(os.environ.get("JDT_WPASS_STREAMS", "0")))
+    # GPU: the deferred W pass (every weight-gradient GEMM of the step, AdamW in the
+    # epilogues) as ONE launch (ops.kernels.gemm_wpass, csrc/gemm.hip gemm_wpass_kernel)
+    # instead of one GEMM per weight round-robin over streams
+    wpass_one_launch: bool = field(default_factory=lambda: os.environ.get("JDT_WPASS_ONE", "1") == "1")
     # S > 1 (xGMI inbox hand-offs): microbatch chains of a stage on concurrent streams
     # (mb_streams of them) -- opt-in, see GPipeTrainer._streams_ok
     multi_stage_streams: bool = field(default_factory=lambda: os.environ.get("JDT_PP_STREAMS", "0") == "1")
@@ -459,9 +463,17 @@ class GPipeTrainer:
             # rows (the GEMMs round-robin over the streams once every chain has finished)
             on.join()
             on.fork()
-            nw = max(1, int(self.cfg.wpass_rr) or len(on.side) + 1)
-            self.model.weight_grads(P, arena, wgrad=self.wgrad, opt=eo, on=lambda j: on(j % nw))
+            if self._wpass_one_ok():
+                with K.gemm_wpass():   # one launch on the main stream
+                    self.model.weight_grads(P, arena, opt=eo)
+            else:
+                nw = max(1, int(self.cfg.wpass_rr) or len(on.side) + 1)
+                self.model.weight_grads(P, arena, wgrad=self.wgrad, opt=eo, on=lambda j: on(j % nw))
         on.join()
+
+    def _wpass_one_ok(self) -> bool:
+        return (self.cfg.wpass_one_launch and self.dev.type == "cuda" and self.wgrad is None
+                and hasattr(self.model, "weight_grads"))
 
     def _overlap_sync_ok(self) -> bool:
         mode = str(self.cfg.overlap_data_sync)
@@ -538,6 +550,8 @@ class GPipeTrainer:
         streams as soon as the chain has produced that part's output gradients
         (TransformerLM.backward ``after`` hook), overlapping the rest of the chain."""
         k = int(self.cfg.wpass_streams)
+        if k <= 1 and self._wpass_one_ok() and hasattr(self.model, "weight_grads_of"):
+            return self._layer_major_one_wpass(batch, P, st, seed, eo, n_mb)
         if k <= 1 or self.dev.type != "cuda" or not hasattr(self.model, "weight_grads_of"):
             return False
         arena = self._wgrad_arena(batch.size)
@@ -558,6 +572,22 @@ class GPipeTrainer:
 
         self.model.backward(P, cache, d, dout_is_dz=True, need_dx=False, after=after)
         on.join()
+        return True
+
+    def _layer_major_one_wpass(self, batch, P, st, seed, eo, n_mb) -> bool:
+        """One stage, one pass over all rows: the forward, the input-gradient chain, then
+        every weight gradient of the step in ONE launch (ops.kernels.gemm_wpass, AdamW in
+        the epilogues), instead of a grouped dW + dX launch per layer."""
+        arena = self._wgrad_arena(batch.size)
+        if arena is None:
+            return False
+        out, cache = self.model.forward(P, batch.inputs, train=True, seed=seed, offset=0, step=st.step_tensor,
+                                        arena=arena, mb=0, n_mb=1)
+        d = arena.head["dlog"] if self.model.has_head else torch.empty_like(out)
+        self.loss_head(out, batch.labels, d, n_parts=n_mb)
+        self.model.backward(P, cache, d, dout_is_dz=True, need_dx=False)
+        with K.gemm_wpass():
+            self.model.weight_grads(P, arena, opt=eo)
         return True
 
     def _mb_stream_ctx(self, arena, n_mb: int) -> "_MbStreams":

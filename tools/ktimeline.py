@@ -3,7 +3,7 @@ window of the last ``n`` complete steps (a step = the span between consecutive l
 the ``marker`` kernel), the wall time with 0, 1, 2, ... kernels running, the summed kernel
 time and launches per step, and the top kernels by summed time.
 
-    python tools/ktimeline.py TRACE.csv [--marker NAME] [--steps N]
+    python tools/ktimeline.py TRACE.csv|RESULTS.db [--marker NAME] [--steps N]
 
 Without --marker the window is the whole trace after the first 20 % (warm-up)."""
 from __future__ import annotations
@@ -19,8 +19,14 @@ def main():
     ap.add_argument("--marker", default=None, help="substring of the kernel that starts each step")
     ap.add_argument("--steps", type=int, default=20)
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(a.trace)))
-    ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+    if a.trace.endswith(".db"):   # rocprofv3's default rocpd (sqlite) output
+        import sqlite3
+
+        con = sqlite3.connect(a.trace)
+        ks = sorted((int(s), int(e), n) for s, e, n in con.execute("select start, end, name from kernels"))
+    else:
+        rows = list(csv.DictReader(open(a.trace)))
+        ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
     if a.marker:
         marks = [s for s, _, n in ks if a.marker in n]
         marks = marks[-(a.steps + 1):]

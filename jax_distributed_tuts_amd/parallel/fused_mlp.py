@@ -858,11 +858,6 @@ class FusedMLPDeep:
             raise RuntimeError("md_bwd dZ split: a column-block barrier timed out (not every workgroup "
                                "resident); results invalid -- rerun with JDT_MD_DZS=0")
         if self.ahead_ok and int(self.ztick[1].item()) != 0:
-            if self.pst_ok and int(self.ztick[1].item()) & 8:
-                # a persistent launch left its grid barrier early: the XCD / top counters
-                # moved without the generation word, so every later launch would be out of
-                # step -- re-zero them (the engine stays unusable until the error is cleared)
-                self.pst_ws.zero_()
             raise RuntimeError("md_bwd run-ahead: tile map or column barrier failed (error word "
                                f"{int(self.ztick[1].item())}); results invalid")
         if self.tx is not None and self.tx.error():

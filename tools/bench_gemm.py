@@ -38,6 +38,9 @@ SHAPES = [
     ("fc1 dX 2k", 2048, 512, 2048, "mk", "nk", False),
     ("fc2 dW 2k", 2048, 512, 2048, "km", "kn", True),
     ("qkv dW 2k", 512, 1536, 2048, "km", "kn", True),
+    ("out fwd 2k", 2048, 512, 512, "mk", "kn", False),
+    ("out dX 2k", 2048, 512, 512, "mk", "nk", False),
+    ("qkv dX 2k", 2048, 512, 1536, "mk", "nk", False),
     ("out dW 2k", 512, 512, 2048, "km", "kn", True),
     ("hyb qkv fwd", 256, 1536, 512, "mk", "kn", False),
     ("hyb fc2 fwd", 256, 512, 2048, "mk", "kn", False),

@@ -3,6 +3,12 @@ cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/r6s4
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 O=gpurun_out/r6s4
 timeout -k 10 300 python tools/bench_wpass.py > $O/wpass.log 2>&1; rc=$?; cat $O/wpass.log | tail -12; [ $rc -eq 0 ] || exit $rc
+: > $O/sweep.log
+for c in -1 10 11 12 13 14 15 16 20 21 22 23 24 25 26 27; do
+  echo "== cfg $c" >> $O/sweep.log
+  timeout -k 10 120 python tools/bench_gemm.py --cfg $c --only "out fwd 2k,out dX 2k,qkv dX 2k,fc1 dX 2k,fc2 fwd 2k" >> $O/sweep.log 2>&1 || { echo "sweep cfg $c failed"; tail -5 $O/sweep.log; exit 3; }
+done
+grep -E "==|2k" $O/sweep.log | head -120
 T="python -u -m pytest -v --timeout 300 --timeout-method thread"
 timeout -k 10 600 $T tests/test_lm_gpu.py > $O/t_lm.log 2>&1; rc=$?
 grep -E "PASS|FAIL|ERROR|passed|failed" $O/t_lm.log | tail -20; echo "lm tests rc=$rc"

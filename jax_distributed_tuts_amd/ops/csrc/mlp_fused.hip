@@ -608,6 +608,9 @@ struct PstRegs {
 struct PstPos {
   int it, n;
   unsigned launch0;
+  // column-block completion counters (mlp2_pst_kernel CBW): after its forward epilogue
+  // every workgroup adds 1 to done[32 * column block]; null = the grid barrier form
+  unsigned* done = nullptr;
 };
 
 // AHEAD (single GPU, fused AdamW, W1^T copy): after its AdamW epilogue every
@@ -1591,6 +1594,16 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
       a.step[0] = step + 1;
       a.ztick[2] = launch_no + 1u;
     }
+    if (PST && pp.done) {
+      // column-block completion (persistent CBW form): this workgroup's epilogue is in
+      // memory -- its logit adds returned (performed at the memory side), its G1 / H1 and
+      // its step-start logits re-arm drained -- then one agent-scope add on the column
+      // block's own line; the next step waits for all of them instead of a grid barrier
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0)
+        __hip_atomic_fetch_add((gu32_t*)(pp.done + 32 * bx), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   STAMP(4);
 #pragma pop_macro("STAMP")
@@ -1730,6 +1743,37 @@ __device__ __forceinline__ bool pst_wait(unsigned* ws, unsigned gen, bool last, 
   return ok_lds[0] != 0;
 }
 
+// Column-block wait (mlp2_pst_kernel CBW): step it's backward needs step it's logits -- the
+// sum of every column block's partials -- and, from its own column block, G1 / H1 and the
+// W2 shadow; all of them are in memory once every column block's NCH workgroups have added
+// to their completion counter (PstPos::done).  Lanes 0 .. nb-1 of wave 0 poll one counter
+// each (sc1) until it reaches `target`; bounded like pst_poll (error bit 8).
+__device__ __forceinline__ bool cb_wait(const unsigned* done, int nb, unsigned target, int* ok_lds, unsigned* errw,
+                                        long long tmo) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned*>(done), (short)0, 32 * 4 * 64, 0x00020000);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    int ok = 1;
+    while (true) {
+      // every lane loads (lanes past nb re-read the last line): no branch around the load
+      const unsigned v = (unsigned)__builtin_amdgcn_raw_buffer_load_b32(r, 32 * 4 * min(lane, nb - 1), 0, 16);
+      if (__builtin_amdgcn_ballot_w64((int)(v - target) < 0) == 0ull) break;
+      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > tmo) {
+        if (lane == 0) atomicOr(errw + 1, 8u);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");
+    }
+    if (lane == 0) ok_lds[0] = ok;
+  }
+  __syncthreads();
+  return ok_lds[0] != 0;
+}
+
 // The AdamW state a persistent launch carries in registers (PstRegs), loaded before its
 // first step and stored after its last: the elements each lane owns in mlp2_bwd_body's
 // phase-3 epilogues (same indices) -- tile waves 4 W1 elements (plus their W1^T bf16
@@ -1841,7 +1885,13 @@ __device__ __forceinline__ void pst_metrics(float* running, int M, const PstRegs
 // the all-reduced sums); b2 stays with the lead's aux wave.  Requires every workgroup of
 // every rank resident (one rank per GPU; two ranks sharing one only while both grids fit:
 // the WPE = 4 variant, <= 128 VGPRs, two workgroups per CU).
-template <int K_IN, int C, int KC, bool TX = false, int WPE = 1>
+//
+// CBW (column-block wait): between steps, instead of the grid barrier, every workgroup
+// waits until every column block's NCH workgroups have finished the step's forward
+// epilogue (PstPos::done: one counter line per column block, monotonic, base ws[1] = the
+// persistent steps run so far) -- one agent-scope add per workgroup and a poll of H/16
+// lines, against the barrier's XCD counter, cross-XCD counter and per-XCD release.
+template <int K_IN, int C, int KC, bool TX = false, int WPE = 1, bool CBW = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE)))
 mlp2_pst_kernel(Mlp2Args a, int n, unsigned* ws, long long tmo) {
   __shared__ int ok_lds[1];
@@ -1853,6 +1903,8 @@ mlp2_pst_kernel(Mlp2Args a, int n, unsigned* ws, long long tmo) {
   const int step0 = a.step[0];
   const unsigned launch0 = a.ztick[2];
   const unsigned gen0 = ws[0];
+  const unsigned cb0 = ws[1];   // CBW: persistent steps before this launch
+  unsigned* const done = CBW ? ws + 32 * 18 : nullptr;
   // the body's ~50 argument words re-read from the kernarg segment each step (laundered
   // pointer) instead of being held live across the loop (by value: 107 SGPRs spilled)
   typedef const __attribute__((address_space(4))) Mlp2Args KArgs;
@@ -1878,17 +1930,26 @@ mlp2_pst_kernel(Mlp2Args a, int n, unsigned* ws, long long tmo) {
     // in VGPRs, and the buffer resources built from them would become waterfall loops
     mlp2_bwd_body<K_IN, C, KC, false, true, TX, false, false, true>(
         *k, __builtin_amdgcn_readfirstlane(bx), __builtin_amdgcn_readfirstlane(by), step0 + it, &R,
-        PstPos{it, n, launch0});
+        PstPos{it, n, launch0, done});
     if (stw && it == n - 2) stw[12] = __builtin_amdgcn_s_memrealtime();
     if (it + 1 < n) {
-      unsigned xcc = 0u;
-      const bool last = pst_arrive(ws, xcc);
-      if (!TX && bx == 0 && by == 0) pst_metrics(a.running, a.M, R, red_lds);
-      // the next step's bias corrections, while the other workgroups arrive
-      const AdamK kn = adam_consts(*kbase, step0 + it + 1);
-      R.rbc1 = kn.rbc1;
-      R.rbc2 = kn.rbc2;
-      if (!pst_wait(ws, gen0 + (unsigned)it + 1u, last, xcc, ok_lds, a.ztick, tmo)) break;
+      if constexpr (CBW) {
+        if (!TX && bx == 0 && by == 0) pst_metrics(a.running, a.M, R, red_lds);
+        const AdamK kn = adam_consts(*kbase, step0 + it + 1);
+        R.rbc1 = kn.rbc1;
+        R.rbc2 = kn.rbc2;
+        constexpr int NCH_ = K_IN / KC;
+        if (!cb_wait(done, a.H / 16, (unsigned)NCH_ * (cb0 + (unsigned)it + 1u), ok_lds, a.ztick, tmo)) break;
+      } else {
+        unsigned xcc = 0u;
+        const bool last = pst_arrive(ws, xcc);
+        if (!TX && bx == 0 && by == 0) pst_metrics(a.running, a.M, R, red_lds);
+        // the next step's bias corrections, while the other workgroups arrive
+        const AdamK kn = adam_consts(*kbase, step0 + it + 1);
+        R.rbc1 = kn.rbc1;
+        R.rbc2 = kn.rbc2;
+        if (!pst_wait(ws, gen0 + (unsigned)it + 1u, last, xcc, ok_lds, a.ztick, tmo)) break;
+      }
     }
     if (stw && it == n - 2) stw[13] = __builtin_amdgcn_s_memrealtime();
   }
@@ -1901,6 +1962,7 @@ mlp2_pst_kernel(Mlp2Args a, int n, unsigned* ws, long long tmo) {
     a.step[0] = step0 + n;
     a.ztick[2] = launch0 + (unsigned)n;
     ws[0] = gen0 + (unsigned)(n - 1);
+    ws[1] = cb0 + (unsigned)n;   // every step of the launch added NCH to every done line
   }
 }
 
@@ -2075,6 +2137,10 @@ JDT_API int jdt_mlp2_pst_tx_ok(int M, int H, int k_in, int nshare) {
 // build of the exchanging persistent kernel
 static int g_pst_share = 1;
 JDT_API void jdt_mlp2_pst_set_share(int n) { g_pst_share = n < 1 ? 1 : n; }
+// between-step synchronisation of the persistent launch: 0 = XCD-hierarchical grid barrier,
+// 1 = column-block completion counters (CBW); ws then needs 32 * (18 + H/16) words
+static int g_pst_cbw = 0;
+JDT_API void jdt_mlp2_pst_set_cbw(int on) { g_pst_cbw = on ? 1 : 0; }
 JDT_API int jdt_mlp2_pst(const Mlp2Args* args, int n, int k_in, unsigned* ws, long long timeout, void* stream) {
   const long long tmo = timeout > 0 ? timeout : 2000000ll;   // s_memrealtime ticks (100 MHz): 20 ms
   const Mlp2Args& a = *args;
@@ -2083,7 +2149,10 @@ JDT_API int jdt_mlp2_pst(const Mlp2Args* args, int n, int k_in, unsigned* ws, lo
     return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool tx = a.tx != nullptr;
-  if (k_in == 784) {
+  if (k_in == 784 && g_pst_cbw && !tx) {
+    const dim3 g(a.H / 16, 784 / mlp2_kc<784>());
+    hipLaunchKernelGGL((mlp2_pst_kernel<784, 10, mlp2_kc<784>(), false, 1, true>), g, dim3(NT), 0, st, a, n, ws, tmo);
+  } else if (k_in == 784) {
     const dim3 g(a.H / 16, 784 / mlp2_kc<784>());
     if (tx && g_pst_share > 1)
       hipLaunchKernelGGL((mlp2_pst_kernel<784, 10, mlp2_kc<784>(), true, 4>), g, dim3(NT), 0, st, a, n, ws, tmo);

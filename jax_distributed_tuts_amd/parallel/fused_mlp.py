@@ -90,6 +90,7 @@ _lib.declare("jdt_mlp2_loop_ok", c_int, [c_int, c_int])
 _lib.declare("jdt_mlp2_pst_ok", c_int, [c_int, c_int, c_int])
 _lib.declare("jdt_mlp2_pst_tx_ok", c_int, [c_int, c_int, c_int, c_int])
 _lib.declare("jdt_mlp2_pst_set_share", None, [c_int])
+_lib.declare("jdt_mlp2_pst_set_cbw", None, [c_int])
 _lib.declare("jdt_mlp2_pst", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_void_p, c_longlong, c_void_p])
 PST_BARRIER_TIMEOUT_S = 0.02   # persistent run-ahead grid barrier bound (x runtime.dist.spin_timeout_s sharing)
 
@@ -268,7 +269,12 @@ class FusedMLP2:
         if self.pst_ok:
             from ..runtime.dist import spin_timeout_s
 
-            self.pst_ws = torch.zeros(32 * 18, dtype=torch.int32, device=dev)
+            # [generation, CBW base] line, barrier counter lines, then one completion-counter
+            # line per column block (CBW, csrc/mlp_fused.hip cb_wait)
+            self.pst_ws = torch.zeros(32 * (18 + 64), dtype=torch.int32, device=dev)
+            # between-step synchronisation: JDT_MLP2_PST_SYNC=barrier (XCD-hierarchical grid
+            # barrier) or colblk (column-block completion counters), one GPU only
+            _lib.lib().jdt_mlp2_pst_set_cbw(int(tx is None and os.environ.get("JDT_MLP2_PST_SYNC", "barrier") == "colblk"))
             # s_memrealtime ticks (100 MHz); grows with the ranks sharing the GPU like the
             # other in-kernel waits
             self.pst_timeout = int(spin_timeout_s(PST_BARRIER_TIMEOUT_S) * 1e8)

@@ -22,11 +22,12 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 
 
-def _run(b, pst, opt, monkeypatch):
+def _run(b, pst, opt, monkeypatch, sync="barrier"):
     from jax_distributed_tuts_amd.models.mlp import Classifier
     from jax_distributed_tuts_amd.parallel.dp import DataParallelTrainer, DPConfig, init_dp
 
     monkeypatch.setenv("JDT_MLP2_PST", pst)
+    monkeypatch.setenv("JDT_MLP2_PST_SYNC", sync)
     st = init_dp(Classifier(), opt, 69, DEV)
     tr = DataParallelTrainer(st, None, DPConfig(4, "kernel"))
     tr.step(b)
@@ -53,12 +54,17 @@ def _run(b, pst, opt, monkeypatch):
     nb = 512 // 16
     assert bool((zt[32:32 * (1 + nb)].view(nb, 32)[:, 0] == 7 * n).all())   # column barriers: 7 per step
     assert bool((zt[32 * (1 + nb):].view(8, 32)[:, :28] == n).all())       # every tile once per step
-    if pst == "1":
+    if pst == "1" and sync == "barrier":
         ws = eng.pst_ws.cpu()
         gens = 6 + 6 + 2 + 1     # grid barriers: n - 1 per persistent launch (7, 7, 3, 2)
         assert int(ws[0]) == gens and int(ws[32]) == 8 * gens
         assert bool((ws[64:320].view(8, 32)[:, 0] == 28 * gens).all())   # 224 workgroups, 28 per XCD
         assert bool((ws[320:576].view(8, 32)[:, 0] == gens).all())       # every XCD released each time
+    if pst == "1" and sync == "colblk":
+        ws = eng.pst_ws.cpu()
+        steps = 7 + 7 + 3 + 2    # persistent steps; every one adds 7 (input chunks) per column block
+        assert int(ws[1]) == steps, int(ws[1])
+        assert bool((ws[32 * 18:32 * 50].view(32, 32)[:, 0] == 7 * steps).all()), ws[32 * 18:32 * 50:32]
     return out
 
 
@@ -88,19 +94,21 @@ def test_persistent_run_ahead_matches_per_step_launches(rows, monkeypatch):
     assert float(sd.max()) <= 2.0 ** -7 * float(res["0"]["shadow"].float().abs().max())
 
 
-@pytest.mark.parametrize("rows", [128, 64])
-def test_persistent_run_ahead_deterministic_is_bitwise_equal(rows, monkeypatch):
+@pytest.mark.parametrize("rows,sync", [(128, "barrier"), (64, "barrier"), (128, "colblk"), (32, "colblk")])
+def test_persistent_run_ahead_deterministic_is_bitwise_equal(rows, sync, monkeypatch):
     """--deterministic (JDT_DETERMINISTIC=1) runs the benchmarked kernels too: the forward
     epilogues store per-column-block partial logits (one set per step % 3) that the next
     step's backward sums in block order, so the persistent launch and the per-step
-    launches are bitwise equal -- parameters, both moments and metrics."""
+    launches are bitwise equal -- parameters, both moments and metrics.  ``sync``: the
+    between-step synchronisation of the persistent launch (grid barrier, or column-block
+    completion counters: JDT_MLP2_PST_SYNC=colblk)."""
     from jax_distributed_tuts_amd.utils.train_state import Batch, adamw
 
     monkeypatch.setenv("JDT_DETERMINISTIC", "1")
     g = torch.Generator().manual_seed(5)
     b = Batch(torch.randn(rows, 784, generator=g).to(DEV),
               torch.randint(0, 10, (rows,), generator=g).to(torch.int32).to(DEV))
-    res = {k: _run(b, k, adamw(1e-3), monkeypatch) for k in ("0", "1")}
+    res = {k: _run(b, k, adamw(1e-3), monkeypatch, sync=sync) for k in ("0", "1")}
     for k in ("p", "m", "v", "metrics", "shadow"):
         assert torch.equal(res["0"][k], res["1"][k]), (k, float((res["0"][k].float() - res["1"][k].float()).abs().max()))
 

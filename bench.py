@@ -239,7 +239,9 @@ def autotune_candidates(args, ws: int):
         return []
     if args.strategy == "fsdp" and args.accum == "kernel":
         if args.num_layers == 2:
-            return [[Candidate("one-launch", {"JDT_FSDP_AHEAD": "1"}, engaged=one),
+            pst = lambda tr: one(tr) and bool(getattr(getattr(tr, "fused", None), "pst_ok", False))  # noqa: E731
+            return [[Candidate("persistent", {"JDT_FSDP_AHEAD": "1", "JDT_FSDP_PST": "1"}, engaged=pst),
+                     Candidate("one-launch", {"JDT_FSDP_AHEAD": "1", "JDT_FSDP_PST": "0"}, engaged=one),
                      Candidate("three-launch", {"JDT_FSDP_AHEAD": "0"}, reference=True)]]
         if args.optimizer == "adamw":
             # deep: one backward launch per hidden layer sending its partials to the shard

@@ -632,7 +632,7 @@ template <int K_IN, int C, int KC, bool LOOP, bool AHEAD = false, bool TX = fals
           bool FX = false, bool PST = false, class AT>
 __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by, const int step_in,
                                               PstRegs* R = nullptr, const PstPos pp = PstPos{0, 1, 0u}) {
-  static_assert(!PST || (AHEAD && !P3S && !FX && !LOOP), "persistent: the run-ahead step (one GPU, or DP TX)");
+  static_assert(!PST || (AHEAD && !P3S && !LOOP), "persistent: the run-ahead step (one GPU, or TX / FX exchange)");
   constexpr bool SCX = LOOP || PST;        // in-launch hand-offs: sc1 loads / stores
   // phase stamps: a persistent launch records step n-2 (a steady step: the last one also
   // stores the optimizer state)
@@ -1152,6 +1152,7 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
       // are summed by rank T % W and pushed back as sums (every rank updates its own copy).
       // Then every rank holds the whole updated tile and runs the next forward from it.
       const TxArgs* X = a.tx;
+      PstRegs* const R_ = R;   // the persistent launch's registers (R names the rank here)
       const int R = fx_R, W = __builtin_amdgcn_readfirstlane(X->world);
       const int T = bx * NCH + by;
       const long pay = __builtin_amdgcn_readfirstlane(X->pay), tiles = __builtin_amdgcn_readfirstlane(X->tiles);
@@ -1240,7 +1241,11 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
             const long li = (long)(trow0 + e - R * fx_rpq) * H + tcol;
             float tp, tm = om[e], tv = ov[e];
             adam_apply(op[e], om[e], ov[e], ev[e], ak, &tp, &tm, &tv);
-            a.pW1[li] = tp; a.mW1[li] = tm; a.vW1[li] = tv;
+            if constexpr (PST) {   // persistent: the owned shard's state stays in registers
+              R_->op[e] = tp; R_->om[e] = tm; R_->ov[e] = tv;
+            } else {
+              a.pW1[li] = tp; a.mW1[li] = tm; a.vW1[li] = tv;
+            }
             pnew[e] = tp;
           } else {
             const int n = (lane >> 4) * 4 + e;
@@ -1248,7 +1253,11 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
             const long li = isb ? (long)(j0 + n - R * fx_hpq) : (long)(j0 + n - R * fx_hpq) * C + ac;
             float tp, tm = om[e], tv = ov[e];
             adam_apply(op[e], om[e], ov[e], ev[e], ak, &tp, &tm, &tv);
-            (isb ? a.pb1 : a.pW2)[li] = tp; (isb ? a.mb1 : a.mW2)[li] = tm; (isb ? a.vb1 : a.vW2)[li] = tv;
+            if constexpr (PST) {
+              R_->op[e] = tp; R_->om[e] = tm; R_->ov[e] = tv;
+            } else {
+              (isb ? a.pb1 : a.pW2)[li] = tp; (isb ? a.mb1 : a.mW2)[li] = tm; (isb ? a.vb1 : a.vW2)[li] = tv;
+            }
             pnew[e] = tp;
           }
         }
@@ -1297,7 +1306,14 @@ __device__ __forceinline__ void mlp2_bwd_body(AT& a, const int bx, const int by,
           }
         }
         if (lead && lane < C) {
-          const float pn = adam_apply_h<LOOP>(qp, qm, qv, rv, ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
+          float pn;
+          if constexpr (PST) {   // b2 (replicated): every rank's own copy, in registers
+            float tp, tm = qm, tv = qv;
+            pn = adam_apply(qp, qm, qv, rv, ak, &tp, &tm, &tv);
+            R_->qp = tp; R_->qm = tm; R_->qv = tv;
+          } else {
+            pn = adam_apply_h<LOOP>(qp, qm, qv, rv, ak, a.pb2 + lane, a.mb2 + lane, a.vb2 + lane);
+          }
           a.sb2[lane] = f2bf(pn);
           a.hand[H + (long)H * C + lane] = pn;
         }
@@ -1778,7 +1794,7 @@ __device__ __forceinline__ bool cb_wait(const unsigned* done, int nb, unsigned t
 // first step and stored after its last: the elements each lane owns in mlp2_bwd_body's
 // phase-3 epilogues (same indices) -- tile waves 4 W1 elements (plus their W1^T bf16
 // copy), the chunk-0 aux wave W2 / b1 (lanes ac <= C) and, in block (0,0), b2.
-template <int K_IN, int C, int KC, bool TX, class AT>
+template <int K_IN, int C, int KC, bool TX, class AT, bool FX = false>
 __device__ __forceinline__ void pst_state_io(AT& a, const int bx, const int by, PstRegs& R, const bool store) {
   constexpr int NTILE = KC / 16;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, H = a.H;
@@ -1788,6 +1804,44 @@ __device__ __forceinline__ void pst_state_io(AT& a, const int bx, const int by, 
   const bool w2l = aux && ac < C;
   const int trow0 = kc0 + min(w, NTILE - 1) * 16 + (lane >> 4) * 4, tcol = j0 + (lane & 15);
   const bool sgd = a.opt_sgd != 0;
+  if constexpr (FX) {
+    // FSDP (mlp2_bwd FX): this rank's LOCAL shards -- W1 rows [R K/W, (R+1) K/W), W2 / b1
+    // rows [R H/W, (R+1) H/W) -- indexed as the body's phase 0 does; only owned elements are
+    // stored back (the others' registers hold clamped, unused values); b2 is replicated.
+    // W1^T is written by the body every step (its non-owned elements come from the owners).
+    const int Rk = __builtin_amdgcn_readfirstlane(a.tx->rank), Wk = __builtin_amdgcn_readfirstlane(a.tx->world);
+    const int rpq = K_IN / Wk, hpq = H / Wk;
+    float* const pW1 = sgpr_ptr(a.pW1); float* const mW1 = sgpr_ptr(a.mW1); float* const vW1 = sgpr_ptr(a.vW1);
+    float* const pW2 = sgpr_ptr(a.pW2); float* const mW2 = sgpr_ptr(a.mW2); float* const vW2 = sgpr_ptr(a.vW2);
+    float* const pb1 = sgpr_ptr(a.pb1); float* const mb1 = sgpr_ptr(a.mb1); float* const vb1 = sgpr_ptr(a.vb1);
+    float* const pb2 = sgpr_ptr(a.pb2); float* const mb2 = sgpr_ptr(a.mb2); float* const vb2 = sgpr_ptr(a.vb2);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = (lane >> 4) * 4 + e;
+      const int lr = aux ? min(max(j0 + n - Rk * hpq, 0), hpq - 1) : min(max(trow0 + e - Rk * rpq, 0), rpq - 1);
+      const long idx = aux ? (w2l ? (long)lr * C + ac : (long)lr) : (long)lr * H + tcol;
+      float* const sp = aux ? (w2l ? pW2 : pb1) : pW1;
+      float* const sm = aux ? (w2l ? mW2 : mb1) : mW1;
+      float* const sv = aux ? (w2l ? vW2 : vb1) : vW1;
+      if (!store) {
+        R.op[e] = ld_global(sp + idx); R.om[e] = ld_global(sm + idx); R.ov[e] = ld_global(sv + idx);
+      } else {
+        const bool owned = aux ? (ac <= C && (j0 + n) / hpq == Rk) : (w < NTILE && (trow0 + e) / rpq == Rk);
+        if (owned) {
+          sp[idx] = R.op[e];
+          if (!sgd) { sm[idx] = R.om[e]; sv[idx] = R.ov[e]; }
+        }
+      }
+    }
+    const int lq = min(lane, C - 1);
+    if (!store) {
+      R.qp = ld_global(pb2 + lq); R.qm = ld_global(mb2 + lq); R.qv = ld_global(vb2 + lq);
+    } else if (bx == 0 && by == 0 && w == NW - 1 && lane < C) {
+      pb2[lane] = R.qp;
+      if (!sgd) { mb2[lane] = R.qm; vb2[lane] = R.qv; }
+    }
+    return;
+  }
   // argument words as scalar values first, then per-lane selects between those values
   // (a select between two fields of the by-value argument block made the compiler give
   // the kernel a private copy of it: a scratch segment, set up at the first launch)
@@ -1891,7 +1945,11 @@ __device__ __forceinline__ void pst_metrics(float* running, int M, const PstRegs
 // epilogue (PstPos::done: one counter line per column block, monotonic, base ws[1] = the
 // persistent steps run so far) -- one agent-scope add per workgroup and a poll of H/16
 // lines, against the barrier's XCD counter, cross-XCD counter and per-XCD release.
-template <int K_IN, int C, int KC, bool TX = false, int WPE = 1, bool CBW = false>
+//
+// FX (with TX): the FSDP form -- every gradient element goes to the rank owning its row,
+// the owner applies the sharded AdamW to its LOCAL state (carried in registers across the
+// steps like the replicated form's) and hands the value back (mlp2_bwd_body FX).
+template <int K_IN, int C, int KC, bool TX = false, int WPE = 1, bool CBW = false, bool FX = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE)))
 mlp2_pst_kernel(Mlp2Args a, int n, unsigned* ws, long long tmo) {
   __shared__ int ok_lds[1];
@@ -1910,7 +1968,7 @@ mlp2_pst_kernel(Mlp2Args a, int n, unsigned* ws, long long tmo) {
   typedef const __attribute__((address_space(4))) Mlp2Args KArgs;
   KArgs* const kbase = (KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
   PstRegs R;
-  pst_state_io<K_IN, C, KC, TX>(a, bx, by, R, false);
+  pst_state_io<K_IN, C, KC, TX, Mlp2Args, FX>(a, bx, by, R, false);
   {
     const AdamK k0 = adam_consts(*kbase, step0);
     R.rbc1 = k0.rbc1;
@@ -1928,7 +1986,7 @@ mlp2_pst_kernel(Mlp2Args a, int n, unsigned* ws, long long tmo) {
     if (stw && it == n - 1) stw[7] = __builtin_amdgcn_s_memrealtime();
     // the tile coordinates re-made scalar each step: carried across the loop they may sit
     // in VGPRs, and the buffer resources built from them would become waterfall loops
-    mlp2_bwd_body<K_IN, C, KC, false, true, TX, false, false, true>(
+    mlp2_bwd_body<K_IN, C, KC, false, true, TX, false, FX, true>(
         *k, __builtin_amdgcn_readfirstlane(bx), __builtin_amdgcn_readfirstlane(by), step0 + it, &R,
         PstPos{it, n, launch0, done});
     if (stw && it == n - 2) stw[12] = __builtin_amdgcn_s_memrealtime();
@@ -1955,7 +2013,7 @@ mlp2_pst_kernel(Mlp2Args a, int n, unsigned* ws, long long tmo) {
   }
   if (it == n) {
     if (!TX && bx == 0 && by == 0) pst_metrics(a.running, a.M, R, red_lds);
-    pst_state_io<K_IN, C, KC, TX>(a, bx, by, R, true);
+    pst_state_io<K_IN, C, KC, TX, Mlp2Args, FX>(a, bx, by, R, true);
   }
   if (stw) stw[6] = (unsigned long long)(bx + 256 * by);
   if (bx == 0 && by == 0 && threadIdx.x == 0 && it == n) {
@@ -2097,7 +2155,7 @@ static int mlp2_ahead_ok_k(int M, int H, int nshare, bool tx) {
 // nshare > 0: the N > 1 form (tile exchange) with `nshare` ranks' grids on this GPU -- every
 // workgroup of every sharing rank's persistent launch resident at once.
 template <int K_IN>
-static int mlp2_pst_ok_k(int M, int H, int nshare) {
+static int mlp2_pst_ok_k(int M, int H, int nshare, bool fx = false) {
   constexpr int KC = mlp2_kc<K_IN>(), NCH = K_IN / KC;
   if (!mlp2_ahead_ok_k<K_IN>(M, H, nshare > 0 ? nshare : 1, nshare > 0)) return 0;
   const int G = (H / 16) * NCH;
@@ -2107,7 +2165,11 @@ static int mlp2_pst_ok_k(int M, int H, int nshare) {
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
   const hipError_t e =
-      nshare > 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, mlp2_pst_kernel<K_IN, 10, KC, true, 4>, NT, 0)
+      fx ? (nshare > 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                             &per, mlp2_pst_kernel<K_IN, 10, KC, true, 4, false, true>, NT, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                             &per, mlp2_pst_kernel<K_IN, 10, KC, true, 1, false, true>, NT, 0))
+      : nshare > 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, mlp2_pst_kernel<K_IN, 10, KC, true, 4>, NT, 0)
       : nshare == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, mlp2_pst_kernel<K_IN, 10, KC, true>, NT, 0)
                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, mlp2_pst_kernel<K_IN, 10, KC>, NT, 0);
   if (e != hipSuccess) return 0;
@@ -2119,11 +2181,12 @@ JDT_API int jdt_mlp2_pst_ok(int M, int H, int k_in) {
   if (k_in == 1024) return mlp2_pst_ok_k<1024>(M, H, 0);
   return 0;
 }
-// the persistent launch with the tile exchange (N > 1 DP), `nshare` ranks per GPU
-JDT_API int jdt_mlp2_pst_tx_ok(int M, int H, int k_in, int nshare) {
+// the persistent launch with the tile exchange (N > 1 DP; fx: the FSDP owner exchange),
+// `nshare` ranks per GPU
+JDT_API int jdt_mlp2_pst_tx_ok(int M, int H, int k_in, int nshare, int fx) {
   if (nshare < 1) return 0;
-  if (k_in == 784) return mlp2_pst_ok_k<784>(M, H, nshare);
-  if (k_in == 1024) return mlp2_pst_ok_k<1024>(M, H, nshare);
+  if (k_in == 784) return mlp2_pst_ok_k<784>(M, H, nshare, fx != 0);
+  if (k_in == 1024) return mlp2_pst_ok_k<1024>(M, H, nshare, fx != 0);
   return 0;
 }
 
@@ -2144,11 +2207,33 @@ JDT_API void jdt_mlp2_pst_set_cbw(int on) { g_pst_cbw = on ? 1 : 0; }
 JDT_API int jdt_mlp2_pst(const Mlp2Args* args, int n, int k_in, unsigned* ws, long long timeout, void* stream) {
   const long long tmo = timeout > 0 ? timeout : 2000000ll;   // s_memrealtime ticks (100 MHz): 20 ms
   const Mlp2Args& a = *args;
-  if (n == 1 || n < 0 || !ws || a.tx_fsdp || !a.fuse_opt || !a.W1T || !a.XR || !a.zslab || !a.ztick || !a.hand ||
+  if (n == 1 || n < 0 || !ws || (a.tx_fsdp && !a.tx) || !a.fuse_opt || !a.W1T || !a.XR || !a.zslab || !a.ztick || !a.hand ||
       !a.lg3 || a.M <= 0 || a.M > 128 || a.H % 128 || (a.tx && !a.running))
     return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool tx = a.tx != nullptr;
+  if (tx && a.tx_fsdp) {   // FSDP owner exchange (mlp2_bwd_body FX)
+    if (k_in == 784) {
+      const dim3 g(a.H / 16, 784 / mlp2_kc<784>());
+      if (g_pst_share > 1)
+        hipLaunchKernelGGL((mlp2_pst_kernel<784, 10, mlp2_kc<784>(), true, 4, false, true>), g, dim3(NT), 0, st, a, n,
+                           ws, tmo);
+      else
+        hipLaunchKernelGGL((mlp2_pst_kernel<784, 10, mlp2_kc<784>(), true, 1, false, true>), g, dim3(NT), 0, st, a, n,
+                           ws, tmo);
+    } else if (k_in == 1024) {
+      const dim3 g(a.H / 16, 1024 / mlp2_kc<1024>());
+      if (g_pst_share > 1)
+        hipLaunchKernelGGL((mlp2_pst_kernel<1024, 10, mlp2_kc<1024>(), true, 4, false, true>), g, dim3(NT), 0, st, a,
+                           n, ws, tmo);
+      else
+        hipLaunchKernelGGL((mlp2_pst_kernel<1024, 10, mlp2_kc<1024>(), true, 1, false, true>), g, dim3(NT), 0, st, a,
+                           n, ws, tmo);
+    } else {
+      return -3;
+    }
+    return HIP_LAUNCH_CHECK();
+  }
   if (k_in == 784 && g_pst_cbw && !tx) {
     const dim3 g(a.H / 16, 784 / mlp2_kc<784>());
     hipLaunchKernelGGL((mlp2_pst_kernel<784, 10, mlp2_kc<784>(), false, 1, true>), g, dim3(NT), 0, st, a, n, ws, tmo);

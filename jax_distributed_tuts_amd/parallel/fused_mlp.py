@@ -88,7 +88,7 @@ _lib.declare("jdt_mlp2_loop", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_void_p,
 
 _lib.declare("jdt_mlp2_loop_ok", c_int, [c_int, c_int])
 _lib.declare("jdt_mlp2_pst_ok", c_int, [c_int, c_int, c_int])
-_lib.declare("jdt_mlp2_pst_tx_ok", c_int, [c_int, c_int, c_int, c_int])
+_lib.declare("jdt_mlp2_pst_tx_ok", c_int, [c_int, c_int, c_int, c_int, c_int])
 _lib.declare("jdt_mlp2_pst_set_share", None, [c_int])
 _lib.declare("jdt_mlp2_pst_set_cbw", None, [c_int])
 _lib.declare("jdt_mlp2_pst", c_int, [ctypes.POINTER(Mlp2Args), c_int, c_int, c_void_p, c_longlong, c_void_p])
@@ -253,17 +253,18 @@ class FusedMLP2:
         # run-ahead call in ONE launch, the AdamW state in registers across them and an
         # XCD-hierarchical grid barrier between steps; one GPU only.  JDT_MLP2_PST=0: one
         # launch per step (A/B).  pst_ws: the barrier's counter lines, zeroed once.
-        # N > 1 (DP one-launch step, ``tx``): the same persistent launch with the tile
-        # exchange inside every step (mlp2_pst_kernel TX), so a replay's n steps are one
-        # launch per rank; JDT_DP_PST=0 keeps one run-ahead launch per step (bench.py's
-        # autotune validates and times both).  Not the FSDP form (its sharded AdamW state
-        # is owner-local, handed back by value every step).
+        # N > 1 (one-launch step, ``tx``): the same persistent launch with the tile
+        # exchange inside every step (mlp2_pst_kernel TX; FSDP: the owner exchange FX, the
+        # owned shard's AdamW state in registers), so a replay's n steps are one launch per
+        # rank; JDT_DP_PST=0 / JDT_FSDP_PST=0 keep one run-ahead launch per step (bench.py's
+        # autotune validates and times both).
         if tx is None:
             self.pst_ok = (self.ahead_ok and os.environ.get("JDT_MLP2_PST", "1") == "1"
                            and bool(_lib.lib().jdt_mlp2_pst_ok(rows, H, K)))
         else:
-            self.pst_ok = (self.ahead_ok and not self.fsdp_tx and os.environ.get("JDT_DP_PST", "1") == "1"
-                           and bool(_lib.lib().jdt_mlp2_pst_tx_ok(rows, H, K, int(ranks_on_gpu))))
+            env = "JDT_FSDP_PST" if self.fsdp_tx else "JDT_DP_PST"
+            self.pst_ok = (self.ahead_ok and os.environ.get(env, "1") == "1"
+                           and bool(_lib.lib().jdt_mlp2_pst_tx_ok(rows, H, K, int(ranks_on_gpu), int(self.fsdp_tx))))
             if self.pst_ok:
                 _lib.lib().jdt_mlp2_pst_set_share(int(ranks_on_gpu))
         if self.pst_ok:

@@ -48,12 +48,12 @@ def test_autotune_validates_and_falls_back(strategy):
     assert rows["three-launch"]["valid"] is True, rows
     assert all(r["us_per_step"] > 0 for r in rows.values()), rows
     print(strategy, "errors of the one-launch form vs three-launch:", rows["one-launch"]["err"])
+    # N > 1 persistent launch (the exchange inside every step): validated like the others
+    assert rows["persistent"]["valid"] is True and rows["persistent"]["engaged"] is True, rows
+    print("errors of the persistent form vs three-launch:", rows["persistent"]["err"])
     if strategy == "dp":
         assert rows["one-launch"]["replicated"] is True
-        # N > 1 persistent launch (tile exchange inside every step): validated like the others
-        assert rows["persistent"]["valid"] is True and rows["persistent"]["engaged"] is True, rows
         assert rows["persistent"]["replicated"] is True
-        print("errors of the persistent form vs three-launch:", rows["persistent"]["err"])
     # the timed run is the faster valid form
     best = min(rows.values(), key=lambda r: r["us_per_step"])["name"]
     assert ok["details"]["autotune"]["stages"][0]["choice"] == best
@@ -66,8 +66,7 @@ def test_autotune_validates_and_falls_back(strategy):
     rows = _rows(j)
     assert rows["one-launch"]["valid"] is False and "differs" in rows["one-launch"]["reason"], rows
     assert rows["one-launch"]["err"]["block"] > 0.05, rows
-    if strategy == "dp":
-        assert rows["persistent"]["valid"] is False and "differs" in rows["persistent"]["reason"], rows
+    assert rows["persistent"]["valid"] is False and "differs" in rows["persistent"]["reason"], rows
     assert "one_launch_fallback" in j["config"], j["config"]
     assert not j["config"].get("step_launches", "").startswith(("1 ", "1/")), j["config"]
     assert j["value"] > 0 and j["n_gpus"] == 2
@@ -82,8 +81,8 @@ def test_autotune_validates_and_falls_back(strategy):
 def test_bench_falls_back_when_the_exchange_fails_without_autotune(strategy):
     ok = _bench(strategy, extra=("--autotune", "off"))
     assert "one_launch_fallback" not in ok["config"]
-    # DP: a 20-step replay is one persistent launch per rank (JDT_DP_PST default on)
-    want = "1/20 (persistent" if strategy == "dp" else "1 (run-ahead mlp2_bwd"
+    # a 20-step replay is one persistent launch per rank (JDT_DP_PST / JDT_FSDP_PST default on)
+    want = "1/20 (persistent"
     assert ok["config"]["step_launches"].startswith(want), ok["config"]
     j = _bench(strategy, 1, extra=("--autotune", "off"))
     assert "one_launch_fallback" in j["config"], j["config"]

@@ -142,6 +142,32 @@ def test_dp_persistent_exchange_matches_per_step_launches(tmp_path, ws, width):
     torch.testing.assert_close(a[0]["metrics"], b[0]["metrics"], rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("ws,hidden", [(2, 512), (4, 256)])
+def test_fsdp_persistent_exchange_matches_per_step_launches(tmp_path, ws, hidden):
+    """N > 1 FSDP, 2-layer: multi-step replays of the one-launch step as ONE persistent
+    launch per rank (mlp2_pst_kernel FX: partials to the row owners, each owner's sharded
+    AdamW state in registers across the steps, values handed back) == one run-ahead launch
+    per step (JDT_FSDP_PST=0), local shards and moments within the logit-atomics bulk
+    bounds of tests/test_mlp2_persistent_gpu.py."""
+    for k in ("1", "0"):
+        _spawn8(XW.fsdp_xgmi, ws, str(tmp_path), True, 7, 2, 1e-8, "0", hidden, k, f"p{k}")
+    a, b = _load(tmp_path, "fsx2p1", ws), _load(tmp_path, "fsx2p0", ws)
+    assert all(o["one_launch"] and o["pst"] for o in a), [(o["one_launch"], o["pst"]) for o in a]
+    assert all(o["one_launch"] and not o["pst"] for o in b)
+    for oa, ob in zip(a, b):
+        for name in oa["local"]:
+            ref = ob["local"][name]
+            d = (oa["local"][name] - ref).abs().flatten().float().sort().values
+            scale = float(ref.abs().max())
+            assert float(d[len(d) // 2]) <= 1e-5 * scale and float(d[int(0.999 * (len(d) - 1))]) <= 1e-4 * scale, name
+        for k in ("m", "v"):
+            d = (oa[k] - ob[k]).abs().float().sort().values
+            scale = float(ob[k].abs().max())
+            print(f"[fsdp pst ws={ws}] {k}: max {float(d[-1]):.3e} median {float(d[len(d) // 2]):.3e}")
+            assert float(d[len(d) // 2]) <= 1e-5 * scale and float(d[int(0.999 * (len(d) - 1))]) <= 1e-4 * scale, k
+    torch.testing.assert_close(a[0]["metrics"], b[0]["metrics"], rtol=1e-5, atol=1e-3)
+
+
 @pytest.mark.parametrize("ws,fused,num_layers,eps,deep_fx,hidden", [
     (2, True, 2, 1e-8, "0", 512), (2, False, 2, 1e-8, "0", 512), (2, True, 4, 1e-8, "0", 512),
     (2, True, 2, 10.0, "0", 512), (2, True, 4, 10.0, "0", 512), (8, True, 2, 10.0, "0", 512),

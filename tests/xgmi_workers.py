@@ -214,7 +214,7 @@ def dp_xgmi(outdir, steps_eager=2, steps_graph=6, dp_ahead="1", num_layers=2, wi
                                 "pst": bool(getattr(tr.fused, "pst_ok", False))})
 
 
-def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2, eps=1e-8, deep_fx="0", hidden=512):
+def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2, eps=1e-8, deep_fx="0", hidden=512, pst="1", tag=""):
     """FSDP (dropout off) with the segmented xGMI gather / reduce-scatter; every rank
     saves its local shard + the partition table for reassembly in the parent.
     num_layers=4: the square 512 x 512 hidden weights are sharded along dim 1 (the
@@ -222,6 +222,7 @@ def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2, eps=1e-8, deep_fx="0", 
     import os
 
     os.environ["JDT_FSDP_DEEP_FX"] = deep_fx
+    os.environ["JDT_FSDP_PST"] = pst   # 1: multi-step replays of the one-launch step as ONE persistent launch
     from data_paral import synthetic_batch
     from jax_distributed_tuts_amd.models.mlp import Classifier
     from jax_distributed_tuts_amd.parallel.dp import shard_batch
@@ -246,7 +247,10 @@ def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2, eps=1e-8, deep_fx="0", 
     torch.cuda.synchronize()
     tr.finalize()
     sp = st.extra["sharded"]
-    _save(outdir, f"fsx{num_layers}", {"local": {n: sp.local.p(n).cpu() for n in sp.part},
+    o = st.opt_state
+    _save(outdir, f"fsx{num_layers}{tag}", {"local": {n: sp.local.p(n).cpu() for n in sp.part},
+                          "m": o["m"][:sp.local.numel].cpu(), "v": o["v"][:sp.local.numel].cpu(),
+                          "pst": bool(getattr(getattr(tr, "fused", None), "pst_ok", False)),
                           "dims": {n: sp.part[n].shard_dim for n in sp.part},
                           "metrics": tr.metrics.cpu(), "comm": tr.comm_backend, "xg_names": list(sp._xg_names),
                           "fused_comm": getattr(tr, "_plan", None) is not None or tr.one_launch,

@@ -313,7 +313,8 @@ def run_autotune(args, dev, build, prepare):
 
         # every candidate is value-checked against its stage's reference form (PP too: the
         # stage kernel, microbatch counts and stream schedules against per-tick launches)
-        rep, t, b = AT.run(cands, build_one, prepare, dev, validate=True, steps=steps, log=log)
+        rep, t, b = AT.run(cands, build_one, prepare, dev, validate=True, steps=steps, log=log,
+                           prepare_probe=lambda tr_, b_: prepare(tr_, b_, spg=AT.VALIDATE_STEPS - 1))
         tables.append(rep)
         chosen_env.update(rep["env"])
         chosen_args.update(rep.get("args", {}))
@@ -411,15 +412,17 @@ def main():
     on_gpu = dev.type == "cuda"
     sync = (lambda: torch.cuda.synchronize()) if on_gpu else (lambda: None)
 
-    def prepare(tr_, batch_):
+    def prepare(tr_, batch_, spg=None):
         """Capture the step the way the timed region replays it (DP always; FSDP and PP
-        when their collectives / stage hand-offs are xGMI kernels or N = 1)."""
+        when their collectives / stage hand-offs are xGMI kernels or N = 1); ``spg``: steps
+        per graph (default the run's; the autotune's probes capture 2-step replays)."""
         if not (on_gpu and not args.no_graph and (args.strategy == "dp" or tr_.capturable)):
             return False
+        spg = args.steps_per_graph if spg is None else spg
         if args.strategy == "dp":
-            tr_.capture(batch_, capture_collectives=args.capture_collectives, steps_per_graph=args.steps_per_graph)
+            tr_.capture(batch_, capture_collectives=args.capture_collectives, steps_per_graph=spg)
         else:
-            tr_.capture(batch_, steps_per_graph=args.steps_per_graph)
+            tr_.capture(batch_, steps_per_graph=spg)
         return True
 
     n_eager = max(1, min(args.warmup, 3))

@@ -220,10 +220,14 @@ def time_candidate(tr, batch, steps: int, dev) -> float:
     return _max(dt / steps * 1e6, dev)
 
 
-def _validate(c: Candidate, build: Callable, dev, validate: bool, ref: Optional[Dict], row: Dict):
+def _validate(c: Candidate, build: Callable, dev, validate: bool, ref: Optional[Dict], row: Dict,
+              prepare_probe: Optional[Callable] = None):
     """Build ``c`` under its env, run the probe steps and fill ``row`` (valid / engaged /
     err / reason).  Returns this candidate's (init, state) snapshots (the reference form's
-    become ``ref``)."""
+    become ``ref``).  ``prepare_probe(tr, batch)`` (optional) captures the trainer after
+    its first eager step so the remaining probe steps run as ONE multi-step replay -- the
+    form the timed run replays (a persistent multi-step launch is then validated itself,
+    not only its one-step sibling); it returns False when there is nothing to capture."""
     if not validate:   # timing only (the in-kernel error words are still checked)
         row["valid"] = True
         return None
@@ -233,8 +237,12 @@ def _validate(c: Candidate, build: Callable, dev, validate: bool, ref: Optional[
         tr, batch = build(PROBE_EPS, c)
         try:
             init = snapshot(tr)
-            for _ in range(VALIDATE_STEPS):
-                tr.step(batch)
+            tr.step(batch)
+            if prepare_probe is not None and hasattr(tr, "run_steps") and prepare_probe(tr, batch):
+                tr.run_steps(batch, VALIDATE_STEPS - 1)
+            else:
+                for _ in range(VALIDATE_STEPS - 1):
+                    tr.step(batch)
             _sync(dev)
             # the form asked for must have engaged on every rank (its engine is built on
             # the first step); otherwise it is the reference form under another name
@@ -289,7 +297,7 @@ def _build_timed(c: Candidate, build: Callable, prepare: Callable, steps: int):
 
 
 def run(cands: List[Candidate], build: Callable, prepare: Callable, dev, validate: bool = True,
-        steps: int = 100, rounds: int = 3, log: Callable = print):
+        steps: int = 100, rounds: int = 3, log: Callable = print, prepare_probe: Optional[Callable] = None):
     """Validate and time ``cands`` (collective: every rank calls it with the same list).
 
     ``build(eps, cand)`` builds a trainer and its batch under the current env (eps: AdamW
@@ -326,7 +334,7 @@ def run(cands: List[Candidate], build: Callable, prepare: Callable, dev, validat
     late = [c for c in order if c.contaminates]
     live = []
     for c in early:
-        snap = _validate(c, build, dev, validate, ref_snap, rows[c.name])
+        snap = _validate(c, build, dev, validate, ref_snap, rows[c.name], prepare_probe)
         if c.reference:
             ref_snap = snap
             if validate and not rows[c.name]["valid"]:
@@ -353,7 +361,7 @@ def run(cands: List[Candidate], build: Callable, prepare: Callable, dev, validat
                 times[c.name].append(time_candidate(tr, batch, steps, dev))
         late_live = []
         for c in late:
-            _validate(c, build, dev, validate, ref_snap, rows[c.name])
+            _validate(c, build, dev, validate, ref_snap, rows[c.name], prepare_probe)
             if rows[c.name]["valid"]:
                 late_live.append(c)
         if late_live:

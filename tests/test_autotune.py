@@ -141,3 +141,29 @@ def test_state_changing_candidate_is_timed_last(gloo1):
     rows = {r["name"]: r for r in report["candidates"]}
     assert rows["ref"]["us_per_step_after_late"] > rows["ref"]["us_per_step"]
     slow["on"] = False
+
+
+def test_probe_runs_the_captured_multi_step_form(gloo1):
+    # a form that is right step by step but wrong in its captured multi-step replay (as a
+    # persistent multi-step launch could be): the probe captures after the first eager
+    # step and replays the rest, so the wrong replay is what gets validated -- and rejected
+    class _Replay(_Trainer):
+        captured = False
+
+        def run_steps(self, batch, n):
+            for _ in range(n):
+                self.step(batch)
+                if self.captured and self.form == "bad-replay":
+                    self.state.params.master.view(32, 32)[:16, :16] += 1e-3
+
+    def prep(tr, b):
+        tr.captured = True
+        return True
+
+    cands = [AT.Candidate("ref", {FORM: "ref"}, reference=True),
+             AT.Candidate("bad-replay", {FORM: "bad-replay"}, engaged=lambda tr: tr.form == "bad-replay")]
+    report, tr, _ = AT.run(cands, lambda eps, c: (_Replay(eps), None), lambda tr, b: None, torch.device("cpu"),
+                           steps=2, rounds=1, log=lambda *a: None, prepare_probe=prep)
+    rows = {r["name"]: r for r in report["candidates"]}
+    assert rows["bad-replay"]["valid"] is False and "differs" in rows["bad-replay"]["reason"], rows
+    assert report["choice"] == "ref"

@@ -1822,6 +1822,11 @@ static const GemmTune kGemmTune[] = {
     {512, 2048, 512, 1, 1, 20, 1, 0},    // fc1 dW, 512 tokens         8.11 (9.80)
     {2048, 512, 512, 1, 1, 20, 1, 0},    // fc2 dW, 512 tokens         8.15 (9.92)
     {2048, 1536, 512, 0, 1, 26, 1, 0},   // qkv fwd (2048 rows)       11.87 (14.92)
+    // round 6: the layer-major LM pass's 2048-row N = 512 GEMMs (the heuristic's 32 x 32
+    // tiles; profiles/r6_s4_gemm_sweep.txt)
+    {2048, 512, 512, 0, 1, 10, 1, 0},    // out fwd 2k                 6.55 (10.32)
+    {2048, 512, 512, 0, 0, 10, 1, 0},    // out dX 2k                  5.92 (9.45)
+    {2048, 512, 1536, 0, 0, 10, 1, 0},   // qkv dX 2k                 11.04 (16.78)
 };
 static bool g_gemm_tune = true;  // jdt_gemm_set_tune(0): heuristic only (A/B)
 

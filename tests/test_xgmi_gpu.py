@@ -148,23 +148,32 @@ def test_fsdp_persistent_exchange_matches_per_step_launches(tmp_path, ws, hidden
     launch per rank (mlp2_pst_kernel FX: partials to the row owners, each owner's sharded
     AdamW state in registers across the steps, values handed back) == one run-ahead launch
     per step (JDT_FSDP_PST=0), local shards and moments within the logit-atomics bulk
-    bounds of tests/test_mlp2_persistent_gpu.py."""
+    bounds of tests/test_mlp2_persistent_gpu.py.  Every tensor is checked on its own, its
+    moments too (m is linear in the gradient, so a lost rank's contribution shows there even
+    where AdamW's scale-invariant update hides it); a tensor too small for a bulk statistic
+    (the 10-element output bias) is held to the p99.9 bound at its maximum."""
     for k in ("1", "0"):
         _spawn8(XW.fsdp_xgmi, ws, str(tmp_path), True, 7, 2, 1e-8, "0", hidden, k, f"p{k}")
     a, b = _load(tmp_path, "fsx2p1", ws), _load(tmp_path, "fsx2p0", ws)
     assert all(o["one_launch"] and o["pst"] for o in a), [(o["one_launch"], o["pst"]) for o in a]
     assert all(o["one_launch"] and not o["pst"] for o in b)
-    for oa, ob in zip(a, b):
+
+    def close(x, ref, what):
+        d = (x - ref).abs().flatten().float().sort().values
+        scale = float(ref.abs().max())
+        med, q999, mx = float(d[len(d) // 2]), float(d[int(0.999 * (len(d) - 1))]), float(d[-1])
+        print(f"[fsdp pst ws={ws}] {what}: n {d.numel()} max {mx:.3e} median {med:.3e} (scale {scale:.3e})")
+        if d.numel() >= 1024:
+            assert med <= 1e-5 * scale and q999 <= 1e-4 * scale, what
+        else:
+            assert mx <= 1e-4 * scale, what
+
+    for r, (oa, ob) in enumerate(zip(a, b)):
         for name in oa["local"]:
-            ref = ob["local"][name]
-            d = (oa["local"][name] - ref).abs().flatten().float().sort().values
-            scale = float(ref.abs().max())
-            assert float(d[len(d) // 2]) <= 1e-5 * scale and float(d[int(0.999 * (len(d) - 1))]) <= 1e-4 * scale, name
-        for k in ("m", "v"):
-            d = (oa[k] - ob[k]).abs().float().sort().values
-            scale = float(ob[k].abs().max())
-            print(f"[fsdp pst ws={ws}] {k}: max {float(d[-1]):.3e} median {float(d[len(d) // 2]):.3e}")
-            assert float(d[len(d) // 2]) <= 1e-5 * scale and float(d[int(0.999 * (len(d) - 1))]) <= 1e-4 * scale, k
+            close(oa["local"][name], ob["local"][name], f"rank {r} {name}")
+            off, n = oa["offsets"][name]
+            for k in ("m", "v"):
+                close(oa[k][off:off + n], ob[k][off:off + n], f"rank {r} {name} {k}")
     torch.testing.assert_close(a[0]["metrics"], b[0]["metrics"], rtol=1e-5, atol=1e-3)
 
 

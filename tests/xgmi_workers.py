@@ -251,6 +251,7 @@ def fsdp_xgmi(outdir, fused=True, steps=3, num_layers=2, eps=1e-8, deep_fx="0", 
     _save(outdir, f"fsx{num_layers}{tag}", {"local": {n: sp.local.p(n).cpu() for n in sp.part},
                           "m": o["m"][:sp.local.numel].cpu(), "v": o["v"][:sp.local.numel].cpu(),
                           "pst": bool(getattr(getattr(tr, "fused", None), "pst_ok", False)),
+                          "offsets": {n: (o_, int(torch.Size(s_).numel())) for n, (o_, s_) in sp.local.offsets.items()},
                           "dims": {n: sp.part[n].shard_dim for n in sp.part},
                           "metrics": tr.metrics.cpu(), "comm": tr.comm_backend, "xg_names": list(sp._xg_names),
                           "fused_comm": getattr(tr, "_plan", None) is not None or tr.one_launch,

@@ -2240,7 +2240,7 @@ JDT_API void jdt_gemm_set_group_tile(int t) { g_group_tile = t; }
 // The W pass (gemm_wpass_kernel): plan the prefix table of `n` weight-gradient problems
 // into `out` (host memory; the caller copies it to the device once and replays it) for
 // tile config `cfg` (0: 64 x 64 of 16x16x32 MFMAs, 1: 64 x 64 of 32x32x16, 2: 128 x 128
-// of 32x32x16, 3: 32 x 64).  Split-K per problem while the whole launch has fewer than
+// of 32x32x16, 3: 32 x 64, 4: 64 x 128, 5: 128 x 64).  Split-K per problem while the whole launch has fewer than
 // two workgroups per CU.  Returns the workgroup count, or < 0 outside the envelope (a
 // problem not "km" x "kn" bf16 with 16-byte aligned operands and fp32 output rows, a
 // shape not a multiple of the tile, K not a multiple of 64, > WP_MAX problems).
@@ -2292,6 +2292,8 @@ JDT_API int jdt_gemm_wpass_plan(const GemmArgs* gs, int n, int cfg, void* out, f
     case 0: case 1: return wpass_plan<64, 64>(gs, n, t, ws, ws_floats, counters, n_counters);
     case 2: return wpass_plan<128, 128>(gs, n, t, ws, ws_floats, counters, n_counters);
     case 3: return wpass_plan<32, 64>(gs, n, t, ws, ws_floats, counters, n_counters);
+    case 4: return wpass_plan<64, 128>(gs, n, t, ws, ws_floats, counters, n_counters);
+    case 5: return wpass_plan<128, 64>(gs, n, t, ws, ws_floats, counters, n_counters);
     default: return -2;
   }
 }
@@ -2305,6 +2307,9 @@ JDT_API int jdt_gemm_wpass_launch(const void* table_dev, int total, int cfg, voi
     case 1: hipLaunchKernelGGL((gemm_wpass_kernel<1, 1, 32, 3>), dim3(total), dim3(256), 0, st, t); break;
     case 2: hipLaunchKernelGGL((gemm_wpass_kernel<2, 2, 32, 3>), dim3(total), dim3(256), 0, st, t); break;
     case 3: hipLaunchKernelGGL((gemm_wpass_kernel<1, 2, 16, 3>), dim3(total), dim3(256), 0, st, t); break;
+    // 2 workgroups per CU (74 KB of LDS each): one's AdamW epilogue under the other's main loop
+    case 4: hipLaunchKernelGGL((gemm_wpass_kernel<1, 2, 32, 3>), dim3(total), dim3(256), 0, st, t); break;
+    case 5: hipLaunchKernelGGL((gemm_wpass_kernel<2, 1, 32, 3>), dim3(total), dim3(256), 0, st, t); break;
     default: return -2;
   }
   return HIP_LAUNCH_CHECK();

@@ -400,7 +400,11 @@ def _launch_gemm(g, batch: int, cfg: int, splits: int, device):
 _GROUP: list = []
 _WPASS: list = []
 _WPASS_PLANS: dict = {}
-WPASS_CFG = int(os.environ.get("JDT_WPASS_CFG", "0"))
+# tile config of the one-launch W pass (csrc/gemm.hip jdt_gemm_wpass_launch): 4 = 64 x 128
+# tiles of 32x32x16 MFMAs, two workgroups per CU (one's AdamW epilogue under the other's
+# main loop) -- 109 us alone vs 126 (cfg 2, 128 x 128) and 143 (cfg 0, 64 x 64); LM step
+# 0.879 vs 0.906 ms (profiles/r6_s6_floor_wpass.txt)
+WPASS_CFG = int(os.environ.get("JDT_WPASS_CFG", "4"))
 
 
 @contextlib.contextmanager

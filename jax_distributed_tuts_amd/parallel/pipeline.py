@@ -136,7 +136,10 @@ class PipeConfig:
     # weight gradients deferred the chains share no buffer (every cross-microbatch
     # accumulation -- bias / LayerNorm / embedding grads, metrics -- is an fp32 atomic,
     # split-K slabs are per stream), and a 512-row microbatch GEMM fills half the CUs.
-    mb_streams: int = field(default_factory=lambda: int(os.environ.get("JDT_MB_STREAMS", "4")))
+    # 0 (default) = auto: 4, except a one-stage model whose layer-major pass takes the
+    # one-launch W pass (below) -- the LM step measured 0.91 ms that way against 1.01 on
+    # 4 microbatch streams (profiles/r6_s5_lm.txt)
+    mb_streams: int = field(default_factory=lambda: int(os.environ.get("JDT_MB_STREAMS", "0")))
     # one stage, layer-major (one pass over all rows), GPU: weight gradients deferred and
     # issued per part on this many streams, overlapping the input-gradient chain
     # (GPipeTrainer._layer_major_wpass); 1 = the weight GEMMs inline in the backward.
@@ -648,7 +651,12 @@ class GPipeTrainer:
         never more than the process's HIP hardware queues (GPU_MAX_HW_QUEUES when set:
         a 4-stream graph on 2 queues crashed the runtime in a probe,
         profiles/r3_lm_mb_streams_ab.txt)."""
-        k = min(int(self.cfg.mb_streams), self.cfg.num_microbatches, hw_queues())
+        want = int(self.cfg.mb_streams)
+        if want <= 0:   # auto: the layer-major pass with its one-launch W pass where it applies
+            one = (self.S == 1 and self.cfg.layer_major_single_stage and _no_dropout(self.model)
+                   and self.cfg.wpass_streams <= 1 and self._wpass_one_ok() and hasattr(self.model, "weight_grads_of"))
+            want = 1 if one else 4
+        k = min(want, self.cfg.num_microbatches, hw_queues())
         ok = (self._streams_ok() and self.cfg.defer_wgrad and hasattr(self.model, "weight_grads")
               and not self.cfg.merge_single_stage)
         return k if ok else 1
@@ -727,7 +735,7 @@ class GPipeTrainer:
         """Concurrent streams of a multi-stage MLP stage's microbatch chains (1: serial)."""
         if self.S == 1 or not self._streams_ok():
             return 1
-        return max(1, min(int(self.cfg.mb_streams), self.cfg.num_microbatches, hw_queues()))
+        return max(1, min(int(self.cfg.mb_streams) or 4, self.cfg.num_microbatches, hw_queues()))
 
     def _compute_fused(self, batch: Batch, eng, n_mb: int, mb: int):
         """The same GPipe fill/drain schedule on the fused stage kernels.  With

@@ -163,7 +163,8 @@ def test_stream_schedules_resolve_on_cpu(monkeypatch):
 
     monkeypatch.delenv("JDT_MB_STREAMS", raising=False)
     monkeypatch.delenv("JDT_LOOP_STREAMS", raising=False)
-    assert PipeConfig().mb_streams == 4 and PipeConfig().wpass_early == 0 and PipeConfig().wpass_rr == 0
+    # mb_streams 0 = auto: 4 streams, or 1 (layer-major) where the one-launch W pass applies (GPU)
+    assert PipeConfig().mb_streams == 0 and PipeConfig().wpass_early == 0 and PipeConfig().wpass_rr == 0
     cfg = TransformerConfig(n_layers=1, d_model=64, n_heads=1, d_ff=128, seq_len=16, vocab_size=64)
     for lm, mode in ((True, "layer-major"), (False, "microbatch-loop")):
         tr, _ = build_lm_pipeline(None, "cpu", cfg, num_microbatches=4, layer_major_single_stage=lm)

@@ -43,7 +43,7 @@ def timed(fn):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cfgs", default="0,1,2,3")
+    ap.add_argument("--cfgs", default="0,1,2,3,4,5")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)

@@ -57,6 +57,7 @@ _SIGS = {
                                  c_float, c_float, c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p]),
     "jdt_gemm": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p]),
     "jdt_gemm_args_size": (c_int, []),
+    "jdt_gemm_set_wt": (c_int, [c_int]),
     "jdt_gemm_group": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_void_p, c_long, c_void_p, c_long, c_void_p]),
     "jdt_gemm_wpass_table_bytes": (c_int, []),
     "jdt_gemm_wpass_plan": (c_int, [ctypes.POINTER(GemmArgs), c_int, c_int, c_void_p, c_void_p, c_long, c_void_p,
@@ -159,6 +160,8 @@ def lib():
             l.jdt_gemm_set_r(int(os.environ["JDT_GEMM_R"]))
         if os.environ.get("JDT_GEMM_GROUP_M"):  # A/B: LDS-DMA GEMM tile order in row-groups of G tiles
             l.jdt_gemm_set_group_m(int(os.environ["JDT_GEMM_GROUP_M"]))
+        if os.environ.get("JDT_GEMM_WT"):  # A/B: write-through GEMM epilogue stores (1: C / Zout, 2: AdamW, 3: both)
+            check(l.jdt_gemm_set_wt(int(os.environ["JDT_GEMM_WT"])), "jdt_gemm_set_wt")
         if os.environ.get("JDT_LN_WAVES"):  # A/B: force LayerNorm-backward waves per workgroup (0 = auto)
             l.jdt_ln_set_waves(int(os.environ["JDT_LN_WAVES"]))
         _lib = l

@@ -86,9 +86,32 @@ __device__ __forceinline__ float opt_update(const GemmArgs& g, const OptBC& bc, 
   return pp;
 }
 
+// Write-through 16-byte store (two relaxed agent-scope 8-byte atomic stores: global_store
+// ... sc1): the line goes past this XCD's L2 while the kernel runs instead of staying
+// dirty until the kernel-end release writes the L2 back (jdt_gemm_set_wt; A/B).
+typedef __attribute__((address_space(1))) unsigned long long gm_u64;
+__device__ __forceinline__ void st16(void* p, u32x4 v, bool wt) {
+  if (wt) {
+    __hip_atomic_store((gm_u64*)p, (unsigned long long)v[0] | ((unsigned long long)v[1] << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gm_u64*)p + 1, (unsigned long long)v[2] | ((unsigned long long)v[3] << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    *reinterpret_cast<u32x4*>(p) = v;
+  }
+}
+__device__ __forceinline__ void st16f(float* p, float4 x, bool wt) {
+  u32x4 v;
+  v[0] = __float_as_uint(x.x); v[1] = __float_as_uint(x.y); v[2] = __float_as_uint(x.z); v[3] = __float_as_uint(x.w);
+  st16(p, v, wt);
+}
+// bit 0: C / Zout stores of the vectorised epilogue; bit 1: its AdamW state and shadow stores
+__device__ int g_gemm_wt_dev = 0;
+
 // The same for 8 consecutive elements (16-byte aligned): p / m / v as float4 pairs,
 // the bf16 shadow as one 16-byte store -- the vectorised epilogue's unit.
-__device__ __forceinline__ u32x4 opt_update8(const GemmArgs& g, const OptBC& bc, long i, const float (&grad)[8]) {
+__device__ __forceinline__ u32x4 opt_update8(const GemmArgs& g, const OptBC& bc, long i, const float (&grad)[8],
+                                             bool wt = false) {
   float4* P4 = reinterpret_cast<float4*>(g.opt_p + i);
   float4* M4 = reinterpret_cast<float4*>(g.opt_m + i);
   float4* V4 = reinterpret_cast<float4*>(g.opt_v + i);
@@ -103,12 +126,12 @@ __device__ __forceinline__ u32x4 opt_update8(const GemmArgs& g, const OptBC& bc,
     v[k] = g.opt_b2 * v[k] + (1.f - g.opt_b2) * gr * gr;
     p[k] -= g.opt_lr * ((m[k] * bc.rbc1) / (sqrtf(v[k] * bc.rbc2) + g.opt_eps) + g.opt_wd * p[k]);
   }
-  P4[0] = make_float4(p[0], p[1], p[2], p[3]);
-  P4[1] = make_float4(p[4], p[5], p[6], p[7]);
-  M4[0] = make_float4(m[0], m[1], m[2], m[3]);
-  M4[1] = make_float4(m[4], m[5], m[6], m[7]);
-  V4[0] = make_float4(v[0], v[1], v[2], v[3]);
-  V4[1] = make_float4(v[4], v[5], v[6], v[7]);
+  st16f(g.opt_p + i, make_float4(p[0], p[1], p[2], p[3]), wt);
+  st16f(g.opt_p + i + 4, make_float4(p[4], p[5], p[6], p[7]), wt);
+  st16f(g.opt_m + i, make_float4(m[0], m[1], m[2], m[3]), wt);
+  st16f(g.opt_m + i + 4, make_float4(m[4], m[5], m[6], m[7]), wt);
+  st16f(g.opt_v + i, make_float4(v[0], v[1], v[2], v[3]), wt);
+  st16f(g.opt_v + i + 4, make_float4(v[4], v[5], v[6], v[7]), wt);
   u32x4 o;
 #pragma unroll
   for (int k = 0; k < 4; ++k) o[k] = (unsigned)f2bf(p[2 * k]) | ((unsigned)f2bf(p[2 * k + 1]) << 16);
@@ -634,6 +657,8 @@ __device__ __forceinline__ void gemm_finish_img(const GemmArgs& g, int tm0, int 
   for (int k = 0; k < 8; ++k) cs[k] = 0.f;
   const long cbase = zoff(g, z, g.sC, g.sC2);
   const OptBC obc = opt_bc(g);
+  const int wtm = g_gemm_wt_dev;
+  const bool wt_c = wtm & 1, wt_o = (wtm >> 1) & 1;
   // rows per unit: one dropout group (4 rows) with dropout, else ONE row -- on a 32-row
   // tile that is 4x the threads of the epilogue busy (NU = one wave's worth of 4-row
   // units), which matters for the memory-heavy epilogues (fused AdamW: 26 B/element)
@@ -663,7 +688,7 @@ __device__ __forceinline__ void gemm_finish_img(const GemmArgs& g, int tm0, int 
         u32x4 o;
 #pragma unroll
         for (int k = 0; k < 4; ++k) o[k] = (unsigned)f2bf(v[2 * k]) | ((unsigned)f2bf(v[2 * k + 1]) << 16);
-        *reinterpret_cast<u32x4*>(static_cast<bf16_t*>(g.Zout) + (long)z * g.sZ + (long)row * g.ldz + col) = o;
+        st16(static_cast<bf16_t*>(g.Zout) + (long)z * g.sZ + (long)row * g.ldz + col, o, wt_c);
       }
       if (g.Zin) {
         const u32x4 p = *reinterpret_cast<const u32x4*>(g.Zin + (long)z * g.sZin + (long)row * g.ldzin + col);
@@ -694,7 +719,7 @@ __device__ __forceinline__ void gemm_finish_img(const GemmArgs& g, int tm0, int 
           Cp[0] = make_float4(0.f, 0.f, 0.f, 0.f);
           Cp[1] = Cp[0];
         }
-        *reinterpret_cast<u32x4*>(g.opt_s + co) = opt_update8(g, obc, co, v);
+        st16(g.opt_s + co, opt_update8(g, obc, co, v, wt_o), wt_o);
       } else if (g.c_f32) {
         float4* Cp = reinterpret_cast<float4*>(static_cast<float*>(g.C) + co);
         float4 o0 = make_float4(v[0], v[1], v[2], v[3]), o1 = make_float4(v[4], v[5], v[6], v[7]);
@@ -703,8 +728,8 @@ __device__ __forceinline__ void gemm_finish_img(const GemmArgs& g, int tm0, int 
           o0.x = c0.x + o0.x; o0.y = c0.y + o0.y; o0.z = c0.z + o0.z; o0.w = c0.w + o0.w;
           o1.x = c1.x + o1.x; o1.y = c1.y + o1.y; o1.z = c1.z + o1.z; o1.w = c1.w + o1.w;
         }
-        Cp[0] = o0;
-        Cp[1] = o1;
+        st16f(reinterpret_cast<float*>(Cp), o0, wt_c);
+        st16f(reinterpret_cast<float*>(Cp + 1), o1, wt_c);
       } else {
         u32x4* Cp = reinterpret_cast<u32x4*>(static_cast<bf16_t*>(g.C) + co);
         u32x4 o;
@@ -722,7 +747,7 @@ __device__ __forceinline__ void gemm_finish_img(const GemmArgs& g, int tm0, int 
 #pragma unroll
           for (int k = 0; k < 4; ++k) o[k] = (unsigned)f2bf(v[2 * k]) | ((unsigned)f2bf(v[2 * k + 1]) << 16);
         }
-        *Cp = o;
+        st16(Cp, o, wt_c);
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) cs[k] += v[k];
@@ -2160,6 +2185,11 @@ JDT_API void jdt_gemm_set_epi_vec(int on) { g_epi_vec = on; }
 JDT_API void jdt_gemm_set_epi_vec_min(long n) { g_epi_vec_min = n; }
 JDT_API void jdt_gemm_set_r(int r) { g_dma_r = r; }
 JDT_API void jdt_gemm_set_tune(int on) { g_gemm_tune = on; }
+// write-through stores in the vectorised GEMM epilogue (bit 0: C / Zout, bit 1: AdamW state
+// + shadow); a device global read once per epilogue, set before any capture (A/B)
+JDT_API int jdt_gemm_set_wt(int mask) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_wt_dev), &mask, sizeof(int)) == hipSuccess ? 0 : -1;
+}
 
 JDT_API int jdt_gemm(const GemmArgs* ga, int batch, int cfg, int splits, float* ws, long ws_floats,
                      unsigned* counters, long n_counters, void* stream) {

@@ -162,6 +162,8 @@ def lib():
             l.jdt_gemm_set_group_m(int(os.environ["JDT_GEMM_GROUP_M"]))
         if os.environ.get("JDT_GEMM_WT"):  # A/B: write-through GEMM epilogue stores (1: C / Zout, 2: AdamW, 3: both)
             check(l.jdt_gemm_set_wt(int(os.environ["JDT_GEMM_WT"])), "jdt_gemm_set_wt")
+        if os.environ.get("JDT_LN_GEMM_CFG"):  # A/B: force the LN-fused GEMM's tile (any row count; 0 = heuristic)
+            l.jdt_gemm_ln_set_cfg(int(os.environ["JDT_LN_GEMM_CFG"]))
         if os.environ.get("JDT_LN_WAVES"):  # A/B: force LayerNorm-backward waves per workgroup (0 = auto)
             l.jdt_ln_set_waves(int(os.environ["JDT_LN_WAVES"]))
         _lib = l

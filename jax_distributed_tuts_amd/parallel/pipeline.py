@@ -553,7 +553,10 @@ class GPipeTrainer:
         streams as soon as the chain has produced that part's output gradients
         (TransformerLM.backward ``after`` hook), overlapping the rest of the chain."""
         k = int(self.cfg.wpass_streams)
-        if k <= 1 and self._wpass_one_ok() and hasattr(self.model, "weight_grads_of"):
+        # (the opt-in layer-by-layer side-stream AdamW needs each layer's gradients final
+        # as the backward passes it: the inline weight GEMMs of the plain pass)
+        if (k <= 1 and self._wpass_one_ok() and hasattr(self.model, "weight_grads_of")
+                and (eo is not None or self._overlapped_opt() is None)):
             return self._layer_major_one_wpass(batch, P, st, seed, eo, n_mb)
         if k <= 1 or self.dev.type != "cuda" or not hasattr(self.model, "weight_grads_of"):
             return False

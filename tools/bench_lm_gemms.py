@@ -5,7 +5,9 @@ GEMM without the epilogue: 50 copies captured in one hipGraph, operands rotated 
 buffer sets so most reads miss the L2 as in the model.  Tells how much of an in-model
 GEMM is the epilogue and how much is the main loop on cold operands.
 
-    python tools/bench_lm_gemms.py
+    python tools/bench_lm_gemms.py [--sweep 10,11,15,...]
+
+--sweep: every case again with each forced tile config (ops.kernels.gemm cfg=).
 """
 from __future__ import annotations
 
@@ -15,6 +17,8 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import argparse  # noqa: E402
 
 from jax_distributed_tuts_amd.ops import kernels as K  # noqa: E402
 
@@ -48,6 +52,9 @@ def timed(fn, n=50, reps=10):
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sweep", default="")
+    a = ap.parse_args()
     torch.cuda.set_device(0)
     W = {n: [bf(k, m) for _ in range(SETS)] for n, (k, m) in
          {"qkv": (D, 3 * D), "out": (D, D), "fc1": (D, F), "fc2": (F, D), "head": (D, V)}.items()}
@@ -86,6 +93,22 @@ def main():
         tot += t
         print(f"{name:18s} {t:7.2f} us  (no epilogue {tp:7.2f})")
     print(f"sum {tot:.1f} us (x4 layers for the per-layer ones in the step)")
+    if not a.sweep:
+        return
+    cfgs = [int(c) for c in a.sweep.split(",")]
+    orig = K.gemm
+    for name, fn, _ in cases:
+        row = []
+        for c in cfgs:
+            K.gemm = lambda *args, _c=c, **kw: orig(*args, cfg=_c, **kw)
+            try:
+                row.append(f"{c}:{timed(fn):6.2f}")
+            except Exception as e:  # noqa: BLE001 -- a tile outside the shape's envelope
+                row.append(f"{c}:  n/a ")
+                print(f"  ({name} cfg {c}: {str(e)[:60]})", file=sys.stderr)
+            finally:
+                K.gemm = orig
+        print(f"{name:18s} " + "  ".join(row))
 
 
 if __name__ == "__main__":

@@ -469,7 +469,8 @@ def main():
     run(args.steps)
     sync()
     D.barrier()
-    sync()
+    if D.is_initialized():
+        sync()   # an RCCL barrier is device work; without a process group there is none to wait for
     dt = time.perf_counter() - t0
     if D.is_initialized():
         t = torch.tensor([dt], dtype=torch.float64, device=dev if D.backend() == "nccl" else "cpu")

@@ -166,6 +166,10 @@ def lib():
             l.jdt_gemm_ln_set_cfg(int(os.environ["JDT_LN_GEMM_CFG"]))
         if os.environ.get("JDT_LN_WAVES"):  # A/B: force LayerNorm-backward waves per workgroup (0 = auto)
             l.jdt_ln_set_waves(int(os.environ["JDT_LN_WAVES"]))
+        if os.environ.get("JDT_XENT_RPW"):  # A/B: force the wide-vocabulary CE kernel's rows per wave
+            l.jdt_xent_set_rpw(int(os.environ["JDT_XENT_RPW"]))
+        if os.environ.get("JDT_LN_ROWS"):  # A/B: force LayerNorm-backward rows per wave (0 = auto)
+            l.jdt_ln_set_rows(int(os.environ["JDT_LN_ROWS"]))
         _lib = l
         return _lib
 
@@ -179,3 +183,4 @@ def stream_ptr(device=None) -> int:
     import torch
 
     return torch.cuda.current_stream(device).cuda_stream
+

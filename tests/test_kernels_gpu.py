@@ -1090,6 +1090,9 @@ def test_overlapped_adamw_equals_single_launch(graph, monkeypatch):
         monkeypatch.setenv("JDT_OVERLAP_OPT", ov[0])
         monkeypatch.setenv("JDT_LM_FUSED_OPT", "0")  # the in-epilogue AdamW would take precedence
         monkeypatch.setenv("JDT_MB_STREAMS", "1")    # layer-major (concurrent microbatch passes otherwise)
+        # the weight GEMMs inline in every variant: the comparison isolates where AdamW runs
+        # (the one-launch W pass, which the overlapped form cannot use, sums in another order)
+        monkeypatch.setenv("JDT_WPASS_ONE", "0")
         tr, lcfg = build_lm_pipeline(mesh, DEV, num_microbatches=4)
         b = lm_batch(lcfg, global_batch=8, seed=1)
         b = Batch(b.inputs.to(DEV), b.labels.to(DEV))

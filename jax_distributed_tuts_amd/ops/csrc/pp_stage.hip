@@ -884,8 +884,10 @@ JDT_API long jdt_pp_stage_gstride(int k) { return ps_g_size(k); }
 // 1 if `nshare` ranks' stage launches (PS_NB workgroups each) can all be resident on
 // this GPU at once (every wait of the launch is on a co-resident workgroup or a
 // neighbour's launch), with half the device's workgroup slots to spare for the other
-// ranks' kernels when the GPU is shared.
-JDT_API int jdt_pp_stage_ok(int first, int last, int nshare) {
+// ranks' kernels when the GPU is shared -- unless `spare` is 0: then every slot may hold
+// a stage workgroup (8 stages x 32 workgroups on the 256 CUs, one per CU: the 8-stage
+// test of the stage protocol on one GPU; the waits' timeouts bound a placement failure).
+JDT_API int jdt_pp_stage_ok(int first, int last, int nshare, int spare) {
   int dev = 0, cus = 0, per = 0;
   if (nshare < 1 || hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -896,7 +898,7 @@ JDT_API int jdt_pp_stage_ok(int first, int last, int nshare) {
   else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pp_stage_kernel<false, false>, PS_NT, 0);
   if (e != hipSuccess || per < 1) return 0;
   const long slots = (long)cus * per;
-  return (long)nshare * PS_NB <= (nshare > 1 ? slots / 2 : slots) ? 1 : 0;
+  return (long)nshare * PS_NB <= (nshare > 1 && spare ? slots / 2 : slots) ? 1 : 0;
 }
 
 // 1 if a chain of `S` stages (S x PS_NB workgroups of the one-GPU chain launch) can all be

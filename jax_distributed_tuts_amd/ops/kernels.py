@@ -50,7 +50,27 @@ def workspace(device):
         w = (torch.empty(WS_FLOATS, dtype=torch.float32, device=device),
              torch.zeros(N_COUNTERS, dtype=torch.int32, device=device))
         _WS[key] = w
+    if device.type == "cuda" and not torch.cuda.is_current_stream_capturing():
+        _capture_workspace(device)
     return w
+
+
+def _capture_workspace(device):
+    """The workspace of torch's default graph-capture stream, made (and its counters
+    zeroed) eagerly: created during a capture instead, the counters' zero-fill kernel
+    would be RECORDED into that graph and run at every replay (4.6 us per LM step)."""
+    cls = torch.cuda.graphs.graph
+    if cls.default_capture_stream is None:
+        cls.default_capture_stream = torch.cuda.Stream()   # what torch.cuda.graph would create
+    s = cls.default_capture_stream
+    key = (device.type, device.index, s.cuda_stream)
+    if key not in _WS and s.device == device:
+        cur = torch.cuda.current_stream(device)
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            _WS[key] = (torch.empty(WS_FLOATS, dtype=torch.float32, device=device),
+                        torch.zeros(N_COUNTERS, dtype=torch.int32, device=device))
+        cur.wait_stream(s)
 
 
 class WGradStream:

@@ -56,7 +56,7 @@ class PsArgs(ctypes.Structure):
 
 _lib.declare("jdt_pp_stage_args_size", c_int, [])
 _lib.declare("jdt_pp_stage_gstride", c_long, [c_int])
-_lib.declare("jdt_pp_stage_ok", c_int, [c_int, c_int, c_int])
+_lib.declare("jdt_pp_stage_ok", c_int, [c_int, c_int, c_int, c_int])
 _lib.declare("jdt_pp_stage", c_int, [ctypes.POINTER(PsArgs), c_int, c_int, c_void_p])
 _lib.declare("jdt_p2p_max_slots", c_int, [])
 _lib.declare("jdt_p2p_peer", c_int, [c_void_p, c_int, ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p),
@@ -121,7 +121,10 @@ def local_ok(trainer, mb: int) -> bool:
         return False
     from ..runtime.dist import ranks_per_gpu
 
-    return bool(_lib.lib().jdt_pp_stage_ok(int(trainer.first), int(trainer.last), ranks_per_gpu()))
+    # JDT_PP_STAGE_SPARE=0: ranks sharing the GPU may fill every workgroup slot with stage
+    # workgroups (tests: the 8-stage protocol on one GPU); default: keep half free
+    spare = 0 if os.environ.get("JDT_PP_STAGE_SPARE") == "0" else 1
+    return bool(_lib.lib().jdt_pp_stage_ok(int(trainer.first), int(trainer.last), ranks_per_gpu(), spare))
 
 
 class PPStageKernel:

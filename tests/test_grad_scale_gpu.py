@@ -293,11 +293,15 @@ def test_xgmi_strategies_grad_scale(tmp_path, kind, ws):
             check_grad(g, want[n], n)
 
 
-@pytest.mark.parametrize("ws", [2, 4])
-def test_pipeline_stage_kernel_adam_scale(tmp_path, ws):
+@pytest.mark.parametrize("ws", [2, 4, 8])
+def test_pipeline_stage_kernel_adam_scale(tmp_path, ws, monkeypatch):
     """One layer per stage, AdamW eps = 10 (update ~ gradient): each stage's step is the
     in-kernel GPipe launch (ops/csrc/pp_stage.hip: dZ hops, dH from the successor's weight
-    image, register-held dW, AdamW at the end) -- its update equals the fp64 oracle's."""
+    image, register-held dW, AdamW at the end) -- its update equals the fp64 oracle's.
+    ws = 8: BASELINE config #4's 8-stage layout, the 8 ranks' stage grids filling the one
+    GPU's 256 CUs (JDT_PP_STAGE_SPARE=0 lifts the half-free rule for ranks sharing it)."""
+    if ws == 8:
+        monkeypatch.setenv("JDT_PP_STAGE_SPARE", "0")
     from pipeline_parallel import pp_mlp_dims
     from jax_distributed_tuts_amd.models.mlp import MLP
     from jax_distributed_tuts_amd.utils.config import dp_config

@@ -296,14 +296,18 @@ def test_pipeline_over_xgmi_matches_single_device(tmp_path, ws, dp, n_hidden):
     assert abs(float(m[0]) - float(rm[0])) <= 2e-3 * abs(float(rm[0])) + 1e-3
 
 
-@pytest.mark.parametrize("ws,n_mb", [(2, 4), (4, 4), (2, 2), (4, 2)])
-def test_pipeline_stage_kernel_equals_per_tick_launches(tmp_path, ws, n_mb):
+@pytest.mark.parametrize("ws,n_mb", [(2, 4), (4, 4), (2, 2), (4, 2), (8, 4), (8, 2)])
+def test_pipeline_stage_kernel_equals_per_tick_launches(tmp_path, ws, n_mb, monkeypatch):
     """The in-kernel GPipe step (one persistent launch per stage: in-kernel inbox waits,
     hand-offs, register-held weight gradients, AdamW at the end) == the per-tick launches
     (receive / md layer kernel / dX GEMM / send per tick), dropout ON: the same Philox
     streams, only fp32 summation order differs.  n_mb = 4 / 2: 32- / 64-row microbatches
-    (16 / 32 rows per row half: the dW k-step's zero rows / whole)."""
+    (16 / 32 rows per row half: the dW k-step's zero rows / whole).  ws = 8: BASELINE
+    config #4's 8 stages, their grids filling the one GPU (JDT_PP_STAGE_SPARE=0)."""
     import functools
+
+    if ws == 8:
+        monkeypatch.setenv("JDT_PP_STAGE_SPARE", "0")
 
     n_hidden = ws   # one layer per stage, the head on the last
     for k in ("1", "0"):

@@ -89,6 +89,9 @@ _SIGS = {
     "jdt_act_bwd": (c_int, [c_void_p, c_void_p, c_int, c_float, c_ulonglong, c_ulonglong, c_void_p, c_void_p, c_int, c_int,
                             c_void_p, c_void_p, c_void_p]),
     "jdt_metrics_fold": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    "jdt_metrics_fold_slab": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "jdt_xent_slab": (c_int, [c_void_p, c_int, c_long, c_void_p, c_int, c_int, c_float, c_void_p, c_long, c_void_p,
+                              c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "jdt_ln_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,
                            c_void_p]),
     "jdt_ln_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

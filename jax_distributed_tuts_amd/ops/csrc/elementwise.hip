@@ -43,6 +43,36 @@ __global__ void metrics_fold_kernel(float* running, float* slot, int n) {
   if (i < n) { running[i] += slot[i]; slot[i] = 0.f; }
 }
 
+// metrics_fold_slab: running[0:4] += slot[0:4] + (sum of the slab's rows as {loss, n,
+// correct, n}); slot = 0, every slab row = 0; then (step non-null) the device step += 1 --
+// the step-end fold of a pass whose CE wrote per-workgroup metric rows (jdt_xent_slab) and
+// whose AdamW ranges ran without advancing the step, beside the W pass that also reads it
+__global__ void __launch_bounds__(256) metrics_fold_slab_kernel(float* running, float* slot, int n,
+                                                                float4* __restrict__ slab, int cap, int* step) {
+  __shared__ float red[3][256];
+  const int t = threadIdx.x;
+  float a = 0.f, b = 0.f, c = 0.f;
+  for (int i = t; i < cap; i += 256) {
+    const float4 r = slab[i];
+    a += r.x; b += r.y; c += r.z;
+    slab[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  red[0][t] = a; red[1][t] = b; red[2][t] = c;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      red[0][t] += red[0][t + o]; red[1][t] += red[1][t + o]; red[2][t] += red[2][t + o];
+    }
+    __syncthreads();
+  }
+  if (t < n) {
+    const float add = t == 0 ? red[0][0] : (t == 2 ? red[2][0] : (t < 4 ? red[1][0] : 0.f));
+    running[t] += slot[t] + add;
+    slot[t] = 0.f;
+  }
+  if (t == 0 && step) step[0] = step[0] + 1;
+}
+
 }  // namespace jdt
 using namespace jdt;
 
@@ -60,5 +90,12 @@ JDT_API int jdt_act_bwd(const void* dh, const void* z, int act, float keep_prob,
 
 JDT_API int jdt_metrics_fold(float* running, float* slot, int n, void* stream) {
   hipLaunchKernelGGL(metrics_fold_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), running, slot, n);
+  return HIP_LAUNCH_CHECK();
+}
+
+JDT_API int jdt_metrics_fold_slab(float* running, float* slot, int n, float* slab, int cap, int* step, void* stream) {
+  if (n > 256 || cap < 0 || (reinterpret_cast<uintptr_t>(slab) & 15)) return -2;
+  hipLaunchKernelGGL(metrics_fold_slab_kernel, dim3(1), dim3(256), 0, static_cast<hipStream_t>(stream), running, slot,
+                     n, reinterpret_cast<float4*>(slab), cap, step);
   return HIP_LAUNCH_CHECK();
 }

@@ -134,7 +134,9 @@ __global__ void __launch_bounds__(256) adamw_ranges_kernel(float* __restrict__ p
     }
     adam_rows<AW_U>(p, g, m, v, shadow, idx, q0, stride, n4, lr, b1, b2, eps, wd, grad_scale, rbc1, rbc2, 1);
   }
-  finish_ticket(step, ticket);
+  // ticket null: the ranges run beside other readers of the step (the LM's W pass on the
+  // main stream); the caller advances the step after both (jdt_metrics_fold_slab)
+  if (ticket) finish_ticket(step, ticket);
 }
 
 // SGD (+ optional heavy-ball momentum and decoupled weight decay)
@@ -198,11 +200,12 @@ JDT_API int jdt_adamw(float* p, float* g, float* m, float* v, void* shadow, long
 }
 
 // ranges: device int64 start[nr] (element offsets, % 4 == 0), prefix[nr] (exclusive sums of
-// the lengths, each % 4 == 0); total = sum of the lengths.  Needs step and ticket.
+// the lengths, each % 4 == 0); total = sum of the lengths.  Needs step; ticket null = the
+// step is NOT advanced (the caller does it once every reader of the step has run).
 JDT_API int jdt_adamw_ranges(float* p, float* g, float* m, float* v, void* shadow, const long* start,
                              const long* prefix, int nr, long total, float lr, float b1, float b2, float eps, float wd,
                              float grad_scale, int* step, unsigned* ticket, void* stream) {
-  if (nr <= 0 || total <= 0 || (total & 3) || !step || !ticket || !shadow) return -2;
+  if (nr <= 0 || total <= 0 || (total & 3) || !step || !shadow) return -2;
   if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
        reinterpret_cast<uintptr_t>(v)) & 15) return -2;
   if (reinterpret_cast<uintptr_t>(shadow) & 7) return -2;

@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(256) xent_vec_kernel(const bf16_t* __restrict_
                                                        const int* __restrict__ labels, int M, int C, int rpw,
                                                        float grad_scale, bf16_t* __restrict__ dlogits, long ldd,
                                                        float* __restrict__ dbias, float* __restrict__ metrics,
-                                                       float* __restrict__ row_loss) {
+                                                       float* __restrict__ row_loss, float4* __restrict__ mslab) {
   __shared__ float red[4][4];
   __shared__ float part[4][512 * NV];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -198,7 +198,19 @@ __global__ void __launch_bounds__(256) xent_vec_kernel(const bf16_t* __restrict_
     for (int c = threadIdx.x; c < C; c += 256) atomicAdd(dbias + c, part[0][c] + part[1][c] + part[2][c] + part[3][c]);
   }
   // loss, validity and correctness are wave-uniform: lane 0 holds the wave's sums
-  if (metrics) xent_metrics_fold(red, w, lane, l_sum, n_valid, n_correct, metrics);
+  if (mslab) {
+    // this workgroup's (loss, n, correct) as one plain 16-byte store into its own slab row:
+    // 4 same-address atomics per workgroup serialise (6.4 us of an 18.3 us launch at M =
+    // 2048, tools/bench_xent.py); the step-end fold sums the rows (jdt_metrics_fold_slab)
+    if (lane == 0) { red[w][0] = l_sum; red[w][1] = n_valid; red[w][2] = n_correct; }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      mslab[blockIdx.x] = make_float4(red[0][0] + red[1][0] + red[2][0] + red[3][0],
+                                      red[0][1] + red[1][1] + red[2][1] + red[3][1],
+                                      red[0][2] + red[1][2] + red[2][2] + red[3][2], 0.f);
+  } else if (metrics) {
+    xent_metrics_fold(red, w, lane, l_sum, n_valid, n_correct, metrics);
+  }
 }
 
 }  // namespace jdt
@@ -207,8 +219,12 @@ using namespace jdt;
 static int g_xent_rpw = 0;
 JDT_API void jdt_xent_set_rpw(int r) { g_xent_rpw = r; }  // sweeps: rows per wave of the wide-vocabulary kernel
 
-JDT_API int jdt_xent(const void* logits, int logits_f32, long ld, const int* labels, int M, int C, float grad_scale,
-                     void* dlogits, long ldd, float* dbias, float* metrics, float* row_loss, void* stream) {
+// mslab (optional, capacity mslab_cap rows of 4 floats, zero on entry): the wide-vocabulary
+// kernel stores each workgroup's metric sums in its own row instead of adding them to
+// `metrics` (which then is not touched); returns 1 if it did, 0 if `metrics` got them.
+JDT_API int jdt_xent_slab(const void* logits, int logits_f32, long ld, const int* labels, int M, int C,
+                          float grad_scale, void* dlogits, long ldd, float* dbias, float* metrics, float* row_loss,
+                          float* mslab, int mslab_cap, void* stream) {
   if (M <= 0) return 0;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (!logits_f32 && C >= 256 && C % 8 == 0 && C <= 2048 && ld % 8 == 0 && ldd % 8 == 0 &&
@@ -219,18 +235,21 @@ JDT_API int jdt_xent(const void* logits, int logits_f32, long ld, const int* lab
     int rpw = M >= 2048 ? 4 : (M >= 512 ? 2 : 1);
     if (g_xent_rpw > 0) rpw = g_xent_rpw;
     dim3 vgrid((M + 4 * rpw - 1) / (4 * rpw));
+    float4* slab = (mslab && (int)vgrid.x <= mslab_cap && (reinterpret_cast<uintptr_t>(mslab) & 15) == 0)
+                       ? reinterpret_cast<float4*>(mslab) : nullptr;
     auto lg = static_cast<const bf16_t*>(logits);
     auto dl = static_cast<bf16_t*>(dlogits);
     if (C <= 512)
       hipLaunchKernelGGL(xent_vec_kernel<1>, vgrid, dim3(256), 0, st, lg, ld, labels, M, C, rpw, grad_scale, dl, ldd,
-                         dbias, metrics, row_loss);
+                         dbias, metrics, row_loss, slab);
     else if (C <= 1024)
       hipLaunchKernelGGL(xent_vec_kernel<2>, vgrid, dim3(256), 0, st, lg, ld, labels, M, C, rpw, grad_scale, dl, ldd,
-                         dbias, metrics, row_loss);
+                         dbias, metrics, row_loss, slab);
     else
       hipLaunchKernelGGL(xent_vec_kernel<4>, vgrid, dim3(256), 0, st, lg, ld, labels, M, C, rpw, grad_scale, dl, ldd,
-                         dbias, metrics, row_loss);
-    return HIP_LAUNCH_CHECK();
+                         dbias, metrics, row_loss, slab);
+    const int rc = HIP_LAUNCH_CHECK();
+    return rc < 0 ? rc : (slab ? 1 : 0);
   }
   dim3 grid((M + 3) / 4);
   if (logits_f32)
@@ -240,4 +259,11 @@ JDT_API int jdt_xent(const void* logits, int logits_f32, long ld, const int* lab
     hipLaunchKernelGGL(xent_kernel<false>, grid, dim3(256), 0, st, logits, ld, labels, M, C, grad_scale,
                        static_cast<bf16_t*>(dlogits), ldd, dbias, metrics, row_loss);
   return HIP_LAUNCH_CHECK();
+}
+
+JDT_API int jdt_xent(const void* logits, int logits_f32, long ld, const int* labels, int M, int C, float grad_scale,
+                     void* dlogits, long ldd, float* dbias, float* metrics, float* row_loss, void* stream) {
+  const int rc = jdt_xent_slab(logits, logits_f32, ld, labels, M, C, grad_scale, dlogits, ldd, dbias, metrics, row_loss,
+                               nullptr, 0, stream);
+  return rc < 0 ? rc : 0;
 }

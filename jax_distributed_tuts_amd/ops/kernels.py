@@ -543,9 +543,13 @@ def _gemm_ref(a, b, a_layout, b_layout, out, accumulate, alpha, bias, act, z_out
 # ----------------------------------------------------------------------------- cross-entropy
 def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, *, grad_scale: float = 1.0,
                  dlogits: Optional[torch.Tensor] = None, dbias: Optional[torch.Tensor] = None,
-                 metrics: Optional[torch.Tensor] = None, row_loss: Optional[torch.Tensor] = None):
+                 metrics: Optional[torch.Tensor] = None, row_loss: Optional[torch.Tensor] = None,
+                 mslab: Optional[torch.Tensor] = None):
     """Fused softmax-CE fwd+bwd.  Writes dlogits = (softmax - onehot) * grad_scale (bf16),
-    adds colsum(dlogits) into dbias, adds [loss_sum, n, correct, n] into metrics (fp32[4])."""
+    adds colsum(dlogits) into dbias, adds [loss_sum, n, correct, n] into metrics (fp32[4]).
+    ``mslab`` (GPU, fp32 [rows, 4], zero): the metric sums may instead go to one row per
+    workgroup (no same-address atomics); the caller then folds with
+    ``metrics_fold_(..., slab=mslab)``, which adds slot and slab."""
     M, C = logits.shape
     if not _is_gpu(logits):
         z = logits.float()
@@ -570,6 +574,14 @@ def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, *, grad_scale: floa
     assert labels.dtype == torch.int32 and labels.is_contiguous() and logits.stride(-1) == 1
     if dlogits is not None:
         assert dlogits.dtype == torch.bfloat16 and dlogits.stride(-1) == 1
+    if mslab is not None and metrics is not None:
+        assert mslab.is_cuda and mslab.dtype == torch.float32 and mslab.shape[-1] == 4 and mslab.is_contiguous()
+        rc = _lib.lib().jdt_xent_slab(_ptr(logits), int(logits.dtype == torch.float32), logits.stride(0),
+                                      _ptr(labels), M, C, float(grad_scale), _ptr(dlogits),
+                                      dlogits.stride(0) if dlogits is not None else 0, _ptr(dbias), _ptr(metrics),
+                                      _ptr(row_loss), _ptr(mslab), int(mslab.shape[0]), _lib.stream_ptr())
+        _lib.check(min(rc, 0), "jdt_xent_slab")   # 1: the slab took the sums, 0: the slot did
+        return row_loss
     rc = _lib.lib().jdt_xent(_ptr(logits), int(logits.dtype == torch.float32), logits.stride(0), _ptr(labels), M, C,
                              float(grad_scale), _ptr(dlogits), dlogits.stride(0) if dlogits is not None else 0,
                              _ptr(dbias), _ptr(metrics), _ptr(row_loss), _lib.stream_ptr())
@@ -662,11 +674,27 @@ def act_bwd(dh: torch.Tensor, z: Optional[torch.Tensor], act: str, *, keep_prob:
     return out
 
 
-def metrics_fold_(running: torch.Tensor, slot: torch.Tensor):
-    """running += slot ; slot = 0 (one tiny kernel, graph-capturable)."""
+def metrics_fold_(running: torch.Tensor, slot: torch.Tensor, slab: Optional[torch.Tensor] = None,
+                  step: Optional[torch.Tensor] = None):
+    """running += slot ; slot = 0 (one tiny kernel, graph-capturable).  ``slab`` (fp32
+    [rows, 4], softmax_xent's per-workgroup metric rows): its row sums are added as
+    {loss, n, correct, n} and it is re-zeroed; ``step`` (device int32[1]): advanced by
+    one in the same launch."""
     if not _is_gpu(running):
         running.add_(slot)
         slot.zero_()
+        if slab is not None:
+            t = slab.sum(0)
+            running[:4].add_(torch.stack([t[0], t[1], t[2], t[1]]))
+            slab.zero_()
+        if step is not None:
+            step.add_(1)
+        return
+    if slab is not None or step is not None:
+        cap = int(slab.shape[0]) if slab is not None else 0
+        rc = _lib.lib().jdt_metrics_fold_slab(_ptr(running), _ptr(slot), int(slot.numel()), _ptr(slab), cap,
+                                              _ptr(step), _lib.stream_ptr())
+        _lib.check(rc, "jdt_metrics_fold_slab")
         return
     rc = _lib.lib().jdt_metrics_fold(_ptr(running), _ptr(slot), int(slot.numel()), _lib.stream_ptr())
     _lib.check(rc, "jdt_metrics_fold")

@@ -233,6 +233,12 @@ class GPipeTrainer:
         P = state.params
         self.dev = P.master.device
         self.metrics = torch.zeros(N_METRIC_SLOTS, dtype=torch.float32, device=self.dev)
+        # the CE's per-workgroup metric rows (ops.kernels.softmax_xent mslab), folded at the
+        # step's end -- only where that fold is local (no data axis: with one, the metric
+        # slots ride the gradient all-reduce); JDT_XENT_SLAB=0 restores the slot atomics
+        self._mslab = (torch.zeros(1024, 4, dtype=torch.float32, device=self.dev)
+                       if (self.dev.type == "cuda" and self.n_dp == 1
+                           and os.environ.get("JDT_XENT_SLAB", "1") != "0") else None)
         self.graph = None
         self._ahead = None
         self.multi = None
@@ -822,7 +828,7 @@ class GPipeTrainer:
         if ov and ov.forked:   # AdamW already forked layer by layer during the backward
             ov.finish()
             with named_scope("sync_metrics"):
-                K.metrics_fold_(self.metrics, P.metrics_slot)
+                K.metrics_fold_(self.metrics, P.metrics_slot, slab=self._mslab)
             return
         if self.wgrad is not None:
             self.wgrad.join()  # every weight-gradient GEMM of the step has landed
@@ -831,9 +837,10 @@ class GPipeTrainer:
         eo = self._epilogue_opt() if self.deep_engine is None and self.stage_engine is None else None
         if eo is not None:
             # weights: updated in their weight-gradient GEMM epilogues; the rest here
+            # (on a side stream beside the W pass it measured slower: BENCH_NOTES round 6)
             eo.finish()
             with named_scope("sync_metrics"):
-                K.metrics_fold_(self.metrics, P.metrics_slot)
+                K.metrics_fold_(self.metrics, P.metrics_slot, slab=self._mslab)
             return
         with named_scope("sync_grads"):
             if self._xg_fused_opt:
@@ -850,7 +857,7 @@ class GPipeTrainer:
                 C.psum_(P.grad, self.mesh, cfg.data_axis)
         st.tx.update(P, st.opt_state, scale)
         with named_scope("sync_metrics"):
-            K.metrics_fold_(self.metrics, P.metrics_slot)
+            K.metrics_fold_(self.metrics, P.metrics_slot, slab=self._mslab)
 
     def set_batch(self, batch: Batch):
         """New data for captured graphs (see DataParallelTrainer.set_batch)."""
@@ -948,7 +955,8 @@ class GPipeTrainer:
         y = self.model.flatten_labels(labels)
         hb = self.model.head_bias_name
         K.softmax_xent(logits, y, grad_scale=n_parts / y.numel(), dlogits=dlogits,
-                       dbias=self.state.params.g(hb) if hb else None, metrics=self.state.params.metrics_slot)
+                       dbias=self.state.params.g(hb) if hb else None, metrics=self.state.params.metrics_slot,
+                       mslab=self._mslab)
 
     def gather_metrics(self) -> torch.Tensor:
         """Metrics live on the last stage; bring them to every pipe member."""

@@ -303,6 +303,32 @@ def test_xent(M, C, dt):
     _close(m_g, m_r, rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("M,C", [(2048, 2048), (512, 2048), (37, 512), (33, 1000)])
+def test_xent_metric_slab_fold(M, C):
+    """Per-workgroup metric rows (softmax_xent mslab) + the step-end fold (slab sums, slot,
+    step advance) == the slot atomics + plain fold; the slab comes back zeroed.  (33, 1000)
+    takes the narrow kernel, which keeps the atomics: the fold still adds the slot."""
+    z = (_mk((M, C), torch.float32, seed=21) * 3).to(torch.bfloat16).to(DEV)
+    y = torch.randint(0, C, (M,), generator=torch.Generator().manual_seed(2)).to(torch.int32).to(DEV)
+    y[1] = -1
+    runs = []
+    for use_slab in (False, True):
+        slot, run = torch.zeros(4, device=DEV), torch.full((4,), 2.0, device=DEV)
+        slab = torch.zeros(1024, 4, device=DEV) if use_slab else None
+        step = torch.zeros(1, dtype=torch.int32, device=DEV) if use_slab else None
+        d = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
+        for _ in range(2):
+            kern.softmax_xent(z, y, grad_scale=1 / M, dlogits=d, metrics=slot, mslab=slab)
+            kern.metrics_fold_(run, slot, slab=slab, step=step)
+        torch.cuda.synchronize()
+        runs.append(run.cpu())
+        if use_slab:
+            assert int(step.item()) == 2
+            assert float(slab.abs().sum()) == 0.0 and float(slot.abs().sum()) == 0.0
+    _close(runs[1], runs[0], rtol=1e-5, atol=1e-3)
+    assert float(runs[1][1]) == 2.0 + 2 * (M - 1)
+
+
 @pytest.mark.parametrize("n", [407050, 3_000_001])   # one partial round / several rounds of AW_U groups per thread
 def test_adamw_and_step_counter(n):
     g = torch.Generator().manual_seed(0)

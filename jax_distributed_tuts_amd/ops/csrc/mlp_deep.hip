@@ -179,17 +179,48 @@ __device__ __forceinline__ float md_adam(float p, float m, float v, float g, con
 // DIRECT (compile-time, as in mlp2_fwd): B fragments straight from the W_i^T copy
 // (mode 1) instead of an LDS transposition of the row-major shadow (mode 0); a
 // runtime branch made the waitcnt pass drain one path's loads at the join.
-template <int K_IN, bool XF32, int XTC, bool HEAD, int C, int RB, bool DIRECT, bool XCD>
-__global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
+constexpr int md_fwd_maxt(int k_in) { return ((k_in + 31) / 32 + MD_NW - 1) / MD_NW; }
+
+// A forward tile's operands that do not depend on the layer input (DIRECT: the W_i^T
+// fragments of this wave's k range, the bias, the head weight): loaded before the input is
+// ready when the tile is the second of a fused pair (md_fwd2_kernel).
+template <int MAXT> struct MdFwdPre { bf16x8 bg[MAXT]; float whv, bv; };
+
+template <int K_IN, bool HEAD, int C>
+__device__ __forceinline__ void md_fwd_wload(const MdArgs& a, int by, int step, MdFwdPre<md_fwd_maxt(K_IN)>& P) {
+  constexpr int NW = MD_NW, KS = (K_IN + 31) / 32, MAXT = md_fwd_maxt(K_IN);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j0 = by * 16, par = step & 1;
+  const int ks0 = (w * KS) / NW, ks1 = ((w + 1) * KS) / NW;
+  // every load unconditional (clamped address; out-of-range values are never used or
+  // are zeroed at the LDS write): a load under a divergent guard is waited for at the join
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    const int ks = min(ks0 + t, ks1 - 1);
+    P.bg[t] = *reinterpret_cast<const bf16x8*>(a.WT + (long)(j0 + (lane & 15)) * a.ldwt + ks * 32 + 8 * (lane >> 4));
+  }
+  const bf16_t* Wh = par ? a.Wh1 : a.Wh0;
+  P.whv = HEAD ? bf2f(Wh[(long)(j0 + min(tid, 16 * C - 1) / C) * C + min(tid, 16 * C - 1) % C]) : 0.f;
+  P.bv = bf2f(a.bs[j0 + (tid & 15)]);
+}
+
+// FM (md_fwd2_kernel, two consecutive hidden layers in one launch): 0 = a standalone
+// launch; 1 = the pair's first layer -- its H rows also leave write-through (sc1) for the
+// second layer's workgroups; 2 = the pair's second layer -- its input X (the first layer's
+// H) loaded sc1, the input-independent operands taken from `pre`.
+template <int K_IN, bool XF32, int XTC, bool HEAD, int C, int RB, bool DIRECT, int FM = 0>
+__device__ __forceinline__ void md_fwd_body(const MdArgs& a, const int bx, const int by,
+                                            const MdFwdPre<md_fwd_maxt(K_IN)>* pre) {
   constexpr int NT = MD_NT, NW = MD_NW;
   constexpr int KS = (K_IN + 31) / 32;
   constexpr int KP = KS * 32;
   constexpr int LDW = KP + 8;
   constexpr int WCH = (K_IN * 2 + NT - 1) / NT;   // 16-byte W chunks per thread (LDS path)
-  constexpr int MAXT = (KS + NW - 1) / NW;
+  constexpr int MAXT = md_fwd_maxt(K_IN);
   constexpr int LDXS = K_IN + 8;
   static_assert(K_IN % XTC == 0 && XTC % 8 == 0 && XTC * 4 <= NT && K_IN % 8 == 0, "IN^T chunking");
-  __shared__ __attribute__((aligned(16))) bf16_t wt[16 * LDW];
+  static_assert(FM == 0 || (DIRECT && !XF32 && RB == 16), "fused pair: bf16 input, W^T fragments, 16-row blocks");
+  __shared__ __attribute__((aligned(16))) bf16_t wt[DIRECT ? 8 : 16 * LDW];
   __shared__ __attribute__((aligned(16))) bf16_t xs[RB * LDXS];
   __shared__ float part[NW][RB][17];
   __shared__ float htile[RB][17];
@@ -197,9 +228,6 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
   __shared__ float bsh[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int M = a.M, N = a.N;
-  int bx = blockIdx.x, by = blockIdx.y;
-  // XCD-contiguous: each XCD takes 4 whole column blocks (1/8 of W_i) over all row blocks
-  if constexpr (XCD) xcd_contiguous_tile(bx, by);
   const int r0 = bx * RB, j0 = by * 16;
   const int step = a.step[0], par = step & 1;
   const unsigned long long doff =
@@ -210,38 +238,40 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
 
   // ---- 1. every global load up front
   u32x4 wv[WCH];
-  bf16x8 bg[MAXT];
-  // every load unconditional (clamped address; out-of-range values are never used or
-  // are zeroed at the LDS write): a load under a divergent guard is waited for at the join
+  MdFwdPre<MAXT> P;
   if constexpr (!DIRECT) {
 #pragma unroll
     for (int t = 0; t < WCH; ++t) {
       const int idx = min(tid + t * NT, K_IN * 2 - 1);
       wv[t] = *reinterpret_cast<const u32x4*>(Ws + (long)(idx >> 1) * N + j0 + (idx & 1) * 8);
     }
-  } else {
-#pragma unroll
-    for (int t = 0; t < MAXT; ++t) {
-      const int ks = min(ks0 + t, ks1 - 1);
-      bg[t] = *reinterpret_cast<const bf16x8*>(a.WT + (long)(j0 + (lane & 15)) * a.ldwt + ks * 32 + 8 * (lane >> 4));
-    }
+  } else if constexpr (FM != 2) {
+    md_fwd_wload<K_IN, HEAD, C>(a, by, step, P);
   }
-  // input row block [RB][K_IN], coalesced 16-byte loads
+  if constexpr (FM == 2) P = *pre;
+  // input row block [RB][K_IN], coalesced 16-byte loads (FM 2: sc1, the hand-off of the
+  // pair's first layer, past this CU's L1 and any stale L2 line)
   constexpr int EPV = XF32 ? 4 : 8;                 // elements per 16-byte vector
   constexpr int XV = RB * K_IN / EPV;
   constexpr int XPT = (XV + NT - 1) / NT;
   u32x4 xv[XPT];
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.X), (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
   for (int e = 0; e < XPT; ++e) {
     const int f = min(tid + e * NT, XV - 1), rl = f / (K_IN / EPV), kv = f % (K_IN / EPV);
-    const char* src =
-        static_cast<const char*>(a.X) + ((long)min(r0 + rl, M - 1) * K_IN + (long)kv * EPV) * (XF32 ? 4 : 2);
-    xv[e] = *reinterpret_cast<const u32x4*>(src);
+    const long off = ((long)min(r0 + rl, M - 1) * K_IN + (long)kv * EPV) * (XF32 ? 4 : 2);
+    if constexpr (FM == 2)
+      xv[e] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)off, 0, 16));
+    else
+      xv[e] = *reinterpret_cast<const u32x4*>(static_cast<const char*>(a.X) + off);
   }
-  float whv = 0.f, bv = 0.f;
-  const bf16_t* Wh = par ? a.Wh1 : a.Wh0;
-  if constexpr (HEAD) whv = bf2f(Wh[(long)(j0 + min(tid, 16 * C - 1) / C) * C + min(tid, 16 * C - 1) % C]);
-  bv = bf2f(a.bs[j0 + (tid & 15)]);
+  const bf16x8* bg = P.bg;
+  const float whv = DIRECT ? P.whv
+                           : (HEAD ? bf2f((par ? a.Wh1 : a.Wh0)[(long)(j0 + min(tid, 16 * C - 1) / C) * C +
+                                                              min(tid, 16 * C - 1) % C])
+                                   : 0.f);
+  const float bv = DIRECT ? P.bv : bf2f(a.bs[j0 + (tid & 15)]);
 
   // ---- 2. LDS images
   if (!direct) {
@@ -360,12 +390,30 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
         }
         gf[e] = gd;
         const bf16_t hb = f2bf(hv);
-        a.Hout[(long)row * N + col] = hb;
+        if constexpr (FM != 1) a.Hout[(long)row * N + col] = hb;
         hv = bf2f(hb);
       }
       htile[rl][c] = hv;
     }
     *reinterpret_cast<float4*>(a.G + ((long)(rowg >> 2) * N + col) * 4) = make_float4(gf[0], gf[1], gf[2], gf[3]);
+  }
+  if constexpr (FM == 1) {
+    // the H tile as 16-byte write-through rows (the pair's second layer reads them across
+    // workgroups within this launch): 16 rows x 2 halves of 8 columns
+    __syncthreads();
+    if (tid < 2 * RB) {
+      const int rl = tid >> 1, h8 = (tid & 1) * 8, row = r0 + rl;
+      unsigned q[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        q[e] = (unsigned)f2bf(htile[rl][h8 + 2 * e]) | ((unsigned)f2bf(htile[rl][h8 + 2 * e + 1]) << 16);
+      const __amdgpu_buffer_rsrc_t hr =
+          __builtin_amdgcn_make_buffer_rsrc(a.Hout, (short)0, M * N * 2, 0x00020000);
+      // rows past M: out of the resource's range, dropped
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned,
+                                                                (u32x4){q[0], q[1], q[2], q[3]}),
+                                             hr, (int)(((long)row * N + j0 + h8) * 2), 0, 16);
+    }
   }
   if (HEAD) {
     __syncthreads();
@@ -381,6 +429,54 @@ __global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
       }
     }
   }
+}
+
+template <int K_IN, bool XF32, int XTC, bool HEAD, int C, int RB, bool DIRECT, bool XCD>
+__global__ void __launch_bounds__(MD_NT) md_fwd_kernel(MdArgs a) {
+  int bx = blockIdx.x, by = blockIdx.y;
+  // XCD-contiguous: each XCD takes 4 whole column blocks (1/8 of W_i) over all row blocks
+  if constexpr (XCD) xcd_contiguous_tile(bx, by);
+  md_fwd_body<K_IN, XF32, XTC, HEAD, C, RB, DIRECT>(a, bx, by, nullptr);
+}
+
+// Two consecutive 512 -> 512 hidden layers' forwards in ONE launch (the 4-layer MLP's
+// layers 1 and 2 + the head logits; layer 0 runs ahead in the previous step's layer-0
+// backward): workgroup (r, c) computes tile (r, c) of layer i, then -- once the 32
+// workgroups of its 16-row block have stored their H_i tiles (write-through) and added to
+// the block's arrival counter -- tile (r, c) of layer i+1 from those 16 rows (sc1 loads).
+// A row of layer i+1 needs only the same row of layer i, so the launch boundary between
+// the two layers becomes a 32-workgroup counter per row block; the second layer's W^T
+// fragments, bias and head weight are loaded before the wait.  rowc: 128-byte lines,
+// [0] error word (bit 0: a row block's wait timed out -- not every workgroup resident),
+// block r's monotonic counter at 32 (1 + r).  Requires every workgroup resident
+// (jdt_md_fwd2_ok).
+__global__ void __launch_bounds__(MD_NT) md_fwd2_kernel(MdArgs a1, MdArgs a2, unsigned* rowc) {
+  const int bx = blockIdx.x, by = blockIdx.y;
+  MdFwdPre<md_fwd_maxt(512)> pre;
+  md_fwd_wload<512, true, 10>(a2, by, a2.step[0], pre);
+  md_fwd_body<512, false, 16, false, 10, 16, true, 1>(a1, bx, by, nullptr);
+  // every wave's write-through H stores have left, then one arrival per workgroup; a launch
+  // adds gridDim.y per block, so the target is the next multiple above this arrival
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* cnt = rowc + 32 * (1 + bx);
+    const unsigned nb = gridDim.y;
+    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = (old / nb + 1u) * nb;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(cnt, (short)0, 4, 0x00020000);
+    while ((int)((unsigned)__builtin_amdgcn_raw_buffer_load_b32(cr, 0, 0, 16) - target) < 0) {
+      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > 2000000ll) {   // 20 ms: a block-mate never ran
+        atomicOr(rowc, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");
+    }
+  }
+  __syncthreads();
+  md_fwd_body<512, false, 16, true, 10, 16, true, 2>(a2, bx, by, &pre);
 }
 
 // ---------------------------------------------------------------------------- backward
@@ -549,7 +645,11 @@ __global__ void __launch_bounds__(MD_NT) __attribute__((amdgpu_waves_per_eu(WPE)
       const long idx = hw ? (long)hrow * C + min(ac, C - 1)
                           : (FX && fx_col) ? (long)wrow * fx_hpq + min(max(tcol - fx_R * fx_hpq, 0), fx_hpq - 1)
                                            : (long)wrow * N + tcol;
-      op[e] = sp[idx]; om[e] = sm[idx]; ov[e] = sv[idx];
+      // (MdArgs::wt bit 4, a timing lab only -- wrong numbers: the AdamW state read from one
+      // 1-KB window and never written back, to price the per-step state traffic the
+      // persistent form would remove)
+      const long sidx = (a.wt & 16) ? (idx & 255) : idx;
+      op[e] = sp[sidx]; om[e] = sm[sidx]; ov[e] = sv[sidx];
       const float* bq = fo ? a.pb : a.gb;
       const float* bmq = fo ? a.mb : a.gb;
       const float* bvq = fo ? a.vb : a.gb;
@@ -996,7 +1096,8 @@ __global__ void __launch_bounds__(MD_NT) __attribute__((amdgpu_waves_per_eu(WPE)
         if (a.fuse_opt) {
           float tp, tm, tv;
           const bf16_t pb = f2bf(md_adam(op[e], om[e], ov[e], acc[e], ak, &tp, &tm, &tv));
-          if (a.wt & 1) {
+          if (a.wt & 16) {
+          } else if (a.wt & 1) {
             md_st(a.pW + idx, tp); md_st(a.mW + idx, tm); md_st(a.vW + idx, tv);
           } else {
             a.pW[idx] = tp; a.mW[idx] = tm; a.vW[idx] = tv;
@@ -1210,6 +1311,34 @@ JDT_API int jdt_md_dzs_ok(int M) {
           hipSuccess)
     return 0;
   return (512 / 16) * (512 / 64) <= cus * p1 && (512 / 16) * (784 / 112) <= cus * p2 ? 1 : 0;
+}
+
+// 1 if md_fwd2_kernel's row-block counters can work for M rows: every workgroup of its
+// (ceil(M / 16), 32) grid resident at once
+JDT_API int jdt_md_fwd2_ok(int M) {
+  if (M <= 0 || M > MD_MPM) return 0;
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, md_fwd2_kernel, MD_NT, 0) != hipSuccess)
+    return 0;
+  return ((M + 15) / 16) * 32 <= cus * per ? 1 : 0;
+}
+
+// layers i (a1) and i + 1 (a2, with the head) of a deep MLP's forward in one launch
+// (md_fwd2_kernel): both 512 -> 512, the W^T copies present (fused-optimizer mode)
+JDT_API int jdt_md_fwd2(const MdArgs* a1, const MdArgs* a2, unsigned* rowc, void* stream) {
+  const MdArgs& x = *a1;
+  const MdArgs& y = *a2;
+  if (x.K != 512 || y.K != 512 || x.N != 512 || y.N != 512 || x.M != y.M || x.M <= 0 || x.M > MD_MPM || y.C != 10 ||
+      !x.WT || !y.WT || !rowc || x.Hout != y.X)
+    return -3;
+  if (x.mb_rows < 0 || (x.mb_rows && (x.mb_rows % 4 || x.M % x.mb_rows)) || y.mb_rows < 0 ||
+      (y.mb_rows && (y.mb_rows % 4 || y.M % y.mb_rows)))
+    return -2;
+  hipLaunchKernelGGL(md_fwd2_kernel, dim3((x.M + 15) / 16, x.N / 16), dim3(MD_NT), 0, static_cast<hipStream_t>(stream),
+                     x, y, rowc);
+  return HIP_LAUNCH_CHECK();
 }
 
 // phase 0: forward of one hidden layer (head = 1: + head logits); phase 1: backward

@@ -575,6 +575,8 @@ _lib.declare("jdt_md_dzs_ok", c_int, [c_int])
 _lib.declare("jdt_md_args_size", c_int, [])
 _lib.declare("jdt_md_ahead_ok", c_int, [c_int])
 _lib.declare("jdt_md_fx_ok", c_int, [c_int, c_int])
+_lib.declare("jdt_md_fwd2_ok", c_int, [c_int])
+_lib.declare("jdt_md_fwd2", c_int, [ctypes.POINTER(MdArgs), ctypes.POINTER(MdArgs), c_void_p, c_void_p])
 
 DEEP_H = 512
 
@@ -675,6 +677,15 @@ class FusedMLPDeep:
         if self.dzs_ok:
             self.dzx = [torch.zeros(H // 16 * 16 * 128, **bf) for _ in range(self.nh - 1)]
             self.dzc = [torch.zeros(32 * (1 + H // 16), dtype=torch.int32, device=dev) for _ in range(self.nh - 1)]
+        # the last two hidden layers' forwards in ONE launch (csrc/mlp_deep.hip md_fwd2_kernel:
+        # a row of layer i+1 needs only that row of layer i, so the launch boundary becomes a
+        # per-row-block arrival counter) -- the run-ahead schedule's whole forward when
+        # L = 4.  Opt-in (JDT_MD_FWD2=1): 23.6k vs 24.0k steps/s, the counter wait costs what the
+        # boundary did (BENCH_NOTES round 6)
+        self.fwd2_ok = (self.ahead_ok and self.world == 1 and tx is None and self.nh >= 3
+                        and os.environ.get("JDT_MD_FWD2", "0") == "1" and bool(_lib.lib().jdt_md_fwd2_ok(rows)))
+        if self.fwd2_ok:
+            self.rowc = torch.zeros(32 * (1 + (rows + 15) // 16), dtype=torch.int32, device=dev)
         if self.ahead_ok:
             nch, tpx = 784 // 112, H // 16 * (784 // 112) // 8
             self.XR = torch.zeros(rows, 784, **bf)
@@ -812,8 +823,12 @@ class FusedMLPDeep:
         elif not torch.cuda.is_current_stream_capturing():
             assert self.ahead_primed, "run_ahead(prologue=False) needs a run-ahead launch just before"
         for _ in range(n):
-            for i in range(1, self.nh):
+            last = self.nh - 2 if self.fwd2_ok else self.nh
+            for i in range(1, last):
                 _lib.check(Lb.jdt_md_layer(ctypes.byref(fwd[i]), 0, int(i == self.nh - 1), s), "md_fwd")
+            if self.fwd2_ok:
+                _lib.check(Lb.jdt_md_fwd2(ctypes.byref(fwd[-2]), ctypes.byref(fwd[-1]), self.rowc.data_ptr(), s),
+                           "md_fwd2")
             for j, a in enumerate(bwd[:-1]):
                 _lib.check(Lb.jdt_md_layer(ctypes.byref(a), 1, int(j == 0), s), "md_bwd")
             _lib.check(Lb.jdt_md_layer(ctypes.byref(self._ahead_args), 2, 0, s), "md_bwd_ahead")
@@ -870,6 +885,9 @@ class FusedMLPDeep:
         if self.tx is not None and self.tx.error():
             raise RuntimeError(f"md_bwd tile exchange: a wait timed out (error word {self.tx.error()}); "
                                "results invalid -- rerun with JDT_DP_AHEAD=0")
+        if self.fwd2_ok and int(self.rowc[0].item()) != 0:
+            raise RuntimeError("md_fwd2: a row-block wait timed out (not every workgroup resident); results "
+                               "invalid -- rerun with JDT_MD_FWD2=0")
         if self.fuse_opt and int(self.state.opt_state["count"].item()) % 2 == 1:
             for i, t in self.par.items():
                 self.P.s(self.kn[i]).copy_(t)

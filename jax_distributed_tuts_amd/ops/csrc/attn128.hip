@@ -100,9 +100,19 @@ __global__ void __launch_bounds__(64) attn128_fwd_kernel(const bf16_t* __restric
                                                          int causal) {
   __shared__ __attribute__((aligned(16))) bf16_t Vs[A_S * A_LD];
   const int lane = threadIdx.x, g = lane >> 4, i16 = lane & 15;
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  // XCD-aware tile map: workgroups are dealt round-robin over the 8 XCDs by linear id, so
+  // the natural (query tile, head) order put a head's query tiles on 8 different XCDs, each
+  // fetching that head's K / V from beyond its L2.  With B*H % 8 == 0 the linear id is
+  // re-read so that all query tiles of a head share one XCD (and its L2 copy of K / V).
+  int qt = blockIdx.x, bh = blockIdx.y;
+  if ((gridDim.y & 7) == 0) {
+    const int L = blockIdx.x + gridDim.x * blockIdx.y, j = L >> 3;
+    qt = j % gridDim.x;
+    bh = (j / gridDim.x) * 8 + (L & 7);
+  }
+  const int b = bh / H, h = bh % H;
   const int d = H * A_D, ld3 = 3 * d;
-  const int q0 = blockIdx.x * 16;
+  const int q0 = qt * 16;
   const bf16_t* base = qkv + (long)b * S * ld3;
   const int nk = causal ? min(S, q0 + 16) : S;  // keys this tile can see
   const int nt = (nk + 15) >> 4;                // 16-key tiles

@@ -645,11 +645,7 @@ __global__ void __launch_bounds__(MD_NT) __attribute__((amdgpu_waves_per_eu(WPE)
       const long idx = hw ? (long)hrow * C + min(ac, C - 1)
                           : (FX && fx_col) ? (long)wrow * fx_hpq + min(max(tcol - fx_R * fx_hpq, 0), fx_hpq - 1)
                                            : (long)wrow * N + tcol;
-      // (MdArgs::wt bit 4, a timing lab only -- wrong numbers: the AdamW state read from one
-      // 1-KB window and never written back, to price the per-step state traffic the
-      // persistent form would remove)
-      const long sidx = (a.wt & 16) ? (idx & 255) : idx;
-      op[e] = sp[sidx]; om[e] = sm[sidx]; ov[e] = sv[sidx];
+      op[e] = sp[idx]; om[e] = sm[idx]; ov[e] = sv[idx];
       const float* bq = fo ? a.pb : a.gb;
       const float* bmq = fo ? a.mb : a.gb;
       const float* bvq = fo ? a.vb : a.gb;
@@ -1096,8 +1092,7 @@ __global__ void __launch_bounds__(MD_NT) __attribute__((amdgpu_waves_per_eu(WPE)
         if (a.fuse_opt) {
           float tp, tm, tv;
           const bf16_t pb = f2bf(md_adam(op[e], om[e], ov[e], acc[e], ak, &tp, &tm, &tv));
-          if (a.wt & 16) {
-          } else if (a.wt & 1) {
+          if (a.wt & 1) {
             md_st(a.pW + idx, tp); md_st(a.mW + idx, tm); md_st(a.vW + idx, tv);
           } else {
             a.pW[idx] = tp; a.mW[idx] = tm; a.vW[idx] = tv;

@@ -199,15 +199,17 @@ __global__ void __launch_bounds__(256) xent_vec_kernel(const bf16_t* __restrict_
   }
   // loss, validity and correctness are wave-uniform: lane 0 holds the wave's sums
   if (mslab) {
-    // this workgroup's (loss, n, correct) as one plain 16-byte store into its own slab row:
-    // 4 same-address atomics per workgroup serialise (6.4 us of an 18.3 us launch at M =
-    // 2048, tools/bench_xent.py); the step-end fold sums the rows (jdt_metrics_fold_slab)
+    // this workgroup's (loss, n, correct) added into its OWN slab row: 4 atomics per
+    // workgroup to the same 4 words serialise (6.4 us of an 18.3 us launch at M = 2048,
+    // tools/bench_xent.py); adds to distinct rows do not.  Added, not stored: several CE
+    // launches (microbatches, possibly on concurrent streams) may land in one step; the
+    // step-end fold sums the rows and re-zeroes them (jdt_metrics_fold_slab)
     if (lane == 0) { red[w][0] = l_sum; red[w][1] = n_valid; red[w][2] = n_correct; }
     __syncthreads();
-    if (threadIdx.x == 0)
-      mslab[blockIdx.x] = make_float4(red[0][0] + red[1][0] + red[2][0] + red[3][0],
-                                      red[0][1] + red[1][1] + red[2][1] + red[3][1],
-                                      red[0][2] + red[1][2] + red[2][2] + red[3][2], 0.f);
+    if (threadIdx.x < 3) {
+      const int k = threadIdx.x;
+      atomicAdd(reinterpret_cast<float*>(mslab + blockIdx.x) + k, red[0][k] + red[1][k] + red[2][k] + red[3][k]);
+    }
   } else if (metrics) {
     xent_metrics_fold(red, w, lane, l_sum, n_valid, n_correct, metrics);
   }

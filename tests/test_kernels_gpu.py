@@ -318,7 +318,9 @@ def test_xent_metric_slab_fold(M, C):
         step = torch.zeros(1, dtype=torch.int32, device=DEV) if use_slab else None
         d = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
         for _ in range(2):
-            kern.softmax_xent(z, y, grad_scale=1 / M, dlogits=d, metrics=slot, mslab=slab)
+            # two CE launches per fold (the per-microbatch schedule): the rows accumulate
+            for _ in range(2):
+                kern.softmax_xent(z, y, grad_scale=1 / M, dlogits=d, metrics=slot, mslab=slab)
             kern.metrics_fold_(run, slot, slab=slab, step=step)
         torch.cuda.synchronize()
         runs.append(run.cpu())
@@ -326,7 +328,7 @@ def test_xent_metric_slab_fold(M, C):
             assert int(step.item()) == 2
             assert float(slab.abs().sum()) == 0.0 and float(slot.abs().sum()) == 0.0
     _close(runs[1], runs[0], rtol=1e-5, atol=1e-3)
-    assert float(runs[1][1]) == 2.0 + 2 * (M - 1)
+    assert float(runs[1][1]) == 2.0 + 4 * (M - 1)
 
 
 @pytest.mark.parametrize("n", [407050, 3_000_001])   # one partial round / several rounds of AW_U groups per thread

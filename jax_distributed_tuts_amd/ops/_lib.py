@@ -67,6 +67,8 @@ _SIGS = {
     "jdt_gemm_set_group_tile": (None, [c_int]),
     "jdt_ln_set_rows": (None, [c_int]),
     "jdt_ln_set_waves": (None, [c_int]),
+    "jdt_ln_set_xcd": (None, [c_int]),
+    "jdt_attn128_set_xcd": (None, [c_int]),
     "jdt_gemm_set_group_m": (None, [c_int]),
     "jdt_gemm_set_epi_vec": (None, [c_int]),
     "jdt_gemm_set_epi_vec_min": (None, [c_long]),
@@ -173,6 +175,10 @@ def lib():
             l.jdt_xent_set_rpw(int(os.environ["JDT_XENT_RPW"]))
         if os.environ.get("JDT_LN_ROWS"):  # A/B: force LayerNorm-backward rows per wave (0 = auto)
             l.jdt_ln_set_rows(int(os.environ["JDT_LN_ROWS"]))
+        if os.environ.get("JDT_LN_XCD"):  # A/B: 0 = LayerNorm row blocks in natural order (not XCD-contiguous)
+            l.jdt_ln_set_xcd(int(os.environ["JDT_LN_XCD"]))
+        if os.environ.get("JDT_ATTN_XCD"):  # A/B: 0 = attention forward tiles in natural order
+            l.jdt_attn128_set_xcd(int(os.environ["JDT_ATTN_XCD"]))
         _lib = l
         return _lib
 

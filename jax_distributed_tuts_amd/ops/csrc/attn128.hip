@@ -97,18 +97,20 @@ __device__ __forceinline__ bf16x8 pack_pair(const f32x4& a, const f32x4& b) {
 // ------------------------------------------------------------------------ forward
 __global__ void __launch_bounds__(64) attn128_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                          float* __restrict__ lse, int S, int H, float scale,
-                                                         int causal) {
+                                                         int causal, int xcd_map) {
   __shared__ __attribute__((aligned(16))) bf16_t Vs[A_S * A_LD];
   const int lane = threadIdx.x, g = lane >> 4, i16 = lane & 15;
   // XCD-aware tile map: workgroups are dealt round-robin over the 8 XCDs by linear id, so
   // the natural (query tile, head) order put a head's query tiles on 8 different XCDs, each
   // fetching that head's K / V from beyond its L2.  With B*H % 8 == 0 the linear id is
-  // re-read so that all query tiles of a head share one XCD (and its L2 copy of K / V).
+  // re-read so that XCD x takes the heads [x BH/8, (x+1) BH/8) -- every query tile of a
+  // head on one XCD (one L2 copy of its K / V), and whole sequences per XCD: the rows the
+  // QKV GEMM's tile map wrote there and the out-projection reads there (gemm_dma_kernel).
   int qt = blockIdx.x, bh = blockIdx.y;
-  if ((gridDim.y & 7) == 0) {
+  if (xcd_map && (gridDim.y & 7) == 0) {
     const int L = blockIdx.x + gridDim.x * blockIdx.y, j = L >> 3;
     qt = j % gridDim.x;
-    bh = (j / gridDim.x) * 8 + (L & 7);
+    bh = (L & 7) * (gridDim.y >> 3) + j / gridDim.x;
   }
   const int b = bh / H, h = bh % H;
   const int d = H * A_D, ld3 = 3 * d;
@@ -212,14 +214,17 @@ __global__ void __launch_bounds__(512) attn128_bwd_kernel(const bf16_t* __restri
                                                           const bf16_t* __restrict__ dout,
                                                           const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
                                                           float* __restrict__ dbias, int S, int H, float scale,
-                                                          int causal) {
+                                                          int causal, int xcd_map) {
   __shared__ __attribute__((aligned(16))) bf16_t Qs[A_S * A_LD];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[A_S * A_LD];
   __shared__ __attribute__((aligned(16))) bf16_t Ks[A_S * A_LD];
   __shared__ __attribute__((aligned(16))) bf16_t dSs[A_S * A_DSLD];
   __shared__ float lse_s[A_S], delta_s[A_S];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i16 = lane & 15;
-  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  // heads [x BH/8, (x+1) BH/8) on XCD x (whole sequences per XCD, as the forward's map)
+  const int bh = (xcd_map && (gridDim.x & 7) == 0) ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3)
+                                                   : blockIdx.x;
+  const int b = bh / H, h = bh % H;
   const int d = H * A_D, ld3 = 3 * d;
   const int Sp = (S + 31) & ~31;  // staged rows (zero past S)
   const bf16_t* base = qkv + (long)b * S * ld3;
@@ -410,11 +415,15 @@ using namespace jdt;
 // 1 if the S <= 128 kernels handle this shape (head dim 64 is the caller's contract)
 JDT_API int jdt_attn128_ok(int S) { return S > 0 && S <= A_S ? 1 : 0; }
 
+static int g_attn_xcd = 1;
+// 0: the attn128 kernels' tiles in natural (query tile, head) order (A/B)
+JDT_API void jdt_attn128_set_xcd(int on) { g_attn_xcd = on; }
+
 JDT_API int jdt_attn128_fwd(const void* qkv, void* out, float* lse, int B, int S, int H, float scale, int causal,
                             void* stream) {
   if (S <= 0 || S > A_S) return -2;
   hipLaunchKernelGGL(attn128_fwd_kernel, dim3((S + 15) / 16, B * H), dim3(64), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const bf16_t*>(qkv), static_cast<bf16_t*>(out), lse, S, H, scale, causal);
+                     static_cast<const bf16_t*>(qkv), static_cast<bf16_t*>(out), lse, S, H, scale, causal, g_attn_xcd);
   return HIP_LAUNCH_CHECK();
 }
 
@@ -423,6 +432,6 @@ JDT_API int jdt_attn128_bwd(const void* qkv, const void* out, const void* dout, 
   if (S <= 0 || S > A_S) return -2;
   hipLaunchKernelGGL(attn128_bwd_kernel, dim3(B * H), dim3(512), 0, static_cast<hipStream_t>(stream),
                      static_cast<const bf16_t*>(qkv), static_cast<const bf16_t*>(out),
-                     static_cast<const bf16_t*>(dout), lse, static_cast<bf16_t*>(dqkv), dbias, S, H, scale, causal);
+                     static_cast<const bf16_t*>(dout), lse, static_cast<bf16_t*>(dqkv), dbias, S, H, scale, causal, g_attn_xcd);
   return HIP_LAUNCH_CHECK();
 }

@@ -11,6 +11,17 @@ namespace jdt {
 
 constexpr int LN_MAXV = 4;  // 4 x 8 x 64 = 2048 columns max
 
+// Row-block index of this workgroup, XCD-contiguous: workgroups are dealt round-robin over
+// the 8 XCDs by id, so XCD x takes blocks [x G/8, (x+1) G/8) -- the rows the neighbouring
+// GEMMs' tile maps (gemm_dma_kernel: contiguous tile ranges per XCD, row-major) produce and
+// consume on that XCD, instead of every 8th block.  JDT_LN_XCD=0 (jdt_ln_set_xcd) restores
+// the natural order.
+__device__ __forceinline__ int ln_block(int xcd_map) {
+  const int G = gridDim.x, b = blockIdx.x;
+  if (!xcd_map || (G & 7)) return b;
+  return (b & 7) * (G >> 3) + (b >> 3);
+}
+
 // Forward: one wave per row.  The affine parameters' loads are issued together
 // with the row's (the previous version computed the statistics first and only
 // then loaded gamma / beta: a second dependent memory round trip), and the two
@@ -20,9 +31,9 @@ template <int NV>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, bf16_t* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                     int T, int d, float eps) {
+                                                     int T, int d, float eps, int xcd_map) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = ln_block(xcd_map) * 4 + (threadIdx.x >> 6);
   if (row >= T) return;
   const bf16_t* xr = x + (long)row * d;
   u32x4 p[NV];
@@ -91,10 +102,11 @@ __global__ void __launch_bounds__(64 * W) ln_bwd_kernel(const bf16_t* __restrict
                                                      const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                      const float* __restrict__ gamma, const bf16_t* __restrict__ dres,
                                                      bf16_t* __restrict__ dx, float* __restrict__ dgamma,
-                                                     float* __restrict__ dbeta, float* __restrict__ dsum, int T, int d) {
+                                                     float* __restrict__ dbeta, float* __restrict__ dsum, int T, int d,
+                                                     int xcd_map) {
   __shared__ float part[W][512 * NV];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r0 = (blockIdx.x * W + w) * R;
+  const int r0 = (ln_block(xcd_map) * W + w) * R;
   float ag[NV][8], ab[NV][8], ad[NV][8], gm[NV][8];
   u32x4 px[R][NV], pd[R][NV], pr[R][NV];
   float mean[R], rstd[R];
@@ -198,6 +210,9 @@ __global__ void __launch_bounds__(64 * W) ln_bwd_kernel(const bf16_t* __restrict
 }  // namespace jdt
 using namespace jdt;
 
+static int g_ln_xcd = 1;
+JDT_API void jdt_ln_set_xcd(int on) { g_ln_xcd = on; }
+
 JDT_API int jdt_ln_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd, int T,
                        int d, float eps, void* stream) {
   if (d % 8 || d > 2048) return -3;
@@ -210,9 +225,9 @@ JDT_API int jdt_ln_fwd(const void* x, const float* gamma, const float* beta, voi
   const bf16_t* xb = static_cast<const bf16_t*>(x);
   bf16_t* yb = static_cast<bf16_t*>(y);
   switch (nv) {
-    case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, st, xb, gamma, beta, yb, mean, rstd, T, d, eps); break;
-    case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, st, xb, gamma, beta, yb, mean, rstd, T, d, eps); break;
-    default: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, st, xb, gamma, beta, yb, mean, rstd, T, d, eps); break;
+    case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, st, xb, gamma, beta, yb, mean, rstd, T, d, eps, g_ln_xcd); break;
+    case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, st, xb, gamma, beta, yb, mean, rstd, T, d, eps, g_ln_xcd); break;
+    default: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, st, xb, gamma, beta, yb, mean, rstd, T, d, eps, g_ln_xcd); break;
   }
   return HIP_LAUNCH_CHECK();
 }
@@ -245,7 +260,7 @@ JDT_API int jdt_ln_bwd(const void* dy, const void* x, const float* mean, const f
   if (R == 0) R = W == 16 ? 2 : (T >= 1024 ? 4 : 2);
 #define JDT_LNB(NV_, R_, W_)                                                                                      \
   hipLaunchKernelGGL((ln_bwd_kernel<NV_, R_, W_>), dim3((T + W_ * R_ - 1) / (W_ * R_)), dim3(64 * W_), 0, st, a, b, \
-                     mean, rstd, gamma, r, o, dgamma, dbeta, dsum, T, d)
+                     mean, rstd, gamma, r, o, dgamma, dbeta, dsum, T, d, g_ln_xcd)
   // register budget: R x NV x 3 row vectors per lane -> R <= 2 at 16 waves, <= 4 at 8
   switch (nv) {
     case 1:

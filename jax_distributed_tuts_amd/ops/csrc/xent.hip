@@ -116,7 +116,10 @@ __global__ void __launch_bounds__(256) xent_vec_kernel(const bf16_t* __restrict_
   for (int k = 0; k < NV; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) db[k][j] = 0.f;
-  const int r0 = (blockIdx.x * 4 + w) * rpw;
+  // row blocks [x G/8, (x+1) G/8) on XCD x: the rows the head GEMM's tile map wrote there and
+  // its input-gradient GEMM reads there (gemm_dma_kernel: contiguous tile ranges per XCD)
+  const int G = gridDim.x, blk = (G & 7) ? blockIdx.x : (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  const int r0 = (blk * 4 + w) * rpw;
   for (int row = r0; row < min(M, r0 + rpw); ++row) {
     const int label = labels[row];
     const bool valid = label >= 0 && label < C;

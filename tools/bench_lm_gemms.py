@@ -54,8 +54,13 @@ def timed(fn, n=50, reps=10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sweep", default="")
+    ap.add_argument("--gm", type=int, default=-1,
+                    help="force the tile row-group size of every GEMM (csrc/gemm.hip group_m; -1 = table)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
+    if a.gm >= 0:
+        from jax_distributed_tuts_amd.ops import _lib
+        _lib.lib().jdt_gemm_set_group_m(a.gm)
     W = {n: [bf(k, m) for _ in range(SETS)] for n, (k, m) in
          {"qkv": (D, 3 * D), "out": (D, D), "fc1": (D, F), "fc2": (F, D), "head": (D, V)}.items()}
     bias = {n: torch.zeros(W[n][0].shape[1], device="cuda") for n in W}

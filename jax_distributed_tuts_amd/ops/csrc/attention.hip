@@ -74,7 +74,14 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const bf16_t* __restrict
   const int t = (int)(i / d), c = (int)(i % d);
   const float g = bf2f(dout[i]);
   atomicAdd(dwte + (long)tok[t] * d + c, g);
-  if (dwpe) atomicAdd(dwpe + (long)(t % S) * d + c, g);
+  // the position table's gradient: a thread of the first sequence sums its (position,
+  // column) over every sequence in order and adds once -- T / S times fewer atomics than
+  // one per token (each position row took T / S same-address adds)
+  if (dwpe && t < S) {
+    float sp = g;
+    for (int q = t + S; q < T; q += S) sp += bf2f(dout[(long)q * d + c]);
+    atomicAdd(dwpe + (long)t * d + c, sp);
+  }
 }
 
 // out[c] += sum_r x[r, c] (bias gradients).  A lane owns 8 adjacent columns

@@ -69,6 +69,7 @@ _SIGS = {
     "jdt_ln_set_waves": (None, [c_int]),
     "jdt_ln_set_xcd": (None, [c_int]),
     "jdt_attn128_set_xcd": (None, [c_int]),
+    "jdt_attn128_set_stamps": (None, [c_void_p]),
     "jdt_gemm_set_group_m": (None, [c_int]),
     "jdt_gemm_set_epi_vec": (None, [c_int]),
     "jdt_gemm_set_epi_vec_min": (None, [c_long]),

@@ -21,8 +21,9 @@
 //   transposing LDS reads); dS also goes to an LDS image [q][key].  After one
 //   barrier, dQ^T = K^T dS^T per wave (16 queries).  dQ / dK / dV leave as 8-byte
 //   stores of 4 consecutive head dims; the fused QKV bias gradient (column sums of
-//   the stored bf16 values) is one atomic per column per wave.  Fixed summation
-//   order throughout (deterministic), no workspace, no atomics on dQ.
+//   the stored bf16 values) is summed per workgroup in LDS and added with one atomic
+//   per column per workgroup.  dQ / dK / dV in a fixed summation order (deterministic),
+//   no workspace, no atomics on dQ.
 #include "common.h"
 
 namespace jdt {
@@ -54,9 +55,11 @@ __device__ __forceinline__ float row16_sum(float v) {
 }
 // Column sums of an accumulator tile whose 16 lanes of a row are summed away: lane
 // (g, i16) of tile `dt` holds values for head dims 16 dt + 4g + e (e = 0..3); after
-// the row sums, lane i16 = e of row g adds dim 16 dt + 4g + e: one atomic
-// instruction (16 active lanes) per tile.
-__device__ __forceinline__ void colsum_atomic(float* dst, const f32x4& v, int g, int i16) {
+// the row sums, lane i16 = e of row g adds dim 16 dt + 4g + e into the workgroup's LDS
+// accumulator, which the workgroup adds to the global bias gradient once per column at its
+// end (each wave adding to global memory itself: ~2 us of the 10-us backward drained
+// those atomics, tools/stamp_attn.py)
+__device__ __forceinline__ void colsum_lds(float* dst, const f32x4& v, int g, int i16) {
   const float s0 = row16_sum(v[0]), s1 = row16_sum(v[1]), s2 = row16_sum(v[2]), s3 = row16_sum(v[3]);
   const float mine = i16 == 0 ? s0 : (i16 == 1 ? s1 : (i16 == 2 ? s2 : s3));
   if (i16 < 4) atomicAdd(dst + 4 * g + i16, mine);
@@ -214,12 +217,19 @@ __global__ void __launch_bounds__(512) attn128_bwd_kernel(const bf16_t* __restri
                                                           const bf16_t* __restrict__ dout,
                                                           const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
                                                           float* __restrict__ dbias, int S, int H, float scale,
-                                                          int causal, int xcd_map) {
+                                                          int causal, int xcd_map, unsigned long long* stamps) {
+  // diagnostic (jdt_attn128_set_stamps): s_memrealtime at the phase ends, [workgroup][8]
+#define A_STAMP(k)                                                                                            \
+  do {                                                                                                        \
+    if (stamps && threadIdx.x == 0) stamps[(long)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();  \
+  } while (0)
+  A_STAMP(0);
   __shared__ __attribute__((aligned(16))) bf16_t Qs[A_S * A_LD];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[A_S * A_LD];
   __shared__ __attribute__((aligned(16))) bf16_t Ks[A_S * A_LD];
   __shared__ __attribute__((aligned(16))) bf16_t dSs[A_S * A_DSLD];
   __shared__ float lse_s[A_S], delta_s[A_S];
+  __shared__ float dbs[3][A_D];   // this head's q / k / v bias-gradient columns (colsum_lds)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i16 = lane & 15;
   // heads [x BH/8, (x+1) BH/8) on XCD x (whole sequences per XCD, as the forward's map)
   const int bh = (xcd_map && (gridDim.x & 7) == 0) ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3)
@@ -255,6 +265,7 @@ __global__ void __launch_bounds__(512) attn128_bwd_kernel(const bf16_t* __restri
     co[i] = ldb16(ro, rowo);
   }
   if (tid < A_S) lse_s[tid] = tid < S ? lse[(long)bh * S + tid] : 0.f;
+  if (tid < 3 * A_D) dbs[tid / A_D][tid % A_D] = 0.f;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int c = tid + 512 * i, r = c >> 3, col = (c & 7) * 8;
@@ -276,6 +287,7 @@ __global__ void __launch_bounds__(512) attn128_bwd_kernel(const bf16_t* __restri
     if ((c & 7) == 0) delta_s[r] = dl;
   }
   __syncthreads();
+  A_STAMP(1);
 
   // ---- dK, dV for this wave's 16 keys over every query tile pair that can see them
   f32x4 dk[4], dv[4];
@@ -345,7 +357,9 @@ __global__ void __launch_bounds__(512) attn128_bwd_kernel(const bf16_t* __restri
     for (int c = lane; c < pend * 64; c += 64)  // 2 x 16 bytes (16 keys) per row
       *reinterpret_cast<u32x4*>(dSs + (c >> 1) * A_DSLD + kb + (c & 1) * 8) = z;
   }
+  A_STAMP(2);
   __syncthreads();
+  A_STAMP(3);
 
   // ---- dQ^T[d][q] = K^T dS^T for queries 16w .. 16w + 15
   const int qb = 16 * w;
@@ -377,9 +391,10 @@ __global__ void __launch_bounds__(512) attn128_bwd_kernel(const bf16_t* __restri
         pk.y = (unsigned)f2bf(r[2]) | ((unsigned)f2bf(r[3]) << 16);
         *reinterpret_cast<uint2*>(row + dt * 16) = pk;
       }
-      if (dbias) colsum_atomic(dbias + h * A_D + dt * 16, r, g, i16);  // over this wave's 16 queries
+      if (dbias) colsum_lds(&dbs[0][dt * 16], r, g, i16);  // over this wave's 16 queries
     }
   }
+  A_STAMP(4);
   // ---- dK, dV: 4 consecutive head dims per lane (8-byte stores)
   if (active) {
     const bool kok = key < S;
@@ -402,11 +417,17 @@ __global__ void __launch_bounds__(512) attn128_bwd_kernel(const bf16_t* __restri
         *reinterpret_cast<uint2*>(row + 2 * d + dt * 16) = pv;
       }
       if (dbias) {  // over this wave's 16 keys
-        colsum_atomic(dbias + d + h * A_D + dt * 16, rk, g, i16);
-        colsum_atomic(dbias + 2 * d + h * A_D + dt * 16, rv, g, i16);
+        colsum_lds(&dbs[1][dt * 16], rk, g, i16);
+        colsum_lds(&dbs[2][dt * 16], rv, g, i16);
       }
     }
   }
+  if (dbias) {
+    __syncthreads();
+    if (tid < 3 * A_D) atomicAdd(dbias + (tid / A_D) * d + h * A_D + tid % A_D, dbs[tid / A_D][tid % A_D]);
+  }
+  A_STAMP(5);
+#undef A_STAMP
 }
 
 }  // namespace jdt
@@ -416,6 +437,9 @@ using namespace jdt;
 JDT_API int jdt_attn128_ok(int S) { return S > 0 && S <= A_S ? 1 : 0; }
 
 static int g_attn_xcd = 1;
+static unsigned long long* g_attn_stamps = nullptr;
+// diagnostic: attn128_bwd_kernel phase stamps into a [grid][8] u64 buffer (null = off; tools/stamp_attn.py)
+JDT_API void jdt_attn128_set_stamps(void* p) { g_attn_stamps = static_cast<unsigned long long*>(p); }
 // 0: the attn128 kernels' tiles in natural (query tile, head) order (A/B)
 JDT_API void jdt_attn128_set_xcd(int on) { g_attn_xcd = on; }
 
@@ -432,6 +456,7 @@ JDT_API int jdt_attn128_bwd(const void* qkv, const void* out, const void* dout, 
   if (S <= 0 || S > A_S) return -2;
   hipLaunchKernelGGL(attn128_bwd_kernel, dim3(B * H), dim3(512), 0, static_cast<hipStream_t>(stream),
                      static_cast<const bf16_t*>(qkv), static_cast<const bf16_t*>(out),
-                     static_cast<const bf16_t*>(dout), lse, static_cast<bf16_t*>(dqkv), dbias, S, H, scale, causal, g_attn_xcd);
+                     static_cast<const bf16_t*>(dout), lse, static_cast<bf16_t*>(dqkv), dbias, S, H, scale, causal, g_attn_xcd,
+                     g_attn_stamps);
   return HIP_LAUNCH_CHECK();
 }

@@ -16,6 +16,7 @@ block range, ``has_embed``/``has_head`` mark the first/last stage.
 from __future__ import annotations
 
 import contextlib
+import os
 
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -24,6 +25,9 @@ import torch
 
 from ..ops import kernels as K
 from ..utils.flat import FlatParams, ParamSpec
+
+# JDT_EMBED_LN=0: the embedding runs as its own launch (embed_fwd) before the first LN1
+_EMBED_LN = os.environ.get("JDT_EMBED_LN", "1") != "0"
 
 
 @dataclass
@@ -164,10 +168,16 @@ class TransformerLM:
         c = self.cfg
         keep = 1.0 - c.dropout_rate if train else 1.0
         A = (lambda l, k: arena.rows(arena.blocks[l][k], mb, n_mb)) if arena is not None else (lambda l, k: None)  # noqa: E731
+        emb = None
         if self.has_embed:
             nseq = x.shape[0]
             tok = x.reshape(-1).contiguous()
-            h = K.embed_fwd(tok, P.s("embed/wte"), P.s("embed/wpe"), c.seq_len)
+            if self.layers and _EMBED_LN:
+                # the embedding is built by the first block's LN1 launch (ln_gemm(embed=))
+                emb = (tok, P.s("embed/wte"), P.s("embed/wpe"), c.seq_len)
+                h = torch.empty(tok.shape[0], c.d_model, dtype=torch.bfloat16, device=tok.device)
+            else:
+                h = K.embed_fwd(tok, P.s("embed/wte"), P.s("embed/wpe"), c.seq_len)
             cache = _Cache(inp=tok, nseq=nseq, seed=seed, keep=keep, step=step, arena=arena, mb=mb, n_mb=n_mb)
         else:
             nseq = x.shape[0] // c.seq_len
@@ -177,7 +187,8 @@ class TransformerLM:
             b = f"block_{l}"
             # LN1 fused into the QKV projection's A operand (one launch; h1 / stats kept for backward)
             qkv, h1, m1, r1 = K.ln_gemm(h, P.p(f"{b}/ln1/scale"), P.p(f"{b}/ln1/bias"), P.s(f"{b}/attn/qkv/kernel"),
-                                        eps=c.ln_eps, bias=P.s(f"{b}/attn/qkv/bias"), y_out=A(l, "h1"))
+                                        eps=c.ln_eps, bias=P.s(f"{b}/attn/qkv/bias"), y_out=A(l, "h1"), embed=emb)
+            emb = None
             o, Pm = K.attention_fwd(qkv, nseq, c.seq_len, c.n_heads, causal=True, o_out=A(l, "o"))
             x2 = K.gemm(o, P.s(f"{b}/attn/out/kernel"), bias=P.s(f"{b}/attn/out/bias"), resid=h)
             z1 = torch.empty(x2.shape[0], c.d_ff, dtype=torch.bfloat16, device=x2.device)

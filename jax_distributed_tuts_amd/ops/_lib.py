@@ -51,6 +51,7 @@ class LnArgs(ctypes.Structure):
 
 _SIGS = {
     "jdt_gemm_ln": (c_int, [ctypes.POINTER(GemmArgs), ctypes.POINTER(LnArgs), c_void_p]),
+    "jdt_gemm_ln_eligible": (c_int, [ctypes.POINTER(GemmArgs), ctypes.POINTER(LnArgs)]),
     "jdt_ln_args_size": (c_int, []),
     "jdt_gemm_ln_set_cfg": (None, [c_int]),
     "jdt_adamw_ranges": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_long,
@@ -97,6 +98,8 @@ _SIGS = {
                               c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "jdt_ln_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,
                            c_void_p]),
+    "jdt_ln_fwd_embed": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_int, c_int, c_float, c_void_p]),
     "jdt_ln_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_int, c_int, c_void_p]),
     "jdt_attn_softmax_fwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),

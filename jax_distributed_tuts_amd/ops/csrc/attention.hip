@@ -54,16 +54,7 @@ __global__ void __launch_bounds__(256) embed_fwd_kernel(const int* __restrict__ 
   const int v = tok[t], pos = t % S;
   const u32x4 a = *reinterpret_cast<const u32x4*>(wte + (long)v * d + c);
   const u32x4 b = *reinterpret_cast<const u32x4*>(wpe + (long)pos * d + c);
-  const unsigned wa[4] = {a.x, a.y, a.z, a.w}, wb[4] = {b.x, b.y, b.z, b.w};
-  unsigned o[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float lo = bf2f((bf16_t)(wa[j] & 0xffff)) + bf2f((bf16_t)(wb[j] & 0xffff));
-    const float hi = bf2f((bf16_t)(wa[j] >> 16)) + bf2f((bf16_t)(wb[j] >> 16));
-    o[j] = (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
-  }
-  u32x4 ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
-  *reinterpret_cast<u32x4*>(out + (long)t * d + c) = ov;
+  *reinterpret_cast<u32x4*>(out + (long)t * d + c) = bf16x8_add(a, b);
 }
 
 __global__ void __launch_bounds__(256) embed_bwd_kernel(const bf16_t* __restrict__ dout, const int* __restrict__ tok,

@@ -96,6 +96,19 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
   return (r0 + r1) + (r2 + r3);
 }
 
+// 8 bf16 sums a + b (fp32 add, round to nearest even): the token + position embedding,
+// shared by embed_fwd_kernel and the embedding-fused LayerNorm so both give the same bits
+__device__ __forceinline__ u32x4 bf16x8_add(u32x4 a, u32x4 b) {
+  u32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float lo = bf2f((bf16_t)(a[j] & 0xffff)) + bf2f((bf16_t)(b[j] & 0xffff));
+    const float hi = bf2f((bf16_t)(a[j] >> 16)) + bf2f((bf16_t)(b[j] >> 16));
+    o[j] = (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+  }
+  return o;
+}
+
 __device__ __forceinline__ float wave_max_dpp(float v) {
   v = fmaxf(v, dpp_mov<0xB1>(v));
   v = fmaxf(v, dpp_mov<0x4E>(v));

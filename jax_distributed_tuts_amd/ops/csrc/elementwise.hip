@@ -47,30 +47,42 @@ __global__ void metrics_fold_kernel(float* running, float* slot, int n) {
 // correct, n}); slot = 0, every slab row = 0; then (step non-null) the device step += 1 --
 // the step-end fold of a pass whose CE wrote per-workgroup metric rows (jdt_xent_slab) and
 // whose AdamW ranges ran without advancing the step, beside the W pass that also reads it
+// Latency-bound (one workgroup, 16 KB): every load -- FOLD_U slab rows per thread, the
+// running / slot values and the step -- is issued before the first use (one memory round
+// trip; the per-row load/store loop was one per 256 rows: 4.6 us per step in the LM), the
+// wave sums are DPP moves and the 4 waves meet in LDS behind one barrier.
+constexpr int FOLD_U = 4;
 __global__ void __launch_bounds__(256) metrics_fold_slab_kernel(float* running, float* slot, int n,
                                                                 float4* __restrict__ slab, int cap, int* step) {
-  __shared__ float red[3][256];
-  const int t = threadIdx.x;
+  __shared__ float red[4][3];
+  const int t = threadIdx.x, w = t >> 6;
+  const float run = t < n ? running[t] : 0.f, sl = t < n ? slot[t] : 0.f;
+  const int sv = (t == 0 && step) ? step[0] : 0;
   float a = 0.f, b = 0.f, c = 0.f;
-  for (int i = t; i < cap; i += 256) {
-    const float4 r = slab[i];
-    a += r.x; b += r.y; c += r.z;
-    slab[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  red[0][t] = a; red[1][t] = b; red[2][t] = c;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (t < o) {
-      red[0][t] += red[0][t + o]; red[1][t] += red[1][t + o]; red[2][t] += red[2][t + o];
+  for (int i0 = 0; i0 < cap; i0 += 256 * FOLD_U) {
+    float4 r[FOLD_U];
+#pragma unroll
+    for (int u = 0; u < FOLD_U; ++u) {
+      const int i = i0 + u * 256 + t;
+      r[u] = i < cap ? slab[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < FOLD_U; ++u) {
+      const int i = i0 + u * 256 + t;
+      a += r[u].x; b += r[u].y; c += r[u].z;
+      if (i < cap) slab[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   }
+  a = wave_sum_dpp(a); b = wave_sum_dpp(b); c = wave_sum_dpp(c);
+  if ((t & 63) == 0) { red[w][0] = a; red[w][1] = b; red[w][2] = c; }
+  __syncthreads();
   if (t < n) {
-    const float add = t == 0 ? red[0][0] : (t == 2 ? red[2][0] : (t < 4 ? red[1][0] : 0.f));
-    running[t] += slot[t] + add;
+    const int k = t == 0 ? 0 : (t == 2 ? 2 : 1);
+    const float add = t < 4 ? (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]) : 0.f;
+    running[t] = run + (sl + add);
     slot[t] = 0.f;
   }
-  if (t == 0 && step) step[0] = step[0] + 1;
+  if (t == 0 && step) step[0] = sv + 1;
 }
 
 }  // namespace jdt

@@ -2294,10 +2294,8 @@ JDT_API int jdt_ln_args_size() { return (int)sizeof(LnArgs); }
 // gemm_ln_kernel).  X [M, K] bf16 (K in {512, 1024}, rows 16-byte aligned), W
 // [K, N] bf16 "kn"; M % 32 == 0, N % 64 == 0.  Returns -2 outside that envelope.
 static int g_ln_cfg = 0;  // jdt_gemm_ln_set_cfg: force a tile (sweeps); 0 = heuristic
-JDT_API int jdt_gemm_ln(const GemmArgs* ga, const LnArgs* la, void* stream) {
-  const GemmArgs& g = *ga;
-  const LnArgs& L = *la;
-  hipStream_t st = static_cast<hipStream_t>(stream);
+// the fused kernel's tile config for (g, L), or -2: not eligible (LN + GEMM run apart)
+static int gemm_ln_cfg(const GemmArgs& g, const LnArgs& L) {
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   if (g.a_f32 || g.b_f32 || !g.b_trans || g.accumulate || g.Zin || g.zin > 1 || (g.K != 512 && g.K != 1024) ||
       g.M % 32 || g.N % 64 || !al(L.X) || !al(L.Y) || !al(g.B) || L.ldx % 8 || L.ldy % 8 || g.ldb % 8 ||
@@ -2313,6 +2311,18 @@ JDT_API int jdt_gemm_ln(const GemmArgs* ga, const LnArgs* la, void* stream) {
     if (g.M > 512 || g.N > 2048) return -2;
     cfg = 1;
   }
+  return g.K == 1024 || cfg <= 4 ? cfg : -2;   // K = 1024 has one config
+}
+
+// 1: jdt_gemm_ln would run the fused kernel for (g, L); 0: it would return -2
+JDT_API int jdt_gemm_ln_eligible(const GemmArgs* ga, const LnArgs* la) { return gemm_ln_cfg(*ga, *la) > 0; }
+
+JDT_API int jdt_gemm_ln(const GemmArgs* ga, const LnArgs* la, void* stream) {
+  const GemmArgs& g = *ga;
+  const LnArgs& L = *la;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int cfg = gemm_ln_cfg(g, L);
+  if (cfg < 0) return -2;
   if (g.K == 1024) return launch_ln<2, 2, 1, 2, 2>(g, L, st);
   switch (cfg) {
     case 1: return launch_ln<2, 2, 1, 2, 1>(g, L, st);   // 32 x 64

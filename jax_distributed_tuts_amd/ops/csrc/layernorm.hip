@@ -27,28 +27,53 @@ __device__ __forceinline__ int ln_block(int xcd_map) {
 // then loaded gamma / beta: a second dependent memory round trip), and the two
 // row reductions are DPP lane moves (wave_sum_dpp) instead of ds_bpermute
 // butterflies.
-template <int NV>
+//
+// EMB: the row is the token + position embedding (the model's first LayerNorm): x =
+// wte[tok[row]] + wpe[row % S] (bf16x8_add, the bits embed_fwd_kernel stores) is built in
+// registers, stored to E.x (the residual stream) and normalised -- the embedding's own
+// launch and its re-read of x go away.
+struct LnEmbed {
+  const int* tok;
+  const bf16_t* wte;
+  const bf16_t* wpe;
+  int S;
+  bf16_t* x;
+};
+
+template <int NV, bool EMB>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, bf16_t* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                     int T, int d, float eps, int xcd_map) {
+                                                     int T, int d, float eps, int xcd_map, LnEmbed E) {
   const int lane = threadIdx.x & 63;
   const int row = ln_block(xcd_map) * 4 + (threadIdx.x >> 6);
   if (row >= T) return;
-  const bf16_t* xr = x + (long)row * d;
-  u32x4 p[NV];
+  const bf16_t* xr = EMB ? E.wte + (long)E.tok[row] * d : x + (long)row * d;
+  const bf16_t* pr = EMB ? E.wpe + (long)(row % E.S) * d : nullptr;
+  u32x4 p[NV], pp[NV];
   float4 g[NV][2], bt[NV][2];
 #pragma unroll
   for (int c = 0; c < NV; ++c) {
     const int col = (c * 64 + lane) * 8;
-    p[c] = (u32x4){0u, 0u, 0u, 0u};
+    p[c] = pp[c] = (u32x4){0u, 0u, 0u, 0u};
     g[c][0] = g[c][1] = bt[c][0] = bt[c][1] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (col < d) {
       p[c] = *reinterpret_cast<const u32x4*>(xr + col);
+      if (EMB) pp[c] = *reinterpret_cast<const u32x4*>(pr + col);
       g[c][0] = *reinterpret_cast<const float4*>(gamma + col);
       g[c][1] = *reinterpret_cast<const float4*>(gamma + col + 4);
       bt[c][0] = *reinterpret_cast<const float4*>(beta + col);
       bt[c][1] = *reinterpret_cast<const float4*>(beta + col + 4);
+    }
+  }
+  if (EMB) {
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      if (col < d) {
+        p[c] = bf16x8_add(p[c], pp[c]);
+        *reinterpret_cast<u32x4*>(E.x + (long)row * d + col) = p[c];
+      }
     }
   }
   float v[NV][8];
@@ -213,23 +238,38 @@ using namespace jdt;
 static int g_ln_xcd = 1;
 JDT_API void jdt_ln_set_xcd(int on) { g_ln_xcd = on; }
 
-JDT_API int jdt_ln_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd, int T,
-                       int d, float eps, void* stream) {
+template <bool EMB>
+static int ln_fwd_launch(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd, int T,
+                         int d, float eps, const LnEmbed& E, void* stream) {
   if (d % 8 || d > 2048) return -3;
   if ((reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta) | reinterpret_cast<uintptr_t>(x) |
        reinterpret_cast<uintptr_t>(y)) & 15)
     return -2;
+  if (EMB && (E.S <= 0 || ((reinterpret_cast<uintptr_t>(E.wte) | reinterpret_cast<uintptr_t>(E.wpe)) & 15))) return -2;
   const int nv = (d / 8 + 63) / 64;
   dim3 grid((T + 3) / 4);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bf16_t* xb = static_cast<const bf16_t*>(x);
   bf16_t* yb = static_cast<bf16_t*>(y);
   switch (nv) {
-    case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, st, xb, gamma, beta, yb, mean, rstd, T, d, eps, g_ln_xcd); break;
-    case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, st, xb, gamma, beta, yb, mean, rstd, T, d, eps, g_ln_xcd); break;
-    default: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, st, xb, gamma, beta, yb, mean, rstd, T, d, eps, g_ln_xcd); break;
+    case 1: hipLaunchKernelGGL((ln_fwd_kernel<1, EMB>), grid, dim3(256), 0, st, xb, gamma, beta, yb, mean, rstd, T, d, eps, g_ln_xcd, E); break;
+    case 2: hipLaunchKernelGGL((ln_fwd_kernel<2, EMB>), grid, dim3(256), 0, st, xb, gamma, beta, yb, mean, rstd, T, d, eps, g_ln_xcd, E); break;
+    default: hipLaunchKernelGGL((ln_fwd_kernel<4, EMB>), grid, dim3(256), 0, st, xb, gamma, beta, yb, mean, rstd, T, d, eps, g_ln_xcd, E); break;
   }
   return HIP_LAUNCH_CHECK();
+}
+
+JDT_API int jdt_ln_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd, int T,
+                       int d, float eps, void* stream) {
+  return ln_fwd_launch<false>(x, gamma, beta, y, mean, rstd, T, d, eps, LnEmbed{}, stream);
+}
+
+// x_out = wte[tok] + wpe[t % S] (bf16, as jdt_embed_fwd) and y = LN(x_out), one launch
+JDT_API int jdt_ln_fwd_embed(const int* tok, const void* wte, const void* wpe, int S, void* x_out, const float* gamma,
+                             const float* beta, void* y, float* mean, float* rstd, int T, int d, float eps,
+                             void* stream) {
+  const LnEmbed E{tok, static_cast<const bf16_t*>(wte), static_cast<const bf16_t*>(wpe), S, static_cast<bf16_t*>(x_out)};
+  return ln_fwd_launch<true>(x_out, gamma, beta, y, mean, rstd, T, d, eps, E, stream);
 }
 
 static int g_ln_rows = 0, g_ln_waves = 0;

@@ -840,10 +840,27 @@ def attention_bwd(do: torch.Tensor, qkv: torch.Tensor, P: torch.Tensor, B: int, 
 
 
 # ----------------------------------------------------------------------------- layernorm / embedding / colsum
-def layernorm_fwd(x, gamma, beta, eps=1e-6, y_out=None):
+def layernorm_fwd(x, gamma, beta, eps=1e-6, y_out=None, embed=None):
     """flax nn.LayerNorm (eps 1e-6); returns (y bf16, mean f32 [T], rstd f32 [T]).
-    ``y_out``: preallocated y (e.g. rows of a deferred-weight-gradient arena)."""
+    ``y_out``: preallocated y (e.g. rows of a deferred-weight-gradient arena).
+    ``embed`` = (tok, wte, wpe, S): ``x`` is an output -- it receives the token +
+    position embedding (``embed_fwd``'s values) and y = LN(x); on the GPU one launch
+    (csrc/layernorm.hip ``jdt_ln_fwd_embed``)."""
     T, d = x.shape
+    if embed is not None and _is_gpu(x):
+        tok, wte, wpe, S = embed
+        assert tok.dtype == torch.int32 and tok.shape == (T,) and wte.shape[1] == d == wpe.shape[1]
+        assert x.is_contiguous() and wte.is_contiguous() and wpe.is_contiguous() and tok.is_contiguous()
+        y = torch.empty_like(x) if y_out is None else y_out
+        assert y.stride(1) == 1 and y.shape == x.shape and y.stride(0) == d
+        mean = torch.empty(T, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(T, dtype=torch.float32, device=x.device)
+        rc = _lib.lib().jdt_ln_fwd_embed(_ptr(tok), _ptr(wte), _ptr(wpe), int(S), _ptr(x), _ptr(gamma), _ptr(beta),
+                                         _ptr(y), _ptr(mean), _ptr(rstd), T, d, float(eps), _lib.stream_ptr())
+        _lib.check(rc, "jdt_ln_fwd_embed")
+        return y, mean, rstd
+    if embed is not None:
+        embed_fwd(*embed, out=x)
     if not _is_gpu(x):
         xf = x.float()
         mean = xf.mean(-1)
@@ -866,13 +883,17 @@ _LN_GEMM = os.environ.get("JDT_LN_GEMM", "1") != "0"
 
 
 def ln_gemm(x, gamma, beta, w, *, eps=1e-6, bias=None, act: str = "none", z_out=None, keep_prob: float = 1.0,
-            seed: int = 0, offset: int = 0, step=None, y_out=None, out=None):
+            seed: int = 0, offset: int = 0, step=None, y_out=None, out=None, embed=None):
     """``gemm(LN(x), w, ...)`` with the LayerNorm fused into the GEMM's A operand
     (csrc/gemm.hip ``gemm_ln_kernel``): returns (C, y = LN(x) bf16, mean, rstd) --
     the same values as ``layernorm_fwd`` followed by ``gemm`` (bit-identical y),
     one launch instead of two.  ``w`` is the [K, N] ("kn") bf16 weight.  Shapes
     outside the fused kernel's envelope (or JDT_LN_GEMM=0, or CPU) run the two ops.
-    ``y_out`` / ``out``: preallocated LN(x) / C (deferred weight-gradient arena rows)."""
+    ``y_out`` / ``out``: preallocated LN(x) / C (deferred weight-gradient arena rows).
+    ``embed`` = (tok, wte, wpe, S): ``x`` is an output that receives the embedding
+    first (the model's first block): folded into the LayerNorm launch where the LN
+    runs apart (``layernorm_fwd(embed=)``), a separate ``embed_fwd`` before the fused
+    kernel."""
     T, d = x.shape
     N = w.shape[-1]
     if _is_gpu(x) and _LN_GEMM and w.dtype == torch.bfloat16 and x.dtype == torch.bfloat16:
@@ -903,11 +924,15 @@ def ln_gemm(x, gamma, beta, w, *, eps=1e-6, bias=None, act: str = "none", z_out=
         L.gamma, L.beta, L.eps = gamma.data_ptr(), beta.data_ptr(), float(eps)
         L.Y, L.ldy, L.mean, L.rstd = y.data_ptr(), y.stride(0), mean.data_ptr(), rstd.data_ptr()
         assert x.stride(1) == 1 and w.stride(1) == 1 and gamma.dtype == beta.dtype == torch.float32
-        rc = _lib.lib().jdt_gemm_ln(ctypes.byref(g), ctypes.byref(L), _lib.stream_ptr())
+        fused = _lib.lib().jdt_gemm_ln_eligible(ctypes.byref(g), ctypes.byref(L))
+        if fused and embed is not None:
+            embed_fwd(*embed, out=x)
+            embed = None
+        rc = _lib.lib().jdt_gemm_ln(ctypes.byref(g), ctypes.byref(L), _lib.stream_ptr()) if fused else -2
         if rc != -2:
             _lib.check(rc, "jdt_gemm_ln")
             return out, y, mean, rstd
-    y, mean, rstd = layernorm_fwd(x, gamma, beta, eps, y_out=y_out)
+    y, mean, rstd = layernorm_fwd(x, gamma, beta, eps, y_out=y_out, embed=embed)
     out = gemm(y, w, bias=bias, act=act, z_out=z_out, keep_prob=keep_prob, seed=seed, offset=offset, step=step,
                out=out)
     return out, y, mean, rstd
@@ -942,13 +967,16 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None, dsum=None,
     return dx
 
 
-def embed_fwd(tok, wte, wpe, S):
+def embed_fwd(tok, wte, wpe, S, out=None):
     T = tok.shape[0]
     d = wte.shape[1]
     if not _is_gpu(tok):
         pos = torch.arange(T) % S
-        return (wte.float()[tok.long()] + wpe.float()[pos]).to(torch.bfloat16)
-    out = torch.empty(T, d, dtype=torch.bfloat16, device=tok.device)
+        e = (wte.float()[tok.long()] + wpe.float()[pos]).to(torch.bfloat16)
+        return e if out is None else out.copy_(e)
+    if out is None:
+        out = torch.empty(T, d, dtype=torch.bfloat16, device=tok.device)
+    assert out.shape == (T, d) and out.is_contiguous() and out.dtype == torch.bfloat16
     rc = _lib.lib().jdt_embed_fwd(_ptr(tok), _ptr(wte), _ptr(wpe), _ptr(out), T, S, d, _lib.stream_ptr())
     _lib.check(rc, "jdt_embed_fwd")
     return out

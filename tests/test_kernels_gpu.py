@@ -948,6 +948,37 @@ def test_ln_gemm_matches_layernorm_then_gemm(M, K, N, act):
     _close(c, ref, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("T,S,d,N", [(2048, 128, 512, 1536), (256, 128, 512, 1536), (333, 111, 1024, 128),
+                                     (96, 32, 2048, 64)])
+def test_embedding_fused_layernorm(T, S, d, N):
+    """layernorm_fwd(embed=) / ln_gemm(embed=) (jdt_ln_fwd_embed: the token + position
+    embedding built inside the LN launch) == embed_fwd then layernorm_fwd: the embedding
+    written to x, LN(x) and its statistics bit-identical; T = 256 takes the fused
+    LN-GEMM route (embedding launched apart), T = 2048 the LN-apart one."""
+    V = 300
+    gen = torch.Generator().manual_seed(8)
+    wte = (torch.randn(V, d, generator=gen) * 0.5).to(torch.bfloat16).to(DEV)
+    wpe = (torch.randn(S, d, generator=gen) * 0.5).to(torch.bfloat16).to(DEV)
+    tok = torch.randint(0, V, (T,), generator=gen).to(torch.int32).to(DEV)
+    gamma = (1 + 0.1 * torch.randn(d, generator=gen)).to(DEV)
+    beta = (0.1 * torch.randn(d, generator=gen)).to(DEV)
+    e_r = kern.embed_fwd(tok, wte, wpe, S)
+    y_r, m_r, r_r = kern.layernorm_fwd(e_r, gamma, beta, 1e-6)
+    x = torch.full((T, d), float("nan"), dtype=torch.bfloat16, device=DEV)
+    y, mean, rstd = kern.layernorm_fwd(x, gamma, beta, 1e-6, embed=(tok, wte, wpe, S))
+    torch.cuda.synchronize()
+    assert torch.equal(x, e_r) and torch.equal(y, y_r) and torch.equal(mean, m_r) and torch.equal(rstd, r_r)
+    # CPU oracle of the embedding itself
+    _close(x, kern.embed_fwd(tok.cpu(), wte.cpu(), wpe.cpu(), S), rtol=0, atol=0)
+    w = (torch.randn(d, N, generator=gen) / d ** 0.5).to(torch.bfloat16).to(DEV)
+    c_r = kern.gemm(y_r, w)
+    x2 = torch.full((T, d), float("nan"), dtype=torch.bfloat16, device=DEV)
+    c, y2, m2, r2 = kern.ln_gemm(x2, gamma, beta, w, eps=1e-6, embed=(tok, wte, wpe, S))
+    torch.cuda.synchronize()
+    assert torch.equal(x2, e_r) and torch.equal(y2, y_r) and torch.equal(m2, m_r) and torch.equal(r2, r_r)
+    _close(c, c_r, rtol=1e-2, atol=1e-2)
+
+
 @pytest.mark.parametrize("B,S,H", [(2, 128, 8), (3, 96, 2), (1, 40, 3), (2, 17, 1), (1, 128, 1)])
 @pytest.mark.parametrize("causal", [True, False])
 def test_attn128_vs_autograd_and_flash(B, S, H, causal):

@@ -87,6 +87,8 @@ def main():
         ("fc2 dX gelu'+db", lambda i: K.gemm(X["d"][i], W["fc2"][i], b_layout="nk", z_in=Z[i], act_bwd="gelu",
                                              dbias=g1, out=outs["f"][i]),
          lambda i: K.gemm(X["d"][i], W["fc2"][i], b_layout="nk", out=outs["f"][i])),
+        ("fc2 dX gelu' no db", lambda i: K.gemm(X["d"][i], W["fc2"][i], b_layout="nk", z_in=Z[i], act_bwd="gelu",
+                                                out=outs["f"][i]), None),
         ("fc1 dX", lambda i: K.gemm(X["f"][i], W["fc1"][i], b_layout="nk", out=outs["d"][i]), None),
         ("out dX", lambda i: K.gemm(X["d"][i], W["out"][i], b_layout="nk", out=outs["d"][i]), None),
         ("qkv dX", lambda i: K.gemm(X["q"][i], W["qkv"][i], b_layout="nk", out=outs["d"][i]), None),

@@ -1,7 +1,7 @@
 set -u
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/r6close3
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/r6close4
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-O=gpurun_out/r6close3
+O=gpurun_out/r6close4
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1; rc=$?
 grep -E "FAILED|passed|failed" $O/pytest_gpu.log | tail -12; echo "pytest rc=$rc"
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
